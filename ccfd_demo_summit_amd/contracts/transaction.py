@@ -1,0 +1,185 @@
+"""Transaction schema and wire codecs.
+
+The reference replays the Kaggle ``creditcard.csv`` dataset onto topic ``odh-demo``
+(README.md:547-548, ProducerDeployment.yaml:94-95): columns ``Time, V1..V28, Amount``
+(+ ``Class`` label).  The dashboards chart ``Amount``, ``V10``, ``V17`` per request
+(deploy/grafana/ModelPrediction.json:104,211,322).  The exact JSON field names the
+reference producer put on the wire are not in the reference, so we
+accept the natural superset:
+
+* JSON per message (compat path): ``{"id":..,"customer_id":..,"Time":..,"V1":..,...,
+  "Amount":..}``; also accepts ``{"features":[30 floats]}`` and the Seldon-style
+  ``{"data":{"ndarray":[[...]]}}`` wrapper.
+* Packed binary batch (``TXB1``, hot path): a columnar micro-batch designed to be
+  consumed zero-copy by the GPU engine (features are one contiguous ``[n,30] f32`` block,
+  16-byte aligned).
+
+Binary layout (little endian)::
+
+    off  size  field
+    0    4     magic  b"TXB1"
+    4    2     version (1)
+    6    2     flags   (bit0: has labels)
+    8    4     n       rows
+    12   4     n_features (30)
+    16   8     base_offset (stream offset of row 0)
+    24   8     reserved
+    32   8n    ids        u64[n]
+    ..   4n    customer   u32[n]   (padded to 16 B)
+    ..   120n  features   f32[n][30] (16-B aligned)
+    ..   n     labels     u8[n]    (if flags & 1)
+"""
+from __future__ import annotations
+
+import json
+import struct
+from dataclasses import dataclass, field
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+FEATURE_NAMES: tuple = ("Time",) + tuple(f"V{i}" for i in range(1, 29)) + ("Amount",)
+N_FEATURES = len(FEATURE_NAMES)          # 30
+TIME_COL = 0
+AMOUNT_COL = N_FEATURES - 1              # 29
+V10_COL = FEATURE_NAMES.index("V10")
+V17_COL = FEATURE_NAMES.index("V17")
+
+TXB_MAGIC = b"TXB1"
+TXB_HEADER = struct.Struct("<4sHHIIQQ")  # 32 bytes
+assert TXB_HEADER.size == 32
+
+
+def _align16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+@dataclass
+class Transaction:
+    id: int
+    customer_id: int
+    features: np.ndarray                  # float32[30]
+    label: Optional[int] = None
+
+    @property
+    def amount(self) -> float:
+        return float(self.features[AMOUNT_COL])
+
+    def to_dict(self) -> dict:
+        d = {"id": int(self.id), "customer_id": int(self.customer_id)}
+        for name, v in zip(FEATURE_NAMES, self.features.tolist()):
+            d[name] = v
+        if self.label is not None:
+            d["Class"] = int(self.label)
+        return d
+
+
+def encode_tx_json(tx: Transaction) -> bytes:
+    return json.dumps(tx.to_dict(), separators=(",", ":")).encode()
+
+
+def decode_tx_json(payload) -> Transaction:
+    """Decode one JSON transaction message (all accepted shapes, see module doc)."""
+    obj = json.loads(payload) if isinstance(payload, (bytes, bytearray, str)) else payload
+    feats = None
+    if "features" in obj:
+        feats = np.asarray(obj["features"], dtype=np.float32)
+    elif "data" in obj:
+        data = obj["data"]
+        if "ndarray" in data:
+            feats = np.asarray(data["ndarray"], dtype=np.float32).reshape(-1)
+        elif "tensor" in data:
+            feats = np.asarray(data["tensor"]["values"], dtype=np.float32)
+    else:
+        feats = np.array([float(obj.get(n, 0.0)) for n in FEATURE_NAMES], dtype=np.float32)
+    if feats is None or feats.shape[0] != N_FEATURES:
+        raise ValueError(f"transaction must carry {N_FEATURES} features")
+    label = obj.get("Class")
+    return Transaction(
+        id=int(obj.get("id", obj.get("tx_id", 0))),
+        customer_id=int(obj.get("customer_id", obj.get("customer", 0))),
+        features=feats,
+        label=None if label is None else int(label),
+    )
+
+
+@dataclass
+class TxBatch:
+    """Columnar micro-batch (host side).  ``features`` is C-contiguous float32 [n,30]."""
+    ids: np.ndarray
+    customer: np.ndarray
+    features: np.ndarray
+    labels: Optional[np.ndarray] = None
+    base_offset: int = 0
+
+    def __post_init__(self):
+        self.ids = np.ascontiguousarray(self.ids, dtype=np.uint64)
+        self.customer = np.ascontiguousarray(self.customer, dtype=np.uint32)
+        self.features = np.ascontiguousarray(self.features, dtype=np.float32)
+        if self.features.ndim != 2 or self.features.shape[1] != N_FEATURES:
+            raise ValueError("features must be [n, 30]")
+        n = self.features.shape[0]
+        if self.ids.shape != (n,) or self.customer.shape != (n,):
+            raise ValueError("ids/customer must be [n]")
+        if self.labels is not None:
+            self.labels = np.ascontiguousarray(self.labels, dtype=np.uint8)
+
+    def __len__(self) -> int:
+        return int(self.features.shape[0])
+
+    @staticmethod
+    def layout(n: int, has_labels: bool):
+        off_ids = 32
+        off_cust = off_ids + 8 * n
+        off_feat = _align16(off_cust + 4 * n)
+        off_lab = off_feat + 4 * N_FEATURES * n
+        end = off_lab + (n if has_labels else 0)
+        return off_ids, off_cust, off_feat, off_lab, _align16(end)
+
+    def encode(self) -> bytes:
+        n = len(self)
+        has_l = self.labels is not None
+        oi, oc, of, ol, end = self.layout(n, has_l)
+        buf = bytearray(end)
+        TXB_HEADER.pack_into(buf, 0, TXB_MAGIC, 1, 1 if has_l else 0, n, N_FEATURES,
+                             int(self.base_offset), 0)
+        buf[oi:oi + 8 * n] = self.ids.tobytes()
+        buf[oc:oc + 4 * n] = self.customer.tobytes()
+        buf[of:of + 4 * N_FEATURES * n] = self.features.tobytes()
+        if has_l:
+            buf[ol:ol + n] = self.labels.tobytes()
+        return bytes(buf)
+
+    @classmethod
+    def decode(cls, payload) -> "TxBatch":
+        mv = memoryview(payload)
+        magic, ver, flags, n, nf, base, _ = TXB_HEADER.unpack_from(mv, 0)
+        if magic != TXB_MAGIC or ver != 1:
+            raise ValueError("not a TXB1 batch")
+        if nf != N_FEATURES:
+            raise ValueError(f"expected {N_FEATURES} features, got {nf}")
+        has_l = bool(flags & 1)
+        oi, oc, of, ol, end = cls.layout(n, has_l)
+        if len(mv) < end:
+            raise ValueError("truncated TXB1 batch")
+        ids = np.frombuffer(mv, np.uint64, n, oi)
+        cust = np.frombuffer(mv, np.uint32, n, oc)
+        feats = np.frombuffer(mv, np.float32, n * N_FEATURES, of).reshape(n, N_FEATURES)
+        labels = np.frombuffer(mv, np.uint8, n, ol) if has_l else None
+        return cls(ids=ids, customer=cust, features=feats, labels=labels, base_offset=base)
+
+    def transactions(self) -> Iterable[Transaction]:
+        for i in range(len(self)):
+            yield Transaction(int(self.ids[i]), int(self.customer[i]), self.features[i],
+                              None if self.labels is None else int(self.labels[i]))
+
+    @classmethod
+    def from_transactions(cls, txs: Sequence[Transaction]) -> "TxBatch":
+        n = len(txs)
+        feats = np.stack([t.features for t in txs]) if n else np.zeros((0, N_FEATURES), np.float32)
+        labels = None
+        if n and all(t.label is not None for t in txs):
+            labels = np.array([t.label for t in txs], np.uint8)
+        return cls(ids=np.array([t.id for t in txs], np.uint64),
+                   customer=np.array([t.customer_id for t in txs], np.uint32),
+                   features=feats, labels=labels)

@@ -1,0 +1,186 @@
+"""Python façade of the native streaming engine (csrc/engine/engine.cpp).
+
+The per-micro-batch loop runs in C++ (host launch cost ~ a few µs per batch would make
+a Python loop the bottleneck); Python drives it in *steps* (``pump(n_batches)``), owns
+device buffers through torch (model blob, epoch counter buffers) and runs the RCCL
+collectives on a side stream between steps (parallel/dp.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops._lib import (FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, EngineConfig, EngineStats,
+                        Flagged, check, last_error, lib)
+from ..ops.kernels import DeviceModel
+
+N_FEATURES = 30
+INPUT_MODES = {"dma": 0, "zerocopy": 1}
+OUTPUT_MODES = {"zerocopy": 0, "dma": 1}
+
+
+class PinnedArray:
+    """numpy view over ``hipHostMalloc`` memory (mapped, portable): the partition log the
+    GPU reads by DMA or directly over PCIe."""
+
+    def __init__(self, shape, dtype=np.float32):
+        self.dtype = np.dtype(dtype)
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        self.nbytes = max(nbytes, 16)
+        self.ptr = lib().ccfd_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"ccfd_host_alloc({self.nbytes}) failed: {last_error()}")
+        buf = (C.c_uint8 * self.nbytes).from_address(self.ptr)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=int(np.prod(self.shape))).reshape(self.shape)
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib().ccfd_host_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class PartitionLog:
+    """One Kafka-partition-like append log of transactions in pinned host memory."""
+
+    def __init__(self, n_rows: int):
+        self.n = int(n_rows)
+        self.feats = PinnedArray((self.n, N_FEATURES), np.float32)
+        self.ids = PinnedArray(self.n, np.uint64)
+        self.customer = PinnedArray(self.n, np.uint32)
+
+    @classmethod
+    def from_arrays(cls, X: np.ndarray, ids=None, customer=None) -> "PartitionLog":
+        log = cls(X.shape[0])
+        log.feats.array[:] = X
+        log.ids.array[:] = np.arange(log.n, dtype=np.uint64) if ids is None else ids
+        log.customer.array[:] = 0 if customer is None else customer
+        return log
+
+    def free(self):
+        for a in (self.feats, self.ids, self.customer):
+            a.free()
+
+
+@dataclass
+class StepStats:
+    batches: int = 0
+    rows: int = 0
+    fraud_rows: int = 0
+    dropped: int = 0
+    wall_s: float = 0.0
+    p50_us: float = 0.0
+    p99_us: float = 0.0
+    max_us: float = 0.0
+    mean_us: float = 0.0
+    lat_hist: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+
+
+class StreamEngine:
+    def __init__(self, dm: DeviceModel, batch: int = 4096, depth: int = 8, streams: int = 2,
+                 input_mode: str = "dma", output_mode: str = "zerocopy", threshold: float = 0.5,
+                 device: Optional[int] = None, flag_capacity: int = 1 << 20):
+        self.dm = dm
+        self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device())
+        self.batch = int(batch)
+        self.threshold = float(threshold)
+        # two epoch counter buffers (X2: one is all-reduced while the other accumulates)
+        self.counters = [torch.zeros(N_COUNTER_SLOTS, dtype=torch.int64, device=self.device) for _ in range(2)]
+        cfg = EngineConfig()
+        cfg.device = self.device.index
+        cfg.model = MODEL_IDS[dm.kind]
+        cfg.blob = dm.blob.data_ptr()
+        cfg.gbdt_trees, cfg.gbdt_depth = dm.trees, dm.depth
+        cfg.threshold = self.threshold
+        cfg.max_batch = self.batch
+        cfg.depth = int(depth)
+        cfg.n_streams = int(streams)
+        cfg.input_mode = INPUT_MODES[input_mode]
+        cfg.output_mode = OUTPUT_MODES[output_mode]
+        cfg.flag_capacity = int(flag_capacity)
+        cfg.counters[0] = self.counters[0].data_ptr()
+        cfg.counters[1] = self.counters[1].data_ptr()
+        torch.cuda.synchronize(self.device)     # counters zeroed before the engine's streams use them
+        self.h = lib().ccfd_engine_create(C.byref(cfg))
+        if not self.h:
+            raise RuntimeError(f"ccfd_engine_create failed: {last_error()}")
+        self.logs: Dict[int, PartitionLog] = {}
+        self._flag_buf = (Flagged * 65536)()
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ccfd_engine_destroy(C.c_void_p(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_log(self, partition: int, log: PartitionLog, cursor: int = 0) -> None:
+        check(lib().ccfd_engine_set_log(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
+                                        C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr),
+                                        log.n, int(cursor)), "ccfd_engine_set_log")
+        self.logs[partition] = log
+
+    def pump(self, n_batches: int, batch_rows: Optional[int] = None, drain: bool = True) -> StepStats:
+        """Score ``n_batches`` micro-batches.  ``drain=False`` keeps up to ``depth`` batches in
+        flight across calls (steady-state streaming); the last call of a run must drain."""
+        st = EngineStats()
+        check(lib().ccfd_engine_pump(C.c_void_p(self.h), int(n_batches), int(batch_rows or self.batch),
+                                     1 if drain else 0, C.byref(st)), "ccfd_engine_pump")
+        return StepStats(st.batches, st.rows, st.fraud_rows, st.flagged_dropped, st.wall_s,
+                         st.lat_p50_us, st.lat_p99_us, st.lat_max_us, st.lat_mean_us,
+                         np.ctypeslib.as_array(st.lat_hist).copy())
+
+    def score(self, X: np.ndarray):
+        """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        n = X.shape[0]
+        proba = np.empty(n, np.float32)
+        route = np.empty(n, np.uint8)
+        check(lib().ccfd_engine_score_sync(C.c_void_p(self.h), X.ctypes.data, n, proba.ctypes.data,
+                                           route.ctypes.data), "ccfd_engine_score_sync")
+        return proba, route
+
+    def flip_epoch(self, side_stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+        """Close the current counter epoch; returns its buffer.  ``side_stream`` is made to
+        wait for every batch submitted in that epoch."""
+        hs = C.c_void_p(side_stream.cuda_stream) if side_stream is not None else None
+        idx = lib().ccfd_engine_flip_epoch(C.c_void_p(self.h), hs)
+        if idx < 0:
+            raise RuntimeError(f"flip_epoch failed: {last_error()}")
+        return self.counters[idx]
+
+    def drain_flagged(self, max_records: int = 1 << 30) -> np.ndarray:
+        out: List[np.ndarray] = []
+        total = 0
+        while total < max_records:
+            k = lib().ccfd_engine_drain_flagged(C.c_void_p(self.h), self._flag_buf,
+                                                min(65536, max_records - total))
+            if k <= 0:
+                break
+            arr = np.frombuffer(self._flag_buf, dtype=np.dtype(FLAGGED_DTYPE), count=k).copy()
+            out.append(arr)
+            total += k
+            if k < 65536:
+                break
+        return np.concatenate(out) if out else np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
+
+    def reset_stats(self) -> None:
+        lib().ccfd_engine_reset_stats(C.c_void_p(self.h))
+
+    def cursor(self, partition: int) -> int:
+        return int(lib().ccfd_engine_cursor(C.c_void_p(self.h), int(partition)))

@@ -1,0 +1,111 @@
+"""ctypes binding of ``libccfd_hip.so`` (C ABI in csrc/include/ccfd_abi.h).
+
+``torch`` must be imported BEFORE the library is loaded: torch's bundled
+``libamdhip64.so`` carries the same soname (``libamdhip64.so.7``), so the dynamic
+linker resolves our NEEDED entry to the runtime torch already loaded and both share one
+HIP runtime (one context, interchangeable device pointers and streams).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the dlopen, see module doc)
+
+_NATIVE = Path(__file__).resolve().parents[1] / "_native"
+LIB_PATH = _NATIVE / "libccfd_hip.so"
+
+MODEL_LR, MODEL_MLP, MODEL_GBDT = 0, 1, 2
+MODEL_IDS = {"lr": MODEL_LR, "mlp": MODEL_MLP, "gbdt": MODEL_GBDT}
+N_COUNTER_SLOTS = 64
+
+
+class ScoreArgs(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("ld", C.c_int64), ("n", C.c_int32), ("model", C.c_int32),
+                ("blob", C.c_void_p), ("threshold", C.c_float), ("gbdt_trees", C.c_int32),
+                ("gbdt_depth", C.c_int32), ("_pad", C.c_int32), ("proba", C.c_void_p),
+                ("route", C.c_void_p), ("counters", C.c_void_p)]
+
+
+class EngineConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("model", C.c_int32), ("blob", C.c_void_p),
+                ("gbdt_trees", C.c_int32), ("gbdt_depth", C.c_int32), ("threshold", C.c_float),
+                ("max_batch", C.c_int32), ("depth", C.c_int32), ("n_streams", C.c_int32),
+                ("input_mode", C.c_int32), ("output_mode", C.c_int32), ("flag_capacity", C.c_int32),
+                ("_pad", C.c_int32), ("counters", C.c_void_p * 2)]
+
+
+class Flagged(C.Structure):
+    _fields_ = [("tx_id", C.c_uint64), ("customer", C.c_uint32), ("proba", C.c_float),
+                ("amount", C.c_float), ("partition", C.c_uint32)]
+
+
+class EngineStats(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("rows", C.c_uint64), ("fraud_rows", C.c_uint64),
+                ("flagged_dropped", C.c_uint64), ("wall_s", C.c_double), ("lat_p50_us", C.c_double),
+                ("lat_p99_us", C.c_double), ("lat_max_us", C.c_double), ("lat_mean_us", C.c_double),
+                ("lat_hist", C.c_uint64 * 256)]
+
+
+FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
+                 ("partition", "<u4")]
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load (building first if needed and a toolchain exists) the native library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            if os.environ.get("CCFD_NO_AUTOBUILD"):
+                raise NativeUnavailable(f"{LIB_PATH} missing (run python -m ccfd_demo_summit_amd.ops.build)")
+            from .build import build
+            build(verbose=False)
+        L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+        L.ccfd_score_launch.argtypes = [C.POINTER(ScoreArgs), C.c_void_p]
+        L.ccfd_score_launch.restype = C.c_int
+        L.ccfd_last_error.restype = C.c_char_p
+        L.ccfd_host_alloc.argtypes = [C.c_size_t]
+        L.ccfd_host_alloc.restype = C.c_void_p
+        L.ccfd_host_free.argtypes = [C.c_void_p]
+        L.ccfd_host_device_ptr.argtypes = [C.c_void_p]
+        L.ccfd_host_device_ptr.restype = C.c_void_p
+        L.ccfd_engine_create.argtypes = [C.POINTER(EngineConfig)]
+        L.ccfd_engine_create.restype = C.c_void_p
+        L.ccfd_engine_destroy.argtypes = [C.c_void_p]
+        L.ccfd_engine_set_log.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_int64, C.c_int64]
+        L.ccfd_engine_pump.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.POINTER(EngineStats)]
+        L.ccfd_engine_score_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        L.ccfd_engine_flip_epoch.argtypes = [C.c_void_p, C.c_void_p]
+        L.ccfd_engine_drain_flagged.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.ccfd_engine_drain_flagged.restype = C.c_int64
+        L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]
+        L.ccfd_engine_cursor.restype = C.c_int64
+        L.ccfd_engine_reset_stats.argtypes = [C.c_void_p]
+        L.ccfd_parse_json_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                            C.c_void_p]
+        L.ccfd_parse_json_batch.restype = C.c_int64
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    return lib().ccfd_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc}): {last_error()}")

@@ -1,0 +1,89 @@
+"""Build the native library ``libccfd_hip.so`` in-tree with hipcc for gfx950.
+
+    python -m ccfd_demo_summit_amd.ops.build [--force] [--jobs N]
+
+Every ``csrc/kernels/*.hip`` (device code, MFMA kernels) and ``csrc/engine/*.cpp``
+(host runtime: streaming engine, ingest parser) is compiled to an object under
+``build/obj`` and linked into ``ccfd_demo_summit_amd/_native/libccfd_hip.so``.  The .so
+is git-ignored but travels to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+CSRC = ROOT / "csrc"
+OBJ = ROOT / "build" / "obj"
+NATIVE = Path(__file__).resolve().parents[1] / "_native"
+LIB = NATIVE / "libccfd_hip.so"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libccfd_hip.so)")
+
+
+def sources():
+    return sorted(CSRC.glob("kernels/*.hip")) + sorted(CSRC.glob("engine/*.cpp"))
+
+
+def _headers_mtime() -> float:
+    hs = list(CSRC.glob("**/*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _compile(src: Path, force: bool) -> Path:
+    obj = OBJ / (src.parent.name + "_" + src.stem + ".o")
+    if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+        return obj
+    cmd = [hipcc(), "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
+           "-Wno-unused-result", "-I", str(CSRC / "include"), "-c", str(src), "-o", str(obj)]
+    if src.suffix == ".cpp":
+        # host-only translation units: no device code object
+        cmd = [hipcc(), "-O3", "-fPIC", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__",
+               "-I", str(CSRC / "include"), "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    NATIVE.mkdir(parents=True, exist_ok=True)
+    srcs = sources()
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or not LIB.exists() or LIB.stat().st_mtime < newest:
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + \
+              [str(o) for o in objs] + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+    if verbose:
+        print(f"[ccfd build] {LIB} ({len(srcs)} sources, arch {ARCH})")
+    return LIB
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=4)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.jobs)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,75 @@
+"""Python API over the fused HIP scoring kernels (csrc/kernels/*.hip).
+
+All functions take torch tensors on the GPU and enqueue on the current torch stream.
+There is deliberately NO silent fallback: on a machine with a GPU these ops either run
+the gfx950 code object or raise (the CPU oracles live in ``models/*.py``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ._lib import MODEL_IDS, N_COUNTER_SLOTS, ScoreArgs, check, lib
+
+N_FEATURES = 30
+
+
+class DeviceModel:
+    """A packed model resident in HBM (the blob is broadcast once over RCCL in DP runs)."""
+
+    def __init__(self, model, device: torch.device | str | int = "cuda"):
+        self.kind = model.kind
+        if self.kind not in MODEL_IDS:
+            raise ValueError(f"no device kernel for model kind {self.kind!r}")
+        blob = np.frombuffer(model.pack(), np.uint8)
+        self.blob = torch.from_numpy(blob.copy()).to(device)
+        self.trees = getattr(model, "n_trees", 0)
+        self.depth = getattr(model, "depth", 0)
+
+    @classmethod
+    def from_blob(cls, kind: str, blob: torch.Tensor, trees: int = 0, depth: int = 0) -> "DeviceModel":
+        self = cls.__new__(cls)
+        self.kind, self.blob, self.trees, self.depth = kind, blob, trees, depth
+        return self
+
+    @property
+    def model_id(self) -> int:
+        return MODEL_IDS[self.kind]
+
+
+def new_counters(device="cuda") -> torch.Tensor:
+    return torch.zeros(N_COUNTER_SLOTS, dtype=torch.int64, device=device)
+
+
+def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
+          proba: Optional[torch.Tensor] = None, route: Optional[torch.Tensor] = None,
+          counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None
+          ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused score of x [n,30] (float32, CUDA): returns (proba_1 [n] f32, route [n] u8)."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES:
+        raise ValueError("x must be a CUDA float32 tensor of shape [n, 30]")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    n = x.shape[0]
+    if proba is None:
+        proba = torch.empty(n, dtype=torch.float32, device=x.device)
+    if route is None:
+        route = torch.empty(n, dtype=torch.uint8, device=x.device)
+    a = ScoreArgs()
+    a.x = x.data_ptr()
+    a.ld = x.stride(0)
+    a.n = n
+    a.model = dm.model_id
+    a.blob = dm.blob.data_ptr()
+    a.threshold = float(threshold)
+    a.gbdt_trees = dm.trees
+    a.gbdt_depth = dm.depth
+    a.proba = proba.data_ptr()
+    a.route = route.data_ptr()
+    a.counters = counters.data_ptr() if counters is not None else None
+    s = stream if stream is not None else torch.cuda.current_stream(x.device)
+    check(lib().ccfd_score_launch(C.byref(a), C.c_void_p(s.cuda_stream)), "ccfd_score_launch")
+    return proba, route

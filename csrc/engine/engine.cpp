@@ -1,0 +1,383 @@
+// Streaming scoring engine: the GPU-resident micro-batcher.
+//
+// Replaces the reference's per-transaction hot loop (router consumes one Kafka message,
+// POSTs it to Seldon, applies Drools, starts a KIE process: SURVEY.md §3.1,
+// deploy/router.yaml:45-70) with:
+//
+//   partition log (pinned host, written by the ingest side)
+//     -> micro-batch of B rows (pointer arithmetic, no copy)
+//     -> [input_mode=DMA]      hipMemcpyAsync H2D into an HBM staging slot
+//        [input_mode=zerocopy] the kernel reads the pinned log over PCIe directly
+//     -> ONE fused kernel (normalize + model + sigmoid + threshold + counters + histogram)
+//     -> proba/route written straight into pinned host result slots (or D2H copy)
+//     -> completion (event) -> flagged transactions pushed to the hand-off ring
+//
+// `depth` micro-batches are in flight over `n_streams` HIP streams, so the H2D copy of
+// batch i+1 overlaps the kernel of batch i and the completion handling of batch i-1.
+// Counters accumulate on the device into one of two epoch buffers; flip_epoch() lets a
+// side stream all-reduce the closed epoch over RCCL while scoring continues (X2).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../include/ccfd_abi.h"
+
+namespace ccfd {
+void set_error(const std::string& e);
+}
+
+namespace {
+
+using ccfd::set_error;
+
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+#define HIPCHK(expr)                                                          \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      set_error(std::string(#expr ": ") + hipGetErrorString(_e));             \
+      return -4;                                                              \
+    }                                                                         \
+  } while (0)
+
+struct Partition {
+  const float* feats = nullptr;      // host pointer
+  const float* feats_dev = nullptr;  // device-visible alias (zero-copy)
+  const uint64_t* ids = nullptr;
+  const uint32_t* cust = nullptr;
+  int64_t n = 0;
+  int64_t cursor = 0;
+};
+
+struct Slot {
+  bool busy = false;
+  int part = 0;
+  int64_t start = 0;
+  int32_t rows = 0;
+  int64_t t_submit = 0;
+  float* d_x = nullptr;
+  float* d_proba = nullptr;
+  uint8_t* d_route = nullptr;
+  float* h_proba = nullptr;        // pinned host
+  uint8_t* h_route = nullptr;
+  float* h_proba_dev = nullptr;    // device alias of the pinned host slot
+  uint8_t* h_route_dev = nullptr;
+  hipEvent_t ev = nullptr;
+};
+
+class Engine {
+ public:
+  ccfd_engine_config cfg{};
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> flip_ev;
+  std::vector<Slot> slots;
+  std::vector<Partition> parts;
+  uint64_t seq = 0;
+  int next_part = 0;
+  int epoch = 0;
+  // flagged hand-off ring (producer: pump thread; consumer: drain, any thread)
+  std::vector<ccfd_flagged> ring;
+  uint64_t ring_head = 0, ring_tail = 0;
+  std::mutex ring_mu;
+  uint64_t dropped = 0;
+  std::vector<float> lat_us;
+  uint64_t lat_hist[256] = {};
+
+  int init(const ccfd_engine_config& c) {
+    cfg = c;
+    if (cfg.max_batch <= 0 || cfg.depth <= 0 || cfg.n_streams <= 0) {
+      set_error("max_batch, depth and n_streams must be > 0");
+      return -1;
+    }
+    if (cfg.blob == nullptr) { set_error("null model blob"); return -1; }
+    HIPCHK(hipSetDevice(cfg.device));
+    streams.resize(cfg.n_streams);
+    flip_ev.resize(cfg.n_streams);
+    for (int i = 0; i < cfg.n_streams; ++i) {
+      HIPCHK(hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&flip_ev[i], hipEventDisableTiming));
+    }
+    slots.resize(cfg.depth);
+    const size_t B = (size_t)cfg.max_batch;
+    for (auto& s : slots) {
+      // HBM staging slot: used by input_mode=DMA and always by score_sync (caller memory
+      // may be pageable, which the GPU must never dereference directly)
+      HIPCHK(hipMalloc(&s.d_x, B * CCFD_N_FEATURES * sizeof(float)));
+      if (cfg.output_mode == 1) {
+        HIPCHK(hipMalloc(&s.d_proba, B * sizeof(float)));
+        HIPCHK(hipMalloc(&s.d_route, B));
+      }
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_proba), B * sizeof(float),
+                           hipHostMallocMapped | hipHostMallocPortable));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_route), B,
+                           hipHostMallocMapped | hipHostMallocPortable));
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_proba_dev), s.h_proba, 0));
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_route_dev), s.h_route, 0));
+      HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    }
+    ring.resize(std::max(1024, cfg.flag_capacity));
+    return 0;
+  }
+
+  ~Engine() {
+    hipSetDevice(cfg.device);
+    for (auto& s : slots) {
+      if (s.busy) hipEventSynchronize(s.ev);
+      if (s.d_x) hipFree(s.d_x);
+      if (s.d_proba) hipFree(s.d_proba);
+      if (s.d_route) hipFree(s.d_route);
+      if (s.h_proba) hipHostFree(s.h_proba);
+      if (s.h_route) hipHostFree(s.h_route);
+      if (s.ev) hipEventDestroy(s.ev);
+    }
+    for (auto e : flip_ev) if (e) hipEventDestroy(e);
+    for (auto st : streams) if (st) hipStreamDestroy(st);
+  }
+
+  int set_log(int p, const float* feats, const uint64_t* ids, const uint32_t* cust, int64_t n, int64_t cursor) {
+    if (p < 0 || p > 4096) { set_error("bad partition index"); return -1; }
+    if (n < cfg.max_batch) { set_error("partition log shorter than one micro-batch"); return -1; }
+    if (reinterpret_cast<uintptr_t>(feats) & 15) { set_error("log must be 16-byte aligned"); return -1; }
+    drain_all();
+    if ((int)parts.size() <= p) parts.resize(p + 1);
+    Partition& P = parts[p];
+    P.feats = feats; P.ids = ids; P.cust = cust; P.n = n; P.cursor = cursor % n;
+    P.feats_dev = feats;
+    if (cfg.input_mode == 1) {
+      void* d = nullptr;
+      HIPCHK(hipHostGetDevicePointer(&d, const_cast<float*>(feats), 0));
+      P.feats_dev = static_cast<const float*>(d);
+    }
+    return 0;
+  }
+
+  void push_flagged(const Slot& s) {
+    const Partition& P = parts[s.part];
+    const uint8_t* r = s.h_route;
+    const int n = s.rows;
+    std::lock_guard<std::mutex> lk(ring_mu);
+    const uint64_t cap = ring.size();
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      std::memcpy(&w, r + i, 8);
+      if (w == 0) continue;
+      for (int k = 0; k < 8; ++k) if (r[i + k]) emit(P, s, i + k, cap);
+    }
+    for (; i < n; ++i) if (r[i]) emit(P, s, i, cap);
+  }
+
+  inline void emit(const Partition& P, const Slot& s, int i, uint64_t cap) {
+    if (ring_tail - ring_head >= cap) { ++dropped; return; }
+    const int64_t row = s.start + i;
+    ccfd_flagged& f = ring[ring_tail % cap];
+    f.tx_id = P.ids ? P.ids[row] : (uint64_t)row;
+    f.customer = P.cust ? P.cust[row] : 0u;
+    f.proba = s.h_proba[i];
+    f.amount = P.feats[row * CCFD_N_FEATURES + CCFD_N_FEATURES - 1];
+    f.partition = (uint32_t)s.part;
+    ++ring_tail;
+  }
+
+  int complete(Slot& s, ccfd_engine_stats* st) {
+    HIPCHK(hipEventSynchronize(s.ev));
+    const int64_t t = now_ns();
+    const double us = (t - s.t_submit) * 1e-3;
+    lat_us.push_back((float)us);
+    const double ns = (double)std::max<int64_t>(1, t - s.t_submit);
+    lat_hist[std::min(255, (int)std::floor(4.0 * std::log2(ns)))]++;
+    uint64_t nf = 0;
+    for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
+    if (nf) push_flagged(s);
+    if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
+    s.busy = false;
+    return 0;
+  }
+
+  int drain_all(ccfd_engine_stats* st = nullptr) {
+    // complete in submission order
+    const int D = (int)slots.size();
+    for (int k = 0; k < D; ++k) {
+      Slot& s = slots[(seq + k) % D];
+      if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
+    }
+    return 0;
+  }
+
+  int submit(Slot& s, const float* x_dev_or_host, const float* x_host, int rows, hipStream_t stream,
+             bool force_dma = false) {
+    s.t_submit = now_ns();
+    const float* xk = x_dev_or_host;
+    if (cfg.input_mode == 0 || force_dma) {
+      HIPCHK(hipMemcpyAsync(s.d_x, x_host, (size_t)rows * CCFD_N_FEATURES * sizeof(float),
+                            hipMemcpyHostToDevice, stream));
+      xk = s.d_x;
+    }
+    ccfd_score_args a{};
+    a.x = xk; a.ld = CCFD_N_FEATURES; a.n = rows; a.model = cfg.model; a.blob = cfg.blob;
+    a.threshold = cfg.threshold; a.gbdt_trees = cfg.gbdt_trees; a.gbdt_depth = cfg.gbdt_depth;
+    a.proba = cfg.output_mode == 1 ? s.d_proba : s.h_proba_dev;
+    a.route = cfg.output_mode == 1 ? s.d_route : s.h_route_dev;
+    a.counters = cfg.counters[epoch & 1];
+    int rc = ccfd_score_launch(&a, stream);
+    if (rc) return rc;
+    if (cfg.output_mode == 1) {
+      HIPCHK(hipMemcpyAsync(s.h_proba, s.d_proba, (size_t)rows * sizeof(float), hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(s.h_route, s.d_route, (size_t)rows, hipMemcpyDeviceToHost, stream));
+    }
+    HIPCHK(hipEventRecord(s.ev, stream));
+    s.busy = true;
+    return 0;
+  }
+
+  int pump(int64_t n_batches, int32_t batch_rows, bool drain, ccfd_engine_stats* st) {
+    HIPCHK(hipSetDevice(cfg.device));
+    if (parts.empty()) { set_error("no partition log registered"); return -1; }
+    if (batch_rows <= 0 || batch_rows > cfg.max_batch) { set_error("bad batch_rows"); return -1; }
+    const int64_t t0 = now_ns();
+    const int D = (int)slots.size();
+    for (int64_t b = 0; b < n_batches; ++b) {
+      Slot& s = slots[seq % D];
+      if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
+      int p = next_part;
+      for (int k = 0; k < (int)parts.size() && parts[p].feats == nullptr; ++k) p = (p + 1) % parts.size();
+      next_part = (p + 1) % (int)parts.size();
+      Partition& P = parts[p];
+      if (P.cursor + batch_rows > P.n) P.cursor = 0;
+      s.part = p; s.start = P.cursor; s.rows = batch_rows;
+      P.cursor += batch_rows;
+      const size_t off = (size_t)s.start * CCFD_N_FEATURES;
+      hipStream_t stream = streams[seq % streams.size()];
+      int rc = submit(s, P.feats_dev + off, P.feats + off, batch_rows, stream);
+      if (rc) return rc;
+      ++seq;
+    }
+    if (drain) {
+      int rc = drain_all(st);
+      if (rc) return rc;
+    }
+    if (st) {
+      st->wall_s += (now_ns() - t0) * 1e-9;
+      st->flagged_dropped = dropped;
+      fill_latency(st);
+    }
+    return 0;
+  }
+
+  void fill_latency(ccfd_engine_stats* st) {
+    std::memcpy(st->lat_hist, lat_hist, sizeof(lat_hist));
+    if (lat_us.empty()) return;
+    std::vector<float> v = lat_us;
+    auto pct = [&](double q) {
+      size_t k = (size_t)std::min<double>(v.size() - 1, std::floor(q * (v.size() - 1) + 0.5));
+      std::nth_element(v.begin(), v.begin() + k, v.end());
+      return (double)v[k];
+    };
+    st->lat_p50_us = pct(0.50);
+    st->lat_p99_us = pct(0.99);
+    double mx = 0, sum = 0;
+    for (float x : lat_us) { mx = std::max<double>(mx, x); sum += x; }
+    st->lat_max_us = mx;
+    st->lat_mean_us = sum / lat_us.size();
+  }
+
+  int score_sync(const float* x, int32_t n, float* proba_out, uint8_t* route_out) {
+    HIPCHK(hipSetDevice(cfg.device));
+    int rc = drain_all();
+    if (rc) return rc;
+    const int D = (int)slots.size();
+    for (int32_t off = 0; off < n; off += cfg.max_batch) {
+      const int rows = std::min<int32_t>(cfg.max_batch, n - off);
+      Slot& s = slots[seq % D];
+      hipStream_t stream = streams[seq % streams.size()];
+      const float* xh = x + (size_t)off * CCFD_N_FEATURES;
+      rc = submit(s, xh, xh, rows, stream, /*force_dma=*/true);
+      if (rc) return rc;
+      ++seq;
+      HIPCHK(hipEventSynchronize(s.ev));
+      s.busy = false;
+      if (proba_out) std::memcpy(proba_out + off, s.h_proba, rows * sizeof(float));
+      if (route_out) std::memcpy(route_out + off, s.h_route, rows);
+    }
+    return 0;
+  }
+
+  int flip_epoch(void* side_stream) {
+    HIPCHK(hipSetDevice(cfg.device));
+    const int closed = epoch & 1;
+    for (size_t i = 0; i < streams.size(); ++i) {
+      HIPCHK(hipEventRecord(flip_ev[i], streams[i]));
+      if (side_stream) HIPCHK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(side_stream), flip_ev[i], 0));
+    }
+    ++epoch;
+    return closed;
+  }
+
+  int64_t drain_flagged(ccfd_flagged* out, int64_t max) {
+    std::lock_guard<std::mutex> lk(ring_mu);
+    const uint64_t cap = ring.size();
+    int64_t k = 0;
+    while (ring_head < ring_tail && k < max) out[k++] = ring[ring_head++ % cap];
+    return k;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+void* ccfd_engine_create(const ccfd_engine_config* cfg) {
+  if (!cfg) { set_error("null config"); return nullptr; }
+  auto* e = new Engine();
+  if (e->init(*cfg) != 0) { delete e; return nullptr; }
+  return e;
+}
+
+void ccfd_engine_destroy(void* eng) { delete static_cast<Engine*>(eng); }
+
+int ccfd_engine_set_log(void* eng, int partition, const float* feats, const uint64_t* ids,
+                        const uint32_t* customer, int64_t n_rows, int64_t cursor) {
+  return static_cast<Engine*>(eng)->set_log(partition, feats, ids, customer, n_rows, cursor);
+}
+
+int ccfd_engine_pump(void* eng, int64_t n_batches, int32_t batch_rows, int32_t drain,
+                     ccfd_engine_stats* st) {
+  return static_cast<Engine*>(eng)->pump(n_batches, batch_rows, drain != 0, st);
+}
+
+int ccfd_engine_score_sync(void* eng, const float* x, int32_t n, float* proba_out, uint8_t* route_out) {
+  return static_cast<Engine*>(eng)->score_sync(x, n, proba_out, route_out);
+}
+
+int ccfd_engine_flip_epoch(void* eng, void* side_stream) {
+  return static_cast<Engine*>(eng)->flip_epoch(side_stream);
+}
+
+int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max) {
+  return static_cast<Engine*>(eng)->drain_flagged(out, max);
+}
+
+int64_t ccfd_engine_cursor(void* eng, int partition) {
+  auto* e = static_cast<Engine*>(eng);
+  if (partition < 0 || partition >= (int)e->parts.size()) return -1;
+  return e->parts[partition].cursor;
+}
+
+void ccfd_engine_reset_stats(void* eng) {
+  auto* e = static_cast<Engine*>(eng);
+  std::memset(e->lat_hist, 0, sizeof(e->lat_hist));
+  e->lat_us.clear();
+}
+
+}  // extern "C"

@@ -1,0 +1,149 @@
+// Native ingest: JSON-per-transaction parser for the compat path of topic `odh-demo`.
+//
+// The reference producer puts one `creditcard.csv` row per Kafka message
+// (README.md:547-548); the router "extracts the features needed for the model"
+// (README.md:549).  This parser does that extraction for a whole fetch of messages at
+// once, straight into a (pinned) [n][30] feature block the engine can hand to the GPU.
+// Accepted shapes (contracts/transaction.py): named columns {"Time","V1".."V28","Amount"}
+// with optional "id"/"customer_id", or {"features":[30 numbers]}.
+#include <cctype>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+
+#include "../include/ccfd_abi.h"
+
+namespace {
+
+struct Cur {
+  const char* p;
+  const char* e;
+  void ws() { while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p; }
+  bool eat(char c) { ws(); if (p < e && *p == c) { ++p; return true; } return false; }
+};
+
+// feature column of a key, or -1 (ids: -2 = id, -3 = customer_id)
+int key_col(const char* k, int n) {
+  if (n == 4 && !std::memcmp(k, "Time", 4)) return 0;
+  if (n == 6 && !std::memcmp(k, "Amount", 6)) return 29;
+  if ((n == 2 || n == 3) && k[0] == 'V') {
+    int v = 0;
+    for (int i = 1; i < n; ++i) { if (!isdigit((unsigned char)k[i])) return -1; v = v * 10 + (k[i] - '0'); }
+    return (v >= 1 && v <= 28) ? v : -1;
+  }
+  if ((n == 2 && !std::memcmp(k, "id", 2)) || (n == 5 && !std::memcmp(k, "tx_id", 5))) return -2;
+  if ((n == 11 && !std::memcmp(k, "customer_id", 11)) || (n == 8 && !std::memcmp(k, "customer", 8))) return -3;
+  if (n == 8 && !std::memcmp(k, "features", 8)) return -4;
+  return -1;
+}
+
+bool parse_number(Cur& c, double* out) {
+  c.ws();
+  if (c.p >= c.e) return false;
+  // strtod needs a terminator; numbers in JSON are short, copy to a small buffer
+  char buf[64];
+  int n = 0;
+  while (c.p < c.e && n < 63 && (isdigit((unsigned char)*c.p) || *c.p == '-' || *c.p == '+' ||
+                                  *c.p == '.' || *c.p == 'e' || *c.p == 'E'))
+    buf[n++] = *c.p++;
+  if (n == 0) return false;
+  buf[n] = 0;
+  char* end = nullptr;
+  *out = std::strtod(buf, &end);
+  return end == buf + n;
+}
+
+bool skip_value(Cur& c);
+
+bool skip_string(Cur& c) {
+  if (!c.eat('"')) return false;
+  while (c.p < c.e) {
+    if (*c.p == '\\') { c.p += 2; continue; }
+    if (*c.p++ == '"') return true;
+  }
+  return false;
+}
+
+bool skip_value(Cur& c) {
+  c.ws();
+  if (c.p >= c.e) return false;
+  char ch = *c.p;
+  if (ch == '"') return skip_string(c);
+  if (ch == '{' || ch == '[') {
+    char close = ch == '{' ? '}' : ']';
+    ++c.p;
+    if (c.eat(close)) return true;
+    for (;;) {
+      if (ch == '{') { if (!skip_string(c) || !c.eat(':')) return false; }
+      if (!skip_value(c)) return false;
+      if (c.eat(',')) continue;
+      return c.eat(close);
+    }
+  }
+  if (!std::strncmp(c.p, "true", 4) && c.e - c.p >= 4) { c.p += 4; return true; }
+  if (!std::strncmp(c.p, "false", 5) && c.e - c.p >= 5) { c.p += 5; return true; }
+  if (!std::strncmp(c.p, "null", 4) && c.e - c.p >= 4) { c.p += 4; return true; }
+  double d;
+  return parse_number(c, &d);
+}
+
+bool parse_one(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust) {
+  Cur c{s, e};
+  for (int k = 0; k < CCFD_N_FEATURES; ++k) f[k] = 0.f;
+  *id = 0; *cust = 0;
+  if (!c.eat('{')) return false;
+  if (c.eat('}')) return false;
+  int seen = 0;
+  for (;;) {
+    c.ws();
+    if (c.p >= c.e || *c.p != '"') return false;
+    const char* k0 = ++c.p;
+    while (c.p < c.e && *c.p != '"') ++c.p;
+    if (c.p >= c.e) return false;
+    const int kn = (int)(c.p - k0);
+    ++c.p;
+    if (!c.eat(':')) return false;
+    const int col = key_col(k0, kn);
+    if (col >= 0) {
+      double d;
+      if (!parse_number(c, &d)) return false;
+      f[col] = (float)d;
+      ++seen;
+    } else if (col == -2 || col == -3) {
+      double d;
+      c.ws();
+      bool quoted = c.eat('"');
+      if (!parse_number(c, &d)) return false;
+      if (quoted && !c.eat('"')) return false;
+      if (col == -2) *id = (uint64_t)d; else *cust = (uint32_t)d;
+    } else if (col == -4) {
+      if (!c.eat('[')) return false;
+      for (int k = 0; k < CCFD_N_FEATURES; ++k) {
+        double d;
+        if (!parse_number(c, &d)) return false;
+        f[k] = (float)d;
+        if (k + 1 < CCFD_N_FEATURES && !c.eat(',')) return false;
+      }
+      if (!c.eat(']')) return false;
+      seen = CCFD_N_FEATURES;
+    } else {
+      if (!skip_value(c)) return false;
+    }
+    if (c.eat(',')) continue;
+    if (!c.eat('}')) return false;
+    break;
+  }
+  return seen > 0;
+}
+
+}  // namespace
+
+extern "C" int64_t ccfd_parse_json_batch(const char* buf, const int64_t* offsets, int64_t n_msgs,
+                                         float* feats, uint64_t* ids, uint32_t* customer) {
+  for (int64_t i = 0; i < n_msgs; ++i) {
+    const char* s = buf + offsets[i];
+    const char* e = buf + offsets[i + 1];
+    if (!parse_one(s, e, feats + i * CCFD_N_FEATURES, ids + i, customer + i)) return -(i + 1);
+  }
+  return n_msgs;
+}

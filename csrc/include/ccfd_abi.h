@@ -1,0 +1,125 @@
+// C ABI of libccfd_hip.so -- the MI355X-native compute + streaming runtime.
+//
+// Python binds this with ctypes (ccfd_demo_summit_amd/ops/_lib.py); every struct here
+// has a ctypes mirror there, keep them in sync (test_abi_layout checks sizes/offsets).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ccfd_model_kind { CCFD_MODEL_LR = 0, CCFD_MODEL_MLP = 1, CCFD_MODEL_GBDT = 2 };
+
+// Cumulative u64 counter slots written by the scoring kernels' epilogue (device side)
+// and all-reduced across ranks (X2 in SURVEY.md §2.4).  Mirrors ops/layout.py.
+enum ccfd_counter_slot {
+  CCFD_CNT_INCOMING = 0,      // transaction.incoming
+  CCFD_CNT_FRAUD = 1,         // transaction.outgoing{type=fraud}
+  CCFD_CNT_STANDARD = 2,      // transaction.outgoing{type=standard}
+  CCFD_CNT_PROBA_E6 = 3,      // sum(round(proba_1 * 1e6))
+  CCFD_CNT_HIST_STD = 8,      // 14 amount buckets, standard route
+  CCFD_CNT_HIST_FRAUD = 24,   // 14 amount buckets, fraud route
+  CCFD_CNT_SLOTS = 64
+};
+#define CCFD_N_AMOUNT_BUCKETS 14
+#define CCFD_N_FEATURES 30
+
+typedef struct ccfd_score_args {
+  const float* x;        // features, row-major [n][ld] (device or host-mapped pointer)
+  int64_t ld;            // row stride in floats (fast path: 30)
+  int32_t n;             // rows
+  int32_t model;         // ccfd_model_kind
+  const void* blob;      // packed model (device memory), see models/*.py pack()
+  float threshold;       // FRAUD_THRESHOLD
+  int32_t gbdt_trees;    // GBDT only
+  int32_t gbdt_depth;    // GBDT only
+  int32_t _pad;
+  float* proba;          // out [n] proba_1 (device or host-mapped), may be NULL
+  uint8_t* route;        // out [n] 1 = fraud route, may be NULL
+  unsigned long long* counters;  // device [CCFD_CNT_SLOTS] accumulated atomically, may be NULL
+} ccfd_score_args;
+
+// Enqueue one fused scoring launch (normalize -> model -> sigmoid -> threshold ->
+// counters/histogram) on `stream` (a hipStream_t; NULL = legacy default stream).
+// Returns 0 or a negative error code (shape/alignment checks happen on the host).
+int ccfd_score_launch(const ccfd_score_args* a, void* stream);
+
+// ---------------------------------------------------------------------------
+// Host memory (pinned, device-mapped; used for partition logs and result rings)
+void* ccfd_host_alloc(size_t bytes);                 // hipHostMalloc(mapped|portable)
+int ccfd_host_free(void* p);
+void* ccfd_host_device_ptr(void* host_ptr);          // hipHostGetDevicePointer
+
+// ---------------------------------------------------------------------------
+// Streaming engine: a GPU-resident micro-batcher over a pinned host partition log.
+typedef struct ccfd_engine_config {
+  int32_t device;
+  int32_t model;
+  const void* blob;            // device pointer (owned by caller)
+  int32_t gbdt_trees, gbdt_depth;
+  float threshold;
+  int32_t max_batch;           // rows per micro-batch (4096)
+  int32_t depth;               // micro-batches in flight
+  int32_t n_streams;           // HIP streams used round-robin
+  int32_t input_mode;          // 0 = DMA H2D into HBM staging, 1 = zero-copy host reads
+  int32_t output_mode;         // 0 = zero-copy host writes, 1 = device + D2H copy
+  int32_t flag_capacity;       // flagged-transaction ring capacity (records)
+  int32_t _pad;
+  unsigned long long* counters[2];  // device counter buffers, alternated per epoch
+} ccfd_engine_config;
+
+typedef struct ccfd_flagged {
+  uint64_t tx_id;
+  uint32_t customer;
+  float proba;
+  float amount;
+  uint32_t partition;
+} ccfd_flagged;   // 24 bytes
+
+typedef struct ccfd_engine_stats {
+  uint64_t batches, rows, fraud_rows, flagged_dropped;
+  double wall_s;
+  double lat_p50_us, lat_p99_us, lat_max_us, lat_mean_us;
+  uint64_t lat_hist[256];      // batch latency histogram in ns, 4 buckets per octave:
+                               // bucket i holds [2^(i/4), 2^((i+1)/4))
+} ccfd_engine_stats;
+
+void* ccfd_engine_create(const ccfd_engine_config* cfg);
+void ccfd_engine_destroy(void* eng);
+const char* ccfd_last_error(void);
+
+// Register partition log p: pinned host features [n_rows][30] (+ optional ids/customer/
+// amount columns).  Rows are consumed from `cursor` and wrap around.
+int ccfd_engine_set_log(void* eng, int partition, const float* feats, const uint64_t* ids,
+                        const uint32_t* customer, int64_t n_rows, int64_t cursor);
+// Score `n_batches` micro-batches of `batch_rows` rows round-robin over the registered
+// partitions.  With drain != 0 it blocks until every submitted batch is complete;
+// otherwise up to `depth` batches stay in flight across calls (no pipeline bubble between
+// steps).  Counts of completed batches accumulate into *st; latency percentiles cover all
+// batches completed since the last ccfd_engine_reset_stats().
+int ccfd_engine_pump(void* eng, int64_t n_batches, int32_t batch_rows, int32_t drain,
+                     ccfd_engine_stats* st);
+// Score one caller-provided batch (pinned host or device pointer) synchronously; proba/route
+// are copied to the caller's host arrays.  Used by predict() serving and tests.
+int ccfd_engine_score_sync(void* eng, const float* x, int32_t n, float* proba_out, uint8_t* route_out);
+// Epoch flip for the X2 all-reduce: subsequent batches accumulate into the other counter
+// buffer; `side_stream` (hipStream_t) is made to wait for every batch of the closed epoch.
+// Returns the index (0/1) of the closed buffer.
+int ccfd_engine_flip_epoch(void* eng, void* side_stream);
+// Drain up to `max` flagged records (fraud route) into `out`; returns count.
+int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
+int64_t ccfd_engine_cursor(void* eng, int partition);
+void ccfd_engine_reset_stats(void* eng);
+
+// ---------------------------------------------------------------------------
+// Native ingest helpers (JSON transaction parser, TXB1 batch codec)
+// Parse `n_msgs` JSON transactions (concatenated, offsets[i]..offsets[i+1]) into
+// feats[n][30], ids[n], customer[n].  Returns number parsed or -(index+1) on error.
+int64_t ccfd_parse_json_batch(const char* buf, const int64_t* offsets, int64_t n_msgs,
+                              float* feats, uint64_t* ids, uint32_t* customer);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,94 @@
+// Shared device helpers for the fused scoring kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../include/ccfd_abi.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace ccfd {
+
+constexpr int kF = CCFD_N_FEATURES;          // 30 raw features
+constexpr int kAmountCol = kF - 1;           // "Amount"
+constexpr int kNB = CCFD_N_AMOUNT_BUCKETS;   // 13 finite bounds + Inf
+constexpr int kTileRows = 16;                // rows per 16x16x32 MFMA tile (one wave)
+constexpr int kTileBytes = kTileRows * kF * 4;   // 1920: contiguous when ld == 30
+constexpr int kHeader = 64;
+
+// Must match contracts/metric_names.py AMOUNT_BUCKETS.
+__device__ __forceinline__ int amount_bucket(float a) {
+  int b = 0;
+  b += a > 1.f;    b += a > 5.f;    b += a > 10.f;   b += a > 25.f;
+  b += a > 50.f;   b += a > 100.f;  b += a > 250.f;  b += a > 500.f;
+  b += a > 1000.f; b += a > 2500.f; b += a > 5000.f; b += a > 10000.f;
+  b += a > 25000.f;
+  return b;   // 0..13, bucket b holds bound[b-1] < a <= bound[b]
+}
+
+__device__ __forceinline__ float sigmoid(float z) { return 1.f / (1.f + __expf(-z)); }
+
+// Per-workgroup epilogue accumulators in LDS.
+struct EpilogueLds {
+  unsigned int hist[2 * kNB];
+  unsigned int fraud;
+  unsigned int rows;
+  unsigned long long psum_e6;
+};
+
+__device__ __forceinline__ void epi_init(EpilogueLds& s) {
+  const int t = threadIdx.x;
+  if (t < 2 * kNB) s.hist[t] = 0;
+  if (t == 0) { s.fraud = 0; s.rows = 0; s.psum_e6 = 0; }
+}
+
+// Flush the workgroup's LDS accumulators into the global u64 counters (one atomic per slot).
+__device__ __forceinline__ void epi_flush(EpilogueLds& s, unsigned long long* cnt) {
+  __syncthreads();
+  if (cnt == nullptr) return;
+  const int t = threadIdx.x;
+  if (t < 2 * kNB) {
+    const unsigned h = s.hist[t];
+    if (h) atomicAdd(&cnt[(t < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + t],
+                     (unsigned long long)h);
+  } else if (t == 64) {
+    atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)s.rows);
+    atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)s.fraud);
+    atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(s.rows - s.fraud));
+    atomicAdd(&cnt[CCFD_CNT_PROBA_E6], s.psum_e6);
+  }
+}
+
+// Wave-level reduction of a u64 over the 64 lanes.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Load one 16-row tile of a packed [n][30] f32 matrix (1920 contiguous bytes) into a
+// wave-private LDS tile with two 16-B loads per lane; rows >= n are zero-filled.
+// `avail` = valid bytes in this tile (multiple of 8).
+__device__ __forceinline__ void load_tile_contig(const float* __restrict__ xt, int avail,
+                                                 float* lds_tile, int lane) {
+  const float4* src = reinterpret_cast<const float4*>(xt);
+  float4* dst = reinterpret_cast<float4*>(lds_tile);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int i = lane + 64 * it;          // float4 index, 120 per tile
+    if (i < kTileBytes / 16) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int off = i * 16;
+      if (off + 16 <= avail) {
+        v = src[i];
+      } else if (off + 8 <= avail) {
+        const float2 h = reinterpret_cast<const float2*>(xt)[2 * i];
+        v.x = h.x; v.y = h.y;
+      }
+      dst[i] = v;
+    }
+  }
+}
+
+}  // namespace ccfd

@@ -1,0 +1,63 @@
+// C-ABI entry point for one fused scoring launch + pinned host memory helpers.
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace ccfd {
+int launch_mlp(const ccfd_score_args& a, hipStream_t s);
+int launch_lr(const ccfd_score_args& a, hipStream_t s);
+int launch_gbdt(const ccfd_score_args& a, hipStream_t s);
+
+thread_local std::string g_last_error;
+void set_error(const std::string& e) { g_last_error = e; }
+}  // namespace ccfd
+
+extern "C" {
+
+const char* ccfd_last_error(void) { return ccfd::g_last_error.c_str(); }
+
+int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
+  using namespace ccfd;
+  if (a == nullptr || a->blob == nullptr || a->x == nullptr) { set_error("null argument"); return -1; }
+  if (a->n < 0) { set_error("n < 0"); return -1; }
+  if (a->n == 0) return 0;
+  if (a->ld < kF || (a->ld & 1) || (reinterpret_cast<uintptr_t>(a->x) & 7)) {
+    set_error("x must be 8-byte aligned with an even row stride >= 30");
+    return -3;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc;
+  switch (a->model) {
+    case CCFD_MODEL_LR: rc = launch_lr(*a, s); break;
+    case CCFD_MODEL_MLP: rc = launch_mlp(*a, s); break;
+    case CCFD_MODEL_GBDT: rc = launch_gbdt(*a, s); break;
+    default: set_error("unknown model kind"); return -2;
+  }
+  if (rc != 0) {
+    hipError_t e = hipGetLastError();
+    set_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
+  }
+  return rc;
+}
+
+void* ccfd_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) {
+    ccfd::set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    return nullptr;
+  }
+  return p;
+}
+
+int ccfd_host_free(void* p) { return hipHostFree(p) == hipSuccess ? 0 : -1; }
+
+void* ccfd_host_device_ptr(void* host_ptr) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host_ptr, 0) != hipSuccess) return nullptr;
+  return d;
+}
+
+}  // extern "C"

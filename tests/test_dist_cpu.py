@@ -1,0 +1,83 @@
+"""Distributed path on CPU: gloo, world_size 2 (SURVEY.md §4.1 "Distributed without a
+cluster"): broadcast weights bit-identical, all-reduced counters == global truth."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ccfd_demo_summit_amd.parallel import assign_partitions, hist_quantile
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.models import build_model
+    from ccfd_demo_summit_amd.parallel import CounterReducer, broadcast_blob, init_distributed
+    ctx = init_distributed(backend="gloo")
+    try:
+        blob = None
+        if ctx.rank == 0:
+            blob = torch.from_numpy(np.frombuffer(build_model("mlp", seed=9).pack(), np.uint8).copy())
+        blob = broadcast_blob(ctx, blob)
+        red = CounterReducer(ctx, torch.device("cpu"))
+        # each rank scores a different number of rows per epoch
+        for epoch in range(3):
+            c = torch.zeros(64, dtype=torch.int64)
+            c[0] = 1000 * (rank + 1) + epoch
+            c[1] = rank + 1
+            red.submit(c, np.full(256, rank + 1, np.int64))
+            assert int(c.sum()) == 0          # epoch buffer zeroed for reuse
+        g, lat = red.snapshot()
+        q.put((rank, bytes(blob.numpy()), g[:2].tolist(), int(lat.sum())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_broadcast_and_counter_allreduce():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert res[0][1] == res[1][1]                 # bit-identical weights
+    from ccfd_demo_summit_amd.models import build_model
+    assert res[0][1] == build_model("mlp", seed=9).pack()
+    truth0 = sum(1000 * (r + 1) + e for r in range(world) for e in range(3))
+    for _, _, g, lat in res:
+        assert g[0] == truth0 and g[1] == 3 * (1 + 2)
+        assert lat == 3 * 256 * (1 + 2)
+
+
+def test_assign_partitions_covers_each_once():
+    for world in (1, 2, 3, 8):
+        seen = []
+        for r in range(world):
+            seen += assign_partitions(16, r, world)
+        assert sorted(seen) == list(range(16))
+
+
+def test_hist_quantile():
+    h = np.zeros(256, np.int64)
+    # 100 samples in bucket of 2^10 ns (bucket index 40 at 4 per octave)
+    h[40] = 100
+    v = hist_quantile(h, 0.5)
+    assert 2 ** 10 <= v < 2 ** 10.25
+    assert hist_quantile(np.zeros(256), 0.5) == 0.0

@@ -1,0 +1,107 @@
+"""Numerics of the fused HIP scoring kernels vs plain fp32 references (SURVEY.md §4.1
+"Kernel correctness": odd batch sizes 1, 31, 4095, 4097, 65536; bf16 <= 1e-2 abs on
+probabilities; GBDT exact)."""
+import numpy as np
+import pytest
+import torch
+
+from ccfd_demo_summit_amd.contracts.metric_names import AMOUNT_BUCKETS
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 31, 4095, 4097, 65536]
+
+
+def _counters_ref(p, route, X):
+    amt = X[:, 29]
+    b = np.searchsorted(np.asarray(AMOUNT_BUCKETS, np.float32), amt, side="left")
+    hist_std = np.bincount(b[route == 0], minlength=14)
+    hist_fr = np.bincount(b[route == 1], minlength=14)
+    return hist_std, hist_fr
+
+
+def _check_counters(cnt, p, route, X):
+    cnt = cnt.cpu().numpy()
+    n = len(p)
+    assert cnt[0] == n
+    assert cnt[1] == route.sum()
+    assert cnt[2] == n - route.sum()
+    assert abs(int(cnt[3]) - int(np.round(p.astype(np.float64) * 1e6).sum())) <= n
+    hs, hf = _counters_ref(p, route, X)
+    np.testing.assert_array_equal(cnt[8:22], hs)
+    np.testing.assert_array_equal(cnt[24:38], hf)
+
+
+@pytest.fixture(scope="module")
+def data():
+    X, y = generate(65536 + 7, seed=11)
+    return X, y
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_mlp_kernel_matches_fp32_reference(gpu, data, n):
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X = data[0][:n]
+    m = build_model("mlp", seed=1, X_ref=data[0][:20000], calibrate_rate=0.01)
+    dm = DeviceModel(m, gpu)
+    cnt = new_counters(gpu)
+    xt = torch.from_numpy(X).to(gpu)
+    p, r = score(dm, xt, 0.5, counters=cnt)
+    torch.cuda.synchronize()
+    p = p.cpu().numpy(); r = r.cpu().numpy()
+    ref32 = m.predict_proba(X)
+    refbf = m.predict_proba(X, emulate_bf16=True)
+    assert np.abs(p - ref32).max() < 1e-2
+    assert np.abs(p - refbf).max() < 2e-3
+    np.testing.assert_array_equal(r, (p >= 0.5).astype(np.uint8))
+    _check_counters(cnt, p, r, X)
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_lr_kernel_matches_fp32_reference(gpu, data, n):
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X = data[0][:n]
+    m = build_model("lr", seed=2, X_ref=data[0][:20000], calibrate_rate=0.01)
+    dm = DeviceModel(m, gpu)
+    cnt = new_counters(gpu)
+    p, r = score(dm, torch.from_numpy(X).to(gpu), 0.5, counters=cnt)
+    torch.cuda.synchronize()
+    p = p.cpu().numpy(); r = r.cpu().numpy()
+    assert np.abs(p - m.predict_proba(X)).max() < 1e-5
+    _check_counters(cnt, p, r, X)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("depth", [6, 3, 8])
+def test_gbdt_kernel_exact(gpu, data, n, depth):
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X = data[0][:n]
+    m = build_model("gbdt", seed=3, X_ref=data[0][:5000], gbdt_trees=100 if depth != 8 else 300,
+                    gbdt_depth=depth)
+    dm = DeviceModel(m, gpu)
+    cnt = new_counters(gpu)
+    p, r = score(dm, torch.from_numpy(X).to(gpu), 0.5, counters=cnt)
+    torch.cuda.synchronize()
+    p = p.cpu().numpy(); r = r.cpu().numpy()
+    ref = m.predict_proba(X)
+    # leaf selection is exact; only the fp32 summation order of the leaves differs
+    assert np.abs(p - ref).max() < 1e-5
+    _check_counters(cnt, p, r, X)
+
+
+def test_strided_input_path(gpu, data):
+    """ld != 30 takes the generic (non-contiguous) loader."""
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, score
+    X = data[0][:1000]
+    big = np.zeros((1000, 32), np.float32)
+    big[:, :30] = X
+    xt = torch.from_numpy(big).to(gpu)[:, :30]
+    for kind in ("mlp", "lr", "gbdt"):
+        m = build_model(kind, seed=5, X_ref=X)
+        dm = DeviceModel(m, gpu)
+        p, _ = score(dm, xt, 0.5)
+        torch.cuda.synchronize()
+        tol = 1e-2 if kind == "mlp" else 1e-5
+        assert np.abs(p.cpu().numpy() - m.predict_proba(X)).max() < tol, kind

@@ -1,0 +1,93 @@
+"""CPU checks of the model families and of the kernel weight packing (the NumPy lane
+emulator walks the exact MFMA fragment maps the HIP kernel uses)."""
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
+from ccfd_demo_summit_amd.models import (LogisticModel, MLPModel, ObliviousGBDT, build_model, load_model,
+                                         save_model)
+from ccfd_demo_summit_amd.models.common import Normalizer, bf16_round
+from ccfd_demo_summit_amd.models.mlp import BLOB_BYTES, emulate_packed_kernel
+
+
+@pytest.fixture(scope="module")
+def X():
+    return generate(20000, seed=3)[0]
+
+
+def test_synthetic_shape_and_prior():
+    X, y = generate(200_000, seed=1)
+    assert X.shape == (200_000, 30) and X.dtype == np.float32
+    assert abs(y.mean() - FRAUD_RATE) < 0.001
+    assert (X[:, 29] >= 0).all() and X[:, 29].max() <= 25691.16 + 1e-3
+    assert np.all(np.diff(X[:, 0]) >= 0)      # Time is monotone
+    # fraud rows are shifted on V14/V17 (negative)
+    assert X[y == 1, 14].mean() < X[y == 0, 14].mean() - 3
+
+
+def test_bf16_round_rne():
+    x = np.array([1.0, 1.00390625, 1.01171875, -2.5, 3.0e38], np.float32)
+    r = bf16_round(x)
+    assert r[0] == 1.0
+    assert r[1] == 1.0            # tie -> even
+    assert r[2] == 1.015625       # tie -> even (up)
+    assert r[3] == -2.5
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 40])
+def test_mlp_packing_emulator_matches_bf16_oracle(X, n):
+    m = build_model("mlp", seed=2, X_ref=X)
+    blob = m.pack()
+    assert len(blob) == BLOB_BYTES
+    pe = emulate_packed_kernel(blob, X[:n])
+    np.testing.assert_allclose(pe, m.predict_proba(X[:n], emulate_bf16=True), atol=1e-6)
+    assert np.abs(pe - m.predict_proba(X[:n])).max() < 1e-2
+
+
+def test_calibration_hits_target_rate(X):
+    for kind in ("lr", "mlp", "gbdt"):
+        m = build_model(kind, seed=4, X_ref=X, calibrate_rate=0.01)
+        rate = (m.predict_proba(X) >= 0.5).mean()
+        assert abs(rate - 0.01) < 0.003, (kind, rate)
+
+
+def test_gbdt_pack_unpack_and_leaf_index(X):
+    g = ObliviousGBDT.random_init(50, 6, seed=1, X_ref=X)
+    g2 = ObliviousGBDT.unpack(g.pack())
+    np.testing.assert_array_equal(g2.feat, g.feat)
+    np.testing.assert_array_equal(g2.leaves, g.leaves)
+    idx = g.leaf_index(X[:5])
+    assert idx.shape == (5, 50) and idx.max() < 64
+    # manual check of one row / tree
+    t, r = 7, 3
+    manual = sum(int(X[r, g.feat[t, d]] > g.thr[t, d]) << d for d in range(6))
+    assert idx[r, t] == manual
+    with pytest.raises(ValueError):
+        ObliviousGBDT(np.zeros((2, 9), np.int32), np.zeros((2, 9), np.float32), np.zeros((2, 512), np.float32))
+
+
+def test_normalizer(X):
+    nz = Normalizer.fit(X)
+    Z = nz(X)
+    assert np.abs(Z.mean(0)).max() < 1e-3
+    assert np.abs(Z.std(0) - 1).max() < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["lr", "mlp", "gbdt"])
+def test_save_load_roundtrip(tmp_path, X, kind):
+    m = build_model(kind, seed=5, X_ref=X)
+    p = tmp_path / f"{kind}.safetensors"
+    save_model(m, str(p), version="3")
+    m2 = load_model(str(p))
+    assert type(m2) is type(m)
+    np.testing.assert_allclose(m2.predict_proba(X[:100]), m.predict_proba(X[:100]), atol=1e-7)
+    assert m2.pack() == m.pack()
+
+
+def test_lr_predict_one(X):
+    m = LogisticModel.random_init(0, Normalizer.fit(X))
+    assert abs(m.predict_one(X[0]) - m.predict_proba(X[:1])[0]) < 1e-7
+
+
+def test_mlp_param_count():
+    assert MLPModel.random_init(0).n_params == 12289
