@@ -1,0 +1,151 @@
+"""Prometheus metrics with the reference names + GPU engine metrics.
+
+Each logical service owns a ``CollectorRegistry`` so it can be scraped on the reference's
+path/port: router ``:8091/prometheus`` (README.md:500-507), KIE ``:8090/rest/metrics``
+(README.md:509-514), model ``:8000/prometheus`` (README.md:292-301).  The six reference
+Grafana dashboards query exactly these names (deploy/grafana/*.json).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Callable, Dict, Optional, Sequence
+
+import numpy as np
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily
+
+from ..contracts import metric_names as M
+
+CONTENT_TYPE = "text/plain; version=0.0.4; charset=utf-8"
+LATENCY_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25,
+                   0.5, 1.0, 2.5, 5.0, 10.0)
+
+
+class RouterMetrics:
+    def __init__(self, registry: Optional[CollectorRegistry] = None):
+        self.registry = registry or CollectorRegistry()
+        r = self.registry
+        self.tx_incoming = Counter(M.TRANSACTION_INCOMING, "Total incoming transactions", registry=r)
+        self.tx_outgoing = Counter(M.TRANSACTION_OUTGOING, "Transactions sent to a business process",
+                                   ["type"], registry=r)
+        self.notif_outgoing = Counter(M.NOTIFICATIONS_OUTGOING, "Customers notified", registry=r)
+        self.notif_incoming = Counter(M.NOTIFICATIONS_INCOMING, "Customer responses", ["response"], registry=r)
+        # pre-create label children so the series exist from the first scrape
+        self.tx_outgoing.labels(type="standard")
+        self.tx_outgoing.labels(type="fraud")
+        self.notif_incoming.labels(response="approved")
+        self.notif_incoming.labels(response="non_approved")
+
+    def expose(self) -> bytes:
+        return generate_latest(self.registry)
+
+
+class KieMetrics:
+    def __init__(self, registry: Optional[CollectorRegistry] = None, buckets: Sequence[float] = M.AMOUNT_BUCKETS):
+        self.registry = registry or CollectorRegistry()
+        r = self.registry
+        b = tuple(buckets) + (float("inf"),)
+        self.investigation = Histogram(M.FRAUD_INVESTIGATION_AMOUNT, "Amount of transactions sent to investigation",
+                                       buckets=b, registry=r)
+        self.approved_low = Histogram(M.FRAUD_APPROVED_LOW_AMOUNT, "Amount of unacknowledged transactions "
+                                      "approved by the DMN (low amount)", buckets=b, registry=r)
+        self.approved = Histogram(M.FRAUD_APPROVED_AMOUNT, "Amount of transactions approved by the customer",
+                                  buckets=b, registry=r)
+        self.rejected = Histogram(M.FRAUD_REJECTED_AMOUNT, "Amount of transactions rejected by the customer",
+                                  buckets=b, registry=r)
+
+    def expose(self) -> bytes:
+        return generate_latest(self.registry)
+
+
+class ModelMetrics:
+    """Model-side gauges (last request) + Seldon engine latency histograms."""
+
+    def __init__(self, registry: Optional[CollectorRegistry] = None, deployment: str = "modelfull",
+                 predictor: str = "modelfull", model_name: str = "modelfull",
+                 model_image: str = "ccfd-mi355x", model_version: str = "1"):
+        self.registry = registry or CollectorRegistry()
+        r = self.registry
+        self.gauges = {n: Gauge(n, f"last request {n}", registry=r) for n in M.MODEL_GAUGES}
+        self.server = Histogram(M.SELDON_SERVER_REQUESTS, "Seldon engine server request latency",
+                                ["status"], buckets=LATENCY_BUCKETS, registry=r)
+        self.client = Histogram(M.SELDON_CLIENT_REQUESTS, "Seldon engine -> model request latency",
+                                list(M.SELDON_CLIENT_LABELS), buckets=LATENCY_BUCKETS, registry=r)
+        self.labels = dict(deployment_name=deployment, predictor_name=predictor, predictor_version="1",
+                           model_name=model_name, model_image=model_image, model_version=model_version)
+
+    def observe_request(self, seconds: float, status: int = 200, model_seconds: Optional[float] = None):
+        self.server.labels(status=str(status)).observe(seconds)
+        self.client.labels(status=str(status), **self.labels).observe(
+            seconds if model_seconds is None else model_seconds)
+
+    def set_last(self, features_row: np.ndarray, proba1: float) -> None:
+        from ..contracts.transaction import AMOUNT_COL, V10_COL, V17_COL
+        self.gauges["proba_1"].set(float(proba1))
+        self.gauges["Amount"].set(float(features_row[AMOUNT_COL]))
+        self.gauges["V17"].set(float(features_row[V17_COL]))
+        self.gauges["V10"].set(float(features_row[V10_COL]))
+
+    def expose(self) -> bytes:
+        return generate_latest(self.registry)
+
+
+class GpuEngineCollector:
+    """Custom collector over the engine's all-reduced device counters (X2) and latency
+    histogram (X3).  ``source()`` returns (counters u64[64], lat_hist u64[256], extra dict)."""
+
+    def __init__(self, source: Callable[[], tuple], rank_label: str = "all"):
+        self.source = source
+        self.rank_label = rank_label
+
+    def collect(self):
+        from ..parallel.dp import hist_quantile
+        got = self.source()
+        if got is None:
+            return
+        cnt, lat, extra = got
+        cnt = np.asarray(cnt, np.int64)
+        rows = CounterMetricFamily(M.GPU_ROWS, "Rows scored on the GPU", labels=["rank"])
+        rows.add_metric([self.rank_label], float(cnt[0]))
+        yield rows
+        fr = GaugeMetricFamily(M.GPU_GLOBAL_FRAUD_RATE, "Global fraud-route rate (all-reduced)",
+                               labels=["rank"])
+        fr.add_metric([self.rank_label], float(cnt[1]) / max(1.0, float(cnt[0])))
+        yield fr
+        h = HistogramMetricFamily(M.GPU_AMOUNT, "Device-side amount histogram by route", labels=["type"])
+        bounds = list(M.AMOUNT_BUCKETS) + [float("inf")]
+        for label, base in (("standard", 8), ("fraud", 24)):
+            counts = cnt[base:base + M.N_AMOUNT_BUCKETS].astype(np.float64)
+            cum = np.cumsum(counts)
+            h.add_metric([label], [(str(b) if b != float("inf") else "+Inf", float(c)) for b, c in zip(bounds, cum)],
+                         sum_value=float("nan"))
+        yield h
+        if lat is not None and np.asarray(lat).sum() > 0:
+            q = GaugeMetricFamily(M.GPU_BATCH_LATENCY.replace("_seconds", "_quantile_seconds"),
+                                  "Micro-batch latency quantiles", labels=["quantile"])
+            for qq in (0.5, 0.9, 0.99):
+                q.add_metric([str(qq)], hist_quantile(lat, qq) * 1e-9)
+            yield q
+        for k, v in (extra or {}).items():
+            g = GaugeMetricFamily(M.GPU_PREFIX + k, k)
+            g.add_metric([], float(v))
+            yield g
+
+
+class MetricsHub:
+    """All registries of an all-in-one deployment, thread-safe to read."""
+
+    def __init__(self):
+        self.router = RouterMetrics()
+        self.kie = KieMetrics()
+        self.model = ModelMetrics()
+        self.gpu_registry = CollectorRegistry()
+        self._lock = threading.Lock()
+
+    def attach_gpu(self, source: Callable[[], tuple]) -> None:
+        self.gpu_registry.register(GpuEngineCollector(source))
+
+    def expose_all(self) -> bytes:
+        with self._lock:
+            return b"".join(generate_latest(r) for r in
+                            (self.router.registry, self.kie.registry, self.model.registry, self.gpu_registry))

@@ -1,0 +1,325 @@
+"""Business-process engine: the standard and fraud processes of the reference's KIE server
+(deploy/ccd-service.yaml; docs/process-fraud.png; README.md:554-605).
+
+Fraud process (explicit state machine of the BPMN):
+
+    start(tx, proba) -> CustomerNotification: publish {customer_id, transaction_id,
+        process_id, ...} to CUSTOMER_NOTIFICATION_TOPIC                (README.md:560,590)
+    event-based gateway, first of:
+      timer expires  -> DMN "Start investigation"                      (README.md:592-596)
+                          approve     -> APPROVED_LOW_AMOUNT  (fraud_approved_low_amount)
+                          investigate -> User Task "Assign case" (fraud_investigation_amount)
+                                         -> prediction service        (README.md:571-581)
+      signal(response) -> true  -> APPROVED_BY_CUSTOMER (fraud_approved_amount)
+                          false -> CANCELLED            (fraud_rejected_amount)  (README.md:597-599)
+
+Standard process: completes immediately as STANDARD (README.md:552).
+
+Time is injected (``clock``) and timers fire from ``tick()``, so the engine is exact and
+deterministic in tests and driven by a periodic task in the service.  Every state change
+is appended to an optional JSONL journal; ``recover()`` rebuilds the in-flight instances
+after a crash (SURVEY.md §5 checkpoint/resume: "in-flight BP instances: an optional
+append-only journal").
+"""
+from __future__ import annotations
+
+import enum
+import heapq
+import itertools
+import json
+import os
+import threading
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from ..contracts.outcomes import CustomerResponse, Outcome
+from .dmn import Decision, investigation_decision
+from .prediction_service import PredictionService
+
+
+class State(str, enum.Enum):
+    WAITING_CUSTOMER = "waiting_customer"
+    USER_TASK = "user_task"
+    COMPLETED = "completed"
+
+
+@dataclass
+class UserTask:
+    id: int
+    instance_id: int
+    name: str = "Assign case"
+    status: str = "Ready"                       # Ready | Completed
+    inputs: Dict[str, Any] = field(default_factory=dict)
+    suggested_outcome: Optional[str] = None
+    confidence: float = 0.0
+    outcome: Optional[str] = None
+    completed_by: Optional[str] = None
+
+
+@dataclass
+class ProcessInstance:
+    id: int
+    process_id: str
+    variables: Dict[str, Any]
+    state: State = State.WAITING_CUSTOMER
+    outcome: Optional[str] = None
+    started: float = 0.0
+    completed: Optional[float] = None
+    timer_due: Optional[float] = None
+    task_id: Optional[int] = None
+    history: List[str] = field(default_factory=list)
+
+    @property
+    def amount(self) -> float:
+        return float(self.variables.get("amount", 0.0))
+
+    @property
+    def proba(self) -> float:
+        return float(self.variables.get("proba", 0.0))
+
+
+class ProcessEngine:
+    FRAUD = "fraud"
+    STANDARD = "standard"
+
+    def __init__(self, notification_timeout_s: float = 30.0, dmn_probability_threshold: float = 0.75,
+                 dmn_amount_threshold: float = 100.0,
+                 publish_notification: Optional[Callable[[Dict[str, Any]], None]] = None,
+                 kie_metrics=None, prediction: Optional[PredictionService] = None,
+                 clock: Callable[[], float] = time.monotonic, journal_path: Optional[str] = None,
+                 keep_completed: int = 100_000):
+        self.timeout = float(notification_timeout_s)
+        self.p_thr = float(dmn_probability_threshold)
+        self.a_thr = float(dmn_amount_threshold)
+        self.publish_notification = publish_notification
+        self.metrics = kie_metrics
+        self.prediction = prediction or PredictionService()
+        self.clock = clock
+        self.instances: Dict[int, ProcessInstance] = {}
+        self.tasks: Dict[int, UserTask] = {}
+        self._timers: List = []
+        self._ids = itertools.count(1)
+        self._task_ids = itertools.count(1)
+        self._lock = threading.RLock()
+        self.outcome_counts: Dict[str, int] = {o.value: 0 for o in Outcome}
+        self.standard_count = 0
+        self.keep_completed = keep_completed
+        self._completed_order: List[int] = []
+        self._journal = open(journal_path, "a", buffering=1) if journal_path else None
+
+    @classmethod
+    def from_config(cls, kie_cfg, **kw) -> "ProcessEngine":
+        pred = kw.pop("prediction", None) or PredictionService(kie_cfg.confidence_threshold)
+        return cls(kie_cfg.notification_timeout_s, kie_cfg.dmn_probability_threshold,
+                   kie_cfg.dmn_amount_threshold, prediction=pred, **kw)
+
+    # ------------------------------------------------------------------ journal
+    def _log(self, inst: ProcessInstance) -> None:
+        if self._journal is None:
+            return
+        d = asdict(inst)
+        d["state"] = inst.state.value
+        rec = {"instance": d}
+        if inst.task_id is not None and inst.task_id in self.tasks:
+            rec["task"] = asdict(self.tasks[inst.task_id])
+        self._journal.write(json.dumps(rec, default=float) + "\n")
+
+    @classmethod
+    def recover(cls, journal_path: str, **kw) -> "ProcessEngine":
+        """Rebuild from the journal (last record per instance wins), then keep appending."""
+        last: Dict[int, dict] = {}
+        if os.path.exists(journal_path):
+            with open(journal_path) as f:
+                for line in f:
+                    line = line.strip()
+                    if line:
+                        rec = json.loads(line)
+                        last[rec["instance"]["id"]] = rec
+        eng = cls(journal_path=journal_path, **kw)
+        max_id, max_task = 0, 0
+        for iid, rec in last.items():
+            d = dict(rec["instance"])
+            d["state"] = State(d["state"])
+            inst = ProcessInstance(**d)
+            eng.instances[iid] = inst
+            max_id = max(max_id, iid)
+            if "task" in rec:
+                t = UserTask(**rec["task"])
+                eng.tasks[t.id] = t
+                max_task = max(max_task, t.id)
+            if inst.state == State.WAITING_CUSTOMER and inst.timer_due is not None:
+                heapq.heappush(eng._timers, (inst.timer_due, iid))
+        eng._ids = itertools.count(max_id + 1)
+        eng._task_ids = itertools.count(max_task + 1)
+        return eng
+
+    # ------------------------------------------------------------------ start
+    def start(self, process_id: str, variables: Dict[str, Any]) -> int:
+        if process_id.endswith(self.STANDARD) or process_id == self.STANDARD:
+            return self.start_standard(variables)
+        return self.start_fraud(variables)
+
+    def start_standard(self, variables: Dict[str, Any]) -> int:
+        with self._lock:
+            iid = next(self._ids)
+            now = self.clock()
+            inst = ProcessInstance(iid, self.STANDARD, dict(variables), State.COMPLETED,
+                                   Outcome.STANDARD.value, now, now, history=["start", "approve"])
+            self.standard_count += 1
+            self.outcome_counts[Outcome.STANDARD.value] += 1
+            self._remember_completed(inst)
+            self._log(inst)
+            return iid
+
+    def start_fraud(self, variables: Dict[str, Any]) -> int:
+        with self._lock:
+            iid = next(self._ids)
+            now = self.clock()
+            inst = ProcessInstance(iid, self.FRAUD, dict(variables), State.WAITING_CUSTOMER, None, now,
+                                   timer_due=now + self.timeout, history=["start", "CustomerNotification"])
+            self.instances[iid] = inst
+            heapq.heappush(self._timers, (inst.timer_due, iid))
+            self._log(inst)
+        if self.publish_notification is not None:
+            self.publish_notification({
+                "customer_id": variables.get("customer_id"),
+                "transaction_id": variables.get("transaction_id", variables.get("tx_id")),
+                "process_id": iid,
+                "amount": variables.get("amount"),
+                "proba": variables.get("proba"),
+            })
+        return iid
+
+    # ------------------------------------------------------------------ signal
+    def signal(self, instance_id: int, name: str, payload: Any) -> bool:
+        """Customer response signal.  Returns False if the instance is not waiting (timer
+        already fired, unknown id, or duplicate delivery -- at-least-once safe)."""
+        with self._lock:
+            inst = self.instances.get(int(instance_id))
+            if inst is None or inst.state != State.WAITING_CUSTOMER:
+                return False
+            approved = _truthy(payload)
+            inst.history.append(f"signal:{name}:{approved}")
+            if approved:
+                self._complete(inst, Outcome.APPROVED_BY_CUSTOMER)
+                if self.metrics:
+                    self.metrics.approved.observe(inst.amount)
+            else:
+                self._complete(inst, Outcome.CANCELLED)
+                if self.metrics:
+                    self.metrics.rejected.observe(inst.amount)
+            return True
+
+    # ------------------------------------------------------------------ timers
+    def tick(self, now: Optional[float] = None) -> int:
+        """Fire every due timer; returns how many fired."""
+        now = self.clock() if now is None else now
+        fired = 0
+        while True:
+            with self._lock:
+                if not self._timers or self._timers[0][0] > now:
+                    break
+                due, iid = heapq.heappop(self._timers)
+                inst = self.instances.get(iid)
+                if inst is None or inst.state != State.WAITING_CUSTOMER or inst.timer_due != due:
+                    continue
+                inst.history.append("timer:Customer notification expired")
+                decision = investigation_decision(inst.proba, inst.amount, self.p_thr, self.a_thr)
+                if decision == Decision.APPROVE:
+                    self._complete(inst, Outcome.APPROVED_LOW_AMOUNT)
+                    if self.metrics:
+                        self.metrics.approved_low.observe(inst.amount)
+                    fired += 1
+                    continue
+                if self.metrics:
+                    self.metrics.investigation.observe(inst.amount)
+                self.outcome_counts[Outcome.INVESTIGATION.value] += 1
+                tid = next(self._task_ids)
+                task = UserTask(tid, iid, inputs={"amount": inst.amount, "proba": inst.proba,
+                                                  "transaction_id": inst.variables.get("transaction_id"),
+                                                  "customer_id": inst.variables.get("customer_id")})
+                self.tasks[tid] = task
+                inst.state = State.USER_TASK
+                inst.task_id = tid
+                inst.history.append("UserTask:Assign case")
+                fired += 1
+            # prediction service outside the lock (may be a remote call)
+            pred = self.prediction.predict(task.inputs)
+            with self._lock:
+                task.suggested_outcome, task.confidence = pred.outcome, pred.confidence
+                if self.prediction.should_auto_complete(pred):
+                    self._complete_task_locked(task, pred.outcome, by="prediction-service")
+                else:
+                    self._log(inst)
+        return fired
+
+    def next_timer_due(self) -> Optional[float]:
+        with self._lock:
+            return self._timers[0][0] if self._timers else None
+
+    # ------------------------------------------------------------------ tasks
+    def list_tasks(self, status: Optional[str] = "Ready") -> List[UserTask]:
+        with self._lock:
+            return [t for t in self.tasks.values() if status is None or t.status == status]
+
+    def complete_task(self, task_id: int, outcome: str, by: str = "investigator") -> bool:
+        with self._lock:
+            task = self.tasks.get(int(task_id))
+            if task is None or task.status == "Completed":
+                return False
+            self._complete_task_locked(task, outcome, by)
+        self.prediction.train(task.inputs, {"outcome": outcome})
+        return True
+
+    def _complete_task_locked(self, task: UserTask, outcome: str, by: str) -> None:
+        task.status, task.outcome, task.completed_by = "Completed", outcome, by
+        inst = self.instances[task.instance_id]
+        res = Outcome.INVESTIGATION_CLOSED_FRAUD if outcome in ("rejected", "fraud", False, "false") \
+            else Outcome.INVESTIGATION_CLOSED_LEGIT
+        inst.history.append(f"task-complete:{outcome}:{by}")
+        self._complete(inst, res)
+
+    # ------------------------------------------------------------------ helpers
+    def _complete(self, inst: ProcessInstance, outcome: Outcome) -> None:
+        inst.state = State.COMPLETED
+        inst.outcome = outcome.value
+        inst.completed = self.clock()
+        inst.timer_due = None
+        self.outcome_counts[outcome.value] += 1
+        self._log(inst)
+        self._remember_completed(inst)
+
+    def _remember_completed(self, inst: ProcessInstance) -> None:
+        if inst.process_id == self.STANDARD:
+            return          # standard instances are counted, not retained (hot path volume)
+        self._completed_order.append(inst.id)
+        while len(self._completed_order) > self.keep_completed:
+            old = self._completed_order.pop(0)
+            gone = self.instances.pop(old, None)
+            if gone is not None and gone.task_id is not None:
+                self.tasks.pop(gone.task_id, None)
+
+    def get(self, instance_id: int) -> Optional[ProcessInstance]:
+        with self._lock:
+            return self.instances.get(int(instance_id))
+
+    def active_count(self) -> int:
+        with self._lock:
+            return sum(1 for i in self.instances.values() if i.state != State.COMPLETED)
+
+    def close(self) -> None:
+        if self._journal:
+            self._journal.close()
+            self._journal = None
+
+
+def _truthy(payload: Any) -> bool:
+    if isinstance(payload, dict):
+        for k in ("response", "approved", "value", "made_transaction"):
+            if k in payload:
+                return _truthy(payload[k])
+        return False
+    if isinstance(payload, str):
+        return payload.strip().lower() in ("true", "1", "yes", "approved", CustomerResponse.APPROVED.value)
+    return bool(payload)

@@ -1,0 +1,101 @@
+"""Transaction router: the replacement for the Camel router ``ccd-fuse`` (deploy/router.yaml;
+README.md:424-459, 543-552, 565-569).
+
+Reference hot loop (per transaction): consume ``odh-demo`` -> POST to Seldon -> Drools ->
+start a KIE process.  Here the router receives WHOLE SCORED MICRO-BATCHES from the GPU
+engine (or from the predict() path) and:
+
+* counts ``transaction.incoming`` and ``transaction.outgoing{type}`` (README.md:524-526);
+* starts a *fraud* process per fraud-routed transaction (KIE hand-off, README.md:552);
+* standard-routed transactions are counted (``standard_mode="count"``, default: at
+  hundreds of millions of tx/s a process instance per legit transaction is not a sane
+  design), or start a standard process each (``"process"``, reference-compatible mode);
+* consumes ``ccd-customer-response`` and signals the waiting fraud process, counting
+  ``notifications.incoming{response}`` (README.md:528-530, 569, 605);
+* counts ``notifications.outgoing`` when a fraud process publishes its notification.
+"""
+from __future__ import annotations
+
+import json
+import threading
+from typing import Any, Dict, Optional
+
+import numpy as np
+
+from ..contracts.outcomes import CustomerResponse, Route
+from ..metrics.exporter import RouterMetrics
+from .rules import RuleSet
+
+
+class Router:
+    def __init__(self, rules: RuleSet, processes, metrics: Optional[RouterMetrics] = None,
+                 standard_mode: str = "count"):
+        if standard_mode not in ("count", "process"):
+            raise ValueError("standard_mode must be 'count' or 'process'")
+        self.rules = rules
+        self.processes = processes            # ProcessEngine or KieClient (start_fraud/start_standard/signal)
+        self.metrics = metrics or RouterMetrics()
+        self.standard_mode = standard_mode
+        self._lock = threading.Lock()
+        self.fraud_started = 0
+        self.signals_ok = 0
+        self.signals_stale = 0
+
+    # ------------------------------------------------------------------ scoring results
+    def on_scored(self, ids, customers, proba, X: Optional[np.ndarray] = None,
+                  amounts: Optional[np.ndarray] = None, routes: Optional[np.ndarray] = None) -> Dict[str, int]:
+        """A scored batch: ``routes`` from the GPU epilogue are used as-is when the rule set is
+        threshold-only; otherwise the rule set is evaluated vectorised on the batch."""
+        proba = np.asarray(proba).reshape(-1)
+        n = proba.shape[0]
+        if amounts is None and X is not None:
+            amounts = np.asarray(X)[:, -1]
+        if routes is None or self.rules.threshold_only is None:
+            routes = self.rules.evaluate(proba, X=X, amount=amounts)
+        routes = np.asarray(routes).reshape(-1)
+        fraud_idx = np.nonzero(routes == Route.FRAUD)[0]
+        self.metrics.tx_incoming.inc(n)
+        self.metrics.tx_outgoing.labels(type="fraud").inc(len(fraud_idx))
+        self.metrics.tx_outgoing.labels(type="standard").inc(n - len(fraud_idx))
+        for i in fraud_idx:
+            self._start_fraud(int(ids[i]), int(customers[i]) if customers is not None else 0,
+                              float(amounts[i]) if amounts is not None else 0.0, float(proba[i]))
+        if self.standard_mode == "process":
+            for i in np.nonzero(routes != Route.FRAUD)[0]:
+                self.processes.start_standard({"transaction_id": int(ids[i]), "proba": float(proba[i]),
+                                               "amount": float(amounts[i]) if amounts is not None else 0.0})
+        return {"incoming": n, "fraud": int(len(fraud_idx)), "standard": int(n - len(fraud_idx))}
+
+    def on_flagged(self, flagged: np.ndarray, total_rows: int) -> Dict[str, int]:
+        """Engine hot path: only fraud-routed rows are materialised on the host (the GPU
+        epilogue counted the rest).  ``flagged`` is the engine's flagged-record array."""
+        nf = int(len(flagged))
+        self.metrics.tx_incoming.inc(total_rows)
+        self.metrics.tx_outgoing.labels(type="fraud").inc(nf)
+        self.metrics.tx_outgoing.labels(type="standard").inc(total_rows - nf)
+        for r in flagged:
+            self._start_fraud(int(r["tx_id"]), int(r["customer"]), float(r["amount"]), float(r["proba"]))
+        return {"incoming": total_rows, "fraud": nf, "standard": total_rows - nf}
+
+    def _start_fraud(self, tx_id: int, customer: int, amount: float, proba: float) -> None:
+        self.processes.start_fraud({"transaction_id": tx_id, "customer_id": customer,
+                                    "amount": amount, "proba": proba})
+        with self._lock:
+            self.fraud_started += 1
+
+    # ------------------------------------------------------------------ notification loop
+    def on_notification_sent(self, _msg: Any = None) -> None:
+        self.metrics.notif_outgoing.inc()
+
+    def on_response(self, raw) -> bool:
+        msg = json.loads(raw) if isinstance(raw, (bytes, bytearray, str)) else raw
+        approved = bool(msg.get("response"))
+        self.metrics.notif_incoming.labels(
+            response=CustomerResponse.from_bool(approved).value).inc()
+        ok = self.processes.signal(int(msg["process_id"]), "customerResponse", approved)
+        with self._lock:
+            if ok:
+                self.signals_ok += 1
+            else:
+                self.signals_stale += 1
+        return ok

@@ -67,28 +67,43 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// Load one 16-row tile of a packed [n][30] f32 matrix (1920 contiguous bytes) into a
-// wave-private LDS tile with two 16-B loads per lane; rows >= n are zero-filled.
-// `avail` = valid bytes in this tile (multiple of 8).
-__device__ __forceinline__ void load_tile_contig(const float* __restrict__ xt, int avail,
-                                                 float* lds_tile, int lane) {
+// One 16-row tile of a packed [n][30] f32 matrix is 1920 contiguous bytes = 120 float4:
+// lane l fetches float4 l and l+64 (full-width coalesced requests, also over PCIe for a
+// host-mapped log).  Split into issue (global -> registers) and store (registers ->
+// wave-private LDS tile) so the next tile's fetch is in flight while this one computes.
+// `avail` = valid bytes in the tile (multiple of 8); bytes past it are zero-filled.
+struct TileRegs { float4 v[2]; };
+
+__device__ __forceinline__ void tile_issue(const float* __restrict__ xt, int avail, int lane, TileRegs& r) {
   const float4* src = reinterpret_cast<const float4*>(xt);
-  float4* dst = reinterpret_cast<float4*>(lds_tile);
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int i = lane + 64 * it;          // float4 index, 120 per tile
+    const int i = lane + 64 * it;
+    const int off = i * 16;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < kTileBytes / 16) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int off = i * 16;
       if (off + 16 <= avail) {
         v = src[i];
       } else if (off + 8 <= avail) {
         const float2 h = reinterpret_cast<const float2*>(xt)[2 * i];
         v.x = h.x; v.y = h.y;
       }
-      dst[i] = v;
     }
+    r.v[it] = v;
   }
+}
+
+__device__ __forceinline__ void tile_store(float* lds_tile, int lane, const TileRegs& r) {
+  float4* dst = reinterpret_cast<float4*>(lds_tile);
+  dst[lane] = r.v[0];
+  if (lane + 64 < kTileBytes / 16) dst[lane + 64] = r.v[1];
+}
+
+__device__ __forceinline__ void load_tile_contig(const float* __restrict__ xt, int avail,
+                                                 float* lds_tile, int lane) {
+  TileRegs r;
+  tile_issue(xt, avail, lane, r);
+  tile_store(lds_tile, lane, r);
 }
 
 }  // namespace ccfd

@@ -44,7 +44,9 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
 
 void* ccfd_host_alloc(size_t bytes) {
   void* p = nullptr;
-  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable);
+  // NumaUser: pages follow the calling thread's NUMA policy (the rank binds itself to its
+  // GPU's socket first, utils/numa.py), so the GPU reads local DRAM over its own PCIe root.
+  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocNumaUser);
   if (e != hipSuccess) {
     ccfd::set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
     return nullptr;

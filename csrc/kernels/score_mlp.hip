@@ -39,7 +39,17 @@ __global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
+  const int ntiles = (a.n + kTileRows - 1) / kTileRows;
+  const int tstride = gridDim.x * kWaves;
+  int tile = blockIdx.x * kWaves + wave;
 
+  // Issue this wave's first input tile BEFORE staging the weights: the (possibly PCIe)
+  // fetch latency of x overlaps the L2 fetch of the model blob.
+  TileRegs pre;
+  auto tile_avail = [&](int t) { return min(kTileRows, a.n - t * kTileRows) * kF * 4; };
+  if constexpr (kContig) {
+    if (tile < ntiles) tile_issue(a.x + (size_t)tile * kTileRows * kF, tile_avail(tile), lane, pre);
+  }
   {  // stage the packed model: 1620 x 16 B
     const int4* src = reinterpret_cast<const int4*>(a.blob);
     int4* dst = reinterpret_cast<int4*>(sblob);
@@ -70,17 +80,18 @@ __global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
 
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
-  const int ntiles = (a.n + kTileRows - 1) / kTileRows;
   float* tile_lds = sx[wave];
 
-  for (int tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
+  for (; tile < ntiles; tile += tstride) {
     const int row = tile * kTileRows + c;
     const bool valid = row < a.n;
     float xv[8];
     if constexpr (kContig) {
-      const int rows_here = min(kTileRows, a.n - tile * kTileRows);
-      load_tile_contig(a.x + (size_t)tile * kTileRows * kF, rows_here * kF * 4, tile_lds, lane);
-      // wave-private tile: a wave barrier orders the ds_write before the ds_read
+      tile_store(tile_lds, lane, pre);
+      // prefetch the next tile of this wave while this one computes
+      const int nxt = tile + tstride;
+      if (nxt < ntiles) tile_issue(a.x + (size_t)nxt * kTileRows * kF, tile_avail(nxt), lane, pre);
+      // wave-private tile: LDS ops of one wave complete in order
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       const float2* r2 = reinterpret_cast<const float2*>(tile_lds + c * kF + 8 * g);
