@@ -44,7 +44,7 @@ def generate(n: int, seed: int = 0, fraud_rate: float = FRAUD_RATE, start_time: 
         m = min(chunk, n - s)
         lab = (rng.random(m) < fraud_rate)
         v = rng.standard_normal((m, 28), dtype=np.float32) * V_STD
-        v[lab] += V_FRAUD_SHIFT * rng.uniform(0.5, 1.5, (int(lab.sum()), 1)).astype(np.float32)
+        v[lab] += V_FRAUD_SHIFT * rng.uniform(0.15, 1.2, (int(lab.sum()), 1)).astype(np.float32)
         amt = np.exp(rng.normal(AMOUNT_LOG_MU, AMOUNT_LOG_SIGMA, m)).astype(np.float32)
         amt[lab] *= rng.uniform(0.3, 3.0, int(lab.sum())).astype(np.float32)
         np.minimum(amt, AMOUNT_MAX, out=amt)

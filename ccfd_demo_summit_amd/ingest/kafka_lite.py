@@ -1,0 +1,247 @@
+"""``kafka-lite``: a single-node broker speaking the Kafka wire protocol subset of
+``kafka_wire`` on top of the in-process log store.
+
+Stands in for the reference's 3-broker Strimzi cluster (deploy/frauddetection_cr.yaml:
+73-77) in development, CI and single-node deployments: every service of the framework
+(producer, engine/router, KIE, notifier) can run as a separate process and talk real Kafka
+protocol to it, and switching to a production cluster is only a ``BROKER_URL`` change.
+
+    python -m ccfd_demo_summit_amd.ingest.kafka_lite --port 9092 --partitions 8
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import struct
+import threading
+from typing import Optional
+
+from .broker import InProcBroker
+from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS,
+                         ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, FETCH, FIND_COORDINATOR, LIST_OFFSETS,
+                         METADATA, OFFSET_COMMIT, OFFSET_FETCH, PRODUCE, SUPPORTED, Reader, Writer,
+                         decode_record_batches, encode_record_batch)
+
+NODE_ID = 1
+
+
+class KafkaLiteServer:
+    def __init__(self, host: str = "127.0.0.1", port: int = 9092, default_partitions: int = 1,
+                 store: Optional[InProcBroker] = None, auto_create: bool = True):
+        self.host = host
+        self.port = port
+        self.store = store or InProcBroker(default_partitions=default_partitions)
+        self.auto_create = auto_create
+        self._server: Optional[asyncio.base_events.Server] = None
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._thread: Optional[threading.Thread] = None
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self):
+        self._server = await asyncio.start_server(self._serve, self.host, self.port)
+        self.port = self._server.sockets[0].getsockname()[1]
+
+    def start_in_thread(self) -> "KafkaLiteServer":
+        ready = threading.Event()
+
+        def run():
+            self._loop = asyncio.new_event_loop()
+            self._loop.run_until_complete(self.start())
+            ready.set()
+            self._loop.run_forever()
+        self._thread = threading.Thread(target=run, daemon=True, name="kafka-lite")
+        self._thread.start()
+        ready.wait(10)
+        return self
+
+    def stop(self):
+        if self._loop is not None:
+            def _close():
+                self._server.close()
+                self._loop.stop()
+            self._loop.call_soon_threadsafe(_close)
+            self._thread.join(5)
+
+    @property
+    def bootstrap(self) -> str:
+        return f"{self.host}:{self.port}"
+
+    # ------------------------------------------------------------------ connection loop
+    async def _serve(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
+        try:
+            while True:
+                hdr = await reader.readexactly(4)
+                size = struct.unpack(">i", hdr)[0]
+                msg = await reader.readexactly(size)
+                r = Reader(msg)
+                api, ver, corr = r.i16(), r.i16(), r.i32()
+                r.string()                                  # client id
+                body = self._dispatch(api, ver, r)
+                out = struct.pack(">i", corr) + body
+                writer.write(struct.pack(">i", len(out)) + out)
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionError):
+            pass
+        finally:
+            writer.close()
+
+    def _topic(self, name: str) -> bool:
+        if name in self.store.topics():
+            return True
+        if self.auto_create:
+            self.store.create_topic(name)
+            return True
+        return False
+
+    def _dispatch(self, api: int, ver: int, r: Reader) -> bytes:
+        if api not in SUPPORTED or ver > SUPPORTED[api]:
+            return Writer().i16(ERR_UNSUPPORTED_VERSION).build()
+        return getattr(self, f"_api_{api}")(r)
+
+    # ------------------------------------------------------------------ APIs
+    def _api_18(self, r: Reader) -> bytes:                  # ApiVersions v0
+        return Writer().i16(ERR_NONE).array(sorted(SUPPORTED.items()), lambda w, kv: w.i16(kv[0]).i16(0).i16(kv[1])).build()
+
+    def _api_3(self, r: Reader) -> bytes:                   # Metadata v1
+        topics = r.array(lambda x: x.string())
+        names = sorted(self.store.topics()) if topics is None else topics
+        w = Writer().array([(NODE_ID, self.host, self.port)], lambda w_, b: w_.i32(b[0]).string(b[1]).i32(b[2]).string(None))
+        w.i32(NODE_ID)
+
+        def topic(w_, name):
+            if not self._topic(name):
+                w_.i16(ERR_UNKNOWN_TOPIC).string(name).i8(0).array([], None)
+                return
+            n = self.store.partitions(name)
+            w_.i16(ERR_NONE).string(name).i8(0).array(range(n), lambda w2, p: w2.i16(0).i32(p).i32(NODE_ID)
+                                                   .array([NODE_ID], lambda w3, x: w3.i32(x))
+                                                   .array([NODE_ID], lambda w3, x: w3.i32(x)))
+        w.array(names, topic)
+        return w.build()
+
+    def _api_19(self, r: Reader) -> bytes:                  # CreateTopics v0
+        def req(x):
+            name, n, _rf = x.string(), x.i32(), x.i16()
+            x.array(lambda y: (y.i32(), y.array(lambda z: z.i32())))
+            x.array(lambda y: (y.string(), y.string()))
+            return name, n
+        reqs = r.array(req)
+        r.i32()
+        res = []
+        for name, n in reqs:
+            if name in self.store.topics():
+                res.append((name, ERR_TOPIC_EXISTS))
+            else:
+                self.store.create_topic(name, max(1, n))
+                res.append((name, ERR_NONE))
+        return Writer().array(res, lambda w, t: w.string(t[0]).i16(t[1])).build()
+
+    def _api_0(self, r: Reader) -> bytes:                   # Produce v3
+        r.string(); r.i16(); r.i32()
+        data = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.bytes_()))))
+        resp = []
+        for topic, parts in data:
+            pr = []
+            self._topic(topic)
+            for p, rb in parts:
+                try:
+                    recs = decode_record_batches(rb or b"", topic, p)
+                    base = self.store.end_offset(topic, p)
+                    for rec in recs:
+                        self.store.produce(topic, rec.value, key=rec.key, partition=p)
+                    pr.append((p, ERR_NONE, base))
+                except Exception:
+                    pr.append((p, 2, -1))
+            resp.append((topic, pr))
+        w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
+        return w.i32(0).build()
+
+    def _api_1(self, r: Reader) -> bytes:                   # Fetch v4
+        r.i32(); r.i32(); r.i32(); max_bytes = r.i32(); r.i8()
+        reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.i32()))))
+        resp = []
+        for topic, parts in reqs:
+            pr = []
+            for p, off, pmax in parts:
+                if topic not in self.store.topics() or p >= self.store.partitions(topic):
+                    pr.append((p, ERR_UNKNOWN_TOPIC, -1, None))
+                    continue
+                hw = self.store.end_offset(topic, p)
+                if off < self.store.begin_offset(topic, p) or off > hw:
+                    pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))
+                    continue
+                recs, size = [], 0
+                for rec in self.store.fetch(topic, p, off, 100_000):
+                    size += len(rec.value or b"") + 32
+                    if recs and size > min(pmax, max_bytes):
+                        break
+                    recs.append(rec)
+                rb = encode_record_batch([x.value for x in recs], [x.key for x in recs], base_offset=off) if recs else b""
+                pr.append((p, ERR_NONE, hw, rb))
+            resp.append((topic, pr))
+        w = Writer().i32(0)
+        w.array(resp, lambda w_, t: w_.string(t[0]).array(
+            t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(q[2]).array([], None).bytes_(q[3])))
+        return w.build()
+
+    def _api_2(self, r: Reader) -> bytes:                   # ListOffsets v1
+        r.i32()
+        reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64()))))
+        resp = []
+        for topic, parts in reqs:
+            pr = []
+            for p, ts in parts:
+                if not self._topic(topic) or p >= self.store.partitions(topic):
+                    pr.append((p, ERR_UNKNOWN_TOPIC, -1))
+                    continue
+                off = self.store.begin_offset(topic, p) if ts == -2 else self.store.end_offset(topic, p)
+                pr.append((p, ERR_NONE, off))
+            resp.append((topic, pr))
+        return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
+            t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(-1).i64(q[2]))).build()
+
+    def _api_10(self, r: Reader) -> bytes:                  # FindCoordinator v0
+        r.string()
+        return Writer().i16(ERR_NONE).i32(NODE_ID).string(self.host).i32(self.port).build()
+
+    def _api_8(self, r: Reader) -> bytes:                   # OffsetCommit v2
+        group = r.string(); r.i32(); r.string(); r.i64()
+        reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.string()))))
+        resp = []
+        for topic, parts in reqs:
+            for p, off, _m in parts:
+                self.store.commit(group, topic, p, off)
+            resp.append((topic, [(p, ERR_NONE) for p, _o, _m in parts]))
+        return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]))).build()
+
+    def _api_9(self, r: Reader) -> bytes:                   # OffsetFetch v1
+        group = r.string()
+        reqs = r.array(lambda x: (x.string(), x.array(lambda y: y.i32())))
+        resp = []
+        for topic, parts in reqs:
+            pr = []
+            for p in parts:
+                c = self.store.committed(group, topic, p)
+                pr.append((p, -1 if c is None else c))
+            resp.append((topic, pr))
+        return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
+            t[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).string(None).i16(ERR_NONE))).build()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=9092)
+    ap.add_argument("--partitions", type=int, default=8)
+    a = ap.parse_args(argv)
+    srv = KafkaLiteServer(a.host, a.port, a.partitions)
+
+    async def run():
+        await srv.start()
+        print(f"[kafka-lite] listening on {a.host}:{srv.port}", flush=True)
+        await asyncio.Event().wait()
+    asyncio.run(run())
+
+
+if __name__ == "__main__":
+    main()

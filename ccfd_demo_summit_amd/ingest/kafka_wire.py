@@ -1,0 +1,545 @@
+"""Kafka wire protocol (subset) -- client side, no third-party Kafka library.
+
+The reference's services talk to a Strimzi Kafka cluster at ``BROKER_URL``
+(``odh-message-bus-kafka-brokers:9092``, deploy/router.yaml:55-56).  There is no Kafka
+client in this image, so the framework speaks the protocol itself:
+
+  ApiVersions v0, Metadata v1, Produce v3, Fetch v4, ListOffsets v1, FindCoordinator v0,
+  OffsetCommit v2, OffsetFetch v1, CreateTopics v0   (all non-flexible encodings)
+
+Records use RecordBatch v2 (magic 2) with CRC-32C computed by the native library
+(csrc/engine/crc32c.cpp, SSE4.2) or a table fallback.  ``KafkaBroker`` exposes the same
+interface as ``InProcBroker`` (produce / fetch / offsets / commit / consumer), so every
+service runs unchanged against either.  Consumers use static partition assignment (the
+engine's ``p % world == rank`` sharding) and commit offsets under their group id;
+the group-membership rebalance protocol (JoinGroup/SyncGroup) is not implemented.
+"""
+from __future__ import annotations
+
+import itertools
+import socket
+import struct
+import threading
+import time
+import zlib
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+from .broker import BrokerError, Record
+
+# --------------------------------------------------------------------------- api keys
+PRODUCE, FETCH, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH, FIND_COORDINATOR = 0, 1, 2, 3, 8, 9, 10
+API_VERSIONS, CREATE_TOPICS = 18, 19
+SUPPORTED = {PRODUCE: 3, FETCH: 4, LIST_OFFSETS: 1, METADATA: 1, OFFSET_COMMIT: 2, OFFSET_FETCH: 1,
+             FIND_COORDINATOR: 0, API_VERSIONS: 0, CREATE_TOPICS: 0}
+
+ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_UNKNOWN_TOPIC, ERR_CORRUPT = 0, 1, 3, 2
+ERR_UNSUPPORTED_VERSION, ERR_TOPIC_EXISTS, ERR_INVALID_REQUEST = 35, 36, 42
+
+# --------------------------------------------------------------------------- crc32c
+_CRC_TABLE = None
+
+
+def _crc32c_py(data: bytes, crc: int = 0) -> int:
+    global _CRC_TABLE
+    if _CRC_TABLE is None:
+        t = []
+        for i in range(256):
+            c = i
+            for _ in range(8):
+                c = (c >> 1) ^ 0x82F63B78 if c & 1 else c >> 1
+            t.append(c)
+        _CRC_TABLE = t
+    crc ^= 0xFFFFFFFF
+    for b in data:
+        crc = _CRC_TABLE[(crc ^ b) & 0xFF] ^ (crc >> 8)
+    return crc ^ 0xFFFFFFFF
+
+
+_native_crc = None
+
+
+def crc32c(data: bytes) -> int:
+    global _native_crc
+    if _native_crc is None:
+        try:
+            import ctypes as C
+            from ..ops._lib import lib
+            f = lib().ccfd_crc32c
+            f.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
+            f.restype = C.c_uint32
+            _native_crc = f
+        except Exception:
+            _native_crc = False
+    if _native_crc:
+        return int(_native_crc(bytes(data), len(data), 0))
+    return _crc32c_py(data)
+
+
+# --------------------------------------------------------------------------- primitives
+class Writer:
+    __slots__ = ("parts",)
+
+    def __init__(self):
+        self.parts: List[bytes] = []
+
+    def i8(self, v):
+        self.parts.append(struct.pack(">b", v)); return self
+
+    def i16(self, v):
+        self.parts.append(struct.pack(">h", v)); return self
+
+    def i32(self, v):
+        self.parts.append(struct.pack(">i", v)); return self
+
+    def u32(self, v):
+        self.parts.append(struct.pack(">I", v)); return self
+
+    def i64(self, v):
+        self.parts.append(struct.pack(">q", v)); return self
+
+    def string(self, s: Optional[str]):
+        if s is None:
+            return self.i16(-1)
+        b = s.encode()
+        self.i16(len(b)); self.parts.append(b); return self
+
+    def bytes_(self, b: Optional[bytes]):
+        if b is None:
+            return self.i32(-1)
+        self.i32(len(b)); self.parts.append(bytes(b)); return self
+
+    def array(self, items, fn):
+        if items is None:
+            return self.i32(-1)
+        items = list(items)
+        self.i32(len(items))
+        for it in items:
+            fn(self, it)
+        return self
+
+    def raw(self, b: bytes):
+        self.parts.append(b); return self
+
+    def build(self) -> bytes:
+        return b"".join(self.parts)
+
+
+class Reader:
+    __slots__ = ("b", "o")
+
+    def __init__(self, b: bytes, o: int = 0):
+        self.b = memoryview(b)
+        self.o = o
+
+    def _u(self, fmt, n):
+        v = struct.unpack_from(fmt, self.b, self.o)[0]
+        self.o += n
+        return v
+
+    def i8(self): return self._u(">b", 1)
+    def i16(self): return self._u(">h", 2)
+    def i32(self): return self._u(">i", 4)
+    def u32(self): return self._u(">I", 4)
+    def i64(self): return self._u(">q", 8)
+
+    def string(self) -> Optional[str]:
+        n = self.i16()
+        if n < 0:
+            return None
+        s = bytes(self.b[self.o:self.o + n]).decode()
+        self.o += n
+        return s
+
+    def bytes_(self) -> Optional[bytes]:
+        n = self.i32()
+        if n < 0:
+            return None
+        v = bytes(self.b[self.o:self.o + n])
+        self.o += n
+        return v
+
+    def array(self, fn) -> Optional[list]:
+        n = self.i32()
+        if n < 0:
+            return None
+        return [fn(self) for _ in range(n)]
+
+    def remaining(self) -> int:
+        return len(self.b) - self.o
+
+
+def _zigzag(v: int) -> int:
+    return (v << 1) ^ (v >> 63)
+
+
+def _varint(v: int) -> bytes:
+    v = _zigzag(v) & 0xFFFFFFFFFFFFFFFF
+    out = bytearray()
+    while True:
+        if v < 0x80:
+            out.append(v)
+            return bytes(out)
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+
+
+def _read_varint(mv, o: int) -> Tuple[int, int]:
+    shift = 0
+    v = 0
+    while True:
+        b = mv[o]
+        o += 1
+        v |= (b & 0x7F) << shift
+        if not b & 0x80:
+            break
+        shift += 7
+    return (v >> 1) ^ -(v & 1), o
+
+
+# --------------------------------------------------------------------------- RecordBatch v2
+def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optional[bytes]]] = None,
+                        base_offset: int = 0, timestamp_ms: Optional[int] = None) -> bytes:
+    ts = int(time.time() * 1000) if timestamp_ms is None else timestamp_ms
+    recs = []
+    for i, v in enumerate(values):
+        k = keys[i] if keys is not None else None
+        body = b"".join([b"\x00", _varint(0), _varint(i),
+                         _varint(-1) if k is None else _varint(len(k)) + k,
+                         _varint(-1) if v is None else _varint(len(v)) + bytes(v), _varint(0)])
+        recs.append(_varint(len(body)) + body)
+    n = len(values)
+    after_crc = struct.pack(">hiqqqhii", 0, max(n - 1, 0), ts, ts, -1, -1, -1, n) + b"".join(recs)
+    crc = crc32c(after_crc)
+    head = struct.pack(">ibI", 0, 2, crc)                 # partitionLeaderEpoch, magic, crc
+    batch_len = len(head) + len(after_crc)
+    return struct.pack(">qi", base_offset, batch_len) + head + after_crc
+
+
+def decode_record_batches(data: bytes, topic: str = "", partition: int = 0,
+                          verify_crc: bool = True) -> List[Record]:
+    out: List[Record] = []
+    mv = memoryview(data)
+    o = 0
+    while o + 12 <= len(data):
+        base_offset, batch_len = struct.unpack_from(">qi", mv, o)
+        end = o + 12 + batch_len
+        if end > len(data):
+            break                                          # partial batch at the end of a fetch
+        _epoch, magic, crc = struct.unpack_from(">ibI", mv, o + 12)
+        if magic != 2:
+            raise BrokerError(f"unsupported record batch magic {magic}")
+        body = mv[o + 21:end]
+        if verify_crc and crc32c(bytes(body)) != crc:
+            raise BrokerError("record batch CRC mismatch")
+        (attrs, _lod, base_ts, _max_ts, _pid, _pep, _bseq, count) = struct.unpack_from(">hiqqqhii", body, 0)
+        if attrs & 0x7:
+            raise BrokerError("compressed record batches are not supported")
+        p = 40 + 21   # header bytes before records, relative to o
+        q = o + p
+        for _ in range(count):
+            ln, q = _read_varint(mv, q)
+            rend = q + ln
+            q += 1                                         # record attributes
+            tsd, q = _read_varint(mv, q)
+            od, q = _read_varint(mv, q)
+            kl, q = _read_varint(mv, q)
+            key = None if kl < 0 else bytes(mv[q:q + kl])
+            q += max(kl, 0)
+            vl, q = _read_varint(mv, q)
+            val = None if vl < 0 else bytes(mv[q:q + vl])
+            q = rend
+            out.append(Record(topic, partition, base_offset + od, key, val, (base_ts + tsd) / 1000.0))
+        o = end
+    return out
+
+
+# --------------------------------------------------------------------------- framing
+def encode_request(api_key: int, version: int, corr: int, client_id: str, body: bytes) -> bytes:
+    hdr = Writer().i16(api_key).i16(version).i32(corr).string(client_id).build()
+    msg = hdr + body
+    return struct.pack(">i", len(msg)) + msg
+
+
+def _recv_exact(sock: socket.socket, n: int) -> bytes:
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("kafka connection closed")
+        buf += chunk
+    return bytes(buf)
+
+
+class Connection:
+    def __init__(self, host: str, port: int, client_id: str = "ccfd-mi355x", timeout: float = 10.0):
+        self.sock = socket.create_connection((host, port), timeout=timeout)
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self.client_id = client_id
+        self._corr = itertools.count(1)
+        self._lock = threading.Lock()
+
+    def request(self, api_key: int, version: int, body: bytes) -> Reader:
+        with self._lock:
+            corr = next(self._corr)
+            self.sock.sendall(encode_request(api_key, version, corr, self.client_id, body))
+            size = struct.unpack(">i", _recv_exact(self.sock, 4))[0]
+            resp = _recv_exact(self.sock, size)
+        r = Reader(resp)
+        got = r.i32()
+        if got != corr:
+            raise BrokerError(f"correlation id mismatch {got} != {corr}")
+        return r
+
+    def close(self):
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
+# --------------------------------------------------------------------------- client
+class KafkaBroker:
+    """Kafka-protocol implementation of the InProcBroker interface (single bootstrap node;
+    partition leaders are looked up from Metadata and connected lazily)."""
+
+    def __init__(self, bootstrap: str, client_id: str = "ccfd-mi355x", timeout: float = 10.0):
+        host, port = bootstrap.rsplit(":", 1)
+        self.timeout = timeout
+        self.client_id = client_id
+        self._bootstrap = (host, int(port))
+        self._conns: Dict[int, Connection] = {}
+        self._nodes: Dict[int, Tuple[str, int]] = {}
+        self._leaders: Dict[Tuple[str, int], int] = {}
+        self._partitions: Dict[str, int] = {}
+        self._boot = Connection(host, int(port), client_id, timeout)
+        self._rr = itertools.count()
+        self.api_versions = self._api_versions()
+
+    def _api_versions(self) -> Dict[int, Tuple[int, int]]:
+        r = self._boot.request(API_VERSIONS, 0, b"")
+        err = r.i16()
+        if err:
+            raise BrokerError(f"ApiVersions error {err}")
+        return {k: (lo, hi) for k, lo, hi in r.array(lambda x: (x.i16(), x.i16(), x.i16()))}
+
+    def _conn(self, node: int) -> Connection:
+        if node not in self._conns:
+            host, port = self._nodes.get(node, self._bootstrap)
+            try:
+                self._conns[node] = Connection(host, port, self.client_id, self.timeout)
+            except OSError:
+                self._conns[node] = Connection(*self._bootstrap, self.client_id, self.timeout)
+        return self._conns[node]
+
+    def metadata(self, topics: Optional[Sequence[str]] = None) -> Dict[str, int]:
+        body = Writer().array(topics, lambda w, t: w.string(t)).build()
+        r = self._boot.request(METADATA, 1, body)
+        brokers = r.array(lambda x: (x.i32(), x.string(), x.i32(), x.string()))
+        for nid, host, port, _rack in brokers:
+            self._nodes[nid] = (host, port)
+        r.i32()                                             # controller id
+
+        def part(x):
+            return x.i16(), x.i32(), x.i32(), x.array(lambda y: y.i32()), x.array(lambda y: y.i32())
+        out = {}
+        for err, name, _internal, parts in r.array(lambda x: (x.i16(), x.string(), x.i8(), x.array(part))):
+            if err:
+                continue
+            out[name] = len(parts)
+            self._partitions[name] = len(parts)
+            for _e, idx, leader, _rep, _isr in parts:
+                self._leaders[(name, idx)] = leader
+        return out
+
+    def create_topic(self, name: str, partitions: Optional[int] = None) -> None:
+        if name in self._partitions or name in self.metadata([name]):
+            return
+        body = (Writer().array([name], lambda w, t: w.string(t).i32(partitions or 1).i16(1)
+                               .array([], None).array([], None)).i32(int(self.timeout * 1000)).build())
+        r = self._boot.request(CREATE_TOPICS, 0, body)
+        for tname, err in r.array(lambda x: (x.string(), x.i16())):
+            if err not in (ERR_NONE, ERR_TOPIC_EXISTS):
+                raise BrokerError(f"CreateTopics {tname}: error {err}")
+        self.metadata([name])
+
+    def partitions(self, topic: str) -> int:
+        if topic not in self._partitions:
+            self.metadata([topic])
+        if topic not in self._partitions:
+            self.create_topic(topic)
+        return self._partitions[topic]
+
+    def _leader(self, topic: str, partition: int) -> Connection:
+        if (topic, partition) not in self._leaders:
+            self.metadata([topic])
+        return self._conn(self._leaders.get((topic, partition), -1))
+
+    # ---------------------------------------------------------------- produce
+    def produce_batch(self, topic: str, partition: int, values: Sequence[bytes],
+                      keys: Optional[Sequence[Optional[bytes]]] = None, acks: int = 1) -> int:
+        rb = encode_record_batch(values, keys)
+        body = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000))
+                .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).bytes_(rb)))
+                .build())
+        r = self._leader(topic, partition).request(PRODUCE, 3, body)
+        resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+        _name, parts = resp[0]
+        _p, err, base, _ts = parts[0]
+        if err:
+            raise BrokerError(f"produce {topic}[{partition}] error {err}")
+        return base
+
+    def produce(self, topic: str, value: bytes, key: Optional[bytes] = None, partition: Optional[int] = None,
+                headers: Tuple = ()) -> Tuple[int, int]:
+        n = self.partitions(topic)
+        if partition is None:
+            partition = (zlib.crc32(key) % n) if key is not None else next(self._rr) % n
+        return partition, self.produce_batch(topic, partition, [value], [key])
+
+    def produce_many(self, topic: str, values: Iterable[bytes], partition: Optional[int] = None) -> int:
+        vals = list(values)
+        if partition is None:
+            n = self.partitions(topic)
+            by: Dict[int, List[bytes]] = {}
+            for v in vals:
+                by.setdefault(next(self._rr) % n, []).append(v)
+            for p, vs in by.items():
+                self.produce_batch(topic, p, vs)
+        else:
+            self.produce_batch(topic, partition, vals)
+        return len(vals)
+
+    # ---------------------------------------------------------------- fetch / offsets
+    def fetch(self, topic: str, partition: int, offset: int, max_records: int = 1000,
+              max_bytes: int = 64 << 20, max_wait_ms: int = 0) -> List[Record]:
+        body = (Writer().i32(-1).i32(max_wait_ms).i32(1 if max_wait_ms else 0).i32(max_bytes).i8(0)
+                .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).i64(offset).i32(max_bytes)))
+                .build())
+        r = self._leader(topic, partition).request(FETCH, 4, body)
+        r.i32()                                             # throttle
+
+        def part(x):
+            idx, err, hw, _lso = x.i32(), x.i16(), x.i64(), x.i64()
+            x.array(lambda y: (y.i64(), y.i64()))
+            return idx, err, hw, x.bytes_()
+        resp = r.array(lambda x: (x.string(), x.array(part)))
+        out: List[Record] = []
+        for _t, parts in resp:
+            for idx, err, _hw, recs in parts:
+                if err == ERR_OFFSET_OUT_OF_RANGE:
+                    return self.fetch(topic, partition, self.begin_offset(topic, partition), max_records, max_bytes)
+                if err:
+                    raise BrokerError(f"fetch {topic}[{idx}] error {err}")
+                if recs:
+                    out.extend(r_ for r_ in decode_record_batches(recs, topic, idx) if r_.offset >= offset)
+        return out[:max_records]
+
+    def _list_offset(self, topic: str, partition: int, ts: int) -> int:
+        body = Writer().i32(-1).array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).i64(ts))).build()
+        r = self._leader(topic, partition).request(LIST_OFFSETS, 1, body)
+        resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+        _p, err, _ts, off = resp[0][1][0]
+        if err:
+            raise BrokerError(f"list offsets {topic}[{partition}] error {err}")
+        return off
+
+    def end_offset(self, topic: str, partition: int) -> int:
+        return self._list_offset(topic, partition, -1)
+
+    def begin_offset(self, topic: str, partition: int) -> int:
+        return self._list_offset(topic, partition, -2)
+
+    def commit(self, group: str, topic: str, partition: int, offset: int) -> None:
+        body = (Writer().string(group).i32(-1).string("").i64(-1)
+                .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).i64(offset).string(None)))
+                .build())
+        r = self._boot.request(OFFSET_COMMIT, 2, body)
+        for _t, parts in r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16())))):
+            for p, err in parts:
+                if err:
+                    raise BrokerError(f"offset commit {topic}[{p}] error {err}")
+
+    def committed(self, group: str, topic: str, partition: int) -> Optional[int]:
+        body = Writer().string(group).array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p))).build()
+        r = self._boot.request(OFFSET_FETCH, 1, body)
+        resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.string(), y.i16()))))
+        _p, off, _meta, err = resp[0][1][0]
+        return None if off < 0 else off
+
+    def lag(self, group: str, topic: str) -> int:
+        tot = 0
+        for p in range(self.partitions(topic)):
+            c = self.committed(group, topic, p)
+            tot += self.end_offset(topic, p) - (c if c is not None else self.begin_offset(topic, p))
+        return tot
+
+    def consumer(self, group: str, topics: Sequence[str], partitions: Optional[Sequence[Tuple[str, int]]] = None,
+                 member_id: Optional[str] = None, auto_commit: bool = False) -> "WireConsumer":
+        return WireConsumer(self, group, list(topics), partitions, auto_commit)
+
+    def wait_for_data(self, predicate, timeout: float) -> bool:
+        end = time.monotonic() + timeout
+        while time.monotonic() < end:
+            if predicate():
+                return True
+            time.sleep(0.005)
+        return predicate()
+
+    def close(self):
+        self._boot.close()
+        for c in self._conns.values():
+            c.close()
+
+
+class WireConsumer:
+    """Statically assigned consumer (``partitions`` or every partition of ``topics``)."""
+
+    def __init__(self, broker: KafkaBroker, group: str, topics: List[str],
+                 partitions: Optional[Sequence[Tuple[str, int]]], auto_commit: bool):
+        self.broker = broker
+        self.group = group
+        self.topics = topics
+        self.auto_commit = auto_commit
+        if partitions is None:
+            partitions = [(t, p) for t in topics for p in range(broker.partitions(t))]
+        self._assignment = list(partitions)
+        self._positions = {}
+        for t, p in self._assignment:
+            c = broker.committed(group, t, p)
+            self._positions[(t, p)] = c if c is not None else broker.begin_offset(t, p)
+        self.closed = False
+
+    @property
+    def assignment(self):
+        return list(self._assignment)
+
+    def poll(self, timeout: float = 0.0, max_records: int = 500) -> List[Record]:
+        out: List[Record] = []
+        end = time.monotonic() + timeout
+        while True:
+            for tp in self._assignment:
+                if len(out) >= max_records:
+                    break
+                recs = self.broker.fetch(tp[0], tp[1], self._positions[tp], max_records - len(out))
+                if recs:
+                    self._positions[tp] = recs[-1].offset + 1
+                    out.extend(recs)
+            if out or time.monotonic() >= end:
+                break
+            time.sleep(0.002)
+        if self.auto_commit and out:
+            self.commit()
+        return out
+
+    def commit(self, offsets=None) -> None:
+        for (t, p), o in (offsets or self._positions).items():
+            self.broker.commit(self.group, t, p, o)
+
+    def position(self, topic: str, partition: int) -> int:
+        return self._positions[(topic, partition)]
+
+    def seek(self, topic: str, partition: int, offset: int) -> None:
+        self._positions[(topic, partition)] = offset
+
+    def close(self) -> None:
+        self.closed = True

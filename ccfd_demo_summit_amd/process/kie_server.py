@@ -1,0 +1,169 @@
+"""KIE-Server-compatible REST front of the process engine (replaces ``ccd-service``:
+deploy/ccd-service.yaml, port 8090; metrics at ``/rest/metrics``, README.md:509-514).
+
+KIE Server REST paths ([EXT], container/process/signal ids configurable):
+  POST /services/rest/server/containers/{c}/processes/{p}/instances            -> instance id
+  POST /services/rest/server/containers/{c}/processes/instances/{i}/signal/{s} -> signal
+  GET  /services/rest/server/containers/{c}/processes/instances/{i}            -> instance
+  GET  /services/rest/server/queries/tasks/instances/pot-owners                -> task list
+  GET  /services/rest/server/containers/{c}/tasks/{t}                          -> task
+  PUT  /services/rest/server/containers/{c}/tasks/{t}/states/completed         -> complete
+  GET  /rest/metrics                                                           -> Prometheus
+A background task fires process timers (``ProcessEngine.tick``).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+from dataclasses import asdict
+from typing import Optional
+
+import requests
+from aiohttp import web
+
+from ..metrics.exporter import CONTENT_TYPE
+from .engine import ProcessEngine
+
+BASE = "/services/rest/server"
+
+
+class KieServer:
+    def __init__(self, engine: ProcessEngine, container_id: str = "ccd-fraud-kjar",
+                 fraud_process_id: str = "ccd-fraud-kjar.CCDProcess",
+                 standard_process_id: str = "ccd-fraud-kjar.StandardProcess", tick_s: float = 0.05):
+        self.engine = engine
+        self.container_id = container_id
+        self.fraud_pid = fraud_process_id
+        self.standard_pid = standard_process_id
+        self.tick_s = tick_s
+        self.app = web.Application()
+        r = self.app.router
+        r.add_post(BASE + "/containers/{c}/processes/{p}/instances", self.start)
+        r.add_post(BASE + "/containers/{c}/processes/instances/{i}/signal/{s}", self.signal)
+        r.add_get(BASE + "/containers/{c}/processes/instances/{i}", self.get_instance)
+        r.add_get(BASE + "/queries/tasks/instances/pot-owners", self.tasks)
+        r.add_get(BASE + "/containers/{c}/tasks/{t}", self.get_task)
+        r.add_put(BASE + "/containers/{c}/tasks/{t}/states/completed", self.complete_task)
+        r.add_get("/rest/metrics", self.metrics)
+        r.add_get(BASE, self.info)
+        self.app.on_startup.append(self._startup)
+        self.app.on_cleanup.append(self._cleanup)
+        self._ticker: Optional[asyncio.Task] = None
+
+    async def _startup(self, _app):
+        async def loop():
+            while True:
+                self.engine.tick()
+                await asyncio.sleep(self.tick_s)
+        self._ticker = asyncio.get_running_loop().create_task(loop())
+
+    async def _cleanup(self, _app):
+        if self._ticker:
+            self._ticker.cancel()
+
+    def _check_container(self, request) -> Optional[web.Response]:
+        c = request.match_info.get("c")
+        if c is not None and c != self.container_id:
+            return web.json_response({"type": "FAILURE", "msg": f"Container {c} is not instantiated."}, status=404)
+        return None
+
+    async def info(self, _request):
+        return web.json_response({"type": "SUCCESS", "msg": "Kie Server info",
+                                  "result": {"kie-server-info": {"id": "ccd-service", "version": "ccfd-mi355x",
+                                                                  "capabilities": ["BPM", "DMN", "Prometheus"]}}})
+
+    async def start(self, request: web.Request):
+        bad = self._check_container(request)
+        if bad:
+            return bad
+        pid = request.match_info["p"]
+        raw = await request.read()
+        variables = json.loads(raw) if raw else {}
+        if pid == self.standard_pid:
+            iid = self.engine.start_standard(variables)
+        elif pid == self.fraud_pid:
+            iid = self.engine.start_fraud(variables)
+        else:
+            return web.json_response({"type": "FAILURE", "msg": f"Could not find process definition {pid}"},
+                                     status=404)
+        return web.json_response(iid, status=201)
+
+    async def signal(self, request: web.Request):
+        bad = self._check_container(request)
+        if bad:
+            return bad
+        raw = await request.read()
+        payload = json.loads(raw) if raw else None
+        ok = self.engine.signal(int(request.match_info["i"]), request.match_info["s"], payload)
+        return web.Response(status=200 if ok else 404)
+
+    async def get_instance(self, request: web.Request):
+        inst = self.engine.get(int(request.match_info["i"]))
+        if inst is None:
+            return web.json_response({"type": "FAILURE"}, status=404)
+        d = asdict(inst)
+        d["state"] = inst.state.value
+        return web.json_response({"process-instance-id": inst.id, "process-id": inst.process_id,
+                                  "process-instance-state": 1 if inst.state.value != "completed" else 2,
+                                  "variables": inst.variables, "outcome": inst.outcome, "detail": d},
+                                 dumps=lambda o: json.dumps(o, default=str))
+
+    async def tasks(self, request: web.Request):
+        status = request.query.get("status", "Ready")
+        ts = self.engine.list_tasks(None if status == "all" else status)
+        return web.json_response({"task-summary": [
+            {"task-id": t.id, "task-name": t.name, "task-status": t.status, "task-proc-inst-id": t.instance_id,
+             "task-container-id": self.container_id, "suggested-outcome": t.suggested_outcome,
+             "confidence": t.confidence} for t in ts]})
+
+    async def get_task(self, request: web.Request):
+        t = self.engine.tasks.get(int(request.match_info["t"]))
+        if t is None:
+            return web.json_response({"type": "FAILURE"}, status=404)
+        return web.json_response(asdict(t), dumps=lambda o: json.dumps(o, default=str))
+
+    async def complete_task(self, request: web.Request):
+        raw = await request.read()
+        out = json.loads(raw) if raw else {}
+        outcome = out.get("outcome", out.get("approved"))
+        ok = self.engine.complete_task(int(request.match_info["t"]), str(outcome))
+        return web.Response(status=201 if ok else 404)
+
+    async def metrics(self, _request):
+        m = self.engine.metrics
+        body = m.expose() if m is not None else b""
+        return web.Response(body=body, headers={"Content-Type": CONTENT_TYPE})
+
+
+class KieClient:
+    """HTTP client with the ProcessEngine hand-off interface (router -> KIE, README.md:552,569)."""
+
+    def __init__(self, url: str, container_id: str = "ccd-fraud-kjar",
+                 fraud_process_id: str = "ccd-fraud-kjar.CCDProcess",
+                 standard_process_id: str = "ccd-fraud-kjar.StandardProcess",
+                 signal_name: str = "customerResponse", timeout_s: float = 5.0):
+        self.base = url.rstrip("/") + BASE
+        self.c = container_id
+        self.fraud_pid = fraud_process_id
+        self.standard_pid = standard_process_id
+        self.signal_name = signal_name
+        self.timeout = timeout_s
+        self.s = requests.Session()
+
+    def _start(self, pid: str, variables) -> int:
+        r = self.s.post(f"{self.base}/containers/{self.c}/processes/{pid}/instances",
+                        data=json.dumps(variables), headers={"Content-Type": "application/json"},
+                        timeout=self.timeout)
+        r.raise_for_status()
+        return int(r.json())
+
+    def start_fraud(self, variables) -> int:
+        return self._start(self.fraud_pid, variables)
+
+    def start_standard(self, variables) -> int:
+        return self._start(self.standard_pid, variables)
+
+    def signal(self, instance_id: int, name: str, payload) -> bool:
+        r = self.s.post(f"{self.base}/containers/{self.c}/processes/instances/{instance_id}/signal/{name or self.signal_name}",
+                        data=json.dumps(payload), headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        return r.status_code == 200

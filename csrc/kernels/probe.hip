@@ -1,0 +1,58 @@
+// Roofline probes for the streaming path: how fast can one MI355X pull bytes from pinned
+// host memory (a) with an SDMA H2D copy, (b) with zero-copy kernel loads over PCIe, and
+// (c) from HBM.  The scoring engine's ceiling is bytes/transaction (120 B of f32
+// features) divided by the best of these, so bench numbers are quoted against them.
+#include <hip/hip_runtime.h>
+
+#include "../include/ccfd_abi.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void read_sum_kernel(const float4* __restrict__ src, size_t n4, float* out) {
+  float acc = 0.f;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = src[i];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  // keep the loads live; one store per thread that is never read back
+  if (acc == 1234.5678f) out[threadIdx.x] = acc;
+}
+
+}  // namespace
+
+extern "C" double ccfd_bw_probe(const void* src, size_t bytes, int mode, int iters, void* dev_scratch) {
+  // mode 0: hipMemcpyAsync H2D (src pinned host) into dev_scratch (>= bytes)
+  // mode 1: zero-copy kernel read of host-mapped src
+  // mode 2: kernel read of device memory src
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1.0;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const float4* p = static_cast<const float4*>(src);
+  if (mode == 1) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(src), 0) != hipSuccess) return -2.0;
+    p = static_cast<const float4*>(d);
+  }
+  const size_t n4 = bytes / 16;
+  auto once = [&]() {
+    if (mode == 0)
+      hipMemcpyAsync(dev_scratch, src, bytes, hipMemcpyHostToDevice, s);
+    else
+      hipLaunchKernelGGL(read_sum_kernel, dim3(2048), dim3(256), 0, s, p, n4, static_cast<float*>(dev_scratch));
+  };
+  once();
+  hipStreamSynchronize(s);
+  hipEventRecord(e0, s);
+  for (int i = 0; i < iters; ++i) once();
+  hipEventRecord(e1, s);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipStreamDestroy(s);
+  return ms > 0 ? (double)bytes * iters / (ms * 1e-3) / 1e9 : -3.0;
+}
