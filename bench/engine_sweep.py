@@ -62,12 +62,16 @@ def main():
             st = e.pump(args.batches, drain=True)
             dt = time.perf_counter() - t0
             e.drain_flagged()
-            res[k].append((st.rows / dt, st.p50_us, st.p99_us))
+            nb = max(1, st.batches)
+            res[k].append((st.rows / dt, st.p50_us, st.p99_us, st.host_submit_s / nb * 1e6,
+                           st.host_wait_s / nb * 1e6, st.host_complete_s / nb * 1e6, dt / nb * 1e6))
     for k, v in res.items():
         tx = sorted(x[0] for x in v)
         print(json.dumps({"mode": k[0], "depth": k[1], "streams": k[2], "batch": k[3],
                           "tx_per_s_median": round(tx[len(tx) // 2] / 1e6, 2), "tx_per_s_max": round(tx[-1] / 1e6, 2),
-                          "p50_us": round(v[-1][1], 1), "p99_us": round(v[-1][2], 1)}), flush=True)
+                          "p50_us": round(v[-1][1], 1), "p99_us": round(v[-1][2], 1),
+                          "us_per_batch": round(v[-1][6], 2), "host_submit_us": round(v[-1][3], 2),
+                          "host_wait_us": round(v[-1][4], 2), "host_complete_us": round(v[-1][5], 2)}), flush=True)
     for e in engines.values():
         e.close()
     log.free()

@@ -85,6 +85,16 @@ class StepStats:
     max_us: float = 0.0
     mean_us: float = 0.0
     lat_hist: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+    host_submit_s: float = 0.0
+    host_wait_s: float = 0.0
+    host_complete_s: float = 0.0
+
+
+def _stats(st: EngineStats) -> StepStats:
+    return StepStats(st.batches, st.rows, st.fraud_rows, st.flagged_dropped, st.wall_s,
+                     st.lat_p50_us, st.lat_p99_us, st.lat_max_us, st.lat_mean_us,
+                     np.ctypeslib.as_array(st.lat_hist).copy(), st.host_submit_ns * 1e-9,
+                     st.host_wait_ns * 1e-9, st.host_complete_ns * 1e-9)
 
 
 class StreamEngine:
@@ -141,9 +151,7 @@ class StreamEngine:
         st = EngineStats()
         check(lib().ccfd_engine_pump(C.c_void_p(self.h), int(n_batches), int(batch_rows or self.batch),
                                      1 if drain else 0, C.byref(st)), "ccfd_engine_pump")
-        return StepStats(st.batches, st.rows, st.fraud_rows, st.flagged_dropped, st.wall_s,
-                         st.lat_p50_us, st.lat_p99_us, st.lat_max_us, st.lat_mean_us,
-                         np.ctypeslib.as_array(st.lat_hist).copy())
+        return _stats(st)
 
     def score(self, X: np.ndarray):
         """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
@@ -178,6 +186,78 @@ class StreamEngine:
             if k < 65536:
                 break
         return np.concatenate(out) if out else np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
+
+    # ------------------------------------------------------------------ ring (streaming) mode
+    def set_ring(self, partition: int, capacity: int) -> PartitionLog:
+        """Register partition ``partition`` as a live SPSC ring of ``capacity`` rows."""
+        log = PartitionLog(capacity)
+        check(lib().ccfd_engine_set_ring(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
+                                         C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr), log.n),
+              "ccfd_engine_set_ring")
+        self.logs[partition] = log
+        return log
+
+    def ring_write(self, partition: int, X: np.ndarray, ids: Optional[np.ndarray] = None,
+                   customer: Optional[np.ndarray] = None, block: bool = True) -> int:
+        """Producer side: append rows (copied into the pinned ring, wrapping as needed).
+        Returns rows written (< len(X) only when ``block`` is False and the ring is full)."""
+        log = self.logs[partition]
+        n = X.shape[0]
+        done = 0
+        row = C.c_int64(0)
+        while done < n:
+            k = lib().ccfd_engine_ring_acquire(C.c_void_p(self.h), int(partition), n - done, C.byref(row))
+            if k < 0:
+                raise RuntimeError("partition is not a ring")
+            if k == 0:
+                if not block:
+                    break
+                import time as _t
+                _t.sleep(50e-6)
+                continue
+            r = row.value
+            log.feats.array[r:r + k] = X[done:done + k]
+            if ids is not None:
+                log.ids.array[r:r + k] = ids[done:done + k]
+            if customer is not None:
+                log.customer.array[r:r + k] = customer[done:done + k]
+            lib().ccfd_engine_ring_commit(C.c_void_p(self.h), int(partition), k)
+            done += k
+        return done
+
+    def ring_write_json(self, partition: int, values) -> int:
+        """Parse JSON transaction messages with the native parser straight into the ring."""
+        log = self.logs[partition]
+        n = len(values)
+        done = 0
+        row = C.c_int64(0)
+        L = lib()
+        while done < n:
+            k = L.ccfd_engine_ring_acquire(C.c_void_p(self.h), int(partition), n - done, C.byref(row))
+            if k <= 0:
+                import time as _t
+                _t.sleep(50e-6)
+                continue
+            r = row.value
+            chunk = values[done:done + k]
+            buf = b"".join(chunk)
+            off = np.zeros(k + 1, np.int64)
+            np.cumsum([len(v) for v in chunk], out=off[1:])
+            got = L.ccfd_parse_json_batch(buf, off.ctypes.data, k, log.feats.ptr + r * 120,
+                                          log.ids.ptr + r * 8, log.customer.ptr + r * 4)
+            if got != k:
+                raise ValueError(f"malformed transaction message #{done - got - 1}")
+            L.ccfd_engine_ring_commit(C.c_void_p(self.h), int(partition), k)
+            done += k
+        return done
+
+    def run(self, budget_us: int = 1000, flush_us: int = 500) -> StepStats:
+        """Consumer side: score whatever the rings hold for ``budget_us``."""
+        st = EngineStats()
+        rc = lib().ccfd_engine_run(C.c_void_p(self.h), int(budget_us), int(flush_us), C.byref(st))
+        if rc < 0:
+            raise RuntimeError(f"ccfd_engine_run failed: {last_error()}")
+        return _stats(st)
 
     def reset_stats(self) -> None:
         lib().ccfd_engine_reset_stats(C.c_void_p(self.h))

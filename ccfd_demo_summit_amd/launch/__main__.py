@@ -1,0 +1,298 @@
+"""Service launcher -- the replacement for the reference's OpenShift objects
+(DeploymentConfigs/Services of deploy/*.yaml; README.md:34-537 deployment order).
+
+    python -m ccfd_demo_summit_amd.launch <service> [options]
+
+services:
+  kafka-lite   single-node Kafka-protocol broker (dev/CI stand-in for Strimzi)
+  seldon       fraud model predict() server            (port 8000, modelfull)
+  usertask     user-task model predict() server         (port 5000, ccfd-seldon-model)
+  kie          business-process server (KIE REST)       (port 8090)
+  notifier     customer notification simulator          (port 8080 health)
+  router       compat router: Kafka -> remote Seldon predict() -> KIE   (port 8091)
+  engine       GPU streaming engine, one rank per GPU (run under torchrun)  (port 8091+rank)
+  producer     transaction producer (synthetic / creditcard.csv)
+  demo         everything in one process over an in-process broker
+  supervise    restart-on-crash supervisor:  supervise [--max-restarts N] -- <cmd...>
+
+Configuration: the reference env var names (BROKER_URL, KAFKA_TOPIC, SELDON_URL, ...),
+an optional --config YAML, then flags (ccfd_demo_summit_amd/config.py).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import threading
+import time
+
+from ..config import load_config
+
+
+def _broker(cfg, inproc=None):
+    if inproc is not None:
+        return inproc
+    from ..ingest.kafka_wire import KafkaBroker
+    return KafkaBroker(cfg.kafka.broker_url)
+
+
+def _model(kind: str, weights: str = None, seed: int = 0):
+    from ..data import FRAUD_RATE, generate
+    from ..models import build_model, load_model
+    if weights:
+        return load_model(weights)
+    X, _ = generate(100_000, seed=seed + 17)
+    return build_model(kind, seed=seed, X_ref=X, calibrate_rate=FRAUD_RATE)
+
+
+def _metrics_app(expose):
+    from aiohttp import web
+
+    from ..metrics.exporter import CONTENT_TYPE
+
+    async def handler(_r):
+        return web.Response(body=expose(), headers={"Content-Type": CONTENT_TYPE})
+    app = web.Application()
+    app.router.add_get("/prometheus", handler)
+    app.router.add_get("/metrics", handler)
+    app.router.add_get("/health/ping", lambda _r: web.json_response({"status": "ok"}))
+    return app
+
+
+def _serve_in_thread(app, host, port):
+    from aiohttp import web
+
+    def run():
+        loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(loop)
+        runner = web.AppRunner(app)
+        loop.run_until_complete(runner.setup())
+        loop.run_until_complete(web.TCPSite(runner, host, port).start())
+        loop.run_forever()
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return t
+
+
+# ---------------------------------------------------------------------------- services
+def cmd_kafka_lite(a, cfg):
+    from ..ingest.kafka_lite import main
+    main(["--host", a.host, "--port", str(a.port or 9092), "--partitions", str(cfg.kafka.partitions)])
+
+
+def cmd_seldon(a, cfg):
+    from ..serving.scorers import make_scorer
+    from ..serving.seldon_server import SeldonServer, run
+    model = _model(cfg.engine.model, a.weights, cfg.seed)
+    scorer = make_scorer(model, cfg.router.fraud_threshold, device=a.device, max_batch=cfg.seldon.max_batch)
+    srv = SeldonServer(scorer, cfg.seldon.model_name, cfg.seldon.token, cfg.seldon.max_batch,
+                       cfg.seldon.max_delay_us)
+    print(f"[seldon] {cfg.seldon.model_name} on {getattr(scorer, 'device', 'cpu')} :{a.port or cfg.seldon.port}", flush=True)
+    run(srv, a.host, a.port or cfg.seldon.port)
+
+
+def cmd_usertask(a, cfg):
+    from ..serving.seldon_server import run, usertask_server
+    run(usertask_server(cfg.seldon.token), a.host, a.port or 5000)
+
+
+def cmd_kie(a, cfg):
+    from aiohttp import web
+
+    from ..metrics.exporter import KieMetrics
+    from ..process.engine import ProcessEngine
+    from ..process.kie_server import KieServer
+    from ..process.notifier import encode_notification
+    from ..process.prediction_service import PredictionService
+    from ..serving.client import SeldonClient
+    broker = _broker(cfg)
+    topic = cfg.kafka.notification_topic
+    client = SeldonClient(cfg.kie.seldon_url, cfg.kie.seldon_endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
+                          cfg.seldon.pool_size) if a.remote_prediction else None
+    eng = ProcessEngine.from_config(
+        cfg.kie, publish_notification=lambda m: broker.produce(topic, encode_notification(m),
+                                                               key=str(m.get("customer_id")).encode()),
+        kie_metrics=KieMetrics(), prediction=PredictionService(cfg.kie.confidence_threshold, client=client),
+        journal_path=a.journal)
+    srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
+    web.run_app(srv.app, host=a.host, port=a.port or cfg.kie.port, print=None, access_log=None)
+
+
+def cmd_notifier(a, cfg):
+    from aiohttp import web
+
+    from ..process.notifier import NotificationService
+    broker = _broker(cfg)
+    ns = NotificationService(lambda raw, key: broker.produce(cfg.kafka.response_topic, raw, key=key),
+                             cfg.notifier.p_reply, cfg.notifier.p_approve, cfg.notifier.mean_delay_s,
+                             cfg.notifier.seed)
+    cons = broker.consumer("notification-service", [cfg.kafka.notification_topic])
+    app = web.Application()
+    app.router.add_get("/health/ping", lambda _r: web.json_response(
+        {"status": "ok", "sent": ns.sent, "replied": ns.replied, "no_reply": ns.no_reply}))
+    _serve_in_thread(app, a.host, a.port or cfg.notifier.port)
+    while True:
+        for r in cons.poll(timeout=0.05, max_records=10_000):
+            ns.handle(r.value)
+        cons.commit()
+        ns.tick()
+
+
+def cmd_router(a, cfg):
+    """Reference-topology router: per fetch, POST the batch to the remote Seldon predict()."""
+    import numpy as np
+
+    from ..contracts import seldon
+    from ..ingest.codec import decode_records
+    from ..metrics.exporter import RouterMetrics
+    from ..process.kie_server import KieClient
+    from ..router.router import Router
+    from ..router.rules import RuleSet
+    from ..serving.client import SeldonClient
+    broker = _broker(cfg)
+    rm = RouterMetrics()
+    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
+                    cfg.kie.signal_name)
+    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), kie, rm)
+    sc = SeldonClient(cfg.seldon.url, cfg.seldon.endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
+                      cfg.seldon.pool_size)
+    _serve_in_thread(_metrics_app(rm.expose), a.host, a.port or cfg.router.port)
+    tx = broker.consumer(cfg.kafka.group_id, [cfg.kafka.transactions_topic])
+    resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic])
+    while True:
+        recs = tx.poll(timeout=0.05, max_records=a.max_batch)
+        if recs:
+            X, ids, cust = decode_records([r.value for r in recs])
+            proba = seldon.proba1_from_response(sc.predict_sync(seldon.build_request(X)))
+            router.on_scored(ids, cust, proba, X=X)
+            tx.commit()
+        for r in resp.poll(max_records=10_000):
+            router.on_response(r.value)
+            rm.notif_outgoing.inc(0)
+        resp.commit()
+
+
+def cmd_engine(a, cfg):
+    import numpy as np
+    import torch
+
+    from ..metrics.exporter import GpuEngineCollector, MetricsHub
+    from ..ops.kernels import DeviceModel
+    from ..parallel.dp import broadcast_blob, init_distributed
+    from ..process.kie_server import KieClient
+    from ..router.router import Router
+    from ..router.rules import RuleSet
+    from ..utils.numa import bind_to_gpu
+    from .engine_service import EngineService, EngineServiceConfig
+    ctx = init_distributed()
+    bind_to_gpu(ctx.device.index)
+    blob = None
+    if ctx.rank == 0:
+        model = _model(cfg.engine.model, a.weights, cfg.seed)
+        blob = torch.from_numpy(np.frombuffer(model.pack(), np.uint8).copy()).to(ctx.device)
+        trees, depth = getattr(model, "n_trees", 0), getattr(model, "depth", 0)
+    else:
+        trees = depth = 0
+    blob = broadcast_blob(ctx, blob)
+    if ctx.initialized:
+        import torch.distributed as dist
+        td = torch.tensor([trees, depth], device=ctx.device)
+        dist.broadcast(td, 0)
+        trees, depth = int(td[0]), int(td[1])
+    dm = DeviceModel.from_blob(cfg.engine.model, blob, trees, depth)
+    broker = _broker(cfg)
+    hub = MetricsHub()
+    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
+    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), kie, hub.router)
+    svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
+        topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
+        depth=cfg.engine.depth, streams=cfg.engine.streams, input_mode=cfg.engine.input_mode,
+        flush_us=cfg.engine.max_delay_us, reduce_period_ms=cfg.engine.reduce_period_ms,
+        threshold=cfg.router.fraud_threshold)).start()
+    hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
+    _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.rank)
+    resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic]) if ctx.rank == 0 else None
+    print(f"[engine] rank {ctx.rank}/{ctx.world} partitions {svc.partitions}", flush=True)
+    try:
+        while True:
+            svc.step()
+            if resp is not None:
+                for r in resp.poll(max_records=10_000):
+                    router.on_response(r.value)
+                resp.commit()
+    finally:
+        svc.stop()
+
+
+def cmd_producer(a, cfg):
+    from ..ingest.producer import ProducerConfig, TransactionProducer
+    pc = ProducerConfig.from_env()
+    pc.fmt, pc.batch, pc.rate_tx_s = a.fmt, a.batch, a.rate
+    if a.csv:
+        pc.source, pc.csv_path = "csv", a.csv
+    broker = _broker(cfg)
+    prod = TransactionProducer(broker, pc)
+    t0 = time.time()
+    n = prod.produce(a.count)
+    print(json.dumps({"produced": n, "seconds": round(time.time() - t0, 3), "topic": pc.topic}), flush=True)
+
+
+def cmd_demo(a, cfg):
+    """All services in one process over an in-process broker; metrics on :8091/prometheus."""
+    from ..ingest.broker import InProcBroker
+    from ..ingest.producer import ProducerConfig, TransactionProducer
+    from ..pipeline import FraudPipeline
+    from ..serving.scorers import make_scorer
+    model = _model(cfg.engine.model, a.weights, cfg.seed)
+    scorer = make_scorer(model, cfg.router.fraud_threshold, device=a.device)
+    pipe = FraudPipeline(cfg, scorer, InProcBroker(default_partitions=cfg.kafka.partitions))
+    _serve_in_thread(_metrics_app(pipe.metrics.expose_all), a.host, a.port or cfg.router.port)
+    prod = TransactionProducer(pipe.broker, ProducerConfig(fmt=a.fmt, batch=a.batch, rate_tx_s=a.rate))
+    t_end = time.time() + a.seconds
+    while time.time() < t_end:
+        prod.produce(a.batch)
+        pipe.step()
+    pipe.run_until_idle(1000)
+    oc = pipe.processes.outcome_counts
+    print(json.dumps({"consumed": pipe.stats.consumed, "outcomes": oc,
+                      "scorer": getattr(scorer, "device", "cpu")}), flush=True)
+
+
+def cmd_supervise(a, cfg):
+    from .supervisor import supervise
+    sys.exit(supervise(a.cmd, max_restarts=a.max_restarts, backoff_s=a.backoff))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="python -m ccfd_demo_summit_amd.launch", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
+                                        "engine", "producer", "demo", "supervise"])
+    ap.add_argument("--config", default=None)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
+    ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
+    ap.add_argument("--journal", default=None, help="KIE: append-only process journal for recovery")
+    ap.add_argument("--remote-prediction", action="store_true", help="KIE: call the user-task model over HTTP")
+    ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--rate", type=float, default=0.0)
+    ap.add_argument("--count", type=int, default=100_000)
+    ap.add_argument("--csv", default=None)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--max-batch", type=int, default=4096)
+    ap.add_argument("--max-restarts", type=int, default=10)
+    ap.add_argument("--backoff", type=float, default=1.0)
+    ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    if a.cmd and a.cmd[0] == "--":
+        a.cmd = a.cmd[1:]
+    cfg = load_config(a.config)
+    globals()["cmd_" + a.service.replace("-", "_")](a, cfg)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+"""Per-GPU streaming engine service -- the hot path of a deployment:
+
+    Kafka (odh-demo, partitions p % W == rank)
+      -> ingest thread: fetch -> TXB1 memcpy / native JSON parse straight into the pinned
+         SPSC ring of the partition (csrc/engine/engine.cpp ring mode)
+      -> engine.run(): fused HIP scoring of full micro-batches, deadline flush of partial ones
+      -> flagged (fraud-routed) transactions -> Router -> KIE hand-off (HTTP KieClient or an
+         in-process ProcessEngine)
+      -> Kafka offsets committed only when every row of a message has been scored and
+         routed (at-least-once; the process engine ignores duplicates)
+      -> every ``reduce_period_ms``: epoch flip + RCCL all-reduce of device counters and
+         latency histograms on a side stream (X2/X3), exported on /prometheus
+
+One process per GPU (torchrun); rank 0 also consumes ``ccd-customer-response`` and signals
+the processes (README.md:569,605).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+import time
+from dataclasses import dataclass
+from typing import Deque, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..contracts.transaction import TXB_MAGIC, TxBatch
+
+
+@dataclass
+class EngineServiceConfig:
+    topic: str = "odh-demo"
+    response_topic: str = "ccd-customer-response"
+    group_id: str = "ccfd-engine"
+    batch: int = 4096
+    depth: int = 8
+    streams: int = 4
+    ring_rows: int = 1 << 20
+    flush_us: int = 500
+    run_budget_us: int = 2000
+    reduce_period_ms: float = 10.0
+    threshold: float = 0.5
+    input_mode: str = "zerocopy"
+    max_fetch: int = 2000
+
+
+class EngineService:
+    def __init__(self, ctx, dm, broker, router, cfg: EngineServiceConfig, reducer=None, partitions=None):
+        from ..engine import StreamEngine
+        from ..parallel.dp import CounterReducer, assign_partitions
+        self.ctx = ctx
+        self.cfg = cfg
+        self.broker = broker
+        self.router = router
+        self.engine = StreamEngine(dm, batch=cfg.batch, depth=cfg.depth, streams=cfg.streams,
+                                   input_mode=cfg.input_mode, threshold=cfg.threshold, device=ctx.device.index)
+        n_parts = broker.partitions(cfg.topic)
+        self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
+        for p in self.partitions:
+            self.engine.set_ring(p, cfg.ring_rows)
+        self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
+            if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
+        self.reducer = reducer or CounterReducer(ctx, ctx.device)
+        # per partition: (ring row end, next kafka offset) of ingested messages, oldest first
+        self._pending: Dict[int, Deque[Tuple[int, int]]] = {p: collections.deque() for p in self.partitions}
+        self._rows_in: Dict[int, int] = {p: 0 for p in self.partitions}
+        self._stop = threading.Event()
+        self._ingest_err: Optional[BaseException] = None
+        self.rows_scored = 0
+        self.last_reduce = time.monotonic()
+        self._lat_prev = np.zeros(256, np.int64)
+
+    # ------------------------------------------------------------------ ingest (producer side)
+    def _ingest_once(self) -> int:
+        recs = self.consumer.poll(timeout=0.001, max_records=self.cfg.max_fetch)
+        n = 0
+        by_part: Dict[int, List] = collections.defaultdict(list)
+        for r in recs:
+            by_part[r.partition].append(r)
+        for p, rs in by_part.items():
+            json_run: List[bytes] = []
+            for r in rs:
+                if r.value[:4] == TXB_MAGIC:
+                    if json_run:
+                        n += self._write_json(p, json_run)
+                        json_run = []
+                    b = TxBatch.decode(r.value)
+                    k = self.engine.ring_write(p, b.features, b.ids, b.customer)
+                    self._rows_in[p] += k
+                    n += k
+                else:
+                    json_run.append(r.value)
+                self._pending[p].append((self._rows_in[p] + (len(json_run) if json_run else 0), r.offset + 1))
+            if json_run:
+                n += self._write_json(p, json_run)
+        return n
+
+    def _write_json(self, p: int, values: List[bytes]) -> int:
+        k = self.engine.ring_write_json(p, values)
+        self._rows_in[p] += k
+        return k
+
+    def _ingest_loop(self):
+        try:
+            while not self._stop.is_set():
+                if self._ingest_once() == 0:
+                    time.sleep(0.0005)
+        except BaseException as e:           # surfaced by step()
+            self._ingest_err = e
+
+    # ------------------------------------------------------------------ consumer side
+    def _commit_done(self) -> None:
+        offs = {}
+        for p in self.partitions:
+            released = self.engine.cursor(p)
+            dq = self._pending[p]
+            last = None
+            while dq and dq[0][0] <= released:
+                last = dq.popleft()[1]
+            if last is not None:
+                offs[(self.cfg.topic, p)] = last
+        if offs:
+            self.consumer.commit(offs)
+
+    def step(self) -> int:
+        if self._ingest_err is not None:
+            raise RuntimeError("ingest thread failed") from self._ingest_err
+        st = self.engine.run(self.cfg.run_budget_us, self.cfg.flush_us)
+        flagged = self.engine.drain_flagged()
+        if st.rows or len(flagged):
+            self.router.on_flagged(flagged, int(st.rows))
+        self.rows_scored += int(st.rows)
+        self._commit_done()
+        now = time.monotonic()
+        if (now - self.last_reduce) * 1e3 >= self.cfg.reduce_period_ms:
+            if self.reducer.done is not None:
+                self.reducer.done.synchronize()
+            lat = st.lat_hist.astype(np.int64)          # cumulative since reset -> send the delta
+            self.reducer.submit(self.engine.flip_epoch(self.reducer.side), lat - self._lat_prev)
+            self._lat_prev = lat
+            self.last_reduce = now
+        return int(st.rows)
+
+    def start(self) -> "EngineService":
+        self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if getattr(self, "_thread", None):
+            self._thread.join(5)
+        self.engine.close()
+
+    def metrics_source(self):
+        c, lat = self.reducer.snapshot()
+        return c, lat, {"rows_scored_local": self.rows_scored}
+
+
+class _StaticInProcConsumer:
+    """Static-assignment consumer over an InProcBroker (same API as WireConsumer)."""
+
+    def __init__(self, broker, group, topic, partitions):
+        self.broker, self.group, self.topic = broker, group, topic
+        self._positions = {}
+        for p in partitions:
+            c = broker.committed(group, topic, p)
+            self._positions[(topic, p)] = c if c is not None else broker.begin_offset(topic, p)
+
+    def poll(self, timeout: float = 0.0, max_records: int = 500):
+        out = []
+        for tp, pos in list(self._positions.items()):
+            recs = self.broker.fetch(tp[0], tp[1], pos, max_records - len(out))
+            if recs:
+                self._positions[tp] = recs[-1].offset + 1
+                out.extend(recs)
+        if not out and timeout:
+            time.sleep(timeout)
+        return out
+
+    def commit(self, offsets=None):
+        for (t, p), o in (offsets or self._positions).items():
+            self.broker.commit(self.group, t, p, o)

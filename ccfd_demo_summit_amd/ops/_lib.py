@@ -26,7 +26,8 @@ class ScoreArgs(C.Structure):
     _fields_ = [("x", C.c_void_p), ("ld", C.c_int64), ("n", C.c_int32), ("model", C.c_int32),
                 ("blob", C.c_void_p), ("threshold", C.c_float), ("gbdt_trees", C.c_int32),
                 ("gbdt_depth", C.c_int32), ("_pad", C.c_int32), ("proba", C.c_void_p),
-                ("route", C.c_void_p), ("counters", C.c_void_p)]
+                ("route", C.c_void_p), ("counters", C.c_void_p), ("slot_ctl", C.c_void_p),
+                ("flag_idx", C.c_void_p), ("done_rec", C.c_void_p), ("done_seq", C.c_uint64)]
 
 
 class EngineConfig(C.Structure):
@@ -46,7 +47,8 @@ class EngineStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("rows", C.c_uint64), ("fraud_rows", C.c_uint64),
                 ("flagged_dropped", C.c_uint64), ("wall_s", C.c_double), ("lat_p50_us", C.c_double),
                 ("lat_p99_us", C.c_double), ("lat_max_us", C.c_double), ("lat_mean_us", C.c_double),
-                ("lat_hist", C.c_uint64 * 256)]
+                ("lat_hist", C.c_uint64 * 256), ("host_submit_ns", C.c_uint64), ("host_wait_ns", C.c_uint64),
+                ("host_complete_ns", C.c_uint64)]
 
 
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
@@ -95,6 +97,13 @@ def lib() -> C.CDLL:
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]
         L.ccfd_engine_cursor.restype = C.c_int64
         L.ccfd_engine_reset_stats.argtypes = [C.c_void_p]
+        L.ccfd_engine_set_ring.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        L.ccfd_engine_ring_acquire.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_int64)]
+        L.ccfd_engine_ring_acquire.restype = C.c_int64
+        L.ccfd_engine_ring_commit.argtypes = [C.c_void_p, C.c_int, C.c_int64]
+        L.ccfd_engine_run.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(EngineStats)]
+        L.ccfd_crc32c.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
+        L.ccfd_crc32c.restype = C.c_uint32
         L.ccfd_parse_json_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                             C.c_void_p]
         L.ccfd_parse_json_batch.restype = C.c_int64

@@ -23,9 +23,17 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 #include "../include/ccfd_abi.h"
 
@@ -58,6 +66,23 @@ struct Partition {
   const uint32_t* cust = nullptr;
   int64_t n = 0;
   int64_t cursor = 0;
+  // ring (streaming) mode: SPSC ring of n rows; producer = ingest thread, consumer = run()
+  bool ring = false;
+  std::atomic<int64_t> head{0};      // rows committed by the producer (monotonic)
+  std::atomic<int64_t> released{0};  // rows whose batches have completed (monotonic)
+  int64_t submitted = 0;             // rows handed to the GPU (consumer-private)
+  std::mutex arr_mu;
+  std::deque<std::pair<int64_t, int64_t>> arrivals;   // (head after commit, t_ns)
+
+  int64_t arrival_of(int64_t row) {   // commit time of `row`
+    std::lock_guard<std::mutex> lk(arr_mu);
+    for (auto& a : arrivals) if (a.first > row) return a.second;
+    return arrivals.empty() ? 0 : arrivals.back().second;
+  }
+  void forget_before(int64_t row) {
+    std::lock_guard<std::mutex> lk(arr_mu);
+    while (!arrivals.empty() && arrivals.front().first <= row) arrivals.pop_front();
+  }
 };
 
 struct Slot {
@@ -66,6 +91,7 @@ struct Slot {
   int64_t start = 0;
   int32_t rows = 0;
   int64_t t_submit = 0;
+  int64_t t_arrival = 0;           // ring mode: commit time of the batch's first row
   float* d_x = nullptr;
   float* d_proba = nullptr;
   uint8_t* d_route = nullptr;
@@ -74,7 +100,22 @@ struct Slot {
   float* h_proba_dev = nullptr;    // device alias of the pinned host slot
   uint8_t* h_route_dev = nullptr;
   hipEvent_t ev = nullptr;
+  // kernel-published completion (flag mode): device ticket counters, compacted flagged
+  // row indices and the {seq, #flagged} record the last workgroup stores to host memory
+  unsigned int* d_ctl = nullptr;
+  unsigned int* h_flag = nullptr;
+  unsigned int* h_flag_dev = nullptr;
+  volatile unsigned long long* h_done = nullptr;
+  unsigned long long* h_done_dev = nullptr;
+  unsigned long long expect = 0;
+  bool use_flag = false;
 };
+
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  _mm_pause();
+#endif
+}
 
 class Engine {
  public:
@@ -82,7 +123,7 @@ class Engine {
   std::vector<hipStream_t> streams;
   std::vector<hipEvent_t> flip_ev;
   std::vector<Slot> slots;
-  std::vector<Partition> parts;
+  std::vector<std::unique_ptr<Partition>> parts;
   uint64_t seq = 0;
   int next_part = 0;
   int epoch = 0;
@@ -93,6 +134,8 @@ class Engine {
   uint64_t dropped = 0;
   std::vector<float> lat_us;
   uint64_t lat_hist[256] = {};
+  uint64_t t_submit_ns = 0, t_wait_ns = 0, t_complete_ns = 0;
+  unsigned long long done_counter = 0;
 
   int init(const ccfd_engine_config& c) {
     cfg = c;
@@ -125,7 +168,18 @@ class Engine {
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_proba_dev), s.h_proba, 0));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_route_dev), s.h_route, 0));
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      HIPCHK(hipMalloc(reinterpret_cast<void**>(&s.d_ctl), 2 * sizeof(unsigned int)));
+      HIPCHK(hipMemset(s.d_ctl, 0, 2 * sizeof(unsigned int)));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_flag), B * sizeof(unsigned int),
+                           hipHostMallocMapped | hipHostMallocPortable));
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_flag_dev), s.h_flag, 0));
+      void* hd = nullptr;
+      HIPCHK(hipHostMalloc(&hd, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+      std::memset(hd, 0, 64);
+      s.h_done = static_cast<volatile unsigned long long*>(hd);
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_done_dev), hd, 0));
     }
+    HIPCHK(hipDeviceSynchronize());
     ring.resize(std::max(1024, cfg.flag_capacity));
     return 0;
   }
@@ -133,13 +187,16 @@ class Engine {
   ~Engine() {
     hipSetDevice(cfg.device);
     for (auto& s : slots) {
-      if (s.busy) hipEventSynchronize(s.ev);
+      if (s.busy) wait_done(s);
       if (s.d_x) hipFree(s.d_x);
       if (s.d_proba) hipFree(s.d_proba);
       if (s.d_route) hipFree(s.d_route);
       if (s.h_proba) hipHostFree(s.h_proba);
       if (s.h_route) hipHostFree(s.h_route);
       if (s.ev) hipEventDestroy(s.ev);
+      if (s.d_ctl) hipFree(s.d_ctl);
+      if (s.h_flag) hipHostFree(s.h_flag);
+      if (s.h_done) hipHostFree(const_cast<unsigned long long*>(s.h_done));
     }
     for (auto e : flip_ev) if (e) hipEventDestroy(e);
     for (auto st : streams) if (st) hipStreamDestroy(st);
@@ -150,8 +207,9 @@ class Engine {
     if (n < cfg.max_batch) { set_error("partition log shorter than one micro-batch"); return -1; }
     if (reinterpret_cast<uintptr_t>(feats) & 15) { set_error("log must be 16-byte aligned"); return -1; }
     drain_all();
-    if ((int)parts.size() <= p) parts.resize(p + 1);
-    Partition& P = parts[p];
+    while ((int)parts.size() <= p) parts.emplace_back(new Partition());
+    Partition& P = *parts[p];
+    P.ring = false;
     P.feats = feats; P.ids = ids; P.cust = cust; P.n = n; P.cursor = cursor % n;
     P.feats_dev = feats;
     if (cfg.input_mode == 1) {
@@ -162,8 +220,15 @@ class Engine {
     return 0;
   }
 
+  void push_flagged_idx(const Slot& s, uint64_t nf) {
+    const Partition& P = *parts[s.part];
+    std::lock_guard<std::mutex> lk(ring_mu);
+    const uint64_t cap = ring.size();
+    for (uint64_t k = 0; k < nf; ++k) emit(P, s, (int)s.h_flag[k], cap);
+  }
+
   void push_flagged(const Slot& s) {
-    const Partition& P = parts[s.part];
+    const Partition& P = *parts[s.part];
     const uint8_t* r = s.h_route;
     const int n = s.rows;
     std::lock_guard<std::mutex> lk(ring_mu);
@@ -190,18 +255,59 @@ class Engine {
     ++ring_tail;
   }
 
+  bool is_done(const Slot& s) {
+    if (s.use_flag) return s.h_done[0] == s.expect;
+    return hipEventQuery(s.ev) == hipSuccess;
+  }
+
+  int wait_done(Slot& s) {
+    if (!s.use_flag) {
+      HIPCHK(hipEventSynchronize(s.ev));
+      return 0;
+    }
+    // spin on the pinned completion record; every 64K spins check the device for errors
+    // and give up after 60 s so a faulted kernel can never hang the host thread
+    const int64_t t0 = now_ns();
+    for (uint64_t it = 0; s.h_done[0] != s.expect; ++it) {
+      cpu_relax();
+      if ((it & 0xFFFF) == 0xFFFF) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) { set_error(std::string("kernel error: ") + hipGetErrorString(e)); return -4; }
+        if (now_ns() - t0 > 60ll * 1000000000ll) { set_error("timeout waiting for micro-batch completion"); return -6; }
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return 0;
+  }
+
   int complete(Slot& s, ccfd_engine_stats* st) {
-    HIPCHK(hipEventSynchronize(s.ev));
+    const int64_t tw = now_ns();
+    { int rc = wait_done(s); if (rc) return rc; }
     const int64_t t = now_ns();
-    const double us = (t - s.t_submit) * 1e-3;
+    t_wait_ns += t - tw;
+    const int64_t t0 = s.t_arrival ? s.t_arrival : s.t_submit;   // ring: end-to-end from commit
+    const double us = (t - t0) * 1e-3;
     lat_us.push_back((float)us);
-    const double ns = (double)std::max<int64_t>(1, t - s.t_submit);
+    const double ns = (double)std::max<int64_t>(1, t - t0);
     lat_hist[std::min(255, (int)std::floor(4.0 * std::log2(ns)))]++;
     uint64_t nf = 0;
-    for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
-    if (nf) push_flagged(s);
+    if (s.use_flag) {
+      nf = s.h_done[1];
+      if (nf) push_flagged_idx(s, nf);
+    } else {
+      for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
+      if (nf) push_flagged(s);
+    }
     if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
+    Partition& P = *parts[s.part];
+    if (P.ring) {
+      // batches of one partition complete in submission order: release in order
+      P.released.store(P.released.load(std::memory_order_relaxed) + s.rows, std::memory_order_release);
+      P.forget_before(P.released.load(std::memory_order_relaxed));
+    }
     s.busy = false;
+    s.t_arrival = 0;
+    t_complete_ns += now_ns() - t;
     return 0;
   }
 
@@ -218,6 +324,7 @@ class Engine {
   int submit(Slot& s, const float* x_dev_or_host, const float* x_host, int rows, hipStream_t stream,
              bool force_dma = false) {
     s.t_submit = now_ns();
+    struct Acc { uint64_t& a; int64_t t0; ~Acc() { a += now_ns() - t0; } } acc{t_submit_ns, s.t_submit};
     const float* xk = x_dev_or_host;
     if (cfg.input_mode == 0 || force_dma) {
       HIPCHK(hipMemcpyAsync(s.d_x, x_host, (size_t)rows * CCFD_N_FEATURES * sizeof(float),
@@ -230,13 +337,21 @@ class Engine {
     a.proba = cfg.output_mode == 1 ? s.d_proba : s.h_proba_dev;
     a.route = cfg.output_mode == 1 ? s.d_route : s.h_route_dev;
     a.counters = cfg.counters[epoch & 1];
+    s.use_flag = cfg.output_mode == 0;
+    if (s.use_flag) {
+      s.expect = ++done_counter;
+      a.slot_ctl = s.d_ctl;
+      a.flag_idx = s.h_flag_dev;
+      a.done_rec = s.h_done_dev;
+      a.done_seq = s.expect;
+    }
     int rc = ccfd_score_launch(&a, stream);
     if (rc) return rc;
     if (cfg.output_mode == 1) {
       HIPCHK(hipMemcpyAsync(s.h_proba, s.d_proba, (size_t)rows * sizeof(float), hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(s.h_route, s.d_route, (size_t)rows, hipMemcpyDeviceToHost, stream));
     }
-    HIPCHK(hipEventRecord(s.ev, stream));
+    if (!s.use_flag) HIPCHK(hipEventRecord(s.ev, stream));
     s.busy = true;
     return 0;
   }
@@ -251,9 +366,11 @@ class Engine {
       Slot& s = slots[seq % D];
       if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
       int p = next_part;
-      for (int k = 0; k < (int)parts.size() && parts[p].feats == nullptr; ++k) p = (p + 1) % parts.size();
+      for (int k = 0; k < (int)parts.size() && (parts[p]->feats == nullptr || parts[p]->ring); ++k)
+        p = (p + 1) % parts.size();
       next_part = (p + 1) % (int)parts.size();
-      Partition& P = parts[p];
+      Partition& P = *parts[p];
+      if (P.ring || P.feats == nullptr) { set_error("pump() needs a replay log partition"); return -1; }
       if (P.cursor + batch_rows > P.n) P.cursor = 0;
       s.part = p; s.start = P.cursor; s.rows = batch_rows;
       P.cursor += batch_rows;
@@ -277,6 +394,9 @@ class Engine {
 
   void fill_latency(ccfd_engine_stats* st) {
     std::memcpy(st->lat_hist, lat_hist, sizeof(lat_hist));
+    st->host_submit_ns = t_submit_ns;
+    st->host_wait_ns = t_wait_ns;
+    st->host_complete_ns = t_complete_ns;
     if (lat_us.empty()) return;
     std::vector<float> v = lat_us;
     auto pct = [&](double q) {
@@ -305,7 +425,8 @@ class Engine {
       rc = submit(s, xh, xh, rows, stream, /*force_dma=*/true);
       if (rc) return rc;
       ++seq;
-      HIPCHK(hipEventSynchronize(s.ev));
+      rc = wait_done(s);
+      if (rc) return rc;
       s.busy = false;
       if (proba_out) std::memcpy(proba_out + off, s.h_proba, rows * sizeof(float));
       if (route_out) std::memcpy(route_out + off, s.h_route, rows);
@@ -322,6 +443,108 @@ class Engine {
     }
     ++epoch;
     return closed;
+  }
+
+  // ------------------------------------------------------------------ ring (streaming) mode
+  int set_ring(int p, float* feats, uint64_t* ids, uint32_t* cust, int64_t cap) {
+    if (p < 0 || p > 4096 || cap < cfg.max_batch) { set_error("bad ring partition/capacity"); return -1; }
+    if (reinterpret_cast<uintptr_t>(feats) & 15) { set_error("ring must be 16-byte aligned"); return -1; }
+    int rc = drain_all();
+    if (rc) return rc;
+    while ((int)parts.size() <= p) parts.emplace_back(new Partition());
+    Partition& P = *parts[p];
+    P.ring = true;
+    P.feats = feats; P.ids = ids; P.cust = cust; P.n = cap; P.cursor = 0;
+    P.head.store(0); P.released.store(0); P.submitted = 0;
+    P.feats_dev = feats;
+    if (cfg.input_mode == 1) {
+      void* d = nullptr;
+      HIPCHK(hipHostGetDevicePointer(&d, feats, 0));
+      P.feats_dev = static_cast<const float*>(d);
+    }
+    return 0;
+  }
+
+  // Producer side: contiguous free rows starting at physical *row (0 if the ring is full).
+  int64_t ring_acquire(int p, int64_t want, int64_t* row) {
+    if (p < 0 || p >= (int)parts.size() || !parts[p]->ring) return -1;
+    Partition& P = *parts[p];
+    const int64_t h = P.head.load(std::memory_order_relaxed);
+    const int64_t free_rows = P.n - (h - P.released.load(std::memory_order_acquire));
+    const int64_t phys = h % P.n;
+    *row = phys;
+    return std::max<int64_t>(0, std::min({want, free_rows, P.n - phys}));
+  }
+
+  int ring_commit(int p, int64_t n) {
+    if (p < 0 || p >= (int)parts.size() || !parts[p]->ring) return -1;
+    Partition& P = *parts[p];
+    const int64_t h = P.head.load(std::memory_order_relaxed) + n;
+    {
+      std::lock_guard<std::mutex> lk(P.arr_mu);
+      P.arrivals.emplace_back(h, now_ns());
+    }
+    P.head.store(h, std::memory_order_release);
+    return 0;
+  }
+
+  // Consumer loop for `budget_us`: submit every full micro-batch (and partial ones whose
+  // first row has waited >= flush_us: deadline flush bounds latency at low load), complete
+  // finished batches; returns the number of batches submitted.
+  int run(int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {
+    HIPCHK(hipSetDevice(cfg.device));
+    const int64_t t0 = now_ns();
+    const int64_t t_end = t0 + budget_us * 1000;
+    const int D = (int)slots.size();
+    int submitted = 0;
+    for (;;) {
+      bool progress = false;
+      // 1) retire completed batches (oldest first) without blocking
+      for (int k = 0; k < D; ++k) {
+        Slot& s = slots[(seq + k) % D];
+        if (!s.busy) continue;
+        if (!is_done(s)) break;
+        int rc = complete(s, st);
+        if (rc) return rc;
+        progress = true;
+      }
+      // 2) submit eligible batches round-robin over ring partitions
+      const int64_t now = now_ns();
+      for (size_t q = 0; q < parts.size(); ++q) {
+        Partition& P = *parts[q];
+        if (!P.ring) continue;
+        const int64_t h = P.head.load(std::memory_order_acquire);
+        int64_t avail = h - P.submitted;
+        while (avail > 0) {
+          Slot& s = slots[seq % D];
+          if (s.busy) break;                               // all slots in flight
+          const int64_t phys = P.submitted % P.n;
+          int64_t rows = std::min<int64_t>({avail, (int64_t)cfg.max_batch, P.n - phys});
+          const bool full = rows == cfg.max_batch || rows == P.n - phys;
+          const int64_t arr = P.arrival_of(P.submitted);
+          if (!full && now - arr < flush_us * 1000) break;  // wait for more rows
+          s.part = (int)q; s.start = phys; s.rows = (int32_t)rows;
+          const size_t off = (size_t)phys * CCFD_N_FEATURES;
+          hipStream_t stream = streams[seq % streams.size()];
+          int rc = submit(s, P.feats_dev + off, P.feats + off, (int)rows, stream);
+          if (rc) return rc;
+          s.t_arrival = arr;
+          ++seq;
+          ++submitted;
+          P.submitted += rows;
+          avail -= rows;
+          progress = true;
+        }
+      }
+      if (now_ns() >= t_end) break;
+      if (!progress) std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+    if (st) {
+      st->wall_s += (now_ns() - t0) * 1e-9;
+      st->flagged_dropped = dropped;
+      fill_latency(st);
+    }
+    return submitted;
   }
 
   int64_t drain_flagged(ccfd_flagged* out, int64_t max) {
@@ -371,12 +594,31 @@ int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max) {
 int64_t ccfd_engine_cursor(void* eng, int partition) {
   auto* e = static_cast<Engine*>(eng);
   if (partition < 0 || partition >= (int)e->parts.size()) return -1;
-  return e->parts[partition].cursor;
+  Partition& P = *e->parts[partition];
+  return P.ring ? P.released.load() : P.cursor;
+}
+
+int ccfd_engine_set_ring(void* eng, int partition, float* feats, uint64_t* ids, uint32_t* customer,
+                         int64_t capacity) {
+  return static_cast<Engine*>(eng)->set_ring(partition, feats, ids, customer, capacity);
+}
+
+int64_t ccfd_engine_ring_acquire(void* eng, int partition, int64_t want, int64_t* row) {
+  return static_cast<Engine*>(eng)->ring_acquire(partition, want, row);
+}
+
+int ccfd_engine_ring_commit(void* eng, int partition, int64_t n) {
+  return static_cast<Engine*>(eng)->ring_commit(partition, n);
+}
+
+int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {
+  return static_cast<Engine*>(eng)->run(budget_us, flush_us, st);
 }
 
 void ccfd_engine_reset_stats(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   std::memset(e->lat_hist, 0, sizeof(e->lat_hist));
+  e->t_submit_ns = e->t_wait_ns = e->t_complete_ns = 0;
   e->lat_us.clear();
 }
 

@@ -39,6 +39,16 @@ typedef struct ccfd_score_args {
   float* proba;          // out [n] proba_1 (device or host-mapped), may be NULL
   uint8_t* route;        // out [n] 1 = fraud route, may be NULL
   unsigned long long* counters;  // device [CCFD_CNT_SLOTS] accumulated atomically, may be NULL
+  // Launch-completion protocol (engine slots; all NULL for a plain launch):
+  //   every workgroup publishes its outputs (system-scope release) and bumps slot_ctl[0];
+  //   fraud-routed rows append their row index to flag_idx (reserved via slot_ctl[1]);
+  //   the LAST workgroup resets slot_ctl, stores done_rec[1] = #flagged and then
+  //   done_rec[0] = done_seq (system-scope release) -> the host polls done_rec[0] in pinned
+  //   memory instead of recording/synchronising a HIP event per micro-batch.
+  unsigned int* slot_ctl;        // device [2], zero-initialised once
+  unsigned int* flag_idx;        // host-mapped [n] row indices of fraud-routed rows
+  unsigned long long* done_rec;  // host-mapped coherent [2]
+  unsigned long long done_seq;
 } ccfd_score_args;
 
 // Enqueue one fused scoring launch (normalize -> model -> sigmoid -> threshold ->
@@ -84,6 +94,10 @@ typedef struct ccfd_engine_stats {
   double lat_p50_us, lat_p99_us, lat_max_us, lat_mean_us;
   uint64_t lat_hist[256];      // batch latency histogram in ns, 4 buckets per octave:
                                // bucket i holds [2^(i/4), 2^((i+1)/4))
+  // host-side time accounting of the submission/completion thread (cumulative ns)
+  uint64_t host_submit_ns;     // H2D enqueue + kernel launch + event record
+  uint64_t host_wait_ns;       // blocked in hipEventSynchronize (GPU not done yet)
+  uint64_t host_complete_ns;   // route scan + flagged hand-off + bookkeeping
 } ccfd_engine_stats;
 
 void* ccfd_engine_create(const ccfd_engine_config* cfg);
@@ -111,6 +125,16 @@ int ccfd_engine_flip_epoch(void* eng, void* side_stream);
 // Drain up to `max` flagged records (fraud route) into `out`; returns count.
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
 int64_t ccfd_engine_cursor(void* eng, int partition);
+
+// Streaming (ring) mode: partition p is an SPSC ring of `capacity` rows in pinned memory.
+// Producer (ingest thread): ring_acquire -> write rows at [row, row+n) -> ring_commit(n).
+// Consumer: ccfd_engine_run() submits full micro-batches, flushes partial ones whose first
+// row has waited `flush_us`, completes finished ones and frees their ring space.
+int ccfd_engine_set_ring(void* eng, int partition, float* feats, uint64_t* ids, uint32_t* customer,
+                         int64_t capacity);
+int64_t ccfd_engine_ring_acquire(void* eng, int partition, int64_t want, int64_t* row);
+int ccfd_engine_ring_commit(void* eng, int partition, int64_t n);
+int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st);
 void ccfd_engine_reset_stats(void* eng);
 
 // ---------------------------------------------------------------------------

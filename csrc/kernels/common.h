@@ -60,6 +60,45 @@ __device__ __forceinline__ void epi_flush(EpilogueLds& s, unsigned long long* cn
   }
 }
 
+// Append the fraud-routed rows of this wave to the slot's compacted flag list: one agent-
+// scope atomic per wave that has any (fraud is ~0.2 % of traffic), then one 4-byte store
+// per flagged row into host-mapped memory.  `fr_lane`: this lane owns a fraud-routed row.
+__device__ __forceinline__ void emit_flagged(const ccfd_score_args& a, bool fr_lane, int row) {
+  if (a.flag_idx == nullptr) return;
+  const unsigned long long m = __ballot(fr_lane);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ffsll((long long)m) - 1;
+  unsigned base = 0;
+  if (lane == leader)
+    base = __hip_atomic_fetch_add(&a.slot_ctl[1], (unsigned)__popcll(m), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  base = __shfl(base, leader);
+  if (fr_lane) a.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
+}
+
+// Completion hand-off to the host, executed by EVERY thread as the kernel's last action
+// (cdna_hip_programming.md §6 Guideline 16 publish recipe, system scope): each storing wave
+// drains its stores, the workgroup barrier, lane 0 releases at system scope and takes a
+// ticket; the last ticket resets the slot and publishes {#flagged, done_seq} to the host.
+__device__ __forceinline__ void signal_done(const ccfd_score_args& a) {
+  if (a.slot_ctl == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned ticket = __hip_atomic_fetch_add(&a.slot_ctl[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (ticket == gridDim.x - 1) {
+      const unsigned nflag = __hip_atomic_load(&a.slot_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.slot_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.slot_ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.done_rec[1], (unsigned long long)nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.done_rec[0], a.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // Wave-level reduction of a u64 over the 64 lanes.
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll

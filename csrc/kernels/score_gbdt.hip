@@ -104,8 +104,10 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a) {
     ps = wave_sum_u64(ps);
     const unsigned nf = __popcll(__ballot(fr));
     if (lane == 0) { epi.fraud = nf; epi.rows = nrows; epi.psum_e6 = ps; }
+    emit_flagged(a, fr, row);
   }
   epi_flush(epi, a.counters);
+  signal_done(a);
 }
 
 template <int D>

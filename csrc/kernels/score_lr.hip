@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void score_lr_kernel(ccfd_score_args a) {
     fraud += __popcll(__ballot(fr && g == 0));
     rows += __popcll(__ballot(valid && g == 0));
     if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
+    emit_flagged(a, fr && g == 0, row);
   }
   psum = wave_sum_u64(psum);
   if (lane == 0) {
@@ -82,6 +83,7 @@ __global__ __launch_bounds__(256) void score_lr_kernel(ccfd_score_args a) {
     atomicAdd(&epi.psum_e6, psum);
   }
   epi_flush(epi, a.counters);
+  signal_done(a);
 }
 
 int launch_lr(const ccfd_score_args& a, hipStream_t s) {

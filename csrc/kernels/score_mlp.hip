@@ -158,6 +158,7 @@ __global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
     fraud += __popcll(mf);
     rows += __popcll(mv);
     if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
+    emit_flagged(a, fr && g == 0, row);
   }
   psum = wave_sum_u64(psum);
   if (lane == 0) {
@@ -166,6 +167,7 @@ __global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
     atomicAdd(&epi.psum_e6, psum);
   }
   epi_flush(epi, a.counters);
+  signal_done(a);
 }
 
 template __global__ void score_mlp_kernel<true>(ccfd_score_args);

@@ -1,0 +1,55 @@
+"""Config-5 path on one GPU: broker -> ingest thread -> pinned rings -> fused kernels ->
+router -> fraud processes, offsets committed after scoring, counters all-reduced."""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def test_engine_service_end_to_end(gpu):
+    from ccfd_demo_summit_amd.ingest import InProcBroker, ProducerConfig, TransactionProducer
+    from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
+    from ccfd_demo_summit_amd.metrics import MetricsHub
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import DistContext
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    from ccfd_demo_summit_amd.router import Router, RuleSet
+
+    X, _ = generate(50_000, seed=1)
+    m = build_model("mlp", seed=3, X_ref=X, calibrate_rate=0.01)
+    broker = InProcBroker(default_partitions=2)
+    broker.create_topic("odh-demo", 2)
+    TransactionProducer(broker, ProducerConfig(fmt="txb1", batch=3000, seed=5)).produce(30_000)
+    TransactionProducer(broker, ProducerConfig(fmt="json", batch=500, seed=6)).produce(2_000)
+    hub = MetricsHub()
+    procs = ProcessEngine(notification_timeout_s=60)
+    router = Router(RuleSet.threshold(0.5), procs, hub.router)
+    ctx = DistContext(0, 1, 0, gpu, "none")
+    svc = EngineService(ctx, DeviceModel(m, gpu), broker, router,
+                        EngineServiceConfig(batch=4096, depth=4, streams=2, ring_rows=16384, flush_us=200,
+                                            reduce_period_ms=1.0)).start()
+    total = 32_000
+    t0 = time.time()
+    while svc.rows_scored < total and time.time() - t0 < 60:
+        svc.step()
+    for _ in range(5):
+        svc.step()
+    svc.reducer.wait()
+    assert svc.rows_scored == total
+    assert broker.lag("ccfd-engine", "odh-demo") == 0
+    assert hub.router.tx_incoming._value.get() == total
+    nf = hub.router.tx_outgoing.labels(type="fraud")._value.get()
+    assert router.fraud_started == nf == procs.active_count()
+    c, lat = svc.reducer.snapshot()
+    if c[0] < total:            # last epoch not flipped yet
+        svc.reducer.submit(svc.engine.flip_epoch(svc.reducer.side), None)
+        c, lat = svc.reducer.snapshot()
+    assert c[0] == total and c[1] == nf
+    assert lat.sum() > 0
+    svc.stop()
