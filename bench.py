@@ -49,6 +49,9 @@ def parse_args(argv=None):
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
+    ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
+                    help="auto = persistent kernel for mlp/lr, per-batch launches for gbdt")
+    ap.add_argument("--persist-grid", type=int, default=0)
     ap.add_argument("--log-rows", type=int, default=1 << 22, help="rows per rank (pinned partition logs)")
     ap.add_argument("--partitions-per-rank", type=int, default=2)
     ap.add_argument("--threshold", type=float, default=0.5)
@@ -78,8 +81,8 @@ def main(argv=None):
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.models import build_model
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
-    from ccfd_demo_summit_amd.parallel import (CounterReducer, all_max, assign_partitions, barrier,
-                                               broadcast_blob, hist_quantile, init_distributed)
+    from ccfd_demo_summit_amd.parallel import (CounterReducer, EpochPipeline, all_max, assign_partitions,
+                                               barrier, broadcast_blob, hist_quantile, init_distributed)
 
     ctx = init_distributed()
     if ctx.world != args.gpus:
@@ -107,6 +110,9 @@ def main(argv=None):
     trees = args.gbdt_trees if args.model == "gbdt" else 0
     depth_t = args.gbdt_depth if args.model == "gbdt" else 0
     dm = DeviceModel.from_blob(args.model, blob, trees, depth_t)
+    exec_mode = args.exec_mode
+    if exec_mode == "auto":
+        exec_mode = "persistent" if args.model in ("mlp", "lr") and args.input_mode == "zerocopy" else "launch"
 
     # ---- this rank's partitions of topic odh-demo (p % W == rank), pre-filled logs
     n_parts = args.partitions_per_rank * W
@@ -115,7 +121,8 @@ def main(argv=None):
     logs = []
     eng = StreamEngine(dm, batch=args.batch, depth=args.depth, streams=args.streams,
                        input_mode=args.input_mode, output_mode=args.output_mode,
-                       threshold=args.threshold, device=dev.index)
+                       threshold=args.threshold, device=dev.index, exec_mode=exec_mode,
+                       persist_grid=args.persist_grid)
     for p in my_parts:
         log = PartitionLog(rows_per_part)
         generate(rows_per_part, seed=args.seed * 7919 + p, out=log.feats.array)
@@ -125,6 +132,7 @@ def main(argv=None):
         logs.append(log)
 
     reducer = CounterReducer(ctx, dev, priority=0)
+    epochs = EpochPipeline(eng, reducer)
     flagged_total = 0
 
     def step(drain: bool):
@@ -132,17 +140,14 @@ def main(argv=None):
         eng.pump(args.batches_per_step, drain=drain)
         # router hand-off of fraud-routed transactions (transaction.outgoing{type=fraud})
         flagged_total += len(eng.drain_flagged())
-        # X2/X3: the previous epoch's reduction finished long ago (one step of slack); flip
-        # the counter epoch and all-reduce the closed buffer on the side stream.
-        if reducer.done is not None:
-            reducer.done.synchronize()
-        closed = eng.flip_epoch(reducer.side)
-        reducer.submit(closed, None)
+        # X2/X3: flip the counter epoch; the previously closed epoch (all of whose batches
+        # have completed by now) is all-reduced over RCCL on the side stream
+        epochs.tick()
 
     for _ in range(args.warmup):
         step(drain=False)
     eng.pump(0, drain=True)
-    reducer.wait()
+    epochs.finish()
     eng.reset_stats()
     c0 = reducer.snapshot()[0]
     rows0, fraud0 = int(c0[0]), int(c0[1])
@@ -154,7 +159,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(drain=(k == args.steps - 1))
-    reducer.wait()
+    epochs.finish()
     torch.cuda.synchronize(dev)
     barrier(ctx)
     t1 = time.perf_counter()
@@ -178,7 +183,8 @@ def main(argv=None):
     p50_unloaded = None
     if not args.no_unloaded_probe:
         probe = StreamEngine(dm, batch=args.batch, depth=1, streams=1, input_mode=args.input_mode,
-                             output_mode=args.output_mode, threshold=args.threshold, device=dev.index)
+                             output_mode=args.output_mode, threshold=args.threshold, device=dev.index,
+                             exec_mode=exec_mode)
         probe.add_log(my_parts[0], logs[0])
         probe.pump(20, drain=True)
         probe.reset_stats()
@@ -207,7 +213,8 @@ def main(argv=None):
                              "gbdt": f"oblivious_gbdt_{args.gbdt_trees}x{args.gbdt_depth}"}[args.model],
                    "global_batch": args.batch * W, "seq_len": 1, "micro_batch": args.batch,
                    "parallelism": f"dp{W}", "input_mode": args.input_mode,
-                   "output_mode": args.output_mode, "depth": args.depth, "streams": args.streams,
+                   "output_mode": args.output_mode, "exec_mode": exec_mode, "depth": args.depth,
+                   "streams": args.streams,
                    "batches_per_step": args.batches_per_step, "numa_node_rank0": numa_node},
         "p50_latency_us": round(p50_us, 2),
         "p99_latency_us": round(p99_us, 2),

@@ -100,7 +100,10 @@ def _stats(st: EngineStats) -> StepStats:
 class StreamEngine:
     def __init__(self, dm: DeviceModel, batch: int = 4096, depth: int = 8, streams: int = 2,
                  input_mode: str = "dma", output_mode: str = "zerocopy", threshold: float = 0.5,
-                 device: Optional[int] = None, flag_capacity: int = 1 << 20):
+                 device: Optional[int] = None, flag_capacity: int = 1 << 20, exec_mode: str = "launch",
+                 persist_grid: int = 0):
+        """exec_mode: "launch" = one fused kernel launch per micro-batch; "persistent" = one
+        long-running kernel fed through a descriptor ring (MLP/LR, zero-copy outputs)."""
         self.dm = dm
         self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device())
         self.batch = int(batch)
@@ -119,9 +122,15 @@ class StreamEngine:
         cfg.input_mode = INPUT_MODES[input_mode]
         cfg.output_mode = OUTPUT_MODES[output_mode]
         cfg.flag_capacity = int(flag_capacity)
+        cfg.exec_mode = {"launch": 0, "persistent": 1}[exec_mode]
+        cfg.persist_grid = int(persist_grid)
+        self.exec_mode = exec_mode
+        self.flips = 0
         cfg.counters[0] = self.counters[0].data_ptr()
         cfg.counters[1] = self.counters[1].data_ptr()
-        torch.cuda.synchronize(self.device)     # counters zeroed before the engine's streams use them
+        # counters zeroed before the engine's streams use them (stream sync, never a device
+        # sync: another engine's persistent kernel may be resident)
+        torch.cuda.current_stream(self.device).synchronize()
         self.h = lib().ccfd_engine_create(C.byref(cfg))
         if not self.h:
             raise RuntimeError(f"ccfd_engine_create failed: {last_error()}")
@@ -170,7 +179,12 @@ class StreamEngine:
         idx = lib().ccfd_engine_flip_epoch(C.c_void_p(self.h), hs)
         if idx < 0:
             raise RuntimeError(f"flip_epoch failed: {last_error()}")
+        self.flips += 1
         return self.counters[idx]
+
+    def epoch_complete(self, flip_count: int) -> bool:
+        """True once every micro-batch submitted before flip number ``flip_count`` completed."""
+        return lib().ccfd_engine_epoch_complete(C.c_void_p(self.h), int(flip_count)) == 1
 
     def drain_flagged(self, max_records: int = 1 << 30) -> np.ndarray:
         out: List[np.ndarray] = []

@@ -41,19 +41,21 @@ class EngineServiceConfig:
     reduce_period_ms: float = 10.0
     threshold: float = 0.5
     input_mode: str = "zerocopy"
+    exec_mode: str = "launch"        # "persistent": one resident kernel fed by a descriptor ring
     max_fetch: int = 2000
 
 
 class EngineService:
     def __init__(self, ctx, dm, broker, router, cfg: EngineServiceConfig, reducer=None, partitions=None):
         from ..engine import StreamEngine
-        from ..parallel.dp import CounterReducer, assign_partitions
+        from ..parallel.dp import CounterReducer, EpochPipeline, assign_partitions
         self.ctx = ctx
         self.cfg = cfg
         self.broker = broker
         self.router = router
         self.engine = StreamEngine(dm, batch=cfg.batch, depth=cfg.depth, streams=cfg.streams,
-                                   input_mode=cfg.input_mode, threshold=cfg.threshold, device=ctx.device.index)
+                                   input_mode=cfg.input_mode, threshold=cfg.threshold, device=ctx.device.index,
+                                   exec_mode=cfg.exec_mode)
         n_parts = broker.partitions(cfg.topic)
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:
@@ -61,6 +63,7 @@ class EngineService:
         self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
             if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
         self.reducer = reducer or CounterReducer(ctx, ctx.device)
+        self.epochs = EpochPipeline(self.engine, self.reducer)
         # per partition: (ring row end, next kafka offset) of ingested messages, oldest first
         self._pending: Dict[int, Deque[Tuple[int, int]]] = {p: collections.deque() for p in self.partitions}
         self._rows_in: Dict[int, int] = {p: 0 for p in self.partitions}
@@ -133,10 +136,8 @@ class EngineService:
         self._commit_done()
         now = time.monotonic()
         if (now - self.last_reduce) * 1e3 >= self.cfg.reduce_period_ms:
-            if self.reducer.done is not None:
-                self.reducer.done.synchronize()
             lat = st.lat_hist.astype(np.int64)          # cumulative since reset -> send the delta
-            self.reducer.submit(self.engine.flip_epoch(self.reducer.side), lat - self._lat_prev)
+            self.epochs.tick(lat - self._lat_prev)
             self._lat_prev = lat
             self.last_reduce = now
         return int(st.rows)

@@ -35,7 +35,8 @@ class EngineConfig(C.Structure):
                 ("gbdt_trees", C.c_int32), ("gbdt_depth", C.c_int32), ("threshold", C.c_float),
                 ("max_batch", C.c_int32), ("depth", C.c_int32), ("n_streams", C.c_int32),
                 ("input_mode", C.c_int32), ("output_mode", C.c_int32), ("flag_capacity", C.c_int32),
-                ("_pad", C.c_int32), ("counters", C.c_void_p * 2)]
+                ("exec_mode", C.c_int32), ("persist_grid", C.c_int32), ("_pad", C.c_int32),
+                ("counters", C.c_void_p * 2)]
 
 
 class Flagged(C.Structure):
@@ -92,6 +93,7 @@ def lib() -> C.CDLL:
         L.ccfd_engine_pump.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.POINTER(EngineStats)]
         L.ccfd_engine_score_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.ccfd_engine_flip_epoch.argtypes = [C.c_void_p, C.c_void_p]
+        L.ccfd_engine_epoch_complete.argtypes = [C.c_void_p, C.c_int64]
         L.ccfd_engine_drain_flagged.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.ccfd_engine_drain_flagged.restype = C.c_int64
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]

@@ -1,6 +1,6 @@
 """Multi-GPU data parallelism (one process per GPU, RCCL over xGMI)."""
-from .dp import (CounterReducer, DistContext, all_max, all_sum, assign_partitions, barrier,
+from .dp import (CounterReducer, DistContext, EpochPipeline, all_max, all_sum, assign_partitions, barrier,
                  broadcast_blob, hist_quantile, init_distributed)
 
-__all__ = ["CounterReducer", "DistContext", "all_max", "all_sum", "assign_partitions", "barrier",
+__all__ = ["CounterReducer", "DistContext", "EpochPipeline", "all_max", "all_sum", "assign_partitions", "barrier",
            "broadcast_blob", "hist_quantile", "init_distributed"]

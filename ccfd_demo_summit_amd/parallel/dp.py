@@ -151,6 +151,39 @@ class CounterReducer:
         return t[:N_COUNTER_SLOTS], t[N_COUNTER_SLOTS:]
 
 
+class EpochPipeline:
+    """Drives X2 for one engine: flip the counter epoch, and hand the CLOSED buffer to the
+    CounterReducer only once every micro-batch of that epoch has completed (in the
+    persistent exec mode there is no per-batch event a stream could wait on, so the host
+    observes completion records instead).  Buffers alternate, so a flip also waits for the
+    previous reduction (one epoch of slack: never on the critical path in steady state)."""
+
+    def __init__(self, engine, reducer: CounterReducer):
+        self.engine = engine
+        self.reducer = reducer
+        self.pending = None          # (buffer, flip_count, lat_delta)
+
+    def tick(self, lat_delta=None) -> None:
+        if self.pending is not None and self.engine.epoch_complete(self.pending[1]):
+            self.reducer.submit(self.pending[0], self.pending[2])
+            self.pending = None
+        if self.pending is None:
+            if self.reducer.done is not None:
+                self.reducer.done.synchronize()
+            buf = self.engine.flip_epoch(self.reducer.side)
+            self.pending = (buf, self.engine.flips, lat_delta)
+
+    def finish(self) -> None:
+        """Call after the engine has drained: reduce the last closed AND the open epoch."""
+        if self.pending is not None:
+            self.reducer.submit(self.pending[0], self.pending[2])
+            self.pending = None
+        if self.reducer.done is not None:
+            self.reducer.done.synchronize()
+        self.reducer.submit(self.engine.flip_epoch(self.reducer.side), None)
+        self.reducer.wait()
+
+
 class _nullctx:
     def __enter__(self):
         return self

@@ -108,7 +108,9 @@ struct Slot {
   volatile unsigned long long* h_done = nullptr;
   unsigned long long* h_done_dev = nullptr;
   unsigned long long expect = 0;
+  volatile unsigned long long* done_ptr = nullptr;   // h_done, or the persistent ctl record
   bool use_flag = false;
+  int64_t seq_no = 0;
 };
 
 inline void cpu_relax() {
@@ -169,7 +171,7 @@ class Engine {
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_route_dev), s.h_route, 0));
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       HIPCHK(hipMalloc(reinterpret_cast<void**>(&s.d_ctl), 2 * sizeof(unsigned int)));
-      HIPCHK(hipMemset(s.d_ctl, 0, 2 * sizeof(unsigned int)));
+      HIPCHK(hipMemsetAsync(s.d_ctl, 0, 2 * sizeof(unsigned int), streams[0]));
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_flag), B * sizeof(unsigned int),
                            hipHostMallocMapped | hipHostMallocPortable));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_flag_dev), s.h_flag, 0));
@@ -179,13 +181,129 @@ class Engine {
       s.h_done = static_cast<volatile unsigned long long*>(hd);
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_done_dev), hd, 0));
     }
-    HIPCHK(hipDeviceSynchronize());
+    // never hipDeviceSynchronize here: another engine's persistent kernel may be resident
+    HIPCHK(hipStreamSynchronize(streams[0]));
     ring.resize(std::max(1024, cfg.flag_capacity));
+    if (cfg.exec_mode == 1) return persist_init();
     return 0;
+  }
+
+  // ------------------------------------------------------------------ persistent mode
+  bool persistent = false;
+  ccfd_persist_ctl* pctl = nullptr;        // host (coherent pinned)
+  ccfd_persist_desc* pdesc = nullptr;      // host (coherent pinned)
+  ccfd_persist_dev* pdev = nullptr;        // device
+  hipStream_t pstream = nullptr;
+  bool prunning = false;
+  int persist_C = 0;
+  int64_t completed_upto = 0;              // batches completed in order (seq count)
+  std::vector<int64_t> flip_seq;           // seq at each epoch flip
+
+  int persist_init() {
+    if (cfg.model != CCFD_MODEL_MLP && cfg.model != CCFD_MODEL_LR) {
+      set_error("persistent exec_mode supports the MLP and LR models");
+      return -1;
+    }
+    if (cfg.output_mode != 0 || cfg.depth > CCFD_PERSIST_MAX_RING) {
+      set_error("persistent exec_mode needs zero-copy outputs and depth <= 64");
+      return -1;
+    }
+    void* p = nullptr;
+    HIPCHK(hipHostMalloc(&p, sizeof(ccfd_persist_ctl), hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+    std::memset(p, 0, sizeof(ccfd_persist_ctl));
+    pctl = static_cast<ccfd_persist_ctl*>(p);
+    HIPCHK(hipHostMalloc(&p, sizeof(ccfd_persist_desc) * cfg.depth,
+                         hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+    std::memset(p, 0, sizeof(ccfd_persist_desc) * cfg.depth);
+    pdesc = static_cast<ccfd_persist_desc*>(p);
+    const int C = (cfg.max_batch + CCFD_PERSIST_ITEM_ROWS - 1) / CCFD_PERSIST_ITEM_ROWS;
+    ccfd_persist_dev init{};
+    for (int i = 0; i < CCFD_PERSIST_MAX_RING; ++i) init.remaining[i] = (unsigned)C;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&pdev), sizeof(ccfd_persist_dev)));
+    HIPCHK(hipMemcpy(pdev, &init, sizeof(init), hipMemcpyHostToDevice));
+    HIPCHK(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
+    persist_C = C;
+    persistent = true;
+    return 0;
+  }
+
+  // Launch the persistent kernel (lazily, at the first post after a halt).  Device state is
+  // re-based on the host's `posted` count: every posted batch has completed (halt drains).
+  int persist_launch() {
+    ccfd_persist_dev init{};
+    init.work_next = (unsigned long long)pctl->posted * (unsigned long long)persist_C;
+    for (int i = 0; i < CCFD_PERSIST_MAX_RING; ++i) init.remaining[i] = (unsigned)persist_C;
+    HIPCHK(hipMemcpyAsync(pdev, &init, sizeof(init), hipMemcpyHostToDevice, pstream));
+    HIPCHK(hipStreamSynchronize(pstream));
+    __atomic_store_n(&pctl->stop, 0ull, __ATOMIC_RELEASE);
+    ccfd_persist_args a{};
+    void* d = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&d, pctl, 0));
+    a.ctl = static_cast<ccfd_persist_ctl*>(d);
+    HIPCHK(hipHostGetDevicePointer(&d, pdesc, 0));
+    a.desc = static_cast<const ccfd_persist_desc*>(d);
+    a.dev = pdev;
+    a.ring = cfg.depth;
+    a.items_per_batch = persist_C;
+    a.model = cfg.model;
+    a.threshold = cfg.threshold;
+    a.blob = cfg.blob;
+    a.counters[0] = cfg.counters[0];
+    a.counters[1] = cfg.counters[1];
+    const int grid = cfg.persist_grid > 0 ? cfg.persist_grid : 256;
+    int rc = ccfd_persist_launch(&a, grid, pstream);
+    if (rc) { set_error("persistent kernel launch failed"); return rc; }
+    prunning = true;
+    return 0;
+  }
+
+  // Stop the persistent kernel: every posted batch must be complete (callers drain first);
+  // all workgroups then wait on an unposted batch, see `stop` and exit.  Bounded wait.
+  int persist_halt() {
+    if (!prunning) return 0;
+    __atomic_store_n(&pctl->stop, 1ull, __ATOMIC_RELEASE);
+    const int64_t t0 = now_ns();
+    hipError_t q;
+    while ((q = hipStreamQuery(pstream)) == hipErrorNotReady) {
+      if (now_ns() - t0 > 20ll * 1000000000ll) { set_error("persistent kernel did not stop"); return -6; }
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    prunning = false;
+    if (q != hipSuccess) { set_error(std::string("persistent kernel: ") + hipGetErrorString(q)); return -4; }
+    return 0;
+  }
+
+  void persist_free() {
+    if (!persistent) return;
+    for (auto& s : slots) if (s.busy) wait_done(s);
+    persist_halt();
+    hipStreamDestroy(pstream);
+    hipFree(pdev);
+    hipHostFree(pdesc);
+    hipHostFree(pctl);
+    persistent = false;
+  }
+
+  // post micro-batch `s` (already filled: part/start/rows) to the persistent kernel
+  void persist_post(Slot& s, const float* x_dev) {
+    const uint64_t sq = seq;                       // caller increments seq after submit
+    ccfd_persist_desc& d = pdesc[sq % cfg.depth];
+    d.x = x_dev;
+    d.proba = s.h_proba_dev;
+    d.route = s.h_route_dev;
+    d.flag_idx = s.h_flag_dev;
+    d.n = s.rows;
+    d.epoch = epoch & 1;
+    d.seq = sq;
+    s.expect = sq + 1;
+    s.use_flag = true;
+    s.done_ptr = reinterpret_cast<volatile unsigned long long*>(pctl->done[sq % cfg.depth]);
+    __atomic_store_n(&pctl->posted, sq + 1, __ATOMIC_RELEASE);
   }
 
   ~Engine() {
     hipSetDevice(cfg.device);
+    persist_free();
     for (auto& s : slots) {
       if (s.busy) wait_done(s);
       if (s.d_x) hipFree(s.d_x);
@@ -256,7 +374,7 @@ class Engine {
   }
 
   bool is_done(const Slot& s) {
-    if (s.use_flag) return s.h_done[0] == s.expect;
+    if (s.use_flag) return s.done_ptr[0] == s.expect;
     return hipEventQuery(s.ev) == hipSuccess;
   }
 
@@ -268,7 +386,7 @@ class Engine {
     // spin on the pinned completion record; every 64K spins check the device for errors
     // and give up after 60 s so a faulted kernel can never hang the host thread
     const int64_t t0 = now_ns();
-    for (uint64_t it = 0; s.h_done[0] != s.expect; ++it) {
+    for (uint64_t it = 0; s.done_ptr[0] != s.expect; ++it) {
       cpu_relax();
       if ((it & 0xFFFF) == 0xFFFF) {
         hipError_t e = hipGetLastError();
@@ -292,7 +410,7 @@ class Engine {
     lat_hist[std::min(255, (int)std::floor(4.0 * std::log2(ns)))]++;
     uint64_t nf = 0;
     if (s.use_flag) {
-      nf = s.h_done[1];
+      nf = s.done_ptr[1];
       if (nf) push_flagged_idx(s, nf);
     } else {
       for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
@@ -307,6 +425,7 @@ class Engine {
     }
     s.busy = false;
     s.t_arrival = 0;
+    completed_upto = std::max<int64_t>(completed_upto, s.seq_no + 1);
     t_complete_ns += now_ns() - t;
     return 0;
   }
@@ -318,14 +437,28 @@ class Engine {
       Slot& s = slots[(seq + k) % D];
       if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
     }
+    // fully drained: let the persistent kernel exit so the device is idle (and a
+    // device-wide synchronize by the caller can never wait on a resident kernel)
+    if (persistent) return persist_halt();
     return 0;
   }
 
   int submit(Slot& s, const float* x_dev_or_host, const float* x_host, int rows, hipStream_t stream,
              bool force_dma = false) {
     s.t_submit = now_ns();
+    s.seq_no = (int64_t)seq;
     struct Acc { uint64_t& a; int64_t t0; ~Acc() { a += now_ns() - t0; } } acc{t_submit_ns, s.t_submit};
     const float* xk = x_dev_or_host;
+    if (persistent) {
+      if (cfg.input_mode == 0 || force_dma) {
+        HIPCHK(hipMemcpy(s.d_x, x_host, (size_t)rows * CCFD_N_FEATURES * sizeof(float), hipMemcpyHostToDevice));
+        xk = s.d_x;
+      }
+      if (!prunning) { int rc = persist_launch(); if (rc) return rc; }
+      persist_post(s, xk);
+      s.busy = true;
+      return 0;
+    }
     if (cfg.input_mode == 0 || force_dma) {
       HIPCHK(hipMemcpyAsync(s.d_x, x_host, (size_t)rows * CCFD_N_FEATURES * sizeof(float),
                             hipMemcpyHostToDevice, stream));
@@ -344,6 +477,7 @@ class Engine {
       a.flag_idx = s.h_flag_dev;
       a.done_rec = s.h_done_dev;
       a.done_seq = s.expect;
+      s.done_ptr = s.h_done;
     }
     int rc = ccfd_score_launch(&a, stream);
     if (rc) return rc;
@@ -428,21 +562,30 @@ class Engine {
       rc = wait_done(s);
       if (rc) return rc;
       s.busy = false;
+      completed_upto = std::max<int64_t>(completed_upto, s.seq_no + 1);
       if (proba_out) std::memcpy(proba_out + off, s.h_proba, rows * sizeof(float));
       if (route_out) std::memcpy(route_out + off, s.h_route, rows);
     }
-    return 0;
+    return persistent ? persist_halt() : 0;
   }
 
   int flip_epoch(void* side_stream) {
     HIPCHK(hipSetDevice(cfg.device));
     const int closed = epoch & 1;
-    for (size_t i = 0; i < streams.size(); ++i) {
-      HIPCHK(hipEventRecord(flip_ev[i], streams[i]));
-      if (side_stream) HIPCHK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(side_stream), flip_ev[i], 0));
+    if (!persistent) {
+      for (size_t i = 0; i < streams.size(); ++i) {
+        HIPCHK(hipEventRecord(flip_ev[i], streams[i]));
+        if (side_stream) HIPCHK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(side_stream), flip_ev[i], 0));
+      }
     }
+    flip_seq.push_back((int64_t)seq);
     ++epoch;
     return closed;
+  }
+
+  int epoch_complete(int64_t flip_count) {
+    if (flip_count <= 0 || flip_count > (int64_t)flip_seq.size()) return -1;
+    return completed_upto >= flip_seq[flip_count - 1] ? 1 : 0;
   }
 
   // ------------------------------------------------------------------ ring (streaming) mode
@@ -585,6 +728,10 @@ int ccfd_engine_score_sync(void* eng, const float* x, int32_t n, float* proba_ou
 
 int ccfd_engine_flip_epoch(void* eng, void* side_stream) {
   return static_cast<Engine*>(eng)->flip_epoch(side_stream);
+}
+
+int ccfd_engine_epoch_complete(void* eng, int64_t flip_count) {
+  return static_cast<Engine*>(eng)->epoch_complete(flip_count);
 }
 
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max) {

@@ -57,6 +57,52 @@ typedef struct ccfd_score_args {
 int ccfd_score_launch(const ccfd_score_args* a, void* stream);
 
 // ---------------------------------------------------------------------------
+// Persistent streaming kernel (exec_mode = 1): ONE long-running launch per engine; the
+// host publishes micro-batch descriptors into a ring in coherent pinned memory and bumps
+// `posted`; resident workgroups claim 64-row work items with one device atomic, wait for
+// the descriptor to be posted, score, and the last workgroup of a micro-batch publishes
+// its completion record.  No per-batch launch, event or copy on the host.
+#define CCFD_PERSIST_MAX_RING 64
+#define CCFD_PERSIST_ITEM_ROWS 64
+
+typedef struct ccfd_persist_desc {   // host-coherent pinned, written before `posted`
+  const float* x;          // device-visible rows [n][30]
+  float* proba;            // host-mapped out [n] (may be NULL)
+  uint8_t* route;          // host-mapped out [n] (may be NULL)
+  unsigned int* flag_idx;  // host-mapped out: compacted fraud-routed row indices
+  int32_t n;
+  int32_t epoch;           // counter buffer index (0/1) for the X2 epoch flip
+  uint64_t seq;            // 0-based micro-batch sequence number
+} ccfd_persist_desc;
+
+typedef struct ccfd_persist_ctl {    // host-coherent pinned
+  uint64_t posted;         // host -> GPU: number of descriptors published
+  uint64_t stop;           // host -> GPU: exit once every posted batch is claimed
+  uint64_t done[CCFD_PERSIST_MAX_RING][2];   // GPU -> host: {seq + 1, #flagged} per ring slot
+  uint64_t exited;         // GPU -> host: workgroups that left the loop
+} ccfd_persist_ctl;
+
+typedef struct ccfd_persist_dev {    // device memory
+  unsigned long long work_next;                   // next work item to claim
+  unsigned int remaining[CCFD_PERSIST_MAX_RING];  // items left per ring slot
+  unsigned int nflag[CCFD_PERSIST_MAX_RING];      // flagged rows per ring slot
+} ccfd_persist_dev;
+
+typedef struct ccfd_persist_args {
+  ccfd_persist_ctl* ctl;           // device alias of the host control block
+  const ccfd_persist_desc* desc;   // device alias of the host descriptor ring
+  ccfd_persist_dev* dev;
+  int32_t ring;                    // R ring slots (<= CCFD_PERSIST_MAX_RING)
+  int32_t items_per_batch;         // ceil(max_batch / 64)
+  int32_t model;                   // MLP or LR
+  float threshold;
+  const void* blob;
+  unsigned long long* counters[2];
+} ccfd_persist_args;
+
+int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* stream);
+
+// ---------------------------------------------------------------------------
 // Host memory (pinned, device-mapped; used for partition logs and result rings)
 void* ccfd_host_alloc(size_t bytes);                 // hipHostMalloc(mapped|portable)
 int ccfd_host_free(void* p);
@@ -76,6 +122,8 @@ typedef struct ccfd_engine_config {
   int32_t input_mode;          // 0 = DMA H2D into HBM staging, 1 = zero-copy host reads
   int32_t output_mode;         // 0 = zero-copy host writes, 1 = device + D2H copy
   int32_t flag_capacity;       // flagged-transaction ring capacity (records)
+  int32_t exec_mode;           // 0 = one fused launch per micro-batch, 1 = persistent kernel
+  int32_t persist_grid;        // workgroups of the persistent kernel (0 = 256)
   int32_t _pad;
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
 } ccfd_engine_config;
@@ -122,6 +170,10 @@ int ccfd_engine_score_sync(void* eng, const float* x, int32_t n, float* proba_ou
 // buffer; `side_stream` (hipStream_t) is made to wait for every batch of the closed epoch.
 // Returns the index (0/1) of the closed buffer.
 int ccfd_engine_flip_epoch(void* eng, void* side_stream);
+// 1 once every micro-batch submitted before the flip that closed `epoch_index` (the value
+// returned by flip) has completed.  Required before reducing a closed epoch buffer in
+// exec_mode 1 (the persistent kernel has no per-batch events a stream could wait on).
+int ccfd_engine_epoch_complete(void* eng, int64_t flip_count);
 // Drain up to `max` flagged records (fraud route) into `out`; returns count.
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
 int64_t ccfd_engine_cursor(void* eng, int partition);

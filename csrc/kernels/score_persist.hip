@@ -1,0 +1,205 @@
+// Persistent streaming scorer (engine exec_mode = 1).
+//
+// One launch lives as long as the engine.  Every resident workgroup loops:
+//   claim work item i (one agent-scope atomic)      -> micro-batch b = i / C, chunk c = i % C
+//   wait until the host has posted b               (thread 0 polls ctl->posted, system scope,
+//                                                   cached in an SGPR; s_sleep back-off)
+//   read descriptor b % R (x, outputs, n, epoch)   -> LDS
+//   4 waves x 16-row tiles = rows [64c, 64c+64) scored with the same fused math as the
+//   per-batch kernels (mlp_core.h), outputs written straight to host-mapped memory,
+//   fraud rows appended to the descriptor's compacted flag list
+//   counters + amount histogram -> counters[desc.epoch] (one atomic set per item)
+//   release (system scope) + ticket on remaining[b % R]; the last ticket publishes
+//   ctl->done[b % R] = {b + 1, #flagged}
+// A workgroup only waits for the HOST (never for another workgroup), so residency of the
+// whole grid is not required and nothing can deadlock; it exits when the host sets `stop`
+// while it waits for an unposted batch.  The host never posts batch b into ring slot
+// b % R before observing done for b - R, which is what makes the slot-local state
+// (remaining/nflag reset by the last ticket) safe to reuse.
+#include "mlp_core.h"
+
+namespace ccfd {
+
+namespace {
+
+template <int kModel>
+__global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
+  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
+  __shared__ __attribute__((aligned(16))) float sx[4][kTileRows * kF + 4];
+  __shared__ EpilogueLds epi;
+  __shared__ ccfd_persist_desc sdesc;
+  __shared__ unsigned long long s_item;
+  __shared__ int s_cmd;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int C = a.items_per_batch;
+
+  if (kModel == CCFD_MODEL_MLP) mlp_stage(a.blob, sblob, tid, 256);
+  else for (int i = tid; i < 448 / 16; i += 256) reinterpret_cast<int4*>(sblob)[i] = reinterpret_cast<const int4*>(a.blob)[i];
+  epi_init(epi);
+  __syncthreads();
+
+  MlpLane L{};
+  float wm[8];
+  if (kModel == CCFD_MODEL_MLP) {
+    L = mlp_lane(sblob, g);
+  } else {
+    const unsigned flags = *reinterpret_cast<const unsigned*>(sblob + 4);
+    L.b3 = *reinterpret_cast<const float*>(sblob + 8);
+    L.log_amount = (flags & 1u) != 0;
+    const float* mu = reinterpret_cast<const float*>(sblob + 64) + 8 * g;
+    const float* isg = reinterpret_cast<const float*>(sblob + 192) + 8 * g;
+    const float* w = reinterpret_cast<const float*>(sblob + 320) + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { L.mu[j] = mu[j]; L.isg[j] = isg[j]; wm[j] = w[j]; }
+  }
+  float* tile_lds = sx[wave];
+  unsigned long long posted_cache = 0;     // thread 0 only
+
+  for (;;) {
+    if (tid == 0) {
+      const unsigned long long item =
+          __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long b = item / (unsigned long long)C;
+      int cmd = 0;
+      unsigned sleep_n = 1;
+      while (posted_cache <= b) {
+        posted_cache = __hip_atomic_load(&a.ctl->posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (posted_cache > b) break;
+        if (__hip_atomic_load(&a.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) { cmd = 1; break; }
+        // back-off: ~1 us .. ~16 us between polls of host memory
+        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(32);
+        sleep_n = sleep_n < 16 ? sleep_n * 2 : 16;
+      }
+      if (!cmd) {
+        const ccfd_persist_desc* d = a.desc + (b % (unsigned long long)a.ring);
+        sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->proba), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->route), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->flag_idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        const unsigned long long ne = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        sdesc.n = (int32_t)(ne & 0xffffffffull);
+        sdesc.epoch = (int32_t)(ne >> 32);
+        sdesc.seq = b;
+      } else {
+        __hip_atomic_fetch_add(&a.ctl->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      s_item = item;
+      s_cmd = cmd;
+    }
+    __syncthreads();
+    if (s_cmd) break;
+
+    const unsigned long long item = s_item;
+    const int chunk = (int)(item % (unsigned long long)C);
+    const int slot = (int)(sdesc.seq % (unsigned long long)a.ring);
+    const int n = sdesc.n;
+    const float* x = sdesc.x;
+    const int tile = chunk * 4 + wave;
+    const int row0 = tile * kTileRows;
+    const int row = row0 + c;
+    const bool valid = row < n;
+
+    if (row0 < n) {                                      // wave-uniform
+      TileRegs r;
+      tile_issue(x + (size_t)row0 * kF, min(kTileRows, n - row0) * kF * 4, lane, r);
+      tile_store(tile_lds, lane, r);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      float xv[8];
+      tile_features(tile_lds, c, g, xv);
+      float p, amount;
+      if (kModel == CCFD_MODEL_MLP) {
+        p = mlp_tile(sblob, L, xv, g, lane, amount);
+      } else {
+        amount = xv[5];
+        if (g == 3) { xv[6] = 0.f; xv[7] = 0.f; if (L.log_amount) xv[5] = log1pf(fmaxf(xv[5], 0.f)); }
+        float z = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z = fmaf((xv[j] - L.mu[j]) * L.isg[j], wm[j], z);
+        z += __shfl_xor(z, 16);
+        z += __shfl_xor(z, 32);
+        p = sigmoid(z + L.b3);
+      }
+      const bool fr = valid && (p >= a.threshold);
+      if (valid && g == 0) {
+        if (sdesc.proba) sdesc.proba[row] = p;
+        if (sdesc.route) sdesc.route[row] = fr ? 1 : 0;
+      }
+      unsigned long long ps = (valid && g == 0) ? (unsigned long long)(p * 1e6f + 0.5f) : 0ull;
+      ps = wave_sum_u64(ps);
+      const unsigned nf = __popcll(__ballot(fr && g == 0));
+      const unsigned nv = __popcll(__ballot(valid && g == 0));
+      if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
+      // compacted flag list (reservation on the slot's device counter)
+      const unsigned long long m = __ballot(fr && g == 0);
+      if (m && sdesc.flag_idx) {
+        const int leader = __builtin_ffsll((long long)m) - 1;
+        unsigned base = 0;
+        if (lane == leader)
+          base = __hip_atomic_fetch_add(&a.dev->nflag[slot], (unsigned)__popcll(m), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        base = __shfl(base, leader);
+        if (fr && g == 0) sdesc.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
+      }
+      if (lane == 0) {
+        atomicAdd(&epi.fraud, nf);
+        atomicAdd(&epi.rows, nv);
+        atomicAdd(&epi.psum_e6, ps);
+      }
+    }
+    // per-item epilogue: counters of this item into the epoch's buffer, reset LDS state
+    __syncthreads();
+    unsigned long long* cnt = a.counters[sdesc.epoch & 1];
+    if (tid < 2 * kNB) {
+      const unsigned h = epi.hist[tid];
+      if (h && cnt) atomicAdd(&cnt[(tid < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + tid],
+                              (unsigned long long)h);
+      epi.hist[tid] = 0;
+    } else if (tid == 64) {
+      if (cnt && epi.rows) {
+        atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)epi.rows);
+        atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)epi.fraud);
+        atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(epi.rows - epi.fraud));
+        atomicAdd(&cnt[CCFD_CNT_PROBA_E6], epi.psum_e6);
+      }
+      epi.rows = 0; epi.fraud = 0; epi.psum_e6 = 0;
+    }
+    // completion: publish this item's outputs, take a ticket, last ticket signals the host
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned left = __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_ACQ_REL,
+                                                   __HIP_MEMORY_SCOPE_AGENT) - 1u;
+      if (left == 0) {
+        const unsigned nflag = __hip_atomic_load(&a.dev->nflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.dev->nflag[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.dev->remaining[slot], (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.ctl->done[slot][1], (unsigned long long)nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ctl->done[slot][0], sdesc.seq + 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+}  // namespace ccfd
+
+extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* stream) {
+  using namespace ccfd;
+  if (!a || !a->ctl || !a->desc || !a->dev || !a->blob) return -1;
+  if (a->ring <= 0 || a->ring > CCFD_PERSIST_MAX_RING || a->items_per_batch <= 0) return -2;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (a->model == CCFD_MODEL_MLP)
+    hipLaunchKernelGGL(persist_kernel<CCFD_MODEL_MLP>, dim3(grid), dim3(256), 0, s, *a);
+  else if (a->model == CCFD_MODEL_LR)
+    hipLaunchKernelGGL(persist_kernel<CCFD_MODEL_LR>, dim3(grid), dim3(256), 0, s, *a);
+  else
+    return -3;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

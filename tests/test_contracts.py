@@ -113,3 +113,14 @@ def test_seldon_codec():
         seldon.parse_request({"nodata": 1})
     with pytest.raises(seldon.SeldonError):
         seldon.parse_request(b"{not json")
+
+
+def test_dashboards_reference_metric_names():
+    from ccfd_demo_summit_amd.metrics.dashboards import all_dashboards
+    text = json.dumps(all_dashboards())
+    for name in ("transaction_incoming_total", "transaction_outgoing_total", "notifications_incoming_total",
+                 "fraud_investigation_amount", "fraud_approved_low_amount", "fraud_approved_amount",
+                 "fraud_rejected_amount", "proba_1", "V17", "V10", "Amount",
+                 "seldon_api_engine_server_requests_seconds_count",
+                 "seldon_api_engine_client_requests_seconds_bucket", "ccfd_gpu_rows_total"):
+        assert name in text, name

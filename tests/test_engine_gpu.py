@@ -17,15 +17,16 @@ def setup(gpu):
     return X, m
 
 
-@pytest.mark.parametrize("input_mode,output_mode", [("dma", "zerocopy"), ("zerocopy", "zerocopy"),
-                                                    ("dma", "dma"), ("zerocopy", "dma")])
-def test_engine_pump_matches_oracle(gpu, setup, input_mode, output_mode):
+@pytest.mark.parametrize("input_mode,output_mode,exec_mode", [
+    ("dma", "zerocopy", "launch"), ("zerocopy", "zerocopy", "launch"), ("dma", "dma", "launch"),
+    ("zerocopy", "dma", "launch"), ("zerocopy", "zerocopy", "persistent"), ("dma", "zerocopy", "persistent")])
+def test_engine_pump_matches_oracle(gpu, setup, input_mode, output_mode, exec_mode):
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
     dm = DeviceModel(m, gpu)
     eng = StreamEngine(dm, batch=4096, depth=4, streams=2, input_mode=input_mode,
-                       output_mode=output_mode)
+                       output_mode=output_mode, exec_mode=exec_mode)
     log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000)
     eng.add_log(0, log)
     st = eng.pump(6)
@@ -60,7 +61,8 @@ def test_engine_score_sync_pageable_input(gpu, setup):
     eng.close()
 
 
-def test_ring_streaming_mode_deadline_flush(gpu, setup):
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     """Live ingest: producer writes into the pinned SPSC ring (rows + JSON), run() scores full
     micro-batches and deadline-flushes the partial tail; ring space is recycled."""
     import json
@@ -69,7 +71,8 @@ def test_ring_streaming_mode_deadline_flush(gpu, setup):
     from ccfd_demo_summit_amd.engine import StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
-    eng = StreamEngine(DeviceModel(m, gpu), batch=1024, depth=4, streams=2, input_mode="zerocopy")
+    eng = StreamEngine(DeviceModel(m, gpu), batch=1024, depth=4, streams=2, input_mode="zerocopy",
+                       exec_mode=exec_mode)
     eng.set_ring(0, 4096)
     n = 10_000                                   # > capacity: exercises wrap + backpressure
     ids = np.arange(n, dtype=np.uint64) + 7
@@ -99,3 +102,28 @@ def test_ring_streaming_mode_deadline_flush(gpu, setup):
     assert got_rows == 300
     assert eng.cursor(0) == n + 300
     eng.close()
+
+
+def test_persistent_engine_many_steps_counters_exact(gpu, setup):
+    """Persistent kernel across repeated halt/relaunch cycles: counters and epochs exact."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import CounterReducer, DistContext, EpochPipeline
+    X, m = setup
+    eng = StreamEngine(DeviceModel(m, gpu), batch=2048, depth=8, input_mode="zerocopy", exec_mode="persistent")
+    log = PartitionLog.from_arrays(X)
+    eng.add_log(0, log)
+    red = CounterReducer(DistContext(0, 1, 0, gpu, "none"), gpu)
+    ep = EpochPipeline(eng, red)
+    total = 0
+    for k in range(12):
+        st = eng.pump(37, batch_rows=2000 if k % 3 else 2048, drain=(k % 4 == 3))
+        total += 37 * (2000 if k % 3 else 2048)
+        ep.tick()
+    eng.pump(0, drain=True)
+    ep.finish()
+    c, _ = red.snapshot()
+    assert c[0] == total
+    assert c[1] + c[2] == total
+    eng.close()
+    log.free()
