@@ -23,6 +23,7 @@ append-only journal").
 """
 from __future__ import annotations
 
+import collections
 import enum
 import heapq
 import itertools
@@ -107,6 +108,10 @@ class ProcessEngine:
         self.keep_completed = keep_completed
         self._completed_order: List[int] = []
         self._journal = open(journal_path, "a", buffering=1) if journal_path else None
+        self.dedupe_window = 1_000_000
+        self._by_tx: Dict[Any, int] = {}
+        self._tx_order = collections.deque()
+        self.duplicates = 0
 
     @classmethod
     def from_config(cls, kie_cfg, **kw) -> "ProcessEngine":
@@ -144,6 +149,10 @@ class ProcessEngine:
             inst = ProcessInstance(**d)
             eng.instances[iid] = inst
             max_id = max(max_id, iid)
+            txid = inst.variables.get("transaction_id")
+            if txid is not None and inst.process_id == cls.FRAUD:
+                eng._by_tx[txid] = iid
+                eng._tx_order.append(txid)
             if "task" in rec:
                 t = UserTask(**rec["task"])
                 eng.tasks[t.id] = t
@@ -173,8 +182,19 @@ class ProcessEngine:
             return iid
 
     def start_fraud(self, variables: Dict[str, Any]) -> int:
+        """Idempotent per transaction id: at-least-once delivery (a re-scored transaction
+        after a rank fail-over) returns the existing instance instead of starting another."""
+        txid = variables.get("transaction_id", variables.get("tx_id"))
         with self._lock:
+            if txid is not None and txid in self._by_tx:
+                self.duplicates += 1
+                return self._by_tx[txid]
             iid = next(self._ids)
+            if txid is not None:
+                self._by_tx[txid] = iid
+                self._tx_order.append(txid)
+                if len(self._tx_order) > self.dedupe_window:
+                    self._by_tx.pop(self._tx_order.popleft(), None)
             now = self.clock()
             inst = ProcessInstance(iid, self.FRAUD, dict(variables), State.WAITING_CUSTOMER, None, now,
                                    timer_due=now + self.timeout, history=["start", "CustomerNotification"])

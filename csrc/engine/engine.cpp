@@ -232,6 +232,8 @@ class Engine {
   int persist_launch() {
     ccfd_persist_dev init{};
     init.work_next = (unsigned long long)pctl->posted * (unsigned long long)persist_C;
+    init.posted = pctl->posted;
+    init.stop = 0;
     for (int i = 0; i < CCFD_PERSIST_MAX_RING; ++i) init.remaining[i] = (unsigned)persist_C;
     HIPCHK(hipMemcpyAsync(pdev, &init, sizeof(init), hipMemcpyHostToDevice, pstream));
     HIPCHK(hipStreamSynchronize(pstream));

@@ -59,11 +59,11 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream);
 // ---------------------------------------------------------------------------
 // Persistent streaming kernel (exec_mode = 1): ONE long-running launch per engine; the
 // host publishes micro-batch descriptors into a ring in coherent pinned memory and bumps
-// `posted`; resident workgroups claim 64-row work items with one device atomic, wait for
+// `posted`; resident workgroups claim 256-row work items with one device atomic, wait for
 // the descriptor to be posted, score, and the last workgroup of a micro-batch publishes
 // its completion record.  No per-batch launch, event or copy on the host.
 #define CCFD_PERSIST_MAX_RING 64
-#define CCFD_PERSIST_ITEM_ROWS 64
+#define CCFD_PERSIST_ITEM_ROWS 256   // 4 waves x 4 tiles x 16 rows
 
 typedef struct ccfd_persist_desc {   // host-coherent pinned, written before `posted`
   const float* x;          // device-visible rows [n][30]
@@ -84,8 +84,12 @@ typedef struct ccfd_persist_ctl {    // host-coherent pinned
 
 typedef struct ccfd_persist_dev {    // device memory
   unsigned long long work_next;                   // next work item to claim
+  unsigned long long posted;                      // device mirror of ctl->posted (doorbell WG)
+  unsigned long long stop;                        // device mirror of ctl->stop
+  unsigned long long _pad;
   unsigned int remaining[CCFD_PERSIST_MAX_RING];  // items left per ring slot
   unsigned int nflag[CCFD_PERSIST_MAX_RING];      // flagged rows per ring slot
+  ccfd_persist_desc desc[CCFD_PERSIST_MAX_RING];  // device mirror of the descriptor ring
 } ccfd_persist_dev;
 
 typedef struct ccfd_persist_args {

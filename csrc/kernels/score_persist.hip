@@ -2,10 +2,13 @@
 //
 // One launch lives as long as the engine.  Every resident workgroup loops:
 //   claim work item i (one agent-scope atomic)      -> micro-batch b = i / C, chunk c = i % C
-//   wait until the host has posted b               (thread 0 polls ctl->posted, system scope,
-//                                                   cached in an SGPR; s_sleep back-off)
-//   read descriptor b % R (x, outputs, n, epoch)   -> LDS
-//   4 waves x 16-row tiles = rows [64c, 64c+64) scored with the same fused math as the
+//   wait until b is posted                          (thread 0 polls the DEVICE mirror kept by
+//                                                   the doorbell workgroup 0, which alone
+//                                                   polls host memory with relaxed system-
+//                                                   scope loads; s_sleep back-off)
+//   read descriptor b % R from the device mirror    -> LDS
+//   4 waves x 4 tiles x 16 rows = rows [256c, 256c+256), next tile prefetched while the
+//   current one computes, scored with the same fused math as the
 //   per-batch kernels (mlp_core.h), outputs written straight to host-mapped memory,
 //   fraud rows appended to the descriptor's compacted flag list
 //   counters + amount histogram -> counters[desc.epoch] (one atomic set per item)
@@ -58,6 +61,43 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   float* tile_lds = sx[wave];
   unsigned long long posted_cache = 0;     // thread 0 only
 
+  // Workgroup 0 is the DOORBELL: its thread 0 alone polls host memory (ctl->posted/stop)
+  // and mirrors new descriptors + the posted count into device memory.  Every other
+  // workgroup polls only the device mirror: hundreds of workgroups polling host memory
+  // would each hold PCIe read requests and starve the feature stream (measured: 2x grid
+  // -> 3x slower before this split).
+  if (blockIdx.x == 0) {
+    if (tid == 0) {
+      unsigned long long mirrored = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned sleep_n = 1;
+      for (;;) {
+        const unsigned long long p = __hip_atomic_load(&a.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (p > mirrored) {
+          for (unsigned long long b = mirrored; b < p; ++b) {
+            const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.desc + (b % (unsigned long long)a.ring));
+            unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
+#pragma unroll
+            for (int w = 0; w < (int)(sizeof(ccfd_persist_desc) / 8); ++w)
+              __hip_atomic_store(dst + w, __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          __hip_atomic_store(&a.dev->posted, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          mirrored = p;
+          sleep_n = 1;
+          continue;
+        }
+        if (__hip_atomic_load(&a.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          __hip_atomic_store(&a.dev->stop, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(&a.ctl->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);   // ~64..1024 cycles
+        sleep_n = sleep_n < 16 ? sleep_n * 2 : 16;
+      }
+    }
+    return;                                              // no barrier is ever used by WG 0
+  }
+
   for (;;) {
     if (tid == 0) {
       const unsigned long long item =
@@ -66,25 +106,22 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       int cmd = 0;
       unsigned sleep_n = 1;
       while (posted_cache <= b) {
-        posted_cache = __hip_atomic_load(&a.ctl->posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if (posted_cache > b) break;
-        if (__hip_atomic_load(&a.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) { cmd = 1; break; }
-        // back-off: ~1 us .. ~16 us between polls of host memory
-        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(32);
-        sleep_n = sleep_n < 16 ? sleep_n * 2 : 16;
+        if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { cmd = 1; break; }
+        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
+        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
       }
       if (!cmd) {
-        const ccfd_persist_desc* d = a.desc + (b % (unsigned long long)a.ring);
-        sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->proba), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->route), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->flag_idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        const unsigned long long ne = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(&d->n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
+        sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(d + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(d + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const unsigned long long ne = __hip_atomic_load(d + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sdesc.n = (int32_t)(ne & 0xffffffffull);
         sdesc.epoch = (int32_t)(ne >> 32);
         sdesc.seq = b;
-      } else {
-        __hip_atomic_fetch_add(&a.ctl->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       s_item = item;
       s_cmd = cmd;
@@ -97,15 +134,23 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     const int slot = (int)(sdesc.seq % (unsigned long long)a.ring);
     const int n = sdesc.n;
     const float* x = sdesc.x;
-    const int tile = chunk * 4 + wave;
-    const int row0 = tile * kTileRows;
-    const int row = row0 + c;
-    const bool valid = row < n;
-
-    if (row0 < n) {                                      // wave-uniform
-      TileRegs r;
-      tile_issue(x + (size_t)row0 * kF, min(kTileRows, n - row0) * kF * 4, lane, r);
-      tile_store(tile_lds, lane, r);
+    constexpr int kTilesPerWave = CCFD_PERSIST_ITEM_ROWS / (4 * kTileRows);
+    const int tile0 = chunk * (4 * kTilesPerWave) + wave;      // wave w: tiles tile0 + 4k
+    auto avail = [&](int t) { return min(kTileRows, n - t * kTileRows) * kF * 4; };
+    TileRegs pre;
+    if (tile0 * kTileRows < n) tile_issue(x + (size_t)tile0 * kTileRows * kF, avail(tile0), lane, pre);
+    unsigned nf_w = 0, nv_w = 0;
+    unsigned long long ps_w = 0;
+#pragma unroll 1
+    for (int k = 0; k < kTilesPerWave; ++k) {
+      const int tile = tile0 + 4 * k;
+      const int row0 = tile * kTileRows;
+      if (row0 >= n) break;                                // wave-uniform
+      const int row = row0 + c;
+      const bool valid = row < n;
+      tile_store(tile_lds, lane, pre);
+      const int nxt = tile + 4;
+      if (k + 1 < kTilesPerWave && nxt * kTileRows < n) tile_issue(x + (size_t)nxt * kTileRows * kF, avail(nxt), lane, pre);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       float xv[8];
@@ -127,14 +172,13 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       if (valid && g == 0) {
         if (sdesc.proba) sdesc.proba[row] = p;
         if (sdesc.route) sdesc.route[row] = fr ? 1 : 0;
+        ps_w += (unsigned long long)(p * 1e6f + 0.5f);
       }
-      unsigned long long ps = (valid && g == 0) ? (unsigned long long)(p * 1e6f + 0.5f) : 0ull;
-      ps = wave_sum_u64(ps);
-      const unsigned nf = __popcll(__ballot(fr && g == 0));
-      const unsigned nv = __popcll(__ballot(valid && g == 0));
+      const unsigned long long m = __ballot(fr && g == 0);
+      nf_w += __popcll(m);
+      nv_w += __popcll(__ballot(valid && g == 0));
       if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
       // compacted flag list (reservation on the slot's device counter)
-      const unsigned long long m = __ballot(fr && g == 0);
       if (m && sdesc.flag_idx) {
         const int leader = __builtin_ffsll((long long)m) - 1;
         unsigned base = 0;
@@ -144,11 +188,12 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
         base = __shfl(base, leader);
         if (fr && g == 0) sdesc.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
       }
-      if (lane == 0) {
-        atomicAdd(&epi.fraud, nf);
-        atomicAdd(&epi.rows, nv);
-        atomicAdd(&epi.psum_e6, ps);
-      }
+    }
+    ps_w = wave_sum_u64(ps_w);
+    if (lane == 0 && nv_w) {
+      atomicAdd(&epi.fraud, nf_w);
+      atomicAdd(&epi.rows, nv_w);
+      atomicAdd(&epi.psum_e6, ps_w);
     }
     // per-item epilogue: counters of this item into the epoch's buffer, reset LDS state
     __syncthreads();
