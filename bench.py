@@ -50,7 +50,7 @@ def parse_args(argv=None):
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
-                    help="auto = persistent kernel for mlp/lr, per-batch launches for gbdt")
+                    help="auto = per-batch launches (see profiles/r1/exec_mode_sweep.txt)")
     ap.add_argument("--persist-grid", type=int, default=0)
     ap.add_argument("--log-rows", type=int, default=1 << 22, help="rows per rank (pinned partition logs)")
     ap.add_argument("--partitions-per-rank", type=int, default=2)
@@ -112,7 +112,10 @@ def main(argv=None):
     dm = DeviceModel.from_blob(args.model, blob, trees, depth_t)
     exec_mode = args.exec_mode
     if exec_mode == "auto":
-        exec_mode = "persistent" if args.model in ("mlp", "lr") and args.input_mode == "zerocopy" else "launch"
+        # measured on MI355X (profiles/r1/exec_mode_sweep.txt): per-batch launches with
+        # kernel-published completion match the persistent kernel's throughput and halve
+        # the unloaded latency, so launch mode is the default.
+        exec_mode = "launch"
 
     # ---- this rank's partitions of topic odh-demo (p % W == rank), pre-filled logs
     n_parts = args.partitions_per_rank * W

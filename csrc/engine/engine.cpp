@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -36,6 +37,7 @@
 #endif
 
 #include "../include/ccfd_abi.h"
+#include "spsc_ring.h"
 
 namespace ccfd {
 void set_error(const std::string& e);
@@ -68,9 +70,7 @@ struct Partition {
   int64_t cursor = 0;
   // ring (streaming) mode: SPSC ring of n rows; producer = ingest thread, consumer = run()
   bool ring = false;
-  std::atomic<int64_t> head{0};      // rows committed by the producer (monotonic)
-  std::atomic<int64_t> released{0};  // rows whose batches have completed (monotonic)
-  int64_t submitted = 0;             // rows handed to the GPU (consumer-private)
+  ccfd::RowRing rr;                  // SPSC row ring (csrc/engine/spsc_ring.h)
   std::mutex arr_mu;
   std::deque<std::pair<int64_t, int64_t>> arrivals;   // (head after commit, t_ns)
 
@@ -196,6 +196,7 @@ class Engine {
   hipStream_t pstream = nullptr;
   bool prunning = false;
   int persist_C = 0;
+  int persist_tpw = 1;
   int64_t completed_upto = 0;              // batches completed in order (seq count)
   std::vector<int64_t> flip_seq;           // seq at each epoch flip
 
@@ -216,7 +217,15 @@ class Engine {
                          hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
     std::memset(p, 0, sizeof(ccfd_persist_desc) * cfg.depth);
     pdesc = static_cast<ccfd_persist_desc*>(p);
-    const int C = (cfg.max_batch + CCFD_PERSIST_ITEM_ROWS - 1) / CCFD_PERSIST_ITEM_ROWS;
+    // work-item size: 64 rows (one 16-row tile per wave) by default; CCFD_PERSIST_ITEM_ROWS
+    // = 128/256 gives each wave 2/4 tiles with a one-tile prefetch (fewer claims per batch)
+    int item_rows = CCFD_PERSIST_ITEM_ROWS;
+    if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) {
+      const int v = std::atoi(e);
+      if (v == 64 || v == 128 || v == 256) item_rows = v;
+    }
+    persist_tpw = item_rows / 64;
+    const int C = (cfg.max_batch + item_rows - 1) / item_rows;
     ccfd_persist_dev init{};
     for (int i = 0; i < CCFD_PERSIST_MAX_RING; ++i) init.remaining[i] = (unsigned)C;
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&pdev), sizeof(ccfd_persist_dev)));
@@ -247,6 +256,7 @@ class Engine {
     a.dev = pdev;
     a.ring = cfg.depth;
     a.items_per_batch = persist_C;
+    a.tiles_per_wave = persist_tpw;
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.blob = cfg.blob;
@@ -422,8 +432,8 @@ class Engine {
     Partition& P = *parts[s.part];
     if (P.ring) {
       // batches of one partition complete in submission order: release in order
-      P.released.store(P.released.load(std::memory_order_relaxed) + s.rows, std::memory_order_release);
-      P.forget_before(P.released.load(std::memory_order_relaxed));
+      P.rr.release_rows(s.rows);
+      P.forget_before(P.rr.released_count());
     }
     s.busy = false;
     s.t_arrival = 0;
@@ -600,7 +610,7 @@ class Engine {
     Partition& P = *parts[p];
     P.ring = true;
     P.feats = feats; P.ids = ids; P.cust = cust; P.n = cap; P.cursor = 0;
-    P.head.store(0); P.released.store(0); P.submitted = 0;
+    P.rr.reset(cap);
     P.feats_dev = feats;
     if (cfg.input_mode == 1) {
       void* d = nullptr;
@@ -613,23 +623,17 @@ class Engine {
   // Producer side: contiguous free rows starting at physical *row (0 if the ring is full).
   int64_t ring_acquire(int p, int64_t want, int64_t* row) {
     if (p < 0 || p >= (int)parts.size() || !parts[p]->ring) return -1;
-    Partition& P = *parts[p];
-    const int64_t h = P.head.load(std::memory_order_relaxed);
-    const int64_t free_rows = P.n - (h - P.released.load(std::memory_order_acquire));
-    const int64_t phys = h % P.n;
-    *row = phys;
-    return std::max<int64_t>(0, std::min({want, free_rows, P.n - phys}));
+    return parts[p]->rr.acquire(want, row);
   }
 
   int ring_commit(int p, int64_t n) {
     if (p < 0 || p >= (int)parts.size() || !parts[p]->ring) return -1;
     Partition& P = *parts[p];
-    const int64_t h = P.head.load(std::memory_order_relaxed) + n;
     {
       std::lock_guard<std::mutex> lk(P.arr_mu);
-      P.arrivals.emplace_back(h, now_ns());
+      P.arrivals.emplace_back(P.rr.head_count() + n, now_ns());
     }
-    P.head.store(h, std::memory_order_release);
+    P.rr.commit(n);                    // publish after the arrival stamp exists
     return 0;
   }
 
@@ -658,15 +662,14 @@ class Engine {
       for (size_t q = 0; q < parts.size(); ++q) {
         Partition& P = *parts[q];
         if (!P.ring) continue;
-        const int64_t h = P.head.load(std::memory_order_acquire);
-        int64_t avail = h - P.submitted;
+        int64_t avail = P.rr.available();
         while (avail > 0) {
           Slot& s = slots[seq % D];
           if (s.busy) break;                               // all slots in flight
-          const int64_t phys = P.submitted % P.n;
+          const int64_t phys = P.rr.take_pos();
           int64_t rows = std::min<int64_t>({avail, (int64_t)cfg.max_batch, P.n - phys});
           const bool full = rows == cfg.max_batch || rows == P.n - phys;
-          const int64_t arr = P.arrival_of(P.submitted);
+          const int64_t arr = P.arrival_of(P.rr.taken());
           if (!full && now - arr < flush_us * 1000) break;  // wait for more rows
           s.part = (int)q; s.start = phys; s.rows = (int32_t)rows;
           const size_t off = (size_t)phys * CCFD_N_FEATURES;
@@ -676,7 +679,7 @@ class Engine {
           s.t_arrival = arr;
           ++seq;
           ++submitted;
-          P.submitted += rows;
+          P.rr.take(rows);
           avail -= rows;
           progress = true;
         }
@@ -744,7 +747,7 @@ int64_t ccfd_engine_cursor(void* eng, int partition) {
   auto* e = static_cast<Engine*>(eng);
   if (partition < 0 || partition >= (int)e->parts.size()) return -1;
   Partition& P = *e->parts[partition];
-  return P.ring ? P.released.load() : P.cursor;
+  return P.ring ? P.rr.released_count() : P.cursor;
 }
 
 int ccfd_engine_set_ring(void* eng, int partition, float* feats, uint64_t* ids, uint32_t* customer,

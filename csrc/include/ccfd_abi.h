@@ -59,11 +59,11 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream);
 // ---------------------------------------------------------------------------
 // Persistent streaming kernel (exec_mode = 1): ONE long-running launch per engine; the
 // host publishes micro-batch descriptors into a ring in coherent pinned memory and bumps
-// `posted`; resident workgroups claim 256-row work items with one device atomic, wait for
+// `posted`; resident workgroups claim 64..256-row work items with one device atomic, wait for
 // the descriptor to be posted, score, and the last workgroup of a micro-batch publishes
 // its completion record.  No per-batch launch, event or copy on the host.
 #define CCFD_PERSIST_MAX_RING 64
-#define CCFD_PERSIST_ITEM_ROWS 256   // 4 waves x 4 tiles x 16 rows
+#define CCFD_PERSIST_ITEM_ROWS 64    // default item: 4 waves x 1 tile x 16 rows
 
 typedef struct ccfd_persist_desc {   // host-coherent pinned, written before `posted`
   const float* x;          // device-visible rows [n][30]
@@ -97,9 +97,10 @@ typedef struct ccfd_persist_args {
   const ccfd_persist_desc* desc;   // device alias of the host descriptor ring
   ccfd_persist_dev* dev;
   int32_t ring;                    // R ring slots (<= CCFD_PERSIST_MAX_RING)
-  int32_t items_per_batch;         // ceil(max_batch / 64)
+  int32_t items_per_batch;         // ceil(max_batch / item_rows)
   int32_t model;                   // MLP or LR
   float threshold;
+  int32_t tiles_per_wave;          // item_rows = 4 waves x tiles_per_wave x 16 rows
   const void* blob;
   unsigned long long* counters[2];
 } ccfd_persist_args;

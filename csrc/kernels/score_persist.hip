@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     const int slot = (int)(sdesc.seq % (unsigned long long)a.ring);
     const int n = sdesc.n;
     const float* x = sdesc.x;
-    constexpr int kTilesPerWave = CCFD_PERSIST_ITEM_ROWS / (4 * kTileRows);
+    const int kTilesPerWave = a.tiles_per_wave;
     const int tile0 = chunk * (4 * kTilesPerWave) + wave;      // wave w: tiles tile0 + 4k
     auto avail = [&](int t) { return min(kTileRows, n - t * kTileRows) * kF * 4; };
     TileRegs pre;
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
 extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* stream) {
   using namespace ccfd;
   if (!a || !a->ctl || !a->desc || !a->dev || !a->blob) return -1;
-  if (a->ring <= 0 || a->ring > CCFD_PERSIST_MAX_RING || a->items_per_batch <= 0) return -2;
+  if (a->ring <= 0 || a->ring > CCFD_PERSIST_MAX_RING || a->items_per_batch <= 0 || a->tiles_per_wave <= 0) return -2;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a->model == CCFD_MODEL_MLP)
     hipLaunchKernelGGL(persist_kernel<CCFD_MODEL_MLP>, dim3(grid), dim3(256), 0, s, *a);

@@ -58,6 +58,21 @@ def test_json_parser_named_columns(L):
     assert cu.tolist() == [i * 3 for i in range(50)]
 
 
+@pytest.mark.parametrize("sanitizer", ["thread", "address,undefined"])
+def test_spsc_ring_stress_under_sanitizers(tmp_path, sanitizer):
+    """The engine's SPSC row ring (csrc/engine/spsc_ring.h) under ThreadSanitizer and
+    ASan/UBSan with randomised producer/consumer timing (SURVEY.md §5 race detection)."""
+    from ccfd_demo_summit_amd.ops.build import CSRC
+    exe = tmp_path / "ring_stress"
+    r = subprocess.run(["g++", "-O1", "-g", "-std=c++17", f"-fsanitize={sanitizer}", "-pthread",
+                        str(CSRC / "tests" / "ring_stress.cpp"), "-o", str(exe)], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip(f"sanitizer build unavailable: {r.stderr[-300:]}")
+    out = subprocess.run([str(exe), "200000", "4093"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "ring stress ok" in out.stdout
+
+
 def test_json_parser_features_array_and_errors(L):
     rc, f, ids, _ = _parse(L, [json.dumps({"features": list(range(30)), "tx_id": "12"})])
     assert rc == 1 and ids[0] == 12
