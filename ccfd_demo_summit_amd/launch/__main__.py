@@ -89,7 +89,20 @@ def cmd_seldon(a, cfg):
     scorer = make_scorer(model, cfg.router.fraud_threshold, device=a.device, max_batch=cfg.seldon.max_batch)
     srv = SeldonServer(scorer, cfg.seldon.model_name, cfg.seldon.token, cfg.seldon.max_batch,
                        cfg.seldon.max_delay_us)
-    print(f"[seldon] {cfg.seldon.model_name} on {getattr(scorer, 'device', 'cpu')} :{a.port or cfg.seldon.port}", flush=True)
+    if a.grpc_port:
+        from ..serving.seldon_grpc import SeldonGrpcServer
+        gsrv = SeldonGrpcServer(scorer, cfg.seldon.model_name, cfg.seldon.token, cfg.seldon.max_batch,
+                                cfg.seldon.max_delay_us, metrics=srv.metrics)
+
+        async def _grpc_up(_app):
+            await gsrv.start(a.host, a.grpc_port)
+
+        async def _grpc_down(_app):
+            await gsrv.stop()
+        srv.app.on_startup.append(_grpc_up)
+        srv.app.on_cleanup.append(_grpc_down)
+    print(f"[seldon] {cfg.seldon.model_name} on {getattr(scorer, 'device', 'cpu')} :{a.port or cfg.seldon.port}"
+          + (f" grpc :{a.grpc_port}" if a.grpc_port else ""), flush=True)
     run(srv, a.host, a.port or cfg.seldon.port)
 
 
@@ -273,6 +286,7 @@ def main(argv=None):
     ap.add_argument("--config", default=None)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--grpc-port", type=int, default=0, help="seldon: also serve seldon.protos gRPC Predict")
     ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--journal", default=None, help="KIE: append-only process journal for recovery")

@@ -7,10 +7,11 @@
 namespace ccfd {
 
 constexpr int kLrBlob = 64 + 3 * 32 * 4;   // models/lr.py BLOB_BYTES
-constexpr int kLrWaves = 4;
 
-template <bool kContig>
-__global__ __launch_bounds__(256) void score_lr_kernel(ccfd_score_args a) {
+// waves per workgroup: see score_mlp.hip (small micro-batches use 1-wave workgroups so the
+// grid covers every CU)
+template <bool kContig, int kLrWaves>
+__global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args a) {
   __shared__ __attribute__((aligned(16))) float sx[kLrWaves][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
   const int tid = threadIdx.x;
@@ -86,15 +87,26 @@ __global__ __launch_bounds__(256) void score_lr_kernel(ccfd_score_args a) {
   signal_done(a);
 }
 
+int mlp_waves_for(int ntiles);   // score_mlp.hip (same policy and CCFD_MLP_WAVES override)
+
+template <int kW>
+static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
+  int grid = (ntiles + kW - 1) / kW;
+  grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
+  if (contig)
+    hipLaunchKernelGGL((score_lr_kernel<true, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  else
+    hipLaunchKernelGGL((score_lr_kernel<false, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+}
+
 int launch_lr(const ccfd_score_args& a, hipStream_t s) {
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
-  int grid = (ntiles + kLrWaves - 1) / kLrWaves;
-  grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
-  if (contig)
-    hipLaunchKernelGGL(score_lr_kernel<true>, dim3(grid), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(score_lr_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+  switch (mlp_waves_for(ntiles)) {
+    case 1: launch_lr_w<1>(a, ntiles, contig, s); break;
+    case 2: launch_lr_w<2>(a, ntiles, contig, s); break;
+    default: launch_lr_w<4>(a, ntiles, contig, s); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

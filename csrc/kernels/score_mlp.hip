@@ -16,14 +16,17 @@
 //  * layer 3 is a 64-term dot product: 16 FMAs per lane + two xor-shuffles.
 //  24 MFMAs (16x16x32) per 16 rows: compute is ~1% of the kernel; it is a latency /
 //  bandwidth kernel, so fusion (one launch, one pass over x) is what matters.
+#include <cstdlib>
+
 #include "mlp_core.h"
 
 namespace ccfd {
 
-constexpr int kWaves = 4;
-
-template <bool kContig>
-__global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
+// Waves per workgroup is a template parameter: a 4096-row micro-batch is only 256 tiles,
+// so 4-wave workgroups would occupy 64 of the 256 CUs and cap the number of outstanding
+// (PCIe zero-copy) reads; small batches launch 1-wave workgroups to spread over every CU.
+template <bool kContig, int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args a) {
   __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
   __shared__ __attribute__((aligned(16))) float sx[kWaves][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
@@ -42,7 +45,7 @@ __global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
   if constexpr (kContig) {
     if (tile < ntiles) tile_issue(a.x + (size_t)tile * kTileRows * kF, tile_avail(tile), lane, pre);
   }
-  mlp_stage(a.blob, sblob, tid, 256);
+  mlp_stage(a.blob, sblob, tid, 64 * kWaves);
   epi_init(epi);
   __syncthreads();
 
@@ -94,18 +97,33 @@ __global__ __launch_bounds__(256) void score_mlp_kernel(ccfd_score_args a) {
   signal_done(a);
 }
 
-template __global__ void score_mlp_kernel<true>(ccfd_score_args);
-template __global__ void score_mlp_kernel<false>(ccfd_score_args);
+template <int kW>
+static void launch_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
+  int grid = (ntiles + kW - 1) / kW;
+  grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
+  if (contig)
+    hipLaunchKernelGGL((score_mlp_kernel<true, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  else
+    hipLaunchKernelGGL((score_mlp_kernel<false, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+}
+
+int mlp_waves_for(int ntiles) {
+  static const int forced = [] {
+    const char* e = std::getenv("CCFD_MLP_WAVES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2 || forced == 4) return forced;
+  return ntiles <= 512 ? 1 : (ntiles <= 1024 ? 2 : 4);   // >= 256 workgroups when possible
+}
 
 int launch_mlp(const ccfd_score_args& a, hipStream_t s) {
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
-  int grid = (ntiles + kWaves - 1) / kWaves;
-  grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
-  if (contig)
-    hipLaunchKernelGGL(score_mlp_kernel<true>, dim3(grid), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(score_mlp_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+  switch (mlp_waves_for(ntiles)) {
+    case 1: launch_w<1>(a, ntiles, contig, s); break;
+    case 2: launch_w<2>(a, ntiles, contig, s); break;
+    default: launch_w<4>(a, ntiles, contig, s); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
