@@ -52,6 +52,10 @@ def parse_args(argv=None):
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
                     help="auto = per-batch launches (see profiles/r1/exec_mode_sweep.txt)")
     ap.add_argument("--persist-grid", type=int, default=0)
+    ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64"],
+                    help="partition-log row format: 30 x f32 (120 B) or W64 (64 B: bf16 V1..V28, "
+                         "f32 Time/Amount; contracts/transaction.py). auto = w64 for mlp/lr "
+                         "(the zero-copy path is PCIe-bound; profiles/r1/wire_sweep.txt), f32 for gbdt")
     ap.add_argument("--log-rows", type=int, default=1 << 22, help="rows per rank (pinned partition logs)")
     ap.add_argument("--partitions-per-rank", type=int, default=2)
     ap.add_argument("--threshold", type=float, default=0.5)
@@ -76,6 +80,8 @@ def baseline_value():
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.wire == "auto":
+        args.wire = "w64" if args.model in ("mlp", "lr") else "f32"
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
@@ -103,13 +109,14 @@ def main(argv=None):
         Xcal, _ = generate(200_000, seed=args.seed + 999)
         model = build_model(args.model, seed=args.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE,
                             threshold=args.threshold, gbdt_trees=args.gbdt_trees, gbdt_depth=args.gbdt_depth)
-        blob = torch.from_numpy(np.frombuffer(model.pack(), np.uint8).copy()).to(dev)
+        packed = model.pack(wire=True) if args.wire == "w64" else model.pack()
+        blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(dev)
     else:
         blob = None
     blob = broadcast_blob(ctx, blob)
     trees = args.gbdt_trees if args.model == "gbdt" else 0
     depth_t = args.gbdt_depth if args.model == "gbdt" else 0
-    dm = DeviceModel.from_blob(args.model, blob, trees, depth_t)
+    dm = DeviceModel.from_blob(args.model, blob, trees, depth_t, wire=args.wire == "w64")
     exec_mode = args.exec_mode
     if exec_mode == "auto":
         # measured on MI355X (profiles/r1/exec_mode_sweep.txt): per-batch launches with
@@ -127,8 +134,13 @@ def main(argv=None):
                        threshold=args.threshold, device=dev.index, exec_mode=exec_mode,
                        persist_grid=args.persist_grid)
     for p in my_parts:
-        log = PartitionLog(rows_per_part)
-        generate(rows_per_part, seed=args.seed * 7919 + p, out=log.feats.array)
+        log = PartitionLog(rows_per_part, wire=args.wire == "w64")
+        if log.wire:
+            Xp, _ = generate(rows_per_part, seed=args.seed * 7919 + p)
+            log.write_rows(0, Xp)           # ingest-side encoding, outside the timed region
+            del Xp
+        else:
+            generate(rows_per_part, seed=args.seed * 7919 + p, out=log.feats.array)
         log.ids.array[:] = np.arange(rows_per_part, dtype=np.uint64) + np.uint64(p) * np.uint64(1 << 40)
         log.customer.array[:] = np.random.default_rng(p).integers(0, 1_000_000, rows_per_part, dtype=np.uint32)
         eng.add_log(p, log)
@@ -209,19 +221,26 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": (round(value / base, 1) if base else None),
         "dtype": "bf16" if args.model == "mlp" else "fp32",
-        "data": ("synthetic creditcard-shaped transactions (30 f32 features) replayed from pinned "
-                 "partition logs; random-init weights, normaliser fitted + output bias calibrated "
-                 "to the 0.172% fraud prior on a synthetic sample"),
+        "data": ("synthetic creditcard-shaped transactions (30 features; log rows "
+                 + ("W64: bf16 V1..V28 + f32 Time/Amount, 64 B" if args.wire == "w64" else "30 x f32, 120 B")
+                 + ") replayed from pinned partition logs; random-init weights, normaliser fitted + "
+                 "output bias calibrated to the 0.172% fraud prior on a synthetic sample"),
         "config": {"model": {"mlp": "mlp_30_128_64_1", "lr": "logreg_30",
                              "gbdt": f"oblivious_gbdt_{args.gbdt_trees}x{args.gbdt_depth}"}[args.model],
                    "global_batch": args.batch * W, "seq_len": 1, "micro_batch": args.batch,
                    "parallelism": f"dp{W}", "input_mode": args.input_mode,
                    "output_mode": args.output_mode, "exec_mode": exec_mode, "depth": args.depth,
+                   "wire": args.wire,
                    "streams": args.streams,
                    "batches_per_step": args.batches_per_step, "numa_node_rank0": numa_node},
         "p50_latency_us": round(p50_us, 2),
         "p99_latency_us": round(p99_us, 2),
         "p50_latency_us_unloaded": None if p50_unloaded is None else round(p50_unloaded, 2),
+        # engine host-thread time per timed micro-batch (cumulative since reset_stats)
+        "host_us_per_batch": {k: round(v * 1e6 / (args.steps * args.batches_per_step), 3) for k, v in
+                              (("submit", st_final.host_submit_s), ("wait", st_final.host_wait_s),
+                               ("complete", st_final.host_complete_s))},
+        "step_us_per_batch": round(elapsed * 1e6 / (args.steps * args.batches_per_step), 3),
         "rows_scored": total_rows,
         "rows_expected": expected,
         "fraud_routed": int(counters[1]) - fraud0,

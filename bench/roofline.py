@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--chunked", action="store_true", help="also probe micro-batch-sized kernels")
     args = ap.parse_args()
     import torch
     from ccfd_demo_summit_amd.engine import PinnedArray
@@ -40,6 +41,21 @@ def main():
     for k in list(out):
         out[k.replace("_GBps", "_tx_ceiling_M_per_s")] = round(out[k] * 1e9 / 120 / 1e6, 1)
         out[k] = round(out[k], 2)
+    if args.chunked:
+        # micro-batch granularity: chunk = rows x 120 B, grid/block like the scoring kernels
+        L.ccfd_bw_probe_chunked.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                            C.c_int, C.c_void_p]
+        L.ccfd_bw_probe_chunked.restype = C.c_double
+        rows_list = [4096, 16384, 65536]
+        out["chunked"] = []
+        for rows in rows_list:
+            chunk = rows * 120
+            for grid, block in ((rows // 64, 256), (rows // 16, 64), (min(2048, rows // 16), 256)):
+                for ns in (1, 4, 8):
+                    gbps = L.ccfd_bw_probe_chunked(C.c_void_p(host.ptr), nbytes, chunk, grid, block, ns, 3,
+                                                   C.c_void_p(dev.data_ptr()))
+                    out["chunked"].append({"rows": rows, "grid": grid, "block": block, "streams": ns,
+                                           "GBps": round(gbps, 2), "tx_M_per_s": round(gbps * 1e9 / 120 / 1e6, 1)})
     print(json.dumps(out))
     host.free()
 

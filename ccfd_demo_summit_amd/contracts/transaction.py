@@ -45,6 +45,53 @@ AMOUNT_COL = N_FEATURES - 1              # 29
 V10_COL = FEATURE_NAMES.index("V10")
 V17_COL = FEATURE_NAMES.index("V17")
 
+# ---------------------------------------------------------------------------------------
+# W64: the engine's packed 64-byte row (partition logs and rings on the zero-copy path).
+# The scoring hot path is bound by host->GPU bytes (PCIe, ~55 GB/s per MI355X), so the log
+# row is sized for it: the 28 PCA components V1..V28 -- zero-centred by construction and fed
+# to bf16 MFMAs anyway -- travel as bf16 (RNE); Time and Amount, whose magnitude needs more
+# than 8 mantissa bits, stay f32.  64 B instead of 120 B per transaction, one float4 per lane
+# (a 16-row tile is one fully coalesced 1 KB wave request).
+#   bytes [0,56)  V1..V28 bf16     [56,60) Time f32     [60,64) Amount f32
+# Wire position p holds canonical feature WIRE_PERM[p]; packed models (pack(wire=True)) are
+# permuted to this order so lane group g of the kernel reads exactly bytes [16g, 16g+16).
+WIRE_ROW_BYTES = 64
+WIRE_PERM = np.array(list(range(1, 29)) + [0, N_FEATURES - 1], np.int64)
+WIRE_AMOUNT_F32 = 15                      # Amount as the 16th f32 word of a W64 row
+
+
+def _bf16_bits(x: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def encode_wire(X: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """float32 [n, 30] canonical rows -> uint8 [n, 64] W64 rows."""
+    X = np.asarray(X, np.float32)
+    n = X.shape[0]
+    if out is None:
+        out = np.empty((n, WIRE_ROW_BYTES), np.uint8)
+    w16 = out.view(np.uint16).reshape(n, 32)
+    w32 = out.view(np.float32).reshape(n, 16)
+    w16[:, :28] = _bf16_bits(X[:, 1:29])
+    w32[:, 14] = X[:, TIME_COL]
+    w32[:, 15] = X[:, AMOUNT_COL]
+    return out
+
+
+def decode_wire(W: np.ndarray) -> np.ndarray:
+    """uint8 [n, 64] W64 rows -> float32 [n, 30] canonical rows (V-columns bf16-exact)."""
+    W = np.ascontiguousarray(W).view(np.uint8).reshape(-1, WIRE_ROW_BYTES)
+    n = W.shape[0]
+    X = np.empty((n, N_FEATURES), np.float32)
+    v = (W.view(np.uint16).reshape(n, 32)[:, :28].astype(np.uint32) << 16).view(np.float32)
+    X[:, 1:29] = v
+    f = W.view(np.float32).reshape(n, 16)
+    X[:, TIME_COL] = f[:, 14]
+    X[:, AMOUNT_COL] = f[:, 15]
+    return X
+
+
 TXB_MAGIC = b"TXB1"
 TXB_HEADER = struct.Struct("<4sHHIIQQ")  # 32 bytes
 assert TXB_HEADER.size == 32

@@ -19,6 +19,7 @@ from ..ops._lib import (FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, EngineConfig,
 from ..ops.kernels import DeviceModel
 
 N_FEATURES = 30
+WIRE_ROW_F32 = 16            # W64 wire row = 64 B = 16 f32 words (contracts.transaction)
 INPUT_MODES = {"dma": 0, "zerocopy": 1}
 OUTPUT_MODES = {"zerocopy": 0, "dma": 1}
 
@@ -51,19 +52,39 @@ class PinnedArray:
             pass
 
 
-class PartitionLog:
-    """One Kafka-partition-like append log of transactions in pinned host memory."""
+def encode_w64(X: np.ndarray, out_ptr: int) -> None:
+    """f32 rows [n, 30] -> W64 wire rows at ``out_ptr`` (native encoder, ingest/encode.cpp)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    if X.ndim != 2 or X.shape[1] != N_FEATURES:
+        raise ValueError("expected [n, 30] float32 rows")
+    if lib().ccfd_encode_w64(X.ctypes.data, X.shape[0], N_FEATURES, C.c_void_p(out_ptr)) != X.shape[0]:
+        raise RuntimeError("ccfd_encode_w64 failed")
 
-    def __init__(self, n_rows: int):
+
+class PartitionLog:
+    """One Kafka-partition-like append log of transactions in pinned host memory.
+
+    ``wire=True`` stores W64 rows (64 B, contracts/transaction.py) instead of 30 x f32."""
+
+    def __init__(self, n_rows: int, wire: bool = False):
         self.n = int(n_rows)
-        self.feats = PinnedArray((self.n, N_FEATURES), np.float32)
+        self.wire = bool(wire)
+        self.row_bytes = 64 if self.wire else 4 * N_FEATURES
+        self.feats = PinnedArray((self.n, WIRE_ROW_F32 if self.wire else N_FEATURES), np.float32)
         self.ids = PinnedArray(self.n, np.uint64)
         self.customer = PinnedArray(self.n, np.uint32)
 
+    def write_rows(self, r: int, X: np.ndarray) -> None:
+        """Store canonical f32 rows X at log rows [r, r + len(X))."""
+        if self.wire:
+            encode_w64(X, self.feats.ptr + r * self.row_bytes)
+        else:
+            self.feats.array[r:r + X.shape[0]] = X
+
     @classmethod
-    def from_arrays(cls, X: np.ndarray, ids=None, customer=None) -> "PartitionLog":
-        log = cls(X.shape[0])
-        log.feats.array[:] = X
+    def from_arrays(cls, X: np.ndarray, ids=None, customer=None, wire: bool = False) -> "PartitionLog":
+        log = cls(X.shape[0], wire=wire)
+        log.write_rows(0, X)
         log.ids.array[:] = np.arange(log.n, dtype=np.uint64) if ids is None else ids
         log.customer.array[:] = 0 if customer is None else customer
         return log
@@ -124,6 +145,8 @@ class StreamEngine:
         cfg.flag_capacity = int(flag_capacity)
         cfg.exec_mode = {"launch": 0, "persistent": 1}[exec_mode]
         cfg.persist_grid = int(persist_grid)
+        self.wire = bool(getattr(dm, "wire", False))
+        cfg.wire = 1 if self.wire else 0
         self.exec_mode = exec_mode
         self.flips = 0
         cfg.counters[0] = self.counters[0].data_ptr()
@@ -149,6 +172,8 @@ class StreamEngine:
             pass
 
     def add_log(self, partition: int, log: PartitionLog, cursor: int = 0) -> None:
+        if log.wire != self.wire:
+            raise ValueError("log row format (wire) does not match the engine's model blob")
         check(lib().ccfd_engine_set_log(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
                                         C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr),
                                         log.n, int(cursor)), "ccfd_engine_set_log")
@@ -166,6 +191,10 @@ class StreamEngine:
         """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
         X = np.ascontiguousarray(X, dtype=np.float32)
         n = X.shape[0]
+        if self.wire:
+            rows = np.empty((n, WIRE_ROW_F32), np.float32)
+            encode_w64(X, rows.ctypes.data)
+            X = rows
         proba = np.empty(n, np.float32)
         route = np.empty(n, np.uint8)
         check(lib().ccfd_engine_score_sync(C.c_void_p(self.h), X.ctypes.data, n, proba.ctypes.data,
@@ -204,7 +233,7 @@ class StreamEngine:
     # ------------------------------------------------------------------ ring (streaming) mode
     def set_ring(self, partition: int, capacity: int) -> PartitionLog:
         """Register partition ``partition`` as a live SPSC ring of ``capacity`` rows."""
-        log = PartitionLog(capacity)
+        log = PartitionLog(capacity, wire=self.wire)
         check(lib().ccfd_engine_set_ring(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
                                          C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr), log.n),
               "ccfd_engine_set_ring")
@@ -230,7 +259,7 @@ class StreamEngine:
                 _t.sleep(50e-6)
                 continue
             r = row.value
-            log.feats.array[r:r + k] = X[done:done + k]
+            log.write_rows(r, X[done:done + k])
             if ids is not None:
                 log.ids.array[r:r + k] = ids[done:done + k]
             if customer is not None:
@@ -257,8 +286,9 @@ class StreamEngine:
             buf = b"".join(chunk)
             off = np.zeros(k + 1, np.int64)
             np.cumsum([len(v) for v in chunk], out=off[1:])
-            got = L.ccfd_parse_json_batch(buf, off.ctypes.data, k, log.feats.ptr + r * 120,
-                                          log.ids.ptr + r * 8, log.customer.ptr + r * 4)
+            parse = L.ccfd_parse_json_batch_w64 if log.wire else L.ccfd_parse_json_batch
+            got = parse(buf, off.ctypes.data, k, log.feats.ptr + r * log.row_bytes,
+                        log.ids.ptr + r * 8, log.customer.ptr + r * 4)
             if got != k:
                 raise ValueError(f"malformed transaction message #{done - got - 1}")
             L.ccfd_engine_ring_commit(C.c_void_p(self.h), int(partition), k)

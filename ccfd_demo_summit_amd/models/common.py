@@ -12,6 +12,7 @@ KPAD = 32            # feature dim padded to one MFMA K-step (16x16x32)
 HEADER_BYTES = 64
 
 FLAG_LOG_AMOUNT = 1  # x[AMOUNT_COL] <- log1p(max(x, 0)) before normalisation
+FLAG_WIRE = 2        # blob feature order is the W64 wire order (contracts.transaction.WIRE_PERM)
 
 
 def bf16_round(x: np.ndarray) -> np.ndarray:
@@ -66,12 +67,15 @@ class Normalizer:
     def flags(self) -> int:
         return FLAG_LOG_AMOUNT if self.log_amount else 0
 
-    def packed(self) -> bytes:
-        """mu[32] then inv_sigma[32] (lane group g reads entries 8g..8g+7)."""
+    def packed(self, wire: bool = False) -> bytes:
+        """mu[32] then inv_sigma[32] (lane group g reads entries 8g..8g+7); ``wire``
+        permutes them to the W64 row order (contracts.transaction.WIRE_PERM)."""
+        from ..contracts.transaction import WIRE_PERM
         mu = np.zeros(KPAD, np.float32)
         isg = np.zeros(KPAD, np.float32)
-        mu[:N_FEATURES] = self.mu
-        isg[:N_FEATURES] = self.inv_sigma
+        perm = WIRE_PERM if wire else np.arange(N_FEATURES)
+        mu[:N_FEATURES] = self.mu[perm]
+        isg[:N_FEATURES] = self.inv_sigma[perm]
         return mu.tobytes() + isg.tobytes()
 
     def state(self) -> dict:

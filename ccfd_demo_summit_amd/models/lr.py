@@ -45,10 +45,14 @@ class LogisticModel:
         z = self.logits(X)
         self.b += float(np.log(threshold / (1 - threshold)) - np.quantile(z, 1.0 - target_rate))
 
-    def pack(self) -> bytes:
+    def pack(self, wire: bool = False) -> bytes:
+        """``wire=True``: weights/normaliser in W64 row order (see models/mlp.py pack)."""
+        from ..contracts.transaction import WIRE_PERM
+        from .common import FLAG_WIRE
         w = np.zeros(KPAD, np.float32)
-        w[:N_FEATURES] = self.w
-        blob = header(b"LR01", self.norm.flags, float(self.b)) + self.norm.packed() + w.tobytes()
+        w[:N_FEATURES] = self.w[WIRE_PERM] if wire else self.w
+        blob = (header(b"LR01", self.norm.flags | (FLAG_WIRE if wire else 0), float(self.b))
+                + self.norm.packed(wire) + w.tobytes())
         assert len(blob) == BLOB_BYTES
         return blob
 

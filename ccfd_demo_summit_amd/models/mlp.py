@@ -36,8 +36,8 @@ from typing import Optional
 
 import numpy as np
 
-from ..contracts.transaction import N_FEATURES
-from .common import (HEADER_BYTES, KPAD, Normalizer, bf16_bits, bf16_round, header, sigmoid)
+from ..contracts.transaction import N_FEATURES, WIRE_PERM, decode_wire, encode_wire
+from .common import (FLAG_WIRE, HEADER_BYTES, KPAD, Normalizer, bf16_bits, bf16_round, header, sigmoid)
 
 H1, H2 = 128, 64
 OFF_NORM = HEADER_BYTES
@@ -110,9 +110,11 @@ class MLPModel:
         self.b3 += float(zt - q)
 
     # ---------------------------------------------------------------- packing
-    def pack(self) -> bytes:
+    def pack(self, wire: bool = False) -> bytes:
+        """``wire=True``: W1 columns and the normaliser in W64 row order, header flag
+        FLAG_WIRE -- the blob for engines whose logs hold W64 rows."""
         W1p = np.zeros((H1, KPAD), np.float32)
-        W1p[:, :N_FEATURES] = self.W1
+        W1p[:, :N_FEATURES] = self.W1[:, WIRE_PERM] if wire else self.W1
         lanes = np.arange(64)
         c, g = lanes & 15, lanes >> 4
         j = np.arange(8)
@@ -127,7 +129,8 @@ class MLPModel:
         b1f = np.stack([self.b1[16 * t + 4 * gi + ri] for t in range(8)])
         b2f = np.stack([self.b2[16 * u + 4 * gi + ri] for u in range(4)])
         w3f = np.stack([self.w3[16 * u + 4 * gi + ri] for u in range(4)])
-        blob = (header(b"MLP1", self.norm.flags, float(self.b3)) + self.norm.packed()
+        blob = (header(b"MLP1", self.norm.flags | (FLAG_WIRE if wire else 0), float(self.b3))
+                + self.norm.packed(wire)
                 + bf16_bits(w1f).tobytes() + bf16_bits(w2f).tobytes()
                 + b1f.astype(np.float32).tobytes() + b2f.astype(np.float32).tobytes()
                 + w3f.astype(np.float32).tobytes())
@@ -170,6 +173,9 @@ def emulate_packed_kernel(blob: bytes, X: np.ndarray) -> np.ndarray:
     w3f = np.frombuffer(b, np.float32, 64, OFF_W3).reshape(4, 4, 4)
 
     X = np.asarray(X, np.float32)
+    if flags & FLAG_WIRE:
+        # the kernel sees W64 rows: bf16 V-columns, permuted to wire order
+        X = decode_wire(encode_wire(X))[:, WIRE_PERM]
     n = X.shape[0]
     out = np.empty(n, np.float32)
     lanes = np.arange(64)

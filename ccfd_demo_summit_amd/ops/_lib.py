@@ -25,7 +25,7 @@ N_COUNTER_SLOTS = 64
 class ScoreArgs(C.Structure):
     _fields_ = [("x", C.c_void_p), ("ld", C.c_int64), ("n", C.c_int32), ("model", C.c_int32),
                 ("blob", C.c_void_p), ("threshold", C.c_float), ("gbdt_trees", C.c_int32),
-                ("gbdt_depth", C.c_int32), ("_pad", C.c_int32), ("proba", C.c_void_p),
+                ("gbdt_depth", C.c_int32), ("flags", C.c_int32), ("proba", C.c_void_p),
                 ("route", C.c_void_p), ("counters", C.c_void_p), ("slot_ctl", C.c_void_p),
                 ("flag_idx", C.c_void_p), ("done_rec", C.c_void_p), ("done_seq", C.c_uint64)]
 
@@ -35,7 +35,7 @@ class EngineConfig(C.Structure):
                 ("gbdt_trees", C.c_int32), ("gbdt_depth", C.c_int32), ("threshold", C.c_float),
                 ("max_batch", C.c_int32), ("depth", C.c_int32), ("n_streams", C.c_int32),
                 ("input_mode", C.c_int32), ("output_mode", C.c_int32), ("flag_capacity", C.c_int32),
-                ("exec_mode", C.c_int32), ("persist_grid", C.c_int32), ("_pad", C.c_int32),
+                ("exec_mode", C.c_int32), ("persist_grid", C.c_int32), ("wire", C.c_int32),
                 ("counters", C.c_void_p * 2)]
 
 
@@ -109,6 +109,11 @@ def lib() -> C.CDLL:
         L.ccfd_parse_json_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                             C.c_void_p]
         L.ccfd_parse_json_batch.restype = C.c_int64
+        L.ccfd_parse_json_batch_w64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                                C.c_void_p]
+        L.ccfd_parse_json_batch_w64.restype = C.c_int64
+        L.ccfd_encode_w64.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+        L.ccfd_encode_w64.restype = C.c_int64
         _lib = L
         return L
 

@@ -20,19 +20,24 @@ N_FEATURES = 30
 class DeviceModel:
     """A packed model resident in HBM (the blob is broadcast once over RCCL in DP runs)."""
 
-    def __init__(self, model, device: torch.device | str | int = "cuda"):
+    def __init__(self, model, device: torch.device | str | int = "cuda", wire: bool = False):
+        """``wire=True``: blob packed for W64 wire rows (MLP / LR; see contracts/transaction.py)."""
         self.kind = model.kind
         if self.kind not in MODEL_IDS:
             raise ValueError(f"no device kernel for model kind {self.kind!r}")
-        blob = np.frombuffer(model.pack(), np.uint8)
+        if wire and self.kind not in ("mlp", "lr"):
+            raise ValueError("W64 wire rows are supported by the MLP and LR kernels")
+        self.wire = bool(wire)
+        blob = np.frombuffer(model.pack(wire=True) if wire else model.pack(), np.uint8)
         self.blob = torch.from_numpy(blob.copy()).to(device)
         self.trees = getattr(model, "n_trees", 0)
         self.depth = getattr(model, "depth", 0)
 
     @classmethod
-    def from_blob(cls, kind: str, blob: torch.Tensor, trees: int = 0, depth: int = 0) -> "DeviceModel":
+    def from_blob(cls, kind: str, blob: torch.Tensor, trees: int = 0, depth: int = 0,
+                  wire: bool = False) -> "DeviceModel":
         self = cls.__new__(cls)
-        self.kind, self.blob, self.trees, self.depth = kind, blob, trees, depth
+        self.kind, self.blob, self.trees, self.depth, self.wire = kind, blob, trees, depth, bool(wire)
         return self
 
     @property
@@ -48,8 +53,13 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
           proba: Optional[torch.Tensor] = None, route: Optional[torch.Tensor] = None,
           counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None
           ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Fused score of x [n,30] (float32, CUDA): returns (proba_1 [n] f32, route [n] u8)."""
-    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES:
+    """Fused score of x [n,30] (float32, CUDA) -- or, for a ``wire`` model, W64 rows
+    ([n,64] uint8 or [n,16] float32 view) -- returns (proba_1 [n] f32, route [n] u8)."""
+    wire = getattr(dm, "wire", False)
+    if wire:
+        if not x.is_cuda or x.dim() != 2 or x.element_size() * x.shape[1] != 64 or not x.is_contiguous():
+            raise ValueError("wire model: x must be contiguous CUDA W64 rows ([n,64] u8 / [n,16] f32)")
+    elif not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES:
         raise ValueError("x must be a CUDA float32 tensor of shape [n, 30]")
     if x.stride(1) != 1:
         x = x.contiguous()
@@ -60,7 +70,8 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
         route = torch.empty(n, dtype=torch.uint8, device=x.device)
     a = ScoreArgs()
     a.x = x.data_ptr()
-    a.ld = x.stride(0)
+    a.ld = 16 if wire else x.stride(0)
+    a.flags = 2 if wire else 0          # CCFD_ARG_WIRE_W64
     a.n = n
     a.model = dm.model_id
     a.blob = dm.blob.data_ptr()

@@ -88,6 +88,9 @@ def _fit(net: nn.Module, Xn: np.ndarray, y: np.ndarray, cfg: TrainConfig, use_bf
 def train_logistic(X: np.ndarray, y: np.ndarray, cfg: TrainConfig = TrainConfig()) -> Tuple[LogisticModel, Dict]:
     norm = Normalizer.fit(X)
     net = nn.Linear(X.shape[1], 1)
+    with torch.no_grad():                 # convex problem: deterministic zero start
+        net.weight.zero_()
+        net.bias.zero_()
     info = _fit(net, norm(X), y, cfg, use_bf16=False)
     w = net.weight.detach().float().cpu().numpy()[0]
     b = float(net.bias.detach().float().cpu().numpy()[0])
@@ -96,6 +99,7 @@ def train_logistic(X: np.ndarray, y: np.ndarray, cfg: TrainConfig = TrainConfig(
 
 def train_mlp(X: np.ndarray, y: np.ndarray, cfg: TrainConfig = TrainConfig()) -> Tuple[MLPModel, Dict]:
     norm = Normalizer.fit(X)
+    torch.manual_seed(cfg.seed)           # reproducible init
     net = nn.Sequential(nn.Linear(X.shape[1], H1), nn.ReLU(), nn.Linear(H1, H2), nn.ReLU(), nn.Linear(H2, 1))
     info = _fit(net, norm(X), y, cfg, use_bf16=cfg.bf16)
     p = [t.detach().float().cpu().numpy() for t in net.parameters()]

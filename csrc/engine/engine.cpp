@@ -146,6 +146,9 @@ class Engine {
       return -1;
     }
     if (cfg.blob == nullptr) { set_error("null model blob"); return -1; }
+    if (cfg.wire && cfg.model == CCFD_MODEL_GBDT) { set_error("W64 wire rows: MLP and LR only"); return -1; }
+    rowf = cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 : CCFD_N_FEATURES;
+    amount_f = cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 - 1 : CCFD_N_FEATURES - 1;
     HIPCHK(hipSetDevice(cfg.device));
     streams.resize(cfg.n_streams);
     flip_ev.resize(cfg.n_streams);
@@ -155,25 +158,30 @@ class Engine {
     }
     slots.resize(cfg.depth);
     const size_t B = (size_t)cfg.max_batch;
+    // zero-copy outputs in fine-grained (coherent) pinned memory: kernels stream them over
+    // PCIe without parking dirty lines in the XCD L2s, which lets every workgroup skip its
+    // system-scope L2 writeback at completion (CCFD_ARG_FENCE_COHERENT).  CCFD_COHERENT_OUT=0
+    // restores non-coherent outputs + per-workgroup release (A/B switch).
+    if (const char* e = std::getenv("CCFD_COHERENT_OUT")) coherent_out = std::atoi(e) != 0;
+    if (const char* e = std::getenv("CCFD_ABLATE")) ablate = std::atoi(e) & 0x70;   // diagnostics only
+    const unsigned out_flags = hipHostMallocMapped | hipHostMallocPortable |
+                               (coherent_out ? hipHostMallocCoherent : 0u);
     for (auto& s : slots) {
       // HBM staging slot: used by input_mode=DMA and always by score_sync (caller memory
       // may be pageable, which the GPU must never dereference directly)
-      HIPCHK(hipMalloc(&s.d_x, B * CCFD_N_FEATURES * sizeof(float)));
+      HIPCHK(hipMalloc(&s.d_x, B * rowf * sizeof(float)));
       if (cfg.output_mode == 1) {
         HIPCHK(hipMalloc(&s.d_proba, B * sizeof(float)));
         HIPCHK(hipMalloc(&s.d_route, B));
       }
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_proba), B * sizeof(float),
-                           hipHostMallocMapped | hipHostMallocPortable));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_route), B,
-                           hipHostMallocMapped | hipHostMallocPortable));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_proba), B * sizeof(float), out_flags));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_route), B, out_flags));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_proba_dev), s.h_proba, 0));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_route_dev), s.h_route, 0));
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       HIPCHK(hipMalloc(reinterpret_cast<void**>(&s.d_ctl), 2 * sizeof(unsigned int)));
       HIPCHK(hipMemsetAsync(s.d_ctl, 0, 2 * sizeof(unsigned int), streams[0]));
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_flag), B * sizeof(unsigned int),
-                           hipHostMallocMapped | hipHostMallocPortable));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_flag), B * sizeof(unsigned int), out_flags));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_flag_dev), s.h_flag, 0));
       void* hd = nullptr;
       HIPCHK(hipHostMalloc(&hd, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
@@ -190,7 +198,11 @@ class Engine {
 
   // ------------------------------------------------------------------ persistent mode
   bool persistent = false;
-  ccfd_persist_ctl* pctl = nullptr;        // host (coherent pinned)
+  bool coherent_out = true;
+  int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, or 16 for W64 wire rows
+  int amount_f = CCFD_N_FEATURES - 1;
+  int ablate = 0;
+  ccfd_persist_ctl* pctl = nullptr;       // host (coherent pinned)
   ccfd_persist_desc* pdesc = nullptr;      // host (coherent pinned)
   ccfd_persist_dev* pdev = nullptr;        // device
   hipStream_t pstream = nullptr;
@@ -257,6 +269,7 @@ class Engine {
     a.ring = cfg.depth;
     a.items_per_batch = persist_C;
     a.tiles_per_wave = persist_tpw;
+    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | (cfg.wire ? CCFD_ARG_WIRE_W64 : 0);
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.blob = cfg.blob;
@@ -380,7 +393,7 @@ class Engine {
     f.tx_id = P.ids ? P.ids[row] : (uint64_t)row;
     f.customer = P.cust ? P.cust[row] : 0u;
     f.proba = s.h_proba[i];
-    f.amount = P.feats[row * CCFD_N_FEATURES + CCFD_N_FEATURES - 1];
+    f.amount = P.feats[row * rowf + amount_f];
     f.partition = (uint32_t)s.part;
     ++ring_tail;
   }
@@ -463,7 +476,7 @@ class Engine {
     const float* xk = x_dev_or_host;
     if (persistent) {
       if (cfg.input_mode == 0 || force_dma) {
-        HIPCHK(hipMemcpy(s.d_x, x_host, (size_t)rows * CCFD_N_FEATURES * sizeof(float), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(s.d_x, x_host, (size_t)rows * rowf * sizeof(float), hipMemcpyHostToDevice));
         xk = s.d_x;
       }
       if (!prunning) { int rc = persist_launch(); if (rc) return rc; }
@@ -472,12 +485,12 @@ class Engine {
       return 0;
     }
     if (cfg.input_mode == 0 || force_dma) {
-      HIPCHK(hipMemcpyAsync(s.d_x, x_host, (size_t)rows * CCFD_N_FEATURES * sizeof(float),
+      HIPCHK(hipMemcpyAsync(s.d_x, x_host, (size_t)rows * rowf * sizeof(float),
                             hipMemcpyHostToDevice, stream));
       xk = s.d_x;
     }
     ccfd_score_args a{};
-    a.x = xk; a.ld = CCFD_N_FEATURES; a.n = rows; a.model = cfg.model; a.blob = cfg.blob;
+    a.x = xk; a.ld = rowf; a.n = rows; a.model = cfg.model; a.blob = cfg.blob;
     a.threshold = cfg.threshold; a.gbdt_trees = cfg.gbdt_trees; a.gbdt_depth = cfg.gbdt_depth;
     a.proba = cfg.output_mode == 1 ? s.d_proba : s.h_proba_dev;
     a.route = cfg.output_mode == 1 ? s.d_route : s.h_route_dev;
@@ -490,7 +503,9 @@ class Engine {
       a.done_rec = s.h_done_dev;
       a.done_seq = s.expect;
       s.done_ptr = s.h_done;
+      a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate;
     }
+    if (cfg.wire) a.flags |= CCFD_ARG_WIRE_W64;
     int rc = ccfd_score_launch(&a, stream);
     if (rc) return rc;
     if (cfg.output_mode == 1) {
@@ -520,7 +535,7 @@ class Engine {
       if (P.cursor + batch_rows > P.n) P.cursor = 0;
       s.part = p; s.start = P.cursor; s.rows = batch_rows;
       P.cursor += batch_rows;
-      const size_t off = (size_t)s.start * CCFD_N_FEATURES;
+      const size_t off = (size_t)s.start * rowf;
       hipStream_t stream = streams[seq % streams.size()];
       int rc = submit(s, P.feats_dev + off, P.feats + off, batch_rows, stream);
       if (rc) return rc;
@@ -567,7 +582,7 @@ class Engine {
       const int rows = std::min<int32_t>(cfg.max_batch, n - off);
       Slot& s = slots[seq % D];
       hipStream_t stream = streams[seq % streams.size()];
-      const float* xh = x + (size_t)off * CCFD_N_FEATURES;
+      const float* xh = x + (size_t)off * rowf;
       rc = submit(s, xh, xh, rows, stream, /*force_dma=*/true);
       if (rc) return rc;
       ++seq;
@@ -672,7 +687,7 @@ class Engine {
           const int64_t arr = P.arrival_of(P.rr.taken());
           if (!full && now - arr < flush_us * 1000) break;  // wait for more rows
           s.part = (int)q; s.start = phys; s.rows = (int32_t)rows;
-          const size_t off = (size_t)phys * CCFD_N_FEATURES;
+          const size_t off = (size_t)phys * rowf;
           hipStream_t stream = streams[seq % streams.size()];
           int rc = submit(s, P.feats_dev + off, P.feats + off, (int)rows, stream);
           if (rc) return rc;

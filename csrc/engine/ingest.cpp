@@ -147,3 +147,40 @@ extern "C" int64_t ccfd_parse_json_batch(const char* buf, const int64_t* offsets
   }
   return n_msgs;
 }
+
+// ---------------------------------------------------------------------------------------
+// W64 wire rows (contracts/transaction.py encode_wire): V1..V28 -> bf16 (round to nearest
+// even), Time and Amount stay f32.  `ld` = f32 stride of the source rows.
+namespace {
+inline uint16_t bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+inline void encode_row_w64(const float* x, uint8_t* out) {
+  uint16_t* h = reinterpret_cast<uint16_t*>(out);
+  for (int k = 0; k < 28; ++k) h[k] = bf16_rne(x[1 + k]);
+  std::memcpy(out + 56, &x[0], 4);
+  std::memcpy(out + 60, &x[CCFD_N_FEATURES - 1], 4);
+}
+}  // namespace
+
+extern "C" int64_t ccfd_encode_w64(const float* x, int64_t n, int64_t ld, uint8_t* out) {
+  if (ld < CCFD_N_FEATURES) return -1;
+  for (int64_t i = 0; i < n; ++i) encode_row_w64(x + i * ld, out + i * CCFD_WIRE_ROW_BYTES);
+  return n;
+}
+
+// JSON messages straight into W64 rows (the ingest path of a wire-format engine ring).
+extern "C" int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* offsets, int64_t n_msgs,
+                                             uint8_t* rows, uint64_t* ids, uint32_t* customer) {
+  float f[CCFD_N_FEATURES];
+  for (int64_t i = 0; i < n_msgs; ++i) {
+    const char* s = buf + offsets[i];
+    const char* e = buf + offsets[i + 1];
+    if (!parse_one(s, e, f, ids + i, customer + i)) return -(i + 1);
+    encode_row_w64(f, rows + i * CCFD_WIRE_ROW_BYTES);
+  }
+  return n_msgs;
+}

@@ -26,6 +26,18 @@ enum ccfd_counter_slot {
 #define CCFD_N_AMOUNT_BUCKETS 14
 #define CCFD_N_FEATURES 30
 
+// ccfd_score_args.flags / ccfd_persist_args.flags: reserved (0).  Completion ordering is
+// fixed: each workgroup releases at system scope, then takes a relaxed ticket.
+#define CCFD_ARG_FENCE_SYS 0
+#define CCFD_ARG_FENCE_COHERENT 1   // outputs live in fine-grained pinned memory (informational)
+#define CCFD_ARG_WIRE_W64 2           // x holds W64 rows (64 B: bf16 V1..V28, f32 Time, f32 Amount)
+#define CCFD_WIRE_ROW_BYTES 64
+// Diagnostic ablations (CCFD_ABLATE env in the engine; never set by bench.py): skip parts
+// of the epilogue to measure what each costs.  Results are incomplete when set.
+#define CCFD_ARG_ABLATE_COUNTERS 16   // no counter/histogram atomics
+#define CCFD_ARG_ABLATE_OUTPUTS 32    // no proba/route stores
+#define CCFD_ARG_ABLATE_FENCE 64      // no per-workgroup system release
+
 typedef struct ccfd_score_args {
   const float* x;        // features, row-major [n][ld] (device or host-mapped pointer)
   int64_t ld;            // row stride in floats (fast path: 30)
@@ -35,7 +47,7 @@ typedef struct ccfd_score_args {
   float threshold;       // FRAUD_THRESHOLD
   int32_t gbdt_trees;    // GBDT only
   int32_t gbdt_depth;    // GBDT only
-  int32_t _pad;
+  int32_t flags;         // CCFD_ARG_* (informational)
   float* proba;          // out [n] proba_1 (device or host-mapped), may be NULL
   uint8_t* route;        // out [n] 1 = fraud route, may be NULL
   unsigned long long* counters;  // device [CCFD_CNT_SLOTS] accumulated atomically, may be NULL
@@ -101,6 +113,7 @@ typedef struct ccfd_persist_args {
   int32_t model;                   // MLP or LR
   float threshold;
   int32_t tiles_per_wave;          // item_rows = 4 waves x tiles_per_wave x 16 rows
+  int32_t flags;                   // CCFD_ARG_* (informational)
   const void* blob;
   unsigned long long* counters[2];
 } ccfd_persist_args;
@@ -129,7 +142,7 @@ typedef struct ccfd_engine_config {
   int32_t flag_capacity;       // flagged-transaction ring capacity (records)
   int32_t exec_mode;           // 0 = one fused launch per micro-batch, 1 = persistent kernel
   int32_t persist_grid;        // workgroups of the persistent kernel (0 = 256)
-  int32_t _pad;
+  int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B, CCFD_WIRE_ROW_BYTES)
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
 } ccfd_engine_config;
 
@@ -200,6 +213,11 @@ void ccfd_engine_reset_stats(void* eng);
 // feats[n][30], ids[n], customer[n].  Returns number parsed or -(index+1) on error.
 int64_t ccfd_parse_json_batch(const char* buf, const int64_t* offsets, int64_t n_msgs,
                               float* feats, uint64_t* ids, uint32_t* customer);
+// Same, straight into W64 wire rows (64 B each).
+int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* offsets, int64_t n_msgs,
+                                  uint8_t* rows, uint64_t* ids, uint32_t* customer);
+// f32 rows (stride ld >= 30) -> W64 wire rows; returns n or -1.
+int64_t ccfd_encode_w64(const float* x, int64_t n, int64_t ld, uint8_t* out);
 
 #ifdef __cplusplus
 }

@@ -52,7 +52,7 @@ __device__ __forceinline__ void epi_flush(EpilogueLds& s, unsigned long long* cn
     const unsigned h = s.hist[t];
     if (h) atomicAdd(&cnt[(t < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + t],
                      (unsigned long long)h);
-  } else if (t == 64) {
+  } else if (t == 2 * kNB) {        // lane 28: valid for 1-wave workgroups too
     atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)s.rows);
     atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)s.fraud);
     atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(s.rows - s.fraud));
@@ -86,9 +86,16 @@ __device__ __forceinline__ void signal_done(const ccfd_score_args& a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned ticket = __hip_atomic_fetch_add(&a.slot_ctl[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // system-scope release: this workgroup's host-visible stores (proba/route/flag list)
+    // are complete at system scope before its ticket -- required across XCDs even for
+    // fine-grained outputs (an s_waitcnt alone only means "accepted by this XCD's L2").
+    // The ticket itself is relaxed: no agent-scope acquire, i.e. no L2 invalidate per
+    // workgroup (the last workgroup reads only atomics).
+    if (!(a.flags & CCFD_ARG_ABLATE_FENCE)) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned ticket = __hip_atomic_fetch_add(&a.slot_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ticket == gridDim.x - 1) {
       const unsigned nflag = __hip_atomic_load(&a.slot_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.slot_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -136,6 +143,30 @@ __device__ __forceinline__ void tile_store(float* lds_tile, int lane, const Tile
   float4* dst = reinterpret_cast<float4*>(lds_tile);
   dst[lane] = r.v[0];
   if (lane + 64 < kTileBytes / 16) dst[lane + 64] = r.v[1];
+}
+
+// W64 wire rows (contracts/transaction.py WIRE_ROW_BYTES): 16 B per lane -- lane (g, c)
+// owns bytes [16g, 16g+16) of row c of the tile, which in wire order are exactly its 8
+// features (g < 3: eight bf16 V-components; g == 3: V25..V28 bf16, Time f32, Amount f32).
+// A 16-row tile is one contiguous 1 KB wave request; no LDS staging is needed.
+struct WireRegs { uint4 v; };
+
+__device__ __forceinline__ void wire_issue(const unsigned char* __restrict__ x, int n, int tile, int c, int g,
+                                           WireRegs& r) {
+  const int row = tile * kTileRows + c;
+  r.v = row < n ? *reinterpret_cast<const uint4*>(x + (size_t)row * CCFD_WIRE_ROW_BYTES + 16 * g)
+                : make_uint4(0u, 0u, 0u, 0u);
+}
+
+__device__ __forceinline__ void wire_features(const WireRegs& r, int g, float xv[8]) {
+  const unsigned w0 = r.v.x, w1 = r.v.y, w2 = r.v.z, w3 = r.v.w;
+  xv[0] = __uint_as_float(w0 << 16); xv[1] = __uint_as_float(w0 & 0xffff0000u);
+  xv[2] = __uint_as_float(w1 << 16); xv[3] = __uint_as_float(w1 & 0xffff0000u);
+  const bool tail = g == 3;
+  xv[4] = tail ? __uint_as_float(w2) : __uint_as_float(w2 << 16);
+  xv[5] = tail ? __uint_as_float(w3) : __uint_as_float(w2 & 0xffff0000u);
+  xv[6] = tail ? 0.f : __uint_as_float(w3 << 16);
+  xv[7] = tail ? 0.f : __uint_as_float(w3 & 0xffff0000u);
 }
 
 __device__ __forceinline__ void load_tile_contig(const float* __restrict__ xt, int avail,

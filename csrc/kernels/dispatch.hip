@@ -23,7 +23,10 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
   if (a == nullptr || a->blob == nullptr || a->x == nullptr) { set_error("null argument"); return -1; }
   if (a->n < 0) { set_error("n < 0"); return -1; }
   if (a->n == 0) return 0;
-  if (a->ld < kF || (a->ld & 1) || (reinterpret_cast<uintptr_t>(a->x) & 7)) {
+  if (a->flags & CCFD_ARG_WIRE_W64) {
+    if (a->model == CCFD_MODEL_GBDT) { set_error("W64 wire rows: MLP and LR kernels only"); return -3; }
+    if (reinterpret_cast<uintptr_t>(a->x) & 15) { set_error("W64 rows must be 16-byte aligned"); return -3; }
+  } else if (a->ld < kF || (a->ld & 1) || (reinterpret_cast<uintptr_t>(a->x) & 7)) {
     set_error("x must be 8-byte aligned with an even row stride >= 30");
     return -3;
   }

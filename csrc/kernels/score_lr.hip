@@ -10,8 +10,11 @@ constexpr int kLrBlob = 64 + 3 * 32 * 4;   // models/lr.py BLOB_BYTES
 
 // waves per workgroup: see score_mlp.hip (small micro-batches use 1-wave workgroups so the
 // grid covers every CU)
-template <bool kContig, int kLrWaves>
+// kMode as in score_mlp.hip: 0 strided f32, 1 contiguous f32, 2 W64 wire rows
+template <int kMode, int kLrWaves>
 __global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args a) {
+  constexpr bool kContig = kMode == 1;
+  constexpr bool kWire = kMode == 2;
   __shared__ __attribute__((aligned(16))) float sx[kLrWaves][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
   const int tid = threadIdx.x;
@@ -50,6 +53,10 @@ __global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args
         const float2 v = (g < 3 || j < 3) ? r2[j] : make_float2(0.f, 0.f);
         xv[2 * j] = v.x; xv[2 * j + 1] = v.y;
       }
+    } else if constexpr (kWire) {
+      WireRegs r;
+      wire_issue(reinterpret_cast<const unsigned char*>(a.x), a.n, tile, c, g, r);
+      wire_features(r, g, xv);
     } else {
       const float* xr = a.x + (size_t)row * a.ld + 8 * g;
 #pragma unroll
@@ -93,10 +100,12 @@ template <int kW>
 static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   int grid = (ntiles + kW - 1) / kW;
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-  if (contig)
-    hipLaunchKernelGGL((score_lr_kernel<true, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  if (a.flags & CCFD_ARG_WIRE_W64)
+    hipLaunchKernelGGL((score_lr_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  else if (contig)
+    hipLaunchKernelGGL((score_lr_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
   else
-    hipLaunchKernelGGL((score_lr_kernel<false, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    hipLaunchKernelGGL((score_lr_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
 }
 
 int launch_lr(const ccfd_score_args& a, hipStream_t s) {

@@ -22,13 +22,18 @@
 
 namespace ccfd {
 
-// Waves per workgroup is a template parameter: a 4096-row micro-batch is only 256 tiles,
-// so 4-wave workgroups would occupy 64 of the 256 CUs and cap the number of outstanding
-// (PCIe zero-copy) reads; small batches launch 1-wave workgroups to spread over every CU.
-template <bool kContig, int kWaves>
+// Waves per workgroup is a template parameter (CCFD_MLP_WAVES=1/2/4): a 4096-row
+// micro-batch is 256 tiles, so 4-wave workgroups occupy 64 CUs per launch; several launches
+// run concurrently on separate streams.  Smaller workgroups spread one launch wider but pay
+// the weight staging and completion ticket more often (profiles/r1/waves_sweep.txt).
+// kMode: 0 = strided f32 rows, 1 = contiguous f32 rows [n][30] (LDS-staged tiles),
+//        2 = W64 wire rows (one 16-B register load per lane, no LDS tile).
+template <int kMode, int kWaves>
 __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args a) {
+  constexpr bool kContig = kMode == 1;
+  constexpr bool kWire = kMode == 2;
   __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
-  __shared__ __attribute__((aligned(16))) float sx[kWaves][kTileRows * kF + 4];
+  __shared__ __attribute__((aligned(16))) float sx[kWire ? 1 : kWaves][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
 
   const int tid = threadIdx.x;
@@ -41,9 +46,14 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
   // Issue this wave's first input tile BEFORE staging the weights: the (possibly PCIe)
   // fetch latency of x overlaps the L2 fetch of the model blob.
   TileRegs pre;
+  WireRegs wpre;
+  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x);
   auto tile_avail = [&](int t) { return min(kTileRows, a.n - t * kTileRows) * kF * 4; };
   if constexpr (kContig) {
     if (tile < ntiles) tile_issue(a.x + (size_t)tile * kTileRows * kF, tile_avail(tile), lane, pre);
+  }
+  if constexpr (kWire) {
+    if (tile < ntiles) wire_issue(xw, a.n, tile, c, g, wpre);
   }
   mlp_stage(a.blob, sblob, tid, 64 * kWaves);
   epi_init(epi);
@@ -53,7 +63,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
   const float thr = a.threshold;
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
-  float* tile_lds = sx[wave];
+  float* tile_lds = sx[kWire ? 0 : wave];
 
   for (; tile < ntiles; tile += tstride) {
     const int row = tile * kTileRows + c;
@@ -68,6 +78,11 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       tile_features(tile_lds, c, g, xv);
+    } else if constexpr (kWire) {
+      const WireRegs cur = wpre;
+      const int nxt = tile + tstride;
+      if (nxt < ntiles) wire_issue(xw, a.n, nxt, c, g, wpre);
+      wire_features(cur, g, xv);
     } else {
       const float* xr = a.x + (size_t)row * a.ld + 8 * g;
 #pragma unroll
@@ -78,8 +93,10 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
     const bool fr = valid && (p >= thr);
 
     if (valid && g == 0) {
-      if (a.proba) a.proba[row] = p;
-      if (a.route) a.route[row] = fr ? 1 : 0;
+      if (!(a.flags & CCFD_ARG_ABLATE_OUTPUTS)) {
+        if (a.proba) a.proba[row] = p;
+        if (a.route) a.route[row] = fr ? 1 : 0;
+      }
       psum += (unsigned long long)(p * 1e6f + 0.5f);
     }
     fraud += __popcll(__ballot(fr && g == 0));
@@ -93,7 +110,7 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
     atomicAdd(&epi.rows, rows);
     atomicAdd(&epi.psum_e6, psum);
   }
-  epi_flush(epi, a.counters);
+  epi_flush(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
   signal_done(a);
 }
 
@@ -101,10 +118,12 @@ template <int kW>
 static void launch_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   int grid = (ntiles + kW - 1) / kW;
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-  if (contig)
-    hipLaunchKernelGGL((score_mlp_kernel<true, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  if (a.flags & CCFD_ARG_WIRE_W64)
+    hipLaunchKernelGGL((score_mlp_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  else if (contig)
+    hipLaunchKernelGGL((score_mlp_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
   else
-    hipLaunchKernelGGL((score_mlp_kernel<false, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    hipLaunchKernelGGL((score_mlp_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
 }
 
 int mlp_waves_for(int ntiles) {
@@ -113,7 +132,8 @@ int mlp_waves_for(int ntiles) {
     return e ? std::atoi(e) : 0;
   }();
   if (forced == 1 || forced == 2 || forced == 4) return forced;
-  return ntiles <= 512 ? 1 : (ntiles <= 1024 ? 2 : 4);   // >= 256 workgroups when possible
+  (void)ntiles;
+  return 4;   // measured: 1-wave workgroups lose (per-workgroup weight staging + completion)
 }
 
 int launch_mlp(const ccfd_score_args& a, hipStream_t s) {

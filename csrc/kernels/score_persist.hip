@@ -106,13 +106,17 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       int cmd = 0;
       unsigned sleep_n = 1;
       while (posted_cache <= b) {
-        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        // relaxed poll; the acquire fence below runs once the item's batch is posted
+        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (posted_cache > b) break;
         if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { cmd = 1; break; }
         for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
         sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
       }
       if (!cmd) {
+        // one acquire per claimed item (not per poll): invalidates this XCD's L2 copies of
+        // non-coherent inputs (a reused ring slot / DMA staging buffer) before they are read
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
         sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -138,7 +142,13 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     const int tile0 = chunk * (4 * kTilesPerWave) + wave;      // wave w: tiles tile0 + 4k
     auto avail = [&](int t) { return min(kTileRows, n - t * kTileRows) * kF * 4; };
     TileRegs pre;
-    if (tile0 * kTileRows < n) tile_issue(x + (size_t)tile0 * kTileRows * kF, avail(tile0), lane, pre);
+    WireRegs wpre;
+    const bool wire = (a.flags & CCFD_ARG_WIRE_W64) != 0;       // uniform per launch
+    const unsigned char* xw = reinterpret_cast<const unsigned char*>(x);
+    if (tile0 * kTileRows < n) {
+      if (wire) wire_issue(xw, n, tile0, c, g, wpre);
+      else tile_issue(x + (size_t)tile0 * kTileRows * kF, avail(tile0), lane, pre);
+    }
     unsigned nf_w = 0, nv_w = 0;
     unsigned long long ps_w = 0;
 #pragma unroll 1
@@ -148,13 +158,19 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       if (row0 >= n) break;                                // wave-uniform
       const int row = row0 + c;
       const bool valid = row < n;
-      tile_store(tile_lds, lane, pre);
       const int nxt = tile + 4;
-      if (k + 1 < kTilesPerWave && nxt * kTileRows < n) tile_issue(x + (size_t)nxt * kTileRows * kF, avail(nxt), lane, pre);
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       float xv[8];
-      tile_features(tile_lds, c, g, xv);
+      if (wire) {
+        const WireRegs cur = wpre;
+        if (k + 1 < kTilesPerWave && nxt * kTileRows < n) wire_issue(xw, n, nxt, c, g, wpre);
+        wire_features(cur, g, xv);
+      } else {
+        tile_store(tile_lds, lane, pre);
+        if (k + 1 < kTilesPerWave && nxt * kTileRows < n) tile_issue(x + (size_t)nxt * kTileRows * kF, avail(nxt), lane, pre);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        tile_features(tile_lds, c, g, xv);
+      }
       float p, amount;
       if (kModel == CCFD_MODEL_MLP) {
         p = mlp_tile(sblob, L, xv, g, lane, amount);
@@ -216,10 +232,11 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+      // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned left = __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_ACQ_REL,
-                                                   __HIP_MEMORY_SCOPE_AGENT) - 1u;
+      const unsigned left =
+          __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
       if (left == 0) {
         const unsigned nflag = __hip_atomic_load(&a.dev->nflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.dev->nflag[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -19,19 +19,27 @@ def setup(gpu):
 
 @pytest.mark.parametrize("input_mode,output_mode,exec_mode", [
     ("dma", "zerocopy", "launch"), ("zerocopy", "zerocopy", "launch"), ("dma", "dma", "launch"),
-    ("zerocopy", "dma", "launch"), ("zerocopy", "zerocopy", "persistent"), ("dma", "zerocopy", "persistent")])
+    ("zerocopy", "dma", "launch"), ("zerocopy", "zerocopy", "persistent"), ("dma", "zerocopy", "persistent"),
+    ("zerocopy", "zerocopy", "launch-wire"), ("dma", "zerocopy", "launch-wire"),
+    ("zerocopy", "zerocopy", "persistent-wire")])
 def test_engine_pump_matches_oracle(gpu, setup, input_mode, output_mode, exec_mode):
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
-    dm = DeviceModel(m, gpu)
+    wire = exec_mode.endswith("-wire")
+    exec_mode = exec_mode.replace("-wire", "")
+    dm = DeviceModel(m, gpu, wire=wire)
     eng = StreamEngine(dm, batch=4096, depth=4, streams=2, input_mode=input_mode,
                        output_mode=output_mode, exec_mode=exec_mode)
-    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000)
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000, wire=wire)
     eng.add_log(0, log)
     st = eng.pump(6)
     assert st.batches == 6 and st.rows == 6 * 4096
-    ref = m.predict_proba(X[:6 * 4096], emulate_bf16=True)
+    if wire:
+        from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
+        ref = m.predict_proba(decode_wire(encode_wire(X[:6 * 4096])), emulate_bf16=True)
+    else:
+        ref = m.predict_proba(X[:6 * 4096], emulate_bf16=True)
     flagged = eng.drain_flagged()
     got = np.zeros(6 * 4096, bool)
     got[(flagged["tx_id"] - 1000).astype(np.int64)] = True
@@ -61,7 +69,7 @@ def test_engine_score_sync_pageable_input(gpu, setup):
     eng.close()
 
 
-@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent", "launch-wire"])
 def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     """Live ingest: producer writes into the pinned SPSC ring (rows + JSON), run() scores full
     micro-batches and deadline-flushes the partial tail; ring space is recycled."""
@@ -71,8 +79,9 @@ def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     from ccfd_demo_summit_amd.engine import StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
-    eng = StreamEngine(DeviceModel(m, gpu), batch=1024, depth=4, streams=2, input_mode="zerocopy",
-                       exec_mode=exec_mode)
+    wire = exec_mode.endswith("-wire")
+    eng = StreamEngine(DeviceModel(m, gpu, wire=wire), batch=1024, depth=4, streams=2, input_mode="zerocopy",
+                       exec_mode=exec_mode.replace("-wire", ""))
     eng.set_ring(0, 4096)
     n = 10_000                                   # > capacity: exercises wrap + backpressure
     ids = np.arange(n, dtype=np.uint64) + 7
@@ -86,7 +95,11 @@ def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
         scored += st.rows
     assert scored == n
     flagged = eng.drain_flagged()
-    ref = m.predict_proba(X[:n], emulate_bf16=True)
+    if wire:
+        from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
+        ref = m.predict_proba(decode_wire(encode_wire(X[:n])), emulate_bf16=True)
+    else:
+        ref = m.predict_proba(X[:n], emulate_bf16=True)
     got = np.zeros(n, bool)
     got[(flagged["tx_id"] - 7).astype(np.int64)] = True
     clear = np.abs(ref - 0.5) > 2e-3

@@ -105,3 +105,28 @@ def test_strided_input_path(gpu, data):
         torch.cuda.synchronize()
         tol = 1e-2 if kind == "mlp" else 1e-5
         assert np.abs(p.cpu().numpy() - m.predict_proba(X)).max() < tol, kind
+
+
+@pytest.mark.parametrize("kind", ["mlp", "lr"])
+@pytest.mark.parametrize("n", [1, 31, 4097, 65536])
+def test_wire_w64_kernel_matches_reference(gpu, data, kind, n):
+    """W64 wire rows (bf16 V-columns): the kernel equals the bf16 oracle evaluated on the
+    decoded rows and stays within 1e-2 of the fp32 model on the original rows."""
+    from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X = data[0][:n]
+    m = build_model(kind, seed=1, X_ref=data[0][:20000], calibrate_rate=0.01)
+    dm = DeviceModel(m, gpu, wire=True)
+    cnt = new_counters(gpu)
+    xw = torch.from_numpy(encode_wire(X)).to(gpu)
+    p, r = score(dm, xw, 0.5, counters=cnt)
+    torch.cuda.synchronize(gpu)
+    p, r = p.cpu().numpy(), r.cpu().numpy()
+    Xd = decode_wire(encode_wire(X))
+    assert np.abs(p - m.predict_proba(X)).max() < 1e-2
+    if kind == "mlp":
+        assert np.abs(p - m.predict_proba(Xd, emulate_bf16=True)).max() < 2e-3
+    else:
+        assert np.abs(p - m.predict_proba(Xd)).max() < 1e-5
+    np.testing.assert_array_equal(r, (p >= 0.5).astype(np.uint8))
+    _check_counters(cnt, p, r, X)

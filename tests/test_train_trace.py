@@ -21,7 +21,7 @@ def data():
 
 def test_train_logistic(data):
     X, y, Xv, yv = data
-    m, info = train_logistic(X, y, TrainConfig(epochs=2, device="cpu"))
+    m, info = train_logistic(X, y, TrainConfig(epochs=3, lr=3e-2, device="cpu"))
     assert evaluate(m, Xv, yv)["roc_auc"] > 0.9
     assert len(m.pack()) == 448
 

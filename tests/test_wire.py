@@ -1,0 +1,73 @@
+"""W64 wire rows (64 B: bf16 V1..V28, f32 Time/Amount): NumPy and native encoders agree
+bit-for-bit, JSON parses straight into W64, and the wire-order packed blob reproduces the
+bf16 oracle through the lane-exact kernel emulator."""
+import ctypes as C
+import json
+
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.contracts import FEATURE_NAMES, WIRE_PERM, decode_wire, encode_wire
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.models import build_model
+from ccfd_demo_summit_amd.models.mlp import emulate_packed_kernel
+
+
+@pytest.fixture(scope="module")
+def L():
+    from ccfd_demo_summit_amd.ops._lib import lib
+    return lib()
+
+
+def test_layout_and_roundtrip():
+    X, _ = generate(500, seed=9)
+    W = encode_wire(X)
+    assert W.shape == (500, 64) and W.dtype == np.uint8
+    Y = decode_wire(W)
+    np.testing.assert_array_equal(Y[:, [0, 29]], X[:, [0, 29]])          # Time / Amount exact
+    rel = np.abs(Y[:, 1:29] - X[:, 1:29]) / np.maximum(np.abs(X[:, 1:29]), 1e-30)
+    assert rel.max() <= 2 ** -8                                           # bf16 RNE
+    assert sorted(WIRE_PERM.tolist()) == list(range(30))
+    assert FEATURE_NAMES[WIRE_PERM[28]] == "Time" and FEATURE_NAMES[WIRE_PERM[29]] == "Amount"
+
+
+def test_native_encoder_bit_exact(L):
+    X, _ = generate(1000, seed=2)
+    X[0, 3] = np.float32(1.0 + 2 ** -8)          # exact tie -> round to even
+    X[1, 4] = -0.0
+    out = np.zeros((1000, 64), np.uint8)
+    assert L.ccfd_encode_w64(X.ctypes.data, 1000, 30, out.ctypes.data) == 1000
+    np.testing.assert_array_equal(out, encode_wire(X))
+
+
+def test_native_json_to_w64(L):
+    X, _ = generate(40, seed=5)
+    msgs = []
+    for i in range(40):
+        d = {"id": i + 7, "customer_id": i}
+        d.update({n: float(v) for n, v in zip(FEATURE_NAMES, X[i])})
+        msgs.append(json.dumps(d).encode())
+    buf = b"".join(msgs)
+    off = np.cumsum([0] + [len(m) for m in msgs]).astype(np.int64)
+    rows = np.zeros((40, 64), np.uint8)
+    ids = np.zeros(40, np.uint64)
+    cu = np.zeros(40, np.uint32)
+    assert L.ccfd_parse_json_batch_w64(buf, off.ctypes.data, 40, rows.ctypes.data, ids.ctypes.data,
+                                       cu.ctypes.data) == 40
+    # JSON floats round-trip through float64 text -> f32 first, exactly like encode_wire(X)
+    np.testing.assert_array_equal(rows, encode_wire(X))
+    assert ids.tolist() == list(range(7, 47))
+
+
+@pytest.mark.parametrize("kind", ["mlp", "lr"])
+def test_wire_blob_matches_oracle(kind):
+    X, _ = generate(3000, seed=11)
+    m = build_model(kind, seed=3, X_ref=X)
+    Xw = decode_wire(encode_wire(X[:48]))
+    if kind == "mlp":
+        got = emulate_packed_kernel(m.pack(wire=True), X[:48])
+        np.testing.assert_allclose(got, m.predict_proba(Xw, emulate_bf16=True), atol=2e-6)
+        # and the wire numerics stay within bf16 noise of the f32 model
+        assert np.abs(got - m.predict_proba(X[:48])).max() < 5e-3
+    blob = np.frombuffer(m.pack(wire=True), np.uint8)
+    assert int(np.frombuffer(blob[4:8].tobytes(), np.uint32)[0]) & 2
