@@ -45,13 +45,15 @@ def parse_args(argv=None):
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
     ap.add_argument("--batch", type=int, default=4096, help="micro-batch rows")
     ap.add_argument("--batches-per-step", type=int, default=256)
-    ap.add_argument("--depth", type=int, default=8, help="micro-batches in flight per GPU")
+    ap.add_argument("--depth", type=int, default=32, help="micro-batches in flight per GPU")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
                     help="auto = per-batch launches (see profiles/r1/exec_mode_sweep.txt)")
     ap.add_argument("--persist-grid", type=int, default=0)
+    ap.add_argument("--coalesce", type=int, default=8,
+                    help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64"],
                     help="partition-log row format: 30 x f32 (120 B) or W64 (64 B: bf16 V1..V28, "
                          "f32 Time/Amount; contracts/transaction.py). auto = w64 for mlp/lr "
@@ -132,7 +134,7 @@ def main(argv=None):
     eng = StreamEngine(dm, batch=args.batch, depth=args.depth, streams=args.streams,
                        input_mode=args.input_mode, output_mode=args.output_mode,
                        threshold=args.threshold, device=dev.index, exec_mode=exec_mode,
-                       persist_grid=args.persist_grid)
+                       persist_grid=args.persist_grid, coalesce=args.coalesce)
     for p in my_parts:
         log = PartitionLog(rows_per_part, wire=args.wire == "w64")
         if log.wire:
@@ -230,7 +232,7 @@ def main(argv=None):
                    "global_batch": args.batch * W, "seq_len": 1, "micro_batch": args.batch,
                    "parallelism": f"dp{W}", "input_mode": args.input_mode,
                    "output_mode": args.output_mode, "exec_mode": exec_mode, "depth": args.depth,
-                   "wire": args.wire,
+                   "wire": args.wire, "coalesce": args.coalesce,
                    "streams": args.streams,
                    "batches_per_step": args.batches_per_step, "numa_node_rank0": numa_node},
         "p50_latency_us": round(p50_us, 2),

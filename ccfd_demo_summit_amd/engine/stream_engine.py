@@ -122,9 +122,11 @@ class StreamEngine:
     def __init__(self, dm: DeviceModel, batch: int = 4096, depth: int = 8, streams: int = 2,
                  input_mode: str = "dma", output_mode: str = "zerocopy", threshold: float = 0.5,
                  device: Optional[int] = None, flag_capacity: int = 1 << 20, exec_mode: str = "launch",
-                 persist_grid: int = 0):
+                 persist_grid: int = 0, coalesce: int = 1):
         """exec_mode: "launch" = one fused kernel launch per micro-batch; "persistent" = one
-        long-running kernel fed through a descriptor ring (MLP/LR, zero-copy outputs)."""
+        long-running kernel fed through a descriptor ring (MLP/LR, zero-copy outputs).
+        coalesce: launch mode -- up to this many ready, log-contiguous micro-batches go out as
+        one launch (MLP, zero-copy in/out); completion stays per micro-batch."""
         self.dm = dm
         self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device())
         self.batch = int(batch)
@@ -145,6 +147,7 @@ class StreamEngine:
         cfg.flag_capacity = int(flag_capacity)
         cfg.exec_mode = {"launch": 0, "persistent": 1}[exec_mode]
         cfg.persist_grid = int(persist_grid)
+        cfg.coalesce = max(1, min(8, int(coalesce)))
         self.wire = bool(getattr(dm, "wire", False))
         cfg.wire = 1 if self.wire else 0
         self.exec_mode = exec_mode

@@ -199,6 +199,7 @@ class Engine {
   // ------------------------------------------------------------------ persistent mode
   bool persistent = false;
   bool coherent_out = true;
+  uint64_t launches = 0;        // coalesced launches issued (stream round-robin)
   int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, or 16 for W64 wire rows
   int amount_f = CCFD_N_FEATURES - 1;
   int ablate = 0;
@@ -517,15 +518,51 @@ class Engine {
     return 0;
   }
 
+  // Coalesced launches (launch mode, zero-copy in/out, MLP): K >= 2 ready micro-batches
+  // that are contiguous in one partition's log go out as ONE kernel launch; each keeps its
+  // own slot, outputs, flag list and kernel-published completion record.
+  int coalesce_max() const {
+    if (persistent || cfg.input_mode != 1 || cfg.output_mode != 0 || cfg.model != CCFD_MODEL_MLP) return 1;
+    return std::max(1, std::min({cfg.coalesce, CCFD_MAX_SUB, (int)slots.size()}));
+  }
+
+  int submit_multi(int p, int64_t start, int32_t rows, int K) {
+    Partition& P = *parts[p];
+    const int D = (int)slots.size();
+    const int64_t t = now_ns();
+    struct Acc { uint64_t& a; int64_t t0; ~Acc() { a += now_ns() - t0; } } acc{t_submit_ns, t};
+    ccfd_multi_args m{};
+    ccfd_score_args& a = m.base;
+    a.x = P.feats_dev + (size_t)start * rowf;
+    a.ld = rowf; a.n = K * rows; a.model = cfg.model; a.blob = cfg.blob;
+    a.threshold = cfg.threshold;
+    a.counters = cfg.counters[epoch & 1];
+    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate |
+              (cfg.wire ? CCFD_ARG_WIRE_W64 : 0);
+    m.nsub = K;
+    m.sub_rows = rows;
+    for (int k = 0; k < K; ++k) {
+      Slot& s = slots[(seq + k) % D];
+      s.t_submit = t;
+      s.seq_no = (int64_t)(seq + k);
+      s.part = p; s.start = start + (int64_t)k * rows; s.rows = rows;
+      s.use_flag = true;
+      s.expect = ++done_counter;
+      s.done_ptr = s.h_done;
+      s.busy = true;
+      m.sub[k] = ccfd_sub_batch{s.h_proba_dev, s.h_route_dev, s.d_ctl, s.h_flag_dev, s.h_done_dev, s.expect};
+    }
+    return ccfd_score_launch_multi(&m, streams[(launches++) % streams.size()]);
+  }
+
   int pump(int64_t n_batches, int32_t batch_rows, bool drain, ccfd_engine_stats* st) {
     HIPCHK(hipSetDevice(cfg.device));
     if (parts.empty()) { set_error("no partition log registered"); return -1; }
     if (batch_rows <= 0 || batch_rows > cfg.max_batch) { set_error("bad batch_rows"); return -1; }
     const int64_t t0 = now_ns();
     const int D = (int)slots.size();
-    for (int64_t b = 0; b < n_batches; ++b) {
-      Slot& s = slots[seq % D];
-      if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
+    const int kmax = coalesce_max();
+    for (int64_t b = 0; b < n_batches;) {
       int p = next_part;
       for (int k = 0; k < (int)parts.size() && (parts[p]->feats == nullptr || parts[p]->ring); ++k)
         p = (p + 1) % parts.size();
@@ -533,6 +570,21 @@ class Engine {
       Partition& P = *parts[p];
       if (P.ring || P.feats == nullptr) { set_error("pump() needs a replay log partition"); return -1; }
       if (P.cursor + batch_rows > P.n) P.cursor = 0;
+      // coalesce up to kmax consecutive micro-batches of this partition into one launch
+      const int K = (int)std::min<int64_t>({(int64_t)kmax, n_batches - b, (P.n - P.cursor) / batch_rows});
+      for (int k = 0; k < K; ++k) {
+        Slot& s = slots[(seq + k) % D];
+        if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
+      }
+      if (K > 1) {
+        int rc = submit_multi(p, P.cursor, batch_rows, K);
+        if (rc) return rc;
+        P.cursor += (int64_t)K * batch_rows;
+        seq += K;
+        b += K;
+        continue;
+      }
+      Slot& s = slots[seq % D];
       s.part = p; s.start = P.cursor; s.rows = batch_rows;
       P.cursor += batch_rows;
       const size_t off = (size_t)s.start * rowf;
@@ -540,6 +592,7 @@ class Engine {
       int rc = submit(s, P.feats_dev + off, P.feats + off, batch_rows, stream);
       if (rc) return rc;
       ++seq;
+      ++b;
     }
     if (drain) {
       int rc = drain_all(st);

@@ -63,6 +63,29 @@ typedef struct ccfd_score_args {
   unsigned long long done_seq;
 } ccfd_score_args;
 
+// Coalesced launch: `nsub` consecutive micro-batches of `sub_rows` rows (contiguous in x,
+// base.n rows in total) scored by ONE launch; every micro-batch keeps its own outputs,
+// flag list and completion record, and its workgroups signal it independently.  Cuts the
+// per-launch host + dispatch cost by nsub while the unit of completion stays the micro-batch.
+#define CCFD_MAX_SUB 8
+typedef struct ccfd_sub_batch {
+  float* proba;
+  uint8_t* route;
+  unsigned int* slot_ctl;
+  unsigned int* flag_idx;
+  unsigned long long* done_rec;
+  unsigned long long done_seq;
+} ccfd_sub_batch;   // 48 bytes
+
+typedef struct ccfd_multi_args {
+  ccfd_score_args base;            // x, n (total), model, blob, threshold, flags, counters
+  int32_t nsub;
+  int32_t sub_rows;
+  ccfd_sub_batch sub[CCFD_MAX_SUB];
+} ccfd_multi_args;
+
+int ccfd_score_launch_multi(const ccfd_multi_args* m, void* stream);
+
 // Enqueue one fused scoring launch (normalize -> model -> sigmoid -> threshold ->
 // counters/histogram) on `stream` (a hipStream_t; NULL = legacy default stream).
 // Returns 0 or a negative error code (shape/alignment checks happen on the host).
@@ -143,6 +166,8 @@ typedef struct ccfd_engine_config {
   int32_t exec_mode;           // 0 = one fused launch per micro-batch, 1 = persistent kernel
   int32_t persist_grid;        // workgroups of the persistent kernel (0 = 256)
   int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B, CCFD_WIRE_ROW_BYTES)
+  int32_t coalesce;            // launch mode: up to this many ready micro-batches per launch (<= 8)
+  int32_t _pad2;
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
 } ccfd_engine_config;
 

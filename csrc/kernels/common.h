@@ -81,7 +81,9 @@ __device__ __forceinline__ void emit_flagged(const ccfd_score_args& a, bool fr_l
 // (cdna_hip_programming.md §6 Guideline 16 publish recipe, system scope): each storing wave
 // drains its stores, the workgroup barrier, lane 0 releases at system scope and takes a
 // ticket; the last ticket resets the slot and publishes {#flagged, done_seq} to the host.
-__device__ __forceinline__ void signal_done(const ccfd_score_args& a) {
+// `nblk`: workgroups that score this micro-batch (gridDim.x for a plain launch, the
+// per-sub-batch share for a coalesced one).
+__device__ __forceinline__ void signal_done(const ccfd_score_args& a, unsigned nblk) {
   if (a.slot_ctl == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -96,7 +98,7 @@ __device__ __forceinline__ void signal_done(const ccfd_score_args& a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const unsigned ticket = __hip_atomic_fetch_add(&a.slot_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ticket == gridDim.x - 1) {
+    if (ticket == nblk - 1) {
       const unsigned nflag = __hip_atomic_load(&a.slot_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.slot_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.slot_ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -174,6 +176,23 @@ __device__ __forceinline__ void load_tile_contig(const float* __restrict__ xt, i
   TileRegs r;
   tile_issue(xt, avail, lane, r);
   tile_store(lds_tile, lane, r);
+}
+
+// Per-micro-batch view of a coalesced launch: sub-batch j of `m` as plain score args.
+// `m` must be addressable memory (the kernarg segment, see score_mlp_multi_kernel).
+__device__ __forceinline__ ccfd_score_args sub_args(const ccfd_multi_args& m, int j) {
+  ccfd_score_args a = m.base;
+  const int64_t r0 = (int64_t)j * m.sub_rows;
+  a.x = m.base.x + r0 * m.base.ld;
+  a.n = (int)min((int64_t)m.sub_rows, (int64_t)m.base.n - r0);
+  const ccfd_sub_batch& sb = m.sub[j];
+  a.proba = sb.proba;
+  a.route = sb.route;
+  a.slot_ctl = sb.slot_ctl;
+  a.flag_idx = sb.flag_idx;
+  a.done_rec = sb.done_rec;
+  a.done_seq = sb.done_seq;
+  return a;
 }
 
 }  // namespace ccfd

@@ -7,6 +7,7 @@
 
 namespace ccfd {
 int launch_mlp(const ccfd_score_args& a, hipStream_t s);
+int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s);
 int launch_lr(const ccfd_score_args& a, hipStream_t s);
 int launch_gbdt(const ccfd_score_args& a, hipStream_t s);
 
@@ -42,6 +43,31 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
     hipError_t e = hipGetLastError();
     set_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
   }
+  return rc;
+}
+
+int ccfd_score_launch_multi(const ccfd_multi_args* m, void* stream) {
+  using namespace ccfd;
+  if (m == nullptr || m->base.blob == nullptr || m->base.x == nullptr) { set_error("null argument"); return -1; }
+  if (m->base.model != CCFD_MODEL_MLP) { set_error("coalesced launch: MLP model only"); return -2; }
+  if (m->nsub < 1 || m->nsub > CCFD_MAX_SUB || m->sub_rows <= 0 ||
+      (int64_t)m->base.n > (int64_t)m->nsub * m->sub_rows || (int64_t)m->base.n <= (int64_t)(m->nsub - 1) * m->sub_rows) {
+    set_error("coalesced launch: bad nsub / sub_rows / n");
+    return -1;
+  }
+  const bool wire = (m->base.flags & CCFD_ARG_WIRE_W64) != 0;
+  if (wire ? (reinterpret_cast<uintptr_t>(m->base.x) & 15) != 0
+           : (m->base.ld != kF || (reinterpret_cast<uintptr_t>(m->base.x) & 15) != 0)) {
+    set_error("coalesced launch: x must be 16-byte aligned contiguous rows");
+    return -3;
+  }
+  for (int j = 0; j < m->nsub; ++j)
+    if (m->sub[j].slot_ctl == nullptr || m->sub[j].done_rec == nullptr) {
+      set_error("coalesced launch: every sub-batch needs a completion record");
+      return -1;
+    }
+  const int rc = launch_mlp_multi(*m, reinterpret_cast<hipStream_t>(stream));
+  if (rc != 0) set_error(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   return rc;
 }
 

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a) {
     emit_flagged(a, fr, row);
   }
   epi_flush(epi, a.counters);
-  signal_done(a);
+  signal_done(a, gridDim.x);
 }
 
 template <int D>

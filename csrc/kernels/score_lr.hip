@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args
     atomicAdd(&epi.psum_e6, psum);
   }
   epi_flush(epi, a.counters);
-  signal_done(a);
+  signal_done(a, gridDim.x);
 }
 
 int mlp_waves_for(int ntiles);   // score_mlp.hip (same policy and CCFD_MLP_WAVES override)

@@ -17,6 +17,7 @@
 //  24 MFMAs (16x16x32) per 16 rows: compute is ~1% of the kernel; it is a latency /
 //  bandwidth kernel, so fusion (one launch, one pass over x) is what matters.
 #include <cstdlib>
+#include <string>
 
 #include "mlp_core.h"
 
@@ -28,11 +29,16 @@ namespace ccfd {
 // the weight staging and completion ticket more often (profiles/r1/waves_sweep.txt).
 // kMode: 0 = strided f32 rows, 1 = contiguous f32 rows [n][30] (LDS-staged tiles),
 //        2 = W64 wire rows (one 16-B register load per lane, no LDS tile).
+// Body shared by the plain and the coalesced launch: workgroup `blk` of the `nblk` that
+// score micro-batch `a`.  Entry points ask for >= 4 waves per SIMD (<= 128 VGPRs): a wave
+// usually scores a single tile, so occupancy (outstanding zero-copy loads) beats hoisting
+// the 24 weight fragments into registers, which the W64 path otherwise does (272 VGPRs).
 template <int kMode, int kWaves>
-__global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args a) {
-  constexpr bool kContig = kMode == 1;
-  constexpr bool kWire = kMode == 2;
-  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
+__device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int nblk) {
+  constexpr bool kContig = (kMode & 3) == 1;
+  constexpr bool kWire = (kMode & 3) == 2;
+  constexpr bool kGW = (kMode & 4) != 0;     // weights read from global (L1/L2), no LDS copy
+  __shared__ __attribute__((aligned(16))) char sblob[kGW ? 16 : kMlpBlob];
   __shared__ __attribute__((aligned(16))) float sx[kWire ? 1 : kWaves][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
 
@@ -40,8 +46,8 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
-  const int tstride = gridDim.x * kWaves;
-  int tile = blockIdx.x * kWaves + wave;
+  const int tstride = nblk * kWaves;
+  int tile = blk * kWaves + wave;
 
   // Issue this wave's first input tile BEFORE staging the weights: the (possibly PCIe)
   // fetch latency of x overlaps the L2 fetch of the model blob.
@@ -55,11 +61,12 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
   if constexpr (kWire) {
     if (tile < ntiles) wire_issue(xw, a.n, tile, c, g, wpre);
   }
-  mlp_stage(a.blob, sblob, tid, 64 * kWaves);
+  if constexpr (!kGW) mlp_stage(a.blob, sblob, tid, 64 * kWaves);
+  const char* W = kGW ? reinterpret_cast<const char*>(a.blob) : sblob;
   epi_init(epi);
   __syncthreads();
 
-  const MlpLane L = mlp_lane(sblob, g);
+  const MlpLane L = mlp_lane(W, g);
   const float thr = a.threshold;
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
@@ -79,17 +86,21 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       tile_features(tile_lds, c, g, xv);
     } else if constexpr (kWire) {
+      // compiler barrier: keep the weight fragments as per-tile LDS reads (not hoisted into
+      // ~100 loop-invariant VGPRs, which would spill under the 128-VGPR occupancy cap)
+      asm volatile("" ::: "memory");
       const WireRegs cur = wpre;
       const int nxt = tile + tstride;
       if (nxt < ntiles) wire_issue(xw, a.n, nxt, c, g, wpre);
       wire_features(cur, g, xv);
     } else {
+      asm volatile("" ::: "memory");   // as above: no hoisted weight fragments
       const float* xr = a.x + (size_t)row * a.ld + 8 * g;
 #pragma unroll
       for (int j = 0; j < 8; ++j) xv[j] = (valid && (8 * g + j) < kF) ? xr[j] : 0.f;
     }
     float amount;
-    const float p = mlp_tile(sblob, L, xv, g, lane, amount);
+    const float p = mlp_tile(W, L, xv, g, lane, amount);
     const bool fr = valid && (p >= thr);
 
     if (valid && g == 0) {
@@ -111,19 +122,66 @@ __global__ __launch_bounds__(64 * kWaves) void score_mlp_kernel(ccfd_score_args 
     atomicAdd(&epi.psum_e6, psum);
   }
   epi_flush(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
-  signal_done(a);
+  signal_done(a, (unsigned)nblk);
+}
+
+template <int kMode, int kWaves>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
+void score_mlp_kernel(ccfd_score_args a) {
+  mlp_body<kMode, kWaves>(a, blockIdx.x, gridDim.x);
+}
+
+// Coalesced launch: workgroups [j*wpb, (j+1)*wpb) score sub-batch j.
+template <int kMode, int kWaves>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
+void score_mlp_multi_kernel(ccfd_multi_args m) {
+  // read the table through the kernarg segment pointer: indexing the by-value parameter
+  // with the (workgroup-uniform) sub index would make the compiler spill it to scratch
+  (void)m;
+  const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int wpb = gridDim.x / mk.nsub;                 // workgroups per sub-batch
+  const int j = blockIdx.x / wpb;
+  mlp_body<kMode, kWaves>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+}
+
+// CCFD_MLP_WEIGHTS=global: MFMA weight fragments read straight from the (L1/L2-resident)
+// blob instead of a per-workgroup LDS copy -- no staging on the critical path and no LDS
+// occupancy limit.  Default: lds.
+// CCFD_MLP_TPW: 16-row tiles per wave (1, 2, 4, 8; default 8).  More tiles per wave = fewer workgroups per
+// micro-batch, i.e. fewer weight-staging copies and completion releases (each wave keeps
+// one tile of prefetch in flight).
+static int mlp_tiles_per_wave() {
+  static const int t = [] {
+    const char* e = std::getenv("CCFD_MLP_TPW");
+    const int v = e ? std::atoi(e) : 8;     // measured best (profiles/r1/launch_sweep.txt)
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 8;
+  }();
+  return t;
+}
+
+static bool mlp_global_weights() {
+  static const bool gw = [] {
+    const char* e = std::getenv("CCFD_MLP_WEIGHTS");
+    return e != nullptr && std::string(e) == "global";
+  }();
+  return gw;
 }
 
 template <int kW>
 static void launch_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
-  int grid = (ntiles + kW - 1) / kW;
+  const int per_wg = kW * mlp_tiles_per_wave();
+  int grid = (ntiles + per_wg - 1) / per_wg;
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-  if (a.flags & CCFD_ARG_WIRE_W64)
-    hipLaunchKernelGGL((score_mlp_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
-  else if (contig)
-    hipLaunchKernelGGL((score_mlp_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
-  else
+  const bool gw = mlp_global_weights();
+  if (a.flags & CCFD_ARG_WIRE_W64) {
+    if (gw) hipLaunchKernelGGL((score_mlp_kernel<6, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    else hipLaunchKernelGGL((score_mlp_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  } else if (contig) {
+    if (gw) hipLaunchKernelGGL((score_mlp_kernel<5, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    else hipLaunchKernelGGL((score_mlp_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  } else {
     hipLaunchKernelGGL((score_mlp_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+  }
 }
 
 int mlp_waves_for(int ntiles) {
@@ -134,6 +192,22 @@ int mlp_waves_for(int ntiles) {
   if (forced == 1 || forced == 2 || forced == 4) return forced;
   (void)ntiles;
   return 4;   // measured: 1-wave workgroups lose (per-workgroup weight staging + completion)
+}
+
+int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
+  constexpr int kW = 4;
+  const int rows_per_wg = kTileRows * kW * mlp_tiles_per_wave();
+  const int wpb = (m.sub_rows + rows_per_wg - 1) / rows_per_wg;
+  const dim3 grid(wpb * m.nsub), block(64 * kW);
+  const bool gw = mlp_global_weights();
+  if (m.base.flags & CCFD_ARG_WIRE_W64) {
+    if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<6, kW>), grid, block, 0, s, m);
+    else hipLaunchKernelGGL((score_mlp_multi_kernel<2, kW>), grid, block, 0, s, m);
+  } else {
+    if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<5, kW>), grid, block, 0, s, m);
+    else hipLaunchKernelGGL((score_mlp_multi_kernel<1, kW>), grid, block, 0, s, m);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_mlp(const ccfd_score_args& a, hipStream_t s) {

@@ -21,16 +21,19 @@ def setup(gpu):
     ("dma", "zerocopy", "launch"), ("zerocopy", "zerocopy", "launch"), ("dma", "dma", "launch"),
     ("zerocopy", "dma", "launch"), ("zerocopy", "zerocopy", "persistent"), ("dma", "zerocopy", "persistent"),
     ("zerocopy", "zerocopy", "launch-wire"), ("dma", "zerocopy", "launch-wire"),
-    ("zerocopy", "zerocopy", "persistent-wire")])
+    ("zerocopy", "zerocopy", "persistent-wire"), ("zerocopy", "zerocopy", "launch-c4"),
+    ("zerocopy", "zerocopy", "launch-wire-c3")])
 def test_engine_pump_matches_oracle(gpu, setup, input_mode, output_mode, exec_mode):
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
+    coalesce = int(exec_mode.split("-c")[1]) if "-c" in exec_mode else 1
+    exec_mode = exec_mode.split("-c")[0]
     wire = exec_mode.endswith("-wire")
     exec_mode = exec_mode.replace("-wire", "")
     dm = DeviceModel(m, gpu, wire=wire)
     eng = StreamEngine(dm, batch=4096, depth=4, streams=2, input_mode=input_mode,
-                       output_mode=output_mode, exec_mode=exec_mode)
+                       output_mode=output_mode, exec_mode=exec_mode, coalesce=coalesce)
     log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000, wire=wire)
     eng.add_log(0, log)
     st = eng.pump(6)
