@@ -50,8 +50,16 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    # Rehearsal knobs (never needed in production): CCFD_DIST_BACKEND=gloo runs the
+    # collectives over gloo while the engines stay on the GPU, and CCFD_DEVICE_MODULO=1 maps
+    # local rank r to GPU r % device_count, so a multi-rank job can be exercised on a box
+    # with fewer GPUs than ranks (RCCL itself refuses two ranks on one GPU).
+    backend = backend or os.environ.get("CCFD_DIST_BACKEND") or None
+    gpu_ok = torch.cuda.is_available()
+    use_gpu = gpu_ok and (backend != "gloo" or os.environ.get("CCFD_DIST_BACKEND") == "gloo")
     if use_gpu:
+        if os.environ.get("CCFD_DEVICE_MODULO") == "1":
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
