@@ -76,9 +76,12 @@ class NotifierConfig:
 class EngineConfig:
     model: str = "mlp"               # lr | mlp | gbdt
     batch: int = 4096                # micro-batch rows (BASELINE config 2)
-    depth: int = 8                   # micro-batches in flight per GPU
-    streams: int = 2                 # HIP streams per engine
-    input_mode: str = "dma"          # dma (H2D into HBM) | zerocopy (kernel reads pinned host)
+    depth: int = 16                  # micro-batches in flight per GPU
+    streams: int = 4                 # HIP streams per engine
+    input_mode: str = "zerocopy"     # dma (H2D into HBM) | zerocopy (kernel reads pinned host)
+    wire: str = "auto"               # ring row format: f32 | w64 | auto (w64 for mlp/lr)
+    coalesce: int = 4                # ready micro-batches per kernel launch (MLP, launch mode)
+    model_watch: str = ""            # hot-swap when this safetensors file changes (rank 0)
     output_mode: str = "zerocopy"    # zerocopy (kernel writes pinned host) | dma
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches
     reduce_period_ms: float = 10.0   # X2 counter all-reduce period
@@ -118,6 +121,9 @@ ENV_MAP = {
     "CCFD_MODEL": ("engine", "model", str),
     "CCFD_BATCH": ("engine", "batch", int),
     "CCFD_DEPTH": ("engine", "depth", int),
+    "CCFD_WIRE": ("engine", "wire", str),
+    "CCFD_COALESCE": ("engine", "coalesce", int),
+    "CCFD_MODEL_WATCH": ("engine", "model_watch", str),
     "CCFD_INPUT_MODE": ("engine", "input_mode", str),
     "CCFD_OUTPUT_MODE": ("engine", "output_mode", str),
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),

@@ -214,6 +214,17 @@ class StreamEngine:
         self.flips += 1
         return self.counters[idx]
 
+    def swap_model(self, dm: DeviceModel) -> None:
+        """Hot swap (runtime X1): in-flight micro-batches finish on the old weights, later ones
+        use ``dm``.  The new model must have the same kernel kind, row format and GBDT shape."""
+        if dm.kind != self.dm.kind or bool(getattr(dm, "wire", False)) != self.wire or \
+                (dm.trees, dm.depth) != (self.dm.trees, self.dm.depth):
+            raise ValueError("hot swap needs a model of the same kind / wire format / tree shape")
+        check(lib().ccfd_engine_set_blob(C.c_void_p(self.h), C.c_void_p(dm.blob.data_ptr())),
+              "ccfd_engine_set_blob")
+        self.dm = dm                     # keeps the new blob alive; the old one may be freed now
+        self.model_version = getattr(self, "model_version", 0) + 1
+
     def epoch_complete(self, flip_count: int) -> bool:
         """True once every micro-batch submitted before flip number ``flip_count`` completed."""
         return lib().ccfd_engine_epoch_complete(C.c_void_p(self.h), int(flip_count)) == 1

@@ -202,9 +202,11 @@ def cmd_engine(a, cfg):
     ctx = init_distributed()
     bind_to_gpu(ctx.device.index)
     blob = None
+    wire = cfg.engine.wire == "w64" or (cfg.engine.wire == "auto" and cfg.engine.model in ("mlp", "lr"))
     if ctx.rank == 0:
         model = _model(cfg.engine.model, a.weights, cfg.seed)
-        blob = torch.from_numpy(np.frombuffer(model.pack(), np.uint8).copy()).to(ctx.device)
+        packed = model.pack(wire=True) if wire else model.pack()
+        blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(ctx.device)
         trees, depth = getattr(model, "n_trees", 0), getattr(model, "depth", 0)
     else:
         trees = depth = 0
@@ -214,7 +216,7 @@ def cmd_engine(a, cfg):
         td = torch.tensor([trees, depth], device=ctx.device)
         dist.broadcast(td, 0)
         trees, depth = int(td[0]), int(td[1])
-    dm = DeviceModel.from_blob(cfg.engine.model, blob, trees, depth)
+    dm = DeviceModel.from_blob(cfg.engine.model, blob, trees, depth, wire=wire)
     broker = _broker(cfg)
     hub = MetricsHub()
     kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
@@ -223,7 +225,8 @@ def cmd_engine(a, cfg):
         topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
         depth=cfg.engine.depth, streams=cfg.engine.streams, input_mode=cfg.engine.input_mode,
         flush_us=cfg.engine.max_delay_us, reduce_period_ms=cfg.engine.reduce_period_ms,
-        threshold=cfg.router.fraud_threshold)).start()
+        threshold=cfg.router.fraud_threshold, coalesce=cfg.engine.coalesce,
+        model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.rank)
     resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic]) if ctx.rank == 0 else None
@@ -286,6 +289,7 @@ def main(argv=None):
     ap.add_argument("--config", default=None)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--watch-model", default=None, help="engine: hot-swap weights when this file changes")
     ap.add_argument("--grpc-port", type=int, default=0, help="seldon: also serve seldon.protos gRPC Predict")
     ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])

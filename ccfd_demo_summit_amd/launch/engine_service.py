@@ -43,6 +43,8 @@ class EngineServiceConfig:
     input_mode: str = "zerocopy"
     exec_mode: str = "launch"        # "persistent": one resident kernel fed by a descriptor ring
     max_fetch: int = 2000
+    coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
+    model_watch: Optional[str] = None   # rank 0: hot-swap when this safetensors file changes
 
 
 class EngineService:
@@ -55,7 +57,7 @@ class EngineService:
         self.router = router
         self.engine = StreamEngine(dm, batch=cfg.batch, depth=cfg.depth, streams=cfg.streams,
                                    input_mode=cfg.input_mode, threshold=cfg.threshold, device=ctx.device.index,
-                                   exec_mode=cfg.exec_mode)
+                                   exec_mode=cfg.exec_mode, coalesce=cfg.coalesce)
         n_parts = broker.partitions(cfg.topic)
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:
@@ -64,6 +66,8 @@ class EngineService:
             if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
         self.reducer = reducer or CounterReducer(ctx, ctx.device)
         self.epochs = EpochPipeline(self.engine, self.reducer)
+        from ..parallel.hotswap import HotSwap
+        self.hotswap = HotSwap(ctx, self.engine, cfg.model_watch)
         # per partition: (ring row end, next kafka offset) of ingested messages, oldest first
         self._pending: Dict[int, Deque[Tuple[int, int]]] = {p: collections.deque() for p in self.partitions}
         self._rows_in: Dict[int, int] = {p: 0 for p in self.partitions}
@@ -140,7 +144,12 @@ class EngineService:
             self.epochs.tick(lat - self._lat_prev)
             self._lat_prev = lat
             self.last_reduce = now
+            self.hotswap.tick()                          # collective: X1 at runtime
         return int(st.rows)
+
+    def request_swap(self, model) -> None:
+        """Publish new weights to every rank at the next epoch tick (call on rank 0)."""
+        self.hotswap.offer(model)
 
     def start(self) -> "EngineService":
         self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")

@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
         L.ccfd_engine_score_sync.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.ccfd_engine_flip_epoch.argtypes = [C.c_void_p, C.c_void_p]
         L.ccfd_engine_epoch_complete.argtypes = [C.c_void_p, C.c_int64]
+        L.ccfd_engine_set_blob.argtypes = [C.c_void_p, C.c_void_p]
         L.ccfd_engine_drain_flagged.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.ccfd_engine_drain_flagged.restype = C.c_int64
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]

@@ -518,11 +518,12 @@ class Engine {
     return 0;
   }
 
-  // Coalesced launches (launch mode, zero-copy in/out, MLP): K >= 2 ready micro-batches
+  // Coalesced launches (launch mode, zero-copy in/out, MLP/LR): K >= 2 ready micro-batches
   // that are contiguous in one partition's log go out as ONE kernel launch; each keeps its
   // own slot, outputs, flag list and kernel-published completion record.
   int coalesce_max() const {
-    if (persistent || cfg.input_mode != 1 || cfg.output_mode != 0 || cfg.model != CCFD_MODEL_MLP) return 1;
+    if (persistent || cfg.input_mode != 1 || cfg.output_mode != 0 ||
+        (cfg.model != CCFD_MODEL_MLP && cfg.model != CCFD_MODEL_LR)) return 1;
     return std::max(1, std::min({cfg.coalesce, CCFD_MAX_SUB, (int)slots.size()}));
   }
 
@@ -649,6 +650,19 @@ class Engine {
     return persistent ? persist_halt() : 0;
   }
 
+  // Model hot swap (X1 at runtime): every in-flight micro-batch completes with the old
+  // weights (and a resident persistent kernel halts), then later submissions read `blob`.
+  // The caller keeps the old blob alive until this returns.
+  int set_blob(const void* blob) {
+    if (blob == nullptr) { set_error("null model blob"); return -1; }
+    HIPCHK(hipSetDevice(cfg.device));
+    int rc = drain_all();
+    if (rc) return rc;
+    if (persistent && prunning) { rc = persist_halt(); if (rc) return rc; }
+    cfg.blob = blob;
+    return 0;
+  }
+
   int flip_epoch(void* side_stream) {
     HIPCHK(hipSetDevice(cfg.device));
     const int closed = epoch & 1;
@@ -735,6 +749,23 @@ class Engine {
           Slot& s = slots[seq % D];
           if (s.busy) break;                               // all slots in flight
           const int64_t phys = P.rr.take_pos();
+          // several full micro-batches ready and contiguous in the ring: one coalesced launch
+          int K = (int)std::min<int64_t>({(int64_t)coalesce_max(), avail / cfg.max_batch,
+                                          (P.n - phys) / cfg.max_batch});
+          for (int k = 1; k < K; ++k)
+            if (slots[(seq + k) % D].busy) { K = k; break; }
+          if (K >= 2) {
+            int rc = submit_multi((int)q, phys, cfg.max_batch, K);
+            if (rc) return rc;
+            for (int k = 0; k < K; ++k)
+              slots[(seq + k) % D].t_arrival = P.arrival_of(P.rr.taken() + (int64_t)k * cfg.max_batch);
+            seq += K;
+            submitted += K;
+            P.rr.take((int64_t)K * cfg.max_batch);
+            avail -= (int64_t)K * cfg.max_batch;
+            progress = true;
+            continue;
+          }
           int64_t rows = std::min<int64_t>({avail, (int64_t)cfg.max_batch, P.n - phys});
           const bool full = rows == cfg.max_batch || rows == P.n - phys;
           const int64_t arr = P.arrival_of(P.rr.taken());
@@ -805,6 +836,10 @@ int ccfd_engine_flip_epoch(void* eng, void* side_stream) {
 
 int ccfd_engine_epoch_complete(void* eng, int64_t flip_count) {
   return static_cast<Engine*>(eng)->epoch_complete(flip_count);
+}
+
+int ccfd_engine_set_blob(void* eng, const void* blob) {
+  return static_cast<Engine*>(eng)->set_blob(blob);
 }
 
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max) {

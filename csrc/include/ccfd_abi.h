@@ -217,6 +217,8 @@ int ccfd_engine_flip_epoch(void* eng, void* side_stream);
 // returned by flip) has completed.  Required before reducing a closed epoch buffer in
 // exec_mode 1 (the persistent kernel has no per-batch events a stream could wait on).
 int ccfd_engine_epoch_complete(void* eng, int64_t flip_count);
+// Hot swap: drain in-flight micro-batches, then score later ones with `blob` (same kind/shape).
+int ccfd_engine_set_blob(void* eng, const void* blob);
 // Drain up to `max` flagged records (fraud route) into `out`; returns count.
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
 int64_t ccfd_engine_cursor(void* eng, int partition);

@@ -171,6 +171,16 @@ __device__ __forceinline__ void wire_features(const WireRegs& r, int g, float xv
   xv[7] = tail ? 0.f : __uint_as_float(w3 & 0xffff0000u);
 }
 
+// Read this lane's 8 features of row c from a wave-private LDS tile [16][30].
+__device__ __forceinline__ void tile_features(const float* tile_lds, int c, int g, float xv[8]) {
+  const float2* r2 = reinterpret_cast<const float2*>(tile_lds + c * kF + 8 * g);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float2 v = (g < 3 || j < 3) ? r2[j] : make_float2(0.f, 0.f);
+    xv[2 * j] = v.x; xv[2 * j + 1] = v.y;
+  }
+}
+
 __device__ __forceinline__ void load_tile_contig(const float* __restrict__ xt, int avail,
                                                  float* lds_tile, int lane) {
   TileRegs r;

@@ -9,6 +9,7 @@ namespace ccfd {
 int launch_mlp(const ccfd_score_args& a, hipStream_t s);
 int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s);
 int launch_lr(const ccfd_score_args& a, hipStream_t s);
+int launch_lr_multi(const ccfd_multi_args& m, hipStream_t s);
 int launch_gbdt(const ccfd_score_args& a, hipStream_t s);
 
 thread_local std::string g_last_error;
@@ -49,7 +50,10 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
 int ccfd_score_launch_multi(const ccfd_multi_args* m, void* stream) {
   using namespace ccfd;
   if (m == nullptr || m->base.blob == nullptr || m->base.x == nullptr) { set_error("null argument"); return -1; }
-  if (m->base.model != CCFD_MODEL_MLP) { set_error("coalesced launch: MLP model only"); return -2; }
+  if (m->base.model != CCFD_MODEL_MLP && m->base.model != CCFD_MODEL_LR) {
+    set_error("coalesced launch: MLP and LR models only");
+    return -2;
+  }
   if (m->nsub < 1 || m->nsub > CCFD_MAX_SUB || m->sub_rows <= 0 ||
       (int64_t)m->base.n > (int64_t)m->nsub * m->sub_rows || (int64_t)m->base.n <= (int64_t)(m->nsub - 1) * m->sub_rows) {
     set_error("coalesced launch: bad nsub / sub_rows / n");
@@ -66,7 +70,8 @@ int ccfd_score_launch_multi(const ccfd_multi_args* m, void* stream) {
       set_error("coalesced launch: every sub-batch needs a completion record");
       return -1;
     }
-  const int rc = launch_mlp_multi(*m, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int rc = m->base.model == CCFD_MODEL_LR ? launch_lr_multi(*m, s) : launch_mlp_multi(*m, s);
   if (rc != 0) set_error(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   return rc;
 }

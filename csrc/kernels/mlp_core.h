@@ -44,16 +44,6 @@ __device__ __forceinline__ MlpLane mlp_lane(const char* sblob, int g) {
   return L;
 }
 
-// Read this lane's 8 features of row c from a wave-private LDS tile [16][30].
-__device__ __forceinline__ void tile_features(const float* tile_lds, int c, int g, float xv[8]) {
-  const float2* r2 = reinterpret_cast<const float2*>(tile_lds + c * kF + 8 * g);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float2 v = (g < 3 || j < 3) ? r2[j] : make_float2(0.f, 0.f);
-    xv[2 * j] = v.x; xv[2 * j + 1] = v.y;
-  }
-}
-
 // proba_1 of row (lane & 15) of the tile; identical in all four lane groups.
 // xv: raw features (consumed); amount_out: raw Amount (valid in lane group 3).
 __device__ __forceinline__ float mlp_tile(const char* sblob, const MlpLane& L, float xv[8], int g, int lane,

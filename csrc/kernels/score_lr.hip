@@ -2,24 +2,41 @@
 // counters.  Same 16-row tile / 4-lanes-per-row layout as score_mlp.hip so the input is
 // read with full-width coalesced loads; the 30-term dot product is 8 FMAs per lane plus
 // two xor-shuffles.  GPU counterpart of the config-1 LR model (BASELINE.json configs[0]).
+// Launch structure mirrors score_mlp.hip: a plain and a coalesced (multi-micro-batch) entry
+// over one body, tiles-per-wave with a one-tile prefetch.
 #include "common.h"
 
 namespace ccfd {
 
 constexpr int kLrBlob = 64 + 3 * 32 * 4;   // models/lr.py BLOB_BYTES
 
-// waves per workgroup: see score_mlp.hip (small micro-batches use 1-wave workgroups so the
-// grid covers every CU)
+int mlp_waves_for(int ntiles);     // score_mlp.hip (same policy and CCFD_MLP_WAVES override)
+int mlp_tiles_per_wave_policy();   // score_mlp.hip (CCFD_MLP_TPW)
+
 // kMode as in score_mlp.hip: 0 strided f32, 1 contiguous f32, 2 W64 wire rows
 template <int kMode, int kLrWaves>
-__global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args a) {
+__device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int nblk) {
   constexpr bool kContig = kMode == 1;
   constexpr bool kWire = kMode == 2;
-  __shared__ __attribute__((aligned(16))) float sx[kLrWaves][kTileRows * kF + 4];
+  __shared__ __attribute__((aligned(16))) float sx[kContig ? kLrWaves : 1][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
+  const int ntiles = (a.n + kTileRows - 1) / kTileRows;
+  const int tstride = nblk * kLrWaves;
+  int tile = blk * kLrWaves + wave;
+
+  TileRegs pre;
+  WireRegs wpre;
+  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x);
+  auto tile_avail = [&](int t) { return min(kTileRows, a.n - t * kTileRows) * kF * 4; };
+  if constexpr (kContig) {
+    if (tile < ntiles) tile_issue(a.x + (size_t)tile * kTileRows * kF, tile_avail(tile), lane, pre);
+  }
+  if constexpr (kWire) {
+    if (tile < ntiles) wire_issue(xw, a.n, tile, c, g, wpre);
+  }
   epi_init(epi);
 
   const char* blob = reinterpret_cast<const char*>(a.blob);
@@ -36,27 +53,22 @@ __global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args
 
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
-  const int ntiles = (a.n + kTileRows - 1) / kTileRows;
-  float* tile_lds = sx[wave];
-  for (int tile = blockIdx.x * kLrWaves + wave; tile < ntiles; tile += gridDim.x * kLrWaves) {
+  float* tile_lds = sx[kContig ? wave : 0];
+  for (; tile < ntiles; tile += tstride) {
     const int row = tile * kTileRows + c;
     const bool valid = row < a.n;
+    const int nxt = tile + tstride;
     float xv[8];
     if constexpr (kContig) {
-      const int rows_here = min(kTileRows, a.n - tile * kTileRows);
-      load_tile_contig(a.x + (size_t)tile * kTileRows * kF, rows_here * kF * 4, tile_lds, lane);
+      tile_store(tile_lds, lane, pre);
+      if (nxt < ntiles) tile_issue(a.x + (size_t)nxt * kTileRows * kF, tile_avail(nxt), lane, pre);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const float2* r2 = reinterpret_cast<const float2*>(tile_lds + c * kF + 8 * g);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float2 v = (g < 3 || j < 3) ? r2[j] : make_float2(0.f, 0.f);
-        xv[2 * j] = v.x; xv[2 * j + 1] = v.y;
-      }
+      tile_features(tile_lds, c, g, xv);
     } else if constexpr (kWire) {
-      WireRegs r;
-      wire_issue(reinterpret_cast<const unsigned char*>(a.x), a.n, tile, c, g, r);
-      wire_features(r, g, xv);
+      const WireRegs cur = wpre;
+      if (nxt < ntiles) wire_issue(xw, a.n, nxt, c, g, wpre);
+      wire_features(cur, g, xv);
     } else {
       const float* xr = a.x + (size_t)row * a.ld + 8 * g;
 #pragma unroll
@@ -91,14 +103,27 @@ __global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args
     atomicAdd(&epi.psum_e6, psum);
   }
   epi_flush(epi, a.counters);
-  signal_done(a, gridDim.x);
+  signal_done(a, (unsigned)nblk);
 }
 
-int mlp_waves_for(int ntiles);   // score_mlp.hip (same policy and CCFD_MLP_WAVES override)
+template <int kMode, int kLrWaves>
+__global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args a) {
+  lr_body<kMode, kLrWaves>(a, blockIdx.x, gridDim.x);
+}
+
+template <int kMode, int kLrWaves>
+__global__ __launch_bounds__(64 * kLrWaves) void score_lr_multi_kernel(ccfd_multi_args m) {
+  (void)m;   // table read through the kernarg segment (see score_mlp_multi_kernel)
+  const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int wpb = gridDim.x / mk.nsub;
+  const int j = blockIdx.x / wpb;
+  lr_body<kMode, kLrWaves>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+}
 
 template <int kW>
 static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
-  int grid = (ntiles + kW - 1) / kW;
+  const int per_wg = kW * mlp_tiles_per_wave_policy();
+  int grid = (ntiles + per_wg - 1) / per_wg;
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
   if (a.flags & CCFD_ARG_WIRE_W64)
     hipLaunchKernelGGL((score_lr_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
@@ -116,6 +141,18 @@ int launch_lr(const ccfd_score_args& a, hipStream_t s) {
     case 2: launch_lr_w<2>(a, ntiles, contig, s); break;
     default: launch_lr_w<4>(a, ntiles, contig, s); break;
   }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_lr_multi(const ccfd_multi_args& m, hipStream_t s) {
+  constexpr int kW = 4;
+  const int rows_per_wg = kTileRows * kW * mlp_tiles_per_wave_policy();
+  const int wpb = (m.sub_rows + rows_per_wg - 1) / rows_per_wg;
+  const dim3 grid(wpb * m.nsub), block(64 * kW);
+  if (m.base.flags & CCFD_ARG_WIRE_W64)
+    hipLaunchKernelGGL((score_lr_multi_kernel<2, kW>), grid, block, 0, s, m);
+  else
+    hipLaunchKernelGGL((score_lr_multi_kernel<1, kW>), grid, block, 0, s, m);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

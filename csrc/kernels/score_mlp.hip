@@ -150,7 +150,9 @@ void score_mlp_multi_kernel(ccfd_multi_args m) {
 // CCFD_MLP_TPW: 16-row tiles per wave (1, 2, 4, 8; default 8).  More tiles per wave = fewer workgroups per
 // micro-batch, i.e. fewer weight-staging copies and completion releases (each wave keeps
 // one tile of prefetch in flight).
-static int mlp_tiles_per_wave() {
+int mlp_tiles_per_wave_policy();
+static int mlp_tiles_per_wave() { return mlp_tiles_per_wave_policy(); }
+int mlp_tiles_per_wave_policy() {
   static const int t = [] {
     const char* e = std::getenv("CCFD_MLP_TPW");
     const int v = e ? std::atoi(e) : 8;     // measured best (profiles/r1/launch_sweep.txt)

@@ -81,3 +81,63 @@ def test_hist_quantile():
     v = hist_quantile(h, 0.5)
     assert 2 ** 10 <= v < 2 ** 10.25
     assert hist_quantile(np.zeros(256), 0.5) == 0.0
+
+
+class _FakeEngine:
+    """Stands in for StreamEngine on CPU: records the blobs it is asked to swap to."""
+
+    def __init__(self):
+        from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+        self.wire = False
+        self.dm = DeviceModel.from_blob("mlp", torch.zeros(16, dtype=torch.uint8))
+        self.swapped = []
+
+    def swap_model(self, dm):
+        self.dm = dm
+        self.swapped.append(bytes(dm.blob.numpy()))
+
+
+def _hotswap_worker(rank, world, port, path, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.models import build_model, save_model
+    from ccfd_demo_summit_amd.parallel import init_distributed
+    from ccfd_demo_summit_amd.parallel.hotswap import HotSwap
+    ctx = init_distributed(backend="gloo")
+    try:
+        eng = _FakeEngine()
+        hs = HotSwap(ctx, eng, watch_path=path if rank == 0 else None)
+        got = [hs.tick()]                                   # nothing offered
+        if rank == 0:
+            hs.offer(build_model("mlp", seed=1))
+        got.append(hs.tick())                               # explicit offer -> swap everywhere
+        if rank == 0:
+            import time
+            time.sleep(0.05)
+            save_model(build_model("mlp", seed=2), path)    # file watch -> second swap
+            os.utime(path, (time.time() + 5, time.time() + 5))
+        got.append(hs.tick())
+        got.append(hs.tick())
+        q.put((rank, got, hs.version, eng.swapped))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_hot_swap_broadcasts_new_weights(tmp_path):
+    from ccfd_demo_summit_amd.models import build_model
+    path = str(tmp_path / "model.safetensors")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_hotswap_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    want = [build_model("mlp", seed=1).pack(), build_model("mlp", seed=2).pack()]
+    for rank, got, version, swapped in res:
+        assert got == [False, True, True, False], (rank, got)
+        assert version == 2
+        assert swapped == want

@@ -72,7 +72,7 @@ def test_engine_score_sync_pageable_input(gpu, setup):
     eng.close()
 
 
-@pytest.mark.parametrize("exec_mode", ["launch", "persistent", "launch-wire"])
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent", "launch-wire", "launch-wire-c4"])
 def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     """Live ingest: producer writes into the pinned SPSC ring (rows + JSON), run() scores full
     micro-batches and deadline-flushes the partial tail; ring space is recycled."""
@@ -82,9 +82,11 @@ def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     from ccfd_demo_summit_amd.engine import StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
+    coalesce = int(exec_mode.split("-c")[1]) if "-c" in exec_mode else 1
+    exec_mode = exec_mode.split("-c")[0]
     wire = exec_mode.endswith("-wire")
-    eng = StreamEngine(DeviceModel(m, gpu, wire=wire), batch=1024, depth=4, streams=2, input_mode="zerocopy",
-                       exec_mode=exec_mode.replace("-wire", ""))
+    eng = StreamEngine(DeviceModel(m, gpu, wire=wire), batch=1024, depth=8, streams=2, input_mode="zerocopy",
+                       exec_mode=exec_mode.replace("-wire", ""), coalesce=coalesce)
     eng.set_ring(0, 4096)
     n = 10_000                                   # > capacity: exercises wrap + backpressure
     ids = np.arange(n, dtype=np.uint64) + 7
@@ -141,5 +143,62 @@ def test_persistent_engine_many_steps_counters_exact(gpu, setup):
     c, _ = red.snapshot()
     assert c[0] == total
     assert c[1] + c[2] == total
+    eng.close()
+    log.free()
+
+
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+def test_hot_swap_between_micro_batches(gpu, setup, exec_mode):
+    """Runtime X1: batches before the swap route with model A, batches after with model B."""
+    from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    X, mA = setup
+    mB = build_model("mlp", seed=77, X_ref=X[:20000], calibrate_rate=0.05)
+    eng = StreamEngine(DeviceModel(mA, gpu, wire=True), batch=4096, depth=4, streams=2, input_mode="zerocopy",
+                       exec_mode=exec_mode, coalesce=2)
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64), wire=True)
+    eng.add_log(0, log)
+    eng.pump(3)
+    eng.swap_model(DeviceModel(mB, gpu, wire=True))
+    eng.pump(3)
+    flagged = eng.drain_flagged()
+    got = np.zeros(6 * 4096, bool)
+    got[flagged["tx_id"].astype(np.int64)] = True
+    Xd = decode_wire(encode_wire(X[:6 * 4096]))
+    ref = np.concatenate([mA.predict_proba(Xd[:3 * 4096], emulate_bf16=True),
+                          mB.predict_proba(Xd[3 * 4096:], emulate_bf16=True)])
+    clear = np.abs(ref - 0.5) > 2e-3
+    np.testing.assert_array_equal(got[clear], (ref >= 0.5)[clear])
+    assert eng.model_version == 1
+    with pytest.raises(ValueError):
+        eng.swap_model(DeviceModel(mB, gpu, wire=False))
+    eng.close()
+    log.free()
+
+
+@pytest.mark.parametrize("wire", [False, True])
+def test_lr_coalesced_pump_matches_oracle(gpu, setup, wire):
+    from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    X, _ = setup
+    m = build_model("lr", seed=5, X_ref=X[:20000], calibrate_rate=0.02)
+    eng = StreamEngine(DeviceModel(m, gpu, wire=wire), batch=4096, depth=8, streams=2, input_mode="zerocopy",
+                       coalesce=4)
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64), wire=wire)
+    eng.add_log(0, log)
+    st = eng.pump(6)
+    assert st.rows == 6 * 4096
+    Xs = decode_wire(encode_wire(X[:6 * 4096])) if wire else X[:6 * 4096]
+    ref = m.predict_proba(Xs)
+    got = np.zeros(6 * 4096, bool)
+    got[eng.drain_flagged()["tx_id"].astype(np.int64)] = True
+    clear = np.abs(ref - 0.5) > 1e-4
+    np.testing.assert_array_equal(got[clear], (ref >= 0.5)[clear])
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    assert int(c[0]) == 6 * 4096
     eng.close()
     log.free()
