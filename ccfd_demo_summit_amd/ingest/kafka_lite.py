@@ -25,6 +25,41 @@ from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_NONE, ERR_OFFSET_OUT_O
 NODE_ID = 1
 
 
+class BrokerMetrics:
+    """The Strimzi/JMX-exporter series the reference's Kafka dashboard queries
+    (deploy/grafana/Kafka.json:119-1093): topic message/byte rates, failed requests,
+    partition/leader counts; under-replicated / offline partitions are 0 on one node."""
+
+    def __init__(self, server: "KafkaLiteServer"):
+        from prometheus_client import CollectorRegistry, Counter
+        from prometheus_client.core import GaugeMetricFamily
+        self.registry = CollectorRegistry()
+        lab = ["topic", "strimzi_io_kind"]
+        mk = lambda n, d: Counter(f"kafka_server_brokertopicmetrics_{n}", d, lab, registry=self.registry)
+        self.messages_in = mk("messagesin", "messages produced")
+        self.bytes_in = mk("bytesin", "bytes produced")
+        self.bytes_out = mk("bytesout", "bytes fetched")
+        self.failed_produce = mk("failedproducerequests", "failed produce requests")
+        self.failed_fetch = mk("failedfetchrequests", "failed fetch requests")
+        srv = server
+
+        class _Gauges:
+            def collect(self_):
+                parts = sum(srv.store.partitions(t) for t in srv.store.topics())
+                for name, v in (("kafka_server_replicamanager_partitioncount", parts),
+                                ("kafka_server_replicamanager_leadercount", parts),
+                                ("kafka_server_replicamanager_underreplicatedpartitions", 0),
+                                ("kafka_controller_kafkacontroller_offlinepartitionscount", 0)):
+                    g = GaugeMetricFamily(name, name, labels=["strimzi_io_kind"])
+                    g.add_metric(["Kafka"], v)
+                    yield g
+        self.registry.register(_Gauges())
+
+    def expose(self) -> bytes:
+        from prometheus_client import generate_latest
+        return generate_latest(self.registry)
+
+
 class KafkaLiteServer:
     def __init__(self, host: str = "127.0.0.1", port: int = 9092, default_partitions: int = 1,
                  store: Optional[InProcBroker] = None, auto_create: bool = True):
@@ -35,6 +70,7 @@ class KafkaLiteServer:
         self._server: Optional[asyncio.base_events.Server] = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._thread: Optional[threading.Thread] = None
+        self.metrics = BrokerMetrics(self)
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
@@ -150,8 +186,11 @@ class KafkaLiteServer:
                     for rec in recs:
                         self.store.produce(topic, rec.value, key=rec.key, partition=p)
                     pr.append((p, ERR_NONE, base))
+                    self.metrics.messages_in.labels(topic, "Kafka").inc(len(recs))
+                    self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
                 except Exception:
                     pr.append((p, 2, -1))
+                    self.metrics.failed_produce.labels(topic, "Kafka").inc()
             resp.append((topic, pr))
         w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
         return w.i32(0).build()
@@ -165,10 +204,12 @@ class KafkaLiteServer:
             for p, off, pmax in parts:
                 if topic not in self.store.topics() or p >= self.store.partitions(topic):
                     pr.append((p, ERR_UNKNOWN_TOPIC, -1, None))
+                    self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     continue
                 hw = self.store.end_offset(topic, p)
                 if off < self.store.begin_offset(topic, p) or off > hw:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))
+                    self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     continue
                 recs, size = [], 0
                 for rec in self.store.fetch(topic, p, off, 100_000):
@@ -178,6 +219,8 @@ class KafkaLiteServer:
                     recs.append(rec)
                 rb = encode_record_batch([x.value for x in recs], [x.key for x in recs], base_offset=off) if recs else b""
                 pr.append((p, ERR_NONE, hw, rb))
+                if rb:
+                    self.metrics.bytes_out.labels(topic, "Kafka").inc(len(rb))
             resp.append((topic, pr))
         w = Writer().i32(0)
         w.array(resp, lambda w_, t: w_.string(t[0]).array(
@@ -233,11 +276,20 @@ def main(argv=None):
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=9092)
     ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--metrics-port", type=int, default=9404, help="Prometheus /metrics (0 = off)")
     a = ap.parse_args(argv)
     srv = KafkaLiteServer(a.host, a.port, a.partitions)
 
     async def run():
         await srv.start()
+        if a.metrics_port:
+            from aiohttp import web
+            app = web.Application()
+            app.router.add_get("/metrics", lambda _r: web.Response(
+                body=srv.metrics.expose(), headers={"Content-Type": "text/plain; version=0.0.4"}))
+            runner = web.AppRunner(app)
+            await runner.setup()
+            await web.TCPSite(runner, a.host, a.metrics_port).start()
         print(f"[kafka-lite] listening on {a.host}:{srv.port}", flush=True)
         await asyncio.Event().wait()
     asyncio.run(run())

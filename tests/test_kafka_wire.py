@@ -71,6 +71,11 @@ def test_client_against_kafka_lite(lite):
     back = TxBatch.decode(kb.fetch("bin", 0, 0)[0].value)
     np.testing.assert_array_equal(back.features, X)
     kb.close()
+    # broker series of the reference's Kafka dashboard (deploy/grafana/Kafka.json)
+    text = lite.metrics.expose().decode()
+    assert 'kafka_server_brokertopicmetrics_messagesin_total{strimzi_io_kind="Kafka",topic="odh-demo"} 31.0' in text
+    assert "kafka_server_brokertopicmetrics_bytesout_total" in text
+    assert 'kafka_server_replicamanager_partitioncount{strimzi_io_kind="Kafka"}' in text
 
 
 def test_pipeline_over_kafka_protocol(lite):
