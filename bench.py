@@ -243,6 +243,10 @@ def main(argv=None):
                               (("submit", st_final.host_submit_s), ("wait", st_final.host_wait_s),
                                ("complete", st_final.host_complete_s))},
         "step_us_per_batch": round(elapsed * 1e6 / (args.steps * args.batches_per_step), 3),
+        # K7: per-micro-batch execution window on the GPU's own clock (rank 0)
+        "device_exec_us_mean": round(st_final.dev_exec_mean_us, 2),
+        "device_exec_us_p50": round(hist_quantile(st_final.dev_hist.astype(np.int64), 0.5) / 1e3, 2)
+        if st_final.dev_batches else None,
         "rows_scored": total_rows,
         "rows_expected": expected,
         "fraud_routed": int(counters[1]) - fraud0,

@@ -109,13 +109,18 @@ class StepStats:
     host_submit_s: float = 0.0
     host_wait_s: float = 0.0
     host_complete_s: float = 0.0
+    dev_batches: int = 0                 # K7: device-clock execution time per micro-batch
+    dev_exec_mean_us: float = 0.0
+    dev_hist: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
 
 
 def _stats(st: EngineStats) -> StepStats:
     return StepStats(st.batches, st.rows, st.fraud_rows, st.flagged_dropped, st.wall_s,
                      st.lat_p50_us, st.lat_p99_us, st.lat_max_us, st.lat_mean_us,
                      np.ctypeslib.as_array(st.lat_hist).copy(), st.host_submit_ns * 1e-9,
-                     st.host_wait_ns * 1e-9, st.host_complete_ns * 1e-9)
+                     st.host_wait_ns * 1e-9, st.host_complete_ns * 1e-9, int(st.dev_batches),
+                     (st.dev_exec_ns / st.dev_batches * 1e-3) if st.dev_batches else 0.0,
+                     np.ctypeslib.as_array(st.dev_hist).copy())
 
 
 class StreamEngine:

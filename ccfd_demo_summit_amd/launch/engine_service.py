@@ -74,6 +74,7 @@ class EngineService:
         self._stop = threading.Event()
         self._ingest_err: Optional[BaseException] = None
         self.rows_scored = 0
+        self.kernel_exec_mean_us = 0.0
         self.last_reduce = time.monotonic()
         self._lat_prev = np.zeros(256, np.int64)
 
@@ -137,6 +138,8 @@ class EngineService:
         if st.rows or len(flagged):
             self.router.on_flagged(flagged, int(st.rows))
         self.rows_scored += int(st.rows)
+        if st.dev_batches:
+            self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
         self._commit_done()
         now = time.monotonic()
         if (now - self.last_reduce) * 1e3 >= self.cfg.reduce_period_ms:
@@ -164,7 +167,9 @@ class EngineService:
 
     def metrics_source(self):
         c, lat = self.reducer.snapshot()
-        return c, lat, {"rows_scored_local": self.rows_scored}
+        return c, lat, {"rows_scored_local": self.rows_scored,
+                        "kernel_exec_mean_us": self.kernel_exec_mean_us,
+                        "model_version": self.hotswap.version}
 
 
 class _StaticInProcConsumer:

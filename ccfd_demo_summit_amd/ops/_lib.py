@@ -49,7 +49,8 @@ class EngineStats(C.Structure):
                 ("flagged_dropped", C.c_uint64), ("wall_s", C.c_double), ("lat_p50_us", C.c_double),
                 ("lat_p99_us", C.c_double), ("lat_max_us", C.c_double), ("lat_mean_us", C.c_double),
                 ("lat_hist", C.c_uint64 * 256), ("host_submit_ns", C.c_uint64), ("host_wait_ns", C.c_uint64),
-                ("host_complete_ns", C.c_uint64)]
+                ("host_complete_ns", C.c_uint64), ("dev_batches", C.c_uint64), ("dev_exec_ns", C.c_uint64),
+                ("dev_hist", C.c_uint64 * 256)]
 
 
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),

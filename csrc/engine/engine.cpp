@@ -137,6 +137,8 @@ class Engine {
   std::vector<float> lat_us;
   uint64_t lat_hist[256] = {};
   uint64_t t_submit_ns = 0, t_wait_ns = 0, t_complete_ns = 0;
+  uint64_t dev_batches = 0, dev_exec_ns = 0, dev_hist[256] = {};
+  double wall_ns_per_tick = 0.0;   // device wall clock (s_memrealtime) period
   unsigned long long done_counter = 0;
 
   int init(const ccfd_engine_config& c) {
@@ -150,6 +152,11 @@ class Engine {
     rowf = cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 : CCFD_N_FEATURES;
     amount_f = cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 - 1 : CCFD_N_FEATURES - 1;
     HIPCHK(hipSetDevice(cfg.device));
+    {
+      int khz = 0;
+      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg.device) == hipSuccess && khz > 0)
+        wall_ns_per_tick = 1e6 / (double)khz;
+    }
     streams.resize(cfg.n_streams);
     flip_ev.resize(cfg.n_streams);
     for (int i = 0; i < cfg.n_streams; ++i) {
@@ -179,8 +186,8 @@ class Engine {
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_proba_dev), s.h_proba, 0));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_route_dev), s.h_route, 0));
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
-      HIPCHK(hipMalloc(reinterpret_cast<void**>(&s.d_ctl), 2 * sizeof(unsigned int)));
-      HIPCHK(hipMemsetAsync(s.d_ctl, 0, 2 * sizeof(unsigned int), streams[0]));
+      HIPCHK(hipMalloc(reinterpret_cast<void**>(&s.d_ctl), 4 * sizeof(unsigned int)));
+      HIPCHK(hipMemsetAsync(s.d_ctl, 0, 4 * sizeof(unsigned int), streams[0]));
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.h_flag), B * sizeof(unsigned int), out_flags));
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.h_flag_dev), s.h_flag, 0));
       void* hd = nullptr;
@@ -438,6 +445,15 @@ class Engine {
     if (s.use_flag) {
       nf = s.done_ptr[1];
       if (nf) push_flagged_idx(s, nf);
+      if (!persistent) {                               // K7: device-clock execution window
+        const uint64_t t0d = s.done_ptr[2], t1d = s.done_ptr[3];
+        if (t1d > t0d && wall_ns_per_tick > 0) {
+          const double dns = (double)(t1d - t0d) * wall_ns_per_tick;
+          dev_exec_ns += (uint64_t)dns;
+          ++dev_batches;
+          dev_hist[std::min(255, (int)std::floor(4.0 * std::log2(std::max(1.0, dns))))]++;
+        }
+      }
     } else {
       for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
       if (nf) push_flagged(s);
@@ -612,6 +628,9 @@ class Engine {
     st->host_submit_ns = t_submit_ns;
     st->host_wait_ns = t_wait_ns;
     st->host_complete_ns = t_complete_ns;
+    st->dev_batches = dev_batches;
+    st->dev_exec_ns = dev_exec_ns;
+    std::memcpy(st->dev_hist, dev_hist, sizeof(dev_hist));
     if (lat_us.empty()) return;
     std::vector<float> v = lat_us;
     auto pct = [&](double q) {
@@ -874,6 +893,8 @@ void ccfd_engine_reset_stats(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   std::memset(e->lat_hist, 0, sizeof(e->lat_hist));
   e->t_submit_ns = e->t_wait_ns = e->t_complete_ns = 0;
+  e->dev_batches = e->dev_exec_ns = 0;
+  std::memset(e->dev_hist, 0, sizeof(e->dev_hist));
   e->lat_us.clear();
 }
 

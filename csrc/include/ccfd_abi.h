@@ -57,9 +57,9 @@ typedef struct ccfd_score_args {
   //   the LAST workgroup resets slot_ctl, stores done_rec[1] = #flagged and then
   //   done_rec[0] = done_seq (system-scope release) -> the host polls done_rec[0] in pinned
   //   memory instead of recording/synchronising a HIP event per micro-batch.
-  unsigned int* slot_ctl;        // device [2], zero-initialised once
+  unsigned int* slot_ctl;        // device [4]: ticket, #flagged, u64 start timestamp (K7)
   unsigned int* flag_idx;        // host-mapped [n] row indices of fraud-routed rows
-  unsigned long long* done_rec;  // host-mapped coherent [2]
+  unsigned long long* done_rec;  // host-mapped coherent [4]: seq, #flagged, t_start, t_end
   unsigned long long done_seq;
 } ccfd_score_args;
 
@@ -189,6 +189,11 @@ typedef struct ccfd_engine_stats {
   uint64_t host_submit_ns;     // H2D enqueue + kernel launch + event record
   uint64_t host_wait_ns;       // blocked in hipEventSynchronize (GPU not done yet)
   uint64_t host_complete_ns;   // route scan + flagged hand-off + bookkeeping
+  // K7 stream_stats: per-micro-batch device execution time measured on the GPU's constant
+  // wall clock (s_memrealtime, first workgroup start -> last workgroup completion)
+  uint64_t dev_batches;
+  uint64_t dev_exec_ns;        // sum
+  uint64_t dev_hist[256];      // same bucketing as lat_hist
 } ccfd_engine_stats;
 
 void* ccfd_engine_create(const ccfd_engine_config* cfg);

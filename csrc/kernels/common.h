@@ -99,6 +99,12 @@ __device__ __forceinline__ void signal_done(const ccfd_score_args& a, unsigned n
     }
     const unsigned ticket = __hip_atomic_fetch_add(&a.slot_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ticket == nblk - 1) {
+      // K7: device-clock execution window of this micro-batch
+      const unsigned long long t_end = wall_clock64();
+      const unsigned long long t_start = __hip_atomic_load(
+          reinterpret_cast<unsigned long long*>(a.slot_ctl + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.done_rec[2], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.done_rec[3], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const unsigned nflag = __hip_atomic_load(&a.slot_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.slot_ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.slot_ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -106,6 +112,13 @@ __device__ __forceinline__ void signal_done(const ccfd_score_args& a, unsigned n
       __hip_atomic_store(&a.done_rec[0], a.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+}
+
+// K7: workgroup 0 of a micro-batch stamps its start on the device wall clock.
+__device__ __forceinline__ void stamp_start(const ccfd_score_args& a, int blk) {
+  if (a.slot_ctl != nullptr && blk == 0 && threadIdx.x == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.slot_ctl + 2), wall_clock64(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Wave-level reduction of a u64 over the 64 lanes.

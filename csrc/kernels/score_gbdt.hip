@@ -32,6 +32,7 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a) {
   const int row0 = blockIdx.x * kGbRows;
   const int nrows = min(kGbRows, a.n - row0);
   epi_init(epi);
+  stamp_start(a, blockIdx.x);
 
   // ---- stage rows feature-major
   if constexpr (kContig) {

@@ -23,6 +23,7 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
+  stamp_start(a, blk);
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
   const int tstride = nblk * kLrWaves;
   int tile = blk * kLrWaves + wave;
