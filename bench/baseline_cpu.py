@@ -33,11 +33,12 @@ import sys
 sys.path.insert(0, {root!r})
 from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
 from ccfd_demo_summit_amd.models import build_model
-from ccfd_demo_summit_amd.serving.scorers import CpuScorer
+from ccfd_demo_summit_amd.serving.scorers import CpuScorer, GpuScorer
 from ccfd_demo_summit_amd.serving.seldon_server import SeldonServer, run
 X, _ = generate(50_000, seed=7)
-m = build_model("lr", seed=0, X_ref=X, calibrate_rate=FRAUD_RATE)
-run(SeldonServer(CpuScorer(m), max_batch=1, max_delay_us=0), host="127.0.0.1", port={port})
+m = build_model({model!r}, seed=0, X_ref=X, calibrate_rate=FRAUD_RATE)
+scorer = GpuScorer(m, max_batch={max_batch}) if {gpu} else CpuScorer(m)
+run(SeldonServer(scorer, max_batch={max_batch}, max_delay_us={delay}), host="127.0.0.1", port={port})
 """
 
 
@@ -54,6 +55,12 @@ def main(argv=None):
     ap.add_argument("--seconds", type=float, default=15.0)
     ap.add_argument("--pool", type=int, default=5, help="SELDON_POOL_SIZE (reference default 5)")
     ap.add_argument("--write", action="store_true", help="write bench/baseline_measured.json")
+    ap.add_argument("--scorer", default="cpu", choices=["cpu", "gpu"],
+                    help="gpu: the same REST server with the fused HIP kernel + dynamic micro-batching")
+    ap.add_argument("--model", default="lr", choices=["lr", "mlp"])
+    ap.add_argument("--max-batch", type=int, default=1, help="server micro-batch cap (1 = reference batch=1)")
+    ap.add_argument("--max-delay-us", type=int, default=0)
+    ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
 
     import requests
@@ -61,11 +68,15 @@ def main(argv=None):
     from ccfd_demo_summit_amd.data import generate
 
     port = _free_port()
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    srv = subprocess.Popen([sys.executable, "-c", SERVER.format(root=str(ROOT), port=port)], env=env)
+    env = dict(os.environ)
+    if args.scorer == "cpu":
+        env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    code = SERVER.format(root=str(ROOT), port=port, model=args.model, gpu=args.scorer == "gpu",
+                         max_batch=args.max_batch, delay=args.max_delay_us)
+    srv = subprocess.Popen([sys.executable, "-c", code], env=env)
     url = f"http://127.0.0.1:{port}/api/v0.1/predictions"
     try:
-        for _ in range(600):
+        for _ in range(1800):
             try:
                 if requests.get(f"http://127.0.0.1:{port}/health/ping", timeout=0.5).ok:
                     break
@@ -101,15 +112,20 @@ def main(argv=None):
         wall = asyncio.run(drive())
         all_lat = np.concatenate([np.asarray(v) for v in lat]) * 1e6
         n = all_lat.size
-        rec = {"cpu_lr_batch1_seldon_rest_tx_per_s": round(n / wall, 1),
+        key = ("cpu_lr_batch1_seldon_rest_tx_per_s" if args.scorer == "cpu" and args.model == "lr"
+               and args.max_batch == 1 else f"{args.scorer}_{args.model}_seldon_rest_tx_per_s")
+        rec = {key: round(n / wall, 1),
                "p50_us": round(float(np.percentile(all_lat, 50)), 1),
                "p99_us": round(float(np.percentile(all_lat, 99)), 1),
                "requests": int(n), "seconds": args.seconds, "pool": args.pool, "wall_s": round(wall, 2),
-               "model": "logistic regression, 30 features", "server": "aiohttp Seldon v0.1, batch=1", "client": "aiohttp, pool concurrent requests",
+               "model": args.model, "scorer": args.scorer, "max_batch": args.max_batch,
+               "server": "aiohttp Seldon v0.1", "client": "aiohttp, pool concurrent batch-1 requests",
                "host_cpus": os.cpu_count(), "label": "measured by us (reference-topology equivalent)"}
         print(json.dumps(rec))
         if args.write:
             (ROOT / "bench" / "baseline_measured.json").write_text(json.dumps(rec, indent=1) + "\n")
+        if args.out:
+            Path(args.out).write_text(json.dumps(rec) + "\n")
         return rec
     finally:
         srv.terminate()
