@@ -1,0 +1,199 @@
+"""End-to-end streaming benchmark: Kafka ingest -> GPU scoring ->
+router -> fraud business process -> customer notification -> response -> process signal,
+with the Prometheus counters checked against the scored volume.
+
+Per rank (one per MI355X under torchrun, partitions p % W == rank):
+
+  producer thread --TXB1 4096-row batches--> broker (in-process, or kafka-lite speaking the
+  Kafka wire protocol over 127.0.0.1) --> EngineService (ingest thread -> pinned ring ->
+  coalesced fused-kernel launches -> flagged rows) --> Router --> ProcessEngine (in-process
+  KIE: fraud BP, notification publish, timers, DMN) --> notification service --> response
+  topic --> Router.on_response --> process signal.
+
+The producer runs open-loop at ``--rate`` tx/s per rank (0 = as fast as the pipeline
+absorbs, with back-pressure on consumer lag so retention never drops unconsumed data).
+Reported: sustained scored tx/s (whole job), ring-arrival -> scored latency p50/p99,
+fraud processes started, notifications/responses, and whether the Prometheus
+``transaction_incoming_total`` equals the rows scored.
+
+    python bench/e2e.py --seconds 20 --broker kafka-lite
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/e2e.py --seconds 20
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import threading
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=20.0)
+    ap.add_argument("--warmup", type=float, default=3.0)
+    ap.add_argument("--broker", default="inproc", choices=["inproc", "kafka-lite"])
+    ap.add_argument("--rate", type=float, default=0.0, help="tx/s per rank (0 = max)")
+    ap.add_argument("--batch", type=int, default=4096, help="rows per TXB1 message / micro-batch")
+    ap.add_argument("--partitions-per-rank", type=int, default=4)
+    ap.add_argument("--max-lag-msgs", type=int, default=64, help="producer back-pressure (messages)")
+    ap.add_argument("--model", default="mlp", choices=["mlp", "lr"])
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args(argv)
+
+    import torch
+    from ccfd_demo_summit_amd.config import load_config
+    from ccfd_demo_summit_amd.contracts import TxBatch
+    from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
+    from ccfd_demo_summit_amd.ingest.broker import InProcBroker
+    from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
+    from ccfd_demo_summit_amd.metrics.exporter import MetricsHub
+    from ccfd_demo_summit_amd.models import build_model
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import all_max, all_sum, barrier, hist_quantile, init_distributed
+    from ccfd_demo_summit_amd.process import NotificationService, PredictionService, ProcessEngine
+    from ccfd_demo_summit_amd.process.notifier import encode_notification
+    from ccfd_demo_summit_amd.router.router import Router
+    from ccfd_demo_summit_amd.router.rules import RuleSet
+
+    ctx = init_distributed()
+    dev = ctx.device
+    cfg = load_config(None)
+    k = cfg.kafka
+    P = args.partitions_per_rank
+    store = InProcBroker(default_partitions=P, retention=4 * args.max_lag_msgs)
+    server = None
+    if args.broker == "kafka-lite":
+        from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+        from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+        server = KafkaLiteServer("127.0.0.1", 0, default_partitions=P, store=store).start_in_thread()
+        broker = KafkaBroker(server.bootstrap)
+        prod_broker = KafkaBroker(server.bootstrap)
+    else:
+        broker = prod_broker = store
+    for t in (k.transactions_topic, k.notification_topic, k.response_topic):
+        store.create_topic(t, P)
+
+    # model (same random-init + calibration as bench.py), W64 rows
+    Xcal, _ = generate(200_000, seed=999)
+    model = build_model(args.model, seed=0, X_ref=Xcal, calibrate_rate=FRAUD_RATE)
+    dm = DeviceModel(model, dev, wire=True)
+
+    hub = MetricsHub()
+    processes = ProcessEngine(cfg.kie.notification_timeout_s, cfg.kie.dmn_probability_threshold,
+                              cfg.kie.dmn_amount_threshold, kie_metrics=hub.kie,
+                              prediction=PredictionService(cfg.kie.confidence_threshold),
+                              publish_notification=lambda msg: (store.produce(
+                                  k.notification_topic, encode_notification(msg), key=str(msg.get("customer_id")).encode()),
+                                  router.on_notification_sent(msg)))
+    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), processes, hub.router)
+    notifier = NotificationService(lambda raw, key: store.produce(k.response_topic, raw, key=key),
+                                   cfg.notifier.p_reply, cfg.notifier.p_approve, 0.05, 7)
+    svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
+        topic=k.transactions_topic, group_id=k.group_id, batch=args.batch, depth=32, streams=4,
+        ring_rows=1 << 20, flush_us=500, run_budget_us=2000, reduce_period_ms=10.0,
+        threshold=cfg.router.fraud_threshold, coalesce=8, max_fetch=64), partitions=list(range(P)))
+    notif_c = store.consumer("notification-service", [k.notification_topic])
+    resp_c = store.consumer(k.group_id + "-responses", [k.response_topic])
+
+    # producer: pre-encoded TXB1 messages, ids patched per message (unique transaction ids)
+    pool = []
+    for i in range(8):
+        X, _ = generate(args.batch, seed=1000 * ctx.rank + i)
+        b = TxBatch(ids=np.zeros(args.batch, np.uint64),
+                    customer=np.random.default_rng(i).integers(0, 1_000_000, args.batch, dtype=np.uint32),
+                    features=X)
+        pool.append(bytearray(b.encode()))
+    stop = threading.Event()
+    produced = [0]
+    id_base = np.uint64(ctx.rank) << np.uint64(48)
+
+    def producer():
+        seq = 0
+        t0 = time.perf_counter()
+        while not stop.is_set():
+            if args.rate > 0 and produced[0] > args.rate * (time.perf_counter() - t0):
+                time.sleep(0.0002)
+                continue
+            if store.lag(k.group_id, k.transactions_topic) > args.max_lag_msgs:
+                time.sleep(0.0002)
+                continue
+            msg = pool[seq % len(pool)]
+            ids = np.frombuffer(msg, np.uint64, args.batch, 32)
+            ids[:] = id_base + np.uint64(seq * args.batch) + np.arange(args.batch, dtype=np.uint64)
+            prod_broker.produce(k.transactions_topic, bytes(msg), partition=seq % P)
+            produced[0] += args.batch
+            seq += 1
+
+    th = threading.Thread(target=producer, daemon=True, name="producer")
+    svc.start()
+    th.start()
+
+    def loop_until(t_end):
+        while time.perf_counter() < t_end:
+            svc.step()
+            for r in notif_c.poll(max_records=10_000):
+                notifier.handle(r.value)
+            notif_c.commit()
+            notifier.tick()
+            for r in resp_c.poll(max_records=10_000):
+                router.on_response(r.value)
+            resp_c.commit()
+            processes.tick()
+
+    loop_until(time.perf_counter() + args.warmup)
+    svc.engine.reset_stats()
+    rows0 = svc.rows_scored
+    fr0 = router.fraud_started
+    barrier(ctx)
+    t0 = time.perf_counter()
+    loop_until(t0 + args.seconds)
+    elapsed = time.perf_counter() - t0
+    rows = svc.rows_scored - rows0
+    stop.set()
+    th.join(5)
+    st = svc.engine.run(0, 0)                       # cumulative stats since reset
+    lat = st.lat_hist.astype(np.int64)
+    tot = all_sum(ctx, float(rows))
+    el = all_max(ctx, elapsed)
+    text = hub.router.expose().decode() if hasattr(hub.router, "expose") else ""
+    prom = {}
+    for line in text.splitlines():
+        for name in ("transaction_incoming_total", "notifications_outgoing_total"):
+            if line.startswith(name + " "):
+                prom[name] = float(line.split()[-1])
+    incoming = prom.get("transaction_incoming_total")
+    out = {
+        "metric": "end-to-end tx/s (Kafka ingest -> GPU score -> route -> BP -> notify)",
+        "value": round(tot / el, 1), "unit": "tx/s", "n_gpus": ctx.world, "seconds": round(el, 2),
+        "broker": args.broker, "rate_per_rank": args.rate, "micro_batch": args.batch, "model": args.model,
+        "ring_arrival_to_scored_p50_us": round(hist_quantile(lat, 0.5) / 1e3, 1),
+        "ring_arrival_to_scored_p99_us": round(hist_quantile(lat, 0.99) / 1e3, 1),
+        "fraud_processes_started_rank0": router.fraud_started - fr0,
+        "notifications_rank0": prom.get("notifications_outgoing_total"),
+        "responses_signalled_rank0": router.signals_ok,
+        "prometheus_transaction_incoming_total_rank0": incoming,
+        "rows_scored_rank0_total": svc.rows_scored,
+        "producer_lag_msgs_rank0": store.lag(k.group_id, k.transactions_topic),
+    }
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+        if args.out:
+            Path(args.out).write_text(json.dumps(out) + "\n")
+    svc.stop()
+    if server is not None:
+        server.stop()
+    if ctx.initialized:
+        import torch.distributed as dist
+        barrier(ctx)
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
