@@ -62,7 +62,11 @@ WIRE_AMOUNT_F32 = 15                      # Amount as the 16th f32 word of a W64
 
 def _bf16_bits(x: np.ndarray) -> np.ndarray:
     u = np.ascontiguousarray(x, np.float32).view(np.uint32)
-    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000                      # keep NaN a (quiet) NaN
+    if nan.any():
+        r[nan] = ((u[nan] >> 16) | 0x0040).astype(np.uint16)
+    return r
 
 
 def encode_wire(X: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:

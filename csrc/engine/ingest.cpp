@@ -155,6 +155,7 @@ namespace {
 inline uint16_t bf16_rne(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((u >> 16) | 0x0040u);   // NaN stays a (quiet) NaN
   u += 0x7FFFu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }

@@ -35,9 +35,12 @@ def test_native_encoder_bit_exact(L):
     X, _ = generate(1000, seed=2)
     X[0, 3] = np.float32(1.0 + 2 ** -8)          # exact tie -> round to even
     X[1, 4] = -0.0
+    X[2, 5] = np.nan
+    X[3, 6] = np.float32(np.inf)
     out = np.zeros((1000, 64), np.uint8)
     assert L.ccfd_encode_w64(X.ctypes.data, 1000, 30, out.ctypes.data) == 1000
     np.testing.assert_array_equal(out, encode_wire(X))
+    assert np.isnan(decode_wire(out)[2, 5]) and np.isinf(decode_wire(out)[3, 6])
 
 
 def test_native_json_to_w64(L):
