@@ -15,7 +15,9 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the dlopen, see module doc)
 
 _NATIVE = Path(__file__).resolve().parents[1] / "_native"
-LIB_PATH = _NATIVE / "libccfd_hip.so"
+# CCFD_SANITIZE=<san>: load the host-sanitizer build (ops/build.py) instead
+_SAN = os.environ.get("CCFD_SANITIZE", "")
+LIB_PATH = _NATIVE / (f"libccfd_hip_{_SAN.replace(',', '_')}.so" if _SAN else "libccfd_hip.so")
 
 MODEL_LR, MODEL_MLP, MODEL_GBDT = 0, 1, 2
 MODEL_IDS = {"lr": MODEL_LR, "mlp": MODEL_MLP, "gbdt": MODEL_GBDT}

@@ -23,6 +23,21 @@ OBJ = ROOT / "build" / "obj"
 NATIVE = Path(__file__).resolve().parents[1] / "_native"
 LIB = NATIVE / "libccfd_hip.so"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+# Host-code sanitizer build: CCFD_SANITIZE=address|undefined|address,undefined
+# instruments the host runtime (csrc/engine/*.cpp) -- never device code -- and links
+# libccfd_hip_<san>.so next to the normal library; load it with the clang runtime preloaded
+# (tests/test_native_cpu.py::test_host_runtime_under_asan).
+SANITIZE = os.environ.get("CCFD_SANITIZE", "")
+
+
+def lib_path(sanitize: str = SANITIZE) -> Path:
+    return LIB if not sanitize else NATIVE / f"libccfd_hip_{sanitize.replace(',', '_')}.so"
+
+
+def asan_runtime() -> str:
+    out = subprocess.run([str(Path(hipcc()).parent.parent / "lib/llvm/bin/clang"), "-print-file-name=libclang_rt.asan-x86_64.so"],
+                         capture_output=True, text=True).stdout.strip()
+    return out
 
 
 def hipcc() -> str:
@@ -41,33 +56,37 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path, force: bool) -> Path:
-    obj = OBJ / (src.parent.name + "_" + src.stem + ".o")
+def _compile(src: Path, force: bool, sanitize: str = "") -> Path:
+    tag = "" if not sanitize or src.suffix != ".cpp" else "_" + sanitize.replace(",", "_")
+    obj = OBJ / (src.parent.name + "_" + src.stem + tag + ".o")
     if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
         return obj
     cmd = [hipcc(), "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall",
            "-Wno-unused-result", "-I", str(CSRC / "include"), "-c", str(src), "-o", str(obj)]
     if src.suffix == ".cpp":
         # host-only translation units: no device code object
-        cmd = [hipcc(), "-O3", "-fPIC", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__",
+        cmd = [hipcc(), "-O1" if sanitize else "-O3", "-fPIC", "-std=c++17", "-Wall",
                "-I", str(CSRC / "include"), "-c", str(src), "-o", str(obj)]
+        if sanitize:
+            cmd[1:1] = [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", "-g"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
+def build(force: bool = False, jobs: int = 4, verbose: bool = True, sanitize: str = SANITIZE) -> Path:
     OBJ.mkdir(parents=True, exist_ok=True)
     NATIVE.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, force, sanitize), srcs))
     newest = max(o.stat().st_mtime for o in objs)
+    LIB = lib_path(sanitize)
     if force or not LIB.exists() or LIB.stat().st_mtime < newest:
         tmp = LIB.with_suffix(".so.tmp")
         cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + \
-              [str(o) for o in objs] + ["-lpthread"]
+              [str(o) for o in objs] + ["-lpthread"] + ([f"-fsanitize={sanitize}", "-shared-libsan"] if sanitize else [])
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -171,6 +171,9 @@ class Engine {
     // restores non-coherent outputs + per-workgroup release (A/B switch).
     if (const char* e = std::getenv("CCFD_COHERENT_OUT")) coherent_out = std::atoi(e) != 0;
     if (const char* e = std::getenv("CCFD_ABLATE")) ablate = std::atoi(e) & 0x70;   // diagnostics only
+    // HIP_LAUNCH_BLOCKING-style debug mode: synchronise after every launch so a kernel fault
+    // is reported against the micro-batch that caused it (SURVEY.md §5 race detection)
+    if (const char* e = std::getenv("CCFD_DEBUG_SYNC")) debug_sync = std::atoi(e) != 0;
     const unsigned out_flags = hipHostMallocMapped | hipHostMallocPortable |
                                (coherent_out ? hipHostMallocCoherent : 0u);
     for (auto& s : slots) {
@@ -210,6 +213,7 @@ class Engine {
   int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, or 16 for W64 wire rows
   int amount_f = CCFD_N_FEATURES - 1;
   int ablate = 0;
+  bool debug_sync = false;
   ccfd_persist_ctl* pctl = nullptr;       // host (coherent pinned)
   ccfd_persist_desc* pdesc = nullptr;      // host (coherent pinned)
   ccfd_persist_dev* pdev = nullptr;        // device
@@ -525,6 +529,7 @@ class Engine {
     if (cfg.wire) a.flags |= CCFD_ARG_WIRE_W64;
     int rc = ccfd_score_launch(&a, stream);
     if (rc) return rc;
+    if (debug_sync) HIPCHK(hipStreamSynchronize(stream));   // CCFD_DEBUG_SYNC: fault -> this batch
     if (cfg.output_mode == 1) {
       HIPCHK(hipMemcpyAsync(s.h_proba, s.d_proba, (size_t)rows * sizeof(float), hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(s.h_route, s.d_route, (size_t)rows, hipMemcpyDeviceToHost, stream));
@@ -569,7 +574,10 @@ class Engine {
       s.busy = true;
       m.sub[k] = ccfd_sub_batch{s.h_proba_dev, s.h_route_dev, s.d_ctl, s.h_flag_dev, s.h_done_dev, s.expect};
     }
-    return ccfd_score_launch_multi(&m, streams[(launches++) % streams.size()]);
+    hipStream_t stream = streams[(launches++) % streams.size()];
+    const int rc = ccfd_score_launch_multi(&m, stream);
+    if (rc == 0 && debug_sync) HIPCHK(hipStreamSynchronize(stream));
+    return rc;
   }
 
   int pump(int64_t n_batches, int32_t batch_rows, bool drain, ccfd_engine_stats* st) {

@@ -2,6 +2,7 @@
 import ctypes as C
 import json
 import subprocess
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -81,3 +82,48 @@ def test_json_parser_features_array_and_errors(L):
     assert rc == -2
     rc, *_ = _parse(L, [json.dumps({"features": [1, 2, 3]})])
     assert rc == -1
+
+
+def test_host_runtime_under_asan(tmp_path):
+    """Host-sanitizer build of the native runtime: the JSON parser (valid,
+    truncated, garbage), W64 encoder and CRC-32C run under clang ASan+UBSan in a child
+    process with the runtime preloaded; any report fails the test."""
+    import os
+    import sys
+    from ccfd_demo_summit_amd.ops.build import asan_runtime, build
+    try:
+        build(sanitize="address,undefined", verbose=False)
+        rt = asan_runtime()
+    except Exception as e:                                   # toolchain without sanitizer runtimes
+        pytest.skip(f"sanitizer build unavailable: {e}")
+    if not rt or not os.path.exists(rt):
+        pytest.skip("clang ASan runtime not found")
+    script = tmp_path / "asan_probe.py"
+    script.write_text(
+        "import json, numpy as np\n"
+        "from ccfd_demo_summit_amd.ops._lib import lib\n"
+        "from ccfd_demo_summit_amd.contracts import FEATURE_NAMES\n"
+        "L = lib()\n"
+        "assert 'address' in L._name, L._name\n"
+        "rng = np.random.default_rng(0)\n"
+        "msgs = [json.dumps({'id': i, **{n: float(v) for n, v in zip(FEATURE_NAMES, rng.standard_normal(30))}}).encode()"
+        " for i in range(200)]\n"
+        "msgs += [b'{\"id\": 1, \"Time\": 1e', b'', b'\\xff\\xfe{', b'{\"features\": [1,2,3,' + b'9,' * 4000 + b'1]}']\n"
+        "for k in range(len(msgs)):\n"
+        "    sub = msgs[k:k + 1]\n"
+        "    buf = b''.join(sub); off = np.array([0, len(buf)], np.int64)\n"
+        "    f = np.zeros((1, 30), np.float32); ids = np.zeros(1, np.uint64); cu = np.zeros(1, np.uint32)\n"
+        "    rows = np.zeros((1, 64), np.uint8)\n"
+        "    L.ccfd_parse_json_batch(buf, off.ctypes.data, 1, f.ctypes.data, ids.ctypes.data, cu.ctypes.data)\n"
+        "    L.ccfd_parse_json_batch_w64(buf, off.ctypes.data, 1, rows.ctypes.data, ids.ctypes.data, cu.ctypes.data)\n"
+        "X = rng.standard_normal((1000, 30)).astype(np.float32)\n"
+        "out = np.zeros((1000, 64), np.uint8)\n"
+        "assert L.ccfd_encode_w64(X.ctypes.data, 1000, 30, out.ctypes.data) == 1000\n"
+        "assert L.ccfd_crc32c(bytes(range(256)) * 100, 25600, 0) != 0\n"
+        "print('asan probe ok')\n")
+    env = dict(os.environ, CCFD_SANITIZE="address,undefined", LD_PRELOAD=rt, CCFD_NO_AUTOBUILD="1",
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               PYTHONPATH=str(Path(__file__).resolve().parents[1]), HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "asan probe ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
