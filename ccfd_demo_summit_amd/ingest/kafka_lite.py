@@ -92,10 +92,15 @@ class KafkaLiteServer:
 
     def stop(self):
         if self._loop is not None:
-            def _close():
+            async def _shutdown():
                 self._server.close()
+                me = asyncio.current_task()
+                tasks = [t for t in asyncio.all_tasks() if t is not me]
+                for t in tasks:                      # open connection handlers
+                    t.cancel()
+                await asyncio.gather(*tasks, return_exceptions=True)
                 self._loop.stop()
-            self._loop.call_soon_threadsafe(_close)
+            asyncio.run_coroutine_threadsafe(_shutdown(), self._loop)
             self._thread.join(5)
 
     @property

@@ -76,3 +76,77 @@ def test_kill_rank_mid_stream_exact_counts():
     assert broker.lag("ccfd-engine", "odh-demo") == 0
     owned = sorted(p for w in workers if w.alive for p in w.leases.owned())
     assert owned == list(range(6))
+
+
+def _elastic_proc(rank, world, store_port, bootstrap, model_seed):
+    import datetime
+    import time as _t
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    store = dist.TCPStore("127.0.0.1", store_port, world + 1, False, timeout=datetime.timedelta(seconds=60))
+    X, _ = generate(8000, seed=2)
+    model = build_model("mlp", seed=model_seed, X_ref=X, calibrate_rate=0.02)
+    broker = KafkaBroker(bootstrap)
+    router = Router(RuleSet.threshold(0.5), ProcessEngine(notification_timeout_s=1e9), RouterMetrics())
+    w = ElasticWorker(rank, PartitionLeases(store, rank, world, 6, ttl_s=1.0), broker, "odh-demo",
+                      CpuScorer(model), router, max_records=100)
+    while not store.check(["stop"]):
+        w.tick()
+        store.set(f"alive/{rank}", str(w.scored_rows))
+        _t.sleep(0.01)
+    broker.close()
+
+
+def test_sigkill_rank_over_tcpstore_and_kafka_protocol():
+    """Real processes: 3 workers share a TCPStore (leases + committed counts) and a kafka-lite
+    broker (Kafka wire protocol); rank 1 is SIGKILLed mid-stream.  Survivors adopt its
+    partitions after the lease TTL and the committed global counts are exact."""
+    import datetime
+    import os
+    import signal
+    import socket
+    import time as _t
+    import torch.distributed as dist
+    import torch.multiprocessing as mp
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    store = dist.TCPStore("127.0.0.1", port, 4, True, timeout=datetime.timedelta(seconds=60), wait_for_workers=False)
+    lite = KafkaLiteServer("127.0.0.1", 0, default_partitions=6).start_in_thread()
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 6)
+    TransactionProducer(kb, ProducerConfig(fmt="json", batch=500, seed=3)).produce(6000)
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_elastic_proc, args=(r, 3, port, lite.bootstrap, 1)) for r in range(3)]
+    for p in ps:
+        p.start()
+    try:
+        reader = PartitionLeases(store, 99, 3, 6, ttl_s=1.0)
+        t0 = _t.time()
+        while _t.time() - t0 < 120:                      # wait until rank 1 is scoring
+            if store.check(["alive/1"]) and int(store.get("alive/1")) > 0:
+                break
+            _t.sleep(0.05)
+        os.kill(ps[1].pid, signal.SIGKILL)              # exact PID of our own child
+        ps[1].join(10)
+        rows = fraud = 0
+        while _t.time() - t0 < 180:
+            rows, fraud = reader.global_counts()
+            if rows >= 6000:
+                break
+            _t.sleep(0.1)
+        store.set("stop", "1")
+        for p in (ps[0], ps[2]):
+            p.join(30)
+        recs = [r for p in range(6) for r in kb.fetch("odh-demo", p, 0, 100_000)]
+        Xall, _, _ = decode_records([r.value for r in recs])
+        X, _ = generate(8000, seed=2)
+        model = build_model("mlp", seed=1, X_ref=X, calibrate_rate=0.02)
+        assert rows == 6000
+        assert fraud == int((model.predict_proba(Xall) >= 0.5).sum())
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+        kb.close()
+        lite.stop()
