@@ -44,6 +44,7 @@ def main(argv=None):
     ap.add_argument("--partitions-per-rank", type=int, default=4)
     ap.add_argument("--max-lag-msgs", type=int, default=64, help="producer back-pressure (messages)")
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr"])
+    ap.add_argument("--flush-us", type=int, default=500, help="deadline flush of partial micro-batches")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
 
@@ -97,7 +98,7 @@ def main(argv=None):
                                    cfg.notifier.p_reply, cfg.notifier.p_approve, 0.05, 7)
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=k.transactions_topic, group_id=k.group_id, batch=args.batch, depth=32, streams=4,
-        ring_rows=1 << 20, flush_us=500, run_budget_us=2000, reduce_period_ms=10.0,
+        ring_rows=1 << 20, flush_us=args.flush_us, run_budget_us=2000, reduce_period_ms=10.0,
         threshold=cfg.router.fraud_threshold, coalesce=8, max_fetch=64), partitions=list(range(P)))
     notif_c = store.consumer("notification-service", [k.notification_topic])
     resp_c = store.consumer(k.group_id + "-responses", [k.response_topic])
@@ -148,7 +149,7 @@ def main(argv=None):
             processes.tick()
 
     loop_until(time.perf_counter() + args.warmup)
-    svc.engine.reset_stats()
+    svc.reset_stats()
     rows0 = svc.rows_scored
     fr0 = router.fraud_started
     barrier(ctx)
@@ -158,8 +159,7 @@ def main(argv=None):
     rows = svc.rows_scored - rows0
     stop.set()
     th.join(5)
-    st = svc.engine.run(0, 0)                       # cumulative stats since reset
-    lat = st.lat_hist.astype(np.int64)
+    lat = svc.latency_hist()                        # cumulative since reset
     tot = all_sum(ctx, float(rows))
     el = all_max(ctx, elapsed)
     text = hub.router.expose().decode() if hasattr(hub.router, "expose") else ""
@@ -173,6 +173,7 @@ def main(argv=None):
         "metric": "end-to-end tx/s (Kafka ingest -> GPU score -> route -> BP -> notify)",
         "value": round(tot / el, 1), "unit": "tx/s", "n_gpus": ctx.world, "seconds": round(el, 2),
         "broker": args.broker, "rate_per_rank": args.rate, "micro_batch": args.batch, "model": args.model,
+        "flush_us": args.flush_us,
         "ring_arrival_to_scored_p50_us": round(hist_quantile(lat, 0.5) / 1e3, 1),
         "ring_arrival_to_scored_p99_us": round(hist_quantile(lat, 0.99) / 1e3, 1),
         "fraud_processes_started_rank0": router.fraud_started - fr0,

@@ -17,6 +17,7 @@ the processes (README.md:569,605).
 from __future__ import annotations
 
 import collections
+import queue
 import threading
 import time
 from dataclasses import dataclass
@@ -25,6 +26,9 @@ from typing import Deque, Dict, List, Optional, Tuple
 import numpy as np
 
 from ..contracts.transaction import TXB_MAGIC, TxBatch
+from ..ops._lib import FLAGGED_DTYPE
+
+FLAGGED_NP = np.dtype(FLAGGED_DTYPE)
 
 
 @dataclass
@@ -44,6 +48,9 @@ class EngineServiceConfig:
     exec_mode: str = "launch"        # "persistent": one resident kernel fed by a descriptor ring
     max_fetch: int = 2000
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
+    score_thread: bool = True        # drive engine.run() from a dedicated thread (GIL released in
+                                     # native code) so scoring latency does not wait on the Python
+                                     # router / process loop
     model_watch: Optional[str] = None   # rank 0: hot-swap when this safetensors file changes
 
 
@@ -77,6 +84,16 @@ class EngineService:
         self.kernel_exec_mean_us = 0.0
         self.last_reduce = time.monotonic()
         self._lat_prev = np.zeros(256, np.int64)
+        # scoring-thread hand-off: rows completed since the last step(), cumulative latency
+        # histogram, and engine-touching tasks (epoch flip + all-reduce, hot swap) that must
+        # run between two run() calls on the scoring thread
+        self._stat_lock = threading.Lock()
+        self._rows_new = 0
+        self._flagged_new: List[np.ndarray] = []
+        self._lat_cum = np.zeros(256, np.int64)
+        self._tasks: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._score_err: Optional[BaseException] = None
+        self._reduce_pending = False
 
     # ------------------------------------------------------------------ ingest (producer side)
     def _ingest_once(self) -> int:
@@ -130,25 +147,109 @@ class EngineService:
         if offs:
             self.consumer.commit(offs)
 
+    def _run_once(self) -> int:
+        st = self.engine.run(self.cfg.run_budget_us, self.cfg.flush_us)
+        # drain on the same thread, right after the rows were counted: the router must see
+        # every completed micro-batch's rows together with its flagged records
+        flagged = self.engine.drain_flagged() if st.rows else None
+        with self._stat_lock:
+            self._rows_new += int(st.rows)
+            if flagged is not None and len(flagged):
+                self._flagged_new.append(flagged)
+            self._lat_cum = st.lat_hist.astype(np.int64)
+            if st.dev_batches:
+                self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
+        return int(st.rows)
+
+    def _reduce(self, lat_cum: np.ndarray) -> None:
+        delta = lat_cum - self._lat_prev                # cumulative since reset -> send the delta
+        if (delta < 0).any():                           # stats were reset in between
+            delta = lat_cum
+        self.epochs.tick(delta)
+        self._lat_prev = lat_cum
+        self.hotswap.tick()                             # collective: X1 at runtime
+        self._reduce_pending = False
+
+    def _score_loop(self) -> None:
+        try:
+            import torch
+            torch.cuda.set_device(self.ctx.device)      # torch's current device is per thread
+            while not self._stop.is_set():
+                while True:
+                    try:
+                        task = self._tasks.get_nowait()
+                    except queue.Empty:
+                        break
+                    task()
+                self._run_once()
+        except BaseException as e:                      # surfaced by step()
+            self._score_err = e
+
     def step(self) -> int:
         if self._ingest_err is not None:
             raise RuntimeError("ingest thread failed") from self._ingest_err
-        st = self.engine.run(self.cfg.run_budget_us, self.cfg.flush_us)
-        flagged = self.engine.drain_flagged()
-        if st.rows or len(flagged):
-            self.router.on_flagged(flagged, int(st.rows))
-        self.rows_scored += int(st.rows)
-        if st.dev_batches:
-            self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
+        if self._score_err is not None:
+            raise RuntimeError("scoring thread failed") from self._score_err
+        threaded = getattr(self, "_score_thread", None) is not None
+        if not threaded:
+            self._run_once()
+        with self._stat_lock:
+            rows, self._rows_new = self._rows_new, 0
+            fl, self._flagged_new = self._flagged_new, []
+            lat_cum = self._lat_cum
+        flagged = np.concatenate(fl) if len(fl) > 1 else (fl[0] if fl else np.zeros(0, FLAGGED_NP))
+        if rows or len(flagged):
+            self.router.on_flagged(flagged, rows)
+        self.rows_scored += rows
         self._commit_done()
         now = time.monotonic()
-        if (now - self.last_reduce) * 1e3 >= self.cfg.reduce_period_ms:
-            lat = st.lat_hist.astype(np.int64)          # cumulative since reset -> send the delta
-            self.epochs.tick(lat - self._lat_prev)
-            self._lat_prev = lat
+        if (now - self.last_reduce) * 1e3 >= self.cfg.reduce_period_ms and not self._reduce_pending:
             self.last_reduce = now
-            self.hotswap.tick()                          # collective: X1 at runtime
-        return int(st.rows)
+            if threaded:
+                self._reduce_pending = True
+                self._tasks.put(lambda lat=lat_cum: self._reduce(lat))
+            else:
+                self._reduce(lat_cum)
+        if threaded and rows == 0:
+            time.sleep(50e-6)                            # nothing new: do not spin the GIL
+        return rows
+
+    def reset_stats(self) -> None:
+        """Zero the engine's latency statistics (on the scoring thread when there is one)."""
+        def _do():
+            self.engine.reset_stats()
+            with self._stat_lock:
+                self._lat_cum = np.zeros(256, np.int64)
+        self._on_engine_thread(_do)
+
+    def _on_engine_thread(self, fn) -> None:
+        if getattr(self, "_score_thread", None) is not None and self._score_thread.is_alive():
+            done = threading.Event()
+            box = []
+
+            def task():
+                try:
+                    fn()
+                except BaseException as e:        # re-raised on the caller's thread
+                    box.append(e)
+                finally:
+                    done.set()
+            self._tasks.put(task)
+            if not done.wait(60):
+                raise TimeoutError("scoring thread did not run the task")
+            if box:
+                raise box[0]
+        else:
+            fn()
+
+    def flush_epochs(self) -> None:
+        """Reduce the pending and the open counter epoch (X2) -- e.g. before reading final counts."""
+        self._on_engine_thread(self.epochs.finish)
+
+    def latency_hist(self) -> np.ndarray:
+        """Cumulative ring-arrival -> scored latency histogram (ns, 4 buckets per octave)."""
+        with self._stat_lock:
+            return self._lat_cum.copy()
 
     def request_swap(self, model) -> None:
         """Publish new weights to every rank at the next epoch tick (call on rank 0)."""
@@ -157,12 +258,17 @@ class EngineService:
     def start(self) -> "EngineService":
         self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")
         self._thread.start()
+        self._score_thread = None
+        if self.cfg.score_thread:
+            self._score_thread = threading.Thread(target=self._score_loop, daemon=True, name="ccfd-score")
+            self._score_thread.start()
         return self
 
     def stop(self) -> None:
         self._stop.set()
-        if getattr(self, "_thread", None):
-            self._thread.join(5)
+        for th in (getattr(self, "_score_thread", None), getattr(self, "_thread", None)):
+            if th is not None:
+                th.join(5)
         self.engine.close()
 
     def metrics_source(self):

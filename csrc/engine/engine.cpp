@@ -32,6 +32,8 @@
 #include <utility>
 #include <vector>
 
+#include <sys/prctl.h>
+
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
@@ -166,9 +168,9 @@ class Engine {
     slots.resize(cfg.depth);
     const size_t B = (size_t)cfg.max_batch;
     // zero-copy outputs in fine-grained (coherent) pinned memory: kernels stream them over
-    // PCIe without parking dirty lines in the XCD L2s, which lets every workgroup skip its
-    // system-scope L2 writeback at completion (CCFD_ARG_FENCE_COHERENT).  CCFD_COHERENT_OUT=0
-    // restores non-coherent outputs + per-workgroup release (A/B switch).
+    // PCIe without parking dirty lines in the XCD L2s (the per-workgroup system-scope release
+    // at completion stays: it is what orders the outputs before the completion record across
+    // XCDs).  CCFD_COHERENT_OUT=0 allocates non-coherent outputs instead (A/B switch).
     if (const char* e = std::getenv("CCFD_COHERENT_OUT")) coherent_out = std::atoi(e) != 0;
     if (const char* e = std::getenv("CCFD_ABLATE")) ablate = std::atoi(e) & 0x70;   // diagnostics only
     // HIP_LAUNCH_BLOCKING-style debug mode: synchronise after every launch so a kernel fault
@@ -751,6 +753,11 @@ class Engine {
   // finished batches; returns the number of batches submitted.
   int run(int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {
     HIPCHK(hipSetDevice(cfg.device));
+    // the default 50 us timer slack would turn every idle 5 us sleep into ~55 us of added
+    // latency; the scoring thread asks for 1 us (per-thread setting, set once)
+    static thread_local bool slack_set = false;
+    if (!slack_set) { prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0); slack_set = true; }
+    int64_t t_progress = now_ns();
     const int64_t t0 = now_ns();
     const int64_t t_end = t0 + budget_us * 1000;
     const int D = (int)slots.size();
@@ -811,7 +818,13 @@ class Engine {
         }
       }
       if (now_ns() >= t_end) break;
-      if (!progress) std::this_thread::sleep_for(std::chrono::microseconds(5));
+      if (progress) {
+        t_progress = now_ns();
+      } else if (now_ns() - t_progress < 50'000) {
+        cpu_relax();                                   // poll: in-flight batches complete in ~20 us
+      } else {
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
+      }
     }
     if (st) {
       st->wall_s += (now_ns() - t0) * 1e-9;

@@ -12,7 +12,8 @@ from ccfd_demo_summit_amd.models import build_model
 pytestmark = pytest.mark.gpu
 
 
-def test_engine_service_end_to_end(gpu):
+@pytest.mark.parametrize("score_thread", [True, False])
+def test_engine_service_end_to_end(gpu, score_thread):
     from ccfd_demo_summit_amd.ingest import InProcBroker, ProducerConfig, TransactionProducer
     from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
     from ccfd_demo_summit_amd.metrics import MetricsHub
@@ -33,7 +34,7 @@ def test_engine_service_end_to_end(gpu):
     ctx = DistContext(0, 1, 0, gpu, "none")
     svc = EngineService(ctx, DeviceModel(m, gpu), broker, router,
                         EngineServiceConfig(batch=4096, depth=4, streams=2, ring_rows=16384, flush_us=200,
-                                            reduce_period_ms=1.0)).start()
+                                            reduce_period_ms=1.0, score_thread=score_thread)).start()
     total = 32_000
     t0 = time.time()
     while svc.rows_scored < total and time.time() - t0 < 60:
@@ -46,7 +47,7 @@ def test_engine_service_end_to_end(gpu):
     assert hub.router.tx_incoming._value.get() == total
     nf = hub.router.tx_outgoing.labels(type="fraud")._value.get()
     assert router.fraud_started == nf == procs.active_count()
-    svc.epochs.finish()          # reduce the pending and the open epoch
+    svc.flush_epochs()           # reduce the pending and the open epoch (on the scoring thread)
     c, lat = svc.reducer.snapshot()
     assert c[0] == total and c[1] == nf
     assert lat.sum() > 0
