@@ -101,6 +101,39 @@ def seldon_dashboard() -> Dict:
     ])
 
 
+def kafka_dashboard() -> Dict:
+    """The broker series of deploy/grafana/Kafka.json:119-1093, served by kafka-lite's
+    /metrics (ingest/kafka_lite.py BrokerMetrics) or a Strimzi JMX exporter."""
+    k = 'strimzi_io_kind="Kafka"'
+    return _dashboard("Kafka", "ccfd-kafka", [
+        _panel("Brokers online", [f"count(kafka_server_replicamanager_leadercount)"], kind="singlestat", w=6, h=4),
+        _panel("Partitions", ["sum(kafka_server_replicamanager_partitioncount)"], kind="singlestat", w=6, h=4),
+        _panel("Under-replicated partitions", ["sum(kafka_server_replicamanager_underreplicatedpartitions)"],
+               kind="singlestat", w=6, h=4),
+        _panel("Offline partitions", ["sum(kafka_controller_kafkacontroller_offlinepartitionscount)"],
+               kind="singlestat", w=6, h=4),
+        _panel("Incoming messages /s", [f"sum without(instance)(rate(kafka_server_brokertopicmetrics_messagesin_total{{{k}}}[5m]))"],
+               unit="ops", legend=["{{topic}}"]),
+        _panel("Incoming bytes /s", [f"sum without(instance)(rate(kafka_server_brokertopicmetrics_bytesin_total{{{k}}}[5m]))"],
+               unit="Bps", legend=["{{topic}}"]),
+        _panel("Outgoing bytes /s", [f"sum without(instance)(rate(kafka_server_brokertopicmetrics_bytesout_total{{{k}}}[5m]))"],
+               unit="Bps", legend=["{{topic}}"]),
+        _panel("Failed produce / fetch", ['sum(kafka_server_brokertopicmetrics_failedproducerequests_total{topic!=""})',
+                                          'sum(kafka_server_brokertopicmetrics_failedfetchrequests_total{topic!=""})'],
+               legend=["produce", "fetch"]),
+    ])
+
+
+def training_dashboard() -> Dict:
+    """Replaces deploy/grafana/SparkMetrics.json (Spark workbench) with the trainer's series."""
+    return _dashboard("Training", "ccfd-train", [
+        _panel("Alive training workers (DDP ranks)", ["ccfd_train_workers"], kind="singlestat", w=6, h=4),
+        _panel("Device memory", ["ccfd_train_device_memory_bytes"], unit="bytes", w=18, h=4),
+        _panel("Loss", ["ccfd_train_loss"], legend=["{{model}}"]),
+        _panel("Samples /s", ["ccfd_train_samples_per_second"], unit="ops", legend=["{{model}}"]),
+    ])
+
+
 def gpu_dashboard() -> Dict:
     return _dashboard("MI355X scoring engine", "ccfd-gpu", [
         _panel("Rows scored /s (whole node)", [f"sum(rate({M.GPU_ROWS}_total[30s]))"], unit="ops"),
@@ -111,13 +144,17 @@ def gpu_dashboard() -> Dict:
         _panel("Global fraud-route rate (RCCL all-reduced)", [M.GPU_GLOBAL_FRAUD_RATE], unit="percentunit"),
         _panel("Amount distribution by route (device histogram)",
                [f"sum by (le, type) (rate({M.GPU_AMOUNT}_bucket[1m]))"], kind="heatmap", w=24),
+        _panel("Kernel execution per micro-batch (device clock, K7)", [M.GPU_PREFIX + "kernel_exec_mean_us"],
+               unit="µs"),
+        _panel("Model version (hot swaps)", [M.GPU_PREFIX + "model_version"], kind="singlestat"),
     ])
 
 
 def all_dashboards() -> Dict[str, Dict]:
     return {"Router.json": router_dashboard(), "KIE.json": kie_dashboard(),
             "ModelPrediction.json": model_dashboard(), "SeldonCore.json": seldon_dashboard(),
-            "GpuEngine.json": gpu_dashboard()}
+            "GpuEngine.json": gpu_dashboard(), "Kafka.json": kafka_dashboard(),
+            "Training.json": training_dashboard()}
 
 
 def write_all(out_dir: str) -> List[str]:

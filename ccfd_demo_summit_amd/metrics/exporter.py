@@ -58,6 +58,25 @@ class KieMetrics:
         return generate_latest(self.registry)
 
 
+class TrainMetrics:
+    """Trainer series (train/trainer.py), the analogue of the reference's Spark workbench
+    dashboard (deploy/grafana/SparkMetrics.json: alive workers, JVM memory): DDP world size,
+    loss, optimizer steps, samples/s and accelerator memory."""
+
+    def __init__(self, registry: Optional[CollectorRegistry] = None):
+        from prometheus_client import Counter as _C, Gauge as _G
+        self.registry = registry or CollectorRegistry()
+        r = self.registry
+        self.workers = _G("ccfd_train_workers", "Data-parallel training ranks alive", registry=r)
+        self.loss = _G("ccfd_train_loss", "Last minibatch loss", ["model"], registry=r)
+        self.steps = _C("ccfd_train_steps", "Optimizer steps", ["model"], registry=r)
+        self.samples_per_s = _G("ccfd_train_samples_per_second", "Training throughput", ["model"], registry=r)
+        self.mem_bytes = _G("ccfd_train_device_memory_bytes", "Device memory allocated", registry=r)
+
+    def expose(self) -> bytes:
+        return generate_latest(self.registry)
+
+
 class ModelMetrics:
     """Model-side gauges (last request) + Seldon engine latency histograms."""
 

@@ -35,6 +35,7 @@ class TrainConfig:
     seed: int = 0
     device: str = "auto"
     bf16: bool = True
+    metrics: Optional[object] = None       # metrics.exporter.TrainMetrics (Training dashboard)
 
 
 def _device(name: str) -> torch.device:
@@ -70,6 +71,12 @@ def _fit(net: nn.Module, Xn: np.ndarray, y: np.ndarray, cfg: TrainConfig, use_bf
     shard = torch.arange(rank, n, world)
     steps = 0
     last = float("nan")
+    tm = cfg.metrics
+    name = "mlp" if isinstance(net, nn.Sequential) else "lr"
+    if tm is not None:
+        tm.workers.set(world)
+    import time as _time
+    t_start = _time.perf_counter()
     for _ in range(cfg.epochs):
         perm = shard[torch.randperm(len(shard), generator=g)].to(dev)
         for s in range(0, len(perm), cfg.batch):
@@ -82,6 +89,12 @@ def _fit(net: nn.Module, Xn: np.ndarray, y: np.ndarray, cfg: TrainConfig, use_bf
             opt.step()
             steps += 1
             last = float(loss.detach())
+            if tm is not None:
+                tm.loss.labels(name).set(last)
+                tm.steps.labels(name).inc()
+                tm.samples_per_s.labels(name).set(steps * cfg.batch / max(1e-9, _time.perf_counter() - t_start))
+                if dev.type == "cuda":
+                    tm.mem_bytes.set(torch.cuda.memory_allocated(dev))
     return {"steps": steps, "final_loss": last, "pos_weight": pw}
 
 

@@ -122,5 +122,21 @@ def test_dashboards_reference_metric_names():
                  "fraud_investigation_amount", "fraud_approved_low_amount", "fraud_approved_amount",
                  "fraud_rejected_amount", "proba_1", "V17", "V10", "Amount",
                  "seldon_api_engine_server_requests_seconds_count",
-                 "seldon_api_engine_client_requests_seconds_bucket", "ccfd_gpu_rows_total"):
+                 "seldon_api_engine_client_requests_seconds_bucket", "ccfd_gpu_rows_total",
+                 "kafka_server_brokertopicmetrics_messagesin_total", "kafka_server_replicamanager_partitioncount",
+                 "kafka_controller_kafkacontroller_offlinepartitionscount", "ccfd_train_workers"):
         assert name in text, name
+    # one generated dashboard per reference dashboard (Spark -> Training) plus the GPU one
+    assert set(all_dashboards()) == {"Router.json", "KIE.json", "ModelPrediction.json", "SeldonCore.json",
+                                     "Kafka.json", "Training.json", "GpuEngine.json"}
+
+
+def test_trainer_exports_training_metrics():
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.metrics.exporter import TrainMetrics
+    from ccfd_demo_summit_amd.train import TrainConfig, train_logistic
+    X, y = generate(5000, seed=1, fraud_rate=0.05)
+    tm = TrainMetrics()
+    train_logistic(X, y, TrainConfig(epochs=1, batch=1000, device="cpu", metrics=tm))
+    text = tm.expose().decode()
+    assert 'ccfd_train_steps_total{model="lr"} 5.0' in text and "ccfd_train_workers 1.0" in text
