@@ -45,8 +45,10 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_broadcast_and_counter_allreduce():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_broadcast_and_counter_allreduce(world):
+    """W ranks on one node (W in {2,4,8}) through the same dist/ code path."""
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -57,13 +59,14 @@ def test_gloo_world2_broadcast_and_counter_allreduce():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort()
-    assert res[0][1] == res[1][1]                 # bit-identical weights
     from ccfd_demo_summit_amd.models import build_model
-    assert res[0][1] == build_model("mlp", seed=9).pack()
+    want = build_model("mlp", seed=9).pack()
+    assert all(r[1] == want for r in res)         # bit-identical weights on every rank
     truth0 = sum(1000 * (r + 1) + e for r in range(world) for e in range(3))
+    ranks_sum = world * (world + 1) // 2
     for _, _, g, lat in res:
-        assert g[0] == truth0 and g[1] == 3 * (1 + 2)
-        assert lat == 3 * 256 * (1 + 2)
+        assert g[0] == truth0 and g[1] == 3 * ranks_sum
+        assert lat == 3 * 256 * ranks_sum
 
 
 def test_assign_partitions_covers_each_once():
