@@ -50,8 +50,9 @@ def parse_args(argv=None):
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
-                    help="auto = per-batch launches (see profiles/r1/exec_mode_sweep.txt)")
-    ap.add_argument("--persist-grid", type=int, default=0)
+                    help="auto = persistent kernel for mlp/lr with zero-copy in/out, coalesced launches "
+                         "otherwise (profiles/r1/persist_sweep.txt)")
+    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default 128)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64"],
@@ -121,10 +122,11 @@ def main(argv=None):
     dm = DeviceModel.from_blob(args.model, blob, trees, depth_t, wire=args.wire == "w64")
     exec_mode = args.exec_mode
     if exec_mode == "auto":
-        # measured on MI355X (profiles/r1/exec_mode_sweep.txt): per-batch launches with
-        # kernel-published completion match the persistent kernel's throughput and halve
-        # the unloaded latency, so launch mode is the default.
-        exec_mode = "launch"
+        # measured on MI355X (profiles/r1/persist_sweep.txt): the persistent kernel with a
+        # parallel doorbell and 512-row work items reaches 0.82e9 tx/s at p50 147 us, above
+        # coalesced launches (0.75e9 at 166 us); GBDT and DMA paths use launches
+        zc = args.input_mode == "zerocopy" and args.output_mode == "zerocopy"
+        exec_mode = "persistent" if args.model in ("mlp", "lr") and zc else "launch"
 
     # ---- this rank's partitions of topic odh-demo (p % W == rank), pre-filled logs
     n_parts = args.partitions_per_rank * W

@@ -248,7 +248,7 @@ class Engine {
     int item_rows = CCFD_PERSIST_ITEM_ROWS;
     if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) {
       const int v = std::atoi(e);
-      if (v == 64 || v == 128 || v == 256) item_rows = v;
+      if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) item_rows = v;
     }
     persist_tpw = item_rows / 64;
     const int C = (cfg.max_batch + item_rows - 1) / item_rows;
@@ -289,7 +289,7 @@ class Engine {
     a.blob = cfg.blob;
     a.counters[0] = cfg.counters[0];
     a.counters[1] = cfg.counters[1];
-    const int grid = cfg.persist_grid > 0 ? cfg.persist_grid : 256;
+    const int grid = cfg.persist_grid > 0 ? cfg.persist_grid : CCFD_PERSIST_GRID;
     int rc = ccfd_persist_launch(&a, grid, pstream);
     if (rc) { set_error("persistent kernel launch failed"); return rc; }
     prunning = true;

@@ -67,32 +67,47 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   // would each hold PCIe read requests and starve the feature stream (measured: 2x grid
   // -> 3x slower before this split).
   if (blockIdx.x == 0) {
-    if (tid == 0) {
+    // The whole first wave mirrors: lane l copies word l % W of descriptor (mirrored + l / W),
+    // so up to 10 newly posted descriptors cost ONE PCIe round trip instead of one per word
+    // (a thread-0 copy loop serialised ~11 us per micro-batch: profiles/r1/persist_sweep.txt).
+    if (wave == 0) {
+      constexpr int kW = (int)(sizeof(ccfd_persist_desc) / 8);
+      constexpr int kPer = 64 / kW;                     // descriptors per wave step
       unsigned long long mirrored = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       unsigned sleep_n = 1;
       for (;;) {
-        const unsigned long long p = __hip_atomic_load(&a.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        unsigned long long p = 0;
+        if (lane == 0) p = __hip_atomic_load(&a.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        p = __shfl(p, 0);
         if (p > mirrored) {
-          for (unsigned long long b = mirrored; b < p; ++b) {
-            const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.desc + (b % (unsigned long long)a.ring));
+          const unsigned long long nb = min(p - mirrored, (unsigned long long)kPer);
+          const int bi = lane / kW, wi = lane % kW;
+          if (bi < (int)nb) {
+            const unsigned long long b = mirrored + bi;
+            const unsigned long long* src =
+                reinterpret_cast<const unsigned long long*>(a.desc + (b % (unsigned long long)a.ring));
             unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
-#pragma unroll
-            for (int w = 0; w < (int)(sizeof(ccfd_persist_desc) / 8); ++w)
-              __hip_atomic_store(dst + w, __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + wi, __hip_atomic_load(src + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
-          __hip_atomic_store(&a.dev->posted, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          mirrored = p;
+          // every lane's descriptor store is ordered before the new posted count
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          mirrored += nb;
+          if (lane == 0) __hip_atomic_store(&a.dev->posted, mirrored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           sleep_n = 1;
           continue;
         }
-        if (__hip_atomic_load(&a.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-          __hip_atomic_store(&a.dev->stop, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(&a.ctl->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        int stop = 0;
+        if (lane == 0) stop = __hip_atomic_load(&a.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+        if (__shfl(stop, 0)) {
+          if (lane == 0) {
+            __hip_atomic_store(&a.dev->stop, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&a.ctl->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
           break;
         }
         for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);   // ~64..1024 cycles
-        sleep_n = sleep_n < 16 ? sleep_n * 2 : 16;
+        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
       }
     }
     return;                                              // no barrier is ever used by WG 0

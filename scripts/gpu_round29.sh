@@ -1,0 +1,9 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+run() { name=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/r29_$name.log 2>&1 || { tail -20 gpurun_out/r29_$name.log; exit 1; }; echo "$name $(tail -1 gpurun_out/r29_$name.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e6,1), d["p50_latency_us"], d["p50_latency_us_unloaded"], d["step_us_per_batch"], d["host_us_per_batch"], d["rows_scored"]==d["rows_expected"])')"; }
+CCFD_PERSIST_ITEM_ROWS=256 run p256_g256_d8 --exec-mode persistent --persist-grid 256 --depth 8 --no-unloaded-probe
+CCFD_PERSIST_ITEM_ROWS=256 run p256_g512_d8 --exec-mode persistent --persist-grid 512 --depth 8 --no-unloaded-probe
+CCFD_PERSIST_ITEM_ROWS=256 run p256_g256_d16 --exec-mode persistent --persist-grid 256 --depth 16 --no-unloaded-probe
+CCFD_PERSIST_ITEM_ROWS=128 run p128_g256_d8 --exec-mode persistent --persist-grid 256 --depth 8 --no-unloaded-probe
+run launch_d8_c4 --depth 8 --coalesce 4 --no-unloaded-probe
