@@ -45,6 +45,9 @@ def main(argv=None):
     ap.add_argument("--max-lag-msgs", type=int, default=64, help="producer back-pressure (messages)")
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr"])
     ap.add_argument("--flush-us", type=int, default=500, help="deadline flush of partial micro-batches")
+    ap.add_argument("--fmt", default="txb1", choices=["txb1", "json"],
+                    help="txb1: one columnar batch per message; json: one transaction per message")
+    ap.add_argument("--python-ingest", action="store_true", help="kafka-lite: use the Python consumer thread")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
 
@@ -68,7 +71,8 @@ def main(argv=None):
     cfg = load_config(None)
     k = cfg.kafka
     P = args.partitions_per_rank
-    store = InProcBroker(default_partitions=P, retention=4 * args.max_lag_msgs)
+    lag_limit = args.max_lag_msgs * (args.batch if args.fmt == "json" else 1)   # in messages
+    store = InProcBroker(default_partitions=P, retention=4 * lag_limit)
     server = None
     if args.broker == "kafka-lite":
         from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
@@ -99,7 +103,8 @@ def main(argv=None):
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=k.transactions_topic, group_id=k.group_id, batch=args.batch, depth=32, streams=4,
         ring_rows=1 << 20, flush_us=args.flush_us, run_budget_us=2000, reduce_period_ms=10.0,
-        threshold=cfg.router.fraud_threshold, coalesce=8, max_fetch=64), partitions=list(range(P)))
+        threshold=cfg.router.fraud_threshold, coalesce=8, max_fetch=64,
+        native_ingest=not args.python_ingest), partitions=list(range(P)))
     notif_c = store.consumer("notification-service", [k.notification_topic])
     resp_c = store.consumer(k.group_id + "-responses", [k.response_topic])
 
@@ -114,6 +119,11 @@ def main(argv=None):
     stop = threading.Event()
     produced = [0]
     id_base = np.uint64(ctx.rank) << np.uint64(48)
+    if args.fmt == "json":                  # per-message JSON: pre-rendered tails, ids formatted per batch
+        from ccfd_demo_summit_amd.contracts import FEATURE_NAMES
+        Xj, _ = generate(args.batch, seed=77 + ctx.rank)
+        tails = [(",\"customer_id\":%d," % (i % 100_000) + ",".join(
+            f'"{n}":{float(v):.6g}' for n, v in zip(FEATURE_NAMES, Xj[i])) + "}").encode() for i in range(args.batch)]
 
     def producer():
         seq = 0
@@ -122,13 +132,18 @@ def main(argv=None):
             if args.rate > 0 and produced[0] > args.rate * (time.perf_counter() - t0):
                 time.sleep(0.0002)
                 continue
-            if store.lag(k.group_id, k.transactions_topic) > args.max_lag_msgs:
+            if store.lag(k.group_id, k.transactions_topic) > lag_limit:
                 time.sleep(0.0002)
                 continue
-            msg = pool[seq % len(pool)]
-            ids = np.frombuffer(msg, np.uint64, args.batch, 32)
-            ids[:] = id_base + np.uint64(seq * args.batch) + np.arange(args.batch, dtype=np.uint64)
-            prod_broker.produce(k.transactions_topic, bytes(msg), partition=seq % P)
+            if args.fmt == "json":
+                b0 = int(id_base) + seq * args.batch
+                msgs = [b'{"id":%d' % (b0 + i) + t for i, t in enumerate(tails)]
+                prod_broker.produce_many(k.transactions_topic, msgs, partition=seq % P)
+            else:
+                msg = pool[seq % len(pool)]
+                ids = np.frombuffer(msg, np.uint64, args.batch, 32)
+                ids[:] = id_base + np.uint64(seq * args.batch) + np.arange(args.batch, dtype=np.uint64)
+                prod_broker.produce(k.transactions_topic, bytes(msg), partition=seq % P)
             produced[0] += args.batch
             seq += 1
 
@@ -173,7 +188,8 @@ def main(argv=None):
         "metric": "end-to-end tx/s (Kafka ingest -> GPU score -> route -> BP -> notify)",
         "value": round(tot / el, 1), "unit": "tx/s", "n_gpus": ctx.world, "seconds": round(el, 2),
         "broker": args.broker, "rate_per_rank": args.rate, "micro_batch": args.batch, "model": args.model,
-        "flush_us": args.flush_us,
+        "flush_us": args.flush_us, "fmt": args.fmt,
+        "ingest": "python" if (args.python_ingest or args.broker == "inproc") else "native",
         "ring_arrival_to_scored_p50_us": round(hist_quantile(lat, 0.5) / 1e3, 1),
         "ring_arrival_to_scored_p99_us": round(hist_quantile(lat, 0.99) / 1e3, 1),
         "fraud_processes_started_rank0": router.fraud_started - fr0,

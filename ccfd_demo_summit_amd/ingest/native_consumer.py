@@ -1,0 +1,137 @@
+"""Python handle of the native Kafka consumer (csrc/engine/kafka_consumer.cpp).
+
+A C++ thread fetches (Kafka Fetch v4 over one TCP connection), validates RecordBatch v2
+CRC-32C, and writes TXB1 batches / JSON transactions straight into the engine's pinned
+partition rings (f32 or W64 rows) -- no Python per message (SURVEY.md §2.4 H1, §7.3 hard
+part 1: JSON-per-transaction at 1M/s is out of reach for a Python consumer loop).
+
+    kc = NativeKafkaConsumer.for_engine(engine, "127.0.0.1:9092", "odh-demo", {p: committed_offset})
+    kc.start()
+    ...
+    for p, off in kc.committable().items(): consumer_group.commit(p, off)   # scored data only
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..ops._lib import check, lib
+
+
+class KcPartition(C.Structure):
+    _fields_ = [("kafka_partition", C.c_int32), ("engine_partition", C.c_int32), ("start_offset", C.c_int64),
+                ("feats", C.c_void_p), ("ids", C.c_void_p), ("customer", C.c_void_p), ("capacity", C.c_int64)]
+
+
+class KcStats(C.Structure):
+    _fields_ = [("records", C.c_uint64), ("rows", C.c_uint64), ("bytes", C.c_uint64),
+                ("errors", C.c_uint64), ("fetches", C.c_uint64)]
+
+
+def _bind(L):
+    if getattr(L, "_kc_bound", False):
+        return L
+    L.ccfd_kc_create_engine.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_void_p, C.c_int, C.c_int]
+    L.ccfd_kc_create_engine.restype = C.c_void_p
+    L.ccfd_kc_create_array.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_void_p, C.c_int, C.c_int]
+    L.ccfd_kc_create_array.restype = C.c_void_p
+    for f in ("ccfd_kc_start",):
+        getattr(L, f).argtypes = [C.c_void_p]
+        getattr(L, f).restype = C.c_int
+    for f in ("ccfd_kc_stop", "ccfd_kc_destroy"):
+        getattr(L, f).argtypes = [C.c_void_p]
+        getattr(L, f).restype = None
+    L.ccfd_kc_committable.argtypes = [C.c_void_p, C.c_int]
+    L.ccfd_kc_committable.restype = C.c_int64
+    L.ccfd_kc_get_stats.argtypes = [C.c_void_p, C.POINTER(KcStats)]
+    L.ccfd_kc_get_stats.restype = None
+    L.ccfd_kc_last_error.argtypes = [C.c_void_p]
+    L.ccfd_kc_last_error.restype = C.c_char_p
+    L._kc_bound = True
+    return L
+
+
+def _split(bootstrap: str):
+    host, _, port = bootstrap.split(",")[0].rpartition(":")
+    return (host or "127.0.0.1"), int(port or 9092)
+
+
+class NativeKafkaConsumer:
+    def __init__(self, handle: int, partitions: List[int], keep=None):
+        self.h = handle
+        self.partitions = list(partitions)
+        self._keep = keep            # buffers the C++ side writes into
+
+    @classmethod
+    def for_engine(cls, engine, bootstrap: str, topic: str, start_offsets: Dict[int, int]) -> "NativeKafkaConsumer":
+        """Consume partitions ``start_offsets`` (kafka partition -> first offset) into the
+        engine rings registered with ``engine.set_ring(p, ...)`` under the same index."""
+        L = _bind(lib())
+        ps = sorted(start_offsets)
+        arr = (KcPartition * len(ps))()
+        for i, p in enumerate(ps):
+            log = engine.logs[p]
+            arr[i] = KcPartition(p, p, int(start_offsets[p]), log.feats.ptr, log.ids.ptr, log.customer.ptr, log.n)
+        host, port = _split(bootstrap)
+        h = L.ccfd_kc_create_engine(C.c_void_p(engine.h), host.encode(), port, topic.encode(), arr, len(ps),
+                                    1 if engine.wire else 0)
+        check(0 if h else -1, "ccfd_kc_create_engine")
+        return cls(h, ps, keep=arr)
+
+    @classmethod
+    def for_arrays(cls, bootstrap: str, topic: str, start_offsets: Dict[int, int], capacity: int,
+                   wire: bool = False) -> "NativeKafkaConsumer":
+        """Test sink: flat numpy arrays per partition (no engine, no GPU)."""
+        L = _bind(lib())
+        ps = sorted(start_offsets)
+        width = 16 if wire else 30
+        bufs = {p: (np.zeros((capacity, width), np.float32), np.zeros(capacity, np.uint64),
+                    np.zeros(capacity, np.uint32)) for p in ps}
+        arr = (KcPartition * len(ps))()
+        for i, p in enumerate(ps):
+            f, ids, cu = bufs[p]
+            arr[i] = KcPartition(p, i, int(start_offsets[p]), f.ctypes.data, ids.ctypes.data, cu.ctypes.data, capacity)
+        host, port = _split(bootstrap)
+        h = L.ccfd_kc_create_array(host.encode(), port, topic.encode(), arr, len(ps), 1 if wire else 0)
+        check(0 if h else -1, "ccfd_kc_create_array")
+        kc = cls(h, ps, keep=(arr, bufs))
+        kc.arrays = bufs
+        return kc
+
+    def start(self) -> "NativeKafkaConsumer":
+        lib().ccfd_kc_start(C.c_void_p(self.h))
+        return self
+
+    def stop(self) -> None:
+        if self.h:
+            lib().ccfd_kc_stop(C.c_void_p(self.h))
+
+    def close(self) -> None:
+        if self.h:
+            lib().ccfd_kc_destroy(C.c_void_p(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self) -> Dict[str, int]:
+        st = KcStats()
+        lib().ccfd_kc_get_stats(C.c_void_p(self.h), C.byref(st))
+        return {k: int(getattr(st, k)) for k, _ in KcStats._fields_}
+
+    def last_error(self) -> str:
+        return (lib().ccfd_kc_last_error(C.c_void_p(self.h)) or b"").decode(errors="replace")
+
+    def committable(self) -> Dict[int, int]:
+        """partition -> next offset to commit (only partitions that advanced)."""
+        out = {}
+        for i, p in enumerate(self.partitions):
+            off = lib().ccfd_kc_committable(C.c_void_p(self.h), i)
+            if off >= 0:
+                out[p] = int(off)
+        return out

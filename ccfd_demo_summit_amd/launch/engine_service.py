@@ -48,6 +48,8 @@ class EngineServiceConfig:
     exec_mode: str = "launch"        # "persistent": one resident kernel fed by a descriptor ring
     max_fetch: int = 2000
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
+    native_ingest: bool = True       # Kafka-protocol brokers: C++ consumer thread fetches and writes
+                                     # rows straight into the rings (ingest/native_consumer.py)
     score_thread: bool = True        # drive engine.run() from a dedicated thread (GIL released in
                                      # native code) so scoring latency does not wait on the Python
                                      # router / process loop
@@ -69,8 +71,19 @@ class EngineService:
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:
             self.engine.set_ring(p, cfg.ring_rows)
-        self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
-            if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
+        self.native = None
+        if cfg.native_ingest and hasattr(broker, "_bootstrap"):
+            from ..ingest.native_consumer import NativeKafkaConsumer
+            starts = {}
+            for p in self.partitions:
+                c = broker.committed(cfg.group_id, cfg.topic, p)
+                starts[p] = c if c is not None else broker.begin_offset(cfg.topic, p)
+            host, port = broker._bootstrap
+            self.native = NativeKafkaConsumer.for_engine(self.engine, f"{host}:{port}", cfg.topic, starts)
+            self.consumer = None
+        else:
+            self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
+                if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
         self.reducer = reducer or CounterReducer(ctx, ctx.device)
         self.epochs = EpochPipeline(self.engine, self.reducer)
         from ..parallel.hotswap import HotSwap
@@ -135,6 +148,10 @@ class EngineService:
 
     # ------------------------------------------------------------------ consumer side
     def _commit_done(self) -> None:
+        if self.native is not None:                     # offsets whose rows are all scored
+            for p, off in self.native.committable().items():
+                self.broker.commit(self.cfg.group_id, self.cfg.topic, p, off)
+            return
         offs = {}
         for p in self.partitions:
             released = self.engine.cursor(p)
@@ -256,8 +273,12 @@ class EngineService:
         self.hotswap.offer(model)
 
     def start(self) -> "EngineService":
-        self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")
-        self._thread.start()
+        if self.native is not None:
+            self._thread = None
+            self.native.start()
+        else:
+            self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")
+            self._thread.start()
         self._score_thread = None
         if self.cfg.score_thread:
             self._score_thread = threading.Thread(target=self._score_loop, daemon=True, name="ccfd-score")
@@ -266,9 +287,13 @@ class EngineService:
 
     def stop(self) -> None:
         self._stop.set()
+        if self.native is not None:
+            self.native.stop()
         for th in (getattr(self, "_score_thread", None), getattr(self, "_thread", None)):
             if th is not None:
                 th.join(5)
+        if self.native is not None:
+            self.native.close()
         self.engine.close()
 
     def metrics_source(self):

@@ -185,3 +185,11 @@ extern "C" int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* off
   }
   return n_msgs;
 }
+
+// Internal entry points for the native Kafka consumer (kafka_consumer.cpp).
+namespace ccfd {
+bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust) {
+  return parse_one(s, e, f, id, cust);
+}
+void encode_w64_row(const float* x, uint8_t* out) { encode_row_w64(x, out); }
+}  // namespace ccfd

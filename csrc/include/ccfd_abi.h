@@ -252,6 +252,35 @@ int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* offsets, int64
 // f32 rows (stride ld >= 30) -> W64 wire rows; returns n or -1.
 int64_t ccfd_encode_w64(const float* x, int64_t n, int64_t ld, uint8_t* out);
 
+// ---------------------------------------------------------------------------
+// Native Kafka consumer (csrc/engine/kafka_consumer.cpp): Fetch v4 -> RecordBatch v2 ->
+// TXB1 / JSON values -> rows in the engine's pinned partition rings.
+typedef struct ccfd_kc_partition {
+  int32_t kafka_partition;   // partition id in the topic
+  int32_t engine_partition;  // ring index in the engine (engine sink)
+  int64_t start_offset;      // first offset to fetch (committed offset)
+  void* feats;               // ring rows (f32[30] or W64), array sink: [capacity] rows
+  uint64_t* ids;
+  uint32_t* customer;
+  int64_t capacity;          // array sink only
+} ccfd_kc_partition;
+
+typedef struct ccfd_kc_stats {
+  uint64_t records, rows, bytes, errors, fetches;
+} ccfd_kc_stats;
+
+void* ccfd_kc_create_engine(void* engine, const char* host, int port, const char* topic,
+                            const ccfd_kc_partition* parts, int n_parts, int wire);
+void* ccfd_kc_create_array(const char* host, int port, const char* topic, const ccfd_kc_partition* parts,
+                           int n_parts, int wire);
+int ccfd_kc_start(void* kc);
+void ccfd_kc_stop(void* kc);
+void ccfd_kc_destroy(void* kc);
+// highest offset whose rows have all been consumed downstream (-1: nothing new)
+int64_t ccfd_kc_committable(void* kc, int part_index);
+void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out);
+const char* ccfd_kc_last_error(void* kc);
+
 #ifdef __cplusplus
 }
 #endif

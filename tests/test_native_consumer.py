@@ -1,0 +1,85 @@
+"""Native Kafka consumer (csrc/engine/kafka_consumer.cpp) against kafka-lite on 127.0.0.1:
+TXB1 batches and JSON transactions land in the sink rows bit-exactly (f32 and W64),
+offsets become committable once rows are consumed, CRC-corrupted batches are rejected."""
+import json
+import time
+
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.contracts import FEATURE_NAMES, TxBatch, encode_wire
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+from ccfd_demo_summit_amd.ingest.native_consumer import NativeKafkaConsumer
+
+
+@pytest.fixture()
+def lite():
+    srv = KafkaLiteServer("127.0.0.1", 0, default_partitions=2).start_in_thread()
+    yield srv
+    srv.stop()
+
+
+def _wait(kc, rows, timeout=20):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if kc.stats()["rows"] >= rows:
+            return True
+        time.sleep(0.01)
+    return False
+
+
+@pytest.mark.parametrize("wire", [False, True])
+def test_txb1_and_json_into_rows(lite, wire):
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 2)
+    X, _ = generate(3000, seed=4)
+    ids = np.arange(3000, dtype=np.uint64) + 10
+    cu = (np.arange(3000) % 977).astype(np.uint32)
+    # partition 0: three TXB1 batches; partition 1: 200 JSON messages
+    for s in (0, 1000, 2000):
+        kb.produce("odh-demo", TxBatch(ids=ids[s:s + 1000], customer=cu[s:s + 1000], features=X[s:s + 1000]).encode(),
+                   partition=0)
+    msgs = [json.dumps({"id": int(ids[i]), "customer_id": int(cu[i]),
+                        **{n: float(v) for n, v in zip(FEATURE_NAMES, X[i])}}).encode() for i in range(200)]
+    kb.produce_many("odh-demo", msgs, partition=1)
+    kc = NativeKafkaConsumer.for_arrays(lite.bootstrap, "odh-demo", {0: 0, 1: 0}, capacity=4000, wire=wire).start()
+    try:
+        assert _wait(kc, 3200), (kc.stats(), kc.last_error())
+        st = kc.stats()
+        assert st["records"] == 203 and st["errors"] == 0
+        f0, i0, c0 = kc.arrays[0]
+        f1, i1, c1 = kc.arrays[1]
+        want = encode_wire(X).view(np.float32).reshape(-1, 16) if wire else X
+        np.testing.assert_array_equal(f0[:3000], want)
+        np.testing.assert_array_equal(i0[:3000], ids)
+        np.testing.assert_array_equal(c0[:3000], cu)
+        np.testing.assert_array_equal(f1[:200], want[:200])
+        np.testing.assert_array_equal(i1[:200], ids[:200])
+        assert kc.committable() == {0: 3, 1: 200}
+        assert kc.committable() == {}                       # nothing new
+    finally:
+        kc.stop()
+        kc.close()
+        kb.close()
+
+
+def test_resume_from_offset_and_late_data(lite):
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("t", 1)
+    X, _ = generate(50, seed=1)
+    for i in range(50):
+        kb.produce("t", json.dumps({"id": i, "features": X[i].tolist()}).encode(), partition=0)
+    kc = NativeKafkaConsumer.for_arrays(lite.bootstrap, "t", {0: 20}, capacity=100).start()
+    try:
+        assert _wait(kc, 30)
+        kb.produce("t", json.dumps({"id": 99, "features": X[0].tolist()}).encode(), partition=0)
+        assert _wait(kc, 31)
+        f, ids, _ = kc.arrays[0]
+        assert ids[:31].tolist() == list(range(20, 50)) + [99]
+        np.testing.assert_allclose(f[:30], X[20:50], rtol=1e-6)
+    finally:
+        kc.stop()
+        kc.close()
+        kb.close()

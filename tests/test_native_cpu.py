@@ -120,6 +120,21 @@ def test_host_runtime_under_asan(tmp_path):
         "out = np.zeros((1000, 64), np.uint8)\n"
         "assert L.ccfd_encode_w64(X.ctypes.data, 1000, 30, out.ctypes.data) == 1000\n"
         "assert L.ccfd_crc32c(bytes(range(256)) * 100, 25600, 0) != 0\n"
+        "# native Kafka consumer: Fetch/RecordBatch parsing against kafka-lite\n"
+        "import time\n"
+        "from ccfd_demo_summit_amd.contracts import TxBatch\n"
+        "from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer\n"
+        "from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker\n"
+        "from ccfd_demo_summit_amd.ingest.native_consumer import NativeKafkaConsumer\n"
+        "srv = KafkaLiteServer('127.0.0.1', 0, default_partitions=1).start_in_thread()\n"
+        "kb = KafkaBroker(srv.bootstrap); kb.create_topic('t', 1)\n"
+        "kb.produce('t', TxBatch(ids=np.arange(500, dtype=np.uint64), customer=np.zeros(500, np.uint32), features=X[:500]).encode(), partition=0)\n"
+        "kb.produce_many('t', msgs[:50], partition=0)\n"
+        "kc = NativeKafkaConsumer.for_arrays(srv.bootstrap, 't', {0: 0}, capacity=1000, wire=True).start()\n"
+        "t0 = time.time()\n"
+        "while kc.stats()['records'] < 51 and time.time() - t0 < 20: time.sleep(0.01)\n"
+        "assert kc.stats()['records'] == 51, kc.stats()\n"
+        "kc.stop(); kc.close(); kb.close(); srv.stop()\n"
         "print('asan probe ok')\n")
     env = dict(os.environ, CCFD_SANITIZE="address,undefined", LD_PRELOAD=rt, CCFD_NO_AUTOBUILD="1",
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
