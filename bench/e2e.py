@@ -174,6 +174,7 @@ def main(argv=None):
     rows = svc.rows_scored - rows0
     stop.set()
     th.join(5)
+    svc.flush_epochs()                              # collective: paired X2 reductions on every rank
     lat = svc.latency_hist()                        # cumulative since reset
     tot = all_sum(ctx, float(rows))
     el = all_max(ctx, elapsed)

@@ -59,7 +59,7 @@ class EngineServiceConfig:
 class EngineService:
     def __init__(self, ctx, dm, broker, router, cfg: EngineServiceConfig, reducer=None, partitions=None):
         from ..engine import StreamEngine
-        from ..parallel.dp import CounterReducer, EpochPipeline, assign_partitions
+        from ..parallel.dp import CounterReducer, EpochPipeline, assign_partitions, x_group
         self.ctx = ctx
         self.cfg = cfg
         self.broker = broker
@@ -84,10 +84,12 @@ class EngineService:
         else:
             self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
                 if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
-        self.reducer = reducer or CounterReducer(ctx, ctx.device)
+        # the scoring thread's collectives (X2 epochs, hot swap, flush) use their own group
+        self.group = x_group(ctx)
+        self.reducer = reducer or CounterReducer(ctx, ctx.device, group=self.group)
         self.epochs = EpochPipeline(self.engine, self.reducer)
         from ..parallel.hotswap import HotSwap
-        self.hotswap = HotSwap(ctx, self.engine, cfg.model_watch)
+        self.hotswap = HotSwap(ctx, self.engine, cfg.model_watch, group=self.group)
         # per partition: (ring row end, next kafka offset) of ingested messages, oldest first
         self._pending: Dict[int, Deque[Tuple[int, int]]] = {p: collections.deque() for p in self.partitions}
         self._rows_in: Dict[int, int] = {p: 0 for p in self.partitions}
@@ -164,8 +166,8 @@ class EngineService:
         if offs:
             self.consumer.commit(offs)
 
-    def _run_once(self) -> int:
-        st = self.engine.run(self.cfg.run_budget_us, self.cfg.flush_us)
+    def _run_once(self, budget_us: Optional[int] = None) -> int:
+        st = self.engine.run(self.cfg.run_budget_us if budget_us is None else budget_us, self.cfg.flush_us)
         # drain on the same thread, right after the rows were counted: the router must see
         # every completed micro-batch's rows together with its flagged records
         flagged = self.engine.drain_flagged() if st.rows else None
@@ -182,7 +184,9 @@ class EngineService:
         delta = lat_cum - self._lat_prev                # cumulative since reset -> send the delta
         if (delta < 0).any():                           # stats were reset in between
             delta = lat_cum
-        self.epochs.tick(delta)
+        # one collective per tick on every rank; waiting for the closed epoch keeps
+        # retiring micro-batches on this (the scoring) thread
+        self.epochs.tick(delta, progress=lambda: self._run_once(0))
         self._lat_prev = lat_cum
         self.hotswap.tick()                             # collective: X1 at runtime
         self._reduce_pending = False
@@ -260,8 +264,24 @@ class EngineService:
             fn()
 
     def flush_epochs(self) -> None:
-        """Reduce the pending and the open counter epoch (X2) -- e.g. before reading final counts."""
-        self._on_engine_thread(self.epochs.finish)
+        """Reduce the pending and the open counter epoch (X2) -- e.g. before reading final counts
+        or stopping.  Collective: every rank calls it.  Ranks first agree on the largest number
+        of epoch ticks any of them has done and catch up, so every collective stays paired
+        even though ticks are scheduled by each rank's own clock."""
+        def _do():
+            n = getattr(self.epochs, "ticks", 0)
+            if self.ctx.initialized:
+                import torch
+                import torch.distributed as dist
+                t = torch.tensor([n], dtype=torch.int64, device=self.ctx.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                target = int(t.item())
+                while getattr(self.epochs, "ticks", 0) < target:
+                    with self._stat_lock:
+                        lat = self._lat_cum
+                    self._reduce(lat)
+            self.epochs.finish()
+        self._on_engine_thread(_do)
 
     def latency_hist(self) -> np.ndarray:
         """Cumulative ring-arrival -> scored latency histogram (ns, 4 buckets per octave)."""

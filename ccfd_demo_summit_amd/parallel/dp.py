@@ -75,26 +75,38 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     return DistContext(rank, world, local, device, "none")
 
 
+def x_group(ctx: DistContext):
+    """A second process group over all ranks for the collectives issued from an engine's
+    scoring thread (X2 epochs, runtime X1).  torch.distributed pairs collectives by call
+    order per group; giving the scoring thread its own group keeps its sequence independent
+    of collectives the main thread issues (barriers, bench reductions).  Collective call:
+    every rank creates it at the same point.  None when not distributed."""
+    if not ctx.initialized:
+        return None
+    return dist.new_group(ranks=list(range(ctx.world)))
+
+
 def assign_partitions(n_partitions: int, rank: int, world: int) -> List[int]:
     """Static consumer-group assignment: partition p -> rank p % world."""
     return [p for p in range(n_partitions) if p % world == rank]
 
 
-def broadcast_blob(ctx: DistContext, blob: Optional[torch.Tensor], src: int = 0) -> torch.Tensor:
+def broadcast_blob(ctx: DistContext, blob: Optional[torch.Tensor], src: int = 0, group=None) -> torch.Tensor:
     """X1: rank ``src`` sends its packed model blob (uint8, on ctx.device) to every rank and
-    every rank verifies the received bytes against the sender's checksum."""
+    every rank verifies the received bytes against the sender's checksum.  ``group``: the
+    process group (the engine thread's X-group at runtime, see ``x_group``)."""
     if not ctx.initialized:
         assert blob is not None
         return blob
     n = torch.tensor([blob.numel() if ctx.rank == src else 0], dtype=torch.int64, device=ctx.device)
-    dist.broadcast(n, src)
+    dist.broadcast(n, src, group=group)
     if ctx.rank != src:
         blob = torch.empty(int(n.item()), dtype=torch.uint8, device=ctx.device)
-    dist.broadcast(blob, src)
+    dist.broadcast(blob, src, group=group)
     ck = _checksum(blob)
     lo, hi = ck.clone(), ck.clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
     if not torch.equal(lo, hi):
         raise RuntimeError("model blob broadcast mismatch between ranks")
     return blob
@@ -113,9 +125,10 @@ class CounterReducer:
     next to the counters, all-reduce (sum) the packed vector, accumulate into ``totals``
     and zero the epoch buffer for reuse.  Nothing here blocks the host on GPU backends."""
 
-    def __init__(self, ctx: DistContext, device: torch.device, priority: int = 0):
+    def __init__(self, ctx: DistContext, device: torch.device, priority: int = 0, group=None):
         self.ctx = ctx
         self.device = device
+        self.group = group
         self.totals = torch.zeros(N_COUNTER_SLOTS + N_LAT_BUCKETS, dtype=torch.int64, device=device)
         self.local_totals = torch.zeros_like(self.totals)
         self.pack = torch.zeros_like(self.totals)
@@ -136,7 +149,7 @@ class CounterReducer:
                 self.pack[N_COUNTER_SLOTS:].zero_()
             self.local_totals += self.pack
             if self.ctx.initialized:
-                dist.all_reduce(self.pack)
+                dist.all_reduce(self.pack, group=self.group)
             self.totals += self.pack
             closed.zero_()
             if self.done is not None:
@@ -171,15 +184,28 @@ class EpochPipeline:
         self.reducer = reducer
         self.pending = None          # (buffer, flip_count, lat_delta)
 
-    def tick(self, lat_delta=None) -> None:
-        if self.pending is not None and self.engine.epoch_complete(self.pending[1]):
+    def tick(self, lat_delta=None, progress=None, timeout_s: float = 30.0) -> None:
+        """One X2 step.  Every call performs exactly ONE collective (the reduction of the
+        previously closed epoch), so ranks that tick the same number of times stay paired
+        whatever their timing: if that epoch has not completed yet, ``progress()`` (e.g.
+        ``engine.run(0, flush)``, which retires finished micro-batches) is driven until it
+        has -- one epoch of slack makes this wait empty in steady state."""
+        self.ticks = getattr(self, "ticks", 0) + 1
+        if self.pending is not None:
+            if not self.engine.epoch_complete(self.pending[1]):
+                import time as _t
+                t0 = _t.monotonic()
+                while not self.engine.epoch_complete(self.pending[1]):
+                    if progress is not None:
+                        progress()
+                    if _t.monotonic() - t0 > timeout_s:
+                        raise TimeoutError("epoch did not complete: engine stalled")
             self.reducer.submit(self.pending[0], self.pending[2])
             self.pending = None
-        if self.pending is None:
-            if self.reducer.done is not None:
-                self.reducer.done.synchronize()
-            buf = self.engine.flip_epoch(self.reducer.side)
-            self.pending = (buf, self.engine.flips, lat_delta)
+        if self.reducer.done is not None:
+            self.reducer.done.synchronize()
+        buf = self.engine.flip_epoch(self.reducer.side)
+        self.pending = (buf, self.engine.flips, lat_delta)
 
     def finish(self) -> None:
         """Call after the engine has drained: reduce the last closed AND the open epoch."""

@@ -30,8 +30,9 @@ from .dp import DistContext, broadcast_blob
 
 
 class HotSwap:
-    def __init__(self, ctx: DistContext, engine, watch_path: Optional[str] = None, src: int = 0):
+    def __init__(self, ctx: DistContext, engine, watch_path: Optional[str] = None, src: int = 0, group=None):
         self.ctx = ctx
+        self.group = group
         self.engine = engine
         self.src = src
         self.version = 0
@@ -72,13 +73,13 @@ class HotSwap:
             hdr[0] = self.version + 1
             hdr[1] = len(blob)
         if self.ctx.initialized:
-            dist.broadcast(hdr, self.src)
+            dist.broadcast(hdr, self.src, group=self.group)
         new_version, nbytes = int(hdr[0].item()), int(hdr[1].item())
         if new_version <= self.version:
             return False
         t = (torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).to(dev)
              if self.ctx.rank == self.src else None)
-        t = broadcast_blob(self.ctx, t, self.src)
+        t = broadcast_blob(self.ctx, t, self.src, group=self.group)
         if t.numel() != nbytes:
             raise RuntimeError("hot swap: blob size mismatch after broadcast")
         self._swap(t)
