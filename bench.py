@@ -161,7 +161,7 @@ def main(argv=None):
         flagged_total += len(eng.drain_flagged())
         # X2/X3: flip the counter epoch; the previously closed epoch (all of whose batches
         # have completed by now) is all-reduced over RCCL on the side stream
-        epochs.tick()
+        epochs.tick(progress=lambda: eng.run(0, 0))   # (retire finished batches if it must wait)
 
     for _ in range(args.warmup):
         step(drain=False)
