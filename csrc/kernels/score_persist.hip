@@ -7,8 +7,9 @@
 //                                                   polls host memory with relaxed system-
 //                                                   scope loads; s_sleep back-off)
 //   read descriptor b % R from the device mirror    -> LDS
-//   4 waves x 4 tiles x 16 rows = rows [256c, 256c+256), next tile prefetched while the
-//   current one computes, scored with the same fused math as the
+//   4 waves x T tiles x 16 rows (item = 64T rows; default T = 8, CCFD_PERSIST_ITEM_ROWS),
+//   next tile prefetched while the current one computes (f32 rows via a wave-private LDS
+//   tile, W64 rows straight into registers), scored with the same fused math as the
 //   per-batch kernels (mlp_core.h), outputs written straight to host-mapped memory,
 //   fraud rows appended to the descriptor's compacted flag list
 //   counters + amount histogram -> counters[desc.epoch] (one atomic set per item)

@@ -52,3 +52,64 @@ def test_engine_service_end_to_end(gpu, score_thread):
     assert c[0] == total and c[1] == nf
     assert lat.sum() > 0
     svc.stop()
+
+
+def test_engine_service_native_kafka_ingest_and_hot_swap(gpu, tmp_path):
+    """kafka-lite (Kafka wire protocol) -> native C++ consumer -> W64 rings -> GPU, and a
+    runtime hot swap triggered by rewriting the watched safetensors file mid-stream."""
+    from ccfd_demo_summit_amd.ingest import ProducerConfig, TransactionProducer
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
+    from ccfd_demo_summit_amd.metrics import MetricsHub
+    from ccfd_demo_summit_amd.models import save_model
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import DistContext
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    from ccfd_demo_summit_amd.router import Router, RuleSet
+
+    X, _ = generate(50_000, seed=1)
+    m1 = build_model("mlp", seed=3, X_ref=X, calibrate_rate=0.01)
+    m2 = build_model("mlp", seed=4, X_ref=X, calibrate_rate=0.05)
+    path = str(tmp_path / "model.safetensors")
+    save_model(m1, path)
+    lite = KafkaLiteServer("127.0.0.1", 0, default_partitions=2).start_in_thread()
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 2)
+    TransactionProducer(kb, ProducerConfig(fmt="txb1", batch=4000, seed=5)).produce(24_000)
+    hub = MetricsHub()
+    procs = ProcessEngine(notification_timeout_s=60)
+    router = Router(RuleSet.threshold(0.5), procs, hub.router)
+    ctx = DistContext(0, 1, 0, gpu, "none")
+    svc = EngineService(ctx, DeviceModel(m1, gpu, wire=True), kb, router,
+                        EngineServiceConfig(batch=4096, depth=8, streams=2, ring_rows=1 << 16, flush_us=200,
+                                            reduce_period_ms=1.0, model_watch=path)).start()
+    try:
+        assert svc.native is not None
+        t0 = time.time()
+        while svc.rows_scored < 24_000 and time.time() - t0 < 60:
+            svc.step()
+        assert svc.rows_scored == 24_000
+        import os
+        save_model(m2, path)
+        os.utime(path, (time.time() + 10, time.time() + 10))
+        t0 = time.time()
+        while svc.hotswap.version < 1 and time.time() - t0 < 30:
+            svc.step()
+        assert svc.hotswap.version == 1 and svc.engine.model_version == 1
+        TransactionProducer(kb, ProducerConfig(fmt="txb1", batch=4000, seed=9)).produce(8_000)
+        t0 = time.time()
+        while svc.rows_scored < 32_000 and time.time() - t0 < 60:
+            svc.step()
+        assert svc.rows_scored == 32_000
+        for _ in range(20):
+            svc.step()
+        assert kb.lag("ccfd-engine", "odh-demo") == 0          # offsets committed after scoring
+        svc.flush_epochs()
+        c, _ = svc.reducer.snapshot()
+        assert c[0] == 32_000
+        assert svc.native.stats()["errors"] == 0
+    finally:
+        svc.stop()
+        kb.close()
+        lite.stop()
