@@ -451,7 +451,7 @@ class Engine {
     if (s.use_flag) {
       nf = s.done_ptr[1];
       if (nf) push_flagged_idx(s, nf);
-      if (!persistent) {                               // K7: device-clock execution window
+      {                                                // K7: device-clock execution window
         const uint64_t t0d = s.done_ptr[2], t1d = s.done_ptr[3];
         if (t1d > t0d && wall_ns_per_tick > 0) {
           const double dns = (double)(t1d - t0d) * wall_ns_per_tick;

@@ -114,7 +114,7 @@ typedef struct ccfd_persist_desc {   // host-coherent pinned, written before `po
 typedef struct ccfd_persist_ctl {    // host-coherent pinned
   uint64_t posted;         // host -> GPU: number of descriptors published
   uint64_t stop;           // host -> GPU: exit once every posted batch is claimed
-  uint64_t done[CCFD_PERSIST_MAX_RING][2];   // GPU -> host: {seq + 1, #flagged} per ring slot
+  uint64_t done[CCFD_PERSIST_MAX_RING][4];   // GPU -> host: {seq + 1, #flagged, t_start, t_end} per ring slot
   uint64_t exited;         // GPU -> host: workgroups that left the loop
 } ccfd_persist_ctl;
 
@@ -126,6 +126,7 @@ typedef struct ccfd_persist_dev {    // device memory
   unsigned int remaining[CCFD_PERSIST_MAX_RING];  // items left per ring slot
   unsigned int nflag[CCFD_PERSIST_MAX_RING];      // flagged rows per ring slot
   ccfd_persist_desc desc[CCFD_PERSIST_MAX_RING];  // device mirror of the descriptor ring
+  unsigned long long tstart[CCFD_PERSIST_MAX_RING];  // K7: device clock when item 0 was claimed
 } ccfd_persist_dev;
 
 typedef struct ccfd_persist_args {

@@ -14,7 +14,7 @@
 //   fraud rows appended to the descriptor's compacted flag list
 //   counters + amount histogram -> counters[desc.epoch] (one atomic set per item)
 //   release (system scope) + ticket on remaining[b % R]; the last ticket publishes
-//   ctl->done[b % R] = {b + 1, #flagged}
+//   ctl->done[b % R] = {b + 1, #flagged, t_start, t_end}
 // A workgroup only waits for the HOST (never for another workgroup), so residency of the
 // whole grid is not required and nothing can deadlock; it exits when the host sets `stop`
 // while it waits for an unposted batch.  The host never posts batch b into ring slot
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   float* tile_lds = sx[wave];
   unsigned long long posted_cache = 0;     // thread 0 only
 
-  // Workgroup 0 is the DOORBELL: its thread 0 alone polls host memory (ctl->posted/stop)
+  // Workgroup 0 is the DOORBELL: its first wave alone polls host memory (ctl->posted/stop)
   // and mirrors new descriptors + the posted count into device memory.  Every other
   // workgroup polls only the device mirror: hundreds of workgroups polling host memory
   // would each hold PCIe read requests and starve the feature stream (measured: 2x grid
@@ -156,6 +156,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     const float* x = sdesc.x;
     const int kTilesPerWave = a.tiles_per_wave;
     const int tile0 = chunk * (4 * kTilesPerWave) + wave;      // wave w: tiles tile0 + 4k
+    if (chunk == 0 && tid == 0)                                // K7: micro-batch start (item 0 claimed first)
+      __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     auto avail = [&](int t) { return min(kTileRows, n - t * kTileRows) * kF * 4; };
     TileRegs pre;
     WireRegs wpre;
@@ -258,6 +260,10 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
         __hip_atomic_store(&a.dev->nflag[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.dev->remaining[slot], (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&a.ctl->done[slot][1], (unsigned long long)nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ctl->done[slot][2],
+                           __hip_atomic_load(&a.dev->tstart[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ctl->done[slot][3], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.ctl->done[slot][0], sdesc.seq + 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
