@@ -49,6 +49,8 @@ def _bind(L):
     L.ccfd_kc_get_stats.restype = None
     L.ccfd_kc_last_error.argtypes = [C.c_void_p]
     L.ccfd_kc_last_error.restype = C.c_char_p
+    L.ccfd_kc_feed_record_set.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    L.ccfd_kc_feed_record_set.restype = C.c_int64
     L._kc_bound = True
     return L
 
@@ -126,6 +128,10 @@ class NativeKafkaConsumer:
 
     def last_error(self) -> str:
         return (lib().ccfd_kc_last_error(C.c_void_p(self.h)) or b"").decode(errors="replace")
+
+    def feed(self, record_set: bytes) -> int:
+        """Parse ``record_set`` as partition 0's fetched bytes (array sink, no socket)."""
+        return int(lib().ccfd_kc_feed_record_set(C.c_void_p(self.h), record_set, len(record_set)))
 
     def committable(self) -> Dict[int, int]:
         """partition -> next offset to commit (only partitions that advanced)."""

@@ -261,7 +261,10 @@ class Consumer {
       if (off_f + 120ull * n > (size_t)vlen) return false;
       const uint8_t* ids = v + off_ids;
       const uint8_t* cu = v + off_cu;
-      const float* f = reinterpret_cast<const float*>(v + off_f);   // 16-B aligned within value
+      // 16-B aligned within the TXB1 value, but the value itself sits at an arbitrary offset
+      // of the fetch buffer: address rows as bytes (UBSan caught the typed-pointer version)
+      const uint8_t* f = v + off_f;
+      constexpr size_t kRow = CCFD_N_FEATURES * sizeof(float);
       const int rb = row_bytes();
       const bool ok = write_rows(pi, n, [&](int64_t row, int64_t s, int64_t k) {
         std::memcpy(sink->ids(pi) + row, ids + 8 * s, 8 * k);
@@ -270,11 +273,11 @@ class Consumer {
         if (wire) {
           float tmp[CCFD_N_FEATURES];
           for (int64_t i = 0; i < k; ++i) {
-            std::memcpy(tmp, f + (s + i) * CCFD_N_FEATURES, sizeof(tmp));   // value may be unaligned
+            std::memcpy(tmp, f + (size_t)(s + i) * kRow, sizeof(tmp));
             ccfd::encode_w64_row(tmp, dst + i * rb);
           }
         } else {
-          std::memcpy(dst, f + s * CCFD_N_FEATURES, (size_t)k * rb);
+          std::memcpy(dst, f + (size_t)s * kRow, (size_t)k * rb);
         }
       });
       *rows_out = ok ? n : 0;
@@ -490,5 +493,15 @@ void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out) {
 }
 
 const char* ccfd_kc_last_error(void* kc) { return static_cast<Consumer*>(kc)->last_err.c_str(); }
+
+// Fuzz / unit entry: feed raw bytes as partition 0's record set of an array-sink consumer
+// (no socket).  Returns records accepted.  Used by tests/test_native_cpu.py under ASan.
+int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n) {
+  auto* c = static_cast<Consumer*>(kc);
+  if (!c || c->ps.empty() || !data || n < 0) return -1;
+  const uint64_t before = c->n_records.load();
+  c->ingest_record_set(0, data, data + n);
+  return (int64_t)(c->n_records.load() - before);
+}
 
 }  // extern "C"

@@ -281,6 +281,7 @@ void ccfd_kc_destroy(void* kc);
 int64_t ccfd_kc_committable(void* kc, int part_index);
 void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out);
 const char* ccfd_kc_last_error(void* kc);
+int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n);   // tests / fuzzing
 
 #ifdef __cplusplus
 }

@@ -135,6 +135,19 @@ def test_host_runtime_under_asan(tmp_path):
         "while kc.stats()['records'] < 51 and time.time() - t0 < 20: time.sleep(0.01)\n"
         "assert kc.stats()['records'] == 51, kc.stats()\n"
         "kc.stop(); kc.close(); kb.close(); srv.stop()\n"
+        "# fuzz the RecordBatch/TXB1/JSON parsers with truncated and bit-flipped record sets\n"
+        "from ccfd_demo_summit_amd.ingest.kafka_wire import encode_record_batch\n"
+        "good = encode_record_batch([TxBatch(ids=np.arange(64, dtype=np.uint64), customer=np.zeros(64, np.uint32), features=X[:64]).encode()] + msgs[:20], [None] * 21, base_offset=0)\n"
+        "fz = NativeKafkaConsumer.for_arrays('127.0.0.1:1', 't', {0: 0}, capacity=100000, wire=False)\n"
+        "assert fz.feed(good) == 21\n"
+        "r = np.random.default_rng(1)\n"
+        "for it in range(3000):\n"
+        "    b = bytearray(good)\n"
+        "    for _ in range(int(r.integers(1, 8))): b[int(r.integers(0, len(b)))] = int(r.integers(0, 256))\n"
+        "    cut = int(r.integers(0, len(b) + 1)) if it % 3 == 0 else len(b)\n"
+        "    fz.feed(bytes(b[:cut]))\n"
+        "    fz.feed(bytes(r.integers(0, 256, int(r.integers(0, 300)), dtype=np.uint8)))\n"
+        "fz.close()\n"
         "print('asan probe ok')\n")
     env = dict(os.environ, CCFD_SANITIZE="address,undefined", LD_PRELOAD=rt, CCFD_NO_AUTOBUILD="1",
                ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
