@@ -73,8 +73,15 @@ class Router:
         self.metrics.tx_incoming.inc(total_rows)
         self.metrics.tx_outgoing.labels(type="fraud").inc(nf)
         self.metrics.tx_outgoing.labels(type="standard").inc(total_rows - nf)
-        for r in flagged:
-            self._start_fraud(int(r["tx_id"]), int(r["customer"]), float(r["amount"]), float(r["proba"]))
+        many = getattr(self.processes, "start_fraud_many", None)
+        if many is not None and nf > 1:                     # one hand-off for the whole step
+            many([{"transaction_id": int(r["tx_id"]), "customer_id": int(r["customer"]),
+                   "amount": float(r["amount"]), "proba": float(r["proba"])} for r in flagged])
+            with self._lock:
+                self.fraud_started += nf
+        else:
+            for r in flagged:
+                self._start_fraud(int(r["tx_id"]), int(r["customer"]), float(r["amount"]), float(r["proba"]))
         return {"incoming": total_rows, "fraud": nf, "standard": total_rows - nf}
 
     def _start_fraud(self, tx_id: int, customer: int, amount: float, proba: float) -> None:

@@ -75,7 +75,7 @@ def test_engine_score_sync_pageable_input(gpu, setup):
     eng.close()
 
 
-@pytest.mark.parametrize("exec_mode", ["launch", "persistent", "launch-wire", "launch-wire-c4"])
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent", "launch-wire", "launch-wire-c4", "persistent-wire"])
 def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     """Live ingest: producer writes into the pinned SPSC ring (rows + JSON), run() scores full
     micro-batches and deadline-flushes the partial tail; ring space is recycled."""

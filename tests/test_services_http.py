@@ -106,4 +106,13 @@ def test_kie_rest_lifecycle():
             assert r.status == 404
             text = await (await cl.get("/rest/metrics")).text()
             assert "fraud_investigation_amount_count 1.0" in text
+            # batch start (engine router hand-off): one request, idempotent per transaction id
+            items = [{"transaction_id": 100 + i, "customer_id": i, "amount": 1.0, "proba": 0.9} for i in range(5)]
+            r = await cl.post(f"{BASE}/containers/{c}/processes/ccd-fraud-kjar.CCDProcess/instances/batch", json=items)
+            assert r.status == 201
+            ids = await r.json()
+            assert len(set(ids)) == 5
+            r = await cl.post(f"{BASE}/containers/{c}/processes/ccd-fraud-kjar.CCDProcess/instances/batch",
+                              json=items[:2])
+            assert await r.json() == ids[:2]                 # duplicates return the same instances
     _run(go())
