@@ -121,3 +121,33 @@ def test_end_to_end_pipeline_counters_match_cpu_truth(fmt):
                  "fraud_rejected_amount_bucket", "proba_1", "V17", "V10", "Amount"):
         assert name in text, name
     pipe.close()
+
+
+def test_router_batches_fraud_hand_off_when_supported():
+    """Engine path: all fraud-routed rows of a step go to KIE in ONE call when the process
+    sink offers start_fraud_many (KieClient's /instances/batch)."""
+    import numpy as np
+    from ccfd_demo_summit_amd.metrics import RouterMetrics
+    from ccfd_demo_summit_amd.ops._lib import FLAGGED_DTYPE
+    from ccfd_demo_summit_amd.router import Router, RuleSet
+
+    class Sink:
+        def __init__(self):
+            self.calls = []
+
+        def start_fraud_many(self, items):
+            self.calls.append(items)
+            return list(range(len(items)))
+
+        def start_fraud(self, v):
+            raise AssertionError("per-row start must not be used")
+
+    sink = Sink()
+    r = Router(RuleSet.threshold(0.5), sink, RouterMetrics())
+    fl = np.zeros(3, dtype=np.dtype(FLAGGED_DTYPE))
+    fl["tx_id"] = [7, 8, 9]
+    fl["proba"] = 0.9
+    res = r.on_flagged(fl, 1000)
+    assert res == {"incoming": 1000, "fraud": 3, "standard": 997}
+    assert len(sink.calls) == 1 and [c["transaction_id"] for c in sink.calls[0]] == [7, 8, 9]
+    assert r.fraud_started == 3
