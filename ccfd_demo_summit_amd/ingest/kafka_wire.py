@@ -271,8 +271,19 @@ def _recv_exact(sock: socket.socket, n: int) -> bytes:
 
 
 class Connection:
-    def __init__(self, host: str, port: int, client_id: str = "ccfd-mi355x", timeout: float = 10.0):
-        self.sock = socket.create_connection((host, port), timeout=timeout)
+    def __init__(self, host: str, port: int, client_id: str = "ccfd-mi355x", timeout: float = 10.0,
+                 connect_wait_s: float = 0.0):
+        """``connect_wait_s``: keep retrying a refused connection this long (services start in
+        any order, like pods waiting for the broker)."""
+        deadline = time.monotonic() + connect_wait_s
+        while True:
+            try:
+                self.sock = socket.create_connection((host, port), timeout=timeout)
+                break
+            except (ConnectionRefusedError, socket.timeout, OSError):
+                if time.monotonic() >= deadline:
+                    raise
+                time.sleep(0.25)
         self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self.client_id = client_id
         self._corr = itertools.count(1)
@@ -302,7 +313,8 @@ class KafkaBroker:
     """Kafka-protocol implementation of the InProcBroker interface (single bootstrap node;
     partition leaders are looked up from Metadata and connected lazily)."""
 
-    def __init__(self, bootstrap: str, client_id: str = "ccfd-mi355x", timeout: float = 10.0):
+    def __init__(self, bootstrap: str, client_id: str = "ccfd-mi355x", timeout: float = 10.0,
+                 connect_wait_s: float = 0.0):
         host, port = bootstrap.rsplit(":", 1)
         self.timeout = timeout
         self.client_id = client_id
@@ -311,7 +323,7 @@ class KafkaBroker:
         self._nodes: Dict[int, Tuple[str, int]] = {}
         self._leaders: Dict[Tuple[str, int], int] = {}
         self._partitions: Dict[str, int] = {}
-        self._boot = Connection(host, int(port), client_id, timeout)
+        self._boot = Connection(host, int(port), client_id, timeout, connect_wait_s=connect_wait_s)
         self._rr = itertools.count()
         self.api_versions = self._api_versions()
 

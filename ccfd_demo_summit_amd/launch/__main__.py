@@ -35,7 +35,7 @@ def _broker(cfg, inproc=None):
     if inproc is not None:
         return inproc
     from ..ingest.kafka_wire import KafkaBroker
-    return KafkaBroker(cfg.kafka.broker_url)
+    return KafkaBroker(cfg.kafka.broker_url, connect_wait_s=120.0)   # wait for the broker to come up
 
 
 def _model(kind: str, weights: str = None, seed: int = 0):
@@ -281,7 +281,14 @@ def cmd_supervise(a, cfg):
     sys.exit(supervise(a.cmd, max_restarts=a.max_restarts, backoff_s=a.backoff))
 
 
-def main(argv=None):
+def parse_args(argv=None) -> argparse.Namespace:
+    """Service name, options (before or after it), and for ``supervise`` the child command
+    after ``--``."""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = []
+    if "--" in argv:
+        i = argv.index("--")
+        argv, cmd = argv[:i], argv[i + 1:]
     ap = argparse.ArgumentParser(prog="python -m ccfd_demo_summit_amd.launch", description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
@@ -304,10 +311,13 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=4096)
     ap.add_argument("--max-restarts", type=int, default=10)
     ap.add_argument("--backoff", type=float, default=1.0)
-    ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
-    if a.cmd and a.cmd[0] == "--":
-        a.cmd = a.cmd[1:]
+    a.cmd = cmd
+    return a
+
+
+def main(argv=None):
+    a = parse_args(argv)
     cfg = load_config(a.config)
     globals()["cmd_" + a.service.replace("-", "_")](a, cfg)
 

@@ -84,7 +84,15 @@ def main(argv=None):
     result = {"ok": False}
     try:
         start("kafka", "kafka-lite", "--host", "127.0.0.1", "--port", str(kport))
-        time.sleep(2.0)
+        t0 = time.time()
+        while True:                                       # broker accepting connections
+            try:
+                socket.create_connection(("127.0.0.1", kport), timeout=1).close()
+                break
+            except OSError:
+                if time.time() - t0 > 180:
+                    raise
+                time.sleep(0.2)
         start("kie", "kie", "--host", "127.0.0.1", "--port", str(kie_port))
         start("notifier", "notifier", "--host", "127.0.0.1", "--port", str(notif_port))
         wait_http(f"http://127.0.0.1:{kie_port}/rest/metrics")

@@ -40,3 +40,13 @@ def test_launch_help_and_demo():
                          capture_output=True, text=True, env=env, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert '"consumed"' in out.stdout
+
+
+def test_launch_options_after_service_name_are_parsed():
+    from ccfd_demo_summit_amd.launch.__main__ import parse_args
+    a = parse_args(["engine", "--port", "18091", "--host", "127.0.0.1", "--watch-model", "m.safetensors"])
+    assert (a.service, a.port, a.host, a.watch_model, a.cmd) == ("engine", 18091, "127.0.0.1", "m.safetensors", [])
+    a = parse_args(["--port", "1", "kafka-lite"])
+    assert a.port == 1 and a.service == "kafka-lite"
+    a = parse_args(["supervise", "--max-restarts", "3", "--", "python", "-c", "print(1)", "--port", "9"])
+    assert a.max_restarts == 3 and a.cmd == ["python", "-c", "print(1)", "--port", "9"] and a.port is None
