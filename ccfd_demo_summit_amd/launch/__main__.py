@@ -174,6 +174,7 @@ def cmd_router(a, cfg):
     _serve_in_thread(_metrics_app(rm.expose), a.host, a.port or cfg.router.port)
     tx = broker.consumer(cfg.kafka.group_id, [cfg.kafka.transactions_topic])
     resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic])
+    notif = broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
     while True:
         recs = tx.poll(timeout=0.05, max_records=a.max_batch)
         if recs:
@@ -183,8 +184,10 @@ def cmd_router(a, cfg):
             tx.commit()
         for r in resp.poll(max_records=10_000):
             router.on_response(r.value)
-            rm.notif_outgoing.inc(0)
         resp.commit()
+        for r in notif.poll(max_records=10_000):
+            router.on_notification_sent(r.value)
+        notif.commit()
 
 
 def cmd_engine(a, cfg):
@@ -230,6 +233,9 @@ def cmd_engine(a, cfg):
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.rank)
     resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic]) if ctx.rank == 0 else None
+    # the router also watches the notification topic KIE publishes to (router.yaml:57-58)
+    notif = (broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
+             if ctx.rank == 0 else None)
     print(f"[engine] rank {ctx.rank}/{ctx.world} partitions {svc.partitions}", flush=True)
     try:
         while True:
@@ -238,6 +244,9 @@ def cmd_engine(a, cfg):
                 for r in resp.poll(max_records=10_000):
                     router.on_response(r.value)
                 resp.commit()
+                for r in notif.poll(max_records=10_000):
+                    router.on_notification_sent(r.value)
+                notif.commit()
     finally:
         svc.stop()
 

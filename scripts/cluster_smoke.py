@@ -100,12 +100,18 @@ def main(argv=None):
         wait_http(f"http://127.0.0.1:{eng_port}/prometheus", timeout=300)
         start("producer", "producer", "--fmt", "txb1", "--batch", "4096", "--count", str(a.count))
         t0 = time.time()
-        sent = a.count
+        sent = None                                       # producer rounds up to whole batches
         got = 0.0
         while time.time() - t0 < a.seconds + 60:
+            if sent is None and procs["producer"].poll() is not None:
+                for line in (logs / "producer.log").read_text().splitlines():
+                    if line.startswith("{") and '"produced"' in line:
+                        sent = int(json.loads(line)["produced"])
+                if sent is None:
+                    raise RuntimeError("producer exited without a report")
             m = scrape(f"http://127.0.0.1:{eng_port}/prometheus")
             got = m.get("transaction_incoming_total", 0.0)
-            if got >= sent:
+            if sent is not None and got >= sent:
                 break
             if procs["engine"].poll() is not None:
                 raise RuntimeError("engine exited")
@@ -115,7 +121,10 @@ def main(argv=None):
         em = scrape(f"http://127.0.0.1:{eng_port}/prometheus")
         km = scrape(f"http://127.0.0.1:{kie_port}/rest/metrics")
         result = {
-            "ok": em.get("transaction_incoming_total", 0.0) == sent,
+            "ok": (sent is not None and em.get("transaction_incoming_total", 0.0) == sent
+                   and em.get('transaction_outgoing_total{type="fraud"}', 0.0) > 0
+                   and em.get("notifications_outgoing_total", 0.0) > 0
+                   and km.get("fraud_approved_amount_count", 0.0) + km.get("fraud_rejected_amount_count", 0.0) > 0),
             "sent": sent, "scored": em.get("transaction_incoming_total"), "seconds": round(dt, 2),
             "fraud_routed": em.get('transaction_outgoing_total{type="fraud"}'),
             "notifications_outgoing": em.get("notifications_outgoing_total"),
