@@ -84,12 +84,14 @@ class EngineService:
         else:
             self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
                 if hasattr(broker, "_boot") else _StaticInProcConsumer(broker, cfg.group_id, cfg.topic, self.partitions)
-        # the scoring thread's collectives (X2 epochs, hot swap, flush) use their own group
+        # the scoring thread's collectives (X2 epochs + hot-swap header, blob broadcast) use
+        # their own group; the flush agreement uses a third one (see flush_epochs)
         self.group = x_group(ctx)
+        self.ctl_group = x_group(ctx)
         self.reducer = reducer or CounterReducer(ctx, ctx.device, group=self.group)
-        self.epochs = EpochPipeline(self.engine, self.reducer)
         from ..parallel.hotswap import HotSwap
         self.hotswap = HotSwap(ctx, self.engine, cfg.model_watch, group=self.group)
+        self.epochs = EpochPipeline(self.engine, self.reducer, ctrl=self.hotswap)
         # per partition: (ring row end, next kafka offset) of ingested messages, oldest first
         self._pending: Dict[int, Deque[Tuple[int, int]]] = {p: collections.deque() for p in self.partitions}
         self._rows_in: Dict[int, int] = {p: 0 for p in self.partitions}
@@ -180,16 +182,19 @@ class EngineService:
                 self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
         return int(st.rows)
 
-    def _reduce(self, lat_cum: np.ndarray) -> None:
+    def _reduce(self, lat_cum: np.ndarray, block: bool = False) -> bool:
         delta = lat_cum - self._lat_prev                # cumulative since reset -> send the delta
         if (delta < 0).any():                           # stats were reset in between
             delta = lat_cum
-        # one collective per tick on every rank; waiting for the closed epoch keeps
-        # retiring micro-batches on this (the scoring) thread
-        self.epochs.tick(delta, progress=lambda: self._run_once(0))
-        self._lat_prev = lat_cum
-        self.hotswap.tick()                             # collective: X1 at runtime
+        # at most one collective per tick, never waiting for a slower rank (block=False: the
+        # tick is skipped while the previous reduction is still in flight); waiting for the
+        # closed epoch keeps retiring micro-batches on this (the scoring) thread
+        ok = self.epochs.tick(delta, progress=lambda: self._run_once(0), block=block)
+        if ok:
+            self._lat_prev = lat_cum
+        self.hotswap.poll()                             # runtime X1: swap once the blob landed
         self._reduce_pending = False
+        return ok
 
     def _score_loop(self) -> None:
         try:
@@ -269,18 +274,20 @@ class EngineService:
         of epoch ticks any of them has done and catch up, so every collective stays paired
         even though ticks are scheduled by each rank's own clock."""
         def _do():
-            n = getattr(self.epochs, "ticks", 0)
             if self.ctx.initialized:
                 import torch
                 import torch.distributed as dist
-                t = torch.tensor([n], dtype=torch.int64, device=self.ctx.device)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                # the tick count is agreed on the control group: the X-group may still carry
+                # this rank's last (async) reduction, which a MAX there would pair against
+                t = torch.tensor([self.epochs.ticks], dtype=torch.int64, device=self.ctx.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctl_group)
                 target = int(t.item())
-                while getattr(self.epochs, "ticks", 0) < target:
+                while self.epochs.ticks < target:       # every rank is here: blocking is safe
                     with self._stat_lock:
                         lat = self._lat_cum
-                    self._reduce(lat)
-            self.epochs.finish()
+                    self._reduce(lat, block=True)
+            self.epochs.finish(progress=lambda: self._run_once(0))
+            self.hotswap.poll(block=True)
         self._on_engine_thread(_do)
 
     def latency_hist(self) -> np.ndarray:

@@ -1,6 +1,6 @@
 """Multi-GPU data parallelism (one process per GPU, RCCL over xGMI)."""
 from .dp import (CounterReducer, DistContext, EpochPipeline, all_max, all_sum, assign_partitions, barrier,
-                 broadcast_blob, hist_quantile, init_distributed)
+                 broadcast_blob, hist_quantile, init_distributed, x_group)
 
 __all__ = ["CounterReducer", "DistContext", "EpochPipeline", "all_max", "all_sum", "assign_partitions", "barrier",
-           "broadcast_blob", "hist_quantile", "init_distributed"]
+           "broadcast_blob", "hist_quantile", "init_distributed", "x_group"]

@@ -118,56 +118,101 @@ def _checksum(blob: torch.Tensor) -> torch.Tensor:
     return torch.stack([b.sum(), (b * (idx % 65521 + 1)).sum()])
 
 
+N_CTRL_SLOTS = 4      # control words carried by the same all-reduce (hot-swap header)
+_K = N_COUNTER_SLOTS + N_LAT_BUCKETS
+
+
 class CounterReducer:
     """X2/X3: periodic all-reduce of epoch counter buffers + latency histograms.
 
-    ``submit(closed, lat_hist)`` enqueues on the side stream: copy the latency histogram
-    next to the counters, all-reduce (sum) the packed vector, accumulate into ``totals``
-    and zero the epoch buffer for reuse.  Nothing here blocks the host on GPU backends."""
+    ``submit(closed, lat_hist, ctrl)`` enqueues on the side stream: copy the counters, the
+    latency histogram and ``N_CTRL_SLOTS`` control words into one packed vector, zero the
+    closed epoch buffer (event ``freed``: a LOCAL dependency only), then start the all-reduce
+    (sum) ASYNCHRONOUSLY.  ``complete()`` folds the result into ``totals``; ``busy()`` says
+    whether the reduction is still waiting for other ranks.  Nothing here makes the host wait
+    for a remote rank unless it asks to (``complete()`` on a busy reducer)."""
 
     def __init__(self, ctx: DistContext, device: torch.device, priority: int = 0, group=None):
         self.ctx = ctx
         self.device = device
         self.group = group
-        self.totals = torch.zeros(N_COUNTER_SLOTS + N_LAT_BUCKETS, dtype=torch.int64, device=device)
+        self.totals = torch.zeros(_K, dtype=torch.int64, device=device)
         self.local_totals = torch.zeros_like(self.totals)
-        self.pack = torch.zeros_like(self.totals)
+        self.pack = torch.zeros(_K + N_CTRL_SLOTS, dtype=torch.int64, device=device)
         self.side = torch.cuda.Stream(device, priority=priority) if device.type == "cuda" else None
         self.done = torch.cuda.Event() if device.type == "cuda" else None
+        self.freed = torch.cuda.Event() if device.type == "cuda" else None
         self.epochs = 0
+        self._work = None
+        self.last_ctrl: Optional[torch.Tensor] = None     # reduced control words of the last completion
 
-    def submit(self, closed: torch.Tensor, lat_hist: Optional[np.ndarray] = None) -> None:
+    def busy(self) -> bool:
+        return self._work is not None and not self._work.is_completed()
+
+    def submit(self, closed: torch.Tensor, lat_hist: Optional[np.ndarray] = None,
+               ctrl: Optional[np.ndarray] = None) -> None:
+        self.complete()                                  # at most one reduction in flight
         ctxm = torch.cuda.stream(self.side) if self.side is not None else _nullctx()
         with ctxm:
             self.pack[:N_COUNTER_SLOTS].copy_(closed, non_blocking=True)
-            if lat_hist is not None:
-                h = torch.from_numpy(np.asarray(lat_hist, np.int64))
+            for lo, hi, v in ((N_COUNTER_SLOTS, _K, lat_hist), (_K, _K + N_CTRL_SLOTS, ctrl)):
+                if v is None:
+                    self.pack[lo:hi].zero_()
+                    continue
+                h = torch.from_numpy(np.ascontiguousarray(v, np.int64))
                 if self.device.type == "cuda":
                     h = h.pin_memory()
-                self.pack[N_COUNTER_SLOTS:].copy_(h, non_blocking=True)
-            else:
-                self.pack[N_COUNTER_SLOTS:].zero_()
-            self.local_totals += self.pack
-            if self.ctx.initialized:
-                dist.all_reduce(self.pack, group=self.group)
-            self.totals += self.pack
+                self.pack[lo:hi].copy_(h, non_blocking=True)
+            self.local_totals += self.pack[:_K]
             closed.zero_()
-            if self.done is not None:
-                self.done.record(self.side)
+            if self.freed is not None:
+                self.freed.record(self.side)
+            if self.ctx.initialized:
+                self._work = dist.all_reduce(self.pack, group=self.group, async_op=True)
+            else:
+                self._fold()
         self.epochs += 1
 
+    def _fold(self) -> None:
+        self.totals += self.pack[:_K]
+        self.last_ctrl = self.pack[_K:].clone()
+        if self.done is not None:
+            self.done.record(self.side)
+
+    def complete(self) -> None:
+        """Fold the in-flight reduction into ``totals`` (blocks only if it is still running)."""
+        if self._work is None:
+            return
+        ctxm = torch.cuda.stream(self.side) if self.side is not None else _nullctx()
+        with ctxm:
+            self._work.wait()            # RCCL: the side stream waits; gloo: the host waits
+            self._work = None
+            self._fold()
+
+    def pop_ctrl(self) -> Optional[np.ndarray]:
+        if self.last_ctrl is None:
+            return None
+        if self.side is not None:
+            self.side.synchronize()
+        v, self.last_ctrl = self.last_ctrl.cpu().numpy(), None
+        return v
+
     def wait(self) -> None:
+        self.complete()
         if self.side is not None:
             self.side.synchronize()
 
     def snapshot(self):
-        """(global counters u64[64], global latency histogram u64[64]) as numpy."""
-        self.wait()
+        """(global counters u64[64], global latency histogram u64[256]) as numpy, as of the
+        last completed reduction (does not wait for one still in flight)."""
+        if self.side is not None:
+            self.side.synchronize()
         t = self.totals.cpu().numpy()
         return t[:N_COUNTER_SLOTS], t[N_COUNTER_SLOTS:]
 
     def local_snapshot(self):
-        self.wait()
+        if self.side is not None:
+            self.side.synchronize()
         t = self.local_totals.cpu().numpy()
         return t[:N_COUNTER_SLOTS], t[N_COUNTER_SLOTS:]
 
@@ -176,45 +221,78 @@ class EpochPipeline:
     """Drives X2 for one engine: flip the counter epoch, and hand the CLOSED buffer to the
     CounterReducer only once every micro-batch of that epoch has completed (in the
     persistent exec mode there is no per-batch event a stream could wait on, so the host
-    observes completion records instead).  Buffers alternate, so a flip also waits for the
-    previous reduction (one epoch of slack: never on the critical path in steady state)."""
+    observes completion records instead).  One epoch of slack: the epoch closed at tick i is
+    reduced at tick i+1, so the completion wait is empty in steady state.
 
-    def __init__(self, engine, reducer: CounterReducer):
+    Pairing rule (ranks tick on their own clocks): every tick that runs issues exactly one
+    collective (none on the first), and a rank never issues its next one before its previous
+    one completed -- so tick counts of any two ranks differ by at most one, and
+    ``tick(block=False)`` returns False instead of waiting when the previous reduction is
+    still waiting for a slower rank.  ``ctrl``: optional object with ``contribute() ->
+    int64[N_CTRL_SLOTS]`` and ``on_reduced(int64[N_CTRL_SLOTS])`` riding in the same
+    all-reduce (the hot-swap header, parallel/hotswap.py)."""
+
+    def __init__(self, engine, reducer: CounterReducer, ctrl=None):
         self.engine = engine
         self.reducer = reducer
+        self.ctrl = ctrl
         self.pending = None          # (buffer, flip_count, lat_delta)
+        self.ticks = 0
 
-    def tick(self, lat_delta=None, progress=None, timeout_s: float = 30.0) -> None:
-        """One X2 step.  Every call performs exactly ONE collective (the reduction of the
-        previously closed epoch), so ranks that tick the same number of times stay paired
-        whatever their timing: if that epoch has not completed yet, ``progress()`` (e.g.
-        ``engine.run(0, flush)``, which retires finished micro-batches) is driven until it
-        has -- one epoch of slack makes this wait empty in steady state."""
-        self.ticks = getattr(self, "ticks", 0) + 1
+    def _progress_until(self, cond, progress, timeout_s: float, what: str) -> None:
+        import time as _t
+        t0 = _t.monotonic()
+        while not cond():
+            if progress is not None:
+                progress()
+            if _t.monotonic() - t0 > timeout_s:
+                raise TimeoutError(what)
+
+    def _complete(self) -> None:
+        self.reducer.complete()
+        if self.ctrl is None:
+            self.reducer.last_ctrl = None
+            return
+        v = self.reducer.pop_ctrl()
+        if v is not None:
+            self.ctrl.on_reduced(v)
+
+    def tick(self, lat_delta=None, progress=None, timeout_s: float = 60.0, block: bool = True) -> bool:
+        """One X2 step; returns False (nothing done) when ``block`` is False and the previous
+        reduction has not completed yet."""
+        if self.reducer.busy():
+            if not block:
+                return False
+            self._progress_until(lambda: not self.reducer.busy(), progress, timeout_s,
+                                 "X2 all-reduce did not complete: a peer rank stopped ticking")
+        self._complete()
+        self.ticks += 1
         if self.pending is not None:
-            if not self.engine.epoch_complete(self.pending[1]):
-                import time as _t
-                t0 = _t.monotonic()
-                while not self.engine.epoch_complete(self.pending[1]):
-                    if progress is not None:
-                        progress()
-                    if _t.monotonic() - t0 > timeout_s:
-                        raise TimeoutError("epoch did not complete: engine stalled")
-            self.reducer.submit(self.pending[0], self.pending[2])
+            self._progress_until(lambda: self.engine.epoch_complete(self.pending[1]), progress, timeout_s,
+                                 "epoch did not complete: engine stalled")
+            ctrl = self.ctrl.contribute() if self.ctrl is not None else None
+            self.reducer.submit(self.pending[0], self.pending[2], ctrl)
             self.pending = None
-        if self.reducer.done is not None:
-            self.reducer.done.synchronize()
+            if self.reducer.freed is not None:
+                self.reducer.freed.synchronize()    # local: the buffer reopened below is zeroed
         buf = self.engine.flip_epoch(self.reducer.side)
         self.pending = (buf, self.engine.flips, lat_delta)
+        return True
 
-    def finish(self) -> None:
-        """Call after the engine has drained: reduce the last closed AND the open epoch."""
+    def finish(self, progress=None, timeout_s: float = 60.0) -> None:
+        """Call after the engine has drained (collective, same program point on every rank):
+        reduce the last closed AND the open epoch."""
+        self._complete()
         if self.pending is not None:
+            self._progress_until(lambda: self.engine.epoch_complete(self.pending[1]), progress, timeout_s,
+                                 "epoch did not complete: engine stalled")
             self.reducer.submit(self.pending[0], self.pending[2])
             self.pending = None
-        if self.reducer.done is not None:
-            self.reducer.done.synchronize()
+        self._complete()
+        if self.reducer.freed is not None:
+            self.reducer.freed.synchronize()
         self.reducer.submit(self.engine.flip_epoch(self.reducer.side), None)
+        self._complete()
         self.reducer.wait()
 
 

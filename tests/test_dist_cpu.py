@@ -39,6 +39,7 @@ def _worker(rank, world, port, q):
             c[1] = rank + 1
             red.submit(c, np.full(256, rank + 1, np.int64))
             assert int(c.sum()) == 0          # epoch buffer zeroed for reuse
+        red.wait()                            # fold the last (async) reduction
         g, lat = red.snapshot()
         q.put((rank, bytes(blob.numpy()), g[:2].tolist(), int(lat.sum())))
     finally:
@@ -144,3 +145,82 @@ def test_hot_swap_broadcasts_new_weights(tmp_path):
         assert got == [False, True, True, False], (rank, got)
         assert version == 2
         assert swapped == want
+
+
+class _FakeEpochEngine(_FakeEngine):
+    """CPU stand-in for the engine's epoch interface (two counter buffers, flip, completion)."""
+
+    def __init__(self):
+        super().__init__()
+        self.counters = [torch.zeros(64, dtype=torch.int64), torch.zeros(64, dtype=torch.int64)]
+        self.cur = 0
+        self.flips = 0
+
+    def flip_epoch(self, side=None):
+        closed, self.cur = self.cur, self.cur ^ 1
+        self.flips += 1
+        return self.counters[closed]
+
+    def epoch_complete(self, flip_count):
+        return True
+
+    def score(self, rows):
+        self.counters[self.cur][0] += rows
+
+
+def _skewed_worker(rank, world, port, q):
+    """Ranks tick on their own clocks (rank 0 five times, the others twice), then meet in a
+    main-group barrier -- the shape that deadlocked when a tick blocked on its all-reduce --
+    then flush: agree the tick count on a control group, catch up, finish."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.models import build_model
+    from ccfd_demo_summit_amd.parallel import CounterReducer, EpochPipeline, init_distributed, x_group
+    from ccfd_demo_summit_amd.parallel.hotswap import HotSwap
+    ctx = init_distributed(backend="gloo")
+    try:
+        xg, cg = x_group(ctx), x_group(ctx)
+        eng = _FakeEpochEngine()
+        hs = HotSwap(ctx, eng, group=xg)
+        red = CounterReducer(ctx, torch.device("cpu"), group=xg)
+        ep = EpochPipeline(eng, red, ctrl=hs)
+        if rank == 0:
+            hs.offer(build_model("mlp", seed=5))
+        ran = []
+        for _ in range(5 if rank == 0 else 2):
+            eng.score(100 * (rank + 1))
+            ran.append(ep.tick(block=False))
+            hs.poll()
+        dist.barrier()                                  # main thread meets the other ranks
+        t = torch.tensor([ep.ticks], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cg)
+        while ep.ticks < int(t):
+            ep.tick(block=True)
+        ep.finish()
+        hs.poll(block=True)
+        g, _ = red.snapshot()
+        q.put((rank, ran, int(g[0]), hs.version, eng.swapped))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_skewed_ticks_never_block_and_flush_pairs():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_skewed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    from ccfd_demo_summit_amd.models import build_model
+    truth = 5 * 100 + 2 * 200
+    for rank, ran, total, version, swapped in res:
+        assert total == truth, (rank, total)
+        assert version == 1 and swapped == [build_model("mlp", seed=5).pack()]
+    # rank 0 could not run ahead by more than one collective: later ticks were deferred
+    assert res[0][1][:2] == [True, True] and False in res[0][1]
