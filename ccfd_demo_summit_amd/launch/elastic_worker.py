@@ -15,11 +15,12 @@ from typing import Dict, Optional
 
 from ..ingest.codec import decode_records
 from ..parallel.elastic import PartitionLeases
+from ..utils.faults import FaultPlan
 
 
 class ElasticWorker:
     def __init__(self, rank: int, leases: PartitionLeases, broker, topic: str, scorer, router,
-                 group: str = "ccfd-engine", max_records: int = 4096):
+                 group: str = "ccfd-engine", max_records: int = 4096, faults: Optional[FaultPlan] = None):
         self.rank = rank
         self.leases = leases
         self.broker = broker
@@ -32,6 +33,8 @@ class ElasticWorker:
         self.counts: Dict[int, list] = {}
         self.alive = True
         self.scored_rows = 0
+        # injected faults (utils/faults.py; CCFD_FAULTS): drop / delay / crash this rank
+        self.faults = faults if faults is not None else FaultPlan.from_env(rank)
 
     def _adopt(self, p: int) -> None:
         off, rows, fraud = self.leases.committed(p)
@@ -46,6 +49,8 @@ class ElasticWorker:
         injection hook: score a batch, then die without committing it."""
         if not self.alive:
             return 0
+        if self.faults is not None:
+            self.faults.step()
         gained, lost = self.leases.tick()
         for p in gained:
             self._adopt(p)
@@ -59,6 +64,8 @@ class ElasticWorker:
             recs = self.broker.fetch(self.topic, p, self.pos[p], self.max_records)
             if not recs:
                 continue
+            if self.faults is not None and self.faults.drop():
+                continue                           # lost in flight: re-fetched from the committed offset
             X, ids, cust = decode_records([r.value for r in recs])
             proba, route = self.scorer.score(X)
             res = self.router.on_scored(ids, cust, proba, X=X, routes=route)

@@ -111,6 +111,10 @@ class EngineService:
         self._tasks: "queue.SimpleQueue" = queue.SimpleQueue()
         self._score_err: Optional[BaseException] = None
         self._reduce_pending = False
+        # injected delay / crash of this rank (utils/faults.py; CCFD_FAULTS).  ``drop`` is not
+        # applied here: this consumer's position advances on poll, so a drop would be real loss
+        from ..utils.faults import FaultPlan
+        self.faults = FaultPlan.from_env(ctx.rank)
 
     # ------------------------------------------------------------------ ingest (producer side)
     def _ingest_once(self) -> int:
@@ -212,6 +216,8 @@ class EngineService:
             self._score_err = e
 
     def step(self) -> int:
+        if self.faults is not None:
+            self.faults.step()
         if self._ingest_err is not None:
             raise RuntimeError("ingest thread failed") from self._ingest_err
         if self._score_err is not None:

@@ -150,3 +150,79 @@ def test_sigkill_rank_over_tcpstore_and_kafka_protocol():
                 p.kill()
         kb.close()
         lite.stop()
+
+
+def test_fault_plan_parse_and_determinism():
+    import pytest
+    from ccfd_demo_summit_amd.utils.faults import FaultPlan, InjectedCrash
+    p = FaultPlan.parse("drop:p=0.5;delay:ms=0.1,p=1,rank=1;crash:after_steps=3,rank=0", rank=0, seed=4)
+    assert [c.kind for c in p.clauses] == ["drop", "delay", "crash"]
+    q = FaultPlan.parse("drop:p=0.5", rank=0, seed=4)
+    assert [p.drop() for _ in range(50)] == [q.drop() for _ in range(50)]      # seeded
+    p.step(); p.step()
+    assert p.injected["delay"] == 0                                           # delay is rank 1's
+    with pytest.raises(InjectedCrash):
+        p.step()
+    with pytest.raises(ValueError):
+        FaultPlan.parse("explode:p=1")
+    with pytest.raises(ValueError):
+        FaultPlan.parse("drop:q=1")
+
+
+def _elastic_cluster(n_workers, faults):
+    X, _ = generate(8000, seed=2)
+    model = build_model("mlp", seed=1, X_ref=X, calibrate_rate=0.02)
+    broker = InProcBroker(default_partitions=6)
+    broker.create_topic("odh-demo", 6)
+    TransactionProducer(broker, ProducerConfig(fmt="json", batch=500, seed=3)).produce(6000)
+    store, clock = MemoryStore(), Clock()
+    procs = ProcessEngine(notification_timeout_s=1e9, clock=clock)
+    workers = []
+    for r in range(n_workers):
+        router = Router(RuleSet.threshold(0.5), procs, RouterMetrics())
+        workers.append(ElasticWorker(r, PartitionLeases(store, r, n_workers, 6, ttl_s=1.0, clock=clock), broker,
+                                     "odh-demo", CpuScorer(model), router, max_records=300,
+                                     faults=faults(r) if faults else None))
+    return model, broker, procs, clock, workers
+
+
+def _truth(model, broker):
+    recs = [r for p in range(6) for r in broker.fetch("odh-demo", p, 0, 100_000)]
+    Xall, _, _ = decode_records([r.value for r in recs])
+    return int((model.predict_proba(Xall) >= 0.5).sum())
+
+
+def test_injected_drops_are_redelivered_exactly_once():
+    """drop faults on every rank: lost batches are re-fetched from the committed offset."""
+    from ccfd_demo_summit_amd.utils.faults import FaultPlan
+    model, broker, procs, clock, workers = _elastic_cluster(
+        3, lambda r: FaultPlan.parse("drop:p=0.3", rank=r, seed=11))
+    for _ in range(200):
+        clock.t += 0.25
+        for w in workers:
+            w.tick()
+    rows, fraud = workers[0].leases.global_counts()
+    assert rows == 6000 and fraud == _truth(model, broker)
+    assert sum(w.faults.injected["drop"] for w in workers) > 0
+    assert len(procs._by_tx) == fraud and broker.lag("ccfd-engine", "odh-demo") == 0
+
+
+def test_injected_crash_partitions_fail_over():
+    """crash fault (mode=raise) on rank 1 after 3 steps: the survivors adopt its partitions."""
+    from ccfd_demo_summit_amd.utils.faults import FaultPlan, InjectedCrash
+    model, broker, procs, clock, workers = _elastic_cluster(
+        3, lambda r: FaultPlan.parse("crash:after_steps=3,rank=1", rank=r))
+    crashed = []
+    for _ in range(200):
+        clock.t += 0.25
+        for w in workers:
+            try:
+                w.tick()
+            except InjectedCrash:
+                w.alive = False
+                crashed.append(w.rank)
+    assert crashed == [1]
+    rows, fraud = workers[0].leases.global_counts()
+    assert rows == 6000 and fraud == _truth(model, broker)
+    owned = sorted(p for w in workers if w.alive for p in w.leases.owned())
+    assert owned == list(range(6))
