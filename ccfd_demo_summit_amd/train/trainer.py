@@ -36,6 +36,8 @@ class TrainConfig:
     device: str = "auto"
     bf16: bool = True
     metrics: Optional[object] = None       # metrics.exporter.TrainMetrics (Training dashboard)
+    graph: bool = True                     # single GPU: replay the whole step as one HIP graph
+    log_every: int = 50                    # graph mode: loss read back every N steps
 
 
 def _device(name: str) -> torch.device:
@@ -77,6 +79,8 @@ def _fit(net: nn.Module, Xn: np.ndarray, y: np.ndarray, cfg: TrainConfig, use_bf
         tm.workers.set(world)
     import time as _time
     t_start = _time.perf_counter()
+    if cfg.graph and dev.type == "cuda" and world == 1 and len(shard) >= cfg.batch:
+        return _fit_graph(model, Xt, yt, loss_fn, opt, shard, g, cfg, use_bf16, pw, name, tm, t_start)
     for _ in range(cfg.epochs):
         perm = shard[torch.randperm(len(shard), generator=g)].to(dev)
         for s in range(0, len(perm), cfg.batch):
@@ -96,6 +100,72 @@ def _fit(net: nn.Module, Xn: np.ndarray, y: np.ndarray, cfg: TrainConfig, use_bf
                 if dev.type == "cuda":
                     tm.mem_bytes.set(torch.cuda.memory_allocated(dev))
     return {"steps": steps, "final_loss": last, "pos_weight": pw}
+
+
+def _fit_graph(model, Xt, yt, loss_fn, opt, shard, g, cfg: TrainConfig, use_bf16: bool, pw: float, name: str,
+               tm, t_start) -> Dict[str, float]:
+    """The training step (gather -> forward -> BCE -> backward -> AdamW) captured once as a
+    HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replayed per step.  A
+    12K-parameter MLP step is ~40 tiny kernels, i.e. launch-bound; a replay is one launch,
+    plus one index copy into the static batch-index buffer.  Batches are full ``cfg.batch``
+    rows (the tail of an epoch that does not fill one is skipped), the optimizer state lives
+    in capturable tensors, and the loss is read back only every ``cfg.log_every`` steps."""
+    import time as _time
+    dev = Xt.device
+    B = cfg.batch
+    for group in opt.param_groups:         # optimizer step must run inside the graph
+        group["capturable"] = True
+    idx = torch.zeros(B, dtype=torch.int64, device=dev)
+    xb = torch.empty(B, Xt.shape[1], dtype=Xt.dtype, device=dev)
+    yb = torch.empty(B, dtype=yt.dtype, device=dev)
+
+    def step():
+        torch.index_select(Xt, 0, idx, out=xb)
+        torch.index_select(yt, 0, idx, out=yb)
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=use_bf16, cache_enabled=False):
+            logit = model(xb).squeeze(-1)
+        loss = loss_fn(logit.float(), yb)
+        loss.backward()
+        opt.step()
+        return loss
+
+    batches = []
+    for _ in range(cfg.epochs):
+        perm = shard[torch.randperm(len(shard), generator=g)].to(dev)
+        batches += [perm[s:s + B] for s in range(0, len(perm) - B + 1, B)]
+    # warm-up (real steps on the first batches) on a side stream, as capture requires
+    warm = min(3, len(batches))
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for k in range(warm):
+            idx.copy_(batches[k])
+            opt.zero_grad(set_to_none=False)
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    opt.zero_grad(set_to_none=False)        # grads stay allocated: the graph accumulates into them
+    with torch.cuda.graph(graph):
+        for p in model.parameters():
+            p.grad.zero_()
+        static_loss = step()
+    last = float("nan")
+    steps = logged = warm
+    for k in range(warm, len(batches)):
+        idx.copy_(batches[k], non_blocking=True)
+        graph.replay()
+        steps += 1
+        if tm is not None and (steps % cfg.log_every == 0 or k == len(batches) - 1):
+            last = float(static_loss.detach())
+            tm.loss.labels(name).set(last)
+            tm.steps.labels(name).inc(steps - logged)
+            logged = steps
+            tm.samples_per_s.labels(name).set(steps * B / max(1e-9, _time.perf_counter() - t_start))
+            tm.mem_bytes.set(torch.cuda.memory_allocated(dev))
+    torch.cuda.synchronize(dev)
+    last = float(static_loss.detach()) if len(batches) > warm else last
+    return {"steps": steps, "final_loss": last, "pos_weight": pw, "graph": True,
+            "seconds": _time.perf_counter() - t_start}
 
 
 def train_logistic(X: np.ndarray, y: np.ndarray, cfg: TrainConfig = TrainConfig()) -> Tuple[LogisticModel, Dict]:
