@@ -19,13 +19,19 @@ K-step s takes tiles 2s and 2s+1 as its B fragment, i.e. element j of group g is
   pi(s,g,j) = 32s + 4g + (j&3) + 16(j>>2)
 and W2 is packed with the same k-permutation, so the sum is unchanged.
 
+W64 wire blobs (``pack(wire=True)``, header flag FLAG_WIRE): the row's 16-B lane chunk IS
+the layer-1 B fragment -- the bf16 V-columns go into the MFMA as raw bits, their
+normalisation folded into W1 (columns x 1/sigma) and b1 (minus W1'.mu); b1 rides in
+K-columns 30/31 as a bf16 hi/lo pair against constant-1 inputs; only Time and Amount are
+normalised in the kernel (lane group 3).  ``wire_logits`` is the numerics oracle of that path.
+
 Blob layout (bytes, all 16-B aligned), ``BLOB_BYTES`` = 25920:
   [0,64)        header: 'MLP1', flags(u32), b3(f32)
   [64,192)      mu[32]   f32   (lane group g reads mu[8g..8g+7])
   [192,320)     isg[32]  f32
   [320,8512)    W1f [8 t][64 lane][8 j]           bf16   W1[16t+(l&15)][8(l>>4)+j]
   [8512,24896)  W2f [4 u][4 s][64 lane][8 j]      bf16   W2[16u+(l&15)][pi(s,l>>4,j)]
-  [24896,25408) b1f [8 t][4 g][4 r]  f32   b1[16t+4g+r]
+  [24896,25408) b1f [8 t][4 g][4 r]  f32   b1[16t+4g+r]        (zero in wire blobs)
   [25408,25664) b2f [4 u][4 g][4 r]  f32   b2[16u+4g+r]
   [25664,25920) w3f [4 u][4 g][4 r]  f32   w3[16u+4g+r]
 """
@@ -36,7 +42,7 @@ from typing import Optional
 
 import numpy as np
 
-from ..contracts.transaction import N_FEATURES, WIRE_PERM, decode_wire, encode_wire
+from ..contracts.transaction import AMOUNT_COL, N_FEATURES, TIME_COL, WIRE_PERM, decode_wire, encode_wire
 from .common import (FLAG_WIRE, HEADER_BYTES, KPAD, Normalizer, bf16_bits, bf16_round, header, sigmoid)
 
 H1, H2 = 128, 64
@@ -48,6 +54,8 @@ OFF_B2 = OFF_B1 + 8 * 4 * 4 * 4
 OFF_W3 = OFF_B2 + 4 * 4 * 4 * 4
 BLOB_BYTES = OFF_W3 + 4 * 4 * 4 * 4
 assert BLOB_BYTES == 25920 and BLOB_BYTES % 16 == 0
+
+WIRE_N_BF16 = 28     # wire positions [0, 28) are bf16 V1..V28 (raw MFMA operands)
 
 
 def _pi(s: int, g: int, j: int) -> int:
@@ -110,11 +118,58 @@ class MLPModel:
         self.b3 += float(zt - q)
 
     # ---------------------------------------------------------------- packing
-    def pack(self, wire: bool = False) -> bytes:
-        """``wire=True``: W1 columns and the normaliser in W64 row order, header flag
-        FLAG_WIRE -- the blob for engines whose logs hold W64 rows."""
+    def _wire_w1(self):
+        """Layer-1 matrix of a wire blob [128, 32] (wire K order; V-normalisation and the
+        bias hi/lo pair folded in), as float32 before bf16 rounding."""
         W1p = np.zeros((H1, KPAD), np.float32)
-        W1p[:, :N_FEATURES] = self.W1[:, WIRE_PERM] if wire else self.W1
+        W1w = self.W1[:, WIRE_PERM].astype(np.float64)
+        mu = self.norm.mu[WIRE_PERM].astype(np.float64)
+        isg = self.norm.inv_sigma[WIRE_PERM].astype(np.float64)
+        v = np.arange(N_FEATURES) < WIRE_N_BF16
+        W1w[:, v] *= isg[v]
+        b1w = self.b1.astype(np.float64) - W1w[:, v] @ mu[v]
+        W1p[:, :N_FEATURES] = W1w
+        hi = bf16_round(b1w.astype(np.float32))
+        W1p[:, N_FEATURES] = hi
+        W1p[:, N_FEATURES + 1] = bf16_round((b1w - hi).astype(np.float32))
+        return W1p
+
+    def wire_inputs(self, X: np.ndarray) -> np.ndarray:
+        """The layer-1 B operand of the wire kernel, [n, 32] float32 (bf16-exact): raw bf16
+        V-columns, bf16 of the normalised Time / Amount, then the two constant-1 bias inputs."""
+        Xd = decode_wire(encode_wire(np.asarray(X, np.float32)))
+        xin = np.ones((Xd.shape[0], KPAD), np.float32)
+        xin[:, :WIRE_N_BF16] = Xd[:, WIRE_PERM[:WIRE_N_BF16]]
+        t = Xd[:, TIME_COL].astype(np.float32)
+        a = Xd[:, AMOUNT_COL].astype(np.float32)
+        if self.norm.log_amount:
+            a = np.log1p(np.maximum(a, 0.0)).astype(np.float32)
+        mu, isg = self.norm.mu, self.norm.inv_sigma
+        xin[:, WIRE_N_BF16] = (t - mu[TIME_COL]) * isg[TIME_COL]
+        xin[:, WIRE_N_BF16 + 1] = (a - mu[AMOUNT_COL]) * isg[AMOUNT_COL]
+        return bf16_round(xin)
+
+    def wire_logits(self, X: np.ndarray) -> np.ndarray:
+        """Numerics oracle of the W64 wire kernel (bf16 operands, fp32/fp64 accumulation)."""
+        xin = self.wire_inputs(X).astype(np.float64)
+        W1p = bf16_round(self._wire_w1()).astype(np.float64)
+        h1 = bf16_round(np.maximum(xin @ W1p.T, 0.0).astype(np.float32)).astype(np.float64)
+        h2 = np.maximum(h1 @ bf16_round(self.W2).T.astype(np.float64) + self.b2, 0.0)
+        return (h2 @ self.w3.astype(np.float64) + self.b3).astype(np.float32)
+
+    def wire_proba(self, X: np.ndarray) -> np.ndarray:
+        return sigmoid(self.wire_logits(X))
+
+    def pack(self, wire: bool = False) -> bytes:
+        """``wire=True``: the W64 wire blob (module docstring) with the normaliser in W64
+        row order and header flag FLAG_WIRE -- the blob for engines whose logs hold W64 rows."""
+        if wire:
+            W1p = self._wire_w1()
+            b1 = np.zeros_like(self.b1)          # folded into W1p columns 30/31
+        else:
+            W1p = np.zeros((H1, KPAD), np.float32)
+            W1p[:, :N_FEATURES] = self.W1
+            b1 = self.b1
         lanes = np.arange(64)
         c, g = lanes & 15, lanes >> 4
         j = np.arange(8)
@@ -126,7 +181,7 @@ class MLPModel:
         rows = 16 * np.arange(4)[:, None, None, None] + c[None, None, :, None]                  # [4 u][1][64][1]
         w2f = self.W2[rows, kidx[None, :, :, :]]
         gi, ri = np.meshgrid(np.arange(4), np.arange(4), indexing="ij")
-        b1f = np.stack([self.b1[16 * t + 4 * gi + ri] for t in range(8)])
+        b1f = np.stack([b1[16 * t + 4 * gi + ri] for t in range(8)])
         b2f = np.stack([self.b2[16 * u + 4 * gi + ri] for u in range(4)])
         w3f = np.stack([self.w3[16 * u + 4 * gi + ri] for u in range(4)])
         blob = (header(b"MLP1", self.norm.flags | (FLAG_WIRE if wire else 0), float(self.b3))
@@ -156,12 +211,15 @@ def emulate_packed_kernel(blob: bytes, X: np.ndarray) -> np.ndarray:
     """Pure-NumPy emulation of score_mlp.hip consuming the packed blob lane by lane.
 
     It walks the same fragment maps as the kernel (per 16-row tile, per lane) so a
-    packing or operand-order bug shows up on CPU, before any GPU run."""
+    packing or operand-order bug shows up on CPU, before any GPU run.  Wire blobs take the
+    wire kernel's operand path (raw bf16 V bits, Time/Amount normalised, constant-1 bias
+    inputs)."""
     b = memoryview(blob)
     flags = int(np.frombuffer(b, np.uint32, 1, 4)[0])
     b3 = float(np.frombuffer(b, np.float32, 1, 8)[0])
     mu = np.frombuffer(b, np.float32, 32, OFF_NORM)
     isg = np.frombuffer(b, np.float32, 32, OFF_NORM + 128)
+    wire = bool(flags & FLAG_WIRE)
 
     def bf(off, n):
         u = np.frombuffer(b, np.uint16, n, off).astype(np.uint32) << 16
@@ -173,7 +231,7 @@ def emulate_packed_kernel(blob: bytes, X: np.ndarray) -> np.ndarray:
     w3f = np.frombuffer(b, np.float32, 64, OFF_W3).reshape(4, 4, 4)
 
     X = np.asarray(X, np.float32)
-    if flags & FLAG_WIRE:
+    if wire:
         # the kernel sees W64 rows: bf16 V-columns, permuted to wire order
         X = decode_wire(encode_wire(X))[:, WIRE_PERM]
     n = X.shape[0]
@@ -202,7 +260,11 @@ def emulate_packed_kernel(blob: bytes, X: np.ndarray) -> np.ndarray:
             if valid[l]:
                 for jj in range(8):
                     k = 8 * g[l] + jj
-                    if k < N_FEATURES:
+                    if wire and k >= N_FEATURES:
+                        xin[l, jj] = 1.0                      # constant-1 bias inputs
+                    elif wire and k < WIRE_N_BF16:
+                        xin[l, jj] = X[rows[l], k]            # raw bf16 bits
+                    elif k < N_FEATURES:
                         v = X[rows[l], k]
                         if (flags & 1) and k == N_FEATURES - 1:
                             v = np.log1p(max(v, 0.0))

@@ -51,10 +51,11 @@ def new_counters(device="cuda") -> torch.Tensor:
 
 def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
           proba: Optional[torch.Tensor] = None, route: Optional[torch.Tensor] = None,
-          counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None
-          ) -> Tuple[torch.Tensor, torch.Tensor]:
+          counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None,
+          flags: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused score of x [n,30] (float32, CUDA) -- or, for a ``wire`` model, W64 rows
-    ([n,64] uint8 or [n,16] float32 view) -- returns (proba_1 [n] f32, route [n] u8)."""
+    ([n,64] uint8 or [n,16] float32 view) -- returns (proba_1 [n] f32, route [n] u8).
+    ``flags``: extra ``CCFD_ARG_*`` bits (ablation switches for profiling)."""
     wire = getattr(dm, "wire", False)
     if wire:
         if not x.is_cuda or x.dim() != 2 or x.element_size() * x.shape[1] != 64 or not x.is_contiguous():
@@ -71,7 +72,7 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
     a = ScoreArgs()
     a.x = x.data_ptr()
     a.ld = 16 if wire else x.stride(0)
-    a.flags = 2 if wire else 0          # CCFD_ARG_WIRE_W64
+    a.flags = (2 if wire else 0) | int(flags)          # CCFD_ARG_WIRE_W64
     a.n = n
     a.model = dm.model_id
     a.blob = dm.blob.data_ptr()

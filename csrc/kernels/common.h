@@ -27,6 +27,42 @@ __device__ __forceinline__ int amount_bucket(float a) {
   return b;   // 0..13, bucket b holds bound[b-1] < a <= bound[b]
 }
 
+// Same bucket as amount_bucket in 26 VALU: one compare + add-with-carry per bound (the
+// compiler's select/shift/add3 form of the sum costs ~4 per bound).  NaN -> bucket 0 like
+// amount_bucket (every ordered compare is false).
+__device__ __forceinline__ int amount_bucket_fast(float a) {
+  int b = 0;
+  asm volatile(
+      "v_cmp_lt_f32_e32 vcc, 0x3f800000, %1\n"   /* 1 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x40a00000, %1\n"   /* 5 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x41200000, %1\n"   /* 10 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x41c80000, %1\n"   /* 25 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x42480000, %1\n"   /* 50 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x42c80000, %1\n"   /* 100 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x437a0000, %1\n"   /* 250 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x43fa0000, %1\n"   /* 500 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x447a0000, %1\n"   /* 1000 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x451c4000, %1\n"   /* 2500 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x459c4000, %1\n"   /* 5000 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x461c4000, %1\n"   /* 10000 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      "v_cmp_lt_f32_e32 vcc, 0x46c35000, %1\n"   /* 25000 < a */
+      "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n"
+      : "+v"(b) : "v"(a) : "vcc");
+  return b;
+}
+
 __device__ __forceinline__ float sigmoid(float z) { return 1.f / (1.f + __expf(-z)); }
 
 // Per-workgroup epilogue accumulators in LDS.

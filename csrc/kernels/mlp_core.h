@@ -97,4 +97,102 @@ __device__ __forceinline__ float mlp_tile(const char* sblob, const MlpLane& L, f
   return sigmoid(z + L.b3);
 }
 
+// ---------------------------------------------------------------------------------------
+// W64 wire rows (blob from models/mlp.py pack(wire=True)).  A lane's 16-B chunk of the row
+// IS its layer-1 B fragment: the bf16 V-columns enter the MFMA as raw bits (their
+// normalisation is folded into W1/b1 at pack time), b1 rides in K-columns 30/31 against
+// constant-1 inputs, and only Time/Amount (lane group 3) are normalised here -- ~10 VALU
+// instead of unpack + 8 x normalise + convert per lane.
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  // one v_cvt_pk_bf16_f32 (RNE); a pair of scalar (__bf16) casts is emitted as two
+  // single-lane converts + v_perm
+  const f32x2 f = {lo, hi};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f, bf16x2));
+}
+
+// relu on two packed bf16: a negative bf16 is a negative int16 (sign bit), so one
+// v_pk_max_i16 against 0 is the ReLU of both halves (relu commutes with RNE rounding).
+__device__ __forceinline__ unsigned relu_pack_bf16x2(float lo, float hi) {
+  s16x2 v = __builtin_bit_cast(s16x2, pack_bf16x2(lo, hi));
+  v = __builtin_elementwise_max(v, (s16x2){0, 0});
+  return __builtin_bit_cast(unsigned, v);
+}
+
+struct MlpWireLane {
+  float t_scale, t_shift;   // Time (wire K 28):   bf16(t * isg - mu * isg)
+  float a_scale, a_shift;   // Amount (wire K 29): log1p as log2 with ln 2 folded into the scale
+  float b3;
+  bool log_amount;
+};
+
+__device__ __forceinline__ MlpWireLane mlp_wire_lane(const char* sblob) {
+  MlpWireLane L;
+  const unsigned flags = *reinterpret_cast<const unsigned*>(sblob + 4);
+  L.b3 = *reinterpret_cast<const float*>(sblob + 8);
+  L.log_amount = (flags & 1u) != 0;
+  const float* mu = reinterpret_cast<const float*>(sblob + kOffNorm);
+  const float* isg = mu + 32;
+  L.t_scale = isg[28];
+  L.t_shift = -mu[28] * isg[28];
+  L.a_scale = isg[29] * (L.log_amount ? 0.693147180559945f : 1.f);
+  L.a_shift = -mu[29] * isg[29];
+  return L;
+}
+
+__device__ __forceinline__ bf16x8 wire_operand(const WireRegs& r, bool g3, const MlpWireLane& L) {
+  const float t = __uint_as_float(r.v.z);
+  float am = __uint_as_float(r.v.w);
+  if (L.log_amount) am = __log2f(1.f + __builtin_amdgcn_fmed3f(am, 0.f, 3.4e38f));   // v_med3 + v_log_f32
+  const unsigned pk = pack_bf16x2(fmaf(t, L.t_scale, L.t_shift), fmaf(am, L.a_scale, L.a_shift));
+  uint4 u = r.v;
+  u.z = g3 ? pk : u.z;
+  u.w = g3 ? 0x3F803F80u : u.w;                         // bf16 1.0, 1.0: the b1 hi/lo inputs
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// proba_1 of row (lane & 15) of the tile from its W64 lane chunk; identical in all four
+// lane groups.  Layer 1 needs no accumulator init (b1 is inside the MFMA), layer-1 ReLU +
+// bf16 pack is 2 VALU per pair, the sigmoid uses the hardware reciprocal.
+__device__ __forceinline__ float mlp_tile_w64(const char* sblob, const MlpWireLane& L, const WireRegs& r,
+                                              int g, int lane) {
+  const bf16x8 xb = wire_operand(r, g == 3, L);
+  const bf16x8* W1f = reinterpret_cast<const bf16x8*>(sblob + kOffW1);
+  const bf16x8* W2f = reinterpret_cast<const bf16x8*>(sblob + kOffW2);
+  const f32x4* b2f = reinterpret_cast<const f32x4*>(sblob + kOffB2);
+  const f32x4* w3f = reinterpret_cast<const f32x4*>(sblob + kOffW3);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W1f[t * 64 + lane], xb, zero, 0, 0, 0);
+  bf16x8 hb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint4 u = make_uint4(relu_pack_bf16x2(acc1[2 * s][0], acc1[2 * s][1]),
+                               relu_pack_bf16x2(acc1[2 * s][2], acc1[2 * s][3]),
+                               relu_pack_bf16x2(acc1[2 * s + 1][0], acc1[2 * s + 1][1]),
+                               relu_pack_bf16x2(acc1[2 * s + 1][2], acc1[2 * s + 1][3]));
+    hb[s] = __builtin_bit_cast(bf16x8, u);
+  }
+  float z = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f32x4 acc = b2f[u * 4 + g];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W2f[(u * 4 + s) * 64 + lane], hb[s], acc, 0, 0, 0);
+    const f32x4 w3v = w3f[u * 4 + g];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) z = fmaf(__builtin_amdgcn_fmed3f(acc[q], 0.f, 3.4e38f), w3v[q], z);   // relu: 1 VALU
+  }
+  z += __shfl_xor(z, 16);
+  z += __shfl_xor(z, 32);
+  return __builtin_amdgcn_rcpf(1.f + __expf(-(z + L.b3)));
+}
+
 }  // namespace ccfd

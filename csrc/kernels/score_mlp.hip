@@ -126,10 +126,99 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
   signal_done(a, (unsigned)nblk);
 }
 
+// W64 wire path (kMode 2): one wave scores 16-row tiles with kPf tiles in flight -- a
+// tile's slot is refilled as soon as its operand is consumed, so a wave keeps kPf-1 1-KB
+// requests outstanding while it computes (HBM-resident launches were memory-latency bound
+// at one tile in flight: profiles/r1/kernel_sol*.json).  Loads are branch-free (rows clamped
+// into the batch; clamped rows are never scored) and the steady-state loop is unrolled kPf
+// times over static ring slots, so no register copy of an in-flight load -- which would
+// force an s_waitcnt vmcnt(0) -- is ever needed; only the < kPf-tile tail rotates the ring.
+template <int kWaves, int kPf>
+__device__ __forceinline__ void mlp_wire_body(const ccfd_score_args& a, int blk, int nblk) {
+  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
+  __shared__ EpilogueLds epi;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  stamp_start(a, blk);
+  const int n = a.n;
+  const int ntiles = (n + kTileRows - 1) / kTileRows;
+  const int tstride = nblk * kWaves;
+  int tile = blk * kWaves + wave;
+  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x) + 16 * g;
+  auto issue = [&](int t, WireRegs& r) __attribute__((always_inline)) {
+    const int row = min(t * kTileRows + c, n - 1);
+    r.v = *reinterpret_cast<const uint4*>(xw + (size_t)row * CCFD_WIRE_ROW_BYTES);
+  };
+  WireRegs ring[kPf];
+#pragma unroll
+  for (int k = 0; k < kPf; ++k) issue(tile + k * tstride, ring[k]);
+  mlp_stage(a.blob, sblob, tid, 64 * kWaves);
+  epi_init(epi);
+  __syncthreads();
+
+  const MlpWireLane L = mlp_wire_lane(sblob);
+  const float thr = a.threshold;
+  const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
+  unsigned fraud = 0, rows = 0;
+  unsigned long long psum = 0;
+  auto finish = [&](float p, float amount, int t) __attribute__((always_inline)) {
+    const int row = t * kTileRows + c;
+    const bool valid = row < n;
+    const bool fr = valid && (p >= thr);
+    if (valid && g == 0) {
+      if (store_out) {
+        if (a.proba) a.proba[row] = p;
+        if (a.route) a.route[row] = fr ? 1 : 0;
+      }
+      psum += (unsigned)(p * 1e6f + 0.5f);
+    }
+    fraud += __popcll(__ballot(fr && g == 0));
+    rows += __popcll(__ballot(valid && g == 0));
+    if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(amount)], 1u);
+    emit_flagged(a, fr && g == 0, row);
+  };
+  // steady state: the kPf strided tiles of a round all exist
+  const int full_end = ntiles - (kPf - 1) * tstride;
+  while (tile < full_end) {
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) {
+      const float amount = __uint_as_float(ring[k].v.w);
+      const float p = mlp_tile_w64(sblob, L, ring[k], g, lane);
+      issue(tile + kPf * tstride, ring[k]);
+      finish(p, amount, tile);
+      tile += tstride;
+    }
+  }
+  // tail: fewer than kPf tiles left, already in flight in ring[0..]
+#pragma unroll 1
+  for (int k = 0; k < kPf && tile < ntiles; ++k) {
+    const WireRegs cur = ring[0];
+#pragma unroll
+    for (int q = 0; q + 1 < kPf; ++q) ring[q] = ring[q + 1];
+    finish(mlp_tile_w64(sblob, L, cur, g, lane), __uint_as_float(cur.v.w), tile);
+    tile += tstride;
+  }
+  psum = wave_sum_u64(psum);
+  if (lane == 0) {
+    atomicAdd(&epi.fraud, fraud);
+    atomicAdd(&epi.rows, rows);
+    atomicAdd(&epi.psum_e6, psum);
+  }
+  epi_flush(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
+  signal_done(a, (unsigned)nblk);
+}
+
 template <int kMode, int kWaves>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_kernel(ccfd_score_args a) {
   mlp_body<kMode, kWaves>(a, blockIdx.x, gridDim.x);
+}
+
+template <int kWaves, int kPf>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
+void score_mlp_wire_kernel(ccfd_score_args a) {
+  mlp_wire_body<kWaves, kPf>(a, blockIdx.x, gridDim.x);
 }
 
 // Coalesced launch: workgroups [j*wpb, (j+1)*wpb) score sub-batch j.
@@ -143,6 +232,35 @@ void score_mlp_multi_kernel(ccfd_multi_args m) {
   const int wpb = gridDim.x / mk.nsub;                 // workgroups per sub-batch
   const int j = blockIdx.x / wpb;
   mlp_body<kMode, kWaves>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+}
+
+template <int kWaves, int kPf>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
+void score_mlp_wire_multi_kernel(ccfd_multi_args m) {
+  (void)m;
+  const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int wpb = gridDim.x / mk.nsub;
+  const int j = blockIdx.x / wpb;
+  mlp_wire_body<kWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+}
+
+// CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4; default 4).
+static int mlp_wire_prefetch() {
+  static const int v = [] {
+    const char* e = std::getenv("CCFD_MLP_PF");
+    const int x = e ? std::atoi(e) : 4;
+    return (x == 1 || x == 2 || x == 4) ? x : 4;
+  }();
+  return v;
+}
+
+template <int kW>
+static void launch_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
+  switch (mlp_wire_prefetch()) {
+    case 1: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 1>), grid, dim3(64 * kW), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
+    default: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
+  }
 }
 
 // CCFD_MLP_WEIGHTS=global: MFMA weight fragments read straight from the (L1/L2-resident)
@@ -174,11 +292,14 @@ template <int kW>
 static void launch_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   const int per_wg = kW * mlp_tiles_per_wave();
   int grid = (ntiles + per_wg - 1) / per_wg;
-  grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
+  // cap: one full residency of the chip (256 CUs x 16 waves at the 128-VGPR cap); a
+  // grid-stride loop covers the rest, so large HBM-resident launches do not pay a second
+  // round of weight staging and counter flushes
+  const int cap = 256 * 16 / kW;
+  grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
   const bool gw = mlp_global_weights();
   if (a.flags & CCFD_ARG_WIRE_W64) {
-    if (gw) hipLaunchKernelGGL((score_mlp_kernel<6, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
-    else hipLaunchKernelGGL((score_mlp_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    launch_wire<kW>(dim3(grid), s, a);
   } else if (contig) {
     if (gw) hipLaunchKernelGGL((score_mlp_kernel<5, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
     else hipLaunchKernelGGL((score_mlp_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
@@ -204,8 +325,11 @@ int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
   const dim3 grid(wpb * m.nsub), block(64 * kW);
   const bool gw = mlp_global_weights();
   if (m.base.flags & CCFD_ARG_WIRE_W64) {
-    if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<6, kW>), grid, block, 0, s, m);
-    else hipLaunchKernelGGL((score_mlp_multi_kernel<2, kW>), grid, block, 0, s, m);
+    switch (mlp_wire_prefetch()) {
+      case 1: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 1>), grid, block, 0, s, m); break;
+      case 2: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 2>), grid, block, 0, s, m); break;
+      default: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 4>), grid, block, 0, s, m); break;
+    }
   } else {
     if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<5, kW>), grid, block, 0, s, m);
     else hipLaunchKernelGGL((score_mlp_multi_kernel<1, kW>), grid, block, 0, s, m);

@@ -46,9 +46,11 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   __syncthreads();
 
   MlpLane L{};
+  MlpWireLane LW{};
   float wm[8];
   if (kModel == CCFD_MODEL_MLP) {
     L = mlp_lane(sblob, g);
+    LW = mlp_wire_lane(sblob);
   } else {
     const unsigned flags = *reinterpret_cast<const unsigned*>(sblob + 4);
     L.b3 = *reinterpret_cast<const float*>(sblob + 8);
@@ -178,10 +180,11 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       const bool valid = row < n;
       const int nxt = tile + 4;
       float xv[8];
+      WireRegs cur_w;
       if (wire) {
-        const WireRegs cur = wpre;
+        cur_w = wpre;
         if (k + 1 < kTilesPerWave && nxt * kTileRows < n) wire_issue(xw, n, nxt, c, g, wpre);
-        wire_features(cur, g, xv);
+        if (kModel != CCFD_MODEL_MLP) wire_features(cur_w, g, xv);
       } else {
         tile_store(tile_lds, lane, pre);
         if (k + 1 < kTilesPerWave && nxt * kTileRows < n) tile_issue(x + (size_t)nxt * kTileRows * kF, avail(nxt), lane, pre);
@@ -191,7 +194,12 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       }
       float p, amount;
       if (kModel == CCFD_MODEL_MLP) {
-        p = mlp_tile(sblob, L, xv, g, lane, amount);
+        if (wire) {        // W64 blob: raw bf16 operands, folded normalisation (mlp_core.h)
+          amount = __uint_as_float(cur_w.v.w);
+          p = mlp_tile_w64(sblob, LW, cur_w, g, lane);
+        } else {
+          p = mlp_tile(sblob, L, xv, g, lane, amount);
+        }
       } else {
         amount = xv[5];
         if (g == 3) { xv[6] = 0.f; xv[7] = 0.f; if (L.log_amount) xv[5] = log1pf(fmaxf(xv[5], 0.f)); }

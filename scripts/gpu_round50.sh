@@ -1,0 +1,13 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r50; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+K="timeout -k 10 120 python bench/kernel_sol.py"
+for pf in 1 2 4; do
+  CCFD_MLP_PF=$pf $K --cases mlp:w64 --tag pf$pf >> $O/sweep.jsonl 2>>$O/err.log || exit 1
+done
+CCFD_MLP_PF=4 $K --cases mlp:w64 --sizes 1048576,16777216 --flags 16 --tag pf4_nocnt >> $O/sweep.jsonl 2>>$O/err.log || exit 1
+cat $O/sweep.jsonl
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+tail -1 $O/bench.log

@@ -40,7 +40,7 @@ def test_engine_pump_matches_oracle(gpu, setup, input_mode, output_mode, exec_mo
     assert st.batches == 6 and st.rows == 6 * 4096
     if wire:
         from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
-        ref = m.predict_proba(decode_wire(encode_wire(X[:6 * 4096])), emulate_bf16=True)
+        ref = m.wire_proba(X[:6 * 4096])
     else:
         ref = m.predict_proba(X[:6 * 4096], emulate_bf16=True)
     flagged = eng.drain_flagged()
@@ -105,7 +105,7 @@ def test_ring_streaming_mode_deadline_flush(gpu, setup, exec_mode):
     flagged = eng.drain_flagged()
     if wire:
         from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
-        ref = m.predict_proba(decode_wire(encode_wire(X[:n])), emulate_bf16=True)
+        ref = m.wire_proba(X[:n])
     else:
         ref = m.predict_proba(X[:n], emulate_bf16=True)
     got = np.zeros(n, bool)
@@ -169,8 +169,7 @@ def test_hot_swap_between_micro_batches(gpu, setup, exec_mode):
     got = np.zeros(6 * 4096, bool)
     got[flagged["tx_id"].astype(np.int64)] = True
     Xd = decode_wire(encode_wire(X[:6 * 4096]))
-    ref = np.concatenate([mA.predict_proba(Xd[:3 * 4096], emulate_bf16=True),
-                          mB.predict_proba(Xd[3 * 4096:], emulate_bf16=True)])
+    ref = np.concatenate([mA.wire_proba(X[:3 * 4096]), mB.wire_proba(X[3 * 4096:6 * 4096])])
     clear = np.abs(ref - 0.5) > 2e-3
     np.testing.assert_array_equal(got[clear], (ref >= 0.5)[clear])
     assert eng.model_version == 1

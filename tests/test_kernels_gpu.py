@@ -125,7 +125,7 @@ def test_wire_w64_kernel_matches_reference(gpu, data, kind, n):
     Xd = decode_wire(encode_wire(X))
     assert np.abs(p - m.predict_proba(X)).max() < 1e-2
     if kind == "mlp":
-        assert np.abs(p - m.predict_proba(Xd, emulate_bf16=True)).max() < 2e-3
+        assert np.abs(p - m.wire_proba(X)).max() < 2e-4
     else:
         assert np.abs(p - m.predict_proba(Xd)).max() < 1e-5
     np.testing.assert_array_equal(r, (p >= 0.5).astype(np.uint8))

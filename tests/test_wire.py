@@ -69,7 +69,9 @@ def test_wire_blob_matches_oracle(kind):
     Xw = decode_wire(encode_wire(X[:48]))
     if kind == "mlp":
         got = emulate_packed_kernel(m.pack(wire=True), X[:48])
-        np.testing.assert_allclose(got, m.predict_proba(Xw, emulate_bf16=True), atol=2e-6)
+        np.testing.assert_allclose(got, m.wire_proba(X[:48]), atol=2e-6)
+        # folding the V-normalisation into W1 stays within bf16 noise of normalise-then-round
+        assert np.abs(got - m.predict_proba(Xw, emulate_bf16=True)).max() < 2e-3
         # and the wire numerics stay within bf16 noise of the f32 model
         assert np.abs(got - m.predict_proba(X[:48])).max() < 5e-3
     blob = np.frombuffer(m.pack(wire=True), np.uint8)
