@@ -42,6 +42,12 @@ class MemoryStore:
                 raise KeyError(key)
             return self._d[key]
 
+    def add(self, key: str, amount: int) -> int:
+        with self._lock:
+            v = int(self._d.get(key, b"0")) + int(amount)
+            self._d[key] = str(v).encode()
+            return v
+
     def check(self, keys: List[str]) -> bool:
         with self._lock:
             return all(k in self._d for k in keys)

@@ -71,12 +71,79 @@ struct EpilogueLds {
   unsigned int fraud;
   unsigned int rows;
   unsigned long long psum_e6;
+  unsigned int hgt[kNB - 1];   // rows with amount > bound i (HistLanes)
 };
 
 __device__ __forceinline__ void epi_init(EpilogueLds& s) {
   const int t = threadIdx.x;
   if (t < 2 * kNB) s.hist[t] = 0;
+  if (t >= 32 && t < 32 + kNB - 1) s.hgt[t - 32] = 0;
   if (t == 0) { s.fraud = 0; s.rows = 0; s.psum_e6 = 0; }
+}
+
+// Amount histogram without per-row atomics or per-row bucket search.  The 13 bucket
+// bounds are spread over the 4 lane groups (lane group g owns bounds g, 4+g, 8+g, 12+g):
+// every lane sees the amount of row (lane & 15) -- broadcast from lane group 3 with one
+// ds_bpermute -- and keeps 4 per-lane counters of "amount > its bounds" (4 compares + 4
+// adds per 16-row tile instead of a 13-compare search + an LDS atomic per row).  At the
+// end the 16 lanes of each group are summed, and bucket counts follow from differences of
+// consecutive "greater-than" counts; the standard-route histogram is all rows minus the
+// fraud-route histogram, which fraud rows (~0.2 %) still add per row into
+// epi.hist[kNB + b].  `am` must be -inf for a row that is not valid.
+struct HistLanes {
+  unsigned cnt[4];
+  float bound[4];
+};
+
+__device__ __forceinline__ void hist_lanes_init(HistLanes& h, int g) {
+  constexpr float kB[16] = {1.f, 5.f, 10.f, 25.f, 50.f, 100.f, 250.f, 500.f, 1000.f, 2500.f,
+                            5000.f, 10000.f, 25000.f, __builtin_inff(), __builtin_inff(), __builtin_inff()};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h.cnt[j] = 0;
+    h.bound[j] = kB[4 * j + g];
+  }
+}
+
+// `am_row`: amount of row (lane & 15) in EVERY lane (or -inf when that row is not valid).
+__device__ __forceinline__ void hist_lanes_add(HistLanes& h, float am_row) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) h.cnt[j] += am_row > h.bound[j] ? 1u : 0u;
+}
+
+__device__ __forceinline__ void hist_lanes_commit(EpilogueLds& e, const HistLanes& h, int g, int c) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned v = h.cnt[j];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 8);
+    const int i = 4 * j + g;
+    if (c == 0 && i < kNB - 1 && v) atomicAdd(&e.hgt[i], v);
+  }
+}
+
+// Flush of a workgroup that built its amount histogram with HistLanes (all rows) plus
+// per-row fraud atomics: standard bucket b = (rows in bucket b) - (fraud rows in bucket b).
+__device__ __forceinline__ void epi_flush_ballot(EpilogueLds& s, unsigned long long* cnt) {
+  __syncthreads();
+  if (cnt == nullptr) return;
+  const int t = threadIdx.x;
+  if (t < kNB) {
+    const unsigned above = t == 0 ? s.rows : s.hgt[t - 1];
+    const unsigned all = above - (t == kNB - 1 ? 0u : s.hgt[t]);
+    const unsigned h = all - s.hist[kNB + t];
+    if (h) atomicAdd(&cnt[CCFD_CNT_HIST_STD + t], (unsigned long long)h);
+  } else if (t < 2 * kNB) {
+    const unsigned h = s.hist[t];
+    if (h) atomicAdd(&cnt[CCFD_CNT_HIST_FRAUD - kNB + t], (unsigned long long)h);
+  } else if (t == 2 * kNB) {
+    atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)s.rows);
+    atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)s.fraud);
+    atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(s.rows - s.fraud));
+    atomicAdd(&cnt[CCFD_CNT_PROBA_E6], s.psum_e6);
+  }
 }
 
 // Flush the workgroup's LDS accumulators into the global u64 counters (one atomic per slot).

@@ -164,6 +164,199 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a, int 
   signal_done(a, gridDim.x);
 }
 
+
+// ---------------------------------------------------------------------------------------
+// v2: rows in registers (contiguous rows whose leaf tables fit in LDS -- the common case).
+// Each WAVE owns its own 64-row chunks (R chunks at a time, R = 2 -> two independent row
+// chains per lane): the chunk is fetched with coalesced float4 loads (also right for a
+// host-mapped log over PCIe), transposed through a wave-private LDS tile, and every lane
+// lifts ITS row's 30 features into VGPRs once.  A tree level is then three VALU -- the
+// wave-uniform feature id indexes the register file (s_set_gpr_idx + v_mov), one compare
+// against the SGPR threshold, one add-with-carry that shifts the leaf index and adds the
+// bit -- instead of an LDS read per level; only the leaf value is gathered from LDS.  All
+// trees run in every wave (no cross-wave partial sums).  The next chunk group is prefetched
+// into registers while the current one is scored.  (v1 above is kept for strided rows and
+// for ensembles whose leaves exceed 64 KB.)
+// ---------------------------------------------------------------------------------------
+constexpr int kGb2Waves = 4;
+
+template <int D, int R>
+__global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
+  constexpr int L = 1 << D;
+  __shared__ __attribute__((aligned(16))) float xs[kGb2Waves][kF][kGbRows + 1];
+  extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L floats
+  __shared__ EpilogueLds epi;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = a.n;
+  const int nchunks = (n + kGbRows - 1) / kGbRows;
+  const int ngroups = (nchunks + R - 1) / R;                  // R chunks per wave step
+  const int gstride = gridDim.x * kGb2Waves;
+  int grp = blockIdx.x * kGb2Waves + wave;
+  epi_init(epi);
+  stamp_start(a, blockIdx.x);
+
+  const char* blob = reinterpret_cast<const char*>(a.blob);
+  const int T = a.gbdt_trees;
+  const float base = *reinterpret_cast<const float*>(blob + 16);
+  const int tdw = ((4 * T * D + 15) & ~15) / 4;
+  // split parameters through the CONSTANT address space: wave-uniform indices then compile
+  // to s_load into SGPRs (the model blob is immutable for the kernel's lifetime)
+  typedef const __attribute__((address_space(4))) int* cint_p;
+  typedef const __attribute__((address_space(4))) float* cflt_p;
+  const cint_p feat = (cint_p)(blob + kHeader);
+  const cflt_p thr = (cflt_p)(blob + kHeader + 4 * tdw);
+  const float* __restrict__ leaves = reinterpret_cast<const float*>(blob + kHeader) + 2 * tdw;
+  {
+    const float4* s4 = reinterpret_cast<const float4*>(leaves);
+    float4* d4 = reinterpret_cast<float4*>(lv);
+    for (int i = tid; i < T * L / 4; i += 256) d4[i] = s4[i];
+  }
+
+  // one 64-row chunk = 480 float4; lane l holds float4 l + 64k (k < 8)
+  auto fetch = [&](int chunk, float4 (&r)[8]) __attribute__((always_inline)) {
+    const int row0 = chunk * kGbRows;
+    const int avail = max(0, min(kGbRows, n - row0)) * kF * 4;
+    const float4* src = reinterpret_cast<const float4*>(a.x + (size_t)row0 * kF);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = lane + 64 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < kGbF4) {
+        if (i * 16 + 16 <= avail) v = src[i];
+        else if (i * 16 + 8 <= avail) { const float2 h = reinterpret_cast<const float2*>(src)[2 * i]; v.x = h.x; v.y = h.y; }
+      }
+      r[k] = v;
+    }
+  };
+  auto lift = [&](const float4 (&r)[8], float (&x)[kF]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = lane + 64 * k;
+      if (i < kGbF4) {
+        const float vv[4] = {r[k].x, r[k].y, r[k].z, r[k].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { const int e = 4 * i + q; xs[wave][e % kF][e / kF] = vv[q]; }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int f = 0; f < kF; ++f) x[f] = xs[wave][f][lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  };
+
+  float4 pre[R][8];
+#pragma unroll
+  for (int q = 0; q < R; ++q) fetch(grp * R + q, pre[q]);
+  __syncthreads();                                            // leaves staged
+
+  unsigned fraud = 0, rows = 0;
+  unsigned long long psum = 0;
+  for (; grp < ngroups; grp += gstride) {
+    // separate arrays per row chain: a 2-D register array indexed by a runtime feature id
+    // is demoted to scratch, two 1-D ones stay in VGPRs (s_set_gpr_idx)
+    float x0[kF], x1[kF];
+    lift(pre[0], x0);
+    if constexpr (R == 2) lift(pre[1], x1);
+    const int nxt = grp + gstride;
+    if (nxt < ngroups) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) fetch(nxt * R + q, pre[q]);
+    }
+    float acc[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) acc[q] = 0.f;
+#pragma unroll 2
+    for (int t = 0; t < T; ++t) {
+      unsigned i0 = 0, i1 = 0;
+#pragma unroll
+      for (int d = D - 1; d >= 0; --d) {                       // MSB first: bit d lands at position d
+        const int f = feat[t * D + d];                          // wave-uniform -> s_load
+        const float th = thr[t * D + d];
+        const float v0 = x0[f];                                 // s_set_gpr_idx + v_mov
+        asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n"
+                     "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                     : "+v"(i0) : "s"(th), "v"(v0) : "vcc");
+        if constexpr (R == 2) {
+          const float v1 = x1[f];
+          asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n"
+                       "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                       : "+v"(i1) : "s"(th), "v"(v1) : "vcc");
+        }
+      }
+      acc[0] += lv[t * L + (int)i0];
+      if constexpr (R == 2) acc[R - 1] += lv[t * L + (int)i1];
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int row = (grp * R + q) * kGbRows + lane;
+      const bool valid = row < n;
+      const float p = sigmoid(base + acc[q]);
+      const bool fr = valid && (p >= a.threshold);
+      if (valid) {
+        if (a.proba) a.proba[row] = p;
+        if (a.route) a.route[row] = fr ? 1 : 0;
+        psum += (unsigned)(p * 1e6f + 0.5f);
+        atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(q == 0 ? x0[kAmountCol] : x1[kAmountCol])], 1u);
+      }
+      fraud += __popcll(__ballot(fr));
+      rows += __popcll(__ballot(valid));
+      emit_flagged(a, fr, row);
+    }
+  }
+  psum = wave_sum_u64(psum);
+  if (lane == 0) {
+    atomicAdd(&epi.fraud, fraud);
+    atomicAdd(&epi.rows, rows);
+    atomicAdd(&epi.psum_e6, psum);
+  }
+  epi_flush(epi, a.counters);
+  signal_done(a, gridDim.x);
+}
+
+// Kernel choice.  v2 wins on large launches (HBM-resident bulk scoring: 2.6 -> 8.8 G rows/s
+// at 16M rows, profiles/r1/gbdt_v2_sweep.jsonl); on streaming micro-batches (<= 64K rows read
+// zero-copy over PCIe) v1's smaller LDS footprint keeps more workgroups -- i.e. more PCIe
+// reads -- in flight (408 vs 345 M tx/s), so v1 stays the default below kGbV2MinRows.
+// CCFD_GBDT_KERNEL=v1|v2 forces one; CCFD_GBDT_R: 64-row chunks per wave step (1|2).
+constexpr int kGbV2MinRows = 262144;
+static int gbdt_v2_rows() {
+  static const int r = [] {
+    const char* e = getenv("CCFD_GBDT_R");
+    return (e && atoi(e) == 1) ? 1 : 2;          // R = 2 measured best (8.8 vs 7.1 G rows/s)
+  }();
+  return r;
+}
+static int gbdt_forced_kernel() {   // 0 = by size, 1 = v1, 2 = v2
+  static const int v = [] {
+    const char* e = getenv("CCFD_GBDT_KERNEL");
+    return !e ? 0 : strcmp(e, "v1") == 0 ? 1 : strcmp(e, "v2") == 0 ? 2 : 0;
+  }();
+  return v;
+}
+
+template <int D, int R>
+static void launch_v2(const ccfd_score_args& a, hipStream_t s) {
+  constexpr int L = 1 << D;
+  const int nchunks = (a.n + kGbRows - 1) / kGbRows;
+  const int ngroups = (nchunks + R - 1) / R;
+  int grid = (ngroups + kGb2Waves - 1) / kGb2Waves;
+  const int cap = 256 * 2;                 // two resident workgroups per CU (LDS: staging + leaves)
+  grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
+  const size_t lds = (size_t)a.gbdt_trees * L * sizeof(float);
+  hipLaunchKernelGGL((score_gbdt_v2_kernel<D, R>), dim3(grid), dim3(256), lds, s, a);
+}
+
+template <int D>
+static void launch_d2(const ccfd_score_args& a, hipStream_t s) {
+  if (gbdt_v2_rows() == 1) launch_v2<D, 1>(a, s);
+  else launch_v2<D, 2>(a, s);
+}
+
 // CCFD_GBDT_CPW: 64-row chunks per workgroup.  Default: a ~256-workgroup grid (one per CU;
 // 4 chunks each on a 65536-row micro-batch).  Measured on MI355X, 100x6 trees, 65536-row
 // batches (profiles/r1/gbdt_sweep.txt): 1 chunk/WG 348M tx/s, 2 -> 368M, 4 -> 412M,
@@ -195,6 +388,22 @@ int launch_gbdt(const ccfd_score_args& a, hipStream_t s) {
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
   if (a.gbdt_trees <= 0) return -2;
   if (a.n <= 0) return 0;
+  const int forced = gbdt_forced_kernel();
+  const bool want_v2 = forced == 2 || (forced == 0 && a.n >= kGbV2MinRows);
+  if (want_v2 && contig && a.gbdt_depth >= 1 && a.gbdt_depth <= 8 &&
+      ((long)a.gbdt_trees << a.gbdt_depth) <= kLeafLds) {
+    switch (a.gbdt_depth) {
+      case 1: launch_d2<1>(a, s); break;
+      case 2: launch_d2<2>(a, s); break;
+      case 3: launch_d2<3>(a, s); break;
+      case 4: launch_d2<4>(a, s); break;
+      case 5: launch_d2<5>(a, s); break;
+      case 6: launch_d2<6>(a, s); break;
+      case 7: launch_d2<7>(a, s); break;
+      default: launch_d2<8>(a, s); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   switch (a.gbdt_depth) {
     case 1: launch_d<1>(a, s, contig); break;
     case 2: launch_d<2>(a, s, contig); break;

@@ -162,6 +162,8 @@ __device__ __forceinline__ void mlp_wire_body(const ccfd_score_args& a, int blk,
   const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
+  HistLanes hl;
+  hist_lanes_init(hl, g);
   auto finish = [&](float p, float amount, int t) __attribute__((always_inline)) {
     const int row = t * kTileRows + c;
     const bool valid = row < n;
@@ -173,10 +175,15 @@ __device__ __forceinline__ void mlp_wire_body(const ccfd_score_args& a, int blk,
       }
       psum += (unsigned)(p * 1e6f + 0.5f);
     }
-    fraud += __popcll(__ballot(fr && g == 0));
-    rows += __popcll(__ballot(valid && g == 0));
-    if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(amount)], 1u);
-    emit_flagged(a, fr && g == 0, row);
+    const unsigned long long frm = __ballot(fr && g == 3);     // same rows as the g == 0 lanes
+    fraud += __popcll(frm);
+    rows += (unsigned)min(kTileRows, n - t * kTileRows);
+    const float am_g3 = (valid && g == 3) ? amount : -__builtin_inff();
+    hist_lanes_add(hl, __shfl(am_g3, 48 + c));
+    if (frm) {                                                   // rare: fraud rows' buckets
+      if (fr && g == 3) atomicAdd(&epi.hist[kNB + amount_bucket_fast(amount)], 1u);
+      emit_flagged(a, fr && g == 0, row);
+    }
   };
   // steady state: the kPf strided tiles of a round all exist
   const int full_end = ntiles - (kPf - 1) * tstride;
@@ -200,12 +207,13 @@ __device__ __forceinline__ void mlp_wire_body(const ccfd_score_args& a, int blk,
     tile += tstride;
   }
   psum = wave_sum_u64(psum);
+  hist_lanes_commit(epi, hl, g, c);
   if (lane == 0) {
     atomicAdd(&epi.fraud, fraud);
     atomicAdd(&epi.rows, rows);
     atomicAdd(&epi.psum_e6, psum);
   }
-  epi_flush(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
+  epi_flush_ballot(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
   signal_done(a, (unsigned)nblk);
 }
 

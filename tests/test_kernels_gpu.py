@@ -91,6 +91,22 @@ def test_gbdt_kernel_exact(gpu, data, n, depth):
     _check_counters(cnt, p, r, X)
 
 
+@pytest.mark.parametrize("depth", [4, 6])
+def test_gbdt_v2_large_launch_exact(gpu, depth):
+    """Launches of >= 256K rows take the rows-in-registers kernel (score_gbdt.hip v2):
+    exact leaf selection, counters and histogram identical to the CPU reference."""
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X, _ = generate(300_007, seed=21)
+    m = build_model("gbdt", seed=4, X_ref=X[:5000], gbdt_trees=100, gbdt_depth=depth)
+    dm = DeviceModel(m, gpu)
+    cnt = new_counters(gpu)
+    p, r = score(dm, torch.from_numpy(X).to(gpu), 0.5, counters=cnt)
+    torch.cuda.synchronize()
+    p = p.cpu().numpy(); r = r.cpu().numpy()
+    assert np.abs(p - m.predict_proba(X)).max() < 1e-5
+    _check_counters(cnt, p, r, X)
+
+
 def test_strided_input_path(gpu, data):
     """ld != 30 takes the generic (non-contiguous) loader."""
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel, score

@@ -94,3 +94,35 @@ def test_async_hot_swap_broadcast_over_rccl(nccl):
     assert hs.poll(block=True)
     assert hs.version == 1 and eng.swapped == [new.pack()]
     assert hs.tick() is False                # nothing offered: header all-reduce only
+
+
+def test_elastic_group_rebuilds_rccl_communicator(nccl):
+    """parallel/membership.py over RCCL: a 1-member ProcessGroupNCCL per generation on a
+    PrefixStore (independent of the default group), async all-reduce of GPU counters polled
+    to completion; a forced new generation aborts the old communicator and builds a new one."""
+    import datetime
+    import time
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.parallel.membership import ElasticCounterReducer, ElasticGroup
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    store = dist.TCPStore("127.0.0.1", port, 1, True, timeout=datetime.timedelta(seconds=30), wait_for_workers=False)
+    grp = ElasticGroup(store, 0, 1, backend="nccl", device=nccl, ttl_s=1.0)
+    red = ElasticCounterReducer(grp, 4)
+    assert grp.tick() and grp.member and grp.members == [0]
+    red.submit(torch.tensor([1, 2, 3, 4], device=nccl))
+    t0 = time.time()
+    while red.completed < 2 and time.time() - t0 < 30:
+        red.progress()
+    assert red.totals.tolist() == [1, 2, 3, 4]
+    # a new generation (e.g. a rank rejoined) -> abort + rebuild, nothing local is lost
+    gen0 = grp.gen
+    red.submit(torch.tensor([10, 0, 0, 0], device=nccl))
+    red.progress()
+    store.set("ccfd/mem/gen", f"{gen0 + 1}:0")
+    assert grp.tick() and grp.gen == gen0 + 1
+    red.on_regroup()
+    t0 = time.time()
+    while red.totals[0].item() < 11 and time.time() - t0 < 30:
+        red.progress()
+    assert red.totals.tolist() == [11, 2, 3, 4]
+    grp.close()
