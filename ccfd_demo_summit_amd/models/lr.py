@@ -46,13 +46,24 @@ class LogisticModel:
         self.b += float(np.log(threshold / (1 - threshold)) - np.quantile(z, 1.0 - target_rate))
 
     def pack(self, wire: bool = False) -> bytes:
-        """``wire=True``: weights/normaliser in W64 row order (see models/mlp.py pack)."""
+        """``wire=True``: weights in W64 row order with the WHOLE normaliser folded in
+        (w' = w * isg, b' = b - sum w * isg * mu; the packed mu/isg become 0/1), so the wire
+        kernel's dot product runs on the raw row values (bf16 V-columns, f32 Time, log1p'd
+        Amount).  Generic kernels reading the same blob compute (x - 0) * 1 * w' -- the
+        same function."""
         from ..contracts.transaction import WIRE_PERM
         from .common import FLAG_WIRE
         w = np.zeros(KPAD, np.float32)
-        w[:N_FEATURES] = self.w[WIRE_PERM] if wire else self.w
-        blob = (header(b"LR01", self.norm.flags | (FLAG_WIRE if wire else 0), float(self.b))
-                + self.norm.packed(wire) + w.tobytes())
+        if wire:
+            wd = self.w[WIRE_PERM].astype(np.float64) * self.norm.inv_sigma[WIRE_PERM].astype(np.float64)
+            b = float(self.b) - float(wd @ self.norm.mu[WIRE_PERM].astype(np.float64))
+            w[:N_FEATURES] = wd
+            ident = Normalizer(np.zeros(N_FEATURES, np.float32), np.ones(N_FEATURES, np.float32),
+                               self.norm.log_amount)
+            blob = header(b"LR01", self.norm.flags | FLAG_WIRE, b) + ident.packed(True) + w.tobytes()
+        else:
+            w[:N_FEATURES] = self.w
+            blob = header(b"LR01", self.norm.flags, float(self.b)) + self.norm.packed(False) + w.tobytes()
         assert len(blob) == BLOB_BYTES
         return blob
 

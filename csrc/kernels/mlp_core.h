@@ -195,4 +195,17 @@ __device__ __forceinline__ float mlp_tile_w64(const char* sblob, const MlpWireLa
   return __builtin_amdgcn_rcpf(1.f + __expf(-(z + L.b3)));
 }
 
+// wire_body.h scorer for the MLP
+struct MlpWireScorer {
+  static constexpr int kLds = kMlpBlob;
+  MlpWireLane L;
+  __device__ __forceinline__ void stage(const ccfd_score_args& a, char* lds, int tid, int nthreads) {
+    mlp_stage(a.blob, lds, tid, nthreads);
+  }
+  __device__ __forceinline__ void lanes(const char* lds, const ccfd_score_args&, int) { L = mlp_wire_lane(lds); }
+  __device__ __forceinline__ float tile(const char* lds, const WireRegs& r, int g, int lane) const {
+    return mlp_tile_w64(lds, L, r, g, lane);
+  }
+};
+
 }  // namespace ccfd

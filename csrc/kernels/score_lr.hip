@@ -5,6 +5,7 @@
 // Launch structure mirrors score_mlp.hip: a plain and a coalesced (multi-micro-batch) entry
 // over one body, tiles-per-wave with a one-tile prefetch.
 #include "common.h"
+#include "wire_body.h"
 
 namespace ccfd {
 
@@ -121,14 +122,74 @@ __global__ __launch_bounds__(64 * kLrWaves) void score_lr_multi_kernel(ccfd_mult
   lr_body<kMode, kLrWaves>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
+
+// W64 wire rows: the blob (models/lr.py pack(wire=True)) has the normaliser folded into w/b,
+// so the dot product runs on the raw row values -- bf16 V-columns widened by one shift/mask,
+// Time as f32, Amount as log2(1 + a) with ln 2 folded into its weight -- through the shared
+// prefetch-ring streaming body (wire_body.h).
+struct LrWireScorer {
+  static constexpr int kLds = 0;
+  float w[8];
+  float b;
+  bool log_amount;
+  __device__ __forceinline__ void stage(const ccfd_score_args&, char*, int, int) {}
+  __device__ __forceinline__ void lanes(const char*, const ccfd_score_args& a, int g) {
+    const char* blob = reinterpret_cast<const char*>(a.blob);
+    const unsigned flags = *reinterpret_cast<const unsigned*>(blob + 4);
+    b = *reinterpret_cast<const float*>(blob + 8);
+    log_amount = (flags & 1u) != 0;
+    const float* wp = reinterpret_cast<const float*>(blob + 320) + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = wp[j];
+    if (g == 3 && log_amount) w[5] *= 0.693147180559945f;
+  }
+  __device__ __forceinline__ float tile(const char*, const WireRegs& r, int g, int) const {
+    const bool g3 = g == 3;
+    const uint4 v = r.v;
+    float am = __uint_as_float(v.w);
+    if (log_amount) am = __log2f(1.f + __builtin_amdgcn_fmed3f(am, 0.f, 3.4e38f));
+    float x[8];
+    x[0] = __uint_as_float(v.x << 16); x[1] = __uint_as_float(v.x & 0xffff0000u);
+    x[2] = __uint_as_float(v.y << 16); x[3] = __uint_as_float(v.y & 0xffff0000u);
+    x[4] = g3 ? __uint_as_float(v.z) : __uint_as_float(v.z << 16);
+    x[5] = g3 ? am : __uint_as_float(v.z & 0xffff0000u);
+    x[6] = g3 ? 0.f : __uint_as_float(v.w << 16);
+    x[7] = g3 ? 0.f : __uint_as_float(v.w & 0xffff0000u);
+    float z = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z = fmaf(w[j], x[j], z);
+    z += __shfl_xor(z, 16);
+    z += __shfl_xor(z, 32);
+    return __builtin_amdgcn_rcpf(1.f + __expf(-(z + b)));
+  }
+};
+
+template <int kLrWaves, int kPf>
+__global__ __launch_bounds__(64 * kLrWaves) void score_lr_wire_kernel(ccfd_score_args a) {
+  wire_stream_body<LrWireScorer, kLrWaves, kPf>(a, blockIdx.x, gridDim.x);
+}
+
+template <int kLrWaves, int kPf>
+__global__ __launch_bounds__(64 * kLrWaves) void score_lr_wire_multi_kernel(ccfd_multi_args m) {
+  (void)m;
+  const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int wpb = gridDim.x / mk.nsub;
+  const int j = blockIdx.x / wpb;
+  wire_stream_body<LrWireScorer, kLrWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+}
+
 template <int kW>
 static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   const int per_wg = kW * mlp_tiles_per_wave_policy();
   int grid = (ntiles + per_wg - 1) / per_wg;
+  if (a.flags & CCFD_ARG_WIRE_W64) {
+    const int cap = 256 * 16 / kW;       // one chip residency, grid-stride beyond (score_mlp.hip)
+    grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
+    hipLaunchKernelGGL((score_lr_wire_kernel<kW, 4>), dim3(grid), dim3(64 * kW), 0, s, a);
+    return;
+  }
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-  if (a.flags & CCFD_ARG_WIRE_W64)
-    hipLaunchKernelGGL((score_lr_kernel<2, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
-  else if (contig)
+  if (contig)
     hipLaunchKernelGGL((score_lr_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
   else
     hipLaunchKernelGGL((score_lr_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
@@ -151,7 +212,7 @@ int launch_lr_multi(const ccfd_multi_args& m, hipStream_t s) {
   const int wpb = (m.sub_rows + rows_per_wg - 1) / rows_per_wg;
   const dim3 grid(wpb * m.nsub), block(64 * kW);
   if (m.base.flags & CCFD_ARG_WIRE_W64)
-    hipLaunchKernelGGL((score_lr_multi_kernel<2, kW>), grid, block, 0, s, m);
+    hipLaunchKernelGGL((score_lr_wire_multi_kernel<kW, 4>), grid, block, 0, s, m);
   else
     hipLaunchKernelGGL((score_lr_multi_kernel<1, kW>), grid, block, 0, s, m);
   return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "mlp_core.h"
+#include "wire_body.h"
 
 namespace ccfd {
 
@@ -126,97 +127,6 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
   signal_done(a, (unsigned)nblk);
 }
 
-// W64 wire path (kMode 2): one wave scores 16-row tiles with kPf tiles in flight -- a
-// tile's slot is refilled as soon as its operand is consumed, so a wave keeps kPf-1 1-KB
-// requests outstanding while it computes (HBM-resident launches were memory-latency bound
-// at one tile in flight: profiles/r1/kernel_sol*.json).  Loads are branch-free (rows clamped
-// into the batch; clamped rows are never scored) and the steady-state loop is unrolled kPf
-// times over static ring slots, so no register copy of an in-flight load -- which would
-// force an s_waitcnt vmcnt(0) -- is ever needed; only the < kPf-tile tail rotates the ring.
-template <int kWaves, int kPf>
-__device__ __forceinline__ void mlp_wire_body(const ccfd_score_args& a, int blk, int nblk) {
-  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
-  __shared__ EpilogueLds epi;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, c = lane & 15;
-  stamp_start(a, blk);
-  const int n = a.n;
-  const int ntiles = (n + kTileRows - 1) / kTileRows;
-  const int tstride = nblk * kWaves;
-  int tile = blk * kWaves + wave;
-  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x) + 16 * g;
-  auto issue = [&](int t, WireRegs& r) __attribute__((always_inline)) {
-    const int row = min(t * kTileRows + c, n - 1);
-    r.v = *reinterpret_cast<const uint4*>(xw + (size_t)row * CCFD_WIRE_ROW_BYTES);
-  };
-  WireRegs ring[kPf];
-#pragma unroll
-  for (int k = 0; k < kPf; ++k) issue(tile + k * tstride, ring[k]);
-  mlp_stage(a.blob, sblob, tid, 64 * kWaves);
-  epi_init(epi);
-  __syncthreads();
-
-  const MlpWireLane L = mlp_wire_lane(sblob);
-  const float thr = a.threshold;
-  const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
-  unsigned fraud = 0, rows = 0;
-  unsigned long long psum = 0;
-  HistLanes hl;
-  hist_lanes_init(hl, g);
-  auto finish = [&](float p, float amount, int t) __attribute__((always_inline)) {
-    const int row = t * kTileRows + c;
-    const bool valid = row < n;
-    const bool fr = valid && (p >= thr);
-    if (valid && g == 0) {
-      if (store_out) {
-        if (a.proba) a.proba[row] = p;
-        if (a.route) a.route[row] = fr ? 1 : 0;
-      }
-      psum += (unsigned)(p * 1e6f + 0.5f);
-    }
-    const unsigned long long frm = __ballot(fr && g == 3);     // same rows as the g == 0 lanes
-    fraud += __popcll(frm);
-    rows += (unsigned)min(kTileRows, n - t * kTileRows);
-    const float am_g3 = (valid && g == 3) ? amount : -__builtin_inff();
-    hist_lanes_add(hl, __shfl(am_g3, 48 + c));
-    if (frm) {                                                   // rare: fraud rows' buckets
-      if (fr && g == 3) atomicAdd(&epi.hist[kNB + amount_bucket_fast(amount)], 1u);
-      emit_flagged(a, fr && g == 0, row);
-    }
-  };
-  // steady state: the kPf strided tiles of a round all exist
-  const int full_end = ntiles - (kPf - 1) * tstride;
-  while (tile < full_end) {
-#pragma unroll
-    for (int k = 0; k < kPf; ++k) {
-      const float amount = __uint_as_float(ring[k].v.w);
-      const float p = mlp_tile_w64(sblob, L, ring[k], g, lane);
-      issue(tile + kPf * tstride, ring[k]);
-      finish(p, amount, tile);
-      tile += tstride;
-    }
-  }
-  // tail: fewer than kPf tiles left, already in flight in ring[0..]
-#pragma unroll 1
-  for (int k = 0; k < kPf && tile < ntiles; ++k) {
-    const WireRegs cur = ring[0];
-#pragma unroll
-    for (int q = 0; q + 1 < kPf; ++q) ring[q] = ring[q + 1];
-    finish(mlp_tile_w64(sblob, L, cur, g, lane), __uint_as_float(cur.v.w), tile);
-    tile += tstride;
-  }
-  psum = wave_sum_u64(psum);
-  hist_lanes_commit(epi, hl, g, c);
-  if (lane == 0) {
-    atomicAdd(&epi.fraud, fraud);
-    atomicAdd(&epi.rows, rows);
-    atomicAdd(&epi.psum_e6, psum);
-  }
-  epi_flush_ballot(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
-  signal_done(a, (unsigned)nblk);
-}
-
 template <int kMode, int kWaves>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_kernel(ccfd_score_args a) {
@@ -226,7 +136,7 @@ void score_mlp_kernel(ccfd_score_args a) {
 template <int kWaves, int kPf>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_wire_kernel(ccfd_score_args a) {
-  mlp_wire_body<kWaves, kPf>(a, blockIdx.x, gridDim.x);
+  wire_stream_body<MlpWireScorer, kWaves, kPf>(a, blockIdx.x, gridDim.x);
 }
 
 // Coalesced launch: workgroups [j*wpb, (j+1)*wpb) score sub-batch j.
@@ -249,7 +159,7 @@ void score_mlp_wire_multi_kernel(ccfd_multi_args m) {
   const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
   const int wpb = gridDim.x / mk.nsub;
   const int j = blockIdx.x / wpb;
-  mlp_wire_body<kWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+  wire_stream_body<MlpWireScorer, kWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
 // CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4; default 4).

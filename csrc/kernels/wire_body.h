@@ -1,0 +1,104 @@
+// Streaming body shared by the W64 wire kernels (MLP, LR): 16-row tiles per wave with a
+// branch-free prefetch ring, the per-tile epilogue (outputs, counters, lane-spread amount
+// histogram, compacted fraud list) and the workgroup flush.  The model math is a Scorer:
+//   static constexpr int kLds;                       LDS bytes the scorer stages (blob copy)
+//   void stage(const ccfd_score_args&, char* lds, int tid, int nthreads);   before the barrier
+//   void lanes(const char* lds, const ccfd_score_args&, int g);            after the barrier
+//   float tile(const char* lds, const WireRegs&, int g, int lane) const;   proba_1 of row lane&15
+#pragma once
+#include "common.h"
+
+namespace ccfd {
+
+// One wave scores 16-row tiles with kPf tiles in flight -- a tile's slot is refilled as
+// soon as its operand is consumed, so a wave keeps kPf-1 1-KB requests outstanding while it
+// computes.  Loads are branch-free (rows clamped into the batch; clamped rows are never
+// scored) and the steady-state loop is unrolled kPf times over static ring slots, so no
+// register copy of an in-flight load -- which would force an s_waitcnt vmcnt(0) -- is ever
+// needed; only the < kPf-tile tail rotates the ring.
+template <class Scorer, int kWaves, int kPf>
+__device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int blk, int nblk) {
+  __shared__ __attribute__((aligned(16))) char lds[Scorer::kLds > 0 ? Scorer::kLds : 16];
+  __shared__ EpilogueLds epi;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  stamp_start(a, blk);
+  const int n = a.n;
+  const int ntiles = (n + kTileRows - 1) / kTileRows;
+  const int tstride = nblk * kWaves;
+  int tile = blk * kWaves + wave;
+  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x) + 16 * g;
+  auto issue = [&](int t, WireRegs& r) __attribute__((always_inline)) {
+    const int row = min(t * kTileRows + c, n - 1);
+    r.v = *reinterpret_cast<const uint4*>(xw + (size_t)row * CCFD_WIRE_ROW_BYTES);
+  };
+  WireRegs ring[kPf];
+#pragma unroll
+  for (int k = 0; k < kPf; ++k) issue(tile + k * tstride, ring[k]);
+  Scorer sc;
+  sc.stage(a, lds, tid, 64 * kWaves);
+  epi_init(epi);
+  __syncthreads();
+  sc.lanes(lds, a, g);
+
+  const float thr = a.threshold;
+  const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
+  unsigned fraud = 0, rows = 0;
+  unsigned long long psum = 0;
+  HistLanes hl;
+  hist_lanes_init(hl, g);
+  auto finish = [&](float p, float amount, int t) __attribute__((always_inline)) {
+    const int row = t * kTileRows + c;
+    const bool valid = row < n;
+    const bool fr = valid && (p >= thr);
+    if (valid && g == 0) {
+      if (store_out) {
+        if (a.proba) a.proba[row] = p;
+        if (a.route) a.route[row] = fr ? 1 : 0;
+      }
+      psum += (unsigned)(p * 1e6f + 0.5f);
+    }
+    const unsigned long long frm = __ballot(fr && g == 3);     // same rows as the g == 0 lanes
+    fraud += __popcll(frm);
+    rows += (unsigned)min(kTileRows, n - t * kTileRows);
+    const float am_g3 = (valid && g == 3) ? amount : -__builtin_inff();
+    hist_lanes_add(hl, __shfl(am_g3, 48 + c));
+    if (frm) {                                                   // rare: fraud rows' buckets
+      if (fr && g == 3) atomicAdd(&epi.hist[kNB + amount_bucket_fast(amount)], 1u);
+      emit_flagged(a, fr && g == 0, row);
+    }
+  };
+  // steady state: the kPf strided tiles of a round all exist
+  const int full_end = ntiles - (kPf - 1) * tstride;
+  while (tile < full_end) {
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) {
+      const float amount = __uint_as_float(ring[k].v.w);
+      const float p = sc.tile(lds, ring[k], g, lane);
+      issue(tile + kPf * tstride, ring[k]);
+      finish(p, amount, tile);
+      tile += tstride;
+    }
+  }
+  // tail: fewer than kPf tiles left, already in flight in ring[0..]
+#pragma unroll 1
+  for (int k = 0; k < kPf && tile < ntiles; ++k) {
+    const WireRegs cur = ring[0];
+#pragma unroll
+    for (int q = 0; q + 1 < kPf; ++q) ring[q] = ring[q + 1];
+    finish(sc.tile(lds, cur, g, lane), __uint_as_float(cur.v.w), tile);
+    tile += tstride;
+  }
+  psum = wave_sum_u64(psum);
+  hist_lanes_commit(epi, hl, g, c);
+  if (lane == 0) {
+    atomicAdd(&epi.fraud, fraud);
+    atomicAdd(&epi.rows, rows);
+    atomicAdd(&epi.psum_e6, psum);
+  }
+  epi_flush_ballot(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
+  signal_done(a, (unsigned)nblk);
+}
+
+}  // namespace ccfd
