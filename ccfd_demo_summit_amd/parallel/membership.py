@@ -7,7 +7,8 @@ DeploymentConfigs: deploy/router.yaml:11-20,75-76, deploy/ccd-service.yaml:11-20
 Here the job's ranks share a KV store that outlives any single rank (the launcher's or the
 test's ``TCPStore``; rank 0's store would die with rank 0) and:
 
-* every rank bumps a heartbeat counter ``hb/<r>`` each tick; an observer calls a rank dead
+* every rank bumps a heartbeat counter ``hb/<r>`` from its own thread (so a blocking group
+  build never makes it look dead); an observer calls a rank dead
   when ITS OWN monotonic clock saw no change of that counter for ``ttl`` (no cross-host
   clock comparison), and a never-seen rank only after a start-up grace;
 * the lowest live rank proposes generation ``g+1 = sorted(live ranks)`` with one
@@ -16,7 +17,9 @@ test's ``TCPStore``; rank 0's store would die with rank 0) and:
 * every member of the new generation builds a FRESH process group for it on a
   ``PrefixStore("g<g>/")`` -- gloo, or RCCL (``ProcessGroupNCCL``) for GPU tensors -- and
   aborts the previous one, so a collective stuck on a dead peer is cancelled instead of
-  hanging the survivors.  ``torch.distributed``'s default group is never touched.
+  hanging the survivors.  A build that times out (a member died mid-rendezvous) bumps the
+  generation with one CAS so every member retries on fresh keys.  ``torch.distributed``'s
+  default group is never touched.
 
 Collectives are only ever issued asynchronously and polled (``ElasticGroup.poll``): a
 failure shows up as an exception (gloo: peer connection reset) or as a generation change
@@ -29,6 +32,7 @@ parallel/elastic.py, which stays the exactly-once source of truth.)
 from __future__ import annotations
 
 import datetime
+import threading
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -112,7 +116,7 @@ class ElasticGroup:
 
     def __init__(self, store, rank: int, world: int, backend: str = "gloo",
                  device: Optional[torch.device] = None, ttl_s: float = 2.0, timeout_s: float = 30.0,
-                 prefix: str = "ccfd/mem/", grace_s: Optional[float] = None):
+                 prefix: str = "ccfd/mem/", grace_s: Optional[float] = None, heartbeat_thread: bool = True):
         self.store = store
         self.rank = rank
         self.backend = backend
@@ -124,6 +128,24 @@ class ElasticGroup:
         self.members: List[int] = []
         self.pg = None
         self.regroups = 0
+        self.build_failures = 0
+        # Heartbeats from their own thread: building a group for a new generation blocks until
+        # every member has joined, and a rank that stopped heartbeating meanwhile would be
+        # declared dead by the others (generation flapping).
+        self._stop = threading.Event()
+        self._hb = None
+        if heartbeat_thread:
+            self.membership.heartbeat()
+            self._hb = threading.Thread(target=self._beat, name=f"ccfd-hb-{rank}", daemon=True)
+            self._hb.start()
+
+    def _beat(self) -> None:
+        period = max(0.01, self.membership.ttl / 5)
+        while not self._stop.wait(period):
+            try:
+                self.membership.heartbeat()
+            except Exception:
+                return                      # store gone: the job is over
 
     @property
     def member(self) -> bool:
@@ -153,7 +175,8 @@ class ElasticGroup:
     def tick(self) -> bool:
         """Heartbeat, propose if leader, and follow the published generation.  Returns True
         when this call switched generations (the caller must treat in-flight work as lost)."""
-        self.membership.heartbeat()
+        if self._hb is None:
+            self.membership.heartbeat()
         self.membership.propose()
         gen, members = self.membership.view()
         if gen == self.gen:
@@ -162,7 +185,16 @@ class ElasticGroup:
         self.gen, self.members = gen, members
         self.regroups += 1
         if self.rank in members:
-            self.pg = self._build(gen, members)
+            try:
+                self.pg = self._build(gen, members)
+            except Exception:
+                # a member never joined generation `gen` (it died, or moved on): bump the
+                # generation with one CAS so every member retries on a fresh key prefix
+                self.pg = None
+                self.build_failures += 1
+                key = f"{self.prefix}gen"
+                cur = f"{gen}:{','.join(str(r) for r in members)}"
+                self.store.compare_set(key, cur, f"{gen + 1}:{','.join(str(r) for r in members)}")
         return True
 
     def all_reduce(self, t: torch.Tensor):
@@ -185,6 +217,7 @@ class ElasticGroup:
         return "done"
 
     def close(self) -> None:
+        self._stop.set()
         self._drop()
 
 
