@@ -13,6 +13,10 @@ services:
   engine       GPU streaming engine, one rank per GPU (run under torchrun)  (port 8091+rank)
   producer     transaction producer (synthetic / creditcard.csv)
   demo         everything in one process over an in-process broker
+  store        the job's shared KV store (TCPStore) for leases / membership   (port 29400)
+  elastic      failure-tolerant scoring rank: partition leases (fail-over, exactly-once
+               committed counts) + membership generations whose process group carries the
+               global X2 counters; a supervised restart rejoins   (--store, --rank, --world)
   supervise    restart-on-crash supervisor:  supervise [--max-restarts N] -- <cmd...>
 
 Configuration: the reference env var names (BROKER_URL, KAFKA_TOPIC, SELDON_URL, ...),
@@ -285,6 +289,75 @@ def cmd_demo(a, cfg):
                       "scorer": getattr(scorer, "device", "cpu")}), flush=True)
 
 
+def cmd_store(a, cfg):
+    """Host the job's TCPStore (it must outlive every rank, so it is its own process)."""
+    import datetime
+
+    import torch.distributed as dist
+    port = a.port or 29400
+    store = dist.TCPStore(a.host if a.host != "0.0.0.0" else "127.0.0.1", port, 1, True,
+                          timeout=datetime.timedelta(seconds=3600), wait_for_workers=False)
+    print(f"[store] TCPStore on :{port}", flush=True)
+    while True:
+        time.sleep(3600)
+        store.check(["__alive__"])
+
+
+def cmd_elastic(a, cfg):
+    """One failure-tolerant scoring rank (parallel/elastic.py leases + parallel/membership.py)."""
+    import datetime
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from ..metrics.exporter import RouterMetrics
+    from ..parallel.elastic import PartitionLeases
+    from ..parallel.membership import ElasticCounterReducer, ElasticGroup
+    from ..process.kie_server import KieClient
+    from ..router.router import Router
+    from ..router.rules import RuleSet
+    from ..serving.scorers import CpuScorer, GpuScorer
+    from .elastic_worker import ElasticWorker
+    host, _, port = a.store.rpartition(":")
+    store = dist.TCPStore(host or "127.0.0.1", int(port), is_master=False,
+                          timeout=datetime.timedelta(seconds=120))
+    model = _model(cfg.engine.model, a.weights)
+    use_gpu = a.device == "gpu" or (a.device == "auto" and torch.cuda.is_available())
+    scorer = (GpuScorer(model, cfg.router.fraud_threshold, device_index=a.rank % max(1, torch.cuda.device_count()))
+              if use_gpu else CpuScorer(model, cfg.router.fraud_threshold))
+    rm = RouterMetrics()
+    if a.kie == "local":
+        from ..process import ProcessEngine
+        sink = ProcessEngine(notification_timeout_s=1e9)
+    else:
+        sink = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
+                         cfg.kie.signal_name)
+    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), sink, rm)
+    broker = _broker(cfg)
+    leases = PartitionLeases(store, a.rank, a.world, a.partitions, ttl_s=a.ttl)
+    worker = ElasticWorker(a.rank, leases, broker, cfg.kafka.transactions_topic, scorer, router,
+                           group=cfg.kafka.group_id, max_records=a.max_batch)
+    grp = ElasticGroup(store, a.rank, a.world, backend="gloo", ttl_s=a.ttl, timeout_s=max(10.0, 5 * a.ttl))
+    x2 = ElasticCounterReducer(grp, 2)
+    _serve_in_thread(_metrics_app(rm.expose), a.host, (a.port or cfg.router.port) + a.rank)
+    t_end = time.time() + a.seconds if a.seconds > 0 else float("inf")
+    last_rows = last_fraud = 0
+    while time.time() < t_end and not store.check(["stop"]):
+        worker.tick()
+        if grp.tick():
+            x2.on_regroup()
+        rows, fraud = worker.routed
+        if rows != last_rows or fraud != last_fraud:
+            x2.submit(torch.tensor([rows - last_rows, fraud - last_fraud], dtype=torch.int64))
+            last_rows, last_fraud = rows, fraud
+        x2.progress()
+        t = x2.totals.tolist()
+        store.set(f"x2/{a.rank}", f"{grp.gen}|{','.join(map(str, grp.members))}|{t[0]},{t[1]}")
+        time.sleep(0.005)
+    grp.close()
+
+
 def cmd_supervise(a, cfg):
     from .supervisor import supervise
     sys.exit(supervise(a.cmd, max_restarts=a.max_restarts, backoff_s=a.backoff))
@@ -301,7 +374,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser(prog="python -m ccfd_demo_summit_amd.launch", description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
-                                        "engine", "producer", "demo", "supervise"])
+                                        "engine", "producer", "demo", "store", "elastic", "supervise"])
     ap.add_argument("--config", default=None)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=None)
@@ -320,8 +393,19 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--max-batch", type=int, default=4096)
     ap.add_argument("--max-restarts", type=int, default=10)
     ap.add_argument("--backoff", type=float, default=1.0)
+    ap.add_argument("--store", default="127.0.0.1:29400", help="elastic: host:port of the job's TCPStore")
+    ap.add_argument("--rank", type=int, default=int(os.environ.get("RANK", "0")))
+    ap.add_argument("--world", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--partitions", type=int, default=0, help="elastic: topic partitions (0 = 2 x world)")
+    ap.add_argument("--ttl", type=float, default=2.0, help="elastic: lease / heartbeat ttl (s)")
+    ap.add_argument("--kie", default="remote", choices=["remote", "local"],
+                    help="elastic: fraud hand-off to KIE_SERVER_URL or an in-process engine")
     a = ap.parse_args(argv)
     a.cmd = cmd
+    if a.service == "elastic" and a.partitions <= 0:
+        a.partitions = 2 * a.world
+    if a.service == "elastic" and a.seconds == 10.0 and "--seconds" not in argv:
+        a.seconds = 0.0                 # elastic ranks run until the store says stop
     return a
 
 

@@ -33,6 +33,7 @@ class ElasticWorker:
         self.counts: Dict[int, list] = {}
         self.alive = True
         self.scored_rows = 0
+        self.routed = [0, 0]             # rows routed, fraud-routed (incl. re-scored rows): X2 feed
         # injected faults (utils/faults.py; CCFD_FAULTS): drop / delay / crash this rank
         self.faults = faults if faults is not None else FaultPlan.from_env(rank)
 
@@ -71,6 +72,8 @@ class ElasticWorker:
             res = self.router.on_scored(ids, cust, proba, X=X, routes=route)
             n += len(X)
             self.scored_rows += len(X)
+            self.routed[0] += res["incoming"]
+            self.routed[1] += res["fraud"]
             if crash_before_commit:
                 self.alive = False                 # dies: no commit, no lease renewal
                 return n

@@ -50,3 +50,59 @@ def test_launch_options_after_service_name_are_parsed():
     assert a.port == 1 and a.service == "kafka-lite"
     a = parse_args(["supervise", "--max-restarts", "3", "--", "python", "-c", "print(1)", "--port", "9"])
     assert a.max_restarts == 3 and a.cmd == ["python", "-c", "print(1)", "--port", "9"] and a.port is None
+
+
+def test_elastic_service_ranks_score_topic_exactly_once():
+    """`launch elastic` ranks (real processes) share a TCPStore and a kafka-lite broker:
+    the topic is scored once (committed counts) and every rank's X2 totals -- reduced over
+    the membership generation's process group -- equal the global counts."""
+    import datetime
+    import os
+    import socket
+    import time
+
+    import torch.distributed as dist
+
+    from ccfd_demo_summit_amd.ingest import ProducerConfig, TransactionProducer
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    from ccfd_demo_summit_amd.parallel.elastic import PartitionLeases
+
+    def free_port():
+        s = socket.socket(); s.bind(("127.0.0.1", 0)); p = s.getsockname()[1]; s.close()
+        return p
+    sport = free_port()
+    store = dist.TCPStore("127.0.0.1", sport, 1, True, timeout=datetime.timedelta(seconds=60), wait_for_workers=False)
+    lite = KafkaLiteServer("127.0.0.1", 0, default_partitions=4).start_in_thread()
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 4)
+    TransactionProducer(kb, ProducerConfig(fmt="json", batch=500, seed=5)).produce(3000)
+    env = dict(os.environ, BROKER_URL=lite.bootstrap, KAFKA_TOPIC="odh-demo")
+    mport = free_port()
+    procs = [subprocess.Popen([sys.executable, "-m", "ccfd_demo_summit_amd.launch", "elastic", "--store",
+                               f"127.0.0.1:{sport}", "--rank", str(r), "--world", "2", "--partitions", "4",
+                               "--device", "cpu", "--kie", "local", "--ttl", "1.0", "--host", "127.0.0.1",
+                               "--port", str(mport)], env=env)
+             for r in range(2)]
+    try:
+        reader = PartitionLeases(store, 99, 2, 4, ttl_s=1.0)
+        t0 = time.time()
+        rows = fraud = 0
+        while time.time() - t0 < 180:
+            rows, fraud = reader.global_counts()
+            x2 = [store.get(f"x2/{r}").decode() if store.check([f"x2/{r}"]) else "" for r in range(2)]
+            if rows == 3000 and all(x.endswith(f"|{rows},{fraud}") for x in x2):
+                break
+            assert all(p.poll() is None for p in procs), "an elastic rank exited"
+            time.sleep(0.1)
+        assert rows == 3000
+        assert all(x.split("|")[1] == "0,1" and x.endswith(f"|3000,{fraud}") for x in x2), x2
+    finally:
+        store.set("stop", "1")
+        for p in procs:
+            try:
+                p.wait(30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        kb.close()
+        lite.stop()
