@@ -12,9 +12,11 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import itertools
 import struct
 import threading
-from typing import Optional
+import time
+from typing import Dict, Optional, Set
 
 from .broker import InProcBroker
 from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS,
@@ -23,6 +25,32 @@ from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_NONE, ERR_OFFSET_OUT_O
                          decode_record_batches, encode_record_batch)
 
 NODE_ID = 1
+ERR_ILLEGAL_GENERATION, ERR_UNKNOWN_MEMBER, ERR_REBALANCE_IN_PROGRESS = 22, 25, 27
+
+
+class _Member:
+    def __init__(self, mid: str, session_ms: int, rebalance_ms: int):
+        self.mid = mid
+        self.session_s = session_ms / 1000.0
+        self.rebalance_s = rebalance_ms / 1000.0
+        self.metadata = b""
+        self.assignment = b""
+        self.last_seen = time.monotonic()
+        self.join_fut: Optional[asyncio.Future] = None
+        self.sync_fut: Optional[asyncio.Future] = None
+
+
+class _Group:
+    """Classic group coordinator state: Empty -> PreparingRebalance (members rejoin) ->
+    CompletingRebalance (leader's SyncGroup) -> Stable."""
+
+    def __init__(self):
+        self.state = "Empty"
+        self.generation = 0
+        self.members: Dict[str, _Member] = {}
+        self.joined: Set[str] = set()
+        self.leader = ""
+        self.deadline_task: Optional[asyncio.Task] = None
 
 
 class BrokerMetrics:
@@ -71,11 +99,15 @@ class KafkaLiteServer:
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._thread: Optional[threading.Thread] = None
         self.metrics = BrokerMetrics(self)
+        self.groups: Dict[str, _Group] = {}
+        self._mid = itertools.count(1)
+        self._reaper: Optional[asyncio.Task] = None
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
         self._server = await asyncio.start_server(self._serve, self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
+        self._reaper = asyncio.get_running_loop().create_task(self._reap_sessions())
 
     def start_in_thread(self) -> "KafkaLiteServer":
         ready = threading.Event()
@@ -118,6 +150,8 @@ class KafkaLiteServer:
                 api, ver, corr = r.i16(), r.i16(), r.i32()
                 r.string()                                  # client id
                 body = self._dispatch(api, ver, r)
+                if not isinstance(body, (bytes, bytearray)):   # group APIs long-poll (JoinGroup, SyncGroup)
+                    body = await body
                 out = struct.pack(">i", corr) + body
                 writer.write(struct.pack(">i", len(out)) + out)
                 await writer.drain()
@@ -275,6 +309,140 @@ class KafkaLiteServer:
         return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
             t[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).string(None).i16(ERR_NONE))).build()
 
+
+    # ------------------------------------------------------------------ group coordinator
+    # JoinGroup v1 / SyncGroup v0 / Heartbeat v0 / LeaveGroup v0 (client: ingest/kafka_group.py)
+    def _prepare_rebalance(self, g: _Group, rebalance_s: float) -> None:
+        if g.state == "PreparingRebalance":
+            return
+        g.state = "PreparingRebalance"
+        g.joined = set()
+        for m in g.members.values():                 # members parked in SyncGroup must rejoin
+            if m.sync_fut is not None and not m.sync_fut.done():
+                m.sync_fut.set_result(Writer().i16(ERR_REBALANCE_IN_PROGRESS).bytes_(b"").build())
+            m.sync_fut = None
+        if g.deadline_task is not None:
+            g.deadline_task.cancel()
+
+        async def deadline():
+            await asyncio.sleep(rebalance_s)
+            if g.state == "PreparingRebalance":     # stragglers are dropped from the group
+                for mid in [m for m in g.members if m not in g.joined]:
+                    del g.members[mid]
+                self._maybe_complete_join(g)
+        g.deadline_task = asyncio.get_running_loop().create_task(deadline())
+
+    def _maybe_complete_join(self, g: _Group) -> None:
+        if g.state != "PreparingRebalance" or not g.joined >= set(g.members):
+            return
+        if g.deadline_task is not None:
+            g.deadline_task.cancel()
+            g.deadline_task = None
+        if not g.members:
+            g.state = "Empty"
+            return
+        g.generation += 1
+        if g.leader not in g.members:
+            g.leader = sorted(g.members)[0]
+        g.state = "CompletingRebalance"
+        everyone = [(m.mid, m.metadata) for m in g.members.values()]
+        for m in g.members.values():
+            m.last_seen = time.monotonic()
+            body = (Writer().i16(ERR_NONE).i32(g.generation).string("range").string(g.leader).string(m.mid)
+                    .array(everyone if m.mid == g.leader else [], lambda w, e: w.string(e[0]).bytes_(e[1])).build())
+            if m.join_fut is not None and not m.join_fut.done():
+                m.join_fut.set_result(body)
+            m.join_fut = None
+
+    def _remove_member(self, g: _Group, mid: str) -> None:
+        m = g.members.pop(mid, None)
+        if m is None:
+            return
+        g.joined.discard(mid)
+        if g.members:
+            self._prepare_rebalance(g, max(x.rebalance_s for x in g.members.values()))
+            self._maybe_complete_join(g)
+        else:
+            g.state = "Empty"
+
+    async def _reap_sessions(self):
+        while True:
+            await asyncio.sleep(0.1)
+            now = time.monotonic()
+            for g in self.groups.values():
+                for mid, m in list(g.members.items()):
+                    parked = m.join_fut is not None and not m.join_fut.done()
+                    if not parked and now - m.last_seen > m.session_s:
+                        self._remove_member(g, mid)
+
+    def _api_11(self, r: Reader):                           # JoinGroup v1 (long poll)
+        group, session_ms, rebalance_ms, mid, _ptype = r.string(), r.i32(), r.i32(), r.string(), r.string()
+        protos = dict(r.array(lambda x: (x.string(), x.bytes_())) or [])
+        g = self.groups.setdefault(group, _Group())
+        if mid and mid not in g.members:
+            return Writer().i16(ERR_UNKNOWN_MEMBER).i32(-1).string("").string("").string(mid).array([], None).build()
+        if not mid:
+            mid = f"member-{next(self._mid)}"
+            g.members[mid] = _Member(mid, session_ms, rebalance_ms)
+        m = g.members[mid]
+        m.metadata = protos.get("range", b"")
+        m.last_seen = time.monotonic()
+        fut = asyncio.get_running_loop().create_future()
+        m.join_fut = fut
+        self._prepare_rebalance(g, rebalance_ms / 1000.0)
+        g.joined.add(mid)
+        self._maybe_complete_join(g)
+        return fut
+
+    def _api_14(self, r: Reader):                           # SyncGroup v0
+        group, gen, mid = r.string(), r.i32(), r.string()
+        assignments = r.array(lambda x: (x.string(), x.bytes_())) or []
+        g = self.groups.get(group)
+        err = None
+        if g is None or mid not in g.members:
+            err = ERR_UNKNOWN_MEMBER
+        elif g.state == "PreparingRebalance":
+            err = ERR_REBALANCE_IN_PROGRESS
+        elif gen != g.generation:
+            err = ERR_ILLEGAL_GENERATION
+        if err is not None:
+            return Writer().i16(err).bytes_(b"").build()
+        m = g.members[mid]
+        m.last_seen = time.monotonic()
+        if mid == g.leader and g.state == "CompletingRebalance":
+            for member, a in assignments:
+                if member in g.members:
+                    g.members[member].assignment = a
+            g.state = "Stable"
+            for o in g.members.values():
+                if o.sync_fut is not None and not o.sync_fut.done():
+                    o.sync_fut.set_result(Writer().i16(ERR_NONE).bytes_(o.assignment).build())
+                o.sync_fut = None
+        if g.state == "Stable":
+            return Writer().i16(ERR_NONE).bytes_(m.assignment).build()
+        fut = asyncio.get_running_loop().create_future()
+        m.sync_fut = fut
+        return fut
+
+    def _api_12(self, r: Reader) -> bytes:                  # Heartbeat v0
+        group, gen, mid = r.string(), r.i32(), r.string()
+        g = self.groups.get(group)
+        if g is None or mid not in g.members:
+            return Writer().i16(ERR_UNKNOWN_MEMBER).build()
+        g.members[mid].last_seen = time.monotonic()
+        if g.state == "PreparingRebalance":
+            return Writer().i16(ERR_REBALANCE_IN_PROGRESS).build()
+        if gen != g.generation:
+            return Writer().i16(ERR_ILLEGAL_GENERATION).build()
+        return Writer().i16(ERR_NONE).build()
+
+    def _api_13(self, r: Reader) -> bytes:                  # LeaveGroup v0
+        group, mid = r.string(), r.string()
+        g = self.groups.get(group)
+        if g is None or mid not in g.members:
+            return Writer().i16(ERR_UNKNOWN_MEMBER).build()
+        self._remove_member(g, mid)
+        return Writer().i16(ERR_NONE).build()
 
 def main(argv=None):
     ap = argparse.ArgumentParser()

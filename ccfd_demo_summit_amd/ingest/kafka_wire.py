@@ -29,8 +29,10 @@ from .broker import BrokerError, Record
 # --------------------------------------------------------------------------- api keys
 PRODUCE, FETCH, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH, FIND_COORDINATOR = 0, 1, 2, 3, 8, 9, 10
 API_VERSIONS, CREATE_TOPICS = 18, 19
+JOIN_GROUP, HEARTBEAT, LEAVE_GROUP, SYNC_GROUP = 11, 12, 13, 14       # ingest/kafka_group.py
 SUPPORTED = {PRODUCE: 3, FETCH: 4, LIST_OFFSETS: 1, METADATA: 1, OFFSET_COMMIT: 2, OFFSET_FETCH: 1,
-             FIND_COORDINATOR: 0, API_VERSIONS: 0, CREATE_TOPICS: 0}
+             FIND_COORDINATOR: 0, API_VERSIONS: 0, CREATE_TOPICS: 0,
+             JOIN_GROUP: 1, HEARTBEAT: 0, LEAVE_GROUP: 0, SYNC_GROUP: 0}
 
 ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_UNKNOWN_TOPIC, ERR_CORRUPT = 0, 1, 3, 2
 ERR_UNSUPPORTED_VERSION, ERR_TOPIC_EXISTS, ERR_INVALID_REQUEST = 35, 36, 42
@@ -488,6 +490,12 @@ class KafkaBroker:
     def consumer(self, group: str, topics: Sequence[str], partitions: Optional[Sequence[Tuple[str, int]]] = None,
                  member_id: Optional[str] = None, auto_commit: bool = False) -> "WireConsumer":
         return WireConsumer(self, group, list(topics), partitions, auto_commit)
+
+    def group_consumer(self, group: str, topics: Sequence[str], **kw):
+        """Consumer-group member (JoinGroup/SyncGroup/Heartbeat, range assignor): partitions are
+        assigned by the group coordinator and move on member failure (ingest/kafka_group.py)."""
+        from .kafka_group import GroupConsumer
+        return GroupConsumer(self, group, topics, client_id=self.client_id, **kw)
 
     def wait_for_data(self, predicate, timeout: float) -> bool:
         end = time.monotonic() + timeout

@@ -42,6 +42,15 @@ def _broker(cfg, inproc=None):
     return KafkaBroker(cfg.kafka.broker_url, connect_wait_s=120.0)   # wait for the broker to come up
 
 
+def _consumer(broker, a, group, topics):
+    """Static consumer (every partition), or with --group-membership a Kafka consumer-group
+    member whose partitions the coordinator assigns and moves on failure -- how the
+    reference's replicated services share a topic (ingest/kafka_group.py)."""
+    if getattr(a, "group_membership", False) and hasattr(broker, "group_consumer"):
+        return broker.group_consumer(group, topics, session_timeout_s=a.session_timeout)
+    return broker.consumer(group, topics)
+
+
 def _model(kind: str, weights: str = None, seed: int = 0):
     from ..data import FRAUD_RATE, generate
     from ..models import build_model, load_model
@@ -145,7 +154,7 @@ def cmd_notifier(a, cfg):
     ns = NotificationService(lambda raw, key: broker.produce(cfg.kafka.response_topic, raw, key=key),
                              cfg.notifier.p_reply, cfg.notifier.p_approve, cfg.notifier.mean_delay_s,
                              cfg.notifier.seed)
-    cons = broker.consumer("notification-service", [cfg.kafka.notification_topic])
+    cons = _consumer(broker, a, "notification-service", [cfg.kafka.notification_topic])
     app = web.Application()
     app.router.add_get("/health/ping", lambda _r: web.json_response(
         {"status": "ok", "sent": ns.sent, "replied": ns.replied, "no_reply": ns.no_reply}))
@@ -176,9 +185,9 @@ def cmd_router(a, cfg):
     sc = SeldonClient(cfg.seldon.url, cfg.seldon.endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
                       cfg.seldon.pool_size)
     _serve_in_thread(_metrics_app(rm.expose), a.host, a.port or cfg.router.port)
-    tx = broker.consumer(cfg.kafka.group_id, [cfg.kafka.transactions_topic])
-    resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic])
-    notif = broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
+    tx = _consumer(broker, a, cfg.kafka.group_id, [cfg.kafka.transactions_topic])
+    resp = _consumer(broker, a, cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic])
+    notif = _consumer(broker, a, cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
     while True:
         recs = tx.poll(timeout=0.05, max_records=a.max_batch)
         if recs:
@@ -393,6 +402,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--max-batch", type=int, default=4096)
     ap.add_argument("--max-restarts", type=int, default=10)
     ap.add_argument("--backoff", type=float, default=1.0)
+    ap.add_argument("--group-membership", action="store_true",
+                    help="router/notifier: join the Kafka consumer group (coordinator-assigned partitions)")
+    ap.add_argument("--session-timeout", type=float, default=10.0, help="consumer-group session timeout (s)")
     ap.add_argument("--store", default="127.0.0.1:29400", help="elastic: host:port of the job's TCPStore")
     ap.add_argument("--rank", type=int, default=int(os.environ.get("RANK", "0")))
     ap.add_argument("--world", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
