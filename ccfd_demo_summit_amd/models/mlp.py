@@ -23,7 +23,9 @@ W64 wire blobs (``pack(wire=True)``, header flag FLAG_WIRE): the row's 16-B lane
 the layer-1 B fragment -- the bf16 V-columns go into the MFMA as raw bits, their
 normalisation folded into W1 (columns x 1/sigma) and b1 (minus W1'.mu); b1 rides in
 K-columns 30/31 as a bf16 hi/lo pair against constant-1 inputs; only Time and Amount are
-normalised in the kernel (lane group 3).  ``wire_logits`` is the numerics oracle of that path.
+normalised in the kernel (lane group 3).  Layer 3 is two more MFMAs on bf16 relu(H2^T) against
+W3pad (w3 in rows 0/4/8/12: z lands in every lane group, no cross-lane reduction), appended
+as ``[25920, 27968)`` (``WIRE_BLOB_BYTES``).  ``wire_logits`` is the numerics oracle of that path.
 
 Blob layout (bytes, all 16-B aligned), ``BLOB_BYTES`` = 25920:
   [0,64)        header: 'MLP1', flags(u32), b3(f32)
@@ -56,6 +58,10 @@ BLOB_BYTES = OFF_W3 + 4 * 4 * 4 * 4
 assert BLOB_BYTES == 25920 and BLOB_BYTES % 16 == 0
 
 WIRE_N_BF16 = 28     # wire positions [0, 28) are bf16 V1..V28 (raw MFMA operands)
+# wire blobs append layer 3 as MFMA A-fragments: W3pad [16 x 64] bf16 with w3 in rows 0, 4, 8,
+# 12 (so every lane group's accumulator register 0 receives z), 2 K-steps x 64 lanes x 8
+OFF_W3F = BLOB_BYTES
+WIRE_BLOB_BYTES = OFF_W3F + 2 * 64 * 8 * 2
 
 
 def _pi(s: int, g: int, j: int) -> int:
@@ -155,7 +161,8 @@ class MLPModel:
         W1p = bf16_round(self._wire_w1()).astype(np.float64)
         h1 = bf16_round(np.maximum(xin @ W1p.T, 0.0).astype(np.float32)).astype(np.float64)
         h2 = np.maximum(h1 @ bf16_round(self.W2).T.astype(np.float64) + self.b2, 0.0)
-        return (h2 @ self.w3.astype(np.float64) + self.b3).astype(np.float32)
+        h2 = bf16_round(h2.astype(np.float32)).astype(np.float64)
+        return (h2 @ bf16_round(self.w3).astype(np.float64) + self.b3).astype(np.float32)
 
     def wire_proba(self, X: np.ndarray) -> np.ndarray:
         return sigmoid(self.wire_logits(X))
@@ -190,6 +197,15 @@ class MLPModel:
                 + b1f.astype(np.float32).tobytes() + b2f.astype(np.float32).tobytes()
                 + w3f.astype(np.float32).tobytes())
         assert len(blob) == BLOB_BYTES, len(blob)
+        if wire:
+            # W3f[s][l][j] = w3[pi(s, l>>4, j)] in rows (l&15) in {0,4,8,12}, else 0
+            w3f = np.zeros((2, 64, 8), np.float32)
+            for s_ in range(2):
+                for ln in range(64):
+                    if (ln & 15) % 4 == 0:
+                        w3f[s_, ln] = [self.w3[_pi(s_, ln >> 4, jj)] for jj in range(8)]
+            blob += bf16_bits(w3f).tobytes()
+            assert len(blob) == WIRE_BLOB_BYTES
         return blob
 
     # ---------------------------------------------------------------- state io
@@ -278,10 +294,18 @@ def emulate_packed_kernel(blob: bytes, X: np.ndarray) -> np.ndarray:
                 Bf = np.concatenate([np.maximum(acc1[2 * s], 0), np.maximum(acc1[2 * s + 1], 0)], axis=1)
                 acc = mfma(W2f[u, s], bf16_round(Bf.astype(np.float32)), acc)
             acc2.append(acc)
-        z = np.zeros(64)
-        for u in range(4):
-            z += (np.maximum(acc2[u], 0) * w3f[u][g]).sum(1)
-        zt = np.array([z[cc] + z[cc + 16] + z[cc + 32] + z[cc + 48] for cc in range(16)]) + b3
+        if wire:
+            W3f = bf(OFF_W3F, 2 * 64 * 8).reshape(2, 64, 8)
+            acc3 = np.zeros((64, 4))
+            for s_ in range(2):
+                Bf = np.concatenate([np.maximum(acc2[2 * s_], 0), np.maximum(acc2[2 * s_ + 1], 0)], axis=1)
+                acc3 = mfma(W3f[s_], bf16_round(Bf.astype(np.float32)), acc3)
+            zt = acc3[:16, 0] + b3                      # lane group 0, register 0: row 0 of D
+        else:
+            z = np.zeros(64)
+            for u in range(4):
+                z += (np.maximum(acc2[u], 0) * w3f[u][g]).sum(1)
+            zt = np.array([z[cc] + z[cc + 16] + z[cc + 32] + z[cc + 48] for cc in range(16)]) + b3
         for cc in range(16):
             if t0 + cc < n:
                 out[t0 + cc] = 1.0 / (1.0 + np.exp(-zt[cc]))

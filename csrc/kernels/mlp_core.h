@@ -14,12 +14,16 @@ constexpr int kOffB1 = kOffW2 + 16 * 64 * 16;
 constexpr int kOffB2 = kOffB1 + 8 * 4 * 16;
 constexpr int kOffW3 = kOffB2 + 4 * 4 * 16;
 static_assert(kOffW3 + 4 * 4 * 16 == kMlpBlob, "blob layout");
+// W64 wire blobs append layer 3 as MFMA A-fragments (models/mlp.py WIRE_BLOB_BYTES)
+constexpr int kOffW3F = kMlpBlob;
+constexpr int kMlpBlobWire = kOffW3F + 2 * 64 * 16;
 
-// Stage the packed model (1620 x 16 B) into LDS; caller synchronises.
-__device__ __forceinline__ void mlp_stage(const void* blob, char* sblob, int tid, int nthreads) {
+// Stage the packed model (bytes / 16 int4) into LDS; caller synchronises.
+__device__ __forceinline__ void mlp_stage(const void* blob, char* sblob, int tid, int nthreads,
+                                          int bytes = kMlpBlob) {
   const int4* src = reinterpret_cast<const int4*>(blob);
   int4* dst = reinterpret_cast<int4*>(sblob);
-  for (int i = tid; i < kMlpBlob / 16; i += nthreads) dst[i] = src[i];
+  for (int i = tid; i < bytes / 16; i += nthreads) dst[i] = src[i];
 }
 
 // Per-lane constants (lane group g = lane >> 4 owns features 8g..8g+7).
@@ -179,28 +183,38 @@ __device__ __forceinline__ float mlp_tile_w64(const char* sblob, const MlpWireLa
                                relu_pack_bf16x2(acc1[2 * s + 1][2], acc1[2 * s + 1][3]));
     hb[s] = __builtin_bit_cast(bf16x8, u);
   }
-  float z = 0.f;
+  // layer 2, then layer 3 as two more MFMAs: relu(H2^T) packed to bf16 exactly like layer 1's
+  // output (K-step s' = M-tiles 2s', 2s'+1) against W3pad, whose rows 0/4/8/12 hold w3 -- so
+  // register 0 of EVERY lane group receives z of row (lane & 15): no cross-lane reduction
+  f32x4 acc2[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     f32x4 acc = b2f[u * 4 + g];
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W2f[(u * 4 + s) * 64 + lane], hb[s], acc, 0, 0, 0);
-    const f32x4 w3v = w3f[u * 4 + g];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) z = fmaf(__builtin_amdgcn_fmed3f(acc[q], 0.f, 3.4e38f), w3v[q], z);   // relu: 1 VALU
+    acc2[u] = acc;
   }
-  z += __shfl_xor(z, 16);
-  z += __shfl_xor(z, 32);
-  return __builtin_amdgcn_rcpf(1.f + __expf(-(z + L.b3)));
+  const bf16x8* W3f = reinterpret_cast<const bf16x8*>(sblob + kOffW3F);
+  f32x4 acc3 = zero;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint4 u4 = make_uint4(relu_pack_bf16x2(acc2[2 * s][0], acc2[2 * s][1]),
+                                relu_pack_bf16x2(acc2[2 * s][2], acc2[2 * s][3]),
+                                relu_pack_bf16x2(acc2[2 * s + 1][0], acc2[2 * s + 1][1]),
+                                relu_pack_bf16x2(acc2[2 * s + 1][2], acc2[2 * s + 1][3]));
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(W3f[s * 64 + lane], __builtin_bit_cast(bf16x8, u4), acc3, 0, 0, 0);
+  }
+  (void)w3f;
+  return __builtin_amdgcn_rcpf(1.f + __expf(-(acc3[0] + L.b3)));
 }
 
 // wire_body.h scorer for the MLP
 struct MlpWireScorer {
-  static constexpr int kLds = kMlpBlob;
+  static constexpr int kLds = kMlpBlobWire;
   MlpWireLane L;
   __device__ __forceinline__ void stage(const ccfd_score_args& a, char* lds, int tid, int nthreads) {
-    mlp_stage(a.blob, lds, tid, nthreads);
+    mlp_stage(a.blob, lds, tid, nthreads, kMlpBlobWire);
   }
   __device__ __forceinline__ void lanes(const char* lds, const ccfd_score_args&, int) { L = mlp_wire_lane(lds); }
   __device__ __forceinline__ float tile(const char* lds, const WireRegs& r, int g, int lane) const {

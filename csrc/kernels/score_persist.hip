@@ -28,7 +28,7 @@ namespace {
 
 template <int kModel>
 __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
-  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlob];
+  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlobWire];
   __shared__ __attribute__((aligned(16))) float sx[4][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
   __shared__ ccfd_persist_desc sdesc;
@@ -40,7 +40,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   const int g = lane >> 4, c = lane & 15;
   const int C = a.items_per_batch;
 
-  if (kModel == CCFD_MODEL_MLP) mlp_stage(a.blob, sblob, tid, 256);
+  if (kModel == CCFD_MODEL_MLP)
+    mlp_stage(a.blob, sblob, tid, 256, (a.flags & CCFD_ARG_WIRE_W64) ? kMlpBlobWire : kMlpBlob);
   else for (int i = tid; i < 448 / 16; i += 256) reinterpret_cast<int4*>(sblob)[i] = reinterpret_cast<const int4*>(a.blob)[i];
   epi_init(epi);
   __syncthreads();
