@@ -209,6 +209,60 @@ __device__ __forceinline__ float mlp_tile_w64(const char* sblob, const MlpWireLa
   return __builtin_amdgcn_rcpf(1.f + __expf(-(acc3[0] + L.b3)));
 }
 
+// Two independent tiles per call: every weight fragment read from LDS feeds two MFMAs (half
+// the LDS traffic per row) and the two dependency chains interleave (ILP 2 per wave).
+__device__ __forceinline__ void mlp_tile_w64_x2(const char* sblob, const MlpWireLane& L, const WireRegs& r0,
+                                                const WireRegs& r1, int g, int lane, float& p0, float& p1) {
+  const bf16x8 xa = wire_operand(r0, g == 3, L);
+  const bf16x8 xb = wire_operand(r1, g == 3, L);
+  const bf16x8* W1f = reinterpret_cast<const bf16x8*>(sblob + kOffW1);
+  const bf16x8* W2f = reinterpret_cast<const bf16x8*>(sblob + kOffW2);
+  const f32x4* b2f = reinterpret_cast<const f32x4*>(sblob + kOffB2);
+  const bf16x8* W3f = reinterpret_cast<const bf16x8*>(sblob + kOffW3F);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  bf16x8 ha[4], hb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const bf16x8 w0 = W1f[(2 * s) * 64 + lane], w1 = W1f[(2 * s + 1) * 64 + lane];
+    const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, xa, zero, 0, 0, 0);
+    const f32x4 b0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, xb, zero, 0, 0, 0);
+    const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, xa, zero, 0, 0, 0);
+    const f32x4 b1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, xb, zero, 0, 0, 0);
+    ha[s] = __builtin_bit_cast(bf16x8, make_uint4(relu_pack_bf16x2(a0[0], a0[1]), relu_pack_bf16x2(a0[2], a0[3]),
+                                                  relu_pack_bf16x2(a1[0], a1[1]), relu_pack_bf16x2(a1[2], a1[3])));
+    hb[s] = __builtin_bit_cast(bf16x8, make_uint4(relu_pack_bf16x2(b0[0], b0[1]), relu_pack_bf16x2(b0[2], b0[3]),
+                                                  relu_pack_bf16x2(b1[0], b1[1]), relu_pack_bf16x2(b1[2], b1[3])));
+  }
+  f32x4 a2[4], b2[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f32x4 aa = b2f[u * 4 + g], bb = aa;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 w = W2f[(u * 4 + s) * 64 + lane];
+      aa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, ha[s], aa, 0, 0, 0);
+      bb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[s], bb, 0, 0, 0);
+    }
+    a2[u] = aa;
+    b2[u] = bb;
+  }
+  f32x4 za = zero, zb = zero;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 w = W3f[s * 64 + lane];
+    const uint4 ua = make_uint4(relu_pack_bf16x2(a2[2 * s][0], a2[2 * s][1]), relu_pack_bf16x2(a2[2 * s][2], a2[2 * s][3]),
+                                relu_pack_bf16x2(a2[2 * s + 1][0], a2[2 * s + 1][1]),
+                                relu_pack_bf16x2(a2[2 * s + 1][2], a2[2 * s + 1][3]));
+    const uint4 ub = make_uint4(relu_pack_bf16x2(b2[2 * s][0], b2[2 * s][1]), relu_pack_bf16x2(b2[2 * s][2], b2[2 * s][3]),
+                                relu_pack_bf16x2(b2[2 * s + 1][0], b2[2 * s + 1][1]),
+                                relu_pack_bf16x2(b2[2 * s + 1][2], b2[2 * s + 1][3]));
+    za = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, __builtin_bit_cast(bf16x8, ua), za, 0, 0, 0);
+    zb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, __builtin_bit_cast(bf16x8, ub), zb, 0, 0, 0);
+  }
+  p0 = __builtin_amdgcn_rcpf(1.f + __expf(-(za[0] + L.b3)));
+  p1 = __builtin_amdgcn_rcpf(1.f + __expf(-(zb[0] + L.b3)));
+}
+
 // wire_body.h scorer for the MLP
 struct MlpWireScorer {
   static constexpr int kLds = kMlpBlobWire;
@@ -219,6 +273,11 @@ struct MlpWireScorer {
   __device__ __forceinline__ void lanes(const char* lds, const ccfd_score_args&, int) { L = mlp_wire_lane(lds); }
   __device__ __forceinline__ float tile(const char* lds, const WireRegs& r, int g, int lane) const {
     return mlp_tile_w64(lds, L, r, g, lane);
+  }
+  static constexpr bool kPair = true;
+  __device__ __forceinline__ void tile2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
+                                        float& p0, float& p1) const {
+    mlp_tile_w64_x2(lds, L, r0, r1, g, lane, p0, p1);
   }
 };
 

@@ -162,6 +162,12 @@ struct LrWireScorer {
     z += __shfl_xor(z, 32);
     return __builtin_amdgcn_rcpf(1.f + __expf(-(z + b)));
   }
+  static constexpr bool kPair = false;
+  __device__ __forceinline__ void tile2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
+                                        float& p0, float& p1) const {
+    p0 = tile(lds, r0, g, lane);
+    p1 = tile(lds, r1, g, lane);
+  }
 };
 
 template <int kLrWaves, int kPf>

@@ -162,12 +162,13 @@ void score_mlp_wire_multi_kernel(ccfd_multi_args m) {
   wire_stream_body<MlpWireScorer, kWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
-// CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4; default 4).
+// CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4; default 2 = one tile pair, measured
+// best with the paired scorer: 32.0 vs 31.0 G rows/s at 4, profiles/r1/kernel_sol_mlp_pair_sweep.jsonl).
 static int mlp_wire_prefetch() {
   static const int v = [] {
     const char* e = std::getenv("CCFD_MLP_PF");
-    const int x = e ? std::atoi(e) : 4;
-    return (x == 1 || x == 2 || x == 4) ? x : 4;
+    const int x = e ? std::atoi(e) : 2;
+    return (x == 1 || x == 2 || x == 4) ? x : 2;
   }();
   return v;
 }
@@ -176,8 +177,8 @@ template <int kW>
 static void launch_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
   switch (mlp_wire_prefetch()) {
     case 1: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 1>), grid, dim3(64 * kW), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
-    default: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
+    default: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
   }
 }
 
@@ -245,8 +246,8 @@ int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
   if (m.base.flags & CCFD_ARG_WIRE_W64) {
     switch (mlp_wire_prefetch()) {
       case 1: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 1>), grid, block, 0, s, m); break;
-      case 2: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 2>), grid, block, 0, s, m); break;
-      default: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 4>), grid, block, 0, s, m); break;
+      default: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 2>), grid, block, 0, s, m); break;
+      case 4: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 4>), grid, block, 0, s, m); break;
     }
   } else {
     if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<5, kW>), grid, block, 0, s, m);

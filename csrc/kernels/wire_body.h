@@ -72,13 +72,27 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
   // steady state: the kPf strided tiles of a round all exist
   const int full_end = ntiles - (kPf - 1) * tstride;
   while (tile < full_end) {
+    if constexpr (Scorer::kPair && kPf % 2 == 0) {
 #pragma unroll
-    for (int k = 0; k < kPf; ++k) {
-      const float amount = __uint_as_float(ring[k].v.w);
-      const float p = sc.tile(lds, ring[k], g, lane);
-      issue(tile + kPf * tstride, ring[k]);
-      finish(p, amount, tile);
-      tile += tstride;
+      for (int k = 0; k < kPf; k += 2) {             // two tiles per scorer call (shared weight reads)
+        const float am0 = __uint_as_float(ring[k].v.w), am1 = __uint_as_float(ring[k + 1].v.w);
+        float p0, p1;
+        sc.tile2(lds, ring[k], ring[k + 1], g, lane, p0, p1);
+        issue(tile + kPf * tstride, ring[k]);
+        issue(tile + (kPf + 1) * tstride, ring[k + 1]);
+        finish(p0, am0, tile);
+        finish(p1, am1, tile + tstride);
+        tile += 2 * tstride;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPf; ++k) {
+        const float amount = __uint_as_float(ring[k].v.w);
+        const float p = sc.tile(lds, ring[k], g, lane);
+        issue(tile + kPf * tstride, ring[k]);
+        finish(p, amount, tile);
+        tile += tstride;
+      }
     }
   }
   // tail: fewer than kPf tiles left, already in flight in ring[0..]
