@@ -140,3 +140,33 @@ def test_trainer_exports_training_metrics():
     train_logistic(X, y, TrainConfig(epochs=1, batch=1000, device="cpu", metrics=tm))
     text = tm.expose().decode()
     assert 'ccfd_train_steps_total{model="lr"} 5.0' in text and "ccfd_train_workers 1.0" in text
+
+
+def test_deploy_manifests_use_real_services_and_reference_names():
+    """deploy/k8s/*.yaml: every container runs a launcher service that exists, and the
+    reference's service names / ports (deploy/model/modelfull.json, deploy/ccd-service.yaml,
+    deploy/router.yaml) are kept."""
+    import glob
+    import re
+
+    import yaml
+
+    from ccfd_demo_summit_amd.launch.__main__ import parse_args
+    services = {}
+    for f in glob.glob("deploy/k8s/*.yaml"):
+        for d in yaml.safe_load_all(open(f)):
+            if not d:
+                continue
+            if d["kind"] == "Service":
+                services[d["metadata"]["name"]] = [p["port"] for p in d["spec"]["ports"]]
+            spec = d.get("spec", {}).get("template", {}).get("spec", {})
+            for c in spec.get("containers", []):
+                cmd = " ".join(c.get("command", []))
+                for svc in re.findall(r"ccfd_demo_summit_amd\.launch (\S+)", cmd):
+                    if svc in ("supervise", "--"):
+                        continue
+                    parse_args([svc])                      # exits on an unknown service
+    assert services["modelfull-modelfull"] == [8000]
+    assert services["ccd-service"] == [8090]
+    assert services["ccd-fuse"] == [8091]
+    assert services["ccfd-seldon-model"] == [5000]
