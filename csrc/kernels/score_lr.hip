@@ -14,11 +14,11 @@ constexpr int kLrBlob = 64 + 3 * 32 * 4;   // models/lr.py BLOB_BYTES
 int mlp_waves_for(int ntiles);     // score_mlp.hip (same policy and CCFD_MLP_WAVES override)
 int mlp_tiles_per_wave_policy();   // score_mlp.hip (CCFD_MLP_TPW)
 
-// kMode as in score_mlp.hip: 0 strided f32, 1 contiguous f32, 2 W64 wire rows
+// f32 rows, kMode as in score_mlp.hip: 0 strided, 1 contiguous (W64 rows: LrWireScorer below)
 template <int kMode, int kLrWaves>
 __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int nblk) {
   constexpr bool kContig = kMode == 1;
-  constexpr bool kWire = kMode == 2;
+  static_assert(kMode != 2, "W64 rows use wire_stream_body");
   __shared__ __attribute__((aligned(16))) float sx[kContig ? kLrWaves : 1][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
   const int tid = threadIdx.x;
@@ -30,14 +30,9 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
   int tile = blk * kLrWaves + wave;
 
   TileRegs pre;
-  WireRegs wpre;
-  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x);
   auto tile_avail = [&](int t) { return min(kTileRows, a.n - t * kTileRows) * kF * 4; };
   if constexpr (kContig) {
     if (tile < ntiles) tile_issue(a.x + (size_t)tile * kTileRows * kF, tile_avail(tile), lane, pre);
-  }
-  if constexpr (kWire) {
-    if (tile < ntiles) wire_issue(xw, a.n, tile, c, g, wpre);
   }
   epi_init(epi);
 
@@ -67,10 +62,6 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       tile_features(tile_lds, c, g, xv);
-    } else if constexpr (kWire) {
-      const WireRegs cur = wpre;
-      if (nxt < ntiles) wire_issue(xw, a.n, nxt, c, g, wpre);
-      wire_features(cur, g, xv);
     } else {
       const float* xr = a.x + (size_t)row * a.ld + 8 * g;
 #pragma unroll
@@ -91,11 +82,11 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
     if (valid && g == 0) {
       if (a.proba) a.proba[row] = p;
       if (a.route) a.route[row] = fr ? 1 : 0;
-      psum += (unsigned long long)(p * 1e6f + 0.5f);
+      psum += (unsigned)(p * 1e6f + 0.5f);
     }
     fraud += __popcll(__ballot(fr && g == 0));
     rows += __popcll(__ballot(valid && g == 0));
-    if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
+    if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(amount)], 1u);
     emit_flagged(a, fr && g == 0, row);
   }
   psum = wave_sum_u64(psum);

@@ -28,19 +28,19 @@ namespace ccfd {
 // micro-batch is 256 tiles, so 4-wave workgroups occupy 64 CUs per launch; several launches
 // run concurrently on separate streams.  Smaller workgroups spread one launch wider but pay
 // the weight staging and completion ticket more often (profiles/r1/waves_sweep.txt).
-// kMode: 0 = strided f32 rows, 1 = contiguous f32 rows [n][30] (LDS-staged tiles),
-//        2 = W64 wire rows (one 16-B register load per lane, no LDS tile).
-// Body shared by the plain and the coalesced launch: workgroup `blk` of the `nblk` that
-// score micro-batch `a`.  Entry points ask for >= 4 waves per SIMD (<= 128 VGPRs): a wave
-// usually scores a single tile, so occupancy (outstanding zero-copy loads) beats hoisting
-// the 24 weight fragments into registers, which the W64 path otherwise does (272 VGPRs).
+// f32 rows (kMode: 0 = strided [n][ld], 1 = contiguous [n][30] through LDS-staged tiles;
+// +4 = weights read from global instead of an LDS copy).  W64 wire rows take the separate
+// wire_stream_body (wire_body.h, MlpWireScorer).  Body shared by the plain and the
+// coalesced launch: workgroup `blk` of the `nblk` that score micro-batch `a`.  Entry points
+// ask for >= 4 waves per SIMD (<= 128 VGPRs): occupancy (outstanding zero-copy loads) beats
+// hoisting the 24 weight fragments into registers.
 template <int kMode, int kWaves>
 __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int nblk) {
   constexpr bool kContig = (kMode & 3) == 1;
-  constexpr bool kWire = (kMode & 3) == 2;
   constexpr bool kGW = (kMode & 4) != 0;     // weights read from global (L1/L2), no LDS copy
+  static_assert((kMode & 3) != 2, "W64 rows use wire_stream_body");
   __shared__ __attribute__((aligned(16))) char sblob[kGW ? 16 : kMlpBlob];
-  __shared__ __attribute__((aligned(16))) float sx[kWire ? 1 : kWaves][kTileRows * kF + 4];
+  __shared__ __attribute__((aligned(16))) float sx[kWaves][kTileRows * kF + 4];
   __shared__ EpilogueLds epi;
 
   const int tid = threadIdx.x;
@@ -54,14 +54,9 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
   // Issue this wave's first input tile BEFORE staging the weights: the (possibly PCIe)
   // fetch latency of x overlaps the L2 fetch of the model blob.
   TileRegs pre;
-  WireRegs wpre;
-  const unsigned char* xw = reinterpret_cast<const unsigned char*>(a.x);
   auto tile_avail = [&](int t) { return min(kTileRows, a.n - t * kTileRows) * kF * 4; };
   if constexpr (kContig) {
     if (tile < ntiles) tile_issue(a.x + (size_t)tile * kTileRows * kF, tile_avail(tile), lane, pre);
-  }
-  if constexpr (kWire) {
-    if (tile < ntiles) wire_issue(xw, a.n, tile, c, g, wpre);
   }
   if constexpr (!kGW) mlp_stage(a.blob, sblob, tid, 64 * kWaves);
   const char* W = kGW ? reinterpret_cast<const char*>(a.blob) : sblob;
@@ -72,7 +67,7 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
   const float thr = a.threshold;
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
-  float* tile_lds = sx[kWire ? 0 : wave];
+  float* tile_lds = sx[wave];
 
   for (; tile < ntiles; tile += tstride) {
     const int row = tile * kTileRows + c;
@@ -87,16 +82,10 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       tile_features(tile_lds, c, g, xv);
-    } else if constexpr (kWire) {
+    } else {
       // compiler barrier: keep the weight fragments as per-tile LDS reads (not hoisted into
       // ~100 loop-invariant VGPRs, which would spill under the 128-VGPR occupancy cap)
       asm volatile("" ::: "memory");
-      const WireRegs cur = wpre;
-      const int nxt = tile + tstride;
-      if (nxt < ntiles) wire_issue(xw, a.n, nxt, c, g, wpre);
-      wire_features(cur, g, xv);
-    } else {
-      asm volatile("" ::: "memory");   // as above: no hoisted weight fragments
       const float* xr = a.x + (size_t)row * a.ld + 8 * g;
 #pragma unroll
       for (int j = 0; j < 8; ++j) xv[j] = (valid && (8 * g + j) < kF) ? xr[j] : 0.f;
@@ -110,11 +99,11 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
         if (a.proba) a.proba[row] = p;
         if (a.route) a.route[row] = fr ? 1 : 0;
       }
-      psum += (unsigned long long)(p * 1e6f + 0.5f);
+      psum += (unsigned)(p * 1e6f + 0.5f);              // p in [0,1]: u32 convert, u64 sum
     }
     fraud += __popcll(__ballot(fr && g == 0));
     rows += __popcll(__ballot(valid && g == 0));
-    if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
+    if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(amount)], 1u);
     emit_flagged(a, fr && g == 0, row);
   }
   psum = wave_sum_u64(psum);
