@@ -100,6 +100,13 @@ def cmd_seldon(a, cfg):
     from ..serving.seldon_server import SeldonServer, run
     model = _model(cfg.engine.model, a.weights, cfg.seed)
     scorer = make_scorer(model, cfg.router.fraud_threshold, device=a.device, max_batch=cfg.seldon.max_batch)
+    if a.native:
+        # C++ epoll front end (csrc/engine/seldon_http.cpp): same routes, JSON and metrics
+        from ..serving.native_seldon import NativeSeldonServer
+        srv = NativeSeldonServer(scorer, a.host, a.port or cfg.seldon.port, cfg.seldon.model_name, cfg.seldon.token)
+        print(f"[seldon] native {cfg.seldon.model_name} on {getattr(scorer, 'device', 'cpu')} :{srv.port}", flush=True)
+        while True:
+            time.sleep(3600)
     srv = SeldonServer(scorer, cfg.seldon.model_name, cfg.seldon.token, cfg.seldon.max_batch,
                        cfg.seldon.max_delay_us)
     if a.grpc_port:
@@ -389,6 +396,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--watch-model", default=None, help="engine: hot-swap weights when this file changes")
     ap.add_argument("--grpc-port", type=int, default=0, help="seldon: also serve seldon.protos gRPC Predict")
+    ap.add_argument("--native", action="store_true", help="seldon: C++ epoll REST front end (dynamic GPU batching)")
     ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--journal", default=None, help="KIE: append-only process journal for recovery")

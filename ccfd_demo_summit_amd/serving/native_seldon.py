@@ -1,0 +1,154 @@
+"""Native Seldon predict() REST front end (csrc/engine/seldon_http.cpp) -- the
+``modelfull-modelfull:8000`` endpoint of the reference (deploy/model/modelfull.json:37-44,
+deploy/router.yaml:65-68) served by a C++ epoll loop that batches every request that
+arrived during the previous GPU call into one fused-kernel launch.
+
+Same routes and JSON as the aiohttp server (serving/seldon_server.py): POST
+``/api/v0.1/predictions``, ``/api/v1.0/predictions``, ``/predict``; GET ``/prometheus``
+(reference metric names: Seldon engine histograms and the proba_1 / Amount / V17 / V10
+gauges, rendered here from the native counters); health routes.  Scoring is a
+``StreamEngine`` over f32 rows (GPU) or any object with ``score(X) -> (proba, route)``
+(CPU, through a ctypes callback -- tests and CPU-only hosts).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+from typing import Optional
+
+import numpy as np
+
+from ..contracts import metric_names as M
+from ..metrics.exporter import LATENCY_BUCKETS
+from ..ops._lib import lib
+
+_SCORE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_float), C.c_void_p)
+_RENDER_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_void_p)
+_NB = 32                                   # native latency buckets (+Inf)
+_STATUS = ("200", "400", "401")
+
+
+def _bind():
+    L = lib()
+    if getattr(L, "_seldon_bound", False):
+        return L
+    L.ccfd_seldon_http_start.restype = C.c_void_p
+    L.ccfd_seldon_http_start.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_double), C.c_int]
+    L.ccfd_seldon_http_port.argtypes = [C.c_void_p]
+    L.ccfd_seldon_http_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.ccfd_seldon_http_stop.argtypes = [C.c_void_p]
+    L.ccfd_http_load.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_double,
+                                 C.POINTER(C.c_double)]
+    L._seldon_bound = True
+    return L
+
+
+class NativeSeldonServer:
+    def __init__(self, scorer, host: str = "0.0.0.0", port: int = 8000, model_name: str = "modelfull",
+                 token: Optional[str] = None, max_batch: int = 65536,
+                 deployment: str = "modelfull", model_image: str = "ccfd-mi355x"):
+        L = _bind()
+        self.model_name = model_name
+        self.labels = dict(deployment_name=deployment, predictor_name=model_name, predictor_version="1",
+                           model_name=model_name, model_image=model_image, model_version="1")
+        engine = None
+        self._score_cb = None
+        eng = getattr(scorer, "engine", scorer)           # GpuScorer -> its StreamEngine
+        if hasattr(eng, "h") and not getattr(eng, "wire", False):
+            engine = C.c_void_p(eng.h)                     # StreamEngine over f32 rows: C++ calls it directly
+        else:
+            def _score(rows, n, proba, _ctx):
+                try:
+                    X = np.ctypeslib.as_array(rows, shape=(n, 30))
+                    p, _r = scorer.score(X)
+                    np.ctypeslib.as_array(proba, shape=(n,))[:] = p
+                    return 0
+                except Exception:                           # scoring failure -> HTTP 500
+                    return -1
+            self._score_cb = _SCORE_FN(_score)
+        self._render_cb = _RENDER_FN(self._render)
+        b = (C.c_double * len(LATENCY_BUCKETS))(*LATENCY_BUCKETS)
+        self.h = L.ccfd_seldon_http_start(host.encode(), int(port), engine,
+                                          C.cast(self._score_cb, C.c_void_p) if self._score_cb else None, None,
+                                          C.cast(self._render_cb, C.c_void_p), None, model_name.encode(),
+                                          (token or "").encode(), int(max_batch), b, len(LATENCY_BUCKETS))
+        if not self.h:
+            raise OSError(f"native Seldon server could not bind {host}:{port}")
+        self.port = L.ccfd_seldon_http_port(self.h)
+        self.scorer = scorer
+
+    # ------------------------------------------------------------------ stats / metrics
+    def stats(self) -> dict:
+        out = (C.c_uint64 * (3 + 3 + 3 + 4 + 3 * (_NB + 1)))()
+        _bind().ccfd_seldon_http_stats(self.h, out)
+        v = list(out)
+        last = [struct.unpack("<f", struct.pack("<I", int(x) & 0xFFFFFFFF))[0] for x in v[9:13]]
+        hist = [v[13 + i * (_NB + 1): 13 + (i + 1) * (_NB + 1)] for i in range(3)]
+        return {"count": dict(zip(_STATUS, v[0:3])), "sum_s": dict(zip(_STATUS, [x * 1e-9 for x in v[3:6]])),
+                "rows": v[6], "batches": v[7], "model_s": v[8] * 1e-9,
+                "last": dict(zip(M.MODEL_GAUGES, last)), "hist": dict(zip(_STATUS, hist))}
+
+    def expose(self) -> bytes:
+        """Prometheus text with the reference names (same series as serving/seldon_server.py;
+        the native path has one latency per request, used for the server and client series)."""
+        from prometheus_client import CollectorRegistry, generate_latest
+        from prometheus_client.core import GaugeMetricFamily, HistogramMetricFamily
+        st = self.stats()
+        nb = len(LATENCY_BUCKETS)
+
+        class _Coll:
+            def collect(self_):
+                srv = HistogramMetricFamily(M.SELDON_SERVER_REQUESTS, "Seldon engine server request latency",
+                                            labels=["status"])
+                cli = HistogramMetricFamily(M.SELDON_CLIENT_REQUESTS, "Seldon engine -> model request latency",
+                                            labels=list(M.SELDON_CLIENT_LABELS))
+                for s in _STATUS:
+                    h = st["hist"][s]
+                    cum, buckets = 0, []
+                    for i, bound in enumerate(LATENCY_BUCKETS):
+                        cum += h[i]
+                        buckets.append((str(bound), cum))
+                    buckets.append(("+Inf", cum + sum(h[nb:])))
+                    srv.add_metric([s], buckets, st["sum_s"][s])
+                    cli.add_metric([s] + [self.labels[k] for k in M.SELDON_CLIENT_LABELS[1:]], buckets, st["sum_s"][s])
+                yield srv
+                yield cli
+                for name, val in st["last"].items():
+                    g = GaugeMetricFamily(name, f"last request {name}")
+                    g.add_metric([], val)
+                    yield g
+        reg = CollectorRegistry()
+        reg.register(_Coll())
+        return generate_latest(reg)
+
+    def _render(self, buf, cap, _ctx) -> int:
+        try:
+            body = self.expose()
+        except Exception:
+            return 0
+        n = min(len(body), int(cap))
+        C.memmove(buf, body, n)
+        return n
+
+    def stop(self) -> None:
+        if self.h:
+            _bind().ccfd_seldon_http_stop(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass
+
+
+def http_load(host: str, port: int, body: bytes, conns: int = 64, seconds: float = 5.0,
+              path: str = "/api/v0.1/predictions") -> dict:
+    """Native keep-alive load generator (csrc/engine/http_load.cpp)."""
+    out = (C.c_double * 5)()
+    rc = _bind().ccfd_http_load(host.encode(), int(port), path.encode(), body, len(body), int(conns),
+                                float(seconds), out)
+    if rc != 0:
+        raise OSError("load generator could not connect")
+    return {"req_per_s": out[0], "p50_us": out[1], "p99_us": out[2], "errors": int(out[3]), "requests": int(out[4])}

@@ -1,0 +1,96 @@
+"""Native Seldon REST front end (csrc/engine/seldon_http.cpp): the reference's predict()
+contract (ndarray / tensor / named columns, Seldon error JSON, token auth), keep-alive,
+dynamic batching, /prometheus with the reference metric names, and the native load
+generator.  CPU: scoring goes through the ctypes scorer callback."""
+import http.client
+import json
+
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.contracts import seldon
+from ccfd_demo_summit_amd.contracts.transaction import FEATURE_NAMES
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.models import build_model
+from ccfd_demo_summit_amd.serving import CpuScorer
+from ccfd_demo_summit_amd.serving.native_seldon import NativeSeldonServer, http_load
+
+
+@pytest.fixture(scope="module")
+def srv():
+    X, _ = generate(5000, seed=3)
+    m = build_model("lr", seed=1, X_ref=X, calibrate_rate=0.05)
+    s = NativeSeldonServer(CpuScorer(m), host="127.0.0.1", port=0)
+    yield s, m, X
+    s.stop()
+
+
+def _post(port, body, path="/api/v0.1/predictions", headers=None, conn=None):
+    c = conn or http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    c.request("POST", path, body=json.dumps(body) if not isinstance(body, (bytes, str)) else body,
+              headers={"Content-Type": "application/json", **(headers or {})})
+    r = c.getresponse()
+    out = r.status, json.loads(r.read())
+    if conn is None:
+        c.close()
+    return out
+
+
+def test_predict_ndarray_tensor_and_named_columns(srv):
+    s, m, X = srv
+    ref = m.predict_proba(X[:5])
+    st, body = _post(s.port, seldon.build_request(X[:5]))
+    assert st == 200 and body["data"]["names"] == ["proba_0", "proba_1"]
+    np.testing.assert_allclose(seldon.proba1_from_response(body), ref, rtol=1e-6, atol=1e-7)
+    assert "puid" in body["meta"] and body["meta"]["requestPath"] == {"modelfull": "modelfull"}
+    st, body = _post(s.port, seldon.build_request(X[:3], tensor=True), path="/predict")
+    assert st == 200 and body["data"]["tensor"]["shape"] == [3, 2]
+    np.testing.assert_allclose(seldon.proba1_from_response(body), ref[:3], rtol=1e-6, atol=1e-7)
+    # columns sent in another order are re-ordered by name
+    perm = np.random.default_rng(0).permutation(30)
+    req = {"data": {"names": [FEATURE_NAMES[i] for i in perm], "ndarray": X[:4, perm].tolist()}}
+    st, body = _post(s.port, req)
+    np.testing.assert_allclose(seldon.proba1_from_response(body), ref[:4], rtol=1e-6, atol=1e-7)
+    # a flat single row
+    st, body = _post(s.port, {"data": {"ndarray": X[0].tolist()}})
+    assert st == 200 and len(body["data"]["ndarray"]) == 1
+
+
+def test_errors_keepalive_metrics_and_health(srv):
+    s, m, X = srv
+    st, body = _post(s.port, b"{not json")
+    assert st == 400 and body["status"]["status"] == "FAILURE"
+    st, body = _post(s.port, {"data": {"ndarray": [[1.0, 2.0]]}})
+    assert st == 400 and "30 features" in body["status"]["info"]
+    c = http.client.HTTPConnection("127.0.0.1", s.port, timeout=10)
+    for i in range(5):                              # one keep-alive connection
+        st, body = _post(s.port, seldon.build_request(X[i:i + 1]), conn=c)
+        assert st == 200
+    c.request("GET", "/prometheus")
+    text = c.getresponse().read().decode()
+    c.request("GET", "/health/ping")
+    assert json.loads(c.getresponse().read())["server"] == "native"
+    c.close()
+    assert 'seldon_api_engine_server_requests_seconds_count{status="200"}' in text
+    assert 'seldon_api_engine_client_requests_seconds_bucket{' in text
+    assert "proba_1 " in text and "Amount " in text
+    st_ = s.stats()
+    assert st_["count"]["400"] >= 2 and st_["count"]["200"] >= 9 and st_["rows"] >= 18
+
+
+def test_token_and_native_load_generator():
+    X, _ = generate(2000, seed=4)
+    m = build_model("lr", seed=2, X_ref=X)
+    s = NativeSeldonServer(CpuScorer(m), host="127.0.0.1", port=0, token="s3cret")
+    try:
+        assert _post(s.port, seldon.build_request(X[:1]))[0] == 401
+        assert _post(s.port, seldon.build_request(X[:1]), headers={"Authorization": "Bearer s3cret"})[0] == 200
+    finally:
+        s.stop()
+    s = NativeSeldonServer(CpuScorer(m), host="127.0.0.1", port=0)
+    try:
+        r = http_load("127.0.0.1", s.port, json.dumps(seldon.build_request(X[:1])).encode(), conns=8, seconds=0.5)
+        assert r["requests"] > 50 and r["errors"] == 0
+        assert s.stats()["batches"] < s.stats()["rows"]          # concurrent requests were batched
+    finally:
+        s.stop()
