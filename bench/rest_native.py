@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--conns", default="1,16,64,256")
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--rows-per-request", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=1, help="server epoll threads (one GPU engine each)")
+    ap.add_argument("--client-threads", type=int, default=0, help="load generator threads (0 = 1 per 64 conns)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from ccfd_demo_summit_amd.contracts import seldon
@@ -32,15 +34,17 @@ def main():
     from ccfd_demo_summit_amd.serving.scorers import make_scorer
     X, _ = generate(100_000, seed=7)
     model = build_model(a.model, seed=0, X_ref=X, calibrate_rate=FRAUD_RATE)
-    scorer = make_scorer(model, 0.5, device=a.device, max_batch=4096)
-    srv = NativeSeldonServer(scorer, "127.0.0.1", 0)
+    scorers = [make_scorer(model, 0.5, device=a.device, max_batch=4096) for _ in range(a.workers)]
+    scorer = scorers[0]
+    srv = NativeSeldonServer(scorers if a.workers > 1 else scorer, "127.0.0.1", 0, workers=a.workers)
     body = json.dumps(seldon.build_request(X[:a.rows_per_request])).encode()
     res = {"metric": "Seldon REST predict() through the native front end", "model": a.model,
-           "scorer": getattr(scorer, "device", "cpu"), "rows_per_request": a.rows_per_request, "runs": []}
+           "scorer": getattr(scorer, "device", "cpu"), "rows_per_request": a.rows_per_request,
+           "server_workers": a.workers, "runs": []}
     http_load("127.0.0.1", srv.port, body, conns=8, seconds=0.5)          # warm-up
     for c in [int(x) for x in a.conns.split(",")]:
         b0 = srv.stats()
-        r = http_load("127.0.0.1", srv.port, body, conns=c, seconds=a.seconds)
+        r = http_load("127.0.0.1", srv.port, body, conns=c, seconds=a.seconds, threads=a.client_threads)
         b1 = srv.stats()
         r.update(conns=c, tx_per_s=round(r["req_per_s"] * a.rows_per_request, 1),
                  mean_rows_per_gpu_call=round((b1["rows"] - b0["rows"]) / max(1, b1["batches"] - b0["batches"]), 2))

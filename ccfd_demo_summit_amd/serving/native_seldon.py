@@ -33,35 +33,46 @@ def _bind():
     if getattr(L, "_seldon_bound", False):
         return L
     L.ccfd_seldon_http_start.restype = C.c_void_p
-    L.ccfd_seldon_http_start.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                         C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_double), C.c_int]
+    L.ccfd_seldon_http_start.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p), C.c_int, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_char_p, C.c_char_p, C.c_int,
+                                         C.POINTER(C.c_double), C.c_int]
     L.ccfd_seldon_http_port.argtypes = [C.c_void_p]
     L.ccfd_seldon_http_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.ccfd_seldon_http_stop.argtypes = [C.c_void_p]
     L.ccfd_http_load.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_double,
-                                 C.POINTER(C.c_double)]
+                                 C.POINTER(C.c_double), C.c_int]
     L._seldon_bound = True
     return L
 
 
 class NativeSeldonServer:
+    """``scorer``: one scorer, or a list (one per epoll worker thread -- GPU engines are not
+    shared between threads; a CPU scorer is reused by every worker)."""
+
     def __init__(self, scorer, host: str = "0.0.0.0", port: int = 8000, model_name: str = "modelfull",
                  token: Optional[str] = None, max_batch: int = 65536,
-                 deployment: str = "modelfull", model_image: str = "ccfd-mi355x"):
+                 deployment: str = "modelfull", model_image: str = "ccfd-mi355x", workers: int = 1):
         L = _bind()
         self.model_name = model_name
         self.labels = dict(deployment_name=deployment, predictor_name=model_name, predictor_version="1",
                            model_name=model_name, model_image=model_image, model_version="1")
-        engine = None
+        scorers = list(scorer) if isinstance(scorer, (list, tuple)) else [scorer]
+        engines = [getattr(sc, "engine", sc) for sc in scorers]         # GpuScorer -> its StreamEngine
+        native = all(hasattr(e, "h") and not getattr(e, "wire", False) for e in engines)
         self._score_cb = None
-        eng = getattr(scorer, "engine", scorer)           # GpuScorer -> its StreamEngine
-        if hasattr(eng, "h") and not getattr(eng, "wire", False):
-            engine = C.c_void_p(eng.h)                     # StreamEngine over f32 rows: C++ calls it directly
+        eng_arr = None
+        if native:
+            workers = len(engines) if len(engines) > 1 else max(1, workers)
+            if len(engines) < workers:
+                raise ValueError("one GPU engine per worker thread")
+            eng_arr = (C.c_void_p * workers)(*[e.h for e in engines[:workers]])
         else:
+            first = scorers[0]
+
             def _score(rows, n, proba, _ctx):
                 try:
                     X = np.ctypeslib.as_array(rows, shape=(n, 30))
-                    p, _r = scorer.score(X)
+                    p, _r = first.score(X)
                     np.ctypeslib.as_array(proba, shape=(n,))[:] = p
                     return 0
                 except Exception:                           # scoring failure -> HTTP 500
@@ -69,7 +80,7 @@ class NativeSeldonServer:
             self._score_cb = _SCORE_FN(_score)
         self._render_cb = _RENDER_FN(self._render)
         b = (C.c_double * len(LATENCY_BUCKETS))(*LATENCY_BUCKETS)
-        self.h = L.ccfd_seldon_http_start(host.encode(), int(port), engine,
+        self.h = L.ccfd_seldon_http_start(host.encode(), int(port), eng_arr, int(max(1, workers)),
                                           C.cast(self._score_cb, C.c_void_p) if self._score_cb else None, None,
                                           C.cast(self._render_cb, C.c_void_p), None, model_name.encode(),
                                           (token or "").encode(), int(max_batch), b, len(LATENCY_BUCKETS))
@@ -77,6 +88,7 @@ class NativeSeldonServer:
             raise OSError(f"native Seldon server could not bind {host}:{port}")
         self.port = L.ccfd_seldon_http_port(self.h)
         self.scorer = scorer
+        self.workers = max(1, workers)
 
     # ------------------------------------------------------------------ stats / metrics
     def stats(self) -> dict:
@@ -144,11 +156,11 @@ class NativeSeldonServer:
 
 
 def http_load(host: str, port: int, body: bytes, conns: int = 64, seconds: float = 5.0,
-              path: str = "/api/v0.1/predictions") -> dict:
-    """Native keep-alive load generator (csrc/engine/http_load.cpp)."""
+              path: str = "/api/v0.1/predictions", threads: int = 0) -> dict:
+    """Native keep-alive load generator (csrc/engine/http_load.cpp); threads 0 = 1 per 64 conns."""
     out = (C.c_double * 5)()
     rc = _bind().ccfd_http_load(host.encode(), int(port), path.encode(), body, len(body), int(conns),
-                                float(seconds), out)
+                                float(seconds), out, int(threads))
     if rc != 0:
         raise OSError("load generator could not connect")
     return {"req_per_s": out[0], "p50_us": out[1], "p99_us": out[2], "errors": int(out[3]), "requests": int(out[4])}

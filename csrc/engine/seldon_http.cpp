@@ -274,19 +274,19 @@ struct Server {
   int max_batch = 65536;
   double bounds[kLatBuckets];
   int nbounds = 0;
-  Stats st;
+  Stats* stp = nullptr;                           // shared by the workers of one server group
   std::unordered_map<int, Conn> conns;
-  uint64_t puid = 0;
+  uint64_t puid = 0;                              // worker index in the top byte
 
   int status_idx(int code) { return code == 200 ? 0 : code == 401 ? 2 : 1; }
   void observe(int code, int64_t dt_ns) {
     const int s = status_idx(code);
-    st.count[s].fetch_add(1, std::memory_order_relaxed);
-    st.sum_ns[s].fetch_add((uint64_t)dt_ns, std::memory_order_relaxed);
+    stp->count[s].fetch_add(1, std::memory_order_relaxed);
+    stp->sum_ns[s].fetch_add((uint64_t)dt_ns, std::memory_order_relaxed);
     const double sec = dt_ns * 1e-9;
     int b = 0;
     while (b < nbounds && sec > bounds[b]) ++b;
-    st.hist[s][b].fetch_add(1, std::memory_order_relaxed);
+    stp->hist[s][b].fetch_add(1, std::memory_order_relaxed);
   }
 
   void queue(int fd, int code, const char* ctype, const std::string& body, bool close_after) {
@@ -455,8 +455,8 @@ struct Server {
       const Pending& l = pend.back();
       const float* x = rows.data() + (l.row0 + l.nrows - 1) * kF;
       const float last[4] = {proba[l.row0 + l.nrows - 1], x[kF - 1], x[17], x[10]};
-      for (int i = 0; i < 4; ++i) { uint32_t b; std::memcpy(&b, &last[i], 4); st.last_bits[i].store(b, std::memory_order_relaxed); }
-      st.model_ns.fetch_add((uint64_t)model_ns, std::memory_order_relaxed);
+      for (int i = 0; i < 4; ++i) { uint32_t b; std::memcpy(&b, &last[i], 4); stp->last_bits[i].store(b, std::memory_order_relaxed); }
+      stp->model_ns.fetch_add((uint64_t)model_ns, std::memory_order_relaxed);
     }
   }
 
@@ -517,8 +517,8 @@ struct Server {
                       : ccfd_engine_score_sync(engine, rows.data() + (size_t)b0 * kF, nb, proba.data() + b0,
                                                route.data() + b0);
         }
-        st.rows.fetch_add((uint64_t)total, std::memory_order_relaxed);
-        st.batches.fetch_add(1, std::memory_order_relaxed);
+        stp->rows.fetch_add((uint64_t)total, std::memory_order_relaxed);
+        stp->batches.fetch_add(1, std::memory_order_relaxed);
         if (rc != 0) {
           for (const Pending& p : pend) { observe(400, now_ns() - p.t0); queue(p.fd, 500, "application/json", error_json(500, "scoring failed"), true); }
         } else {
@@ -533,84 +533,108 @@ struct Server {
   }
 };
 
+struct Group {
+  std::vector<Server*> workers;
+  Stats st;
+  int port = 0;
+};
+
 }  // namespace
 
 extern "C" {
 
-// Start a server on host:port (port 0 = ephemeral).  Scoring: `engine` (a ccfd engine
-// handle scoring f32 rows) or, if non-null, `scorer(rows, n, proba, ctx)`.  `render` fills
-// the /prometheus body.  `bounds`: latency histogram upper bounds in seconds (<= 32).
-void* ccfd_seldon_http_start(const char* host, int port, void* engine, void* scorer, void* score_ctx, void* render,
-                             void* render_ctx, const char* model, const char* token, int max_batch,
+// Start a server on host:port (port 0 = ephemeral) with `n_workers` epoll threads sharing the
+// port (SO_REUSEPORT: the kernel spreads connections).  Scoring: worker i calls engine
+// `engines[i]` (a ccfd engine over f32 rows; engines are not shared between threads) or, if
+// non-null, `scorer(rows, n, proba, ctx)`.  `render` fills the /prometheus body.  `bounds`:
+// latency histogram upper bounds in seconds (<= 32).
+void* ccfd_seldon_http_start(const char* host, int port, void** engines, int n_workers, void* scorer, void* score_ctx,
+                             void* render, void* render_ctx, const char* model, const char* token, int max_batch,
                              const double* bounds, int nbounds) {
-  auto* s = new Server();
-  s->engine = engine;
-  s->scorer = reinterpret_cast<score_fn>(scorer);
-  s->score_ctx = score_ctx;
-  s->render = reinterpret_cast<render_fn>(render);
-  s->render_ctx = render_ctx;
-  s->model = model ? model : "modelfull";
-  s->token = token ? token : "";
-  s->max_batch = max_batch > 0 ? max_batch : 65536;
-  s->nbounds = std::min(std::max(nbounds, 0), kLatBuckets);
-  for (int i = 0; i < s->nbounds; ++i) s->bounds[i] = bounds[i];
+  if (n_workers < 1 || (!scorer && !engines)) return nullptr;
+  auto* g = new Group();
   for (int i = 0; i < 3; ++i) {
-    s->st.count[i] = 0; s->st.sum_ns[i] = 0;
-    for (int b = 0; b <= kLatBuckets; ++b) s->st.hist[i][b] = 0;
+    g->st.count[i] = 0; g->st.sum_ns[i] = 0;
+    for (int b = 0; b <= kLatBuckets; ++b) g->st.hist[i][b] = 0;
   }
-  s->st.rows = 0; s->st.batches = 0; s->st.model_ns = 0;
-  for (int i = 0; i < 4; ++i) s->st.last_bits[i] = 0;
-  if (!s->engine && !s->scorer) { delete s; return nullptr; }
-  s->lfd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
-  int one = 1;
-  setsockopt(s->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-  sockaddr_in a{};
-  a.sin_family = AF_INET;
-  a.sin_port = htons((uint16_t)port);
-  a.sin_addr.s_addr = (host && *host && std::strcmp(host, "0.0.0.0")) ? inet_addr(host) : INADDR_ANY;
-  if (::bind(s->lfd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0 || ::listen(s->lfd, 1024) != 0) {
-    ::close(s->lfd);
-    delete s;
-    return nullptr;
+  g->st.rows = 0; g->st.batches = 0; g->st.model_ns = 0;
+  for (int i = 0; i < 4; ++i) g->st.last_bits[i] = 0;
+  for (int w = 0; w < n_workers; ++w) {
+    auto* s = new Server();
+    s->engine = engines ? engines[w] : nullptr;
+    s->scorer = reinterpret_cast<score_fn>(scorer);
+    s->score_ctx = score_ctx;
+    s->render = reinterpret_cast<render_fn>(render);
+    s->render_ctx = render_ctx;
+    s->model = model ? model : "modelfull";
+    s->token = token ? token : "";
+    s->max_batch = max_batch > 0 ? max_batch : 65536;
+    s->nbounds = std::min(std::max(nbounds, 0), kLatBuckets);
+    for (int i = 0; i < s->nbounds; ++i) s->bounds[i] = bounds[i];
+    s->stp = &g->st;
+    s->puid = (uint64_t)w << 56;
+    s->lfd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    int one = 1;
+    setsockopt(s->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    setsockopt(s->lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)(w == 0 ? port : g->port));
+    a.sin_addr.s_addr = (host && *host && std::strcmp(host, "0.0.0.0")) ? inet_addr(host) : INADDR_ANY;
+    if ((!s->engine && !s->scorer) || ::bind(s->lfd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0 ||
+        ::listen(s->lfd, 1024) != 0) {
+      ::close(s->lfd);
+      delete s;
+      for (Server* o : g->workers) { o->stop.store(true); o->th.join(); ::close(o->efd); ::close(o->lfd); delete o; }
+      delete g;
+      return nullptr;
+    }
+    if (w == 0) {
+      socklen_t al = sizeof a;
+      getsockname(s->lfd, reinterpret_cast<sockaddr*>(&a), &al);
+      g->port = ntohs(a.sin_port);
+    }
+    s->port = g->port;
+    s->efd = epoll_create1(0);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = s->lfd;
+    epoll_ctl(s->efd, EPOLL_CTL_ADD, s->lfd, &ev);
+    s->th = std::thread([s] { s->loop(); });
+    g->workers.push_back(s);
   }
-  socklen_t al = sizeof a;
-  getsockname(s->lfd, reinterpret_cast<sockaddr*>(&a), &al);
-  s->port = ntohs(a.sin_port);
-  s->efd = epoll_create1(0);
-  epoll_event ev{};
-  ev.events = EPOLLIN;
-  ev.data.fd = s->lfd;
-  epoll_ctl(s->efd, EPOLL_CTL_ADD, s->lfd, &ev);
-  s->th = std::thread([s] { s->loop(); });
-  return s;
+  return g;
 }
 
-int ccfd_seldon_http_port(void* h) { return h ? static_cast<Server*>(h)->port : -1; }
+int ccfd_seldon_http_port(void* h) { return h ? static_cast<Group*>(h)->port : -1; }
 
 // stats: [count x3, sum_ns x3, rows, batches, model_ns, last_bits x4, hist 3 x (32+1)] (u64)
 int ccfd_seldon_http_stats(void* h, uint64_t* out) {
   if (!h) return -1;
-  Server* s = static_cast<Server*>(h);
+  Stats& st = static_cast<Group*>(h)->st;
   int k = 0;
-  for (int i = 0; i < 3; ++i) out[k++] = s->st.count[i].load();
-  for (int i = 0; i < 3; ++i) out[k++] = s->st.sum_ns[i].load();
-  out[k++] = s->st.rows.load();
-  out[k++] = s->st.batches.load();
-  out[k++] = s->st.model_ns.load();
-  for (int i = 0; i < 4; ++i) out[k++] = s->st.last_bits[i].load();
+  for (int i = 0; i < 3; ++i) out[k++] = st.count[i].load();
+  for (int i = 0; i < 3; ++i) out[k++] = st.sum_ns[i].load();
+  out[k++] = st.rows.load();
+  out[k++] = st.batches.load();
+  out[k++] = st.model_ns.load();
+  for (int i = 0; i < 4; ++i) out[k++] = st.last_bits[i].load();
   for (int i = 0; i < 3; ++i)
-    for (int b = 0; b <= kLatBuckets; ++b) out[k++] = s->st.hist[i][b].load();
+    for (int b = 0; b <= kLatBuckets; ++b) out[k++] = st.hist[i][b].load();
   return k;
 }
 
 void ccfd_seldon_http_stop(void* h) {
   if (!h) return;
-  Server* s = static_cast<Server*>(h);
-  s->stop.store(true);
-  if (s->th.joinable()) s->th.join();
-  ::close(s->efd);
-  ::close(s->lfd);
-  delete s;
+  Group* g = static_cast<Group*>(h);
+  for (Server* s : g->workers) s->stop.store(true);
+  for (Server* s : g->workers) {
+    if (s->th.joinable()) s->th.join();
+    ::close(s->efd);
+    ::close(s->lfd);
+    delete s;
+  }
+  delete g;
 }
 
 }  // extern "C"

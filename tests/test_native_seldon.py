@@ -94,3 +94,18 @@ def test_token_and_native_load_generator():
         assert s.stats()["batches"] < s.stats()["rows"]          # concurrent requests were batched
     finally:
         s.stop()
+
+
+def test_multi_worker_server_shares_port_and_stats():
+    X, _ = generate(2000, seed=5)
+    m = build_model("lr", seed=3, X_ref=X)
+    s = NativeSeldonServer(CpuScorer(m), host="127.0.0.1", port=0, workers=3)
+    try:
+        r = http_load("127.0.0.1", s.port, json.dumps(seldon.build_request(X[:2])).encode(), conns=12,
+                      seconds=0.5, threads=3)
+        assert r["errors"] == 0 and r["requests"] > 30
+        assert s.stats()["count"]["200"] >= r["requests"]
+        st, body = _post(s.port, seldon.build_request(X[:3]))
+        np.testing.assert_allclose(seldon.proba1_from_response(body), m.predict_proba(X[:3]), rtol=1e-6, atol=1e-7)
+    finally:
+        s.stop()
