@@ -103,7 +103,10 @@ def cmd_seldon(a, cfg):
     if a.native:
         # C++ epoll front end (csrc/engine/seldon_http.cpp): same routes, JSON and metrics
         from ..serving.native_seldon import NativeSeldonServer
-        srv = NativeSeldonServer(scorer, a.host, a.port or cfg.seldon.port, cfg.seldon.model_name, cfg.seldon.token)
+        scorers = [scorer] + [make_scorer(model, cfg.router.fraud_threshold, device=a.device,
+                                          max_batch=cfg.seldon.max_batch) for _ in range(a.workers - 1)]
+        srv = NativeSeldonServer(scorers if a.workers > 1 else scorer, a.host, a.port or cfg.seldon.port,
+                                 cfg.seldon.model_name, cfg.seldon.token, workers=a.workers)
         print(f"[seldon] native {cfg.seldon.model_name} on {getattr(scorer, 'device', 'cpu')} :{srv.port}", flush=True)
         while True:
             time.sleep(3600)
@@ -397,6 +400,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--watch-model", default=None, help="engine: hot-swap weights when this file changes")
     ap.add_argument("--grpc-port", type=int, default=0, help="seldon: also serve seldon.protos gRPC Predict")
     ap.add_argument("--native", action="store_true", help="seldon: C++ epoll REST front end (dynamic GPU batching)")
+    ap.add_argument("--workers", type=int, default=1, help="seldon --native: epoll worker threads (one engine each)")
     ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--journal", default=None, help="KIE: append-only process journal for recovery")
