@@ -44,6 +44,8 @@ namespace {
 
 constexpr int kF = CCFD_N_FEATURES;
 constexpr int kLatBuckets = 32;               // upper bounds supplied by the caller (seconds)
+constexpr size_t kMaxBody = 64u << 20;        // 413 above this (a predict body is ~1 KB per row)
+constexpr size_t kMaxHeader = 64u << 10;      // a request head longer than this closes the connection
 
 typedef int (*score_fn)(const float* rows, int32_t n, float* proba, void* ctx);
 typedef int32_t (*render_fn)(char* buf, int32_t cap, void* ctx);
@@ -294,7 +296,7 @@ struct Server {
     if (it == conns.end()) return;
     char hdr[256];
     const char* reason = code == 200 ? "OK" : code == 400 ? "Bad Request" : code == 401 ? "Unauthorized" :
-                         code == 404 ? "Not Found" : "Error";
+                         code == 404 ? "Not Found" : code == 413 ? "Payload Too Large" : "Error";
     const int n = std::snprintf(hdr, sizeof hdr, "HTTP/1.1 %d %s\r\nContent-Type: %s\r\nContent-Length: %zu\r\n%s\r\n",
                                 code, reason, ctype, body.size(), close_after ? "Connection: close\r\n" : "");
     it->second.out.append(hdr, n);
@@ -352,7 +354,10 @@ struct Server {
     size_t off = 0;
     for (;;) {
       const size_t hend = c.in.find("\r\n\r\n", off);
-      if (hend == std::string::npos) break;
+      if (hend == std::string::npos) {
+        if (c.in.size() - off > kMaxHeader) { c.closing = true; off = c.in.size(); }
+        break;
+      }
       const char* h = c.in.data() + off;
       const char* he = c.in.data() + hend;
       // request line
@@ -384,6 +389,11 @@ struct Server {
       }
       if (!authed && !query.empty() && query.find("access_token=" + token) != std::string::npos) authed = true;
       const size_t body0 = hend + 4;
+      if (clen > kMaxBody) {                                 // never buffer an unbounded body
+        queue(fd, 413, "application/json", error_json(413, "request body too large"), true);
+        off = c.in.size();
+        break;
+      }
       if (c.in.size() < body0 + clen) break;                 // body not complete yet
       const char* body = c.in.data() + body0;
       const int64_t t0 = now_ns();
@@ -604,6 +614,16 @@ void* ccfd_seldon_http_start(const char* host, int port, void** engines, int n_w
     g->workers.push_back(s);
   }
   return g;
+}
+
+// Fuzz / test entry: parse a Seldon request body; returns rows or -1.
+int64_t ccfd_seldon_parse_fuzz(const char* buf, int64_t len, float* rows_out, int64_t max_rows) {
+  std::vector<float> rows;
+  bool tensor = false;
+  std::string err;
+  const int n = parse_seldon(buf, (size_t)len, rows, &tensor, &err);
+  if (n > 0 && rows_out) std::memcpy(rows_out, rows.data(), sizeof(float) * (size_t)std::min<int64_t>(n, max_rows) * kF);
+  return n;
 }
 
 int ccfd_seldon_http_port(void* h) { return h ? static_cast<Group*>(h)->port : -1; }

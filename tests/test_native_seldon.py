@@ -109,3 +109,77 @@ def test_multi_worker_server_shares_port_and_stats():
         np.testing.assert_allclose(seldon.proba1_from_response(body), m.predict_proba(X[:3]), rtol=1e-6, atol=1e-7)
     finally:
         s.stop()
+
+
+def test_native_seldon_parser_and_server_under_asan(tmp_path):
+    """Host ASan+UBSan build: the Seldon JSON parser on mutated bodies, and the live server on
+    garbage, truncated, oversized and pipelined requests over raw sockets."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    from ccfd_demo_summit_amd.ops.build import asan_runtime, build
+    try:
+        build(sanitize="address,undefined", verbose=False)
+        rt = asan_runtime()
+    except Exception as e:
+        pytest.skip(f"sanitizer build unavailable: {e}")
+    if not rt or not os.path.exists(rt):
+        pytest.skip("clang ASan runtime not found")
+    script = tmp_path / "asan_seldon.py"
+    script.write_text(
+        "import ctypes as C, json, socket, numpy as np\n"
+        "from ccfd_demo_summit_amd.ops._lib import lib\n"
+        "from ccfd_demo_summit_amd.contracts import seldon\n"
+        "from ccfd_demo_summit_amd.data import generate\n"
+        "from ccfd_demo_summit_amd.models import build_model\n"
+        "from ccfd_demo_summit_amd.serving import CpuScorer\n"
+        "from ccfd_demo_summit_amd.serving.native_seldon import NativeSeldonServer\n"
+        "L = lib(); assert 'address' in L._name\n"
+        "L.ccfd_seldon_parse_fuzz.restype = C.c_int64\n"
+        "L.ccfd_seldon_parse_fuzz.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_int64]\n"
+        "X, _ = generate(64, seed=1)\n"
+        "good = [json.dumps(seldon.build_request(X[:3])).encode(), json.dumps(seldon.build_request(X[:2], tensor=True)).encode(),\n"
+        "        json.dumps({'data': {'ndarray': X[0].tolist()}}).encode()]\n"
+        "out = np.zeros((8, 30), np.float32)\n"
+        "assert L.ccfd_seldon_parse_fuzz(good[0], len(good[0]), out.ctypes.data, 8) == 3\n"
+        "r = np.random.default_rng(2)\n"
+        "for it in range(4000):\n"
+        "    b = bytearray(good[it % 3])\n"
+        "    for _ in range(int(r.integers(1, 6))): b[int(r.integers(0, len(b)))] = int(r.integers(0, 256))\n"
+        "    b = bytes(b[:int(r.integers(0, len(b) + 1))]) if it % 2 else bytes(b)\n"
+        "    L.ccfd_seldon_parse_fuzz(b, len(b), out.ctypes.data, 8)\n"
+        "    L.ccfd_seldon_parse_fuzz(b'[' * 200 + b'{' * 200, 400, out.ctypes.data, 8)\n"
+        "m = build_model('lr', seed=1, X_ref=X)\n"
+        "srv = NativeSeldonServer(CpuScorer(m), host='127.0.0.1', port=0, workers=2)\n"
+        "def send(raw, read=True):\n"
+        "    s = socket.create_connection(('127.0.0.1', srv.port), timeout=5)\n"
+        "    s.sendall(raw)\n"
+        "    data = b''\n"
+        "    if read:\n"
+        "        s.shutdown(socket.SHUT_WR)\n"
+        "        try:\n"
+        "            while True:\n"
+        "                d = s.recv(65536)\n"
+        "                if not d: break\n"
+        "                data += d\n"
+        "        except socket.timeout: pass\n"
+        "    s.close(); return data\n"
+        "req = lambda body: b'POST /api/v0.1/predictions HTTP/1.1\\r\\nContent-Length: %d\\r\\n\\r\\n' % len(body) + body\n"
+        "assert b'200 OK' in send(req(good[0]))\n"
+        "assert send(req(good[0]) * 5).count(b'200 OK') == 5\n"
+        "assert b'413' in send(b'POST /predict HTTP/1.1\\r\\nContent-Length: 999999999999\\r\\n\\r\\n')\n"
+        "for it in range(300):\n"
+        "    b = bytearray(req(good[it % 3]))\n"
+        "    for _ in range(int(r.integers(1, 6))): b[int(r.integers(0, len(b)))] = int(r.integers(0, 256))\n"
+        "    send(bytes(b[:int(r.integers(0, len(b) + 1))]), read=(it % 4 == 0))\n"
+        "    send(bytes(r.integers(0, 256, int(r.integers(0, 2000)), dtype=np.uint8)), read=False)\n"
+        "assert b'200 OK' in send(req(good[1]))\n"
+        "srv.stop()\n"
+        "print('asan seldon ok')\n")
+    env = dict(os.environ, CCFD_SANITIZE="address,undefined", LD_PRELOAD=rt, CCFD_NO_AUTOBUILD="1",
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               PYTHONPATH=str(Path(__file__).resolve().parents[1]), HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0 and "asan seldon ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
