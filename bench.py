@@ -153,6 +153,7 @@ def main(argv=None):
     reducer = CounterReducer(ctx, dev, priority=0)
     epochs = EpochPipeline(eng, reducer)
     flagged_total = 0
+    x2_s = [0.0]
 
     def step(drain: bool):
         nonlocal flagged_total
@@ -161,7 +162,9 @@ def main(argv=None):
         flagged_total += len(eng.drain_flagged())
         # X2/X3: flip the counter epoch; the previously closed epoch (all of whose batches
         # have completed by now) is all-reduced over RCCL on the side stream
+        tx = time.perf_counter()
         epochs.tick(progress=lambda: eng.run(0, 0))   # (retire finished batches if it must wait)
+        x2_s[0] += time.perf_counter() - tx
 
     for _ in range(args.warmup):
         step(drain=False)
@@ -172,6 +175,7 @@ def main(argv=None):
     rows0, fraud0 = int(c0[0]), int(c0[1])
     eng.drain_flagged()          # warmup hand-offs are not part of the timed run
     flagged_total = 0
+    x2_s[0] = 0.0
     barrier(ctx)
     torch.cuda.synchronize(dev)
 
@@ -244,6 +248,8 @@ def main(argv=None):
         "host_us_per_batch": {k: round(v * 1e6 / (args.steps * args.batches_per_step), 3) for k, v in
                               (("submit", st_final.host_submit_s), ("wait", st_final.host_wait_s),
                                ("complete", st_final.host_complete_s))},
+        # host time per step spent in the X2 tick (epoch flip + side-stream all-reduce issue)
+        "host_us_per_step_x2": round(x2_s[0] * 1e6 / args.steps, 2),
         "step_us_per_batch": round(elapsed * 1e6 / (args.steps * args.batches_per_step), 3),
         # K7: per-micro-batch execution window on the GPU's own clock (rank 0)
         "device_exec_us_mean": round(st_final.dev_exec_mean_us, 2),

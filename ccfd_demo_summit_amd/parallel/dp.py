@@ -42,7 +42,7 @@ class DistContext:
 
     @property
     def initialized(self) -> bool:
-        return self.world > 1 and dist.is_initialized()
+        return (self.world > 1 or self.backend != "none") and dist.is_initialized()
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> DistContext:
@@ -54,6 +54,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     # collectives over gloo while the engines stay on the GPU, and CCFD_DEVICE_MODULO=1 maps
     # local rank r to GPU r % device_count, so a multi-rank job can be exercised on a box
     # with fewer GPUs than ranks (RCCL itself refuses two ranks on one GPU).
+    # CCFD_FORCE_PG=1 builds the process group even at WORLD_SIZE=1, so a one-GPU box runs
+    # the real RCCL collectives (X1/X2/X3 kernels next to the persistent scoring kernel).
     backend = backend or os.environ.get("CCFD_DIST_BACKEND") or None
     gpu_ok = torch.cuda.is_available()
     use_gpu = gpu_ok and (backend != "gloo" or os.environ.get("CCFD_DIST_BACKEND") == "gloo")
@@ -64,9 +66,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("CCFD_FORCE_PG") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         be = backend or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device

@@ -224,3 +224,34 @@ def test_skewed_ticks_never_block_and_flush_pairs():
         assert version == 1 and swapped == [build_model("mlp", seed=5).pack()]
     # rank 0 could not run ahead by more than one collective: later ticks were deferred
     assert res[0][1][:2] == [True, True] and False in res[0][1]
+
+
+def _forced_worker(port, q):
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), CCFD_FORCE_PG="1")
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.parallel import CounterReducer, all_max, init_distributed
+    ctx = init_distributed(backend="gloo")
+    try:
+        red = CounterReducer(ctx, torch.device("cpu"))
+        c = torch.zeros(64, dtype=torch.int64)
+        c[0] = 7
+        red.submit(c, np.ones(256, np.int64))
+        red.wait()
+        g, lat = red.snapshot()
+        q.put((ctx.initialized, int(g[0]), int(lat.sum()), all_max(ctx, 1.5)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_forced_process_group_at_world_one():
+    """CCFD_FORCE_PG=1: a one-rank job still runs every collective (the one-GPU rehearsal of
+    the N>1 bench path over real RCCL)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(_free_port(), q))
+    p.start()
+    init, rows, lat, mx = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert init and rows == 7 and lat == 256 and mx == 1.5
