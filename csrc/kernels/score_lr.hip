@@ -4,6 +4,8 @@
 // two xor-shuffles.  GPU counterpart of the config-1 LR model (BASELINE.json configs[0]).
 // Launch structure mirrors score_mlp.hip: a plain and a coalesced (multi-micro-batch) entry
 // over one body, tiles-per-wave with a one-tile prefetch.
+#include <cstdlib>
+
 #include "common.h"
 #include "wire_body.h"
 
@@ -175,14 +177,40 @@ __global__ __launch_bounds__(64 * kLrWaves) void score_lr_wire_multi_kernel(ccfd
   wire_stream_body<LrWireScorer, kLrWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
+// CCFD_LR_PF: W64 tiles in flight per wave (2, 4, 8; default 4).  CCFD_LR_OCC: resident
+// waves per SIMD the wire grid is sized for (4 or 8; default 4).  The LR scorer stages no
+// LDS and needs few VGPRs, so both only trade bytes in flight against grid-stride overhead.
+static int lr_env(const char* name, int def, int a, int b, int c) {
+  const char* e = std::getenv(name);
+  const int x = e ? std::atoi(e) : def;
+  return (x == a || x == b || x == c) ? x : def;
+}
+static int lr_wire_prefetch() {
+  static const int v = lr_env("CCFD_LR_PF", 4, 2, 4, 8);
+  return v;
+}
+static int lr_wire_occupancy() {
+  static const int v = lr_env("CCFD_LR_OCC", 4, 4, 8, 4);
+  return v;
+}
+
+template <int kW>
+static void launch_lr_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
+  switch (lr_wire_prefetch()) {
+    case 2: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
+    default: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 8>), grid, dim3(64 * kW), 0, s, a); break;
+  }
+}
+
 template <int kW>
 static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   const int per_wg = kW * mlp_tiles_per_wave_policy();
   int grid = (ntiles + per_wg - 1) / per_wg;
   if (a.flags & CCFD_ARG_WIRE_W64) {
-    const int cap = 256 * 16 / kW;       // one chip residency, grid-stride beyond (score_mlp.hip)
+    const int cap = 256 * 4 * lr_wire_occupancy() / kW;   // one chip residency, grid-stride beyond
     grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
-    hipLaunchKernelGGL((score_lr_wire_kernel<kW, 4>), dim3(grid), dim3(64 * kW), 0, s, a);
+    launch_lr_wire<kW>(dim3(grid), s, a);
     return;
   }
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
