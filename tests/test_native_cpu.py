@@ -155,3 +155,31 @@ def test_host_runtime_under_asan(tmp_path):
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "asan probe ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+_EDGE_NUMBERS = ["0", "-0.0", "1", "-1.35981", "0.000123456", "123456.789", "1e5", "1E+5", "-2.5e-3",
+                 "1.5E-30", "3.4028235e38", "1e-45", "0.1", "0.30000000000000004", "123456789012345678901",
+                 "12345678.12345678", "9007199254740993", "1.7976931348623157e300", "4.9406564584124654e-324",
+                 "00012.5", "7.", "-.5e1", "+3.25", "1234567890123456789"]
+
+
+@pytest.mark.parametrize("pad", [0, 24])
+def test_json_parser_numbers_match_python_float(L, pad):
+    """The fast decimal path (8-digit SWAR + Clinger) returns what strtod returns, at the end of
+    a message (per-digit tail) and with 8+ readable bytes after the number (SWAR)."""
+    body = []
+    for i, s in enumerate(_EDGE_NUMBERS):
+        tail = "," + '"x":' + "1" * pad if pad else ""
+        body.append('{"features":[' + ",".join([s] * 30) + "]" + tail + "}")
+    rc, f, _, _ = _parse(L, body)
+    assert rc == len(body)
+    for i, s in enumerate(_EDGE_NUMBERS):
+        with np.errstate(over="ignore"):
+            want = np.float32(float(s))
+        assert f[i, 0] == want and f[i, 29] == want, (s, f[i, 0], want)
+
+
+def test_json_parser_rejects_malformed_numbers(L):
+    for bad in ("-", "1e", "1e+", ".", "--1", "1.2.3"):
+        rc, _, _, _ = _parse(L, ['{"features":[' + ",".join([bad] * 30) + "]}"])
+        assert rc == -1, bad
