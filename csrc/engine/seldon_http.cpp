@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "../include/ccfd_abi.h"
+#include "json_num.h"
 
 extern "C" int ccfd_engine_score_sync(void* eng, const float* x, int32_t n, float* proba_out, uint8_t* route_out);
 
@@ -66,16 +67,10 @@ struct Cur {
 
 bool parse_num(Cur& c, float* out) {
   c.ws();
-  char buf[64];
-  int n = 0;
-  while (c.p < c.e && n < 63 && (std::isdigit((unsigned char)*c.p) || *c.p == '-' || *c.p == '+' || *c.p == '.' ||
-                                  *c.p == 'e' || *c.p == 'E'))
-    buf[n++] = *c.p++;
-  if (n == 0) return false;
-  buf[n] = 0;
-  char* end = nullptr;
-  *out = std::strtof(buf, &end);
-  return end == buf + n;
+  double d;
+  if (!ccfd::json::parse_number(c.p, c.e, &d)) return false;
+  *out = (float)d;                  // decimal -> double -> float, as json.loads + float32 in Python
+  return true;
 }
 
 bool parse_str(Cur& c, std::string* out) {
