@@ -98,11 +98,30 @@ class InProcBroker:
             return partition, off
 
     def produce_many(self, topic: str, values: Iterable[bytes], partition: Optional[int] = None) -> int:
-        n = 0
-        for v in values:
-            self.produce(topic, v, partition=partition)
-            n += 1
-        return n
+        """Append many records; with an explicit partition this takes the lock and wakes the
+        consumers once for the whole batch (the one-transaction-per-message producer path)."""
+        if partition is None:
+            n = 0
+            for v in values:
+                self.produce(topic, v)
+                n += 1
+            return n
+        self.create_topic(topic)
+        now = time.time()
+        with self._cv:
+            parts = self._topics[topic]
+            if not 0 <= partition < len(parts):
+                raise BrokerError(f"{topic}: no partition {partition}")
+            P = parts[partition]
+            off = P.end
+            recs = [Record(topic, partition, off + i, None, bytes(v), now) for i, v in enumerate(values)]
+            P.records.extend(recs)
+            if self.retention is not None and len(P.records) > self.retention:
+                drop = len(P.records) - self.retention
+                del P.records[:drop]
+                P.base += drop
+            self._cv.notify_all()
+            return len(recs)
 
     def fetch(self, topic: str, partition: int, offset: int, max_records: int = 1000) -> List[Record]:
         with self._cv:

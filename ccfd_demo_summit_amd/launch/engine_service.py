@@ -115,30 +115,41 @@ class EngineService:
         # applied here: this consumer's position advances on poll, so a drop would be real loss
         from ..utils.faults import FaultPlan
         self.faults = FaultPlan.from_env(ctx.rank)
+        self._fetch = self.cfg.max_fetch
 
     # ------------------------------------------------------------------ ingest (producer side)
     def _ingest_once(self) -> int:
-        recs = self.consumer.poll(timeout=0.001, max_records=self.cfg.max_fetch)
+        # max_fetch counts messages: a TXB1 message carries a whole micro-batch, a JSON one a
+        # single transaction, so a JSON feed is polled a micro-batch of messages at a time
+        recs = self.consumer.poll(timeout=0.001, max_records=self._fetch)
         n = 0
         by_part: Dict[int, List] = collections.defaultdict(list)
         for r in recs:
             by_part[r.partition].append(r)
+        saw_json = False
         for p, rs in by_part.items():
             json_run: List[bytes] = []
+            last_off = -1
             for r in rs:
                 if r.value[:4] == TXB_MAGIC:
                     if json_run:
                         n += self._write_json(p, json_run)
+                        self._pending[p].append((self._rows_in[p], last_off + 1))
                         json_run = []
                     b = TxBatch.decode(r.value)
                     k = self.engine.ring_write(p, b.features, b.ids, b.customer)
                     self._rows_in[p] += k
                     n += k
+                    self._pending[p].append((self._rows_in[p], r.offset + 1))
                 else:
                     json_run.append(r.value)
-                self._pending[p].append((self._rows_in[p] + (len(json_run) if json_run else 0), r.offset + 1))
-            if json_run:
+                    last_off = r.offset
+            if json_run:                     # one commit point per run of JSON messages
+                saw_json = True
                 n += self._write_json(p, json_run)
+                self._pending[p].append((self._rows_in[p], last_off + 1))
+        if recs:
+            self._fetch = max(self.cfg.max_fetch, self.cfg.batch) if saw_json else self.cfg.max_fetch
         return n
 
     def _write_json(self, p: int, values: List[bytes]) -> int:
