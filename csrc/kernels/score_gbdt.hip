@@ -179,6 +179,10 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a, int 
 // for ensembles whose leaves exceed 64 KB.)
 // ---------------------------------------------------------------------------------------
 constexpr int kGb2Waves = 4;
+#ifndef CCFD_GBDT_TREE_BLOCK
+#define CCFD_GBDT_TREE_BLOCK 4
+#endif
+constexpr int kGbTb = CCFD_GBDT_TREE_BLOCK;    // trees whose split parameters are loaded together
 
 template <int D, int R>
 __global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
@@ -270,13 +274,14 @@ __global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
     float acc[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) acc[q] = 0.f;
-#pragma unroll 2
-    for (int t = 0; t < T; ++t) {
+    // one tree: D levels of (s_set_gpr_idx + v_mov, v_cmp, v_addc) per row chain, then the
+    // leaf gathered from LDS
+    auto tree = [&](int t, const int* fs, const float* ths) __attribute__((always_inline)) {
       unsigned i0 = 0, i1 = 0;
 #pragma unroll
       for (int d = D - 1; d >= 0; --d) {                       // MSB first: bit d lands at position d
-        const int f = feat[t * D + d];                          // wave-uniform -> s_load
-        const float th = thr[t * D + d];
+        const int f = fs[d];
+        const float th = ths[d];
         const float v0 = x0[f];                                 // s_set_gpr_idx + v_mov
         asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n"
                      "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
@@ -290,6 +295,26 @@ __global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
       }
       acc[0] += lv[t * L + (int)i0];
       if constexpr (R == 2) acc[R - 1] += lv[t * L + (int)i1];
+    };
+    // Split parameters of kGbTb trees at a time: one batch of s_load_dwordx8/x16 and ONE
+    // s_waitcnt per block instead of two scalar-load round trips per tree (scalar loads
+    // return out of order, so every wait is lgkmcnt(0) and nothing else hides it at the
+    // 2 waves/SIMD this kernel's LDS footprint allows).
+    int t = 0;
+    for (; t + kGbTb <= T; t += kGbTb) {
+      int fb[kGbTb * D];
+      float tb[kGbTb * D];
+#pragma unroll
+      for (int j = 0; j < kGbTb * D; ++j) { fb[j] = feat[t * D + j]; tb[j] = thr[t * D + j]; }
+#pragma unroll
+      for (int k = 0; k < kGbTb; ++k) tree(t + k, fb + k * D, tb + k * D);
+    }
+    for (; t < T; ++t) {
+      int fb[D];
+      float tb[D];
+#pragma unroll
+      for (int j = 0; j < D; ++j) { fb[j] = feat[t * D + j]; tb[j] = thr[t * D + j]; }
+      tree(t, fb, tb);
     }
 #pragma unroll
     for (int q = 0; q < R; ++q) {
