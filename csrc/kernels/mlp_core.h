@@ -281,4 +281,83 @@ struct MlpWireScorer {
   }
 };
 
+// Same math with every weight fragment held in VGPRs for the kernel's lifetime (26 bf16x8
+// A-fragments + the lane group's 4 b2 quads = 120 VGPRs): no LDS read or lgkmcnt wait on the
+// MFMA chain.  Needs the 256-VGPR budget of 2 waves/SIMD (score_mlp_wire_reg_kernel).
+struct MlpWireRegScorer {
+  static constexpr int kLds = kMlpBlobWire;
+  MlpWireLane L;
+  bf16x8 w1[8], w2[16], w3[2];
+  f32x4 b2[4];
+  __device__ __forceinline__ void stage(const ccfd_score_args& a, char* lds, int tid, int nthreads) {
+    mlp_stage(a.blob, lds, tid, nthreads, kMlpBlobWire);
+  }
+  __device__ __forceinline__ void lanes(const char* lds, const ccfd_score_args&, int g) {
+    L = mlp_wire_lane(lds);
+    const int lane = threadIdx.x & 63;
+    const bf16x8* W1f = reinterpret_cast<const bf16x8*>(lds + kOffW1);
+    const bf16x8* W2f = reinterpret_cast<const bf16x8*>(lds + kOffW2);
+    const bf16x8* W3f = reinterpret_cast<const bf16x8*>(lds + kOffW3F);
+    const f32x4* b2f = reinterpret_cast<const f32x4*>(lds + kOffB2);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) w1[t] = W1f[t * 64 + lane];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w2[t] = W2f[t * 64 + lane];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) w3[t] = W3f[t * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b2[u] = b2f[u * 4 + g];
+  }
+  __device__ __forceinline__ void tile2(const char*, const WireRegs& r0, const WireRegs& r1, int g, int,
+                                        float& p0, float& p1) const {
+    const bf16x8 xa = wire_operand(r0, g == 3, L);
+    const bf16x8 xb = wire_operand(r1, g == 3, L);
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 ha[4], hb[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[2 * s], xa, zero, 0, 0, 0);
+      const f32x4 b0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[2 * s], xb, zero, 0, 0, 0);
+      const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[2 * s + 1], xa, zero, 0, 0, 0);
+      const f32x4 b1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[2 * s + 1], xb, zero, 0, 0, 0);
+      ha[s] = __builtin_bit_cast(bf16x8, make_uint4(relu_pack_bf16x2(a0[0], a0[1]), relu_pack_bf16x2(a0[2], a0[3]),
+                                                    relu_pack_bf16x2(a1[0], a1[1]), relu_pack_bf16x2(a1[2], a1[3])));
+      hb[s] = __builtin_bit_cast(bf16x8, make_uint4(relu_pack_bf16x2(b0[0], b0[1]), relu_pack_bf16x2(b0[2], b0[3]),
+                                                    relu_pack_bf16x2(b1[0], b1[1]), relu_pack_bf16x2(b1[2], b1[3])));
+    }
+    f32x4 a2[4], b2v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4 aa = b2[u], bb = b2[u];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        aa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2[u * 4 + s], ha[s], aa, 0, 0, 0);
+        bb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2[u * 4 + s], hb[s], bb, 0, 0, 0);
+      }
+      a2[u] = aa;
+      b2v[u] = bb;
+    }
+    f32x4 za = zero, zb = zero;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint4 ua = make_uint4(relu_pack_bf16x2(a2[2 * s][0], a2[2 * s][1]), relu_pack_bf16x2(a2[2 * s][2], a2[2 * s][3]),
+                                  relu_pack_bf16x2(a2[2 * s + 1][0], a2[2 * s + 1][1]),
+                                  relu_pack_bf16x2(a2[2 * s + 1][2], a2[2 * s + 1][3]));
+      const uint4 ub = make_uint4(relu_pack_bf16x2(b2v[2 * s][0], b2v[2 * s][1]), relu_pack_bf16x2(b2v[2 * s][2], b2v[2 * s][3]),
+                                  relu_pack_bf16x2(b2v[2 * s + 1][0], b2v[2 * s + 1][1]),
+                                  relu_pack_bf16x2(b2v[2 * s + 1][2], b2v[2 * s + 1][3]));
+      za = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[s], __builtin_bit_cast(bf16x8, ua), za, 0, 0, 0);
+      zb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[s], __builtin_bit_cast(bf16x8, ub), zb, 0, 0, 0);
+    }
+    p0 = __builtin_amdgcn_rcpf(1.f + __expf(-(za[0] + L.b3)));
+    p1 = __builtin_amdgcn_rcpf(1.f + __expf(-(zb[0] + L.b3)));
+  }
+  __device__ __forceinline__ float tile(const char* lds, const WireRegs& r, int g, int lane) const {
+    float p0, p1;
+    tile2(lds, r, r, g, lane, p0, p1);
+    return p0;
+  }
+  static constexpr bool kPair = true;
+};
+
 }  // namespace ccfd

@@ -220,9 +220,25 @@ static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipSt
     hipLaunchKernelGGL((score_lr_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
 }
 
+// CCFD_LR_WAVES: waves per workgroup of the W64 single launch (4, 8, 16; default 16 -- one
+// counter flush per 16 waves; G rows/s at 1M / 4M / 16M rows: 16.3 / 44.4 / 61.1 with 4,
+// 35.5 / 67.9 / 66.1 with 16, profiles/r1/kernel_sol_lr_wg_sweep.txt).
+static int lr_wire_waves() {
+  static const int v = lr_env("CCFD_LR_WAVES", 16, 4, 8, 16);
+  return v;
+}
+
 int launch_lr(const ccfd_score_args& a, hipStream_t s) {
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
+  if (a.flags & CCFD_ARG_WIRE_W64) {
+    switch (lr_wire_waves()) {
+      case 4: launch_lr_w<4>(a, ntiles, contig, s); break;
+      case 8: launch_lr_w<8>(a, ntiles, contig, s); break;
+      default: launch_lr_w<16>(a, ntiles, contig, s); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   switch (mlp_waves_for(ntiles)) {
     case 1: launch_lr_w<1>(a, ntiles, contig, s); break;
     case 2: launch_lr_w<2>(a, ntiles, contig, s); break;

@@ -128,6 +128,12 @@ void score_mlp_wire_kernel(ccfd_score_args a) {
   wire_stream_body<MlpWireScorer, kWaves, kPf>(a, blockIdx.x, gridDim.x);
 }
 
+template <int kWaves, int kPf>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2)))
+void score_mlp_wire_reg_kernel(ccfd_score_args a) {
+  wire_stream_body<MlpWireRegScorer, kWaves, kPf>(a, blockIdx.x, gridDim.x);
+}
+
 // Coalesced launch: workgroups [j*wpb, (j+1)*wpb) score sub-batch j.
 template <int kMode, int kWaves>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
@@ -162,8 +168,28 @@ static int mlp_wire_prefetch() {
   return v;
 }
 
+// CCFD_MLP_REGW (default 1): W64 weights resident in VGPRs at 2 waves/SIMD
+// (MlpWireRegScorer); 0 = per-tile LDS fragment reads at 4 waves/SIMD (MlpWireScorer).
+// Measured with 8-wave workgroups (profiles/r1/kernel_sol_mlp_wg_regw_sweep.txt).
+static bool mlp_reg_weights() {
+  static const bool v = [] {
+    const char* e = std::getenv("CCFD_MLP_REGW");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 template <int kW>
 static void launch_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
+  if (kW <= 8 && mlp_reg_weights()) {     // 2 waves/SIMD: at most 8 waves per workgroup
+    const int cap = 256 * 8 / kW;          // 2 waves/SIMD residency
+    if ((int)grid.x > cap) grid.x = cap;
+    switch (mlp_wire_prefetch()) {
+      case 4: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
+      default: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
+    }
+    return;
+  }
   switch (mlp_wire_prefetch()) {
     case 1: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 1>), grid, dim3(64 * kW), 0, s, a); break;
     default: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
@@ -221,7 +247,7 @@ int mlp_waves_for(int ntiles) {
     const char* e = std::getenv("CCFD_MLP_WAVES");
     return e ? std::atoi(e) : 0;
   }();
-  if (forced == 1 || forced == 2 || forced == 4) return forced;
+  if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16) return forced;
   (void)ntiles;
   return 4;   // measured: 1-wave workgroups lose (per-workgroup weight staging + completion)
 }
@@ -245,10 +271,30 @@ int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// Waves per workgroup of the W64 single launch: CCFD_MLP_WAVES when set, else 8 -- half the
+// blob stagings and counter flushes of 4-wave groups, and the widest group the 2-waves/SIMD
+// register-weight kernel allows (+47 % at 256K-1M rows, same at 16M).
+static int mlp_wire_waves(int ntiles) {
+  static const bool forced = std::getenv("CCFD_MLP_WAVES") != nullptr;
+  return forced ? mlp_waves_for(ntiles) : 8;
+}
+
 int launch_mlp(const ccfd_score_args& a, hipStream_t s) {
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
-  switch (mlp_waves_for(ntiles)) {
+  const int w = (a.flags & CCFD_ARG_WIRE_W64) ? mlp_wire_waves(ntiles) : mlp_waves_for(ntiles);
+  if ((a.flags & CCFD_ARG_WIRE_W64) && (w == 8 || w == 16)) {
+    // wider workgroups for the W64 path: one blob staging, flush and completion release per
+    // 8 or 16 waves instead of per 4
+    const int per_wg = w * mlp_tiles_per_wave();
+    int grid = (ntiles + per_wg - 1) / per_wg;
+    const int cap = 256 * 16 / w;
+    grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
+    if (w == 8) launch_wire<8>(dim3(grid), s, a);
+    else launch_wire<16>(dim3(grid), s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
+  switch (w) {
     case 1: launch_w<1>(a, ntiles, contig, s); break;
     case 2: launch_w<2>(a, ntiles, contig, s); break;
     default: launch_w<4>(a, ntiles, contig, s); break;
