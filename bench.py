@@ -45,7 +45,9 @@ def parse_args(argv=None):
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
     ap.add_argument("--batch", type=int, default=4096, help="micro-batch rows")
     ap.add_argument("--batches-per-step", type=int, default=256)
-    ap.add_argument("--depth", type=int, default=32, help="micro-batches in flight per GPU")
+    ap.add_argument("--depth", type=int, default=16,
+                    help="micro-batches in flight per GPU (16 = p50 <= 80 us at the PCIe-bound rate: "
+                         "profiles/r2/operating_curve.txt)")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
@@ -64,9 +66,26 @@ def parse_args(argv=None):
     ap.add_argument("--threshold", type=float, default=0.5)
     ap.add_argument("--gbdt-trees", type=int, default=100)
     ap.add_argument("--gbdt-depth", type=int, default=6)
-    ap.add_argument("--x2-every", type=int, default=8,
-                    help="steps between X2 counter all-reduces (8 x ~1.3 ms = the >= 10 ms reduction "
-                         "period of SURVEY.md 2.5); a step count, so every rank issues the same collectives")
+    ap.add_argument("--x2-every", type=int, default=0,
+                    help="steps between X2 counter all-reduces (SURVEY.md 2.5: >= 10 ms period); a step "
+                         "count, so every rank issues the same collectives.  0 = derive from "
+                         "--x2-period-ms and the calibrated step time")
+    ap.add_argument("--x2-period-ms", type=float, default=10.0,
+                    help="target X2 all-reduce period; --x2-every is derived from the calibrated step "
+                         "time when --x2-every is 0 (default)")
+    ap.add_argument("--min-timed-s", type=float, default=1.5,
+                    help="sustained measurement: after warmup, --batches-per-step is raised (same value "
+                         "on every rank) so that the K timed steps last at least this long")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow a rehearsal topology (WORLD_SIZE != --gpus, gloo collectives, several "
+                         "ranks per GPU); the JSON line is then labelled rehearsal and must not be "
+                         "quoted as an N-GPU number")
+    ap.add_argument("--probe-ms", type=float, default=200.0,
+                    help="per-rank zero-copy H2D bandwidth probe, all ranks concurrently (0 = off)")
+    ap.add_argument("--precision-rows", type=int, default=1 << 20,
+                    help="rows scored through the device kernel and compared with the fp32 oracle")
+    ap.add_argument("--no-f32-probe", action="store_true",
+                    help="skip the secondary f32-wire throughput run (W64 headline only)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-unloaded-probe", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
@@ -84,6 +103,131 @@ def baseline_value():
     return None
 
 
+def _fail(msg: str) -> None:
+    print(f"[bench] FATAL: {msg}", file=sys.stderr, flush=True)
+    raise SystemExit(3)
+
+
+def _device_ident(ctx, dev) -> dict:
+    import socket
+    import torch
+    p = torch.cuda.get_device_properties(dev.index)
+    return {"rank": ctx.rank, "host": socket.gethostname(), "device": dev.index,
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "name": p.name}
+
+
+def _verify_topology(args, ctx, ident: dict):
+    """An N-GPU number must come from N ranks, one per distinct GPU, over RCCL.  Returns
+    (per-rank device identities, problems); exits non-zero on any problem unless
+    --rehearsal (then the line is labelled a rehearsal)."""
+    problems = []
+    if ctx.world != args.gpus:
+        problems.append(f"--gpus {args.gpus} but WORLD_SIZE={ctx.world}")
+    if ctx.world > 1 and ctx.backend != "nccl":
+        problems.append(f"backend {ctx.backend!r} (an N>1 run must use nccl = RCCL over xGMI)")
+    if os.environ.get("CCFD_DEVICE_MODULO") == "1" and ctx.world > 1:
+        problems.append("CCFD_DEVICE_MODULO=1 maps several ranks onto one GPU")
+    idents = [ident]
+    if ctx.initialized:
+        import torch.distributed as dist
+        idents = [None] * ctx.world
+        dist.all_gather_object(idents, ident)
+        seen = {}
+        for d in idents:
+            key = (d["host"], d["pci"])
+            if key in seen:
+                problems.append(f"ranks {seen[key]} and {d['rank']} share GPU {d['pci']} on {d['host']}")
+            seen.setdefault(key, d["rank"])
+        if dist.get_world_size() != ctx.world:
+            problems.append(f"process group size {dist.get_world_size()} != WORLD_SIZE {ctx.world}")
+    if problems and not args.rehearsal:
+        for m in problems:
+            if ctx.rank == 0:
+                print(f"[bench] topology check failed: {m}", file=sys.stderr)
+        _fail("refusing to report an N-GPU number from this topology (use --rehearsal to run anyway)")
+    return idents, problems
+
+
+def _h2d_probe(lib_, ms: float, mb: int = 256) -> float:
+    """Zero-copy kernel read bandwidth from this rank's pinned host memory (GB/s), run for
+    ~``ms`` (the bench/roofline.py method); all ranks run it at once, so host-DRAM and
+    PCIe-root contention between ranks shows up here."""
+    import ctypes as C
+    import torch
+    from ccfd_demo_summit_amd.engine import PinnedArray
+    L = lib_()
+    L.ccfd_bw_probe.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p]
+    L.ccfd_bw_probe.restype = C.c_double
+    nbytes = mb << 20
+    host = PinnedArray(nbytes // 4, "float32")
+    host.array[:] = 1.0
+    scratch = torch.empty(1 << 16, dtype=torch.uint8, device="cuda")
+    try:
+        one = L.ccfd_bw_probe(C.c_void_p(host.ptr), nbytes, 1, 1, C.c_void_p(scratch.data_ptr()))
+        iters = max(1, int(ms / 1e3 * one * 1e9 / nbytes)) if one > 0 else 1
+        return float(L.ccfd_bw_probe(C.c_void_p(host.ptr), nbytes, 1, iters, C.c_void_p(scratch.data_ptr())))
+    finally:
+        host.free()
+
+
+def _precision(model, dm, args, dev):
+    """Device kernel vs the fp32 oracle on ``--precision-rows`` rows, through the SAME row
+    format and blob as the headline (W64 wire rows when args.wire == 'w64')."""
+    import torch
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.engine.stream_engine import WIRE_ROW_F32, encode_w64
+    from ccfd_demo_summit_amd.ops.kernels import score
+    n = int(args.precision_rows)
+    X, _ = generate(n, seed=args.seed + 4242)
+    if args.wire == "w64":
+        rows = np.empty((n, WIRE_ROW_F32), np.float32)
+        encode_w64(X, rows.ctypes.data)
+        xt = torch.from_numpy(rows).to(dev)
+    else:
+        xt = torch.from_numpy(X).to(dev)
+    pd, rd = score(dm, xt, threshold=args.threshold)
+    torch.cuda.synchronize(dev)
+    pd = pd.cpu().numpy().astype(np.float64)
+    rd = rd.cpu().numpy()
+    p32 = model.predict_proba(X).astype(np.float64)
+    r32 = (p32 >= args.threshold)
+    dp = np.abs(pd - p32)
+    flips = (rd.astype(bool) != r32)
+    outside = np.abs(p32 - args.threshold) > 1e-2
+    return {"rows": n, "oracle": "fp32 numpy predict_proba on the unquantised f32 rows",
+            "row_format": args.wire, "max_abs_dp": float(dp.max()), "mean_abs_dp": float(dp.mean()),
+            "route_flips": int(flips.sum()), "route_flip_rate": float(flips.mean()),
+            "route_flips_outside_1e-2_band": int((flips & outside).sum()),
+            "fraud_routed_fp32": int(r32.sum()), "fraud_routed_device": int(rd.astype(bool).sum())}
+
+
+def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
+    """Secondary run: same model on 30 x f32 (120 B) rows, same engine knobs; tx/s only."""
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    dm32 = DeviceModel(model, dev)
+    rows = 1 << 20
+    log = PartitionLog(rows)
+    generate(rows, seed=args.seed + 77, out=log.feats.array)
+    log.ids.array[:] = np.arange(rows, dtype=np.uint64)
+    eng = StreamEngine(dm32, batch=args.batch, depth=args.depth, streams=args.streams,
+                       input_mode=args.input_mode, output_mode=args.output_mode, threshold=args.threshold,
+                       device=dev.index, exec_mode=exec_mode, persist_grid=args.persist_grid,
+                       coalesce=args.coalesce)
+    eng.add_log(0, log)
+    eng.pump(256, drain=True)
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds:
+        n += eng.pump(512, drain=False).rows
+    n += eng.pump(0, drain=True).rows
+    dt = time.perf_counter() - t0
+    eng.close()
+    log.free()
+    return n / dt
+
+
 def main(argv=None):
     args = parse_args(argv)
     if args.wire == "auto":
@@ -92,25 +236,24 @@ def main(argv=None):
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.models import build_model
+    from ccfd_demo_summit_amd.ops._lib import lib
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     from ccfd_demo_summit_amd.parallel import (CounterReducer, EpochPipeline, all_max, assign_partitions,
                                                barrier, broadcast_blob, hist_quantile, init_distributed)
 
-    ctx = init_distributed()
-    if ctx.world != args.gpus:
-        if ctx.rank == 0:
-            print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ctx.world}; using WORLD_SIZE",
-                  file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
+    ctx = init_distributed()
     dev = ctx.device
     W = ctx.world
+    idents, problems = _verify_topology(args, ctx, _device_ident(ctx, dev))
     from ccfd_demo_summit_amd.utils.numa import bind_to_gpu
     numa_node = bind_to_gpu(dev.index)     # pinned logs + host threads on the GPU's socket
 
     # ---- model: rank 0 builds (random init of the named architecture; normaliser fitted and
     # output bias calibrated on a synthetic sample so ~0.17 % of traffic routes to the fraud
     # process, like the dataset prior), X1 broadcast over RCCL to every rank.
+    model = None
     if ctx.rank == 0:
         Xcal, _ = generate(200_000, seed=args.seed + 999)
         model = build_model(args.model, seed=args.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE,
@@ -130,6 +273,13 @@ def main(argv=None):
         # coalesced launches (0.75e9 at 166 us); GBDT and DMA paths use launches
         zc = args.input_mode == "zerocopy" and args.output_mode == "zerocopy"
         exec_mode = "persistent" if args.model in ("mlp", "lr") and zc else "launch"
+
+    # ---- per-rank H2D ceiling probe, all ranks at once (attributes any scaling loss to the
+    # host side: DRAM / PCIe root contention shows up as a lower per-rank GB/s at N > 1)
+    h2d_gbps = None
+    if args.probe_ms > 0 and args.input_mode == "zerocopy":
+        barrier(ctx)
+        h2d_gbps = _h2d_probe(lib, args.probe_ms)
 
     # ---- this rank's partitions of topic odh-demo (p % W == rank), pre-filled logs
     n_parts = args.partitions_per_rank * W
@@ -157,16 +307,19 @@ def main(argv=None):
     epochs = EpochPipeline(eng, reducer)
     flagged_total = 0
     x2_s = [0.0]
-
     nstep = [0]
+    bps = [args.batches_per_step]
+    x2_every = [max(1, args.x2_every or 8)]
+
+    rows_local = [0]
 
     def step(drain: bool):
         nonlocal flagged_total
-        eng.pump(args.batches_per_step, drain=drain)
+        rows_local[0] += eng.pump(bps[0], drain=drain).rows
         # router hand-off of fraud-routed transactions (transaction.outgoing{type=fraud})
         flagged_total += len(eng.drain_flagged())
         nstep[0] += 1
-        if nstep[0] % max(1, args.x2_every):
+        if nstep[0] % x2_every[0]:
             return
         # X2/X3: flip the counter epoch; the previously closed epoch (all of whose batches
         # have completed by now) is all-reduced over RCCL on the side stream
@@ -176,6 +329,17 @@ def main(argv=None):
 
     for _ in range(args.warmup):
         step(drain=False)
+    # ---- calibration (untimed): size a step so the K timed steps are a sustained run of at
+    # least --min-timed-s; every rank takes the max, so all ranks run the same work
+    tc = time.perf_counter()
+    cal_steps = 4
+    for _ in range(cal_steps):
+        step(drain=False)
+    per_batch_s = all_max(ctx, (time.perf_counter() - tc) / (cal_steps * bps[0]))
+    need = int(np.ceil(args.min_timed_s * 1.05 / max(1, args.steps) / max(per_batch_s, 1e-9)))
+    bps[0] = max(args.batches_per_step, need)
+    step_s_est = bps[0] * per_batch_s
+    x2_every[0] = args.x2_every or max(1, int(round(args.x2_period_ms / 1e3 / max(step_s_est, 1e-9))))
     eng.pump(0, drain=True)
     epochs.finish()
     eng.reset_stats()
@@ -185,6 +349,7 @@ def main(argv=None):
     flagged_total = 0
     x2_s[0] = 0.0
     nstep[0] = 0
+    rows_local[0] = 0
     barrier(ctx)
     torch.cuda.synchronize(dev)
 
@@ -193,12 +358,14 @@ def main(argv=None):
         step(drain=(k == args.steps - 1))
     epochs.finish()
     torch.cuda.synchronize(dev)
+    t_local = time.perf_counter() - t0
     barrier(ctx)
     t1 = time.perf_counter()
     elapsed = all_max(ctx, t1 - t0)
 
     # latency: per-rank histogram of the timed batches, merged over ranks (X3)
     st_final = eng.pump(0, drain=True)
+    rows_local[0] += st_final.rows
     lat_local = st_final.lat_hist.astype(np.int64)
     lat_t = torch.from_numpy(lat_local).to(dev)
     if ctx.initialized:
@@ -207,9 +374,28 @@ def main(argv=None):
     lat = lat_t.cpu().numpy()
     counters, _ = reducer.snapshot()
     total_rows = int(counters[0] - rows0)
-    expected = args.steps * args.batches_per_step * args.batch * W
+    expected = args.steps * bps[0] * args.batch * W
     p50_us = hist_quantile(lat, 0.50) / 1e3
     p99_us = hist_quantile(lat, 0.99) / 1e3
+    nb_local = args.steps * bps[0]
+    rank_info = {
+        "rank": ctx.rank, "pci": idents[ctx.rank]["pci"] if ctx.initialized else idents[0]["pci"],
+        "host": (idents[ctx.rank] if ctx.initialized else idents[0])["host"],
+        "numa_node": numa_node,
+        "rows": int(rows_local[0]),
+        "tx_s": round(rows_local[0] / t_local, 1) if t_local > 0 else None,
+        "local_timed_s": round(t_local, 4),
+        "p50_latency_us": round(hist_quantile(lat_local, 0.5) / 1e3, 2),
+        "device_exec_us_p50": round(hist_quantile(st_final.dev_hist.astype(np.int64), 0.5) / 1e3, 2)
+        if st_final.dev_batches else None,
+        "host_wait_us_per_batch": round(st_final.host_wait_s * 1e6 / nb_local, 3),
+        "h2d_zerocopy_GBps": None if h2d_gbps is None else round(h2d_gbps, 2),
+    }
+    per_rank = [rank_info]
+    if ctx.initialized:
+        import torch.distributed as dist
+        per_rank = [None] * W
+        dist.all_gather_object(per_rank, rank_info)
 
     # unloaded latency probe (not timed): one micro-batch at a time, depth 1
     p50_unloaded = None
@@ -223,9 +409,21 @@ def main(argv=None):
         sp = probe.pump(200, drain=True)
         p50_unloaded = sp.p50_us
         probe.close()
+    eng.close()
+    for log in logs:
+        log.free()
+
+    # precision evidence + f32-row throughput (rank 0, after the timed region)
+    precision = f32_rate = None
+    if ctx.rank == 0:
+        if args.precision_rows > 0:
+            precision = _precision(model, dm, args, dev)
+        if args.wire == "w64" and not args.no_f32_probe:
+            f32_rate = _f32_wire_rate(args, model, dev, exec_mode)
 
     value = total_rows / elapsed
     base = baseline_value()
+    rehearsal = bool(problems)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -236,7 +434,11 @@ def main(argv=None):
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
+        # context only: config 1 is OUR CPU batch=1 LR REST measurement, not a
+        # published reference number and not the same model
         "vs_baseline": (round(value / base, 1) if base else None),
+        "vs_baseline_note": "ratio to config 1 (CPU LR batch=1 Seldon REST, measured by us); "
+                            "the reference publishes no numbers",
         "dtype": "bf16" if args.model == "mlp" else "fp32",
         "data": ("synthetic creditcard-shaped transactions (30 features; log rows "
                  + ("W64: bf16 V1..V28 + f32 Time/Amount, 64 B" if args.wire == "w64" else "30 x f32, 120 B")
@@ -245,30 +447,40 @@ def main(argv=None):
         "config": {"model": {"mlp": "mlp_30_128_64_1", "lr": "logreg_30",
                              "gbdt": f"oblivious_gbdt_{args.gbdt_trees}x{args.gbdt_depth}"}[args.model],
                    "global_batch": args.batch * W, "seq_len": 1, "micro_batch": args.batch,
-                   "parallelism": f"dp{W}", "input_mode": args.input_mode,
+                   "parallelism": f"dp{W}" + ("-rehearsal" if rehearsal else ""),
+                   "input_mode": args.input_mode,
                    "output_mode": args.output_mode, "exec_mode": exec_mode, "depth": args.depth,
                    "wire": args.wire, "coalesce": args.coalesce,
                    "streams": args.streams,
-                   "batches_per_step": args.batches_per_step, "x2_every_steps": args.x2_every,
+                   "batches_per_step": bps[0], "x2_every_steps": x2_every[0],
                    "numa_node_rank0": numa_node},
+        "timed_region_s": round(elapsed, 4),
+        "backend": ctx.backend,
+        "world_size": W,
+        "rehearsal": rehearsal,
+        "topology_problems": problems,
         "p50_latency_us": round(p50_us, 2),
         "p99_latency_us": round(p99_us, 2),
         "p50_latency_us_unloaded": None if p50_unloaded is None else round(p50_unloaded, 2),
         # engine host-thread time per timed micro-batch (cumulative since reset_stats)
-        "host_us_per_batch": {k: round(v * 1e6 / (args.steps * args.batches_per_step), 3) for k, v in
+        "host_us_per_batch": {k: round(v * 1e6 / nb_local, 3) for k, v in
                               (("submit", st_final.host_submit_s), ("wait", st_final.host_wait_s),
                                ("complete", st_final.host_complete_s))},
         # host time per step spent in the X2 tick (epoch flip + side-stream all-reduce issue)
         "host_us_per_step_x2": round(x2_s[0] * 1e6 / args.steps, 2),
-        "step_us_per_batch": round(elapsed * 1e6 / (args.steps * args.batches_per_step), 3),
+        "step_us_per_batch": round(elapsed * 1e6 / nb_local, 3),
         # K7: per-micro-batch execution window on the GPU's own clock (rank 0)
         "device_exec_us_mean": round(st_final.dev_exec_mean_us, 2),
-        "device_exec_us_p50": round(hist_quantile(st_final.dev_hist.astype(np.int64), 0.5) / 1e3, 2)
-        if st_final.dev_batches else None,
+        "device_exec_us_p50": rank_info["device_exec_us_p50"],
         "rows_scored": total_rows,
         "rows_expected": expected,
         "fraud_routed": int(counters[1]) - fraud0,
         "flagged_handed_off_rank0": flagged_total,
+        "per_rank": per_rank,
+        "h2d_zerocopy_ceiling_tx_s_rank0": (None if h2d_gbps is None else
+                                            round(h2d_gbps * 1e9 / (64 if args.wire == "w64" else 120), 1)),
+        "f32_wire_tx_s": None if f32_rate is None else round(f32_rate, 1),
+        "precision_vs_fp32": precision,
     }
     if total_rows != expected and ctx.rank == 0:
         print(f"[bench] WARNING: counted {total_rows} rows, expected {expected}", file=sys.stderr)
@@ -277,11 +489,12 @@ def main(argv=None):
         print(line, flush=True)
         if args.out:
             Path(args.out).write_text(line + "\n")
-    eng.close()
     if ctx.initialized:
         import torch.distributed as dist
         barrier(ctx)
         dist.destroy_process_group()
+    if total_rows != expected:
+        raise SystemExit(4)
 
 
 if __name__ == "__main__":

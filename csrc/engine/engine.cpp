@@ -49,6 +49,8 @@ namespace {
 
 using ccfd::set_error;
 
+std::atomic<int> g_persist_engines{0};     // persistent engines alive in this process
+
 inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -136,7 +138,14 @@ class Engine {
   uint64_t ring_head = 0, ring_tail = 0;
   std::mutex ring_mu;
   uint64_t dropped = 0;
-  std::vector<float> lat_us;
+  // per-batch latency: O(1) memory however long the engine runs (a long-lived service
+  // scores ~2e5 batches/s): count/sum/max, a 0.25-us linear histogram up to 4 ms for the
+  // reported quantiles, and the 4-buckets-per-octave log histogram merged over ranks (X3)
+  static constexpr int kFineBuckets = 16384;
+  static constexpr double kFineUs = 0.25;
+  uint64_t lat_n = 0, lat_over = 0;
+  double lat_sum_us = 0.0, lat_max_us = 0.0;
+  std::vector<uint32_t> lat_fine = std::vector<uint32_t>(kFineBuckets, 0u);
   uint64_t lat_hist[256] = {};
   uint64_t t_submit_ns = 0, t_wait_ns = 0, t_complete_ns = 0;
   uint64_t dev_batches = 0, dev_exec_ns = 0, dev_hist[256] = {};
@@ -210,6 +219,7 @@ class Engine {
 
   // ------------------------------------------------------------------ persistent mode
   bool persistent = false;
+  bool persist_counted = false;            // holds one of the process's persistent-queue slots
   bool coherent_out = true;
   uint64_t launches = 0;        // coalesced launches issued (stream round-robin)
   int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, or 16 for W64 wire rows
@@ -256,7 +266,26 @@ class Engine {
     for (int i = 0; i < CCFD_PERSIST_MAX_RING; ++i) init.remaining[i] = (unsigned)C;
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&pdev), sizeof(ccfd_persist_dev)));
     HIPCHK(hipMemcpy(pdev, &init, sizeof(init), hipMemcpyHostToDevice));
-    HIPCHK(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
+    // The persistent kernel never ends, and the HIP runtime multiplexes streams onto
+    // GPU_MAX_HW_QUEUES hardware queues PER PRIORITY LEVEL: any stream that shares the
+    // kernel's queue sits behind it forever (measured: the 4th normal-priority torch stream
+    // created after the engine stalled; tests/helpers/queue_probe.py).  The kernel's stream
+    // therefore takes the LEAST priority level, which neither torch (0 / -1) nor RCCL use,
+    // and at most GPU_MAX_HW_QUEUES persistent engines may exist per process.
+    {
+      int least = 0, greatest = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      int max_q = 4;
+      if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) max_q = std::max(1, std::atoi(e));
+      if (g_persist_engines.fetch_add(1) >= max_q) {
+        g_persist_engines.fetch_sub(1);
+        set_error("more persistent engines than GPU_MAX_HW_QUEUES in one process: their kernels would share "
+                  "a hardware queue");
+        return -1;
+      }
+      persist_counted = true;
+      HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, least));
+    }
     persist_C = C;
     persistent = true;
     return 0;
@@ -313,13 +342,19 @@ class Engine {
   }
 
   void persist_free() {
-    if (!persistent) return;
+    if (!persistent) {
+      if (persist_counted) g_persist_engines.fetch_sub(1);
+      persist_counted = false;
+      return;
+    }
     for (auto& s : slots) if (s.busy) wait_done(s);
     persist_halt();
     hipStreamDestroy(pstream);
     hipFree(pdev);
     hipHostFree(pdesc);
     hipHostFree(pctl);
+    if (persist_counted) g_persist_engines.fetch_sub(1);
+    persist_counted = false;
     persistent = false;
   }
 
@@ -444,7 +479,13 @@ class Engine {
     t_wait_ns += t - tw;
     const int64_t t0 = s.t_arrival ? s.t_arrival : s.t_submit;   // ring: end-to-end from commit
     const double us = (t - t0) * 1e-3;
-    lat_us.push_back((float)us);
+    ++lat_n;
+    lat_sum_us += us;
+    lat_max_us = std::max(lat_max_us, us);
+    {
+      const double fb = us / kFineUs;
+      if (fb < kFineBuckets) ++lat_fine[(size_t)fb]; else ++lat_over;
+    }
     const double ns = (double)std::max<int64_t>(1, t - t0);
     lat_hist[std::min(255, (int)std::floor(4.0 * std::log2(ns)))]++;
     uint64_t nf = 0;
@@ -633,6 +674,25 @@ class Engine {
     return 0;
   }
 
+  // nearest-rank quantile from the fine histogram (bucket midpoint); samples beyond its
+  // range report the max
+  double fine_quantile(double q) const {
+    const uint64_t k = (uint64_t)std::floor(q * (double)(lat_n - 1) + 0.5);
+    uint64_t c = 0;
+    for (int i = 0; i < kFineBuckets; ++i) {
+      c += lat_fine[i];
+      if (c > k) return (i + 0.5) * kFineUs;
+    }
+    return lat_max_us;
+  }
+
+  void reset_latency() {
+    lat_n = lat_over = 0;
+    lat_sum_us = lat_max_us = 0.0;
+    std::fill(lat_fine.begin(), lat_fine.end(), 0u);
+    std::memset(lat_hist, 0, sizeof(lat_hist));
+  }
+
   void fill_latency(ccfd_engine_stats* st) {
     std::memcpy(st->lat_hist, lat_hist, sizeof(lat_hist));
     st->host_submit_ns = t_submit_ns;
@@ -641,19 +701,11 @@ class Engine {
     st->dev_batches = dev_batches;
     st->dev_exec_ns = dev_exec_ns;
     std::memcpy(st->dev_hist, dev_hist, sizeof(dev_hist));
-    if (lat_us.empty()) return;
-    std::vector<float> v = lat_us;
-    auto pct = [&](double q) {
-      size_t k = (size_t)std::min<double>(v.size() - 1, std::floor(q * (v.size() - 1) + 0.5));
-      std::nth_element(v.begin(), v.begin() + k, v.end());
-      return (double)v[k];
-    };
-    st->lat_p50_us = pct(0.50);
-    st->lat_p99_us = pct(0.99);
-    double mx = 0, sum = 0;
-    for (float x : lat_us) { mx = std::max<double>(mx, x); sum += x; }
-    st->lat_max_us = mx;
-    st->lat_mean_us = sum / lat_us.size();
+    if (lat_n == 0) return;
+    st->lat_p50_us = fine_quantile(0.50);
+    st->lat_p99_us = fine_quantile(0.99);
+    st->lat_max_us = lat_max_us;
+    st->lat_mean_us = lat_sum_us / (double)lat_n;
   }
 
   int score_sync(const float* x, int32_t n, float* proba_out, uint8_t* route_out) {
@@ -912,11 +964,10 @@ int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_
 
 void ccfd_engine_reset_stats(void* eng) {
   auto* e = static_cast<Engine*>(eng);
-  std::memset(e->lat_hist, 0, sizeof(e->lat_hist));
+  e->reset_latency();
   e->t_submit_ns = e->t_wait_ns = e->t_complete_ns = 0;
   e->dev_batches = e->dev_exec_ns = 0;
   std::memset(e->dev_hist, 0, sizeof(e->dev_hist));
-  e->lat_us.clear();
 }
 
 }  // extern "C"

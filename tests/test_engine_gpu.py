@@ -204,3 +204,15 @@ def test_lr_coalesced_pump_matches_oracle(gpu, setup, wire):
     assert int(c[0]) == 6 * 4096
     eng.close()
     log.free()
+
+
+def test_persistent_queue_isolation(gpu):
+    """While the persistent kernel is resident, fresh torch streams (normal and high
+    priority) and the default stream still make progress: the kernel owns a hardware queue
+    no other stream is mapped onto (GPU_MAX_HW_QUEUES=4 multiplexes streams onto queues)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    probe = Path(__file__).parent / "helpers" / "queue_probe.py"
+    r = subprocess.run([sys.executable, str(probe), "12"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "ALL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
