@@ -97,7 +97,7 @@ class GroupConsumer:
         self.join()
 
     def _coordinator(self) -> Tuple[str, int]:
-        r = self.broker._boot.request(10, 0, Writer().string(self.group).build())     # FindCoordinator v0
+        r = self.broker._boot_request(10, 0, Writer().string(self.group).build())     # FindCoordinator v0
         err = r.i16()
         if err:
             raise BrokerError(f"FindCoordinator error {err}")

@@ -1,12 +1,25 @@
-"""``kafka-lite``: a single-node broker speaking the Kafka wire protocol subset of
-``kafka_wire`` on top of the in-process log store.
+"""``kafka-lite``: a broker (or a small multi-broker cluster) speaking the Kafka wire
+protocol subset of ``kafka_wire``.
 
 Stands in for the reference's 3-broker Strimzi cluster (deploy/frauddetection_cr.yaml:
 73-77) in development, CI and single-node deployments: every service of the framework
 (producer, engine/router, KIE, notifier) can run as a separate process and talk real Kafka
 protocol to it, and switching to a production cluster is only a ``BROKER_URL`` change.
 
-    python -m ccfd_demo_summit_amd.ingest.kafka_lite --port 9092 --partitions 8
+Storage keeps producer RecordBatches verbatim (``batch_store.py``): Produce validates the
+CRC and stamps the base offset, Fetch slices stored batches -- no per-record work.
+
+``KafkaLiteCluster(n)`` runs n broker listeners (node ids 1..n) over one shared log store,
+with partition leadership spread over the nodes (p -> node p % n).  Produce / Fetch /
+ListOffsets sent to a node that does not lead the partition answer NOT_LEADER_FOR_PARTITION,
+Metadata reports per-partition leaders, ``move_leader`` moves one partition and
+``fail_node`` closes a broker and fails its partitions over to the next live node (the
+controller's job), so clients have to route by leader and recover like against a real
+cluster.  Replication is not simulated beyond that (one shared store): replicas = every
+node, ISR = the live nodes, so the under-replicated / offline-partition series of the
+reference's Kafka dashboard (deploy/grafana/Kafka.json:127-355) move when a node fails.
+
+    python -m ccfd_demo_summit_amd.ingest.kafka_lite --port 9092 --partitions 8 [--nodes 3]
 """
 from __future__ import annotations
 
@@ -16,13 +29,13 @@ import itertools
 import struct
 import threading
 import time
-from typing import Dict, Optional, Set
+from typing import Dict, List, Optional, Set, Tuple
 
-from .broker import InProcBroker
-from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS,
-                         ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, FETCH, FIND_COORDINATOR, LIST_OFFSETS,
-                         METADATA, OFFSET_COMMIT, OFFSET_FETCH, PRODUCE, SUPPORTED, Reader, Writer,
-                         decode_record_batches, encode_record_batch)
+from .batch_store import BatchStore, InvalidBatch
+from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER,
+                         ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION,
+                         FETCH, FIND_COORDINATOR, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH, PRODUCE,
+                         SUPPORTED, Reader, Writer)
 
 NODE_ID = 1
 ERR_ILLEGAL_GENERATION, ERR_UNKNOWN_MEMBER, ERR_REBALANCE_IN_PROGRESS = 22, 25, 27
@@ -53,12 +66,69 @@ class _Group:
         self.deadline_task: Optional[asyncio.Task] = None
 
 
+class ClusterState:
+    """Node table + partition leadership (the controller's view) shared by the listeners."""
+
+    def __init__(self, store: BatchStore):
+        self.store = store
+        self.nodes: Dict[int, List] = {}                  # id -> [host, port, alive]
+        self.leaders: Dict[Tuple[str, int], int] = {}
+        self.groups: Dict[str, _Group] = {}
+        self.mid = itertools.count(1)
+        self.lock = threading.Lock()
+        self.leader_moves = 0
+
+    def live(self) -> List[int]:
+        return sorted(n for n, v in self.nodes.items() if v[2])
+
+    def leader(self, topic: str, partition: int) -> int:
+        with self.lock:
+            key = (topic, partition)
+            if key not in self.leaders:
+                ids = sorted(self.nodes)
+                cand = ids[partition % len(ids)]
+                if not self.nodes[cand][2]:
+                    live = self.live()
+                    cand = live[partition % len(live)] if live else -1
+                self.leaders[key] = cand
+            return self.leaders[key]
+
+    def move_leader(self, topic: str, partition: int, node: int) -> None:
+        with self.lock:
+            if node not in self.nodes or not self.nodes[node][2]:
+                raise ValueError(f"node {node} is not a live broker")
+            self.leaders[(topic, partition)] = node
+            self.leader_moves += 1
+
+    def fail_node(self, node: int) -> None:
+        """Broker failure as the controller sees it: the node leaves the ISR and every
+        partition it led moves to the next live node."""
+        with self.lock:
+            self.nodes[node][2] = False
+            live = sorted(n for n, v in self.nodes.items() if v[2])
+            for key, lead in list(self.leaders.items()):
+                if lead == node:
+                    self.leaders[key] = live[key[1] % len(live)] if live else -1
+                    self.leader_moves += 1
+
+    def under_replicated(self) -> int:
+        dead = len(self.nodes) - len(self.live())
+        return self.partition_count() if dead else 0
+
+    def offline(self) -> int:
+        return sum(1 for t, n in self.store.topics().items() for p in range(n) if self.leader(t, p) < 0)
+
+    def partition_count(self) -> int:
+        return sum(self.store.topics().values())
+
+
 class BrokerMetrics:
     """The Strimzi/JMX-exporter series the reference's Kafka dashboard queries
     (deploy/grafana/Kafka.json:119-1093): topic message/byte rates, failed requests,
-    partition/leader counts; under-replicated / offline partitions are 0 on one node."""
+    partition/leader counts, under-replicated and offline partitions (from the cluster
+    state: non-zero while a node is down / a partition has no live leader)."""
 
-    def __init__(self, server: "KafkaLiteServer"):
+    def __init__(self, cluster: ClusterState):
         from prometheus_client import CollectorRegistry, Counter
         from prometheus_client.core import GaugeMetricFamily
         self.registry = CollectorRegistry()
@@ -69,15 +139,16 @@ class BrokerMetrics:
         self.bytes_out = mk("bytesout", "bytes fetched")
         self.failed_produce = mk("failedproducerequests", "failed produce requests")
         self.failed_fetch = mk("failedfetchrequests", "failed fetch requests")
-        srv = server
+        cl = cluster
 
         class _Gauges:
             def collect(self_):
-                parts = sum(srv.store.partitions(t) for t in srv.store.topics())
-                for name, v in (("kafka_server_replicamanager_partitioncount", parts),
-                                ("kafka_server_replicamanager_leadercount", parts),
-                                ("kafka_server_replicamanager_underreplicatedpartitions", 0),
-                                ("kafka_controller_kafkacontroller_offlinepartitionscount", 0)):
+                for name, v in (("kafka_server_replicamanager_partitioncount", cl.partition_count()),
+                                ("kafka_server_replicamanager_leadercount",
+                                 cl.partition_count() - cl.offline()),
+                                ("kafka_server_replicamanager_underreplicatedpartitions", cl.under_replicated()),
+                                ("kafka_controller_kafkacontroller_offlinepartitionscount", cl.offline()),
+                                ("kafka_controller_kafkacontroller_activebrokercount", len(cl.live()))):
                     g = GaugeMetricFamily(name, name, labels=["strimzi_io_kind"])
                     g.add_metric(["Kafka"], v)
                     yield g
@@ -89,24 +160,33 @@ class BrokerMetrics:
 
 
 class KafkaLiteServer:
+    """One broker listener.  Alone it is a one-node cluster; ``KafkaLiteCluster`` builds
+    several over a shared store / cluster state / metrics."""
+
     def __init__(self, host: str = "127.0.0.1", port: int = 9092, default_partitions: int = 1,
-                 store: Optional[InProcBroker] = None, auto_create: bool = True):
+                 store: Optional[BatchStore] = None, auto_create: bool = True, node_id: int = NODE_ID,
+                 cluster: Optional[ClusterState] = None, metrics: Optional[BrokerMetrics] = None):
         self.host = host
         self.port = port
-        self.store = store or InProcBroker(default_partitions=default_partitions)
+        self.store = store or BatchStore(default_partitions=default_partitions)
         self.auto_create = auto_create
+        self.node_id = node_id
+        self.cluster = cluster or ClusterState(self.store)
+        self.cluster.nodes.setdefault(node_id, [host, port, True])
         self._server: Optional[asyncio.base_events.Server] = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._thread: Optional[threading.Thread] = None
-        self.metrics = BrokerMetrics(self)
-        self.groups: Dict[str, _Group] = {}
-        self._mid = itertools.count(1)
+        self.metrics = metrics or BrokerMetrics(self.cluster)
+        self.groups = self.cluster.groups
+        self._mid = self.cluster.mid
         self._reaper: Optional[asyncio.Task] = None
+        self._writers: Set[asyncio.StreamWriter] = set()
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
         self._server = await asyncio.start_server(self._serve, self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
+        self.cluster.nodes[self.node_id] = [self.host, self.port, True]
         self._reaper = asyncio.get_running_loop().create_task(self._reap_sessions())
 
     def start_in_thread(self) -> "KafkaLiteServer":
@@ -121,6 +201,15 @@ class KafkaLiteServer:
         self._thread.start()
         ready.wait(10)
         return self
+
+    async def close_listener(self):
+        """Stop accepting and drop every open connection (a broker crash, seen from clients)."""
+        if self._server is not None:
+            self._server.close()
+        if self._reaper is not None:
+            self._reaper.cancel()
+        for w in list(self._writers):
+            w.close()
 
     def stop(self):
         if self._loop is not None:
@@ -141,6 +230,7 @@ class KafkaLiteServer:
 
     # ------------------------------------------------------------------ connection loop
     async def _serve(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
+        self._writers.add(writer)
         try:
             while True:
                 hdr = await reader.readexactly(4)
@@ -158,6 +248,7 @@ class KafkaLiteServer:
         except (asyncio.IncompleteReadError, ConnectionError):
             pass
         finally:
+            self._writers.discard(writer)
             writer.close()
 
     def _topic(self, name: str) -> bool:
@@ -173,6 +264,14 @@ class KafkaLiteServer:
             return Writer().i16(ERR_UNSUPPORTED_VERSION).build()
         return getattr(self, f"_api_{api}")(r)
 
+    def _partition_error(self, topic: str, p: int) -> int:
+        """ERR_NONE when this node leads an existing partition."""
+        if topic not in self.store.topics() or not 0 <= p < self.store.partitions(topic):
+            return ERR_UNKNOWN_TOPIC
+        if self.cluster.leader(topic, p) != self.node_id:
+            return ERR_NOT_LEADER
+        return ERR_NONE
+
     # ------------------------------------------------------------------ APIs
     def _api_18(self, r: Reader) -> bytes:                  # ApiVersions v0
         return Writer().i16(ERR_NONE).array(sorted(SUPPORTED.items()), lambda w, kv: w.i16(kv[0]).i16(0).i16(kv[1])).build()
@@ -180,17 +279,24 @@ class KafkaLiteServer:
     def _api_3(self, r: Reader) -> bytes:                   # Metadata v1
         topics = r.array(lambda x: x.string())
         names = sorted(self.store.topics()) if topics is None else topics
-        w = Writer().array([(NODE_ID, self.host, self.port)], lambda w_, b: w_.i32(b[0]).string(b[1]).i32(b[2]).string(None))
-        w.i32(NODE_ID)
+        cl = self.cluster
+        live = cl.live()
+        w = Writer().array([(n, cl.nodes[n][0], cl.nodes[n][1]) for n in live],
+                           lambda w_, b: w_.i32(b[0]).string(b[1]).i32(b[2]).string(None))
+        w.i32(live[0] if live else -1)                      # controller id
+        replicas = sorted(cl.nodes)
 
         def topic(w_, name):
             if not self._topic(name):
                 w_.i16(ERR_UNKNOWN_TOPIC).string(name).i8(0).array([], None)
                 return
             n = self.store.partitions(name)
-            w_.i16(ERR_NONE).string(name).i8(0).array(range(n), lambda w2, p: w2.i16(0).i32(p).i32(NODE_ID)
-                                                   .array([NODE_ID], lambda w3, x: w3.i32(x))
-                                                   .array([NODE_ID], lambda w3, x: w3.i32(x)))
+
+            def part(w2, p):
+                lead = cl.leader(name, p)
+                w2.i16(ERR_NONE if lead >= 0 else 5).i32(p).i32(lead)
+                w2.array(replicas, lambda w3, x: w3.i32(x)).array(live, lambda w3, x: w3.i32(x))
+            w_.i16(ERR_NONE).string(name).i8(0).array(range(n), part)
         w.array(names, topic)
         return w.build()
 
@@ -211,7 +317,7 @@ class KafkaLiteServer:
                 res.append((name, ERR_NONE))
         return Writer().array(res, lambda w, t: w.string(t[0]).i16(t[1])).build()
 
-    def _api_0(self, r: Reader) -> bytes:                   # Produce v3
+    def _api_0(self, r: Reader) -> bytes:                   # Produce v3: batches stored verbatim
         r.string(); r.i16(); r.i32()
         data = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.bytes_()))))
         resp = []
@@ -219,30 +325,34 @@ class KafkaLiteServer:
             pr = []
             self._topic(topic)
             for p, rb in parts:
+                err = self._partition_error(topic, p)
+                if err:
+                    pr.append((p, err, -1))
+                    self.metrics.failed_produce.labels(topic, "Kafka").inc()
+                    continue
                 try:
-                    recs = decode_record_batches(rb or b"", topic, p)
-                    base = self.store.end_offset(topic, p)
-                    for rec in recs:
-                        self.store.produce(topic, rec.value, key=rec.key, partition=p)
+                    base, nrec = self.store.append_raw(topic, p, rb or b"")
                     pr.append((p, ERR_NONE, base))
-                    self.metrics.messages_in.labels(topic, "Kafka").inc(len(recs))
+                    self.metrics.messages_in.labels(topic, "Kafka").inc(nrec)
                     self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
-                except Exception:
-                    pr.append((p, 2, -1))
+                except InvalidBatch:
+                    pr.append((p, ERR_CORRUPT, -1))
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
             resp.append((topic, pr))
         w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
         return w.i32(0).build()
 
-    def _api_1(self, r: Reader) -> bytes:                   # Fetch v4
+    def _api_1(self, r: Reader) -> bytes:                   # Fetch v4: stored batches, sliced
         r.i32(); r.i32(); r.i32(); max_bytes = r.i32(); r.i8()
         reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.i32()))))
         resp = []
+        budget = max_bytes
         for topic, parts in reqs:
             pr = []
             for p, off, pmax in parts:
-                if topic not in self.store.topics() or p >= self.store.partitions(topic):
-                    pr.append((p, ERR_UNKNOWN_TOPIC, -1, None))
+                err = self._partition_error(topic, p)
+                if err:
+                    pr.append((p, err, -1, None))
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     continue
                 hw = self.store.end_offset(topic, p)
@@ -250,13 +360,8 @@ class KafkaLiteServer:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     continue
-                recs, size = [], 0
-                for rec in self.store.fetch(topic, p, off, 100_000):
-                    size += len(rec.value or b"") + 32
-                    if recs and size > min(pmax, max_bytes):
-                        break
-                    recs.append(rec)
-                rb = encode_record_batch([x.value for x in recs], [x.key for x in recs], base_offset=off) if recs else b""
+                rb = self.store.fetch_raw(topic, p, off, max(1, min(pmax, budget))) if budget > 0 else b""
+                budget -= len(rb)
                 pr.append((p, ERR_NONE, hw, rb))
                 if rb:
                     self.metrics.bytes_out.labels(topic, "Kafka").inc(len(rb))
@@ -273,8 +378,10 @@ class KafkaLiteServer:
         for topic, parts in reqs:
             pr = []
             for p, ts in parts:
-                if not self._topic(topic) or p >= self.store.partitions(topic):
-                    pr.append((p, ERR_UNKNOWN_TOPIC, -1))
+                self._topic(topic)
+                err = self._partition_error(topic, p)
+                if err:
+                    pr.append((p, err, -1))
                     continue
                 off = self.store.begin_offset(topic, p) if ts == -2 else self.store.end_offset(topic, p)
                 pr.append((p, ERR_NONE, off))
@@ -284,7 +391,10 @@ class KafkaLiteServer:
 
     def _api_10(self, r: Reader) -> bytes:                  # FindCoordinator v0
         r.string()
-        return Writer().i16(ERR_NONE).i32(NODE_ID).string(self.host).i32(self.port).build()
+        live = self.cluster.live()
+        node = live[0] if live else self.node_id             # group state is shared: any node works
+        host, port, _ = self.cluster.nodes[node]
+        return Writer().i16(ERR_NONE).i32(node).string(host).i32(port).build()
 
     def _api_8(self, r: Reader) -> bytes:                   # OffsetCommit v2
         group = r.string(); r.i32(); r.string(); r.i64()
@@ -308,7 +418,6 @@ class KafkaLiteServer:
             resp.append((topic, pr))
         return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
             t[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).string(None).i16(ERR_NONE))).build()
-
 
     # ------------------------------------------------------------------ group coordinator
     # JoinGroup v1 / SyncGroup v0 / Heartbeat v0 / LeaveGroup v0 (client: ingest/kafka_group.py)
@@ -444,26 +553,99 @@ class KafkaLiteServer:
         self._remove_member(g, mid)
         return Writer().i16(ERR_NONE).build()
 
+
+class KafkaLiteCluster:
+    """``n`` broker listeners (node ids 1..n, ports ``base_port + i`` or ephemeral) on one
+    event loop over a shared store: leadership p -> node (p % n) + 1 until moved."""
+
+    def __init__(self, n: int = 3, host: str = "127.0.0.1", base_port: int = 0, default_partitions: int = 1,
+                 auto_create: bool = True):
+        self.store = BatchStore(default_partitions=default_partitions)
+        self.state = ClusterState(self.store)
+        self.metrics = BrokerMetrics(self.state)
+        self.nodes = [KafkaLiteServer(host, base_port + i if base_port else 0, store=self.store,
+                                      auto_create=auto_create, node_id=i + 1, cluster=self.state,
+                                      metrics=self.metrics) for i in range(n)]
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._thread: Optional[threading.Thread] = None
+
+    async def start(self):
+        for s in self.nodes:
+            await s.start()
+
+    def start_in_thread(self) -> "KafkaLiteCluster":
+        ready = threading.Event()
+
+        def run():
+            self._loop = asyncio.new_event_loop()
+            for s in self.nodes:
+                s._loop = self._loop
+            self._loop.run_until_complete(self.start())
+            ready.set()
+            self._loop.run_forever()
+        self._thread = threading.Thread(target=run, daemon=True, name="kafka-lite-cluster")
+        self._thread.start()
+        ready.wait(10)
+        return self
+
+    @property
+    def bootstrap(self) -> str:
+        return self.nodes[0].bootstrap
+
+    @property
+    def bootstrap_all(self) -> str:
+        return ",".join(s.bootstrap for s in self.nodes)
+
+    def leader(self, topic: str, partition: int) -> int:
+        return self.state.leader(topic, partition)
+
+    def move_leader(self, topic: str, partition: int, node: int) -> None:
+        self.state.move_leader(topic, partition, node)
+
+    def fail_node(self, node: int) -> None:
+        """Close broker ``node`` (listener + open connections) and fail its partitions over."""
+        self.state.fail_node(node)
+        srv = self.nodes[node - 1]
+        if self._loop is not None:
+            asyncio.run_coroutine_threadsafe(srv.close_listener(), self._loop).result(5)
+
+    def stop(self):
+        if self._loop is not None:
+            async def _shutdown():
+                for s in self.nodes:
+                    if s._server is not None:
+                        s._server.close()
+                me = asyncio.current_task()
+                tasks = [t for t in asyncio.all_tasks() if t is not me]
+                for t in tasks:
+                    t.cancel()
+                await asyncio.gather(*tasks, return_exceptions=True)
+                self._loop.stop()
+            asyncio.run_coroutine_threadsafe(_shutdown(), self._loop)
+            self._thread.join(5)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default="0.0.0.0")
-    ap.add_argument("--port", type=int, default=9092)
+    ap.add_argument("--port", type=int, default=9092, help="first node's port (node i listens on port + i)")
     ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--nodes", type=int, default=1, help="broker listeners (leadership spread over them)")
     ap.add_argument("--metrics-port", type=int, default=9404, help="Prometheus /metrics (0 = off)")
     a = ap.parse_args(argv)
-    srv = KafkaLiteServer(a.host, a.port, a.partitions)
+    cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions)
 
     async def run():
-        await srv.start()
+        await cl.start()
         if a.metrics_port:
             from aiohttp import web
             app = web.Application()
             app.router.add_get("/metrics", lambda _r: web.Response(
-                body=srv.metrics.expose(), headers={"Content-Type": "text/plain; version=0.0.4"}))
+                body=cl.metrics.expose(), headers={"Content-Type": "text/plain; version=0.0.4"}))
             runner = web.AppRunner(app)
             await runner.setup()
             await web.TCPSite(runner, a.host, a.metrics_port).start()
-        print(f"[kafka-lite] listening on {a.host}:{srv.port}", flush=True)
+        print(f"[kafka-lite] {a.nodes} node(s) listening on {cl.bootstrap_all}", flush=True)
         await asyncio.Event().wait()
     asyncio.run(run())
 

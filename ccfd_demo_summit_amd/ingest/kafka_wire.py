@@ -8,11 +8,16 @@ client in this image, so the framework speaks the protocol itself:
   OffsetCommit v2, OffsetFetch v1, CreateTopics v0   (all non-flexible encodings)
 
 Records use RecordBatch v2 (magic 2) with CRC-32C computed by the native library
-(csrc/engine/crc32c.cpp, SSE4.2) or a table fallback.  ``KafkaBroker`` exposes the same
-interface as ``InProcBroker`` (produce / fetch / offsets / commit / consumer), so every
-service runs unchanged against either.  Consumers use static partition assignment (the
-engine's ``p % world == rank`` sharding) and commit offsets under their group id;
-the group-membership rebalance protocol (JoinGroup/SyncGroup) is not implemented.
+(csrc/engine/crc32c.cpp, SSE4.2) or a table fallback; gzip-compressed batches (codec 1)
+are decoded and can be produced, other codecs are refused explicitly.  ``KafkaBroker``
+exposes the same interface as ``InProcBroker`` (produce / fetch / offsets / commit /
+consumer), so every service runs unchanged against either.  It takes a comma-separated
+bootstrap list, routes Produce / Fetch / ListOffsets to each partition's leader from
+Metadata, and on NOT_LEADER / UNKNOWN_TOPIC_OR_PARTITION / LEADER_NOT_AVAILABLE or a dead
+connection refreshes metadata and retries (leader moves and broker failover); offsets are
+committed to the group coordinator (FindCoordinator).  Static consumers (``consumer``) use
+the engine's ``p % world == rank`` sharding; group membership (JoinGroup / SyncGroup /
+Heartbeat) lives in ``kafka_group.py``.
 """
 from __future__ import annotations
 
@@ -35,6 +40,8 @@ SUPPORTED = {PRODUCE: 3, FETCH: 4, LIST_OFFSETS: 1, METADATA: 1, OFFSET_COMMIT: 
              JOIN_GROUP: 1, HEARTBEAT: 0, LEAVE_GROUP: 0, SYNC_GROUP: 0}
 
 ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_UNKNOWN_TOPIC, ERR_CORRUPT = 0, 1, 3, 2
+ERR_LEADER_NOT_AVAILABLE, ERR_NOT_LEADER, ERR_NOT_COORDINATOR = 5, 6, 16
+RETRIABLE = (ERR_UNKNOWN_TOPIC, ERR_LEADER_NOT_AVAILABLE, ERR_NOT_LEADER, ERR_NOT_COORDINATOR)
 ERR_UNSUPPORTED_VERSION, ERR_TOPIC_EXISTS, ERR_INVALID_REQUEST = 35, 36, 42
 
 # --------------------------------------------------------------------------- crc32c
@@ -199,8 +206,13 @@ def _read_varint(mv, o: int) -> Tuple[int, int]:
 
 
 # --------------------------------------------------------------------------- RecordBatch v2
+CODEC_NONE, CODEC_GZIP = 0, 1
+_CODEC_NAMES = {1: "gzip", 2: "snappy", 3: "lz4", 4: "zstd"}
+
+
 def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optional[bytes]]] = None,
-                        base_offset: int = 0, timestamp_ms: Optional[int] = None) -> bytes:
+                        base_offset: int = 0, timestamp_ms: Optional[int] = None,
+                        compression: int = CODEC_NONE) -> bytes:
     ts = int(time.time() * 1000) if timestamp_ms is None else timestamp_ms
     recs = []
     for i, v in enumerate(values):
@@ -210,7 +222,13 @@ def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optiona
                          _varint(-1) if v is None else _varint(len(v)) + bytes(v), _varint(0)])
         recs.append(_varint(len(body)) + body)
     n = len(values)
-    after_crc = struct.pack(">hiqqqhii", 0, max(n - 1, 0), ts, ts, -1, -1, -1, n) + b"".join(recs)
+    records = b"".join(recs)
+    if compression == CODEC_GZIP:
+        import gzip
+        records = gzip.compress(records, compresslevel=1)
+    elif compression != CODEC_NONE:
+        raise BrokerError(f"unsupported compression codec {compression}")
+    after_crc = struct.pack(">hiqqqhii", compression, max(n - 1, 0), ts, ts, -1, -1, -1, n) + records
     crc = crc32c(after_crc)
     head = struct.pack(">ibI", 0, 2, crc)                 # partitionLeaderEpoch, magic, crc
     batch_len = len(head) + len(after_crc)
@@ -234,10 +252,15 @@ def decode_record_batches(data: bytes, topic: str = "", partition: int = 0,
         if verify_crc and crc32c(bytes(body)) != crc:
             raise BrokerError("record batch CRC mismatch")
         (attrs, _lod, base_ts, _max_ts, _pid, _pep, _bseq, count) = struct.unpack_from(">hiqqqhii", body, 0)
-        if attrs & 0x7:
-            raise BrokerError("compressed record batches are not supported")
-        p = 40 + 21   # header bytes before records, relative to o
-        q = o + p
+        codec = attrs & 0x7
+        q = o + 61                                         # first record
+        rmv = mv
+        if codec == CODEC_GZIP:
+            rmv = memoryview(zlib.decompress(bytes(mv[q:end]), 47))   # gzip or zlib header
+            q = 0
+        elif codec:
+            raise BrokerError(f"unsupported compression codec {_CODEC_NAMES.get(codec, codec)}")
+        mv_outer, mv = mv, rmv
         for _ in range(count):
             ln, q = _read_varint(mv, q)
             rend = q + ln
@@ -251,6 +274,7 @@ def decode_record_batches(data: bytes, topic: str = "", partition: int = 0,
             val = None if vl < 0 else bytes(mv[q:q + vl])
             q = rend
             out.append(Record(topic, partition, base_offset + od, key, val, (base_ts + tsd) / 1000.0))
+        mv = mv_outer
         o = end
     return out
 
@@ -312,25 +336,52 @@ class Connection:
 
 # --------------------------------------------------------------------------- client
 class KafkaBroker:
-    """Kafka-protocol implementation of the InProcBroker interface (single bootstrap node;
-    partition leaders are looked up from Metadata and connected lazily)."""
+    """Kafka-protocol implementation of the InProcBroker interface.  ``bootstrap`` is
+    ``host:port[,host:port...]``; partition leaders come from Metadata and are connected
+    lazily; leader moves and broker failures are recovered by refresh + retry."""
+
+    RETRIES = 8
 
     def __init__(self, bootstrap: str, client_id: str = "ccfd-mi355x", timeout: float = 10.0,
-                 connect_wait_s: float = 0.0):
-        host, port = bootstrap.rsplit(":", 1)
+                 connect_wait_s: float = 0.0, compression: int = CODEC_NONE):
         self.timeout = timeout
         self.client_id = client_id
-        self._bootstrap = (host, int(port))
+        self.compression = compression
+        self._seeds = [(h, int(pt)) for h, pt in (x.strip().rsplit(":", 1) for x in bootstrap.split(",") if x.strip())]
+        self._bootstrap = self._seeds[0]
         self._conns: Dict[int, Connection] = {}
         self._nodes: Dict[int, Tuple[str, int]] = {}
         self._leaders: Dict[Tuple[str, int], int] = {}
         self._partitions: Dict[str, int] = {}
-        self._boot = Connection(host, int(port), client_id, timeout, connect_wait_s=connect_wait_s)
+        self._coord: Dict[str, int] = {}
+        self._boot = self._connect_any(connect_wait_s)
         self._rr = itertools.count()
+        self.retries_done = 0                               # refresh-and-retry count (tests, metrics)
         self.api_versions = self._api_versions()
 
+    def _connect_any(self, wait_s: float = 0.0) -> Connection:
+        cands = self._seeds + [a for a in self._nodes.values() if a not in self._seeds]
+        deadline = time.monotonic() + wait_s
+        while True:
+            for host, port in cands:
+                try:
+                    return Connection(host, port, self.client_id, self.timeout)
+                except OSError:
+                    continue
+            if time.monotonic() >= deadline:
+                raise BrokerError(f"no reachable broker in {cands}")
+            time.sleep(0.25)
+
+    def _boot_request(self, api: int, ver: int, body: bytes) -> Reader:
+        try:
+            return self._boot.request(api, ver, body)
+        except (OSError, ConnectionError):
+            self._boot.close()
+            self._boot = self._connect_any(self.timeout)
+            return self._boot.request(api, ver, body)
+
     def _api_versions(self) -> Dict[int, Tuple[int, int]]:
-        r = self._boot.request(API_VERSIONS, 0, b"")
+        r = self._boot_request(API_VERSIONS, 0, b"")
         err = r.i16()
         if err:
             raise BrokerError(f"ApiVersions error {err}")
@@ -338,19 +389,25 @@ class KafkaBroker:
 
     def _conn(self, node: int) -> Connection:
         if node not in self._conns:
-            host, port = self._nodes.get(node, self._bootstrap)
-            try:
-                self._conns[node] = Connection(host, port, self.client_id, self.timeout)
-            except OSError:
-                self._conns[node] = Connection(*self._bootstrap, self.client_id, self.timeout)
+            if node not in self._nodes:
+                raise BrokerError(f"unknown broker node {node}")
+            self._conns[node] = Connection(*self._nodes[node], self.client_id, self.timeout)
         return self._conns[node]
+
+    def _drop(self, node: int) -> None:
+        c = self._conns.pop(node, None)
+        if c is not None:
+            c.close()
 
     def metadata(self, topics: Optional[Sequence[str]] = None) -> Dict[str, int]:
         body = Writer().array(topics, lambda w, t: w.string(t)).build()
-        r = self._boot.request(METADATA, 1, body)
+        r = self._boot_request(METADATA, 1, body)
         brokers = r.array(lambda x: (x.i32(), x.string(), x.i32(), x.string()))
-        for nid, host, port, _rack in brokers:
-            self._nodes[nid] = (host, port)
+        nodes = {nid: (host, port) for nid, host, port, _rack in brokers}
+        for nid in list(self._conns):
+            if nodes.get(nid) != self._nodes.get(nid):
+                self._drop(nid)                             # broker gone or moved
+        self._nodes = nodes
         r.i32()                                             # controller id
 
         def part(x):
@@ -370,7 +427,7 @@ class KafkaBroker:
             return
         body = (Writer().array([name], lambda w, t: w.string(t).i32(partitions or 1).i16(1)
                                .array([], None).array([], None)).i32(int(self.timeout * 1000)).build())
-        r = self._boot.request(CREATE_TOPICS, 0, body)
+        r = self._boot_request(CREATE_TOPICS, 0, body)
         for tname, err in r.array(lambda x: (x.string(), x.i16())):
             if err not in (ERR_NONE, ERR_TOPIC_EXISTS):
                 raise BrokerError(f"CreateTopics {tname}: error {err}")
@@ -383,25 +440,55 @@ class KafkaBroker:
             self.create_topic(topic)
         return self._partitions[topic]
 
-    def _leader(self, topic: str, partition: int) -> Connection:
+    def leader_of(self, topic: str, partition: int) -> int:
         if (topic, partition) not in self._leaders:
             self.metadata([topic])
-        return self._conn(self._leaders.get((topic, partition), -1))
+        return self._leaders.get((topic, partition), -1)
+
+    def _on_leader(self, topic: str, partition: int, api: int, ver: int, body: bytes, parse):
+        """Send to the partition leader; ``parse(reader) -> (error code, result)``.  Retriable
+        errors and dead connections refresh metadata and retry with back-off."""
+        last = None
+        for attempt in range(self.RETRIES):
+            node = self.leader_of(topic, partition)
+            try:
+                if node < 0:
+                    raise BrokerError(f"{topic}[{partition}] has no leader")
+                err, res = parse(self._conn(node).request(api, ver, body))
+            except (OSError, ConnectionError, BrokerError) as e:
+                last = e
+                self._drop(node)
+                err = ERR_LEADER_NOT_AVAILABLE
+            if err not in RETRIABLE:
+                if err:
+                    raise BrokerError(f"{topic}[{partition}] api {api} error {err}")
+                return res
+            self.retries_done += 1
+            self._leaders.pop((topic, partition), None)
+            time.sleep(min(0.5, 0.01 * (2 ** attempt)))
+            try:
+                self.metadata([topic])
+            except (OSError, ConnectionError, BrokerError) as e:
+                last = e
+        raise BrokerError(f"{topic}[{partition}]: leader not reachable after {self.RETRIES} tries ({last})")
 
     # ---------------------------------------------------------------- produce
     def produce_batch(self, topic: str, partition: int, values: Sequence[bytes],
                       keys: Optional[Sequence[Optional[bytes]]] = None, acks: int = 1) -> int:
-        rb = encode_record_batch(values, keys)
+        rb = encode_record_batch(values, keys, compression=self.compression)
+        return self.produce_raw(topic, partition, rb, acks)
+
+    def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
+        """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
         body = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000))
-                .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).bytes_(rb)))
+                .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).bytes_(record_set)))
                 .build())
-        r = self._leader(topic, partition).request(PRODUCE, 3, body)
-        resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
-        _name, parts = resp[0]
-        _p, err, base, _ts = parts[0]
-        if err:
-            raise BrokerError(f"produce {topic}[{partition}] error {err}")
-        return base
+
+        def parse(r):
+            resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+            _p, err, base, _ts = resp[0][1][0]
+            return err, base
+        return self._on_leader(topic, partition, PRODUCE, 3, body, parse)
 
     def produce(self, topic: str, value: bytes, key: Optional[bytes] = None, partition: Optional[int] = None,
                 headers: Tuple = ()) -> Tuple[int, int]:
@@ -424,38 +511,44 @@ class KafkaBroker:
         return len(vals)
 
     # ---------------------------------------------------------------- fetch / offsets
-    def fetch(self, topic: str, partition: int, offset: int, max_records: int = 1000,
-              max_bytes: int = 64 << 20, max_wait_ms: int = 0) -> List[Record]:
+    def fetch_raw(self, topic: str, partition: int, offset: int, max_bytes: int = 64 << 20,
+                  max_wait_ms: int = 0) -> Tuple[int, int, bytes]:
+        """(error, high watermark, record set bytes) from the leader; retriable errors are
+        retried, OFFSET_OUT_OF_RANGE is returned to the caller."""
         body = (Writer().i32(-1).i32(max_wait_ms).i32(1 if max_wait_ms else 0).i32(max_bytes).i8(0)
                 .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).i64(offset).i32(max_bytes)))
                 .build())
-        r = self._leader(topic, partition).request(FETCH, 4, body)
-        r.i32()                                             # throttle
 
-        def part(x):
-            idx, err, hw, _lso = x.i32(), x.i16(), x.i64(), x.i64()
-            x.array(lambda y: (y.i64(), y.i64()))
-            return idx, err, hw, x.bytes_()
-        resp = r.array(lambda x: (x.string(), x.array(part)))
-        out: List[Record] = []
-        for _t, parts in resp:
-            for idx, err, _hw, recs in parts:
-                if err == ERR_OFFSET_OUT_OF_RANGE:
-                    return self.fetch(topic, partition, self.begin_offset(topic, partition), max_records, max_bytes)
-                if err:
-                    raise BrokerError(f"fetch {topic}[{idx}] error {err}")
-                if recs:
-                    out.extend(r_ for r_ in decode_record_batches(recs, topic, idx) if r_.offset >= offset)
+        def parse(r):
+            r.i32()                                         # throttle
+
+            def part(x):
+                idx, err, hw, _lso = x.i32(), x.i16(), x.i64(), x.i64()
+                x.array(lambda y: (y.i64(), y.i64()))
+                return idx, err, hw, x.bytes_()
+            _t, parts = r.array(lambda x: (x.string(), x.array(part)))[0]
+            _idx, err, hw, recs = parts[0]
+            if err == ERR_OFFSET_OUT_OF_RANGE:
+                return ERR_NONE, (err, hw, b"")
+            return err, (err, hw, recs or b"")
+        return self._on_leader(topic, partition, FETCH, 4, body, parse)
+
+    def fetch(self, topic: str, partition: int, offset: int, max_records: int = 1000,
+              max_bytes: int = 64 << 20, max_wait_ms: int = 0) -> List[Record]:
+        err, _hw, recs = self.fetch_raw(topic, partition, offset, max_bytes, max_wait_ms)
+        if err == ERR_OFFSET_OUT_OF_RANGE:
+            return self.fetch(topic, partition, self.begin_offset(topic, partition), max_records, max_bytes)
+        out = [r_ for r_ in decode_record_batches(recs, topic, partition) if r_.offset >= offset] if recs else []
         return out[:max_records]
 
     def _list_offset(self, topic: str, partition: int, ts: int) -> int:
         body = Writer().i32(-1).array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).i64(ts))).build()
-        r = self._leader(topic, partition).request(LIST_OFFSETS, 1, body)
-        resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
-        _p, err, _ts, off = resp[0][1][0]
-        if err:
-            raise BrokerError(f"list offsets {topic}[{partition}] error {err}")
-        return off
+
+        def parse(r):
+            resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+            _p, err, _ts, off = resp[0][1][0]
+            return err, off
+        return self._on_leader(topic, partition, LIST_OFFSETS, 1, body, parse)
 
     def end_offset(self, topic: str, partition: int) -> int:
         return self._list_offset(topic, partition, -1)
@@ -463,19 +556,43 @@ class KafkaBroker:
     def begin_offset(self, topic: str, partition: int) -> int:
         return self._list_offset(topic, partition, -2)
 
+    def _coordinator(self, group: str) -> Connection:
+        if group not in self._coord:
+            r = self._boot_request(FIND_COORDINATOR, 0, Writer().string(group).build())
+            err, node, host, port = r.i16(), r.i32(), r.string(), r.i32()
+            if err:
+                raise BrokerError(f"FindCoordinator {group}: error {err}")
+            self._nodes.setdefault(node, (host, port))
+            self._coord[group] = node
+        return self._conn(self._coord[group])
+
+    def _on_coordinator(self, group: str, api: int, ver: int, body: bytes) -> Reader:
+        for attempt in range(self.RETRIES):
+            try:
+                return self._coordinator(group).request(api, ver, body)
+            except (OSError, ConnectionError) as e:
+                node = self._coord.pop(group, None)
+                if node is not None:
+                    self._drop(node)
+                self.retries_done += 1
+                time.sleep(min(0.5, 0.01 * (2 ** attempt)))
+                last = e
+        raise BrokerError(f"group {group}: coordinator not reachable ({last})")
+
     def commit(self, group: str, topic: str, partition: int, offset: int) -> None:
         body = (Writer().string(group).i32(-1).string("").i64(-1)
                 .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).i64(offset).string(None)))
                 .build())
-        r = self._boot.request(OFFSET_COMMIT, 2, body)
+        r = self._on_coordinator(group, OFFSET_COMMIT, 2, body)
         for _t, parts in r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16())))):
             for p, err in parts:
                 if err:
+                    self._coord.pop(group, None)
                     raise BrokerError(f"offset commit {topic}[{p}] error {err}")
 
     def committed(self, group: str, topic: str, partition: int) -> Optional[int]:
         body = Writer().string(group).array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p))).build()
-        r = self._boot.request(OFFSET_FETCH, 1, body)
+        r = self._on_coordinator(group, OFFSET_FETCH, 1, body)
         resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.string(), y.i16()))))
         _p, off, _meta, err = resp[0][1][0]
         return None if off < 0 else off

@@ -1,9 +1,12 @@
 """Python handle of the native Kafka consumer (csrc/engine/kafka_consumer.cpp).
 
-A C++ thread fetches (Kafka Fetch v4 over one TCP connection), validates RecordBatch v2
-CRC-32C, and writes TXB1 batches / JSON transactions straight into the engine's pinned
-partition rings (f32 or W64 rows) -- no Python per message (SURVEY.md §2.4 H1, §7.3 hard
-part 1: JSON-per-transaction at 1M/s is out of reach for a Python consumer loop).
+A C++ thread looks up partition leaders (Metadata v1), keeps one connection per leader
+broker, fetches (Fetch v4) from all leaders in parallel, validates RecordBatch v2 CRC-32C
+(uncompressed or gzip), and writes TXB1 batches / JSON transactions straight into the
+engine's pinned partition rings (f32 or W64 rows) -- no Python per message (SURVEY.md §2.4
+H1, §7.3 hard part 1: JSON-per-transaction at 1M/s is out of reach for a Python consumer
+loop).  Leader moves / broker failures refresh metadata and continue from the same offset;
+OFFSET_OUT_OF_RANGE follows ``offset_reset`` (earliest / latest / none).
 
     kc = NativeKafkaConsumer.for_engine(engine, "127.0.0.1:9092", "odh-demo", {p: committed_offset})
     kc.start()
@@ -27,7 +30,11 @@ class KcPartition(C.Structure):
 
 class KcStats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("rows", C.c_uint64), ("bytes", C.c_uint64),
-                ("errors", C.c_uint64), ("fetches", C.c_uint64)]
+                ("errors", C.c_uint64), ("fetches", C.c_uint64), ("metadata_refreshes", C.c_uint64),
+                ("offset_resets", C.c_uint64), ("leaders", C.c_uint64)]
+
+
+RESET_POLICIES = {"earliest": 0, "latest": 1, "none": 2}
 
 
 def _bind(L):
@@ -51,13 +58,18 @@ def _bind(L):
     L.ccfd_kc_last_error.restype = C.c_char_p
     L.ccfd_kc_feed_record_set.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
     L.ccfd_kc_feed_record_set.restype = C.c_int64
+    L.ccfd_kc_set_offset_reset.argtypes = [C.c_void_p, C.c_int]
+    L.ccfd_kc_set_offset_reset.restype = C.c_int
+    L.ccfd_kc_position.argtypes = [C.c_void_p, C.c_int]
+    L.ccfd_kc_position.restype = C.c_int64
     L._kc_bound = True
     return L
 
 
 def _split(bootstrap: str):
-    host, _, port = bootstrap.split(",")[0].rpartition(":")
-    return (host or "127.0.0.1"), int(port or 9092)
+    """The native side takes the whole bootstrap list ("h1:p1,h2:p2"); ``port`` is the
+    default for entries without one."""
+    return bootstrap.strip(), 9092
 
 
 class NativeKafkaConsumer:
@@ -101,6 +113,15 @@ class NativeKafkaConsumer:
         kc = cls(h, ps, keep=(arr, bufs))
         kc.arrays = bufs
         return kc
+
+    def set_offset_reset(self, policy: str) -> "NativeKafkaConsumer":
+        """auto.offset.reset on OFFSET_OUT_OF_RANGE: earliest / latest / none (before start)."""
+        check(lib().ccfd_kc_set_offset_reset(C.c_void_p(self.h), RESET_POLICIES[policy]), "ccfd_kc_set_offset_reset")
+        return self
+
+    def position(self) -> Dict[int, int]:
+        """partition -> next offset the consumer will fetch."""
+        return {p: int(lib().ccfd_kc_position(C.c_void_p(self.h), i)) for i, p in enumerate(self.partitions)}
 
     def start(self) -> "NativeKafkaConsumer":
         lib().ccfd_kc_start(C.c_void_p(self.h))

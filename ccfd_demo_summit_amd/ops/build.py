@@ -86,7 +86,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True, sanitize: st
     if force or not LIB.exists() or LIB.stat().st_mtime < newest:
         tmp = LIB.with_suffix(".so.tmp")
         cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + \
-              [str(o) for o in objs] + ["-lpthread"] + ([f"-fsanitize={sanitize}", "-shared-libsan"] if sanitize else [])
+              [str(o) for o in objs] + ["-lpthread", "-lz"] + ([f"-fsanitize={sanitize}", "-shared-libsan"] if sanitize else [])
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

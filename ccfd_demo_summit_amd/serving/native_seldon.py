@@ -25,7 +25,7 @@ from ..ops._lib import lib
 _SCORE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_float), C.c_void_p)
 _RENDER_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_void_p)
 _NB = 32                                   # native latency buckets (+Inf)
-_STATUS = ("200", "400", "401")
+_STATUS = ("200", "400", "401", "500")
 
 
 def _bind():
@@ -92,13 +92,16 @@ class NativeSeldonServer:
 
     # ------------------------------------------------------------------ stats / metrics
     def stats(self) -> dict:
-        out = (C.c_uint64 * (3 + 3 + 3 + 4 + 3 * (_NB + 1)))()
+        ns = len(_STATUS)
+        out = (C.c_uint64 * (2 * ns + 3 + 4 + ns * (_NB + 1)))()
         _bind().ccfd_seldon_http_stats(self.h, out)
         v = list(out)
-        last = [struct.unpack("<f", struct.pack("<I", int(x) & 0xFFFFFFFF))[0] for x in v[9:13]]
-        hist = [v[13 + i * (_NB + 1): 13 + (i + 1) * (_NB + 1)] for i in range(3)]
-        return {"count": dict(zip(_STATUS, v[0:3])), "sum_s": dict(zip(_STATUS, [x * 1e-9 for x in v[3:6]])),
-                "rows": v[6], "batches": v[7], "model_s": v[8] * 1e-9,
+        b0 = 2 * ns + 3
+        last = [struct.unpack("<f", struct.pack("<I", int(x) & 0xFFFFFFFF))[0] for x in v[b0:b0 + 4]]
+        h0 = b0 + 4
+        hist = [v[h0 + i * (_NB + 1): h0 + (i + 1) * (_NB + 1)] for i in range(ns)]
+        return {"count": dict(zip(_STATUS, v[0:ns])), "sum_s": dict(zip(_STATUS, [x * 1e-9 for x in v[ns:2 * ns]])),
+                "rows": v[2 * ns], "batches": v[2 * ns + 1], "model_s": v[2 * ns + 2] * 1e-9,
                 "last": dict(zip(M.MODEL_GAUGES, last)), "hist": dict(zip(_STATUS, hist))}
 
     def expose(self) -> bytes:

@@ -70,9 +70,10 @@ bool skip_value(Cur& c) {
       return c.eat(close);
     }
   }
-  if (!std::strncmp(c.p, "true", 4) && c.e - c.p >= 4) { c.p += 4; return true; }
-  if (!std::strncmp(c.p, "false", 5) && c.e - c.p >= 5) { c.p += 5; return true; }
-  if (!std::strncmp(c.p, "null", 4) && c.e - c.p >= 4) { c.p += 4; return true; }
+  // length first: the input is not NUL-terminated
+  if (c.e - c.p >= 4 && !std::memcmp(c.p, "true", 4)) { c.p += 4; return true; }
+  if (c.e - c.p >= 5 && !std::memcmp(c.p, "false", 5)) { c.p += 5; return true; }
+  if (c.e - c.p >= 4 && !std::memcmp(c.p, "null", 4)) { c.p += 4; return true; }
   double d;
   return parse_number(c, &d);
 }
@@ -114,7 +115,15 @@ bool parse_one(const char* s, const char* e, float* f, uint64_t* id, uint32_t* c
       bool quoted = c.eat('"');
       if (!parse_number(c, &d)) return false;
       if (quoted && !c.eat('"')) return false;
-      if (col == -2) *id = (uint64_t)d; else *cust = (uint32_t)d;
+      // ids are non-negative integers: anything else (negative, NaN, beyond the type) is a
+      // malformed message, never an undefined float->int conversion
+      if (col == -2) {
+        if (!(d >= 0.0 && d < 18446744073709551616.0)) return false;
+        *id = (uint64_t)d;
+      } else {
+        if (!(d >= 0.0 && d < 4294967296.0)) return false;
+        *cust = (uint32_t)d;
+      }
     } else if (col == -4) {
       if (!c.eat('[')) return false;
       for (int k = 0; k < CCFD_N_FEATURES; ++k) {

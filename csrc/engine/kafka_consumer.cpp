@@ -1,29 +1,44 @@
-// Native Kafka consumer: Fetch v4 over one TCP connection -> RecordBatch v2 (CRC-32C
-// checked) -> rows written straight into the engine's pinned partition rings (SURVEY.md
-// §2.4 H1 "C++ Kafka ingest ... writes directly into ring slots").
+// Native Kafka consumer: Metadata v1 -> one TCP connection per partition leader ->
+// Fetch v4 -> RecordBatch v2 (CRC-32C checked; uncompressed or gzip) -> rows written
+// straight into the engine's pinned partition rings (SURVEY.md §2.4 H1 "C++ Kafka ingest ...
+// writes directly into ring slots").
 //
-// One consumer thread per rank serves that rank's partitions of one topic.  Each record
-// value is either a TXB1 columnar batch (contracts/transaction.py: ids, customers and f32
-// rows are copied / W64-encoded row-block by row-block) or one JSON transaction (parsed by
-// the native parser, ingest.cpp).  Offsets: after the rows of a record are committed to
-// the ring, (ring rows written, next offset) is queued; ccfd_kc_committable() returns the
-// highest offset whose rows the engine has already released (scored), so the caller
-// commits consumer-group offsets only for scored data (at-least-once).
+// One consumer thread per rank serves that rank's partitions of one topic.  Each round it
+// sends one Fetch to EVERY leader broker first and then reads the responses, so brokers
+// serve in parallel (the reference's consumers dial the 3-broker service,
+// deploy/router.yaml:55-56, deploy/frauddetection_cr.yaml:75-77).  Partition errors:
+//   NOT_LEADER_FOR_PARTITION / UNKNOWN_TOPIC_OR_PARTITION / LEADER_NOT_AVAILABLE /
+//   REPLICA_NOT_AVAILABLE, or a dead connection -> metadata refresh, reconnect, continue
+//   from the same offset (nothing skipped, nothing duplicated downstream);
+//   OFFSET_OUT_OF_RANGE -> ListOffsets reset per policy (earliest / latest / none = stop
+//   the partition and report);
+//   anything else -> counted and reported through ccfd_kc_last_error (never silently).
+// Each record value is either a TXB1 columnar batch (contracts/transaction.py: ids,
+// customers and f32 rows are copied / W64-encoded row-block by row-block) or one JSON
+// transaction (parsed by the native parser, ingest.cpp).  Offsets: after the rows of a
+// record are committed to the ring, (ring rows written, next offset) is queued;
+// ccfd_kc_committable() returns the highest offset whose rows the engine has already
+// released (scored), so the caller commits consumer-group offsets only for scored data
+// (at-least-once).
 //
 // Sinks: an engine ring (production) or a flat array (tests; no GPU needed).
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -123,55 +138,75 @@ struct PState {
   int32_t kafka_partition = 0;
   int64_t next_offset = 0;
   int64_t rows_in = 0;
+  int32_t leader = -1;          // broker node id (-1: unknown -> metadata refresh)
+  bool stopped = false;         // OFFSET_OUT_OF_RANGE under policy "none"
+  bool reset = false;           // OFFSET_OUT_OF_RANGE seen: ListOffsets before the next fetch
   std::deque<std::pair<int64_t, int64_t>> pending;   // (rows_in after record, next offset)
+};
+
+// Kafka error codes handled by the consumer
+constexpr int16_t kErrOffsetOutOfRange = 1, kErrUnknownTopicOrPartition = 3, kErrLeaderNotAvailable = 5,
+                  kErrNotLeader = 6, kErrReplicaNotAvailable = 9;
+
+struct Conn {                   // one broker connection
+  std::string host;
+  int port = 0;
+  int fd = -1;
+  int32_t corr = 0;
+  int32_t expect = 0;           // correlation id of the request in flight (0: none)
 };
 
 class Consumer {
  public:
-  std::string host, topic, client = "ccfd-native";
-  int port = 9092;
+  std::vector<std::pair<std::string, int>> seeds;   // bootstrap list
+  std::string topic, client = "ccfd-native";
   int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64
+  int reset_policy = CCFD_KC_RESET_EARLIEST;
   Sink* sink = nullptr;
   std::vector<PState> ps;
-  std::mutex mu;                // guards ps[*].pending / next_offset reads from other threads
+  std::mutex mu;                // guards ps[*].pending / next_offset / last_err reads from other threads
   std::atomic<bool> stop{false};
   std::atomic<uint64_t> n_records{0}, n_rows{0}, n_bytes{0}, n_errors{0}, n_fetches{0};
+  std::atomic<uint64_t> n_meta{0}, n_resets{0}, n_leaders{0};
   std::thread th;
-  int fd = -1;
-  int32_t corr = 0;
+  std::map<int32_t, Conn> brokers;                  // node id -> connection
+  bool meta_stale = true;
   int max_wait_ms = 5;
   std::string last_err;
+  std::vector<uint8_t> inflated;                    // gzip scratch (consumer thread only)
 
   ~Consumer() {
     stop.store(true);
     if (th.joinable()) th.join();
-    if (fd >= 0) ::close(fd);
+    for (auto& kv : brokers) if (kv.second.fd >= 0) ::close(kv.second.fd);
     delete sink;
   }
 
-  bool connect_broker() {
+  void error(const std::string& e) {
+    n_errors.fetch_add(1);
+    std::lock_guard<std::mutex> lk(mu);
+    last_err = e;
+  }
+
+  static int dial(const std::string& host, int port) {
     addrinfo hints{}, *res = nullptr;
     hints.ai_family = AF_INET;
     hints.ai_socktype = SOCK_STREAM;
-    if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res) {
-      last_err = "resolve " + host;
-      return false;
-    }
-    fd = ::socket(res->ai_family, res->ai_socktype, res->ai_protocol);
-    if (fd < 0 || ::connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
-      freeaddrinfo(res);
-      last_err = "connect " + host + ":" + std::to_string(port);
-      return false;
-    }
+    if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res) return -1;
+    int fd = ::socket(res->ai_family, res->ai_socktype, res->ai_protocol);
+    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) != 0) { ::close(fd); fd = -1; }
     freeaddrinfo(res);
+    if (fd < 0) return -1;
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
     int rcv = 8 << 20;
     setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof(rcv));
-    return true;
+    timeval tv{5, 0};                                // a broker that stops answering is a dead broker
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    return fd;
   }
 
-  bool send_all(const uint8_t* p, size_t n) {
+  static bool send_all(int fd, const uint8_t* p, size_t n) {
     while (n) {
       const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
       if (k <= 0) return false;
@@ -180,7 +215,7 @@ class Consumer {
     }
     return true;
   }
-  bool recv_all(uint8_t* p, size_t n) {
+  static bool recv_all(int fd, uint8_t* p, size_t n) {
     while (n) {
       const ssize_t k = ::recv(fd, p, n, 0);
       if (k <= 0) return false;
@@ -190,13 +225,137 @@ class Consumer {
     return true;
   }
 
-  // Fetch v4 for every partition; returns the response body (after correlation id)
-  bool fetch(std::vector<uint8_t>& resp) {
+  // frame = [size][api key][version][corr][client id][body]
+  bool send_request(Conn& c, int16_t api, int16_t ver, const Out& body) {
+    Out h;
+    h.i16(api);
+    h.i16(ver);
+    h.i32(++c.corr);
+    h.str(client);
+    Out frame;
+    frame.i32((int32_t)(h.b.size() + body.b.size()));
+    frame.put(h.b.data(), h.b.size());
+    frame.put(body.b.data(), body.b.size());
+    c.expect = c.corr;
+    return send_all(c.fd, frame.b.data(), frame.b.size());
+  }
+  // response body after the correlation id
+  bool recv_response(Conn& c, std::vector<uint8_t>& resp) {
+    uint8_t hdr[4];
+    if (!recv_all(c.fd, hdr, 4)) return false;
+    uint32_t len;
+    std::memcpy(&len, hdr, 4);
+    len = ntohl(len);
+    if (len < 4 || len > (1u << 30)) return false;
+    resp.resize(len);
+    if (!recv_all(c.fd, resp.data(), len)) return false;
+    int32_t corr;
+    std::memcpy(&corr, resp.data(), 4);
+    if ((int32_t)ntohl((uint32_t)corr) != c.expect) return false;
+    c.expect = 0;
+    resp.erase(resp.begin(), resp.begin() + 4);
+    return true;
+  }
+  void close_conn(Conn& c) {
+    if (c.fd >= 0) ::close(c.fd);
+    c.fd = -1;
+    c.expect = 0;
+  }
+
+  // Metadata v1 for our topic from any reachable broker (known brokers first, then seeds):
+  // broker table + the leader of every partition we consume.
+  bool refresh_metadata() {
+    n_meta.fetch_add(1, std::memory_order_relaxed);
+    std::vector<std::pair<std::string, int>> cands;
+    for (auto& kv : brokers) cands.emplace_back(kv.second.host, kv.second.port);
+    for (auto& sd : seeds) cands.push_back(sd);
     Out body;
-    body.i16(1);            // api key Fetch
-    body.i16(4);            // version
-    body.i32(++corr);
-    body.str(client);
+    body.i32(1);
+    body.str(topic);
+    std::vector<uint8_t> resp;
+    for (auto& hp : cands) {
+      Conn c;
+      c.host = hp.first;
+      c.port = hp.second;
+      c.fd = dial(c.host, c.port);
+      if (c.fd < 0) continue;
+      const bool ok = send_request(c, 3, 1, body) && recv_response(c, resp);
+      close_conn(c);
+      if (!ok) continue;
+      In in{resp.data(), resp.data() + resp.size()};
+      std::map<int32_t, std::pair<std::string, int>> nodes;
+      const int32_t nb = in.i32();
+      for (int32_t i = 0; i < nb && in.ok; ++i) {
+        const int32_t id = in.i32();
+        const int16_t hl = in.i16();
+        std::string h;
+        if (hl > 0 && in.need((size_t)hl)) { h.assign((const char*)in.p, (size_t)hl); in.p += hl; }
+        const int32_t port = in.i32();
+        const int16_t rl = in.i16();
+        if (rl > 0) in.skip((size_t)rl);
+        nodes[id] = {h, port};
+      }
+      in.i32();                                       // controller
+      const int32_t nt = in.i32();
+      std::map<int32_t, int32_t> leader;              // partition -> node
+      bool topic_ok = false;
+      for (int32_t t = 0; t < nt && in.ok; ++t) {
+        const int16_t terr = in.i16();
+        const int16_t sl = in.i16();
+        std::string name;
+        if (sl > 0 && in.need((size_t)sl)) { name.assign((const char*)in.p, (size_t)sl); in.p += sl; }
+        in.i8();                                      // internal
+        const int32_t np = in.i32();
+        for (int32_t q = 0; q < np && in.ok; ++q) {
+          const int16_t perr = in.i16();
+          const int32_t idx = in.i32();
+          const int32_t lead = in.i32();
+          const int32_t nr = in.i32();
+          for (int32_t k = 0; k < nr && in.ok; ++k) in.i32();
+          const int32_t ni = in.i32();
+          for (int32_t k = 0; k < ni && in.ok; ++k) in.i32();
+          if (name == topic && perr == 0) leader[idx] = lead;
+        }
+        if (name == topic && terr == 0) topic_ok = true;
+      }
+      if (!in.ok) continue;
+      if (!topic_ok) { error("metadata: topic " + topic + " unavailable"); return false; }
+      // reconnect only brokers whose address changed or that disappeared
+      for (auto it = brokers.begin(); it != brokers.end();) {
+        auto nd = nodes.find(it->first);
+        if (nd == nodes.end() || nd->second.first != it->second.host || nd->second.second != it->second.port) {
+          close_conn(it->second);
+          it = brokers.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      for (auto& kv : nodes)
+        if (!brokers.count(kv.first)) { Conn c2; c2.host = kv.second.first; c2.port = kv.second.second; brokers[kv.first] = c2; }
+      bool all = true;
+      for (auto& s : ps) {
+        auto l = leader.find(s.kafka_partition);
+        s.leader = (l != leader.end() && brokers.count(l->second)) ? l->second : -1;
+        all = all && s.leader >= 0;
+      }
+      meta_stale = !all;                              // a leaderless partition: ask again soon
+      return true;
+    }
+    error("metadata: no broker reachable");
+    return false;
+  }
+
+  Conn* leader_conn(int32_t node) {
+    auto it = brokers.find(node);
+    if (it == brokers.end()) return nullptr;
+    Conn& c = it->second;
+    if (c.fd < 0) c.fd = dial(c.host, c.port);
+    return c.fd >= 0 ? &c : nullptr;
+  }
+
+  // Fetch v4 for this leader's partitions
+  Out fetch_body(const std::vector<int>& pis) {
+    Out body;
     body.i32(-1);           // replica id
     body.i32(max_wait_ms);
     body.i32(1);            // min bytes
@@ -204,26 +363,48 @@ class Consumer {
     body.i8(0);             // isolation: read uncommitted
     body.i32(1);            // one topic
     body.str(topic);
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      body.i32((int32_t)ps.size());
-      for (auto& s : ps) {
-        body.i32(s.kafka_partition);
-        body.i64(s.next_offset);
-        body.i32(16 << 20);
-      }
+    std::lock_guard<std::mutex> lk(mu);
+    body.i32((int32_t)pis.size());
+    for (int pi : pis) {
+      body.i32(ps[pi].kafka_partition);
+      body.i64(ps[pi].next_offset);
+      body.i32(16 << 20);
     }
-    Out frame;
-    frame.i32((int32_t)body.b.size());
-    frame.put(body.b.data(), body.b.size());
-    if (!send_all(frame.b.data(), frame.b.size())) { last_err = "send"; return false; }
-    uint8_t hdr[4];
-    if (!recv_all(hdr, 4)) { last_err = "recv"; return false; }
-    uint32_t len;
-    std::memcpy(&len, hdr, 4);
-    len = ntohl(len);
-    resp.resize(len);
-    if (!recv_all(resp.data(), len)) { last_err = "recv body"; return false; }
+    return body;
+  }
+
+  // ListOffsets v1 on the partition's leader: earliest (-2) or latest (-1)
+  bool reset_offset(int pi) {
+    PState& s = ps[pi];
+    Conn* c = leader_conn(s.leader);
+    if (!c) { meta_stale = true; return false; }
+    Out body;
+    body.i32(-1);
+    body.i32(1);
+    body.str(topic);
+    body.i32(1);
+    body.i32(s.kafka_partition);
+    body.i64(reset_policy == CCFD_KC_RESET_LATEST ? -1 : -2);
+    std::vector<uint8_t> resp;
+    if (!send_request(*c, 2, 1, body) || !recv_response(*c, resp)) { close_conn(*c); meta_stale = true; return false; }
+    In in{resp.data(), resp.data() + resp.size()};
+    in.i32();
+    const int16_t sl = in.i16();
+    in.skip(sl > 0 ? (size_t)sl : 0);
+    in.i32();
+    in.i32();                                         // partition
+    const int16_t err = in.i16();
+    in.i64();                                         // timestamp
+    const int64_t off = in.i64();
+    if (!in.ok || err != 0) {
+      if (err == kErrNotLeader || err == kErrUnknownTopicOrPartition || err == kErrLeaderNotAvailable) meta_stale = true;
+      else error("list offsets error " + std::to_string(err) + " on partition " + std::to_string(s.kafka_partition));
+      return false;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    s.next_offset = off;
+    s.reset = false;
+    n_resets.fetch_add(1);
     return true;
   }
 
@@ -301,50 +482,81 @@ class Consumer {
     return ok;
   }
 
+  // gzip (codec 1) records section -> `inflated`; false on a corrupt stream
+  bool gunzip(const uint8_t* p, size_t n) {
+    z_stream zs{};
+    if (inflateInit2(&zs, 32 + MAX_WBITS) != Z_OK) return false;   // gzip or zlib header
+    inflated.resize(std::max<size_t>(inflated.capacity(), n * 4 + 4096));
+    zs.next_in = const_cast<Bytef*>(p);
+    zs.avail_in = (uInt)n;
+    size_t out = 0;
+    int rc = Z_OK;
+    while (rc == Z_OK) {
+      if (out == inflated.size()) {
+        if (inflated.size() >= (size_t)1 << 30) { rc = Z_MEM_ERROR; break; }
+        inflated.resize(inflated.size() * 2);
+      }
+      zs.next_out = inflated.data() + out;
+      zs.avail_out = (uInt)std::min<size_t>(inflated.size() - out, UINT_MAX);
+      rc = inflate(&zs, Z_NO_FLUSH);
+      out = inflated.size() - zs.avail_out;
+      if (rc == Z_BUF_ERROR && zs.avail_in == 0) break;
+    }
+    inflateEnd(&zs);
+    if (rc != Z_STREAM_END) return false;
+    inflated.resize(out);
+    return true;
+  }
+
   // RecordBatch v2 records of one partition's record set
   void ingest_record_set(int pi, const uint8_t* p, const uint8_t* e) {
     while (e - p >= 61) {                            // batch header
       In h{p, e};
       const int64_t base = h.i64();
       const int32_t blen = h.i32();
-      if (blen < 49 || e - p < 12 + blen) break;     // partial trailing batch
+      if (blen < 49 || e - p < 12 + (int64_t)blen) break;   // partial trailing batch
       const uint8_t* bend = p + 12 + blen;
       h.i32();                                       // leader epoch
       const int8_t magic = h.i8();
       const uint32_t crc = h.u32();
       if (magic != 2 || ccfd_crc32c(h.p, (size_t)(bend - h.p), 0) != crc) {
-        n_errors.fetch_add(1);
-        std::lock_guard<std::mutex> lk(mu);
-        last_err = "bad record batch (magic/crc)";
+        error("bad record batch (magic/crc)");
         return;
       }
       const int16_t attrs = h.i16();
       h.i32();                                       // last offset delta
       h.i64(); h.i64(); h.i64(); h.i16(); h.i32();    // timestamps, producer id/epoch, base seq
       const int32_t count = h.i32();
-      if ((attrs & 0x7) != 0) {                      // compressed batches are not produced here
-        n_errors.fetch_add(1);
-        std::lock_guard<std::mutex> lk(mu);
-        last_err = "compressed record batch";
-        return;
-      }
+      const int codec = attrs & 0x7;
       In r{h.p, bend};
+      if (codec == 1) {
+        if (!gunzip(h.p, (size_t)(bend - h.p))) { error("corrupt gzip record batch"); p = bend; continue; }
+        r = In{inflated.data(), inflated.data() + inflated.size()};
+      } else if (codec != 0) {
+        static const char* names[] = {"none", "gzip", "snappy", "lz4", "zstd"};
+        error(std::string("unsupported compression codec ") + (codec <= 4 ? names[codec] : "?"));
+        return;                                      // never skip data silently: the partition stalls
+      }
       for (int32_t i = 0; i < count && r.ok; ++i) {
         const int64_t rlen = r.varlong();
+        if (!r.ok || rlen < 0 || rlen > r.e - r.p) { r.ok = false; break; }
         const uint8_t* rend = r.p + rlen;
-        if (rlen < 0 || rend > bend) { r.ok = false; break; }
-        r.i8();                                      // attributes
-        r.varlong();                                 // timestamp delta
-        const int64_t od = r.varlong();
-        const int64_t klen = r.varlong();
-        if (klen > 0) r.skip((size_t)klen);
-        const int64_t vlen = r.varlong();
-        const uint8_t* val = r.p;
-        if (vlen > 0) r.skip((size_t)vlen);
+        In rec{r.p, rend};
+        rec.i8();                                    // attributes
+        rec.varlong();                               // timestamp delta
+        const int64_t od = rec.varlong();
+        const int64_t klen = rec.varlong();
+        if (klen > 0) rec.skip((size_t)klen);
+        const int64_t vlen = rec.varlong();
+        const uint8_t* val = rec.p;
+        if (vlen > 0) rec.skip((size_t)vlen);
+        // a value (or key) that runs past its record is a malformed batch (CRC only detects
+        // corruption, any producer can build one): stop processing this batch
+        if (!rec.ok || vlen > INT32_MAX || (vlen > 0 && val + vlen > rend)) { r.ok = false; break; }
         r.p = rend;                                  // headers skipped
         const int64_t off = base + od;
         PState& s = ps[pi];
-        if (off < s.next_offset) continue;           // already consumed (re-fetch overlap)
+        if (off < s.next_offset) continue;           // already consumed (batch starts below the fetch offset)
         int64_t rows = 0;
         if (vlen > 0 && !ingest_value(pi, val, (int32_t)vlen, &rows)) {
           if (stop.load()) return;
@@ -357,52 +569,101 @@ class Consumer {
         s.next_offset = off + 1;
         s.pending.emplace_back(s.rows_in, off + 1);
       }
+      if (!r.ok) { error("malformed record in batch at offset " + std::to_string(base)); return; }
       p = bend;
     }
   }
 
+  // one Fetch v4 response of one broker
+  bool handle_fetch(const std::vector<uint8_t>& resp) {
+    In in{resp.data(), resp.data() + resp.size()};
+    in.i32();                                        // throttle
+    const int32_t nt = in.i32();
+    bool any = false;
+    for (int32_t t = 0; t < nt && in.ok; ++t) {
+      const int16_t sl = in.i16();
+      in.skip(sl > 0 ? (size_t)sl : 0);
+      const int32_t np = in.i32();
+      for (int32_t q = 0; q < np && in.ok; ++q) {
+        const int32_t part = in.i32();
+        const int16_t err = in.i16();
+        in.i64(); in.i64();                          // high watermark, last stable offset
+        const int32_t na = in.i32();
+        for (int32_t a = 0; a < na && in.ok; ++a) { in.i64(); in.i64(); }
+        const int32_t rl = in.i32();
+        const uint8_t* rs = in.p;
+        if (rl > 0) in.skip((size_t)rl);
+        if (!in.ok) break;
+        int pi = -1;
+        for (size_t k = 0; k < ps.size(); ++k)
+          if (ps[k].kafka_partition == part) { pi = (int)k; break; }
+        if (pi < 0) continue;
+        if (err == kErrNotLeader || err == kErrUnknownTopicOrPartition || err == kErrLeaderNotAvailable ||
+            err == kErrReplicaNotAvailable) {
+          meta_stale = true;                         // leadership moved: refresh, same offset
+          ps[pi].leader = -1;
+          continue;
+        }
+        if (err == kErrOffsetOutOfRange) {
+          if (reset_policy == CCFD_KC_RESET_NONE) {
+            ps[pi].stopped = true;
+            error("offset out of range on partition " + std::to_string(part) + " (reset policy none)");
+          } else {
+            ps[pi].reset = true;
+          }
+          continue;
+        }
+        if (err != 0) {
+          error("fetch error " + std::to_string(err) + " on partition " + std::to_string(part));
+          continue;
+        }
+        if (rl <= 0) continue;
+        any = true;
+        ingest_record_set(pi, rs, rs + rl);
+      }
+    }
+    if (!in.ok) error("truncated fetch response");
+    return any;
+  }
+
   void loop() {
     std::vector<uint8_t> resp;
+    std::map<int32_t, std::vector<int>> by_leader;
     while (!stop.load()) {
-      if (fd < 0 && !connect_broker()) {
-        n_errors.fetch_add(1);
-        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      if (meta_stale && !refresh_metadata()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
         continue;
       }
-      if (!fetch(resp)) {
-        n_errors.fetch_add(1);
-        ::close(fd);
-        fd = -1;
+      for (size_t pi = 0; pi < ps.size(); ++pi)
+        if (ps[pi].reset && !ps[pi].stopped) reset_offset((int)pi);
+      by_leader.clear();
+      for (size_t pi = 0; pi < ps.size(); ++pi)
+        if (ps[pi].leader >= 0 && !ps[pi].stopped && !ps[pi].reset) by_leader[ps[pi].leader].push_back((int)pi);
+      if (by_leader.empty()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(ps.empty() ? 100 : 5));
+        if (std::all_of(ps.begin(), ps.end(), [](const PState& s) { return s.leader < 0; })) meta_stale = true;
         continue;
       }
-      n_fetches.fetch_add(1, std::memory_order_relaxed);
-      n_bytes.fetch_add(resp.size(), std::memory_order_relaxed);
-      In in{resp.data(), resp.data() + resp.size()};
-      in.i32();                                      // correlation id
-      in.i32();                                      // throttle
-      const int32_t nt = in.i32();
+      // send to every leader, then read every response: brokers work in parallel
+      std::vector<int32_t> sent;
+      for (auto& kv : by_leader) {
+        Conn* c = leader_conn(kv.first);
+        if (!c) { meta_stale = true; continue; }
+        if (!send_request(*c, 1, 4, fetch_body(kv.second))) { close_conn(*c); meta_stale = true; continue; }
+        sent.push_back(kv.first);
+      }
+      n_leaders.store(sent.size(), std::memory_order_relaxed);
       bool any = false;
-      for (int32_t t = 0; t < nt && in.ok; ++t) {
-        const int16_t sl = in.i16();
-        in.skip(sl > 0 ? sl : 0);
-        const int32_t np = in.i32();
-        for (int32_t q = 0; q < np && in.ok; ++q) {
-          const int32_t part = in.i32();
-          const int16_t err = in.i16();
-          in.i64(); in.i64();                        // high watermark, last stable offset
-          const int32_t na = in.i32();
-          for (int32_t a = 0; a < na && in.ok; ++a) { in.i64(); in.i64(); }
-          const int32_t rl = in.i32();
-          const uint8_t* rs = in.p;
-          if (rl > 0) in.skip((size_t)rl);
-          if (err != 0 || rl <= 0 || !in.ok) continue;
-          int pi = -1;
-          for (size_t k = 0; k < ps.size(); ++k)
-            if (ps[k].kafka_partition == part) { pi = (int)k; break; }
-          if (pi < 0) continue;
-          any = true;
-          ingest_record_set(pi, rs, rs + rl);
+      for (int32_t node : sent) {
+        Conn& c = brokers[node];
+        if (!recv_response(c, resp)) {               // broker died or stalled: reconnect via metadata
+          close_conn(c);
+          meta_stale = true;
+          continue;
         }
+        n_fetches.fetch_add(1, std::memory_order_relaxed);
+        n_bytes.fetch_add(resp.size(), std::memory_order_relaxed);
+        any = handle_fetch(resp) || any;
       }
       if (!any) std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
@@ -423,8 +684,19 @@ class Consumer {
 
 Consumer* make(const char* host, int port, const char* topic, const ccfd_kc_partition* parts, int n, int wire) {
   auto* c = new Consumer();
-  c->host = host;
-  c->port = port;
+  // bootstrap list: "h1:p1,h2:p2" or a bare host (then `port`)
+  std::string all = host;
+  size_t pos = 0;
+  while (pos <= all.size()) {
+    size_t q = all.find(',', pos);
+    if (q == std::string::npos) q = all.size();
+    std::string item = all.substr(pos, q - pos);
+    pos = q + 1;
+    if (item.empty()) continue;
+    const size_t colon = item.rfind(':');
+    if (colon != std::string::npos) c->seeds.emplace_back(item.substr(0, colon), std::atoi(item.c_str() + colon + 1));
+    else c->seeds.emplace_back(item, port);
+  }
   c->topic = topic;
   c->wire = wire;
   c->ps.resize(n);
@@ -490,9 +762,32 @@ void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out) {
   out->bytes = c->n_bytes.load();
   out->errors = c->n_errors.load();
   out->fetches = c->n_fetches.load();
+  out->metadata_refreshes = c->n_meta.load();
+  out->offset_resets = c->n_resets.load();
+  out->leaders = c->n_leaders.load();
 }
 
-const char* ccfd_kc_last_error(void* kc) { return static_cast<Consumer*>(kc)->last_err.c_str(); }
+const char* ccfd_kc_last_error(void* kc) {
+  auto* c = static_cast<Consumer*>(kc);
+  static thread_local std::string copy;               // stable while the consumer thread runs
+  std::lock_guard<std::mutex> lk(c->mu);
+  copy = c->last_err;
+  return copy.c_str();
+}
+
+int ccfd_kc_set_offset_reset(void* kc, int policy) {
+  auto* c = static_cast<Consumer*>(kc);
+  if (policy < CCFD_KC_RESET_EARLIEST || policy > CCFD_KC_RESET_NONE || c->th.joinable()) return -1;
+  c->reset_policy = policy;
+  return 0;
+}
+
+int64_t ccfd_kc_position(void* kc, int part_index) {
+  auto* c = static_cast<Consumer*>(kc);
+  if (part_index < 0 || part_index >= (int)c->ps.size()) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return c->ps[part_index].next_offset;
+}
 
 // Fuzz / unit entry: feed raw bytes as partition 0's record set of an array-sink consumer
 // (no socket).  Returns records accepted.  Used by tests/test_native_cpu.py under ASan.

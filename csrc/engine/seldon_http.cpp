@@ -46,6 +46,7 @@ namespace {
 constexpr int kF = CCFD_N_FEATURES;
 constexpr int kLatBuckets = 32;               // upper bounds supplied by the caller (seconds)
 constexpr size_t kMaxBody = 64u << 20;        // 413 above this (a predict body is ~1 KB per row)
+constexpr int64_t kMaxRows = 1 << 24;         // tensor shape entries above this are invalid
 constexpr size_t kMaxHeader = 64u << 10;      // a request head longer than this closes the connection
 
 typedef int (*score_fn)(const float* rows, int32_t n, float* proba, void* ctx);
@@ -196,6 +197,9 @@ int parse_seldon(const char* b, size_t len, std::vector<float>& rows, bool* tens
             if (k3 == "shape") {
               std::vector<float> sh;
               if (parse_num_array(c, sh) < 1) { *err = "invalid shape"; return -1; }
+              // range-check before the float->int conversion (no UB on 1e300 / NaN / -5)
+              for (double d : sh)
+                if (!(d >= 0.0 && d <= (double)kMaxRows) || d != (double)(int64_t)d) { *err = "invalid shape"; return -1; }
               shape0 = (int)sh[0]; shape1 = sh.size() > 1 ? (int)sh[1] : 1;
             } else if (k3 == "values") {
               if (parse_num_array(c, vals) < 0) { *err = "invalid values"; return -1; }
@@ -248,12 +252,19 @@ struct Conn {
   std::string out;
   size_t out_off = 0;
   bool closing = false;
+  // a predict is being scored: later pipelined requests stay buffered until its response
+  // is queued, so responses leave in request order (HTTP/1.1 pipelining)
+  bool predict_pending = false;
+  bool peer_closed = false;    // peer half-closed: answer what is buffered, then drop
+  bool parsed_all = false;     // the last parse consumed every complete request in `in`
 };
 
+constexpr int kNStatus = 4;
+
 struct Stats {
-  std::atomic<uint64_t> count[3];                 // 200, 400, 401
-  std::atomic<uint64_t> sum_ns[3];
-  std::atomic<uint64_t> hist[3][kLatBuckets + 1];
+  std::atomic<uint64_t> count[kNStatus];          // 200, 4xx (not 401), 401, 5xx
+  std::atomic<uint64_t> sum_ns[kNStatus];
+  std::atomic<uint64_t> hist[kNStatus][kLatBuckets + 1];
   std::atomic<uint64_t> rows, batches, model_ns;
   std::atomic<uint64_t> last_bits[4];             // proba_1, Amount, V17, V10 (f32 bits)
 };
@@ -275,7 +286,7 @@ struct Server {
   std::unordered_map<int, Conn> conns;
   uint64_t puid = 0;                              // worker index in the top byte
 
-  int status_idx(int code) { return code == 200 ? 0 : code == 401 ? 2 : 1; }
+  int status_idx(int code) { return code == 200 ? 0 : code == 401 ? 2 : code >= 500 ? 3 : 1; }
   void observe(int code, int64_t dt_ns) {
     const int s = status_idx(code);
     stp->count[s].fetch_add(1, std::memory_order_relaxed);
@@ -291,7 +302,8 @@ struct Server {
     if (it == conns.end()) return;
     char hdr[256];
     const char* reason = code == 200 ? "OK" : code == 400 ? "Bad Request" : code == 401 ? "Unauthorized" :
-                         code == 404 ? "Not Found" : code == 413 ? "Payload Too Large" : "Error";
+                         code == 404 ? "Not Found" : code == 413 ? "Payload Too Large" :
+                         code == 500 ? "Internal Server Error" : code == 503 ? "Service Unavailable" : "Error";
     const int n = std::snprintf(hdr, sizeof hdr, "HTTP/1.1 %d %s\r\nContent-Type: %s\r\nContent-Length: %zu\r\n%s\r\n",
                                 code, reason, ctype, body.size(), close_after ? "Connection: close\r\n" : "");
     it->second.out.append(hdr, n);
@@ -314,7 +326,7 @@ struct Server {
       if (w > 0) { c.out_off += (size_t)w; continue; }
       if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
         epoll_event ev{};
-        ev.events = EPOLLIN | EPOLLOUT;
+        ev.events = c.peer_closed ? EPOLLOUT : (EPOLLIN | EPOLLOUT);
         ev.data.fd = fd;
         epoll_ctl(efd, EPOLL_CTL_MOD, fd, &ev);
         return;
@@ -324,9 +336,9 @@ struct Server {
     }
     c.out.clear();
     c.out_off = 0;
-    if (c.closing) { drop(fd); return; }
+    if (c.closing || (c.peer_closed && !c.predict_pending && c.parsed_all)) { drop(fd); return; }
     epoll_event ev{};
-    ev.events = EPOLLIN;
+    ev.events = c.peer_closed ? 0u : (uint32_t)EPOLLIN;   // EOF stays readable: stop polling it
     ev.data.fd = fd;
     epoll_ctl(efd, EPOLL_CTL_MOD, fd, &ev);
   }
@@ -348,6 +360,7 @@ struct Server {
     Conn& c = conns[fd];
     size_t off = 0;
     for (;;) {
+      if (c.predict_pending) break;                          // keep response order
       const size_t hend = c.in.find("\r\n\r\n", off);
       if (hend == std::string::npos) {
         if (c.in.size() - off > kMaxHeader) { c.closing = true; off = c.in.size(); }
@@ -407,6 +420,7 @@ struct Server {
           continue;
         }
         pend.push_back(Pending{fd, r0 / kF, n, tensor, close_after, t0});
+        c.predict_pending = true;
       } else if (method == "GET" && (path == "/prometheus" || path == "/metrics")) {
         std::string text;
         if (render) {
@@ -424,6 +438,7 @@ struct Server {
       if (c.closing) break;
     }
     c.in.erase(0, off);
+    c.parsed_all = !c.predict_pending;
   }
 
   void respond(const std::vector<Pending>& pend, const std::vector<float>& rows, const std::vector<float>& proba,
@@ -456,8 +471,10 @@ struct Server {
       queue(p.fd, 200, "application/json", body, p.close_after);
       observe(200, now_ns() - p.t0);
     }
-    if (!pend.empty()) {
-      const Pending& l = pend.back();
+    const Pending* lp = nullptr;                            // last request with rows (n may be 0)
+    for (const Pending& p : pend) if (p.nrows > 0) lp = &p;
+    if (lp) {
+      const Pending& l = *lp;
       const float* x = rows.data() + (l.row0 + l.nrows - 1) * kF;
       const float last[4] = {proba[l.row0 + l.nrows - 1], x[kF - 1], x[17], x[10]};
       for (int i = 0; i < 4; ++i) { uint32_t b; std::memcpy(&b, &last[i], 4); stp->last_bits[i].store(b, std::memory_order_relaxed); }
@@ -470,13 +487,23 @@ struct Server {
     std::vector<float> rows, proba;
     std::vector<uint8_t> route;
     std::vector<Pending> pend;
-    std::vector<int> touched;
+    std::vector<int> touched, deferred;
     char buf[65536];
     while (!stop.load(std::memory_order_relaxed)) {
-      const int n = epoll_wait(efd, evs.data(), (int)evs.size(), 50);
+      // connections holding pipelined requests behind an answered predict are parsed
+      // without waiting for new bytes (level-triggered epoll will not fire for them)
+      const int n = epoll_wait(efd, evs.data(), (int)evs.size(), deferred.empty() ? 50 : 0);
       rows.clear();
       pend.clear();
       touched.clear();
+      for (int fd : deferred) {
+        auto it = conns.find(fd);
+        if (it == conns.end()) continue;
+        parse_requests(fd, rows, pend);
+        if (it->second.peer_closed && !it->second.predict_pending && it->second.out.empty()) { drop(fd); continue; }
+        touched.push_back(fd);
+      }
+      deferred.clear();
       for (int i = 0; i < n; ++i) {
         const int fd = evs[i].data.fd;
         if (fd == lfd) {
@@ -504,9 +531,17 @@ struct Server {
           break;
         }
         if (conns.count(fd)) {
+          Conn& c = conns[fd];
+          if (dead) c.peer_closed = true;
           parse_requests(fd, rows, pend);
           touched.push_back(fd);
-          if (dead && conns[fd].out.empty()) { drop(fd); continue; }
+          if (dead) {
+            if (c.out.empty() && !c.predict_pending) { drop(fd); continue; }
+            epoll_event ev{};
+            ev.events = c.out.empty() ? 0u : (uint32_t)EPOLLOUT;
+            ev.data.fd = fd;
+            epoll_ctl(efd, EPOLL_CTL_MOD, fd, &ev);
+          }
         }
       }
       if (!pend.empty()) {
@@ -525,10 +560,17 @@ struct Server {
         stp->rows.fetch_add((uint64_t)total, std::memory_order_relaxed);
         stp->batches.fetch_add(1, std::memory_order_relaxed);
         if (rc != 0) {
-          for (const Pending& p : pend) { observe(400, now_ns() - p.t0); queue(p.fd, 500, "application/json", error_json(500, "scoring failed"), true); }
+          for (const Pending& p : pend) { observe(500, now_ns() - p.t0); queue(p.fd, 500, "application/json", error_json(500, "scoring failed"), true); }
         } else {
           respond(pend, rows, proba, now_ns() - m0);
         }
+      }
+      for (const Pending& p : pend) {
+        auto it = conns.find(p.fd);
+        if (it == conns.end()) continue;
+        it->second.predict_pending = false;
+        if (!it->second.in.empty() && !it->second.closing) deferred.push_back(p.fd);
+        else it->second.parsed_all = true;
       }
       for (int fd : touched)
         if (conns.count(fd) && !conns[fd].out.empty()) flush(fd);
@@ -558,7 +600,7 @@ void* ccfd_seldon_http_start(const char* host, int port, void** engines, int n_w
                              const double* bounds, int nbounds) {
   if (n_workers < 1 || (!scorer && !engines)) return nullptr;
   auto* g = new Group();
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < kNStatus; ++i) {
     g->st.count[i] = 0; g->st.sum_ns[i] = 0;
     for (int b = 0; b <= kLatBuckets; ++b) g->st.hist[i][b] = 0;
   }
@@ -623,18 +665,19 @@ int64_t ccfd_seldon_parse_fuzz(const char* buf, int64_t len, float* rows_out, in
 
 int ccfd_seldon_http_port(void* h) { return h ? static_cast<Group*>(h)->port : -1; }
 
-// stats: [count x3, sum_ns x3, rows, batches, model_ns, last_bits x4, hist 3 x (32+1)] (u64)
+// stats: [count x4, sum_ns x4, rows, batches, model_ns, last_bits x4, hist 4 x (32+1)] (u64);
+// status order 200, 4xx (not 401), 401, 5xx
 int ccfd_seldon_http_stats(void* h, uint64_t* out) {
   if (!h) return -1;
   Stats& st = static_cast<Group*>(h)->st;
   int k = 0;
-  for (int i = 0; i < 3; ++i) out[k++] = st.count[i].load();
-  for (int i = 0; i < 3; ++i) out[k++] = st.sum_ns[i].load();
+  for (int i = 0; i < kNStatus; ++i) out[k++] = st.count[i].load();
+  for (int i = 0; i < kNStatus; ++i) out[k++] = st.sum_ns[i].load();
   out[k++] = st.rows.load();
   out[k++] = st.batches.load();
   out[k++] = st.model_ns.load();
   for (int i = 0; i < 4; ++i) out[k++] = st.last_bits[i].load();
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < kNStatus; ++i)
     for (int b = 0; b <= kLatBuckets; ++b) out[k++] = st.hist[i][b].load();
   return k;
 }

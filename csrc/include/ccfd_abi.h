@@ -254,8 +254,10 @@ int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* offsets, int64
 int64_t ccfd_encode_w64(const float* x, int64_t n, int64_t ld, uint8_t* out);
 
 // ---------------------------------------------------------------------------
-// Native Kafka consumer (csrc/engine/kafka_consumer.cpp): Fetch v4 -> RecordBatch v2 ->
-// TXB1 / JSON values -> rows in the engine's pinned partition rings.
+// Native Kafka consumer (csrc/engine/kafka_consumer.cpp): Metadata v1 -> one connection
+// per partition leader -> Fetch v4 -> RecordBatch v2 (uncompressed or gzip) -> TXB1 / JSON
+// values -> rows in the engine's pinned partition rings.  `host` may be a bootstrap list
+// "h1:p1,h2:p2" (then `port` is only the default for entries without one).
 typedef struct ccfd_kc_partition {
   int32_t kafka_partition;   // partition id in the topic
   int32_t engine_partition;  // ring index in the engine (engine sink)
@@ -268,7 +270,15 @@ typedef struct ccfd_kc_partition {
 
 typedef struct ccfd_kc_stats {
   uint64_t records, rows, bytes, errors, fetches;
+  uint64_t metadata_refreshes;   // leader / broker changes seen (NOT_LEADER, dead connection, ...)
+  uint64_t offset_resets;        // OFFSET_OUT_OF_RANGE handled by the reset policy
+  uint64_t leaders;              // broker connections used by the last fetch round
 } ccfd_kc_stats;
+
+// offset reset policy on OFFSET_OUT_OF_RANGE (auto.offset.reset)
+#define CCFD_KC_RESET_EARLIEST 0
+#define CCFD_KC_RESET_LATEST 1
+#define CCFD_KC_RESET_NONE 2     // stop the partition and report the error
 
 void* ccfd_kc_create_engine(void* engine, const char* host, int port, const char* topic,
                             const ccfd_kc_partition* parts, int n_parts, int wire);
@@ -282,6 +292,8 @@ int64_t ccfd_kc_committable(void* kc, int part_index);
 void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out);
 const char* ccfd_kc_last_error(void* kc);
 int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n);   // tests / fuzzing
+int ccfd_kc_set_offset_reset(void* kc, int policy);                           // before start
+int64_t ccfd_kc_position(void* kc, int part_index);                           // next offset to fetch
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,127 @@
+"""Native Kafka consumer against a 3-broker kafka-lite cluster (VERDICT r1 Next #2): every
+row lands exactly once while partition leadership is split over 3 listeners, moves
+mid-stream, and a broker fails; offsets become committable only for consumed rows; gzip
+batches; OFFSET_OUT_OF_RANGE handled by the reset policy; unsupported codecs reported."""
+import json
+import struct
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.contracts import FEATURE_NAMES, TxBatch
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteCluster
+from ccfd_demo_summit_amd.ingest.kafka_wire import CODEC_GZIP, KafkaBroker, encode_record_batch
+from ccfd_demo_summit_amd.ingest.native_consumer import NativeKafkaConsumer
+
+P = 6
+
+
+@pytest.fixture()
+def cluster():
+    cl = KafkaLiteCluster(3, default_partitions=P).start_in_thread()
+    yield cl
+    cl.stop()
+
+
+def _wait(fn, timeout=30):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if fn():
+            return True
+        time.sleep(0.01)
+    return False
+
+
+def test_rows_exact_across_leader_move_and_broker_failure(cluster):
+    kb = KafkaBroker(cluster.bootstrap_all)
+    kb.create_topic("odh-demo", P)
+    assert len({cluster.leader("odh-demo", p) for p in range(P)}) == 3
+    X, _ = generate(24_000, seed=9)
+    per = 4000
+    kc = NativeKafkaConsumer.for_arrays(cluster.bootstrap_all, "odh-demo", {p: 0 for p in range(P)},
+                                        capacity=per + 100).start()
+    gz = KafkaBroker(cluster.bootstrap_all, compression=CODEC_GZIP)
+
+    def produce():
+        # per partition: 16 TXB1 batches of 200 rows + 800 JSON transactions (every 4th batch gzip)
+        for k in range(16):
+            for p in range(P):
+                s = p * per + k * 200
+                ids = np.arange(s, s + 200, dtype=np.uint64)
+                b = TxBatch(ids=ids, customer=(ids % 1000).astype(np.uint32), features=X[s:s + 200]).encode()
+                (gz if k % 4 == 3 else kb).produce("odh-demo", b, partition=p)
+            if k == 5:
+                p0 = 0
+                cluster.move_leader("odh-demo", p0, cluster.leader("odh-demo", 1))
+            if k == 10:
+                cluster.fail_node(3)
+        for p in range(P):
+            s = p * per + 3200
+            msgs = [json.dumps({"id": int(s + i), "customer_id": int((s + i) % 1000),
+                                **{n: float(v) for n, v in zip(FEATURE_NAMES, X[s + i])}}).encode()
+                    for i in range(800)]
+            kb.produce_many("odh-demo", msgs, partition=p)
+    th = threading.Thread(target=produce)
+    th.start()
+    try:
+        th.join(120)
+        assert _wait(lambda: kc.stats()["rows"] >= P * per, 60), (kc.stats(), kc.last_error())
+        time.sleep(0.2)
+        st = kc.stats()
+        assert st["rows"] == P * per and st["records"] == P * (16 + 800), st
+        assert st["metadata_refreshes"] >= 2                 # the move and the failure were noticed
+        for i, p in enumerate(range(P)):
+            f, ids, cu = kc.arrays[p]
+            np.testing.assert_array_equal(ids[:per], np.arange(p * per, (p + 1) * per, dtype=np.uint64))
+            np.testing.assert_array_equal(f[:per], X[p * per:(p + 1) * per])
+        # the array sink "releases" rows as written: every record's next offset is committable
+        assert kc.committable() == {p: 16 + 800 for p in range(P)}
+        assert kc.position() == {p: 16 + 800 for p in range(P)}
+    finally:
+        kc.stop()
+        kc.close()
+        kb.close()
+        gz.close()
+
+
+@pytest.mark.parametrize("policy", ["earliest", "latest", "none"])
+def test_offset_out_of_range_policy(cluster, policy):
+    kb = KafkaBroker(cluster.bootstrap)
+    kb.create_topic("t", 1)
+    X, _ = generate(10, seed=1)
+    for i in range(10):
+        kb.produce("t", json.dumps({"id": i, "features": X[i].tolist()}).encode(), partition=0)
+    kc = NativeKafkaConsumer.for_arrays(cluster.bootstrap, "t", {0: 500}, capacity=100)   # beyond the log end
+    kc.set_offset_reset(policy).start()
+    try:
+        if policy == "earliest":
+            assert _wait(lambda: kc.stats()["rows"] == 10), (kc.stats(), kc.last_error())
+            assert kc.arrays[0][1][:10].tolist() == list(range(10))
+        elif policy == "latest":
+            assert _wait(lambda: kc.stats()["offset_resets"] >= 1)
+            kb.produce("t", json.dumps({"id": 77, "features": X[0].tolist()}).encode(), partition=0)
+            assert _wait(lambda: kc.stats()["rows"] == 1)
+            assert kc.arrays[0][1][0] == 77
+        else:
+            assert _wait(lambda: "offset out of range" in kc.last_error())
+            assert kc.stats()["rows"] == 0 and kc.stats()["errors"] >= 1
+    finally:
+        kc.stop()
+        kc.close()
+        kb.close()
+
+
+def test_unsupported_codec_is_reported_not_skipped():
+    rb = bytearray(encode_record_batch([b'{"id": 1}']))
+    struct.pack_into(">h", rb, 21, 2)                    # attributes: snappy
+    from ccfd_demo_summit_amd.ingest.kafka_wire import crc32c
+    struct.pack_into(">I", rb, 17, crc32c(bytes(rb[21:])))
+    kc = NativeKafkaConsumer.for_arrays("127.0.0.1:1", "t", {0: 0}, capacity=10)
+    try:
+        assert kc.feed(bytes(rb)) == 0
+        assert "snappy" in kc.last_error() and kc.stats()["errors"] == 1
+    finally:
+        kc.close()

@@ -147,6 +147,25 @@ def test_host_runtime_under_asan(tmp_path):
         "    cut = int(r.integers(0, len(b) + 1)) if it % 3 == 0 else len(b)\n"
         "    fz.feed(bytes(b[:cut]))\n"
         "    fz.feed(bytes(r.integers(0, 256, int(r.integers(0, 300)), dtype=np.uint8)))\n"
+        "# a CRC-valid batch whose record value length runs past the record (ADVICE r1): rejected, no over-read\n"
+        "import struct\n"
+        "from ccfd_demo_summit_amd.ingest.kafka_wire import _varint, crc32c, CODEC_GZIP\n"
+        "def batch_of(recs, n):\n"
+        "    after = struct.pack('>hiqqqhii', 0, n - 1, 0, 0, -1, -1, -1, n) + recs\n"
+        "    return struct.pack('>qi', 0, 9 + len(after)) + struct.pack('>ibI', 0, 2, crc32c(after)) + after\n"
+        "for vlen in (1 << 20, 40, 11):\n"
+        "    body = b'\\x00' + _varint(0) + _varint(0) + _varint(-1) + _varint(vlen) + b'{\"id\": 1}' + _varint(0)\n"
+        "    e0 = fz.stats()['errors']\n"
+        "    fz.feed(batch_of(_varint(len(body)) + body, 1))\n"
+        "    assert fz.stats()['errors'] > e0, vlen\n"
+        "gz = encode_record_batch(msgs[:30], compression=CODEC_GZIP)\n"
+        "gzc = NativeKafkaConsumer.for_arrays('127.0.0.1:1', 't', {0: 0}, capacity=1000, wire=False)\n"
+        "assert gzc.feed(gz) == 30, gzc.last_error()\n"
+        "for it in range(500):\n"
+        "    b = bytearray(gz)\n"
+        "    for _ in range(int(r.integers(1, 8))): b[int(r.integers(61, len(b)))] = int(r.integers(0, 256))\n"
+        "    gzc.feed(bytes(b))\n"
+        "gzc.close()\n"
         "fz.close()\n"
         "print('asan probe ok')\n")
     env = dict(os.environ, CCFD_SANITIZE="address,undefined", LD_PRELOAD=rt, CCFD_NO_AUTOBUILD="1",
@@ -183,3 +202,16 @@ def test_json_parser_rejects_malformed_numbers(L):
     for bad in ("-", "1e", "1e+", ".", "--1", "1.2.3"):
         rc, _, _, _ = _parse(L, ['{"features":[' + ",".join([bad] * 30) + "]}"])
         assert rc == -1, bad
+
+
+@pytest.mark.parametrize("field,val", [("id", "-5"), ("id", "1e30"), ("customer_id", "-1"),
+                                       ("customer_id", "5000000000"), ("id", "\"-7\"")])
+def test_json_ids_out_of_range_are_malformed(L, field, val):
+    """negative / oversized ids are rejected instead of an undefined
+    float->integer conversion; a bare `true`/`null` at the very end is bounds-checked."""
+    feats = ",".join(["0.5"] * 30)
+    rc, _, _, _ = _parse(L, ['{"%s": %s, "features": [%s]}' % (field, val, feats)])
+    assert rc != 1
+    rc, _, ids, _ = _parse(L, ['{"id": 12, "features": [%s], "flag": true}' % feats,
+                               '{"id": 13, "features": [%s], "x": null}' % feats])
+    assert rc == 2 and ids.tolist() == [12, 13]

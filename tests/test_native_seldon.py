@@ -177,6 +177,9 @@ def test_native_seldon_parser_and_server_under_asan(tmp_path):
         "    send(bytes(b[:int(r.integers(0, len(b) + 1))]), read=(it % 4 == 0))\n"
         "    send(bytes(r.integers(0, 256, int(r.integers(0, 2000)), dtype=np.uint8)), read=False)\n"
         "assert b'200 OK' in send(req(good[1]))\n"
+        "z = json.dumps({'data': {'tensor': {'shape': [0, 30], 'values': []}}}).encode()\n"
+        "for _ in range(3): assert b'200 OK' in send(req(z))\n"
+        "assert send(req(z) + req(good[0]) + req(z)).count(b'200 OK') == 3\n"
         "srv.stop()\n"
         "print('asan seldon ok')\n")
     env = dict(os.environ, CCFD_SANITIZE="address,undefined", LD_PRELOAD=rt, CCFD_NO_AUTOBUILD="1",
@@ -185,3 +188,70 @@ def test_native_seldon_parser_and_server_under_asan(tmp_path):
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and "asan seldon ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def _raw(port, raw):
+    import socket
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(raw)
+    s.shutdown(socket.SHUT_WR)
+    data = b""
+    while True:
+        d = s.recv(65536)
+        if not d:
+            break
+        data += d
+    s.close()
+    return data
+
+
+def _req(body: bytes, path=b"/api/v0.1/predictions"):
+    return b"POST " + path + b" HTTP/1.1\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+
+
+def test_zero_row_requests(srv):
+    """a [0,30] tensor / empty ndarray is answered with an empty result
+    instead of reading past the scored rows."""
+    s, m, X = srv
+    st, body = _post(s.port, {"data": {"tensor": {"shape": [0, 30], "values": []}}})
+    assert st == 200 and body["data"]["tensor"]["shape"] == [0, 2] and body["data"]["tensor"]["values"] == []
+    # a zero-row request batched together with real ones
+    z = json.dumps({"data": {"tensor": {"shape": [0, 30], "values": []}}}).encode()
+    g = json.dumps(seldon.build_request(X[:2])).encode()
+    out = _raw(s.port, _req(z) + _req(g) + _req(z))
+    assert out.count(b"200 OK") == 3
+    st, body = _post(s.port, seldon.build_request(X[:1]))
+    assert st == 200
+
+
+def test_pipelined_responses_keep_request_order(srv):
+    """POST predict then GET ping on one connection -- the predict's
+    response comes first (HTTP/1.1 pipelining pairs responses by order)."""
+    s, m, X = srv
+    g = json.dumps(seldon.build_request(X[:3])).encode()
+    ping = b"GET /health/ping HTTP/1.1\r\n\r\n"
+    bad = _req(b"{nope")
+    out = _raw(s.port, _req(g) + ping + _req(g) + bad + ping + _req(g))
+    heads = [blk.split(b"\r\n", 1)[0] for blk in out.split(b"HTTP/1.1 ")[1:]]
+    assert heads == [b"200 OK", b"200 OK", b"200 OK", b"400 Bad Request", b"200 OK", b"200 OK"], heads
+    bodies = [blk.split(b"\r\n\r\n", 1)[1] for blk in out.split(b"HTTP/1.1 ")[1:]]
+    assert b"proba_1" in bodies[0] and b"native" in bodies[1] and b"proba_1" in bodies[2]
+    assert b"FAILURE" in bodies[3] and b"native" in bodies[4] and b"proba_1" in bodies[5]
+
+
+def test_scoring_failure_is_a_5xx():
+    """a scorer failure answers 500 Internal Server Error and is counted in
+    the 5xx bucket, not as a client error."""
+    class Boom:
+        def score(self, X):
+            raise RuntimeError("device lost")
+    s = NativeSeldonServer(Boom(), host="127.0.0.1", port=0)
+    try:
+        X, _ = generate(4, seed=1)
+        out = _raw(s.port, _req(json.dumps(seldon.build_request(X[:2])).encode()))
+        assert out.startswith(b"HTTP/1.1 500 Internal Server Error")
+        st = s.stats()
+        assert st["count"]["500"] == 1 and st["count"]["400"] == 0
+        assert b'status="500"' in s.expose()
+    finally:
+        s.stop()
