@@ -34,6 +34,16 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 
+def _prom(hub) -> dict:
+    text = hub.router.expose().decode() if hasattr(hub.router, "expose") else ""
+    prom = {}
+    for line in text.splitlines():
+        for name in ("transaction_incoming_total", "notifications_outgoing_total"):
+            if line.startswith(name + " "):
+                prom[name] = float(line.split()[-1])
+    return prom
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=20.0)
@@ -48,6 +58,13 @@ def main(argv=None):
     ap.add_argument("--fmt", default="txb1", choices=["txb1", "json"],
                     help="txb1: one columnar batch per message; json: one transaction per message")
     ap.add_argument("--python-ingest", action="store_true", help="kafka-lite: use the Python consumer thread")
+    ap.add_argument("--prefill-s", type=float, default=0.0,
+                    help="consumer-only mode: the producer fills the topic for this long BEFORE the "
+                         "engine starts and stops there; the timed window then measures ingest + "
+                         "scoring capacity alone (engine vs producer/broker capacity)")
+    ap.add_argument("--kafka-nodes", type=int, default=1, help="kafka-lite broker listeners")
+    ap.add_argument("--ingest-threads", type=int, default=0,
+                    help="native consumer threads per rank (0 = 1 for TXB1, one per partition for JSON)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
 
@@ -72,18 +89,25 @@ def main(argv=None):
     k = cfg.kafka
     P = args.partitions_per_rank
     lag_limit = args.max_lag_msgs * (args.batch if args.fmt == "json" else 1)   # in messages
-    store = InProcBroker(default_partitions=P, retention=4 * lag_limit)
+    prefill = args.prefill_s > 0
+    # notification / response topics stay in-process (side channels of this rank); the
+    # transactions topic is the in-process broker or kafka-lite's verbatim batch store
+    store = InProcBroker(default_partitions=P, retention=None if prefill else 4 * lag_limit)
+    tx_store = store
     server = None
     if args.broker == "kafka-lite":
-        from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+        from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteCluster
         from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
-        server = KafkaLiteServer("127.0.0.1", 0, default_partitions=P, store=store).start_in_thread()
-        broker = KafkaBroker(server.bootstrap)
-        prod_broker = KafkaBroker(server.bootstrap)
+        server = KafkaLiteCluster(args.kafka_nodes, "127.0.0.1", 0, default_partitions=P,
+                                  retention_batches=None if prefill else 4 * args.max_lag_msgs).start_in_thread()
+        tx_store = server.store
+        broker = KafkaBroker(server.bootstrap_all)
+        prod_broker = KafkaBroker(server.bootstrap_all)
     else:
         broker = prod_broker = store
-    for t in (k.transactions_topic, k.notification_topic, k.response_topic):
+    for t in (k.notification_topic, k.response_topic):
         store.create_topic(t, P)
+    tx_store.create_topic(k.transactions_topic, P)
 
     # model (same random-init + calibration as bench.py), W64 rows
     Xcal, _ = generate(200_000, seed=999)
@@ -104,7 +128,8 @@ def main(argv=None):
         topic=k.transactions_topic, group_id=k.group_id, batch=args.batch, depth=32, streams=4,
         ring_rows=1 << 20, flush_us=args.flush_us, run_budget_us=2000, reduce_period_ms=10.0,
         threshold=cfg.router.fraud_threshold, coalesce=8, max_fetch=64,
-        native_ingest=not args.python_ingest), partitions=list(range(P)))
+        native_ingest=not args.python_ingest,
+        ingest_threads=args.ingest_threads or (P if args.fmt == "json" else 1)), partitions=list(range(P)))
     notif_c = store.consumer("notification-service", [k.notification_topic])
     resp_c = store.consumer(k.group_id + "-responses", [k.response_topic])
 
@@ -125,14 +150,14 @@ def main(argv=None):
         tails = [(",\"customer_id\":%d," % (i % 100_000) + ",".join(
             f'"{n}":{float(v):.6g}' for n, v in zip(FEATURE_NAMES, Xj[i])) + "}").encode() for i in range(args.batch)]
 
-    def producer():
-        seq = 0
+    def producer(until=None):
+        seq = producer.seq
         t0 = time.perf_counter()
-        while not stop.is_set():
+        while not stop.is_set() and (until is None or time.perf_counter() < until):
             if args.rate > 0 and produced[0] > args.rate * (time.perf_counter() - t0):
                 time.sleep(0.0002)
                 continue
-            if store.lag(k.group_id, k.transactions_topic) > lag_limit:
+            if until is None and tx_store.lag(k.group_id, k.transactions_topic) > lag_limit:
                 time.sleep(0.0002)
                 continue
             if args.fmt == "json":
@@ -146,10 +171,17 @@ def main(argv=None):
                 prod_broker.produce(k.transactions_topic, bytes(msg), partition=seq % P)
             produced[0] += args.batch
             seq += 1
+        producer.seq = seq
+    producer.seq = 0
 
     th = threading.Thread(target=producer, daemon=True, name="producer")
+    if prefill:                                     # fill the topic first, untimed
+        tp = time.perf_counter()
+        producer(until=tp + args.prefill_s)
+        prefill_rate = produced[0] / (time.perf_counter() - tp)
     svc.start()
-    th.start()
+    if not prefill:
+        th.start()
 
     def loop_until(t_end):
         while time.perf_counter() < t_end:
@@ -167,23 +199,22 @@ def main(argv=None):
     svc.reset_stats()
     rows0 = svc.rows_scored
     fr0 = router.fraud_started
+    sig0 = router.signals_ok
+    notif0 = _prom(hub).get("notifications_outgoing_total", 0.0)
+    inc0 = _prom(hub).get("transaction_incoming_total", 0.0)
     barrier(ctx)
     t0 = time.perf_counter()
     loop_until(t0 + args.seconds)
     elapsed = time.perf_counter() - t0
     rows = svc.rows_scored - rows0
     stop.set()
-    th.join(5)
+    if th.is_alive():
+        th.join(5)
     svc.flush_epochs()                              # collective: paired X2 reductions on every rank
     lat = svc.latency_hist()                        # cumulative since reset
     tot = all_sum(ctx, float(rows))
     el = all_max(ctx, elapsed)
-    text = hub.router.expose().decode() if hasattr(hub.router, "expose") else ""
-    prom = {}
-    for line in text.splitlines():
-        for name in ("transaction_incoming_total", "notifications_outgoing_total"):
-            if line.startswith(name + " "):
-                prom[name] = float(line.split()[-1])
+    prom = _prom(hub)
     incoming = prom.get("transaction_incoming_total")
     out = {
         "metric": "end-to-end tx/s (Kafka ingest -> GPU score -> route -> BP -> notify)",
@@ -193,12 +224,19 @@ def main(argv=None):
         "ingest": "python" if (args.python_ingest or args.broker == "inproc") else "native",
         "ring_arrival_to_scored_p50_us": round(hist_quantile(lat, 0.5) / 1e3, 1),
         "ring_arrival_to_scored_p99_us": round(hist_quantile(lat, 0.99) / 1e3, 1),
+        # every counter below is a delta over the timed window (rank 0)
         "fraud_processes_started_rank0": router.fraud_started - fr0,
-        "notifications_rank0": prom.get("notifications_outgoing_total"),
-        "responses_signalled_rank0": router.signals_ok,
+        "notifications_rank0": prom.get("notifications_outgoing_total", 0.0) - notif0,
+        "responses_signalled_rank0": router.signals_ok - sig0,
+        "prometheus_transaction_incoming_rank0": (incoming or 0.0) - inc0,
+        "rows_scored_rank0": svc.rows_scored - rows0,
         "prometheus_transaction_incoming_total_rank0": incoming,
         "rows_scored_rank0_total": svc.rows_scored,
-        "producer_lag_msgs_rank0": store.lag(k.group_id, k.transactions_topic),
+        "producer_lag_msgs_rank0": tx_store.lag(k.group_id, k.transactions_topic),
+        "mode": "consumer-only (pre-filled topic)" if prefill else "producer running",
+        "prefill_producer_tx_s_rank0": round(prefill_rate, 1) if prefill else None,
+        "kafka_nodes": args.kafka_nodes if args.broker == "kafka-lite" else None,
+        "ingest_threads": len(svc.natives) if svc.natives else None,
     }
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)

@@ -61,6 +61,8 @@ class KieConfig:
 class RouterConfig:
     fraud_threshold: float = 0.5                              # FRAUD_THRESHOLD (router.yaml:69-70)
     port: int = 8091                                          # README.md:503-506
+    rules: str = ""                  # ROUTER_RULES: routing rule file or inline rules ("when ... then
+                                     # fraud; otherwise standard"); "" = the reference threshold rule
 
 
 @dataclass
@@ -81,6 +83,7 @@ class EngineConfig:
     input_mode: str = "zerocopy"     # dma (H2D into HBM) | zerocopy (kernel reads pinned host)
     wire: str = "auto"               # ring row format: f32 | w64 | auto (w64 for mlp/lr)
     coalesce: int = 4                # ready micro-batches per kernel launch (MLP, launch mode)
+    ingest_threads: int = 1          # native Kafka consumer threads per rank (partitions split)
     model_watch: str = ""            # hot-swap when this safetensors file changes (rank 0)
     output_mode: str = "zerocopy"    # zerocopy (kernel writes pinned host) | dma
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches
@@ -117,6 +120,7 @@ ENV_MAP = {
     "SELDON_POOL_SIZE": ("seldon", "pool_size", int),
     "CONFIDENCE_THRESHOLD": ("kie", "confidence_threshold", float),
     "FRAUD_THRESHOLD": ("router", "fraud_threshold", float),
+    "ROUTER_RULES": ("router", "rules", str),
     # framework-specific keys
     "CCFD_MODEL": ("engine", "model", str),
     "CCFD_BATCH": ("engine", "batch", int),
@@ -127,6 +131,7 @@ ENV_MAP = {
     "CCFD_INPUT_MODE": ("engine", "input_mode", str),
     "CCFD_OUTPUT_MODE": ("engine", "output_mode", str),
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),
+    "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),
 }
 
 

@@ -127,11 +127,13 @@ class StreamEngine:
     def __init__(self, dm: DeviceModel, batch: int = 4096, depth: int = 8, streams: int = 2,
                  input_mode: str = "dma", output_mode: str = "zerocopy", threshold: float = 0.5,
                  device: Optional[int] = None, flag_capacity: int = 1 << 20, exec_mode: str = "launch",
-                 persist_grid: int = 0, coalesce: int = 1):
+                 persist_grid: int = 0, coalesce: int = 1, rules=None):
         """exec_mode: "launch" = one fused kernel launch per micro-batch; "persistent" = one
         long-running kernel fed through a descriptor ring (MLP/LR, zero-copy outputs).
         coalesce: launch mode -- up to this many ready, log-contiguous micro-batches go out as
-        one launch (MLP, zero-copy in/out); completion stays per micro-batch."""
+        one launch (MLP, zero-copy in/out); completion stays per micro-batch.
+        rules: a compiled routing rule set (ops.kernels.DeviceRules) evaluated per row in the
+        kernels' epilogue instead of ``proba >= threshold`` (kept alive by the engine)."""
         self.dm = dm
         self.device = torch.device("cuda", device if device is not None else torch.cuda.current_device())
         self.batch = int(batch)
@@ -157,6 +159,8 @@ class StreamEngine:
         cfg.wire = 1 if self.wire else 0
         self.exec_mode = exec_mode
         self.flips = 0
+        self.rules = rules
+        cfg.rules = rules.ptr if rules is not None else None
         cfg.counters[0] = self.counters[0].data_ptr()
         cfg.counters[1] = self.counters[1].data_ptr()
         # counters zeroed before the engine's streams use them (stream sync, never a device

@@ -181,3 +181,9 @@ class BatchStore:
     def committed(self, group: str, topic: str, partition: int) -> Optional[int]:
         with self._lock:
             return self._committed.get((group, topic, partition))
+
+    def lag(self, group: str, topic: str) -> int:
+        """Records not yet committed by ``group`` (consumer lag, summed over partitions)."""
+        with self._lock:
+            return sum(L.end - self._committed.get((group, topic, p), L.begin)
+                       for p, L in enumerate(self._topics.get(topic, [])))

@@ -559,8 +559,8 @@ class KafkaLiteCluster:
     event loop over a shared store: leadership p -> node (p % n) + 1 until moved."""
 
     def __init__(self, n: int = 3, host: str = "127.0.0.1", base_port: int = 0, default_partitions: int = 1,
-                 auto_create: bool = True):
-        self.store = BatchStore(default_partitions=default_partitions)
+                 auto_create: bool = True, retention_batches: Optional[int] = None):
+        self.store = BatchStore(default_partitions=default_partitions, retention_batches=retention_batches)
         self.state = ClusterState(self.store)
         self.metrics = BrokerMetrics(self.state)
         self.nodes = [KafkaLiteServer(host, base_port + i if base_port else 0, store=self.store,

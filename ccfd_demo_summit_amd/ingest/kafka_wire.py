@@ -210,10 +210,46 @@ CODEC_NONE, CODEC_GZIP = 0, 1
 _CODEC_NAMES = {1: "gzip", 2: "snappy", 3: "lz4", 4: "zstd"}
 
 
+_native_enc = None
+
+
+def _native_encoder():
+    global _native_enc
+    if _native_enc is None:
+        try:
+            import ctypes as C
+            from ..ops._lib import lib
+            L = lib()
+            L.ccfd_kafka_encode_batch.argtypes = [C.c_char_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64]
+            L.ccfd_kafka_encode_batch.restype = C.c_int64
+            L.ccfd_kafka_batch_bound.argtypes = [C.c_int64, C.c_int64]
+            L.ccfd_kafka_batch_bound.restype = C.c_int64
+            _native_enc = L
+        except Exception:
+            _native_enc = False
+    return _native_enc
+
+
 def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optional[bytes]]] = None,
                         base_offset: int = 0, timestamp_ms: Optional[int] = None,
                         compression: int = CODEC_NONE) -> bytes:
     ts = int(time.time() * 1000) if timestamp_ms is None else timestamp_ms
+    n = len(values)
+    if (n >= 8 and compression == CODEC_NONE and base_offset == 0 and (keys is None or all(k is None for k in keys))
+            and all(v is not None for v in values)):
+        L = _native_encoder()
+        if L:                                   # native framing (csrc/engine/kafka_codec.cpp)
+            import numpy as np
+            buf = b"".join(values)
+            off = np.zeros(n + 1, np.int64)
+            np.cumsum([len(v) for v in values], out=off[1:])
+            out = bytearray(L.ccfd_kafka_batch_bound(n, len(buf)))
+            import ctypes as C
+            ob = (C.c_char * len(out)).from_buffer(out)
+            k = L.ccfd_kafka_encode_batch(buf, off.ctypes.data, n, ts, C.addressof(ob), len(out))
+            if k > 0:
+                del ob
+                return bytes(out[:k])
     recs = []
     for i, v in enumerate(values):
         k = keys[i] if keys is not None else None

@@ -191,7 +191,7 @@ def cmd_router(a, cfg):
     rm = RouterMetrics()
     kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
                     cfg.kie.signal_name)
-    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), kie, rm)
+    router = Router(RuleSet.from_config(cfg.router), kie, rm)
     sc = SeldonClient(cfg.seldon.url, cfg.seldon.endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
                       cfg.seldon.pool_size)
     _serve_in_thread(_metrics_app(rm.expose), a.host, a.port or cfg.router.port)
@@ -246,12 +246,13 @@ def cmd_engine(a, cfg):
     broker = _broker(cfg)
     hub = MetricsHub()
     kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
-    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), kie, hub.router)
+    router = Router(RuleSet.from_config(cfg.router), kie, hub.router)
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
         depth=cfg.engine.depth, streams=cfg.engine.streams, input_mode=cfg.engine.input_mode,
         flush_us=cfg.engine.max_delay_us, reduce_period_ms=cfg.engine.reduce_period_ms,
         threshold=cfg.router.fraud_threshold, coalesce=cfg.engine.coalesce,
+        ingest_threads=cfg.engine.ingest_threads,
         model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.rank)
@@ -352,7 +353,7 @@ def cmd_elastic(a, cfg):
     else:
         sink = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
                          cfg.kie.signal_name)
-    router = Router(RuleSet.threshold(cfg.router.fraud_threshold), sink, rm)
+    router = Router(RuleSet.from_config(cfg.router), sink, rm)
     broker = _broker(cfg)
     leases = PartitionLeases(store, a.rank, a.world, a.partitions, ttl_s=a.ttl)
     worker = ElasticWorker(a.rank, leases, broker, cfg.kafka.transactions_topic, scorer, router,
@@ -395,6 +396,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
                                         "engine", "producer", "demo", "store", "elastic", "supervise"])
     ap.add_argument("--config", default=None)
+    ap.add_argument("--rules", default=None, help="router/engine/demo: routing rule file (overrides ROUTER_RULES)")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--watch-model", default=None, help="engine: hot-swap weights when this file changes")
@@ -435,7 +437,7 @@ def parse_args(argv=None) -> argparse.Namespace:
 
 def main(argv=None):
     a = parse_args(argv)
-    cfg = load_config(a.config)
+    cfg = load_config(a.config, overrides={"router.rules": a.rules} if a.rules else None)
     globals()["cmd_" + a.service.replace("-", "_")](a, cfg)
 
 

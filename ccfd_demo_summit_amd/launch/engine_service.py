@@ -50,6 +50,8 @@ class EngineServiceConfig:
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
     native_ingest: bool = True       # Kafka-protocol brokers: C++ consumer thread fetches and writes
                                      # rows straight into the rings (ingest/native_consumer.py)
+    ingest_threads: int = 1          # native consumers per rank, partitions split between them
+                                     # (one JSON message per transaction is parse-bound per thread)
     score_thread: bool = True        # drive engine.run() from a dedicated thread (GIL released in
                                      # native code) so scoring latency does not wait on the Python
                                      # router / process loop
@@ -64,22 +66,40 @@ class EngineService:
         self.cfg = cfg
         self.broker = broker
         self.router = router
+        # routing rules: the reference threshold rule runs as the kernels' `proba >= T` test;
+        # any other rule set (config router.rules / ROUTER_RULES) is compiled to a device
+        # program interpreted in the same epilogue (router/rules.py, csrc/kernels/rules.h), so
+        # the flagged rows the router receives are already rule-routed
+        self.device_rules = None
+        rules = getattr(router, "rules", None)
+        threshold = cfg.threshold
+        if rules is not None:
+            if rules.threshold_only is not None:
+                threshold = rules.threshold_only
+            else:
+                from ..ops.kernels import DeviceRules
+                self.device_rules = DeviceRules(rules, ctx.device)
         self.engine = StreamEngine(dm, batch=cfg.batch, depth=cfg.depth, streams=cfg.streams,
-                                   input_mode=cfg.input_mode, threshold=cfg.threshold, device=ctx.device.index,
-                                   exec_mode=cfg.exec_mode, coalesce=cfg.coalesce)
+                                   input_mode=cfg.input_mode, threshold=threshold, device=ctx.device.index,
+                                   exec_mode=cfg.exec_mode, coalesce=cfg.coalesce, rules=self.device_rules)
         n_parts = broker.partitions(cfg.topic)
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:
             self.engine.set_ring(p, cfg.ring_rows)
         self.native = None
+        self.natives = []
         if cfg.native_ingest and hasattr(broker, "_bootstrap"):
             from ..ingest.native_consumer import NativeKafkaConsumer
             starts = {}
             for p in self.partitions:
                 c = broker.committed(cfg.group_id, cfg.topic, p)
                 starts[p] = c if c is not None else broker.begin_offset(cfg.topic, p)
-            host, port = broker._bootstrap
-            self.native = NativeKafkaConsumer.for_engine(self.engine, f"{host}:{port}", cfg.topic, starts)
+            seeds = ",".join(f"{h}:{pt}" for h, pt in getattr(broker, "_seeds", [broker._bootstrap]))
+            nt = max(1, min(int(cfg.ingest_threads), len(self.partitions)))
+            for i in range(nt):
+                mine = {p: starts[p] for j, p in enumerate(self.partitions) if j % nt == i}
+                self.natives.append(NativeKafkaConsumer.for_engine(self.engine, seeds, cfg.topic, mine))
+            self.native = self.natives[0]
             self.consumer = None
         else:
             self.consumer = broker.consumer(cfg.group_id, [cfg.topic], partitions=[(cfg.topic, p) for p in self.partitions]) \
@@ -168,8 +188,9 @@ class EngineService:
     # ------------------------------------------------------------------ consumer side
     def _commit_done(self) -> None:
         if self.native is not None:                     # offsets whose rows are all scored
-            for p, off in self.native.committable().items():
-                self.broker.commit(self.cfg.group_id, self.cfg.topic, p, off)
+            for kc in self.natives:
+                for p, off in kc.committable().items():
+                    self.broker.commit(self.cfg.group_id, self.cfg.topic, p, off)
             return
         offs = {}
         for p in self.partitions:
@@ -319,7 +340,8 @@ class EngineService:
     def start(self) -> "EngineService":
         if self.native is not None:
             self._thread = None
-            self.native.start()
+            for kc in self.natives:
+                kc.start()
         else:
             self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")
             self._thread.start()
@@ -331,13 +353,13 @@ class EngineService:
 
     def stop(self) -> None:
         self._stop.set()
-        if self.native is not None:
-            self.native.stop()
+        for kc in self.natives:
+            kc.stop()
         for th in (getattr(self, "_score_thread", None), getattr(self, "_thread", None)):
             if th is not None:
                 th.join(5)
-        if self.native is not None:
-            self.native.close()
+        for kc in self.natives:
+            kc.close()
         self.engine.close()
 
     def metrics_source(self):

@@ -29,7 +29,8 @@ class ScoreArgs(C.Structure):
                 ("blob", C.c_void_p), ("threshold", C.c_float), ("gbdt_trees", C.c_int32),
                 ("gbdt_depth", C.c_int32), ("flags", C.c_int32), ("proba", C.c_void_p),
                 ("route", C.c_void_p), ("counters", C.c_void_p), ("slot_ctl", C.c_void_p),
-                ("flag_idx", C.c_void_p), ("done_rec", C.c_void_p), ("done_seq", C.c_uint64)]
+                ("flag_idx", C.c_void_p), ("done_rec", C.c_void_p), ("done_seq", C.c_uint64),
+                ("rules", C.c_void_p)]
 
 
 class EngineConfig(C.Structure):
@@ -38,7 +39,8 @@ class EngineConfig(C.Structure):
                 ("max_batch", C.c_int32), ("depth", C.c_int32), ("n_streams", C.c_int32),
                 ("input_mode", C.c_int32), ("output_mode", C.c_int32), ("flag_capacity", C.c_int32),
                 ("exec_mode", C.c_int32), ("persist_grid", C.c_int32), ("wire", C.c_int32),
-                ("coalesce", C.c_int32), ("_pad2", C.c_int32), ("counters", C.c_void_p * 2)]
+                ("coalesce", C.c_int32), ("_pad2", C.c_int32), ("counters", C.c_void_p * 2),
+                ("rules", C.c_void_p)]
 
 
 class Flagged(C.Structure):

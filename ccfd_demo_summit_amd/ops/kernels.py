@@ -45,6 +45,21 @@ class DeviceModel:
         return MODEL_IDS[self.kind]
 
 
+class DeviceRules:
+    """A compiled routing rule set resident in HBM (``RuleSet.device_program``); pass it to
+    ``score(..., rules=)`` / ``StreamEngine(rules=)`` and the kernels' epilogue routes by the
+    rules instead of ``proba >= threshold``."""
+
+    def __init__(self, ruleset, device: torch.device | str | int = "cuda"):
+        self.ruleset = ruleset
+        prog = np.frombuffer(ruleset.device_program(), np.uint8)
+        self.prog = torch.from_numpy(prog.copy()).to(device)
+
+    @property
+    def ptr(self) -> int:
+        return self.prog.data_ptr()
+
+
 def new_counters(device="cuda") -> torch.Tensor:
     return torch.zeros(N_COUNTER_SLOTS, dtype=torch.int64, device=device)
 
@@ -52,7 +67,7 @@ def new_counters(device="cuda") -> torch.Tensor:
 def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
           proba: Optional[torch.Tensor] = None, route: Optional[torch.Tensor] = None,
           counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None,
-          flags: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+          flags: int = 0, rules: Optional[DeviceRules] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused score of x [n,30] (float32, CUDA) -- or, for a ``wire`` model, W64 rows
     ([n,64] uint8 or [n,16] float32 view) -- returns (proba_1 [n] f32, route [n] u8).
     ``flags``: extra ``CCFD_ARG_*`` bits (ablation switches for profiling)."""
@@ -82,6 +97,7 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
     a.proba = proba.data_ptr()
     a.route = route.data_ptr()
     a.counters = counters.data_ptr() if counters is not None else None
+    a.rules = rules.ptr if rules is not None else None
     s = stream if stream is not None else torch.cuda.current_stream(x.device)
     check(lib().ccfd_score_launch(C.byref(a), C.c_void_p(s.cuda_stream)), "ccfd_score_launch")
     return proba, route

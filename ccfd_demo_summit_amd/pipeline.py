@@ -56,7 +56,7 @@ class FraudPipeline:
             cfg.kie.notification_timeout_s, cfg.kie.dmn_probability_threshold, cfg.kie.dmn_amount_threshold,
             publish_notification=self._publish_notification, kie_metrics=self.metrics.kie,
             prediction=PredictionService(cfg.kie.confidence_threshold), clock=clock, journal_path=journal_path)
-        self.router = Router(rules or RuleSet.threshold(cfg.router.fraud_threshold), self.processes,
+        self.router = Router(rules or RuleSet.from_config(cfg.router), self.processes,
                              self.metrics.router)
         self.notifier = NotificationService(self._publish_response, cfg.notifier.p_reply, cfg.notifier.p_approve,
                                             cfg.notifier.mean_delay_s, cfg.notifier.seed, clock)

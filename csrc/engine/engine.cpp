@@ -315,6 +315,7 @@ class Engine {
     a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | (cfg.wire ? CCFD_ARG_WIRE_W64 : 0);
     a.model = cfg.model;
     a.threshold = cfg.threshold;
+    a.rules = cfg.rules;
     a.blob = cfg.blob;
     a.counters[0] = cfg.counters[0];
     a.counters[1] = cfg.counters[1];
@@ -544,6 +545,7 @@ class Engine {
         xk = s.d_x;
       }
       if (!prunning) { int rc = persist_launch(); if (rc) return rc; }
+      s.rows = rows;                    // the descriptor's row count (score_sync does not set it)
       persist_post(s, xk);
       s.busy = true;
       return 0;
@@ -556,6 +558,7 @@ class Engine {
     ccfd_score_args a{};
     a.x = xk; a.ld = rowf; a.n = rows; a.model = cfg.model; a.blob = cfg.blob;
     a.threshold = cfg.threshold; a.gbdt_trees = cfg.gbdt_trees; a.gbdt_depth = cfg.gbdt_depth;
+    a.rules = cfg.rules;
     a.proba = cfg.output_mode == 1 ? s.d_proba : s.h_proba_dev;
     a.route = cfg.output_mode == 1 ? s.d_route : s.h_route_dev;
     a.counters = cfg.counters[epoch & 1];
@@ -601,6 +604,7 @@ class Engine {
     a.x = P.feats_dev + (size_t)start * rowf;
     a.ld = rowf; a.n = K * rows; a.model = cfg.model; a.blob = cfg.blob;
     a.threshold = cfg.threshold;
+    a.rules = cfg.rules;
     a.counters = cfg.counters[epoch & 1];
     a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate |
               (cfg.wire ? CCFD_ARG_WIRE_W64 : 0);

@@ -38,6 +38,36 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_ABLATE_OUTPUTS 32    // no proba/route stores
 #define CCFD_ARG_ABLATE_FENCE 64      // no per-workgroup system release
 
+// Routing rule program (router/rules.py RuleSet.device_program): the configurable routing
+// rules (reference "Drools rules", README.md:427) evaluated per row in the scoring
+// kernels' epilogue instead of the plain `proba >= threshold` test.  Postfix code over a
+// <= CCFD_RULE_MAX_STACK-deep f32 stack; rules are tried in order, the first whose
+// condition holds decides the route, DEFAULT applies otherwise.  Variables: 0 = proba_1,
+// 1 + j = feature j in reference column order (Time, V1..V28, Amount).
+#define CCFD_RULE_MAX_OPS 48
+#define CCFD_RULE_MAX_STACK 8
+enum ccfd_rule_opcode {
+  CCFD_RULE_END = 0,     // pop cond; first true rule sets route = arg
+  CCFD_RULE_VAR = 1,     // push variable arg
+  CCFD_RULE_CONST = 2,   // push imm
+  CCFD_RULE_ADD = 3, CCFD_RULE_SUB = 4, CCFD_RULE_MUL = 5, CCFD_RULE_DIV = 6,
+  CCFD_RULE_NEG = 7, CCFD_RULE_ABS = 8, CCFD_RULE_LOG1P = 9, CCFD_RULE_MIN = 10, CCFD_RULE_MAX = 11,
+  CCFD_RULE_GT = 12, CCFD_RULE_GE = 13, CCFD_RULE_LT = 14, CCFD_RULE_LE = 15, CCFD_RULE_EQ = 16,
+  CCFD_RULE_NE = 17, CCFD_RULE_AND = 18, CCFD_RULE_OR = 19, CCFD_RULE_NOT = 20
+};
+typedef struct ccfd_rule_op {
+  int16_t op;
+  int16_t arg;
+  float imm;
+} ccfd_rule_op;
+typedef struct ccfd_rule_prog {   // device memory
+  int32_t n_ops;
+  int32_t default_route;          // 1 = fraud, 0 = standard
+  int32_t n_rules;
+  int32_t max_stack;
+  ccfd_rule_op ops[CCFD_RULE_MAX_OPS];
+} ccfd_rule_prog;
+
 typedef struct ccfd_score_args {
   const float* x;        // features, row-major [n][ld] (device or host-mapped pointer)
   int64_t ld;            // row stride in floats (fast path: 30)
@@ -61,6 +91,7 @@ typedef struct ccfd_score_args {
   unsigned int* flag_idx;        // host-mapped [n] row indices of fraud-routed rows
   unsigned long long* done_rec;  // host-mapped coherent [4]: seq, #flagged, t_start, t_end
   unsigned long long done_seq;
+  const ccfd_rule_prog* rules;   // device; NULL = route by `proba >= threshold`
 } ccfd_score_args;
 
 // Coalesced launch: `nsub` consecutive micro-batches of `sub_rows` rows (contiguous in x,
@@ -141,6 +172,7 @@ typedef struct ccfd_persist_args {
   int32_t flags;                   // CCFD_ARG_* (informational)
   const void* blob;
   unsigned long long* counters[2];
+  const ccfd_rule_prog* rules;     // device; NULL = threshold route
 } ccfd_persist_args;
 
 int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* stream);
@@ -171,6 +203,7 @@ typedef struct ccfd_engine_config {
   int32_t coalesce;            // launch mode: up to this many ready micro-batches per launch (<= 8)
   int32_t _pad2;
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
+  const ccfd_rule_prog* rules;      // device rule program (owned by caller); NULL = threshold
 } ccfd_engine_config;
 
 typedef struct ccfd_flagged {

@@ -16,6 +16,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "rules.h"
 
 namespace ccfd {
 
@@ -62,7 +63,7 @@ __device__ __forceinline__ void gb_store(float (*xs)[kGbRows], int tid, const Gb
 // fetching before this one drains (one workgroup per chunk filled every CU slot with
 // workgroups waiting on PCIe and serialised consecutive batches).  The leaf tables are
 // staged into LDS once per workgroup when they fit (T * 2^D <= 16384 floats).
-template <int D, bool kContig>
+template <int D, bool kContig, bool kR>
 __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a, int cpw) {
   constexpr int L = 1 << D;
   __shared__ __attribute__((aligned(16))) float xs[kF][kGbRows];
@@ -145,7 +146,10 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a, int 
       const float z = base + part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
       const float p = sigmoid(z);
       const bool valid = lane < nrows;
-      const bool fr = valid && (p >= a.threshold);
+      // configurable routing rules: row = lane, its features are column xs[*][lane]
+      bool fr;
+      if constexpr (kR) fr = valid && rule_route(a.rules, p, [&](int j) { return xs[j][lane]; });
+      else fr = valid && (p >= a.threshold);
       const int row = row0 + lane;
       if (valid) {
         if (a.proba) a.proba[row] = p;
@@ -184,7 +188,7 @@ constexpr int kGb2Waves = 4;
 #endif
 constexpr int kGbTb = CCFD_GBDT_TREE_BLOCK;    // trees whose split parameters are loaded together
 
-template <int D, int R>
+template <int D, int R, bool kR>
 __global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
   constexpr int L = 1 << D;
   __shared__ __attribute__((aligned(16))) float xs[kGb2Waves][kF][kGbRows + 1];
@@ -321,7 +325,9 @@ __global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
       const int row = (grp * R + q) * kGbRows + lane;
       const bool valid = row < n;
       const float p = sigmoid(base + acc[q]);
-      const bool fr = valid && (p >= a.threshold);
+      bool fr;
+      if constexpr (kR) fr = valid && rule_route(a.rules, p, [&](int j) { return q == 0 ? x0[j] : x1[j]; });
+      else fr = valid && (p >= a.threshold);
       if (valid) {
         if (a.proba) a.proba[row] = p;
         if (a.route) a.route[row] = fr ? 1 : 0;
@@ -364,7 +370,7 @@ static int gbdt_forced_kernel() {   // 0 = by size, 1 = v1, 2 = v2
   return v;
 }
 
-template <int D, int R>
+template <int D, int R, bool kR>
 static void launch_v2(const ccfd_score_args& a, hipStream_t s) {
   constexpr int L = 1 << D;
   const int nchunks = (a.n + kGbRows - 1) / kGbRows;
@@ -373,13 +379,14 @@ static void launch_v2(const ccfd_score_args& a, hipStream_t s) {
   const int cap = 256 * 2;                 // two resident workgroups per CU (LDS: staging + leaves)
   grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
   const size_t lds = (size_t)a.gbdt_trees * L * sizeof(float);
-  hipLaunchKernelGGL((score_gbdt_v2_kernel<D, R>), dim3(grid), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((score_gbdt_v2_kernel<D, R, kR>), dim3(grid), dim3(256), lds, s, a);
 }
 
 template <int D>
 static void launch_d2(const ccfd_score_args& a, hipStream_t s) {
-  if (gbdt_v2_rows() == 1) launch_v2<D, 1>(a, s);
-  else launch_v2<D, 2>(a, s);
+  const bool r = a.rules != nullptr;
+  if (gbdt_v2_rows() == 1) { if (r) launch_v2<D, 1, true>(a, s); else launch_v2<D, 1, false>(a, s); }
+  else { if (r) launch_v2<D, 2, true>(a, s); else launch_v2<D, 2, false>(a, s); }
 }
 
 // CCFD_GBDT_CPW: 64-row chunks per workgroup.  Default: a ~256-workgroup grid (one per CU;
@@ -403,10 +410,15 @@ static void launch_d(const ccfd_score_args& a, hipStream_t s, bool contig) {
   const int cpw = gbdt_chunks_per_wg(nchunks);
   const int grid = (nchunks + cpw - 1) / cpw;
   const size_t lds = (size_t)min(a.gbdt_trees, kLeafLds / L) * L * sizeof(float);
-  if (contig)
-    hipLaunchKernelGGL((score_gbdt_kernel<D, true>), dim3(grid), dim3(256), lds, s, a, cpw);
+  const bool r = a.rules != nullptr;    // routing rules: separate instantiation (register budget)
+  if (contig && r)
+    hipLaunchKernelGGL((score_gbdt_kernel<D, true, true>), dim3(grid), dim3(256), lds, s, a, cpw);
+  else if (contig)
+    hipLaunchKernelGGL((score_gbdt_kernel<D, true, false>), dim3(grid), dim3(256), lds, s, a, cpw);
+  else if (r)
+    hipLaunchKernelGGL((score_gbdt_kernel<D, false, true>), dim3(grid), dim3(256), lds, s, a, cpw);
   else
-    hipLaunchKernelGGL((score_gbdt_kernel<D, false>), dim3(grid), dim3(256), lds, s, a, cpw);
+    hipLaunchKernelGGL((score_gbdt_kernel<D, false, false>), dim3(grid), dim3(256), lds, s, a, cpw);
 }
 
 int launch_gbdt(const ccfd_score_args& a, hipStream_t s) {

@@ -17,7 +17,7 @@ int mlp_waves_for(int ntiles);     // score_mlp.hip (same policy and CCFD_MLP_WA
 int mlp_tiles_per_wave_policy();   // score_mlp.hip (CCFD_MLP_TPW)
 
 // f32 rows, kMode as in score_mlp.hip: 0 strided, 1 contiguous (W64 rows: LrWireScorer below)
-template <int kMode, int kLrWaves>
+template <int kMode, int kLrWaves, bool kR>
 __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int nblk) {
   constexpr bool kContig = kMode == 1;
   static_assert(kMode != 2, "W64 rows use wire_stream_body");
@@ -80,7 +80,13 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
     z += __shfl_xor(z, 16);
     z += __shfl_xor(z, 32);
     const float p = sigmoid(z + b);
-    const bool fr = valid && (p >= a.threshold);
+    bool fr;
+    if constexpr (kR) {                                 // configurable routing rules (rules.h)
+      if (g == 3) xv[5] = amount;
+      fr = valid && rule_route(a.rules, __shfl(p, c), [&](int j) { return lane_feature<false>(xv, j, c); });
+    } else {
+      fr = valid && (p >= a.threshold);
+    }
     if (valid && g == 0) {
       if (a.proba) a.proba[row] = p;
       if (a.route) a.route[row] = fr ? 1 : 0;
@@ -101,18 +107,18 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
   signal_done(a, (unsigned)nblk);
 }
 
-template <int kMode, int kLrWaves>
+template <int kMode, int kLrWaves, bool kR>
 __global__ __launch_bounds__(64 * kLrWaves) void score_lr_kernel(ccfd_score_args a) {
-  lr_body<kMode, kLrWaves>(a, blockIdx.x, gridDim.x);
+  lr_body<kMode, kLrWaves, kR>(a, blockIdx.x, gridDim.x);
 }
 
-template <int kMode, int kLrWaves>
+template <int kMode, int kLrWaves, bool kR>
 __global__ __launch_bounds__(64 * kLrWaves) void score_lr_multi_kernel(ccfd_multi_args m) {
   (void)m;   // table read through the kernarg segment (see score_mlp_multi_kernel)
   const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
   const int wpb = gridDim.x / mk.nsub;
   const int j = blockIdx.x / wpb;
-  lr_body<kMode, kLrWaves>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+  lr_body<kMode, kLrWaves, kR>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
 
@@ -163,18 +169,18 @@ struct LrWireScorer {
   }
 };
 
-template <int kLrWaves, int kPf>
+template <int kLrWaves, int kPf, bool kR>
 __global__ __launch_bounds__(64 * kLrWaves) void score_lr_wire_kernel(ccfd_score_args a) {
-  wire_stream_body<LrWireScorer, kLrWaves, kPf>(a, blockIdx.x, gridDim.x);
+  wire_stream_body<LrWireScorer, kLrWaves, kPf, kR>(a, blockIdx.x, gridDim.x);
 }
 
-template <int kLrWaves, int kPf>
+template <int kLrWaves, int kPf, bool kR>
 __global__ __launch_bounds__(64 * kLrWaves) void score_lr_wire_multi_kernel(ccfd_multi_args m) {
   (void)m;
   const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
   const int wpb = gridDim.x / mk.nsub;
   const int j = blockIdx.x / wpb;
-  wire_stream_body<LrWireScorer, kLrWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+  wire_stream_body<LrWireScorer, kLrWaves, kPf, kR>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
 // CCFD_LR_PF: W64 tiles in flight per wave (2, 4, 8; default 4).  CCFD_LR_OCC: resident
@@ -194,30 +200,30 @@ static int lr_wire_occupancy() {
   return v;
 }
 
-template <int kW>
+template <int kW, bool kR>
 static void launch_lr_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
   switch (lr_wire_prefetch()) {
-    case 2: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
-    default: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 8>), grid, dim3(64 * kW), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 2, kR>), grid, dim3(64 * kW), 0, s, a); break;
+    default: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 4, kR>), grid, dim3(64 * kW), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((score_lr_wire_kernel<kW, 8, kR>), grid, dim3(64 * kW), 0, s, a); break;
   }
 }
 
-template <int kW>
+template <int kW, bool kR>
 static void launch_lr_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   const int per_wg = kW * mlp_tiles_per_wave_policy();
   int grid = (ntiles + per_wg - 1) / per_wg;
   if (a.flags & CCFD_ARG_WIRE_W64) {
     const int cap = 256 * 4 * lr_wire_occupancy() / kW;   // one chip residency, grid-stride beyond
     grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
-    launch_lr_wire<kW>(dim3(grid), s, a);
+    launch_lr_wire<kW, kR>(dim3(grid), s, a);
     return;
   }
   grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
   if (contig)
-    hipLaunchKernelGGL((score_lr_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    hipLaunchKernelGGL((score_lr_kernel<1, kW, kR>), dim3(grid), dim3(64 * kW), 0, s, a);
   else
-    hipLaunchKernelGGL((score_lr_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    hipLaunchKernelGGL((score_lr_kernel<0, kW, kR>), dim3(grid), dim3(64 * kW), 0, s, a);
 }
 
 // CCFD_LR_WAVES: waves per workgroup of the W64 single launch (4, 8, 16; default 16 -- one
@@ -228,35 +234,45 @@ static int lr_wire_waves() {
   return v;
 }
 
-int launch_lr(const ccfd_score_args& a, hipStream_t s) {
+template <bool kR>
+static int launch_lr_t(const ccfd_score_args& a, hipStream_t s) {
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
   if (a.flags & CCFD_ARG_WIRE_W64) {
     switch (lr_wire_waves()) {
-      case 4: launch_lr_w<4>(a, ntiles, contig, s); break;
-      case 8: launch_lr_w<8>(a, ntiles, contig, s); break;
-      default: launch_lr_w<16>(a, ntiles, contig, s); break;
+      case 4: launch_lr_w<4, kR>(a, ntiles, contig, s); break;
+      case 8: launch_lr_w<8, kR>(a, ntiles, contig, s); break;
+      default: launch_lr_w<16, kR>(a, ntiles, contig, s); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }
   switch (mlp_waves_for(ntiles)) {
-    case 1: launch_lr_w<1>(a, ntiles, contig, s); break;
-    case 2: launch_lr_w<2>(a, ntiles, contig, s); break;
-    default: launch_lr_w<4>(a, ntiles, contig, s); break;
+    case 1: launch_lr_w<1, kR>(a, ntiles, contig, s); break;
+    case 2: launch_lr_w<2, kR>(a, ntiles, contig, s); break;
+    default: launch_lr_w<4, kR>(a, ntiles, contig, s); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_lr_multi(const ccfd_multi_args& m, hipStream_t s) {
+int launch_lr(const ccfd_score_args& a, hipStream_t s) {
+  return a.rules ? launch_lr_t<true>(a, s) : launch_lr_t<false>(a, s);
+}
+
+template <bool kR>
+static int launch_lr_multi_t(const ccfd_multi_args& m, hipStream_t s) {
   constexpr int kW = 4;
   const int rows_per_wg = kTileRows * kW * mlp_tiles_per_wave_policy();
   const int wpb = (m.sub_rows + rows_per_wg - 1) / rows_per_wg;
   const dim3 grid(wpb * m.nsub), block(64 * kW);
   if (m.base.flags & CCFD_ARG_WIRE_W64)
-    hipLaunchKernelGGL((score_lr_wire_multi_kernel<kW, 4>), grid, block, 0, s, m);
+    hipLaunchKernelGGL((score_lr_wire_multi_kernel<kW, 4, kR>), grid, block, 0, s, m);
   else
-    hipLaunchKernelGGL((score_lr_multi_kernel<1, kW>), grid, block, 0, s, m);
+    hipLaunchKernelGGL((score_lr_multi_kernel<1, kW, kR>), grid, block, 0, s, m);
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_lr_multi(const ccfd_multi_args& m, hipStream_t s) {
+  return m.base.rules ? launch_lr_multi_t<true>(m, s) : launch_lr_multi_t<false>(m, s);
 }
 
 }  // namespace ccfd

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "mlp_core.h"
+#include "rules.h"
 #include "wire_body.h"
 
 namespace ccfd {
@@ -34,7 +35,7 @@ namespace ccfd {
 // coalesced launch: workgroup `blk` of the `nblk` that score micro-batch `a`.  Entry points
 // ask for >= 4 waves per SIMD (<= 128 VGPRs): occupancy (outstanding zero-copy loads) beats
 // hoisting the 24 weight fragments into registers.
-template <int kMode, int kWaves>
+template <int kMode, int kWaves, bool kR>
 __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int nblk) {
   constexpr bool kContig = (kMode & 3) == 1;
   constexpr bool kGW = (kMode & 4) != 0;     // weights read from global (L1/L2), no LDS copy
@@ -92,7 +93,13 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
     }
     float amount;
     const float p = mlp_tile(W, L, xv, g, lane, amount);
-    const bool fr = valid && (p >= thr);
+    bool fr;
+    if constexpr (kR) {                                 // configurable routing rules (rules.h)
+      if (g == 3) xv[5] = amount;                       // mlp_tile replaced Amount by its log1p
+      fr = valid && rule_route(a.rules, __shfl(p, c), [&](int j) { return lane_feature<false>(xv, j, c); });
+    } else {
+      fr = valid && (p >= thr);
+    }
 
     if (valid && g == 0) {
       if (!(a.flags & CCFD_ARG_ABLATE_OUTPUTS)) {
@@ -116,26 +123,26 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
   signal_done(a, (unsigned)nblk);
 }
 
-template <int kMode, int kWaves>
+template <int kMode, int kWaves, bool kR>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_kernel(ccfd_score_args a) {
-  mlp_body<kMode, kWaves>(a, blockIdx.x, gridDim.x);
+  mlp_body<kMode, kWaves, kR>(a, blockIdx.x, gridDim.x);
 }
 
-template <int kWaves, int kPf>
+template <int kWaves, int kPf, bool kR>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_wire_kernel(ccfd_score_args a) {
-  wire_stream_body<MlpWireScorer, kWaves, kPf>(a, blockIdx.x, gridDim.x);
+  wire_stream_body<MlpWireScorer, kWaves, kPf, kR>(a, blockIdx.x, gridDim.x);
 }
 
-template <int kWaves, int kPf>
+template <int kWaves, int kPf, bool kR>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(2)))
 void score_mlp_wire_reg_kernel(ccfd_score_args a) {
-  wire_stream_body<MlpWireRegScorer, kWaves, kPf>(a, blockIdx.x, gridDim.x);
+  wire_stream_body<MlpWireRegScorer, kWaves, kPf, kR>(a, blockIdx.x, gridDim.x);
 }
 
 // Coalesced launch: workgroups [j*wpb, (j+1)*wpb) score sub-batch j.
-template <int kMode, int kWaves>
+template <int kMode, int kWaves, bool kR>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_multi_kernel(ccfd_multi_args m) {
   // read the table through the kernarg segment pointer: indexing the by-value parameter
@@ -144,17 +151,17 @@ void score_mlp_multi_kernel(ccfd_multi_args m) {
   const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
   const int wpb = gridDim.x / mk.nsub;                 // workgroups per sub-batch
   const int j = blockIdx.x / wpb;
-  mlp_body<kMode, kWaves>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+  mlp_body<kMode, kWaves, kR>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
-template <int kWaves, int kPf>
+template <int kWaves, int kPf, bool kR>
 __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(4)))
 void score_mlp_wire_multi_kernel(ccfd_multi_args m) {
   (void)m;
   const ccfd_multi_args& mk = *(const ccfd_multi_args*)__builtin_amdgcn_kernarg_segment_ptr();
   const int wpb = gridDim.x / mk.nsub;
   const int j = blockIdx.x / wpb;
-  wire_stream_body<MlpWireScorer, kWaves, kPf>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
+  wire_stream_body<MlpWireScorer, kWaves, kPf, kR>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
 // CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4; default 2 = one tile pair, measured
@@ -179,21 +186,21 @@ static bool mlp_reg_weights() {
   return v;
 }
 
-template <int kW>
+template <int kW, bool kR>
 static void launch_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
   if (kW <= 8 && mlp_reg_weights()) {     // 2 waves/SIMD: at most 8 waves per workgroup
     const int cap = 256 * 8 / kW;          // 2 waves/SIMD residency
     if ((int)grid.x > cap) grid.x = cap;
     switch (mlp_wire_prefetch()) {
-      case 4: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
-      default: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
+      case 4: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 4, kR>), grid, dim3(64 * kW), 0, s, a); break;
+      default: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 2, kR>), grid, dim3(64 * kW), 0, s, a); break;
     }
     return;
   }
   switch (mlp_wire_prefetch()) {
-    case 1: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 1>), grid, dim3(64 * kW), 0, s, a); break;
-    default: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 2>), grid, dim3(64 * kW), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 4>), grid, dim3(64 * kW), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 1, kR>), grid, dim3(64 * kW), 0, s, a); break;
+    default: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 2, kR>), grid, dim3(64 * kW), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((score_mlp_wire_kernel<kW, 4, kR>), grid, dim3(64 * kW), 0, s, a); break;
   }
 }
 
@@ -222,7 +229,7 @@ static bool mlp_global_weights() {
   return gw;
 }
 
-template <int kW>
+template <int kW, bool kR>
 static void launch_w(const ccfd_score_args& a, int ntiles, bool contig, hipStream_t s) {
   const int per_wg = kW * mlp_tiles_per_wave();
   int grid = (ntiles + per_wg - 1) / per_wg;
@@ -233,12 +240,12 @@ static void launch_w(const ccfd_score_args& a, int ntiles, bool contig, hipStrea
   grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
   const bool gw = mlp_global_weights();
   if (a.flags & CCFD_ARG_WIRE_W64) {
-    launch_wire<kW>(dim3(grid), s, a);
+    launch_wire<kW, kR>(dim3(grid), s, a);
   } else if (contig) {
-    if (gw) hipLaunchKernelGGL((score_mlp_kernel<5, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
-    else hipLaunchKernelGGL((score_mlp_kernel<1, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    if (gw) hipLaunchKernelGGL((score_mlp_kernel<5, kW, kR>), dim3(grid), dim3(64 * kW), 0, s, a);
+    else hipLaunchKernelGGL((score_mlp_kernel<1, kW, kR>), dim3(grid), dim3(64 * kW), 0, s, a);
   } else {
-    hipLaunchKernelGGL((score_mlp_kernel<0, kW>), dim3(grid), dim3(64 * kW), 0, s, a);
+    hipLaunchKernelGGL((score_mlp_kernel<0, kW, kR>), dim3(grid), dim3(64 * kW), 0, s, a);
   }
 }
 
@@ -252,7 +259,8 @@ int mlp_waves_for(int ntiles) {
   return 4;   // measured: 1-wave workgroups lose (per-workgroup weight staging + completion)
 }
 
-int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
+template <bool kR>
+static int launch_mlp_multi_t(const ccfd_multi_args& m, hipStream_t s) {
   constexpr int kW = 4;
   const int rows_per_wg = kTileRows * kW * mlp_tiles_per_wave();
   const int wpb = (m.sub_rows + rows_per_wg - 1) / rows_per_wg;
@@ -260,15 +268,19 @@ int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
   const bool gw = mlp_global_weights();
   if (m.base.flags & CCFD_ARG_WIRE_W64) {
     switch (mlp_wire_prefetch()) {
-      case 1: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 1>), grid, block, 0, s, m); break;
-      default: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 2>), grid, block, 0, s, m); break;
-      case 4: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 4>), grid, block, 0, s, m); break;
+      case 1: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 1, kR>), grid, block, 0, s, m); break;
+      default: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 2, kR>), grid, block, 0, s, m); break;
+      case 4: hipLaunchKernelGGL((score_mlp_wire_multi_kernel<kW, 4, kR>), grid, block, 0, s, m); break;
     }
   } else {
-    if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<5, kW>), grid, block, 0, s, m);
-    else hipLaunchKernelGGL((score_mlp_multi_kernel<1, kW>), grid, block, 0, s, m);
+    if (gw) hipLaunchKernelGGL((score_mlp_multi_kernel<5, kW, kR>), grid, block, 0, s, m);
+    else hipLaunchKernelGGL((score_mlp_multi_kernel<1, kW, kR>), grid, block, 0, s, m);
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s) {
+  return m.base.rules ? launch_mlp_multi_t<true>(m, s) : launch_mlp_multi_t<false>(m, s);
 }
 
 // Waves per workgroup of the W64 single launch: CCFD_MLP_WAVES when set, else 8 -- half the
@@ -279,7 +291,8 @@ static int mlp_wire_waves(int ntiles) {
   return forced ? mlp_waves_for(ntiles) : 8;
 }
 
-int launch_mlp(const ccfd_score_args& a, hipStream_t s) {
+template <bool kR>
+static int launch_mlp_t(const ccfd_score_args& a, hipStream_t s) {
   const int ntiles = (a.n + kTileRows - 1) / kTileRows;
   const bool contig = a.ld == kF && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
   const int w = (a.flags & CCFD_ARG_WIRE_W64) ? mlp_wire_waves(ntiles) : mlp_waves_for(ntiles);
@@ -290,16 +303,20 @@ int launch_mlp(const ccfd_score_args& a, hipStream_t s) {
     int grid = (ntiles + per_wg - 1) / per_wg;
     const int cap = 256 * 16 / w;
     grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
-    if (w == 8) launch_wire<8>(dim3(grid), s, a);
-    else launch_wire<16>(dim3(grid), s, a);
+    if (w == 8) launch_wire<8, kR>(dim3(grid), s, a);
+    else launch_wire<16, kR>(dim3(grid), s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }
   switch (w) {
-    case 1: launch_w<1>(a, ntiles, contig, s); break;
-    case 2: launch_w<2>(a, ntiles, contig, s); break;
-    default: launch_w<4>(a, ntiles, contig, s); break;
+    case 1: launch_w<1, kR>(a, ntiles, contig, s); break;
+    case 2: launch_w<2, kR>(a, ntiles, contig, s); break;
+    default: launch_w<4, kR>(a, ntiles, contig, s); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_mlp(const ccfd_score_args& a, hipStream_t s) {
+  return a.rules ? launch_mlp_t<true>(a, s) : launch_mlp_t<false>(a, s);
 }
 
 }  // namespace ccfd

@@ -21,12 +21,13 @@
 // b % R before observing done for b - R, which is what makes the slot-local state
 // (remaining/nflag reset by the last ticket) safe to reuse.
 #include "mlp_core.h"
+#include "rules.h"
 
 namespace ccfd {
 
 namespace {
 
-template <int kModel>
+template <int kModel, bool kR>
 __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   __shared__ __attribute__((aligned(16))) char sblob[kMlpBlobWire];
   __shared__ __attribute__((aligned(16))) float sx[4][kTileRows * kF + 4];
@@ -211,7 +212,22 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
         z += __shfl_xor(z, 32);
         p = sigmoid(z + L.b3);
       }
-      const bool fr = valid && (p >= a.threshold);
+      bool fr;
+      if constexpr (kR) {                               // configurable routing rules (rules.h)
+        float xr[8];
+        if (wire) {
+          wire_features(cur_w, g, xr);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xr[j] = xv[j];
+          if (g == 3) xr[5] = amount;                   // the model replaced Amount by its log1p
+        }
+        const float pr = __shfl(p, c);
+        fr = valid && (wire ? rule_route(a.rules, pr, [&](int j) { return lane_feature<true>(xr, j, c); })
+                            : rule_route(a.rules, pr, [&](int j) { return lane_feature<false>(xr, j, c); }));
+      } else {
+        fr = valid && (p >= a.threshold);
+      }
       if (valid && g == 0) {
         if (sdesc.proba) sdesc.proba[row] = p;
         if (sdesc.route) sdesc.route[row] = fr ? 1 : 0;
@@ -288,11 +304,15 @@ extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* s
   if (!a || !a->ctl || !a->desc || !a->dev || !a->blob) return -1;
   if (a->ring <= 0 || a->ring > CCFD_PERSIST_MAX_RING || a->items_per_batch <= 0 || a->tiles_per_wave <= 0) return -2;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (a->model == CCFD_MODEL_MLP)
-    hipLaunchKernelGGL(persist_kernel<CCFD_MODEL_MLP>, dim3(grid), dim3(256), 0, s, *a);
-  else if (a->model == CCFD_MODEL_LR)
-    hipLaunchKernelGGL(persist_kernel<CCFD_MODEL_LR>, dim3(grid), dim3(256), 0, s, *a);
-  else
+  // routing rules: separate instantiations, so threshold-only kernels keep their registers
+  if (a->model == CCFD_MODEL_MLP) {
+    if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, true>), dim3(grid), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, false>), dim3(grid), dim3(256), 0, s, *a);
+  } else if (a->model == CCFD_MODEL_LR) {
+    if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_LR, true>), dim3(grid), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_LR, false>), dim3(grid), dim3(256), 0, s, *a);
+  } else {
     return -3;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -7,6 +7,7 @@
 //   float tile(const char* lds, const WireRegs&, int g, int lane) const;   proba_1 of row lane&15
 #pragma once
 #include "common.h"
+#include "rules.h"
 
 namespace ccfd {
 
@@ -16,7 +17,9 @@ namespace ccfd {
 // scored) and the steady-state loop is unrolled kPf times over static ring slots, so no
 // register copy of an in-flight load -- which would force an s_waitcnt vmcnt(0) -- is ever
 // needed; only the < kPf-tile tail rotates the ring.
-template <class Scorer, int kWaves, int kPf>
+// kR: the launch carries a routing rule program (a.rules); instantiated separately so the
+// threshold-only kernels keep their register allocation.
+template <class Scorer, int kWaves, int kPf, bool kR = false>
 __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int blk, int nblk) {
   __shared__ __attribute__((aligned(16))) char lds[Scorer::kLds > 0 ? Scorer::kLds : 16];
   __shared__ EpilogueLds epi;
@@ -48,10 +51,22 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
   unsigned long long psum = 0;
   HistLanes hl;
   hist_lanes_init(hl, g);
-  auto finish = [&](float p, float amount, int t) __attribute__((always_inline)) {
+  // routing rules (when configured) read the tile's features, so they are evaluated while
+  // the tile's registers are still live -- before its ring slot is refilled
+  const ccfd_rule_prog* rules = a.rules;
+  auto rule_of = [&](const WireRegs& r, float p) __attribute__((always_inline)) {
+    if constexpr (kR) {
+      float xv[8];
+      wire_features(r, g, xv);
+      return rule_route(rules, __shfl(p, c), [&](int j) { return lane_feature<true>(xv, j, c); });
+    } else {
+      return false;
+    }
+  };
+  auto finish = [&](float p, float amount, int t, bool rf) __attribute__((always_inline)) {
     const int row = t * kTileRows + c;
     const bool valid = row < n;
-    const bool fr = valid && (p >= thr);
+    const bool fr = valid && (kR ? rf : (p >= thr));
     if (valid && g == 0) {
       if (store_out) {
         if (a.proba) a.proba[row] = p;
@@ -78,10 +93,12 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
         const float am0 = __uint_as_float(ring[k].v.w), am1 = __uint_as_float(ring[k + 1].v.w);
         float p0, p1;
         sc.tile2(lds, ring[k], ring[k + 1], g, lane, p0, p1);
+        const bool rf0 = rule_of(ring[k], p0);
+        const bool rf1 = rule_of(ring[k + 1], p1);
         issue(tile + kPf * tstride, ring[k]);
         issue(tile + (kPf + 1) * tstride, ring[k + 1]);
-        finish(p0, am0, tile);
-        finish(p1, am1, tile + tstride);
+        finish(p0, am0, tile, rf0);
+        finish(p1, am1, tile + tstride, rf1);
         tile += 2 * tstride;
       }
     } else {
@@ -89,8 +106,9 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
       for (int k = 0; k < kPf; ++k) {
         const float amount = __uint_as_float(ring[k].v.w);
         const float p = sc.tile(lds, ring[k], g, lane);
+        const bool rf = rule_of(ring[k], p);
         issue(tile + kPf * tstride, ring[k]);
-        finish(p, amount, tile);
+        finish(p, amount, tile, rf);
         tile += tstride;
       }
     }
@@ -101,7 +119,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     const WireRegs cur = ring[0];
 #pragma unroll
     for (int q = 0; q + 1 < kPf; ++q) ring[q] = ring[q + 1];
-    finish(sc.tile(lds, cur, g, lane), __uint_as_float(cur.v.w), tile);
+    const float p = sc.tile(lds, cur, g, lane);
+    finish(p, __uint_as_float(cur.v.w), tile, rule_of(cur, p));
     tile += tstride;
   }
   psum = wave_sum_u64(psum);

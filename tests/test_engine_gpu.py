@@ -216,3 +216,21 @@ def test_persistent_queue_isolation(gpu):
     probe = Path(__file__).parent / "helpers" / "queue_probe.py"
     r = subprocess.run([sys.executable, str(probe), "12"], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "ALL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+@pytest.mark.parametrize("wire", [False, True])
+def test_engine_score_sync_every_exec_mode(gpu, setup, exec_mode, wire):
+    """StreamEngine.score (synchronous DMA path, used by the native Seldon REST server) scores
+    every row in persistent mode too (round-1 bug: the descriptor carried a stale row count
+    of 0, so the resident kernel completed the batch without scoring it)."""
+    from ccfd_demo_summit_amd.engine import StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    X, m = setup
+    eng = StreamEngine(DeviceModel(m, gpu, wire=wire), batch=4096, depth=4, streams=2, input_mode="zerocopy",
+                       exec_mode=exec_mode)
+    p, r = eng.score(X[:10_000])
+    eng.close()
+    ref = m.wire_proba(X[:10_000]) if wire else m.predict_proba(X[:10_000], emulate_bf16=True)
+    assert np.abs(p - ref).max() < 2e-3
+    np.testing.assert_array_equal(r, (p >= 0.5).astype(np.uint8))
