@@ -43,24 +43,27 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
-    ap.add_argument("--batch", type=int, default=4096, help="micro-batch rows")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="micro-batch rows (default: the BASELINE config's -- 4096 for mlp/lr, 65536 for gbdt)")
     ap.add_argument("--batches-per-step", type=int, default=256)
-    ap.add_argument("--depth", type=int, default=16,
-                    help="micro-batches in flight per GPU (16 = p50 <= 80 us at the PCIe-bound rate: "
-                         "profiles/r2/operating_curve.txt)")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="micro-batches in flight per GPU (default 16 for mlp/lr = p50 <= 80 us at the "
+                         "PCIe-bound rate, profiles/r2/operating_curve.txt; 6 for gbdt = 1.66e9 tx/s at "
+                         "p50 225 us with 65536-row batches, profiles/r2/gbdt_g32_persist_sweep.jsonl)")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
-                    help="auto = persistent kernel for mlp/lr with zero-copy in/out, coalesced launches "
-                         "otherwise (profiles/r1/persist_sweep.txt)")
+                    help="auto = persistent kernel for mlp/lr and for gbdt on G32 rows with zero-copy "
+                         "in/out, launches otherwise (profiles/r1/persist_sweep.txt, profiles/r2/)")
     ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default 128)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
-    ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64"],
-                    help="partition-log row format: 30 x f32 (120 B) or W64 (64 B: bf16 V1..V28, "
-                         "f32 Time/Amount; contracts/transaction.py). auto = w64 for mlp/lr "
-                         "(the zero-copy path is PCIe-bound; profiles/r1/wire_sweep.txt), f32 for gbdt")
+    ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64", "g32"],
+                    help="partition-log row format: 30 x f32 (120 B), W64 (64 B: bf16 V1..V28, "
+                         "f32 Time/Amount) or G32 (32 B, GBDT: u8 bin per feature against the "
+                         "ensemble's split table -- exact; contracts/transaction.py). auto = w64 for "
+                         "mlp/lr (the zero-copy path is PCIe-bound; profiles/r1/wire_sweep.txt), g32 for gbdt")
     ap.add_argument("--log-rows", type=int, default=1 << 22, help="rows per rank (pinned partition logs)")
     ap.add_argument("--partitions-per-rank", type=int, default=2)
     ap.add_argument("--threshold", type=float, default=0.5)
@@ -175,13 +178,17 @@ def _precision(model, dm, args, dev):
     format and blob as the headline (W64 wire rows when args.wire == 'w64')."""
     import torch
     from ccfd_demo_summit_amd.data import generate
-    from ccfd_demo_summit_amd.engine.stream_engine import WIRE_ROW_F32, encode_w64
+    from ccfd_demo_summit_amd.engine.stream_engine import G32_ROW_F32, WIRE_ROW_F32, encode_g32, encode_w64
     from ccfd_demo_summit_amd.ops.kernels import score
     n = int(args.precision_rows)
     X, _ = generate(n, seed=args.seed + 4242)
     if args.wire == "w64":
         rows = np.empty((n, WIRE_ROW_F32), np.float32)
         encode_w64(X, rows.ctypes.data)
+        xt = torch.from_numpy(rows).to(dev)
+    elif args.wire == "g32":
+        rows = np.empty((n, G32_ROW_F32), np.float32)
+        encode_g32(X, dm.bins, rows.ctypes.data)
         xt = torch.from_numpy(rows).to(dev)
     else:
         xt = torch.from_numpy(X).to(dev)
@@ -207,6 +214,8 @@ def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     dm32 = DeviceModel(model, dev)
+    if args.model == "gbdt":
+        exec_mode = "launch"                # the persistent GBDT kernel reads G32 rows only
     rows = 1 << 20
     log = PartitionLog(rows)
     generate(rows, seed=args.seed + 77, out=log.feats.array)
@@ -231,7 +240,13 @@ def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
 def main(argv=None):
     args = parse_args(argv)
     if args.wire == "auto":
-        args.wire = "w64" if args.model in ("mlp", "lr") else "f32"
+        args.wire = "w64" if args.model in ("mlp", "lr") else "g32"
+    if args.batch is None:
+        args.batch = 65536 if args.model == "gbdt" else 4096
+    if args.depth is None:
+        args.depth = 6 if args.model == "gbdt" else 16
+    if (args.wire == "w64" and args.model == "gbdt") or (args.wire == "g32" and args.model != "gbdt"):
+        _fail(f"--wire {args.wire} does not apply to --model {args.model}")
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
@@ -254,25 +269,36 @@ def main(argv=None):
     # output bias calibrated on a synthetic sample so ~0.17 % of traffic routes to the fraud
     # process, like the dataset prior), X1 broadcast over RCCL to every rank.
     model = None
+    bins_t = None
     if ctx.rank == 0:
         Xcal, _ = generate(200_000, seed=args.seed + 999)
         model = build_model(args.model, seed=args.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE,
                             threshold=args.threshold, gbdt_trees=args.gbdt_trees, gbdt_depth=args.gbdt_depth)
-        packed = model.pack(wire=True) if args.wire == "w64" else model.pack()
+        if args.wire == "g32":
+            spec = model.bin_spec()
+            packed = model.pack(bins=spec)
+            bins_t = torch.from_numpy(np.frombuffer(spec.to_bytes(), np.uint8).copy()).to(dev)
+        else:
+            packed = model.pack(wire=True) if args.wire == "w64" else model.pack()
         blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(dev)
     else:
         blob = None
     blob = broadcast_blob(ctx, blob)
+    bins = None
+    if args.wire == "g32":          # the bin table travels with the blob (every rank encodes its logs)
+        from ccfd_demo_summit_amd.models.gbdt import BinSpec
+        bins = BinSpec.from_bytes(broadcast_blob(ctx, bins_t).cpu().numpy().tobytes())
     trees = args.gbdt_trees if args.model == "gbdt" else 0
     depth_t = args.gbdt_depth if args.model == "gbdt" else 0
-    dm = DeviceModel.from_blob(args.model, blob, trees, depth_t, wire=args.wire == "w64")
+    dm = DeviceModel.from_blob(args.model, blob, trees, depth_t, wire=args.wire == "w64", bins=bins)
     exec_mode = args.exec_mode
     if exec_mode == "auto":
         # measured on MI355X (profiles/r1/persist_sweep.txt): the persistent kernel with a
         # parallel doorbell and 512-row work items reaches 0.82e9 tx/s at p50 147 us, above
-        # coalesced launches (0.75e9 at 166 us); GBDT and DMA paths use launches
+        # coalesced launches (0.75e9 at 166 us); GBDT on G32 rows: 1.68e9 persistent vs 1.07e9
+        # with launches (profiles/r2/gbdt_g32_*_sweep.jsonl); DMA paths use launches
         zc = args.input_mode == "zerocopy" and args.output_mode == "zerocopy"
-        exec_mode = "persistent" if args.model in ("mlp", "lr") and zc else "launch"
+        exec_mode = "persistent" if zc and (args.model in ("mlp", "lr") or args.wire == "g32") else "launch"
 
     # ---- per-rank H2D ceiling probe, all ranks at once (attributes any scaling loss to the
     # host side: DRAM / PCIe root contention shows up as a lower per-rank GB/s at N > 1)
@@ -291,8 +317,8 @@ def main(argv=None):
                        threshold=args.threshold, device=dev.index, exec_mode=exec_mode,
                        persist_grid=args.persist_grid, coalesce=args.coalesce)
     for p in my_parts:
-        log = PartitionLog(rows_per_part, wire=args.wire == "w64")
-        if log.wire:
+        log = PartitionLog(rows_per_part, wire=args.wire == "w64", bins=bins)
+        if log.row_format != "f32":
             Xp, _ = generate(rows_per_part, seed=args.seed * 7919 + p)
             log.write_rows(0, Xp)           # ingest-side encoding, outside the timed region
             del Xp
@@ -418,7 +444,7 @@ def main(argv=None):
     if ctx.rank == 0:
         if args.precision_rows > 0:
             precision = _precision(model, dm, args, dev)
-        if args.wire == "w64" and not args.no_f32_probe:
+        if args.wire in ("w64", "g32") and not args.no_f32_probe:
             f32_rate = _f32_wire_rate(args, model, dev, exec_mode)
 
     value = total_rows / elapsed
@@ -441,7 +467,10 @@ def main(argv=None):
                             "the reference publishes no numbers",
         "dtype": "bf16" if args.model == "mlp" else "fp32",
         "data": ("synthetic creditcard-shaped transactions (30 features; log rows "
-                 + ("W64: bf16 V1..V28 + f32 Time/Amount, 64 B" if args.wire == "w64" else "30 x f32, 120 B")
+                 + {"w64": "W64: bf16 V1..V28 + f32 Time/Amount, 64 B",
+                    "g32": "G32: u8 bin of each feature against the ensemble's split thresholds "
+                           "(exact for oblivious trees) + amount bucket + table stamp, 32 B",
+                    "f32": "30 x f32, 120 B"}[args.wire]
                  + ") replayed from pinned partition logs; random-init weights, normaliser fitted + "
                  "output bias calibrated to the 0.172% fraud prior on a synthetic sample"),
         "config": {"model": {"mlp": "mlp_30_128_64_1", "lr": "logreg_30",
@@ -475,10 +504,11 @@ def main(argv=None):
         "rows_scored": total_rows,
         "rows_expected": expected,
         "fraud_routed": int(counters[1]) - fraud0,
+        "wire_stale_rows": int(counters[4]),      # G32 rows refused for a foreign bin-table stamp
         "flagged_handed_off_rank0": flagged_total,
         "per_rank": per_rank,
         "h2d_zerocopy_ceiling_tx_s_rank0": (None if h2d_gbps is None else
-                                            round(h2d_gbps * 1e9 / (64 if args.wire == "w64" else 120), 1)),
+                                            round(h2d_gbps * 1e9 / {"w64": 64, "g32": 32, "f32": 120}[args.wire], 1)),
         "f32_wire_tx_s": None if f32_rate is None else round(f32_rate, 1),
         "precision_vs_fp32": precision,
     }
@@ -493,7 +523,7 @@ def main(argv=None):
         import torch.distributed as dist
         barrier(ctx)
         dist.destroy_process_group()
-    if total_rows != expected:
+    if total_rows != expected or int(counters[4]) != 0:
         raise SystemExit(4)
 
 

@@ -27,6 +27,34 @@ BF16_DENSE_TFLOPS = 2500.0
 MLP_FLOP_PER_ROW = 24 * 16 * 16 * 32 * 2 / 16     # padded MFMA work actually issued
 
 
+class _HostRows:
+    """Quacks like the CUDA row tensor score() expects, but points at pinned host memory
+    (the device alias of a PinnedArray): the kernel reads it zero-copy over PCIe."""
+
+    def __init__(self, pinned, n, cols, dtype):
+        from ccfd_demo_summit_amd.ops._lib import lib
+        import torch
+        self._p, self.shape, self.dtype = pinned, (n, cols), dtype
+        self._ptr = lib().ccfd_host_device_ptr(pinned.ptr)
+        self.is_cuda, self.device = True, torch.device("cuda", 0)
+
+    def dim(self):
+        return 2
+
+    def element_size(self):
+        import torch
+        return torch.empty(0, dtype=self.dtype).element_size()
+
+    def is_contiguous(self):
+        return True
+
+    def stride(self, d):
+        return (self.shape[1], 1)[d]
+
+    def data_ptr(self):
+        return self._ptr
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="4096,65536,1048576,16777216")
@@ -35,6 +63,9 @@ def main():
     ap.add_argument("--flags", type=int, default=0, help="extra CCFD_ARG_* bits (16 = no counter atomics, "
                     "32 = no proba/route stores)")
     ap.add_argument("--tag", default="", help="label copied into every result line")
+    ap.add_argument("--host", action="store_true",
+                    help="rows in pinned host memory read zero-copy over PCIe (the streaming input path) "
+                         "instead of HBM: one launch per size, no engine")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import torch
@@ -45,11 +76,11 @@ def main():
 
     dev = torch.device("cuda", 0)
     sizes = [int(s) for s in args.sizes.split(",")]
-    cases = [tuple(c.split(":")) for c in args.cases.split(",")]
+    cases = [tuple(c.replace("/", ":").split(":")) for c in args.cases.split(",")]   # kind:wire or kind/wire
     nmax = max(sizes)
     X, _ = generate(1 << 20, seed=3)
     reps = (nmax + X.shape[0] - 1) // X.shape[0]
-    xf = xw = None
+    xf = xw = xg = None
     if any(w == "f32" for _, w in cases):
         xf = torch.from_numpy(X).to(dev).repeat(reps, 1)[:nmax].contiguous()
     if any(w == "w64" for _, w in cases):
@@ -57,11 +88,18 @@ def main():
     results = []
     for kind, wire in cases:
         m = build_model(kind, seed=0, X_ref=X[:100_000], calibrate_rate=0.01)
-        dm = DeviceModel(m, dev, wire=(wire == "w64"))
-        x_all = xw if wire == "w64" else xf
-        in_bytes = 64 if wire == "w64" else 120
+        dm = DeviceModel(m, dev, wire=(wire == "w64"), bins=True if wire == "g32" else None)
+        if wire == "g32":
+            xg = torch.from_numpy(dm.bins.encode(X)).to(dev).repeat(reps, 1)[:nmax].contiguous()
+        x_all = {"w64": xw, "g32": xg}.get(wire, xf)
+        in_bytes = {"w64": 64, "g32": 32}.get(wire, 120)
+        host_rows = None
+        if args.host:
+            from ccfd_demo_summit_amd.engine import PinnedArray
+            host_rows = PinnedArray((nmax, in_bytes // 4), "float32")
+            host_rows.array[:] = x_all.view(torch.float32).reshape(nmax, in_bytes // 4).cpu().numpy()
         for n in sizes:
-            x = x_all[:n]
+            x = x_all[:n] if host_rows is None else _HostRows(host_rows, n, x_all.shape[1], x_all.dtype)
             proba = torch.empty(n, dtype=torch.float32, device=dev)
             route = torch.empty(n, dtype=torch.uint8, device=dev)
             ctr = new_counters(dev)
@@ -79,6 +117,7 @@ def main():
             rows_s = n / (us * 1e-6)
             gbps = rows_s * (in_bytes + 5) / 1e9
             r = {"tag": args.tag, "flags": args.flags, "model": kind, "wire": wire, "rows": n,
+                 "rows_in": "host-zerocopy" if args.host else "hbm",
                  "us_per_launch": round(us, 2), "G_rows_per_s": round(rows_s / 1e9, 3), "GBps": round(gbps, 1),
                  "frac_hbm_roofline": round(gbps / HBM_GBPS_MEASURED, 3)}
             if kind == "mlp":

@@ -96,6 +96,47 @@ def decode_wire(W: np.ndarray) -> np.ndarray:
     return X
 
 
+# ---------------------------------------------------------------------------------------
+# G32: the 32-byte row of the tree-ensemble (GBDT) path.  A tree only tests ``x_j > thr``;
+# with feature j's sorted split thresholds as bin edges, bin_j(x) = #{edges_j < x} and
+# ``x_j > edges_j[k]`` <=> ``bin_j(x) > k`` for every float x (NaN -> 0, every test false),
+# so one byte per feature carries exactly what the ensemble can see.  The bin table belongs
+# to the model (models/gbdt.py BinSpec); rows carry its stamp so a row encoded for another
+# table is detected (counted, never silently mis-scored).
+#   bytes [0,30)  bin of Time, V1..V28, Amount (u8)   [30] amount bucket (K6 histogram)
+#   [31]          bin-table stamp 1..255
+# Amount itself stays host-side (the flagged-record column of the partition log).
+G32_ROW_BYTES = 32
+
+
+def amount_bucket(amount: np.ndarray) -> np.ndarray:
+    """K6 histogram bucket (metric_names.AMOUNT_BUCKETS, csrc/kernels/common.h amount_bucket)."""
+    from .metric_names import AMOUNT_BUCKETS
+    a = np.asarray(amount, np.float32)
+    b = np.zeros(a.shape, np.uint8)
+    for bound in AMOUNT_BUCKETS:
+        b += (a > np.float32(bound)).astype(np.uint8)
+    return b
+
+
+def encode_g32(X: np.ndarray, edges: Sequence[np.ndarray], stamp: int,
+               out: Optional[np.ndarray] = None) -> np.ndarray:
+    """float32 [n, 30] canonical rows -> uint8 [n, 32] G32 rows (numpy oracle of the native
+    ccfd_encode_g32).  ``edges[j]``: ascending float32 bin edges of feature j (<= 255)."""
+    X = np.asarray(X, np.float32)
+    n = X.shape[0]
+    if out is None:
+        out = np.empty((n, G32_ROW_BYTES), np.uint8)
+    for j in range(N_FEATURES):
+        e = np.asarray(edges[j], np.float32)
+        b = np.searchsorted(e, X[:, j], side="left")          # #edges < x (ascending edges)
+        b[np.isnan(X[:, j])] = 0
+        out[:, j] = b.astype(np.uint8)
+    out[:, 30] = amount_bucket(X[:, AMOUNT_COL])
+    out[:, 31] = np.uint8(stamp)
+    return out
+
+
 TXB_MAGIC = b"TXB1"
 TXB_HEADER = struct.Struct("<4sHHIIQQ")  # 32 bytes
 assert TXB_HEADER.size == 32

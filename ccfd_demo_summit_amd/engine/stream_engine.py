@@ -14,12 +14,13 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..ops._lib import (FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, EngineConfig, EngineStats,
+from ..ops._lib import (FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig, EngineStats,
                         Flagged, check, last_error, lib)
-from ..ops.kernels import DeviceModel
+from ..ops.kernels import ROW_BYTES, DeviceModel
 
 N_FEATURES = 30
 WIRE_ROW_F32 = 16            # W64 wire row = 64 B = 16 f32 words (contracts.transaction)
+G32_ROW_F32 = 8              # G32 row = 32 B (contracts.transaction)
 INPUT_MODES = {"dma": 0, "zerocopy": 1}
 OUTPUT_MODES = {"zerocopy": 0, "dma": 1}
 
@@ -61,37 +62,58 @@ def encode_w64(X: np.ndarray, out_ptr: int) -> None:
         raise RuntimeError("ccfd_encode_w64 failed")
 
 
+def encode_g32(X: np.ndarray, bins, out_ptr: int, amount_ptr: Optional[int] = None) -> None:
+    """f32 rows [n, 30] -> G32 rows at ``out_ptr`` against ``bins`` (models.gbdt.BinSpec),
+    Amount column to ``amount_ptr`` (native encoder, csrc/engine/ingest.cpp)."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    if X.ndim != 2 or X.shape[1] != N_FEATURES:
+        raise ValueError("expected [n, 30] float32 rows")
+    flat, off = bins.flat, bins.offsets
+    if lib().ccfd_encode_g32(X.ctypes.data, X.shape[0], N_FEATURES, flat.ctypes.data, off.ctypes.data,
+                             int(bins.stamp), C.c_void_p(out_ptr), C.c_void_p(amount_ptr)) != X.shape[0]:
+        raise RuntimeError("ccfd_encode_g32 failed")
+
+
 class PartitionLog:
     """One Kafka-partition-like append log of transactions in pinned host memory.
 
-    ``wire=True`` stores W64 rows (64 B, contracts/transaction.py) instead of 30 x f32."""
+    ``wire=True`` stores W64 rows (64 B, contracts/transaction.py) instead of 30 x f32;
+    ``bins=BinSpec`` stores G32 rows (32 B, GBDT) plus a host-side Amount column."""
 
-    def __init__(self, n_rows: int, wire: bool = False):
+    def __init__(self, n_rows: int, wire: bool = False, bins=None):
         self.n = int(n_rows)
         self.wire = bool(wire)
-        self.row_bytes = 64 if self.wire else 4 * N_FEATURES
-        self.feats = PinnedArray((self.n, WIRE_ROW_F32 if self.wire else N_FEATURES), np.float32)
+        self.bins = bins
+        if bins is not None and wire:
+            raise ValueError("a log holds one row format: W64 (wire) or G32 (bins)")
+        self.row_format = "g32" if bins is not None else "w64" if self.wire else "f32"
+        self.row_bytes = ROW_BYTES[self.row_format]
+        self.feats = PinnedArray((self.n, self.row_bytes // 4), np.float32)
         self.ids = PinnedArray(self.n, np.uint64)
         self.customer = PinnedArray(self.n, np.uint32)
+        self.amount = PinnedArray(self.n, np.float32) if bins is not None else None
 
     def write_rows(self, r: int, X: np.ndarray) -> None:
         """Store canonical f32 rows X at log rows [r, r + len(X))."""
-        if self.wire:
+        if self.row_format == "g32":
+            encode_g32(X, self.bins, self.feats.ptr + r * self.row_bytes, self.amount.ptr + 4 * r)
+        elif self.wire:
             encode_w64(X, self.feats.ptr + r * self.row_bytes)
         else:
             self.feats.array[r:r + X.shape[0]] = X
 
     @classmethod
-    def from_arrays(cls, X: np.ndarray, ids=None, customer=None, wire: bool = False) -> "PartitionLog":
-        log = cls(X.shape[0], wire=wire)
+    def from_arrays(cls, X: np.ndarray, ids=None, customer=None, wire: bool = False, bins=None) -> "PartitionLog":
+        log = cls(X.shape[0], wire=wire, bins=bins)
         log.write_rows(0, X)
         log.ids.array[:] = np.arange(log.n, dtype=np.uint64) if ids is None else ids
         log.customer.array[:] = 0 if customer is None else customer
         return log
 
     def free(self):
-        for a in (self.feats, self.ids, self.customer):
-            a.free()
+        for a in (self.feats, self.ids, self.customer, self.amount):
+            if a is not None:
+                a.free()
 
 
 @dataclass
@@ -156,7 +178,12 @@ class StreamEngine:
         cfg.persist_grid = int(persist_grid)
         cfg.coalesce = max(1, min(8, int(coalesce)))
         self.wire = bool(getattr(dm, "wire", False))
-        cfg.wire = 1 if self.wire else 0
+        self.row_format = dm.row_format
+        self.bins = getattr(dm, "bins", None)
+        if self.bins is not None and rules is not None and rules.ruleset.feature_vars():
+            raise ValueError("G32 rows carry bins, not feature values: routing rules may only use proba_1 "
+                             "(use f32 rows for rules over transaction columns)")
+        cfg.wire = ROW_FORMATS[self.row_format]
         self.exec_mode = exec_mode
         self.flips = 0
         self.rules = rules
@@ -183,12 +210,20 @@ class StreamEngine:
         except Exception:
             pass
 
+    def _check_log(self, log: PartitionLog) -> None:
+        if log.row_format != self.row_format:
+            raise ValueError(f"log rows are {log.row_format}, the engine's model blob expects {self.row_format}")
+        if self.row_format == "g32" and log.bins.stamp != self.bins.stamp:
+            raise ValueError("log was G32-encoded against another bin table than the model's")
+
     def add_log(self, partition: int, log: PartitionLog, cursor: int = 0) -> None:
-        if log.wire != self.wire:
-            raise ValueError("log row format (wire) does not match the engine's model blob")
+        self._check_log(log)
         check(lib().ccfd_engine_set_log(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
                                         C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr),
                                         log.n, int(cursor)), "ccfd_engine_set_log")
+        if log.amount is not None:
+            check(lib().ccfd_engine_set_amount(C.c_void_p(self.h), int(partition), C.c_void_p(log.amount.ptr)),
+                  "ccfd_engine_set_amount")
         self.logs[partition] = log
 
     def pump(self, n_batches: int, batch_rows: Optional[int] = None, drain: bool = True) -> StepStats:
@@ -203,7 +238,11 @@ class StreamEngine:
         """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
         X = np.ascontiguousarray(X, dtype=np.float32)
         n = X.shape[0]
-        if self.wire:
+        if self.row_format == "g32":
+            rows = np.empty((n, G32_ROW_F32), np.float32)
+            encode_g32(X, self.bins, rows.ctypes.data)
+            X = rows
+        elif self.wire:
             rows = np.empty((n, WIRE_ROW_F32), np.float32)
             encode_w64(X, rows.ctypes.data)
             X = rows
@@ -226,9 +265,12 @@ class StreamEngine:
     def swap_model(self, dm: DeviceModel) -> None:
         """Hot swap (runtime X1): in-flight micro-batches finish on the old weights, later ones
         use ``dm``.  The new model must have the same kernel kind, row format and GBDT shape."""
-        if dm.kind != self.dm.kind or bool(getattr(dm, "wire", False)) != self.wire or \
+        if dm.kind != self.dm.kind or dm.row_format != self.row_format or \
                 (dm.trees, dm.depth) != (self.dm.trees, self.dm.depth):
             raise ValueError("hot swap needs a model of the same kind / wire format / tree shape")
+        if self.row_format == "g32" and dm.bins.stamp != self.bins.stamp:
+            raise ValueError("G32 hot swap: pack the new ensemble against the live bin table "
+                             "(DeviceModel(model, bins=engine.bins)); its thresholds must be bin edges")
         check(lib().ccfd_engine_set_blob(C.c_void_p(self.h), C.c_void_p(dm.blob.data_ptr())),
               "ccfd_engine_set_blob")
         self.dm = dm                     # keeps the new blob alive; the old one may be freed now
@@ -256,10 +298,13 @@ class StreamEngine:
     # ------------------------------------------------------------------ ring (streaming) mode
     def set_ring(self, partition: int, capacity: int) -> PartitionLog:
         """Register partition ``partition`` as a live SPSC ring of ``capacity`` rows."""
-        log = PartitionLog(capacity, wire=self.wire)
+        log = PartitionLog(capacity, wire=self.wire, bins=self.bins)
         check(lib().ccfd_engine_set_ring(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
                                          C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr), log.n),
               "ccfd_engine_set_ring")
+        if log.amount is not None:
+            check(lib().ccfd_engine_set_amount(C.c_void_p(self.h), int(partition), C.c_void_p(log.amount.ptr)),
+                  "ccfd_engine_set_amount")
         self.logs[partition] = log
         return log
 
@@ -309,9 +354,16 @@ class StreamEngine:
             buf = b"".join(chunk)
             off = np.zeros(k + 1, np.int64)
             np.cumsum([len(v) for v in chunk], out=off[1:])
-            parse = L.ccfd_parse_json_batch_w64 if log.wire else L.ccfd_parse_json_batch
-            got = parse(buf, off.ctypes.data, k, log.feats.ptr + r * log.row_bytes,
-                        log.ids.ptr + r * 8, log.customer.ptr + r * 4)
+            if log.row_format == "g32":               # parse to f32, then bin
+                tmp = np.empty((k, N_FEATURES), np.float32)
+                got = L.ccfd_parse_json_batch(buf, off.ctypes.data, k, tmp.ctypes.data,
+                                              log.ids.ptr + r * 8, log.customer.ptr + r * 4)
+                if got == k:
+                    log.write_rows(r, tmp)
+            else:
+                parse = L.ccfd_parse_json_batch_w64 if log.wire else L.ccfd_parse_json_batch
+                got = parse(buf, off.ctypes.data, k, log.feats.ptr + r * log.row_bytes,
+                            log.ids.ptr + r * 8, log.customer.ptr + r * 4)
             if got != k:
                 raise ValueError(f"malformed transaction message #{done - got - 1}")
             L.ccfd_engine_ring_commit(C.c_void_p(self.h), int(partition), k)

@@ -13,12 +13,18 @@ Blob for the kernel (16-B aligned sections):
   feat    i32  [T][D]
   thr     f32  [T][D]
   leaves  f32  [T][2^D]
+
+G32 rows (contracts/transaction.py, csrc/kernels/score_gbdt_g32.hip) carry one byte per
+feature: its bin against a ``BinSpec`` (the ensemble's sorted split thresholds per
+feature).  The 'GBB1' blob replaces ``thr`` by the split's bin index ``k`` (i32), so the
+kernel's ``bin > k`` is exactly the f32 ``x > thr``; header word 5 is the spec's stamp.
 """
 from __future__ import annotations
 
 import struct
+import zlib
 from dataclasses import dataclass
-from typing import Optional
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -26,6 +32,91 @@ from ..contracts.transaction import N_FEATURES
 from .common import HEADER_BYTES, header, pad16, sigmoid
 
 MAX_DEPTH = 8
+MAX_BINS = 255          # split thresholds per feature a G32 byte can index
+
+
+@dataclass
+class BinSpec:
+    """Per-feature bin edges of the G32 row format: ascending, distinct float32 thresholds
+    (<= 255 per feature).  ``stamp`` (1..255) is written into every encoded row and into
+    the GBB1 blob; the kernel refuses rows whose stamp differs (CCFD_CNT_WIRE_STALE).
+
+    A model can be packed against any spec whose edges CONTAIN its thresholds -- e.g. a
+    retrained ensemble against the spec the live partition logs were encoded with, so a hot
+    swap needs no re-encoding while the split set stays inside it."""
+    edges: List[np.ndarray]
+
+    def __post_init__(self):
+        if len(self.edges) != N_FEATURES:
+            raise ValueError(f"need bin edges for all {N_FEATURES} features")
+        out = []
+        for j, e in enumerate(self.edges):
+            e = np.ascontiguousarray(e, np.float32).reshape(-1)
+            if e.size > MAX_BINS:
+                raise ValueError(f"feature {j}: {e.size} split thresholds > {MAX_BINS} (G32 bins are u8)")
+            if np.isnan(e).any() or (e.size > 1 and not (np.diff(e) > 0).all()):
+                raise ValueError(f"feature {j}: bin edges must be ascending, distinct and not NaN")
+            out.append(e)
+        self.edges = out
+
+    @classmethod
+    def from_thresholds(cls, feat: np.ndarray, thr: np.ndarray) -> "BinSpec":
+        feat = np.asarray(feat).reshape(-1)
+        thr = np.asarray(thr, np.float32).reshape(-1)
+        t = [thr[feat == j] for j in range(N_FEATURES)]
+        return cls([np.unique(e[~np.isnan(e)]) for e in t])     # NaN splits never fire: k = 255
+
+    @property
+    def offsets(self) -> np.ndarray:
+        off = np.zeros(N_FEATURES + 1, np.int32)
+        np.cumsum([e.size for e in self.edges], out=off[1:])
+        return off
+
+    @property
+    def flat(self) -> np.ndarray:
+        return np.concatenate(self.edges).astype(np.float32) if any(e.size for e in self.edges) \
+            else np.zeros(1, np.float32)
+
+    @property
+    def stamp(self) -> int:
+        """1..255 digest of the edge table (0 is never valid: zeroed memory is stale)."""
+        h = zlib.crc32(self.offsets.tobytes() + self.flat.tobytes())
+        return 1 + h % 255
+
+    def bin_index(self, feat: np.ndarray, thr: np.ndarray) -> np.ndarray:
+        """k with edges[feat][k] == thr for every split (ValueError if a threshold is missing)."""
+        feat = np.asarray(feat)
+        thr = np.asarray(thr, np.float32)
+        k = np.empty(feat.shape, np.int32)
+        for idx in np.ndindex(feat.shape):
+            if np.isnan(thr[idx]):            # `x > NaN` is always false: no u8 bin exceeds 255
+                k[idx] = MAX_BINS
+                continue
+            e = self.edges[int(feat[idx])]
+            i = int(np.searchsorted(e, thr[idx]))
+            if i >= e.size or e[i] != thr[idx]:
+                raise ValueError(f"split threshold {float(thr[idx])!r} of feature {int(feat[idx])} "
+                                 "is not a bin edge of this spec")
+            k[idx] = i
+        return k
+
+    def encode(self, X: np.ndarray) -> np.ndarray:
+        """numpy oracle of the native encoder: f32 [n,30] -> u8 [n,32] G32 rows."""
+        from ..contracts.transaction import encode_g32
+        return encode_g32(X, self.edges, self.stamp)
+
+    def to_bytes(self) -> bytes:
+        """offsets i32[31] + edges f32[...] (the X1 broadcast payload next to the blob)."""
+        return self.offsets.tobytes() + np.concatenate(self.edges + [np.zeros(0, np.float32)]).tobytes()
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "BinSpec":
+        off = np.frombuffer(b, np.int32, N_FEATURES + 1)
+        e = np.frombuffer(b, np.float32, int(off[-1]), 4 * (N_FEATURES + 1))
+        return cls([e[off[j]:off[j + 1]].copy() for j in range(N_FEATURES)])
+
+    def contains(self, other: "BinSpec") -> bool:
+        return all(np.isin(o, e).all() for o, e in zip(other.edges, self.edges))
 
 
 @dataclass
@@ -91,11 +182,21 @@ class ObliviousGBDT:
         z = self.raw_score(X)
         self.base += float(np.log(threshold / (1 - threshold)) - np.quantile(z, 1.0 - target_rate))
 
-    def pack(self) -> bytes:
+    def bin_spec(self) -> BinSpec:
+        """The smallest G32 bin table of this ensemble: its distinct thresholds per feature."""
+        return BinSpec.from_thresholds(self.feat, self.thr)
+
+    def pack(self, wire: bool = False, bins: Optional[BinSpec] = None) -> bytes:
+        """GBT1 blob for f32 rows, or (``bins``) the GBB1 blob for G32 rows of that spec."""
+        if wire:
+            raise ValueError("W64 wire rows are for the MLP / LR kernels; GBDT uses G32 (bins=)")
         T, D = self.feat.shape
-        blob = header(b"GBT1", 0, T, D, float(self.base))
-        blob += pad16(self.feat.tobytes()) + pad16(self.thr.tobytes()) + pad16(self.leaves.tobytes())
-        return blob
+        if bins is None:
+            blob = header(b"GBT1", 0, T, D, float(self.base))
+            return blob + pad16(self.feat.tobytes()) + pad16(self.thr.tobytes()) + pad16(self.leaves.tobytes())
+        k = bins.bin_index(self.feat, self.thr)
+        blob = header(b"GBB1", 0, T, D, float(self.base), int(bins.stamp))
+        return blob + pad16(self.feat.tobytes()) + pad16(k.tobytes()) + pad16(self.leaves.tobytes())
 
     @staticmethod
     def blob_offsets(T: int, D: int):

@@ -12,37 +12,52 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from ._lib import MODEL_IDS, N_COUNTER_SLOTS, ScoreArgs, check, lib
+from ._lib import ARG_WIRE_G32, ARG_WIRE_W64, MODEL_IDS, N_COUNTER_SLOTS, ScoreArgs, check, lib
 
 N_FEATURES = 30
+ROW_BYTES = {"f32": 4 * N_FEATURES, "w64": 64, "g32": 32}
 
 
 class DeviceModel:
     """A packed model resident in HBM (the blob is broadcast once over RCCL in DP runs)."""
 
-    def __init__(self, model, device: torch.device | str | int = "cuda", wire: bool = False):
-        """``wire=True``: blob packed for W64 wire rows (MLP / LR; see contracts/transaction.py)."""
+    def __init__(self, model, device: torch.device | str | int = "cuda", wire: bool = False, bins=None):
+        """``wire=True``: blob packed for W64 wire rows (MLP / LR; see contracts/transaction.py).
+        ``bins``: GBDT on G32 rows -- ``True`` for the model's own bin table, or a
+        ``models.gbdt.BinSpec`` containing its thresholds (e.g. the live logs' spec)."""
         self.kind = model.kind
         if self.kind not in MODEL_IDS:
             raise ValueError(f"no device kernel for model kind {self.kind!r}")
         if wire and self.kind not in ("mlp", "lr"):
             raise ValueError("W64 wire rows are supported by the MLP and LR kernels")
+        if bins is not None and bins is not False and self.kind != "gbdt":
+            raise ValueError("G32 rows (bins=) are for the GBDT kernel")
         self.wire = bool(wire)
-        blob = np.frombuffer(model.pack(wire=True) if wire else model.pack(), np.uint8)
-        self.blob = torch.from_numpy(blob.copy()).to(device)
+        self.bins = (model.bin_spec() if bins is True else bins) if bins not in (None, False) else None
+        if self.bins is not None:
+            packed = model.pack(bins=self.bins)
+        else:
+            packed = model.pack(wire=True) if wire else model.pack()
+        self.blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(device)
         self.trees = getattr(model, "n_trees", 0)
         self.depth = getattr(model, "depth", 0)
 
     @classmethod
     def from_blob(cls, kind: str, blob: torch.Tensor, trees: int = 0, depth: int = 0,
-                  wire: bool = False) -> "DeviceModel":
+                  wire: bool = False, bins=None) -> "DeviceModel":
         self = cls.__new__(cls)
         self.kind, self.blob, self.trees, self.depth, self.wire = kind, blob, trees, depth, bool(wire)
+        self.bins = bins
         return self
 
     @property
     def model_id(self) -> int:
         return MODEL_IDS[self.kind]
+
+    @property
+    def row_format(self) -> str:
+        """Row layout the blob expects: "f32" (30 x f32), "w64" or "g32"."""
+        return "g32" if getattr(self, "bins", None) is not None else "w64" if self.wire else "f32"
 
 
 class DeviceRules:
@@ -69,12 +84,17 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
           counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None,
           flags: int = 0, rules: Optional[DeviceRules] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused score of x [n,30] (float32, CUDA) -- or, for a ``wire`` model, W64 rows
-    ([n,64] uint8 or [n,16] float32 view) -- returns (proba_1 [n] f32, route [n] u8).
+    ([n,64] uint8 or [n,16] float32 view), for a ``bins`` model G32 rows ([n,32] uint8) --
+    returns (proba_1 [n] f32, route [n] u8).
     ``flags``: extra ``CCFD_ARG_*`` bits (ablation switches for profiling)."""
-    wire = getattr(dm, "wire", False)
+    fmt = dm.row_format
+    wire = fmt != "f32"
     if wire:
-        if not x.is_cuda or x.dim() != 2 or x.element_size() * x.shape[1] != 64 or not x.is_contiguous():
-            raise ValueError("wire model: x must be contiguous CUDA W64 rows ([n,64] u8 / [n,16] f32)")
+        rb = ROW_BYTES[fmt]
+        if not x.is_cuda or x.dim() != 2 or x.element_size() * x.shape[1] != rb or not x.is_contiguous():
+            raise ValueError(f"{fmt} model: x must be contiguous CUDA {fmt.upper()} rows ([n,{rb}] u8)")
+        if fmt == "g32" and rules is not None and rules.ruleset.feature_vars():
+            raise ValueError("G32 rows carry bins, not feature values: routing rules may only use proba_1")
     elif not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES:
         raise ValueError("x must be a CUDA float32 tensor of shape [n, 30]")
     if x.stride(1) != 1:
@@ -86,8 +106,8 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
         route = torch.empty(n, dtype=torch.uint8, device=x.device)
     a = ScoreArgs()
     a.x = x.data_ptr()
-    a.ld = 16 if wire else x.stride(0)
-    a.flags = (2 if wire else 0) | int(flags)          # CCFD_ARG_WIRE_W64
+    a.ld = ROW_BYTES[fmt] // 4 if wire else x.stride(0)
+    a.flags = {"f32": 0, "w64": ARG_WIRE_W64, "g32": ARG_WIRE_G32}[fmt] | int(flags)
     a.n = n
     a.model = dm.model_id
     a.blob = dm.blob.data_ptr()

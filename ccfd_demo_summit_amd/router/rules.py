@@ -255,6 +255,17 @@ class RuleSet:
         head = np.array([len(ops), int(self.default), len(self.rules), depth[1]], np.int32)
         return head.tobytes() + prog.tobytes()
 
+    def feature_vars(self) -> set:
+        """Transaction columns the rules read (``amount`` reported as ``Amount``); empty when
+        the rules only look at ``proba`` -- the only rule sets G32 (binned) rows can route."""
+        out = set()
+        for r in self.rules:
+            for n in ast.walk(ast.parse(r.expr, mode="eval")):
+                if isinstance(n, ast.Name) and n.id not in self.constants and n.id not in _FUNCS \
+                        and n.id != "proba":
+                    out.add("Amount" if n.id == "amount" else n.id)
+        return out
+
     @property
     def threshold_only(self) -> Optional[float]:
         """The threshold if this rule set is exactly ``proba >= T -> fraud, else standard``."""

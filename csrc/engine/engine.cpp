@@ -70,6 +70,7 @@ struct Partition {
   const float* feats_dev = nullptr;  // device-visible alias (zero-copy)
   const uint64_t* ids = nullptr;
   const uint32_t* cust = nullptr;
+  const float* amount = nullptr;     // G32 rows: host-side Amount column (flagged records)
   int64_t n = 0;
   int64_t cursor = 0;
   // ring (streaming) mode: SPSC ring of n rows; producer = ingest thread, consumer = run()
@@ -159,9 +160,12 @@ class Engine {
       return -1;
     }
     if (cfg.blob == nullptr) { set_error("null model blob"); return -1; }
-    if (cfg.wire && cfg.model == CCFD_MODEL_GBDT) { set_error("W64 wire rows: MLP and LR only"); return -1; }
-    rowf = cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 : CCFD_N_FEATURES;
-    amount_f = cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 - 1 : CCFD_N_FEATURES - 1;
+    if (cfg.wire < 0 || cfg.wire > 2) { set_error("wire must be 0 (f32), 1 (W64) or 2 (G32)"); return -1; }
+    if (cfg.wire == 1 && cfg.model == CCFD_MODEL_GBDT) { set_error("W64 wire rows: MLP and LR only"); return -1; }
+    if (cfg.wire == 2 && cfg.model != CCFD_MODEL_GBDT) { set_error("G32 rows: GBDT only"); return -1; }
+    rowf = cfg.wire == 2 ? CCFD_G32_ROW_BYTES / 4 : cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 : CCFD_N_FEATURES;
+    amount_f = cfg.wire == 2 ? -1 : cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 - 1 : CCFD_N_FEATURES - 1;
+    wire_flag = cfg.wire == 2 ? CCFD_ARG_WIRE_G32 : cfg.wire ? CCFD_ARG_WIRE_W64 : 0;
     HIPCHK(hipSetDevice(cfg.device));
     {
       int khz = 0;
@@ -222,8 +226,9 @@ class Engine {
   bool persist_counted = false;            // holds one of the process's persistent-queue slots
   bool coherent_out = true;
   uint64_t launches = 0;        // coalesced launches issued (stream round-robin)
-  int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, or 16 for W64 wire rows
-  int amount_f = CCFD_N_FEATURES - 1;
+  int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, 16 for W64, 8 for G32 rows
+  int amount_f = CCFD_N_FEATURES - 1;   // word of Amount in a row (-1: G32, host-side column)
+  int wire_flag = 0;            // CCFD_ARG_WIRE_* of the row format
   int ablate = 0;
   bool debug_sync = false;
   ccfd_persist_ctl* pctl = nullptr;       // host (coherent pinned)
@@ -237,8 +242,9 @@ class Engine {
   std::vector<int64_t> flip_seq;           // seq at each epoch flip
 
   int persist_init() {
-    if (cfg.model != CCFD_MODEL_MLP && cfg.model != CCFD_MODEL_LR) {
-      set_error("persistent exec_mode supports the MLP and LR models");
+    const bool g32 = cfg.model == CCFD_MODEL_GBDT && cfg.wire == 2;
+    if (cfg.model != CCFD_MODEL_MLP && cfg.model != CCFD_MODEL_LR && !g32) {
+      set_error("persistent exec_mode supports the MLP and LR models, and GBDT on G32 rows");
       return -1;
     }
     if (cfg.output_mode != 0 || cfg.depth > CCFD_PERSIST_MAX_RING) {
@@ -255,12 +261,13 @@ class Engine {
     pdesc = static_cast<ccfd_persist_desc*>(p);
     // work-item size: 64 rows (one 16-row tile per wave) by default; CCFD_PERSIST_ITEM_ROWS
     // = 128/256 gives each wave 2/4 tiles with a one-tile prefetch (fewer claims per batch)
-    int item_rows = CCFD_PERSIST_ITEM_ROWS;
+    // GBDT on G32 rows: items of 4 waves x 64-row chunks (256 / 512 / 1024 rows, default 512)
+    int item_rows = g32 ? 512 : CCFD_PERSIST_ITEM_ROWS;
     if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) {
       const int v = std::atoi(e);
-      if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) item_rows = v;
+      if (v == 256 || v == 512 || v == 1024 || (!g32 && (v == 64 || v == 128))) item_rows = v;
     }
-    persist_tpw = item_rows / 64;
+    persist_tpw = g32 ? item_rows / 256 : item_rows / 64;
     const int C = (cfg.max_batch + item_rows - 1) / item_rows;
     ccfd_persist_dev init{};
     for (int i = 0; i < CCFD_PERSIST_MAX_RING; ++i) init.remaining[i] = (unsigned)C;
@@ -312,13 +319,17 @@ class Engine {
     a.ring = cfg.depth;
     a.items_per_batch = persist_C;
     a.tiles_per_wave = persist_tpw;
-    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | (cfg.wire ? CCFD_ARG_WIRE_W64 : 0);
+    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | wire_flag;
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;
     a.blob = cfg.blob;
     a.counters[0] = cfg.counters[0];
     a.counters[1] = cfg.counters[1];
+    a.gbdt_trees = cfg.gbdt_trees;
+    a.gbdt_depth = cfg.gbdt_depth;
+    // 128 (+ doorbell) resident workgroups for every model: GBDT G32 measured 1.68e9 tx/s at
+    // 128 vs 1.62e9 at 256 and 1.34e9 at 768 (profiles/r2/gbdt_g32_persist_sweep.jsonl)
     const int grid = cfg.persist_grid > 0 ? cfg.persist_grid : CCFD_PERSIST_GRID;
     int rc = ccfd_persist_launch(&a, grid, pstream);
     if (rc) { set_error("persistent kernel launch failed"); return rc; }
@@ -404,6 +415,7 @@ class Engine {
     Partition& P = *parts[p];
     P.ring = false;
     P.feats = feats; P.ids = ids; P.cust = cust; P.n = n; P.cursor = cursor % n;
+    P.amount = nullptr;
     P.feats_dev = feats;
     if (cfg.input_mode == 1) {
       void* d = nullptr;
@@ -443,7 +455,7 @@ class Engine {
     f.tx_id = P.ids ? P.ids[row] : (uint64_t)row;
     f.customer = P.cust ? P.cust[row] : 0u;
     f.proba = s.h_proba[i];
-    f.amount = P.feats[row * rowf + amount_f];
+    f.amount = amount_f >= 0 ? P.feats[row * rowf + amount_f] : (P.amount ? P.amount[row] : __builtin_nanf(""));
     f.partition = (uint32_t)s.part;
     ++ring_tail;
   }
@@ -572,7 +584,7 @@ class Engine {
       s.done_ptr = s.h_done;
       a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate;
     }
-    if (cfg.wire) a.flags |= CCFD_ARG_WIRE_W64;
+    a.flags |= wire_flag;
     int rc = ccfd_score_launch(&a, stream);
     if (rc) return rc;
     if (debug_sync) HIPCHK(hipStreamSynchronize(stream));   // CCFD_DEBUG_SYNC: fault -> this batch
@@ -606,8 +618,7 @@ class Engine {
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;
     a.counters = cfg.counters[epoch & 1];
-    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate |
-              (cfg.wire ? CCFD_ARG_WIRE_W64 : 0);
+    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate | wire_flag;
     m.nsub = K;
     m.sub_rows = rows;
     for (int k = 0; k < K; ++k) {
@@ -777,6 +788,7 @@ class Engine {
     Partition& P = *parts[p];
     P.ring = true;
     P.feats = feats; P.ids = ids; P.cust = cust; P.n = cap; P.cursor = 0;
+    P.amount = nullptr;
     P.rr.reset(cap);
     P.feats_dev = feats;
     if (cfg.input_mode == 1) {
@@ -947,6 +959,15 @@ int64_t ccfd_engine_cursor(void* eng, int partition) {
   if (partition < 0 || partition >= (int)e->parts.size()) return -1;
   Partition& P = *e->parts[partition];
   return P.ring ? P.rr.released_count() : P.cursor;
+}
+
+int ccfd_engine_set_amount(void* eng, int partition, const float* amount) {
+  auto* e = static_cast<Engine*>(eng);
+  if (partition < 0 || partition >= (int)e->parts.size()) { set_error("bad partition index"); return -1; }
+  int rc = e->drain_all();
+  if (rc) return rc;
+  e->parts[partition]->amount = amount;
+  return 0;
 }
 
 int ccfd_engine_set_ring(void* eng, int partition, float* feats, uint64_t* ids, uint32_t* customer,

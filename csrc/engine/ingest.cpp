@@ -194,6 +194,47 @@ extern "C" int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* off
   return n_msgs;
 }
 
+// ---------------------------------------------------------------------------------------
+// G32 rows (GBDT; ccfd_abi.h, contracts/transaction.py encode_g32): byte j = #{edges_j < x_j}
+// (lower_bound; NaN compares false everywhere -> 0), byte 30 = amount bucket with the
+// device's bounds (common.h amount_bucket), byte 31 = bin-table stamp.
+namespace {
+constexpr float kAmountBounds[CCFD_N_AMOUNT_BUCKETS - 1] = {1.f, 5.f, 10.f, 25.f, 50.f, 100.f, 250.f,
+                                                            500.f, 1000.f, 2500.f, 5000.f, 10000.f, 25000.f};
+inline uint8_t amount_bucket_host(float a) {
+  int b = 0;
+  for (float bound : kAmountBounds) b += a > bound ? 1 : 0;
+  return (uint8_t)b;
+}
+inline uint8_t bin_of(const float* e, int ne, float x) {
+  int lo = 0, hi = ne;                 // first edge >= x  ==  #edges < x  (edges ascending)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (e[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return (uint8_t)lo;
+}
+}  // namespace
+
+extern "C" int64_t ccfd_encode_g32(const float* x, int64_t n, int64_t ld, const float* edges,
+                                   const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
+  if (ld < CCFD_N_FEATURES || n < 0 || stamp < 1 || stamp > 255 || !edges || !offsets || !out) return -1;
+  for (int j = 0; j < CCFD_N_FEATURES; ++j) {
+    const int ne = offsets[j + 1] - offsets[j];
+    if (offsets[j] < 0 || ne < 0 || ne > 255) return -1;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const float* r = x + i * ld;
+    uint8_t* o = out + i * CCFD_G32_ROW_BYTES;
+    for (int j = 0; j < CCFD_N_FEATURES; ++j)
+      o[j] = bin_of(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]);
+    o[30] = amount_bucket_host(r[CCFD_N_FEATURES - 1]);
+    o[31] = (uint8_t)stamp;
+    if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
+  }
+  return n;
+}
+
 // Internal entry points for the native Kafka consumer (kafka_consumer.cpp).
 namespace ccfd {
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust) {

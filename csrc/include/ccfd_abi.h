@@ -19,6 +19,7 @@ enum ccfd_counter_slot {
   CCFD_CNT_FRAUD = 1,         // transaction.outgoing{type=fraud}
   CCFD_CNT_STANDARD = 2,      // transaction.outgoing{type=standard}
   CCFD_CNT_PROBA_E6 = 3,      // sum(round(proba_1 * 1e6))
+  CCFD_CNT_WIRE_STALE = 4,    // G32 rows whose bin stamp != the model's (proba NaN, standard route)
   CCFD_CNT_HIST_STD = 8,      // 14 amount buckets, standard route
   CCFD_CNT_HIST_FRAUD = 24,   // 14 amount buckets, fraud route
   CCFD_CNT_SLOTS = 64
@@ -32,6 +33,12 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_FENCE_COHERENT 1   // outputs live in fine-grained pinned memory (informational)
 #define CCFD_ARG_WIRE_W64 2           // x holds W64 rows (64 B: bf16 V1..V28, f32 Time, f32 Amount)
 #define CCFD_WIRE_ROW_BYTES 64
+// G32 rows (GBDT only, 32 B): byte j < 30 = bin of feature j against the model's split
+// table (#edges_j < x_j, so `x_j > thr` == `bin_j > k(thr)` exactly), byte 30 = amount
+// bucket (K6), byte 31 = bin-table stamp (1..255; rows encoded for another table are
+// counted in CCFD_CNT_WIRE_STALE and not scored).  Amount itself stays host-side.
+#define CCFD_ARG_WIRE_G32 4
+#define CCFD_G32_ROW_BYTES 32
 // Diagnostic ablations (CCFD_ABLATE env in the engine; never set by bench.py): skip parts
 // of the epilogue to measure what each costs.  Results are incomplete when set.
 #define CCFD_ARG_ABLATE_COUNTERS 16   // no counter/histogram atomics
@@ -166,20 +173,21 @@ typedef struct ccfd_persist_args {
   ccfd_persist_dev* dev;
   int32_t ring;                    // R ring slots (<= CCFD_PERSIST_MAX_RING)
   int32_t items_per_batch;         // ceil(max_batch / item_rows)
-  int32_t model;                   // MLP or LR
+  int32_t model;                   // MLP, LR, or GBDT on G32 rows
   float threshold;
   int32_t tiles_per_wave;          // item_rows = 4 waves x tiles_per_wave x 16 rows
   int32_t flags;                   // CCFD_ARG_* (informational)
   const void* blob;
   unsigned long long* counters[2];
   const ccfd_rule_prog* rules;     // device; NULL = threshold route
+  int32_t gbdt_trees, gbdt_depth;  // GBDT (G32 rows): tiles_per_wave = 64-row chunks per wave per item
 } ccfd_persist_args;
 
 int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* stream);
 
 // ---------------------------------------------------------------------------
 // Host memory (pinned, device-mapped; used for partition logs and result rings)
-void* ccfd_host_alloc(size_t bytes);                 // hipHostMalloc(mapped|portable)
+void* ccfd_host_alloc(size_t bytes);                 // hipHostMalloc(mapped|portable|NumaUser)
 int ccfd_host_free(void* p);
 void* ccfd_host_device_ptr(void* host_ptr);          // hipHostGetDevicePointer
 
@@ -199,7 +207,7 @@ typedef struct ccfd_engine_config {
   int32_t flag_capacity;       // flagged-transaction ring capacity (records)
   int32_t exec_mode;           // 0 = one fused launch per micro-batch, 1 = persistent kernel
   int32_t persist_grid;        // workgroups of the persistent kernel (0 = 256)
-  int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B, CCFD_WIRE_ROW_BYTES)
+  int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B); 2 = G32 rows (32 B, GBDT)
   int32_t coalesce;            // launch mode: up to this many ready micro-batches per launch (<= 8)
   int32_t _pad2;
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
@@ -262,6 +270,9 @@ int ccfd_engine_set_blob(void* eng, const void* blob);
 // Drain up to `max` flagged records (fraud route) into `out`; returns count.
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
 int64_t ccfd_engine_cursor(void* eng, int partition);
+// G32 logs/rings: host-side Amount column of partition p (the flagged-record amount; the
+// rows themselves carry only its bucket).  Call after set_log / set_ring.
+int ccfd_engine_set_amount(void* eng, int partition, const float* amount);
 
 // Streaming (ring) mode: partition p is an SPSC ring of `capacity` rows in pinned memory.
 // Producer (ingest thread): ring_acquire -> write rows at [row, row+n) -> ring_commit(n).
@@ -285,6 +296,11 @@ int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* offsets, int64
                                   uint8_t* rows, uint64_t* ids, uint32_t* customer);
 // f32 rows (stride ld >= 30) -> W64 wire rows; returns n or -1.
 int64_t ccfd_encode_w64(const float* x, int64_t n, int64_t ld, uint8_t* out);
+// f32 rows -> G32 rows against a bin table: `edges` = the sorted split thresholds of every
+// feature back to back, feature j owning edges[offsets[j] .. offsets[j+1]) (<= 255 each);
+// `stamp` in 1..255.  amount_out (may be NULL) receives the raw Amount column.  Returns n or -1.
+int64_t ccfd_encode_g32(const float* x, int64_t n, int64_t ld, const float* edges, const int32_t* offsets,
+                        int32_t stamp, uint8_t* out, float* amount_out);
 
 // ---------------------------------------------------------------------------
 // Native Kafka consumer (csrc/engine/kafka_consumer.cpp): Metadata v1 -> one connection

@@ -11,6 +11,7 @@ int launch_mlp_multi(const ccfd_multi_args& m, hipStream_t s);
 int launch_lr(const ccfd_score_args& a, hipStream_t s);
 int launch_lr_multi(const ccfd_multi_args& m, hipStream_t s);
 int launch_gbdt(const ccfd_score_args& a, hipStream_t s);
+int launch_gbdt_g32(const ccfd_score_args& a, hipStream_t s);
 
 thread_local std::string g_last_error;
 void set_error(const std::string& e) { g_last_error = e; }
@@ -25,6 +26,14 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
   if (a == nullptr || a->blob == nullptr || a->x == nullptr) { set_error("null argument"); return -1; }
   if (a->n < 0) { set_error("n < 0"); return -1; }
   if (a->n == 0) return 0;
+  if (a->flags & CCFD_ARG_WIRE_G32) {
+    if (a->model != CCFD_MODEL_GBDT) { set_error("G32 rows: GBDT kernel only"); return -3; }
+    if (reinterpret_cast<uintptr_t>(a->x) & 15) { set_error("G32 rows must be 16-byte aligned"); return -3; }
+    const int rc = launch_gbdt_g32(*a, reinterpret_cast<hipStream_t>(stream));
+    if (rc == -2) set_error("G32 launch: bad tree shape (depth 1..8, leaf tables <= 64 KB)");
+    else if (rc != 0) set_error(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return rc;
+  }
   if (a->flags & CCFD_ARG_WIRE_W64) {
     if (a->model == CCFD_MODEL_GBDT) { set_error("W64 wire rows: MLP and LR kernels only"); return -3; }
     if (reinterpret_cast<uintptr_t>(a->x) & 15) { set_error("W64 rows must be 16-byte aligned"); return -3; }

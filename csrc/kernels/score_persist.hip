@@ -1,4 +1,5 @@
-// Persistent streaming scorer (engine exec_mode = 1).
+// Persistent streaming scorer (engine exec_mode = 1), MLP and LR; protocol helpers in
+// persist_core.h (the GBDT G32 persistent kernel shares them, score_gbdt_g32.hip).
 //
 // One launch lives as long as the engine.  Every resident workgroup loops:
 //   claim work item i (one agent-scope atomic)      -> micro-batch b = i / C, chunk c = i % C
@@ -21,9 +22,12 @@
 // b % R before observing done for b - R, which is what makes the slot-local state
 // (remaining/nflag reset by the last ticket) safe to reuse.
 #include "mlp_core.h"
+#include "persist_core.h"
 #include "rules.h"
 
 namespace ccfd {
+
+int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s);   // score_gbdt_g32.hip
 
 namespace {
 
@@ -66,90 +70,14 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   float* tile_lds = sx[wave];
   unsigned long long posted_cache = 0;     // thread 0 only
 
-  // Workgroup 0 is the DOORBELL: its first wave alone polls host memory (ctl->posted/stop)
-  // and mirrors new descriptors + the posted count into device memory.  Every other
-  // workgroup polls only the device mirror: hundreds of workgroups polling host memory
-  // would each hold PCIe read requests and starve the feature stream (measured: 2x grid
-  // -> 3x slower before this split).
+  // Workgroup 0 is the DOORBELL (persist_core.h): its first wave alone polls host memory.
   if (blockIdx.x == 0) {
-    // The whole first wave mirrors: lane l copies word l % W of descriptor (mirrored + l / W),
-    // so up to 10 newly posted descriptors cost ONE PCIe round trip instead of one per word
-    // (a thread-0 copy loop serialised ~11 us per micro-batch: profiles/r1/persist_sweep.txt).
-    if (wave == 0) {
-      constexpr int kW = (int)(sizeof(ccfd_persist_desc) / 8);
-      constexpr int kPer = 64 / kW;                     // descriptors per wave step
-      unsigned long long mirrored = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned sleep_n = 1;
-      for (;;) {
-        unsigned long long p = 0;
-        if (lane == 0) p = __hip_atomic_load(&a.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        p = __shfl(p, 0);
-        if (p > mirrored) {
-          const unsigned long long nb = min(p - mirrored, (unsigned long long)kPer);
-          const int bi = lane / kW, wi = lane % kW;
-          if (bi < (int)nb) {
-            const unsigned long long b = mirrored + bi;
-            const unsigned long long* src =
-                reinterpret_cast<const unsigned long long*>(a.desc + (b % (unsigned long long)a.ring));
-            unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
-            __hip_atomic_store(dst + wi, __hip_atomic_load(src + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          // every lane's descriptor store is ordered before the new posted count
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          mirrored += nb;
-          if (lane == 0) __hip_atomic_store(&a.dev->posted, mirrored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          sleep_n = 1;
-          continue;
-        }
-        int stop = 0;
-        if (lane == 0) stop = __hip_atomic_load(&a.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-        if (__shfl(stop, 0)) {
-          if (lane == 0) {
-            __hip_atomic_store(&a.dev->stop, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&a.ctl->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-          break;
-        }
-        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);   // ~64..1024 cycles
-        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
-      }
-    }
+    if (wave == 0) persist_doorbell(a, lane);
     return;                                              // no barrier is ever used by WG 0
   }
 
   for (;;) {
-    if (tid == 0) {
-      const unsigned long long item =
-          __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long b = item / (unsigned long long)C;
-      int cmd = 0;
-      unsigned sleep_n = 1;
-      while (posted_cache <= b) {
-        // relaxed poll; the acquire fence below runs once the item's batch is posted
-        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (posted_cache > b) break;
-        if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { cmd = 1; break; }
-        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
-        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
-      }
-      if (!cmd) {
-        // one acquire per claimed item (not per poll): invalidates this XCD's L2 copies of
-        // non-coherent inputs (a reused ring slot / DMA staging buffer) before they are read
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
-        sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(d + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(d + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        const unsigned long long ne = __hip_atomic_load(d + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sdesc.n = (int32_t)(ne & 0xffffffffull);
-        sdesc.epoch = (int32_t)(ne >> 32);
-        sdesc.seq = b;
-      }
-      s_item = item;
-      s_cmd = cmd;
-    }
+    if (tid == 0) persist_claim(a, C, posted_cache, sdesc, s_item, s_cmd);
     __syncthreads();
     if (s_cmd) break;
 
@@ -237,16 +165,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       nf_w += __popcll(m);
       nv_w += __popcll(__ballot(valid && g == 0));
       if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
-      // compacted flag list (reservation on the slot's device counter)
-      if (m && sdesc.flag_idx) {
-        const int leader = __builtin_ffsll((long long)m) - 1;
-        unsigned base = 0;
-        if (lane == leader)
-          base = __hip_atomic_fetch_add(&a.dev->nflag[slot], (unsigned)__popcll(m), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        base = __shfl(base, leader);
-        if (fr && g == 0) sdesc.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
-      }
+      persist_emit_flagged(a, sdesc, slot, m, fr && g == 0, row, lane);
     }
     ps_w = wave_sum_u64(ps_w);
     if (lane == 0 && nv_w) {
@@ -254,44 +173,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       atomicAdd(&epi.rows, nv_w);
       atomicAdd(&epi.psum_e6, ps_w);
     }
-    // per-item epilogue: counters of this item into the epoch's buffer, reset LDS state
-    __syncthreads();
-    unsigned long long* cnt = a.counters[sdesc.epoch & 1];
-    if (tid < 2 * kNB) {
-      const unsigned h = epi.hist[tid];
-      if (h && cnt) atomicAdd(&cnt[(tid < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + tid],
-                              (unsigned long long)h);
-      epi.hist[tid] = 0;
-    } else if (tid == 64) {
-      if (cnt && epi.rows) {
-        atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)epi.rows);
-        atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)epi.fraud);
-        atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(epi.rows - epi.fraud));
-        atomicAdd(&cnt[CCFD_CNT_PROBA_E6], epi.psum_e6);
-      }
-      epi.rows = 0; epi.fraud = 0; epi.psum_e6 = 0;
-    }
-    // completion: publish this item's outputs, take a ticket, last ticket signals the host
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned left =
-          __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
-      if (left == 0) {
-        const unsigned nflag = __hip_atomic_load(&a.dev->nflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.dev->nflag[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.dev->remaining[slot], (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.ctl->done[slot][1], (unsigned long long)nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.ctl->done[slot][2],
-                           __hip_atomic_load(&a.dev->tstart[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.ctl->done[slot][3], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.ctl->done[slot][0], sdesc.seq + 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
+    persist_item_done(a, epi, sdesc, slot, C, tid);
   }
 }
 
@@ -311,6 +193,8 @@ extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* s
   } else if (a->model == CCFD_MODEL_LR) {
     if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_LR, true>), dim3(grid), dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_LR, false>), dim3(grid), dim3(256), 0, s, *a);
+  } else if (a->model == CCFD_MODEL_GBDT && (a->flags & CCFD_ARG_WIRE_G32)) {
+    return launch_persist_gbdt_g32(*a, grid, s);
   } else {
     return -3;
   }

@@ -76,3 +76,67 @@ def test_wire_blob_matches_oracle(kind):
         assert np.abs(got - m.predict_proba(X[:48])).max() < 5e-3
     blob = np.frombuffer(m.pack(wire=True), np.uint8)
     assert int(np.frombuffer(blob[4:8].tobytes(), np.uint32)[0]) & 2
+
+
+# ---------------------------------------------------------------------------------------
+# G32 rows (GBDT): bins against the ensemble's split table are exact for every float
+def _g32_case(seed=0, n=20000):
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT
+    X, _ = generate(n, seed=seed)
+    m = ObliviousGBDT.random_init(100, 6, seed=seed, X_ref=X)
+    m.thr[3, 2] = np.nan                      # a split that never fires
+    X[5, 3] = np.nan
+    X[6, 29] = np.nan
+    X[7, 2] = np.inf
+    X[8, 2] = -np.inf
+    X[9, :] = m.thr[0, 0]                     # values equal to thresholds
+    X[10, :] = -0.0
+    return X, m
+
+
+def test_g32_bins_reproduce_every_split_decision():
+    X, m = _g32_case()
+    spec = m.bin_spec()
+    k = spec.bin_index(m.feat, m.thr)
+    rows = spec.encode(X)
+    np.testing.assert_array_equal(rows[:, m.feat].astype(np.int32) > k[None], X[:, m.feat] > m.thr[None])
+    assert (rows[:, 31] == spec.stamp).all() and 1 <= spec.stamp <= 255
+
+
+def test_g32_native_encoder_matches_numpy_oracle():
+    from ccfd_demo_summit_amd.engine.stream_engine import G32_ROW_F32, encode_g32
+    X, m = _g32_case(seed=1)
+    spec = m.bin_spec()
+    out = np.empty((X.shape[0], G32_ROW_F32), np.float32)
+    am = np.empty(X.shape[0], np.float32)
+    encode_g32(X, spec, out.ctypes.data, am.ctypes.data)
+    np.testing.assert_array_equal(out.view(np.uint8), spec.encode(X))
+    np.testing.assert_array_equal(am, X[:, 29])
+    from ccfd_demo_summit_amd.contracts.metric_names import AMOUNT_BUCKETS
+    b = np.searchsorted(np.asarray(AMOUNT_BUCKETS, np.float32), X[:, 29], side="left")
+    b[np.isnan(X[:, 29])] = 0
+    np.testing.assert_array_equal(out.view(np.uint8)[:, 30], b)
+
+
+def test_g32_blob_and_spec_roundtrip():
+    import struct
+    from ccfd_demo_summit_amd.models.gbdt import BinSpec, ObliviousGBDT
+    X, m = _g32_case(seed=2)
+    spec = m.bin_spec()
+    s2 = BinSpec.from_bytes(spec.to_bytes())
+    assert s2.stamp == spec.stamp and all(np.array_equal(a, b) for a, b in zip(s2.edges, spec.edges))
+    blob = m.pack(bins=spec)
+    assert blob[:4] == b"GBB1" and struct.unpack_from("<i", blob, 20)[0] == spec.stamp
+    off_f, off_k, off_l, end = ObliviousGBDT.blob_offsets(m.n_trees, m.depth)
+    k = np.frombuffer(blob, np.int32, m.feat.size, off_k).reshape(m.feat.shape)
+    assert k[3, 2] == 255                       # NaN split: no u8 bin exceeds it
+    # a superset table accepts the model; a table missing one of its thresholds refuses it
+    wide = BinSpec([np.union1d(e, np.float32([1e9])) for e in spec.edges])
+    assert wide.contains(spec) and wide.stamp != spec.stamp
+    m.pack(bins=wide)
+    narrow = BinSpec([e[1:] if j == int(m.feat[0, 0]) else e for j, e in enumerate(spec.edges)])
+    with pytest.raises(ValueError, match="not a bin edge"):
+        m.pack(bins=narrow)
+    with pytest.raises(ValueError):
+        BinSpec([np.arange(300, dtype=np.float32)] + [np.zeros(0, np.float32)] * 29)
