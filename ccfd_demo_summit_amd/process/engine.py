@@ -106,7 +106,7 @@ class ProcessEngine:
         self.outcome_counts: Dict[str, int] = {o.value: 0 for o in Outcome}
         self.standard_count = 0
         self.keep_completed = keep_completed
-        self._completed_order: List[int] = []
+        self._completed_order: collections.deque = collections.deque()   # O(1) eviction
         self._journal = open(journal_path, "a", buffering=1) if journal_path else None
         self.dedupe_window = 1_000_000
         self._by_tx: Dict[Any, int] = {}
@@ -315,7 +315,7 @@ class ProcessEngine:
             return          # standard instances are counted, not retained (hot path volume)
         self._completed_order.append(inst.id)
         while len(self._completed_order) > self.keep_completed:
-            old = self._completed_order.pop(0)
+            old = self._completed_order.popleft()
             gone = self.instances.pop(old, None)
             if gone is not None and gone.task_id is not None:
                 self.tasks.pop(gone.task_id, None)

@@ -198,20 +198,48 @@ def _quantile_borders(X: np.ndarray, n_bins: int) -> np.ndarray:
 
 def train_oblivious_gbdt(X: np.ndarray, y: np.ndarray, n_trees: int = 100, depth: int = 6,
                          learning_rate: float = 0.1, n_bins: int = 32, l2: float = 1.0,
-                         device: str = "auto") -> Tuple[ObliviousGBDT, Dict]:
+                         device: str = "auto", borders: Optional[np.ndarray] = None) -> Tuple[ObliviousGBDT, Dict]:
     """Level-wise oblivious boosting on logloss.  At each level one (feature, border) is
-    chosen for ALL current leaves (maximum summed second-order gain)."""
+    chosen for ALL current leaves (maximum summed second-order gain).
+
+    Data-parallel when torch.distributed is initialised (the reference's 2-executor Spark
+    training, deploy/frauddetection_cr.yaml:27,34-35): like the DDP trainers every rank
+    passes the same X and works on its shard (rows rank::world); the borders come from
+    rank 0 (broadcast), and the per-level gradient/hessian histograms,
+    the leaf sums and the base-rate statistics are all-reduced (SUM), so every rank grows
+    the same trees -- the ones a single process would grow on the union of the shards, up to
+    float summation order.  ``borders`` [F, n_bins-1]: use these split candidates instead of
+    quantiles of X."""
     dev = _device(device)
+    rank, world = _ddp_ctx()
+
+    def allreduce(t: torch.Tensor) -> torch.Tensor:
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t)
+        return t
+
     X = np.asarray(X, np.float32)
+    if borders is None:
+        borders = _quantile_borders(X, n_bins)                      # [F, B-1]
+    if world > 1:
+        X, y = X[rank::world], np.asarray(y)[rank::world]
     n, F = X.shape
-    borders = _quantile_borders(X, n_bins)                          # [F, B-1]
+    borders = np.ascontiguousarray(borders, np.float32)
+    n_bins = borders.shape[1] + 1
+    if world > 1:                                                   # rank 0's split candidates
+        import torch.distributed as dist
+        bt0 = torch.from_numpy(borders).to(dev)
+        dist.broadcast(bt0, 0)
+        borders = bt0.cpu().numpy()
     # bin index of every value: number of borders strictly below it -> x > border[b] iff bin > b
     bins = np.empty((n, F), np.int64)
     for f in range(F):
         bins[:, f] = np.searchsorted(borders[f], X[:, f], side="left")
     bt = torch.from_numpy(bins).to(dev)
     yt = torch.from_numpy(y.astype(np.float32)).to(dev)
-    p0 = float(np.clip(y.mean(), 1e-6, 1 - 1e-6))
+    stats = allreduce(torch.tensor([float(y.sum()), float(n)], dtype=torch.float64, device=dev))
+    p0 = float(np.clip(float(stats[0]) / max(float(stats[1]), 1.0), 1e-6, 1 - 1e-6))
     base = math.log(p0 / (1 - p0))
     raw = torch.full((n,), base, device=dev)
     feat = np.zeros((n_trees, depth), np.int32)
@@ -229,8 +257,8 @@ def train_oblivious_gbdt(X: np.ndarray, y: np.ndarray, n_trees: int = 100, depth
             key = (leaf[:, None] * F + fidx[None, :]) * B + bt          # [n, F]
             G = torch.zeros(L * F * B, device=dev).scatter_add_(0, key.reshape(-1), grad[:, None].expand(n, F).reshape(-1))
             H = torch.zeros(L * F * B, device=dev).scatter_add_(0, key.reshape(-1), hess[:, None].expand(n, F).reshape(-1))
-            G = G.view(L, F, B)
-            H = H.view(L, F, B)
+            G = allreduce(G).view(L, F, B)
+            H = allreduce(H).view(L, F, B)
             Gl = G.cumsum(-1)[..., :-1]                                # split after bin b: left = bins <= b
             Hl = H.cumsum(-1)[..., :-1]
             Gt = G.sum(-1, keepdim=True)
@@ -242,15 +270,16 @@ def train_oblivious_gbdt(X: np.ndarray, y: np.ndarray, n_trees: int = 100, depth
             feat[t, d] = f
             thr[t, d] = borders[f, b]
             leaf = leaf | ((bt[:, f] > b).long() << d)
-        Gs = torch.zeros(1 << depth, device=dev).scatter_add_(0, leaf, grad)
-        Hs = torch.zeros(1 << depth, device=dev).scatter_add_(0, leaf, hess)
+        Gs = allreduce(torch.zeros(1 << depth, device=dev).scatter_add_(0, leaf, grad))
+        Hs = allreduce(torch.zeros(1 << depth, device=dev).scatter_add_(0, leaf, hess))
         vals = -learning_rate * Gs / (Hs + l2)
         leaves[t] = vals.cpu().numpy()
         raw = raw + vals[leaf]
     model = ObliviousGBDT(feat, thr, leaves, float(base))
     with torch.no_grad():
-        ll = float(torch.nn.functional.binary_cross_entropy_with_logits(raw, yt))
-    return model, {"train_logloss": ll, "trees": n_trees, "depth": depth}
+        ll_sum = torch.nn.functional.binary_cross_entropy_with_logits(raw, yt, reduction="sum").double()
+        ll = float(allreduce(ll_sum.reshape(1))[0]) / max(float(stats[1]), 1.0)
+    return model, {"train_logloss": ll, "trees": n_trees, "depth": depth, "world": world}
 
 
 def evaluate(model, X: np.ndarray, y: np.ndarray) -> Dict[str, float]:
