@@ -239,22 +239,22 @@ def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
 
 def main(argv=None):
     args = parse_args(argv)
-    if args.wire == "auto":
-        args.wire = "w64" if args.model in ("mlp", "lr") else "g32"
+    from ccfd_demo_summit_amd.parallel.dp import resolve_row_format
+    try:
+        args.wire = resolve_row_format(args.model, args.wire)   # auto: w64 for mlp/lr, g32 for gbdt
+    except ValueError as e:
+        _fail(str(e))
     if args.batch is None:
         args.batch = 65536 if args.model == "gbdt" else 4096
     if args.depth is None:
         args.depth = 6 if args.model == "gbdt" else 16
-    if (args.wire == "w64" and args.model == "gbdt") or (args.wire == "g32" and args.model != "gbdt"):
-        _fail(f"--wire {args.wire} does not apply to --model {args.model}")
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.models import build_model
     from ccfd_demo_summit_amd.ops._lib import lib
-    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     from ccfd_demo_summit_amd.parallel import (CounterReducer, EpochPipeline, all_max, assign_partitions,
-                                               barrier, broadcast_blob, hist_quantile, init_distributed)
+                                               barrier, broadcast_model, hist_quantile, init_distributed)
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
@@ -269,28 +269,12 @@ def main(argv=None):
     # output bias calibrated on a synthetic sample so ~0.17 % of traffic routes to the fraud
     # process, like the dataset prior), X1 broadcast over RCCL to every rank.
     model = None
-    bins_t = None
     if ctx.rank == 0:
         Xcal, _ = generate(200_000, seed=args.seed + 999)
         model = build_model(args.model, seed=args.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE,
                             threshold=args.threshold, gbdt_trees=args.gbdt_trees, gbdt_depth=args.gbdt_depth)
-        if args.wire == "g32":
-            spec = model.bin_spec()
-            packed = model.pack(bins=spec)
-            bins_t = torch.from_numpy(np.frombuffer(spec.to_bytes(), np.uint8).copy()).to(dev)
-        else:
-            packed = model.pack(wire=True) if args.wire == "w64" else model.pack()
-        blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(dev)
-    else:
-        blob = None
-    blob = broadcast_blob(ctx, blob)
-    bins = None
-    if args.wire == "g32":          # the bin table travels with the blob (every rank encodes its logs)
-        from ccfd_demo_summit_amd.models.gbdt import BinSpec
-        bins = BinSpec.from_bytes(broadcast_blob(ctx, bins_t).cpu().numpy().tobytes())
-    trees = args.gbdt_trees if args.model == "gbdt" else 0
-    depth_t = args.gbdt_depth if args.model == "gbdt" else 0
-    dm = DeviceModel.from_blob(args.model, blob, trees, depth_t, wire=args.wire == "w64", bins=bins)
+    dm = broadcast_model(ctx, model, args.model, args.wire)     # X1 (+ the G32 bin table)
+    bins = dm.bins
     exec_mode = args.exec_mode
     if exec_mode == "auto":
         # measured on MI355X (profiles/r1/persist_sweep.txt): the persistent kernel with a

@@ -53,7 +53,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=4096, help="rows per TXB1 message / micro-batch")
     ap.add_argument("--partitions-per-rank", type=int, default=4)
     ap.add_argument("--max-lag-msgs", type=int, default=64, help="producer back-pressure (messages)")
-    ap.add_argument("--model", default="mlp", choices=["mlp", "lr"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"],
+                    help="gbdt: 100x6 oblivious ensemble on G32 rows (binned at ingest)")
     ap.add_argument("--flush-us", type=int, default=500, help="deadline flush of partial micro-batches")
     ap.add_argument("--fmt", default="txb1", choices=["txb1", "json"],
                     help="txb1: one columnar batch per message; json: one transaction per message")
@@ -109,10 +110,10 @@ def main(argv=None):
         store.create_topic(t, P)
     tx_store.create_topic(k.transactions_topic, P)
 
-    # model (same random-init + calibration as bench.py), W64 rows
+    # model (same random-init + calibration as bench.py), W64 rows (G32 for the GBDT)
     Xcal, _ = generate(200_000, seed=999)
     model = build_model(args.model, seed=0, X_ref=Xcal, calibrate_rate=FRAUD_RATE)
-    dm = DeviceModel(model, dev, wire=True)
+    dm = DeviceModel(model, dev, wire=args.model != "gbdt", bins=True if args.model == "gbdt" else None)
 
     hub = MetricsHub()
     processes = ProcessEngine(cfg.kie.notification_timeout_s, cfg.kie.dmn_probability_threshold,

@@ -3,7 +3,7 @@
 A C++ thread looks up partition leaders (Metadata v1), keeps one connection per leader
 broker, fetches (Fetch v4) from all leaders in parallel, validates RecordBatch v2 CRC-32C
 (uncompressed or gzip), and writes TXB1 batches / JSON transactions straight into the
-engine's pinned partition rings (f32 or W64 rows) -- no Python per message (SURVEY.md §2.4
+engine's pinned partition rings (f32, W64 or G32 rows) -- no Python per message (SURVEY.md §2.4
 H1, §7.3 hard part 1: JSON-per-transaction at 1M/s is out of reach for a Python consumer
 loop).  Leader moves / broker failures refresh metadata and continue from the same offset;
 OFFSET_OUT_OF_RANGE follows ``offset_reset`` (earliest / latest / none).
@@ -25,7 +25,8 @@ from ..ops._lib import check, lib
 
 class KcPartition(C.Structure):
     _fields_ = [("kafka_partition", C.c_int32), ("engine_partition", C.c_int32), ("start_offset", C.c_int64),
-                ("feats", C.c_void_p), ("ids", C.c_void_p), ("customer", C.c_void_p), ("capacity", C.c_int64)]
+                ("feats", C.c_void_p), ("ids", C.c_void_p), ("customer", C.c_void_p), ("capacity", C.c_int64),
+                ("amount", C.c_void_p)]
 
 
 class KcStats(C.Structure):
@@ -35,6 +36,8 @@ class KcStats(C.Structure):
 
 
 RESET_POLICIES = {"earliest": 0, "latest": 1, "none": 2}
+ROW_CODES = {"f32": 0, "w64": 1, "g32": 2}
+ROW_WIDTH = {"f32": 30, "w64": 16, "g32": 8}          # f32 words per row
 
 
 def _bind(L):
@@ -62,6 +65,8 @@ def _bind(L):
     L.ccfd_kc_set_offset_reset.restype = C.c_int
     L.ccfd_kc_position.argtypes = [C.c_void_p, C.c_int]
     L.ccfd_kc_position.restype = C.c_int64
+    L.ccfd_kc_set_bins.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
+    L.ccfd_kc_set_bins.restype = C.c_int
     L._kc_bound = True
     return L
 
@@ -87,31 +92,48 @@ class NativeKafkaConsumer:
         arr = (KcPartition * len(ps))()
         for i, p in enumerate(ps):
             log = engine.logs[p]
-            arr[i] = KcPartition(p, p, int(start_offsets[p]), log.feats.ptr, log.ids.ptr, log.customer.ptr, log.n)
+            arr[i] = KcPartition(p, p, int(start_offsets[p]), log.feats.ptr, log.ids.ptr, log.customer.ptr, log.n,
+                                 log.amount.ptr if log.amount is not None else None)
         host, port = _split(bootstrap)
         h = L.ccfd_kc_create_engine(C.c_void_p(engine.h), host.encode(), port, topic.encode(), arr, len(ps),
-                                    1 if engine.wire else 0)
+                                    ROW_CODES[engine.row_format])
         check(0 if h else -1, "ccfd_kc_create_engine")
-        return cls(h, ps, keep=arr)
+        kc = cls(h, ps, keep=arr)
+        if engine.row_format == "g32":
+            kc._set_bins(engine.bins)
+        return kc
+
+    def _set_bins(self, bins) -> None:
+        """G32 sink: rows are binned at ingest against ``bins`` (models.gbdt.BinSpec)."""
+        flat, off = bins.flat, bins.offsets
+        self._bins_keep = (flat, off)
+        check(lib().ccfd_kc_set_bins(C.c_void_p(self.h), flat.ctypes.data, off.ctypes.data, int(bins.stamp)),
+              "ccfd_kc_set_bins")
 
     @classmethod
     def for_arrays(cls, bootstrap: str, topic: str, start_offsets: Dict[int, int], capacity: int,
-                   wire: bool = False) -> "NativeKafkaConsumer":
-        """Test sink: flat numpy arrays per partition (no engine, no GPU)."""
+                   wire: bool = False, bins=None) -> "NativeKafkaConsumer":
+        """Test sink: flat numpy arrays per partition (no engine, no GPU): ``arrays[p]`` =
+        (rows, ids, customer), ``amounts[p]`` = the Amount column of G32 rows (``bins``)."""
         L = _bind(lib())
         ps = sorted(start_offsets)
-        width = 16 if wire else 30
-        bufs = {p: (np.zeros((capacity, width), np.float32), np.zeros(capacity, np.uint64),
+        fmt = "g32" if bins is not None else "w64" if wire else "f32"
+        bufs = {p: (np.zeros((capacity, ROW_WIDTH[fmt]), np.float32), np.zeros(capacity, np.uint64),
                     np.zeros(capacity, np.uint32)) for p in ps}
+        amounts = {p: np.zeros(capacity, np.float32) for p in ps}
         arr = (KcPartition * len(ps))()
         for i, p in enumerate(ps):
             f, ids, cu = bufs[p]
-            arr[i] = KcPartition(p, i, int(start_offsets[p]), f.ctypes.data, ids.ctypes.data, cu.ctypes.data, capacity)
+            arr[i] = KcPartition(p, i, int(start_offsets[p]), f.ctypes.data, ids.ctypes.data, cu.ctypes.data, capacity,
+                                 amounts[p].ctypes.data)
         host, port = _split(bootstrap)
-        h = L.ccfd_kc_create_array(host.encode(), port, topic.encode(), arr, len(ps), 1 if wire else 0)
+        h = L.ccfd_kc_create_array(host.encode(), port, topic.encode(), arr, len(ps), ROW_CODES[fmt])
         check(0 if h else -1, "ccfd_kc_create_array")
-        kc = cls(h, ps, keep=(arr, bufs))
+        kc = cls(h, ps, keep=(arr, bufs, amounts))
         kc.arrays = bufs
+        kc.amounts = amounts
+        if bins is not None:
+            kc._set_bins(bins)
         return kc
 
     def set_offset_reset(self, policy: str) -> "NativeKafkaConsumer":
@@ -124,7 +146,7 @@ class NativeKafkaConsumer:
         return {p: int(lib().ccfd_kc_position(C.c_void_p(self.h), i)) for i, p in enumerate(self.partitions)}
 
     def start(self) -> "NativeKafkaConsumer":
-        lib().ccfd_kc_start(C.c_void_p(self.h))
+        check(lib().ccfd_kc_start(C.c_void_p(self.h)), "ccfd_kc_start")
         return self
 
     def stop(self) -> None:

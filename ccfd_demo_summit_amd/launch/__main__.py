@@ -219,7 +219,7 @@ def cmd_engine(a, cfg):
 
     from ..metrics.exporter import GpuEngineCollector, MetricsHub
     from ..ops.kernels import DeviceModel
-    from ..parallel.dp import broadcast_blob, init_distributed
+    from ..parallel.dp import broadcast_model, init_distributed, resolve_row_format
     from ..process.kie_server import KieClient
     from ..router.router import Router
     from ..router.rules import RuleSet
@@ -227,22 +227,9 @@ def cmd_engine(a, cfg):
     from .engine_service import EngineService, EngineServiceConfig
     ctx = init_distributed()
     bind_to_gpu(ctx.device.index)
-    blob = None
-    wire = cfg.engine.wire == "w64" or (cfg.engine.wire == "auto" and cfg.engine.model in ("mlp", "lr"))
-    if ctx.rank == 0:
-        model = _model(cfg.engine.model, a.weights, cfg.seed)
-        packed = model.pack(wire=True) if wire else model.pack()
-        blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(ctx.device)
-        trees, depth = getattr(model, "n_trees", 0), getattr(model, "depth", 0)
-    else:
-        trees = depth = 0
-    blob = broadcast_blob(ctx, blob)
-    if ctx.initialized:
-        import torch.distributed as dist
-        td = torch.tensor([trees, depth], device=ctx.device)
-        dist.broadcast(td, 0)
-        trees, depth = int(td[0]), int(td[1])
-    dm = DeviceModel.from_blob(cfg.engine.model, blob, trees, depth, wire=wire)
+    fmt = resolve_row_format(cfg.engine.model, cfg.engine.wire)
+    model = _model(cfg.engine.model, a.weights, cfg.seed) if ctx.rank == 0 else None
+    dm = broadcast_model(ctx, model, cfg.engine.model, fmt)      # X1 (+ G32 bin table)
     broker = _broker(cfg)
     hub = MetricsHub()
     kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)

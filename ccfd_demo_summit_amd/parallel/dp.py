@@ -116,6 +116,43 @@ def broadcast_blob(ctx: DistContext, blob: Optional[torch.Tensor], src: int = 0,
     return blob
 
 
+def resolve_row_format(kind: str, wire: str = "auto") -> str:
+    """Partition-log row format of a model kind: ``auto`` = W64 for the MLP / LR kernels,
+    G32 for GBDT (the PCIe-byte-optimal exact or bf16 formats, contracts/transaction.py)."""
+    if wire == "auto":
+        return "g32" if kind == "gbdt" else "w64"
+    if (wire == "w64" and kind == "gbdt") or (wire == "g32" and kind != "gbdt"):
+        raise ValueError(f"row format {wire} does not apply to model kind {kind}")
+    return wire
+
+
+def broadcast_model(ctx: DistContext, model, kind: str, row_format: str, group=None):
+    """X1 for a whole device model: rank 0 packs ``model`` for ``row_format`` (f32 / w64 /
+    g32) and broadcasts the blob -- plus, for G32, the bin table every rank encodes its
+    partition logs with, and the tree shape; every rank returns an equal DeviceModel.
+    ``model`` is only read on rank 0."""
+    from ..models.gbdt import BinSpec
+    from ..ops.kernels import DeviceModel
+    blob = spec_t = None
+    shape = torch.zeros(2, dtype=torch.int64, device=ctx.device)
+    if ctx.rank == 0:
+        if row_format == "g32":
+            spec = model.bin_spec()
+            packed = model.pack(bins=spec)
+            spec_t = torch.from_numpy(np.frombuffer(spec.to_bytes(), np.uint8).copy()).to(ctx.device)
+        else:
+            packed = model.pack(wire=True) if row_format == "w64" else model.pack()
+        blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(ctx.device)
+        shape[0], shape[1] = getattr(model, "n_trees", 0), getattr(model, "depth", 0)
+    blob = broadcast_blob(ctx, blob, group=group)
+    if ctx.initialized:
+        dist.broadcast(shape, 0, group=group)
+    bins = None
+    if row_format == "g32":
+        bins = BinSpec.from_bytes(broadcast_blob(ctx, spec_t, group=group).cpu().numpy().tobytes())
+    return DeviceModel.from_blob(kind, blob, int(shape[0]), int(shape[1]), wire=row_format == "w64", bins=bins)
+
+
 def _checksum(blob: torch.Tensor) -> torch.Tensor:
     b = blob.to(torch.int64)
     idx = torch.arange(b.numel(), device=b.device, dtype=torch.int64)

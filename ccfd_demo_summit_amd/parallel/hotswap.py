@@ -56,8 +56,15 @@ class HotSwap:
         self.swaps = 0
 
     def offer(self, model) -> None:
-        """Queue ``model`` (same kind as the running one) for the next announcement.  Rank ``src``."""
-        blob = model.pack(wire=True) if getattr(self.engine, "wire", False) else model.pack()
+        """Queue ``model`` (same kind as the running one) for the next announcement.  Rank ``src``.
+        G32 engines (GBDT): the ensemble is packed against the LIVE bin table, so the
+        partition logs need no re-encoding; ValueError if a split threshold is not one of its
+        edges (a retrain that moves thresholds needs a new table: restart with re-encoding)."""
+        bins = getattr(self.engine, "bins", None)
+        if bins is not None:
+            blob = model.pack(bins=bins)
+        else:
+            blob = model.pack(wire=True) if getattr(self.engine, "wire", False) else model.pack()
         with self._lock:
             self._offer = blob
 
@@ -137,5 +144,6 @@ class HotSwap:
     def _swap(self, blob: torch.Tensor) -> None:
         from ..ops.kernels import DeviceModel
         cur = self.engine.dm
-        dm = DeviceModel.from_blob(cur.kind, blob, cur.trees, cur.depth, wire=getattr(cur, "wire", False))
+        dm = DeviceModel.from_blob(cur.kind, blob, cur.trees, cur.depth, wire=getattr(cur, "wire", False),
+                                   bins=getattr(cur, "bins", None))
         self.engine.swap_model(dm)

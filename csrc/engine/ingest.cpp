@@ -214,22 +214,32 @@ inline uint8_t bin_of(const float* e, int ne, float x) {
   }
   return (uint8_t)lo;
 }
+
+inline void encode_row_g32(const float* r, uint8_t* o, const float* edges, const int32_t* offsets, int32_t stamp) {
+  for (int j = 0; j < CCFD_N_FEATURES; ++j)
+    o[j] = bin_of(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]);
+  o[30] = amount_bucket_host(r[CCFD_N_FEATURES - 1]);
+  o[31] = (uint8_t)stamp;
+}
 }  // namespace
+
+namespace ccfd {
+bool g32_table_ok(const float* edges, const int32_t* offsets, int32_t stamp) {
+  if (stamp < 1 || stamp > 255 || !edges || !offsets) return false;
+  for (int j = 0; j < CCFD_N_FEATURES; ++j) {
+    const int ne = offsets[j + 1] - offsets[j];
+    if (offsets[j] < 0 || ne < 0 || ne > 255) return false;
+  }
+  return true;
+}
+}  // namespace ccfd
 
 extern "C" int64_t ccfd_encode_g32(const float* x, int64_t n, int64_t ld, const float* edges,
                                    const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
-  if (ld < CCFD_N_FEATURES || n < 0 || stamp < 1 || stamp > 255 || !edges || !offsets || !out) return -1;
-  for (int j = 0; j < CCFD_N_FEATURES; ++j) {
-    const int ne = offsets[j + 1] - offsets[j];
-    if (offsets[j] < 0 || ne < 0 || ne > 255) return -1;
-  }
+  if (ld < CCFD_N_FEATURES || n < 0 || !out || !ccfd::g32_table_ok(edges, offsets, stamp)) return -1;
   for (int64_t i = 0; i < n; ++i) {
     const float* r = x + i * ld;
-    uint8_t* o = out + i * CCFD_G32_ROW_BYTES;
-    for (int j = 0; j < CCFD_N_FEATURES; ++j)
-      o[j] = bin_of(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]);
-    o[30] = amount_bucket_host(r[CCFD_N_FEATURES - 1]);
-    o[31] = (uint8_t)stamp;
+    encode_row_g32(r, out + i * CCFD_G32_ROW_BYTES, edges, offsets, stamp);
     if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
   }
   return n;
@@ -241,4 +251,7 @@ bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32
   return parse_one(s, e, f, id, cust);
 }
 void encode_w64_row(const float* x, uint8_t* out) { encode_row_w64(x, out); }
+void encode_g32_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp) {
+  encode_row_g32(x, out, edges, offsets, stamp);
+}
 }  // namespace ccfd

@@ -53,6 +53,8 @@ namespace ccfd {
 void set_error(const std::string& e);
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust);
 void encode_w64_row(const float* x, uint8_t* out);
+void encode_g32_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp);
+bool g32_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
 }  // namespace ccfd
 
 namespace {
@@ -102,6 +104,7 @@ struct Sink {
   virtual uint8_t* feats(int p) = 0;
   virtual uint64_t* ids(int p) = 0;
   virtual uint32_t* cust(int p) = 0;
+  virtual float* amount(int p) = 0;         // G32: host-side Amount column (may be NULL)
   virtual int64_t released(int p) = 0;      // rows consumed downstream (for offset commits)
   virtual ~Sink() = default;
 };
@@ -116,6 +119,7 @@ struct EngineSink : Sink {
   uint8_t* feats(int p) override { return (uint8_t*)parts[p].feats; }
   uint64_t* ids(int p) override { return parts[p].ids; }
   uint32_t* cust(int p) override { return parts[p].customer; }
+  float* amount(int p) override { return parts[p].amount; }
   int64_t released(int p) override { return ccfd_engine_cursor(eng, parts[p].engine_partition); }
 };
 
@@ -131,6 +135,7 @@ struct ArraySink : Sink {                  // tests: flat arrays, no wrap, "rele
   uint8_t* feats(int p) override { return (uint8_t*)parts[p].feats; }
   uint64_t* ids(int p) override { return parts[p].ids; }
   uint32_t* cust(int p) override { return parts[p].customer; }
+  float* amount(int p) override { return parts[p].amount; }
   int64_t released(int p) override { return used[p]; }
 };
 
@@ -160,7 +165,10 @@ class Consumer {
  public:
   std::vector<std::pair<std::string, int>> seeds;   // bootstrap list
   std::string topic, client = "ccfd-native";
-  int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64
+  int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64, 2 = G32
+  std::vector<float> g32_edges;                     // G32 bin table (ccfd_kc_set_bins)
+  std::vector<int32_t> g32_off;
+  int32_t g32_stamp = 0;
   int reset_policy = CCFD_KC_RESET_EARLIEST;
   Sink* sink = nullptr;
   std::vector<PState> ps;
@@ -428,7 +436,21 @@ class Consumer {
     return true;
   }
 
-  const int row_bytes() const { return wire ? CCFD_WIRE_ROW_BYTES : CCFD_N_FEATURES * 4; }
+  const int row_bytes() const {
+    return wire == 2 ? CCFD_G32_ROW_BYTES : wire ? CCFD_WIRE_ROW_BYTES : CCFD_N_FEATURES * 4;
+  }
+
+  // one canonical f32 row into the sink's row format at ring row `row`
+  void put_row(int pi, const float* x, uint8_t* dst, int64_t row) {
+    if (wire == 2) {
+      ccfd::encode_g32_row(x, dst, g32_edges.data(), g32_off.data(), g32_stamp);
+      if (float* am = sink->amount(pi)) am[row] = x[CCFD_N_FEATURES - 1];
+    } else if (wire) {
+      ccfd::encode_w64_row(x, dst);
+    } else {
+      std::memcpy(dst, x, CCFD_N_FEATURES * sizeof(float));
+    }
+  }
 
   bool ingest_value(int pi, const uint8_t* v, int32_t vlen, int64_t* rows_out) {
     *rows_out = 0;
@@ -455,7 +477,7 @@ class Consumer {
           float tmp[CCFD_N_FEATURES];
           for (int64_t i = 0; i < k; ++i) {
             std::memcpy(tmp, f + (size_t)(s + i) * kRow, sizeof(tmp));
-            ccfd::encode_w64_row(tmp, dst + i * rb);
+            put_row(pi, tmp, dst + i * rb, row + i);
           }
         } else {
           std::memcpy(dst, f + (size_t)s * kRow, (size_t)k * rb);
@@ -474,9 +496,7 @@ class Consumer {
     const bool ok = write_rows(pi, 1, [&](int64_t row, int64_t, int64_t) {
       sink->ids(pi)[row] = id;
       sink->cust(pi)[row] = cust;
-      uint8_t* dst = sink->feats(pi) + row * rb;
-      if (wire) ccfd::encode_w64_row(x, dst);
-      else std::memcpy(dst, x, rb);
+      put_row(pi, x, sink->feats(pi) + row * rb, row);
     });
     *rows_out = ok ? 1 : 0;
     return ok;
@@ -733,9 +753,20 @@ void* ccfd_kc_create_array(const char* host, int port, const char* topic, const 
   return c;
 }
 
+int ccfd_kc_set_bins(void* kc, const float* edges, const int32_t* offsets, int32_t stamp) {
+  auto* c = static_cast<Consumer*>(kc);
+  if (c->th.joinable()) { ccfd::set_error("kc: set_bins after start"); return -1; }
+  if (!ccfd::g32_table_ok(edges, offsets, stamp)) { ccfd::set_error("kc: bad G32 bin table"); return -1; }
+  c->g32_off.assign(offsets, offsets + CCFD_N_FEATURES + 1);
+  c->g32_edges.assign(edges, edges + std::max(1, offsets[CCFD_N_FEATURES]));
+  c->g32_stamp = stamp;
+  return 0;
+}
+
 int ccfd_kc_start(void* kc) {
   auto* c = static_cast<Consumer*>(kc);
   if (c->th.joinable()) return 0;
+  if (c->wire == 2 && c->g32_stamp == 0) { ccfd::set_error("kc: G32 sink without a bin table"); return -1; }
   c->stop.store(false);
   c->th = std::thread([c] { c->loop(); });
   return 0;

@@ -315,6 +315,7 @@ typedef struct ccfd_kc_partition {
   uint64_t* ids;
   uint32_t* customer;
   int64_t capacity;          // array sink only
+  float* amount;             // G32 rows: host-side Amount column ([capacity] rows), may be NULL
 } ccfd_kc_partition;
 
 typedef struct ccfd_kc_stats {
@@ -343,6 +344,9 @@ const char* ccfd_kc_last_error(void* kc);
 int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n);   // tests / fuzzing
 int ccfd_kc_set_offset_reset(void* kc, int policy);                           // before start
 int64_t ccfd_kc_position(void* kc, int part_index);                           // next offset to fetch
+// G32 sinks (wire = 2): the bin table rows are encoded against (ccfd_encode_g32 layout);
+// required before ccfd_kc_start.  The table is copied.
+int ccfd_kc_set_bins(void* kc, const float* edges, const int32_t* offsets, int32_t stamp);
 
 #ifdef __cplusplus
 }

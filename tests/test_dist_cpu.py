@@ -255,3 +255,45 @@ def test_forced_process_group_at_world_one():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert init and rows == 7 and lat == 256 and mx == 1.5
+
+
+def _model_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.models import build_model
+    from ccfd_demo_summit_amd.parallel import broadcast_model, init_distributed, resolve_row_format
+    ctx = init_distributed(backend="gloo")
+    try:
+        out = {}
+        X, _ = generate(4000, seed=5)
+        for kind in ("gbdt", "mlp"):
+            fmt = resolve_row_format(kind)
+            m = build_model(kind, seed=3, X_ref=X) if ctx.rank == 0 else None
+            dm = broadcast_model(ctx, m, kind, fmt)
+            enc = dm.bins.encode(X[:100]).tobytes() if dm.bins is not None else b""
+            out[kind] = (fmt, bytes(dm.blob.numpy()), dm.trees, dm.depth, dm.row_format, enc)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_model_carries_g32_bin_table():
+    """X1 of a whole device model: every rank gets the same blob, tree shape and (G32) bin
+    table, so every rank encodes its own partition logs identically."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_model_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    fmt, blob, trees, depth, row_format, enc = res[0]["gbdt"]
+    assert fmt == row_format == "g32" and blob[:4] == b"GBB1" and (trees, depth) == (100, 6) and len(enc) == 3200
+    assert res[0]["mlp"][0] == res[0]["mlp"][4] == "w64"

@@ -1,5 +1,5 @@
 """Native Kafka consumer (csrc/engine/kafka_consumer.cpp) against kafka-lite on 127.0.0.1:
-TXB1 batches and JSON transactions land in the sink rows bit-exactly (f32 and W64),
+TXB1 batches and JSON transactions land in the sink rows bit-exactly (f32, W64 and G32),
 offsets become committable once rows are consumed, CRC-corrupted batches are rejected."""
 import json
 import time
@@ -12,6 +12,7 @@ from ccfd_demo_summit_amd.data import generate
 from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
 from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
 from ccfd_demo_summit_amd.ingest.native_consumer import NativeKafkaConsumer
+from ccfd_demo_summit_amd.models import build_model
 
 
 @pytest.fixture()
@@ -30,8 +31,8 @@ def _wait(kc, rows, timeout=20):
     return False
 
 
-@pytest.mark.parametrize("wire", [False, True])
-def test_txb1_and_json_into_rows(lite, wire):
+@pytest.mark.parametrize("fmt", ["f32", "w64", "g32"])
+def test_txb1_and_json_into_rows(lite, fmt):
     kb = KafkaBroker(lite.bootstrap)
     kb.create_topic("odh-demo", 2)
     X, _ = generate(3000, seed=4)
@@ -44,14 +45,20 @@ def test_txb1_and_json_into_rows(lite, wire):
     msgs = [json.dumps({"id": int(ids[i]), "customer_id": int(cu[i]),
                         **{n: float(v) for n, v in zip(FEATURE_NAMES, X[i])}}).encode() for i in range(200)]
     kb.produce_many("odh-demo", msgs, partition=1)
-    kc = NativeKafkaConsumer.for_arrays(lite.bootstrap, "odh-demo", {0: 0, 1: 0}, capacity=4000, wire=wire).start()
+    bins = build_model("gbdt", seed=2, X_ref=X).bin_spec() if fmt == "g32" else None
+    kc = NativeKafkaConsumer.for_arrays(lite.bootstrap, "odh-demo", {0: 0, 1: 0}, capacity=4000, wire=fmt == "w64",
+                                        bins=bins).start()
     try:
         assert _wait(kc, 3200), (kc.stats(), kc.last_error())
         st = kc.stats()
         assert st["records"] == 203 and st["errors"] == 0
         f0, i0, c0 = kc.arrays[0]
         f1, i1, c1 = kc.arrays[1]
-        want = encode_wire(X).view(np.float32).reshape(-1, 16) if wire else X
+        want = {"f32": lambda: X, "w64": lambda: encode_wire(X).view(np.float32).reshape(-1, 16),
+                "g32": lambda: bins.encode(X).view(np.float32).reshape(-1, 8)}[fmt]()
+        if fmt == "g32":             # G32 rows keep Amount host-side (flagged-record column)
+            np.testing.assert_array_equal(kc.amounts[0][:3000], X[:, 29])
+            np.testing.assert_array_equal(kc.amounts[1][:200], X[:200, 29])
         np.testing.assert_array_equal(f0[:3000], want)
         np.testing.assert_array_equal(i0[:3000], ids)
         np.testing.assert_array_equal(c0[:3000], cu)
