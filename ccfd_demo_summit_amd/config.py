@@ -131,6 +131,7 @@ ENV_MAP = {
     "CCFD_INPUT_MODE": ("engine", "input_mode", str),
     "CCFD_OUTPUT_MODE": ("engine", "output_mode", str),
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),
+    "CCFD_KAFKA_PARTITIONS": ("kafka", "partitions", int),
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),
 }
 

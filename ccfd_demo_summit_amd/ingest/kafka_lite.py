@@ -165,14 +165,17 @@ class KafkaLiteServer:
 
     def __init__(self, host: str = "127.0.0.1", port: int = 9092, default_partitions: int = 1,
                  store: Optional[BatchStore] = None, auto_create: bool = True, node_id: int = NODE_ID,
-                 cluster: Optional[ClusterState] = None, metrics: Optional[BrokerMetrics] = None):
+                 cluster: Optional[ClusterState] = None, metrics: Optional[BrokerMetrics] = None,
+                 advertise: Optional[str] = None):
         self.host = host
         self.port = port
+        # host clients are told to connect to (Metadata); a 0.0.0.0 bind needs a real name
+        self.advertise = advertise or host
         self.store = store or BatchStore(default_partitions=default_partitions)
         self.auto_create = auto_create
         self.node_id = node_id
         self.cluster = cluster or ClusterState(self.store)
-        self.cluster.nodes.setdefault(node_id, [host, port, True])
+        self.cluster.nodes.setdefault(node_id, [self.advertise, port, True])
         self._server: Optional[asyncio.base_events.Server] = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._thread: Optional[threading.Thread] = None
@@ -186,7 +189,7 @@ class KafkaLiteServer:
     async def start(self):
         self._server = await asyncio.start_server(self._serve, self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
-        self.cluster.nodes[self.node_id] = [self.host, self.port, True]
+        self.cluster.nodes[self.node_id] = [self.advertise, self.port, True]
         self._reaper = asyncio.get_running_loop().create_task(self._reap_sessions())
 
     def start_in_thread(self) -> "KafkaLiteServer":
@@ -559,13 +562,14 @@ class KafkaLiteCluster:
     event loop over a shared store: leadership p -> node (p % n) + 1 until moved."""
 
     def __init__(self, n: int = 3, host: str = "127.0.0.1", base_port: int = 0, default_partitions: int = 1,
-                 auto_create: bool = True, retention_batches: Optional[int] = None):
+                 auto_create: bool = True, retention_batches: Optional[int] = None,
+                 advertise: Optional[str] = None):
         self.store = BatchStore(default_partitions=default_partitions, retention_batches=retention_batches)
         self.state = ClusterState(self.store)
         self.metrics = BrokerMetrics(self.state)
         self.nodes = [KafkaLiteServer(host, base_port + i if base_port else 0, store=self.store,
                                       auto_create=auto_create, node_id=i + 1, cluster=self.state,
-                                      metrics=self.metrics) for i in range(n)]
+                                      metrics=self.metrics, advertise=advertise) for i in range(n)]
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._thread: Optional[threading.Thread] = None
 
@@ -632,8 +636,9 @@ def main(argv=None):
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--nodes", type=int, default=1, help="broker listeners (leadership spread over them)")
     ap.add_argument("--metrics-port", type=int, default=9404, help="Prometheus /metrics (0 = off)")
+    ap.add_argument("--advertise", default=None, help="host name put in Metadata (default: --host)")
     a = ap.parse_args(argv)
-    cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions)
+    cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions, advertise=a.advertise)
 
     async def run():
         await cl.start()

@@ -4,7 +4,7 @@
     python -m ccfd_demo_summit_amd.launch <service> [options]
 
 services:
-  kafka-lite   single-node Kafka-protocol broker (dev/CI stand-in for Strimzi)
+  kafka-lite   Kafka-protocol broker, --nodes N listeners (dev/CI stand-in for Strimzi)
   seldon       fraud model predict() server            (port 8000, modelfull)
   usertask     user-task model predict() server         (port 5000, ccfd-seldon-model)
   kie          business-process server (KIE REST)       (port 8090)
@@ -18,6 +18,8 @@ services:
                committed counts) + membership generations whose process group carries the
                global X2 counters; a supervised restart rejoins   (--store, --rank, --world)
   supervise    restart-on-crash supervisor:  supervise [--max-restarts N] -- <cmd...>
+  operator     FraudDetection CR -> Kubernetes manifests (--render) or a local reconcile
+               loop of supervised services (--local); accepts the reference's OpenDataHub CR
 
 Configuration: the reference env var names (BROKER_URL, KAFKA_TOPIC, SELDON_URL, ...),
 an optional --config YAML, then flags (ccfd_demo_summit_amd/config.py).
@@ -92,7 +94,8 @@ def _serve_in_thread(app, host, port):
 # ---------------------------------------------------------------------------- services
 def cmd_kafka_lite(a, cfg):
     from ..ingest.kafka_lite import main
-    main(["--host", a.host, "--port", str(a.port or 9092), "--partitions", str(cfg.kafka.partitions)])
+    main(["--host", a.host, "--port", str(a.port or 9092), "--partitions", str(cfg.kafka.partitions),
+          "--nodes", str(a.nodes)] + (["--advertise", a.advertise] if a.advertise else []))
 
 
 def cmd_seldon(a, cfg):
@@ -365,6 +368,33 @@ def cmd_elastic(a, cfg):
     grp.close()
 
 
+def cmd_operator(a, cfg):
+    """FraudDetection CR (or the reference's OpenDataHub CR) -> Kubernetes manifests
+    (--render FILE, '-' = stdout) and/or a local reconcile loop of supervised processes
+    (--local; edits of the CR file scale the running deployment)."""
+    from ..operator import LocalOperator, dump, load, render, validate
+    if not a.cr:
+        raise SystemExit("operator: --cr FILE required")
+    spec = load(a.cr)
+    for n in spec.notes:
+        print(f"[operator] note: {n}", file=sys.stderr)
+    if a.render:
+        manifests = render(spec)
+        probs = validate(manifests)
+        if probs:
+            raise SystemExit("operator: invalid rendering:\n  " + "\n  ".join(probs))
+        text = dump(manifests, f"# rendered from {a.cr} by `launch operator --render`\n")
+        if a.render == "-":
+            sys.stdout.write(text)
+        else:
+            with open(a.render, "w") as f:
+                f.write(text)
+    if a.local:
+        op = LocalOperator(spec, workdir=os.getcwd(), status_path=a.status)
+        t_end = time.time() + a.seconds if "--seconds" in sys.argv else None
+        op.run(a.cr, until=(lambda: time.time() >= t_end) if t_end else None)
+
+
 def cmd_supervise(a, cfg):
     from .supervisor import supervise
     sys.exit(supervise(a.cmd, max_restarts=a.max_restarts, backoff_s=a.backoff))
@@ -381,8 +411,15 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser(prog="python -m ccfd_demo_summit_amd.launch", description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
-                                        "engine", "producer", "demo", "store", "elastic", "supervise"])
+                                        "engine", "producer", "demo", "store", "elastic", "supervise",
+                                        "operator"])
     ap.add_argument("--config", default=None)
+    ap.add_argument("--nodes", type=int, default=1, help="kafka-lite: broker listeners (port, port+1, ...)")
+    ap.add_argument("--advertise", default=None, help="kafka-lite: broker host name clients are given")
+    ap.add_argument("--cr", default=None, help="operator: FraudDetection (or OpenDataHub) CR file")
+    ap.add_argument("--render", default=None, help="operator: write Kubernetes manifests here ('-' = stdout)")
+    ap.add_argument("--local", action="store_true", help="operator: reconcile the CR into local processes")
+    ap.add_argument("--status", default=None, help="operator --local: status JSON file")
     ap.add_argument("--rules", default=None, help="router/engine/demo: routing rule file (overrides ROUTER_RULES)")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=None)

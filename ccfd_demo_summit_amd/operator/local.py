@@ -1,0 +1,217 @@
+"""Local operator: reconciles a FraudDetection CR into supervised processes on this host --
+what the ODH operator does with the reference's CR on a cluster (deploy/frauddetection_cr.yaml;
+SURVEY.md §2.1 C18/C20, §1 L0), for a single MI355X node without Kubernetes.
+
+``reconcile()`` compares the desired replicas of every service (from the CR) with the live
+processes: it starts missing replicas, restarts exited ones (crash-loop back-off like the
+reference's ``restartPolicy: Always`` DeploymentConfigs), stops surplus replicas when the CR
+scales down, and writes a status document (per service: desired / ready / restarts, the
+CR generation it reflects).  ``run()`` re-reads the CR file when it changes, so editing the
+CR is how the local deployment is scaled -- the same declarative loop as on a cluster.
+
+Every replica is its own process group (never exec'd from a GPU-initialised parent); stop
+sends SIGTERM, waits ``grace_s`` (the reference's terminationGracePeriodSeconds 30), then
+SIGKILLs the group.  Local ports: replica r of a service listens on its base port + r.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+from .spec import FraudDetectionSpec, load
+
+PY = [sys.executable, "-m", "ccfd_demo_summit_amd.launch"]
+
+
+@dataclass
+class Replica:
+    proc: subprocess.Popen
+    started: float
+    restarts: int = 0
+    last_exit: Optional[int] = None
+
+
+@dataclass
+class ServiceState:
+    desired: int = 0
+    replicas: Dict[int, Replica] = field(default_factory=dict)
+    restarts: int = 0
+    backoff_until: Dict[int, float] = field(default_factory=dict)
+
+
+def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offset: int = 0) -> Dict[str, tuple]:
+    """service -> (desired replicas, argv factory(replica index), env) for a one-node run;
+    every port is the service's reference port + ``port_offset`` (+ replica index)."""
+    o = port_offset
+    kafka_port = 9092 + o
+    broker = (spec.kafka.bootstrap if not spec.kafka.deploy
+              else ",".join(f"{host}:{kafka_port + i}" for i in range(spec.kafka.brokers)))
+    env = {"BROKER_URL": broker, "KIE_SERVER_URL": f"http://{host}:{8090 + o}", "SELDON_URL": f"http://{host}:{8000 + o}",
+           "CCFD_KAFKA_BACKEND": "kafka", "CCFD_KAFKA_PARTITIONS": str(spec.kafka.partitions),
+           "CCFD_MODEL": spec.engine.model, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    if spec.engine.rules:
+        env["ROUTER_RULES"] = spec.engine.rules
+    env.update(spec.env)
+    w = ["--weights", spec.engine.weights] if spec.engine.weights else []
+    svc: Dict[str, tuple] = {}
+    if spec.kafka.deploy:
+        svc["kafka"] = (1, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite",
+                                      "--nodes", str(spec.kafka.brokers), "--port", str(kafka_port), "--host", host,
+                                      "--partitions", str(spec.kafka.partitions), "--metrics-port", str(9404 + o)])
+    if spec.usertask.deploy:
+        svc["usertask"] = (spec.usertask.replicas, lambda r: PY + ["usertask", "--host", host, "--port", str(5000 + o + r)])
+    if spec.seldon.deploy:
+        svc["seldon"] = (spec.seldon.replicas, lambda r: PY + ["seldon", "--host", host, "--port", str(8000 + o + r)] + w
+                         + (["--native", "--workers", str(spec.seldon.workers)] if spec.seldon.native else []))
+    if spec.kie.deploy:
+        svc["kie"] = (spec.kie.replicas, lambda r: PY + ["kie", "--host", host, "--port", str(8090 + o + r),
+                                                         "--remote-prediction"])
+    if spec.notifier.deploy:
+        svc["notifier"] = (spec.notifier.replicas, lambda r: PY + ["notifier", "--host", host,
+                                                                   "--port", str(8080 + o + r)])
+    if spec.engine.deploy:
+        svc["engine"] = (spec.engine.nodes, lambda r: [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+                                                       "--nproc-per-node", str(spec.engine.gpus_per_node),
+                                                       "--master-addr", "127.0.0.1", "--master-port", str(29500 + o + r)]
+                         + ["-m", "ccfd_demo_summit_amd.launch", "engine", "--host", host,
+                            "--port", str(8091 + o + 16 * r)] + w)
+    if spec.router.deploy:
+        svc["router"] = (spec.router.replicas, lambda r: PY + ["router", "--group-membership", "--host", host,
+                                                               "--port", str(8191 + o + r)])
+    if spec.producer.deploy:
+        svc["producer"] = (1, lambda r: PY + ["producer", "--fmt", spec.producer.format,
+                                              "--count", str(spec.producer.count)])
+    return {k: (n, f, env) for k, (n, f) in svc.items()}
+
+
+class LocalOperator:
+    def __init__(self, spec: FraudDetectionSpec, workdir: str = ".", status_path: Optional[str] = None,
+                 commands: Optional[Dict[str, tuple]] = None, grace_s: float = 30.0, backoff_s: float = 1.0,
+                 max_backoff_s: float = 30.0, log: Callable[[str], None] = print, port_offset: int = 0):
+        self.spec = spec
+        self.workdir = workdir
+        self.status_path = status_path
+        self.grace_s = grace_s
+        self.backoff_s = backoff_s
+        self.max_backoff_s = max_backoff_s
+        self.log = log
+        self.generation = 1
+        self._commands_override = commands
+        self.port_offset = port_offset
+        self.services: Dict[str, ServiceState] = {}
+        self._commands = commands if commands is not None else local_commands(spec, port_offset=port_offset)
+
+    # ------------------------------------------------------------------ spec changes
+    def update(self, spec: FraudDetectionSpec) -> None:
+        """A new CR generation: the next reconcile converges to it."""
+        self.spec = spec
+        self.generation += 1
+        if self._commands_override is None:
+            self._commands = local_commands(spec, port_offset=self.port_offset)
+
+    def _start(self, name: str, r: int) -> Replica:
+        _, argv_of, env = self._commands[name]
+        e = dict(os.environ)
+        e.update(env)
+        p = subprocess.Popen(argv_of(r), cwd=self.workdir, env=e, start_new_session=True,
+                             stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        return Replica(p, time.time())
+
+    def _stop(self, rep: Replica) -> None:
+        if rep.proc.poll() is None:
+            try:
+                os.killpg(rep.proc.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                return
+            try:
+                rep.proc.wait(timeout=self.grace_s)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(rep.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                rep.proc.wait()
+
+    def reconcile(self) -> Dict[str, Dict[str, int]]:
+        now = time.time()
+        for name in list(self.services):
+            if name not in self._commands:                  # service removed from the CR
+                st = self.services.pop(name)
+                for rep in st.replicas.values():
+                    self._stop(rep)
+        for name, (desired, _argv, _env) in self._commands.items():
+            st = self.services.setdefault(name, ServiceState())
+            st.desired = desired
+            for r in sorted((k for k in st.replicas if k >= desired), reverse=True):   # scale down: highest first
+                self._stop(st.replicas.pop(r))
+                st.backoff_until.pop(r, None)
+            for r in range(desired):
+                rep = st.replicas.get(r)
+                if rep is not None and rep.proc.poll() is None:
+                    continue
+                if rep is not None:                                    # exited: restart with back-off
+                    if now < st.backoff_until.get(r, 0.0):
+                        continue
+                    rc = rep.proc.returncode
+                    nxt = self._start(name, r)
+                    nxt.restarts, nxt.last_exit = rep.restarts + 1, rc
+                    st.replicas[r] = nxt
+                    st.restarts += 1
+                    delay = min(self.max_backoff_s, self.backoff_s * (2 ** min(nxt.restarts, 10)))
+                    st.backoff_until[r] = now + delay
+                    self.log(f"[operator] {name}[{r}] exited rc={rc}: restarted (#{nxt.restarts})")
+                else:
+                    st.replicas[r] = self._start(name, r)
+        status = self.status()
+        if self.status_path:
+            tmp = self.status_path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(status, f, indent=1)
+            os.replace(tmp, self.status_path)
+        return status["services"]
+
+    def status(self) -> Dict:
+        svc = {}
+        for name, st in self.services.items():
+            ready = sum(1 for rep in st.replicas.values() if rep.proc.poll() is None)
+            svc[name] = {"desired": st.desired, "ready": ready, "restarts": st.restarts,
+                         "pids": sorted(rep.proc.pid for rep in st.replicas.values() if rep.proc.poll() is None)}
+        return {"name": self.spec.name, "observedGeneration": self.generation, "services": svc,
+                "notes": list(self.spec.notes)}
+
+    def shutdown(self) -> None:
+        for st in self.services.values():
+            for rep in st.replicas.values():
+                self._stop(rep)
+            st.replicas.clear()
+
+    def run(self, cr_path: str, interval_s: float = 1.0, until: Optional[Callable[[], bool]] = None) -> None:
+        """Reconcile loop; re-reads ``cr_path`` whenever it changes (a scale / config edit)."""
+        mtime = os.path.getmtime(cr_path)
+        stopping = {"flag": False}
+
+        def on_signal(_s, _f):
+            stopping["flag"] = True
+        old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+        try:
+            while not stopping["flag"] and not (until and until()):
+                m = os.path.getmtime(cr_path)
+                if m != mtime:
+                    mtime = m
+                    try:
+                        self.update(load(cr_path))
+                        self.log(f"[operator] CR generation {self.generation}")
+                    except Exception as e:                  # keep the running generation
+                        self.log(f"[operator] invalid CR update ignored: {e}")
+                self.reconcile()
+                time.sleep(interval_s)
+        finally:
+            self.shutdown()
+            for s, h in old.items():
+                signal.signal(s, h)

@@ -1,0 +1,255 @@
+"""FraudDetection CR -> Kubernetes manifests (what an operator's reconcile writes to the API
+server).  Service names, ports and env keys are the reference's (deploy/router.yaml,
+deploy/ccd-service.yaml, deploy/notification-service.yaml, deploy/model/modelfull.json,
+deploy/kafka/ProducerDeployment.yaml), so clients and the Grafana dashboards keep working;
+deploy/k8s/ccfd-mi355x.yaml is this module's output for deploy/cr/frauddetection-mi355x.yaml.
+
+``validate(manifests)`` is the structural check the tests run on every rendering: object
+identity, selector <-> template label agreement, Service -> workload selection, ports,
+ConfigMap references, env keys against the reference's contract, GPU requests only where
+a GPU is used.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Any, Dict, List
+
+import yaml
+
+from .spec import FraudDetectionSpec
+
+LAUNCH = ["python", "-m", "ccfd_demo_summit_amd.launch"]
+GRAFANA_DIR = Path(__file__).resolve().parents[2] / "deploy" / "grafana"
+
+
+def _container(spec: FraudDetectionSpec, name: str, command: List[str], ports=(), gpus: int = 0,
+               env=None, envfrom: bool = True) -> Dict[str, Any]:
+    c: Dict[str, Any] = {"name": name, "image": spec.image, "workingDir": "/app", "command": command}
+    if envfrom:
+        c["envFrom"] = [{"configMapRef": {"name": "ccfd-env"}}]
+    if env:
+        c["env"] = [{"name": k, "value": str(v)} for k, v in env.items()]
+    if ports:
+        c["ports"] = [dict(p) for p in ports]
+    if gpus:
+        c["resources"] = {"limits": {"amd.com/gpu": gpus}}
+    return c
+
+
+def _workload(kind: str, name: str, app: str, replicas: int, containers, annotations=None, grace: int = 30,
+              extra_spec=None, volumes=None) -> Dict[str, Any]:
+    tmpl_meta: Dict[str, Any] = {"labels": {"app": app}}
+    if annotations:
+        tmpl_meta["annotations"] = annotations
+    pod: Dict[str, Any] = {"terminationGracePeriodSeconds": grace, "containers": containers}
+    if volumes:
+        pod["volumes"] = volumes
+    spec: Dict[str, Any] = {"replicas": replicas, "selector": {"matchLabels": {"app": app}},
+                            "template": {"metadata": tmpl_meta, "spec": pod}}
+    if kind == "StatefulSet":
+        spec["serviceName"] = name
+    spec.update(extra_spec or {})
+    return {"apiVersion": "apps/v1", "kind": kind, "metadata": {"name": name, "labels": {"app": app}}, "spec": spec}
+
+
+def _service(name: str, app: str, ports) -> Dict[str, Any]:
+    return {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name},
+            "spec": {"selector": {"app": app}, "ports": [dict(p) for p in ports]}}
+
+
+def _scrape(path: str, port: int) -> Dict[str, str]:
+    return {"prometheus.io/scrape": "true", "prometheus.io/path": path, "prometheus.io/port": str(port)}
+
+
+def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
+    from ..parallel.dp import resolve_row_format
+    spec.validate()
+    out: List[Dict[str, Any]] = []
+    env = {"BROKER_URL": spec.broker_url, "KAFKA_TOPIC": "odh-demo",
+           "CUSTOMER_NOTIFICATION_TOPIC": "ccd-customer-outgoing", "CUSTOMER_RESPONSE_TOPIC": "ccd-customer-response",
+           "KIE_SERVER_URL": "http://ccd-service:8090", "SELDON_URL": "http://modelfull-modelfull:8000",
+           "SELDON_ENDPOINT": "api/v0.1/predictions", "FRAUD_THRESHOLD": "0.5", "CONFIDENCE_THRESHOLD": "1.0",
+           "CCFD_MODEL": spec.engine.model, "CCFD_WIRE": resolve_row_format(spec.engine.model, spec.engine.row_format)}
+    if spec.engine.rules:
+        env["ROUTER_RULES"] = spec.engine.rules
+    env.update(spec.env)
+    data = dict(env)
+    data["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"          # dmabuf IPC for RCCL / cross-process tensors
+    out.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "ccfd-env"}, "data": data})
+    weights = ["--weights", spec.engine.weights] if spec.engine.weights else []
+
+    if spec.kafka.deploy:
+        # kafka-lite: one process, `brokers` listeners over a shared controller/store (the
+        # Strimzi cluster of frauddetection_cr.yaml:71-77 in miniature)
+        name = f"{spec.kafka.cluster_name}-kafka"
+        ports = [{"containerPort": 9092 + i, "name": f"broker-{i}"} for i in range(spec.kafka.brokers)]
+        ports.append({"containerPort": 9404, "name": "metrics"})
+        out.append(_workload("StatefulSet", name, name, 1, [_container(
+            spec, "kafka", LAUNCH + ["kafka-lite", "--nodes", str(spec.kafka.brokers), "--port", "9092",
+                                     "--advertise", f"{name}-brokers"],
+            ports=ports, env={"CCFD_KAFKA_PARTITIONS": spec.kafka.partitions}, envfrom=False)],
+            annotations=_scrape("/metrics", 9404)))
+        for svc in (f"{name}-brokers", f"{name}-bootstrap"):
+            out.append(_service(svc, name, [{"name": f"broker-{i}", "port": 9092 + i, "targetPort": 9092 + i}
+                                            for i in range(spec.kafka.brokers)]))
+
+    if spec.engine.deploy:
+        g = spec.engine.gpus_per_node
+        cmd = LAUNCH + ["supervise", "--", "python", "-m", "torch.distributed.run", "--standalone",
+                        "--nproc-per-node", str(g)] + LAUNCH[1:] + ["engine"] + weights
+        out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", spec.engine.nodes, [_container(
+            spec, "engine", cmd, ports=[{"containerPort": 8091, "name": "metrics"}], gpus=g)],
+            annotations=_scrape("/prometheus", 8091)))
+
+    if spec.seldon.deploy:
+        cmd = LAUNCH + ["seldon", "--device", "auto"] + weights
+        if spec.seldon.native:
+            cmd += ["--native", "--workers", str(spec.seldon.workers)]
+        out.append(_workload("Deployment", "modelfull-modelfull", "modelfull", spec.seldon.replicas, [_container(
+            spec, "modelfull", cmd, ports=[{"containerPort": 8000, "name": "http"}], gpus=spec.seldon.gpus)],
+            annotations=_scrape("/prometheus", 8000), grace=20))
+        out.append(_service("modelfull-modelfull", "modelfull", [{"name": "http", "port": 8000, "targetPort": 8000}]))
+
+    if spec.usertask.deploy:
+        out.append(_workload("Deployment", "ccfd-seldon-model", "ccfd-seldon-model", spec.usertask.replicas,
+                             [_container(spec, "usertask", LAUNCH + ["usertask", "--port", "5000"],
+                                         ports=[{"containerPort": 5000, "name": "http"}], envfrom=False)]))
+        out.append(_service("ccfd-seldon-model", "ccfd-seldon-model", [{"name": "http", "port": 5000, "targetPort": 5000}]))
+
+    if spec.kie.deploy:
+        out.append(_workload(
+            "Deployment", "ccd-service", "ccd-service", spec.kie.replicas,
+            [dict(_container(spec, "kie", LAUNCH + ["kie", "--journal", "/data/bp-journal.jsonl", "--remote-prediction"],
+                             ports=[{"containerPort": 8090, "name": "http"}],
+                             env={"SELDON_URL": "ccfd-seldon-model:5000", "SELDON_ENDPOINT": "predict"}),
+                  volumeMounts=[{"name": "journal", "mountPath": "/data"}])],
+            annotations=_scrape("/rest/metrics", 8090),
+            extra_spec={"strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxSurge": "25%", "maxUnavailable": "25%"}}},
+            volumes=[{"name": "journal", "emptyDir": {}}]))
+        out.append(_service("ccd-service", "ccd-service", [{"name": "http", "port": 8090, "targetPort": 8090}]))
+
+    if spec.notifier.deploy:
+        out.append(_workload("Deployment", "ccfd-notification-service", "ccfd-notification-service",
+                             spec.notifier.replicas, [_container(spec, "notifier", LAUNCH + ["notifier"],
+                                                                 ports=[{"containerPort": 8080, "name": "health"}])]))
+
+    if spec.router.deploy:
+        out.append(_workload("Deployment", "ccd-fuse", "ccd-fuse", spec.router.replicas, [_container(
+            spec, "router", LAUNCH + ["supervise", "--"] + LAUNCH + ["router", "--group-membership"],
+            ports=[{"containerPort": 8091, "name": "metrics"}])], annotations=_scrape("/prometheus", 8091),
+            extra_spec={"strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": "25%", "maxSurge": "25%"}}}))
+        out.append(_service("ccd-fuse", "ccd-fuse", [{"name": "metrics", "port": 8091, "targetPort": 8091}]))
+
+    if spec.producer.deploy:
+        p = spec.producer
+        out.append({"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "kafka-producer"},
+                    "spec": {"template": {"metadata": {"labels": {"app": "kafka-producer"}}, "spec": {
+                        "restartPolicy": "OnFailure",
+                        "containers": [_container(spec, "producer", LAUNCH + ["producer", "--fmt", p.format,
+                                                                              "--count", str(p.count)],
+                                                  env={"topic": "odh-demo", "bootstrap": spec.broker_url,
+                                                       "filename": p.csv})]}}}})
+
+    if spec.training.deploy:
+        t = spec.training
+        cmd = ["python", "-m", "torch.distributed.run", "--standalone", "--nproc-per-node", str(t.workers),
+               "-m", "ccfd_demo_summit_amd.train", "--model", t.model, "--out", "/models/model.safetensors"]
+        out.append({"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "ccfd-training"},
+                    "spec": {"template": {"metadata": {"labels": {"app": "ccfd-training"}}, "spec": {
+                        "restartPolicy": "OnFailure",
+                        "containers": [dict(_container(spec, "train", cmd, gpus=t.gpus * t.workers),
+                                            volumeMounts=[{"name": "models", "mountPath": "/models"}])],
+                        "volumes": [{"name": "models", "emptyDir": {}}]}}}})
+
+    if spec.monitoring.deploy:
+        jobs = [{"job_name": "ccfd-pods", "kubernetes_sd_configs": [{"role": "pod"}],
+                 "relabel_configs": [
+                     {"source_labels": ["__meta_kubernetes_pod_annotation_prometheus_io_scrape"], "action": "keep",
+                      "regex": "true"},
+                     {"source_labels": ["__meta_kubernetes_pod_annotation_prometheus_io_path"],
+                      "target_label": "__metrics_path__", "regex": "(.+)"},
+                     {"source_labels": ["__address__", "__meta_kubernetes_pod_annotation_prometheus_io_port"],
+                      "target_label": "__address__", "regex": "([^:]+)(?::\\d+)?;(\\d+)", "replacement": "$1:$2"}]}]
+        out.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "ccfd-prometheus"},
+                    "data": {"prometheus.yml": yaml.safe_dump({"global": {"scrape_interval": "5s"},
+                                                               "scrape_configs": jobs}, sort_keys=False)}})
+        boards = sorted(p.name for p in GRAFANA_DIR.glob("*.json")) if GRAFANA_DIR.is_dir() else []
+        out.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "ccfd-grafana-dashboards",
+                                                                          "annotations": {"ccfd/source": "deploy/grafana"}},
+                    "data": {b: f"deploy/grafana/{b}" for b in boards}})
+    return out
+
+
+def dump(manifests: List[Dict[str, Any]], header: str = "") -> str:
+    return header + yaml.safe_dump_all(manifests, sort_keys=False, width=120)
+
+
+# --------------------------------------------------------------------------- validation
+def validate(manifests: List[Dict[str, Any]]) -> List[str]:
+    """Structural problems of a rendering (empty list = valid)."""
+    from ..config import ENV_MAP
+    from ..contracts.env import REFERENCE_ENV
+    probs: List[str] = []
+    seen = set()
+    workloads = []
+    configmaps = {m["metadata"]["name"] for m in manifests if m.get("kind") == "ConfigMap"}
+    allowed_env = set(REFERENCE_ENV) | set(ENV_MAP) | {"HSA_ENABLE_IPC_MODE_LEGACY", "CCFD_KAFKA_PARTITIONS"}
+    for m in manifests:
+        for k in ("apiVersion", "kind", "metadata"):
+            if k not in m:
+                probs.append(f"object without {k}: {m}")
+        key = (m.get("kind"), m.get("metadata", {}).get("name"))
+        if key in seen:
+            probs.append(f"duplicate {key}")
+        seen.add(key)
+        kind = m.get("kind")
+        if kind == "ConfigMap":
+            for k in m.get("data", {}):
+                if m["metadata"]["name"] == "ccfd-env" and k not in allowed_env:
+                    probs.append(f"ccfd-env: unknown env key {k}")
+        if kind in ("Deployment", "StatefulSet", "Job"):
+            tmpl = m["spec"]["template"]
+            labels = tmpl.get("metadata", {}).get("labels", {})
+            if kind != "Job":
+                sel = m["spec"]["selector"]["matchLabels"]
+                if any(labels.get(k) != v for k, v in sel.items()):
+                    probs.append(f"{key}: selector {sel} does not match template labels {labels}")
+                if m["spec"].get("replicas", 1) < 0:
+                    probs.append(f"{key}: negative replicas")
+                workloads.append(labels)
+            ports = set()
+            for c in tmpl["spec"]["containers"]:
+                if not c.get("image") or not c.get("command"):
+                    probs.append(f"{key}/{c.get('name')}: image and command required")
+                for p in c.get("ports", []):
+                    if p["containerPort"] in ports:
+                        probs.append(f"{key}: duplicate container port {p['containerPort']}")
+                    ports.add(p["containerPort"])
+                for ef in c.get("envFrom", []):
+                    if ef["configMapRef"]["name"] not in configmaps:
+                        probs.append(f"{key}: envFrom unknown ConfigMap {ef['configMapRef']['name']}")
+                for e in c.get("env", []):
+                    if e["name"] not in allowed_env:
+                        probs.append(f"{key}: unknown env key {e['name']}")
+                gpu = c.get("resources", {}).get("limits", {}).get("amd.com/gpu", 0)
+                if gpu and c["name"] not in ("engine", "modelfull", "train"):
+                    probs.append(f"{key}: GPU requested by {c['name']}")
+                if c["name"] == "engine":
+                    cmd = c["command"]
+                    nproc = int(cmd[cmd.index("--nproc-per-node") + 1])
+                    if nproc != gpu:
+                        probs.append(f"{key}: {nproc} ranks for {gpu} GPUs (one rank per GPU)")
+            m["_ports"] = ports
+    for m in manifests:
+        if m.get("kind") == "Service":
+            sel = m["spec"]["selector"]
+            targets = [w for w in manifests if w.get("kind") in ("Deployment", "StatefulSet")
+                       and all(w["spec"]["template"]["metadata"]["labels"].get(k) == v for k, v in sel.items())]
+            if not targets:
+                probs.append(f"Service {m['metadata']['name']}: selects no workload")
+            for p in m["spec"]["ports"]:
+                if targets and all(p["targetPort"] not in t.get("_ports", ()) for t in targets):
+                    probs.append(f"Service {m['metadata']['name']}: targetPort {p['targetPort']} not exposed")
+    for m in manifests:
+        m.pop("_ports", None)
+    return probs

@@ -1,0 +1,176 @@
+"""Operator analogue: the FraudDetection CR parses and validates,
+renders into a structurally valid set of Kubernetes objects (the checked-in
+deploy/k8s/ccfd-mi355x.yaml IS that rendering), the reference's OpenDataHub CR maps onto it,
+and the local reconcile loop starts / restarts / scales / stops supervised processes -- including
+a real 3-listener kafka-lite cluster that a Kafka client then uses."""
+import copy
+import os
+import random
+import signal
+import sys
+import time
+from pathlib import Path
+
+import pytest
+import yaml
+
+from ccfd_demo_summit_amd.operator import (FraudDetectionSpec, LocalOperator, SpecError, load, parse, render,
+                                           validate)
+
+ROOT = Path(__file__).resolve().parents[1]
+CR = ROOT / "deploy" / "cr" / "frauddetection-mi355x.yaml"
+
+
+def _doc():
+    return yaml.safe_load(CR.read_text())
+
+
+def test_default_cr_renders_the_checked_in_manifests():
+    spec = load(str(CR))
+    ms = render(spec)
+    assert validate(ms) == []
+    checked_in = [d for d in yaml.safe_load_all((ROOT / "deploy/k8s/ccfd-mi355x.yaml").read_text()) if d]
+    assert checked_in == ms, "deploy/k8s/ccfd-mi355x.yaml is stale: re-render it from the CR"
+    kinds = {(m["kind"], m["metadata"]["name"]) for m in ms}
+    # the reference's service names (router.yaml, ccd-service.yaml, modelfull.json, ...)
+    for k in [("Service", "modelfull-modelfull"), ("Service", "ccd-service"), ("Service", "ccfd-seldon-model"),
+              ("Deployment", "ccfd-notification-service"), ("Job", "kafka-producer"),
+              ("Service", "odh-message-bus-kafka-brokers"), ("StatefulSet", "ccfd-engine")]:
+        assert k in kinds, k
+
+
+def test_cr_fields_drive_the_rendering():
+    d = _doc()
+    d["spec"]["kafka"]["brokers"] = 5
+    d["spec"]["engine"].update(nodes=2, gpusPerNode=4, model="gbdt")
+    d["spec"]["seldon"]["replicas"] = 3
+    d["spec"]["router"] = {"deploy": True, "replicas": 2}
+    d["spec"]["training"] = {"deploy": True, "workers": 4, "model": "gbdt", "gpus": 1}
+    ms = render(parse(d))
+    assert validate(ms) == []
+    by = {(m["kind"], m["metadata"]["name"]): m for m in ms}
+    env = by[("ConfigMap", "ccfd-env")]["data"]
+    assert env["BROKER_URL"].count(",") == 4 and env["CCFD_WIRE"] == "g32" and env["CCFD_MODEL"] == "gbdt"
+    eng = by[("StatefulSet", "ccfd-engine")]
+    c = eng["spec"]["template"]["spec"]["containers"][0]
+    assert eng["spec"]["replicas"] == 2 and c["resources"]["limits"]["amd.com/gpu"] == 4
+    assert c["command"][c["command"].index("--nproc-per-node") + 1] == "4"
+    assert by[("Deployment", "modelfull-modelfull")]["spec"]["replicas"] == 3
+    assert by[("Deployment", "ccd-fuse")]["spec"]["replicas"] == 2
+    kafka = by[("StatefulSet", "odh-message-bus-kafka")]["spec"]["template"]["spec"]["containers"][0]
+    assert len([p for p in kafka["ports"] if p["name"].startswith("broker")]) == 5
+    train = by[("Job", "ccfd-training")]["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert train[train.index("--nproc-per-node") + 1] == "4" and "gbdt" in train
+
+
+@pytest.mark.parametrize("patch,msg", [
+    (lambda s: s["engine"].update(gpusPerNode=9), "gpus_per_node"),
+    (lambda s: s["engine"].update(model="gbdt", rowFormat="w64"), "row_format"),
+    (lambda s: s["env"].update(NOT_A_KEY="1"), "unknown keys"),
+    (lambda s: s["kafka"].update(replicas=3), "unknown field"),
+    (lambda s: s["seldon"].update(replicas="two"), "integer"),
+    (lambda s: s["kafka"].update(deploy=False), "bootstrap"),
+])
+def test_invalid_crs_are_refused(patch, msg):
+    d = _doc()
+    patch(d["spec"])
+    with pytest.raises(SpecError, match=msg):
+        parse(d)
+
+
+def test_reference_opendatahub_cr_maps_onto_the_stack():
+    odh = {"apiVersion": "opendatahub.io/v1alpha1", "kind": "OpenDataHub", "metadata": {"name": "example"},
+           "spec": {"aicoe-jupyterhub": {"odh_deploy": True, "spark_worker_nodes": 2},
+                    "spark-operator": {"odh_deploy": True}, "seldon": {"odh_deploy": True},
+                    "kafka": {"odh_deploy": True, "kafka_cluster_name": "odh-message-bus",
+                              "kafka_broker_replicas": 3, "kafka_zookeeper_replicas": 3},
+                    "monitoring": {"odh_deploy": True}, "beakerx": {"odh_deploy": False}}}
+    spec = parse(odh)
+    assert spec.kafka.brokers == 3 and spec.kafka.cluster_name == "odh-message-bus"
+    assert spec.training.deploy and spec.training.workers == 2 and spec.seldon.deploy and spec.monitoring.deploy
+    assert any("zookeeper" in n for n in spec.notes) and any("notebook" in n for n in spec.notes)
+    assert spec.broker_url.startswith("odh-message-bus-kafka-brokers:9092")
+    assert validate(render(spec)) == []
+
+
+def test_validate_reports_broken_manifests():
+    ms = render(load(str(CR)))
+    bad = copy.deepcopy(ms)
+    by = {(m["kind"], m["metadata"]["name"]): m for m in bad}
+    by[("Deployment", "ccd-service")]["spec"]["selector"]["matchLabels"]["app"] = "nope"
+    by[("Service", "modelfull-modelfull")]["spec"]["ports"][0]["targetPort"] = 1234
+    eng = by[("StatefulSet", "ccfd-engine")]["spec"]["template"]["spec"]["containers"][0]
+    eng["resources"]["limits"]["amd.com/gpu"] = 4
+    by[("Deployment", "ccfd-notification-service")]["spec"]["template"]["spec"]["containers"][0]["env"] = \
+        [{"name": "WHATEVER", "value": "1"}]
+    probs = "\n".join(validate(bad))
+    assert "does not match template labels" in probs
+    assert "targetPort 1234" in probs
+    assert "8 ranks for 4 GPUs" in probs
+    assert "unknown env key WHATEVER" in probs
+
+
+SLEEPER = [sys.executable, "-c", "import time; time.sleep(120)"]
+
+
+def test_local_operator_reconciles_restarts_scales_and_stops(tmp_path):
+    spec = FraudDetectionSpec()
+    cmds = {"router": (2, lambda r: SLEEPER, {}), "kie": (1, lambda r: SLEEPER, {})}
+    status = tmp_path / "status.json"
+    op = LocalOperator(spec, status_path=str(status), commands=cmds, grace_s=5, backoff_s=0.0, log=lambda m: None)
+    try:
+        st = op.reconcile()
+        assert st["router"]["ready"] == 2 and st["kie"]["ready"] == 1
+        victim = op.services["router"].replicas[1].proc
+        os.killpg(victim.pid, signal.SIGKILL)
+        victim.wait()
+        st = op.reconcile()
+        assert st["router"]["ready"] == 2 and st["router"]["restarts"] == 1
+        assert op.services["router"].replicas[1].proc.pid != victim.pid
+        # a new CR generation scales the router down to 1 and removes kie
+        op._commands = {"router": (1, lambda r: SLEEPER, {})}
+        op.generation += 1
+        st = op.reconcile()
+        assert st == {"router": {"desired": 1, "ready": 1, "restarts": 1,
+                                 "pids": [op.services["router"].replicas[0].proc.pid]}}
+        import json
+        doc = json.loads(status.read_text())
+        assert doc["observedGeneration"] == 2 and doc["services"]["router"]["ready"] == 1
+    finally:
+        procs = [rep.proc for st in op.services.values() for rep in st.replicas.values()]
+        op.shutdown()
+    assert all(p.poll() is not None for p in procs)
+
+
+def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
+    """Only the CR's kafka section deployed: the operator starts kafka-lite with 3 listeners
+    and a Kafka client produces to / fetches from it through the bootstrap list."""
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    d = _doc()
+    for k in ("engine", "seldon", "usertask", "kie", "notifier", "producer", "monitoring"):
+        d["spec"][k]["deploy"] = False
+    d["spec"]["kafka"].update(brokers=3, partitions=6)
+    spec = parse(d)
+    off = random.randint(20000, 40000)
+    op = LocalOperator(spec, workdir=str(ROOT), commands=None, grace_s=5, log=lambda m: None, port_offset=off)
+    try:
+        assert op.reconcile()["kafka"]["ready"] == 1
+        bootstrap = ",".join(f"127.0.0.1:{9092 + off + i}" for i in range(3))
+        kb = KafkaBroker(bootstrap, connect_wait_s=60.0)
+        try:
+            kb.create_topic("odh-demo", 6)
+            for p in range(6):
+                kb.produce("odh-demo", f"tx-{p}".encode(), partition=p)
+            c = kb.consumer("g", ["odh-demo"])
+            got = []
+            t0 = time.time()
+            while len(got) < 6 and time.time() - t0 < 30:
+                got += [r.value for r in c.poll(max_records=100)]
+            assert sorted(got) == sorted(f"tx-{p}".encode() for p in range(6))
+            kb.metadata(["odh-demo"])
+            leaders = {n for (t, _p), n in kb._leaders.items() if t == "odh-demo"}
+            assert len(leaders) == 3                                           # leadership spread over 3 nodes
+        finally:
+            kb.close()
+    finally:
+        op.shutdown()
