@@ -7,6 +7,7 @@ the GBDT (train/trainer.py); rank 0 evaluates and writes.
 
     python -m ccfd_demo_summit_amd.train --model mlp --out model.safetensors
     torchrun --nproc-per-node 2 -m ccfd_demo_summit_amd.train --model gbdt --csv creditcard.csv --out m.st
+    python -m ccfd_demo_summit_amd.train --from-catboost model.json --out m.st   # import, no training
 """
 from __future__ import annotations
 
@@ -33,7 +34,17 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--version", default="1")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--from-catboost", default=None,
+                    help="import an oblivious CatBoost JSON model (models/gbdt_import.py) instead of training")
     a = ap.parse_args(argv)
+    if a.from_catboost:
+        from ..models import save_model
+        from ..models.gbdt_import import from_catboost_json
+        m = from_catboost_json(a.from_catboost)
+        save_model(m, a.out, version=a.version)
+        print(json.dumps({"model": "gbdt", "imported": a.from_catboost, "out": a.out, "trees": m.n_trees,
+                          "depth": m.depth}), flush=True)
+        return 0
 
     import torch
     import torch.distributed as dist
