@@ -485,6 +485,8 @@ def main(argv=None):
         # K7: per-micro-batch execution window on the GPU's own clock (rank 0)
         "device_exec_us_mean": round(st_final.dev_exec_mean_us, 2),
         "device_exec_us_p50": rank_info["device_exec_us_p50"],
+        "device_exec_us_p99": (round(hist_quantile(st_final.dev_hist.astype(np.int64), 0.99) / 1e3, 2)
+                               if st_final.dev_batches else None),
         "rows_scored": total_rows,
         "rows_expected": expected,
         "fraud_routed": int(counters[1]) - fraud0,

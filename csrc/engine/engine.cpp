@@ -153,6 +153,63 @@ class Engine {
   double wall_ns_per_tick = 0.0;   // device wall clock (s_memrealtime) period
   unsigned long long done_counter = 0;
 
+  // Completion stamper (CCFD_COMPLETION_THREAD, default on): a host thread that watches the
+  // kernel-published completion records of the in-flight micro-batches and stamps the host
+  // time each one lands, so a batch's latency ends when its results are in host memory, not
+  // when the pump thread next looks (between pump() calls the caller runs the router
+  // hand-off and the X2 tick: without the stamper those milliseconds were charged to every
+  // batch that completed meanwhile -- the p99 tail).  One packed word per slot: the low 16
+  // bits of the awaited sequence number << 48 | ns since the engine started (48 bits), so a
+  // stamp can never be attributed to another use of the slot.
+  bool stamper_on = false;
+  int64_t stamp_base_ns = 0;
+  std::unique_ptr<std::atomic<unsigned long long>[]> st_armed;            // awaited seq (0 = idle)
+  std::unique_ptr<std::atomic<const volatile unsigned long long*>[]> st_ptr;
+  std::unique_ptr<std::atomic<uint64_t>[]> st_word;                       // tag << 48 | t
+  std::thread stamper;
+  std::atomic<bool> stamper_stop{false};
+
+  static constexpr uint64_t kStampMask = (1ull << 48) - 1;
+
+  void stamper_loop() {
+    prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+    const int D = (int)slots.size();
+    while (!stamper_stop.load(std::memory_order_relaxed)) {
+      bool any = false;
+      for (int i = 0; i < D; ++i) {
+        const unsigned long long e = st_armed[i].load(std::memory_order_acquire);
+        if (!e) continue;
+        any = true;
+        const uint64_t tag = (uint64_t)(e & 0xffffull) << 48;
+        if ((st_word[i].load(std::memory_order_relaxed) & ~kStampMask) == tag) continue;   // stamped
+        const volatile unsigned long long* p = st_ptr[i].load(std::memory_order_relaxed);
+        if (p && p[0] == e)
+          st_word[i].store(tag | ((uint64_t)(now_ns() - stamp_base_ns) & kStampMask), std::memory_order_release);
+      }
+      if (any) cpu_relax();
+      else std::this_thread::sleep_for(std::chrono::microseconds(2));
+    }
+  }
+
+  // after s.done_ptr / s.expect are set for a kernel-published completion
+  void arm(Slot& s) {
+    if (!stamper_on) return;
+    const size_t i = (size_t)(&s - slots.data());
+    st_ptr[i].store(s.done_ptr, std::memory_order_relaxed);
+    st_armed[i].store(s.expect, std::memory_order_release);
+  }
+
+  // host time the completion record of `s` landed (stamper), else `fallback`
+  int64_t landed_ns(Slot& s, int64_t fallback) {
+    if (!stamper_on || !s.use_flag) return fallback;
+    const size_t i = (size_t)(&s - slots.data());
+    const uint64_t w = st_word[i].load(std::memory_order_acquire);
+    st_armed[i].store(0, std::memory_order_relaxed);
+    if ((w >> 48) != (s.expect & 0xffffull)) return fallback;
+    const int64_t t = stamp_base_ns + (int64_t)(w & kStampMask);
+    return (t <= fallback && t >= s.t_submit) ? t : fallback;
+  }
+
   int init(const ccfd_engine_config& c) {
     cfg = c;
     if (cfg.max_batch <= 0 || cfg.depth <= 0 || cfg.n_streams <= 0) {
@@ -217,6 +274,17 @@ class Engine {
     // never hipDeviceSynchronize here: another engine's persistent kernel may be resident
     HIPCHK(hipStreamSynchronize(streams[0]));
     ring.resize(std::max(1024, cfg.flag_capacity));
+    stamper_on = true;
+    if (const char* e = std::getenv("CCFD_COMPLETION_THREAD")) stamper_on = std::atoi(e) != 0;
+    if (stamper_on) {
+      const size_t D = slots.size();
+      st_armed.reset(new std::atomic<unsigned long long>[D]);
+      st_ptr.reset(new std::atomic<const volatile unsigned long long*>[D]);
+      st_word.reset(new std::atomic<uint64_t>[D]);
+      for (size_t i = 0; i < D; ++i) { st_armed[i] = 0; st_ptr[i] = nullptr; st_word[i] = 0; }
+      stamp_base_ns = now_ns();
+      stamper = std::thread([this] { stamper_loop(); });
+    }
     if (cfg.exec_mode == 1) return persist_init();
     return 0;
   }
@@ -384,10 +452,13 @@ class Engine {
     s.expect = sq + 1;
     s.use_flag = true;
     s.done_ptr = reinterpret_cast<volatile unsigned long long*>(pctl->done[sq % cfg.depth]);
+    arm(s);
     __atomic_store_n(&pctl->posted, sq + 1, __ATOMIC_RELEASE);
   }
 
   ~Engine() {
+    stamper_stop.store(true);
+    if (stamper.joinable()) stamper.join();
     hipSetDevice(cfg.device);
     persist_free();
     for (auto& s : slots) {
@@ -491,7 +562,8 @@ class Engine {
     const int64_t t = now_ns();
     t_wait_ns += t - tw;
     const int64_t t0 = s.t_arrival ? s.t_arrival : s.t_submit;   // ring: end-to-end from commit
-    const double us = (t - t0) * 1e-3;
+    const int64_t t_landed = landed_ns(s, t);                   // results in host memory
+    const double us = (t_landed - t0) * 1e-3;
     ++lat_n;
     lat_sum_us += us;
     lat_max_us = std::max(lat_max_us, us);
@@ -582,6 +654,7 @@ class Engine {
       a.done_rec = s.h_done_dev;
       a.done_seq = s.expect;
       s.done_ptr = s.h_done;
+      arm(s);
       a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate;
     }
     a.flags |= wire_flag;
@@ -629,6 +702,7 @@ class Engine {
       s.use_flag = true;
       s.expect = ++done_counter;
       s.done_ptr = s.h_done;
+      arm(s);
       s.busy = true;
       m.sub[k] = ccfd_sub_batch{s.h_proba_dev, s.h_route_dev, s.d_ctl, s.h_flag_dev, s.h_done_dev, s.expect};
     }
@@ -738,6 +812,7 @@ class Engine {
       ++seq;
       rc = wait_done(s);
       if (rc) return rc;
+      landed_ns(s, 0);                                 // disarm the stamper
       s.busy = false;
       completed_upto = std::max<int64_t>(completed_upto, s.seq_no + 1);
       if (proba_out) std::memcpy(proba_out + off, s.h_proba, rows * sizeof(float));
