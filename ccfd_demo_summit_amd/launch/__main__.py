@@ -391,8 +391,8 @@ def cmd_operator(a, cfg):
                 f.write(text)
     if a.local:
         op = LocalOperator(spec, workdir=os.getcwd(), status_path=a.status)
-        t_end = time.time() + a.seconds if "--seconds" in sys.argv else None
-        op.run(a.cr, until=(lambda: time.time() >= t_end) if t_end else None)
+        t_end = time.time() + a.seconds
+        op.run(a.cr, until=(lambda: time.time() >= t_end) if a.seconds > 0 else None)
 
 
 def cmd_supervise(a, cfg):
@@ -454,8 +454,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     a.cmd = cmd
     if a.service == "elastic" and a.partitions <= 0:
         a.partitions = 2 * a.world
-    if a.service == "elastic" and a.seconds == 10.0 and "--seconds" not in argv:
-        a.seconds = 0.0                 # elastic ranks run until the store says stop
+    if a.service in ("elastic", "operator") and a.seconds == 10.0 and "--seconds" not in argv:
+        a.seconds = 0.0                 # elastic ranks / the operator run until stopped
     return a
 
 

@@ -127,6 +127,10 @@ class GpuEngineCollector:
         rows = CounterMetricFamily(M.GPU_ROWS, "Rows scored on the GPU", labels=["rank"])
         rows.add_metric([self.rank_label], float(cnt[0]))
         yield rows
+        stale = CounterMetricFamily(M.GPU_PREFIX + "wire_stale_rows",
+                                    "G32 rows refused for another bin table's stamp (never scored)", labels=["rank"])
+        stale.add_metric([self.rank_label], float(cnt[4]))
+        yield stale
         fr = GaugeMetricFamily(M.GPU_GLOBAL_FRAUD_RATE, "Global fraud-route rate (all-reduced)",
                                labels=["rank"])
         fr.add_metric([self.rank_label], float(cnt[1]) / max(1.0, float(cnt[0])))

@@ -22,6 +22,7 @@ import subprocess
 import sys
 import time
 from dataclasses import dataclass, field
+from pathlib import Path
 from typing import Callable, Dict, List, Optional
 
 from .spec import FraudDetectionSpec, load
@@ -119,6 +120,8 @@ class LocalOperator:
         _, argv_of, env = self._commands[name]
         e = dict(os.environ)
         e.update(env)
+        root = str(Path(__file__).resolve().parents[2])             # the package, from any cwd
+        e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
         p = subprocess.Popen(argv_of(r), cwd=self.workdir, env=e, start_new_session=True,
                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         return Replica(p, time.time())
