@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -183,9 +184,12 @@ class Engine {
         const uint64_t tag = (uint64_t)(e & 0xffffull) << 48;
         if ((st_word[i].load(std::memory_order_relaxed) & ~kStampMask) == tag) continue;   // stamped
         const volatile unsigned long long* p = st_ptr[i].load(std::memory_order_relaxed);
-        if (p && p[0] == e)
+        if (p && p[0] == e) {
           st_word[i].store(tag | ((uint64_t)(now_ns() - stamp_base_ns) & kStampMask), std::memory_order_release);
+          stamps_written.fetch_add(1, std::memory_order_relaxed);
+        }
       }
+      stamper_iters.fetch_add(1, std::memory_order_relaxed);
       if (any) cpu_relax();
       else std::this_thread::sleep_for(std::chrono::microseconds(2));
     }
@@ -200,14 +204,19 @@ class Engine {
   }
 
   // host time the completion record of `s` landed (stamper), else `fallback`
+  uint64_t stamp_used = 0, stamp_missed = 0, stamp_rejected = 0;   // CCFD_STAMPER_DEBUG report
+  std::atomic<uint64_t> stamps_written{0}, stamper_iters{0};
+
   int64_t landed_ns(Slot& s, int64_t fallback) {
     if (!stamper_on || !s.use_flag) return fallback;
     const size_t i = (size_t)(&s - slots.data());
     const uint64_t w = st_word[i].load(std::memory_order_acquire);
     st_armed[i].store(0, std::memory_order_relaxed);
-    if ((w >> 48) != (s.expect & 0xffffull)) return fallback;
+    if ((w >> 48) != (s.expect & 0xffffull)) { ++stamp_missed; return fallback; }
     const int64_t t = stamp_base_ns + (int64_t)(w & kStampMask);
-    return (t <= fallback && t >= s.t_submit) ? t : fallback;
+    if (t <= fallback && t >= s.t_submit) { ++stamp_used; return t; }
+    ++stamp_rejected;
+    return fallback;
   }
 
   int init(const ccfd_engine_config& c) {
@@ -459,6 +468,11 @@ class Engine {
   ~Engine() {
     stamper_stop.store(true);
     if (stamper.joinable()) stamper.join();
+    if (std::getenv("CCFD_STAMPER_DEBUG"))
+      std::fprintf(stderr, "[engine] completion stamps used %llu missed %llu rejected %llu written %llu iters %llu\n",
+                   (unsigned long long)stamp_used, (unsigned long long)stamp_missed,
+                   (unsigned long long)stamp_rejected, (unsigned long long)stamps_written.load(),
+                   (unsigned long long)stamper_iters.load());
     hipSetDevice(cfg.device);
     persist_free();
     for (auto& s : slots) {
@@ -564,6 +578,7 @@ class Engine {
     const int64_t t0 = s.t_arrival ? s.t_arrival : s.t_submit;   // ring: end-to-end from commit
     const int64_t t_landed = landed_ns(s, t);                   // results in host memory
     const double us = (t_landed - t0) * 1e-3;
+
     ++lat_n;
     lat_sum_us += us;
     lat_max_us = std::max(lat_max_us, us);
@@ -571,7 +586,7 @@ class Engine {
       const double fb = us / kFineUs;
       if (fb < kFineBuckets) ++lat_fine[(size_t)fb]; else ++lat_over;
     }
-    const double ns = (double)std::max<int64_t>(1, t - t0);
+    const double ns = (double)std::max<int64_t>(1, t_landed - t0);
     lat_hist[std::min(255, (int)std::floor(4.0 * std::log2(ns)))]++;
     uint64_t nf = 0;
     if (s.use_flag) {

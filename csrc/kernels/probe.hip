@@ -94,3 +94,48 @@ extern "C" double ccfd_bw_probe_chunked(const void* src_host, size_t bytes, size
   for (int i = 0; i < nstreams; ++i) hipStreamDestroy(ss[i]);
   return sec > 0 ? (double)(nchunks * chunk) * iters / sec / 1e9 : -3.0;
 }
+
+// Mixed feed: can the H2D link carry more than one feeder alone?  A fraction `zc_frac` of
+// `bytes` is read by a zero-copy kernel while `n_sdma` streams copy the rest (equal slices)
+// with SDMA, all concurrently; returns the aggregate GB/s over host wall time.  (Roofline
+// question behind the W64 headline: 55.3 GB/s zero-copy vs 57.2 GB/s SDMA alone.)
+extern "C" double ccfd_bw_probe_mix(const void* src_host, size_t bytes, int n_sdma, double zc_frac, int iters,
+                                    void* dev_scratch) {
+  if (n_sdma < 0 || n_sdma > 8 || zc_frac < 0.0 || zc_frac > 1.0 || iters < 1) return -1.0;
+  if (n_sdma == 0 && zc_frac < 1.0) return -1.0;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(src_host), 0) != hipSuccess) return -2.0;
+  const size_t zc = ((size_t)(zc_frac * (double)bytes)) & ~(size_t)4095;
+  const size_t rest = bytes - zc;
+  hipStream_t ks, ss[8];
+  hipStreamCreateWithFlags(&ks, hipStreamNonBlocking);
+  for (int i = 0; i < n_sdma; ++i) hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking);
+  const char* hsrc = static_cast<const char*>(src_host);
+  char* dst = static_cast<char*>(dev_scratch);
+  auto pass = [&]() {
+    if (zc)
+      hipLaunchKernelGGL(read_sum_kernel, dim3(2048), dim3(256), 0, ks, reinterpret_cast<const float4*>(d), zc / 16,
+                         reinterpret_cast<float*>(dst));
+    if (n_sdma > 0 && rest) {
+      const size_t slice = (rest / n_sdma) & ~(size_t)4095;
+      for (int i = 0; i < n_sdma; ++i) {
+        const size_t off = zc + (size_t)i * slice;
+        const size_t len = i + 1 == n_sdma ? bytes - off : slice;
+        hipMemcpyAsync(dst + off, hsrc + off, len, hipMemcpyHostToDevice, ss[i]);
+      }
+    }
+  };
+  auto sync = [&]() {
+    hipStreamSynchronize(ks);
+    for (int i = 0; i < n_sdma; ++i) hipStreamSynchronize(ss[i]);
+  };
+  pass();
+  sync();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < iters; ++i) pass();
+  sync();
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  hipStreamDestroy(ks);
+  for (int i = 0; i < n_sdma; ++i) hipStreamDestroy(ss[i]);
+  return s > 0 ? (double)bytes * iters / s / 1e9 : -3.0;
+}
