@@ -120,6 +120,16 @@ def test_host_runtime_under_asan(tmp_path):
         "out = np.zeros((1000, 64), np.uint8)\n"
         "assert L.ccfd_encode_w64(X.ctypes.data, 1000, 30, out.ctypes.data) == 1000\n"
         "assert L.ccfd_crc32c(bytes(range(256)) * 100, 25600, 0) != 0\n"
+        "# G32 encoder (binary search over the bin table), incl. NaN/inf rows and a refused table\n"
+        "from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT\n"
+        "spec = ObliviousGBDT.random_init(50, 6, seed=0, X_ref=X).bin_spec()\n"
+        "flat, offs = spec.flat, spec.offsets\n"
+        "X[3, 4] = np.nan; X[5, 6] = np.inf\n"
+        "g = np.zeros((1000, 32), np.uint8); am = np.zeros(1000, np.float32)\n"
+        "assert L.ccfd_encode_g32(X.ctypes.data, 1000, 30, flat.ctypes.data, offs.ctypes.data, spec.stamp, g.ctypes.data, am.ctypes.data) == 1000\n"
+        "assert (g == spec.encode(X)).all()\n"
+        "bad = offs.copy(); bad[5] = bad[6] + 1\n"
+        "assert L.ccfd_encode_g32(X.ctypes.data, 1000, 30, flat.ctypes.data, bad.ctypes.data, spec.stamp, g.ctypes.data, None) == -1\n"
         "# native Kafka consumer: Fetch/RecordBatch parsing against kafka-lite\n"
         "import time\n"
         "from ccfd_demo_summit_amd.contracts import TxBatch\n"
@@ -130,11 +140,13 @@ def test_host_runtime_under_asan(tmp_path):
         "kb = KafkaBroker(srv.bootstrap); kb.create_topic('t', 1)\n"
         "kb.produce('t', TxBatch(ids=np.arange(500, dtype=np.uint64), customer=np.zeros(500, np.uint32), features=X[:500]).encode(), partition=0)\n"
         "kb.produce_many('t', msgs[:50], partition=0)\n"
-        "kc = NativeKafkaConsumer.for_arrays(srv.bootstrap, 't', {0: 0}, capacity=1000, wire=True).start()\n"
-        "t0 = time.time()\n"
-        "while kc.stats()['records'] < 51 and time.time() - t0 < 20: time.sleep(0.01)\n"
-        "assert kc.stats()['records'] == 51, kc.stats()\n"
-        "kc.stop(); kc.close(); kb.close(); srv.stop()\n"
+        "for kw in ({'wire': True}, {'bins': spec}):\n"
+        "    kc = NativeKafkaConsumer.for_arrays(srv.bootstrap, 't', {0: 0}, capacity=1000, **kw).start()\n"
+        "    t0 = time.time()\n"
+        "    while kc.stats()['records'] < 51 and time.time() - t0 < 20: time.sleep(0.01)\n"
+        "    assert kc.stats()['records'] == 51, kc.stats()\n"
+        "    kc.stop(); kc.close()\n"
+        "kb.close(); srv.stop()\n"
         "# fuzz the RecordBatch/TXB1/JSON parsers with truncated and bit-flipped record sets\n"
         "from ccfd_demo_summit_amd.ingest.kafka_wire import encode_record_batch\n"
         "good = encode_record_batch([TxBatch(ids=np.arange(64, dtype=np.uint64), customer=np.zeros(64, np.uint32), features=X[:64]).encode()] + msgs[:20], [None] * 21, base_offset=0)\n"
