@@ -133,9 +133,11 @@ def test_g32_engine_pump_exact(gpu, input_mode, exec_mode):
     bad.free()
 
 
-def test_g32_hot_swap_inside_live_bin_table(gpu):
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+def test_g32_hot_swap_inside_live_bin_table(gpu, exec_mode):
     """A retrained ensemble whose thresholds are edges of the live table swaps in without
-    re-encoding the logs (same stamp); leaves come from the new model."""
+    re-encoding the logs (same stamp); leaves come from the new model (the persistent
+    kernel re-stages its leaf tables on the relaunch after the swap)."""
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
@@ -143,7 +145,7 @@ def test_g32_hot_swap_inside_live_bin_table(gpu):
     X, _ = generate(B * 2, seed=45)
     m1 = build_model("gbdt", seed=10, X_ref=X, calibrate_rate=0.01)
     dm1 = DeviceModel(m1, gpu, bins=True)
-    eng = StreamEngine(dm1, batch=B, depth=2, streams=1, input_mode="zerocopy")
+    eng = StreamEngine(dm1, batch=B, depth=2, streams=1, input_mode="zerocopy", exec_mode=exec_mode)
     log = PartitionLog.from_arrays(X, bins=dm1.bins)
     eng.add_log(0, log)
     eng.pump(2)
@@ -157,3 +159,34 @@ def test_g32_hot_swap_inside_live_bin_table(gpu):
         eng.swap_model(DeviceModel(build_model("gbdt", seed=11, X_ref=X), gpu, bins=True))
     eng.close()
     log.free()
+
+
+def test_g32_persistent_engine_with_routing_rules(gpu):
+    """proba-only rule sets on the persistent G32 kernel (its kR instantiation): every row
+    routes like RuleSet.evaluate on the device probabilities; counters agree."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, DeviceRules
+    from ccfd_demo_summit_amd.router.rules import RuleSet
+    B = 8192
+    X, _ = generate(B * 3, seed=46)
+    m = build_model("gbdt", seed=12, X_ref=X[:20000], calibrate_rate=0.05)
+    dm = DeviceModel(m, gpu, bins=True)
+    rs = RuleSet.parse("when proba >= 0.8 then fraud\nwhen proba < 0.001 then fraud\notherwise standard")
+    eng = StreamEngine(dm, batch=B, depth=3, streams=1, input_mode="zerocopy", exec_mode="persistent",
+                       rules=DeviceRules(rs, gpu))
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64), bins=dm.bins)
+    eng.add_log(0, log)
+    st = eng.pump(3)
+    want = rs.evaluate(m.predict_proba(X)).astype(bool)
+    got = np.zeros(len(X), bool)
+    got[eng.drain_flagged()["tx_id"].astype(np.int64)] = True
+    p = m.predict_proba(X)
+    clear = (np.abs(p - 0.8) > 1e-5) & (np.abs(p - 0.001) > 1e-6)     # fp32 summation order only
+    np.testing.assert_array_equal(got[clear], want[clear])
+    assert st.fraud_rows == got.sum() and st.rows == len(X)
+    with pytest.raises(ValueError, match="proba_1"):
+        StreamEngine(dm, batch=B, depth=2, streams=1, exec_mode="persistent",
+                     rules=DeviceRules(RuleSet.parse("when V17 < -3 then fraud\notherwise standard"), gpu))
+    eng.close()
+    log.free()
+
