@@ -231,12 +231,19 @@ def cmd_engine(a, cfg):
     ctx = init_distributed()
     bind_to_gpu(ctx.device.index)
     fmt = resolve_row_format(cfg.engine.model, cfg.engine.wire)
+    rules = RuleSet.from_config(cfg.router)
+    if fmt == "g32" and rules.feature_vars():
+        # G32 rows carry bins, not feature values: rules over transaction columns need the
+        # values, so this deployment scores GBDT on f32 rows (exact, 120 B/row)
+        print(f"[engine] routing rules read {sorted(rules.feature_vars())}: GBDT on f32 rows instead of G32",
+              flush=True)
+        fmt = "f32"
     model = _model(cfg.engine.model, a.weights, cfg.seed) if ctx.rank == 0 else None
     dm = broadcast_model(ctx, model, cfg.engine.model, fmt)      # X1 (+ G32 bin table)
     broker = _broker(cfg)
     hub = MetricsHub()
     kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
-    router = Router(RuleSet.from_config(cfg.router), kie, hub.router)
+    router = Router(rules, kie, hub.router)
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
         depth=cfg.engine.depth, streams=cfg.engine.streams, input_mode=cfg.engine.input_mode,
