@@ -148,7 +148,11 @@ def cmd_kie(a, cfg):
     from ..serving.client import SeldonClient
     broker = _broker(cfg)
     topic = cfg.kafka.notification_topic
-    client = SeldonClient(cfg.kie.seldon_url, cfg.kie.seldon_endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
+    # the KIE pod's own SELDON_URL / SELDON_ENDPOINT name ITS prediction-service target (the
+    # user-task model, ccd-service.yaml:61-62), not the router's fraud model
+    url = os.environ.get("SELDON_URL") or cfg.kie.seldon_url
+    endpoint = os.environ.get("SELDON_ENDPOINT") or cfg.kie.seldon_endpoint
+    client = SeldonClient(url, endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
                           cfg.seldon.pool_size) if a.remote_prediction else None
     eng = ProcessEngine.from_config(
         cfg.kie, publish_notification=lambda m: broker.produce(topic, encode_notification(m),

@@ -44,6 +44,10 @@ class ServiceState:
     replicas: Dict[int, Replica] = field(default_factory=dict)
     restarts: int = 0
     backoff_until: Dict[int, float] = field(default_factory=dict)
+    job: bool = False                       # run-to-completion (Job): restart only on failure
+    succeeded: set = field(default_factory=set)
+
+JOBS = ("producer", "training")             # Kubernetes Jobs in the rendering (restartPolicy OnFailure)
 
 
 def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offset: int = 0) -> Dict[str, tuple]:
@@ -88,7 +92,10 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     if spec.producer.deploy:
         svc["producer"] = (1, lambda r: PY + ["producer", "--fmt", spec.producer.format,
                                               "--count", str(spec.producer.count)])
-    return {k: (n, f, env) for k, (n, f) in svc.items()}
+    own = {k: dict(env) for k in svc}
+    if "kie" in own:               # the KIE pod's prediction service targets the user-task model
+        own["kie"].update(SELDON_URL=f"http://{host}:{5000 + o}", SELDON_ENDPOINT="predict")
+    return {k: (n, f, own[k]) for k, (n, f) in svc.items()}
 
 
 class LocalOperator:
@@ -149,7 +156,7 @@ class LocalOperator:
                 for rep in st.replicas.values():
                     self._stop(rep)
         for name, (desired, _argv, _env) in self._commands.items():
-            st = self.services.setdefault(name, ServiceState())
+            st = self.services.setdefault(name, ServiceState(job=name in JOBS))
             st.desired = desired
             for r in sorted((k for k in st.replicas if k >= desired), reverse=True):   # scale down: highest first
                 self._stop(st.replicas.pop(r))
@@ -157,6 +164,11 @@ class LocalOperator:
             for r in range(desired):
                 rep = st.replicas.get(r)
                 if rep is not None and rep.proc.poll() is None:
+                    continue
+                if r in st.succeeded:
+                    continue
+                if rep is not None and st.job and rep.proc.returncode == 0:   # a Job that completed
+                    st.succeeded.add(r)
                     continue
                 if rep is not None:                                    # exited: restart with back-off
                     if now < st.backoff_until.get(r, 0.0):
@@ -185,6 +197,8 @@ class LocalOperator:
             ready = sum(1 for rep in st.replicas.values() if rep.proc.poll() is None)
             svc[name] = {"desired": st.desired, "ready": ready, "restarts": st.restarts,
                          "pids": sorted(rep.proc.pid for rep in st.replicas.values() if rep.proc.poll() is None)}
+            if st.job:
+                svc[name]["succeeded"] = len(st.succeeded)
         return {"name": self.spec.name, "observedGeneration": self.generation, "services": svc,
                 "notes": list(self.spec.notes)}
 

@@ -142,6 +142,31 @@ def test_local_operator_reconciles_restarts_scales_and_stops(tmp_path):
     assert all(p.poll() is not None for p in procs)
 
 
+def test_local_operator_jobs_run_to_completion():
+    """producer / training are Jobs: a successful exit completes them, a failure restarts."""
+    ok = [sys.executable, "-c", "pass"]
+    bad_then_ok = [sys.executable, "-c", "import os,sys; p='/tmp/ccfd_op_job_marker_%d' % os.getppid(); "
+                   "sys.exit(0) if os.path.exists(p) else (open(p,'w').close(), sys.exit(3))"]
+    op = LocalOperator(FraudDetectionSpec(), commands={"producer": (1, lambda r: ok, {}),
+                                                       "training": (1, lambda r: bad_then_ok, {})},
+                       grace_s=5, backoff_s=0.0, log=lambda m: None)
+    try:
+        for _ in range(40):
+            st = op.reconcile()
+            if st["producer"].get("succeeded") == 1 and st["training"].get("succeeded") == 1:
+                break
+            time.sleep(0.1)
+        assert st["producer"]["succeeded"] == 1 and st["producer"]["restarts"] == 0
+        assert st["training"]["succeeded"] == 1 and st["training"]["restarts"] == 1
+        assert op.reconcile()["producer"]["ready"] == 0          # not restarted after success
+    finally:
+        op.shutdown()
+        try:
+            os.remove(f"/tmp/ccfd_op_job_marker_{os.getpid()}")
+        except OSError:
+            pass
+
+
 def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
     """Only the CR's kafka section deployed: the operator starts kafka-lite with 3 listeners
     and a Kafka client produces to / fetches from it through the bootstrap list."""
