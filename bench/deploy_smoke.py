@@ -72,11 +72,16 @@ def main(argv=None) -> int:
     finally:
         op.shutdown()
     rows = _sum(eng, "ccfd_gpu_rows_total") or _sum(eng, "ccfd_gpu_rows")
-    started = {k: v for k, v in kie.items() if "process" in k and "start" in k}
+    # KIE outcome histograms (README.md:532-537): how many fraud processes ended which way
+    outcomes = {k.split("{")[0][:-len("_count")]: v for k, v in kie.items()
+                if k.split("{")[0].endswith("_count") and k.startswith("fraud_")}
     out = {"seconds": round(time.time() - t0, 1), "model": a.model, "gpus": a.gpus,
            "gpu_rows_scored": rows, "engine_metrics": len(eng), "kie_metrics": len(kie),
-           "kie_started": started,
+           "kie_fraud_outcomes": outcomes,
+           "transaction_incoming": _sum(eng, "transaction_incoming_total"),
+           "transaction_outgoing": {k: v for k, v in eng.items() if k.startswith("transaction_outgoing_total")},
            "notifications": _sum(eng, "notifications_outgoing_total"),
+           "responses": _sum(eng, "notifications_incoming_total"),
            "restarts": {k: v["restarts"] for k, v in status.items()},
            "services": {k: v["ready"] for k, v in status.items()}}
     line = json.dumps(out)
