@@ -83,7 +83,8 @@ def main(argv=None) -> int:
            "notifications": _sum(eng, "notifications_outgoing_total"),
            "responses": _sum(eng, "notifications_incoming_total"),
            "restarts": {k: v["restarts"] for k, v in status.items()},
-           "services": {k: v["ready"] for k, v in status.items()}}
+           "services": {k: v["ready"] for k, v in status.items()},
+           "healthy": {k: v["healthy"] for k, v in status.items() if "healthy" in v}}
     line = json.dumps(out)
     print(line, flush=True)
     if a.out:

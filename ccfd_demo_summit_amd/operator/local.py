@@ -5,8 +5,10 @@ SURVEY.md §2.1 C18/C20, §1 L0), for a single MI355X node without Kubernetes.
 ``reconcile()`` compares the desired replicas of every service (from the CR) with the live
 processes: it starts missing replicas, restarts exited ones (crash-loop back-off like the
 reference's ``restartPolicy: Always`` DeploymentConfigs), stops surplus replicas when the CR
-scales down, and writes a status document (per service: desired / ready / restarts, the
-CR generation it reflects).  ``run()`` re-reads the CR file when it changes, so editing the
+scales down, health-checks every replica on the route its Kubernetes probes use (a replica
+that keeps failing after its start window is killed and restarted, like a liveness probe),
+and writes a status document (per service: desired / ready (running) / healthy / restarts,
+the CR generation it reflects).  ``run()`` re-reads the CR file when it changes, so editing the
 CR is how the local deployment is scaled -- the same declarative loop as on a cluster.
 
 Every replica is its own process group (never exec'd from a GPU-initialised parent); stop
@@ -18,6 +20,7 @@ from __future__ import annotations
 import json
 import os
 import signal
+import socket
 import subprocess
 import sys
 import time
@@ -36,6 +39,8 @@ class Replica:
     started: float
     restarts: int = 0
     last_exit: Optional[int] = None
+    healthy: bool = False
+    probe_fails: int = 0
 
 
 @dataclass
@@ -50,9 +55,24 @@ class ServiceState:
 JOBS = ("producer", "training")             # Kubernetes Jobs in the rendering (restartPolicy OnFailure)
 
 
+def probe_ok(target: tuple, timeout_s: float = 0.5) -> bool:
+    """One health check: ("http", url) -> 2xx, ("tcp", host, port) -> connect succeeds."""
+    try:
+        if target[0] == "tcp":
+            with socket.create_connection((target[1], target[2]), timeout=timeout_s):
+                return True
+        import urllib.request
+        with urllib.request.urlopen(target[1], timeout=timeout_s) as r:
+            return 200 <= r.status < 300
+    except Exception:
+        return False
+
+
 def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offset: int = 0) -> Dict[str, tuple]:
-    """service -> (desired replicas, argv factory(replica index), env) for a one-node run;
-    every port is the service's reference port + ``port_offset`` (+ replica index)."""
+    """service -> (desired replicas, argv factory(replica index), env, probe) for a one-node
+    run; every port is the service's reference port + ``port_offset`` (+ replica index).
+    ``probe`` is (target factory(replica index), start seconds) -- the same health routes the
+    rendered readiness / liveness probes use (render.py) -- or None."""
     o = port_offset
     kafka_port = 9092 + o
     broker = (spec.kafka.bootstrap if not spec.kafka.deploy
@@ -95,13 +115,21 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     own = {k: dict(env) for k in svc}
     if "kie" in own:               # the KIE pod's prediction service targets the user-task model
         own["kie"].update(SELDON_URL=f"http://{host}:{5000 + o}", SELDON_ENDPOINT="predict")
-    return {k: (n, f, own[k]) for k, (n, f) in svc.items()}
+
+    def http(port, path, stride=1):
+        return lambda r: ("http", f"http://{host}:{port + o + stride * r}{path}")
+    probes = {"kafka": (lambda r: ("tcp", host, kafka_port), 20),
+              "usertask": (http(5000, "/health/ping"), 30), "seldon": (http(8000, "/health/ping"), 60),
+              "kie": (http(8090, "/services/rest/server"), 30), "notifier": (http(8080, "/health/ping"), 30),
+              "engine": (http(8091, "/health/ping", 16), 120), "router": (http(8191, "/health/ping"), 30)}
+    return {k: (n, f, own[k], probes.get(k)) for k, (n, f) in svc.items()}
 
 
 class LocalOperator:
     def __init__(self, spec: FraudDetectionSpec, workdir: str = ".", status_path: Optional[str] = None,
                  commands: Optional[Dict[str, tuple]] = None, grace_s: float = 30.0, backoff_s: float = 1.0,
-                 max_backoff_s: float = 30.0, log: Callable[[str], None] = print, port_offset: int = 0):
+                 max_backoff_s: float = 30.0, log: Callable[[str], None] = print, port_offset: int = 0,
+                 liveness_failures: int = 6):
         self.spec = spec
         self.workdir = workdir
         self.status_path = status_path
@@ -112,6 +140,7 @@ class LocalOperator:
         self.generation = 1
         self._commands_override = commands
         self.port_offset = port_offset
+        self.liveness_failures = liveness_failures
         self.services: Dict[str, ServiceState] = {}
         self._commands = commands if commands is not None else local_commands(spec, port_offset=port_offset)
 
@@ -124,7 +153,7 @@ class LocalOperator:
             self._commands = local_commands(spec, port_offset=self.port_offset)
 
     def _start(self, name: str, r: int) -> Replica:
-        _, argv_of, env = self._commands[name]
+        _, argv_of, env = self._commands[name][:3]
         e = dict(os.environ)
         e.update(env)
         root = str(Path(__file__).resolve().parents[2])             # the package, from any cwd
@@ -155,7 +184,8 @@ class LocalOperator:
                 st = self.services.pop(name)
                 for rep in st.replicas.values():
                     self._stop(rep)
-        for name, (desired, _argv, _env) in self._commands.items():
+        for name, cmd in self._commands.items():
+            desired, probe = cmd[0], (cmd[3] if len(cmd) > 3 else None)
             st = self.services.setdefault(name, ServiceState(job=name in JOBS))
             st.desired = desired
             for r in sorted((k for k in st.replicas if k >= desired), reverse=True):   # scale down: highest first
@@ -164,7 +194,17 @@ class LocalOperator:
             for r in range(desired):
                 rep = st.replicas.get(r)
                 if rep is not None and rep.proc.poll() is None:
-                    continue
+                    if probe is None:
+                        continue
+                    # readiness / liveness: failures before the start window are not counted;
+                    # ``liveness_failures`` in a row after it kill the (hung) replica -> restart
+                    target_of, start_s = probe
+                    rep.healthy = probe_ok(target_of(r))
+                    rep.probe_fails = 0 if rep.healthy else rep.probe_fails + (now - rep.started >= start_s)
+                    if rep.probe_fails < self.liveness_failures:
+                        continue
+                    self.log(f"[operator] {name}[{r}] failed {rep.probe_fails} liveness probes: killing it")
+                    self._stop(rep)
                 if r in st.succeeded:
                     continue
                 if rep is not None and st.job and rep.proc.returncode == 0:   # a Job that completed
@@ -197,6 +237,10 @@ class LocalOperator:
             ready = sum(1 for rep in st.replicas.values() if rep.proc.poll() is None)
             svc[name] = {"desired": st.desired, "ready": ready, "restarts": st.restarts,
                          "pids": sorted(rep.proc.pid for rep in st.replicas.values() if rep.proc.poll() is None)}
+            cmd = self._commands.get(name)
+            if cmd is not None and len(cmd) > 3 and cmd[3] is not None:
+                svc[name]["healthy"] = sum(1 for rep in st.replicas.values()
+                                           if rep.healthy and rep.proc.poll() is None)
             if st.job:
                 svc[name]["succeeded"] = len(st.succeeded)
         return {"name": self.spec.name, "observedGeneration": self.generation, "services": svc,

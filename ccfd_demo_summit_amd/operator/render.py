@@ -22,8 +22,15 @@ LAUNCH = ["python", "-m", "ccfd_demo_summit_amd.launch"]
 GRAFANA_DIR = Path(__file__).resolve().parents[2] / "deploy" / "grafana"
 
 
+def _probes(path: str, port: int, start_s: int = 30) -> Dict[str, Any]:
+    """readiness + liveness on a service's health route (tcp when ``path`` is None)."""
+    act = {"httpGet": {"path": path, "port": port}} if path else {"tcpSocket": {"port": port}}
+    return {"readinessProbe": dict(act, periodSeconds=5, failureThreshold=3),
+            "livenessProbe": dict(act, initialDelaySeconds=start_s, periodSeconds=10, failureThreshold=6)}
+
+
 def _container(spec: FraudDetectionSpec, name: str, command: List[str], ports=(), gpus: int = 0,
-               env=None, envfrom: bool = True) -> Dict[str, Any]:
+               env=None, envfrom: bool = True, probe=None) -> Dict[str, Any]:
     c: Dict[str, Any] = {"name": name, "image": spec.image, "workingDir": "/app", "command": command}
     if envfrom:
         c["envFrom"] = [{"configMapRef": {"name": "ccfd-env"}}]
@@ -33,6 +40,8 @@ def _container(spec: FraudDetectionSpec, name: str, command: List[str], ports=()
         c["ports"] = [dict(p) for p in ports]
     if gpus:
         c["resources"] = {"limits": {"amd.com/gpu": gpus}}
+    if probe:
+        c.update(_probes(*probe))
     return c
 
 
@@ -87,7 +96,8 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
         out.append(_workload("StatefulSet", name, name, 1, [_container(
             spec, "kafka", LAUNCH + ["kafka-lite", "--nodes", str(spec.kafka.brokers), "--port", "9092",
                                      "--advertise", f"{name}-brokers"],
-            ports=ports, env={"CCFD_KAFKA_PARTITIONS": spec.kafka.partitions}, envfrom=False)],
+            ports=ports, env={"CCFD_KAFKA_PARTITIONS": spec.kafka.partitions}, envfrom=False,
+            probe=(None, 9092, 20))],
             annotations=_scrape("/metrics", 9404)))
         for svc in (f"{name}-brokers", f"{name}-bootstrap"):
             out.append(_service(svc, name, [{"name": f"broker-{i}", "port": 9092 + i, "targetPort": 9092 + i}
@@ -98,7 +108,8 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
         cmd = LAUNCH + ["supervise", "--", "python", "-m", "torch.distributed.run", "--standalone",
                         "--nproc-per-node", str(g)] + LAUNCH[1:] + ["engine"] + weights
         out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", spec.engine.nodes, [_container(
-            spec, "engine", cmd, ports=[{"containerPort": 8091, "name": "metrics"}], gpus=g)],
+            spec, "engine", cmd, ports=[{"containerPort": 8091, "name": "metrics"}], gpus=g,
+            probe=("/health/ping", 8091, 120))],
             annotations=_scrape("/prometheus", 8091)))
 
     if spec.seldon.deploy:
@@ -106,14 +117,16 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
         if spec.seldon.native:
             cmd += ["--native", "--workers", str(spec.seldon.workers)]
         out.append(_workload("Deployment", "modelfull-modelfull", "modelfull", spec.seldon.replicas, [_container(
-            spec, "modelfull", cmd, ports=[{"containerPort": 8000, "name": "http"}], gpus=spec.seldon.gpus)],
+            spec, "modelfull", cmd, ports=[{"containerPort": 8000, "name": "http"}], gpus=spec.seldon.gpus,
+            probe=("/health/ping", 8000, 60))],
             annotations=_scrape("/prometheus", 8000), grace=20))
         out.append(_service("modelfull-modelfull", "modelfull", [{"name": "http", "port": 8000, "targetPort": 8000}]))
 
     if spec.usertask.deploy:
         out.append(_workload("Deployment", "ccfd-seldon-model", "ccfd-seldon-model", spec.usertask.replicas,
                              [_container(spec, "usertask", LAUNCH + ["usertask", "--port", "5000"],
-                                         ports=[{"containerPort": 5000, "name": "http"}], envfrom=False)]))
+                                         ports=[{"containerPort": 5000, "name": "http"}], envfrom=False,
+                                         probe=("/health/ping", 5000, 30))]))
         out.append(_service("ccfd-seldon-model", "ccfd-seldon-model", [{"name": "http", "port": 5000, "targetPort": 5000}]))
 
     if spec.kie.deploy:
@@ -121,7 +134,8 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
             "Deployment", "ccd-service", "ccd-service", spec.kie.replicas,
             [dict(_container(spec, "kie", LAUNCH + ["kie", "--journal", "/data/bp-journal.jsonl", "--remote-prediction"],
                              ports=[{"containerPort": 8090, "name": "http"}],
-                             env={"SELDON_URL": "ccfd-seldon-model:5000", "SELDON_ENDPOINT": "predict"}),
+                             env={"SELDON_URL": "ccfd-seldon-model:5000", "SELDON_ENDPOINT": "predict"},
+                             probe=("/services/rest/server", 8090, 30)),
                   volumeMounts=[{"name": "journal", "mountPath": "/data"}])],
             annotations=_scrape("/rest/metrics", 8090),
             extra_spec={"strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxSurge": "25%", "maxUnavailable": "25%"}}},
@@ -131,12 +145,14 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
     if spec.notifier.deploy:
         out.append(_workload("Deployment", "ccfd-notification-service", "ccfd-notification-service",
                              spec.notifier.replicas, [_container(spec, "notifier", LAUNCH + ["notifier"],
-                                                                 ports=[{"containerPort": 8080, "name": "health"}])]))
+                                                                 ports=[{"containerPort": 8080, "name": "health"}],
+                                                                 probe=("/health/ping", 8080, 30))]))
 
     if spec.router.deploy:
         out.append(_workload("Deployment", "ccd-fuse", "ccd-fuse", spec.router.replicas, [_container(
             spec, "router", LAUNCH + ["supervise", "--"] + LAUNCH + ["router", "--group-membership"],
-            ports=[{"containerPort": 8091, "name": "metrics"}])], annotations=_scrape("/prometheus", 8091),
+            ports=[{"containerPort": 8091, "name": "metrics"}], probe=("/health/ping", 8091, 30))],
+            annotations=_scrape("/prometheus", 8091),
             extra_spec={"strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxUnavailable": "25%", "maxSurge": "25%"}}}))
         out.append(_service("ccd-fuse", "ccd-fuse", [{"name": "metrics", "port": 8091, "targetPort": 8091}]))
 
@@ -231,6 +247,12 @@ def validate(manifests: List[Dict[str, Any]]) -> List[str]:
                 for e in c.get("env", []):
                     if e["name"] not in allowed_env:
                         probs.append(f"{key}: unknown env key {e['name']}")
+                for pk in ("readinessProbe", "livenessProbe"):
+                    pr = c.get(pk)
+                    if pr:
+                        port = (pr.get("httpGet") or pr.get("tcpSocket") or {}).get("port")
+                        if port not in {p["containerPort"] for p in c.get("ports", [])}:
+                            probs.append(f"{key}/{c['name']}: {pk} on undeclared port {port}")
                 gpu = c.get("resources", {}).get("limits", {}).get("amd.com/gpu", 0)
                 if gpu and c["name"] not in ("engine", "modelfull", "train"):
                     probs.append(f"{key}: GPU requested by {c['name']}")

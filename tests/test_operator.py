@@ -93,6 +93,26 @@ def test_reference_opendatahub_cr_maps_onto_the_stack():
     assert validate(render(spec)) == []
 
 
+def test_every_long_running_container_has_health_probes():
+    """Deployments / StatefulSets carry readiness + liveness probes on the service's own health
+    route (engine /health/ping :8091, KIE /services/rest/server :8090, kafka tcp :9092, ...)."""
+    ms = render(load(str(CR)))
+    seen = {}
+    for m in ms:
+        if m["kind"] not in ("Deployment", "StatefulSet"):
+            continue
+        for c in m["spec"]["template"]["spec"]["containers"]:
+            assert "readinessProbe" in c and "livenessProbe" in c, (m["metadata"]["name"], c["name"])
+            seen[c["name"]] = c["livenessProbe"]
+    assert seen["engine"]["httpGet"] == {"path": "/health/ping", "port": 8091}
+    assert seen["kie"]["httpGet"]["path"] == "/services/rest/server"
+    assert seen["kafka"]["tcpSocket"] == {"port": 9092}
+    bad = copy.deepcopy(ms)
+    eng = next(m for m in bad if m["metadata"]["name"] == "ccfd-engine")
+    eng["spec"]["template"]["spec"]["containers"][0]["livenessProbe"]["httpGet"]["port"] = 9999
+    assert any("livenessProbe on undeclared port 9999" in p for p in validate(bad))
+
+
 def test_validate_reports_broken_manifests():
     ms = render(load(str(CR)))
     bad = copy.deepcopy(ms)
@@ -165,6 +185,39 @@ def test_local_operator_jobs_run_to_completion():
             os.remove(f"/tmp/ccfd_op_job_marker_{os.getpid()}")
         except OSError:
             pass
+
+
+def test_local_operator_liveness_probe_restarts_a_hung_replica():
+    """A replica that is running but never answers its health route is killed after
+    ``liveness_failures`` probes and restarted; one that answers is reported healthy."""
+    port = random.randint(41000, 49000)
+    http = [sys.executable, "-c", "import http.server as h; h.HTTPServer(('127.0.0.1', %d), "
+            "h.SimpleHTTPRequestHandler).serve_forever()" % port]
+    cmds = {"hung": (1, lambda r: SLEEPER, {}, (lambda r: ("tcp", "127.0.0.1", port + 1), 0)),
+            "web": (1, lambda r: http, {}, (lambda r: ("http", f"http://127.0.0.1:{port}/"), 0))}
+    op = LocalOperator(FraudDetectionSpec(), workdir="/tmp", commands=cmds, grace_s=5, backoff_s=0.0,
+                       log=lambda m: None, liveness_failures=3)
+    try:
+        first = None
+        for _ in range(60):
+            st = op.reconcile()
+            first = first or op.services["hung"].replicas[0].proc.pid
+            if st["hung"]["restarts"] >= 1 and st["web"]["healthy"] == 1:
+                break
+            time.sleep(0.1)
+        assert st["hung"]["restarts"] >= 1 and st["hung"]["healthy"] == 0
+        assert op.services["hung"].replicas[0].proc.pid != first
+        assert st["web"]["healthy"] == 1 and st["web"]["restarts"] == 0
+    finally:
+        op.shutdown()
+
+
+def test_local_commands_probe_the_rendered_health_routes():
+    from ccfd_demo_summit_amd.operator import local_commands
+    cmds = local_commands(load(str(CR)), port_offset=100)
+    assert cmds["engine"][3][0](1) == ("http", "http://127.0.0.1:8207/health/ping")
+    assert cmds["kie"][3][0](0) == ("http", "http://127.0.0.1:8190/services/rest/server")
+    assert cmds["kafka"][3][0](0)[0] == "tcp" and cmds["producer"][3] is None
 
 
 def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
