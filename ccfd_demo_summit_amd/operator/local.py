@@ -7,7 +7,8 @@ processes: it starts missing replicas, restarts exited ones (crash-loop back-off
 reference's ``restartPolicy: Always`` DeploymentConfigs), stops surplus replicas when the CR
 scales down, health-checks every replica on the route its Kubernetes probes use (a replica
 that keeps failing after its start window is killed and restarted, like a liveness probe),
-and writes a status document (per service: desired / ready (running) / healthy / restarts,
+replaces replicas whose command or environment changed with the CR a few at a time
+(rolling update), and writes a status document (per service: desired / ready (running) / healthy / restarts,
 the CR generation it reflects).  ``run()`` re-reads the CR file when it changes, so editing the
 CR is how the local deployment is scaled -- the same declarative loop as on a cluster.
 
@@ -41,6 +42,7 @@ class Replica:
     last_exit: Optional[int] = None
     healthy: bool = False
     probe_fails: int = 0
+    template: str = ""                      # argv + env it was started with (rolling updates)
 
 
 @dataclass
@@ -51,6 +53,7 @@ class ServiceState:
     backoff_until: Dict[int, float] = field(default_factory=dict)
     job: bool = False                       # run-to-completion (Job): restart only on failure
     succeeded: set = field(default_factory=set)
+    rollouts: int = 0                       # replicas replaced because their template changed
 
 JOBS = ("producer", "training")             # Kubernetes Jobs in the rendering (restartPolicy OnFailure)
 
@@ -152,15 +155,19 @@ class LocalOperator:
         if self._commands_override is None:
             self._commands = local_commands(spec, port_offset=self.port_offset)
 
+    def _template(self, name: str, r: int) -> str:
+        _, argv_of, env = self._commands[name][:3]
+        return json.dumps([list(argv_of(r)), sorted((str(k), str(v)) for k, v in env.items())])
+
     def _start(self, name: str, r: int) -> Replica:
         _, argv_of, env = self._commands[name][:3]
         e = dict(os.environ)
-        e.update(env)
+        e.update({str(k): str(v) for k, v in env.items()})
         root = str(Path(__file__).resolve().parents[2])             # the package, from any cwd
         e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
         p = subprocess.Popen(argv_of(r), cwd=self.workdir, env=e, start_new_session=True,
                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-        return Replica(p, time.time())
+        return Replica(p, time.time(), template=self._template(name, r))
 
     def _stop(self, rep: Replica) -> None:
         if rep.proc.poll() is None:
@@ -223,6 +230,8 @@ class LocalOperator:
                     self.log(f"[operator] {name}[{r}] exited rc={rc}: restarted (#{nxt.restarts})")
                 else:
                     st.replicas[r] = self._start(name, r)
+            if not st.job:
+                self._roll(name, st, desired, probe)
         status = self.status()
         if self.status_path:
             tmp = self.status_path + ".tmp"
@@ -231,12 +240,31 @@ class LocalOperator:
             os.replace(tmp, self.status_path)
         return status["services"]
 
+    def _roll(self, name: str, st: ServiceState, desired: int, probe) -> None:
+        """Rolling update (the reference DeploymentConfigs' Rolling strategy, maxUnavailable
+        25 %): replicas whose argv / env changed with the CR are replaced -- stop, then start on
+        the same port -- at most max(1, desired // 4) unavailable at a time; with a probe a new
+        replica counts as unavailable until its health route answers."""
+        outdated = [r for r in sorted(st.replicas) if st.replicas[r].proc.poll() is None
+                    and st.replicas[r].template != self._template(name, r)]
+        if not outdated:
+            return
+        unavailable = sum(1 for rep in st.replicas.values()
+                          if rep.proc.poll() is not None or (probe is not None and not rep.healthy))
+        for r in outdated[:max(0, max(1, desired // 4) - unavailable)]:
+            self._stop(st.replicas[r])
+            st.replicas[r] = self._start(name, r)
+            st.rollouts += 1
+            self.log(f"[operator] {name}[{r}] rolled to generation {self.generation}")
+
     def status(self) -> Dict:
         svc = {}
         for name, st in self.services.items():
             ready = sum(1 for rep in st.replicas.values() if rep.proc.poll() is None)
             svc[name] = {"desired": st.desired, "ready": ready, "restarts": st.restarts,
                          "pids": sorted(rep.proc.pid for rep in st.replicas.values() if rep.proc.poll() is None)}
+            if st.rollouts:
+                svc[name]["rollouts"] = st.rollouts
             cmd = self._commands.get(name)
             if cmd is not None and len(cmd) > 3 and cmd[3] is not None:
                 svc[name]["healthy"] = sum(1 for rep in st.replicas.values()

@@ -187,6 +187,31 @@ def test_local_operator_jobs_run_to_completion():
             pass
 
 
+def test_local_operator_rolls_a_changed_template_a_quarter_at_a_time():
+    """A CR generation that changes a service's command replaces its replicas with at most
+    max(1, n // 4) unavailable at a time, without counting them as crash restarts."""
+    version = {"v": "1"}
+    cmd = lambda r: [sys.executable, "-c", "import time; time.sleep(120)", version["v"]]
+    op = LocalOperator(FraudDetectionSpec(), commands={"kie": (8, cmd, {})}, grace_s=5, backoff_s=0.0,
+                       log=lambda m: None)
+    try:
+        op.reconcile()
+        old = set(op.status()["services"]["kie"]["pids"])
+        version["v"] = "2"
+        op.generation += 1
+        rolled = []
+        for _ in range(10):
+            st = op.reconcile()["kie"]
+            rolled.append(st.get("rollouts", 0))
+            if rolled[-1] == 8:
+                break
+        assert rolled[:4] == [2, 4, 6, 8]                       # 8 // 4 = 2 replaced per pass
+        assert st["ready"] == 8 and st["restarts"] == 0 and not (set(st["pids"]) & old)
+        assert op.reconcile()["kie"]["rollouts"] == 8           # converged: nothing more to roll
+    finally:
+        op.shutdown()
+
+
 def test_local_operator_liveness_probe_restarts_a_hung_replica():
     """A replica that is running but never answers its health route is killed after
     ``liveness_failures`` probes and restarted; one that answers is reported healthy."""
