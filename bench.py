@@ -49,7 +49,9 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=None,
                     help="micro-batches in flight per GPU (default 16 for mlp/lr = p50 <= 80 us at the "
                          "PCIe-bound rate, profiles/r2/operating_curve.txt; 6 for gbdt = 1.66e9 tx/s at "
-                         "p50 225 us with 65536-row batches, profiles/r2/gbdt_g32_persist_sweep.jsonl)")
+                         "p50 225 us with 65536-row batches, profiles/r2/gbdt_g32_persist_sweep.jsonl; "
+                         "--batch 16384 --depth 8 trades 3%% of that for p50 74 us, "
+                         "profiles/r2/gbdt_g32_operating_curve.jsonl)")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
     ap.add_argument("--output-mode", default="zerocopy", choices=["zerocopy", "dma"])
