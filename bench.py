@@ -47,8 +47,8 @@ def parse_args(argv=None):
                     help="micro-batch rows (default: the BASELINE config's -- 4096 for mlp/lr, 65536 for gbdt)")
     ap.add_argument("--batches-per-step", type=int, default=256)
     ap.add_argument("--depth", type=int, default=None,
-                    help="micro-batches in flight per GPU (default 16 for mlp/lr = p50 <= 80 us at the "
-                         "PCIe-bound rate, profiles/r2/operating_curve.txt; 6 for gbdt = 1.66e9 tx/s at "
+                    help="micro-batches in flight per GPU (default 12 for mlp/lr = p50 53 us at the "
+                         "PCIe-bound rate, profiles/r2/persist_full_item/; 6 for gbdt = 1.66e9 tx/s at "
                          "p50 225 us with 65536-row batches, profiles/r2/gbdt_g32_persist_sweep.jsonl; "
                          "--batch 16384 --depth 8 trades 3%% of that for p50 74 us, "
                          "profiles/r2/gbdt_g32_operating_curve.jsonl)")
@@ -58,7 +58,7 @@ def parse_args(argv=None):
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
                     help="auto = persistent kernel for mlp/lr and for gbdt on G32 rows with zero-copy "
                          "in/out, launches otherwise (profiles/r1/persist_sweep.txt, profiles/r2/)")
-    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default 128)")
+    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 128 otherwise)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64", "g32"],
@@ -249,7 +249,7 @@ def main(argv=None):
     if args.batch is None:
         args.batch = 65536 if args.model == "gbdt" else 4096
     if args.depth is None:
-        args.depth = 6 if args.model == "gbdt" else 16
+        args.depth = 6 if args.model == "gbdt" else 12
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine

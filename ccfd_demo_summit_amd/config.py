@@ -78,7 +78,7 @@ class NotifierConfig:
 class EngineConfig:
     model: str = "mlp"               # lr | mlp | gbdt
     batch: int = 4096                # micro-batch rows (BASELINE config 2)
-    depth: int = 16                  # micro-batches in flight per GPU
+    depth: int = 12                  # micro-batches in flight per GPU (p50 53 us at the PCIe rate)
     streams: int = 4                 # HIP streams per engine
     input_mode: str = "zerocopy"     # dma (H2D into HBM) | zerocopy (kernel reads pinned host)
     wire: str = "auto"               # ring row format: f32 | w64 | g32 | auto (w64 for mlp/lr, g32 for gbdt)

@@ -339,7 +339,12 @@ class Engine {
     // work-item size: 64 rows (one 16-row tile per wave) by default; CCFD_PERSIST_ITEM_ROWS
     // = 128/256 gives each wave 2/4 tiles with a one-tile prefetch (fewer claims per batch)
     // GBDT on G32 rows: items of 4 waves x 64-row chunks (256 / 512 / 1024 rows, default 512)
-    int item_rows = g32 ? 512 : CCFD_PERSIST_ITEM_ROWS;
+    // W64 rows on 64 workgroups, every tile of an item in flight at once (score_persist.hip):
+    // MLP 512-row items -- 8.63e8 tx/s at p50 53 us and depth 12 vs 8.56e8 at 72 us for
+    // 256-row items on 128 workgroups at depth 16; LR 256-row items (8.47e8 at 56 us; 512:
+    // 7.3e8) -- profiles/r2/persist_full_item/
+    const bool w64 = (wire_flag & CCFD_ARG_WIRE_W64) != 0;
+    int item_rows = (g32 || (w64 && cfg.model == CCFD_MODEL_MLP)) ? 512 : CCFD_PERSIST_ITEM_ROWS;
     if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) {
       const int v = std::atoi(e);
       if (v == 256 || v == 512 || v == 1024 || (!g32 && (v == 64 || v == 128))) item_rows = v;
@@ -405,9 +410,11 @@ class Engine {
     a.counters[1] = cfg.counters[1];
     a.gbdt_trees = cfg.gbdt_trees;
     a.gbdt_depth = cfg.gbdt_depth;
-    // 128 (+ doorbell) resident workgroups for every model: GBDT G32 measured 1.68e9 tx/s at
-    // 128 vs 1.62e9 at 256 and 1.34e9 at 768 (profiles/r2/gbdt_g32_persist_sweep.jsonl)
-    const int grid = cfg.persist_grid > 0 ? cfg.persist_grid : CCFD_PERSIST_GRID;
+    // resident workgroups (+ the doorbell): 128 for GBDT G32 (1.68e9 tx/s vs 1.62e9 at 256 and
+    // 1.34e9 at 768, profiles/r2/gbdt_g32_persist_sweep.jsonl) and f32 rows; 64 for W64 rows
+    // (their 512-row items keep 32 KB per workgroup in flight)
+    const int grid = cfg.persist_grid > 0 ? cfg.persist_grid
+                     : (wire_flag & CCFD_ARG_WIRE_W64) ? CCFD_PERSIST_GRID_W64 : CCFD_PERSIST_GRID;
     int rc = ccfd_persist_launch(&a, grid, pstream);
     if (rc) { set_error("persistent kernel launch failed"); return rc; }
     prunning = true;

@@ -136,8 +136,9 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream);
 // the descriptor to be posted, score, and the last workgroup of a micro-batch publishes
 // its completion record.  No per-batch launch, event or copy on the host.
 #define CCFD_PERSIST_MAX_RING 64
-#define CCFD_PERSIST_ITEM_ROWS 256   // default item: 4 waves x 4 tiles x 16 rows (profiles/r2/operating_curve.txt)
+#define CCFD_PERSIST_ITEM_ROWS 256   // default item of f32 rows: 4 waves x 4 tiles x 16 rows (W64: 512, G32: 512)
 #define CCFD_PERSIST_GRID 128        // default resident workgroups (+ the doorbell workgroup 0)
+#define CCFD_PERSIST_GRID_W64 64     // ... for W64 rows (512-row items, every tile in flight)
 
 typedef struct ccfd_persist_desc {   // host-coherent pinned, written before `posted`
   const float* x;          // device-visible rows [n][30]

@@ -21,6 +21,8 @@
 // while it waits for an unposted batch.  The host never posts batch b into ring slot
 // b % R before observing done for b - R, which is what makes the slot-local state
 // (remaining/nflag reset by the last ticket) safe to reuse.
+#include <type_traits>
+
 #include "mlp_core.h"
 #include "persist_core.h"
 #include "rules.h"
@@ -91,65 +93,27 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     if (chunk == 0 && tid == 0)                                // K7: micro-batch start (item 0 claimed first)
       __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     auto avail = [&](int t) { return min(kTileRows, n - t * kTileRows) * kF * 4; };
-    TileRegs pre;
-    WireRegs wpre;
     const bool wire = (a.flags & CCFD_ARG_WIRE_W64) != 0;       // uniform per launch
     const unsigned char* xw = reinterpret_cast<const unsigned char*>(x);
-    if (tile0 * kTileRows < n) {
-      if (wire) wire_issue(xw, n, tile0, c, g, wpre);
-      else tile_issue(x + (size_t)tile0 * kTileRows * kF, avail(tile0), lane, pre);
-    }
     unsigned nf_w = 0, nv_w = 0;
     unsigned long long ps_w = 0;
-#pragma unroll 1
-    for (int k = 0; k < kTilesPerWave; ++k) {
-      const int tile = tile0 + 4 * k;
-      const int row0 = tile * kTileRows;
-      if (row0 >= n) break;                                // wave-uniform
-      const int row = row0 + c;
-      const bool valid = row < n;
-      const int nxt = tile + 4;
-      float xv[8];
-      WireRegs cur_w;
-      if (wire) {
-        cur_w = wpre;
-        if (k + 1 < kTilesPerWave && nxt * kTileRows < n) wire_issue(xw, n, nxt, c, g, wpre);
-        if (kModel != CCFD_MODEL_MLP) wire_features(cur_w, g, xv);
-      } else {
-        tile_store(tile_lds, lane, pre);
-        if (k + 1 < kTilesPerWave && nxt * kTileRows < n) tile_issue(x + (size_t)nxt * kTileRows * kF, avail(nxt), lane, pre);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        tile_features(tile_lds, c, g, xv);
-      }
-      float p, amount;
-      if (kModel == CCFD_MODEL_MLP) {
-        if (wire) {        // W64 blob: raw bf16 operands, folded normalisation (mlp_core.h)
-          amount = __uint_as_float(cur_w.v.w);
-          p = mlp_tile_w64(sblob, LW, cur_w, g, lane);
-        } else {
-          p = mlp_tile(sblob, L, xv, g, lane, amount);
-        }
-      } else {
-        amount = xv[5];
-        if (g == 3) { xv[6] = 0.f; xv[7] = 0.f; if (L.log_amount) xv[5] = log1pf(fmaxf(xv[5], 0.f)); }
-        float z = 0.f;
+    // LR on one lane group's 8 features (the g == 3 group also carries Time / Amount)
+    auto lr_p = [&](float (&xv)[8]) __attribute__((always_inline)) {
+      if (g == 3) { xv[6] = 0.f; xv[7] = 0.f; if (L.log_amount) xv[5] = log1pf(fmaxf(xv[5], 0.f)); }
+      float z = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) z = fmaf((xv[j] - L.mu[j]) * L.isg[j], wm[j], z);
-        z += __shfl_xor(z, 16);
-        z += __shfl_xor(z, 32);
-        p = sigmoid(z + L.b3);
-      }
+      for (int j = 0; j < 8; ++j) z = fmaf((xv[j] - L.mu[j]) * L.isg[j], wm[j], z);
+      z += __shfl_xor(z, 16);
+      z += __shfl_xor(z, 32);
+      return sigmoid(z + L.b3);
+    };
+    // per-tile epilogue: outputs, route, counters, amount histogram, compacted fraud list;
+    // xr = the tile's raw features (routing rules only)
+    auto finish = [&](float p, float amount, int tile, float (&xr)[8]) __attribute__((always_inline)) {
+      const int row = tile * kTileRows + c;
+      const bool valid = row < n;
       bool fr;
       if constexpr (kR) {                               // configurable routing rules (rules.h)
-        float xr[8];
-        if (wire) {
-          wire_features(cur_w, g, xr);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) xr[j] = xv[j];
-          if (g == 3) xr[5] = amount;                   // the model replaced Amount by its log1p
-        }
         const float pr = __shfl(p, c);
         fr = valid && (wire ? rule_route(a.rules, pr, [&](int j) { return lane_feature<true>(xr, j, c); })
                             : rule_route(a.rules, pr, [&](int j) { return lane_feature<false>(xr, j, c); }));
@@ -166,6 +130,86 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       nv_w += __popcll(__ballot(valid && g == 0));
       if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
       persist_emit_flagged(a, sdesc, slot, m, fr && g == 0, row, lane);
+    };
+    // W64 items of 4 or 8 tiles per wave (256 / 512 rows; 256 is the default): every tile of
+    // the item in flight at once -- the item costs one PCIe round trip instead of one per
+    // tile, so fewer rows in flight keep the link busy (lower p50 at the same rate) -- and
+    // scored in pairs (mlp_tile_w64_x2: one LDS weight read feeds two MFMAs)
+    auto full_item = [&](auto kT) __attribute__((always_inline)) {
+      constexpr int T = decltype(kT)::value;
+      WireRegs r[T];
+#pragma unroll
+      for (int k = 0; k < T; ++k) wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
+#pragma unroll
+      for (int k = 0; k < T; k += 2) {
+        const int ta = tile0 + 4 * k;
+        if (ta * kTileRows >= n) break;                    // wave-uniform
+        float pa, pb;
+        float xa[8], xb[8];
+        if (kModel == CCFD_MODEL_MLP) {
+          mlp_tile_w64_x2(sblob, LW, r[k], r[k + 1], g, lane, pa, pb);
+          if constexpr (kR) { wire_features(r[k], g, xa); wire_features(r[k + 1], g, xb); }
+        } else {
+          wire_features(r[k], g, xa);
+          wire_features(r[k + 1], g, xb);
+          float la[8], lb[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { la[j] = xa[j]; lb[j] = xb[j]; }
+          pa = lr_p(la);
+          pb = lr_p(lb);
+        }
+        finish(pa, __uint_as_float(r[k].v.w), ta, xa);
+        finish(pb, __uint_as_float(r[k + 1].v.w), ta + 4, xb);   // rows >= n: no-op epilogue
+      }
+    };
+    if (wire && kTilesPerWave == 4) {
+      full_item(std::integral_constant<int, 4>{});
+    } else if (wire && kTilesPerWave == 8) {
+      full_item(std::integral_constant<int, 8>{});
+    } else {
+      TileRegs pre;
+      WireRegs wpre;
+      if (tile0 * kTileRows < n) {
+        if (wire) wire_issue(xw, n, tile0, c, g, wpre);
+        else tile_issue(x + (size_t)tile0 * kTileRows * kF, avail(tile0), lane, pre);
+      }
+#pragma unroll 1
+      for (int k = 0; k < kTilesPerWave; ++k) {
+        const int tile = tile0 + 4 * k;
+        const int row0 = tile * kTileRows;
+        if (row0 >= n) break;                                // wave-uniform
+        const int nxt = tile + 4;
+        float xv[8];
+        WireRegs cur_w;
+        if (wire) {
+          cur_w = wpre;
+          if (k + 1 < kTilesPerWave && nxt * kTileRows < n) wire_issue(xw, n, nxt, c, g, wpre);
+          if (kModel != CCFD_MODEL_MLP || kR) wire_features(cur_w, g, xv);
+        } else {
+          tile_store(tile_lds, lane, pre);
+          if (k + 1 < kTilesPerWave && nxt * kTileRows < n) tile_issue(x + (size_t)nxt * kTileRows * kF, avail(nxt), lane, pre);
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          tile_features(tile_lds, c, g, xv);
+        }
+        float xr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xr[j] = xv[j];
+        float p, amount;
+        if (kModel == CCFD_MODEL_MLP) {
+          if (wire) {        // W64 blob: raw bf16 operands, folded normalisation (mlp_core.h)
+            amount = __uint_as_float(cur_w.v.w);
+            p = mlp_tile_w64(sblob, LW, cur_w, g, lane);
+          } else {
+            p = mlp_tile(sblob, L, xv, g, lane, amount);
+            if (g == 3) xr[5] = amount;                    // the model replaced Amount by its log1p
+          }
+        } else {
+          amount = xv[5];
+          p = lr_p(xv);
+        }
+        finish(p, amount, tile, xr);
+      }
     }
     ps_w = wave_sum_u64(ps_w);
     if (lane == 0 && nv_w) {

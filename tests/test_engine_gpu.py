@@ -234,3 +234,41 @@ def test_engine_score_sync_every_exec_mode(gpu, setup, exec_mode, wire):
     ref = m.wire_proba(X[:10_000]) if wire else m.predict_proba(X[:10_000], emulate_bf16=True)
     assert np.abs(p - ref).max() < 2e-3
     np.testing.assert_array_equal(r, (p >= 0.5).astype(np.uint8))
+
+
+@pytest.mark.parametrize("kind", ["mlp", "lr"])
+@pytest.mark.parametrize("item_rows", [64, 128, 256, 512, 1024])
+def test_persistent_wire_item_sizes_exact(gpu, setup, monkeypatch, kind, item_rows):
+    """Every persistent work-item size on W64 rows -- 256 / 512 take the all-tiles-in-flight
+    paired path, the others the one-tile prefetch loop -- scores every row once, full and
+    partial micro-batches alike: rows, routes and the proba sum match the wire oracle."""
+    from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    X, m = setup
+    if kind == "lr":
+        m = build_model("lr", seed=5, X_ref=X[:20000], calibrate_rate=0.01)
+    monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
+    eng = StreamEngine(DeviceModel(m, gpu, wire=True), batch=4096, depth=4, streams=1, exec_mode="persistent")
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000, wire=True)
+    eng.add_log(0, log)
+    a = eng.pump(3)
+    b = eng.pump(2, batch_rows=1000)                  # partial items: 1000 = 3 x 256 + 232
+    n = 3 * 4096 + 2000
+    assert a.rows + b.rows == n
+    Xw = X[:n]
+    ref = m.wire_proba(Xw) if kind == "mlp" else m.predict_proba(decode_wire(encode_wire(Xw)))
+    flagged = eng.drain_flagged()
+    got = np.zeros(n, bool)
+    got[(flagged["tx_id"] - 1000).astype(np.int64)] = True
+    clear = np.abs(ref - 0.5) > 2e-3
+    np.testing.assert_array_equal(got[clear], (ref >= 0.5)[clear])
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    c = c.cpu().numpy()
+    assert c[0] == n and c[1] == len(flagged) and c[1] + c[2] == n
+    assert abs(int(c[3]) - float(np.round(ref.astype(np.float64) * 1e6).sum())) < 2e-4 * n * 1e6 / 100
+    assert int(c[8:22].sum() + c[24:38].sum()) == n          # amount histogram covers every row
+    eng.close()
+    log.free()
