@@ -48,9 +48,9 @@ def parse_args(argv=None):
     ap.add_argument("--batches-per-step", type=int, default=256)
     ap.add_argument("--depth", type=int, default=None,
                     help="micro-batches in flight per GPU (default 12 for mlp/lr = p50 53 us at the "
-                         "PCIe-bound rate, profiles/r2/persist_full_item/; 6 for gbdt = 1.66e9 tx/s at "
-                         "p50 225 us with 65536-row batches, profiles/r2/gbdt_g32_persist_sweep.jsonl; "
-                         "--batch 16384 --depth 8 trades 3%% of that for p50 74 us, "
+                         "PCIe-bound rate, profiles/r2/persist_full_item/; 3 for gbdt = 1.67e9 tx/s at "
+                         "p50 107 us with 65536-row batches, profiles/r2/persist_full_item/g32_inflight_ab.jsonl; "
+                         "--batch 16384 --depth 8 gives p50 74 us at 1.64e9, "
                          "profiles/r2/gbdt_g32_operating_curve.jsonl)")
     ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--input-mode", default="zerocopy", choices=["dma", "zerocopy"])
@@ -249,7 +249,7 @@ def main(argv=None):
     if args.batch is None:
         args.batch = 65536 if args.model == "gbdt" else 4096
     if args.depth is None:
-        args.depth = 6 if args.model == "gbdt" else 12
+        args.depth = 3 if args.model == "gbdt" else 12
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine

@@ -44,6 +44,7 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_ABLATE_COUNTERS 16   // no counter/histogram atomics
 #define CCFD_ARG_ABLATE_OUTPUTS 32    // no proba/route stores
 #define CCFD_ARG_ABLATE_FENCE 64      // no per-workgroup system release
+#define CCFD_ARG_CHUNK_RING 128       // persistent G32: one-chunk prefetch ring (default) instead of the whole item in flight
 
 // Routing rule program (router/rules.py RuleSet.device_program): the configurable routing
 // rules (reference "Drools rules", README.md:427) evaluated per row in the scoring

@@ -19,6 +19,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <type_traits>
+
 #include "common.h"
 #include "persist_core.h"
 #include "rules.h"
@@ -271,16 +273,9 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     if (item == 0 && tid == 0)                            // K7: micro-batch start (item 0 claimed first)
       __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int c0 = item * (kG32Waves * cpw) + wave;       // this wave's chunks: c0 + 4k
-    G32Row pre;
-    if (c0 * kG32Rows < n) g32_fetch(xb, n, c0, lane, pre);
     unsigned fraud = 0, rows = 0, stale = 0;
     unsigned long long psum = 0;
-#pragma unroll 1
-    for (int k = 0; k < cpw; ++k) {
-      const int chunk = c0 + kG32Waves * k;
-      if (chunk * kG32Rows >= n) break;                   // wave-uniform
-      G32Row cur = pre;
-      if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) g32_fetch(xb, n, chunk + kG32Waves, lane, pre);
+    auto score_chunk = [&](int chunk, G32Row& cur) __attribute__((always_inline)) {
       g32_rows(xt[wave], lane, cur);
       unsigned b0[kF];
       const unsigned meta = g32_lift(cur, b0);
@@ -304,6 +299,41 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       rows += __popcll(__ballot(valid));
       stale += __popcll(__ballot(valid && !fresh));
       persist_emit_flagged(a, sdesc, slot, m, fr, row, lane);
+    };
+    // CCFD_G32_INFLIGHT=1: every chunk of the wave's share of the item in flight at once
+    // (static registers: no copy of a pending load, so no vmcnt(0) between chunks)
+    auto full_item = [&](auto kC) __attribute__((always_inline)) {
+      constexpr int CPW = decltype(kC)::value;
+      G32Row r[CPW];
+#pragma unroll
+      for (int k = 0; k < CPW; ++k) {
+        const int chunk = c0 + kG32Waves * k;
+        if (chunk * kG32Rows < n) g32_fetch(xb, n, chunk, lane, r[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < CPW; ++k) {
+        const int chunk = c0 + kG32Waves * k;
+        if (chunk * kG32Rows >= n) break;                 // wave-uniform
+        score_chunk(chunk, r[k]);
+      }
+    };
+    if (a.flags & CCFD_ARG_CHUNK_RING) {                  // default: one chunk ahead
+      G32Row pre;
+      if (c0 * kG32Rows < n) g32_fetch(xb, n, c0, lane, pre);
+#pragma unroll 1
+      for (int k = 0; k < cpw; ++k) {
+        const int chunk = c0 + kG32Waves * k;
+        if (chunk * kG32Rows >= n) break;                 // wave-uniform
+        G32Row cur = pre;
+        if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) g32_fetch(xb, n, chunk + kG32Waves, lane, pre);
+        score_chunk(chunk, cur);
+      }
+    } else if (cpw == 1) {
+      full_item(std::integral_constant<int, 1>{});
+    } else if (cpw == 2) {
+      full_item(std::integral_constant<int, 2>{});
+    } else {
+      full_item(std::integral_constant<int, 4>{});        // 1024-row items (engine accepts 256/512/1024)
     }
     psum = wave_sum_u64(psum);
     if (lane == 0 && rows) {
@@ -318,7 +348,14 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
 }
 
 template <int D>
-static int launch_persist_g32_d(const ccfd_persist_args& a, int grid, hipStream_t s) {
+static int launch_persist_g32_d(const ccfd_persist_args& a0, int grid, hipStream_t s) {
+  ccfd_persist_args a = a0;
+  // one-chunk prefetch ring by default: at BASELINE config 4 (65536-row batches) it measured
+  // 1.67e9 tx/s at p50 107 us (depth 3) vs 1.64e9 with the whole item in flight (VALU-heavy
+  // trees overlap the next chunk's load better); CCFD_G32_INFLIGHT=1 selects the latter.
+  // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
+  const char* e = getenv("CCFD_G32_INFLIGHT");
+  if (!e || atoi(e) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
   const size_t lds = (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
   if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true>), dim3(grid), dim3(256), lds, s, a);
   else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false>), dim3(grid), dim3(256), lds, s, a);

@@ -190,3 +190,38 @@ def test_g32_persistent_engine_with_routing_rules(gpu):
     eng.close()
     log.free()
 
+
+
+@pytest.mark.parametrize("inflight", ["0", "1"])
+@pytest.mark.parametrize("item_rows", [256, 512, 1024])
+def test_g32_persistent_item_modes_exact(gpu, monkeypatch, inflight, item_rows):
+    """Both persistent G32 item loops (one-chunk ring, default; whole item in flight,
+    CCFD_G32_INFLIGHT=1) at every item size, full and partial micro-batches: routes are the
+    f32 oracle's and the proba sum / histogram cover every row once."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    monkeypatch.setenv("CCFD_G32_INFLIGHT", inflight)
+    monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
+    B = 8192
+    X, _ = generate(B * 3 + 3000, seed=45)
+    m = build_model("gbdt", seed=10, X_ref=X[:20000], calibrate_rate=0.05)
+    dm = DeviceModel(m, gpu, bins=True)
+    eng = StreamEngine(dm, batch=B, depth=3, streams=1, exec_mode="persistent")
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 7, bins=dm.bins)
+    eng.add_log(0, log)
+    n = 2 * B + 2 * 1300                                       # 1300 = 2 x 512 + 276: partial items
+    assert eng.pump(2).rows + eng.pump(2, batch_rows=1300).rows == n
+    pr = m.predict_proba(X[:n])
+    fl = eng.drain_flagged()
+    got = np.zeros(n, bool)
+    got[(fl["tx_id"] - 7).astype(np.int64)] = True
+    np.testing.assert_array_equal(got, pr >= 0.5)
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    c = c.cpu().numpy()
+    assert c[0] == n and c[1] == (pr >= 0.5).sum() and c[4] == 0
+    assert abs(int(c[3]) - float(np.round(pr.astype(np.float64) * 1e6).sum())) <= n
+    assert int(c[8:22].sum() + c[24:38].sum()) == n
+    eng.close()
+    log.free()
