@@ -170,6 +170,15 @@ class ObliviousGBDT:
         bits = X[:, self.feat] > self.thr[None]             # [n, T, D]
         return (bits.astype(np.int64) << np.arange(self.depth)).sum(-1)   # [n, T]
 
+    def leaf_index_g32(self, rows: np.ndarray, bins: Optional["BinSpec"] = None) -> np.ndarray:
+        """Leaf indices from G32 rows (u8 [n,32], ``BinSpec.encode``) -- the device kernel's
+        form of every level, ``bin[f] > k`` with k the threshold's edge index -- [n, T]."""
+        spec = bins if bins is not None else self.bin_spec()
+        k = spec.bin_index(self.feat, self.thr)              # [T, D]; NaN thresholds: 255
+        b = np.asarray(rows, np.uint8)[:, :N_FEATURES].astype(np.int32)
+        bits = b[:, self.feat] > k[None]
+        return (bits.astype(np.int64) << np.arange(self.depth)).sum(-1)
+
     def raw_score(self, X: np.ndarray) -> np.ndarray:
         idx = self.leaf_index(X)
         vals = self.leaves[np.arange(self.n_trees)[None, :], idx]
