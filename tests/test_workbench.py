@@ -4,6 +4,8 @@ f32 model's, the saved safetensors reload to the same probabilities."""
 import importlib.util
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -29,8 +31,6 @@ def test_leaf_index_g32_matches_f32_with_non_finite_inputs():
     sp = m.bin_spec()
     np.testing.assert_array_equal(m.leaf_index(X), m.leaf_index_g32(sp.encode(X), sp))
 
-
-import pytest  # noqa: E402
 
 
 @pytest.mark.gpu
