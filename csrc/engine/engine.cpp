@@ -255,6 +255,8 @@ class Engine {
     // HIP_LAUNCH_BLOCKING-style debug mode: synchronise after every launch so a kernel fault
     // is reported against the micro-batch that caused it (SURVEY.md §5 race detection)
     if (const char* e = std::getenv("CCFD_DEBUG_SYNC")) debug_sync = std::atoi(e) != 0;
+    if (const char* e = std::getenv("CCFD_SYNC_ZC_ROWS")) sync_zc_rows = std::max(0, std::atoi(e));
+    sync_zc_rows = std::min(sync_zc_rows, cfg.max_batch);
     const unsigned out_flags = hipHostMallocMapped | hipHostMallocPortable |
                                (coherent_out ? hipHostMallocCoherent : 0u);
     for (auto& s : slots) {
@@ -308,6 +310,13 @@ class Engine {
   int wire_flag = 0;            // CCFD_ARG_WIRE_* of the row format
   int ablate = 0;
   bool debug_sync = false;
+  // score_sync of small pageable batches (the REST front end: 1..~50 rows per call) copies
+  // the rows into this pinned, mapped buffer and the kernel reads them zero-copy, instead of
+  // a staged pageable hipMemcpy before the launch (CCFD_SYNC_ZC_ROWS, default 512; 0 = off)
+  float* sync_stage = nullptr;
+  const float* sync_stage_dev = nullptr;
+  int sync_zc_rows = 512;
+  bool keep_resident = false;     // ccfd_engine_keep_resident: score_sync leaves the persistent kernel up
   ccfd_persist_ctl* pctl = nullptr;       // host (coherent pinned)
   ccfd_persist_desc* pdesc = nullptr;      // host (coherent pinned)
   ccfd_persist_dev* pdev = nullptr;        // device
@@ -482,6 +491,7 @@ class Engine {
                    (unsigned long long)stamper_iters.load());
     hipSetDevice(cfg.device);
     persist_free();
+    if (sync_stage) hipHostFree(sync_stage);
     for (auto& s : slots) {
       if (s.busy) wait_done(s);
       if (s.d_x) hipFree(s.d_x);
@@ -626,7 +636,7 @@ class Engine {
     return 0;
   }
 
-  int drain_all(ccfd_engine_stats* st = nullptr) {
+  int drain_all(ccfd_engine_stats* st = nullptr, bool halt = true) {
     // complete in submission order
     const int D = (int)slots.size();
     for (int k = 0; k < D; ++k) {
@@ -635,18 +645,20 @@ class Engine {
     }
     // fully drained: let the persistent kernel exit so the device is idle (and a
     // device-wide synchronize by the caller can never wait on a resident kernel)
-    if (persistent) return persist_halt();
+    if (persistent && halt) return persist_halt();
     return 0;
   }
 
+  // force_dma: x is pageable, stage it through the slot's device buffer; force_zc: x is a
+  // device pointer of mapped host memory the kernel reads directly, whatever the input mode
   int submit(Slot& s, const float* x_dev_or_host, const float* x_host, int rows, hipStream_t stream,
-             bool force_dma = false) {
+             bool force_dma = false, bool force_zc = false) {
     s.t_submit = now_ns();
     s.seq_no = (int64_t)seq;
     struct Acc { uint64_t& a; int64_t t0; ~Acc() { a += now_ns() - t0; } } acc{t_submit_ns, s.t_submit};
     const float* xk = x_dev_or_host;
     if (persistent) {
-      if (cfg.input_mode == 0 || force_dma) {
+      if ((cfg.input_mode == 0 || force_dma) && !force_zc) {
         HIPCHK(hipMemcpy(s.d_x, x_host, (size_t)rows * rowf * sizeof(float), hipMemcpyHostToDevice));
         xk = s.d_x;
       }
@@ -656,7 +668,7 @@ class Engine {
       s.busy = true;
       return 0;
     }
-    if (cfg.input_mode == 0 || force_dma) {
+    if ((cfg.input_mode == 0 || force_dma) && !force_zc) {
       HIPCHK(hipMemcpyAsync(s.d_x, x_host, (size_t)rows * rowf * sizeof(float),
                             hipMemcpyHostToDevice, stream));
       xk = s.d_x;
@@ -819,9 +831,16 @@ class Engine {
     st->lat_mean_us = lat_sum_us / (double)lat_n;
   }
 
+  int halt_resident() {
+    if (!persistent || !prunning) return 0;
+    HIPCHK(hipSetDevice(cfg.device));
+    const int rc = drain_all();
+    return rc ? rc : persist_halt();
+  }
+
   int score_sync(const float* x, int32_t n, float* proba_out, uint8_t* route_out) {
     HIPCHK(hipSetDevice(cfg.device));
-    int rc = drain_all();
+    int rc = drain_all(nullptr, /*halt=*/!keep_resident);
     if (rc) return rc;
     const int D = (int)slots.size();
     for (int32_t off = 0; off < n; off += cfg.max_batch) {
@@ -829,7 +848,22 @@ class Engine {
       Slot& s = slots[seq % D];
       hipStream_t stream = streams[seq % streams.size()];
       const float* xh = x + (size_t)off * rowf;
-      rc = submit(s, xh, xh, rows, stream, /*force_dma=*/true);
+      if (rows <= sync_zc_rows) {
+        if (!sync_stage) {
+          void* p = nullptr;
+          HIPCHK(hipHostMalloc(&p, (size_t)sync_zc_rows * rowf * sizeof(float),
+                               hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+          sync_stage = static_cast<float*>(p);
+          void* d = nullptr;
+          HIPCHK(hipHostGetDevicePointer(&d, p, 0));
+          sync_stage_dev = static_cast<const float*>(d);
+        }
+        // the previous batch has completed (wait_done below), so the stage is free
+        std::memcpy(sync_stage, xh, (size_t)rows * rowf * sizeof(float));
+        rc = submit(s, sync_stage_dev, sync_stage, rows, stream, /*force_dma=*/false, /*force_zc=*/true);
+      } else {
+        rc = submit(s, xh, xh, rows, stream, /*force_dma=*/true);
+      }
       if (rc) return rc;
       ++seq;
       rc = wait_done(s);
@@ -840,7 +874,7 @@ class Engine {
       if (proba_out) std::memcpy(proba_out + off, s.h_proba, rows * sizeof(float));
       if (route_out) std::memcpy(route_out + off, s.h_route, rows);
     }
-    return persistent ? persist_halt() : 0;
+    return persistent && !keep_resident ? persist_halt() : 0;
   }
 
   // Model hot swap (X1 at runtime): every in-flight micro-batch completes with the old
@@ -1056,6 +1090,17 @@ int64_t ccfd_engine_cursor(void* eng, int partition) {
   if (partition < 0 || partition >= (int)e->parts.size()) return -1;
   Partition& P = *e->parts[partition];
   return P.ring ? P.rr.released_count() : P.cursor;
+}
+
+int ccfd_engine_halt(void* eng) {
+  if (!eng) return -1;
+  return static_cast<Engine*>(eng)->halt_resident();
+}
+
+int ccfd_engine_keep_resident(void* eng, int on) {
+  if (!eng) return -1;
+  static_cast<Engine*>(eng)->keep_resident = on != 0;
+  return 0;
 }
 
 int ccfd_engine_set_amount(void* eng, int partition, const float* amount) {

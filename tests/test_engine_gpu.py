@@ -272,3 +272,49 @@ def test_persistent_wire_item_sizes_exact(gpu, setup, monkeypatch, kind, item_ro
     assert int(c[8:22].sum() + c[24:38].sum()) == n          # amount histogram covers every row
     eng.close()
     log.free()
+
+
+@pytest.mark.parametrize("wire", [False, True])
+def test_score_sync_small_batches_zero_copy_stage(gpu, setup, monkeypatch, wire):
+    """score() of small pageable batches goes through the pinned zero-copy stage
+    (CCFD_SYNC_ZC_ROWS, the REST front end's path); larger ones through the DMA staging:
+    outputs are identical to the all-DMA engine's at every size across the cut-over."""
+    from ccfd_demo_summit_amd.engine import StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    X, m = setup
+    out = {}
+    for zc in ("0", "512"):
+        monkeypatch.setenv("CCFD_SYNC_ZC_ROWS", zc)
+        eng = StreamEngine(DeviceModel(m, gpu, wire=wire), batch=1024, depth=2, input_mode="dma")
+        out[zc] = [eng.score(X[7:7 + n]) for n in (1, 31, 511, 512, 513, 1024, 3000)]
+        eng.close()
+    for (p0, r0), (p1, r1) in zip(out["0"], out["512"]):
+        np.testing.assert_array_equal(p0, p1)
+        np.testing.assert_array_equal(r0, r1)
+    ref = m.wire_proba(X[7:3007]) if wire else m.predict_proba(X[7:3007])
+    assert np.abs(out["512"][-1][0] - ref).max() < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["mlp", "lr"])
+def test_resident_persistent_scorer_matches_launch(gpu, setup, kind):
+    """GpuScorer(exec_mode="persistent"): the kernel stays resident across score() calls
+    (keep_resident) and every small request batch scores exactly like the launch-mode scorer;
+    close() halts it."""
+    from ccfd_demo_summit_amd.serving.scorers import GpuScorer
+    X, m = setup
+    if kind == "lr":
+        m = build_model("lr", seed=5, X_ref=X[:20000], calibrate_rate=0.01)
+    a = GpuScorer(m, 0.5, max_batch=1024)
+    b = GpuScorer(m, 0.5, max_batch=1024, exec_mode="persistent")
+    assert b.exec_mode == "persistent"
+    off = 0
+    for n in (1, 2, 31, 64, 500, 1024, 1500, 1, 7):
+        pa, ra = a.score(X[off:off + n])
+        pb, rb = b.score(X[off:off + n])
+        np.testing.assert_array_equal(pa, pb)
+        np.testing.assert_array_equal(ra, rb)
+        off += n
+    # a resident kernel never finishes, and hipFree synchronises the device: every other
+    # engine of the process frees only after the resident ones halted (GpuScorer.close)
+    a.close()
+    b.close()
