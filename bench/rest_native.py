@@ -25,8 +25,6 @@ def main():
     ap.add_argument("--rows-per-request", type=int, default=1)
     ap.add_argument("--workers", type=int, default=1, help="server epoll threads (one GPU engine each)")
     ap.add_argument("--client-threads", type=int, default=0, help="load generator threads (0 = 1 per 64 conns)")
-    ap.add_argument("--exec-mode", default="launch", choices=["launch", "persistent"],
-                    help="GPU scorer: a kernel launch per call, or a resident kernel (MLP/LR)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from ccfd_demo_summit_amd.contracts import seldon
@@ -36,13 +34,12 @@ def main():
     from ccfd_demo_summit_amd.serving.scorers import make_scorer
     X, _ = generate(100_000, seed=7)
     model = build_model(a.model, seed=0, X_ref=X, calibrate_rate=FRAUD_RATE)
-    kw = {"exec_mode": a.exec_mode} if a.device != "cpu" and a.exec_mode != "launch" else {}
-    scorers = [make_scorer(model, 0.5, device=a.device, max_batch=4096, **kw) for _ in range(a.workers)]
+    scorers = [make_scorer(model, 0.5, device=a.device, max_batch=4096) for _ in range(a.workers)]
     scorer = scorers[0]
     srv = NativeSeldonServer(scorers if a.workers > 1 else scorer, "127.0.0.1", 0, workers=a.workers)
     body = json.dumps(seldon.build_request(X[:a.rows_per_request])).encode()
     res = {"metric": "Seldon REST predict() through the native front end", "model": a.model,
-           "scorer": getattr(scorer, "device", "cpu"), "exec_mode": getattr(scorer, "exec_mode", None), "rows_per_request": a.rows_per_request,
+           "scorer": getattr(scorer, "device", "cpu"), "rows_per_request": a.rows_per_request,
            "server_workers": a.workers, "runs": []}
     http_load("127.0.0.1", srv.port, body, conns=8, seconds=0.5)          # warm-up
     for c in [int(x) for x in a.conns.split(",")]:

@@ -234,15 +234,6 @@ class StreamEngine:
                                      1 if drain else 0, C.byref(st)), "ccfd_engine_pump")
         return _stats(st)
 
-    def keep_resident(self, on: bool = True) -> None:
-        """Persistent engines: leave the kernel resident across score() calls (a request /
-        response server); by default every score() halts it again."""
-        check(lib().ccfd_engine_keep_resident(C.c_void_p(self.h), 1 if on else 0), "ccfd_engine_keep_resident")
-
-    def halt(self) -> None:
-        """Halt a resident persistent kernel (relaunched by the next submission)."""
-        check(lib().ccfd_engine_halt(C.c_void_p(self.h)), "ccfd_engine_halt")
-
     def score(self, X: np.ndarray):
         """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
         X = np.ascontiguousarray(X, dtype=np.float32)

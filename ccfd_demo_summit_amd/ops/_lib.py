@@ -127,8 +127,6 @@ def lib() -> C.CDLL:
                                       C.c_void_p, C.c_void_p]
         L.ccfd_encode_g32.restype = C.c_int64
         L.ccfd_engine_set_amount.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
-        L.ccfd_engine_keep_resident.argtypes = [C.c_void_p, C.c_int]
-        L.ccfd_engine_halt.argtypes = [C.c_void_p]
         _lib = L
         return L
 

@@ -316,7 +316,6 @@ class Engine {
   float* sync_stage = nullptr;
   const float* sync_stage_dev = nullptr;
   int sync_zc_rows = 512;
-  bool keep_resident = false;     // ccfd_engine_keep_resident: score_sync leaves the persistent kernel up
   ccfd_persist_ctl* pctl = nullptr;       // host (coherent pinned)
   ccfd_persist_desc* pdesc = nullptr;      // host (coherent pinned)
   ccfd_persist_dev* pdev = nullptr;        // device
@@ -636,7 +635,7 @@ class Engine {
     return 0;
   }
 
-  int drain_all(ccfd_engine_stats* st = nullptr, bool halt = true) {
+  int drain_all(ccfd_engine_stats* st = nullptr) {
     // complete in submission order
     const int D = (int)slots.size();
     for (int k = 0; k < D; ++k) {
@@ -645,7 +644,7 @@ class Engine {
     }
     // fully drained: let the persistent kernel exit so the device is idle (and a
     // device-wide synchronize by the caller can never wait on a resident kernel)
-    if (persistent && halt) return persist_halt();
+    if (persistent) return persist_halt();
     return 0;
   }
 
@@ -831,16 +830,9 @@ class Engine {
     st->lat_mean_us = lat_sum_us / (double)lat_n;
   }
 
-  int halt_resident() {
-    if (!persistent || !prunning) return 0;
-    HIPCHK(hipSetDevice(cfg.device));
-    const int rc = drain_all();
-    return rc ? rc : persist_halt();
-  }
-
   int score_sync(const float* x, int32_t n, float* proba_out, uint8_t* route_out) {
     HIPCHK(hipSetDevice(cfg.device));
-    int rc = drain_all(nullptr, /*halt=*/!keep_resident);
+    int rc = drain_all();
     if (rc) return rc;
     const int D = (int)slots.size();
     for (int32_t off = 0; off < n; off += cfg.max_batch) {
@@ -874,7 +866,7 @@ class Engine {
       if (proba_out) std::memcpy(proba_out + off, s.h_proba, rows * sizeof(float));
       if (route_out) std::memcpy(route_out + off, s.h_route, rows);
     }
-    return persistent && !keep_resident ? persist_halt() : 0;
+    return persistent ? persist_halt() : 0;
   }
 
   // Model hot swap (X1 at runtime): every in-flight micro-batch completes with the old
@@ -1090,17 +1082,6 @@ int64_t ccfd_engine_cursor(void* eng, int partition) {
   if (partition < 0 || partition >= (int)e->parts.size()) return -1;
   Partition& P = *e->parts[partition];
   return P.ring ? P.rr.released_count() : P.cursor;
-}
-
-int ccfd_engine_halt(void* eng) {
-  if (!eng) return -1;
-  return static_cast<Engine*>(eng)->halt_resident();
-}
-
-int ccfd_engine_keep_resident(void* eng, int on) {
-  if (!eng) return -1;
-  static_cast<Engine*>(eng)->keep_resident = on != 0;
-  return 0;
 }
 
 int ccfd_engine_set_amount(void* eng, int partition, const float* amount) {

@@ -275,14 +275,6 @@ int64_t ccfd_engine_cursor(void* eng, int partition);
 // G32 logs/rings: host-side Amount column of partition p (the flagged-record amount; the
 // rows themselves carry only its bucket).  Call after set_log / set_ring.
 int ccfd_engine_set_amount(void* eng, int partition, const float* amount);
-// Persistent engines: keep the kernel resident across ccfd_engine_score_sync calls (a
-// request/response server scoring one small batch at a time) instead of halting it after
-// each call.  No-op for launch-mode engines.
-int ccfd_engine_keep_resident(void* eng, int on);
-// Halt a resident persistent kernel (it relaunches at the next submission).  A resident kernel
-// never completes and hipFree / hipHostFree synchronise the device, so every resident kernel
-// of the process must be halted before any engine is destroyed or device memory is freed.
-int ccfd_engine_halt(void* eng);
 
 // Streaming (ring) mode: partition p is an SPSC ring of `capacity` rows in pinned memory.
 // Producer (ingest thread): ring_acquire -> write rows at [row, row+n) -> ring_commit(n).

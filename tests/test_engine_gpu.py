@@ -294,27 +294,3 @@ def test_score_sync_small_batches_zero_copy_stage(gpu, setup, monkeypatch, wire)
     ref = m.wire_proba(X[7:3007]) if wire else m.predict_proba(X[7:3007])
     assert np.abs(out["512"][-1][0] - ref).max() < 1e-2
 
-
-@pytest.mark.parametrize("kind", ["mlp", "lr"])
-def test_resident_persistent_scorer_matches_launch(gpu, setup, kind):
-    """GpuScorer(exec_mode="persistent"): the kernel stays resident across score() calls
-    (keep_resident) and every small request batch scores exactly like the launch-mode scorer;
-    close() halts it."""
-    from ccfd_demo_summit_amd.serving.scorers import GpuScorer
-    X, m = setup
-    if kind == "lr":
-        m = build_model("lr", seed=5, X_ref=X[:20000], calibrate_rate=0.01)
-    a = GpuScorer(m, 0.5, max_batch=1024)
-    b = GpuScorer(m, 0.5, max_batch=1024, exec_mode="persistent")
-    assert b.exec_mode == "persistent"
-    off = 0
-    for n in (1, 2, 31, 64, 500, 1024, 1500, 1, 7):
-        pa, ra = a.score(X[off:off + n])
-        pb, rb = b.score(X[off:off + n])
-        np.testing.assert_array_equal(pa, pb)
-        np.testing.assert_array_equal(ra, rb)
-        off += n
-    # a resident kernel never finishes, and hipFree synchronises the device: every other
-    # engine of the process frees only after the resident ones halted (GpuScorer.close)
-    a.close()
-    b.close()
