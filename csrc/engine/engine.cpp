@@ -256,6 +256,7 @@ class Engine {
     // is reported against the micro-batch that caused it (SURVEY.md §5 race detection)
     if (const char* e = std::getenv("CCFD_DEBUG_SYNC")) debug_sync = std::atoi(e) != 0;
     if (const char* e = std::getenv("CCFD_SYNC_ZC_ROWS")) sync_zc_rows = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("CCFD_IDLE_FLUSH_US")) idle_flush_ns = (int64_t)std::atoi(e) * 1000;
     sync_zc_rows = std::min(sync_zc_rows, cfg.max_batch);
     const unsigned out_flags = hipHostMallocMapped | hipHostMallocPortable |
                                (coherent_out ? hipHostMallocCoherent : 0u);
@@ -316,6 +317,9 @@ class Engine {
   float* sync_stage = nullptr;
   const float* sync_stage_dev = nullptr;
   int sync_zc_rows = 512;
+  // run(): a partial batch goes out once its oldest row is idle_flush_ns old if nothing is in
+  // flight (CCFD_IDLE_FLUSH_US; < 0 = off: partial batches wait for the flush deadline)
+  int64_t idle_flush_ns = 20'000;
   ccfd_persist_ctl* pctl = nullptr;       // host (coherent pinned)
   ccfd_persist_desc* pdesc = nullptr;      // host (coherent pinned)
   ccfd_persist_dev* pdev = nullptr;        // device
@@ -942,6 +946,12 @@ class Engine {
   // Consumer loop for `budget_us`: submit every full micro-batch (and partial ones whose
   // first row has waited >= flush_us: deadline flush bounds latency at low load), complete
   // finished batches; returns the number of batches submitted.
+  bool nothing_in_flight() const {
+    for (const Slot& s : slots)
+      if (s.busy) return false;
+    return true;
+  }
+
   int run(int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {
     HIPCHK(hipSetDevice(cfg.device));
     // the default 50 us timer slack would turn every idle 5 us sleep into ~55 us of added
@@ -994,7 +1004,13 @@ class Engine {
           int64_t rows = std::min<int64_t>({avail, (int64_t)cfg.max_batch, P.n - phys});
           const bool full = rows == cfg.max_batch || rows == P.n - phys;
           const int64_t arr = P.arrival_of(P.rr.taken());
-          if (!full && now - arr < flush_us * 1000) break;  // wait for more rows
+          // a partial batch waits for more rows until its deadline -- unless the GPU has
+          // nothing in flight (work-conserving: at low / moderate arrival rates a row is
+          // scored right away instead of after flush_us; under load the in-flight batches
+          // give the ring time to fill, so batches grow back to max_batch)
+          if (!full && now - arr < flush_us * 1000 &&
+              !(idle_flush_ns >= 0 && now - arr >= idle_flush_ns && nothing_in_flight()))
+            break;
           s.part = (int)q; s.start = phys; s.rows = (int32_t)rows;
           const size_t off = (size_t)phys * rowf;
           hipStream_t stream = streams[seq % streams.size()];
