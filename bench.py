@@ -58,6 +58,9 @@ def parse_args(argv=None):
     ap.add_argument("--exec-mode", default="auto", choices=["auto", "launch", "persistent"],
                     help="auto = persistent kernel for mlp/lr and for gbdt on G32 rows with zero-copy "
                          "in/out, launches otherwise (profiles/r1/persist_sweep.txt, profiles/r2/)")
+    ap.add_argument("--trace", default=None,
+                    help="rank 0: write a Chrome / Perfetto timeline of the last 65536 timed micro-batches "
+                         "(per-batch stage trace: queued, in flight, device, hand-off)")
     ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 128 otherwise)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
@@ -355,6 +358,8 @@ def main(argv=None):
     eng.pump(0, drain=True)
     epochs.finish()
     eng.reset_stats()
+    if args.trace and ctx.rank == 0:
+        eng.enable_trace(65536)
     c0 = reducer.snapshot()[0]
     rows0, fraud0 = int(c0[0]), int(c0[1])
     eng.drain_flagged()          # warmup hand-offs are not part of the timed run
@@ -378,6 +383,9 @@ def main(argv=None):
     # latency: per-rank histogram of the timed batches, merged over ranks (X3)
     st_final = eng.pump(0, drain=True)
     rows_local[0] += st_final.rows
+    if args.trace and ctx.rank == 0:
+        from ccfd_demo_summit_amd.utils.tracing import dump_batch_trace
+        dump_batch_trace(eng.read_trace(), args.trace, name=f"engine rank 0 ({args.model})")
     lat_local = st_final.lat_hist.astype(np.int64)
     lat_t = torch.from_numpy(lat_local).to(dev)
     if ctx.initialized:

@@ -14,8 +14,8 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..ops._lib import (FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig, EngineStats,
-                        Flagged, check, last_error, lib)
+from ..ops._lib import (BATCH_TRACE_DTYPE, FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig,
+                        EngineStats, Flagged, check, last_error, lib)
 from ..ops.kernels import ROW_BYTES, DeviceModel
 
 N_FEATURES = 30
@@ -380,6 +380,23 @@ class StreamEngine:
 
     def reset_stats(self) -> None:
         lib().ccfd_engine_reset_stats(C.c_void_p(self.h))
+
+    def enable_trace(self, capacity: int = 65536) -> None:
+        """Keep the stage timestamps of the last ``capacity`` completed micro-batches
+        (0 = off); ``read_trace()`` returns them, ``utils.tracing.batch_trace_events`` turns
+        them into a Chrome / Perfetto timeline."""
+        check(lib().ccfd_engine_trace_enable(C.c_void_p(self.h), int(capacity)), "ccfd_engine_trace_enable")
+        self._trace_cap = int(capacity)
+
+    def read_trace(self) -> np.ndarray:
+        """Structured array (BATCH_TRACE_DTYPE), oldest batch first."""
+        out = np.zeros(getattr(self, "_trace_cap", 0), BATCH_TRACE_DTYPE)
+        if out.size == 0:
+            return out
+        n = lib().ccfd_engine_trace_read(C.c_void_p(self.h), out.ctypes.data, out.size)
+        if n < 0:
+            raise RuntimeError(f"ccfd_engine_trace_read failed: {last_error()}")
+        return out[:n]
 
     def cursor(self, partition: int) -> int:
         return int(lib().ccfd_engine_cursor(C.c_void_p(self.h), int(partition)))

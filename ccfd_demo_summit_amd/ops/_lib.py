@@ -63,6 +63,11 @@ class EngineStats(C.Structure):
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
                  ("partition", "<u4")]
 
+# ccfd_batch_trace (ccfd_abi.h): per-micro-batch stage timestamps
+BATCH_TRACE_DTYPE = [("seq", "<i8"), ("partition", "<i4"), ("rows", "<i4"), ("t_arrival", "<i8"),
+                     ("t_submit", "<i8"), ("t_landed", "<i8"), ("t_complete", "<i8"), ("dev_start", "<i8"),
+                     ("dev_end", "<i8"), ("flagged", "<i4"), ("pad", "<i4")]
+
 _lib = None
 _lock = threading.Lock()
 
@@ -108,6 +113,8 @@ def lib() -> C.CDLL:
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]
         L.ccfd_engine_cursor.restype = C.c_int64
         L.ccfd_engine_reset_stats.argtypes = [C.c_void_p]
+        L.ccfd_engine_trace_enable.argtypes = [C.c_void_p, C.c_int32]
+        L.ccfd_engine_trace_read.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.ccfd_engine_set_ring.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         L.ccfd_engine_ring_acquire.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_int64)]
         L.ccfd_engine_ring_acquire.restype = C.c_int64

@@ -98,3 +98,44 @@ class Tracer:
 
 
 tracer = Tracer()
+
+
+def batch_trace_events(trace, pid: int = 0, name: str = "engine") -> List[Dict[str, Any]]:
+    """Chrome trace events of an engine's per-batch stage trace (``StreamEngine.read_trace``):
+    one track per stage -- ``queued`` (ring arrival -> submit), ``in flight`` (submit ->
+    completion record in host memory), ``device`` (first item claimed -> last item done,
+    aligned to the host clock) and ``hand-off`` (landed -> retired by the engine thread).
+
+    The device clock has its own epoch: it is aligned by the smallest ``t_landed - dev_end``
+    over the trace (the fastest observed completion-record round trip), so device spans sit
+    just before the host saw their completion and never after it."""
+    import numpy as np
+    tr = np.asarray(trace)
+    ev: List[Dict[str, Any]] = [{"name": "process_name", "ph": "M", "pid": pid, "args": {"name": name}}]
+    for tid, label in enumerate(("queued", "in flight", "device", "hand-off")):
+        ev.append({"name": "thread_name", "ph": "M", "pid": pid, "tid": tid, "args": {"name": label}})
+    if tr.size == 0:
+        return ev
+    dev = tr["dev_end"] > 0
+    off = int((tr["t_landed"][dev] - tr["dev_end"][dev]).min()) if dev.any() else 0
+    t0 = int(min(tr["t_submit"].min(), tr["t_arrival"][tr["t_arrival"] > 0].min()
+                 if (tr["t_arrival"] > 0).any() else tr["t_submit"].min()))
+
+    def span(tid, a, b, e):
+        ev.append({"name": f"batch {int(e['seq'])}", "ph": "X", "pid": pid, "tid": tid, "ts": (a - t0) / 1e3,
+                   "dur": max(0, b - a) / 1e3, "args": {"rows": int(e["rows"]), "partition": int(e["partition"]),
+                                                        "flagged": int(e["flagged"])}})
+    for e in tr:
+        if e["t_arrival"] > 0:
+            span(0, int(e["t_arrival"]), int(e["t_submit"]), e)
+        span(1, int(e["t_submit"]), int(e["t_landed"]), e)
+        if e["dev_end"] > 0:
+            span(2, int(e["dev_start"]) + off, int(e["dev_end"]) + off, e)
+        span(3, int(e["t_landed"]), int(e["t_complete"]), e)
+    return ev
+
+
+def dump_batch_trace(trace, path: str, **kw) -> str:
+    with open(path, "w") as f:
+        json.dump({"traceEvents": batch_trace_events(trace, **kw), "displayTimeUnit": "ns"}, f)
+    return path

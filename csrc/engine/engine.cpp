@@ -151,6 +151,8 @@ class Engine {
   uint64_t lat_hist[256] = {};
   uint64_t t_submit_ns = 0, t_wait_ns = 0, t_complete_ns = 0;
   uint64_t dev_batches = 0, dev_exec_ns = 0, dev_hist[256] = {};
+  std::vector<ccfd_batch_trace> trace;     // per-batch stage trace ring (ccfd_engine_trace_enable)
+  uint64_t trace_n = 0;                    // entries ever written
   double wall_ns_per_tick = 0.0;   // device wall clock (s_memrealtime) period
   unsigned long long done_counter = 0;
 
@@ -626,6 +628,21 @@ class Engine {
       if (nf) push_flagged(s);
     }
     if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
+    if (!trace.empty()) {
+      ccfd_batch_trace& e = trace[trace_n++ % trace.size()];
+      e.seq = s.seq_no;
+      e.partition = s.part;
+      e.rows = s.rows;
+      e.t_arrival = s.t_arrival;
+      e.t_submit = s.t_submit;
+      e.t_landed = t_landed;
+      e.t_complete = now_ns();
+      const bool dev = s.use_flag && wall_ns_per_tick > 0 && s.done_ptr[3] > s.done_ptr[2];
+      e.dev_start = dev ? (int64_t)((double)s.done_ptr[2] * wall_ns_per_tick) : 0;
+      e.dev_end = dev ? (int64_t)((double)s.done_ptr[3] * wall_ns_per_tick) : 0;
+      e.flagged = (int32_t)nf;
+      e.pad = 0;
+    }
     Partition& P = *parts[s.part];
     if (P.ring) {
       // batches of one partition complete in submission order: release in order
@@ -1124,6 +1141,26 @@ int ccfd_engine_ring_commit(void* eng, int partition, int64_t n) {
 
 int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {
   return static_cast<Engine*>(eng)->run(budget_us, flush_us, st);
+}
+
+int ccfd_engine_trace_enable(void* eng, int32_t capacity) {
+  if (!eng || capacity < 0 || capacity > (1 << 24)) return -1;
+  Engine* e = static_cast<Engine*>(eng);
+  e->trace.assign((size_t)capacity, ccfd_batch_trace{});
+  e->trace_n = 0;
+  return 0;
+}
+
+int ccfd_engine_trace_read(void* eng, ccfd_batch_trace* out, int32_t max) {
+  if (!eng || (!out && max > 0) || max < 0) return -1;
+  Engine* e = static_cast<Engine*>(eng);
+  const uint64_t cap = e->trace.size();
+  if (cap == 0) return 0;
+  const uint64_t have = std::min<uint64_t>(e->trace_n, cap);
+  const uint64_t n = std::min<uint64_t>(have, (uint64_t)max);
+  const uint64_t first = e->trace_n - n;                 // the newest n, oldest first
+  for (uint64_t i = 0; i < n; ++i) out[i] = e->trace[(first + i) % cap];
+  return (int)n;
 }
 
 void ccfd_engine_reset_stats(void* eng) {

@@ -287,6 +287,26 @@ int ccfd_engine_ring_commit(void* eng, int partition, int64_t n);
 int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st);
 void ccfd_engine_reset_stats(void* eng);
 
+// Per-micro-batch stage trace (SURVEY.md §5 "per-stage timestamps in a ring buffer"): the
+// last `capacity` completed batches, host times in ns of the engine's monotonic clock, device
+// times in ns of the GPU wall clock (its own epoch; tools align the two).  capacity 0 = off.
+typedef struct {
+  int64_t seq;          // submission number
+  int32_t partition;    // partition (log / ring) index; score() batches are not traced
+  int32_t rows;
+  int64_t t_arrival;    // oldest row committed to the ring (0: pre-filled log / score())
+  int64_t t_submit;     // descriptor posted / kernel launched
+  int64_t t_landed;     // completion record seen in host memory (completion stamper)
+  int64_t t_complete;   // retired by the engine thread (flagged rows handed off)
+  int64_t dev_start;    // first item claimed / first workgroup started (device clock, ns)
+  int64_t dev_end;      // last item done (device clock, ns); 0 when outputs went by DMA
+  int32_t flagged;
+  int32_t pad;
+} ccfd_batch_trace;
+int ccfd_engine_trace_enable(void* eng, int32_t capacity);
+// copies the retained entries, oldest first; returns the number written (<= max)
+int ccfd_engine_trace_read(void* eng, ccfd_batch_trace* out, int32_t max);
+
 // ---------------------------------------------------------------------------
 // Native ingest helpers (JSON transaction parser, TXB1 batch codec)
 // Parse `n_msgs` JSON transactions (concatenated, offsets[i]..offsets[i+1]) into

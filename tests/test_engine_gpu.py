@@ -294,3 +294,29 @@ def test_score_sync_small_batches_zero_copy_stage(gpu, setup, monkeypatch, wire)
     ref = m.wire_proba(X[7:3007]) if wire else m.predict_proba(X[7:3007])
     assert np.abs(out["512"][-1][0] - ref).max() < 1e-2
 
+
+
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+def test_batch_stage_trace(gpu, setup, exec_mode, tmp_path):
+    """Per-batch stage trace ring: one entry per retired micro-batch (the newest `capacity`),
+    stages in order (submit <= landed <= retired, device window non-empty), rows and flagged
+    counts match the pump, and the Chrome conversion writes a loadable timeline."""
+    import json
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.utils.tracing import dump_batch_trace
+    X, m = setup
+    eng = StreamEngine(DeviceModel(m, gpu, wire=True), batch=2048, depth=4, streams=2, exec_mode=exec_mode)
+    log = PartitionLog.from_arrays(X, wire=True)
+    eng.add_log(0, log)
+    eng.enable_trace(8)
+    st = eng.pump(11)
+    tr = eng.read_trace()
+    assert len(tr) == 8 and list(tr["seq"]) == list(range(3, 11))          # newest 8, oldest first
+    assert (tr["rows"] == 2048).all() and int(st.fraud_rows) >= int(tr["flagged"].sum())
+    assert (tr["t_submit"] <= tr["t_landed"]).all() and (tr["t_landed"] <= tr["t_complete"]).all()
+    assert (tr["dev_end"] > tr["dev_start"]).all() and (tr["dev_start"] > 0).all()
+    doc = json.loads(open(dump_batch_trace(tr, str(tmp_path / "t.json"))).read())
+    assert len([e for e in doc["traceEvents"] if e["ph"] == "X"]) == 3 * 8   # no ring arrival in pump
+    eng.close()
+    log.free()
