@@ -8,9 +8,10 @@
 //                                                   polls host memory with relaxed system-
 //                                                   scope loads; s_sleep back-off)
 //   read descriptor b % R from the device mirror    -> LDS
-//   4 waves x T tiles x 16 rows (item = 64T rows; default T = 8, CCFD_PERSIST_ITEM_ROWS),
-//   next tile prefetched while the current one computes (f32 rows via a wave-private LDS
-//   tile, W64 rows straight into registers), scored with the same fused math as the
+//   4 waves x T tiles x 16 rows (item = 64T rows, CCFD_PERSIST_ITEM_ROWS; engine defaults
+//   T = 8 for the MLP on W64 rows, 4 otherwise): W64 items of 4 / 8 tiles issue every tile
+//   at once and score them in pairs, other sizes prefetch the next tile while the current
+//   one computes (f32 rows via a wave-private LDS tile); the same fused math as the
 //   per-batch kernels (mlp_core.h), outputs written straight to host-mapped memory,
 //   fraud rows appended to the descriptor's compacted flag list
 //   counters + amount histogram -> counters[desc.epoch] (one atomic set per item)
@@ -131,8 +132,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
       persist_emit_flagged(a, sdesc, slot, m, fr && g == 0, row, lane);
     };
-    // W64 items of 4 or 8 tiles per wave (256 / 512 rows; 256 is the default): every tile of
-    // the item in flight at once -- the item costs one PCIe round trip instead of one per
+    // W64 items of 4 or 8 tiles per wave (256 / 512 rows: the LR / MLP defaults): every tile
+    // of the item in flight at once -- the item costs one PCIe round trip instead of one per
     // tile, so fewer rows in flight keep the link busy (lower p50 at the same rate) -- and
     // scored in pairs (mlp_tile_w64_x2: one LDS weight read feeds two MFMAs)
     auto full_item = [&](auto kT) __attribute__((always_inline)) {
@@ -192,9 +193,11 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
           tile_features(tile_lds, c, g, xv);
         }
-        float xr[8];
+        float xr[8];                                         // raw features for the rules
+        if constexpr (kR) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xr[j] = xv[j];
+          for (int j = 0; j < 8; ++j) xr[j] = xv[j];
+        }
         float p, amount;
         if (kModel == CCFD_MODEL_MLP) {
           if (wire) {        // W64 blob: raw bf16 operands, folded normalisation (mlp_core.h)
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
             p = mlp_tile_w64(sblob, LW, cur_w, g, lane);
           } else {
             p = mlp_tile(sblob, L, xv, g, lane, amount);
-            if (g == 3) xr[5] = amount;                    // the model replaced Amount by its log1p
+            if (kR && g == 3) xr[5] = amount;              // the model replaced Amount by its log1p
           }
         } else {
           amount = xv[5];
