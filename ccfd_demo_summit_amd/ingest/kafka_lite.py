@@ -32,10 +32,8 @@ import time
 from typing import Dict, List, Optional, Set, Tuple
 
 from .batch_store import BatchStore, InvalidBatch
-from .kafka_wire import (API_VERSIONS, CREATE_TOPICS, ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER,
-                         ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION,
-                         FETCH, FIND_COORDINATOR, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH, PRODUCE,
-                         SUPPORTED, Reader, Writer)
+from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS,
+                         ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
 
 NODE_ID = 1
 ERR_ILLEGAL_GENERATION, ERR_UNKNOWN_MEMBER, ERR_REBALANCE_IN_PROGRESS = 22, 25, 27

@@ -16,7 +16,7 @@ OFFSET_OUT_OF_RANGE follows ``offset_reset`` (earliest / latest / none).
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 import numpy as np
 

@@ -8,7 +8,7 @@ Grafana dashboards query exactly these names (deploy/grafana/*.json).
 from __future__ import annotations
 
 import threading
-from typing import Callable, Dict, Optional, Sequence
+from typing import Callable, Optional, Sequence
 
 import numpy as np
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest

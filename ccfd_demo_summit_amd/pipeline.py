@@ -12,12 +12,11 @@ engine ignores duplicate signals.
 """
 from __future__ import annotations
 
-import json
+
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable, Dict, Optional
 
-import numpy as np
 
 from .config import Config
 from .ingest.broker import InProcBroker
