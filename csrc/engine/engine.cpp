@@ -459,10 +459,11 @@ class Engine {
     }
     for (auto& s : slots) if (s.busy) wait_done(s);
     persist_halt();
-    hipStreamDestroy(pstream);
-    hipFree(pdev);
-    hipHostFree(pdesc);
-    hipHostFree(pctl);
+    // teardown: nothing useful can be done about a failed release, so results are dropped
+    (void)hipStreamDestroy(pstream);
+    (void)hipFree(pdev);
+    (void)hipHostFree(pdesc);
+    (void)hipHostFree(pctl);
     if (persist_counted) g_persist_engines.fetch_sub(1);
     persist_counted = false;
     persistent = false;
@@ -494,23 +495,23 @@ class Engine {
                    (unsigned long long)stamp_used, (unsigned long long)stamp_missed,
                    (unsigned long long)stamp_rejected, (unsigned long long)stamps_written.load(),
                    (unsigned long long)stamper_iters.load());
-    hipSetDevice(cfg.device);
+    (void)hipSetDevice(cfg.device);
     persist_free();
-    if (sync_stage) hipHostFree(sync_stage);
+    if (sync_stage) (void)hipHostFree(sync_stage);
     for (auto& s : slots) {
       if (s.busy) wait_done(s);
-      if (s.d_x) hipFree(s.d_x);
-      if (s.d_proba) hipFree(s.d_proba);
-      if (s.d_route) hipFree(s.d_route);
-      if (s.h_proba) hipHostFree(s.h_proba);
-      if (s.h_route) hipHostFree(s.h_route);
-      if (s.ev) hipEventDestroy(s.ev);
-      if (s.d_ctl) hipFree(s.d_ctl);
-      if (s.h_flag) hipHostFree(s.h_flag);
-      if (s.h_done) hipHostFree(const_cast<unsigned long long*>(s.h_done));
+      if (s.d_x) (void)hipFree(s.d_x);
+      if (s.d_proba) (void)hipFree(s.d_proba);
+      if (s.d_route) (void)hipFree(s.d_route);
+      if (s.h_proba) (void)hipHostFree(s.h_proba);
+      if (s.h_route) (void)hipHostFree(s.h_route);
+      if (s.ev) (void)hipEventDestroy(s.ev);
+      if (s.d_ctl) (void)hipFree(s.d_ctl);
+      if (s.h_flag) (void)hipHostFree(s.h_flag);
+      if (s.h_done) (void)hipHostFree(const_cast<unsigned long long*>(s.h_done));
     }
-    for (auto e : flip_ev) if (e) hipEventDestroy(e);
-    for (auto st : streams) if (st) hipStreamDestroy(st);
+    for (auto e : flip_ev) if (e) (void)hipEventDestroy(e);
+    for (auto st : streams) if (st) (void)hipStreamDestroy(st);
   }
 
   int set_log(int p, const float* feats, const uint64_t* ids, const uint32_t* cust, int64_t n, int64_t cursor) {

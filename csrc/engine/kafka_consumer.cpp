@@ -436,7 +436,7 @@ class Consumer {
     return true;
   }
 
-  const int row_bytes() const {
+  int row_bytes() const {
     return wire == 2 ? CCFD_G32_ROW_BYTES : wire ? CCFD_WIRE_ROW_BYTES : CCFD_N_FEATURES * 4;
   }
 

@@ -27,35 +27,44 @@ extern "C" double ccfd_bw_probe(const void* src, size_t bytes, int mode, int ite
   // mode 0: hipMemcpyAsync H2D (src pinned host) into dev_scratch (>= bytes)
   // mode 1: zero-copy kernel read of host-mapped src
   // mode 2: kernel read of device memory src
+  // returns GB/s, or < 0 on a bad argument (-1), pointer (-2), timing (-3) or HIP error (-4)
+  if (!src || !dev_scratch || bytes < 16 || iters < 1 || mode < 0 || mode > 2) return -1.0;
+  bool ok = true;
+  auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
   hipStream_t s;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1.0;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -4.0;
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  chk(hipEventCreate(&e0));
+  chk(hipEventCreate(&e1));
   const float4* p = static_cast<const float4*>(src);
   if (mode == 1) {
     void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, const_cast<void*>(src), 0) != hipSuccess) return -2.0;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(src), 0) != hipSuccess) ok = false;
     p = static_cast<const float4*>(d);
   }
   const size_t n4 = bytes / 16;
   auto once = [&]() {
-    if (mode == 0)
-      hipMemcpyAsync(dev_scratch, src, bytes, hipMemcpyHostToDevice, s);
-    else
+    if (mode == 0) {
+      chk(hipMemcpyAsync(dev_scratch, src, bytes, hipMemcpyHostToDevice, s));
+    } else {
       hipLaunchKernelGGL(read_sum_kernel, dim3(2048), dim3(256), 0, s, p, n4, static_cast<float*>(dev_scratch));
+      chk(hipGetLastError());
+    }
   };
-  once();
-  hipStreamSynchronize(s);
-  hipEventRecord(e0, s);
-  for (int i = 0; i < iters; ++i) once();
-  hipEventRecord(e1, s);
-  hipEventSynchronize(e1);
   float ms = 0.f;
-  hipEventElapsedTime(&ms, e0, e1);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipStreamDestroy(s);
+  if (ok) {
+    once();
+    chk(hipStreamSynchronize(s));
+    chk(hipEventRecord(e0, s));
+    for (int i = 0; i < iters && ok; ++i) once();
+    chk(hipEventRecord(e1, s));
+    chk(hipEventSynchronize(e1));
+    chk(hipEventElapsedTime(&ms, e0, e1));
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
+  if (!ok) return -4.0;
   return ms > 0 ? (double)bytes * iters / (ms * 1e-3) / 1e9 : -3.0;
 }
 
@@ -66,32 +75,39 @@ extern "C" double ccfd_bw_probe(const void* src, size_t bytes, int mode, int ite
 // roofline survives at micro-batch granularity.
 extern "C" double ccfd_bw_probe_chunked(const void* src_host, size_t bytes, size_t chunk, int grid, int block,
                                         int nstreams, int iters, void* dev_scratch) {
-  if (nstreams < 1 || nstreams > 16 || chunk < 16 || grid < 1 || block < 64 || block > 256) return -1.0;
+  if (nstreams < 1 || nstreams > 16 || chunk < 16 || grid < 1 || block < 64 || block > 256 || iters < 1 ||
+      bytes < chunk)
+    return -1.0;
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, const_cast<void*>(src_host), 0) != hipSuccess) return -2.0;
+  bool ok = true;
+  auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
   const char* base = static_cast<const char*>(d);
-  hipStream_t ss[16];
-  for (int i = 0; i < nstreams; ++i) hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking);
+  hipStream_t ss[16] = {};
+  for (int i = 0; i < nstreams; ++i) chk(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
   const size_t nchunks = bytes / chunk;
   auto pass = [&]() {
-    for (size_t c = 0; c < nchunks; ++c)
+    for (size_t c = 0; c < nchunks && ok; ++c) {
       hipLaunchKernelGGL(read_sum_kernel, dim3(grid), dim3(block), 0, ss[c % nstreams],
                          reinterpret_cast<const float4*>(base + c * chunk), chunk / 16,
                          static_cast<float*>(dev_scratch));
+      chk(hipGetLastError());
+    }
   };
-  pass();
-  for (int i = 0; i < nstreams; ++i) hipStreamSynchronize(ss[i]);
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  // time on the host: several streams run concurrently, so bracket all of them
-  auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < iters; ++i) pass();
-  for (int i = 0; i < nstreams; ++i) hipStreamSynchronize(ss[i]);
-  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  for (int i = 0; i < nstreams; ++i) hipStreamDestroy(ss[i]);
+  auto sync = [&]() { for (int i = 0; i < nstreams; ++i) chk(hipStreamSynchronize(ss[i])); };
+  double sec = 0.0;
+  if (ok) {
+    pass();
+    sync();
+    // time on the host: several streams run concurrently, so bracket all of them
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters && ok; ++i) pass();
+    sync();
+    sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  for (int i = 0; i < nstreams; ++i)
+    if (ss[i]) (void)hipStreamDestroy(ss[i]);
+  if (!ok) return -4.0;
   return sec > 0 ? (double)(nchunks * chunk) * iters / sec / 1e9 : -3.0;
 }
 
@@ -105,37 +121,46 @@ extern "C" double ccfd_bw_probe_mix(const void* src_host, size_t bytes, int n_sd
   if (n_sdma == 0 && zc_frac < 1.0) return -1.0;
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, const_cast<void*>(src_host), 0) != hipSuccess) return -2.0;
+  bool ok = true;
+  auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
   const size_t zc = ((size_t)(zc_frac * (double)bytes)) & ~(size_t)4095;
   const size_t rest = bytes - zc;
-  hipStream_t ks, ss[8];
-  hipStreamCreateWithFlags(&ks, hipStreamNonBlocking);
-  for (int i = 0; i < n_sdma; ++i) hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking);
+  hipStream_t ks = nullptr, ss[8] = {};
+  chk(hipStreamCreateWithFlags(&ks, hipStreamNonBlocking));
+  for (int i = 0; i < n_sdma; ++i) chk(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
   const char* hsrc = static_cast<const char*>(src_host);
   char* dst = static_cast<char*>(dev_scratch);
   auto pass = [&]() {
-    if (zc)
+    if (zc) {
       hipLaunchKernelGGL(read_sum_kernel, dim3(2048), dim3(256), 0, ks, reinterpret_cast<const float4*>(d), zc / 16,
                          reinterpret_cast<float*>(dst));
+      chk(hipGetLastError());
+    }
     if (n_sdma > 0 && rest) {
       const size_t slice = (rest / n_sdma) & ~(size_t)4095;
       for (int i = 0; i < n_sdma; ++i) {
         const size_t off = zc + (size_t)i * slice;
         const size_t len = i + 1 == n_sdma ? bytes - off : slice;
-        hipMemcpyAsync(dst + off, hsrc + off, len, hipMemcpyHostToDevice, ss[i]);
+        chk(hipMemcpyAsync(dst + off, hsrc + off, len, hipMemcpyHostToDevice, ss[i]));
       }
     }
   };
   auto sync = [&]() {
-    hipStreamSynchronize(ks);
-    for (int i = 0; i < n_sdma; ++i) hipStreamSynchronize(ss[i]);
+    chk(hipStreamSynchronize(ks));
+    for (int i = 0; i < n_sdma; ++i) chk(hipStreamSynchronize(ss[i]));
   };
-  pass();
-  sync();
-  const auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < iters; ++i) pass();
-  sync();
-  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  hipStreamDestroy(ks);
-  for (int i = 0; i < n_sdma; ++i) hipStreamDestroy(ss[i]);
+  double s = 0.0;
+  if (ok) {
+    pass();
+    sync();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters && ok; ++i) pass();
+    sync();
+    s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  if (ks) (void)hipStreamDestroy(ks);
+  for (int i = 0; i < n_sdma; ++i)
+    if (ss[i]) (void)hipStreamDestroy(ss[i]);
+  if (!ok) return -4.0;
   return s > 0 ? (double)bytes * iters / s / 1e9 : -3.0;
 }

@@ -11,8 +11,6 @@
 
 namespace ccfd {
 
-constexpr int kLrBlob = 64 + 3 * 32 * 4;   // models/lr.py BLOB_BYTES
-
 int mlp_waves_for(int ntiles);     // score_mlp.hip (same policy and CCFD_MLP_WAVES override)
 int mlp_tiles_per_wave_policy();   // score_mlp.hip (CCFD_MLP_TPW)
 
