@@ -279,6 +279,7 @@ def main(argv=None):
         model = build_model(args.model, seed=args.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE,
                             threshold=args.threshold, gbdt_trees=args.gbdt_trees, gbdt_depth=args.gbdt_depth)
     dm = broadcast_model(ctx, model, args.model, args.wire)     # X1 (+ the G32 bin table)
+    args.wire = dm.row_format          # G32 falls back to f32 rows for unbinnable ensembles
     bins = dm.bins
     exec_mode = args.exec_mode
     if exec_mode == "auto":

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import warnings
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -130,27 +131,41 @@ def broadcast_model(ctx: DistContext, model, kind: str, row_format: str, group=N
     """X1 for a whole device model: rank 0 packs ``model`` for ``row_format`` (f32 / w64 /
     g32) and broadcasts the blob -- plus, for G32, the bin table every rank encodes its
     partition logs with, and the tree shape; every rank returns an equal DeviceModel.
-    ``model`` is only read on rank 0."""
+    ``model`` is only read on rank 0.
+
+    G32 needs at most 255 distinct split thresholds per feature (u8 bins).  An ensemble with
+    more (e.g. a large import) falls back to f32 rows on every rank: rank 0 decides and the
+    decision travels in the header broadcast ahead of the blob, so all ranks agree.  Callers
+    take the row format from the returned model (``DeviceModel.row_format``)."""
     from ..models.gbdt import BinSpec
     from ..ops.kernels import DeviceModel
+    codes = {"f32": 0, "w64": 1, "g32": 2}
     blob = spec_t = None
-    shape = torch.zeros(2, dtype=torch.int64, device=ctx.device)
+    header = torch.zeros(3, dtype=torch.int64, device=ctx.device)      # trees, depth, row format
     if ctx.rank == 0:
-        if row_format == "g32":
-            spec = model.bin_spec()
+        fmt = row_format
+        if fmt == "g32":
+            try:
+                spec = model.bin_spec()
+            except ValueError as e:                 # > 255 thresholds on a feature
+                warnings.warn(f"G32 rows impossible for this ensemble ({e}); scoring f32 rows")
+                fmt = "f32"
+        if fmt == "g32":
             packed = model.pack(bins=spec)
             spec_t = torch.from_numpy(np.frombuffer(spec.to_bytes(), np.uint8).copy()).to(ctx.device)
         else:
-            packed = model.pack(wire=True) if row_format == "w64" else model.pack()
+            packed = model.pack(wire=True) if fmt == "w64" else model.pack()
         blob = torch.from_numpy(np.frombuffer(packed, np.uint8).copy()).to(ctx.device)
-        shape[0], shape[1] = getattr(model, "n_trees", 0), getattr(model, "depth", 0)
-    blob = broadcast_blob(ctx, blob, group=group)
+        header[0], header[1] = getattr(model, "n_trees", 0), getattr(model, "depth", 0)
+        header[2] = codes[fmt]
     if ctx.initialized:
-        dist.broadcast(shape, 0, group=group)
+        dist.broadcast(header, 0, group=group)
+    fmt = {v: k for k, v in codes.items()}[int(header[2])]
+    blob = broadcast_blob(ctx, blob, group=group)
     bins = None
-    if row_format == "g32":
+    if fmt == "g32":
         bins = BinSpec.from_bytes(broadcast_blob(ctx, spec_t, group=group).cpu().numpy().tobytes())
-    return DeviceModel.from_blob(kind, blob, int(shape[0]), int(shape[1]), wire=row_format == "w64", bins=bins)
+    return DeviceModel.from_blob(kind, blob, int(header[0]), int(header[1]), wire=fmt == "w64", bins=bins)
 
 
 def _checksum(blob: torch.Tensor) -> torch.Tensor:

@@ -427,8 +427,13 @@ class Engine {
     // resident workgroups (+ the doorbell): 128 for GBDT G32 (1.68e9 tx/s vs 1.62e9 at 256 and
     // 1.34e9 at 768, profiles/r2/gbdt_g32_persist_sweep.jsonl) and f32 rows; 64 for W64 rows
     // (their 512-row items keep 32 KB per workgroup in flight)
+    // G32 ensembles well beyond BASELINE's 100 x 6 are VALU-bound, not PCIe-bound: one
+    // workgroup per CU (700 x 6: 7.3e8 tx/s at 256 vs 3.8e8 at 128,
+    // profiles/r2/g32_large_ensembles/)
+    const bool big_trees = (wire_flag & CCFD_ARG_WIRE_G32) && cfg.gbdt_trees * cfg.gbdt_depth > 1200;
     const int grid = cfg.persist_grid > 0 ? cfg.persist_grid
-                     : (wire_flag & CCFD_ARG_WIRE_W64) ? CCFD_PERSIST_GRID_W64 : CCFD_PERSIST_GRID;
+                     : (wire_flag & CCFD_ARG_WIRE_W64) ? CCFD_PERSIST_GRID_W64
+                     : big_trees ? 2 * CCFD_PERSIST_GRID : CCFD_PERSIST_GRID;
     int rc = ccfd_persist_launch(&a, grid, pstream);
     if (rc) { set_error("persistent kernel launch failed"); return rc; }
     prunning = true;

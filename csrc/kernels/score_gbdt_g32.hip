@@ -29,7 +29,7 @@ namespace ccfd {
 
 constexpr int kG32Rows = 64;        // rows per wave chunk (one per lane)
 constexpr int kG32Waves = 4;
-constexpr int kG32LeafLds = 16384;  // floats: leaf tables must fit in 64 KB of LDS
+constexpr int kG32LeafLds = 16384;  // floats: leaf tables up to 64 KB are staged in LDS, larger ones read from L2
 #ifndef CCFD_G32_TREE_BLOCK
 #define CCFD_G32_TREE_BLOCK 4
 #endif
@@ -133,7 +133,15 @@ __device__ __forceinline__ void g32_stage_leaves(const char* blob, int T, float*
   for (int i = (nl & ~3) + tid; i < nl; i += nthreads) lv[i] = src[i];
 }
 
-template <int D, int R, bool kR>
+// Leaf tables of T * 2^D floats up to kG32LeafLds are staged in LDS; larger ensembles
+// (kGL: e.g. CatBoost's default 1000 x depth 6 = 250 KB) gather their leaves straight from
+// the blob in global memory -- read-only and L2-resident, one gather per tree and row chain.
+__device__ __forceinline__ const float* g32_leaves_global(const char* blob, int T, int D) {
+  const int tdw = ((4 * T * D + 15) & ~15) / 4;
+  return reinterpret_cast<const float*>(blob + kHeader + 8 * tdw);
+}
+
+template <int D, int R, bool kR, bool kGL>
 __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) {
   extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L floats
   __shared__ uint4 xt[kG32Waves][128];                         // per-wave chunk transpose
@@ -165,8 +173,10 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
   // s_load into SGPRs (the model blob is immutable for the kernel's lifetime)
   const g32_cint_p feat = (g32_cint_p)(blob + kHeader);
   const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
-  g32_stage_leaves<D>(blob, T, lv, tid, 256);
-  __syncthreads();                                              // leaves staged
+  const float* leaves = lv;
+  if constexpr (kGL) leaves = g32_leaves_global(blob, T, D);
+  else g32_stage_leaves<D>(blob, T, lv, tid, 256);
+  __syncthreads();                                              // leaves staged, epi initialised
 
   const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
   unsigned fraud = 0, rows = 0, stale = 0;
@@ -190,7 +200,7 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
       for (int q = 0; q < R; ++q) g32_fetch(xb, n, nxt * R + q, lane, pre[q]);
     }
     float acc[R];
-    g32_trees<D, R>(b0, b1, lv, feat, kbin, T, acc);
+    g32_trees<D, R>(b0, b1, leaves, feat, kbin, T, acc);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int row = (grp * R + q) * kG32Rows + lane;
@@ -232,7 +242,7 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
 // in every workgroup), and a claimed item is 4 waves x `cpw` 64-row chunks, the next chunk
 // of a wave in flight while the current one is evaluated.
 // ---------------------------------------------------------------------------------------
-template <int D, bool kR>
+template <int D, bool kR, bool kGL>
 __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args a) {
   extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L floats
   __shared__ uint4 xt[kG32Waves][128];
@@ -257,7 +267,9 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   const int tdw = ((4 * T * D + 15) & ~15) / 4;
   const g32_cint_p feat = (g32_cint_p)(blob + kHeader);
   const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
-  g32_stage_leaves<D>(blob, T, lv, tid, 256);
+  const float* leaves = lv;
+  if constexpr (kGL) leaves = g32_leaves_global(blob, T, D);
+  else g32_stage_leaves<D>(blob, T, lv, tid, 256);
   epi_init(epi);
   __syncthreads();
   unsigned long long posted_cache = 0;                    // thread 0 only
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       unsigned b0[kF];
       const unsigned meta = g32_lift(cur, b0);
       float acc[1];
-      g32_trees<D, 1>(b0, b0, lv, feat, kbin, T, acc);
+      g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
       const int row = chunk * kG32Rows + lane;
       const bool valid = row < n;
       const bool fresh = ((meta >> 8) & 0xffu) == stamp;
@@ -356,15 +368,20 @@ static int launch_persist_g32_d(const ccfd_persist_args& a0, int grid, hipStream
   // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
   const char* e = getenv("CCFD_G32_INFLIGHT");
   if (!e || atoi(e) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
-  const size_t lds = (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
-  if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true>), dim3(grid), dim3(256), lds, s, a);
-  else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false>), dim3(grid), dim3(256), lds, s, a);
+  const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds;       // leaves gathered from global
+  const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
+  if (gl) {
+    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, true>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, true>), dim3(grid), dim3(256), 0, s, a);
+  } else {
+    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, false>), dim3(grid), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, false>), dim3(grid), dim3(256), lds, s, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s) {
   if (a.gbdt_trees <= 0 || a.gbdt_depth < 1 || a.gbdt_depth > 8) return -2;
-  if (((long)a.gbdt_trees << a.gbdt_depth) > kG32LeafLds) return -2;
   switch (a.gbdt_depth) {
     case 1: return launch_persist_g32_d<1>(a, grid, s);
     case 2: return launch_persist_g32_d<2>(a, grid, s);
@@ -396,9 +413,15 @@ static void launch_g32_r(const ccfd_score_args& a, hipStream_t s) {
   int grid = (ngroups + kG32Waves - 1) / kG32Waves;
   const int cap = 256 * wgs_per_cu;
   grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
-  const size_t lds = (size_t)a.gbdt_trees * L * sizeof(float);
-  if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true>), dim3(grid), dim3(256), lds, s, a);
-  else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false>), dim3(grid), dim3(256), lds, s, a);
+  const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds;       // leaves gathered from global
+  const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * L * sizeof(float);
+  if (gl) {
+    if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, true>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false, true>), dim3(grid), dim3(256), 0, s, a);
+  } else {
+    if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, false>), dim3(grid), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false, false>), dim3(grid), dim3(256), lds, s, a);
+  }
 }
 
 template <int D>
@@ -410,7 +433,6 @@ static void launch_g32_d(const ccfd_score_args& a, hipStream_t s) {
 
 int launch_gbdt_g32(const ccfd_score_args& a, hipStream_t s) {
   if (a.gbdt_trees <= 0 || a.gbdt_depth < 1 || a.gbdt_depth > 8) return -2;
-  if (((long)a.gbdt_trees << a.gbdt_depth) > kG32LeafLds) return -2;   // leaf tables must fit in LDS
   if (a.n <= 0) return 0;
   switch (a.gbdt_depth) {
     case 1: launch_g32_d<1>(a, s); break;

@@ -225,3 +225,56 @@ def test_g32_persistent_item_modes_exact(gpu, monkeypatch, inflight, item_rows):
     assert int(c[8:22].sum() + c[24:38].sum()) == n
     eng.close()
     log.free()
+
+
+@pytest.mark.parametrize("trees,depth", [(700, 6), (120, 8)])
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+def test_g32_large_ensembles_gather_leaves_from_global(gpu, trees, depth, exec_mode):
+    """Ensembles whose leaf tables exceed the 64 KB LDS stage (700 x 64 and 120 x 256 leaves)
+    gather their leaves from the blob in global memory instead of being refused: routes equal
+    the f32 oracle's, probabilities within float summation order, on launch and persistent."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    B = 8192
+    X, _ = generate(B * 3 + 500, seed=46)
+    m = build_model("gbdt", seed=11, X_ref=X[:20000], calibrate_rate=0.02, gbdt_trees=trees, gbdt_depth=depth)
+    assert m.n_trees * (1 << m.depth) > 16384
+    dm = DeviceModel(m, gpu, bins=True)
+    eng = StreamEngine(dm, batch=B, depth=3, streams=1, exec_mode=exec_mode)
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 7, bins=dm.bins)
+    eng.add_log(0, log)
+    n = 2 * B + 1234
+    assert eng.pump(2).rows + eng.pump(1, batch_rows=1234).rows == n
+    pr = m.predict_proba(X[:n])
+    fl = eng.drain_flagged()
+    got = np.zeros(n, bool)
+    got[(fl["tx_id"] - 7).astype(np.int64)] = True
+    np.testing.assert_array_equal(got, pr >= 0.5)
+    p, r = eng.score(X[:3000])
+    assert np.abs(p - m.predict_proba(X[:3000])).max() < 2e-5
+    eng.close()
+    log.free()
+
+
+def test_unbinnable_ensemble_falls_back_to_f32_rows(gpu):
+    """> 255 distinct thresholds on a feature: G32 is impossible, and broadcast_model hands
+    every rank an f32-row model (the decision travels in the X1 header) that scores exactly."""
+    from ccfd_demo_summit_amd.engine import StreamEngine
+    from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT
+    from ccfd_demo_summit_amd.parallel import broadcast_model, init_distributed
+    X, _ = generate(30000, seed=47)
+    T = 300
+    feat = np.zeros((T, 2), np.int32)                 # every split on feature 0: 600 thresholds
+    thr = np.quantile(X[:, 0], np.linspace(0.01, 0.99, 2 * T)).astype(np.float32).reshape(T, 2)
+    rng = np.random.default_rng(3)
+    m = ObliviousGBDT(feat, thr, (rng.standard_normal((T, 4)) * 0.05).astype(np.float32), -1.0)
+    with pytest.raises(ValueError):
+        m.bin_spec()
+    ctx = init_distributed()
+    with pytest.warns(UserWarning, match="G32 rows impossible"):
+        dm = broadcast_model(ctx, m, "gbdt", "g32")
+    assert dm.row_format == "f32" and dm.bins is None
+    eng = StreamEngine(dm, batch=4096, depth=2)
+    p, _ = eng.score(X[:5000])
+    assert np.abs(p - m.predict_proba(X[:5000])).max() < 2e-5
+    eng.close()
