@@ -155,3 +155,57 @@ def test_catboost_import_refuses_what_the_kernels_cannot_run():
         from_catboost_json(doc)
     with pytest.raises(ValueError, match="oblivious"):
         from_catboost_json({"trees": []})
+
+
+def _sk_data(n=6000, seed=8):
+    from ccfd_demo_summit_amd.data import generate
+    X, y = generate(n, seed=seed, fraud_rate=0.05)
+    return X.astype(np.float64), y
+
+
+def test_sklearn_logistic_regression_import_matches_predict_proba():
+    """models/sklearn_import.py: a fitted LogisticRegression (bare and behind a StandardScaler)
+    scores like sklearn's own predict_proba[:, 1]."""
+    from sklearn.linear_model import LogisticRegression
+    from sklearn.pipeline import make_pipeline
+    from sklearn.preprocessing import StandardScaler
+    from ccfd_demo_summit_amd.models.sklearn_import import from_sklearn
+    X, y = _sk_data()
+    for est in (make_pipeline(StandardScaler(), LogisticRegression(max_iter=300)),
+                LogisticRegression(max_iter=2000, C=0.1)):
+        est.fit(X, y)
+        m = from_sklearn(est)
+        assert m.kind == "lr"
+        np.testing.assert_allclose(m.predict_proba(X[:2000]), est.predict_proba(X[:2000])[:, 1], atol=2e-6)
+
+
+def test_sklearn_mlp_import_matches_predict_proba_and_refuses_other_shapes():
+    import warnings
+    from sklearn.exceptions import ConvergenceWarning
+    from sklearn.neural_network import MLPClassifier
+    from sklearn.pipeline import Pipeline
+    from sklearn.preprocessing import MinMaxScaler, StandardScaler
+    from ccfd_demo_summit_amd.models import load_model, save_model
+    from ccfd_demo_summit_amd.models.sklearn_import import from_sklearn
+    X, y = _sk_data()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", ConvergenceWarning)
+        pipe = Pipeline([("scale", StandardScaler()),
+                         ("mlp", MLPClassifier(hidden_layer_sizes=(128, 64), max_iter=15, random_state=0))]).fit(X, y)
+        small = MLPClassifier(hidden_layer_sizes=(32,), max_iter=5, random_state=0).fit(X, y)
+        tanh = MLPClassifier(hidden_layer_sizes=(128, 64), activation="tanh", max_iter=3, random_state=0).fit(X, y)
+    m = from_sklearn(pipe)
+    assert m.kind == "mlp"
+    np.testing.assert_allclose(m.predict_proba(X[:2000]), pipe.predict_proba(X[:2000])[:, 1], atol=2e-5)
+    import os
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        save_model(m, os.path.join(d, "m.safetensors"))
+        back = load_model(os.path.join(d, "m.safetensors"))
+    np.testing.assert_allclose(back.predict_proba(X[:500]), m.predict_proba(X[:500]), atol=1e-7)
+    with pytest.raises(ValueError, match="30 -> 128 -> 64 -> 1"):
+        from_sklearn(small)
+    with pytest.raises(ValueError, match="relu"):
+        from_sklearn(tanh)
+    with pytest.raises(ValueError, match="StandardScaler"):
+        from_sklearn(Pipeline([("s", MinMaxScaler()), ("mlp", pipe.steps[-1][1])]))
