@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--host", action="store_true",
                     help="rows in pinned host memory read zero-copy over PCIe (the streaming input path) "
                          "instead of HBM: one launch per size, no engine")
+    ap.add_argument("--gbdt-trees", type=int, default=100)
+    ap.add_argument("--gbdt-depth", type=int, default=6)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import torch
@@ -87,7 +89,8 @@ def main():
         xw = torch.from_numpy(encode_wire(X)).to(dev).repeat(reps, 1)[:nmax].contiguous()
     results = []
     for kind, wire in cases:
-        m = build_model(kind, seed=0, X_ref=X[:100_000], calibrate_rate=0.01)
+        m = build_model(kind, seed=0, X_ref=X[:100_000], calibrate_rate=0.01, gbdt_trees=args.gbdt_trees,
+                        gbdt_depth=args.gbdt_depth)
         dm = DeviceModel(m, dev, wire=(wire == "w64"), bins=True if wire == "g32" else None)
         if wire == "g32":
             xg = torch.from_numpy(dm.bins.encode(X)).to(dev).repeat(reps, 1)[:nmax].contiguous()

@@ -368,7 +368,8 @@ static int launch_persist_g32_d(const ccfd_persist_args& a0, int grid, hipStream
   // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
   const char* e = getenv("CCFD_G32_INFLIGHT");
   if (!e || atoi(e) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
-  const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds;       // leaves gathered from global
+  const char* eg = getenv("CCFD_G32_GLOBAL_LEAVES");              // A/B knob: force the L2 path
+  const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || (eg && atoi(eg) == 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
   if (gl) {
     if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, true>), dim3(grid), dim3(256), 0, s, a);
@@ -413,7 +414,10 @@ static void launch_g32_r(const ccfd_score_args& a, hipStream_t s) {
   int grid = (ngroups + kG32Waves - 1) / kG32Waves;
   const int cap = 256 * wgs_per_cu;
   grid = grid < 1 ? 1 : (grid > cap ? cap : grid);
-  const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds;       // leaves gathered from global
+  // a launch re-stages the leaves in every workgroup: past 32 KB of leaves the L2 gather wins
+  // (250 x 6 at 1 M rows: 5.3 vs 4.0 G rows/s; 100 x 6: LDS 14.2 vs 13.1 at 16 M rows,
+  // profiles/r2/g32_large_ensembles/lds_vs_global_*.jsonl)
+  const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds / 2 || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * L * sizeof(float);
   if (gl) {
     if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, true>), dim3(grid), dim3(256), 0, s, a);
