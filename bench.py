@@ -252,7 +252,9 @@ def main(argv=None):
     if args.batch is None:
         args.batch = 65536 if args.model == "gbdt" else 4096
     if args.depth is None:
-        args.depth = 3 if args.model == "gbdt" else 12
+        # gbdt: 3 micro-batches saturate PCIe for BASELINE's 100 x 6; ensembles past 1200 tree
+        # levels a row are VALU-bound and need 6 in flight (profiles/r2/g32_large_ensembles/)
+        args.depth = (6 if args.gbdt_trees * args.gbdt_depth > 1200 else 3) if args.model == "gbdt" else 12
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine

@@ -358,7 +358,11 @@ class Engine {
     // 256-row items on 128 workgroups at depth 16; LR 256-row items (8.47e8 at 56 us; 512:
     // 7.3e8) -- profiles/r2/persist_full_item/
     const bool w64 = (wire_flag & CCFD_ARG_WIRE_W64) != 0;
-    int item_rows = (g32 || (w64 && cfg.model == CCFD_MODEL_MLP)) ? 512 : CCFD_PERSIST_ITEM_ROWS;
+    // G32 ensembles far beyond BASELINE's 100 x 6 (> 1200 tree levels a row) are VALU-bound:
+    // 256-row items on 512 workgroups spread them over more waves (700 x 6 at depth 6:
+    // 1.01e9 tx/s vs 7.3e8 with 512-row items on 256, profiles/r2/g32_large_ensembles/)
+    const bool big_trees = g32 && cfg.gbdt_trees * cfg.gbdt_depth > 1200;
+    int item_rows = big_trees ? 256 : (g32 || (w64 && cfg.model == CCFD_MODEL_MLP)) ? 512 : CCFD_PERSIST_ITEM_ROWS;
     if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) {
       const int v = std::atoi(e);
       if (v == 256 || v == 512 || v == 1024 || (!g32 && (v == 64 || v == 128))) item_rows = v;
@@ -427,13 +431,13 @@ class Engine {
     // resident workgroups (+ the doorbell): 128 for GBDT G32 (1.68e9 tx/s vs 1.62e9 at 256 and
     // 1.34e9 at 768, profiles/r2/gbdt_g32_persist_sweep.jsonl) and f32 rows; 64 for W64 rows
     // (their 512-row items keep 32 KB per workgroup in flight)
-    // G32 ensembles well beyond BASELINE's 100 x 6 are VALU-bound, not PCIe-bound: one
-    // workgroup per CU (700 x 6: 7.3e8 tx/s at 256 vs 3.8e8 at 128,
-    // profiles/r2/g32_large_ensembles/)
+    // G32 ensembles well beyond BASELINE's 100 x 6 are VALU-bound, not PCIe-bound: two
+    // workgroups per CU (see persist_init; 700 x 6: 3.8e8 tx/s at 128, 7.3e8 at 256 and
+    // 1.01e9 at 512 with 256-row items, profiles/r2/g32_large_ensembles/)
     const bool big_trees = (wire_flag & CCFD_ARG_WIRE_G32) && cfg.gbdt_trees * cfg.gbdt_depth > 1200;
     const int grid = cfg.persist_grid > 0 ? cfg.persist_grid
                      : (wire_flag & CCFD_ARG_WIRE_W64) ? CCFD_PERSIST_GRID_W64
-                     : big_trees ? 2 * CCFD_PERSIST_GRID : CCFD_PERSIST_GRID;
+                     : big_trees ? 4 * CCFD_PERSIST_GRID : CCFD_PERSIST_GRID;
     int rc = ccfd_persist_launch(&a, grid, pstream);
     if (rc) { set_error("persistent kernel launch failed"); return rc; }
     prunning = true;
