@@ -256,7 +256,9 @@ def cmd_engine(a, cfg):
         ingest_threads=cfg.engine.ingest_threads,
         model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
-    _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.rank)
+    # node-local port: every node's (pod's) local rank 0 serves the base port its probes and
+    # scrape annotation name, whatever its global rank in a multi-node job
+    _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.local_rank)
     resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic]) if ctx.rank == 0 else None
     # the router also watches the notification topic KIE publishes to (router.yaml:57-58)
     notif = (broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])

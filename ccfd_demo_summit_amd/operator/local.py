@@ -72,8 +72,9 @@ def probe_ok(target: tuple, timeout_s: float = 0.5) -> bool:
 
 
 def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offset: int = 0) -> Dict[str, tuple]:
-    """service -> (desired replicas, argv factory(replica index), env, probe) for a one-node
-    run; every port is the service's reference port + ``port_offset`` (+ replica index).
+    """service -> (desired replicas, argv factory(replica index), env (a dict, or a factory of
+    the replica index), probe) for a one-node run; every port is the service's reference
+    port + ``port_offset`` (+ replica index).
     ``probe`` is (target factory(replica index), start seconds) -- the same health routes the
     rendered readiness / liveness probes use (render.py) -- or None."""
     o = port_offset
@@ -104,10 +105,15 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
         svc["notifier"] = (spec.notifier.replicas, lambda r: PY + ["notifier", "--host", host,
                                                                    "--port", str(8080 + o + r)])
     if spec.engine.deploy:
-        svc["engine"] = (spec.engine.nodes, lambda r: [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
-                                                       "--nproc-per-node", str(spec.engine.gpus_per_node),
-                                                       "--master-addr", "127.0.0.1", "--master-port", str(29500 + o + r)]
-                         + ["-m", "ccfd_demo_summit_amd.launch", "engine", "--host", host,
+        g, nodes = spec.engine.gpus_per_node, spec.engine.nodes
+        # engine.nodes > 1 on one host: replica r plays node r of ONE job (c10d rendezvous on
+        # 127.0.0.1) and sees GPUs [r*g, (r+1)*g) -- the same world the cluster rendering builds
+        dist_args = (["--nnodes", "1", "--master-addr", "127.0.0.1", "--master-port", str(29500 + o)]
+                     if nodes == 1 else
+                     ["--nnodes", str(nodes), "--rdzv-backend", "c10d", "--rdzv-id", f"ccfd-engine-{o}",
+                      "--rdzv-endpoint", f"127.0.0.1:{29500 + o}"])
+        svc["engine"] = (nodes, lambda r: [sys.executable, "-m", "torch.distributed.run"] + dist_args
+                         + ["--nproc-per-node", str(g), "-m", "ccfd_demo_summit_amd.launch", "engine", "--host", host,
                             "--port", str(8091 + o + 16 * r)] + w)
     if spec.router.deploy:
         svc["router"] = (spec.router.replicas, lambda r: PY + ["router", "--group-membership", "--host", host,
@@ -118,6 +124,9 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     own = {k: dict(env) for k in svc}
     if "kie" in own:               # the KIE pod's prediction service targets the user-task model
         own["kie"].update(SELDON_URL=f"http://{host}:{5000 + o}", SELDON_ENDPOINT="predict")
+    if "engine" in own and spec.engine.nodes > 1:
+        base, g = own["engine"], spec.engine.gpus_per_node
+        own["engine"] = lambda r: dict(base, HIP_VISIBLE_DEVICES=",".join(str(r * g + i) for i in range(g)))
 
     def http(port, path, stride=1):
         return lambda r: ("http", f"http://{host}:{port + o + stride * r}{path}")
@@ -155,12 +164,16 @@ class LocalOperator:
         if self._commands_override is None:
             self._commands = local_commands(spec, port_offset=self.port_offset)
 
+    def _env(self, name: str, r: int) -> Dict[str, str]:
+        env = self._commands[name][2]
+        return env(r) if callable(env) else env           # per-replica env (e.g. its GPUs)
+
     def _template(self, name: str, r: int) -> str:
-        _, argv_of, env = self._commands[name][:3]
-        return json.dumps([list(argv_of(r)), sorted((str(k), str(v)) for k, v in env.items())])
+        argv_of = self._commands[name][1]
+        return json.dumps([list(argv_of(r)), sorted((str(k), str(v)) for k, v in self._env(name, r).items())])
 
     def _start(self, name: str, r: int) -> Replica:
-        _, argv_of, env = self._commands[name][:3]
+        argv_of, env = self._commands[name][1], self._env(name, r)
         e = dict(os.environ)
         e.update({str(k): str(v) for k, v in env.items()})
         root = str(Path(__file__).resolve().parents[2])             # the package, from any cwd

@@ -45,6 +45,9 @@ def _container(spec: FraudDetectionSpec, name: str, command: List[str], ports=()
     return c
 
 
+RDZV_PORT = 29400        # multi-node engine: torchrun c10d rendezvous on pod ccfd-engine-0
+
+
 def _workload(kind: str, name: str, app: str, replicas: int, containers, annotations=None, grace: int = 30,
               extra_spec=None, volumes=None) -> Dict[str, Any]:
     tmpl_meta: Dict[str, Any] = {"labels": {"app": app}}
@@ -104,12 +107,23 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
                                             for i in range(spec.kafka.brokers)]))
 
     if spec.engine.deploy:
-        g = spec.engine.gpus_per_node
-        cmd = LAUNCH + ["supervise", "--", "python", "-m", "torch.distributed.run", "--standalone",
-                        "--nproc-per-node", str(g)] + LAUNCH[1:] + ["engine"] + weights
-        out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", spec.engine.nodes, [_container(
-            spec, "engine", cmd, ports=[{"containerPort": 8091, "name": "metrics"}], gpus=g,
-            probe=("/health/ping", 8091, 120))],
+        g, nodes = spec.engine.gpus_per_node, spec.engine.nodes
+        # one data-parallel job over every engine pod: ranks own partitions p = rank (mod
+        # nodes x GPUs), so the pods must share ONE world -- torchrun's c10d rendezvous hosted
+        # by pod 0 (stable name through the headless service) assigns the ranks
+        dist_args = (["--standalone"] if nodes == 1 else
+                     ["--nnodes", str(nodes), "--rdzv-backend", "c10d", "--rdzv-id", "ccfd-engine",
+                      "--rdzv-endpoint", f"ccfd-engine-0.ccfd-engine:{RDZV_PORT}"])
+        cmd = LAUNCH + ["supervise", "--", "python", "-m", "torch.distributed.run"] + dist_args + [
+            "--nproc-per-node", str(g)] + LAUNCH[1:] + ["engine"] + weights
+        ports = [{"containerPort": 8091, "name": "metrics"}]
+        if nodes > 1:
+            ports.append({"containerPort": RDZV_PORT, "name": "rendezvous"})
+            out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "ccfd-engine"},
+                        "spec": {"clusterIP": "None", "selector": {"app": "ccfd-engine"},
+                                 "ports": [{"name": "rendezvous", "port": RDZV_PORT, "targetPort": RDZV_PORT}]}})
+        out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", nodes, [_container(
+            spec, "engine", cmd, ports=ports, gpus=g, probe=("/health/ping", 8091, 120))],
             annotations=_scrape("/prometheus", 8091)))
 
     if spec.seldon.deploy:
@@ -261,6 +275,19 @@ def validate(manifests: List[Dict[str, Any]]) -> List[str]:
                     nproc = int(cmd[cmd.index("--nproc-per-node") + 1])
                     if nproc != gpu:
                         probs.append(f"{key}: {nproc} ranks for {gpu} GPUs (one rank per GPU)")
+                    nodes = m["spec"].get("replicas", 1)
+                    if nodes > 1:
+                        # every pod must join ONE world, or each would score the same partitions
+                        nn = int(cmd[cmd.index("--nnodes") + 1]) if "--nnodes" in cmd else 1
+                        if nn != nodes or "--rdzv-endpoint" not in cmd:
+                            probs.append(f"{key}: {nodes} engine pods without a shared rendezvous "
+                                         f"(--nnodes {nn}): each pod would score the same partitions")
+                        headless = [x for x in manifests if x.get("kind") == "Service"
+                                    and x["metadata"]["name"] == m["spec"].get("serviceName")
+                                    and x["spec"].get("clusterIP") == "None"]
+                        if not headless:
+                            probs.append(f"{key}: no headless Service {m['spec'].get('serviceName')} for the pods' "
+                                         "stable names")
             m["_ports"] = ports
     for m in manifests:
         if m.get("kind") == "Service":

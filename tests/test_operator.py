@@ -93,6 +93,34 @@ def test_reference_opendatahub_cr_maps_onto_the_stack():
     assert validate(render(spec)) == []
 
 
+def test_multi_node_engine_is_one_rendezvous_job():
+    """engine.nodes > 1: the pods join ONE torchrun world (c10d rendezvous on ccfd-engine-0
+    behind a headless Service) so ranks own disjoint partitions; separate per-pod jobs -- each
+    scoring the same partitions -- are refused by validate(); the local operator gives every
+    replica its own GPUs of the same world."""
+    d = _doc()
+    d["spec"]["engine"].update(nodes=3, gpusPerNode=8)
+    ms = render(parse(d))
+    assert validate(ms) == []
+    by = {(m["kind"], m["metadata"]["name"]): m for m in ms}
+    assert by[("Service", "ccfd-engine")]["spec"]["clusterIP"] == "None"
+    sts = by[("StatefulSet", "ccfd-engine")]
+    cmd = sts["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert cmd[cmd.index("--nnodes") + 1] == "3" and "ccfd-engine-0.ccfd-engine:29400" in cmd
+    bad = copy.deepcopy(ms)
+    c = next(m for m in bad if m["kind"] == "StatefulSet" and m["metadata"]["name"] == "ccfd-engine")
+    c["spec"]["template"]["spec"]["containers"][0]["command"] = [x for x in cmd if x not in ("--nnodes", "3")]
+    bad = [m for m in bad if not (m["kind"] == "Service" and m["metadata"]["name"] == "ccfd-engine")]
+    probs = "\n".join(validate(bad))
+    assert "without a shared rendezvous" in probs and "no headless Service" in probs
+    from ccfd_demo_summit_amd.operator import local_commands
+    d["spec"]["engine"].update(gpusPerNode=2)
+    n, argv_of, env_of, _ = local_commands(parse(d), port_offset=50)["engine"]
+    assert n == 3 and [env_of(r)["HIP_VISIBLE_DEVICES"] for r in range(3)] == ["0,1", "2,3", "4,5"]
+    a0, a2 = argv_of(0), argv_of(2)
+    assert a0[a0.index("--rdzv-endpoint") + 1] == a2[a2.index("--rdzv-endpoint") + 1] == "127.0.0.1:29550"
+
+
 def test_every_long_running_container_has_health_probes():
     """Deployments / StatefulSets carry readiness + liveness probes on the service's own health
     route (engine /health/ping :8091, KIE /services/rest/server :8090, kafka tcp :9092, ...)."""
