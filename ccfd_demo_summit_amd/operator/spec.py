@@ -112,6 +112,11 @@ class FraudDetectionSpec:
             raise SpecError("kafka.brokers and kafka.partitions must be >= 1")
         if self.engine.deploy and (self.engine.nodes < 1 or not 1 <= self.engine.gpus_per_node <= 8):
             raise SpecError("engine.nodes >= 1 and 1 <= engine.gpus_per_node <= 8 (one rank per GPU of a node)")
+        ranks = self.engine.nodes * self.engine.gpus_per_node
+        if self.engine.deploy and self.kafka.deploy and self.kafka.partitions < ranks:
+            # ranks own partitions p = rank (mod world): a rank without one would sit idle
+            raise SpecError(f"kafka.partitions {self.kafka.partitions} < {ranks} engine ranks "
+                            f"(nodes x gpusPerNode): every rank needs at least one partition")
         if self.engine.model not in ("mlp", "lr", "gbdt"):
             raise SpecError(f"engine.model {self.engine.model!r}: mlp | lr | gbdt")
         from ..parallel.dp import resolve_row_format

@@ -43,6 +43,7 @@ def test_cr_fields_drive_the_rendering():
     d = _doc()
     d["spec"]["kafka"]["brokers"] = 5
     d["spec"]["engine"].update(nodes=2, gpusPerNode=4, model="gbdt")
+    d["spec"]["kafka"]["partitions"] = 16
     d["spec"]["seldon"]["replicas"] = 3
     d["spec"]["router"] = {"deploy": True, "replicas": 2}
     d["spec"]["training"] = {"deploy": True, "workers": 4, "model": "gbdt", "gpus": 1}
@@ -70,6 +71,7 @@ def test_cr_fields_drive_the_rendering():
     (lambda s: s["kafka"].update(replicas=3), "unknown field"),
     (lambda s: s["seldon"].update(replicas="two"), "integer"),
     (lambda s: s["kafka"].update(deploy=False), "bootstrap"),
+    (lambda s: s["engine"].update(nodes=3, gpusPerNode=8), "every rank needs at least one partition"),
 ])
 def test_invalid_crs_are_refused(patch, msg):
     d = _doc()
@@ -100,6 +102,7 @@ def test_multi_node_engine_is_one_rendezvous_job():
     replica its own GPUs of the same world."""
     d = _doc()
     d["spec"]["engine"].update(nodes=3, gpusPerNode=8)
+    d["spec"]["kafka"]["partitions"] = 24
     ms = render(parse(d))
     assert validate(ms) == []
     by = {(m["kind"], m["metadata"]["name"]): m for m in ms}
