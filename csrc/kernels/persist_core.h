@@ -1,5 +1,5 @@
 // Protocol of the persistent streaming kernels (engine exec_mode = 1), shared by the MLP/LR
-// kernel (score_persist.hip) and the GBDT G32 kernel (score_gbdt_g32.hip):
+// kernel (score_persist.hip) and the GBDT G32 kernel (score_gbdt_g32_persist.hip):
 //   * workgroup 0's first wave is the DOORBELL: it alone polls host memory and mirrors newly
 //     posted descriptors + the posted count into device memory;
 //   * every other workgroup claims work items with one agent-scope atomic, waits for the

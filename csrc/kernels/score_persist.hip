@@ -1,5 +1,5 @@
 // Persistent streaming scorer (engine exec_mode = 1), MLP and LR; protocol helpers in
-// persist_core.h (the GBDT G32 persistent kernel shares them, score_gbdt_g32.hip).
+// persist_core.h (the GBDT G32 persistent kernel shares them, score_gbdt_g32_persist.hip).
 //
 // One launch lives as long as the engine.  Every resident workgroup loops:
 //   claim work item i (one agent-scope atomic)      -> micro-batch b = i / C, chunk c = i % C
@@ -30,7 +30,7 @@
 
 namespace ccfd {
 
-int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s);   // score_gbdt_g32.hip
+int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s);   // score_gbdt_g32_persist.hip
 
 namespace {
 
