@@ -153,6 +153,8 @@ class Engine {
   uint64_t dev_batches = 0, dev_exec_ns = 0, dev_hist[256] = {};
   std::vector<ccfd_batch_trace> trace;     // per-batch stage trace ring (ccfd_engine_trace_enable)
   uint64_t trace_n = 0;                    // entries ever written
+  std::mutex trace_mu;                     // the ring may be read from another thread
+  std::atomic<bool> trace_on{false};       // fast check on the completion path
   double wall_ns_per_tick = 0.0;   // device wall clock (s_memrealtime) period
   unsigned long long done_counter = 0;
 
@@ -602,6 +604,24 @@ class Engine {
     return 0;
   }
 
+  void record_trace(const Slot& s, int64_t t_landed, uint64_t nf) {
+    std::lock_guard<std::mutex> lk(trace_mu);
+    if (trace.empty()) return;
+    ccfd_batch_trace& e = trace[trace_n++ % trace.size()];
+    e.seq = s.seq_no;
+    e.partition = s.part;
+    e.rows = s.rows;
+    e.t_arrival = s.t_arrival;
+    e.t_submit = s.t_submit;
+    e.t_landed = t_landed;
+    e.t_complete = now_ns();
+    const bool dev = s.use_flag && wall_ns_per_tick > 0 && s.done_ptr[3] > s.done_ptr[2];
+    e.dev_start = dev ? (int64_t)((double)s.done_ptr[2] * wall_ns_per_tick) : 0;
+    e.dev_end = dev ? (int64_t)((double)s.done_ptr[3] * wall_ns_per_tick) : 0;
+    e.flagged = (int32_t)nf;
+    e.pad = 0;
+  }
+
   int complete(Slot& s, ccfd_engine_stats* st) {
     const int64_t tw = now_ns();
     { int rc = wait_done(s); if (rc) return rc; }
@@ -638,21 +658,7 @@ class Engine {
       if (nf) push_flagged(s);
     }
     if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
-    if (!trace.empty()) {
-      ccfd_batch_trace& e = trace[trace_n++ % trace.size()];
-      e.seq = s.seq_no;
-      e.partition = s.part;
-      e.rows = s.rows;
-      e.t_arrival = s.t_arrival;
-      e.t_submit = s.t_submit;
-      e.t_landed = t_landed;
-      e.t_complete = now_ns();
-      const bool dev = s.use_flag && wall_ns_per_tick > 0 && s.done_ptr[3] > s.done_ptr[2];
-      e.dev_start = dev ? (int64_t)((double)s.done_ptr[2] * wall_ns_per_tick) : 0;
-      e.dev_end = dev ? (int64_t)((double)s.done_ptr[3] * wall_ns_per_tick) : 0;
-      e.flagged = (int32_t)nf;
-      e.pad = 0;
-    }
+    if (trace_on.load(std::memory_order_relaxed)) record_trace(s, t_landed, nf);
     Partition& P = *parts[s.part];
     if (P.ring) {
       // batches of one partition complete in submission order: release in order
@@ -1156,14 +1162,17 @@ int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_
 int ccfd_engine_trace_enable(void* eng, int32_t capacity) {
   if (!eng || capacity < 0 || capacity > (1 << 24)) return -1;
   Engine* e = static_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->trace_mu);
   e->trace.assign((size_t)capacity, ccfd_batch_trace{});
   e->trace_n = 0;
+  e->trace_on.store(capacity > 0, std::memory_order_relaxed);
   return 0;
 }
 
 int ccfd_engine_trace_read(void* eng, ccfd_batch_trace* out, int32_t max) {
   if (!eng || (!out && max > 0) || max < 0) return -1;
   Engine* e = static_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->trace_mu);
   const uint64_t cap = e->trace.size();
   if (cap == 0) return 0;
   const uint64_t have = std::min<uint64_t>(e->trace_n, cap);
