@@ -62,39 +62,49 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
   }
 }
 
+// Thread 0: read the descriptor of posted micro-batch b into `sdesc` (one acquire per item,
+// not per poll: it invalidates this XCD's L2 copies of non-coherent inputs -- a reused ring
+// slot / DMA staging buffer -- before they are read).
+__device__ __forceinline__ void persist_read_desc(const ccfd_persist_args& a, unsigned long long b,
+                                                  ccfd_persist_desc& sdesc) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
+  sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(d + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(d + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const unsigned long long ne = __hip_atomic_load(d + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  sdesc.n = (int32_t)(ne & 0xffffffffull);
+  sdesc.epoch = (int32_t)(ne >> 32);
+  sdesc.seq = b;
+}
+
+// Thread 0: wait until claimed item `item`'s micro-batch is posted, then read its descriptor;
+// returns 1 (and reads nothing) when the host stopped the kernel instead.
+__device__ __forceinline__ int persist_wait_item(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
+                                                 unsigned long long item, ccfd_persist_desc& sdesc) {
+  const unsigned long long b = item / (unsigned long long)C;
+  unsigned sleep_n = 1;
+  while (posted_cache <= b) {
+    // relaxed poll; the acquire fence in persist_read_desc runs once the batch is posted
+    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (posted_cache > b) break;
+    if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 1;
+    for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
+    sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
+  }
+  persist_read_desc(a, b, sdesc);
+  return 0;
+}
+
 // Thread 0: claim the next work item, wait for its micro-batch, read its descriptor into
 // `sdesc`.  Sets cmd = 1 when the host stopped the kernel instead.
 __device__ __forceinline__ void persist_claim(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
                                               ccfd_persist_desc& sdesc, unsigned long long& s_item, int& s_cmd) {
   const unsigned long long item =
       __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long b = item / (unsigned long long)C;
-  int cmd = 0;
-  unsigned sleep_n = 1;
-  while (posted_cache <= b) {
-    // relaxed poll; the acquire fence below runs once the item's batch is posted
-    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (posted_cache > b) break;
-    if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { cmd = 1; break; }
-    for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
-    sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
-  }
-  if (!cmd) {
-    // one acquire per claimed item (not per poll): invalidates this XCD's L2 copies of
-    // non-coherent inputs (a reused ring slot / DMA staging buffer) before they are read
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
-    sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(d + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(d + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned long long ne = __hip_atomic_load(d + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sdesc.n = (int32_t)(ne & 0xffffffffull);
-    sdesc.epoch = (int32_t)(ne >> 32);
-    sdesc.seq = b;
-  }
+  s_cmd = persist_wait_item(a, C, posted_cache, item, sdesc);
   s_item = item;
-  s_cmd = cmd;
 }
 
 // Append this wave's fraud-routed rows (fr_lane; m = __ballot(fr_lane)) to the slot's

@@ -40,44 +40,64 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   __syncthreads();
   unsigned long long posted_cache = 0;                    // thread 0 only
 
+  // per-item accumulators of this wave (flushed by item_flush)
+  unsigned fraud = 0, rows = 0, stale = 0;
+  unsigned long long psum = 0;
+  auto score_chunk = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, G32Row& cur)
+      __attribute__((always_inline)) {
+    g32_rows(xt[wave], lane, cur);
+    unsigned b0[kF];
+    const unsigned meta = g32_lift(cur, b0);
+    float acc[1];
+    g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
+    const int row = chunk * kG32Rows + lane;
+    const bool valid = row < n;
+    const bool fresh = ((meta >> 8) & 0xffu) == stamp;
+    const float p = fresh ? sigmoid(base + acc[0]) : __builtin_nanf("");
+    bool fr;
+    if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
+    else fr = valid && fresh && (p >= a.threshold);
+    if (valid) {
+      if (d.proba) d.proba[row] = p;
+      if (d.route) d.route[row] = fr ? 1 : 0;
+      if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
+      atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
+    }
+    const unsigned long long m = __ballot(fr);
+    fraud += __popcll(m);
+    rows += __popcll(__ballot(valid));
+    stale += __popcll(__ballot(valid && !fresh));
+    persist_emit_flagged(a, d, slot, m, fr, row, lane);
+  };
+  auto item_flush = [&](const ccfd_persist_desc& d, int slot) __attribute__((always_inline)) {
+    psum = wave_sum_u64(psum);
+    if (lane == 0 && rows) {
+      atomicAdd(&epi.fraud, fraud);
+      atomicAdd(&epi.rows, rows);
+      atomicAdd(&epi.psum_e6, psum);
+      unsigned long long* cnt = a.counters[d.epoch & 1];
+      if (stale && cnt) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)stale);
+    }
+    fraud = rows = stale = 0;
+    psum = 0;
+    persist_item_done(a, epi, d, slot, C, tid);
+  };
+  auto k7_start = [&](unsigned long long it, int slot) __attribute__((always_inline)) {
+    if (it % (unsigned long long)C == 0 && tid == 0)      // K7: micro-batch start (item 0 claimed first)
+      __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
   for (;;) {
     if (tid == 0) persist_claim(a, C, posted_cache, sdesc, s_item, s_cmd);
     __syncthreads();
     if (s_cmd) break;
+    const ccfd_persist_desc& d = sdesc;
     const int item = (int)(s_item % (unsigned long long)C);
-    const int slot = (int)(sdesc.seq % (unsigned long long)a.ring);
-    const int n = sdesc.n;
-    const unsigned char* xb = reinterpret_cast<const unsigned char*>(sdesc.x);
-    if (item == 0 && tid == 0)                            // K7: micro-batch start (item 0 claimed first)
-      __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int slot = (int)(d.seq % (unsigned long long)a.ring);
+    const int n = d.n;
+    const unsigned char* xb = reinterpret_cast<const unsigned char*>(d.x);
+    k7_start(s_item, slot);
     const int c0 = item * (kG32Waves * cpw) + wave;       // this wave's chunks: c0 + 4k
-    unsigned fraud = 0, rows = 0, stale = 0;
-    unsigned long long psum = 0;
-    auto score_chunk = [&](int chunk, G32Row& cur) __attribute__((always_inline)) {
-      g32_rows(xt[wave], lane, cur);
-      unsigned b0[kF];
-      const unsigned meta = g32_lift(cur, b0);
-      float acc[1];
-      g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
-      const int row = chunk * kG32Rows + lane;
-      const bool valid = row < n;
-      const bool fresh = ((meta >> 8) & 0xffu) == stamp;
-      const float p = fresh ? sigmoid(base + acc[0]) : __builtin_nanf("");
-      bool fr;
-      if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
-      else fr = valid && fresh && (p >= a.threshold);
-      if (valid) {
-        if (sdesc.proba) sdesc.proba[row] = p;
-        if (sdesc.route) sdesc.route[row] = fr ? 1 : 0;
-        if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
-        atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
-      }
-      const unsigned long long m = __ballot(fr);
-      fraud += __popcll(m);
-      rows += __popcll(__ballot(valid));
-      stale += __popcll(__ballot(valid && !fresh));
-      persist_emit_flagged(a, sdesc, slot, m, fr, row, lane);
-    };
     // CCFD_G32_INFLIGHT=1: every chunk of the wave's share of the item in flight at once
     // (static registers: no copy of a pending load, so no vmcnt(0) between chunks)
     auto full_item = [&](auto kC) __attribute__((always_inline)) {
@@ -92,7 +112,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       for (int k = 0; k < CPW; ++k) {
         const int chunk = c0 + kG32Waves * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
-        score_chunk(chunk, r[k]);
+        score_chunk(d, slot, n, chunk, r[k]);
       }
     };
     if (a.flags & CCFD_ARG_CHUNK_RING) {                  // default: one chunk ahead
@@ -102,9 +122,9 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       for (int k = 0; k < cpw; ++k) {
         const int chunk = c0 + kG32Waves * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
-        G32Row cur = pre;
+        G32Row cur_row = pre;
         if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) g32_fetch(xb, n, chunk + kG32Waves, lane, pre);
-        score_chunk(chunk, cur);
+        score_chunk(d, slot, n, chunk, cur_row);
       }
     } else if (cpw == 1) {
       full_item(std::integral_constant<int, 1>{});
@@ -113,15 +133,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     } else {
       full_item(std::integral_constant<int, 4>{});        // 1024-row items (engine accepts 256/512/1024)
     }
-    psum = wave_sum_u64(psum);
-    if (lane == 0 && rows) {
-      atomicAdd(&epi.fraud, fraud);
-      atomicAdd(&epi.rows, rows);
-      atomicAdd(&epi.psum_e6, psum);
-      unsigned long long* cnt = a.counters[sdesc.epoch & 1];
-      if (stale && cnt) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)stale);
-    }
-    persist_item_done(a, epi, sdesc, slot, C, tid);
+    item_flush(d, slot);
   }
 }
 
