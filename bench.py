@@ -64,11 +64,13 @@ def parse_args(argv=None):
     ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 128 otherwise)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
-    ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64", "g32"],
+    ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64", "g32", "g20"],
                     help="partition-log row format: 30 x f32 (120 B), W64 (64 B: bf16 V1..V28, "
-                         "f32 Time/Amount) or G32 (32 B, GBDT: u8 bin per feature against the "
-                         "ensemble's split table -- exact; contracts/transaction.py). auto = w64 for "
-                         "mlp/lr (the zero-copy path is PCIe-bound; profiles/r1/wire_sweep.txt), g32 for gbdt")
+                         "f32 Time/Amount), G32 (32 B, GBDT: u8 bin per feature against the "
+                         "ensemble's split table -- exact; contracts/transaction.py) or G20 (20 B: the "
+                         "same bins, 5 bits each, for <= 31 thresholds a feature). auto = w64 for "
+                         "mlp/lr (the zero-copy path is PCIe-bound; profiles/r1/wire_sweep.txt), g20 for "
+                         "gbdt (widening to g32 / f32 when the ensemble's bin table needs it)")
     ap.add_argument("--log-rows", type=int, default=1 << 22, help="rows per rank (pinned partition logs)")
     ap.add_argument("--partitions-per-rank", type=int, default=2)
     ap.add_argument("--threshold", type=float, default=0.5)
@@ -183,16 +185,16 @@ def _precision(model, dm, args, dev):
     format and blob as the headline (W64 wire rows when args.wire == 'w64')."""
     import torch
     from ccfd_demo_summit_amd.data import generate
-    from ccfd_demo_summit_amd.engine.stream_engine import G32_ROW_F32, WIRE_ROW_F32, encode_g32, encode_w64
-    from ccfd_demo_summit_amd.ops.kernels import score
+    from ccfd_demo_summit_amd.engine.stream_engine import WIRE_ROW_F32, encode_g32, encode_w64
+    from ccfd_demo_summit_amd.ops.kernels import ROW_BYTES, score
     n = int(args.precision_rows)
     X, _ = generate(n, seed=args.seed + 4242)
     if args.wire == "w64":
         rows = np.empty((n, WIRE_ROW_F32), np.float32)
         encode_w64(X, rows.ctypes.data)
         xt = torch.from_numpy(rows).to(dev)
-    elif args.wire == "g32":
-        rows = np.empty((n, G32_ROW_F32), np.float32)
+    elif args.wire in ("g32", "g20"):
+        rows = np.empty((n, ROW_BYTES[args.wire] // 4), np.float32)
         encode_g32(X, dm.bins, rows.ctypes.data)
         xt = torch.from_numpy(rows).to(dev)
     else:
@@ -220,7 +222,7 @@ def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     dm32 = DeviceModel(model, dev)
     if args.model == "gbdt":
-        exec_mode = "launch"                # the persistent GBDT kernel reads G32 rows only
+        exec_mode = "launch"                # the persistent GBDT kernel reads binned rows only
     rows = 1 << 20
     log = PartitionLog(rows)
     generate(rows, seed=args.seed + 77, out=log.feats.array)
@@ -246,7 +248,7 @@ def main(argv=None):
     args = parse_args(argv)
     from ccfd_demo_summit_amd.parallel.dp import resolve_row_format
     try:
-        args.wire = resolve_row_format(args.model, args.wire)   # auto: w64 for mlp/lr, g32 for gbdt
+        args.wire = resolve_row_format(args.model, args.wire)   # auto: w64 for mlp/lr, g20 for gbdt
     except ValueError as e:
         _fail(str(e))
     if args.batch is None:
@@ -290,7 +292,7 @@ def main(argv=None):
         # coalesced launches (0.75e9 at 166 us); GBDT on G32 rows: 1.68e9 persistent vs 1.07e9
         # with launches (profiles/r2/gbdt_g32_*_sweep.jsonl); DMA paths use launches
         zc = args.input_mode == "zerocopy" and args.output_mode == "zerocopy"
-        exec_mode = "persistent" if zc and (args.model in ("mlp", "lr") or args.wire == "g32") else "launch"
+        exec_mode = "persistent" if zc and (args.model in ("mlp", "lr") or args.wire in ("g32", "g20")) else "launch"
 
     # ---- per-rank H2D ceiling probe, all ranks at once (attributes any scaling loss to the
     # host side: DRAM / PCIe root contention shows up as a lower per-rank GB/s at N > 1)
@@ -441,7 +443,7 @@ def main(argv=None):
     if ctx.rank == 0:
         if args.precision_rows > 0:
             precision = _precision(model, dm, args, dev)
-        if args.wire in ("w64", "g32") and not args.no_f32_probe:
+        if args.wire in ("w64", "g32", "g20") and not args.no_f32_probe:
             f32_rate = _f32_wire_rate(args, model, dev, exec_mode)
 
     value = total_rows / elapsed
@@ -467,6 +469,8 @@ def main(argv=None):
                  + {"w64": "W64: bf16 V1..V28 + f32 Time/Amount, 64 B",
                     "g32": "G32: u8 bin of each feature against the ensemble's split thresholds "
                            "(exact for oblivious trees) + amount bucket + table stamp, 32 B",
+                    "g20": "G20: 5-bit bin of each feature against the ensemble's split thresholds "
+                           "(exact for oblivious trees, <= 31 a feature) + amount bucket + table stamp, 20 B",
                     "f32": "30 x f32, 120 B"}[args.wire]
                  + ") replayed from pinned partition logs; random-init weights, normaliser fitted + "
                  "output bias calibrated to the 0.172% fraud prior on a synthetic sample"),
@@ -507,7 +511,7 @@ def main(argv=None):
         "flagged_handed_off_rank0": flagged_total,
         "per_rank": per_rank,
         "h2d_zerocopy_ceiling_tx_s_rank0": (None if h2d_gbps is None else
-                                            round(h2d_gbps * 1e9 / {"w64": 64, "g32": 32, "f32": 120}[args.wire], 1)),
+                                            round(h2d_gbps * 1e9 / {"w64": 64, "g32": 32, "g20": 20, "f32": 120}[args.wire], 1)),
         "f32_wire_tx_s": None if f32_rate is None else round(f32_rate, 1),
         "precision_vs_fp32": precision,
     }

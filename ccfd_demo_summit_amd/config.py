@@ -81,7 +81,7 @@ class EngineConfig:
     depth: int = 12                  # micro-batches in flight per GPU (p50 53 us at the PCIe rate)
     streams: int = 4                 # HIP streams per engine
     input_mode: str = "zerocopy"     # dma (H2D into HBM) | zerocopy (kernel reads pinned host)
-    wire: str = "auto"               # ring row format: f32 | w64 | g32 | auto (w64 for mlp/lr, g32 for gbdt)
+    wire: str = "auto"               # ring row format: f32 | w64 | g32 | g20 | auto (w64 for mlp/lr, g20 for gbdt)
     coalesce: int = 4                # ready micro-batches per kernel launch (MLP, launch mode)
     ingest_threads: int = 1          # native Kafka consumer threads per rank (partitions split)
     model_watch: str = ""            # hot-swap when this safetensors file changes (rank 0)

@@ -10,6 +10,7 @@ from .transaction import (
     FEATURE_NAMES, N_FEATURES, AMOUNT_COL, TIME_COL, Transaction,
     encode_tx_json, decode_tx_json, TxBatch,
     WIRE_ROW_BYTES, WIRE_PERM, encode_wire, decode_wire, G32_ROW_BYTES, encode_g32, amount_bucket,
+    G20_ROW_BYTES, encode_g20, decode_g20_bins,
 )
 from .outcomes import Outcome, Route, CustomerResponse
 from . import seldon, metric_names, env

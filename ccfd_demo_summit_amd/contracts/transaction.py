@@ -137,6 +137,53 @@ def encode_g32(X: np.ndarray, edges: Sequence[np.ndarray], stamp: int,
     return out
 
 
+# G20: the same bins packed 5 bits each for bin tables of <= 31 edges per feature (every
+# BASELINE-size 100 x 6 ensemble: ~20 distinct thresholds a feature), little-endian over
+# the row's 160 bits -- bits [5j, 5j+5) bin of feature j, [150, 154) amount bucket,
+# [154, 160) bin-table stamp 1..63.  20 B a row: 1.6x the rows of G32 per PCIe byte.
+G20_ROW_BYTES = 20
+
+
+def encode_g20(X: np.ndarray, edges: Sequence[np.ndarray], stamp: int,
+               out: Optional[np.ndarray] = None) -> np.ndarray:
+    """float32 [n, 30] canonical rows -> uint8 [n, 20] G20 rows (numpy oracle of the native
+    ccfd_encode_g20).  ``edges[j]``: ascending float32 bin edges of feature j (<= 31)."""
+    g = encode_g32(X, edges, stamp)
+    if (g[:, :N_FEATURES] > 31).any() or not 1 <= stamp <= 63:
+        raise ValueError("G20 rows need <= 31 bin edges per feature and a stamp in 1..63")
+    n = g.shape[0]
+    acc = np.zeros((n, 3), np.uint64)                        # 3 x 64 bits >= 160
+    fields = [(5 * j, g[:, j]) for j in range(N_FEATURES)] + [(150, g[:, 30]), (154, g[:, 31])]
+    for bit, v in fields:
+        v = v.astype(np.uint64)
+        w, sh = bit >> 6, bit & 63
+        acc[:, w] |= v << np.uint64(sh)
+        if sh + 6 > 64:
+            acc[:, w + 1] |= v >> np.uint64(64 - sh)
+    if out is None:
+        out = np.empty((n, G20_ROW_BYTES), np.uint8)
+    out[:] = acc.view(np.uint8).reshape(n, 24)[:, :G20_ROW_BYTES]
+    return out
+
+
+def decode_g20_bins(rows: np.ndarray) -> np.ndarray:
+    """uint8 [n, 20] G20 rows -> uint8 [n, 32] in the G32 byte layout (bins, bucket, stamp)."""
+    r = np.ascontiguousarray(rows, np.uint8).reshape(-1, G20_ROW_BYTES)
+    n = r.shape[0]
+    pad = np.zeros((n, 24), np.uint8)
+    pad[:, :G20_ROW_BYTES] = r
+    acc = pad.view(np.uint64).reshape(n, 3)
+    out = np.empty((n, G32_ROW_BYTES), np.uint8)
+    fields = [(5 * j, 5) for j in range(N_FEATURES)] + [(150, 4), (154, 6)]
+    for i, (bit, width) in enumerate(fields):
+        w, sh = bit >> 6, bit & 63
+        v = acc[:, w] >> np.uint64(sh)
+        if sh + width > 64:
+            v = v | (acc[:, w + 1] << np.uint64(64 - sh))
+        out[:, i] = (v & np.uint64((1 << width) - 1)).astype(np.uint8)
+    return out
+
+
 TXB_MAGIC = b"TXB1"
 TXB_HEADER = struct.Struct("<4sHHIIQQ")  # 32 bytes
 assert TXB_HEADER.size == 32

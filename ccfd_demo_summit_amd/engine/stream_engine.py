@@ -14,13 +14,14 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..ops._lib import (BATCH_TRACE_DTYPE, FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig,
+from ..ops._lib import (BATCH_TRACE_DTYPE, BIN_FORMATS, FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig,
                         EngineStats, Flagged, check, last_error, lib)
 from ..ops.kernels import ROW_BYTES, DeviceModel
 
 N_FEATURES = 30
 WIRE_ROW_F32 = 16            # W64 wire row = 64 B = 16 f32 words (contracts.transaction)
 G32_ROW_F32 = 8              # G32 row = 32 B (contracts.transaction)
+G20_ROW_F32 = 5              # G20 row = 20 B (contracts.transaction)
 INPUT_MODES = {"dma": 0, "zerocopy": 1}
 OUTPUT_MODES = {"zerocopy": 0, "dma": 1}
 
@@ -63,22 +64,28 @@ def encode_w64(X: np.ndarray, out_ptr: int) -> None:
 
 
 def encode_g32(X: np.ndarray, bins, out_ptr: int, amount_ptr: Optional[int] = None) -> None:
-    """f32 rows [n, 30] -> G32 rows at ``out_ptr`` against ``bins`` (models.gbdt.BinSpec),
-    Amount column to ``amount_ptr`` (native encoder, csrc/engine/ingest.cpp)."""
+    """f32 rows [n, 30] -> G32 rows (G20 rows for a 5-bit ``bins``) at ``out_ptr`` against
+    ``bins`` (models.gbdt.BinSpec), Amount column to ``amount_ptr`` (native encoders,
+    csrc/engine/ingest.cpp)."""
     X = np.ascontiguousarray(X, dtype=np.float32)
     if X.ndim != 2 or X.shape[1] != N_FEATURES:
         raise ValueError("expected [n, 30] float32 rows")
     flat, off = bins.flat, bins.offsets
-    if lib().ccfd_encode_g32(X.ctypes.data, X.shape[0], N_FEATURES, flat.ctypes.data, off.ctypes.data,
-                             int(bins.stamp), C.c_void_p(out_ptr), C.c_void_p(amount_ptr)) != X.shape[0]:
-        raise RuntimeError("ccfd_encode_g32 failed")
+    fn = lib().ccfd_encode_g20 if bins.bits == 5 else lib().ccfd_encode_g32
+    if fn(X.ctypes.data, X.shape[0], N_FEATURES, flat.ctypes.data, off.ctypes.data,
+          int(bins.stamp), C.c_void_p(out_ptr), C.c_void_p(amount_ptr)) != X.shape[0]:
+        raise RuntimeError(f"ccfd_encode_{bins.row_format} failed")
+
+
+encode_bins = encode_g32
 
 
 class PartitionLog:
     """One Kafka-partition-like append log of transactions in pinned host memory.
 
     ``wire=True`` stores W64 rows (64 B, contracts/transaction.py) instead of 30 x f32;
-    ``bins=BinSpec`` stores G32 rows (32 B, GBDT) plus a host-side Amount column."""
+    ``bins=BinSpec`` stores G32 rows (32 B, GBDT) -- G20 rows (20 B) for a 5-bit spec --
+    plus a host-side Amount column."""
 
     def __init__(self, n_rows: int, wire: bool = False, bins=None):
         self.n = int(n_rows)
@@ -86,7 +93,7 @@ class PartitionLog:
         self.bins = bins
         if bins is not None and wire:
             raise ValueError("a log holds one row format: W64 (wire) or G32 (bins)")
-        self.row_format = "g32" if bins is not None else "w64" if self.wire else "f32"
+        self.row_format = bins.row_format if bins is not None else "w64" if self.wire else "f32"
         self.row_bytes = ROW_BYTES[self.row_format]
         self.feats = PinnedArray((self.n, self.row_bytes // 4), np.float32)
         self.ids = PinnedArray(self.n, np.uint64)
@@ -95,7 +102,7 @@ class PartitionLog:
 
     def write_rows(self, r: int, X: np.ndarray) -> None:
         """Store canonical f32 rows X at log rows [r, r + len(X))."""
-        if self.row_format == "g32":
+        if self.row_format in BIN_FORMATS:
             encode_g32(X, self.bins, self.feats.ptr + r * self.row_bytes, self.amount.ptr + 4 * r)
         elif self.wire:
             encode_w64(X, self.feats.ptr + r * self.row_bytes)
@@ -213,7 +220,7 @@ class StreamEngine:
     def _check_log(self, log: PartitionLog) -> None:
         if log.row_format != self.row_format:
             raise ValueError(f"log rows are {log.row_format}, the engine's model blob expects {self.row_format}")
-        if self.row_format == "g32" and log.bins.stamp != self.bins.stamp:
+        if self.row_format in BIN_FORMATS and log.bins.stamp != self.bins.stamp:
             raise ValueError("log was G32-encoded against another bin table than the model's")
 
     def add_log(self, partition: int, log: PartitionLog, cursor: int = 0) -> None:
@@ -238,8 +245,8 @@ class StreamEngine:
         """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
         X = np.ascontiguousarray(X, dtype=np.float32)
         n = X.shape[0]
-        if self.row_format == "g32":
-            rows = np.empty((n, G32_ROW_F32), np.float32)
+        if self.row_format in BIN_FORMATS:
+            rows = np.empty((n, ROW_BYTES[self.row_format] // 4), np.float32)
             encode_g32(X, self.bins, rows.ctypes.data)
             X = rows
         elif self.wire:
@@ -268,7 +275,7 @@ class StreamEngine:
         if dm.kind != self.dm.kind or dm.row_format != self.row_format or \
                 (dm.trees, dm.depth) != (self.dm.trees, self.dm.depth):
             raise ValueError("hot swap needs a model of the same kind / wire format / tree shape")
-        if self.row_format == "g32" and dm.bins.stamp != self.bins.stamp:
+        if self.row_format in BIN_FORMATS and dm.bins.stamp != self.bins.stamp:
             raise ValueError("G32 hot swap: pack the new ensemble against the live bin table "
                              "(DeviceModel(model, bins=engine.bins)); its thresholds must be bin edges")
         check(lib().ccfd_engine_set_blob(C.c_void_p(self.h), C.c_void_p(dm.blob.data_ptr())),
@@ -354,7 +361,7 @@ class StreamEngine:
             buf = b"".join(chunk)
             off = np.zeros(k + 1, np.int64)
             np.cumsum([len(v) for v in chunk], out=off[1:])
-            if log.row_format == "g32":               # parse to f32, then bin
+            if log.row_format in BIN_FORMATS:         # parse to f32, then bin
                 tmp = np.empty((k, N_FEATURES), np.float32)
                 got = L.ccfd_parse_json_batch(buf, off.ctypes.data, k, tmp.ctypes.data,
                                               log.ids.ptr + r * 8, log.customer.ptr + r * 4)

@@ -36,8 +36,8 @@ class KcStats(C.Structure):
 
 
 RESET_POLICIES = {"earliest": 0, "latest": 1, "none": 2}
-ROW_CODES = {"f32": 0, "w64": 1, "g32": 2}
-ROW_WIDTH = {"f32": 30, "w64": 16, "g32": 8}          # f32 words per row
+ROW_CODES = {"f32": 0, "w64": 1, "g32": 2, "g20": 3}
+ROW_WIDTH = {"f32": 30, "w64": 16, "g32": 8, "g20": 5}   # f32 words per row
 
 
 def _bind(L):
@@ -99,7 +99,7 @@ class NativeKafkaConsumer:
                                     ROW_CODES[engine.row_format])
         check(0 if h else -1, "ccfd_kc_create_engine")
         kc = cls(h, ps, keep=arr)
-        if engine.row_format == "g32":
+        if engine.row_format in ("g32", "g20"):
             kc._set_bins(engine.bins)
         return kc
 
@@ -117,7 +117,7 @@ class NativeKafkaConsumer:
         (rows, ids, customer), ``amounts[p]`` = the Amount column of G32 rows (``bins``)."""
         L = _bind(lib())
         ps = sorted(start_offsets)
-        fmt = "g32" if bins is not None else "w64" if wire else "f32"
+        fmt = bins.row_format if bins is not None else "w64" if wire else "f32"
         bufs = {p: (np.zeros((capacity, ROW_WIDTH[fmt]), np.float32), np.zeros(capacity, np.uint64),
                     np.zeros(capacity, np.uint32)) for p in ps}
         amounts = {p: np.zeros(capacity, np.float32) for p in ps}

@@ -236,7 +236,7 @@ def cmd_engine(a, cfg):
     bind_to_gpu(ctx.device.index)
     fmt = resolve_row_format(cfg.engine.model, cfg.engine.wire)
     rules = RuleSet.from_config(cfg.router)
-    if fmt == "g32" and rules.feature_vars():
+    if fmt in ("g32", "g20") and rules.feature_vars():
         # G32 rows carry bins, not feature values: rules over transaction columns need the
         # values, so this deployment scores GBDT on f32 rows (exact, 120 B/row)
         print(f"[engine] routing rules read {sorted(rules.feature_vars())}: GBDT on f32 rows instead of G32",

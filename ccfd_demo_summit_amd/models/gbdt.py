@@ -33,6 +33,7 @@ from .common import HEADER_BYTES, header, pad16, sigmoid
 
 MAX_DEPTH = 8
 MAX_BINS = 255          # split thresholds per feature a G32 byte can index
+G20_MAX_EDGES = 31      # ... and a G20 five-bit field (contracts/transaction.py encode_g20)
 
 
 @dataclass
@@ -45,15 +46,20 @@ class BinSpec:
     retrained ensemble against the spec the live partition logs were encoded with, so a hot
     swap needs no re-encoding while the split set stays inside it."""
     edges: List[np.ndarray]
+    bits: int = 8            # 8: G32 rows (u8 bins); 5: G20 rows (<= 31 edges per feature)
 
     def __post_init__(self):
         if len(self.edges) != N_FEATURES:
             raise ValueError(f"need bin edges for all {N_FEATURES} features")
+        if self.bits not in (8, 5):
+            raise ValueError("bin width is 8 (G32 rows) or 5 (G20 rows)")
+        cap = MAX_BINS if self.bits == 8 else G20_MAX_EDGES
         out = []
         for j, e in enumerate(self.edges):
             e = np.ascontiguousarray(e, np.float32).reshape(-1)
-            if e.size > MAX_BINS:
-                raise ValueError(f"feature {j}: {e.size} split thresholds > {MAX_BINS} (G32 bins are u8)")
+            if e.size > cap:
+                raise ValueError(f"feature {j}: {e.size} split thresholds > {cap} "
+                                 f"({'G32 bins are u8' if self.bits == 8 else 'G20 bins are 5 bits'})")
             if np.isnan(e).any() or (e.size > 1 and not (np.diff(e) > 0).all()):
                 raise ValueError(f"feature {j}: bin edges must be ascending, distinct and not NaN")
             out.append(e)
@@ -65,6 +71,18 @@ class BinSpec:
         thr = np.asarray(thr, np.float32).reshape(-1)
         t = [thr[feat == j] for j in range(N_FEATURES)]
         return cls([np.unique(e[~np.isnan(e)]) for e in t])     # NaN splits never fire: k = 255
+
+    @property
+    def row_format(self) -> str:
+        return "g32" if self.bits == 8 else "g20"
+
+    @property
+    def fits_g20(self) -> bool:
+        return all(e.size <= G20_MAX_EDGES for e in self.edges)
+
+    def with_bits(self, bits: int) -> "BinSpec":
+        """The same edges for the other row format (ValueError if they do not fit)."""
+        return BinSpec([e.copy() for e in self.edges], bits=bits)
 
     @property
     def offsets(self) -> np.ndarray:
@@ -79,9 +97,10 @@ class BinSpec:
 
     @property
     def stamp(self) -> int:
-        """1..255 digest of the edge table (0 is never valid: zeroed memory is stale)."""
+        """1..255 digest of the edge table (1..63 for G20 rows, whose stamp field is 6 bits;
+        0 is never valid: zeroed memory is stale)."""
         h = zlib.crc32(self.offsets.tobytes() + self.flat.tobytes())
-        return 1 + h % 255
+        return 1 + h % (255 if self.bits == 8 else 63)
 
     def bin_index(self, feat: np.ndarray, thr: np.ndarray) -> np.ndarray:
         """k with edges[feat][k] == thr for every split (ValueError if a threshold is missing)."""
@@ -101,19 +120,20 @@ class BinSpec:
         return k
 
     def encode(self, X: np.ndarray) -> np.ndarray:
-        """numpy oracle of the native encoder: f32 [n,30] -> u8 [n,32] G32 rows."""
-        from ..contracts.transaction import encode_g32
-        return encode_g32(X, self.edges, self.stamp)
+        """numpy oracle of the native encoder: f32 [n,30] -> u8 [n,32] G32 rows (or u8 [n,20]
+        G20 rows for a 5-bit spec)."""
+        from ..contracts.transaction import encode_g20, encode_g32
+        return (encode_g32 if self.bits == 8 else encode_g20)(X, self.edges, self.stamp)
 
     def to_bytes(self) -> bytes:
         """offsets i32[31] + edges f32[...] (the X1 broadcast payload next to the blob)."""
         return self.offsets.tobytes() + np.concatenate(self.edges + [np.zeros(0, np.float32)]).tobytes()
 
     @classmethod
-    def from_bytes(cls, b: bytes) -> "BinSpec":
+    def from_bytes(cls, b: bytes, bits: int = 8) -> "BinSpec":
         off = np.frombuffer(b, np.int32, N_FEATURES + 1)
         e = np.frombuffer(b, np.float32, int(off[-1]), 4 * (N_FEATURES + 1))
-        return cls([e[off[j]:off[j + 1]].copy() for j in range(N_FEATURES)])
+        return cls([e[off[j]:off[j + 1]].copy() for j in range(N_FEATURES)], bits=bits)
 
     def contains(self, other: "BinSpec") -> bool:
         return all(np.isin(o, e).all() for o, e in zip(other.edges, self.edges))
@@ -175,7 +195,11 @@ class ObliviousGBDT:
         form of every level, ``bin[f] > k`` with k the threshold's edge index -- [n, T]."""
         spec = bins if bins is not None else self.bin_spec()
         k = spec.bin_index(self.feat, self.thr)              # [T, D]; NaN thresholds: 255
-        b = np.asarray(rows, np.uint8)[:, :N_FEATURES].astype(np.int32)
+        if spec.bits == 5:
+            from ..contracts.transaction import decode_g20_bins
+            b = decode_g20_bins(rows).astype(np.int32)
+        else:
+            b = np.asarray(rows, np.uint8)[:, :N_FEATURES].astype(np.int32)
         bits = b[:, self.feat] > k[None]
         return (bits.astype(np.int64) << np.arange(self.depth)).sum(-1)
 
@@ -191,9 +215,11 @@ class ObliviousGBDT:
         z = self.raw_score(X)
         self.base += float(np.log(threshold / (1 - threshold)) - np.quantile(z, 1.0 - target_rate))
 
-    def bin_spec(self) -> BinSpec:
-        """The smallest G32 bin table of this ensemble: its distinct thresholds per feature."""
-        return BinSpec.from_thresholds(self.feat, self.thr)
+    def bin_spec(self, bits: int = 8) -> BinSpec:
+        """The smallest bin table of this ensemble -- its distinct thresholds per feature --
+        for G32 rows (``bits=8``) or G20 rows (``bits=5``; ValueError past 31 a feature)."""
+        spec = BinSpec.from_thresholds(self.feat, self.thr)
+        return spec if bits == 8 else spec.with_bits(bits)
 
     def pack(self, wire: bool = False, bins: Optional[BinSpec] = None) -> bytes:
         """GBT1 blob for f32 rows, or (``bins``) the GBB1 blob for G32 rows of that spec."""

@@ -45,7 +45,7 @@ class EngineSpec:
     gpus_per_node: int = 8           # ranks per pod (torchrun), one per GPU
     model: str = "mlp"
     weights: str = ""                # safetensors file (models.save_model); "" = random init
-    row_format: str = "auto"         # f32 | w64 | g32 | auto
+    row_format: str = "auto"         # f32 | w64 | g32 | g20 | auto
     rules: str = ""                  # routing rule text or file (ROUTER_RULES)
 
 

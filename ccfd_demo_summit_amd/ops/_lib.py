@@ -23,8 +23,9 @@ MODEL_LR, MODEL_MLP, MODEL_GBDT = 0, 1, 2
 MODEL_IDS = {"lr": MODEL_LR, "mlp": MODEL_MLP, "gbdt": MODEL_GBDT}
 N_COUNTER_SLOTS = 64
 CNT_WIRE_STALE = 4        # ccfd_abi.h CCFD_CNT_WIRE_STALE
-ARG_WIRE_W64, ARG_WIRE_G32 = 2, 4
-ROW_FORMATS = {"f32": 0, "w64": 1, "g32": 2}      # ccfd_engine_config.wire
+ARG_WIRE_W64, ARG_WIRE_G32, ARG_WIRE_G20 = 2, 4, 8
+ROW_FORMATS = {"f32": 0, "w64": 1, "g32": 2, "g20": 3}      # ccfd_engine_config.wire
+BIN_FORMATS = ("g32", "g20")                                # rows of per-feature bins (GBDT)
 
 
 class ScoreArgs(C.Structure):
@@ -133,6 +134,9 @@ def lib() -> C.CDLL:
         L.ccfd_encode_g32.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
                                       C.c_void_p, C.c_void_p]
         L.ccfd_encode_g32.restype = C.c_int64
+        L.ccfd_encode_g20.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
+                                      C.c_void_p, C.c_void_p]
+        L.ccfd_encode_g20.restype = C.c_int64
         L.ccfd_engine_set_amount.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         _lib = L
         return L

@@ -12,10 +12,12 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from ._lib import ARG_WIRE_G32, ARG_WIRE_W64, MODEL_IDS, N_COUNTER_SLOTS, ScoreArgs, check, lib
+from ._lib import (ARG_WIRE_G20, ARG_WIRE_G32, ARG_WIRE_W64, BIN_FORMATS, MODEL_IDS, N_COUNTER_SLOTS, ScoreArgs,
+                   check, lib)
 
 N_FEATURES = 30
-ROW_BYTES = {"f32": 4 * N_FEATURES, "w64": 64, "g32": 32}
+ROW_BYTES = {"f32": 4 * N_FEATURES, "w64": 64, "g32": 32, "g20": 20}
+WIRE_FLAGS = {"f32": 0, "w64": ARG_WIRE_W64, "g32": ARG_WIRE_G32, "g20": ARG_WIRE_G32 | ARG_WIRE_G20}
 
 
 class DeviceModel:
@@ -23,8 +25,10 @@ class DeviceModel:
 
     def __init__(self, model, device: torch.device | str | int = "cuda", wire: bool = False, bins=None):
         """``wire=True``: blob packed for W64 wire rows (MLP / LR; see contracts/transaction.py).
-        ``bins``: GBDT on G32 rows -- ``True`` for the model's own bin table, or a
-        ``models.gbdt.BinSpec`` containing its thresholds (e.g. the live logs' spec)."""
+        ``bins``: GBDT on binned rows -- ``True`` for the model's own G32 bin table, ``"g20"``
+        for the same table on 20-byte G20 rows (<= 31 thresholds a feature), or a
+        ``models.gbdt.BinSpec`` containing its thresholds (e.g. the live logs' spec; its
+        ``bits`` select G32 or G20)."""
         self.kind = model.kind
         if self.kind not in MODEL_IDS:
             raise ValueError(f"no device kernel for model kind {self.kind!r}")
@@ -33,7 +37,11 @@ class DeviceModel:
         if bins is not None and bins is not False and self.kind != "gbdt":
             raise ValueError("G32 rows (bins=) are for the GBDT kernel")
         self.wire = bool(wire)
-        self.bins = (model.bin_spec() if bins is True else bins) if bins not in (None, False) else None
+        if bins is True or bins == "g32":
+            bins = model.bin_spec()
+        elif isinstance(bins, str) and bins == "g20":
+            bins = model.bin_spec(bits=5)
+        self.bins = bins if bins is not False else None
         if self.bins is not None:
             packed = model.pack(bins=self.bins)
         else:
@@ -56,8 +64,9 @@ class DeviceModel:
 
     @property
     def row_format(self) -> str:
-        """Row layout the blob expects: "f32" (30 x f32), "w64" or "g32"."""
-        return "g32" if getattr(self, "bins", None) is not None else "w64" if self.wire else "f32"
+        """Row layout the blob expects: "f32" (30 x f32), "w64", "g32" or "g20"."""
+        bins = getattr(self, "bins", None)
+        return bins.row_format if bins is not None else "w64" if self.wire else "f32"
 
 
 class DeviceRules:
@@ -84,7 +93,7 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
           counters: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None,
           flags: int = 0, rules: Optional[DeviceRules] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused score of x [n,30] (float32, CUDA) -- or, for a ``wire`` model, W64 rows
-    ([n,64] uint8 or [n,16] float32 view), for a ``bins`` model G32 rows ([n,32] uint8) --
+    ([n,64] uint8 or [n,16] float32 view), for a ``bins`` model G32 / G20 rows ([n,32] / [n,20] u8) --
     returns (proba_1 [n] f32, route [n] u8).
     ``flags``: extra ``CCFD_ARG_*`` bits (ablation switches for profiling)."""
     fmt = dm.row_format
@@ -93,8 +102,8 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
         rb = ROW_BYTES[fmt]
         if not x.is_cuda or x.dim() != 2 or x.element_size() * x.shape[1] != rb or not x.is_contiguous():
             raise ValueError(f"{fmt} model: x must be contiguous CUDA {fmt.upper()} rows ([n,{rb}] u8)")
-        if fmt == "g32" and rules is not None and rules.ruleset.feature_vars():
-            raise ValueError("G32 rows carry bins, not feature values: routing rules may only use proba_1")
+        if fmt in BIN_FORMATS and rules is not None and rules.ruleset.feature_vars():
+            raise ValueError("G32 / G20 rows carry bins, not feature values: routing rules may only use proba_1")
     elif not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != N_FEATURES:
         raise ValueError("x must be a CUDA float32 tensor of shape [n, 30]")
     if x.stride(1) != 1:
@@ -107,7 +116,7 @@ def score(dm: DeviceModel, x: torch.Tensor, threshold: float = 0.5,
     a = ScoreArgs()
     a.x = x.data_ptr()
     a.ld = ROW_BYTES[fmt] // 4 if wire else x.stride(0)
-    a.flags = {"f32": 0, "w64": ARG_WIRE_W64, "g32": ARG_WIRE_G32}[fmt] | int(flags)
+    a.flags = WIRE_FLAGS[fmt] | int(flags)
     a.n = n
     a.model = dm.model_id
     a.blob = dm.blob.data_ptr()

@@ -119,10 +119,11 @@ def broadcast_blob(ctx: DistContext, blob: Optional[torch.Tensor], src: int = 0,
 
 def resolve_row_format(kind: str, wire: str = "auto") -> str:
     """Partition-log row format of a model kind: ``auto`` = W64 for the MLP / LR kernels,
-    G32 for GBDT (the PCIe-byte-optimal exact or bf16 formats, contracts/transaction.py)."""
+    G20 for GBDT (the PCIe-byte-optimal exact or bf16 formats, contracts/transaction.py;
+    ``broadcast_model`` widens G20 -> G32 -> f32 when an ensemble's bin table needs it)."""
     if wire == "auto":
-        return "g32" if kind == "gbdt" else "w64"
-    if (wire == "w64" and kind == "gbdt") or (wire == "g32" and kind != "gbdt"):
+        return "g20" if kind == "gbdt" else "w64"
+    if (wire == "w64" and kind == "gbdt") or (wire in ("g32", "g20") and kind != "gbdt"):
         raise ValueError(f"row format {wire} does not apply to model kind {kind}")
     return wire
 
@@ -133,24 +134,31 @@ def broadcast_model(ctx: DistContext, model, kind: str, row_format: str, group=N
     partition logs with, and the tree shape; every rank returns an equal DeviceModel.
     ``model`` is only read on rank 0.
 
-    G32 needs at most 255 distinct split thresholds per feature (u8 bins).  An ensemble with
-    more (e.g. a large import) falls back to f32 rows on every rank: rank 0 decides and the
-    decision travels in the header broadcast ahead of the blob, so all ranks agree.  Callers
-    take the row format from the returned model (``DeviceModel.row_format``)."""
+    G20 needs at most 31 distinct split thresholds per feature (5-bit bins), G32 at most 255
+    (u8 bins).  An ensemble with more widens to the next format (G20 -> G32 -> f32 rows) on
+    every rank: rank 0 decides and the decision travels in the header broadcast ahead of
+    the blob, so all ranks agree.  Callers take the row format from the returned model
+    (``DeviceModel.row_format``)."""
     from ..models.gbdt import BinSpec
     from ..ops.kernels import DeviceModel
-    codes = {"f32": 0, "w64": 1, "g32": 2}
+    codes = {"f32": 0, "w64": 1, "g32": 2, "g20": 3}
     blob = spec_t = None
     header = torch.zeros(3, dtype=torch.int64, device=ctx.device)      # trees, depth, row format
     if ctx.rank == 0:
         fmt = row_format
+        if fmt == "g20":
+            try:
+                spec = model.bin_spec(bits=5)
+            except ValueError as e:                 # > 31 thresholds on a feature
+                warnings.warn(f"G20 rows impossible for this ensemble ({e}); trying G32 rows")
+                fmt = "g32"
         if fmt == "g32":
             try:
                 spec = model.bin_spec()
             except ValueError as e:                 # > 255 thresholds on a feature
                 warnings.warn(f"G32 rows impossible for this ensemble ({e}); scoring f32 rows")
                 fmt = "f32"
-        if fmt == "g32":
+        if fmt in ("g32", "g20"):
             packed = model.pack(bins=spec)
             spec_t = torch.from_numpy(np.frombuffer(spec.to_bytes(), np.uint8).copy()).to(ctx.device)
         else:
@@ -163,8 +171,9 @@ def broadcast_model(ctx: DistContext, model, kind: str, row_format: str, group=N
     fmt = {v: k for k, v in codes.items()}[int(header[2])]
     blob = broadcast_blob(ctx, blob, group=group)
     bins = None
-    if fmt == "g32":
-        bins = BinSpec.from_bytes(broadcast_blob(ctx, spec_t, group=group).cpu().numpy().tobytes())
+    if fmt in ("g32", "g20"):
+        bins = BinSpec.from_bytes(broadcast_blob(ctx, spec_t, group=group).cpu().numpy().tobytes(),
+                                  bits=8 if fmt == "g32" else 5)
     return DeviceModel.from_blob(kind, blob, int(header[0]), int(header[1]), wire=fmt == "w64", bins=bins)
 
 

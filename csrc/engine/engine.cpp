@@ -230,12 +230,14 @@ class Engine {
       return -1;
     }
     if (cfg.blob == nullptr) { set_error("null model blob"); return -1; }
-    if (cfg.wire < 0 || cfg.wire > 2) { set_error("wire must be 0 (f32), 1 (W64) or 2 (G32)"); return -1; }
+    if (cfg.wire < 0 || cfg.wire > 3) { set_error("wire must be 0 (f32), 1 (W64), 2 (G32) or 3 (G20)"); return -1; }
     if (cfg.wire == 1 && cfg.model == CCFD_MODEL_GBDT) { set_error("W64 wire rows: MLP and LR only"); return -1; }
-    if (cfg.wire == 2 && cfg.model != CCFD_MODEL_GBDT) { set_error("G32 rows: GBDT only"); return -1; }
-    rowf = cfg.wire == 2 ? CCFD_G32_ROW_BYTES / 4 : cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 : CCFD_N_FEATURES;
-    amount_f = cfg.wire == 2 ? -1 : cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 - 1 : CCFD_N_FEATURES - 1;
-    wire_flag = cfg.wire == 2 ? CCFD_ARG_WIRE_G32 : cfg.wire ? CCFD_ARG_WIRE_W64 : 0;
+    if (cfg.wire >= 2 && cfg.model != CCFD_MODEL_GBDT) { set_error("G32 / G20 rows: GBDT only"); return -1; }
+    rowf = cfg.wire == 3 ? CCFD_G20_ROW_BYTES / 4 : cfg.wire == 2 ? CCFD_G32_ROW_BYTES / 4
+         : cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 : CCFD_N_FEATURES;
+    amount_f = cfg.wire >= 2 ? -1 : cfg.wire ? CCFD_WIRE_ROW_BYTES / 4 - 1 : CCFD_N_FEATURES - 1;
+    wire_flag = cfg.wire == 3 ? (CCFD_ARG_WIRE_G32 | CCFD_ARG_WIRE_G20) : cfg.wire == 2 ? CCFD_ARG_WIRE_G32
+              : cfg.wire ? CCFD_ARG_WIRE_W64 : 0;
     HIPCHK(hipSetDevice(cfg.device));
     {
       int khz = 0;
@@ -310,7 +312,7 @@ class Engine {
   bool persist_counted = false;            // holds one of the process's persistent-queue slots
   bool coherent_out = true;
   uint64_t launches = 0;        // coalesced launches issued (stream round-robin)
-  int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, 16 for W64, 8 for G32 rows
+  int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, 16 for W64, 8 for G32, 5 for G20 rows
   int amount_f = CCFD_N_FEATURES - 1;   // word of Amount in a row (-1: G32, host-side column)
   int wire_flag = 0;            // CCFD_ARG_WIRE_* of the row format
   int ablate = 0;
@@ -335,9 +337,9 @@ class Engine {
   std::vector<int64_t> flip_seq;           // seq at each epoch flip
 
   int persist_init() {
-    const bool g32 = cfg.model == CCFD_MODEL_GBDT && cfg.wire == 2;
+    const bool g32 = cfg.model == CCFD_MODEL_GBDT && cfg.wire >= 2;     // G32 or G20 rows
     if (cfg.model != CCFD_MODEL_MLP && cfg.model != CCFD_MODEL_LR && !g32) {
-      set_error("persistent exec_mode supports the MLP and LR models, and GBDT on G32 rows");
+      set_error("persistent exec_mode supports the MLP and LR models, and GBDT on G32 / G20 rows");
       return -1;
     }
     if (cfg.output_mode != 0 || cfg.depth > CCFD_PERSIST_MAX_RING) {

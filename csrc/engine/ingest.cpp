@@ -221,6 +221,21 @@ inline void encode_row_g32(const float* r, uint8_t* o, const float* edges, const
   o[30] = amount_bucket_host(r[CCFD_N_FEATURES - 1]);
   o[31] = (uint8_t)stamp;
 }
+
+// G20 rows (ccfd_abi.h): the same bins, 5 bits each, little-endian over 160 bits; the amount
+// bucket at bit 150 and the 6-bit stamp at bit 154.
+inline void encode_row_g20(const float* r, uint8_t* o, const float* edges, const int32_t* offsets, int32_t stamp) {
+  uint32_t w[6] = {0, 0, 0, 0, 0, 0};  // 5 dwords + one spill dword for the funnel below
+  auto put = [&](int bit, uint32_t v) {   // v < 2^6
+    w[bit >> 5] |= v << (bit & 31);
+    if ((bit & 31) + 6 > 32) w[(bit >> 5) + 1] |= v >> (32 - (bit & 31));
+  };
+  for (int j = 0; j < CCFD_N_FEATURES; ++j)
+    put(5 * j, bin_of(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]));
+  put(150, amount_bucket_host(r[CCFD_N_FEATURES - 1]));
+  w[4] |= (uint32_t)(stamp & 63) << (154 - 128);
+  memcpy(o, w, CCFD_G20_ROW_BYTES);
+}
 }  // namespace
 
 namespace ccfd {
@@ -230,6 +245,12 @@ bool g32_table_ok(const float* edges, const int32_t* offsets, int32_t stamp) {
     const int ne = offsets[j + 1] - offsets[j];
     if (offsets[j] < 0 || ne < 0 || ne > 255) return false;
   }
+  return true;
+}
+bool g20_table_ok(const float* edges, const int32_t* offsets, int32_t stamp) {
+  if (stamp > 63 || !g32_table_ok(edges, offsets, stamp)) return false;
+  for (int j = 0; j < CCFD_N_FEATURES; ++j)
+    if (offsets[j + 1] - offsets[j] > CCFD_G20_MAX_EDGES) return false;
   return true;
 }
 }  // namespace ccfd
@@ -245,6 +266,17 @@ extern "C" int64_t ccfd_encode_g32(const float* x, int64_t n, int64_t ld, const 
   return n;
 }
 
+extern "C" int64_t ccfd_encode_g20(const float* x, int64_t n, int64_t ld, const float* edges,
+                                   const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
+  if (ld < CCFD_N_FEATURES || n < 0 || !out || !ccfd::g20_table_ok(edges, offsets, stamp)) return -1;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* r = x + i * ld;
+    encode_row_g20(r, out + i * CCFD_G20_ROW_BYTES, edges, offsets, stamp);
+    if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
+  }
+  return n;
+}
+
 // Internal entry points for the native Kafka consumer (kafka_consumer.cpp).
 namespace ccfd {
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust) {
@@ -253,5 +285,8 @@ bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32
 void encode_w64_row(const float* x, uint8_t* out) { encode_row_w64(x, out); }
 void encode_g32_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp) {
   encode_row_g32(x, out, edges, offsets, stamp);
+}
+void encode_g20_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp) {
+  encode_row_g20(x, out, edges, offsets, stamp);
 }
 }  // namespace ccfd

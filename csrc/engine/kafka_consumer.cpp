@@ -54,7 +54,9 @@ void set_error(const std::string& e);
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust);
 void encode_w64_row(const float* x, uint8_t* out);
 void encode_g32_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp);
+void encode_g20_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp);
 bool g32_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
+bool g20_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
 }  // namespace ccfd
 
 namespace {
@@ -165,7 +167,7 @@ class Consumer {
  public:
   std::vector<std::pair<std::string, int>> seeds;   // bootstrap list
   std::string topic, client = "ccfd-native";
-  int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64, 2 = G32
+  int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64, 2 = G32, 3 = G20
   std::vector<float> g32_edges;                     // G32 bin table (ccfd_kc_set_bins)
   std::vector<int32_t> g32_off;
   int32_t g32_stamp = 0;
@@ -437,13 +439,14 @@ class Consumer {
   }
 
   int row_bytes() const {
-    return wire == 2 ? CCFD_G32_ROW_BYTES : wire ? CCFD_WIRE_ROW_BYTES : CCFD_N_FEATURES * 4;
+    return wire == 3 ? CCFD_G20_ROW_BYTES : wire == 2 ? CCFD_G32_ROW_BYTES : wire ? CCFD_WIRE_ROW_BYTES
+                                                                                : CCFD_N_FEATURES * 4;
   }
 
   // one canonical f32 row into the sink's row format at ring row `row`
   void put_row(int pi, const float* x, uint8_t* dst, int64_t row) {
-    if (wire == 2) {
-      ccfd::encode_g32_row(x, dst, g32_edges.data(), g32_off.data(), g32_stamp);
+    if (wire >= 2) {
+      (wire == 3 ? ccfd::encode_g20_row : ccfd::encode_g32_row)(x, dst, g32_edges.data(), g32_off.data(), g32_stamp);
       if (float* am = sink->amount(pi)) am[row] = x[CCFD_N_FEATURES - 1];
     } else if (wire) {
       ccfd::encode_w64_row(x, dst);
@@ -756,7 +759,10 @@ void* ccfd_kc_create_array(const char* host, int port, const char* topic, const 
 int ccfd_kc_set_bins(void* kc, const float* edges, const int32_t* offsets, int32_t stamp) {
   auto* c = static_cast<Consumer*>(kc);
   if (c->th.joinable()) { ccfd::set_error("kc: set_bins after start"); return -1; }
-  if (!ccfd::g32_table_ok(edges, offsets, stamp)) { ccfd::set_error("kc: bad G32 bin table"); return -1; }
+  if (!(c->wire == 3 ? ccfd::g20_table_ok : ccfd::g32_table_ok)(edges, offsets, stamp)) {
+    ccfd::set_error(c->wire == 3 ? "kc: bad G20 bin table" : "kc: bad G32 bin table");
+    return -1;
+  }
   c->g32_off.assign(offsets, offsets + CCFD_N_FEATURES + 1);
   c->g32_edges.assign(edges, edges + std::max(1, offsets[CCFD_N_FEATURES]));
   c->g32_stamp = stamp;
@@ -766,7 +772,7 @@ int ccfd_kc_set_bins(void* kc, const float* edges, const int32_t* offsets, int32
 int ccfd_kc_start(void* kc) {
   auto* c = static_cast<Consumer*>(kc);
   if (c->th.joinable()) return 0;
-  if (c->wire == 2 && c->g32_stamp == 0) { ccfd::set_error("kc: G32 sink without a bin table"); return -1; }
+  if (c->wire >= 2 && c->g32_stamp == 0) { ccfd::set_error("kc: G32/G20 sink without a bin table"); return -1; }
   c->stop.store(false);
   c->th = std::thread([c] { c->loop(); });
   return 0;

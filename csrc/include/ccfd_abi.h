@@ -39,6 +39,13 @@ enum ccfd_counter_slot {
 // counted in CCFD_CNT_WIRE_STALE and not scored).  Amount itself stays host-side.
 #define CCFD_ARG_WIRE_G32 4
 #define CCFD_G32_ROW_BYTES 32
+// G20 rows (GBDT only, 20 B; flags carry WIRE_G32 | WIRE_G20): the same bins packed 5 bits
+// each for bin tables of <= 31 edges per feature -- bits [5j, 5j+5) = bin of feature j,
+// bits [150, 154) = amount bucket, bits [154, 160) = bin-table stamp (1..63).  Little-endian
+// bit order over the 5 dwords of the row.  0.625x the bytes of a G32 row, equally exact.
+#define CCFD_ARG_WIRE_G20 8
+#define CCFD_G20_ROW_BYTES 20
+#define CCFD_G20_MAX_EDGES 31
 // Diagnostic ablations (CCFD_ABLATE env in the engine; never set by bench.py): skip parts
 // of the epilogue to measure what each costs.  Results are incomplete when set.
 #define CCFD_ARG_ABLATE_COUNTERS 16   // no counter/histogram atomics
@@ -209,7 +216,7 @@ typedef struct ccfd_engine_config {
   int32_t flag_capacity;       // flagged-transaction ring capacity (records)
   int32_t exec_mode;           // 0 = one fused launch per micro-batch, 1 = persistent kernel
   int32_t persist_grid;        // workgroups of the persistent kernel (0 = 256)
-  int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B); 2 = G32 rows (32 B, GBDT)
+  int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B); 2 = G32 rows (32 B, GBDT); 3 = G20 (20 B, GBDT)
   int32_t coalesce;            // launch mode: up to this many ready micro-batches per launch (<= 8)
   int32_t _pad2;
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
@@ -323,6 +330,9 @@ int64_t ccfd_encode_w64(const float* x, int64_t n, int64_t ld, uint8_t* out);
 // `stamp` in 1..255.  amount_out (may be NULL) receives the raw Amount column.  Returns n or -1.
 int64_t ccfd_encode_g32(const float* x, int64_t n, int64_t ld, const float* edges, const int32_t* offsets,
                         int32_t stamp, uint8_t* out, float* amount_out);
+// Same table -> G20 rows (<= 31 edges per feature, stamp 1..63); returns n or -1.
+int64_t ccfd_encode_g20(const float* x, int64_t n, int64_t ld, const float* edges, const int32_t* offsets,
+                        int32_t stamp, uint8_t* out, float* amount_out);
 
 // ---------------------------------------------------------------------------
 // Native Kafka consumer (csrc/engine/kafka_consumer.cpp): Metadata v1 -> one connection
@@ -366,7 +376,7 @@ const char* ccfd_kc_last_error(void* kc);
 int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n);   // tests / fuzzing
 int ccfd_kc_set_offset_reset(void* kc, int policy);                           // before start
 int64_t ccfd_kc_position(void* kc, int part_index);                           // next offset to fetch
-// G32 sinks (wire = 2): the bin table rows are encoded against (ccfd_encode_g32 layout);
+// G32 / G20 sinks (wire = 2 / 3): the bin table rows are encoded against (ccfd_encode_g32 layout);
 // required before ccfd_kc_start.  The table is copied.
 int ccfd_kc_set_bins(void* kc, const float* edges, const int32_t* offsets, int32_t stamp);
 

@@ -28,7 +28,11 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream) {
   if (a->n == 0) return 0;
   if (a->flags & CCFD_ARG_WIRE_G32) {
     if (a->model != CCFD_MODEL_GBDT) { set_error("G32 rows: GBDT kernel only"); return -3; }
-    if (reinterpret_cast<uintptr_t>(a->x) & 15) { set_error("G32 rows must be 16-byte aligned"); return -3; }
+    const bool g20 = (a->flags & CCFD_ARG_WIRE_G20) != 0;     // dword loads: 4-byte aligned rows
+    if (reinterpret_cast<uintptr_t>(a->x) & (g20 ? 3 : 15)) {
+      set_error(g20 ? "G20 rows must be 4-byte aligned" : "G32 rows must be 16-byte aligned");
+      return -3;
+    }
     const int rc = launch_gbdt_g32(*a, reinterpret_cast<hipStream_t>(stream));
     if (rc == -2) set_error("G32 launch: bad tree shape (depth 1..8, leaf tables <= 64 KB)");
     else if (rc != 0) set_error(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));

@@ -75,6 +75,58 @@ __device__ __forceinline__ unsigned g32_byte(const G32Row& r, int j) {   // j co
   return (w >> (8 * (j & 3))) & 0xffu;
 }
 
+// G20 rows (ccfd_abi.h: 30 bins of 5 bits, amount bucket at bit 150, 6-bit stamp at bit
+// 154) -- 5 dwords a row, a 64-row chunk is 1280 B.  Lane l fetches dwords 64k + l (k < 5):
+// every load instruction is one contiguous 256 B wave request, and only 4-byte alignment is
+// needed wherever a micro-batch starts in the log.  Dwords past the batch are clamped to
+// its last dword (never scored).  The row lands in r.lo.xyzw, r.hi.x.
+constexpr int kG20Words = CCFD_G20_ROW_BYTES / 4;
+
+__device__ __forceinline__ void g20_fetch(const unsigned char* __restrict__ x, int n, int chunk, int lane,
+                                          G32Row& r) {
+  const unsigned* __restrict__ xw = reinterpret_cast<const unsigned*>(x);
+  const long last = (long)n * kG20Words - 1;
+  const long w0 = (long)chunk * (kG32Rows * kG20Words) + lane;
+  r.lo.x = xw[min(w0, last)];
+  r.lo.y = xw[min(w0 + 64, last)];
+  r.lo.z = xw[min(w0 + 128, last)];
+  r.lo.w = xw[min(w0 + 192, last)];
+  r.hi.x = xw[min(w0 + 256, last)];
+}
+
+// Wave-private LDS transpose of a G20 chunk: dword 64k + l is written by lane l, lane l then
+// reads its row's dwords 5l .. 5l+4 (stride 5: conflict-free over the 32 banks).
+__device__ __forceinline__ void g20_rows(uint4* __restrict__ t4, int lane, G32Row& r) {
+  unsigned* t = reinterpret_cast<unsigned*>(t4);
+  t[lane] = r.lo.x;
+  t[64 + lane] = r.lo.y;
+  t[128 + lane] = r.lo.z;
+  t[192 + lane] = r.lo.w;
+  t[256 + lane] = r.hi.x;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const unsigned* q = t + kG20Words * lane;
+  r.lo.x = q[0];
+  r.lo.y = q[1];
+  r.lo.z = q[2];
+  r.lo.w = q[3];
+  r.hi.x = q[4];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// Lift a transposed G20 row's 30 five-bit bins (compile-time offsets: one v_bfe, or a
+// v_alignbit + v_and where a field straddles two dwords); returns bucket | stamp << 8.
+__device__ __forceinline__ unsigned g20_lift(const G32Row& r, unsigned (&b)[kF]) {
+  const unsigned w[kG20Words + 1] = {r.lo.x, r.lo.y, r.lo.z, r.lo.w, r.hi.x, 0u};
+#pragma unroll
+  for (int j = 0; j < kF; ++j) {
+    const int bit = 5 * j, wi = bit >> 5, sh = bit & 31;
+    b[j] = (sh + 5 <= 32 ? (w[wi] >> sh) : __builtin_amdgcn_alignbit(w[wi + 1], w[wi], sh)) & 31u;
+  }
+  return ((r.hi.x >> 22) & 0xfu) | ((r.hi.x >> 26) << 8);
+}
+
 typedef const __attribute__((address_space(4))) int* g32_cint_p;   // split params -> s_load
 
 // Sum of the T trees' leaves for R row chains whose bins are lifted into b0 (/ b1).  Per
@@ -124,6 +176,23 @@ __device__ __forceinline__ unsigned g32_lift(const G32Row& r, unsigned (&b)[kF])
 #pragma unroll
   for (int j = 0; j < kF; ++j) b[j] = g32_byte(r, j);
   return r.hi.w >> 16;
+}
+
+// Row-format policy of the binned-row kernels: G32 (u8 bins) or G20 (5-bit bins).
+template <bool kG20>
+__device__ __forceinline__ void gx_fetch(const unsigned char* __restrict__ x, int n, int chunk, int lane, G32Row& r) {
+  if constexpr (kG20) g20_fetch(x, n, chunk, lane, r);
+  else g32_fetch(x, n, chunk, lane, r);
+}
+template <bool kG20>
+__device__ __forceinline__ void gx_rows(uint4* __restrict__ t, int lane, G32Row& r) {
+  if constexpr (kG20) g20_rows(t, lane, r);
+  else g32_rows(t, lane, r);
+}
+template <bool kG20>
+__device__ __forceinline__ unsigned gx_lift(const G32Row& r, unsigned (&b)[kF]) {
+  if constexpr (kG20) return g20_lift(r, b);
+  else return g32_lift(r, b);
 }
 
 // Stage the T * 2^D leaf table (blob section after feat / kbin) into LDS.

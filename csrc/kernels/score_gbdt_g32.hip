@@ -1,10 +1,10 @@
-// G32 oblivious-GBDT scorer, one launch per micro-batch (engine exec_mode = 0, score_sync).
+// G32 / G20 oblivious-GBDT scorer, one launch per micro-batch (engine exec_mode = 0, score_sync).
 // Row format, level form and layout: g32_core.h; persistent variant: score_gbdt_g32_persist.hip.
 #include "g32_core.h"
 
 namespace ccfd {
 
-template <int D, int R, bool kR, bool kGL>
+template <int D, int R, bool kR, bool kGL, bool kG20>
 __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) {
   extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L floats
   __shared__ uint4 xt[kG32Waves][128];                         // per-wave chunk transpose
@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
   // rows first: the host-memory latency overlaps the leaf staging below
   G32Row pre[R];
 #pragma unroll
-  for (int q = 0; q < R; ++q) g32_fetch(xb, n, grp * R + q, lane, pre[q]);
+  for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, grp * R + q, lane, pre[q]);
 
   epi_init(epi);
   stamp_start(a, blockIdx.x);
@@ -48,19 +48,19 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
     // separate 1-D arrays per row chain: indexed by a runtime (wave-uniform) feature id they
     // stay in VGPRs (v_movrel); a 2-D array would be demoted to scratch
     unsigned b0[kF], b1[kF];
-    unsigned meta[R];                                           // bytes 30, 31: bucket, stamp
+    unsigned meta[R];                                           // bucket | stamp << 8
     G32Row cur = pre[0];
-    g32_rows(xt[wave], lane, cur);
-    meta[0] = g32_lift(cur, b0);
+    gx_rows<kG20>(xt[wave], lane, cur);
+    meta[0] = gx_lift<kG20>(cur, b0);
     if constexpr (R == 2) {
       cur = pre[1];
-      g32_rows(xt[wave], lane, cur);
-      meta[1] = g32_lift(cur, b1);
+      gx_rows<kG20>(xt[wave], lane, cur);
+      meta[1] = gx_lift<kG20>(cur, b1);
     }
     const int nxt = grp + gstride;
     if (nxt < ngroups) {
 #pragma unroll
-      for (int q = 0; q < R; ++q) g32_fetch(xb, n, nxt * R + q, lane, pre[q]);
+      for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, nxt * R + q, lane, pre[q]);
     }
     float acc[R];
     g32_trees<D, R>(b0, b1, leaves, feat, kbin, T, acc);
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
 // Grid: one wave per R-chunk group, capped at CCFD_G32_WGS_PER_CU workgroups per CU (grid-
 // stride beyond).  A 65536-row micro-batch is 1024 chunks = 256 workgroups at R = 1: every
 // CU has its rows in flight at once.  CCFD_G32_R: 64-row chunks per wave step (1 | 2).
-template <int D, int R>
+template <int D, int R, bool kG20>
 static void launch_g32_r(const ccfd_score_args& a, hipStream_t s) {
   constexpr int L = 1 << D;
   const int wgs_per_cu = g32_env("CCFD_G32_WGS_PER_CU", 4, 1, 8);   // read per launch: sweepable in-process
@@ -117,19 +117,23 @@ static void launch_g32_r(const ccfd_score_args& a, hipStream_t s) {
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds / 2 || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * L * sizeof(float);
   if (gl) {
-    if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, true>), dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false, true>), dim3(grid), dim3(256), 0, s, a);
+    if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, true, kG20>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false, true, kG20>), dim3(grid), dim3(256), 0, s, a);
   } else {
-    if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, false>), dim3(grid), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false, false>), dim3(grid), dim3(256), lds, s, a);
+    if (a.rules) hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, true, false, kG20>), dim3(grid), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((score_gbdt_g32_kernel<D, R, false, false, kG20>), dim3(grid), dim3(256), lds, s, a);
   }
 }
 
 template <int D>
 static void launch_g32_d(const ccfd_score_args& a, hipStream_t s) {
+  if (a.flags & CCFD_ARG_WIRE_G20) {             // G20: one chunk per wave step
+    launch_g32_r<D, 1, true>(a, s);
+    return;
+  }
   const int r = g32_env("CCFD_G32_R", 1, 1, 2);
-  if (r == 2) launch_g32_r<D, 2>(a, s);
-  else launch_g32_r<D, 1>(a, s);
+  if (r == 2) launch_g32_r<D, 2, false>(a, s);
+  else launch_g32_r<D, 1, false>(a, s);
 }
 
 int launch_gbdt_g32(const ccfd_score_args& a, hipStream_t s) {

@@ -1,4 +1,4 @@
-// G32 oblivious-GBDT scorer, persistent variant (engine exec_mode = 1; protocol in
+// G32 / G20 oblivious-GBDT scorer, persistent variant (engine exec_mode = 1; protocol in
 // persist_core.h; row format and level form in g32_core.h).  The leaf tables
 // are staged into LDS ONCE per resident workgroup (a launch per micro-batch re-stages them
 // in every workgroup), and a claimed item is 4 waves x `cpw` 64-row chunks, the next chunk
@@ -8,7 +8,7 @@
 
 namespace ccfd {
 
-template <int D, bool kR, bool kGL>
+template <int D, bool kR, bool kGL, bool kG20>
 __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args a) {
   extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L floats
   __shared__ uint4 xt[kG32Waves][128];
@@ -45,9 +45,9 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   unsigned long long psum = 0;
   auto score_chunk = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, G32Row& cur)
       __attribute__((always_inline)) {
-    g32_rows(xt[wave], lane, cur);
+    gx_rows<kG20>(xt[wave], lane, cur);
     unsigned b0[kF];
-    const unsigned meta = g32_lift(cur, b0);
+    const unsigned meta = gx_lift<kG20>(cur, b0);
     float acc[1];
     g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
     const int row = chunk * kG32Rows + lane;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
 #pragma unroll
       for (int k = 0; k < CPW; ++k) {
         const int chunk = c0 + kG32Waves * k;
-        if (chunk * kG32Rows < n) g32_fetch(xb, n, chunk, lane, r[k]);
+        if (chunk * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk, lane, r[k]);
       }
 #pragma unroll
       for (int k = 0; k < CPW; ++k) {
@@ -117,13 +117,13 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     };
     if (a.flags & CCFD_ARG_CHUNK_RING) {                  // default: one chunk ahead
       G32Row pre;
-      if (c0 * kG32Rows < n) g32_fetch(xb, n, c0, lane, pre);
+      if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre);
 #pragma unroll 1
       for (int k = 0; k < cpw; ++k) {
         const int chunk = c0 + kG32Waves * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
         G32Row cur_row = pre;
-        if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) g32_fetch(xb, n, chunk + kG32Waves, lane, pre);
+        if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kG32Waves, lane, pre);
         score_chunk(d, slot, n, chunk, cur_row);
       }
     } else if (cpw == 1) {
@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   }
 }
 
-template <int D>
-static int launch_persist_g32_d(const ccfd_persist_args& a0, int grid, hipStream_t s) {
+template <int D, bool kG20>
+static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream_t s) {
   ccfd_persist_args a = a0;
   // one-chunk prefetch ring by default: at BASELINE config 4 (65536-row batches) it measured
   // 1.67e9 tx/s at p50 107 us (depth 3) vs 1.64e9 with the whole item in flight (VALU-heavy
@@ -148,13 +148,19 @@ static int launch_persist_g32_d(const ccfd_persist_args& a0, int grid, hipStream
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
   if (gl) {
-    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, true>), dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, true>), dim3(grid), dim3(256), 0, s, a);
+    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, true, kG20>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, true, kG20>), dim3(grid), dim3(256), 0, s, a);
   } else {
-    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, false>), dim3(grid), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, false>), dim3(grid), dim3(256), lds, s, a);
+    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, false, kG20>), dim3(grid), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, false, kG20>), dim3(grid), dim3(256), lds, s, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+template <int D>
+static int launch_persist_g32_d(const ccfd_persist_args& a, int grid, hipStream_t s) {
+  return (a.flags & CCFD_ARG_WIRE_G20) ? launch_persist_g32_f<D, true>(a, grid, s)
+                                       : launch_persist_g32_f<D, false>(a, grid, s);
 }
 
 int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s) {

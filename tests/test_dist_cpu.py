@@ -268,20 +268,20 @@ def _model_worker(rank, world, port, q):
     try:
         out = {}
         X, _ = generate(4000, seed=5)
-        for kind in ("gbdt", "mlp"):
-            fmt = resolve_row_format(kind)
+        for key, kind, wire in (("gbdt", "gbdt", "auto"), ("gbdt_g32", "gbdt", "g32"), ("mlp", "mlp", "auto")):
+            fmt = resolve_row_format(kind, wire)
             m = build_model(kind, seed=3, X_ref=X) if ctx.rank == 0 else None
             dm = broadcast_model(ctx, m, kind, fmt)
             enc = dm.bins.encode(X[:100]).tobytes() if dm.bins is not None else b""
-            out[kind] = (fmt, bytes(dm.blob.numpy()), dm.trees, dm.depth, dm.row_format, enc)
+            out[key] = (fmt, bytes(dm.blob.numpy()), dm.trees, dm.depth, dm.row_format, enc)
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
 def test_broadcast_model_carries_g32_bin_table():
-    """X1 of a whole device model: every rank gets the same blob, tree shape and (G32) bin
-    table, so every rank encodes its own partition logs identically."""
+    """X1 of a whole device model: every rank gets the same blob, tree shape and (G20 by
+    default, or G32) bin table, so every rank encodes its own partition logs identically."""
     world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
@@ -295,5 +295,7 @@ def test_broadcast_model_carries_g32_bin_table():
         assert p.exitcode == 0
     assert res[0] == res[1]
     fmt, blob, trees, depth, row_format, enc = res[0]["gbdt"]
+    assert fmt == row_format == "g20" and blob[:4] == b"GBB1" and (trees, depth) == (100, 6) and len(enc) == 2000
+    fmt, blob, trees, depth, row_format, enc = res[0]["gbdt_g32"]
     assert fmt == row_format == "g32" and blob[:4] == b"GBB1" and (trees, depth) == (100, 6) and len(enc) == 3200
     assert res[0]["mlp"][0] == res[0]["mlp"][4] == "w64"

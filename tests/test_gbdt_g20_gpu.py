@@ -1,0 +1,162 @@
+"""G20 rows (GBDT bins packed 5 bits each, csrc/kernels/g32_core.h g20_*): the launch and
+persistent binned-row kernels choose exactly the f32 oracle's leaves on 20-byte rows, at any
+4-byte-aligned start, counters and histogram exact, stale stamps detected, and broadcast_model
+widens G20 -> G32 when an ensemble's table needs more than 31 edges a feature
+(BASELINE.json configs[3])."""
+import numpy as np
+import pytest
+import torch
+
+from ccfd_demo_summit_amd.data import generate
+from ccfd_demo_summit_amd.models import build_model
+
+from test_kernels_gpu import _check_counters
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(seed, X_ref, trees=100, depth=6, rate=0.01):
+    m = build_model("gbdt", seed=seed, X_ref=X_ref, gbdt_trees=trees, gbdt_depth=depth, calibrate_rate=rate)
+    assert m.bin_spec().fits_g20, "test ensemble must fit 5-bit bins"
+    return m
+
+
+@pytest.fixture(scope="module")
+def data():
+    X, _ = generate(65536 + 7, seed=51)
+    X[3, 5] = np.nan
+    X[4, 2] = np.inf
+    X[5, 7] = -np.inf
+    return X
+
+
+@pytest.mark.parametrize("n", [1, 31, 4097, 65543])
+@pytest.mark.parametrize("depth", [6, 3, 8])
+def test_g20_kernel_exact(gpu, data, n, depth):
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X = data[:n]
+    m = _model(3, generate(5000, seed=2)[0], trees=100 if depth != 8 else 40, depth=depth)
+    dm = DeviceModel(m, gpu, bins="g20")
+    assert dm.row_format == "g20"
+    rows = torch.from_numpy(dm.bins.encode(X)).to(gpu)
+    cnt = new_counters(gpu)
+    p, r = score(dm, rows, 0.5, counters=cnt)
+    torch.cuda.synchronize(gpu)
+    p, r = p.cpu().numpy(), r.cpu().numpy()
+    ref = m.predict_proba(X)
+    assert np.abs(p - ref).max() < 1e-5
+    np.testing.assert_array_equal(r, (ref >= 0.5).astype(np.uint8))
+    _check_counters(cnt, p, r, X)
+    assert int(cnt[4]) == 0
+
+
+def test_g20_unaligned_start_and_stale_stamp(gpu, data):
+    """A batch starting at row 1 of a buffer is only 4-byte aligned (20 B rows): the dword
+    loads still read it exactly; rows of another stamp are counted, not scored."""
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
+    X = data[:4098]
+    m = _model(6, X)
+    dm = DeviceModel(m, gpu, bins="g20")
+    enc = dm.bins.encode(X)
+    st = dm.bins.stamp
+    bad_stamp = (st % 63) + 1
+    enc[101:201, 19] = (enc[101:201, 19] & 0x03) | (bad_stamp << 2)   # stamp = bits 154..159
+    enc[301, :] = 0
+    full = torch.from_numpy(enc).to(gpu)
+    view = full[1:]
+    assert view.data_ptr() % 16 == 4
+    cnt = new_counters(gpu)
+    p, r = score(dm, view, 0.5, counters=cnt)
+    torch.cuda.synchronize(gpu)
+    p, r = p.cpu().numpy(), r.cpu().numpy()
+    assert int(cnt[4]) == 101 and int(cnt[0]) == 4097
+    assert np.isnan(p[100:200]).all() and np.isnan(p[300]) and not r[100:200].any()
+    ok = np.ones(4097, bool)
+    ok[100:200] = False
+    ok[300] = False
+    assert np.abs(p[ok] - m.predict_proba(X[1:])[ok]).max() < 1e-5
+
+
+@pytest.mark.parametrize("input_mode,exec_mode", [("zerocopy", "launch"), ("dma", "launch"),
+                                                   ("zerocopy", "persistent"), ("dma", "persistent")])
+def test_g20_engine_pump_exact(gpu, input_mode, exec_mode):
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    B = 8192
+    X, _ = generate(B * 4 + 100, seed=54)
+    m = _model(8, X[:20000])
+    dm = DeviceModel(m, gpu, bins="g20")
+    eng = StreamEngine(dm, batch=B, depth=4, streams=2, input_mode=input_mode, exec_mode=exec_mode)
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 7, bins=dm.bins)
+    assert log.row_format == "g20" and log.row_bytes == 20
+    eng.add_log(0, log)
+    st = eng.pump(4)
+    assert st.rows == 4 * B
+    ref = m.predict_proba(X[:4 * B]) >= 0.5
+    fl = eng.drain_flagged()
+    got = np.zeros(4 * B, bool)
+    got[(fl["tx_id"] - 7).astype(np.int64)] = True
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_allclose(fl["amount"], X[(fl["tx_id"] - 7).astype(np.int64), 29])
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    c = c.cpu().numpy()
+    assert c[0] == 4 * B and c[1] == ref.sum() and c[4] == 0
+    p, _ = eng.score(X[:1000])
+    assert np.abs(p - m.predict_proba(X[:1000])).max() < 1e-5
+    eng.close()
+    log.free()
+
+
+@pytest.mark.parametrize("inflight", ["0", "1"])
+@pytest.mark.parametrize("item_rows", [256, 1024])
+def test_g20_persistent_partial_batches_exact(gpu, monkeypatch, inflight, item_rows):
+    """Both persistent item loops, partial micro-batches starting at rows that are not a
+    multiple of 4 (4-byte-aligned G20 rows): every row scored once, routes exact."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    monkeypatch.setenv("CCFD_G32_INFLIGHT", inflight)
+    monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
+    B = 8192
+    X, _ = generate(B * 3 + 3000, seed=55)
+    m = _model(10, X[:20000], rate=0.05)
+    dm = DeviceModel(m, gpu, bins="g20")
+    eng = StreamEngine(dm, batch=B, depth=3, streams=1, exec_mode="persistent")
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 7, bins=dm.bins)
+    eng.add_log(0, log)
+    n = 1301 + B + 2 * 1303
+    assert eng.pump(1, batch_rows=1301).rows + eng.pump(1).rows + eng.pump(2, batch_rows=1303).rows == n
+    pr = m.predict_proba(X[:n])
+    fl = eng.drain_flagged()
+    got = np.zeros(n, bool)
+    got[(fl["tx_id"] - 7).astype(np.int64)] = True
+    np.testing.assert_array_equal(got, pr >= 0.5)
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    c = c.cpu().numpy()
+    assert c[0] == n and c[1] == (pr >= 0.5).sum() and c[4] == 0
+    assert int(c[8:22].sum() + c[24:38].sum()) == n
+    eng.close()
+    log.free()
+
+
+def test_broadcast_model_widens_g20_to_g32(gpu):
+    """> 31 thresholds on a feature: G20 is impossible, broadcast_model hands out a G32 model."""
+    from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT
+    from ccfd_demo_summit_amd.ops.kernels import score
+    from ccfd_demo_summit_amd.parallel import broadcast_model, init_distributed
+    X, _ = generate(30000, seed=57)
+    T = 40
+    feat = np.zeros((T, 2), np.int32)                 # 80 thresholds on feature 0
+    thr = np.quantile(X[:, 0], np.linspace(0.01, 0.99, 2 * T)).astype(np.float32).reshape(T, 2)
+    rng = np.random.default_rng(3)
+    m = ObliviousGBDT(feat, thr, (rng.standard_normal((T, 4)) * 0.05).astype(np.float32), -1.0)
+    ctx = init_distributed()
+    with pytest.warns(UserWarning, match="G20 rows impossible"):
+        dm = broadcast_model(ctx, m, "gbdt", "g20")
+    assert dm.row_format == "g32"
+    p, _ = score(dm, torch.from_numpy(dm.bins.encode(X[:5000])).to(gpu))
+    torch.cuda.synchronize(gpu)
+    assert np.abs(p.cpu().numpy() - m.predict_proba(X[:5000])).max() < 2e-5

@@ -1,5 +1,5 @@
 """Native Kafka consumer (csrc/engine/kafka_consumer.cpp) against kafka-lite on 127.0.0.1:
-TXB1 batches and JSON transactions land in the sink rows bit-exactly (f32, W64 and G32),
+TXB1 batches and JSON transactions land in the sink rows bit-exactly (f32, W64, G32 and G20),
 offsets become committable once rows are consumed, CRC-corrupted batches are rejected."""
 import json
 import time
@@ -31,7 +31,7 @@ def _wait(kc, rows, timeout=20):
     return False
 
 
-@pytest.mark.parametrize("fmt", ["f32", "w64", "g32"])
+@pytest.mark.parametrize("fmt", ["f32", "w64", "g32", "g20"])
 def test_txb1_and_json_into_rows(lite, fmt):
     kb = KafkaBroker(lite.bootstrap)
     kb.create_topic("odh-demo", 2)
@@ -45,7 +45,7 @@ def test_txb1_and_json_into_rows(lite, fmt):
     msgs = [json.dumps({"id": int(ids[i]), "customer_id": int(cu[i]),
                         **{n: float(v) for n, v in zip(FEATURE_NAMES, X[i])}}).encode() for i in range(200)]
     kb.produce_many("odh-demo", msgs, partition=1)
-    bins = build_model("gbdt", seed=2, X_ref=X).bin_spec() if fmt == "g32" else None
+    bins = build_model("gbdt", seed=2, X_ref=X).bin_spec(bits=8 if fmt == "g32" else 5) if fmt[0] == "g" else None
     kc = NativeKafkaConsumer.for_arrays(lite.bootstrap, "odh-demo", {0: 0, 1: 0}, capacity=4000, wire=fmt == "w64",
                                         bins=bins).start()
     try:
@@ -55,8 +55,9 @@ def test_txb1_and_json_into_rows(lite, fmt):
         f0, i0, c0 = kc.arrays[0]
         f1, i1, c1 = kc.arrays[1]
         want = {"f32": lambda: X, "w64": lambda: encode_wire(X).view(np.float32).reshape(-1, 16),
-                "g32": lambda: bins.encode(X).view(np.float32).reshape(-1, 8)}[fmt]()
-        if fmt == "g32":             # G32 rows keep Amount host-side (flagged-record column)
+                "g32": lambda: bins.encode(X).view(np.float32).reshape(-1, 8),
+                "g20": lambda: bins.encode(X).view(np.float32).reshape(-1, 5)}[fmt]()
+        if fmt[0] == "g":            # G32 / G20 rows keep Amount host-side (flagged-record column)
             np.testing.assert_array_equal(kc.amounts[0][:3000], X[:, 29])
             np.testing.assert_array_equal(kc.amounts[1][:200], X[:200, 29])
         np.testing.assert_array_equal(f0[:3000], want)

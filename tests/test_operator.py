@@ -51,7 +51,7 @@ def test_cr_fields_drive_the_rendering():
     assert validate(ms) == []
     by = {(m["kind"], m["metadata"]["name"]): m for m in ms}
     env = by[("ConfigMap", "ccfd-env")]["data"]
-    assert env["BROKER_URL"].count(",") == 4 and env["CCFD_WIRE"] == "g32" and env["CCFD_MODEL"] == "gbdt"
+    assert env["BROKER_URL"].count(",") == 4 and env["CCFD_WIRE"] == "g20" and env["CCFD_MODEL"] == "gbdt"
     eng = by[("StatefulSet", "ccfd-engine")]
     c = eng["spec"]["template"]["spec"]["containers"][0]
     assert eng["spec"]["replicas"] == 2 and c["resources"]["limits"]["amd.com/gpu"] == 4

@@ -140,3 +140,60 @@ def test_g32_blob_and_spec_roundtrip():
         m.pack(bins=narrow)
     with pytest.raises(ValueError):
         BinSpec([np.arange(300, dtype=np.float32)] + [np.zeros(0, np.float32)] * 29)
+
+
+# ---------------------------------------------------------------------------------------
+# G20 rows: the same bins packed 5 bits each (<= 31 edges a feature), equally exact
+def _g20_case(seed=0, n=20000):
+    X, m = _g32_case(seed=seed, n=n)
+    keep = m.bin_spec()
+    if not keep.fits_g20:                     # a 100 x 6 draw can exceed 31 on one feature
+        m = type(m)(m.feat[:60], m.thr[:60], m.leaves[:60], m.base)
+    return X, m
+
+
+def test_g20_bins_reproduce_every_split_decision():
+    from ccfd_demo_summit_amd.contracts import decode_g20_bins
+    X, m = _g20_case()
+    spec = m.bin_spec(bits=5)
+    assert spec.row_format == "g20" and 1 <= spec.stamp <= 63
+    rows = spec.encode(X)
+    assert rows.shape == (X.shape[0], 20)
+    g = decode_g20_bins(rows)
+    g32 = m.bin_spec().encode(X)
+    np.testing.assert_array_equal(g[:, :31], g32[:, :31])       # bins + amount bucket
+    assert (g[:, 31] == spec.stamp).all()
+    np.testing.assert_array_equal(m.leaf_index_g32(rows, spec), m.leaf_index(X))
+
+
+def test_g20_native_encoder_matches_numpy_oracle():
+    from ccfd_demo_summit_amd.engine.stream_engine import G20_ROW_F32, encode_g32
+    X, m = _g20_case(seed=1)
+    spec = m.bin_spec(bits=5)
+    out = np.empty((X.shape[0], G20_ROW_F32), np.float32)
+    am = np.empty(X.shape[0], np.float32)
+    encode_g32(X, spec, out.ctypes.data, am.ctypes.data)
+    np.testing.assert_array_equal(out.view(np.uint8), spec.encode(X))
+    np.testing.assert_array_equal(am, X[:, 29])
+
+
+def test_g20_spec_limits_and_roundtrip():
+    from ccfd_demo_summit_amd.models.gbdt import BinSpec
+    X, m = _g20_case(seed=2)
+    spec = m.bin_spec(bits=5)
+    s2 = BinSpec.from_bytes(spec.to_bytes(), bits=5)
+    assert s2.stamp == spec.stamp and s2.row_format == "g20"
+    edges = [np.arange(32, dtype=np.float32)] + [np.zeros(0, np.float32)] * 29
+    with pytest.raises(ValueError, match="5 bits"):
+        BinSpec(edges, bits=5)
+    assert not BinSpec(edges).fits_g20
+    from ccfd_demo_summit_amd.ops._lib import lib
+    import ctypes as C
+    flat, off = BinSpec(edges).flat, BinSpec(edges).offsets
+    out = np.zeros((4, 20), np.uint8)
+    # the native encoder refuses a table a 5-bit field cannot index, and stamps past 63
+    assert lib().ccfd_encode_g20(X.ctypes.data, 4, 30, flat.ctypes.data, off.ctypes.data, 5,
+                                 C.c_void_p(out.ctypes.data), None) == -1
+    f2, o2 = spec.flat, spec.offsets
+    assert lib().ccfd_encode_g20(X.ctypes.data, 4, 30, f2.ctypes.data, o2.ctypes.data, 64,
+                                 C.c_void_p(out.ctypes.data), None) == -1
