@@ -61,7 +61,7 @@ def parse_args(argv=None):
     ap.add_argument("--trace", default=None,
                     help="rank 0: write a Chrome / Perfetto timeline of the last 65536 timed micro-batches "
                          "(per-batch stage trace: queued, in flight, device, hand-off)")
-    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 128 otherwise)")
+    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 192 for G20, 128 otherwise)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64", "g32", "g20"],
@@ -256,7 +256,10 @@ def main(argv=None):
     if args.depth is None:
         # gbdt: 3 micro-batches saturate PCIe for BASELINE's 100 x 6; ensembles past 1200 tree
         # levels a row are VALU-bound and need 6 in flight (profiles/r2/g32_large_ensembles/)
-        args.depth = (6 if args.gbdt_trees * args.gbdt_depth > 1200 else 3) if args.model == "gbdt" else 12
+        # G20 rows (1.6x the rows per byte of G32): 4 in flight (2.51e9 vs 2.31e9 tx/s at 3,
+        # profiles/r2/g20/sweep.txt)
+        args.depth = (6 if args.gbdt_trees * args.gbdt_depth > 1200 else 4 if args.wire == "g20" else 3) \
+            if args.model == "gbdt" else 12
     import torch
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine

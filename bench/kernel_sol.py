@@ -91,11 +91,11 @@ def main():
     for kind, wire in cases:
         m = build_model(kind, seed=0, X_ref=X[:100_000], calibrate_rate=0.01, gbdt_trees=args.gbdt_trees,
                         gbdt_depth=args.gbdt_depth)
-        dm = DeviceModel(m, dev, wire=(wire == "w64"), bins=True if wire == "g32" else None)
-        if wire == "g32":
+        dm = DeviceModel(m, dev, wire=(wire == "w64"), bins=wire if wire in ("g32", "g20") else None)
+        if wire in ("g32", "g20"):
             xg = torch.from_numpy(dm.bins.encode(X)).to(dev).repeat(reps, 1)[:nmax].contiguous()
-        x_all = {"w64": xw, "g32": xg}.get(wire, xf)
-        in_bytes = {"w64": 64, "g32": 32}.get(wire, 120)
+        x_all = {"w64": xw, "g32": xg, "g20": xg}.get(wire, xf)
+        in_bytes = {"w64": 64, "g32": 32, "g20": 20}.get(wire, 120)
         host_rows = None
         if args.host:
             from ccfd_demo_summit_amd.engine import PinnedArray

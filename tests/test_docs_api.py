@@ -31,4 +31,4 @@ def test_api_doc_gpu_blocks_run(gpu, tmp_path, monkeypatch):
     exec(b[1], ns)
     assert ns["st"].rows == 100 * 4096 and ns["proba"].shape == (1000,)
     exec(b[2], ns)
-    assert ns["dm"].row_format == "g32" and ns["mine"]
+    assert ns["dm"].row_format == "g20" and ns["mine"]
