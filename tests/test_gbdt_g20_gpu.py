@@ -160,3 +160,53 @@ def test_broadcast_model_widens_g20_to_g32(gpu):
     p, _ = score(dm, torch.from_numpy(dm.bins.encode(X[:5000])).to(gpu))
     torch.cuda.synchronize(gpu)
     assert np.abs(p.cpu().numpy() - m.predict_proba(X[:5000])).max() < 2e-5
+
+
+@pytest.mark.parametrize("exec_mode", ["launch", "persistent"])
+def test_g20_rules_hot_swap_and_global_leaves(gpu, exec_mode):
+    """The kernels' other G20 instantiations: proba-only routing rules (kR), a hot swap inside
+    the live bin table, and a 70 x 8 ensemble whose 17920 leaves exceed both LDS stages (kGL)."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel, DeviceRules
+    from ccfd_demo_summit_amd.router.rules import RuleSet
+    B = 8192
+    X, _ = generate(B * 3, seed=58)
+    # rules
+    m = _model(12, X[:20000], rate=0.05)
+    dm = DeviceModel(m, gpu, bins="g20")
+    rs = RuleSet.parse("when proba >= 0.8 then fraud\nwhen proba < 0.001 then fraud\notherwise standard")
+    eng = StreamEngine(dm, batch=B, depth=3, streams=1, exec_mode=exec_mode, rules=DeviceRules(rs, gpu))
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64), bins=dm.bins)
+    eng.add_log(0, log)
+    st = eng.pump(3)
+    p = m.predict_proba(X)
+    want = rs.evaluate(p).astype(bool)
+    got = np.zeros(len(X), bool)
+    got[eng.drain_flagged()["tx_id"].astype(np.int64)] = True
+    clear = (np.abs(p - 0.8) > 1e-5) & (np.abs(p - 0.001) > 1e-6)
+    np.testing.assert_array_equal(got[clear], want[clear])
+    assert st.fraud_rows == got.sum() and st.rows == len(X)
+    # hot swap: a permuted, rescaled ensemble packed against the live table
+    perm = np.random.default_rng(0).permutation(m.n_trees)
+    m2 = ObliviousGBDT(m.feat[perm], m.thr[perm], (m.leaves[perm] * 1.5).astype(np.float32), m.base)
+    eng.swap_model(DeviceModel(m2, gpu, bins=dm.bins))
+    p2, _ = eng.score(X[:2000])
+    assert np.abs(p2 - m2.predict_proba(X[:2000])).max() < 1e-5
+    eng.close()
+    log.free()
+    # leaves gathered from global memory
+    big = build_model("gbdt", seed=13, X_ref=X[:20000], gbdt_trees=70, gbdt_depth=8, calibrate_rate=0.02)
+    assert big.bin_spec().fits_g20 and big.n_trees * (1 << big.depth) > 16384
+    dmb = DeviceModel(big, gpu, bins="g20")
+    eng = StreamEngine(dmb, batch=B, depth=3, streams=1, exec_mode=exec_mode)
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 7, bins=dmb.bins)
+    eng.add_log(0, log)
+    n = 2 * B + 1234
+    assert eng.pump(2).rows + eng.pump(1, batch_rows=1234).rows == n
+    fl = eng.drain_flagged()
+    got = np.zeros(n, bool)
+    got[(fl["tx_id"] - 7).astype(np.int64)] = True
+    np.testing.assert_array_equal(got, big.predict_proba(X[:n]) >= 0.5)
+    eng.close()
+    log.free()
