@@ -128,7 +128,7 @@ class GpuEngineCollector:
         rows.add_metric([self.rank_label], float(cnt[0]))
         yield rows
         stale = CounterMetricFamily(M.GPU_PREFIX + "wire_stale_rows",
-                                    "G32 rows refused for another bin table's stamp (never scored)", labels=["rank"])
+                                    "G32 / G20 rows refused for another bin table's stamp (never scored)", labels=["rank"])
         stale.add_metric([self.rank_label], float(cnt[4]))
         yield stale
         fr = GaugeMetricFamily(M.GPU_GLOBAL_FRAUD_RATE, "Global fraud-route rate (all-reduced)",

@@ -1,5 +1,5 @@
 """GBDT weight import ("a GBDT weight importer"): oblivious ensembles
-trained elsewhere -> ``ObliviousGBDT`` (and from there the G32 / f32 device kernels).
+trained elsewhere -> ``ObliviousGBDT`` (and from there the G20 / G32 / f32 device kernels).
 
 CatBoost's default trees are oblivious -- the model family of BASELINE.json config 4 -- and
 its JSON dump (``model.save_model(path, format="json")``) carries everything the kernels

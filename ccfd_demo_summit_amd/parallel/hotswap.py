@@ -57,7 +57,7 @@ class HotSwap:
 
     def offer(self, model) -> None:
         """Queue ``model`` (same kind as the running one) for the next announcement.  Rank ``src``.
-        G32 engines (GBDT): the ensemble is packed against the LIVE bin table, so the
+        G32 / G20 engines (GBDT): the ensemble is packed against the LIVE bin table, so the
         partition logs need no re-encoding; ValueError if a split threshold is not one of its
         edges (a retrain that moves thresholds needs a new table: restart with re-encoding)."""
         bins = getattr(self.engine, "bins", None)

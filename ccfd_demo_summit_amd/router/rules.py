@@ -257,7 +257,7 @@ class RuleSet:
 
     def feature_vars(self) -> set:
         """Transaction columns the rules read (``amount`` reported as ``Amount``); empty when
-        the rules only look at ``proba`` -- the only rule sets G32 (binned) rows can route."""
+        the rules only look at ``proba`` -- the only rule sets G32 / G20 (binned) rows can route."""
         out = set()
         for r in self.rules:
             for n in ast.walk(ast.parse(r.expr, mode="eval")):

@@ -19,7 +19,7 @@ enum ccfd_counter_slot {
   CCFD_CNT_FRAUD = 1,         // transaction.outgoing{type=fraud}
   CCFD_CNT_STANDARD = 2,      // transaction.outgoing{type=standard}
   CCFD_CNT_PROBA_E6 = 3,      // sum(round(proba_1 * 1e6))
-  CCFD_CNT_WIRE_STALE = 4,    // G32 rows whose bin stamp != the model's (proba NaN, standard route)
+  CCFD_CNT_WIRE_STALE = 4,    // G32 / G20 rows whose bin stamp != the model's (proba NaN, standard route)
   CCFD_CNT_HIST_STD = 8,      // 14 amount buckets, standard route
   CCFD_CNT_HIST_FRAUD = 24,   // 14 amount buckets, fraud route
   CCFD_CNT_SLOTS = 64
