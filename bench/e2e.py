@@ -113,7 +113,11 @@ def main(argv=None):
     # model (same random-init + calibration as bench.py), W64 rows (G32 for the GBDT)
     Xcal, _ = generate(200_000, seed=999)
     model = build_model(args.model, seed=0, X_ref=Xcal, calibrate_rate=FRAUD_RATE)
-    dm = DeviceModel(model, dev, wire=args.model != "gbdt", bins=True if args.model == "gbdt" else None)
+    bins = None
+    if args.model == "gbdt":                  # G20 rows when the bin table fits 5 bits, else G32
+        spec = model.bin_spec()
+        bins = spec.with_bits(5) if spec.fits_g20 else spec
+    dm = DeviceModel(model, dev, wire=args.model != "gbdt", bins=bins)
 
     hub = MetricsHub()
     processes = ProcessEngine(cfg.kie.notification_timeout_s, cfg.kie.dmn_probability_threshold,
@@ -130,7 +134,10 @@ def main(argv=None):
         ring_rows=1 << 20, flush_us=args.flush_us, run_budget_us=2000, reduce_period_ms=10.0,
         threshold=cfg.router.fraud_threshold, coalesce=8, max_fetch=64,
         native_ingest=not args.python_ingest,
-        ingest_threads=args.ingest_threads or (P if args.fmt == "json" else 1)), partitions=list(range(P)))
+        # JSON parsing and G20 / G32 binning (GBDT) are per-row work on the ingest thread: one
+        # consumer thread per partition; TXB1 into W64 / f32 rows is a copy, one thread suffices
+        ingest_threads=args.ingest_threads or (P if args.fmt == "json" or dm.row_format in ("g20", "g32") else 1)),
+        partitions=list(range(P)))
     notif_c = store.consumer("notification-service", [k.notification_topic])
     resp_c = store.consumer(k.group_id + "-responses", [k.response_topic])
 
@@ -220,7 +227,7 @@ def main(argv=None):
     out = {
         "metric": "end-to-end tx/s (Kafka ingest -> GPU score -> route -> BP -> notify)",
         "value": round(tot / el, 1), "unit": "tx/s", "n_gpus": ctx.world, "seconds": round(el, 2),
-        "broker": args.broker, "rate_per_rank": args.rate, "micro_batch": args.batch, "model": args.model,
+        "broker": args.broker, "rate_per_rank": args.rate, "micro_batch": args.batch, "model": args.model, "row_format": dm.row_format,
         "flush_us": args.flush_us, "fmt": args.fmt,
         "ingest": "python" if (args.python_ingest or args.broker == "inproc") else "native",
         "ring_arrival_to_scored_p50_us": round(hist_quantile(lat, 0.5) / 1e3, 1),

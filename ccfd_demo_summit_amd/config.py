@@ -83,7 +83,8 @@ class EngineConfig:
     input_mode: str = "zerocopy"     # dma (H2D into HBM) | zerocopy (kernel reads pinned host)
     wire: str = "auto"               # ring row format: f32 | w64 | g32 | g20 | auto (w64 for mlp/lr, g20 for gbdt)
     coalesce: int = 4                # ready micro-batches per kernel launch (MLP, launch mode)
-    ingest_threads: int = 1          # native Kafka consumer threads per rank (partitions split)
+    ingest_threads: int = 0          # native Kafka consumer threads per rank (partitions split; 0 = auto:
+                                     # one per partition for GBDT's binned rows, else 1)
     model_watch: str = ""            # hot-swap when this safetensors file changes (rank 0)
     output_mode: str = "zerocopy"    # zerocopy (kernel writes pinned host) | dma
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches

@@ -50,7 +50,9 @@ class EngineServiceConfig:
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
     native_ingest: bool = True       # Kafka-protocol brokers: C++ consumer thread fetches and writes
                                      # rows straight into the rings (ingest/native_consumer.py)
-    ingest_threads: int = 1          # native consumers per rank, partitions split between them
+    ingest_threads: int = 0          # native consumers per rank, partitions split between them
+                                     # (0 = auto: one per partition for G20 / G32 rows, whose
+                                     # binning is per-row ingest work, else 1)
                                      # (one JSON message per transaction is parse-bound per thread)
     score_thread: bool = True        # drive engine.run() from a dedicated thread (GIL released in
                                      # native code) so scoring latency does not wait on the Python
@@ -95,7 +97,8 @@ class EngineService:
                 c = broker.committed(cfg.group_id, cfg.topic, p)
                 starts[p] = c if c is not None else broker.begin_offset(cfg.topic, p)
             seeds = ",".join(f"{h}:{pt}" for h, pt in getattr(broker, "_seeds", [broker._bootstrap]))
-            nt = max(1, min(int(cfg.ingest_threads), len(self.partitions)))
+            want = int(cfg.ingest_threads) or (len(self.partitions) if self.engine.row_format in ("g20", "g32") else 1)
+            nt = max(1, min(want, len(self.partitions)))
             for i in range(nt):
                 mine = {p: starts[p] for j, p in enumerate(self.partitions) if j % nt == i}
                 self.natives.append(NativeKafkaConsumer.for_engine(self.engine, seeds, cfg.topic, mine))
