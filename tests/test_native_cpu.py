@@ -86,7 +86,7 @@ def test_json_parser_features_array_and_errors(L):
 
 def test_host_runtime_under_asan(tmp_path):
     """Host-sanitizer build of the native runtime: the JSON parser (valid,
-    truncated, garbage), W64 encoder and CRC-32C run under clang ASan+UBSan in a child
+    truncated, garbage), W64 / G32 / G20 encoders and CRC-32C run under clang ASan+UBSan in a child
     process with the runtime preloaded; any report fails the test."""
     import os
     import sys
@@ -130,6 +130,11 @@ def test_host_runtime_under_asan(tmp_path):
         "assert (g == spec.encode(X)).all()\n"
         "bad = offs.copy(); bad[5] = bad[6] + 1\n"
         "assert L.ccfd_encode_g32(X.ctypes.data, 1000, 30, flat.ctypes.data, bad.ctypes.data, spec.stamp, g.ctypes.data, None) == -1\n"
+        "# G20 encoder (5-bit fields straddling dwords) against the numpy oracle\n"
+        "s5 = spec.with_bits(5)\n"
+        "g5 = np.zeros((1000, 20), np.uint8)\n"
+        "assert L.ccfd_encode_g20(X.ctypes.data, 1000, 30, flat.ctypes.data, offs.ctypes.data, s5.stamp, g5.ctypes.data, am.ctypes.data) == 1000\n"
+        "assert (g5 == s5.encode(X)).all()\n"
         "# native Kafka consumer: Fetch/RecordBatch parsing against kafka-lite\n"
         "import time\n"
         "from ccfd_demo_summit_amd.contracts import TxBatch\n"
