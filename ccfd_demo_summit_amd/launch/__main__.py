@@ -237,13 +237,13 @@ def cmd_engine(a, cfg):
     fmt = resolve_row_format(cfg.engine.model, cfg.engine.wire)
     rules = RuleSet.from_config(cfg.router)
     if fmt in ("g32", "g20") and rules.feature_vars():
-        # G32 rows carry bins, not feature values: rules over transaction columns need the
-        # values, so this deployment scores GBDT on f32 rows (exact, 120 B/row)
-        print(f"[engine] routing rules read {sorted(rules.feature_vars())}: GBDT on f32 rows instead of G32",
-              flush=True)
+        # G20 / G32 rows carry bins, not feature values: rules over transaction columns need
+        # the values, so this deployment scores GBDT on f32 rows (exact, 120 B/row)
+        print(f"[engine] routing rules read {sorted(rules.feature_vars())}: GBDT on f32 rows instead of "
+              f"{fmt.upper()}", flush=True)
         fmt = "f32"
     model = _model(cfg.engine.model, a.weights, cfg.seed) if ctx.rank == 0 else None
-    dm = broadcast_model(ctx, model, cfg.engine.model, fmt)      # X1 (+ G32 bin table)
+    dm = broadcast_model(ctx, model, cfg.engine.model, fmt)      # X1 (+ G20 / G32 bin table)
     broker = _broker(cfg)
     hub = MetricsHub()
     kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
