@@ -1,3 +1,6 @@
+#!/usr/bin/env bash
+# Two rocprofv3 --pmc passes over the G20 GBDT launch kernel on 16M HBM-resident rows
+# (profiles/r2/g20/pmc_gbdt_g20.txt).  gpurun -- 'bash scripts/pmc_g20.sh'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 O=gpurun_out/pmc_g20; mkdir -p $O
