@@ -405,5 +405,20 @@ class StreamEngine:
             raise RuntimeError(f"ccfd_engine_trace_read failed: {last_error()}")
         return out[:n]
 
+    def progress(self) -> Dict[str, int]:
+        """Non-blocking counters for watchdog diagnostics (racy snapshot)."""
+        v = np.zeros(5, np.int64)
+        if getattr(self, "h", None):
+            lib().ccfd_engine_progress(C.c_void_p(self.h), v.ctypes.data)
+        return {"submitted": int(v[0]), "completed": int(v[1]), "persist_posted": int(v[2]),
+                "persist_resident": int(v[3]), "in_flight": int(v[4])}
+
+    def emergency_stop(self, timeout_ms: int = 5000) -> int:
+        """Watchdog exit path: make a resident persistent kernel leave before the process
+        ends (0 = nothing resident / drained, -6 = still resident after ``timeout_ms``)."""
+        if not getattr(self, "h", None):
+            return 0
+        return int(lib().ccfd_engine_emergency_stop(C.c_void_p(self.h), int(timeout_ms)))
+
     def cursor(self, partition: int) -> int:
         return int(lib().ccfd_engine_cursor(C.c_void_p(self.h), int(partition)))

@@ -58,7 +58,10 @@ class EngineStats(C.Structure):
                 ("lat_p99_us", C.c_double), ("lat_max_us", C.c_double), ("lat_mean_us", C.c_double),
                 ("lat_hist", C.c_uint64 * 256), ("host_submit_ns", C.c_uint64), ("host_wait_ns", C.c_uint64),
                 ("host_complete_ns", C.c_uint64), ("dev_batches", C.c_uint64), ("dev_exec_ns", C.c_uint64),
-                ("dev_hist", C.c_uint64 * 256)]
+                ("dev_hist", C.c_uint64 * 256), ("lat_hist_rows", C.c_uint64 * 256),
+                ("dev_hist_rows", C.c_uint64 * 256), ("last_seq", C.c_uint64), ("last_tx_id", C.c_uint64),
+                ("last_proba", C.c_float), ("last_amount", C.c_float), ("last_partition", C.c_int32),
+                ("last_row_bytes", C.c_int32), ("last_row", C.c_uint8 * 128)]
 
 
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
@@ -114,6 +117,8 @@ def lib() -> C.CDLL:
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]
         L.ccfd_engine_cursor.restype = C.c_int64
         L.ccfd_engine_reset_stats.argtypes = [C.c_void_p]
+        L.ccfd_engine_progress.argtypes = [C.c_void_p, C.c_void_p]
+        L.ccfd_engine_emergency_stop.argtypes = [C.c_void_p, C.c_int]
         L.ccfd_engine_trace_enable.argtypes = [C.c_void_p, C.c_int32]
         L.ccfd_engine_trace_read.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.ccfd_engine_set_ring.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
@@ -137,6 +142,15 @@ def lib() -> C.CDLL:
         L.ccfd_encode_g20.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
                                       C.c_void_p, C.c_void_p]
         L.ccfd_encode_g20.restype = C.c_int64
+        for name in ("ccfd_encode_g32_ref", "ccfd_encode_g20_ref"):       # scalar oracles
+            fn = getattr(L, name)
+            fn.argtypes = L.ccfd_encode_g32.argtypes
+            fn.restype = C.c_int64
+        L.ccfd_encode_bins_mt.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
+                                          C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
+        L.ccfd_encode_bins_mt.restype = C.c_int64
+        L.ccfd_host_read_bw.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_double]
+        L.ccfd_host_read_bw.restype = C.c_double
         L.ccfd_engine_set_amount.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         _lib = L
         return L

@@ -210,6 +210,14 @@ class CounterReducer:
         self.epochs = 0
         self._work = None
         self.last_ctrl: Optional[torch.Tensor] = None     # reduced control words of the last completion
+        # SUM is the X2 reduction.  At world 1 RCCL elides an in-place SUM (no device kernel);
+        # CCFD_X2_ONE_RANK_KERNEL=1 (evidence runs only, one-GPU boxes) makes it an AVG -- the
+        # identity at world 1 -- which RCCL executes as its OneRankReduce kernel on the
+        # communicator stream, so a kernel trace shows where the W > 1 reduction kernel runs
+        # relative to the scoring kernel (profiles/r3/x2_overlap/)
+        self._op = dist.ReduceOp.SUM
+        if os.environ.get("CCFD_X2_ONE_RANK_KERNEL") == "1" and ctx.world == 1:
+            self._op = dist.ReduceOp.AVG
 
     def busy(self) -> bool:
         return self._work is not None and not self._work.is_completed()
@@ -233,7 +241,7 @@ class CounterReducer:
             if self.freed is not None:
                 self.freed.record(self.side)
             if self.ctx.initialized:
-                self._work = dist.all_reduce(self.pack, group=self.group, async_op=True)
+                self._work = dist.all_reduce(self.pack, op=self._op, group=self.group, async_op=True)
             else:
                 self._fold()
         self.epochs += 1

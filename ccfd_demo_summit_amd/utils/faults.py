@@ -12,7 +12,9 @@ X2 pairing under skew) can be exercised on purpose:
 * ``delay`` -- the rank stalls for ``ms`` before a step (a slow or descheduled rank; peers must
   not block on it);
 * ``crash`` -- the rank dies: ``mode=exit`` ends the process with ``os._exit`` (no cleanup,
-  like SIGKILL), ``mode=raise`` raises :class:`InjectedCrash` (in-process tests).
+  like SIGKILL), ``mode=raise`` raises :class:`InjectedCrash` (in-process tests);
+* ``stall`` -- the rank hangs for good at ``after_steps`` (a peer wedged in a collective or a
+  kernel that never completes): nothing but a watchdog (utils/watchdog.py) or a kill ends it.
 
 A plan is a ``;``-separated list of ``kind:key=value,...`` clauses, from ``CCFD_FAULTS`` or
 code, each optionally restricted to one rank::
@@ -37,11 +39,11 @@ class InjectedCrash(RuntimeError):
 
 @dataclass
 class FaultClause:
-    kind: str                                  # drop | delay | crash
+    kind: str                                  # drop | delay | crash | stall
     p: float = 1.0                             # per-step probability (drop, delay)
     ms: float = 0.0                            # delay length
     rank: Optional[int] = None                 # None: every rank
-    after_steps: Optional[int] = None          # crash: at this step count
+    after_steps: Optional[int] = None          # crash / stall: at this step count
     after_s: Optional[float] = None            # crash: this long after the plan was armed
     mode: str = "raise"                        # crash: raise | exit
 
@@ -52,7 +54,7 @@ class FaultPlan:
     seed: int = 0
     rank: int = 0
     steps: int = 0
-    injected: Dict[str, int] = field(default_factory=lambda: {"drop": 0, "delay": 0, "crash": 0})
+    injected: Dict[str, int] = field(default_factory=lambda: {"drop": 0, "delay": 0, "crash": 0, "stall": 0})
 
     def __post_init__(self):
         self._rng = np.random.default_rng(self.seed * 1_000_003 + self.rank)
@@ -64,7 +66,7 @@ class FaultPlan:
         for part in filter(None, (s.strip() for s in spec.split(";"))):
             kind, _, args = part.partition(":")
             kind = kind.strip()
-            if kind not in ("drop", "delay", "crash"):
+            if kind not in ("drop", "delay", "crash", "stall"):
                 raise ValueError(f"unknown fault kind {kind!r}")
             c = FaultClause(kind)
             for kv in filter(None, (s.strip() for s in args.split(","))):
@@ -101,6 +103,10 @@ class FaultPlan:
             if c.kind == "delay" and c.ms > 0 and self._rng.random() < c.p:
                 self.injected["delay"] += 1
                 time.sleep(c.ms / 1e3)
+            elif c.kind == "stall" and (c.after_steps is None or self.steps >= c.after_steps):
+                self.injected["stall"] += 1
+                while True:                             # wedged: only a watchdog / kill ends it
+                    time.sleep(3600)
             elif c.kind == "crash":
                 due = (c.after_steps is not None and self.steps >= c.after_steps) or \
                       (c.after_s is not None and time.monotonic() - self._t0 >= c.after_s)

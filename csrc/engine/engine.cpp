@@ -50,7 +50,10 @@ namespace {
 
 using ccfd::set_error;
 
-std::atomic<int> g_persist_engines{0};     // persistent engines alive in this process
+// persistent engines alive in this process, per device: hardware queues belong to a device,
+// so the GPU_MAX_HW_QUEUES bound is per device, not per process
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_persist_engines[kMaxDevices];
 
 inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -147,10 +150,16 @@ class Engine {
   static constexpr double kFineUs = 0.25;
   uint64_t lat_n = 0, lat_over = 0;
   double lat_sum_us = 0.0, lat_max_us = 0.0;
-  std::vector<uint32_t> lat_fine = std::vector<uint32_t>(kFineBuckets, 0u);
+  std::vector<uint64_t> lat_fine = std::vector<uint64_t>(kFineBuckets, 0u);   // u64: never wraps
   uint64_t lat_hist[256] = {};
   uint64_t t_submit_ns = 0, t_wait_ns = 0, t_complete_ns = 0;
   uint64_t dev_batches = 0, dev_exec_ns = 0, dev_hist[256] = {};
+  uint64_t lat_hist_rows[256] = {}, dev_hist_rows[256] = {};   // row-weighted (Seldon histograms)
+  // last completed transaction (model "last request" gauges)
+  uint64_t last_seq = 0, last_tx_id = 0;
+  float last_proba = 0.f, last_amount = 0.f;
+  int32_t last_partition = -1;
+  uint8_t last_row[128] = {};
   std::vector<ccfd_batch_trace> trace;     // per-batch stage trace ring (ccfd_engine_trace_enable)
   uint64_t trace_n = 0;                    // entries ever written
   std::mutex trace_mu;                     // the ring may be read from another thread
@@ -346,6 +355,20 @@ class Engine {
       set_error("persistent exec_mode needs zero-copy outputs and depth <= 64");
       return -1;
     }
+    // take this device's persistent-queue slot before allocating anything, so a refusal
+    // leaks nothing (see the stream-priority note below)
+    if (cfg.device < 0 || cfg.device >= kMaxDevices) { set_error("device index out of range"); return -1; }
+    {
+      int max_q = 4;
+      if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) max_q = std::max(1, std::atoi(e));
+      if (g_persist_engines[cfg.device].fetch_add(1) >= max_q) {
+        g_persist_engines[cfg.device].fetch_sub(1);
+        set_error("more persistent engines on one device than GPU_MAX_HW_QUEUES in one process: their "
+                  "kernels would share a hardware queue");
+        return -1;
+      }
+      persist_counted = true;
+    }
     void* p = nullptr;
     HIPCHK(hipHostMalloc(&p, sizeof(ccfd_persist_ctl), hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
     std::memset(p, 0, sizeof(ccfd_persist_ctl));
@@ -386,15 +409,6 @@ class Engine {
     {
       int least = 0, greatest = 0;
       HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      int max_q = 4;
-      if (const char* e = std::getenv("GPU_MAX_HW_QUEUES")) max_q = std::max(1, std::atoi(e));
-      if (g_persist_engines.fetch_add(1) >= max_q) {
-        g_persist_engines.fetch_sub(1);
-        set_error("more persistent engines than GPU_MAX_HW_QUEUES in one process: their kernels would share "
-                  "a hardware queue");
-        return -1;
-      }
-      persist_counted = true;
       HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, least));
     }
     persist_C = C;
@@ -469,8 +483,13 @@ class Engine {
   }
 
   void persist_free() {
-    if (!persistent) {
-      if (persist_counted) g_persist_engines.fetch_sub(1);
+    if (!persistent) {                       // refused or failed part-way through persist_init
+      if (pstream) (void)hipStreamDestroy(pstream);
+      if (pdev) (void)hipFree(pdev);
+      if (pdesc) (void)hipHostFree(pdesc);
+      if (pctl) (void)hipHostFree(pctl);
+      pstream = nullptr; pdev = nullptr; pdesc = nullptr; pctl = nullptr;
+      if (persist_counted) g_persist_engines[cfg.device].fetch_sub(1);
       persist_counted = false;
       return;
     }
@@ -481,7 +500,7 @@ class Engine {
     (void)hipFree(pdev);
     (void)hipHostFree(pdesc);
     (void)hipHostFree(pctl);
-    if (persist_counted) g_persist_engines.fetch_sub(1);
+    if (persist_counted) g_persist_engines[cfg.device].fetch_sub(1);
     persist_counted = false;
     persistent = false;
   }
@@ -645,7 +664,11 @@ class Engine {
       if (fb < kFineBuckets) ++lat_fine[(size_t)fb]; else ++lat_over;
     }
     const double ns = (double)std::max<int64_t>(1, t_landed - t0);
-    lat_hist[std::min(255, (int)std::floor(4.0 * std::log2(ns)))]++;
+    {
+      const int b = std::min(255, (int)std::floor(4.0 * std::log2(ns)));
+      lat_hist[b]++;
+      lat_hist_rows[b] += (uint64_t)s.rows;
+    }
     uint64_t nf = 0;
     if (s.use_flag) {
       nf = s.done_ptr[1];
@@ -656,7 +679,9 @@ class Engine {
           const double dns = (double)(t1d - t0d) * wall_ns_per_tick;
           dev_exec_ns += (uint64_t)dns;
           ++dev_batches;
-          dev_hist[std::min(255, (int)std::floor(4.0 * std::log2(std::max(1.0, dns))))]++;
+          const int b = std::min(255, (int)std::floor(4.0 * std::log2(std::max(1.0, dns))));
+          dev_hist[b]++;
+          dev_hist_rows[b] += (uint64_t)s.rows;
         }
       }
     } else {
@@ -666,6 +691,15 @@ class Engine {
     if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
     if (trace_on.load(std::memory_order_relaxed)) record_trace(s, t_landed, nf);
     Partition& P = *parts[s.part];
+    if (s.rows > 0 && P.feats) {                     // "last request" record (still unreleased)
+      const int64_t row = s.start + s.rows - 1;
+      std::memcpy(last_row, P.feats + row * rowf, (size_t)rowf * sizeof(float));
+      last_tx_id = P.ids ? P.ids[row] : (uint64_t)row;
+      last_proba = s.h_proba[s.rows - 1];
+      last_amount = amount_f >= 0 ? P.feats[row * rowf + amount_f] : (P.amount ? P.amount[row] : __builtin_nanf(""));
+      last_partition = s.part;
+      ++last_seq;
+    }
     if (P.ring) {
       // batches of one partition complete in submission order: release in order
       P.rr.release_rows(s.rows);
@@ -854,8 +888,9 @@ class Engine {
   void reset_latency() {
     lat_n = lat_over = 0;
     lat_sum_us = lat_max_us = 0.0;
-    std::fill(lat_fine.begin(), lat_fine.end(), 0u);
+    std::fill(lat_fine.begin(), lat_fine.end(), 0ull);
     std::memset(lat_hist, 0, sizeof(lat_hist));
+    std::memset(lat_hist_rows, 0, sizeof(lat_hist_rows));
   }
 
   void fill_latency(ccfd_engine_stats* st) {
@@ -866,6 +901,15 @@ class Engine {
     st->dev_batches = dev_batches;
     st->dev_exec_ns = dev_exec_ns;
     std::memcpy(st->dev_hist, dev_hist, sizeof(dev_hist));
+    std::memcpy(st->lat_hist_rows, lat_hist_rows, sizeof(lat_hist_rows));
+    std::memcpy(st->dev_hist_rows, dev_hist_rows, sizeof(dev_hist_rows));
+    st->last_seq = last_seq;
+    st->last_tx_id = last_tx_id;
+    st->last_proba = last_proba;
+    st->last_amount = last_amount;
+    st->last_partition = last_partition;
+    st->last_row_bytes = rowf * (int32_t)sizeof(float);
+    std::memcpy(st->last_row, last_row, sizeof(last_row));
     if (lat_n == 0) return;
     st->lat_p50_us = fine_quantile(0.50);
     st->lat_p99_us = fine_quantile(0.99);
@@ -1139,6 +1183,38 @@ int64_t ccfd_engine_cursor(void* eng, int partition) {
   return P.ring ? P.rr.released_count() : P.cursor;
 }
 
+// Watchdog diagnostics (racy reads of plain counters; never blocks): out[0] = micro-batches
+// submitted, out[1] = completed in order, out[2] = persistent descriptors posted (-1 when not
+// persistent), out[3] = persistent kernel resident (0/1), out[4] = batches in flight.
+int ccfd_engine_progress(void* eng, int64_t* out) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!out) return -1;
+  out[0] = (int64_t)e->seq;
+  out[1] = e->completed_upto;
+  out[2] = e->persistent && e->pctl ? (int64_t)__atomic_load_n(&e->pctl->posted, __ATOMIC_RELAXED) : -1;
+  out[3] = e->prunning ? 1 : 0;
+  int64_t busy = 0;
+  for (const auto& s : e->slots) busy += s.busy ? 1 : 0;
+  out[4] = busy;
+  return 0;
+}
+
+// Watchdog exit path: ask a resident persistent kernel to leave (the stop word every
+// waiting workgroup polls) and wait up to `timeout_ms` for its grid to drain, so a process
+// that is about to _exit never leaves a resident kernel behind.  Touches only the host
+// control record and queries the kernel's stream.  0 = no kernel resident / drained.
+int ccfd_engine_emergency_stop(void* eng, int timeout_ms) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!e->persistent || !e->pctl || !e->prunning) return 0;
+  __atomic_store_n(&e->pctl->stop, 1ull, __ATOMIC_RELEASE);
+  const int64_t t0 = now_ns();
+  while (hipStreamQuery(e->pstream) == hipErrorNotReady) {
+    if (now_ns() - t0 > (int64_t)timeout_ms * 1000000ll) return -6;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  return 0;
+}
+
 int ccfd_engine_set_amount(void* eng, int partition, const float* amount) {
   auto* e = static_cast<Engine*>(eng);
   if (partition < 0 || partition >= (int)e->parts.size()) { set_error("bad partition index"); return -1; }
@@ -1194,6 +1270,7 @@ void ccfd_engine_reset_stats(void* eng) {
   e->t_submit_ns = e->t_wait_ns = e->t_complete_ns = 0;
   e->dev_batches = e->dev_exec_ns = 0;
   std::memset(e->dev_hist, 0, sizeof(e->dev_hist));
+  std::memset(e->dev_hist_rows, 0, sizeof(e->dev_hist_rows));
 }
 
 }  // extern "C"

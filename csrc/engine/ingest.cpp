@@ -10,9 +10,13 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <thread>
+#include <vector>
 
 #include "../include/ccfd_abi.h"
 #include "json_num.h"
+#include "binenc.h"
 
 namespace {
 
@@ -197,44 +201,43 @@ extern "C" int64_t ccfd_parse_json_batch_w64(const char* buf, const int64_t* off
 // ---------------------------------------------------------------------------------------
 // G32 rows (GBDT; ccfd_abi.h, contracts/transaction.py encode_g32): byte j = #{edges_j < x_j}
 // (lower_bound; NaN compares false everywhere -> 0), byte 30 = amount bucket with the
-// device's bounds (common.h amount_bucket), byte 31 = bin-table stamp.
+// device's bounds (common.h amount_bucket), byte 31 = bin-table stamp.  G20 rows: the same
+// bins, 5 bits each, little-endian over 160 bits; the amount bucket at bit 150 and the 6-bit
+// stamp at bit 154.  Encoded by the branch-free SIMD BinPlan (binenc.h); the scalar
+// binary-search encoders stay as `_ref` entry points (oracle for tests and the microbench).
 namespace {
-constexpr float kAmountBounds[CCFD_N_AMOUNT_BUCKETS - 1] = {1.f, 5.f, 10.f, 25.f, 50.f, 100.f, 250.f,
-                                                            500.f, 1000.f, 2500.f, 5000.f, 10000.f, 25000.f};
-inline uint8_t amount_bucket_host(float a) {
-  int b = 0;
-  for (float bound : kAmountBounds) b += a > bound ? 1 : 0;
-  return (uint8_t)b;
-}
-inline uint8_t bin_of(const float* e, int ne, float x) {
-  int lo = 0, hi = ne;                 // first edge >= x  ==  #edges < x  (edges ascending)
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (e[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return (uint8_t)lo;
-}
+using ccfd::amount_bucket_host;
+using ccfd::bin_of_ref;
 
-inline void encode_row_g32(const float* r, uint8_t* o, const float* edges, const int32_t* offsets, int32_t stamp) {
+inline void encode_row_g32_ref(const float* r, uint8_t* o, const float* edges, const int32_t* offsets, int32_t stamp) {
   for (int j = 0; j < CCFD_N_FEATURES; ++j)
-    o[j] = bin_of(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]);
+    o[j] = bin_of_ref(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]);
   o[30] = amount_bucket_host(r[CCFD_N_FEATURES - 1]);
   o[31] = (uint8_t)stamp;
 }
 
-// G20 rows (ccfd_abi.h): the same bins, 5 bits each, little-endian over 160 bits; the amount
-// bucket at bit 150 and the 6-bit stamp at bit 154.
-inline void encode_row_g20(const float* r, uint8_t* o, const float* edges, const int32_t* offsets, int32_t stamp) {
+inline void encode_row_g20_ref(const float* r, uint8_t* o, const float* edges, const int32_t* offsets, int32_t stamp) {
   uint32_t w[6] = {0, 0, 0, 0, 0, 0};  // 5 dwords + one spill dword for the funnel below
   auto put = [&](int bit, uint32_t v) {   // v < 2^6
     w[bit >> 5] |= v << (bit & 31);
     if ((bit & 31) + 6 > 32) w[(bit >> 5) + 1] |= v >> (32 - (bit & 31));
   };
   for (int j = 0; j < CCFD_N_FEATURES; ++j)
-    put(5 * j, bin_of(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]));
+    put(5 * j, bin_of_ref(edges + offsets[j], offsets[j + 1] - offsets[j], r[j]));
   put(150, amount_bucket_host(r[CCFD_N_FEATURES - 1]));
   w[4] |= (uint32_t)(stamp & 63) << (154 - 128);
   memcpy(o, w, CCFD_G20_ROW_BYTES);
+}
+
+int64_t encode_plan(const float* x, int64_t n, int64_t ld, const ccfd::BinPlan& plan, uint8_t* out,
+                    float* amount_out) {
+  const int rb = plan.g20 ? CCFD_G20_ROW_BYTES : CCFD_G32_ROW_BYTES;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* r = x + i * ld;
+    plan.encode(r, out + i * rb);
+    if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
+  }
+  return n;
 }
 }  // namespace
 
@@ -258,22 +261,63 @@ bool g20_table_ok(const float* edges, const int32_t* offsets, int32_t stamp) {
 extern "C" int64_t ccfd_encode_g32(const float* x, int64_t n, int64_t ld, const float* edges,
                                    const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
   if (ld < CCFD_N_FEATURES || n < 0 || !out || !ccfd::g32_table_ok(edges, offsets, stamp)) return -1;
-  for (int64_t i = 0; i < n; ++i) {
-    const float* r = x + i * ld;
-    encode_row_g32(r, out + i * CCFD_G32_ROW_BYTES, edges, offsets, stamp);
-    if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
-  }
-  return n;
+  ccfd::BinPlan plan;
+  if (!plan.build(edges, offsets, stamp, false)) return -1;
+  return encode_plan(x, n, ld, plan, out, amount_out);
 }
 
 extern "C" int64_t ccfd_encode_g20(const float* x, int64_t n, int64_t ld, const float* edges,
                                    const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
   if (ld < CCFD_N_FEATURES || n < 0 || !out || !ccfd::g20_table_ok(edges, offsets, stamp)) return -1;
+  ccfd::BinPlan plan;
+  if (!plan.build(edges, offsets, stamp, true)) return -1;
+  return encode_plan(x, n, ld, plan, out, amount_out);
+}
+
+// The pre-SIMD encoders (scalar binary search a feature), kept as the exactness oracle and
+// the microbench baseline (bench/encode_bench.py).
+extern "C" int64_t ccfd_encode_g32_ref(const float* x, int64_t n, int64_t ld, const float* edges,
+                                       const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
+  if (ld < CCFD_N_FEATURES || n < 0 || !out || !ccfd::g32_table_ok(edges, offsets, stamp)) return -1;
   for (int64_t i = 0; i < n; ++i) {
     const float* r = x + i * ld;
-    encode_row_g20(r, out + i * CCFD_G20_ROW_BYTES, edges, offsets, stamp);
+    encode_row_g32_ref(r, out + i * CCFD_G32_ROW_BYTES, edges, offsets, stamp);
     if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
   }
+  return n;
+}
+
+extern "C" int64_t ccfd_encode_g20_ref(const float* x, int64_t n, int64_t ld, const float* edges,
+                                       const int32_t* offsets, int32_t stamp, uint8_t* out, float* amount_out) {
+  if (ld < CCFD_N_FEATURES || n < 0 || !out || !ccfd::g20_table_ok(edges, offsets, stamp)) return -1;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* r = x + i * ld;
+    encode_row_g20_ref(r, out + i * CCFD_G20_ROW_BYTES, edges, offsets, stamp);
+    if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
+  }
+  return n;
+}
+
+// Multi-threaded encode of a large block (log fill, bench attribution): rows split over
+// `threads` std::threads.  Returns n or -1.
+extern "C" int64_t ccfd_encode_bins_mt(const float* x, int64_t n, int64_t ld, const float* edges,
+                                       const int32_t* offsets, int32_t stamp, int32_t g20, uint8_t* out,
+                                       float* amount_out, int32_t threads) {
+  if (ld < CCFD_N_FEATURES || n < 0 || !out || threads < 1 || threads > 256) return -1;
+  if (!(g20 ? ccfd::g20_table_ok : ccfd::g32_table_ok)(edges, offsets, stamp)) return -1;
+  ccfd::BinPlan plan;
+  if (!plan.build(edges, offsets, stamp, g20 != 0)) return -1;
+  const int rb = g20 ? CCFD_G20_ROW_BYTES : CCFD_G32_ROW_BYTES;
+  const int64_t per = (n + threads - 1) / threads;
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) {
+    const int64_t a = (int64_t)t * per, b = std::min<int64_t>(n, a + per);
+    if (a >= b) break;
+    th.emplace_back([=, &plan] {
+      encode_plan(x + a * ld, b - a, ld, plan, out + a * rb, amount_out ? amount_out + a : nullptr);
+    });
+  }
+  for (auto& t : th) t.join();
   return n;
 }
 
@@ -283,10 +327,5 @@ bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32
   return parse_one(s, e, f, id, cust);
 }
 void encode_w64_row(const float* x, uint8_t* out) { encode_row_w64(x, out); }
-void encode_g32_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp) {
-  encode_row_g32(x, out, edges, offsets, stamp);
-}
-void encode_g20_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp) {
-  encode_row_g20(x, out, edges, offsets, stamp);
-}
+void encode_bins_row(const BinPlan& plan, const float* x, uint8_t* out) { plan.encode(x, out); }
 }  // namespace ccfd

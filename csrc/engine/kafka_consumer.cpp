@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "../include/ccfd_abi.h"
+#include "binenc.h"
 
 extern "C" uint32_t ccfd_crc32c(const void* data, size_t n, uint32_t seed);
 
@@ -53,8 +54,7 @@ namespace ccfd {
 void set_error(const std::string& e);
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust);
 void encode_w64_row(const float* x, uint8_t* out);
-void encode_g32_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp);
-void encode_g20_row(const float* x, uint8_t* out, const float* edges, const int32_t* offsets, int32_t stamp);
+void encode_bins_row(const BinPlan& plan, const float* x, uint8_t* out);
 bool g32_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
 bool g20_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
 }  // namespace ccfd
@@ -168,8 +168,7 @@ class Consumer {
   std::vector<std::pair<std::string, int>> seeds;   // bootstrap list
   std::string topic, client = "ccfd-native";
   int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64, 2 = G32, 3 = G20
-  std::vector<float> g32_edges;                     // G32 bin table (ccfd_kc_set_bins)
-  std::vector<int32_t> g32_off;
+  ccfd::BinPlan bins;                               // G32 / G20 bin table (ccfd_kc_set_bins), SIMD plan
   int32_t g32_stamp = 0;
   int reset_policy = CCFD_KC_RESET_EARLIEST;
   Sink* sink = nullptr;
@@ -446,7 +445,7 @@ class Consumer {
   // one canonical f32 row into the sink's row format at ring row `row`
   void put_row(int pi, const float* x, uint8_t* dst, int64_t row) {
     if (wire >= 2) {
-      (wire == 3 ? ccfd::encode_g20_row : ccfd::encode_g32_row)(x, dst, g32_edges.data(), g32_off.data(), g32_stamp);
+      ccfd::encode_bins_row(bins, x, dst);
       if (float* am = sink->amount(pi)) am[row] = x[CCFD_N_FEATURES - 1];
     } else if (wire) {
       ccfd::encode_w64_row(x, dst);
@@ -553,7 +552,10 @@ class Consumer {
       const int codec = attrs & 0x7;
       In r{h.p, bend};
       if (codec == 1) {
-        if (!gunzip(h.p, (size_t)(bend - h.p))) { error("corrupt gzip record batch"); p = bend; continue; }
+        // a batch that passes its CRC but does not inflate is never skipped: a later batch would
+        // move next_offset past its records and commit them unread (at-least-once broken) --
+        // the partition stalls on it, like an unsupported codec below
+        if (!gunzip(h.p, (size_t)(bend - h.p))) { error("corrupt gzip record batch"); return; }
         r = In{inflated.data(), inflated.data() + inflated.size()};
       } else if (codec != 0) {
         static const char* names[] = {"none", "gzip", "snappy", "lz4", "zstd"};
@@ -763,8 +765,7 @@ int ccfd_kc_set_bins(void* kc, const float* edges, const int32_t* offsets, int32
     ccfd::set_error(c->wire == 3 ? "kc: bad G20 bin table" : "kc: bad G32 bin table");
     return -1;
   }
-  c->g32_off.assign(offsets, offsets + CCFD_N_FEATURES + 1);
-  c->g32_edges.assign(edges, edges + std::max(1, offsets[CCFD_N_FEATURES]));
+  if (!c->bins.build(edges, offsets, stamp, c->wire == 3)) { ccfd::set_error("kc: bin plan allocation failed"); return -1; }
   c->g32_stamp = stamp;
   return 0;
 }

@@ -247,6 +247,21 @@ typedef struct ccfd_engine_stats {
   uint64_t dev_batches;
   uint64_t dev_exec_ns;        // sum
   uint64_t dev_hist[256];      // same bucketing as lat_hist
+  // row-weighted twins of lat_hist / dev_hist (each batch adds its row count): per-transaction
+  // latency distributions, exported as the Seldon engine's server / client request histograms
+  // (deploy/grafana/SeldonCore.json:119-531; one scored transaction = one reference request)
+  uint64_t lat_hist_rows[256];
+  uint64_t dev_hist_rows[256];
+  // the last scored transaction (the reference model's "last request" gauges proba_1 / Amount /
+  // V17 / V10, deploy/grafana/ModelPrediction.json:96-322): its raw log row in the engine's row
+  // format (f32[30], W64, G32 or G20), proba, Amount and id; last_seq = 0 until one completed
+  uint64_t last_seq;
+  uint64_t last_tx_id;
+  float last_proba;
+  float last_amount;
+  int32_t last_partition;
+  int32_t last_row_bytes;
+  uint8_t last_row[128];
 } ccfd_engine_stats;
 
 void* ccfd_engine_create(const ccfd_engine_config* cfg);
@@ -280,6 +295,10 @@ int ccfd_engine_set_blob(void* eng, const void* blob);
 // Drain up to `max` flagged records (fraud route) into `out`; returns count.
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
 int64_t ccfd_engine_cursor(void* eng, int partition);
+// Watchdog diagnostics: submitted, completed, persistent posted (-1), kernel resident, in flight.
+int ccfd_engine_progress(void* eng, int64_t* out5);
+// Watchdog exit path: stop a resident persistent kernel, wait <= timeout_ms for it to drain.
+int ccfd_engine_emergency_stop(void* eng, int timeout_ms);
 // G32 logs/rings: host-side Amount column of partition p (the flagged-record amount; the
 // rows themselves carry only its bucket).  Call after set_log / set_ring.
 int ccfd_engine_set_amount(void* eng, int partition, const float* amount);

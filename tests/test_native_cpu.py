@@ -232,3 +232,116 @@ def test_json_ids_out_of_range_are_malformed(L, field, val):
     rc, _, ids, _ = _parse(L, ['{"id": 12, "features": [%s], "flag": true}' % feats,
                                '{"id": 13, "features": [%s], "x": null}' % feats])
     assert rc == 2 and ids.tolist() == [12, 13]
+
+
+def _edge_table(rng, ne_max, g20):
+    """A random BinSpec-shaped table: sorted per-feature edges incl. duplicates-free ties with
+    the input values, empty features and the format's maximum edge count."""
+    edges, offs = [], [0]
+    for j in range(30):
+        ne = int(rng.integers(0, ne_max + 1)) if j not in (0, 7) else (ne_max if j == 0 else 0)
+        e = np.unique(rng.standard_normal(ne).astype(np.float32) * 2)
+        edges.append(e)
+        offs.append(offs[-1] + len(e))
+    flat = np.concatenate(edges).astype(np.float32) if offs[-1] else np.zeros(1, np.float32)
+    return np.ascontiguousarray(flat), np.asarray(offs, np.int32)
+
+
+@pytest.mark.parametrize("g20", [False, True])
+def test_simd_encoder_matches_reference(L, g20):
+    """The branch-free AVX2 bin encoder (csrc/engine/binenc.h) is bit-exact against the scalar
+    binary-search encoder it replaced, for NaN / +-inf / values equal to an edge, every table
+    width up to the format's maximum (31 edges G20, 255 G32), and the multi-threaded entry."""
+    rng = np.random.default_rng(11 + g20)
+    ne_max = 31 if g20 else 255
+    rb = 20 if g20 else 32
+    for trial in range(6):
+        flat, offs = _edge_table(rng, ne_max, g20)
+        n = 5000
+        X = rng.standard_normal((n, 30)).astype(np.float32) * 2
+        # exact ties with edges, specials
+        for j in range(30):
+            ne = offs[j + 1] - offs[j]
+            if ne:
+                k = rng.integers(0, n, 200)
+                X[k, j] = flat[offs[j] + rng.integers(0, ne, 200)]
+        X[rng.integers(0, n, 50), rng.integers(0, 30, 50)] = np.nan
+        X[rng.integers(0, n, 50), rng.integers(0, 30, 50)] = np.inf
+        X[rng.integers(0, n, 50), rng.integers(0, 30, 50)] = -np.inf
+        X[rng.integers(0, n, 20), rng.integers(0, 30, 20)] = -0.0
+        stamp = int(rng.integers(1, 63))
+        fn, ref = (L.ccfd_encode_g20, L.ccfd_encode_g20_ref) if g20 else (L.ccfd_encode_g32, L.ccfd_encode_g32_ref)
+        a = np.zeros((n, rb), np.uint8)
+        b = np.zeros((n, rb), np.uint8)
+        am = np.zeros(n, np.float32)
+        assert fn(X.ctypes.data, n, 30, flat.ctypes.data, offs.ctypes.data, stamp, a.ctypes.data, am.ctypes.data) == n
+        assert ref(X.ctypes.data, n, 30, flat.ctypes.data, offs.ctypes.data, stamp, b.ctypes.data, None) == n
+        assert (a == b).all(), np.argwhere(a != b)[:5]
+        np.testing.assert_array_equal(am, X[:, 29])
+        c = np.zeros((n, rb), np.uint8)
+        assert L.ccfd_encode_bins_mt(X.ctypes.data, n, 30, flat.ctypes.data, offs.ctypes.data, stamp, int(g20),
+                                     c.ctypes.data, None, 3) == n
+        assert (c == b).all()
+
+
+def test_simd_encoder_is_faster(L):
+    """Microbench guard: the SIMD encoder beats the scalar binary search it replaced on a
+    BASELINE-shaped table (100 x 6 ensemble: ~20 edges a feature); the measured ratio on the
+    GPU box's host goes into profiles/r3/encode/ (bench/encode_bench.py)."""
+    import time
+    rng = np.random.default_rng(3)
+    from ccfd_demo_summit_amd.models.gbdt import ObliviousGBDT
+    X = rng.standard_normal((200_000, 30)).astype(np.float32)
+    spec = ObliviousGBDT.random_init(100, 6, seed=0, X_ref=X[:20000]).bin_spec(bits=5)
+    out = np.zeros((len(X), 20), np.uint8)
+    flat, offs = spec.flat, spec.offsets
+    args = (X.ctypes.data, len(X), 30, flat.ctypes.data, offs.ctypes.data, spec.stamp, out.ctypes.data, None)
+
+    def best(fn):
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            fn(*args)
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+    t_ref, t_simd = best(L.ccfd_encode_g20_ref), best(L.ccfd_encode_g20)
+    assert t_simd * 1.5 < t_ref, (t_simd, t_ref)
+
+
+def test_host_read_bw_probe(L):
+    from ccfd_demo_summit_amd.engine.stream_engine import PinnedArray  # noqa: F401  (GPU-free import)
+    buf = np.zeros((64 << 20) // 8 + 8, np.uint64)
+    p = buf.ctypes.data
+    p = p + (-p) % 32
+    gbps = L.ccfd_host_read_bw(C.c_void_p(p), 64 << 20, 2, 0.05)
+    assert gbps > 0.5, gbps
+    assert L.ccfd_host_read_bw(C.c_void_p(p), 100, 2, 0.01) < 0
+
+
+def test_corrupt_gzip_batch_stalls_partition(L):
+    """a CRC-valid gzip batch that does not inflate must stall the partition (error
+    reported, nothing after it consumed) instead of being skipped -- a later batch would move
+    the offset past the lost records and they would be committed unread."""
+    import struct
+    import zlib
+    from ccfd_demo_summit_amd.ingest.kafka_wire import CODEC_GZIP, crc32c, encode_record_batch
+    from ccfd_demo_summit_amd.ingest.native_consumer import NativeKafkaConsumer
+    msgs = [json.dumps({"id": i, **{n: float(i) for n in FEATURE_NAMES}}).encode() for i in range(10)]
+    gz = bytearray(encode_record_batch(msgs[:5], compression=CODEC_GZIP, base_offset=0))
+    hdr = 12 + 9 + 40          # base/len, epoch/magic/crc, attrs..count
+    body = bytearray(gz[hdr:])
+    for i in range(12, len(body) - 8):            # wreck the deflate stream, keep the gzip header
+        body[i] ^= 0x5A
+    after = bytes(gz[21:hdr]) + bytes(body)
+    bad = struct.pack(">qi", 0, 9 + len(after)) + struct.pack(">ibI", 0, 2, crc32c(after)) + after
+    assert zlib.crc32(bad) != zlib.crc32(bytes(gz))
+    good = encode_record_batch(msgs[5:], base_offset=5)
+    kc = NativeKafkaConsumer.for_arrays("127.0.0.1:1", "t", {0: 0}, capacity=1000, wire=False)
+    try:
+        kc.feed(bad + good)
+        st = kc.stats()
+        assert st["records"] == 0, st                 # the valid batch behind it is NOT consumed
+        assert "gzip" in kc.last_error()
+        assert kc.committable() == {}
+    finally:
+        kc.close()
