@@ -192,7 +192,7 @@ def _h2d_probe(lib_, ms: float, mb: int = 256) -> float:
         host.free()
 
 
-def _host_read_probe(lib_, seconds: float, mb: int = 512):
+def _host_read_probe(lib_, seconds: float, mb: int = 2048):
     """CPU streaming-read GB/s of this rank's NUMA node (the process is already bound to its
     GPU's node): the DRAM side of the zero-copy path, which N ranks on one socket share."""
     import ctypes as C

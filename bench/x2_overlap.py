@@ -54,8 +54,20 @@ def load(path_or_dir: str):
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
-    return n[-120:]
+    """Demangled name without its trailing argument list (names like
+    ``void (anonymous namespace)::oneRankReduce<...>(void*, ...)`` keep their scope)."""
+    n = name.strip()
+    if n.endswith(")"):
+        depth = 0
+        for i in range(len(n) - 1, -1, -1):
+            depth += {")": 1, "(": -1}.get(n[i], 0)
+            if depth == 0:
+                n = n[:i]
+                break
+    return n[-140:]
+
+
+RCCL_RE = re.compile(r"nccl|rccl|oneRankReduce", re.I)
 
 
 def analyse(rows):
@@ -83,7 +95,7 @@ def analyse(rows):
                   "queues": sorted(x for x in d["queues"] if x is not None),
                   "streams": sorted(x for x in d["streams"] if x is not None),
                   "dur_ns_p50": ds[len(ds) // 2], "dur_ns_max": ds[-1],
-                  "rccl": bool(re.search(r"nccl|rccl", k, re.I))}
+                  "rccl": bool(RCCL_RE.search(k))}
     span = sum(r["end"] - r["start"] for r in persist)
     return {
         "persist_kernel": {"dispatches": len(persist), "resident_ns_total": span,

@@ -87,6 +87,10 @@ class EngineConfig:
                                      # one per partition for GBDT's binned rows, else 1)
     model_watch: str = ""            # hot-swap when this safetensors file changes (rank 0)
     output_mode: str = "zerocopy"    # zerocopy (kernel writes pinned host) | dma
+    exec_mode: str = "auto"          # persistent | launch | auto (persistent for zero-copy in/out:
+                                     # the mode bench.py measures; launch_/engine_service.py)
+    handoff_capacity: int = 1 << 21  # fraud starts queued for KIE before scoring pauses (back-pressure)
+    handoff_workers: int = 2         # pooled HTTP workers of the KIE hand-off (router/handoff.py)
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches
     reduce_period_ms: float = 10.0   # X2 counter all-reduce period
     gbdt_trees: int = 100
@@ -131,6 +135,8 @@ ENV_MAP = {
     "CCFD_MODEL_WATCH": ("engine", "model_watch", str),
     "CCFD_INPUT_MODE": ("engine", "input_mode", str),
     "CCFD_OUTPUT_MODE": ("engine", "output_mode", str),
+    "CCFD_EXEC_MODE": ("engine", "exec_mode", str),
+    "CCFD_HANDOFF_CAPACITY": ("engine", "handoff_capacity", int),
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),
     "CCFD_KAFKA_PARTITIONS": ("kafka", "partitions", int),
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),

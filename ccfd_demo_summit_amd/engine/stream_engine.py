@@ -124,6 +124,46 @@ class PartitionLog:
 
 
 @dataclass
+class LastScored:
+    """The last transaction the engine scored (the reference model's "last request":
+    deploy/grafana/ModelPrediction.json:96-322 plots proba_1, Amount, V17, V10 of it).
+    ``row`` holds its raw log row in the engine's row format."""
+    tx_id: int
+    proba: float
+    amount: float
+    partition: int
+    row: bytes
+    row_format: str
+
+    def features(self, bins=None) -> np.ndarray:
+        """float32 [30] canonical row: exact for f32 rows, bf16-exact V-columns for W64 rows;
+        for G32 / G20 rows (bins against the ensemble's split table) each feature is the
+        midpoint of its bin interval (the end edge for the two open bins, NaN without
+        ``bins``) and Amount is exact (the host-side column)."""
+        from ..contracts.transaction import AMOUNT_COL, decode_g20_bins, decode_wire
+        if self.row_format == "f32":
+            return np.frombuffer(self.row[:120], np.float32).copy()
+        if self.row_format == "w64":
+            return decode_wire(np.frombuffer(self.row[:64], np.uint8))[0]
+        g = np.frombuffer(self.row[:32], np.uint8) if self.row_format == "g32" else \
+            decode_g20_bins(np.frombuffer(self.row[:20], np.uint8))[0]
+        x = np.full(N_FEATURES, np.nan, np.float32)
+        if bins is not None:
+            for j, e in enumerate(bins.edges):
+                b = int(g[j])
+                if e.size == 0:
+                    continue
+                if b == 0:
+                    x[j] = e[0]
+                elif b >= e.size:
+                    x[j] = e[-1]
+                else:
+                    x[j] = 0.5 * (float(e[b - 1]) + float(e[b]))
+        x[AMOUNT_COL] = self.amount
+        return x
+
+
+@dataclass
 class StepStats:
     batches: int = 0
     rows: int = 0
@@ -141,15 +181,30 @@ class StepStats:
     dev_batches: int = 0                 # K7: device-clock execution time per micro-batch
     dev_exec_mean_us: float = 0.0
     dev_hist: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+    # row-weighted twins (Seldon request histograms: one transaction = one request)
+    lat_hist_rows: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+    dev_hist_rows: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+    last_seq: int = 0                    # batches that produced a "last scored" record
+    last: Optional[LastScored] = None
+
+
+_FMT_BY_ROW_BYTES = {120: "f32", 64: "w64", 32: "g32", 20: "g20"}
 
 
 def _stats(st: EngineStats) -> StepStats:
+    last = None
+    if st.last_seq:
+        nb = int(st.last_row_bytes)
+        last = LastScored(int(st.last_tx_id), float(st.last_proba), float(st.last_amount),
+                          int(st.last_partition), bytes(st.last_row[:nb]), _FMT_BY_ROW_BYTES.get(nb, "f32"))
     return StepStats(st.batches, st.rows, st.fraud_rows, st.flagged_dropped, st.wall_s,
                      st.lat_p50_us, st.lat_p99_us, st.lat_max_us, st.lat_mean_us,
                      np.ctypeslib.as_array(st.lat_hist).copy(), st.host_submit_ns * 1e-9,
                      st.host_wait_ns * 1e-9, st.host_complete_ns * 1e-9, int(st.dev_batches),
                      (st.dev_exec_ns / st.dev_batches * 1e-3) if st.dev_batches else 0.0,
-                     np.ctypeslib.as_array(st.dev_hist).copy())
+                     np.ctypeslib.as_array(st.dev_hist).copy(),
+                     np.ctypeslib.as_array(st.lat_hist_rows).copy(),
+                     np.ctypeslib.as_array(st.dev_hist_rows).copy(), int(st.last_seq), last)
 
 
 class StreamEngine:

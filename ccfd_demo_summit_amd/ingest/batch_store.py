@@ -90,6 +90,11 @@ class BatchStore:
         with self._lock:
             return {t: len(p) for t, p in self._topics.items()}
 
+    def stored_bytes(self) -> int:
+        """Bytes of record batches the log holds (the broker's working set)."""
+        with self._lock:
+            return sum(L.nbytes for parts in self._topics.values() for L in parts)
+
     def partitions(self, topic: str) -> int:
         self.create_topic(topic)
         return len(self._topics[topic])

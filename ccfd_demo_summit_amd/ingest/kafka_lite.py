@@ -120,11 +120,97 @@ class ClusterState:
         return sum(self.store.topics().values())
 
 
+class _GcTimer:
+    """Process-wide garbage-collection time per generation (one ``gc.callbacks`` hook)."""
+
+    def __init__(self):
+        import gc
+        self.s = [0.0, 0.0, 0.0]
+        self.n = [0, 0, 0]
+        self._t0 = 0.0
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self._t0 = time.perf_counter()
+        else:
+            g = min(2, int(info.get("generation", 0)))
+            self.s[g] += time.perf_counter() - self._t0
+            self.n[g] += 1
+
+
+_GC = None
+
+
+def gc_timer() -> _GcTimer:
+    global _GC
+    if _GC is None:
+        _GC = _GcTimer()
+    return _GC
+
+
+class ProcessResourceCollector:
+    """The broker-process series of the reference's Kafka dashboard -- CPU, memory and GC
+    (deploy/grafana/Kafka.json:416 ``process_cpu_seconds_total``, :499 ``jvm_memory_bytes_used``,
+    :582 ``jvm_gc_collection_seconds_sum``), all labelled ``strimzi_io_kind="Kafka"`` as the
+    Strimzi pod labels make them.  kafka-lite is not a JVM; the names are kept so the
+    dashboard works unchanged, with these meanings:
+
+    * ``process_cpu_seconds_total`` -- user + system CPU seconds of the broker process;
+    * ``jvm_memory_bytes_used{area="heap"}`` -- bytes of record batches the log holds (the
+      broker's data working set), ``{area="nonheap"}`` -- the rest of the resident set;
+      ``jvm_memory_bytes_max{area="heap"}`` -- physical memory (the ceiling of the log);
+    * ``jvm_gc_collection_seconds`` (summary, ``gc`` = Python collector generation) -- time
+      the broker process spent in garbage collection, measured with ``gc.callbacks``.
+    """
+
+    def __init__(self, store, labels=("strimzi_io_kind",), values=("Kafka",)):
+        self.store = store
+        self.labels = list(labels)
+        self.values = list(values)
+        self.gc = gc_timer()
+
+    def collect(self):
+        import os
+        from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, SummaryMetricFamily
+        t = os.times()
+        c = CounterMetricFamily("process_cpu_seconds", "Broker process CPU seconds (user + system)",
+                                labels=self.labels)
+        c.add_metric(self.values, t.user + t.system)
+        yield c
+        rss = 0
+        try:
+            with open("/proc/self/statm") as f:
+                rss = int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+        except (OSError, ValueError):
+            pass
+        heap = self.store.stored_bytes() if self.store is not None else 0
+        used = GaugeMetricFamily("jvm_memory_bytes_used", "Broker memory in use (heap = log working set)",
+                                 labels=["area"] + self.labels)
+        used.add_metric(["heap"] + self.values, float(heap))
+        used.add_metric(["nonheap"] + self.values, float(max(0, rss - heap)))
+        yield used
+        mx = GaugeMetricFamily("jvm_memory_bytes_max", "Broker memory ceiling (physical memory)",
+                               labels=["area"] + self.labels)
+        try:
+            phys = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
+        except (OSError, ValueError):
+            phys = 0
+        mx.add_metric(["heap"] + self.values, float(phys))
+        yield mx
+        g = SummaryMetricFamily("jvm_gc_collection_seconds", "Time spent in garbage collection",
+                                labels=["gc"] + self.labels)
+        for gen in range(3):
+            g.add_metric([f"python-gen{gen}"] + self.values, count_value=self.gc.n[gen], sum_value=self.gc.s[gen])
+        yield g
+
+
 class BrokerMetrics:
     """The Strimzi/JMX-exporter series the reference's Kafka dashboard queries
     (deploy/grafana/Kafka.json:119-1093): topic message/byte rates, failed requests,
     partition/leader counts, under-replicated and offline partitions (from the cluster
-    state: non-zero while a node is down / a partition has no live leader)."""
+    state: non-zero while a node is down / a partition has no live leader), and the
+    broker-process CPU / memory / GC panels (ProcessResourceCollector)."""
 
     def __init__(self, cluster: ClusterState):
         from prometheus_client import CollectorRegistry, Counter
@@ -137,6 +223,7 @@ class BrokerMetrics:
         self.bytes_out = mk("bytesout", "bytes fetched")
         self.failed_produce = mk("failedproducerequests", "failed produce requests")
         self.failed_fetch = mk("failedfetchrequests", "failed fetch requests")
+        self._seen: Set[str] = set()
         cl = cluster
 
         class _Gauges:
@@ -151,6 +238,16 @@ class BrokerMetrics:
                     g.add_metric(["Kafka"], v)
                     yield g
         self.registry.register(_Gauges())
+        self.registry.register(ProcessResourceCollector(cl.store))
+
+    def topic(self, name: str) -> None:
+        """Create every per-topic series at 0 the first time a topic is used, so the failed
+        produce / fetch panels (Kafka.json:1017,1093) read 0 instead of "no data"."""
+        if name in self._seen:
+            return
+        self._seen.add(name)
+        for c in (self.messages_in, self.bytes_in, self.bytes_out, self.failed_produce, self.failed_fetch):
+            c.labels(name, "Kafka")
 
     def expose(self) -> bytes:
         from prometheus_client import generate_latest
@@ -325,6 +422,7 @@ class KafkaLiteServer:
         for topic, parts in data:
             pr = []
             self._topic(topic)
+            self.metrics.topic(topic)
             for p, rb in parts:
                 err = self._partition_error(topic, p)
                 if err:
@@ -350,6 +448,7 @@ class KafkaLiteServer:
         budget = max_bytes
         for topic, parts in reqs:
             pr = []
+            self.metrics.topic(topic)
             for p, off, pmax in parts:
                 err = self._partition_error(topic, p)
                 if err:

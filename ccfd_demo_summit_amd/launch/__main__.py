@@ -224,33 +224,37 @@ def cmd_engine(a, cfg):
     import numpy as np
     import torch
 
-    from ..metrics.exporter import GpuEngineCollector, MetricsHub
+    from prometheus_client import CollectorRegistry, generate_latest
+
+    from ..metrics.exporter import EngineModelCollector, GpuEngineCollector, MetricsHub
     from ..ops.kernels import DeviceModel
     from ..parallel.dp import broadcast_model, init_distributed, resolve_row_format
     from ..process.kie_server import KieClient
+    from ..router.handoff import KieHandoff
     from ..router.router import Router
     from ..router.rules import RuleSet
     from ..utils.numa import bind_to_gpu
-    from .engine_service import EngineService, EngineServiceConfig
+    from .engine_service import EngineService, EngineServiceConfig, rule_safe_row_format
     ctx = init_distributed()
     bind_to_gpu(ctx.device.index)
-    fmt = resolve_row_format(cfg.engine.model, cfg.engine.wire)
     rules = RuleSet.from_config(cfg.router)
-    if fmt in ("g32", "g20") and rules.feature_vars():
-        # G20 / G32 rows carry bins, not feature values: rules over transaction columns need
-        # the values, so this deployment scores GBDT on f32 rows (exact, 120 B/row)
-        print(f"[engine] routing rules read {sorted(rules.feature_vars())}: GBDT on f32 rows instead of "
-              f"{fmt.upper()}", flush=True)
-        fmt = "f32"
+    fmt, why = rule_safe_row_format(cfg.engine.model, resolve_row_format(cfg.engine.model, cfg.engine.wire), rules)
+    if why:
+        print(f"[engine] {why}", flush=True)
     model = _model(cfg.engine.model, a.weights, cfg.seed) if ctx.rank == 0 else None
     dm = broadcast_model(ctx, model, cfg.engine.model, fmt)      # X1 (+ G20 / G32 bin table)
     broker = _broker(cfg)
     hub = MetricsHub()
-    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
-    router = Router(rules, kie, hub.router)
+    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
+                    cfg.kie.signal_name, timeout_s=cfg.seldon.timeout_ms / 1e3, pool_size=cfg.seldon.pool_size)
+    # fraud starts and response signals go through a bounded async queue with pooled,
+    # retried HTTP: a slow or absent KIE never stalls scoring, commits or X2 (router/handoff.py)
+    handoff = KieHandoff(kie, capacity=cfg.engine.handoff_capacity, workers=cfg.engine.handoff_workers)
+    router = Router(rules, kie, hub.router, handoff=handoff)
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
         depth=cfg.engine.depth, streams=cfg.engine.streams, input_mode=cfg.engine.input_mode,
+        output_mode=cfg.engine.output_mode, exec_mode=cfg.engine.exec_mode,
         flush_us=cfg.engine.max_delay_us, reduce_period_ms=cfg.engine.reduce_period_ms,
         threshold=cfg.router.fraud_threshold, coalesce=cfg.engine.coalesce,
         ingest_threads=cfg.engine.ingest_threads,
@@ -258,7 +262,18 @@ def cmd_engine(a, cfg):
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     # node-local port: every node's (pod's) local rank 0 serves the base port its probes and
     # scrape annotation name, whatever its global rank in a multi-node job
-    _serve_in_thread(_metrics_app(hub.expose_all), a.host, (a.port or cfg.router.port) + ctx.local_rank)
+    _serve_in_thread(_metrics_app(lambda: hub.expose_all(include_model=False)), a.host,
+                     (a.port or cfg.router.port) + ctx.local_rank)
+    # the model's own endpoint (the reference's modelfull :8000/prometheus, README.md:292-301):
+    # last-request gauges + Seldon engine histograms of THIS rank's streamed traffic
+    mport = cfg.seldon.port if a.model_metrics_port is None else a.model_metrics_port
+    if mport:
+        model_reg = CollectorRegistry()
+        model_reg.register(EngineModelCollector(svc.model_source, bins=dm.bins, model_name=cfg.seldon.model_name,
+                                                deployment=cfg.seldon.model_name, predictor=cfg.seldon.model_name))
+        _serve_in_thread(_metrics_app(lambda: generate_latest(model_reg)), a.host, mport + ctx.local_rank)
+    print(f"[engine] rank {ctx.rank}: exec_mode {svc.exec_mode}, rows {dm.row_format}, "
+          f"model metrics :{(mport + ctx.local_rank) if mport else 'off'}", flush=True)
     resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic]) if ctx.rank == 0 else None
     # the router also watches the notification topic KIE publishes to (router.yaml:57-58)
     notif = (broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
@@ -266,7 +281,7 @@ def cmd_engine(a, cfg):
     print(f"[engine] rank {ctx.rank}/{ctx.world} partitions {svc.partitions}", flush=True)
     try:
         while True:
-            svc.step()
+            svc.step()           # never raises on a KIE outage: the hand-off retries, commits wait
             if resp is not None:
                 for r in resp.poll(max_records=10_000):
                     router.on_response(r.value)
@@ -276,6 +291,7 @@ def cmd_engine(a, cfg):
                 notif.commit()
     finally:
         svc.stop()
+        handoff.close(drain_s=5.0)
 
 
 def cmd_producer(a, cfg):
@@ -437,6 +453,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--watch-model", default=None, help="engine: hot-swap weights when this file changes")
+    ap.add_argument("--model-metrics-port", type=int, default=None,
+                    help="engine: port (+ local rank) of the model's /prometheus (proba_1 / Amount / V17 / V10, "
+                         "seldon_api_engine_*); default SELDON port 8000, 0 = off")
     ap.add_argument("--grpc-port", type=int, default=0, help="seldon: also serve seldon.protos gRPC Predict")
     ap.add_argument("--native", action="store_true", help="seldon: C++ epoll REST front end (dynamic GPU batching)")
     ap.add_argument("--workers", type=int, default=1, help="seldon --native: epoll worker threads (one engine each)")

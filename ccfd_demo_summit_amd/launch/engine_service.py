@@ -4,10 +4,13 @@
       -> ingest thread: fetch -> TXB1 memcpy / native JSON parse straight into the pinned
          SPSC ring of the partition (csrc/engine/engine.cpp ring mode)
       -> engine.run(): fused HIP scoring of full micro-batches, deadline flush of partial ones
-      -> flagged (fraud-routed) transactions -> Router -> KIE hand-off (HTTP KieClient or an
-         in-process ProcessEngine)
-      -> Kafka offsets committed only when every row of a message has been scored and
-         routed (at-least-once; the process engine ignores duplicates)
+      -> flagged (fraud-routed) transactions -> Router -> KIE hand-off: a bounded async queue
+         drained by pooled HTTP workers with retry/back-off (router/handoff.py), or an
+         in-process ProcessEngine; a KIE outage never raises out of step()
+      -> Kafka offsets committed only when every row of a message has been scored and the
+         hand-off batch carrying its fraud rows is acknowledged (at-least-once; fraud starts
+         are idempotent per transaction id, so every fraud-routed row starts exactly once);
+         a full hand-off queue pauses scoring (rings fill, consumers stop fetching)
       -> every ``reduce_period_ms``: epoch flip + RCCL all-reduce of device counters and
          latency histograms on a side stream (X2/X3), exported on /prometheus
 
@@ -45,7 +48,11 @@ class EngineServiceConfig:
     reduce_period_ms: float = 10.0
     threshold: float = 0.5
     input_mode: str = "zerocopy"
-    exec_mode: str = "launch"        # "persistent": one resident kernel fed by a descriptor ring
+    output_mode: str = "zerocopy"    # zerocopy (kernel writes pinned host slots) | dma
+    exec_mode: str = "auto"          # "persistent": one resident kernel fed by a descriptor ring;
+                                     # "launch": a fused launch per (coalesced) micro-batch;
+                                     # auto = persistent for zero-copy in/out (MLP / LR, GBDT on
+                                     # G20 / G32 rows) -- bench.py's measured mode, else launch
     max_fetch: int = 2000
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
     native_ingest: bool = True       # Kafka-protocol brokers: C++ consumer thread fetches and writes
@@ -58,6 +65,37 @@ class EngineServiceConfig:
                                      # native code) so scoring latency does not wait on the Python
                                      # router / process loop
     model_watch: Optional[str] = None   # rank 0: hot-swap when this safetensors file changes
+    handoff_hold_low: float = 0.5    # a held (full) hand-off queue resumes scoring below this fill
+
+
+def rule_safe_row_format(model_kind: str, fmt: str, rules) -> Tuple[str, str]:
+    """(row format, reason or "") so device routing rules see what the reference's Drools
+    rules see -- the raw transaction values:
+
+    * W64 rows store V1..V28 as bf16 (Time / Amount stay f32): a rule over a V-column, e.g.
+      ``V17 < -2.5``, could flip for values within ~0.008 of its cutoff, so rules reading any
+      V-column score f32 rows (ADVICE r2);
+    * G20 / G32 rows carry bins, not values: rules over any transaction column need f32 rows.
+    Rules over ``proba`` only keep the compact format."""
+    used = rules.feature_vars() if rules is not None else set()
+    if fmt == "w64" and used - {"Time", "Amount"}:
+        return "f32", (f"routing rules read {sorted(used)}: scoring f32 rows instead of W64 "
+                       "(bf16 V-columns would move rule cutoffs)")
+    if fmt in ("g32", "g20") and used:
+        return "f32", f"routing rules read {sorted(used)}: GBDT on f32 rows instead of {fmt.upper()}"
+    return fmt, ""
+
+
+def resolve_exec_mode(exec_mode: str, model_kind: str, row_format: str, input_mode: str,
+                      output_mode: str) -> str:
+    """``auto`` -> the mode bench.py measures: the persistent kernel whenever inputs and
+    outputs are zero-copy and the model has a persistent kernel (MLP / LR on any rows, GBDT
+    on G20 / G32 rows); coalesced launches otherwise (DMA paths, GBDT on f32 rows)."""
+    if exec_mode != "auto":
+        return exec_mode
+    zc = input_mode == "zerocopy" and output_mode == "zerocopy"
+    ok = model_kind in ("mlp", "lr") or row_format in ("g32", "g20")
+    return "persistent" if zc and ok else "launch"
 
 
 class EngineService:
@@ -81,9 +119,11 @@ class EngineService:
             else:
                 from ..ops.kernels import DeviceRules
                 self.device_rules = DeviceRules(rules, ctx.device)
+        self.exec_mode = resolve_exec_mode(cfg.exec_mode, dm.kind, dm.row_format, cfg.input_mode, cfg.output_mode)
         self.engine = StreamEngine(dm, batch=cfg.batch, depth=cfg.depth, streams=cfg.streams,
-                                   input_mode=cfg.input_mode, threshold=threshold, device=ctx.device.index,
-                                   exec_mode=cfg.exec_mode, coalesce=cfg.coalesce, rules=self.device_rules)
+                                   input_mode=cfg.input_mode, output_mode=cfg.output_mode, threshold=threshold,
+                                   device=ctx.device.index, exec_mode=self.exec_mode, coalesce=cfg.coalesce,
+                                   rules=self.device_rules)
         n_parts = broker.partitions(cfg.topic)
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:
@@ -139,6 +179,19 @@ class EngineService:
         from ..utils.faults import FaultPlan
         self.faults = FaultPlan.from_env(ctx.rank)
         self._fetch = self.cfg.max_fetch
+        # commit gating on the KIE hand-off: offsets released by scoring (snapshotted on the
+        # scoring thread right after the flagged rows of the same batches were drained) wait
+        # here with the hand-off sequence number that carries those fraud rows
+        self.handoff = getattr(router, "handoff", None)
+        self._commit_snap: Dict[int, int] = {}
+        self._commit_wait: Deque[Tuple[int, Dict[int, int]]] = collections.deque()
+        self.held = False                  # hand-off queue full: scoring paused (back-pressure)
+        self.hold_events = 0
+        # "last request" of the reference model's gauges (proba_1 / Amount / V17 / V10) and the
+        # row-weighted latency histograms behind the Seldon engine series (metrics/exporter.py)
+        self.last_scored = None
+        self._lat_rows_cum = np.zeros(256, np.int64)
+        self._dev_rows_cum = np.zeros(256, np.int64)
 
     # ------------------------------------------------------------------ ingest (producer side)
     def _ingest_once(self) -> int:
@@ -189,15 +242,26 @@ class EngineService:
             self._ingest_err = e
 
     # ------------------------------------------------------------------ consumer side
-    def _commit_done(self) -> None:
-        if self.native is not None:                     # offsets whose rows are all scored
+    def _snapshot_commits(self) -> Dict[int, int]:
+        """Scoring thread, right after drain_flagged: what the completed batches released --
+        native consumers: partition -> next offset to commit; Python consumer: partition ->
+        released ring rows (mapped to offsets through ``_pending`` at commit time)."""
+        if self.native is not None:
+            out: Dict[int, int] = {}
             for kc in self.natives:
-                for p, off in kc.committable().items():
-                    self.broker.commit(self.cfg.group_id, self.cfg.topic, p, off)
+                out.update(kc.committable())
+            return out
+        return {p: self.engine.cursor(p) for p in self.partitions}
+
+    def _commit(self, snap: Dict[int, int]) -> None:
+        if not snap:
+            return
+        if self.native is not None:                     # offsets whose rows are all scored
+            for p, off in snap.items():
+                self.broker.commit(self.cfg.group_id, self.cfg.topic, p, off)
             return
         offs = {}
-        for p in self.partitions:
-            released = self.engine.cursor(p)
+        for p, released in snap.items():
             dq = self._pending[p]
             last = None
             while dq and dq[0][0] <= released:
@@ -207,16 +271,42 @@ class EngineService:
         if offs:
             self.consumer.commit(offs)
 
+    def _commit_done(self) -> None:
+        """Commit every snapshot whose fraud rows the hand-off has acknowledged (all of them
+        when the hand-off is synchronous)."""
+        merged: Dict[int, int] = {}
+        while self._commit_wait:
+            seq, snap = self._commit_wait[0]
+            if self.handoff is not None and not self.handoff.acked(seq):
+                break
+            self._commit_wait.popleft()
+            for p, v in snap.items():
+                merged[p] = max(merged.get(p, v), v)
+        self._commit(merged)
+
+    def commits_pending(self) -> int:
+        return len(self._commit_wait)
+
     def _run_once(self, budget_us: Optional[int] = None) -> int:
         st = self.engine.run(self.cfg.run_budget_us if budget_us is None else budget_us, self.cfg.flush_us)
         # drain on the same thread, right after the rows were counted: the router must see
-        # every completed micro-batch's rows together with its flagged records
+        # every completed micro-batch's rows together with its flagged records; the commit
+        # snapshot follows the drain, so it never covers a row whose fraud record is not yet
+        # in _flagged_new (only this thread completes batches)
         flagged = self.engine.drain_flagged() if st.rows else None
+        snap = self._snapshot_commits() if st.rows else None
         with self._stat_lock:
             self._rows_new += int(st.rows)
             if flagged is not None and len(flagged):
                 self._flagged_new.append(flagged)
+            if snap:
+                for p, v in snap.items():
+                    self._commit_snap[p] = max(self._commit_snap.get(p, v), v)
             self._lat_cum = st.lat_hist.astype(np.int64)
+            self._lat_rows_cum = st.lat_hist_rows.astype(np.int64)
+            self._dev_rows_cum = st.dev_hist_rows.astype(np.int64)
+            if st.last_seq:
+                self.last_scored = st.last
             if st.dev_batches:
                 self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
         return int(st.rows)
@@ -246,6 +336,9 @@ class EngineService:
                     except queue.Empty:
                         break
                     task()
+                if self.held:                           # hand-off back-pressure: rings fill,
+                    time.sleep(200e-6)                  # the Kafka consumers stop fetching
+                    continue
                 self._run_once()
         except BaseException as e:                      # surfaced by step()
             self._score_err = e
@@ -258,15 +351,28 @@ class EngineService:
         if self._score_err is not None:
             raise RuntimeError("scoring thread failed") from self._score_err
         threaded = getattr(self, "_score_thread", None) is not None
-        if not threaded:
+        if self.handoff is not None:
+            if not self.held and self.handoff.full():
+                self.held = True
+                self.hold_events += 1
+            elif self.held and self.handoff.has_room(self.cfg.handoff_hold_low):
+                self.held = False
+        if not threaded and not self.held:
             self._run_once()
         with self._stat_lock:
             rows, self._rows_new = self._rows_new, 0
             fl, self._flagged_new = self._flagged_new, []
+            snap, self._commit_snap = self._commit_snap, {}
             lat_cum = self._lat_cum
         flagged = np.concatenate(fl) if len(fl) > 1 else (fl[0] if fl else np.zeros(0, FLAGGED_NP))
+        seq = -1
         if rows or len(flagged):
-            self.router.on_flagged(flagged, rows)
+            self.router.on_flagged(flagged, rows)      # enqueues; never blocks on KIE
+            seq = getattr(self.router, "last_handoff_seq", -1)
+        if snap:
+            if self.handoff is not None and seq < 0:
+                seq = self.handoff.last_seq()          # no new fraud rows: wait for the earlier ones
+            self._commit_wait.append((seq, snap))
         self.rows_scored += rows
         self._commit_done()
         now = time.monotonic()
@@ -367,9 +473,26 @@ class EngineService:
 
     def metrics_source(self):
         c, lat = self.reducer.snapshot()
-        return c, lat, {"rows_scored_local": self.rows_scored,
-                        "kernel_exec_mean_us": self.kernel_exec_mean_us,
-                        "model_version": self.hotswap.version}
+        extra = {"rows_scored_local": self.rows_scored,
+                 "kernel_exec_mean_us": self.kernel_exec_mean_us,
+                 "model_version": self.hotswap.version,
+                 "commits_pending": len(self._commit_wait), "handoff_held": int(self.held)}
+        if self.handoff is not None:
+            hs = self.handoff.stats()
+            extra.update(handoff_queue_depth=hs["depth"], handoff_retries=hs["retries"],
+                         handoff_acked=hs["acked"], handoff_failed=hs["failed"])
+        return c, lat, extra
+
+    def model_source(self) -> dict:
+        """The model / Seldon series' inputs (metrics/exporter.py EngineModelCollector): last
+        scored transaction, row-weighted arrival->scored and device-exec histograms, malformed
+        messages (status 400) and rows the kernel refused (status 500); local to this rank,
+        like each Seldon replica's own series."""
+        malformed = sum(kc.stats()["errors"] for kc in self.natives) if self.natives else 0
+        refused = int(self.reducer.local_snapshot()[0][4])        # CNT_WIRE_STALE, this rank
+        with self._stat_lock:
+            return {"last": self.last_scored, "lat_rows": self._lat_rows_cum.copy(),
+                    "dev_rows": self._dev_rows_cum.copy(), "malformed": malformed, "refused": refused}
 
 
 class _StaticInProcConsumer:

@@ -121,6 +121,11 @@ def kafka_dashboard() -> Dict:
         _panel("Failed produce / fetch", ['sum(kafka_server_brokertopicmetrics_failedproducerequests_total{topic!=""})',
                                           'sum(kafka_server_brokertopicmetrics_failedfetchrequests_total{topic!=""})'],
                legend=["produce", "fetch"]),
+        # broker process resources (Kafka.json:416,499,582; ingest/kafka_lite.py ProcessResourceCollector)
+        _panel("Broker CPU", [f"rate(process_cpu_seconds_total{{{k}}}[2m])"], unit="percentunit", w=8),
+        _panel("Broker memory", [f"sum without(area)(jvm_memory_bytes_used{{{k}}})"], unit="bytes", w=8),
+        _panel("Time in GC", [f"sum without(gc)(rate(jvm_gc_collection_seconds_sum{{{k}}}[5m]))"],
+               unit="percentunit", w=8),
     ])
 
 
@@ -131,6 +136,14 @@ def training_dashboard() -> Dict:
         _panel("Device memory", ["ccfd_train_device_memory_bytes"], unit="bytes", w=18, h=4),
         _panel("Loss", ["ccfd_train_loss"], legend=["{{model}}"]),
         _panel("Samples /s", ["ccfd_train_samples_per_second"], unit="ops", legend=["{{model}}"]),
+        # the reference workbench board's series (SparkMetrics.json:119-352; exporter.TrainMetrics)
+        _panel("Alive workers (Spark name)", ["metrics_master_aliveworkers_value"], kind="singlestat", w=6, h=4),
+        _panel("Memory used / max", ["sum(jvm_memory_bytes_used) / sum(jvm_memory_bytes_max) * 100"],
+               kind="singlestat", w=6, h=4),
+        _panel("Host memory (heap analogue)", ['jvm_memory_bytes_used{area="heap", job="Spark Metrics"}'],
+               unit="bytes", w=6, h=4),
+        _panel("Live device tensors (eden analogue)", ["metrics_jvm_pools_ps_eden_space_used_value"], unit="bytes",
+               w=6, h=4),
     ])
 
 

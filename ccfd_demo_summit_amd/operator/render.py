@@ -46,6 +46,7 @@ def _container(spec: FraudDetectionSpec, name: str, command: List[str], ports=()
 
 
 RDZV_PORT = 29400        # multi-node engine: torchrun c10d rendezvous on pod ccfd-engine-0
+TRAIN_METRICS_PORT = 8095   # trainer /metrics (+ local rank): the SparkMetrics dashboard's series
 
 
 def _workload(kind: str, name: str, app: str, replicas: int, containers, annotations=None, grace: int = 30,
@@ -81,7 +82,8 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
            "CUSTOMER_NOTIFICATION_TOPIC": "ccd-customer-outgoing", "CUSTOMER_RESPONSE_TOPIC": "ccd-customer-response",
            "KIE_SERVER_URL": "http://ccd-service:8090", "SELDON_URL": "http://modelfull-modelfull:8000",
            "SELDON_ENDPOINT": "api/v0.1/predictions", "FRAUD_THRESHOLD": "0.5", "CONFIDENCE_THRESHOLD": "1.0",
-           "CCFD_MODEL": spec.engine.model, "CCFD_WIRE": resolve_row_format(spec.engine.model, spec.engine.row_format)}
+           "CCFD_MODEL": spec.engine.model, "CCFD_WIRE": resolve_row_format(spec.engine.model, spec.engine.row_format),
+           "CCFD_EXEC_MODE": spec.engine.exec_mode, "CCFD_OUTPUT_MODE": spec.engine.output_mode}
     if spec.engine.rules:
         env["ROUTER_RULES"] = spec.engine.rules
     env.update(spec.env)
@@ -116,7 +118,11 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
                       "--rdzv-endpoint", f"ccfd-engine-0.ccfd-engine:{RDZV_PORT}"])
         cmd = LAUNCH + ["supervise", "--", "python", "-m", "torch.distributed.run"] + dist_args + [
             "--nproc-per-node", str(g)] + LAUNCH[1:] + ["engine"] + weights
-        ports = [{"containerPort": 8091, "name": "metrics"}]
+        # rank r also serves the model's own /prometheus on 8000 + r (launch engine
+        # --model-metrics-port): proba_1 / Amount / V17 / V10 + seldon_api_engine_* of its traffic,
+        # scraped by the "ccfd-model" job below (one target per declared port)
+        ports = [{"containerPort": 8091, "name": "metrics"}] + \
+            [{"containerPort": 8000 + r, "name": f"model-{r}"} for r in range(g)]
         if nodes > 1:
             ports.append({"containerPort": RDZV_PORT, "name": "rendezvous"})
             out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "ccfd-engine"},
@@ -183,11 +189,15 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
     if spec.training.deploy:
         t = spec.training
         cmd = ["python", "-m", "torch.distributed.run", "--standalone", "--nproc-per-node", str(t.workers),
-               "-m", "ccfd_demo_summit_amd.train", "--model", t.model, "--out", "/models/model.safetensors"]
+               "-m", "ccfd_demo_summit_amd.train", "--model", t.model, "--out", "/models/model.safetensors",
+               "--metrics-port", str(TRAIN_METRICS_PORT)]
         out.append({"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "ccfd-training"},
                     "spec": {"template": {"metadata": {"labels": {"app": "ccfd-training"}}, "spec": {
                         "restartPolicy": "OnFailure",
-                        "containers": [dict(_container(spec, "train", cmd, gpus=t.gpus * t.workers),
+                        "containers": [dict(_container(spec, "train", cmd, gpus=t.gpus * t.workers,
+                                                       ports=[{"containerPort": TRAIN_METRICS_PORT + r,
+                                                               "name": f"spark-metrics-{r}"}
+                                                              for r in range(t.workers)]),
                                             volumeMounts=[{"name": "models", "mountPath": "/models"}])],
                         "volumes": [{"name": "models", "emptyDir": {}}]}}}})
 
@@ -199,7 +209,19 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
                      {"source_labels": ["__meta_kubernetes_pod_annotation_prometheus_io_path"],
                       "target_label": "__metrics_path__", "regex": "(.+)"},
                      {"source_labels": ["__address__", "__meta_kubernetes_pod_annotation_prometheus_io_port"],
-                      "target_label": "__address__", "regex": "([^:]+)(?::\\d+)?;(\\d+)", "replacement": "$1:$2"}]}]
+                      "target_label": "__address__", "regex": "([^:]+)(?::\\d+)?;(\\d+)", "replacement": "$1:$2"}]},
+                # the engine ranks' model endpoints (8000 + r): ModelPrediction.json selects
+                # instance=~".*:8000", SeldonCore.json sums every rank
+                {"job_name": "ccfd-model", "metrics_path": "/prometheus", "kubernetes_sd_configs": [{"role": "pod"}],
+                 "relabel_configs": [
+                     {"source_labels": ["__meta_kubernetes_pod_container_port_name"], "action": "keep",
+                      "regex": "model-\\d+"}]},
+                # the trainer: SparkMetrics.json selects job="Spark Metrics" (its series are the
+                # Spark analogues of metrics/exporter.py TrainMetrics)
+                {"job_name": "Spark Metrics", "metrics_path": "/metrics", "kubernetes_sd_configs": [{"role": "pod"}],
+                 "relabel_configs": [
+                     {"source_labels": ["__meta_kubernetes_pod_container_port_name"], "action": "keep",
+                      "regex": "spark-metrics-\\d+"}]}]
         out.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "ccfd-prometheus"},
                     "data": {"prometheus.yml": yaml.safe_dump({"global": {"scrape_interval": "5s"},
                                                                "scrape_configs": jobs}, sort_keys=False)}})

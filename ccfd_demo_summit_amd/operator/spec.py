@@ -46,6 +46,8 @@ class EngineSpec:
     model: str = "mlp"
     weights: str = ""                # safetensors file (models.save_model); "" = random init
     row_format: str = "auto"         # f32 | w64 | g32 | g20 | auto
+    exec_mode: str = "auto"          # persistent | launch | auto (persistent for zero-copy in/out)
+    output_mode: str = "zerocopy"    # zerocopy | dma
     rules: str = ""                  # routing rule text or file (ROUTER_RULES)
 
 
@@ -117,6 +119,12 @@ class FraudDetectionSpec:
             # ranks own partitions p = rank (mod world): a rank without one would sit idle
             raise SpecError(f"kafka.partitions {self.kafka.partitions} < {ranks} engine ranks "
                             f"(nodes x gpusPerNode): every rank needs at least one partition")
+        if self.engine.exec_mode not in ("auto", "persistent", "launch"):
+            raise SpecError(f"engine.exec_mode {self.engine.exec_mode!r}: auto | persistent | launch")
+        if self.engine.output_mode not in ("zerocopy", "dma"):
+            raise SpecError(f"engine.output_mode {self.engine.output_mode!r}: zerocopy | dma")
+        if self.engine.exec_mode == "persistent" and self.engine.output_mode != "zerocopy":
+            raise SpecError("engine.exec_mode persistent needs engine.output_mode zerocopy")
         if self.engine.model not in ("mlp", "lr", "gbdt"):
             raise SpecError(f"engine.model {self.engine.model!r}: mlp | lr | gbdt")
         from ..parallel.dp import resolve_row_format

@@ -210,14 +210,17 @@ class CounterReducer:
         self.epochs = 0
         self._work = None
         self.last_ctrl: Optional[torch.Tensor] = None     # reduced control words of the last completion
-        # SUM is the X2 reduction.  At world 1 RCCL elides an in-place SUM (no device kernel);
-        # CCFD_X2_ONE_RANK_KERNEL=1 (evidence runs only, one-GPU boxes) makes it an AVG -- the
-        # identity at world 1 -- which RCCL executes as its OneRankReduce kernel on the
-        # communicator stream, so a kernel trace shows where the W > 1 reduction kernel runs
-        # relative to the scoring kernel (profiles/r3/x2_overlap/)
+        # At world 1 RCCL elides the in-place int64 SUM entirely (no device kernel, measured:
+        # profiles/r3/x2_overlap/).  CCFD_X2_ONE_RANK_KERNEL=1 (evidence runs on a one-GPU box
+        # only) adds, per X2 tick, one float32 AVG all-reduce of the same size on the same
+        # communicator -- RCCL runs that as its oneRankReduce device kernel on the
+        # communicator's stream -- so a kernel trace shows where an X2 reduction kernel
+        # executes relative to the resident scoring kernel
         self._op = dist.ReduceOp.SUM
-        if os.environ.get("CCFD_X2_ONE_RANK_KERNEL") == "1" and ctx.world == 1:
-            self._op = dist.ReduceOp.AVG
+        self._kernel_probe = None
+        self._probe_work = None
+        if os.environ.get("CCFD_X2_ONE_RANK_KERNEL") == "1" and ctx.world == 1 and ctx.initialized:
+            self._kernel_probe = torch.ones(_K + N_CTRL_SLOTS, dtype=torch.float32, device=device)
 
     def busy(self) -> bool:
         return self._work is not None and not self._work.is_completed()
@@ -242,6 +245,9 @@ class CounterReducer:
                 self.freed.record(self.side)
             if self.ctx.initialized:
                 self._work = dist.all_reduce(self.pack, op=self._op, group=self.group, async_op=True)
+                if self._kernel_probe is not None:
+                    self._probe_work = dist.all_reduce(self._kernel_probe, op=dist.ReduceOp.AVG,
+                                                       group=self.group, async_op=True)
             else:
                 self._fold()
         self.epochs += 1
@@ -260,6 +266,9 @@ class CounterReducer:
         with ctxm:
             self._work.wait()            # RCCL: the side stream waits; gloo: the host waits
             self._work = None
+            if self._probe_work is not None:
+                self._probe_work.wait()
+                self._probe_work = None
             self._fold()
 
     def pop_ctrl(self) -> Optional[np.ndarray]:

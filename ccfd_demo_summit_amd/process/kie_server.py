@@ -157,19 +157,36 @@ class KieServer:
 
 
 class KieClient:
-    """HTTP client with the ProcessEngine hand-off interface (router -> KIE, README.md:552,569)."""
+    """HTTP client with the ProcessEngine hand-off interface (router -> KIE, README.md:552,569).
+
+    Pooled: each calling thread (e.g. the KieHandoff workers, router/handoff.py) gets its own
+    keep-alive session with up to ``pool_size`` connections -- the KIE analogue of the
+    reference's SELDON_POOL_SIZE / SELDON_TIMEOUT client settings (README.md:386-393)."""
 
     def __init__(self, url: str, container_id: str = "ccd-fraud-kjar",
                  fraud_process_id: str = "ccd-fraud-kjar.CCDProcess",
                  standard_process_id: str = "ccd-fraud-kjar.StandardProcess",
-                 signal_name: str = "customerResponse", timeout_s: float = 5.0):
+                 signal_name: str = "customerResponse", timeout_s: float = 5.0, pool_size: int = 5):
+        import threading
         self.base = url.rstrip("/") + BASE
         self.c = container_id
         self.fraud_pid = fraud_process_id
         self.standard_pid = standard_process_id
         self.signal_name = signal_name
         self.timeout = timeout_s
-        self.s = requests.Session()
+        self.pool_size = max(1, int(pool_size))
+        self._tls = threading.local()
+
+    @property
+    def s(self) -> requests.Session:
+        sess = getattr(self._tls, "session", None)
+        if sess is None:
+            sess = requests.Session()
+            ad = requests.adapters.HTTPAdapter(pool_connections=1, pool_maxsize=self.pool_size)
+            sess.mount("http://", ad)
+            sess.mount("https://", ad)
+            self._tls.session = sess
+        return sess
 
     def _start(self, pid: str, variables) -> int:
         r = self.s.post(f"{self.base}/containers/{self.c}/processes/{pid}/instances",
@@ -196,4 +213,6 @@ class KieClient:
     def signal(self, instance_id: int, name: str, payload) -> bool:
         r = self.s.post(f"{self.base}/containers/{self.c}/processes/instances/{instance_id}/signal/{name or self.signal_name}",
                         data=json.dumps(payload), headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        if r.status_code >= 500:
+            r.raise_for_status()              # transient: the hand-off retries it
         return r.status_code == 200

@@ -29,7 +29,10 @@ from .rules import RuleSet
 
 class Router:
     def __init__(self, rules: RuleSet, processes, metrics: Optional[RouterMetrics] = None,
-                 standard_mode: str = "count"):
+                 standard_mode: str = "count", handoff=None):
+        """``handoff``: a router.handoff.KieHandoff -- fraud starts and customer-response
+        signals are then enqueued (pooled, retried, never blocking the caller) instead of
+        sent synchronously; ``last_handoff_seq`` is the sequence number of the latest one."""
         if standard_mode not in ("count", "process"):
             raise ValueError("standard_mode must be 'count' or 'process'")
         self.rules = rules
@@ -40,6 +43,8 @@ class Router:
         self.fraud_started = 0
         self.signals_ok = 0
         self.signals_stale = 0
+        self.handoff = handoff
+        self.last_handoff_seq = -1
 
     # ------------------------------------------------------------------ scoring results
     def on_scored(self, ids, customers, proba, X: Optional[np.ndarray] = None,
@@ -73,6 +78,16 @@ class Router:
         self.metrics.tx_incoming.inc(total_rows)
         self.metrics.tx_outgoing.labels(type="fraud").inc(nf)
         self.metrics.tx_outgoing.labels(type="standard").inc(total_rows - nf)
+        if self.handoff is not None:                        # async, retried, acked later
+            if nf:
+                self.last_handoff_seq = self.handoff.submit_starts(
+                    [{"transaction_id": int(r["tx_id"]), "customer_id": int(r["customer"]),
+                      "amount": float(r["amount"]), "proba": float(r["proba"])} for r in flagged])
+                with self._lock:
+                    self.fraud_started += nf
+            else:
+                self.last_handoff_seq = -1
+            return {"incoming": total_rows, "fraud": nf, "standard": total_rows - nf}
         many = getattr(self.processes, "start_fraud_many", None)
         if many is not None and nf > 1:                     # one hand-off for the whole step
             many([{"transaction_id": int(r["tx_id"]), "customer_id": int(r["customer"]),
@@ -99,6 +114,9 @@ class Router:
         approved = bool(msg.get("response"))
         self.metrics.notif_incoming.labels(
             response=CustomerResponse.from_bool(approved).value).inc()
+        if self.handoff is not None:                        # outcome counted by the hand-off
+            self.last_handoff_seq = self.handoff.submit_signal(int(msg["process_id"]), "customerResponse", approved)
+            return True
         ok = self.processes.signal(int(msg["process_id"]), "customerResponse", approved)
         with self._lock:
             if ok:

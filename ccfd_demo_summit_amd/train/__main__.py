@@ -19,6 +19,30 @@ import sys
 import numpy as np
 
 
+def _serve_metrics(port: int):
+    """TrainMetrics on :port/metrics in a daemon thread (stdlib HTTP server)."""
+    import threading
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+    from ..metrics.exporter import CONTENT_TYPE, TrainMetrics
+    tm = TrainMetrics()
+
+    class H(BaseHTTPRequestHandler):
+        def do_GET(self):
+            body = tm.expose()
+            self.send_response(200)
+            self.send_header("Content-Type", CONTENT_TYPE)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+    srv = ThreadingHTTPServer(("0.0.0.0", port), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return tm
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--model", default="mlp", choices=["lr", "mlp", "gbdt"])
@@ -34,6 +58,12 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--version", default="1")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--max-borders", type=int, default=31,
+                    help="GBDT: split candidates per feature (<= 31 keeps every trained ensemble on the "
+                         "20-byte G20 row format; <= 255 for G32)")
+    ap.add_argument("--metrics-port", type=int, default=0,
+                    help="serve the trainer's /metrics (the SparkMetrics dashboard series) on this port "
+                         "(+ rank) while training; 0 = off")
     ap.add_argument("--from-catboost", default=None,
                     help="import an oblivious CatBoost JSON model (models/gbdt_import.py) instead of training")
     a = ap.parse_args(argv)
@@ -54,6 +84,10 @@ def main(argv=None) -> int:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    tm = None
+    if a.metrics_port:
+        tm = _serve_metrics(a.metrics_port + int(os.environ.get("LOCAL_RANK", "0")))
+        tm.workers.set(world)
     if world > 1 and not dist.is_initialized():
         use_gpu = a.device != "cpu" and torch.cuda.is_available()
         if use_gpu:
@@ -74,9 +108,10 @@ def main(argv=None) -> int:
     if world > 1 and dev == "auto" and torch.cuda.is_available():
         dev = f"cuda:{torch.cuda.current_device()}"
     if a.model == "gbdt":
-        model, info = train_oblivious_gbdt(X[tr], y[tr], n_trees=a.trees, depth=a.depth, device=dev)
+        model, info = train_oblivious_gbdt(X[tr], y[tr], n_trees=a.trees, depth=a.depth, device=dev,
+                                           n_bins=a.max_borders + 1)
     else:
-        cfg = TrainConfig(epochs=a.epochs, batch=a.batch, device=dev, seed=a.seed)
+        cfg = TrainConfig(epochs=a.epochs, batch=a.batch, device=dev, seed=a.seed, metrics=tm)
         model, info = (train_mlp if a.model == "mlp" else train_logistic)(X[tr], y[tr], cfg)
     if rank == 0:
         metrics = evaluate(model, X[te], y[te]) if n_test and 0 < y[te].sum() < n_test else {}

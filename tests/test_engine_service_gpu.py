@@ -113,3 +113,108 @@ def test_engine_service_native_kafka_ingest_and_hot_swap(gpu, tmp_path):
         svc.stop()
         kb.close()
         lite.stop()
+
+
+def test_persistent_engine_service_kafka_kie_outage_exactly_once(gpu):
+    """The deployed path: EngineService in exec_mode persistent (the
+    bench's mode, now the default for zero-copy) fed by the native Kafka consumer from
+    kafka-lite (TXB1 batches + one JSON transaction per message), fraud rows handed to a KIE
+    server over HTTP through the async hand-off -- and KIE goes away for 5 s mid-stream
+    (2.5 s connection refused, 2.5 s of 503s).  No exception leaves step(); offsets are held
+    while hand-offs are unacknowledged; afterwards every row is scored once, the committed
+    lag is 0, and every fraud-routed transaction is started exactly once.  The model's
+    last-request gauges and Seldon histograms come from the same streamed traffic."""
+    from ccfd_demo_summit_amd.contracts import TxBatch
+    from ccfd_demo_summit_amd.contracts.transaction import Transaction, encode_tx_json
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
+    from ccfd_demo_summit_amd.metrics import MetricsHub
+    from ccfd_demo_summit_amd.metrics.exporter import EngineModelCollector
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import DistContext
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    from ccfd_demo_summit_amd.process.kie_server import KieClient
+    from ccfd_demo_summit_amd.router import Router, RuleSet
+    from ccfd_demo_summit_amd.router.handoff import KieHandoff
+    from prometheus_client import CollectorRegistry, generate_latest
+    from tests.helpers.faulty_proxy import FaultyProxy
+    from tests.helpers.kie_thread import KieThread
+
+    n_txb, n_json = 24_000, 12_000
+    X, _ = generate(n_txb + n_json, seed=11)
+    ids = np.arange(1, n_txb + n_json + 1, dtype=np.uint64) + np.uint64(7 << 32)
+    m = build_model("mlp", seed=3, X_ref=X, calibrate_rate=0.02)
+    lite = KafkaLiteServer("127.0.0.1", 0, default_partitions=2).start_in_thread()
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 2)
+    procs = ProcessEngine(notification_timeout_s=1e9)
+    kie = KieThread(procs)
+    px = FaultyProxy(kie.port)
+    client = KieClient(px.url, timeout_s=1.0, pool_size=4)
+    ho = KieHandoff(client, workers=2, backoff_s=0.02, max_backoff_s=0.3)
+    hub = MetricsHub()
+    router = Router(RuleSet.threshold(0.5), client, hub.router, handoff=ho)
+    ctx = DistContext(0, 1, 0, gpu, "none")
+    dm = DeviceModel(m, gpu, wire=True)
+    svc = EngineService(ctx, dm, kb, router,
+                        EngineServiceConfig(batch=4096, depth=8, streams=2, ring_rows=1 << 16, flush_us=200,
+                                            reduce_period_ms=1.0)).start()
+    try:
+        assert svc.exec_mode == "persistent" and svc.native is not None
+        for k in range(0, n_txb, 2000):                      # TXB1 micro-batches, both partitions
+            kb.produce("odh-demo", TxBatch(ids=ids[k:k + 2000], customer=(ids[k:k + 2000] % 999).astype(np.uint32),
+                                           features=X[k:k + 2000]).encode(), partition=(k // 2000) % 2)
+        t0 = time.time()
+        while svc.rows_scored < n_txb and time.time() - t0 < 60:
+            svc.step()
+        assert svc.rows_scored == n_txb
+        # KIE outage, while JSON transactions (the reference's wire format) keep arriving
+        px.set_mode("refuse")
+        msgs = [encode_tx_json(Transaction(int(ids[i]), int(ids[i] % 999), X[i])) for i in range(n_txb, n_txb + n_json)]
+        for p in range(2):
+            kb.produce_many("odh-demo", msgs[p::2], partition=p)
+        t_out = time.time()
+        held_seen = False
+        while time.time() - t_out < 5.0:
+            if time.time() - t_out > 2.5 and px.mode != "503":
+                px.set_mode("503")
+            svc.step()                                        # must never raise
+            held_seen |= svc.commits_pending() > 0 and kb.lag("ccfd-engine", "odh-demo") > 0
+        assert svc.rows_scored == n_txb + n_json
+        assert held_seen, "offsets were committed past unacknowledged fraud hand-offs"
+        assert ho.stats()["retries"] > 0
+        px.set_mode("pass")
+        t0 = time.time()
+        while (ho.depth() or svc.commits_pending() or kb.lag("ccfd-engine", "odh-demo")) and time.time() - t0 < 60:
+            svc.step()
+        assert kb.lag("ccfd-engine", "odh-demo") == 0 and ho.depth() == 0
+        nf = int(hub.router.tx_outgoing.labels(type="fraud")._value.get())
+        started = sorted(int(i.variables["transaction_id"]) for i in procs.instances.values())
+        assert len(started) == len(set(started)) == nf == router.fraud_started > 0
+        # routes: the device's fraud set vs the fp32 oracle -- any difference only inside the
+        # bf16 rounding band around the threshold
+        p32 = m.predict_proba(X)
+        want = set(ids[p32 >= 0.5].tolist())
+        diff = want.symmetric_difference(started)
+        band = {int(ids[i]) for i in np.nonzero(np.abs(p32 - 0.5) < 0.01)[0]}
+        assert diff <= band, sorted(diff - band)[:5]
+        # the model / Seldon series of the streamed traffic (ModelPrediction / SeldonCore boards)
+        ms = svc.model_source()
+        assert ms["last"] is not None and int(ms["lat_rows"].sum()) == n_txb + n_json
+        assert ms["malformed"] == 0 and ms["refused"] == 0
+        assert int(ms["last"].tx_id) in set(ids.tolist())
+        reg = CollectorRegistry()
+        reg.register(EngineModelCollector(svc.model_source))
+        text = generate_latest(reg).decode()
+        for name in ("proba_1 ", "Amount ", "V17 ", "V10 ",
+                     'seldon_api_engine_server_requests_seconds_count{status="200"} %d.0' % (n_txb + n_json),
+                     "seldon_api_engine_client_requests_seconds_bucket{"):
+            assert name in text, name
+    finally:
+        svc.stop()
+        ho.close(drain_s=1.0)
+        px.close()
+        kie.close()
+        kb.close()
+        lite.stop()

@@ -1,0 +1,143 @@
+"""Router -> KIE hand-off under a KIE outage (README.md:552,569):
+the hand-off never blocks or raises on the scoring path, retries through a 5 s outage
+(connection refused, then 5xx), and afterwards every fraud-routed transaction has been
+started exactly once; offsets are committed only behind acknowledged hand-offs."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.ops._lib import FLAGGED_DTYPE
+from ccfd_demo_summit_amd.process import ProcessEngine
+from ccfd_demo_summit_amd.process.kie_server import KieClient
+from ccfd_demo_summit_amd.router import Router, RuleSet
+from ccfd_demo_summit_amd.router.handoff import KieHandoff
+from tests.helpers.faulty_proxy import FaultyProxy
+from tests.helpers.kie_thread import KieThread
+
+
+def _flagged(ids):
+    f = np.zeros(len(ids), np.dtype(FLAGGED_DTYPE))
+    f["tx_id"] = ids
+    f["customer"] = ids % 1000
+    f["proba"] = 0.9
+    f["amount"] = 42.0
+    return f
+
+
+@pytest.fixture()
+def kie():
+    procs = ProcessEngine(notification_timeout_s=1e9)
+    k = KieThread(procs)
+    px = FaultyProxy(k.port)
+    yield procs, k, px
+    px.close()
+    k.close()
+
+
+def test_kie_outage_never_blocks_and_starts_exactly_once(kie):
+    procs, _, px = kie
+    client = KieClient(px.url, timeout_s=1.0, pool_size=4)
+    ho = KieHandoff(client, workers=3, max_batch=64, backoff_s=0.02, max_backoff_s=0.4)
+    router = Router(RuleSet.threshold(0.5), client, handoff=ho)
+    rng = np.random.default_rng(0)
+    next_id = 1
+    sent = []
+    worst_call = 0.0
+    t_start = time.monotonic()
+    outage = (0.6, 5.6)                       # 2.5 s refused, then 2.5 s of 503s
+    while time.monotonic() - t_start < 7.5:
+        el = time.monotonic() - t_start
+        want = "pass" if not outage[0] <= el < outage[1] else ("refuse" if el < outage[0] + 2.5 else "503")
+        if px.mode != want:
+            px.set_mode(want)
+        n = int(rng.integers(1, 40))
+        ids = np.arange(next_id, next_id + n, dtype=np.uint64)
+        next_id += n
+        sent.extend(ids.tolist())
+        t0 = time.perf_counter()
+        router.on_flagged(_flagged(ids), 4096)                 # must never block or raise
+        worst_call = max(worst_call, time.perf_counter() - t0)
+        time.sleep(0.01)
+    assert worst_call < 0.05, worst_call
+    assert ho.drain(30), ho.stats()
+    st = ho.stats()
+    assert st["retries"] > 0 and st["failed"] == 0 and st["depth"] == 0
+    assert st["acked"] == st["submitted"] == len(sent)
+    # every fraud-routed transaction started exactly once (re-sent batches were deduplicated)
+    started = {inst.variables["transaction_id"] for inst in procs.instances.values()}
+    assert started == set(sent)
+    assert len(procs.instances) == len(sent)
+    assert router.fraud_started == len(sent)
+    ho.close()
+
+
+def test_acked_seq_is_a_contiguous_prefix():
+    """Out-of-order completion across workers: acked_seq only advances over a prefix."""
+    gate = threading.Event()
+    done = []
+
+    class Sink:
+        def start_fraud_many(self, items):
+            if items[0]["transaction_id"] == 0:
+                gate.wait(5)                       # the first batch is slow
+            done.append(items[0]["transaction_id"])
+
+        def start_fraud(self, v):
+            self.start_fraud_many([v])
+
+    ho = KieHandoff(Sink(), workers=3, max_batch=2)
+    s0 = ho.submit_starts([{"transaction_id": 0}, {"transaction_id": 1}])
+    s1 = ho.submit_starts([{"transaction_id": 2}, {"transaction_id": 3}])
+    t0 = time.time()
+    while 2 not in done and time.time() - t0 < 5:
+        time.sleep(0.01)
+    assert 2 in done and not ho.acked(s0) and not ho.acked(s1)
+    gate.set()
+    assert ho.drain(5) and ho.acked(s1)
+    ho.close()
+
+
+def test_full_queue_reports_backpressure():
+    block = threading.Event()
+
+    class Sink:
+        def start_fraud_many(self, items):
+            block.wait(5)
+
+        def start_fraud(self, v):
+            block.wait(5)
+    ho = KieHandoff(Sink(), capacity=100, workers=1, max_batch=50)
+    ho.submit_starts([{"transaction_id": i} for i in range(150)])
+    assert ho.full() and not ho.has_room()
+    block.set()
+    assert ho.drain(5) and ho.has_room() and ho.depth() == 0
+    ho.close()
+
+
+def test_non_retryable_answer_is_reported_not_wedged():
+    class Sink:
+        def start_fraud_many(self, items):
+            raise ValueError("404 container not instantiated")
+    ho = KieHandoff(Sink(), workers=1)
+    ho.submit_starts([{"transaction_id": 1}, {"transaction_id": 2}])
+    assert ho.drain(5)
+    assert ho.stats()["failed"] == 1 and ho.failed[0][0] == "start"
+    ho.close()
+
+
+def test_signals_go_through_the_handoff(kie):
+    procs, _, px = kie
+    client = KieClient(px.url, timeout_s=1.0)
+    ho = KieHandoff(client, workers=1, backoff_s=0.02)
+    router = Router(RuleSet.threshold(0.5), client, handoff=ho)
+    iid = procs.start_fraud({"transaction_id": 77, "customer_id": 1, "amount": 5.0, "proba": 0.9})
+    px.set_mode("refuse")
+    assert router.on_response(b'{"process_id": %d, "response": true}' % iid)   # queued, no raise
+    time.sleep(0.3)
+    px.set_mode("pass")
+    assert ho.drain(10)
+    assert procs.get(iid).outcome == "approved_by_customer"
+    assert ho.stats()["signals_ok"] == 1 and ho.stats()["retries"] > 0
+    ho.close()

@@ -106,3 +106,20 @@ def test_elastic_service_ranks_score_topic_exactly_once():
                 p.kill()
         kb.close()
         lite.stop()
+
+
+def test_rule_safe_row_format():
+    """Device routing rules see what the reference's Drools rules see: rules over
+    V-columns move off W64's bf16 V-columns onto f32 rows; Time / Amount rules stay on W64 (those
+    columns are f32 there); binned G20 / G32 rows only serve proba-only rules."""
+    from ccfd_demo_summit_amd.launch.engine_service import rule_safe_row_format
+    from ccfd_demo_summit_amd.router.rules import RuleSet
+    v = RuleSet.parse("when proba >= 0.5 or V17 < -2.5 then fraud\notherwise standard")
+    amt = RuleSet.parse("when proba >= 0.5 and amount > 100 then fraud\notherwise standard")
+    p = RuleSet.parse("when proba >= 0.7 then fraud\notherwise standard")
+    assert rule_safe_row_format("mlp", "w64", v)[0] == "f32"
+    assert rule_safe_row_format("mlp", "w64", amt) == ("w64", "")
+    assert rule_safe_row_format("mlp", "w64", p) == ("w64", "")
+    assert rule_safe_row_format("gbdt", "g20", amt)[0] == "f32"
+    assert rule_safe_row_format("gbdt", "g20", p) == ("g20", "")
+    assert rule_safe_row_format("mlp", "f32", v) == ("f32", "")

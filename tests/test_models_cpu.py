@@ -209,3 +209,20 @@ def test_sklearn_mlp_import_matches_predict_proba_and_refuses_other_shapes():
         from_sklearn(tanh)
     with pytest.raises(ValueError, match="StandardScaler"):
         from_sklearn(Pipeline([("s", MinMaxScaler()), ("mlp", pipe.steps[-1][1])]))
+
+
+def test_trained_gbdt_100x6_stays_on_g20_rows():
+    """a TRAINED 100 x 6 ensemble (not only the random one) must keep the
+    20-byte G20 row format: the trainer's split candidates are capped at 31 borders a feature
+    (train/__main__.py --max-borders, n_bins = 32), so however the splits concentrate on few
+    features, no feature exceeds 31 distinct thresholds."""
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.train.trainer import train_oblivious_gbdt
+    Xt, yt = generate(30_000, seed=5, fraud_rate=0.02)
+    m, _ = train_oblivious_gbdt(Xt, yt, n_trees=100, depth=6, device="cpu", n_bins=32)
+    spec = m.bin_spec(bits=5)                           # raises if any feature needs > 31 edges
+    ne = np.diff(spec.offsets)
+    assert spec.row_format == "g20" and ne.max() <= 31
+    # without the cap (255 candidates a feature) the same data can exceed G20's 31 edges
+    m2, _ = train_oblivious_gbdt(Xt, yt, n_trees=100, depth=6, device="cpu", n_bins=256)
+    assert np.diff(m2.bin_spec().offsets).max() >= np.diff(spec.offsets).max()
