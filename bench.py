@@ -436,6 +436,12 @@ def main(argv=None):
 
     wd_state.update(engine=eng, epochs=epochs, phase="warmup")
     watchdog.on_fire = lambda: eng.emergency_stop(5000)     # never exit with a resident kernel
+    import signal
+
+    def _term(signum, _frame):                 # an outer SIGTERM: the kernel leaves first
+        eng.emergency_stop(5000)
+        os._exit(128 + signum)
+    signal.signal(signal.SIGTERM, _term)
 
     def step(drain: bool):
         nonlocal flagged_total

@@ -1,0 +1,381 @@
+#!/usr/bin/env python3
+"""Config 5 in the DEPLOYED topology: every service its own OS process, talking over the
+network the way the reference's pods do (README.md:543-569; deploy/router.yaml:55-70;
+deploy/frauddetection_cr.yaml:73-77):
+
+    producer x P  --(Kafka wire: one JSON transaction per message, or TXB1)-->
+    kafka-lite (3 broker listeners, one process)  -->
+    engine ranks under torchrun (partitions p % W == rank; native consumers; persistent
+    kernel; RCCL X1/X2/X3)  --(HTTP, async hand-off)-->  KIE (fraud BP, one process)
+    KIE --(ccd-customer-outgoing)--> notifier process --(ccd-customer-response)--> engine
+    rank 0 --(HTTP signal)--> KIE
+
+Throughput and latency are read from the services' own Prometheus endpoints (router
+``transaction_incoming_total`` on 8091 + r, the engine's X3-merged latency quantiles, the
+model endpoint's ``seldon_api_engine_*`` histograms), sampled every ``--sample-s`` over the
+``--seconds`` window; after the producers stop the harness waits for the consumer-group lag
+to reach 0 and the hand-off to drain, then checks:
+
+* ``transaction_incoming_total`` (all ranks) == transactions produced (all producers);
+* every partition of the topic consumed by exactly one rank (the ranks' partition lists);
+* KIE started one fraud process per fraud-routed transaction (router counters, all ranks)
+  and saw no duplicate start it had to drop (exactly once);
+* every selector of the reference's six Grafana dashboards matches a scraped series
+  (metrics/promql.py; tests/fixtures/reference_dashboard_exprs.json).
+
+The JSON line states ``topology: "shared"`` (vs bench/e2e.py's per-rank stacks).
+
+    python bench/deploy_topology.py --seconds 60 --producers 3 --fmt json         # 1 GPU
+    python bench/deploy_topology.py --ranks 4 --rehearsal --seconds 20             # 4 ranks, 1 GPU, gloo
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+from pathlib import Path
+from typing import Dict, List, Optional
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+PY = sys.executable
+
+
+def free_ports(n: int, contiguous: int = 1) -> List[int]:
+    """n base ports, each followed by contiguous-1 free ports."""
+    out = []
+    base = 20000 + (os.getpid() * 37) % 20000
+    p = base
+    while len(out) < n:
+        ok = True
+        for k in range(contiguous):
+            s = socket.socket()
+            try:
+                s.bind(("127.0.0.1", p + k))
+            except OSError:
+                ok = False
+            finally:
+                s.close()
+            if not ok:
+                break
+        if ok:
+            out.append(p)
+            p += contiguous + 1
+        else:
+            p += 1
+    return out
+
+
+def wait_port(port: int, timeout: float = 120.0) -> None:
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+            return
+        except OSError:
+            time.sleep(0.2)
+    raise TimeoutError(f"port {port} did not open")
+
+
+def http_text(url: str, timeout: float = 5.0) -> str:
+    with urllib.request.urlopen(url, timeout=timeout) as r:
+        return r.read().decode()
+
+
+def metric_sum(text: str, name: str, labels: Optional[Dict[str, str]] = None) -> float:
+    from prometheus_client.parser import text_string_to_metric_families
+    tot = 0.0
+    for fam in text_string_to_metric_families(text):
+        for s in fam.samples:
+            if s.name == name and all(s.labels.get(k) == v for k, v in (labels or {}).items()):
+                tot += s.value
+    return tot
+
+
+def hist_quantile_le(text: str, name: str, q: float, labels: Optional[Dict[str, str]] = None) -> Optional[float]:
+    """histogram_quantile over Prometheus ``le`` buckets (linear inside a bucket)."""
+    from prometheus_client.parser import text_string_to_metric_families
+    b: Dict[float, float] = {}
+    for fam in text_string_to_metric_families(text):
+        for s in fam.samples:
+            if s.name == name + "_bucket" and all(s.labels.get(k) == v for k, v in (labels or {}).items()):
+                le = float("inf") if s.labels["le"] == "+Inf" else float(s.labels["le"])
+                b[le] = b.get(le, 0.0) + s.value
+    if not b:
+        return None
+    les = sorted(b)
+    tot = b[les[-1]]
+    if tot <= 0:
+        return None
+    target = q * tot
+    prev_le, prev_c = 0.0, 0.0
+    for le in les:
+        c = b[le]
+        if c >= target:
+            if le == float("inf"):
+                return prev_le
+            return prev_le + (le - prev_le) * (target - prev_c) / max(c - prev_c, 1e-12)
+        prev_le, prev_c = le, c
+    return les[-2] if len(les) > 1 else None
+
+
+class Proc:
+    def __init__(self, name: str, cmd: List[str], env: Dict[str, str], log_dir: Path):
+        self.name = name
+        self.log = open(log_dir / f"{name}.log", "w")
+        self.p = subprocess.Popen(cmd, env=env, stdout=self.log, stderr=subprocess.STDOUT, cwd=str(ROOT),
+                                  start_new_session=True)
+        self.path = log_dir / f"{name}.log"
+
+    def alive(self) -> bool:
+        return self.p.poll() is None
+
+    def stop(self, sig=signal.SIGTERM, wait: float = 10.0) -> Optional[int]:
+        if self.p.poll() is None:
+            try:
+                os.killpg(self.p.pid, sig)            # the process group this harness started
+            except ProcessLookupError:
+                pass
+            try:
+                self.p.wait(wait)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(self.p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                self.p.wait(5)
+        self.log.close()
+        return self.p.returncode
+
+    def text(self) -> str:
+        try:
+            return self.path.read_text()
+        except OSError:
+            return ""
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--seconds", type=float, default=60.0, help="producer window (sustained rate)")
+    ap.add_argument("--ranks", type=int, default=1, help="engine ranks (torchrun --nproc-per-node)")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="several ranks on one GPU: gloo collectives + CCFD_DEVICE_MODULO (functional check)")
+    ap.add_argument("--producers", type=int, default=3)
+    ap.add_argument("--rate", type=float, default=0.0, help="total produce rate tx/s (0 = open loop, max)")
+    ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
+    ap.add_argument("--batch", type=int, default=4096, help="messages (json) / rows (txb1) per produce request")
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--kafka-nodes", type=int, default=3)
+    ap.add_argument("--retention-batches", type=int, default=500,
+                    help="kafka-lite batches kept per partition (~2 MB each): a consumer that falls this far
+                         "behind loses data and the incoming == produced check fails")
+    ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
+    ap.add_argument("--ingest-threads", type=int, default=0, help="native consumers per rank (0 = partitions / ranks)")
+    ap.add_argument("--notification-timeout-s", type=float, default=30.0)
+    ap.add_argument("--sample-s", type=float, default=5.0)
+    ap.add_argument("--drain-timeout-s", type=float, default=120.0)
+    ap.add_argument("--log-dir", default="gpurun_out/deploy_topology")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    log_dir = ROOT / a.log_dir
+    log_dir.mkdir(parents=True, exist_ok=True)
+
+    kafka_port, = free_ports(1, a.kafka_nodes)
+    metrics_port, kie_port, notif_port, master_port = free_ports(4)
+    router_base, = free_ports(1, a.ranks)
+    model_base, = free_ports(1, a.ranks)
+    brokers = ",".join(f"127.0.0.1:{kafka_port + i}" for i in range(a.kafka_nodes))
+    env = dict(os.environ, PYTHONPATH=str(ROOT), BROKER_URL=brokers, KIE_SERVER_URL=f"http://127.0.0.1:{kie_port}",
+               CCFD_KAFKA_BACKEND="kafka", CCFD_KAFKA_PARTITIONS=str(a.partitions), CCFD_MODEL=a.model,
+               HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    if a.model == "gbdt":
+        env.setdefault("CCFD_WIRE", "auto")
+    procs: List[Proc] = []
+    out: Dict = {"metric": "end-to-end tx/s, deployed topology (separate processes)", "topology": "shared",
+                 "n_gpus": 1 if a.rehearsal else a.ranks, "ranks": a.ranks, "rehearsal": a.rehearsal,
+                 "fmt": a.fmt, "producers": a.producers, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
+                 "model": a.model}
+    try:
+        L = "ccfd_demo_summit_amd.launch"
+        procs.append(Proc("kafka-lite", [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
+                                         "--port", str(kafka_port), "--nodes", str(a.kafka_nodes),
+                                         "--partitions", str(a.partitions), "--metrics-port", str(metrics_port),
+                                         "--retention-batches", str(a.retention_batches)], env, log_dir))
+        wait_port(kafka_port, 60)
+        from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+        kb = KafkaBroker(brokers, connect_wait_s=30)
+        for t, n in (("odh-demo", a.partitions), ("ccd-customer-outgoing", 4), ("ccd-customer-response", 4)):
+            kb.create_topic(t, n)
+        kie_env = dict(env)
+        kie_env["CCFD_KIE_NOTIFICATION_TIMEOUT_S"] = str(a.notification_timeout_s)
+        procs.append(Proc("kie", [PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_port)], kie_env, log_dir))
+        procs.append(Proc("notifier", [PY, "-m", L, "notifier", "--host", "127.0.0.1", "--port", str(notif_port)],
+                          env, log_dir))
+        wait_port(kie_port, 60)
+        eng_env = dict(env)
+        eng_env["CCFD_INGEST_THREADS"] = str(a.ingest_threads or max(1, a.partitions // a.ranks))
+        if a.rehearsal:
+            eng_env.update(CCFD_DIST_BACKEND="gloo", CCFD_DEVICE_MODULO="1")
+        eng_cmd = [PY, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(a.ranks),
+                   "--master-addr", "127.0.0.1", "--master-port", str(master_port),
+                   "-m", L, "engine", "--host", "127.0.0.1", "--port", str(router_base),
+                   "--model-metrics-port", str(model_base)]
+        procs.append(Proc("engine", eng_cmd, eng_env, log_dir))
+        eng = procs[-1]
+        t0 = time.time()
+        while time.time() - t0 < 300:
+            parts = re.findall(r"\[engine\] rank (\d+)/(\d+) partitions \[([0-9, ]*)\]", eng.text())
+            if len(parts) >= a.ranks:
+                break
+            if not eng.alive():
+                raise RuntimeError("engine exited during start-up:\n" + eng.text()[-3000:])
+            time.sleep(0.5)
+        else:
+            raise TimeoutError("engine ranks did not come up:\n" + eng.text()[-3000:])
+        owners: Dict[int, List[int]] = {}
+        for r, _w, plist in parts:
+            for p in (int(x) for x in plist.replace(" ", "").split(",") if x):
+                owners.setdefault(p, []).append(int(r))
+        out["partition_owners"] = {str(p): owners.get(p, []) for p in range(a.partitions)}
+        out["every_partition_exactly_one_rank"] = all(len(owners.get(p, [])) == 1 for p in range(a.partitions))
+        for r in range(a.ranks):
+            wait_port(router_base + r, 60)
+
+        def scrape_all():
+            rows = fraud = 0.0
+            texts = {}
+            for r in range(a.ranks):
+                t = http_text(f"http://127.0.0.1:{router_base + r}/prometheus")
+                texts[f"router{r}"] = t
+                rows += metric_sum(t, "transaction_incoming_total")
+                fraud += metric_sum(t, "transaction_outgoing_total", {"type": "fraud"})
+            return rows, fraud, texts
+
+        # ---- producers: open loop (or --rate split), time-bounded; distinct id ranges
+        prods = []
+        per_rate = a.rate / a.producers if a.rate > 0 else 0.0
+        for i in range(a.producers):
+            prods.append(Proc(f"producer{i}", [PY, "-m", L, "producer", "--fmt", a.fmt, "--batch", str(a.batch),
+                                               "--count", "0", "--seconds", str(a.seconds), "--rate", str(per_rate),
+                                               "--id-base", str((i + 1) << 40), "--seed-offset", str(i * 101)],
+                              env, log_dir))
+        procs.extend(prods)
+        # wait until all producers rendered their pools and started (first tx seen)
+        rows_prev, _, _ = scrape_all()
+        t_start = time.time()
+        while time.time() - t_start < 120:
+            rows_now, _, _ = scrape_all()
+            if rows_now > rows_prev:
+                break
+            time.sleep(0.2)
+        samples = []
+        t_w0 = time.time()
+        r_w0, f_w0, _ = scrape_all()
+        last_t, last_r = t_w0, r_w0
+        while any(p.alive() for p in prods):
+            time.sleep(a.sample_s)
+            now = time.time()
+            r_now, _, _ = scrape_all()
+            samples.append({"t_s": round(now - t_w0, 1), "tx_s": round((r_now - last_r) / (now - last_t), 1),
+                            "lag_msgs": kb.lag("ccfd-engine", "odh-demo")})
+            last_t, last_r = now, r_now
+        t_w1 = time.time()
+        r_w1, _, _ = scrape_all()
+        produced_lines = []
+        for p in prods:
+            m = re.findall(r'(\{"produced".*\})', p.text())
+            if m:
+                produced_lines.append(json.loads(m[-1]))
+        produced = sum(d["produced"] for d in produced_lines)
+        # ---- drain: consumer lag 0 and the engine counters settled
+        t_d = time.time()
+        while time.time() - t_d < a.drain_timeout_s:
+            rows_all, fraud_all, texts = scrape_all()
+            if kb.lag("ccfd-engine", "odh-demo") == 0 and rows_all >= produced:
+                break
+            time.sleep(0.5)
+        time.sleep(2.0)                                  # last hand-offs / X2 ticks
+        rows_all, fraud_all, texts = scrape_all()
+        steady = [s["tx_s"] for s in samples[1:-1]] or [s["tx_s"] for s in samples]
+        out.update({
+            "value": round((r_w1 - r_w0) / max(t_w1 - t_w0, 1e-9), 1), "unit": "tx/s",
+            "window_s": round(t_w1 - t_w0, 1), "samples": samples,
+            "min_sample_tx_s": min(steady) if steady else None,
+            "producers_tx_s": [d["tx_s"] for d in produced_lines],
+            "produced_total": produced,
+            "transaction_incoming_total": rows_all,
+            "incoming_equals_produced": int(rows_all) == int(produced),
+            "drain_s": round(time.time() - t_d, 1),
+            "final_lag_msgs": kb.lag("ccfd-engine", "odh-demo"),
+        })
+        # ---- latency: the engine's X3-merged arrival -> scored quantiles (micro-batch
+        # weighted, exported by rank 0 .. W-1 identically) and the Seldon histogram (row-weighted,
+        # coarse buckets) summed over the ranks' model endpoints
+        t0_text = texts["router0"]
+        q = {}
+        from prometheus_client.parser import text_string_to_metric_families
+        for fam in text_string_to_metric_families(t0_text):
+            for s in fam.samples:
+                if s.name == "ccfd_gpu_batch_latency_quantile_seconds":
+                    q[s.labels["quantile"]] = s.value
+        out["arrival_to_scored_p50_us"] = round(q.get("0.5", float("nan")) * 1e6, 1)
+        out["arrival_to_scored_p99_us"] = round(q.get("0.99", float("nan")) * 1e6, 1)
+        model_texts = [http_text(f"http://127.0.0.1:{model_base + r}/prometheus") for r in range(a.ranks)]
+        mt = "\n".join(model_texts)
+        for qq in (0.5, 0.99):
+            v = hist_quantile_le(mt, "seldon_api_engine_server_requests_seconds", qq, {"status": "200"})
+            out[f"seldon_server_p{int(qq * 100)}_us_bucketed"] = None if v is None else round(v * 1e6, 1)
+        # ---- KIE: exactly one fraud process per fraud-routed transaction (the async hand-off
+        # may still be delivering the last batches)
+        t_k = time.time()
+        while True:
+            stats = json.loads(http_text(f"http://127.0.0.1:{kie_port}/rest/stats"))
+            if int(stats["fraud_started"]) >= int(fraud_all) or time.time() - t_k > 30:
+                break
+            time.sleep(0.5)
+        out["fraud_routed_total"] = fraud_all
+        out["kie"] = stats
+        out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
+        out["kie_duplicates"] = stats["duplicates"]
+        try:
+            out["notifier"] = json.loads(http_text(f"http://127.0.0.1:{notif_port}/health/ping"))
+        except Exception as e:
+            out["notifier"] = {"error": repr(e)}
+        # ---- the reference dashboards against everything this deployment serves
+        from ccfd_demo_summit_amd.metrics import promql
+        series = []
+        for r in range(a.ranks):
+            series += promql.scrape(f"http://127.0.0.1:{router_base + r}/prometheus", "ccfd-pods")
+            series += promql.scrape(f"http://127.0.0.1:{model_base + r}/prometheus", "ccfd-model",
+                                    instance=f"engine-{r}:8000")   # k8s: <pod ip>:8000 (operator/render.py)
+        series += promql.scrape(f"http://127.0.0.1:{kie_port}/rest/metrics", "ccfd-pods")
+        series += promql.scrape(f"http://127.0.0.1:{metrics_port}/metrics", "ccfd-pods")
+        fx = json.loads((ROOT / "tests/fixtures/reference_dashboard_exprs.json").read_text())
+        exprs = {k: [e["expr"] for e in v] for k, v in fx["dashboards"].items() if k != "SparkMetrics.json"}
+        rep = promql.check(exprs, series)
+        out["reference_dashboards"] = {"selectors": rep["selectors"], "matched": rep["matched"],
+                                       "unmatched": [u["selector"] for u in rep["unmatched"]],
+                                       "note": "SparkMetrics.json: the trainer is not part of this topology "
+                                               "(tests/test_dashboard_conformance.py scrapes it)"}
+        ok = (out["incoming_equals_produced"] and out["every_partition_exactly_one_rank"]
+              and out["kie_fraud_started_equals_routed"] and not rep["unmatched"])
+        out["checks_passed"] = bool(ok)
+    finally:
+        for p in reversed(procs):
+            p.stop(wait=40.0 if p.name == "engine" else 10.0)   # the engine drains on SIGTERM
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.out:
+        Path(a.out).write_text(line + "\n")
+    return 0 if out.get("checks_passed") else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

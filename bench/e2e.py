@@ -17,7 +17,13 @@ fraud processes started, notifications/responses, and whether the Prometheus
 ``transaction_incoming_total`` equals the rows scored.
 
     python bench/e2e.py --seconds 20 --broker kafka-lite
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/e2e.py --seconds 20
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/e2e.py --seconds 20 --allow-isolated
+
+Topology: every rank builds its OWN broker, producer, KIE and notifier in-process, so at
+N > 1 this measures N isolated stacks, not one topic sharded over N GPUs with one KIE
+(config 5 as deployed).  The JSON line says so (``topology``); an N > 1 run is refused
+unless ``--allow-isolated``.  The deployed topology -- separate processes, one shared
+kafka-lite topic, torchrun engine ranks, one KIE -- is bench/deploy_topology.py.
 """
 from __future__ import annotations
 
@@ -66,8 +72,16 @@ def main(argv=None):
     ap.add_argument("--kafka-nodes", type=int, default=1, help="kafka-lite broker listeners")
     ap.add_argument("--ingest-threads", type=int, default=0,
                     help="native consumer threads per rank (0 = 1 for TXB1, one per partition for JSON)")
+    ap.add_argument("--allow-isolated", action="store_true",
+                    help="run at N > 1 ranks anyway: N private broker/KIE stacks (labelled topology "
+                         "isolated-per-rank); the shared deployed topology is bench/deploy_topology.py")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
+    import os as _os
+    if int(_os.environ.get("WORLD_SIZE", "1")) > 1 and not args.allow_isolated:
+        raise SystemExit("bench/e2e.py at WORLD_SIZE > 1 builds one private broker + KIE per rank (isolated "
+                         "stacks, not config 5): use bench/deploy_topology.py --ranks N for the shared "
+                         "topology, or pass --allow-isolated to label the run as such")
 
     import torch
     from ccfd_demo_summit_amd.config import load_config
@@ -226,6 +240,8 @@ def main(argv=None):
     incoming = prom.get("transaction_incoming_total")
     out = {
         "metric": "end-to-end tx/s (Kafka ingest -> GPU score -> route -> BP -> notify)",
+        # in-process services; at N > 1 one private stack per rank (see the module doc)
+        "topology": "single-process" if ctx.world == 1 else "isolated-per-rank",
         "value": round(tot / el, 1), "unit": "tx/s", "n_gpus": ctx.world, "seconds": round(el, 2),
         "broker": args.broker, "rate_per_rank": args.rate, "micro_batch": args.batch, "model": args.model, "row_format": dm.row_format,
         "flush_us": args.flush_us, "fmt": args.fmt,

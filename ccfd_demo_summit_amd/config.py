@@ -140,6 +140,7 @@ ENV_MAP = {
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),
     "CCFD_KAFKA_PARTITIONS": ("kafka", "partitions", int),
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),
+    "CCFD_KIE_NOTIFICATION_TIMEOUT_S": ("kie", "notification_timeout_s", float),
 }
 
 

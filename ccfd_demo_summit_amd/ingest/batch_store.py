@@ -48,7 +48,7 @@ def split_batches(data: bytes, verify_crc: bool = True) -> List[Tuple[int, int, 
             raise InvalidBatch("truncated record batch")
         if magic != 2:
             raise InvalidBatch(f"unsupported magic {magic}")
-        if verify_crc and crc32c(bytes(mv[o + 21:end])) != crc:
+        if verify_crc and crc32c(mv[o + 21:end]) != crc:
             raise InvalidBatch("record batch CRC mismatch")
         count = struct.unpack_from(">i", mv, o + _COUNT_OFF)[0]
         if count < 0 or last < 0 or (count and last != count - 1):
@@ -115,10 +115,12 @@ class BatchStore:
             nrec = 0
             now = time.time()
             for last, count, _attrs, mv in batches:
-                b = bytearray(mv)
+                # a writable view is memory the broker owns (kafka-lite receives each produce
+                # request into its own buffer): kept as is, no copy; anything else is copied once
+                b = mv if not mv.readonly else bytearray(mv)
                 struct.pack_into(">q", b, 0, L.end)          # broker-assigned base offset
                 L.bases.append(L.end)
-                L.batches.append(bytes(b))
+                L.batches.append(b)
                 L.ts.append(now)
                 L.end += last + 1
                 L.nbytes += len(b)
@@ -143,10 +145,15 @@ class BatchStore:
     def fetch_raw(self, topic: str, partition: int, offset: int, max_bytes: int) -> bytes:
         """Whole stored batches from the one containing ``offset``, up to ``max_bytes`` (at
         least one batch, like Kafka, so an oversized batch is never stuck)."""
+        return b"".join(self.fetch_parts(topic, partition, offset, max_bytes))
+
+    def fetch_parts(self, topic: str, partition: int, offset: int, max_bytes: int) -> list:
+        """``fetch_raw`` as the list of stored batches themselves (no copy; a fetch response
+        is written to the socket from them)."""
         with self._lock:
             L = self._log(topic, partition)
             if offset >= L.end or not L.batches:
-                return b""
+                return []
             i = max(0, bisect.bisect_right(L.bases, offset) - 1)
             out, size = [], 0
             while i < len(L.batches):
@@ -156,7 +163,7 @@ class BatchStore:
                 out.append(b)
                 size += len(b)
                 i += 1
-            return b"".join(out)
+            return out
 
     def fetch(self, topic: str, partition: int, offset: int, max_records: int = 1000) -> List[Record]:
         from .kafka_wire import decode_record_batches

@@ -254,6 +254,124 @@ class BrokerMetrics:
         return generate_latest(self.registry)
 
 
+class _KafkaConn(asyncio.BufferedProtocol):
+    """One client connection: requests are received straight into memory the broker owns
+    (``recv_into``, no stream-reader copies) and handled from a memoryview of it.  A large
+    request (>= BIG, e.g. a produce of a 4096-message RecordBatch) is received into its own
+    buffer, which the log then keeps as is: produced record batches are never copied
+    (batch_store.append_raw stores views); small requests share a compacting ring buffer,
+    and a small produce request is copied out of it before handling.  Responses keep request
+    order (a long-polling group request holds the ones behind it); reading pauses while the
+    client is slow to take responses (write-side back-pressure)."""
+
+    MAX_FRAME = 256 << 20
+    BIG = 1 << 16
+
+    def __init__(self, server: "KafkaLiteServer"):
+        self.server = server
+        self.buf = bytearray(1 << 18)              # ring for headers + small frames
+        self.w = 0
+        self.frame = None                          # dedicated buffer of the big frame in progress
+        self.fw = 0
+        self.transport = None
+        self.busy = False                          # awaiting a long-polling response
+        self.pending = None
+
+    # asyncio.BufferedProtocol
+    def connection_made(self, transport):
+        import collections
+        self.transport = transport
+        self.pending = collections.deque()
+        self.server._writers.add(self)
+
+    def connection_lost(self, exc):
+        self.server._writers.discard(self)
+
+    def pause_writing(self):
+        self.transport.pause_reading()
+
+    def resume_writing(self):
+        self.transport.resume_reading()
+
+    def get_buffer(self, sizehint):
+        if self.frame is not None:
+            return memoryview(self.frame)[self.fw:]
+        if len(self.buf) - self.w < 1 << 15:       # small frames only: bounded growth
+            nb = bytearray(2 * len(self.buf))
+            nb[:self.w] = self.buf[:self.w]
+            self.buf = nb                          # the transport holds no view across calls
+        return memoryview(self.buf)[self.w:]
+
+    def buffer_updated(self, nbytes):
+        if self.frame is not None:
+            self.fw += nbytes
+            if self.fw == len(self.frame):
+                f, self.frame = self.frame, None
+                self._handle(memoryview(f), owned=True)
+            return
+        self.w += nbytes
+        r = 0
+        mv = memoryview(self.buf)
+        try:
+            while self.w - r >= 4:
+                size = struct.unpack_from(">i", self.buf, r)[0]
+                if size < 0 or size > self.MAX_FRAME:
+                    self.transport.close()
+                    return
+                have = self.w - r - 4
+                if have < size:
+                    if size >= self.BIG:           # receive the rest into its own buffer
+                        self.frame = bytearray(size)
+                        self.frame[:have] = self.buf[r + 4:self.w]
+                        self.fw = have
+                        r = self.w
+                    break
+                msg = mv[r + 4:r + 4 + size]
+                if size >= 2 and msg[0] == 0 and msg[1] == 0:     # produce (api 0): own copy
+                    self._handle(memoryview(bytearray(msg)), owned=True)
+                else:
+                    self._handle(msg, owned=False)
+                r += 4 + size
+        finally:
+            mv.release()
+        if r:                                      # keep the partial frame at the front
+            tail = self.w - r
+            self.buf[:tail] = self.buf[r:self.w]
+            self.w = tail
+
+    def _handle(self, msg, owned: bool):
+        if self.busy:
+            self.pending.append(bytes(msg))
+            return
+        try:
+            out = self.server._frame(msg)
+        except Exception:                          # malformed request: drop the connection
+            self.transport.close()
+            return
+        if isinstance(out, (bytes, bytearray)):
+            self.transport.write(out)
+            return
+        if isinstance(out, list):
+            self.transport.writelines(out)
+            return
+        self.busy = True
+        asyncio.ensure_future(self._finish(out))
+
+    async def _finish(self, coro):
+        try:
+            self.transport.write(await coro)
+        except Exception:
+            self.transport.close()
+            return
+        self.busy = False
+        while self.pending and not self.busy and not self.transport.is_closing():
+            self._handle(memoryview(bytearray(self.pending.popleft())), owned=True)
+
+    def close(self):
+        if self.transport is not None:
+            self.transport.close()
+
+
 class KafkaLiteServer:
     """One broker listener.  Alone it is a one-node cluster; ``KafkaLiteCluster`` builds
     several over a shared store / cluster state / metrics."""
@@ -278,11 +396,12 @@ class KafkaLiteServer:
         self.groups = self.cluster.groups
         self._mid = self.cluster.mid
         self._reaper: Optional[asyncio.Task] = None
-        self._writers: Set[asyncio.StreamWriter] = set()
+        self._writers: Set["_KafkaConn"] = set()
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
-        self._server = await asyncio.start_server(self._serve, self.host, self.port)
+        loop = asyncio.get_running_loop()
+        self._server = await loop.create_server(lambda: _KafkaConn(self), self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
         self.cluster.nodes[self.node_id] = [self.advertise, self.port, True]
         self._reaper = asyncio.get_running_loop().create_task(self._reap_sessions())
@@ -307,7 +426,7 @@ class KafkaLiteServer:
         if self._reaper is not None:
             self._reaper.cancel()
         for w in list(self._writers):
-            w.close()
+            w.close()                               # _KafkaConn.close: transport close
 
     def stop(self):
         if self._loop is not None:
@@ -327,27 +446,22 @@ class KafkaLiteServer:
         return f"{self.host}:{self.port}"
 
     # ------------------------------------------------------------------ connection loop
-    async def _serve(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
-        self._writers.add(writer)
-        try:
-            while True:
-                hdr = await reader.readexactly(4)
-                size = struct.unpack(">i", hdr)[0]
-                msg = await reader.readexactly(size)
-                r = Reader(msg)
-                api, ver, corr = r.i16(), r.i16(), r.i32()
-                r.string()                                  # client id
-                body = self._dispatch(api, ver, r)
-                if not isinstance(body, (bytes, bytearray)):   # group APIs long-poll (JoinGroup, SyncGroup)
-                    body = await body
-                out = struct.pack(">i", corr) + body
-                writer.write(struct.pack(">i", len(out)) + out)
-                await writer.drain()
-        except (asyncio.IncompleteReadError, ConnectionError):
-            pass
-        finally:
-            self._writers.discard(writer)
-            writer.close()
+    def _frame(self, msg) -> object:
+        """One request frame (memoryview) -> the response frame (bytes), or an awaitable of it
+        (the group APIs long-poll: JoinGroup, SyncGroup)."""
+        r = Reader(msg)
+        api, ver, corr = r.i16(), r.i16(), r.i32()
+        r.string()                                  # client id
+        body = self._dispatch(api, ver, r)
+        if isinstance(body, list):                 # response parts, written without joining
+            return [struct.pack(">ii", sum(len(b) for b in body) + 4, corr)] + body
+        if not isinstance(body, (bytes, bytearray)):
+            async def later():
+                b = await body
+                out = struct.pack(">i", corr) + b
+                return struct.pack(">i", len(out)) + out
+            return later()
+        return struct.pack(">ii", len(body) + 4, corr) + body
 
     def _topic(self, name: str) -> bool:
         if name in self.store.topics():
@@ -417,7 +531,7 @@ class KafkaLiteServer:
 
     def _api_0(self, r: Reader) -> bytes:                   # Produce v3: batches stored verbatim
         r.string(); r.i16(); r.i32()
-        data = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.bytes_()))))
+        data = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.view_()))))
         resp = []
         for topic, parts in data:
             pr = []
@@ -460,16 +574,25 @@ class KafkaLiteServer:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     continue
-                rb = self.store.fetch_raw(topic, p, off, max(1, min(pmax, budget))) if budget > 0 else b""
-                budget -= len(rb)
+                rb = self.store.fetch_parts(topic, p, off, max(1, min(pmax, budget))) if budget > 0 else []
+                n = sum(len(b) for b in rb)
+                budget -= n
                 pr.append((p, ERR_NONE, hw, rb))
-                if rb:
-                    self.metrics.bytes_out.labels(topic, "Kafka").inc(len(rb))
+                if n:
+                    self.metrics.bytes_out.labels(topic, "Kafka").inc(n)
             resp.append((topic, pr))
+
+        def records(w2, q):
+            w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(q[2]).array([], None)
+            if q[3] is None:
+                w2.i32(-1)
+                return
+            w2.i32(sum(len(b) for b in q[3]))
+            for b in q[3]:                         # the stored batches, by reference
+                w2.raw(b)
         w = Writer().i32(0)
-        w.array(resp, lambda w_, t: w_.string(t[0]).array(
-            t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(q[2]).array([], None).bytes_(q[3])))
-        return w.build()
+        w.array(resp, lambda w_, t: w_.string(t[0]).array(t[1], records))
+        return w.parts                             # a list: written with one gather (_KafkaConn)
 
     def _api_2(self, r: Reader) -> bytes:                   # ListOffsets v1
         r.i32()
@@ -734,8 +857,11 @@ def main(argv=None):
     ap.add_argument("--nodes", type=int, default=1, help="broker listeners (leadership spread over them)")
     ap.add_argument("--metrics-port", type=int, default=9404, help="Prometheus /metrics (0 = off)")
     ap.add_argument("--advertise", default=None, help="host name put in Metadata (default: --host)")
+    ap.add_argument("--retention-batches", type=int, default=0,
+                    help="record batches kept per partition (0 = unbounded)")
     a = ap.parse_args(argv)
-    cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions, advertise=a.advertise)
+    cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions, advertise=a.advertise,
+                          retention_batches=a.retention_batches or None)
 
     async def run():
         await cl.start()

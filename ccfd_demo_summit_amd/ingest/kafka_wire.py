@@ -80,6 +80,14 @@ def crc32c(data: bytes) -> int:
         except Exception:
             _native_crc = False
     if _native_crc:
+        if isinstance(data, memoryview) and not data.readonly and data.contiguous:
+            import ctypes as C                    # zero-copy: a writable buffer's address
+            n = data.nbytes
+            buf = (C.c_char * n).from_buffer(data)
+            try:
+                return int(_native_crc(C.cast(buf, C.c_char_p), n, 0))
+            finally:
+                del buf
         return int(_native_crc(bytes(data), len(data), 0))
     return _crc32c_py(data)
 
@@ -164,6 +172,17 @@ class Reader:
         if n < 0:
             return None
         v = bytes(self.b[self.o:self.o + n])
+        self.o += n
+        return v
+
+    def view_(self) -> Optional[memoryview]:
+        """Like ``bytes_`` without the copy: a view into the request buffer, valid only while
+        the request is being handled (kafka-lite copies a produce request's batches once,
+        into its log)."""
+        n = self.i32()
+        if n < 0:
+            return None
+        v = self.b[self.o:self.o + n]
         self.o += n
         return v
 
@@ -322,6 +341,21 @@ def encode_request(api_key: int, version: int, corr: int, client_id: str, body: 
     return struct.pack(">i", len(msg)) + msg
 
 
+def _sendall_parts(sock: socket.socket, parts: Sequence) -> None:
+    """sendall over a list of buffers without joining them (scatter-gather ``sendmsg``): a
+    produce request's RecordBatch goes to the socket straight from where it was encoded."""
+    views = [memoryview(p).cast("B") for p in parts if len(p)]
+    while views:
+        n = sock.sendmsg(views[:64])
+        while n:
+            if n >= len(views[0]):
+                n -= len(views[0])
+                views.pop(0)
+            else:
+                views[0] = views[0][n:]
+                n = 0
+
+
 def _recv_exact(sock: socket.socket, n: int) -> bytes:
     buf = bytearray()
     while len(buf) < n:
@@ -351,10 +385,16 @@ class Connection:
         self._corr = itertools.count(1)
         self._lock = threading.Lock()
 
-    def request(self, api_key: int, version: int, body: bytes) -> Reader:
+    def request(self, api_key: int, version: int, body) -> Reader:
+        """``body``: bytes, or a list of buffers sent as they are (no concatenation)."""
         with self._lock:
             corr = next(self._corr)
-            self.sock.sendall(encode_request(api_key, version, corr, self.client_id, body))
+            if isinstance(body, list):
+                hdr = Writer().i16(api_key).i16(version).i32(corr).string(self.client_id).build()
+                n = len(hdr) + sum(len(b) for b in body)
+                _sendall_parts(self.sock, [struct.pack(">i", n) + hdr] + body)
+            else:
+                self.sock.sendall(encode_request(api_key, version, corr, self.client_id, body))
             size = struct.unpack(">i", _recv_exact(self.sock, 4))[0]
             resp = _recv_exact(self.sock, size)
         r = Reader(resp)
@@ -516,9 +556,11 @@ class KafkaBroker:
 
     def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
-        body = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000))
-                .array([topic], lambda w, t: w.string(t).array([partition], lambda w2, p: w2.i32(p).bytes_(record_set)))
-                .build())
+        # [acks, timeout, 1 topic, 1 partition, record set size] + the record set itself, sent
+        # without copying it into the request (Connection.request scatter-gather)
+        head = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000)).i32(1).string(topic)
+                .i32(1).i32(partition).i32(len(record_set)).build())
+        body = [head, record_set]
 
         def parse(r):
             resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))

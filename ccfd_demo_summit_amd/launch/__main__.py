@@ -154,9 +154,10 @@ def cmd_kie(a, cfg):
     endpoint = os.environ.get("SELDON_ENDPOINT") or cfg.kie.seldon_endpoint
     client = SeldonClient(url, endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
                           cfg.seldon.pool_size) if a.remote_prediction else None
+    from ..ingest.producer import BatchingPublisher
+    pub = BatchingPublisher(broker, topic)          # notifications leave in batches, off the request path
     eng = ProcessEngine.from_config(
-        cfg.kie, publish_notification=lambda m: broker.produce(topic, encode_notification(m),
-                                                               key=str(m.get("customer_id")).encode()),
+        cfg.kie, publish_notification=lambda m: pub.publish(encode_notification(m)),
         kie_metrics=KieMetrics(), prediction=PredictionService(cfg.kie.confidence_threshold, client=client),
         journal_path=a.journal)
     srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
@@ -279,6 +280,13 @@ def cmd_engine(a, cfg):
     notif = (broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
              if ctx.rank == 0 else None)
     print(f"[engine] rank {ctx.rank}/{ctx.world} partitions {svc.partitions}", flush=True)
+    # SIGTERM (pod deletion, torchrun shutdown, a supervisor) ends the loop through the
+    # `finally` below: the engine drains and its persistent kernel leaves before exit
+    import signal
+
+    def _term(*_a):
+        raise SystemExit(0)
+    signal.signal(signal.SIGTERM, _term)
     try:
         while True:
             svc.step()           # never raises on a KIE outage: the hand-off retries, commits wait
@@ -297,14 +305,22 @@ def cmd_engine(a, cfg):
 def cmd_producer(a, cfg):
     from ..ingest.producer import ProducerConfig, TransactionProducer
     pc = ProducerConfig.from_env()
-    pc.fmt, pc.batch, pc.rate_tx_s = a.fmt, a.batch, a.rate
+    pc.fmt, pc.batch, pc.rate_tx_s, pc.id_base, pc.seed = a.fmt, a.batch, a.rate, a.id_base, a.seed_offset
     if a.csv:
         pc.source, pc.csv_path = "csv", a.csv
     broker = _broker(cfg)
     prod = TransactionProducer(broker, pc)
-    t0 = time.time()
-    n = prod.produce(a.count)
-    print(json.dumps({"produced": n, "seconds": round(time.time() - t0, 3), "topic": pc.topic}), flush=True)
+    if a.fmt == "json" and pc.source == "synthetic":
+        prod._ensure_pool()                 # render the message pool before the clock starts
+        prod._native_json_record_set()      # (and load the native encoder)
+        prod._seq = 0
+    t0 = time.perf_counter()
+    # --seconds with --count 0: a time-bounded open-loop run (deployment benchmarks)
+    until = t0 + a.seconds if a.count <= 0 else None
+    n = prod.produce(a.count if a.count > 0 else 1 << 62, until=until)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"produced": n, "seconds": round(dt, 3), "tx_s": round(n / max(dt, 1e-9), 1),
+                      "topic": pc.topic, "fmt": pc.fmt, "id_base": pc.id_base}), flush=True)
 
 
 def cmd_demo(a, cfg):
@@ -466,7 +482,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--rate", type=float, default=0.0)
-    ap.add_argument("--count", type=int, default=100_000)
+    ap.add_argument("--count", type=int, default=100_000, help="producer: transactions (0 = run --seconds)")
+    ap.add_argument("--id-base", type=int, default=0, help="producer: first transaction id")
+    ap.add_argument("--seed-offset", type=int, default=0, help="producer: synthetic data seed")
     ap.add_argument("--csv", default=None)
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--max-batch", type=int, default=4096)

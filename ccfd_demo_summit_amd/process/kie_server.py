@@ -46,6 +46,7 @@ class KieServer:
         r.add_get(BASE + "/containers/{c}/tasks/{t}", self.get_task)
         r.add_put(BASE + "/containers/{c}/tasks/{t}/states/completed", self.complete_task)
         r.add_get("/rest/metrics", self.metrics)
+        r.add_get("/rest/stats", self.stats)
         r.add_get(BASE, self.info)
         self.app.on_startup.append(self._startup)
         self.app.on_cleanup.append(self._cleanup)
@@ -149,6 +150,17 @@ class KieServer:
         outcome = out.get("outcome", out.get("approved"))
         ok = self.engine.complete_task(int(request.match_info["t"]), str(outcome))
         return web.Response(status=201 if ok else 404)
+
+    async def stats(self, _request):
+        """Process counts (deployment checks: every fraud-routed transaction started once)."""
+        e = self.engine
+        with e._lock:
+            fraud = sum(1 for i in e.instances.values() if i.process_id == e.FRAUD)
+            body = {"fraud_instances_retained": fraud, "fraud_started": len(e._by_tx), "duplicates": e.duplicates,
+                    "standard_started": e.standard_count, "active": sum(1 for i in e.instances.values()
+                                                                        if i.state.value != "completed"),
+                    "outcomes": dict(e.outcome_counts), "next_instance_id": None}
+        return web.json_response(body)
 
     async def metrics(self, _request):
         m = self.engine.metrics

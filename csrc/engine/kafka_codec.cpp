@@ -32,6 +32,12 @@ inline uint8_t* put_varint(uint8_t* p, int64_t v) {
   return p;
 }
 
+int64_t finish_batch_impl(uint8_t* out, uint8_t* p, int64_t n, int64_t ts_ms);
+// RecordBatch v2 header + CRC over the records written at out + 61 .. p
+inline int64_t finish_batch(uint8_t* out, uint8_t* p, int64_t n, int64_t ts_ms) {
+  return finish_batch_impl(out, p, n, ts_ms);
+}
+
 }  // namespace
 
 extern "C" {
@@ -63,6 +69,52 @@ int64_t ccfd_kafka_encode_batch(const uint8_t* buf, const int64_t* off, int64_t 
     p += vlen;
     *p++ = 0;
   }
+  return finish_batch(out, p, n, ts_ms);
+}
+
+// The producer's hot path for the reference wire format (one JSON transaction per message,
+// README.md:547-548): message i = `{"id":<id0 + i>` + tail[(start + i) % n_pool], the tails
+// being pre-rendered `,"customer_id":..,"Time":..,...,"Amount":..}` bodies
+// (ingest/producer.py json_tail) -- the id is formatted here, so a RecordBatch of n
+// messages is built without a Python object per message.  Returns bytes written or -1.
+int64_t ccfd_kafka_encode_json_batch(const uint8_t* pool, const int64_t* pool_off, int64_t n_pool, int64_t start,
+                                     int64_t n, uint64_t id0, int64_t ts_ms, uint8_t* out, int64_t cap) {
+  if (!pool || !pool_off || !out || n <= 0 || n > INT32_MAX || n_pool <= 0 || start < 0 || cap < 61) return -1;
+  uint8_t* p = out + 61;
+  uint8_t* const end = out + cap;
+  char idbuf[32];
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t k = (start + i) % n_pool;
+    const int64_t tlen = pool_off[k + 1] - pool_off[k];
+    if (tlen < 0) return -1;
+    // decimal id
+    uint64_t v = id0 + (uint64_t)i;
+    int nd = 0;
+    do { idbuf[31 - nd++] = (char)('0' + v % 10); v /= 10; } while (v);
+    const int64_t vlen = 6 + nd + tlen;                // {"id": + digits + tail
+    const int64_t body = 1 + 1 + varint_len(i) + 1 + varint_len(vlen) + vlen + 1;
+    if (end - p < varint_len(body) + body) return -1;
+    p = put_varint(p, body);
+    *p++ = 0;
+    *p++ = 0;
+    p = put_varint(p, i);
+    *p++ = 1;
+    p = put_varint(p, vlen);
+    std::memcpy(p, "{\"id\":", 6);
+    p += 6;
+    std::memcpy(p, idbuf + 32 - nd, (size_t)nd);
+    p += nd;
+    std::memcpy(p, pool + pool_off[k], (size_t)tlen);
+    p += tlen;
+    *p++ = 0;
+  }
+  return finish_batch(out, p, n, ts_ms);
+}
+
+}  // extern "C"
+
+namespace {
+int64_t finish_batch_impl(uint8_t* out, uint8_t* p, int64_t n, int64_t ts_ms) {
   const int64_t total = p - out;
   uint8_t* h = out;
   h = put_be64(h, 0);                                // base offset (the broker assigns it)
@@ -82,5 +134,4 @@ int64_t ccfd_kafka_encode_batch(const uint8_t* buf, const int64_t* off, int64_t 
   put_be32(crc_at, ccfd_crc32c(out + 21, (size_t)(total - 21), 0));
   return total;
 }
-
-}  // extern "C"
+}  // namespace

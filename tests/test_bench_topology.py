@@ -80,3 +80,18 @@ def test_single_rank_mismatch_refused():
     idents, problems = bench._verify_topology(SimpleNamespace(gpus=1, rehearsal=False), ctx,
                                               {"rank": 0, "host": "h", "device": 0, "pci": "p", "name": "x"})
     assert problems == [] and idents[0]["pci"] == "p"
+
+
+def test_e2e_refuses_isolated_stacks_at_n_gt_1():
+    """bench/e2e.py builds a private broker + KIE per rank: at WORLD_SIZE > 1 that is N isolated
+    stacks, not config 5 -- refused without --allow-isolated, and labelled when allowed."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench", "e2e.py"), "--seconds", "1"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0 and "deploy_topology.py" in r.stderr, r.stderr[-500:]
+    src = open(os.path.join(root, "bench", "e2e.py")).read()
+    assert '"isolated-per-rank"' in src and '"topology"' in src
