@@ -174,8 +174,8 @@ def main(argv=None):
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--kafka-nodes", type=int, default=3)
     ap.add_argument("--retention-batches", type=int, default=500,
-                    help="kafka-lite batches kept per partition (~2 MB each): a consumer that falls this far
-                         "behind loses data and the incoming == produced check fails")
+                    help="kafka-lite batches kept per partition (~2 MB each): a consumer that falls this "
+                         "far behind loses data and the incoming == produced check fails")
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
     ap.add_argument("--ingest-threads", type=int, default=0, help="native consumers per rank (0 = partitions / ranks)")
     ap.add_argument("--notification-timeout-s", type=float, default=30.0)

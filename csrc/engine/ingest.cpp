@@ -231,12 +231,7 @@ inline void encode_row_g20_ref(const float* r, uint8_t* o, const float* edges, c
 
 int64_t encode_plan(const float* x, int64_t n, int64_t ld, const ccfd::BinPlan& plan, uint8_t* out,
                     float* amount_out) {
-  const int rb = plan.g20 ? CCFD_G20_ROW_BYTES : CCFD_G32_ROW_BYTES;
-  for (int64_t i = 0; i < n; ++i) {
-    const float* r = x + i * ld;
-    plan.encode(r, out + i * rb);
-    if (amount_out) amount_out[i] = r[CCFD_N_FEATURES - 1];
-  }
+  plan.encode_rows(x, n, ld, out, amount_out);
   return n;
 }
 }  // namespace
@@ -328,4 +323,7 @@ bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32
 }
 void encode_w64_row(const float* x, uint8_t* out) { encode_row_w64(x, out); }
 void encode_bins_row(const BinPlan& plan, const float* x, uint8_t* out) { plan.encode(x, out); }
+void encode_bins_rows(const BinPlan& plan, const float* x, int64_t n, int64_t ld, uint8_t* out, float* amount_out) {
+  plan.encode_rows(x, n, ld, out, amount_out);
+}
 }  // namespace ccfd

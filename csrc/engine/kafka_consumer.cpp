@@ -55,6 +55,7 @@ void set_error(const std::string& e);
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust);
 void encode_w64_row(const float* x, uint8_t* out);
 void encode_bins_row(const BinPlan& plan, const float* x, uint8_t* out);
+void encode_bins_rows(const BinPlan& plan, const float* x, int64_t n, int64_t ld, uint8_t* out, float* amount_out);
 bool g32_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
 bool g20_table_ok(const float* edges, const int32_t* offsets, int32_t stamp);
 }  // namespace ccfd
@@ -169,6 +170,7 @@ class Consumer {
   std::string topic, client = "ccfd-native";
   int wire = 0;                 // sink row format: 0 = f32[30], 1 = W64, 2 = G32, 3 = G20
   ccfd::BinPlan bins;                               // G32 / G20 bin table (ccfd_kc_set_bins), SIMD plan
+  std::vector<float> scratch;                       // aligned copy of a TXB1 block being binned
   int32_t g32_stamp = 0;
   int reset_policy = CCFD_KC_RESET_EARLIEST;
   Sink* sink = nullptr;
@@ -475,7 +477,14 @@ class Consumer {
         std::memcpy(sink->ids(pi) + row, ids + 8 * s, 8 * k);
         std::memcpy(sink->cust(pi) + row, cu + 4 * s, 4 * k);
         uint8_t* dst = sink->feats(pi) + row * rb;
-        if (wire) {
+        if (wire >= 2) {
+          // binned rows: the block goes through the SIMD plan (16 rows at a time with
+          // AVX-512) from an aligned copy (the value sits at any offset of the fetch buffer)
+          scratch.resize((size_t)k * CCFD_N_FEATURES);
+          std::memcpy(scratch.data(), f + (size_t)s * kRow, (size_t)k * kRow);
+          float* am = sink->amount(pi);
+          ccfd::encode_bins_rows(bins, scratch.data(), k, CCFD_N_FEATURES, dst, am ? am + row : nullptr);
+        } else if (wire) {
           float tmp[CCFD_N_FEATURES];
           for (int64_t i = 0; i < k; ++i) {
             std::memcpy(tmp, f + (size_t)(s + i) * kRow, sizeof(tmp));
