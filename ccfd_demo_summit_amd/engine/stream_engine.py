@@ -26,6 +26,19 @@ INPUT_MODES = {"dma": 0, "zerocopy": 1}
 OUTPUT_MODES = {"zerocopy": 0, "dma": 1}
 
 
+def same_bins(a, b) -> bool:
+    """Two bin tables (models.gbdt.BinSpec) are the same table: same width and identical edge
+    arrays.  The 6-bit (G20) / 8-bit (G32) in-row stamp is only a last-resort device check --
+    two different tables share a G20 stamp with probability ~1/63 -- so the host
+    compares the full table wherever it can."""
+    if a is None or b is None:
+        return a is b
+    if a.bits != b.bits or len(a.edges) != len(b.edges):
+        return False
+    return all(x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
+               for x, y in zip(a.edges, b.edges))
+
+
 class PinnedArray:
     """numpy view over ``hipHostMalloc`` memory (mapped, portable): the partition log the
     GPU reads by DMA or directly over PCIe."""
@@ -275,8 +288,8 @@ class StreamEngine:
     def _check_log(self, log: PartitionLog) -> None:
         if log.row_format != self.row_format:
             raise ValueError(f"log rows are {log.row_format}, the engine's model blob expects {self.row_format}")
-        if self.row_format in BIN_FORMATS and log.bins.stamp != self.bins.stamp:
-            raise ValueError("log was G32-encoded against another bin table than the model's")
+        if self.row_format in BIN_FORMATS and not same_bins(log.bins, self.bins):
+            raise ValueError("log was G32 / G20-encoded against another bin table than the model's")
 
     def add_log(self, partition: int, log: PartitionLog, cursor: int = 0) -> None:
         self._check_log(log)
@@ -330,7 +343,7 @@ class StreamEngine:
         if dm.kind != self.dm.kind or dm.row_format != self.row_format or \
                 (dm.trees, dm.depth) != (self.dm.trees, self.dm.depth):
             raise ValueError("hot swap needs a model of the same kind / wire format / tree shape")
-        if self.row_format in BIN_FORMATS and dm.bins.stamp != self.bins.stamp:
+        if self.row_format in BIN_FORMATS and not same_bins(dm.bins, self.bins):
             raise ValueError("G32 hot swap: pack the new ensemble against the live bin table "
                              "(DeviceModel(model, bins=engine.bins)); its thresholds must be bin edges")
         check(lib().ccfd_engine_set_blob(C.c_void_p(self.h), C.c_void_p(dm.blob.data_ptr())),

@@ -226,3 +226,23 @@ def test_trained_gbdt_100x6_stays_on_g20_rows():
     # without the cap (255 candidates a feature) the same data can exceed G20's 31 edges
     m2, _ = train_oblivious_gbdt(Xt, yt, n_trees=100, depth=6, device="cpu", n_bins=256)
     assert np.diff(m2.bin_spec().offsets).max() >= np.diff(spec.offsets).max()
+
+
+def test_same_bins_compares_the_whole_table_not_the_stamp():
+    """the in-row stamp is 6 bits for G20 -- two different tables collide ~1/63 of
+    the time; the host-side checks (log vs model, hot swap) compare the full edge table."""
+    from ccfd_demo_summit_amd.engine.stream_engine import same_bins
+    from ccfd_demo_summit_amd.models.gbdt import BinSpec
+    rng = np.random.default_rng(0)
+    base = [np.unique(rng.standard_normal(10).astype(np.float32)) for _ in range(30)]
+    a = BinSpec([e.copy() for e in base], bits=5)
+    assert same_bins(a, BinSpec([e.copy() for e in base], bits=5))
+    assert not same_bins(a, a.with_bits(8))
+    # find a different table with the same G20 stamp: the stamp alone would accept it
+    for k in range(2000):
+        e2 = [e.copy() for e in base]
+        e2[k % 30] = np.unique(np.append(e2[k % 30], np.float32(5.0 + k)))
+        b = BinSpec(e2, bits=5)
+        if b.stamp == a.stamp:
+            break
+    assert b.stamp == a.stamp and not same_bins(a, b)
