@@ -48,11 +48,14 @@ sys.path.insert(0, str(ROOT))
 PY = sys.executable
 
 
+_PORT_CURSOR = [20000 + (os.getpid() * 37) % 20000]
+
+
 def free_ports(n: int, contiguous: int = 1) -> List[int]:
-    """n base ports, each followed by contiguous-1 free ports."""
+    """n base ports, each followed by contiguous-1 free ports; never hands out a port twice
+    in this process (the services bind them later)."""
     out = []
-    base = 20000 + (os.getpid() * 37) % 20000
-    p = base
+    p = _PORT_CURSOR[0]
     while len(out) < n:
         ok = True
         for k in range(contiguous):
@@ -70,6 +73,7 @@ def free_ports(n: int, contiguous: int = 1) -> List[int]:
             p += contiguous + 1
         else:
             p += 1
+    _PORT_CURSOR[0] = p
     return out
 
 
