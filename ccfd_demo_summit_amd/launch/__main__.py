@@ -261,10 +261,13 @@ def cmd_engine(a, cfg):
         ingest_threads=cfg.engine.ingest_threads,
         model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
+    # the process's node-local rank (torchrun LOCAL_RANK) -- not the device index, which a
+    # several-ranks-per-GPU rehearsal (CCFD_DEVICE_MODULO) maps onto the same GPU
+    port_rank = int(os.environ.get("LOCAL_RANK", ctx.local_rank))
     # node-local port: every node's (pod's) local rank 0 serves the base port its probes and
     # scrape annotation name, whatever its global rank in a multi-node job
     _serve_in_thread(_metrics_app(lambda: hub.expose_all(include_model=False)), a.host,
-                     (a.port or cfg.router.port) + ctx.local_rank)
+                     (a.port or cfg.router.port) + port_rank)
     # the model's own endpoint (the reference's modelfull :8000/prometheus, README.md:292-301):
     # last-request gauges + Seldon engine histograms of THIS rank's streamed traffic
     mport = cfg.seldon.port if a.model_metrics_port is None else a.model_metrics_port
@@ -272,9 +275,9 @@ def cmd_engine(a, cfg):
         model_reg = CollectorRegistry()
         model_reg.register(EngineModelCollector(svc.model_source, bins=dm.bins, model_name=cfg.seldon.model_name,
                                                 deployment=cfg.seldon.model_name, predictor=cfg.seldon.model_name))
-        _serve_in_thread(_metrics_app(lambda: generate_latest(model_reg)), a.host, mport + ctx.local_rank)
+        _serve_in_thread(_metrics_app(lambda: generate_latest(model_reg)), a.host, mport + port_rank)
     print(f"[engine] rank {ctx.rank}: exec_mode {svc.exec_mode}, rows {dm.row_format}, "
-          f"model metrics :{(mport + ctx.local_rank) if mport else 'off'}", flush=True)
+          f"model metrics :{(mport + port_rank) if mport else 'off'}", flush=True)
     resp = broker.consumer(cfg.kafka.group_id + "-responses", [cfg.kafka.response_topic]) if ctx.rank == 0 else None
     # the router also watches the notification topic KIE publishes to (router.yaml:57-58)
     notif = (broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
