@@ -319,6 +319,22 @@ def main(argv=None):
             "drain_s": round(time.time() - t_d, 1),
             "final_lag_msgs": kb.lag("ccfd-engine", "odh-demo"),
         })
+        # ---- ingest attribution: the engine's native consumer threads (ccfd_gpu_ingest_*)
+        att = {}
+        for key in ("ingest_threads", "ingest_io_seconds", "ingest_parse_seconds", "ingest_encode_seconds",
+                    "ingest_ring_wait_seconds", "ingest_rows"):
+            att[key] = sum(metric_sum(texts[f"router{r}"], "ccfd_gpu_" + key) for r in range(a.ranks))
+        if att.get("ingest_threads"):
+            ts = att["ingest_threads"] * max(1e-9, t_w1 - t_start)    # thread-seconds since producers began
+            out["ingest_attribution"] = {
+                "threads": int(att["ingest_threads"]),
+                "broker_io_frac": round(att["ingest_io_seconds"] / ts, 3),
+                "parse_frac": round(att["ingest_parse_seconds"] / ts, 3),
+                "encode_frac": round(att["ingest_encode_seconds"] / ts, 3),
+                "ring_full_wait_frac": round(att["ingest_ring_wait_seconds"] / ts, 3),
+                "parse_ns_per_msg": round(att["ingest_parse_seconds"] * 1e9 / max(1.0, att["ingest_rows"]), 1),
+                "note": "fractions of the consumer threads' wall time since the producers started "
+                        "(includes start-up idle); cumulative counters of the whole run"}
         # ---- latency: the engine's X3-merged arrival -> scored quantiles (micro-batch
         # weighted, exported by rank 0 .. W-1 identically) and the Seldon histogram (row-weighted,
         # coarse buckets) summed over the ranks' model endpoints

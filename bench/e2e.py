@@ -224,10 +224,18 @@ def main(argv=None):
     sig0 = router.signals_ok
     notif0 = _prom(hub).get("notifications_outgoing_total", 0.0)
     inc0 = _prom(hub).get("transaction_incoming_total", 0.0)
+    def kc_totals():
+        tot = {}
+        for kc in svc.natives or []:
+            for k, v in kc.stats().items():
+                tot[k] = tot.get(k, 0) + v
+        return tot
+    kc0 = kc_totals()
     barrier(ctx)
     t0 = time.perf_counter()
     loop_until(t0 + args.seconds)
     elapsed = time.perf_counter() - t0
+    kc1 = kc_totals()
     rows = svc.rows_scored - rows0
     stop.set()
     if th.is_alive():
@@ -262,6 +270,20 @@ def main(argv=None):
         "kafka_nodes": args.kafka_nodes if args.broker == "kafka-lite" else None,
         "ingest_threads": len(svc.natives) if svc.natives else None,
     }
+    if kc1:
+        # where the native consumer threads spent the window (rank 0): waiting on the broker,
+        # parsing responses, writing / encoding rows into the rings, blocked on full rings
+        d = {k: kc1.get(k, 0) - kc0.get(k, 0) for k in kc1}
+        th = max(1, len(svc.natives)) * elapsed
+        rows_in = max(1, d.get("rows", 0))
+        out["ingest_attribution_rank0"] = {
+            "thread_seconds": round(th, 2),
+            "broker_io_frac": round(d["io_ns"] * 1e-9 / th, 3),
+            "parse_frac": round((d["handle_ns"] - d["encode_ns"] - d["ring_wait_ns"]) * 1e-9 / th, 3),
+            "encode_frac": round(d["encode_ns"] * 1e-9 / th, 3),
+            "ring_full_wait_frac": round(d["ring_wait_ns"] * 1e-9 / th, 3),
+            "encode_ns_per_row": round(d["encode_ns"] / rows_in, 2),
+            "rows_ingested": d.get("rows", 0)}
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
         if args.out:

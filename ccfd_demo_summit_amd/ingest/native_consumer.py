@@ -32,7 +32,8 @@ class KcPartition(C.Structure):
 class KcStats(C.Structure):
     _fields_ = [("records", C.c_uint64), ("rows", C.c_uint64), ("bytes", C.c_uint64),
                 ("errors", C.c_uint64), ("fetches", C.c_uint64), ("metadata_refreshes", C.c_uint64),
-                ("offset_resets", C.c_uint64), ("leaders", C.c_uint64)]
+                ("offset_resets", C.c_uint64), ("leaders", C.c_uint64), ("io_ns", C.c_uint64),
+                ("handle_ns", C.c_uint64), ("encode_ns", C.c_uint64), ("ring_wait_ns", C.c_uint64)]
 
 
 RESET_POLICIES = {"earliest": 0, "latest": 1, "none": 2}

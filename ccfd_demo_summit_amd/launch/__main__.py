@@ -167,9 +167,12 @@ def cmd_kie(a, cfg):
 def cmd_notifier(a, cfg):
     from aiohttp import web
 
+    from ..ingest.producer import BatchingPublisher
     from ..process.notifier import NotificationService
     broker = _broker(cfg)
-    ns = NotificationService(lambda raw, key: broker.produce(cfg.kafka.response_topic, raw, key=key),
+    # replies leave in batches (one produce request per linger period, not per reply)
+    pub = BatchingPublisher(broker, cfg.kafka.response_topic)
+    ns = NotificationService(lambda raw, key: pub.publish(raw),
                              cfg.notifier.p_reply, cfg.notifier.p_approve, cfg.notifier.mean_delay_s,
                              cfg.notifier.seed)
     cons = _consumer(broker, a, "notification-service", [cfg.kafka.notification_topic])
@@ -301,8 +304,10 @@ def cmd_engine(a, cfg):
                     router.on_notification_sent(r.value)
                 notif.commit()
     finally:
-        svc.stop()
+        svc.stop()                    # drains; a resident persistent kernel halts here
         handoff.close(drain_s=5.0)
+        print(f"[engine] rank {ctx.rank} stopped: rows scored {svc.rows_scored}, hand-off "
+              f"{json.dumps(handoff.stats())}", flush=True)
 
 
 def cmd_producer(a, cfg):

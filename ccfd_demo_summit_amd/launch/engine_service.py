@@ -477,6 +477,20 @@ class EngineService:
                  "kernel_exec_mean_us": self.kernel_exec_mean_us,
                  "model_version": self.hotswap.version,
                  "commits_pending": len(self._commit_wait), "handoff_held": int(self.held)}
+        if self.natives:
+            # where the native consumer threads spend their time (cumulative seconds):
+            # broker I/O, response parsing, row writing / encoding, waiting on full rings
+            tot: Dict[str, int] = {}
+            for kc in self.natives:
+                for k, v in kc.stats().items():
+                    tot[k] = tot.get(k, 0) + v
+            extra.update(ingest_threads=len(self.natives), ingest_rows=tot.get("rows", 0),
+                         ingest_errors=tot.get("errors", 0),
+                         ingest_io_seconds=tot.get("io_ns", 0) * 1e-9,
+                         ingest_parse_seconds=(tot.get("handle_ns", 0) - tot.get("encode_ns", 0)
+                                               - tot.get("ring_wait_ns", 0)) * 1e-9,
+                         ingest_encode_seconds=tot.get("encode_ns", 0) * 1e-9,
+                         ingest_ring_wait_seconds=tot.get("ring_wait_ns", 0) * 1e-9)
         if self.handoff is not None:
             hs = self.handoff.stats()
             extra.update(handoff_queue_depth=hs["depth"], handoff_retries=hs["retries"],

@@ -179,6 +179,11 @@ class Consumer {
   std::atomic<bool> stop{false};
   std::atomic<uint64_t> n_records{0}, n_rows{0}, n_bytes{0}, n_errors{0}, n_fetches{0};
   std::atomic<uint64_t> n_meta{0}, n_resets{0}, n_leaders{0};
+  std::atomic<uint64_t> t_io{0}, t_handle{0}, t_encode{0}, t_ring_wait{0};   // ns, see ccfd_kc_stats
+  static int64_t mono_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
   std::thread th;
   std::map<int32_t, Conn> brokers;                  // node id -> connection
   bool meta_stale = true;
@@ -429,10 +434,14 @@ class Consumer {
       if (k < 0) return false;
       if (k == 0) {                                   // ring full: wait for the engine
         if (stop.load(std::memory_order_relaxed)) return false;
+        const int64_t tw = mono_ns();
         std::this_thread::sleep_for(std::chrono::microseconds(20));
+        t_ring_wait.fetch_add((uint64_t)(mono_ns() - tw), std::memory_order_relaxed);
         continue;
       }
+      const int64_t te = mono_ns();
       fn(row, done, k);
+      t_encode.fetch_add((uint64_t)(mono_ns() - te), std::memory_order_relaxed);
       sink->commit(pi, k);
       done += k;
     }
@@ -680,6 +689,7 @@ class Consumer {
       }
       // send to every leader, then read every response: brokers work in parallel
       std::vector<int32_t> sent;
+      int64_t ti = mono_ns();
       for (auto& kv : by_leader) {
         Conn* c = leader_conn(kv.first);
         if (!c) { meta_stale = true; continue; }
@@ -690,14 +700,20 @@ class Consumer {
       bool any = false;
       for (int32_t node : sent) {
         Conn& c = brokers[node];
-        if (!recv_response(c, resp)) {               // broker died or stalled: reconnect via metadata
+        const bool ok = recv_response(c, resp);
+        t_io.fetch_add((uint64_t)(mono_ns() - ti), std::memory_order_relaxed);
+        if (!ok) {                                   // broker died or stalled: reconnect via metadata
           close_conn(c);
           meta_stale = true;
+          ti = mono_ns();
           continue;
         }
         n_fetches.fetch_add(1, std::memory_order_relaxed);
         n_bytes.fetch_add(resp.size(), std::memory_order_relaxed);
+        const int64_t th = mono_ns();
         any = handle_fetch(resp) || any;
+        ti = mono_ns();
+        t_handle.fetch_add((uint64_t)(ti - th), std::memory_order_relaxed);
       }
       if (!any) std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
@@ -809,6 +825,10 @@ void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out) {
   out->bytes = c->n_bytes.load();
   out->errors = c->n_errors.load();
   out->fetches = c->n_fetches.load();
+  out->io_ns = c->t_io.load();
+  out->handle_ns = c->t_handle.load();
+  out->encode_ns = c->t_encode.load();
+  out->ring_wait_ns = c->t_ring_wait.load();
   out->metadata_refreshes = c->n_meta.load();
   out->offset_resets = c->n_resets.load();
   out->leaders = c->n_leaders.load();

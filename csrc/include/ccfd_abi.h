@@ -375,6 +375,11 @@ typedef struct ccfd_kc_stats {
   uint64_t metadata_refreshes;   // leader / broker changes seen (NOT_LEADER, dead connection, ...)
   uint64_t offset_resets;        // OFFSET_OUT_OF_RANGE handled by the reset policy
   uint64_t leaders;              // broker connections used by the last fetch round
+  // time attribution of the consumer thread (ns, cumulative): waiting on brokers (send +
+  // receive of Fetch), handling responses (RecordBatch / TXB1 / JSON parsing + the two
+  // below), writing rows into the ring (copy / W64 / G20 / G32 encoding), and blocked on a
+  // full ring (engine back-pressure)
+  uint64_t io_ns, handle_ns, encode_ns, ring_wait_ns;
 } ccfd_kc_stats;
 
 // offset reset policy on OFFSET_OUT_OF_RANGE (auto.offset.reset)

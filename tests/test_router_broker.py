@@ -151,3 +151,25 @@ def test_router_batches_fraud_hand_off_when_supported():
     assert res == {"incoming": 1000, "fraud": 3, "standard": 997}
     assert len(sink.calls) == 1 and [c["transaction_id"] for c in sink.calls[0]] == [7, 8, 9]
     assert r.fraud_started == 3
+
+
+def test_batching_publisher_delivers_everything_in_few_requests():
+    """KIE notifications / notifier replies leave in batches (ingest/producer.py
+    BatchingPublisher): everything published arrives, in far fewer produce calls."""
+    from ccfd_demo_summit_amd.ingest import InProcBroker
+    from ccfd_demo_summit_amd.ingest.producer import BatchingPublisher
+
+    class Counting(InProcBroker):
+        calls = 0
+
+        def produce_many(self, topic, values, partition=None):
+            Counting.calls += 1
+            return super().produce_many(topic, values, partition=partition)
+    b = Counting(default_partitions=3)
+    b.create_topic("ccd-customer-outgoing", 3)
+    pub = BatchingPublisher(b, "ccd-customer-outgoing", linger_s=0.005)
+    for i in range(5000):
+        pub.publish(b'{"n": %d}' % i)
+    pub.close()
+    got = sorted(int(r.value[6:-1]) for p in range(3) for r in b.fetch("ccd-customer-outgoing", p, 0, 10_000))
+    assert got == list(range(5000)) and Counting.calls < 100
