@@ -40,6 +40,7 @@ class KieServer:
         r = self.app.router
         r.add_post(BASE + "/containers/{c}/processes/{p}/instances", self.start)
         r.add_post(BASE + "/containers/{c}/processes/{p}/instances/batch", self.start_batch)
+        r.add_post(BASE + "/containers/{c}/processes/instances/signal/batch", self.signal_batch)
         r.add_post(BASE + "/containers/{c}/processes/instances/{i}/signal/{s}", self.signal)
         r.add_get(BASE + "/containers/{c}/processes/instances/{i}", self.get_instance)
         r.add_get(BASE + "/queries/tasks/instances/pot-owners", self.tasks)
@@ -118,6 +119,19 @@ class KieServer:
         payload = json.loads(raw) if raw else None
         ok = self.engine.signal(int(request.match_info["i"]), request.match_info["s"], payload)
         return web.Response(status=200 if ok else 404)
+
+    async def signal_batch(self, request: web.Request):
+        """Extension for the engine's hand-off: many customer-response signals in ONE request
+        (a JSON list of {"instance_id", "signal", "payload"}); answers a list of booleans
+        (False: the instance was no longer waiting -- timer fired, duplicate, unknown)."""
+        bad = self._check_container(request)
+        if bad:
+            return bad
+        items = json.loads(await request.read() or b"[]")
+        if not isinstance(items, list):
+            return web.json_response({"type": "FAILURE", "msg": "expected a JSON list"}, status=400)
+        return web.json_response([bool(self.engine.signal(int(it["instance_id"]), it.get("signal", "customerResponse"),
+                                                          it.get("payload"))) for it in items])
 
     async def get_instance(self, request: web.Request):
         inst = self.engine.get(int(request.match_info["i"]))
@@ -221,6 +235,17 @@ class KieClient:
 
     def start_standard(self, variables) -> int:
         return self._start(self.standard_pid, variables)
+
+    def signal_many(self, items) -> list:
+        """Many signals in one request (``signal/batch`` extension): items of
+        (instance_id, name, payload); returns one bool per item."""
+        if not items:
+            return []
+        body = [{"instance_id": int(i), "signal": n or self.signal_name, "payload": p} for i, n, p in items]
+        r = self.s.post(f"{self.base}/containers/{self.c}/processes/instances/signal/batch",
+                        data=json.dumps(body), headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        r.raise_for_status()
+        return [bool(x) for x in r.json()]
 
     def signal(self, instance_id: int, name: str, payload) -> bool:
         r = self.s.post(f"{self.base}/containers/{self.c}/processes/instances/{instance_id}/signal/{name or self.signal_name}",

@@ -147,9 +147,9 @@ class KieHandoff:
             t.join(2.0)
 
     # ------------------------------------------------------------------ worker side
-    def _ack(self, seq: int, n_items: int) -> None:
+    def _ack_many(self, seqs: List[int], n_items: int) -> None:
         with self._cv:
-            self._done.add(seq)
+            self._done.update(seqs)
             while self.acked_seq + 1 in self._done:
                 self._done.discard(self.acked_seq + 1)
                 self.acked_seq += 1
@@ -158,6 +158,13 @@ class KieHandoff:
             self._cv.notify_all()
 
     def _deliver(self, kind: str, payload: Any) -> None:
+        if kind == "signals":                       # consecutive signals, one request
+            res = self.sink.signal_many(payload)
+            ok = sum(1 for x in res if x)
+            with self._cv:
+                self.signals_ok += ok
+                self.signals_stale += len(res) - ok
+            return
         if kind == "start":
             many = getattr(self.sink, "start_fraud_many", None)
             if many is not None and len(payload) > 1:
@@ -182,7 +189,17 @@ class KieHandoff:
                 if self._stop and not self._q:
                     return
                 seq, kind, payload = self._q.popleft()
-            n_items = len(payload) if kind == "start" else 1
+                seqs = [seq]
+                if kind == "signal" and hasattr(self.sink, "signal_many"):
+                    # coalesce the run of signals queued behind this one (customer responses
+                    # arrive one per message; one HTTP request per signal would cap them)
+                    batch = [payload]
+                    while self._q and self._q[0][1] == "signal" and len(batch) < self.max_batch:
+                        s2, _k, p2 = self._q.popleft()
+                        seqs.append(s2)
+                        batch.append(p2)
+                    kind, payload = "signals", batch
+            n_items = len(payload) if kind in ("start", "signals") else 1
             delay = self.backoff_s
             t_fail = None
             while True:
@@ -209,7 +226,7 @@ class KieHandoff:
                     delay = min(self.max_backoff_s, delay * 2)
             if t_fail is not None:
                 self.outage_s += time.monotonic() - t_fail
-            self._ack(seq, n_items)
+            self._ack_many(seqs, n_items)
 
     def stats(self) -> Dict[str, Any]:
         with self._cv:

@@ -141,3 +141,32 @@ def test_signals_go_through_the_handoff(kie):
     assert procs.get(iid).outcome == "approved_by_customer"
     assert ho.stats()["signals_ok"] == 1 and ho.stats()["retries"] > 0
     ho.close()
+
+
+def test_signals_are_coalesced_into_batch_requests(kie):
+    """Customer responses arrive one per message; the hand-off sends the queued run of them
+    as ONE `signal/batch` request (an HTTP request per signal capped the response loop)."""
+    procs, _, px = kie
+    client = KieClient(px.url, timeout_s=2.0)
+    calls = []
+    orig = client.signal_many
+
+    def counting(items):
+        calls.append(len(items))
+        return orig(items)
+    client.signal_many = counting
+    ho = KieHandoff(client, workers=1, backoff_s=0.02)
+    iids = [procs.start_fraud({"transaction_id": 1000 + i, "customer_id": i, "amount": 5.0, "proba": 0.9})
+            for i in range(200)]
+    px.set_mode("refuse")                        # let the signals pile up behind an outage
+    for k, iid in enumerate(iids):
+        ho.submit_signal(iid, "customerResponse", k % 2 == 0)
+    ho.submit_signal(iids[0], "customerResponse", True)     # duplicate: stale, not an error
+    time.sleep(0.2)
+    px.set_mode("pass")
+    assert ho.drain(10)
+    st = ho.stats()
+    assert st["signals_ok"] == 200 and st["signals_stale"] == 1 and st["failed"] == 0
+    assert calls and all(c == 201 for c in calls), calls     # every attempt (retries too) is one batch
+    assert sum(1 for i in iids if procs.get(i).outcome == "approved_by_customer") == 100
+    ho.close()
