@@ -183,6 +183,10 @@ def main(argv=None):
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
     ap.add_argument("--ingest-threads", type=int, default=0, help="native consumers per rank (0 = partitions / ranks)")
     ap.add_argument("--notification-timeout-s", type=float, default=30.0)
+    ap.add_argument("--kie-outage-at", type=float, default=0.0,
+                    help="SIGKILL the KIE process this many seconds into the window (0 = never) ...")
+    ap.add_argument("--kie-outage-s", type=float, default=5.0,
+                    help="... and restart it from its journal this long after")
     ap.add_argument("--sample-s", type=float, default=5.0)
     ap.add_argument("--drain-timeout-s", type=float, default=120.0)
     ap.add_argument("--log-dir", default="gpurun_out/deploy_topology")
@@ -219,7 +223,11 @@ def main(argv=None):
             kb.create_topic(t, n)
         kie_env = dict(env)
         kie_env["CCFD_KIE_NOTIFICATION_TIMEOUT_S"] = str(a.notification_timeout_s)
-        procs.append(Proc("kie", [PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_port)], kie_env, log_dir))
+        journal = log_dir / "kie-journal.jsonl"
+        if journal.exists():
+            journal.unlink()
+        kie_cmd = [PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_port), "--journal", str(journal)]
+        procs.append(Proc("kie", kie_cmd, kie_env, log_dir))
         procs.append(Proc("notifier", [PY, "-m", L, "notifier", "--host", "127.0.0.1", "--port", str(notif_port)],
                           env, log_dir))
         wait_port(kie_port, 60)
@@ -283,8 +291,19 @@ def main(argv=None):
         t_w0 = time.time()
         r_w0, f_w0, _ = scrape_all()
         last_t, last_r = t_w0, r_w0
+        outage = {}
         while any(p.alive() for p in prods):
-            time.sleep(a.sample_s)
+            if a.kie_outage_at > 0 and not outage and time.time() - t_w0 >= a.kie_outage_at:
+                kie = [p for p in procs if p.name == "kie"][0]
+                kie.stop(sig=signal.SIGKILL, wait=5)           # a crashed KIE pod
+                outage = {"killed_at_s": round(time.time() - t_w0, 1)}
+            if outage and "restarted_at_s" not in outage and \
+                    time.time() - t_w0 >= a.kie_outage_at + a.kie_outage_s:
+                procs.append(Proc("kie-restarted", kie_cmd, kie_env, log_dir))   # recovers the journal
+                outage["restarted_at_s"] = round(time.time() - t_w0, 1)
+            time.sleep(min(a.sample_s, 1.0) if a.kie_outage_at > 0 else a.sample_s)
+            if time.time() - last_t < a.sample_s:
+                continue
             now = time.time()
             r_now, _, _ = scrape_all()
             samples.append({"t_s": round(now - t_w0, 1), "tx_s": round((r_now - last_r) / (now - last_t), 1),
@@ -362,6 +381,10 @@ def main(argv=None):
             time.sleep(0.5)
         out["fraud_routed_total"] = fraud_all
         out["kie"] = stats
+        if outage:
+            out["kie_outage"] = dict(outage, recovered=re.findall(r"\[kie\] recovered.*", "".join(
+                p.text() for p in procs if p.name == "kie-restarted")))
+            wait_port(kie_port, 1)
         out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
         out["kie_duplicates"] = stats["duplicates"]
         try:

@@ -156,10 +156,18 @@ def cmd_kie(a, cfg):
                           cfg.seldon.pool_size) if a.remote_prediction else None
     from ..ingest.producer import BatchingPublisher
     pub = BatchingPublisher(broker, topic)          # notifications leave in batches, off the request path
-    eng = ProcessEngine.from_config(
-        cfg.kie, publish_notification=lambda m: pub.publish(encode_notification(m)),
-        kie_metrics=KieMetrics(), prediction=PredictionService(cfg.kie.confidence_threshold, client=client),
-        journal_path=a.journal)
+    kw = dict(publish_notification=lambda m: pub.publish(encode_notification(m)), kie_metrics=KieMetrics(),
+              prediction=PredictionService(cfg.kie.confidence_threshold, client=client))
+    if a.journal and os.path.exists(a.journal):
+        # restart after a crash: in-flight instances, timers and the per-transaction dedupe
+        # index come back from the journal, so re-sent fraud starts are recognised
+        eng = ProcessEngine.recover(a.journal, notification_timeout_s=cfg.kie.notification_timeout_s,
+                                    dmn_probability_threshold=cfg.kie.dmn_probability_threshold,
+                                    dmn_amount_threshold=cfg.kie.dmn_amount_threshold, **kw)
+        print(f"[kie] recovered {len(eng.instances)} instances ({len(eng._by_tx)} fraud transactions) "
+              f"from {a.journal}", flush=True)
+    else:
+        eng = ProcessEngine.from_config(cfg.kie, journal_path=a.journal, **kw)
     srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
     web.run_app(srv.app, host=a.host, port=a.port or cfg.kie.port, print=None, access_log=None)
 

@@ -139,8 +139,16 @@ class ProcessEngine:
                 for line in f:
                     line = line.strip()
                     if line:
-                        rec = json.loads(line)
+                        try:
+                            rec = json.loads(line)
+                        except json.JSONDecodeError:
+                            continue        # the torn last line of a killed process
                         last[rec["instance"]["id"]] = rec
+        if os.path.exists(journal_path) and os.path.getsize(journal_path) > 0:
+            with open(journal_path, "rb+") as f:            # end a torn last line, so the
+                f.seek(-1, os.SEEK_END)                      # next record starts on its own
+                if f.read(1) != b"\n":
+                    f.write(b"\n")
         eng = cls(journal_path=journal_path, **kw)
         max_id, max_task = 0, 0
         for iid, rec in last.items():

@@ -144,3 +144,23 @@ def test_notifier_deterministic():
     assert o1 == o2
     assert ns1.sent == 200 and ns1.replied + ns1.no_reply == 200
     assert 100 < ns1.replied < 180
+
+
+def test_journal_recovery_survives_a_torn_last_line(tmp_path):
+    """A KIE killed mid-write (SIGKILL) leaves a partial last journal line; recovery skips it
+    and keeps the per-transaction dedupe index, so re-sent fraud starts are not doubled."""
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    j = str(tmp_path / "j.jsonl")
+    e = ProcessEngine(notification_timeout_s=60, journal_path=j)
+    ids = [e.start_fraud({"transaction_id": t, "customer_id": 1, "amount": 5.0, "proba": 0.9}) for t in range(10)]
+    e.close()
+    with open(j, "a") as f:
+        f.write('{"instance": {"id": 99, "process_id": "fr')           # torn write
+    r = ProcessEngine.recover(j, notification_timeout_s=60)
+    assert sorted(r.instances) == sorted(ids)
+    assert r.start_fraud({"transaction_id": 3, "customer_id": 1, "amount": 5.0, "proba": 0.9}) == ids[3]
+    assert r.duplicates == 1
+    r.start_fraud({"transaction_id": 50, "customer_id": 1, "amount": 5.0, "proba": 0.9})
+    r.close()
+    r2 = ProcessEngine.recover(j, notification_timeout_s=60)        # the record after the torn line survives
+    assert len(r2.instances) == 11 and 50 in r2._by_tx
