@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-3 GPU pass G: the deployed topology with TXB1 batches (the hot-path wire format),
+# MLP and GBDT (G20 binned at ingest), open loop.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r3g
+mkdir -p $O
+step() { echo "[r3g] $(date +%T) $*"; }
+step deploy topology mlp txb1 open loop 30 s
+timeout -k 30 360 python bench/deploy_topology.py --seconds 30 --producers 4 --rate 0 --fmt txb1 \
+    --log-dir $O/topo_txb1_mlp --out $O/topo_txb1_mlp.json > $O/topo_txb1_mlp.log 2>&1 || { tail -40 $O/topo_txb1_mlp.log; exit 1; }
+tail -c 1500 $O/topo_txb1_mlp.json
+step deploy topology gbdt txb1 open loop 30 s
+timeout -k 30 360 python bench/deploy_topology.py --model gbdt --seconds 30 --producers 4 --rate 0 --fmt txb1 \
+    --log-dir $O/topo_txb1_gbdt --out $O/topo_txb1_gbdt.json > $O/topo_txb1_gbdt.log 2>&1 || { tail -40 $O/topo_txb1_gbdt.log; exit 1; }
+tail -c 1500 $O/topo_txb1_gbdt.json
+step done
