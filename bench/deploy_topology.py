@@ -223,9 +223,10 @@ def main(argv=None):
             kb.create_topic(t, n)
         kie_env = dict(env)
         kie_env["CCFD_KIE_NOTIFICATION_TIMEOUT_S"] = str(a.notification_timeout_s)
-        journal = log_dir / "kie-journal.jsonl"
-        if journal.exists():
-            journal.unlink()
+        # the journal grows ~1 KB per fraud process: keep it out of the log directory
+        import tempfile
+        jdir = tempfile.mkdtemp(prefix="ccfd-kie-journal-")
+        journal = Path(jdir) / "kie-journal.jsonl"
         kie_cmd = [PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_port), "--journal", str(journal)]
         procs.append(Proc("kie", kie_cmd, kie_env, log_dir))
         procs.append(Proc("notifier", [PY, "-m", L, "notifier", "--host", "127.0.0.1", "--port", str(notif_port)],
@@ -413,6 +414,11 @@ def main(argv=None):
     finally:
         for p in reversed(procs):
             p.stop(wait=40.0 if p.name == "engine" else 10.0)   # the engine drains on SIGTERM
+        if "jdir" in locals():
+            import shutil
+            if journal.exists():
+                out["kie_journal_bytes"] = journal.stat().st_size
+            shutil.rmtree(jdir, ignore_errors=True)
     line = json.dumps(out)
     print(line, flush=True)
     if a.out:
