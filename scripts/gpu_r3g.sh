@@ -15,4 +15,12 @@ step deploy topology gbdt txb1 open loop 30 s
 timeout -k 30 360 python bench/deploy_topology.py --model gbdt --seconds 30 --producers 4 --rate 0 --fmt txb1 \
     --log-dir $O/topo_txb1_gbdt --out $O/topo_txb1_gbdt.json > $O/topo_txb1_gbdt.log 2>&1 || { tail -40 $O/topo_txb1_gbdt.log; exit 1; }
 tail -c 1500 $O/topo_txb1_gbdt.json
+step deploy topology with KIE crash + journal restart
+timeout -k 30 420 python bench/deploy_topology.py --seconds 60 --producers 3 --rate 1200000 --fmt json \
+    --kie-outage-at 20 --kie-outage-s 5 --log-dir $O/topo_kie_crash --out $O/topo_kie_crash.json > $O/topo_kie_crash.log 2>&1 \
+    || { tail -40 $O/topo_kie_crash.log; exit 1; }
+tail -c 600 $O/topo_kie_crash.json
+step bench default
+timeout -k 10 300 python bench.py --out $O/bench_default.json > $O/bench_default.log 2>&1 || { tail -30 $O/bench_default.log; exit 1; }
+du -sh gpurun_out
 step done
