@@ -243,7 +243,8 @@ def _encode_cost(args, dm, rows: int):
     ns = best(fn, a)
     ns_ref = best(ref, a, reps=1)
     ne = np.diff(offs)
-    return {"row_format": args.wire, "host_encode_ns_per_row": round(ns, 2),
+    isa = {2: "avx512", 1: "avx2", 0: "scalar"}.get(int(L.ccfd_encode_isa(int(args.wire == "g20"))), "?")
+    return {"row_format": args.wire, "host_encode_ns_per_row": round(ns, 2), "host_encode_isa": isa,
             "host_encode_ns_per_row_scalar_ref": round(ns_ref, 2),
             "max_thresholds_per_feature": int(ne.max()), "mean_thresholds_per_feature": round(float(ne.mean()), 2)}
 

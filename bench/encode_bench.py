@@ -59,6 +59,16 @@ def measure(rows: int = 1_000_000, threads: int = 8, trained: bool = False, seed
     ref_out = out.copy()
     ns_simd = ns_per_row(simd, args, rows)
     assert (out == ref_out).all(), "SIMD encoder disagrees with the scalar oracle"
+    isa = {2: "avx512", 1: "avx2", 0: "scalar"}.get(int(L.ccfd_encode_isa(int(bits == 5))), "?")
+    ns_avx2 = None
+    if isa == "avx512":                       # the AVX2 path on the same host, for the record
+        os.environ["CCFD_ENCODE_NO_AVX512"] = "1"
+        try:
+            out[:] = 0
+            ns_avx2 = round(ns_per_row(simd, args, rows), 2)
+            assert (out == ref_out).all(), "AVX2 encoder disagrees with the scalar oracle"
+        finally:
+            del os.environ["CCFD_ENCODE_NO_AVX512"]
     mt_args = args[:6] + (int(bits == 5), out.ctypes.data, am.ctypes.data, threads)
     ns_mt = ns_per_row(L.ccfd_encode_bins_mt, mt_args, rows)
     ne = np.diff(offs)
@@ -66,6 +76,7 @@ def measure(rows: int = 1_000_000, threads: int = 8, trained: bool = False, seed
             "model": f"oblivious_gbdt_100x6_{'trained' if trained else 'random'}",
             "max_thresholds_per_feature": int(ne.max()), "mean_thresholds_per_feature": round(float(ne.mean()), 2),
             "ns_per_row_scalar_ref": round(ns_ref, 2), "ns_per_row_simd": round(ns_simd, 2),
+            "isa": isa, "ns_per_row_avx2": ns_avx2,
             "speedup_1thread": round(ns_ref / ns_simd, 2),
             "threads": threads, "ns_per_row_simd_mt": round(ns_mt, 3),
             "rows_per_s_1thread": round(1e9 / ns_simd, 1), "rows_per_s_mt": round(1e9 / ns_mt, 1),

@@ -149,6 +149,8 @@ def lib() -> C.CDLL:
         L.ccfd_encode_bins_mt.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
                                           C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
         L.ccfd_encode_bins_mt.restype = C.c_int64
+        L.ccfd_encode_isa.argtypes = [C.c_int32]
+        L.ccfd_encode_isa.restype = C.c_int32
         L.ccfd_host_read_bw.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_double]
         L.ccfd_host_read_bw.restype = C.c_double
         L.ccfd_engine_set_amount.argtypes = [C.c_void_p, C.c_int, C.c_void_p]

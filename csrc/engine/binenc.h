@@ -50,6 +50,22 @@ inline uint8_t amount_bucket_host(float a) {
   return (uint8_t)b;
 }
 
+// 16 G20 rows as five 32-bit word vectors (lane = row) -> row-major 16 x 5 dwords: output
+// register m holds flat dwords 16m + i = (row (16m + i) / 5, word (16m + i) % 5)
+struct G20OutTable {
+  alignas(64) int32_t idx[5][16];
+  uint16_t mask[5][5];
+  constexpr G20OutTable() : idx(), mask() {
+    for (int m = 0; m < 5; ++m)
+      for (int i = 0; i < 16; ++i) {
+        const int f = 16 * m + i;
+        idx[m][i] = f / 5;
+        mask[m][f % 5] = (uint16_t)(mask[m][f % 5] | (1u << i));
+      }
+  }
+};
+inline constexpr G20OutTable kG20Out{};
+
 struct BinPlan {
   float* pad = nullptr;                // 64-byte aligned, per feature nv[j] * 8 floats
   int32_t base[CCFD_N_FEATURES] = {};  // float offset of feature j in `pad`
@@ -129,33 +145,70 @@ struct BinPlan {
     for (int j = 0; j < CCFD_N_FEATURES; ++j) b[j] = bin_scalar(j, x[j]);
   }
 
-  // OR 16 fields (u32 lanes, < 64) at bit `bit` into the rows' 3 x 64-bit words
-  // (w[word][half]: half 0 = rows 0..7, 1 = rows 8..15)
-  __attribute__((target("avx512f,avx512dq"))) static void put_field(__m512i (*w)[2], __m512i v16, int bit) {
-    const __m512i v[2] = {_mm512_cvtepu32_epi64(_mm512_castsi512_si256(v16)),
-                          _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(v16, 1))};
-    const int wd = bit >> 6, sh = bit & 63;
-    for (int h = 0; h < 2; ++h) {
-      w[wd][h] = _mm512_or_si512(w[wd][h], _mm512_sll_epi64(v[h], _mm_cvtsi32_si128(sh)));
-      if (sh + 6 > 64) w[wd + 1][h] = _mm512_or_si512(w[wd + 1][h], _mm512_srl_epi64(v[h], _mm_cvtsi32_si128(64 - sh)));
+  // OR 16 fields (u32 lanes, < 64) at bit `bit` of the rows' five 32-bit words (lane = row)
+  __attribute__((target("avx512f"))) static void put_field(__m512i* w, __m512i v16, int bit) {
+    const int wd = bit >> 5, sh = bit & 31;
+    w[wd] = _mm512_or_si512(w[wd], _mm512_slli_epi32(v16, (unsigned)sh));
+    if (sh + 6 > 32) w[wd + 1] = _mm512_or_si512(w[wd + 1], _mm512_srli_epi32(v16, (unsigned)(32 - sh)));
+  }
+
+  // In-register 16x16 transpose: r[i] = row i (16 floats) -> r[j] = column j of the 16 rows.
+  // 64 shuffles (32-bit unpack, 64-bit shuffle, two 128-bit lane shuffles) instead of 16
+  // gathers: a zmm gather is ~20 uops on both Zen 4/5 and Golden Cove.
+  __attribute__((target("avx512f"))) static void transpose16(__m512* r) {
+    __m512 t[16];
+    for (int i = 0; i < 16; i += 2) {
+      t[i] = _mm512_unpacklo_ps(r[i], r[i + 1]);
+      t[i + 1] = _mm512_unpackhi_ps(r[i], r[i + 1]);
+    }
+    for (int i = 0; i < 16; i += 4) {              // r[i + q], lane k: rows i..i+3 of column 4k + q
+      r[i] = _mm512_shuffle_ps(t[i], t[i + 2], _MM_SHUFFLE(1, 0, 1, 0));
+      r[i + 1] = _mm512_shuffle_ps(t[i], t[i + 2], _MM_SHUFFLE(3, 2, 3, 2));
+      r[i + 2] = _mm512_shuffle_ps(t[i + 1], t[i + 3], _MM_SHUFFLE(1, 0, 1, 0));
+      r[i + 3] = _mm512_shuffle_ps(t[i + 1], t[i + 3], _MM_SHUFFLE(3, 2, 3, 2));
+    }
+    for (int q = 0; q < 4; ++q) {
+      t[q] = _mm512_shuffle_f32x4(r[q], r[4 + q], 0x88);          // columns q, 8+q of rows 0..7
+      t[4 + q] = _mm512_shuffle_f32x4(r[q], r[4 + q], 0xdd);      // columns 4+q, 12+q
+      t[8 + q] = _mm512_shuffle_f32x4(r[8 + q], r[12 + q], 0x88); // same, rows 8..15
+      t[12 + q] = _mm512_shuffle_f32x4(r[8 + q], r[12 + q], 0xdd);
+    }
+    for (int q = 0; q < 4; ++q) {
+      r[q] = _mm512_shuffle_f32x4(t[q], t[8 + q], 0x88);
+      r[8 + q] = _mm512_shuffle_f32x4(t[q], t[8 + q], 0xdd);
+      r[4 + q] = _mm512_shuffle_f32x4(t[4 + q], t[12 + q], 0x88);
+      r[12 + q] = _mm512_shuffle_f32x4(t[4 + q], t[12 + q], 0xdd);
     }
   }
 
-  // 16 G20 rows (row stride `ld` floats) -> out[16][20]; Amount column -> amount_out[16]
+  // 16 G20 rows (row stride `ld` >= 30 floats) -> out[16][20]; Amount column -> amount_out[16].
+  // The rows are read with two overlapping 16-float loads each (features 0..15 and 14..29, no
+  // read past feature 29) and transposed in registers; the packed words go out with plain
+  // stores (a zmm scatter is microcoded on Zen 4/5).
   __attribute__((target("avx512f,avx512dq"))) void encode16_g20_avx512(const float* x, int64_t ld, uint8_t* out,
                                                                       float* amount_out) const {
-    const __m512i iota = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-    const __m512i vidx = _mm512_mullo_epi32(iota, _mm512_set1_epi32((int)ld));
-    __m512i w[3][2];
-    for (int a = 0; a < 3; ++a) w[a][0] = w[a][1] = _mm512_setzero_si512();
-    __m512 xa = _mm512_setzero_ps();
+    __m512 lo16[16], hi16[16];
+    for (int r = 0; r < 16; ++r) {
+      lo16[r] = _mm512_loadu_ps(x + r * ld);
+      hi16[r] = _mm512_loadu_ps(x + r * ld + (CCFD_N_FEATURES - 16));
+    }
+    transpose16(lo16);
+    transpose16(hi16);
+    __m512i w[5];
+    for (int a = 0; a < 5; ++a) w[a] = _mm512_setzero_si512();
+    const __m512 xa = hi16[15];
     for (int j = 0; j < CCFD_N_FEATURES; ++j) {
-      const __m512 xv = _mm512_i32gather_ps(vidx, x + j, 4);
-      if (j == CCFD_N_FEATURES - 1) xa = xv;
+      const __m512 xv = j < 16 ? lo16[j] : hi16[j - (CCFD_N_FEATURES - 16)];
       const float* e = pad + base[j];
-      const __m512 e0 = _mm512_loadu_ps(e), e1 = _mm512_loadu_ps(e + 16);
-      __m512i lo = _mm512_setzero_si512();
-      for (int st = 16; st >= 1; st >>= 1) {           // branch-free lower_bound over 32 lanes
+      // branch-free lower_bound over 32 lanes: the first two steps pick between broadcast
+      // edges (15; 7 / 23), the last three permute (vpermt2ps) the two edge registers
+      const __mmask16 m16 = _mm512_cmp_ps_mask(_mm512_set1_ps(e[15]), xv, _CMP_LT_OQ);
+      const __m512 e8 = _mm512_mask_blend_ps(m16, _mm512_set1_ps(e[7]), _mm512_set1_ps(e[23]));
+      const __mmask16 m8 = _mm512_cmp_ps_mask(e8, xv, _CMP_LT_OQ);
+      __m512i lo = _mm512_maskz_mov_epi32(m16, _mm512_set1_epi32(16));
+      lo = _mm512_mask_add_epi32(lo, m8, lo, _mm512_set1_epi32(8));
+      const __m512 e0 = _mm512_load_ps(e), e1 = _mm512_load_ps(e + 16);
+      for (int st = 4; st >= 1; st >>= 1) {
         const __m512i idx = _mm512_add_epi32(lo, _mm512_set1_epi32(st - 1));
         const __m512 ec = _mm512_permutex2var_ps(e0, idx, e1);
         const __mmask16 m = _mm512_cmp_ps_mask(ec, xv, _CMP_LT_OQ);
@@ -170,12 +223,13 @@ struct BinPlan {
     }
     put_field(w, amt, 150);
     put_field(w, _mm512_set1_epi32(stamp & 63), 154);
-    const __m512i off8 = _mm512_mullo_epi64(_mm512_setr_epi64(0, 1, 2, 3, 4, 5, 6, 7), _mm512_set1_epi64(CCFD_G20_ROW_BYTES));
-    for (int h = 0; h < 2; ++h) {
-      uint8_t* o = out + (size_t)h * 8 * CCFD_G20_ROW_BYTES;
-      _mm512_i64scatter_epi64(o, off8, w[0][h], 1);
-      _mm512_i64scatter_epi64(o + 8, off8, w[1][h], 1);
-      _mm512_i64scatter_epi32(o + 16, off8, _mm512_cvtepi64_epi32(w[2][h]), 1);
+    // five word vectors (lane = row) -> 16 rows x 5 dwords, row-major: output register m holds
+    // flat dwords 16m..16m+15 = (row, word) = divmod(16m + i, 5), gathered by masked permutes
+    for (int m = 0; m < 5; ++m) {
+      const __m512i ix = _mm512_load_si512(kG20Out.idx[m]);
+      __m512i o = _mm512_maskz_permutexvar_epi32(kG20Out.mask[m][0], ix, w[0]);
+      for (int k = 1; k < 5; ++k) o = _mm512_mask_permutexvar_epi32(o, kG20Out.mask[m][k], ix, w[k]);
+      _mm512_storeu_si512(out + 64 * m, o);
     }
     if (amount_out) _mm512_storeu_ps(amount_out, xa);
   }
@@ -184,7 +238,7 @@ struct BinPlan {
   void encode_rows(const float* x, int64_t n, int64_t ld, uint8_t* out, float* amount_out) const {
     const int rb = g20 ? CCFD_G20_ROW_BYTES : CCFD_G32_ROW_BYTES;
     int64_t i = 0;
-    if (avx512) {
+    if (avx512 && ld >= CCFD_N_FEATURES) {
       float amt[16];
       for (; i + 16 <= n; i += 16) {
         encode16_g20_avx512(x + i * ld, ld, out + i * rb, amount_out ? amount_out + i : amt);

@@ -316,6 +316,16 @@ extern "C" int64_t ccfd_encode_bins_mt(const float* x, int64_t n, int64_t ld, co
   return n;
 }
 
+// Which encoder a G20 / G32 BinPlan runs on this host: 2 = AVX-512 16-row (G20 only),
+// 1 = AVX2 compare + popcount, 0 = scalar (CCFD_ENCODE_NO_AVX512 honoured).
+extern "C" int32_t ccfd_encode_isa(int32_t g20) {
+  const float e = 0.f;
+  const int32_t offs[CCFD_N_FEATURES + 1] = {};
+  ccfd::BinPlan plan;
+  if (!plan.build(&e, offs, 1, g20 != 0)) return -1;
+  return plan.avx512 ? 2 : plan.simd ? 1 : 0;
+}
+
 // Internal entry points for the native Kafka consumer (kafka_consumer.cpp).
 namespace ccfd {
 bool parse_json_row(const char* s, const char* e, float* f, uint64_t* id, uint32_t* cust) {

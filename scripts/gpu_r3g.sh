@@ -22,5 +22,10 @@ timeout -k 30 420 python bench/deploy_topology.py --seconds 60 --producers 3 --r
 tail -c 600 $O/topo_kie_crash.json
 step bench default
 timeout -k 10 300 python bench.py --out $O/bench_default.json > $O/bench_default.log 2>&1 || { tail -30 $O/bench_default.log; exit 1; }
+step encoder microbench, AVX-512 16-row G20 path vs AVX2 on the box host
+timeout -k 10 300 python bench/encode_bench.py --rows 2000000 --threads 8 --out $O/encode_g20.json > $O/encode.log 2>&1 || { tail -30 $O/encode.log; exit 1; }
+cat $O/encode_g20.json
+step bench gbdt
+timeout -k 10 300 python bench.py --model gbdt --out $O/bench_gbdt.json > $O/bench_gbdt.log 2>&1 || { tail -30 $O/bench_gbdt.log; exit 1; }
 du -sh gpurun_out
 step done
