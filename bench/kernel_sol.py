@@ -7,7 +7,7 @@ This bench removes PCIe: rows live in HBM, one launch scores ``B`` rows, and the
 compared with the two ceilings of the kernel on MI355X:
 
 * HBM: bytes read + written per row / measured HBM read bandwidth (bench/roofline.py);
-* MFMA (MLP only): 24 ``mfma_f32_16x16x32_bf16`` per 16 rows = 24.6 KFLOP/row against the
+* MFMA (MLP only): 26 ``mfma_f32_16x16x32_bf16`` per 16 rows = 26.6 KFLOP/row against the
   dense bf16 peak (2.5 PFLOP/s, no sparsity).
 
     python bench/kernel_sol.py [--out profiles/r1/kernel_sol.json]
@@ -24,7 +24,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 HBM_GBPS_MEASURED = 7071.5          # profiles/r1/roofline.json hbm_read_GBps
 BF16_DENSE_TFLOPS = 2500.0
-MLP_FLOP_PER_ROW = 24 * 16 * 16 * 32 * 2 / 16     # padded MFMA work actually issued
+MLP_FLOP_PER_ROW = 26 * 16 * 16 * 32 * 2 / 16     # padded MFMA work actually issued (8 + 16 + 2 per 16 rows)
 
 
 class _HostRows:

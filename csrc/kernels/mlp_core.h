@@ -211,8 +211,10 @@ __device__ __forceinline__ float mlp_tile_w64(const char* sblob, const MlpWireLa
 
 // Two independent tiles per call: every weight fragment read from LDS feeds two MFMAs (half
 // the LDS traffic per row) and the two dependency chains interleave (ILP 2 per wave).
-__device__ __forceinline__ void mlp_tile_w64_x2(const char* sblob, const MlpWireLane& L, const WireRegs& r0,
-                                                const WireRegs& r1, int g, int lane, float& p0, float& p1) {
+__device__ __forceinline__ float mlp_proba_of_logit(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+
+__device__ __forceinline__ void mlp_logit_w64_x2(const char* sblob, const MlpWireLane& L, const WireRegs& r0,
+                                                 const WireRegs& r1, int g, int lane, float& z0, float& z1) {
   const bf16x8 xa = wire_operand(r0, g == 3, L);
   const bf16x8 xb = wire_operand(r1, g == 3, L);
   const bf16x8* W1f = reinterpret_cast<const bf16x8*>(sblob + kOffW1);
@@ -259,8 +261,16 @@ __device__ __forceinline__ void mlp_tile_w64_x2(const char* sblob, const MlpWire
     za = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, __builtin_bit_cast(bf16x8, ua), za, 0, 0, 0);
     zb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, __builtin_bit_cast(bf16x8, ub), zb, 0, 0, 0);
   }
-  p0 = __builtin_amdgcn_rcpf(1.f + __expf(-(za[0] + L.b3)));
-  p1 = __builtin_amdgcn_rcpf(1.f + __expf(-(zb[0] + L.b3)));
+  z0 = za[0] + L.b3;
+  z1 = zb[0] + L.b3;
+}
+
+__device__ __forceinline__ void mlp_tile_w64_x2(const char* sblob, const MlpWireLane& L, const WireRegs& r0,
+                                                const WireRegs& r1, int g, int lane, float& p0, float& p1) {
+  float z0, z1;
+  mlp_logit_w64_x2(sblob, L, r0, r1, g, lane, z0, z1);
+  p0 = mlp_proba_of_logit(z0);
+  p1 = mlp_proba_of_logit(z1);
 }
 
 // wire_body.h scorer for the MLP
@@ -275,10 +285,16 @@ struct MlpWireScorer {
     return mlp_tile_w64(lds, L, r, g, lane);
   }
   static constexpr bool kPair = true;
+  static constexpr bool kQuad = true;
   __device__ __forceinline__ void tile2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
                                         float& p0, float& p1) const {
     mlp_tile_w64_x2(lds, L, r0, r1, g, lane, p0, p1);
   }
+  __device__ __forceinline__ void logit2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
+                                         float& z0, float& z1) const {
+    mlp_logit_w64_x2(lds, L, r0, r1, g, lane, z0, z1);
+  }
+  __device__ __forceinline__ float proba(float z) const { return mlp_proba_of_logit(z); }
 };
 
 // Same math with every weight fragment held in VGPRs for the kernel's lifetime (26 bf16x8
@@ -308,8 +324,8 @@ struct MlpWireRegScorer {
 #pragma unroll
     for (int u = 0; u < 4; ++u) b2[u] = b2f[u * 4 + g];
   }
-  __device__ __forceinline__ void tile2(const char*, const WireRegs& r0, const WireRegs& r1, int g, int,
-                                        float& p0, float& p1) const {
+  __device__ __forceinline__ void logit2(const char*, const WireRegs& r0, const WireRegs& r1, int g, int,
+                                         float& z0, float& z1) const {
     const bf16x8 xa = wire_operand(r0, g == 3, L);
     const bf16x8 xb = wire_operand(r1, g == 3, L);
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
@@ -349,15 +365,24 @@ struct MlpWireRegScorer {
       za = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[s], __builtin_bit_cast(bf16x8, ua), za, 0, 0, 0);
       zb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[s], __builtin_bit_cast(bf16x8, ub), zb, 0, 0, 0);
     }
-    p0 = __builtin_amdgcn_rcpf(1.f + __expf(-(za[0] + L.b3)));
-    p1 = __builtin_amdgcn_rcpf(1.f + __expf(-(zb[0] + L.b3)));
+    z0 = za[0] + L.b3;
+    z1 = zb[0] + L.b3;
   }
+  __device__ __forceinline__ void tile2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
+                                        float& p0, float& p1) const {
+    float z0, z1;
+    logit2(lds, r0, r1, g, lane, z0, z1);
+    p0 = mlp_proba_of_logit(z0);
+    p1 = mlp_proba_of_logit(z1);
+  }
+  __device__ __forceinline__ float proba(float z) const { return mlp_proba_of_logit(z); }
   __device__ __forceinline__ float tile(const char* lds, const WireRegs& r, int g, int lane) const {
     float p0, p1;
     tile2(lds, r, r, g, lane, p0, p1);
     return p0;
   }
   static constexpr bool kPair = true;
+  static constexpr bool kQuad = true;
 };
 
 }  // namespace ccfd

@@ -140,7 +140,11 @@ struct LrWireScorer {
     for (int j = 0; j < 8; ++j) w[j] = wp[j];
     if (g == 3 && log_amount) w[5] *= 0.693147180559945f;
   }
-  __device__ __forceinline__ float tile(const char*, const WireRegs& r, int g, int) const {
+  __device__ __forceinline__ float tile(const char* lds, const WireRegs& r, int g, int lane) const {
+    return proba(logit(lds, r, g, lane));
+  }
+  __device__ __forceinline__ float proba(float z) const { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+  __device__ __forceinline__ float logit(const char*, const WireRegs& r, int g, int) const {
     const bool g3 = g == 3;
     const uint4 v = r.v;
     float am = __uint_as_float(v.w);
@@ -157,9 +161,15 @@ struct LrWireScorer {
     for (int j = 0; j < 8; ++j) z = fmaf(w[j], x[j], z);
     z += __shfl_xor(z, 16);
     z += __shfl_xor(z, 32);
-    return __builtin_amdgcn_rcpf(1.f + __expf(-(z + b)));
+    return z + b;
   }
   static constexpr bool kPair = false;
+  static constexpr bool kQuad = true;
+  __device__ __forceinline__ void logit2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
+                                         float& z0, float& z1) const {
+    z0 = logit(lds, r0, g, lane);
+    z1 = logit(lds, r1, g, lane);
+  }
   __device__ __forceinline__ void tile2(const char* lds, const WireRegs& r0, const WireRegs& r1, int g, int lane,
                                         float& p0, float& p1) const {
     p0 = tile(lds, r0, g, lane);

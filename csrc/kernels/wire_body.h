@@ -5,6 +5,9 @@
 //   void stage(const ccfd_score_args&, char* lds, int tid, int nthreads);   before the barrier
 //   void lanes(const char* lds, const ccfd_score_args&, int g);            after the barrier
 //   float tile(const char* lds, const WireRegs&, int g, int lane) const;   proba_1 of row lane&15
+// and, for the four-tile epilogue (kQuad, kPf == 4, no routing rules):
+//   float logit(const char* lds, const WireRegs&, int g, int lane) const;  logit of row lane&15
+//   float proba(float z) const;                                            sigmoid of a logit
 #pragma once
 #include "common.h"
 #include "rules.h"
@@ -86,7 +89,58 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
   };
   // steady state: the kPf strided tiles of a round all exist
   const int full_end = ntiles - (kPf - 1) * tstride;
-  while (tile < full_end) {
+  // Four-tile epilogue: every lane's proba_1 / logit is replicated over the 4 lane groups, so
+  // lane group g finishes tile g of the round -- one sigmoid, one threshold, one 64-lane store,
+  // one ballot per counter for 64 rows instead of four 16-lane passes.  The amount histogram
+  // becomes 13 wave-uniform "amount > bound" ballot popcounts (SALU) per 64 rows.
+  unsigned hgt[kNB - 1];
+#pragma unroll
+  for (int j = 0; j < kNB - 1; ++j) hgt[j] = 0;
+  constexpr bool kQuadPath = Scorer::kQuad && kPf == 4 && !kR;
+  if constexpr (kQuadPath) {
+    constexpr float kB[kNB - 1] = {1.f, 5.f, 10.f, 25.f, 50.f, 100.f, 250.f, 500.f, 1000.f, 2500.f,
+                                   5000.f, 10000.f, 25000.f};
+    while (tile < full_end) {
+      float z[4], am[4];
+      if constexpr (Scorer::kPair) {
+        sc.logit2(lds, ring[0], ring[1], g, lane, z[0], z[1]);
+        sc.logit2(lds, ring[2], ring[3], g, lane, z[2], z[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[k] = sc.logit(lds, ring[k], g, lane);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        am[k] = __shfl(__uint_as_float(ring[k].v.w), 48 + c);     // Amount of row c of tile k
+        issue(tile + (4 + k) * tstride, ring[k]);
+      }
+      const float zs = g == 0 ? z[0] : g == 1 ? z[1] : g == 2 ? z[2] : z[3];
+      const float ams = g == 0 ? am[0] : g == 1 ? am[1] : g == 2 ? am[2] : am[3];
+      const float p = sc.proba(zs);
+      const int row = (tile + g * tstride) * kTileRows + c;
+      const bool valid = row < n;
+      const bool fr = valid && p >= thr;
+      if (valid) {
+        if (store_out) {
+          if (a.proba) a.proba[row] = p;
+          if (a.route) a.route[row] = fr ? 1 : 0;
+        }
+        psum += (unsigned)(p * 1e6f + 0.5f);
+      }
+      const unsigned long long frm = __ballot(fr);
+      fraud += __popcll(frm);
+      rows += __popcll(__ballot(valid));
+      const float amv = valid ? ams : -__builtin_inff();
+#pragma unroll
+      for (int j = 0; j < kNB - 1; ++j) hgt[j] += __popcll(__ballot(amv > kB[j]));
+      if (frm) {                                                  // rare: fraud rows' buckets
+        if (fr) atomicAdd(&epi.hist[kNB + amount_bucket_fast(ams)], 1u);
+        emit_flagged(a, fr, row);
+      }
+      tile += 4 * tstride;
+    }
+  }
+  while (!kQuadPath && tile < full_end) {
     if constexpr (Scorer::kPair && kPf % 2 == 0) {
 #pragma unroll
       for (int k = 0; k < kPf; k += 2) {             // two tiles per scorer call (shared weight reads)
@@ -125,6 +179,13 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
   }
   psum = wave_sum_u64(psum);
   hist_lanes_commit(epi, hl, g, c);
+  if constexpr (kQuadPath) {
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < kNB - 1; ++j)
+        if (hgt[j]) atomicAdd(&epi.hgt[j], hgt[j]);
+    }
+  }
   if (lane == 0) {
     atomicAdd(&epi.fraud, fraud);
     atomicAdd(&epi.rows, rows);
