@@ -15,4 +15,7 @@ for pf in 2 4; do
   CCFD_MLP_PF=$pf timeout -k 10 300 python bench/kernel_sol.py --cases mlp:w64,lr:w64 --sizes 1048576,16777216 --tag pf$pf > $O/sol_pf$pf.jsonl 2>$O/sol_pf$pf.err || { tail -20 $O/sol_pf$pf.err; exit 1; }
   cat $O/sol_pf$pf.jsonl
 done
+step latency breakdown of the persistent MLP W64 path
+timeout -k 10 300 python bench/experiments/latency_breakdown.py --depths 1,2,4,8,12 --batches 4000 > $O/latency_breakdown.jsonl 2>$O/latency_breakdown.err || { tail -20 $O/latency_breakdown.err; exit 1; }
+cat $O/latency_breakdown.jsonl
 step done
