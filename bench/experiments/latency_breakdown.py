@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--depths", default="1,2,4,8,12")
     ap.add_argument("--batches", type=int, default=4000)
     ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--grid", type=int, default=0, help="persistent grid (0 = engine default)")
+    ap.add_argument("--grids", default="0", help="comma list of persistent grids (0 = engine default)")
+    ap.add_argument("--items", default="0", help="comma list of CCFD_PERSIST_ITEM_ROWS (0 = engine default)")
     ap.add_argument("--log-rows", type=int, default=1 << 21)
     ap.add_argument("--tag", default="")
     ap.add_argument("--out", default=None)
@@ -56,10 +57,16 @@ def main():
     log.write_rows(0, Xl)
     del Xl
     out = []
-    for depth in [int(d) for d in a.depths.split(",")]:
+    pts = [(int(i), int(gr), int(d)) for i in a.items.split(",") for gr in a.grids.split(",")
+           for d in a.depths.split(",")]
+    for item, grid, depth in pts:
+        if item:
+            os.environ["CCFD_PERSIST_ITEM_ROWS"] = str(item)
+        else:
+            os.environ.pop("CCFD_PERSIST_ITEM_ROWS", None)
         eng = StreamEngine(dm, batch=a.batch, depth=depth, streams=1, input_mode="zerocopy",
                            output_mode="zerocopy", device=0, exec_mode="persistent",
-                           persist_grid=a.grid)
+                           persist_grid=grid)
         eng.add_log(0, log)
         eng.pump(500, drain=True)                      # warm: kernel resident, pages touched
         eng.reset_stats()
@@ -86,7 +93,7 @@ def main():
              "p50_post_to_start_us_rel": pct(post_to_start, 50),
              "p50_end_to_landed_us_rel": pct(end_to_landed, 50),
              "p50_host_pickup_us": pct(pickup, 50),
-             "grid": a.grid or "default", "item_rows": os.environ.get("CCFD_PERSIST_ITEM_ROWS", "default")}
+             "grid": grid or "default", "item_rows": item or "default"}
         print(json.dumps(r), flush=True)
         out.append(r)
     if a.out:

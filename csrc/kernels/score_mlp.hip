@@ -164,15 +164,18 @@ void score_mlp_wire_multi_kernel(ccfd_multi_args m) {
   wire_stream_body<MlpWireScorer, kWaves, kPf, kR>(sub_args(mk, j), blockIdx.x - j * wpb, wpb);
 }
 
-// CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4; default 2 = one tile pair, measured
-// best with the paired scorer: 32.0 vs 31.0 G rows/s at 4, profiles/r1/kernel_sol_mlp_pair_sweep.jsonl).
-static int mlp_wire_prefetch() {
-  static const int v = [] {
+// CCFD_MLP_PF: W64 tiles in flight per wave (1, 2, 4).  LDS-weight kernels (coalesced
+// launches): default 2 = one tile pair (32.0 vs 31.0 G rows/s at 4,
+// profiles/r1/kernel_sol_mlp_pair_sweep.jsonl).  Register-weight kernel (single launches):
+// default 4, which takes the four-tile epilogue of wire_body.h (30.1 -> 36.9 G rows/s at 16M
+// HBM-resident rows, profiles/r3/kernel_sol/).
+static int mlp_wire_prefetch(int dflt = 2) {
+  static const int forced = [] {                   // read once: this runs per launch
     const char* e = std::getenv("CCFD_MLP_PF");
-    const int x = e ? std::atoi(e) : 2;
-    return (x == 1 || x == 2 || x == 4) ? x : 2;
+    const int x = e ? std::atoi(e) : 0;
+    return (x == 1 || x == 2 || x == 4) ? x : 0;
   }();
-  return v;
+  return forced ? forced : dflt;
 }
 
 // CCFD_MLP_REGW (default 1): W64 weights resident in VGPRs at 2 waves/SIMD
@@ -191,7 +194,7 @@ static void launch_wire(dim3 grid, hipStream_t s, const ccfd_score_args& a) {
   if (kW <= 8 && mlp_reg_weights()) {     // 2 waves/SIMD: at most 8 waves per workgroup
     const int cap = 256 * 8 / kW;          // 2 waves/SIMD residency
     if ((int)grid.x > cap) grid.x = cap;
-    switch (mlp_wire_prefetch()) {
+    switch (mlp_wire_prefetch(4)) {
       case 4: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 4, kR>), grid, dim3(64 * kW), 0, s, a); break;
       default: hipLaunchKernelGGL((score_mlp_wire_reg_kernel<kW, 2, kR>), grid, dim3(64 * kW), 0, s, a); break;
     }
