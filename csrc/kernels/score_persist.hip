@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
       persist_emit_flagged(a, sdesc, slot, m, fr && g == 0, row, lane);
     };
-    // W64 items of 4 or 8 tiles per wave (256 / 512 rows: the LR / MLP defaults): every tile
+    // W64 items of 2, 4 or 8 tiles per wave (128 / 256 / 512 rows): every tile
     // of the item in flight at once -- the item costs one PCIe round trip instead of one per
     // tile, so fewer rows in flight keep the link busy (lower p50 at the same rate) -- and
     // scored in pairs (mlp_tile_w64_x2: one LDS weight read feeds two MFMAs)
@@ -163,7 +163,9 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
         finish(pb, __uint_as_float(r[k + 1].v.w), ta + 4, xb);   // rows >= n: no-op epilogue
       }
     };
-    if (wire && kTilesPerWave == 4) {
+    if (wire && kTilesPerWave == 2) {
+      full_item(std::integral_constant<int, 2>{});
+    } else if (wire && kTilesPerWave == 4) {
       full_item(std::integral_constant<int, 4>{});
     } else if (wire && kTilesPerWave == 8) {
       full_item(std::integral_constant<int, 8>{});

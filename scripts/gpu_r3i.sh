@@ -13,4 +13,7 @@ cat $O/latency_sweep.jsonl
 step kernel_sol default PF
 timeout -k 10 300 python bench/kernel_sol.py --cases mlp:w64 --sizes 1048576,16777216 --tag quad_default > $O/sol_default.jsonl 2>$O/sol_default.err || { tail -20 $O/sol_default.err; exit 1; }
 cat $O/sol_default.jsonl
+step doorbell probe: host-memory vs fine-grained VRAM doorbell round trip
+timeout -k 10 120 ./scripts/bin/doorbell_probe > $O/doorbell_probe.jsonl 2>&1 || { cat $O/doorbell_probe.jsonl; exit 1; }
+cat $O/doorbell_probe.jsonl
 step done
