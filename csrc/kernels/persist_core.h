@@ -122,6 +122,28 @@ __device__ __forceinline__ void persist_emit_flagged(const ccfd_persist_args& a,
   if (fr_lane) sdesc.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
 }
 
+// One thread: system-scope release of this item's outputs, then a ticket on the slot; the last
+// ticket publishes ctl->done[slot] = {seq + 1, #flagged, t_start, t_end} for the host.
+__device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const ccfd_persist_desc& sdesc, int slot,
+                                               int C) {
+  // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned left =
+      __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
+  if (left == 0) {
+    const unsigned nflag = __hip_atomic_load(&a.dev->nflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.dev->nflag[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.dev->remaining[slot], (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.ctl->done[slot][1], (unsigned long long)nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.ctl->done[slot][2],
+                       __hip_atomic_load(&a.dev->tstart[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.ctl->done[slot][3], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.ctl->done[slot][0], sdesc.seq + 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // All threads, after the item's rows are scored: flush the item's counters (LDS state is
 // reset for the next item), publish its outputs and take the slot's ticket; the last
 // ticket completes the micro-batch for the host.
@@ -146,24 +168,7 @@ __device__ __forceinline__ void persist_item_done(const ccfd_persist_args& a, Ep
   // completion: publish this item's outputs, take a ticket, last ticket signals the host
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
-    // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned left =
-        __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
-    if (left == 0) {
-      const unsigned nflag = __hip_atomic_load(&a.dev->nflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.dev->nflag[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.dev->remaining[slot], (unsigned)C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.ctl->done[slot][1], (unsigned long long)nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.ctl->done[slot][2],
-                         __hip_atomic_load(&a.dev->tstart[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.ctl->done[slot][3], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.ctl->done[slot][0], sdesc.seq + 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (tid == 0) persist_ticket(a, sdesc, slot, C);
 }
 
 }  // namespace ccfd

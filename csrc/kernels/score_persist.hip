@@ -226,6 +226,137 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   }
 }
 
+// Wave-level work items (CCFD_ARG_WAVE_ITEMS; MLP on W64 rows).  Every wave of a resident
+// workgroup is an independent worker: it claims an item of T tiles (16 T rows), waits for its
+// micro-batch, issues all T tile loads at once, scores them in pairs, flushes the item's
+// counters with one lane-parallel atomic set and takes the slot's ticket -- no workgroup
+// barrier anywhere in the loop.  A CU reading host memory sustains only ~2 GB/s (bounded
+// outstanding requests over a ~2 us PCIe round trip), so a 4096-row micro-batch spread over
+// 32 waves on up to 32 CUs finishes far sooner than as 8 workgroup items of 512 rows on 8 CUs
+// (profiles/r3/latency/), and four waves per CU keep four items in flight where the workgroup
+// loop kept one.  Counters: the amount histogram is 13 wave-uniform "amount > bound" ballot
+// popcounts per tile (all rows, and for the rare fraud-routed rows), turned into per-bucket
+// counts by lanes 0..13 at the end of the item.
+template <bool kR, int T>
+__global__ __launch_bounds__(256) void persist_wave_kernel(ccfd_persist_args a) {
+  static_assert(T % 2 == 0, "tiles are scored in pairs");
+  __shared__ __attribute__((aligned(16))) char sblob[kMlpBlobWire];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int C = a.items_per_batch;
+  mlp_stage(a.blob, sblob, tid, 256, kMlpBlobWire);
+  __syncthreads();                                       // the only barrier: weights staged
+  if (blockIdx.x == 0) {                                 // the DOORBELL (persist_core.h)
+    if (wave == 0) persist_doorbell(a, lane);
+    return;
+  }
+  const MlpWireLane LW = mlp_wire_lane(sblob);
+  constexpr float kB[kNB - 1] = {1.f, 5.f, 10.f, 25.f, 50.f, 100.f, 250.f, 500.f, 1000.f, 2500.f,
+                                 5000.f, 10000.f, 25000.f};
+  unsigned long long posted_cache = 0;                   // lane 0 only
+  for (;;) {
+    unsigned long long item = 0;
+    int stop = 0;
+    if (lane == 0) {
+      item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long b = item / (unsigned long long)C;
+      unsigned sleep_n = 1;
+      while (posted_cache <= b) {
+        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (posted_cache > b) break;
+        if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = 1; break; }
+        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
+        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
+      }
+    }
+    if (__shfl(stop, 0)) break;
+    item = __shfl(item, 0);
+    ccfd_persist_desc d;
+    persist_read_desc(a, item / (unsigned long long)C, d);
+    const int chunk = (int)(item % (unsigned long long)C);
+    const int slot = (int)(d.seq % (unsigned long long)a.ring);
+    const int n = d.n;
+    const int tile0 = chunk * T;
+    if (chunk == 0 && lane == 0)                         // K7: micro-batch start
+      __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned char* xw = reinterpret_cast<const unsigned char*>(d.x);
+    WireRegs r[T];
+#pragma unroll
+    for (int k = 0; k < T; ++k) wire_issue(xw, n, tile0 + k, c, g, r[k]);
+    unsigned nf = 0, nv = 0;
+    unsigned long long ps = 0;
+    unsigned gt[kNB - 1], fgt[kNB - 1];
+#pragma unroll
+    for (int j = 0; j < kNB - 1; ++j) gt[j] = fgt[j] = 0;
+    auto finish = [&](float p, const WireRegs& rr, int tile) __attribute__((always_inline)) {
+      const int row = tile * kTileRows + c;
+      const bool valid = row < n;
+      bool fr;
+      if constexpr (kR) {
+        float xr[8];
+        wire_features(rr, g, xr);
+        fr = valid && rule_route(a.rules, __shfl(p, c), [&](int j) { return lane_feature<true>(xr, j, c); });
+      } else {
+        fr = valid && p >= a.threshold;
+      }
+      const bool v0 = valid && g == 0;
+      if (v0) {
+        if (d.proba) d.proba[row] = p;
+        if (d.route) d.route[row] = fr ? 1 : 0;
+        ps += (unsigned long long)(p * 1e6f + 0.5f);
+      }
+      const bool f0 = fr && g == 0;
+      const unsigned long long m = __ballot(f0);
+      nf += __popcll(m);
+      nv += __popcll(__ballot(v0));
+      const float am = __shfl(__uint_as_float(rr.v.w), 48 + c);     // Amount of row c (lane group 3)
+#pragma unroll
+      for (int j = 0; j < kNB - 1; ++j) gt[j] += __popcll(__ballot(v0 && am > kB[j]));
+      if (m) {                                                      // rare: fraud-routed rows
+#pragma unroll
+        for (int j = 0; j < kNB - 1; ++j) fgt[j] += __popcll(__ballot(f0 && am > kB[j]));
+        persist_emit_flagged(a, d, slot, m, f0, row, lane);
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < T; k += 2) {
+      if ((tile0 + k) * kTileRows >= n) break;                      // wave-uniform
+      float pa, pb;
+      mlp_tile_w64_x2(sblob, LW, r[k], r[k + 1], g, lane, pa, pb);
+      finish(pa, r[k], tile0 + k);
+      finish(pb, r[k + 1], tile0 + k + 1);                          // rows >= n: no-op epilogue
+    }
+    ps = wave_sum_u64(ps);
+    unsigned long long* cnt = a.counters[d.epoch & 1];
+    if (cnt && nv) {
+      // lane t < 14: bucket t = (# above bound t-1) - (# above bound t); lanes 14..17: totals
+      unsigned v_all = 0, v_fr = 0, lo_all = nv, lo_fr = nf;
+#pragma unroll
+      for (int j = 0; j < kNB; ++j) {
+        const unsigned hi_all = j < kNB - 1 ? gt[j] : 0u, hi_fr = j < kNB - 1 ? fgt[j] : 0u;
+        if (lane == j) { v_all = lo_all - hi_all; v_fr = lo_fr - hi_fr; }
+        lo_all = hi_all;
+        lo_fr = hi_fr;
+      }
+      if (lane < kNB) {
+        if (v_all - v_fr) atomicAdd(&cnt[CCFD_CNT_HIST_STD + lane], (unsigned long long)(v_all - v_fr));
+        if (v_fr) atomicAdd(&cnt[CCFD_CNT_HIST_FRAUD + lane], (unsigned long long)v_fr);
+      } else if (lane == kNB) {
+        atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)nv);
+      } else if (lane == kNB + 1) {
+        if (nf) atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)nf);
+      } else if (lane == kNB + 2) {
+        if (nv - nf) atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(nv - nf));
+      } else if (lane == kNB + 3) {
+        atomicAdd(&cnt[CCFD_CNT_PROBA_E6], ps);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // outputs + counters issued
+    if (lane == 0) persist_ticket(a, d, slot, C);
+  }
+}
+
 }  // namespace
 
 }  // namespace ccfd
@@ -236,7 +367,21 @@ extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* s
   if (a->ring <= 0 || a->ring > CCFD_PERSIST_MAX_RING || a->items_per_batch <= 0 || a->tiles_per_wave <= 0) return -2;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // routing rules: separate instantiations, so threshold-only kernels keep their registers
-  if (a->model == CCFD_MODEL_MLP) {
+  if (a->model == CCFD_MODEL_MLP && (a->flags & CCFD_ARG_WAVE_ITEMS)) {
+    if (!(a->flags & CCFD_ARG_WIRE_W64)) return -2;
+    const bool r = a->rules != nullptr;
+    switch (a->tiles_per_wave) {
+      case 2: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 2>), dim3(grid), dim3(256), 0, s, *a);
+              else hipLaunchKernelGGL((persist_wave_kernel<false, 2>), dim3(grid), dim3(256), 0, s, *a); break;
+      case 4: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 4>), dim3(grid), dim3(256), 0, s, *a);
+              else hipLaunchKernelGGL((persist_wave_kernel<false, 4>), dim3(grid), dim3(256), 0, s, *a); break;
+      case 8: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 8>), dim3(grid), dim3(256), 0, s, *a);
+              else hipLaunchKernelGGL((persist_wave_kernel<false, 8>), dim3(grid), dim3(256), 0, s, *a); break;
+      case 16: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 16>), dim3(grid), dim3(256), 0, s, *a);
+               else hipLaunchKernelGGL((persist_wave_kernel<false, 16>), dim3(grid), dim3(256), 0, s, *a); break;
+      default: return -2;
+    }
+  } else if (a->model == CCFD_MODEL_MLP) {
     if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, true>), dim3(grid), dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, false>), dim3(grid), dim3(256), 0, s, *a);
   } else if (a->model == CCFD_MODEL_LR) {

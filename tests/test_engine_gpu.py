@@ -274,6 +274,45 @@ def test_persistent_wire_item_sizes_exact(gpu, setup, monkeypatch, kind, item_ro
     log.free()
 
 
+@pytest.mark.parametrize("tiles", [2, 4, 8, 16])
+def test_persistent_wave_items_exact(gpu, setup, monkeypatch, tiles):
+    """Wave-level work items (CCFD_PERSIST_WAVE_ITEMS, MLP on W64 rows): every row scored once
+    for full and partial micro-batches, routes equal the wire oracle, and the counters --
+    incoming / fraud / standard, the proba sum and BOTH amount histograms -- equal the ones
+    recomputed on the host from the device routes."""
+    from ccfd_demo_summit_amd.contracts.metric_names import AMOUNT_BUCKETS
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    X, m = setup
+    monkeypatch.setenv("CCFD_PERSIST_WAVE_ITEMS", "1")
+    monkeypatch.setenv("CCFD_PERSIST_WAVE_TILES", str(tiles))
+    eng = StreamEngine(DeviceModel(m, gpu, wire=True), batch=4096, depth=6, streams=1, exec_mode="persistent")
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000, wire=True)
+    eng.add_log(0, log)
+    a = eng.pump(5)
+    b = eng.pump(3, batch_rows=1000)                  # partial items and a partial last tile
+    n = 5 * 4096 + 3000
+    assert a.rows + b.rows == n
+    ref = m.wire_proba(X[:n])
+    flagged = eng.drain_flagged()
+    got = np.zeros(n, bool)
+    got[(flagged["tx_id"] - 1000).astype(np.int64)] = True
+    assert len(flagged) == got.sum()                  # no row flagged twice
+    clear = np.abs(ref - 0.5) > 2e-3
+    np.testing.assert_array_equal(got[clear], (ref >= 0.5)[clear])
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    c = c.cpu().numpy()
+    assert c[0] == n and c[1] == got.sum() and c[2] == n - got.sum()
+    assert abs(int(c[3]) - float(np.round(ref.astype(np.float64) * 1e6).sum())) < 2e-4 * n * 1e6 / 100
+    bk = np.searchsorted(np.asarray(AMOUNT_BUCKETS, np.float32), X[:n, 29], side="left")
+    np.testing.assert_array_equal(c[8:22], np.bincount(bk[~got], minlength=14))
+    np.testing.assert_array_equal(c[24:38], np.bincount(bk[got], minlength=14))
+    eng.close()
+    log.free()
+
+
 @pytest.mark.parametrize("wire", [False, True])
 def test_score_sync_small_batches_zero_copy_stage(gpu, setup, monkeypatch, wire):
     """score() of small pageable batches goes through the pinned zero-copy stage
