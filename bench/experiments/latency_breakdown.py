@@ -38,8 +38,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--grids", default="0", help="comma list of persistent grids (0 = engine default)")
     ap.add_argument("--items", default="0", help="comma list of CCFD_PERSIST_ITEM_ROWS (0 = engine default)")
-    ap.add_argument("--wave-tiles", default="0", help="comma list of CCFD_PERSIST_WAVE_TILES; 0 = workgroup "
-                                                     "items (CCFD_PERSIST_WAVE_ITEMS off)")
+    ap.add_argument("--pipe", default="0", help="comma list of CCFD_PERSIST_PIPE values (1 = pipelined "
+                                               "static items, 0 = claimed workgroup items)")
     ap.add_argument("--log-rows", type=int, default=1 << 21)
     ap.add_argument("--tag", default="")
     ap.add_argument("--out", default=None)
@@ -59,14 +59,10 @@ def main():
     log.write_rows(0, Xl)
     del Xl
     out = []
-    pts = [(int(w), int(i), int(gr), int(d)) for w in a.wave_tiles.split(",") for i in a.items.split(",")
+    pts = [(int(w), int(i), int(gr), int(d)) for w in a.pipe.split(",") for i in a.items.split(",")
            for gr in a.grids.split(",") for d in a.depths.split(",")]
-    for wave, item, grid, depth in pts:
-        if wave:
-            os.environ["CCFD_PERSIST_WAVE_ITEMS"] = "1"
-            os.environ["CCFD_PERSIST_WAVE_TILES"] = str(wave)
-        else:
-            os.environ.pop("CCFD_PERSIST_WAVE_ITEMS", None)
+    for pipe, item, grid, depth in pts:
+        os.environ["CCFD_PERSIST_PIPE"] = str(pipe)
         if item:
             os.environ["CCFD_PERSIST_ITEM_ROWS"] = str(item)
         else:
@@ -100,8 +96,8 @@ def main():
              "p50_post_to_start_us_rel": pct(post_to_start, 50),
              "p50_end_to_landed_us_rel": pct(end_to_landed, 50),
              "p50_host_pickup_us": pct(pickup, 50),
-             "grid": grid or "default", "item_rows": (16 * wave) if wave else (item or "default"),
-             "items": "wave" if wave else "workgroup"}
+             "grid": grid or "default", "item_rows": item or "default",
+             "items": "pipelined-static" if pipe else "claimed"}
         print(json.dumps(r), flush=True)
         out.append(r)
     if a.out:

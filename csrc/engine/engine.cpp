@@ -342,7 +342,7 @@ class Engine {
   bool prunning = false;
   int persist_C = 0;
   int persist_tpw = 1;
-  bool persist_wave = false;
+  bool persist_pipe = false;
   int64_t completed_upto = 0;              // batches completed in order (seq count)
   std::vector<int64_t> flip_seq;           // seq at each epoch flip
 
@@ -396,21 +396,17 @@ class Engine {
       if (v == 256 || v == 512 || v == 1024 || (!g32 && (v == 64 || v == 128))) item_rows = v;
     }
     persist_tpw = g32 ? item_rows / 256 : item_rows / 64;
-    // CCFD_PERSIST_WAVE_ITEMS=1 (MLP on W64 rows): every wave claims its own item of
-    // CCFD_PERSIST_WAVE_TILES (2/4/8/16, default 8) 16-row tiles (score_persist.hip
-    // persist_wave_kernel) -- a micro-batch spreads over more CUs, no workgroup barriers
-    persist_wave = false;
+    // CCFD_PERSIST_PIPE=1 (MLP on W64 rows): statically assigned 64- or 128-row items
+    // (CCFD_PERSIST_ITEM_ROWS, default 64) with the next item's rows fetched while the
+    // current one is scored (score_persist.hip persist_pipe_kernel)
+    persist_pipe = false;
     if (w64 && cfg.model == CCFD_MODEL_MLP) {
-      if (const char* e = std::getenv("CCFD_PERSIST_WAVE_ITEMS")) persist_wave = std::atoi(e) != 0;
+      if (const char* e = std::getenv("CCFD_PERSIST_PIPE")) persist_pipe = std::atoi(e) != 0;
     }
-    if (persist_wave) {
-      int t = 8;
-      if (const char* e = std::getenv("CCFD_PERSIST_WAVE_TILES")) {
-        const int v = std::atoi(e);
-        if (v == 2 || v == 4 || v == 8 || v == 16) t = v;
-      }
-      persist_tpw = t;
-      item_rows = 16 * t;
+    if (persist_pipe) {
+      item_rows = 64;
+      if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) if (std::atoi(e) == 128) item_rows = 128;
+      persist_tpw = item_rows / 64;
     }
     const int C = (cfg.max_batch + item_rows - 1) / item_rows;
     ccfd_persist_dev init{};
@@ -455,7 +451,7 @@ class Engine {
     a.items_per_batch = persist_C;
     a.tiles_per_wave = persist_tpw;
     a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | wire_flag |
-              (persist_wave ? CCFD_ARG_WAVE_ITEMS : 0);
+              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0);
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;

@@ -52,8 +52,8 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_ABLATE_OUTPUTS 32    // no proba/route stores
 #define CCFD_ARG_ABLATE_FENCE 64      // no per-workgroup system release
 #define CCFD_ARG_CHUNK_RING 128       // persistent G32: one-chunk prefetch ring (default) instead of the whole item in flight
-#define CCFD_ARG_WAVE_ITEMS 256       // persistent W64 MLP/LR: every WAVE claims its own work item of
-                                      // tiles_per_wave x 16 rows (no workgroup barrier per item)
+#define CCFD_ARG_PIPE_ITEMS 256       // persistent W64 MLP: statically assigned 64/128-row items, the next
+                                      // item's rows fetched while the current one is scored
 
 // Routing rule program (router/rules.py RuleSet.device_program): the configurable routing
 // rules (reference "Drools rules", README.md:427) evaluated per row in the scoring

@@ -226,69 +226,96 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
   }
 }
 
-// Wave-level work items (CCFD_ARG_WAVE_ITEMS; MLP on W64 rows).  Every wave of a resident
-// workgroup is an independent worker: it claims an item of T tiles (16 T rows), waits for its
-// micro-batch, issues all T tile loads at once, scores them in pairs, flushes the item's
-// counters with one lane-parallel atomic set and takes the slot's ticket -- no workgroup
-// barrier anywhere in the loop.  A CU reading host memory sustains only ~2 GB/s (bounded
-// outstanding requests over a ~2 us PCIe round trip), so a 4096-row micro-batch spread over
-// 32 waves on up to 32 CUs finishes far sooner than as 8 workgroup items of 512 rows on 8 CUs
-// (profiles/r3/latency/), and four waves per CU keep four items in flight where the workgroup
-// loop kept one.  Counters: the amount histogram is 13 wave-uniform "amount > bound" ballot
-// popcounts per tile (all rows, and for the rare fraud-routed rows), turned into per-bucket
-// counts by lanes 0..13 at the end of the item.
+// Pipelined static work items (CCFD_ARG_PIPE_ITEMS; MLP on W64 rows).  A CU reading host
+// memory sustains only ~2 GB/s (a few KB of requests outstanding over a ~2 us PCIe round
+// trip), so a micro-batch finishes soonest when its 256 KB is spread over many CUs: small
+// items (64 / 128 rows, one per workgroup).  The claim-score-release chain of one item is
+// ~9 us of latency, though (atomic claim, descriptor read, PCIe round trip, output release,
+// ticket), which with one item per workgroup at a time capped small items far below the link
+// (profiles/r3/latency/latency_sweep_workgroup_items.jsonl).  Here:
+//   * items are assigned statically -- worker w (workgroup 1 + w of W) takes items
+//     base + w, base + w + W, ... -- so there is no claim atomic and a worker knows its next
+//     item without asking;
+//   * while item i is scored, the descriptor of item i + W is read and its rows are already
+//     in flight (when its micro-batch is posted), so one item's release / ticket overlaps the
+//     next item's PCIe round trip;
+//   * a worker waiting for a batch several batches ahead of the posted count sleeps longer,
+//     so idle workers do not hammer the device `posted` word.
+// T = tiles per wave per item (1: 64-row items, 2: 128-row items).
+__device__ __forceinline__ int persist_try_item(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
+                                                unsigned long long item, ccfd_persist_desc& sdesc) {
+  const unsigned long long b = item / (unsigned long long)C;
+  if (posted_cache <= b)
+    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (posted_cache <= b) return 0;
+  persist_read_desc(a, b, sdesc);
+  return 1;
+}
+
+__device__ __forceinline__ int persist_wait_far(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
+                                                unsigned long long item, ccfd_persist_desc& sdesc) {
+  const unsigned long long b = item / (unsigned long long)C;
+  unsigned sleep_n = 1;
+  while (posted_cache <= b) {
+    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (posted_cache > b) break;
+    if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 1;
+    if (b - posted_cache >= 2) {                 // >= 2 batches ahead: ~1 us naps
+      for (int k = 0; k < 4; ++k) __builtin_amdgcn_s_sleep(8);
+    } else {
+      for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
+      sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
+    }
+  }
+  persist_read_desc(a, b, sdesc);
+  return 0;
+}
+
 template <bool kR, int T>
-__global__ __launch_bounds__(256) void persist_wave_kernel(ccfd_persist_args a) {
-  static_assert(T % 2 == 0, "tiles are scored in pairs");
+__global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) {
+  static_assert(T == 1 || T == 2, "64- or 128-row items");
   __shared__ __attribute__((aligned(16))) char sblob[kMlpBlobWire];
+  __shared__ EpilogueLds epi;
+  __shared__ ccfd_persist_desc sdesc[2];
+  // two flags: s_pre (next item prefetched) and s_cmd (stop) are each rewritten by thread 0
+  // only after a barrier that every thread passes after reading the previous value
+  __shared__ int s_pre, s_cmd;
+
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int C = a.items_per_batch;
   mlp_stage(a.blob, sblob, tid, 256, kMlpBlobWire);
-  __syncthreads();                                       // the only barrier: weights staged
+  epi_init(epi);
+  __syncthreads();
   if (blockIdx.x == 0) {                                 // the DOORBELL (persist_core.h)
     if (wave == 0) persist_doorbell(a, lane);
     return;
   }
   const MlpWireLane LW = mlp_wire_lane(sblob);
-  constexpr float kB[kNB - 1] = {1.f, 5.f, 10.f, 25.f, 50.f, 100.f, 250.f, 500.f, 1000.f, 2500.f,
-                                 5000.f, 10000.f, 25000.f};
-  unsigned long long posted_cache = 0;                   // lane 0 only
-  for (;;) {
-    unsigned long long item = 0;
-    int stop = 0;
-    if (lane == 0) {
-      item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long b = item / (unsigned long long)C;
-      unsigned sleep_n = 1;
-      while (posted_cache <= b) {
-        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (posted_cache > b) break;
-        if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = 1; break; }
-        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
-        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
-      }
-    }
-    if (__shfl(stop, 0)) break;
-    item = __shfl(item, 0);
-    ccfd_persist_desc d;
-    persist_read_desc(a, item / (unsigned long long)C, d);
-    const int chunk = (int)(item % (unsigned long long)C);
+  const unsigned long long W = gridDim.x - 1;
+  unsigned long long item = __hip_atomic_load(&a.dev->work_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                            (unsigned long long)(blockIdx.x - 1);
+  unsigned long long posted_cache = 0;                   // thread 0 only
+
+  auto stamp = [&](const ccfd_persist_desc& d, unsigned long long it) __attribute__((always_inline)) {
+    if (it % (unsigned long long)C == 0)                // K7: micro-batch start
+      __hip_atomic_store(&a.dev->tstart[d.seq % (unsigned long long)a.ring], wall_clock64(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto issue = [&](const ccfd_persist_desc& d, unsigned long long it, WireRegs (&r)[T]) __attribute__((always_inline)) {
+    const int tile0 = (int)(it % (unsigned long long)C) * (4 * T) + wave;   // wave w: tiles tile0 + 4k
+    const unsigned char* xw = reinterpret_cast<const unsigned char*>(d.x);
+#pragma unroll
+    for (int k = 0; k < T; ++k) wire_issue(xw, d.n, tile0 + 4 * k, c, g, r[k]);
+  };
+  // score item `it` (rows in r), counters into LDS, outputs to the host, then release + ticket
+  auto score = [&](const ccfd_persist_desc& d, unsigned long long it, const WireRegs (&r)[T]) __attribute__((always_inline)) {
     const int slot = (int)(d.seq % (unsigned long long)a.ring);
     const int n = d.n;
-    const int tile0 = chunk * T;
-    if (chunk == 0 && lane == 0)                         // K7: micro-batch start
-      __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned char* xw = reinterpret_cast<const unsigned char*>(d.x);
-    WireRegs r[T];
-#pragma unroll
-    for (int k = 0; k < T; ++k) wire_issue(xw, n, tile0 + k, c, g, r[k]);
-    unsigned nf = 0, nv = 0;
-    unsigned long long ps = 0;
-    unsigned gt[kNB - 1], fgt[kNB - 1];
-#pragma unroll
-    for (int j = 0; j < kNB - 1; ++j) gt[j] = fgt[j] = 0;
+    const int tile0 = (int)(it % (unsigned long long)C) * (4 * T) + wave;
+    unsigned nf_w = 0, nv_w = 0;
+    unsigned long long ps_w = 0;
     auto finish = [&](float p, const WireRegs& rr, int tile) __attribute__((always_inline)) {
       const int row = tile * kTileRows + c;
       const bool valid = row < n;
@@ -298,62 +325,76 @@ __global__ __launch_bounds__(256) void persist_wave_kernel(ccfd_persist_args a) 
         wire_features(rr, g, xr);
         fr = valid && rule_route(a.rules, __shfl(p, c), [&](int j) { return lane_feature<true>(xr, j, c); });
       } else {
-        fr = valid && p >= a.threshold;
+        fr = valid && (p >= a.threshold);
       }
-      const bool v0 = valid && g == 0;
-      if (v0) {
+      if (valid && g == 0) {
         if (d.proba) d.proba[row] = p;
         if (d.route) d.route[row] = fr ? 1 : 0;
-        ps += (unsigned long long)(p * 1e6f + 0.5f);
+        ps_w += (unsigned long long)(p * 1e6f + 0.5f);
       }
-      const bool f0 = fr && g == 0;
-      const unsigned long long m = __ballot(f0);
-      nf += __popcll(m);
-      nv += __popcll(__ballot(v0));
-      const float am = __shfl(__uint_as_float(rr.v.w), 48 + c);     // Amount of row c (lane group 3)
-#pragma unroll
-      for (int j = 0; j < kNB - 1; ++j) gt[j] += __popcll(__ballot(v0 && am > kB[j]));
-      if (m) {                                                      // rare: fraud-routed rows
-#pragma unroll
-        for (int j = 0; j < kNB - 1; ++j) fgt[j] += __popcll(__ballot(f0 && am > kB[j]));
-        persist_emit_flagged(a, d, slot, m, f0, row, lane);
-      }
+      const unsigned long long m = __ballot(fr && g == 0);
+      nf_w += __popcll(m);
+      nv_w += __popcll(__ballot(valid && g == 0));
+      const float amount = __uint_as_float(rr.v.w);
+      if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(amount)], 1u);
+      persist_emit_flagged(a, d, slot, m, fr && g == 0, row, lane);
     };
-#pragma unroll
-    for (int k = 0; k < T; k += 2) {
-      if ((tile0 + k) * kTileRows >= n) break;                      // wave-uniform
-      float pa, pb;
-      mlp_tile_w64_x2(sblob, LW, r[k], r[k + 1], g, lane, pa, pb);
-      finish(pa, r[k], tile0 + k);
-      finish(pb, r[k + 1], tile0 + k + 1);                          // rows >= n: no-op epilogue
-    }
-    ps = wave_sum_u64(ps);
-    unsigned long long* cnt = a.counters[d.epoch & 1];
-    if (cnt && nv) {
-      // lane t < 14: bucket t = (# above bound t-1) - (# above bound t); lanes 14..17: totals
-      unsigned v_all = 0, v_fr = 0, lo_all = nv, lo_fr = nf;
-#pragma unroll
-      for (int j = 0; j < kNB; ++j) {
-        const unsigned hi_all = j < kNB - 1 ? gt[j] : 0u, hi_fr = j < kNB - 1 ? fgt[j] : 0u;
-        if (lane == j) { v_all = lo_all - hi_all; v_fr = lo_fr - hi_fr; }
-        lo_all = hi_all;
-        lo_fr = hi_fr;
-      }
-      if (lane < kNB) {
-        if (v_all - v_fr) atomicAdd(&cnt[CCFD_CNT_HIST_STD + lane], (unsigned long long)(v_all - v_fr));
-        if (v_fr) atomicAdd(&cnt[CCFD_CNT_HIST_FRAUD + lane], (unsigned long long)v_fr);
-      } else if (lane == kNB) {
-        atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)nv);
-      } else if (lane == kNB + 1) {
-        if (nf) atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)nf);
-      } else if (lane == kNB + 2) {
-        if (nv - nf) atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(nv - nf));
-      } else if (lane == kNB + 3) {
-        atomicAdd(&cnt[CCFD_CNT_PROBA_E6], ps);
+    if (tile0 * kTileRows < n) {
+      if constexpr (T == 2) {
+        float pa, pb;
+        mlp_tile_w64_x2(sblob, LW, r[0], r[1], g, lane, pa, pb);
+        finish(pa, r[0], tile0);
+        finish(pb, r[1], tile0 + 4);                     // rows >= n: no-op epilogue
+      } else {
+        finish(mlp_tile_w64(sblob, LW, r[0], g, lane), r[0], tile0);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // outputs + counters issued
-    if (lane == 0) persist_ticket(a, d, slot, C);
+    ps_w = wave_sum_u64(ps_w);
+    if (lane == 0 && nv_w) {
+      atomicAdd(&epi.fraud, nf_w);
+      atomicAdd(&epi.rows, nv_w);
+      atomicAdd(&epi.psum_e6, ps_w);
+    }
+    persist_item_done(a, epi, d, slot, C, tid);
+  };
+  // one pipeline stage: score `it` from (dc, rc) while item it + W is fetched into (dn, rn);
+  // returns true when the host stopped the kernel
+  auto stage = [&](ccfd_persist_desc& dc, const WireRegs (&rc)[T], ccfd_persist_desc& dn, WireRegs (&rn)[T],
+                   unsigned long long it) __attribute__((always_inline)) {
+    const unsigned long long nx = it + W;
+    if (tid == 0) {
+      s_pre = persist_try_item(a, C, posted_cache, nx, dn);
+      if (s_pre) stamp(dn, nx);
+    }
+    __syncthreads();
+    const bool pre = s_pre != 0;
+    if (pre) issue(dn, nx, rn);                          // next item's rows in flight now
+    score(dc, it, rc);                                   // ends with barriers (persist_item_done)
+    if (!pre) {
+      if (tid == 0) {
+        s_cmd = persist_wait_far(a, C, posted_cache, nx, dn);
+        if (!s_cmd) stamp(dn, nx);
+      }
+      __syncthreads();
+      if (s_cmd) return true;
+      issue(dn, nx, rn);
+    }
+    return false;
+  };
+
+  if (tid == 0) {
+    s_cmd = persist_wait_far(a, C, posted_cache, item, sdesc[0]);
+    if (!s_cmd) stamp(sdesc[0], item);
+  }
+  __syncthreads();
+  if (s_cmd) return;
+  WireRegs ra[T], rb[T];
+  issue(sdesc[0], item, ra);
+  for (;;) {
+    if (stage(sdesc[0], ra, sdesc[1], rb, item)) break;
+    item += W;
+    if (stage(sdesc[1], rb, sdesc[0], ra, item)) break;
+    item += W;
   }
 }
 
@@ -367,18 +408,14 @@ extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* s
   if (a->ring <= 0 || a->ring > CCFD_PERSIST_MAX_RING || a->items_per_batch <= 0 || a->tiles_per_wave <= 0) return -2;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // routing rules: separate instantiations, so threshold-only kernels keep their registers
-  if (a->model == CCFD_MODEL_MLP && (a->flags & CCFD_ARG_WAVE_ITEMS)) {
-    if (!(a->flags & CCFD_ARG_WIRE_W64)) return -2;
+  if (a->model == CCFD_MODEL_MLP && (a->flags & CCFD_ARG_PIPE_ITEMS)) {
+    if (!(a->flags & CCFD_ARG_WIRE_W64) || grid < 2) return -2;
     const bool r = a->rules != nullptr;
     switch (a->tiles_per_wave) {
-      case 2: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 2>), dim3(grid), dim3(256), 0, s, *a);
-              else hipLaunchKernelGGL((persist_wave_kernel<false, 2>), dim3(grid), dim3(256), 0, s, *a); break;
-      case 4: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 4>), dim3(grid), dim3(256), 0, s, *a);
-              else hipLaunchKernelGGL((persist_wave_kernel<false, 4>), dim3(grid), dim3(256), 0, s, *a); break;
-      case 8: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 8>), dim3(grid), dim3(256), 0, s, *a);
-              else hipLaunchKernelGGL((persist_wave_kernel<false, 8>), dim3(grid), dim3(256), 0, s, *a); break;
-      case 16: if (r) hipLaunchKernelGGL((persist_wave_kernel<true, 16>), dim3(grid), dim3(256), 0, s, *a);
-               else hipLaunchKernelGGL((persist_wave_kernel<false, 16>), dim3(grid), dim3(256), 0, s, *a); break;
+      case 1: if (r) hipLaunchKernelGGL((persist_pipe_kernel<true, 1>), dim3(grid), dim3(256), 0, s, *a);
+              else hipLaunchKernelGGL((persist_pipe_kernel<false, 1>), dim3(grid), dim3(256), 0, s, *a); break;
+      case 2: if (r) hipLaunchKernelGGL((persist_pipe_kernel<true, 2>), dim3(grid), dim3(256), 0, s, *a);
+              else hipLaunchKernelGGL((persist_pipe_kernel<false, 2>), dim3(grid), dim3(256), 0, s, *a); break;
       default: return -2;
     }
   } else if (a->model == CCFD_MODEL_MLP) {

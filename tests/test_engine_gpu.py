@@ -274,23 +274,25 @@ def test_persistent_wire_item_sizes_exact(gpu, setup, monkeypatch, kind, item_ro
     log.free()
 
 
-@pytest.mark.parametrize("tiles", [2, 4, 8, 16])
-def test_persistent_wave_items_exact(gpu, setup, monkeypatch, tiles):
-    """Wave-level work items (CCFD_PERSIST_WAVE_ITEMS, MLP on W64 rows): every row scored once
-    for full and partial micro-batches, routes equal the wire oracle, and the counters --
-    incoming / fraud / standard, the proba sum and BOTH amount histograms -- equal the ones
-    recomputed on the host from the device routes."""
+@pytest.mark.parametrize("item_rows,grid", [(64, 0), (128, 0), (64, 3), (128, 200)])
+def test_persistent_pipe_items_exact(gpu, setup, monkeypatch, item_rows, grid):
+    """Pipelined static work items (CCFD_PERSIST_PIPE, MLP on W64 rows; grid 3 = two workers
+    that each own every other item): every row scored once for full and partial micro-batches,
+    routes equal the wire oracle, and the counters -- incoming / fraud / standard, the proba
+    sum and BOTH amount histograms -- equal the ones recomputed on the host from the device
+    routes; the kernel halts and relaunches between pump calls."""
     from ccfd_demo_summit_amd.contracts.metric_names import AMOUNT_BUCKETS
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     X, m = setup
-    monkeypatch.setenv("CCFD_PERSIST_WAVE_ITEMS", "1")
-    monkeypatch.setenv("CCFD_PERSIST_WAVE_TILES", str(tiles))
-    eng = StreamEngine(DeviceModel(m, gpu, wire=True), batch=4096, depth=6, streams=1, exec_mode="persistent")
+    monkeypatch.setenv("CCFD_PERSIST_PIPE", "1")
+    monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
+    eng = StreamEngine(DeviceModel(m, gpu, wire=True), batch=4096, depth=6, streams=1, exec_mode="persistent",
+                       persist_grid=grid)
     log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64) + 1000, wire=True)
     eng.add_log(0, log)
-    a = eng.pump(5)
-    b = eng.pump(3, batch_rows=1000)                  # partial items and a partial last tile
+    a = eng.pump(5, drain=True)
+    b = eng.pump(3, batch_rows=1000, drain=True)      # partial items and a partial last tile
     n = 5 * 4096 + 3000
     assert a.rows + b.rows == n
     ref = m.wire_proba(X[:n])

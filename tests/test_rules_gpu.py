@@ -63,7 +63,7 @@ def test_kernel_routes_equal_host_rules(gpu, kind, wire, n, text):
 
 
 @pytest.mark.parametrize("exec_mode,wire", [("launch", False), ("launch", True), ("persistent", True),
-                                            ("persistent", False), ("persistent_wave", True)])
+                                            ("persistent", False), ("persistent_pipe", True)])
 def test_engine_routes_by_rules(gpu, monkeypatch, exec_mode, wire):
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel, DeviceRules
@@ -71,8 +71,8 @@ def test_engine_routes_by_rules(gpu, monkeypatch, exec_mode, wire):
     m = build_model("mlp", seed=4, X_ref=X[:20000], calibrate_rate=0.05)
     rs = RuleSet.parse(RULES3)
     dm = DeviceModel(m, gpu, wire=wire)
-    if exec_mode == "persistent_wave":            # wave-level work items (score_persist.hip)
-        monkeypatch.setenv("CCFD_PERSIST_WAVE_ITEMS", "1")
+    if exec_mode == "persistent_pipe":            # pipelined static items (score_persist.hip)
+        monkeypatch.setenv("CCFD_PERSIST_PIPE", "1")
         exec_mode = "persistent"
     eng = StreamEngine(dm, batch=4096, depth=4, streams=2, input_mode="zerocopy", exec_mode=exec_mode,
                        rules=DeviceRules(rs, gpu))
