@@ -266,7 +266,7 @@ class Engine {
     // at completion stays: it is what orders the outputs before the completion record across
     // XCDs).  CCFD_COHERENT_OUT=0 allocates non-coherent outputs instead (A/B switch).
     if (const char* e = std::getenv("CCFD_COHERENT_OUT")) coherent_out = std::atoi(e) != 0;
-    if (const char* e = std::getenv("CCFD_ABLATE")) ablate = std::atoi(e) & 0x70;   // diagnostics only
+    if (const char* e = std::getenv("CCFD_ABLATE")) ablate = std::atoi(e) & 0x270;  // diagnostics only
     // HIP_LAUNCH_BLOCKING-style debug mode: synchronise after every launch so a kernel fault
     // is reported against the micro-batch that caused it (SURVEY.md §5 race detection)
     if (const char* e = std::getenv("CCFD_DEBUG_SYNC")) debug_sync = std::atoi(e) != 0;
@@ -451,7 +451,7 @@ class Engine {
     a.items_per_batch = persist_C;
     a.tiles_per_wave = persist_tpw;
     a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | wire_flag |
-              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0);
+              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0) | (ablate & (CCFD_ARG_ABLATE_FENCE | CCFD_ARG_ABLATE_ACQUIRE));
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;

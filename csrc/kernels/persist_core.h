@@ -67,7 +67,7 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
 // slot / DMA staging buffer -- before they are read).
 __device__ __forceinline__ void persist_read_desc(const ccfd_persist_args& a, unsigned long long b,
                                                   ccfd_persist_desc& sdesc) {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (!(a.flags & CCFD_ARG_ABLATE_ACQUIRE)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
   sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -127,7 +127,7 @@ __device__ __forceinline__ void persist_emit_flagged(const ccfd_persist_args& a,
 __device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const ccfd_persist_desc& sdesc, int slot,
                                                int C) {
   // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (!(a.flags & CCFD_ARG_ABLATE_FENCE)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned left =
       __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
