@@ -224,9 +224,14 @@ class StreamEngine:
     def __init__(self, dm: DeviceModel, batch: int = 4096, depth: int = 8, streams: int = 2,
                  input_mode: str = "dma", output_mode: str = "zerocopy", threshold: float = 0.5,
                  device: Optional[int] = None, flag_capacity: int = 1 << 20, exec_mode: str = "launch",
-                 persist_grid: int = 0, coalesce: int = 1, rules=None):
+                 persist_grid: int = 0, coalesce: int = 1, rules=None, persist_items: str = "auto"):
         """exec_mode: "launch" = one fused kernel launch per micro-batch; "persistent" = one
         long-running kernel fed through a descriptor ring (MLP/LR, zero-copy outputs).
+        persist_items (persistent MLP on W64 rows): "claimed" = 512-row items claimed by 64
+        workgroups (the throughput point: 8.7e8 tx/s at 12 batches in flight); "pipelined" =
+        static 128-row items over 128 workgroups with the next item's rows fetched while the
+        current one is scored (the latency point: 19 us vs 29 us unloaded, better up to ~4
+        batches in flight; profiles/r3/latency/); "auto" = claimed unless CCFD_PERSIST_PIPE=1.
         coalesce: launch mode -- up to this many ready, log-contiguous micro-batches go out as
         one launch (MLP, zero-copy in/out); completion stays per micro-batch.
         rules: a compiled routing rule set (ops.kernels.DeviceRules) evaluated per row in the
@@ -252,6 +257,8 @@ class StreamEngine:
         cfg.exec_mode = {"launch": 0, "persistent": 1}[exec_mode]
         cfg.persist_grid = int(persist_grid)
         cfg.coalesce = max(1, min(8, int(coalesce)))
+        cfg.persist_items = {"auto": 0, "claimed": 1, "pipelined": 2}[persist_items]
+        self.persist_items = persist_items
         self.wire = bool(getattr(dm, "wire", False))
         self.row_format = dm.row_format
         self.bins = getattr(dm, "bins", None)

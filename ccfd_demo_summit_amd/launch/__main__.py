@@ -269,7 +269,7 @@ def cmd_engine(a, cfg):
         output_mode=cfg.engine.output_mode, exec_mode=cfg.engine.exec_mode,
         flush_us=cfg.engine.max_delay_us, reduce_period_ms=cfg.engine.reduce_period_ms,
         threshold=cfg.router.fraud_threshold, coalesce=cfg.engine.coalesce,
-        ingest_threads=cfg.engine.ingest_threads,
+        ingest_threads=cfg.engine.ingest_threads, persist_items=cfg.engine.persist_items,
         model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     # the process's node-local rank (torchrun LOCAL_RANK) -- not the device index, which a

@@ -54,6 +54,9 @@ class EngineServiceConfig:
                                      # auto = persistent for zero-copy in/out (MLP / LR, GBDT on
                                      # G20 / G32 rows) -- bench.py's measured mode, else launch
     max_fetch: int = 2000
+    persist_items: str = "pipelined"  # persistent MLP on W64 rows: a ring-fed service runs far below
+                                      # the link rate (batches in flight ~1), where pipelined 128-row
+                                      # items cut a batch's latency 29 -> 19 us (StreamEngine)
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
     native_ingest: bool = True       # Kafka-protocol brokers: C++ consumer thread fetches and writes
                                      # rows straight into the rings (ingest/native_consumer.py)
@@ -123,7 +126,7 @@ class EngineService:
         self.engine = StreamEngine(dm, batch=cfg.batch, depth=cfg.depth, streams=cfg.streams,
                                    input_mode=cfg.input_mode, output_mode=cfg.output_mode, threshold=threshold,
                                    device=ctx.device.index, exec_mode=self.exec_mode, coalesce=cfg.coalesce,
-                                   rules=self.device_rules)
+                                   rules=self.device_rules, persist_items=cfg.persist_items)
         n_parts = broker.partitions(cfg.topic)
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:

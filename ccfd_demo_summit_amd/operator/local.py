@@ -84,7 +84,7 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     env = {"BROKER_URL": broker, "KIE_SERVER_URL": f"http://{host}:{8090 + o}", "SELDON_URL": f"http://{host}:{8000 + o}",
            "CCFD_KAFKA_BACKEND": "kafka", "CCFD_KAFKA_PARTITIONS": str(spec.kafka.partitions),
            "CCFD_MODEL": spec.engine.model, "CCFD_EXEC_MODE": spec.engine.exec_mode,
-           "CCFD_OUTPUT_MODE": spec.engine.output_mode, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+           "CCFD_OUTPUT_MODE": spec.engine.output_mode, "CCFD_PERSIST_ITEMS": spec.engine.persist_items, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
     if spec.engine.rules:
         env["ROUTER_RULES"] = spec.engine.rules
     env.update(spec.env)

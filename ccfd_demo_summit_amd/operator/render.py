@@ -83,7 +83,7 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
            "KIE_SERVER_URL": "http://ccd-service:8090", "SELDON_URL": "http://modelfull-modelfull:8000",
            "SELDON_ENDPOINT": "api/v0.1/predictions", "FRAUD_THRESHOLD": "0.5", "CONFIDENCE_THRESHOLD": "1.0",
            "CCFD_MODEL": spec.engine.model, "CCFD_WIRE": resolve_row_format(spec.engine.model, spec.engine.row_format),
-           "CCFD_EXEC_MODE": spec.engine.exec_mode, "CCFD_OUTPUT_MODE": spec.engine.output_mode}
+           "CCFD_EXEC_MODE": spec.engine.exec_mode, "CCFD_OUTPUT_MODE": spec.engine.output_mode, "CCFD_PERSIST_ITEMS": spec.engine.persist_items}
     if spec.engine.rules:
         env["ROUTER_RULES"] = spec.engine.rules
     env.update(spec.env)

@@ -48,6 +48,7 @@ class EngineSpec:
     row_format: str = "auto"         # f32 | w64 | g32 | g20 | auto
     exec_mode: str = "auto"          # persistent | launch | auto (persistent for zero-copy in/out)
     output_mode: str = "zerocopy"    # zerocopy | dma
+    persist_items: str = "pipelined" # persistent MLP on W64 rows: pipelined (latency) | claimed (throughput)
     rules: str = ""                  # routing rule text or file (ROUTER_RULES)
 
 
@@ -121,6 +122,8 @@ class FraudDetectionSpec:
                             f"(nodes x gpusPerNode): every rank needs at least one partition")
         if self.engine.exec_mode not in ("auto", "persistent", "launch"):
             raise SpecError(f"engine.exec_mode {self.engine.exec_mode!r}: auto | persistent | launch")
+        if self.engine.persist_items not in ("pipelined", "claimed", "auto"):
+            raise SpecError(f"engine.persist_items {self.engine.persist_items!r}: pipelined | claimed | auto")
         if self.engine.output_mode not in ("zerocopy", "dma"):
             raise SpecError(f"engine.output_mode {self.engine.output_mode!r}: zerocopy | dma")
         if self.engine.exec_mode == "persistent" and self.engine.output_mode != "zerocopy":

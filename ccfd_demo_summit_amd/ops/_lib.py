@@ -43,7 +43,7 @@ class EngineConfig(C.Structure):
                 ("max_batch", C.c_int32), ("depth", C.c_int32), ("n_streams", C.c_int32),
                 ("input_mode", C.c_int32), ("output_mode", C.c_int32), ("flag_capacity", C.c_int32),
                 ("exec_mode", C.c_int32), ("persist_grid", C.c_int32), ("wire", C.c_int32),
-                ("coalesce", C.c_int32), ("_pad2", C.c_int32), ("counters", C.c_void_p * 2),
+                ("coalesce", C.c_int32), ("persist_items", C.c_int32), ("counters", C.c_void_p * 2),
                 ("rules", C.c_void_p)]
 
 

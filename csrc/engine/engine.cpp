@@ -396,16 +396,21 @@ class Engine {
       if (v == 256 || v == 512 || v == 1024 || (!g32 && (v == 64 || v == 128))) item_rows = v;
     }
     persist_tpw = g32 ? item_rows / 256 : item_rows / 64;
-    // CCFD_PERSIST_PIPE=1 (MLP on W64 rows): statically assigned 64- or 128-row items
-    // (CCFD_PERSIST_ITEM_ROWS, default 64) with the next item's rows fetched while the
-    // current one is scored (score_persist.hip persist_pipe_kernel)
+    // Pipelined static items (MLP on W64 rows, score_persist.hip persist_pipe_kernel): a
+    // micro-batch spread over 32 workgroups / CUs, the next item's rows fetched while the
+    // current one is scored -- 19 us unloaded latency vs 29 us for claimed 512-row items,
+    // better up to ~4 batches in flight, capped near 6.5e8 tx/s beyond
+    // (profiles/r3/latency/).  cfg.persist_items: 2 = pipelined, 1 = claimed, 0 = env
+    // CCFD_PERSIST_PIPE (default claimed).  CCFD_PERSIST_ITEM_ROWS = 64 / 128 (default 128).
     persist_pipe = false;
     if (w64 && cfg.model == CCFD_MODEL_MLP) {
-      if (const char* e = std::getenv("CCFD_PERSIST_PIPE")) persist_pipe = std::atoi(e) != 0;
+      if (cfg.persist_items == 2) persist_pipe = true;
+      else if (cfg.persist_items == 0)
+        if (const char* e = std::getenv("CCFD_PERSIST_PIPE")) persist_pipe = std::atoi(e) != 0;
     }
     if (persist_pipe) {
-      item_rows = 64;
-      if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) if (std::atoi(e) == 128) item_rows = 128;
+      item_rows = 128;
+      if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) if (std::atoi(e) == 64) item_rows = 64;
       persist_tpw = item_rows / 64;
     }
     const int C = (cfg.max_batch + item_rows - 1) / item_rows;
@@ -471,6 +476,7 @@ class Engine {
     // 2.35e9 at 256 (profiles/r2/g20/sweep.txt)
     const bool big_trees = (wire_flag & CCFD_ARG_WIRE_G32) && cfg.gbdt_trees * cfg.gbdt_depth > 1200;
     const int grid = cfg.persist_grid > 0 ? cfg.persist_grid
+                     : persist_pipe ? CCFD_PERSIST_GRID
                      : (wire_flag & CCFD_ARG_WIRE_W64) ? CCFD_PERSIST_GRID_W64
                      : big_trees ? 4 * CCFD_PERSIST_GRID
                      : (wire_flag & CCFD_ARG_WIRE_G20) ? CCFD_PERSIST_GRID_G20 : CCFD_PERSIST_GRID;

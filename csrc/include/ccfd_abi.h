@@ -222,7 +222,8 @@ typedef struct ccfd_engine_config {
   int32_t persist_grid;        // workgroups of the persistent kernel (0 = 256)
   int32_t wire;                // 0 = f32 rows [30]; 1 = W64 rows (64 B); 2 = G32 rows (32 B, GBDT); 3 = G20 (20 B, GBDT)
   int32_t coalesce;            // launch mode: up to this many ready micro-batches per launch (<= 8)
-  int32_t _pad2;
+  int32_t persist_items;       // persistent MLP on W64 rows: 0 = env (CCFD_PERSIST_PIPE), 1 = claimed
+                               // 512-row items (throughput), 2 = pipelined 128-row items (latency)
   unsigned long long* counters[2];  // device counter buffers, alternated per epoch
   const ccfd_rule_prog* rules;      // device rule program (owned by caller); NULL = threshold
 } ccfd_engine_config;
