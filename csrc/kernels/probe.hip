@@ -4,7 +4,11 @@
 // features) divided by the best of these, so bench numbers are quoted against them.
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <chrono>
+#include <cstdlib>
+#include <cstring>
 
 #include "../include/ccfd_abi.h"
 
@@ -21,7 +25,70 @@ __global__ __launch_bounds__(256) void read_sum_kernel(const float4* __restrict_
   if (acc == 1234.5678f) out[threadIdx.x] = acc;
 }
 
+// Workgroup b reads whole `blk`-byte blocks in a scattered order (odd multiplicative hash of
+// the block index, a permutation when the block count is a power of two): every workgroup on
+// its own page-sized stretch at a time, like the persistent kernel's small items.
+__global__ __launch_bounds__(256) void read_blocks_kernel(const char* __restrict__ src, size_t nblk, size_t blk,
+                                                          float* out) {
+  float acc = 0.f;
+  for (size_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const size_t pb = (b * 2654435761ull) & (nblk - 1);
+    const float4* p = reinterpret_cast<const float4*>(src + pb * blk);
+    for (size_t i = threadIdx.x; i < blk / 16; i += blockDim.x) {
+      const float4 v = p[i];
+      acc += v.x + v.y + v.z + v.w;
+    }
+  }
+  if (acc == 1234.5678f) out[threadIdx.x] = acc;
+}
+
 }  // namespace
+
+// Pinned host memory backed by transparent huge pages where the kernel grants them
+// (2 MB-aligned anonymous mapping, MADV_HUGEPAGE, faulted in, then hipHostRegister): fewer
+// GPU / IOMMU translations per byte for zero-copy reads.  NULL on failure.
+extern "C" void* ccfd_host_alloc_huge(size_t bytes) {
+  const size_t align = (size_t)2 << 20;
+  bytes = (bytes + align - 1) & ~(align - 1);
+  void* p = mmap(nullptr, bytes + align, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  char* a = reinterpret_cast<char*>(((uintptr_t)p + align - 1) & ~(uintptr_t)(align - 1));
+  (void)madvise(a, bytes, MADV_HUGEPAGE);
+  std::memset(a, 0, bytes);
+  if (hipHostRegister(a, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+    munmap(p, bytes + align);
+    return nullptr;
+  }
+  return a;
+}
+
+// Zero-copy read GB/s of `bytes` at `src_host` in `blk`-byte blocks (power-of-two count),
+// `grid` workgroups of 256 threads, `iters` passes (host wall clock after one warm pass).
+extern "C" double ccfd_bw_probe_blocks(const void* src_host, size_t bytes, size_t blk, int grid, int iters,
+                                       void* dev_scratch) {
+  if (!src_host || !dev_scratch || blk < 256 || (blk & 15) || grid < 1 || iters < 1) return -1.0;
+  size_t nblk = 1;
+  while (nblk * 2 * blk <= bytes) nblk *= 2;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(src_host), 0) != hipSuccess) return -2.0;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -4.0;
+  bool ok = true;
+  auto once = [&]() {
+    hipLaunchKernelGGL(read_blocks_kernel, dim3(grid), dim3(256), 0, s, static_cast<const char*>(d), nblk, blk,
+                       static_cast<float*>(dev_scratch));
+    ok = ok && hipGetLastError() == hipSuccess;
+  };
+  once();
+  ok = ok && hipStreamSynchronize(s) == hipSuccess;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < iters && ok; ++i) once();
+  ok = ok && hipStreamSynchronize(s) == hipSuccess;
+  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  (void)hipStreamDestroy(s);
+  if (!ok) return -4.0;
+  return sec > 0 ? (double)(nblk * blk) * iters / sec / 1e9 : -3.0;
+}
 
 extern "C" double ccfd_bw_probe(const void* src, size_t bytes, int mode, int iters, void* dev_scratch) {
   // mode 0: hipMemcpyAsync H2D (src pinned host) into dev_scratch (>= bytes)

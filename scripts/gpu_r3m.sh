@@ -7,6 +7,9 @@ export TMPDIR=/tmp
 O=gpurun_out/r3m
 mkdir -p $O
 step() { echo "[r3m] $(date +%T) $*"; }
+step pinned pages probe
+timeout -k 10 120 python bench/experiments/pinned_pages.py --mb 1024 > $O/pinned_pages.jsonl 2>$O/pinned_pages.err || { tail -20 $O/pinned_pages.err; exit 1; }
+cat $O/pinned_pages.jsonl
 step engine + service GPU tests
 timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_rules_gpu.py tests/test_engine_service_gpu.py -x -q --timeout 180 --timeout-method thread > $O/pytest_engine.log 2>&1 || { tail -40 $O/pytest_engine.log; exit 1; }
 tail -3 $O/pytest_engine.log
