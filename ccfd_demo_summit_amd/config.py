@@ -89,7 +89,7 @@ class EngineConfig:
     output_mode: str = "zerocopy"    # zerocopy (kernel writes pinned host) | dma
     exec_mode: str = "auto"          # persistent | launch | auto (persistent for zero-copy in/out:
                                      # the mode bench.py measures; launch_/engine_service.py)
-    persist_items: str = "pipelined" # persistent MLP on W64 rows: pipelined (latency) | claimed (throughput)
+    persist_items: str = "auto"      # persistent MLP on W64 rows: claimed (throughput, = auto) | pipelined
     handoff_capacity: int = 1 << 21  # fraud starts queued for KIE before scoring pauses (back-pressure)
     handoff_workers: int = 2         # pooled HTTP workers of the KIE hand-off (router/handoff.py)
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches

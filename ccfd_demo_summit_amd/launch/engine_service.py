@@ -54,9 +54,9 @@ class EngineServiceConfig:
                                      # auto = persistent for zero-copy in/out (MLP / LR, GBDT on
                                      # G20 / G32 rows) -- bench.py's measured mode, else launch
     max_fetch: int = 2000
-    persist_items: str = "pipelined"  # persistent MLP on W64 rows: a ring-fed service runs far below
-                                      # the link rate (batches in flight ~1), where pipelined 128-row
-                                      # items cut a batch's latency 29 -> 19 us (StreamEngine)
+    persist_items: str = "auto"      # persistent MLP on W64 rows: claimed (throughput) | pipelined
+                                     # (a lone full batch 29 -> 19 us; no e2e change in the deployed
+                                     # topology, profiles/r3/latency/) | auto = claimed
     coalesce: int = 4                # ready micro-batches per launch (launch mode, MLP)
     native_ingest: bool = True       # Kafka-protocol brokers: C++ consumer thread fetches and writes
                                      # rows straight into the rings (ingest/native_consumer.py)

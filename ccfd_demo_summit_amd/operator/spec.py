@@ -48,7 +48,7 @@ class EngineSpec:
     row_format: str = "auto"         # f32 | w64 | g32 | g20 | auto
     exec_mode: str = "auto"          # persistent | launch | auto (persistent for zero-copy in/out)
     output_mode: str = "zerocopy"    # zerocopy | dma
-    persist_items: str = "pipelined" # persistent MLP on W64 rows: pipelined (latency) | claimed (throughput)
+    persist_items: str = "auto"      # persistent MLP on W64 rows: claimed (throughput, = auto) | pipelined
     rules: str = ""                  # routing rule text or file (ROUTER_RULES)
 
 
