@@ -180,6 +180,36 @@ __device__ __forceinline__ void emit_flagged(const ccfd_score_args& a, bool fr_l
   if (fr_lane) a.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
 }
 
+// Per-wave LDS staging of fraud-routed row indices for the streaming bodies.  Appending
+// costs LDS writes only: emit_flagged's reservation is a global atomic WITH return, and the
+// wait for its result (s_waitcnt vmcnt(0)) drains every row load the wave has in flight --
+// at a 1 % fraud rate half the four-tile rounds of the W64 kernels paid that.  The wave
+// reserves space in the batch's flag list once per >= 64 flagged rows and once at the end.
+struct FlagStage {
+  unsigned* buf;      // this wave's 128 LDS entries
+  unsigned n;         // staged rows (wave-uniform)
+};
+
+__device__ __forceinline__ void flag_flush(const ccfd_score_args& a, FlagStage& f, int lane) {
+  if (f.n == 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");       // this wave's LDS writes first
+  unsigned base = 0;
+  if (lane == 0) base = __hip_atomic_fetch_add(&a.slot_ctl[1], f.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  base = __shfl(base, 0);
+  for (unsigned i = (unsigned)lane; i < f.n; i += 64) a.flag_idx[base + i] = f.buf[i];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");       // reads done before reuse
+  f.n = 0;
+}
+
+// m = __ballot(fr_lane), known non-zero by the caller
+__device__ __forceinline__ void flag_push(const ccfd_score_args& a, FlagStage& f, unsigned long long m, bool fr_lane,
+                                          int row, int lane) {
+  if (a.flag_idx == nullptr) return;
+  if (fr_lane) f.buf[f.n + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
+  f.n += (unsigned)__popcll(m);
+  if (f.n > 64) flag_flush(a, f, lane);           // room for one more 64-row ballot
+}
+
 // Completion hand-off to the host, executed by EVERY thread as the kernel's last action
 // (cdna_hip_programming.md §6 Guideline 16 publish recipe, system scope): each storing wave
 // drains its stores, the workgroup barrier, lane 0 releases at system scope and takes a

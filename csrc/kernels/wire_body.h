@@ -26,6 +26,7 @@ template <class Scorer, int kWaves, int kPf, bool kR = false>
 __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int blk, int nblk) {
   __shared__ __attribute__((aligned(16))) char lds[Scorer::kLds > 0 ? Scorer::kLds : 16];
   __shared__ EpilogueLds epi;
+  __shared__ unsigned flbuf[kWaves][128];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -50,6 +51,7 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
 
   const float thr = a.threshold;
   const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
+  FlagStage fls{flbuf[wave], 0u};
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
   HistLanes hl;
@@ -84,7 +86,7 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     hist_lanes_add(hl, __shfl(am_g3, 48 + c));
     if (frm) {                                                   // rare: fraud rows' buckets
       if (fr && g == 3) atomicAdd(&epi.hist[kNB + amount_bucket_fast(amount)], 1u);
-      emit_flagged(a, fr && g == 0, row);
+      flag_push(a, fls, frm, fr && g == 3, row, lane);
     }
   };
   // steady state: the kPf strided tiles of a round all exist
@@ -135,7 +137,7 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
       for (int j = 0; j < kNB - 1; ++j) hgt[j] += __popcll(__ballot(amv > kB[j]));
       if (frm) {                                                  // rare: fraud rows' buckets
         if (fr) atomicAdd(&epi.hist[kNB + amount_bucket_fast(ams)], 1u);
-        emit_flagged(a, fr, row);
+        flag_push(a, fls, frm, fr, row, lane);
       }
       tile += 4 * tstride;
     }
@@ -177,6 +179,7 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     finish(p, __uint_as_float(cur.v.w), tile, rule_of(cur, p));
     tile += tstride;
   }
+  if (a.flag_idx != nullptr) flag_flush(a, fls, lane);
   psum = wave_sum_u64(psum);
   hist_lanes_commit(epi, hl, g, c);
   if constexpr (kQuadPath) {
