@@ -86,7 +86,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     hist_lanes_add(hl, __shfl(am_g3, 48 + c));
     if (frm) {                                                   // rare: fraud rows' buckets
       if (fr && g == 3) atomicAdd(&epi.hist[kNB + amount_bucket_fast(amount)], 1u);
-      flag_push(a, fls, frm, fr && g == 3, row, lane);
+      if (a.flags & CCFD_ARG_FLAG_DIRECT) emit_flagged(a, fr && g == 3, row);
+      else flag_push(a, fls, frm, fr && g == 3, row, lane);
     }
   };
   // steady state: the kPf strided tiles of a round all exist
@@ -137,7 +138,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
       for (int j = 0; j < kNB - 1; ++j) hgt[j] += __popcll(__ballot(amv > kB[j]));
       if (frm) {                                                  // rare: fraud rows' buckets
         if (fr) atomicAdd(&epi.hist[kNB + amount_bucket_fast(ams)], 1u);
-        flag_push(a, fls, frm, fr, row, lane);
+        if (a.flags & CCFD_ARG_FLAG_DIRECT) emit_flagged(a, fr, row);
+        else flag_push(a, fls, frm, fr, row, lane);
       }
       tile += 4 * tstride;
     }
