@@ -456,7 +456,8 @@ class Engine {
     a.items_per_batch = persist_C;
     a.tiles_per_wave = persist_tpw;
     a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | wire_flag |
-              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0) | (ablate & (CCFD_ARG_ABLATE_FENCE | CCFD_ARG_ABLATE_ACQUIRE));
+              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0) | (ablate & (CCFD_ARG_ABLATE_FENCE | CCFD_ARG_ABLATE_ACQUIRE | CCFD_ARG_ABLATE_COUNTERS |
+                        CCFD_ARG_ABLATE_OUTPUTS));
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;

@@ -150,7 +150,7 @@ __device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const
 __device__ __forceinline__ void persist_item_done(const ccfd_persist_args& a, EpilogueLds& epi,
                                                   const ccfd_persist_desc& sdesc, int slot, int C, int tid) {
   __syncthreads();
-  unsigned long long* cnt = a.counters[sdesc.epoch & 1];
+  unsigned long long* cnt = (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters[sdesc.epoch & 1];
   if (tid < 2 * kNB) {
     const unsigned h = epi.hist[tid];
     if (h && cnt) atomicAdd(&cnt[(tid < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + tid],
