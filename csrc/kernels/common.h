@@ -17,6 +17,35 @@ constexpr int kTileRows = 16;                // rows per 16x16x32 MFMA tile (one
 constexpr int kTileBytes = kTileRows * kF * 4;   // 1920: contiguous when ld == 30
 constexpr int kHeader = 64;
 
+// Row loads and output stores through the GLOBAL address space.  A generic pointer (every
+// pointer read from a descriptor or struct) compiles to FLAT instructions, and a FLAT
+// load / store counts on LGKM_CNT as well as VM_CNT: each `s_waitcnt lgkmcnt(0)` that an
+// LDS or scalar read of the epilogue needs then also waited for the wave's outstanding
+// host-memory traffic -- a proba store over PCIe before the next tile's weight reads, a
+// prefetched row chunk before the current chunk's LDS transpose.  Global instructions count
+// on VM_CNT only.  Every pointer handed to these is device memory or host memory mapped
+// into the GPU's address space, never LDS.
+#define CCFD_GAS __attribute__((address_space(1)))
+typedef unsigned ccfd_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned ccfd_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+template <class T>
+__device__ __forceinline__ void st_g(T* p, T v) { *(CCFD_GAS T*)p = v; }
+template <class T>
+__device__ __forceinline__ T ld_g(const T* p) { return *(const CCFD_GAS T*)p; }
+__device__ __forceinline__ uint4 ld_g16(const void* p) {            // 16-byte aligned
+  const ccfd_u32x4 v = *(const CCFD_GAS ccfd_u32x4*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ld_g16_a4(const void* p) {         // 4-byte aligned
+  const ccfd_u32x4_a4 v = *(const CCFD_GAS ccfd_u32x4_a4*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 ld_g16f(const void* p) {
+  const uint4 v = ld_g16(p);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
 // Must match contracts/metric_names.py AMOUNT_BUCKETS.
 __device__ __forceinline__ int amount_bucket(float a) {
   int b = 0;
@@ -177,7 +206,7 @@ __device__ __forceinline__ void emit_flagged(const ccfd_score_args& a, bool fr_l
     base = __hip_atomic_fetch_add(&a.slot_ctl[1], (unsigned)__popcll(m), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
   base = __shfl(base, leader);
-  if (fr_lane) a.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
+  if (fr_lane) st_g(a.flag_idx + base + __popcll(m & ((1ull << lane) - 1ull)), (unsigned)row);
 }
 
 // Per-wave LDS staging of fraud-routed row indices for the streaming bodies.  Appending
@@ -196,7 +225,7 @@ __device__ __forceinline__ void flag_flush(const ccfd_score_args& a, FlagStage& 
   unsigned base = 0;
   if (lane == 0) base = __hip_atomic_fetch_add(&a.slot_ctl[1], f.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   base = __shfl(base, 0);
-  for (unsigned i = (unsigned)lane; i < f.n; i += 64) a.flag_idx[base + i] = f.buf[i];
+  for (unsigned i = (unsigned)lane; i < f.n; i += 64) st_g(a.flag_idx + base + i, f.buf[i]);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");       // reads done before reuse
   f.n = 0;
 }
@@ -277,10 +306,10 @@ __device__ __forceinline__ void tile_issue(const float* __restrict__ xt, int ava
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < kTileBytes / 16) {
       if (off + 16 <= avail) {
-        v = src[i];
+        v = ld_g16f(src + i);
       } else if (off + 8 <= avail) {
-        const float2 h = reinterpret_cast<const float2*>(xt)[2 * i];
-        v.x = h.x; v.y = h.y;
+        v.x = ld_g(xt + 4 * i);
+        v.y = ld_g(xt + 4 * i + 1);
       }
     }
     r.v[it] = v;
@@ -302,8 +331,7 @@ struct WireRegs { uint4 v; };
 __device__ __forceinline__ void wire_issue(const unsigned char* __restrict__ x, int n, int tile, int c, int g,
                                            WireRegs& r) {
   const int row = tile * kTileRows + c;
-  r.v = row < n ? *reinterpret_cast<const uint4*>(x + (size_t)row * CCFD_WIRE_ROW_BYTES + 16 * g)
-                : make_uint4(0u, 0u, 0u, 0u);
+  r.v = row < n ? ld_g16(x + (size_t)row * CCFD_WIRE_ROW_BYTES + 16 * g) : make_uint4(0u, 0u, 0u, 0u);
 }
 
 __device__ __forceinline__ void wire_features(const WireRegs& r, int g, float xv[8]) {

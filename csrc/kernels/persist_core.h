@@ -119,7 +119,7 @@ __device__ __forceinline__ void persist_emit_flagged(const ccfd_persist_args& a,
     base = __hip_atomic_fetch_add(&a.dev->nflag[slot], (unsigned)__popcll(m), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
   base = __shfl(base, leader);
-  if (fr_lane) sdesc.flag_idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned)row;
+  if (fr_lane) st_g(sdesc.flag_idx + base + __popcll(m & ((1ull << lane) - 1ull)), (unsigned)row);
 }
 
 // One thread: system-scope release of this item's outputs, then a ticket on the slot; the last

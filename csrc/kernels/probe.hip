@@ -42,7 +42,66 @@ __global__ __launch_bounds__(256) void read_blocks_kernel(const char* __restrict
   if (acc == 1234.5678f) out[threadIdx.x] = acc;
 }
 
+// Same stream as read_sum_kernel with a `W`-byte load per lane (4: one dword, 8, 16): how
+// the wave instruction's width (256 B / 512 B / 1 KB contiguous) sets the zero-copy rate.
+template <int W>
+__global__ __launch_bounds__(256) void read_sum_width_kernel(const unsigned* __restrict__ src, size_t nw, float* out) {
+  constexpr int K = W / 4;
+  unsigned acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw / K; i += stride) {
+    if constexpr (K == 1) {
+      acc += src[i];
+    } else if constexpr (K == 2) {
+      const uint2 v = reinterpret_cast<const uint2*>(src)[i];
+      acc += v.x + v.y;
+    } else {
+      const uint4 v = reinterpret_cast<const uint4*>(src)[i];
+      acc += v.x + v.y + v.z + v.w;
+    }
+  }
+  if (acc == 0x12345678u) out[threadIdx.x] = (float)acc;
+}
+
 }  // namespace
+
+// Zero-copy read GB/s of `bytes` of pinned host memory with `width`-byte loads per lane
+// (4, 8 or 16), `grid` x 256 threads, `iters` passes (events around the timed passes).
+extern "C" double ccfd_bw_probe_width(const void* src_host, size_t bytes, int width, int grid, int iters,
+                                      void* dev_scratch) {
+  if (!src_host || !dev_scratch || bytes < 16 || grid < 1 || iters < 1 || (width != 4 && width != 8 && width != 16))
+    return -1.0;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(src_host), 0) != hipSuccess) return -2.0;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -4.0;
+  bool ok = true;
+  const size_t nw = bytes / 4;
+  auto once = [&]() {
+    const unsigned* p = static_cast<const unsigned*>(d);
+    float* o = static_cast<float*>(dev_scratch);
+    if (width == 4) hipLaunchKernelGGL(read_sum_width_kernel<4>, dim3(grid), dim3(256), 0, s, p, nw, o);
+    else if (width == 8) hipLaunchKernelGGL(read_sum_width_kernel<8>, dim3(grid), dim3(256), 0, s, p, nw, o);
+    else hipLaunchKernelGGL(read_sum_width_kernel<16>, dim3(grid), dim3(256), 0, s, p, nw, o);
+    ok = ok && hipGetLastError() == hipSuccess;
+  };
+  hipEvent_t e0, e1;
+  ok = ok && hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
+  float ms = 0.f;
+  if (ok) {
+    once();
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    ok = ok && hipEventRecord(e0, s) == hipSuccess;
+    for (int i = 0; i < iters && ok; ++i) once();
+    ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+         hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  (void)hipStreamDestroy(s);
+  if (!ok) return -4.0;
+  return ms > 0 ? (double)(nw / (width / 4)) * width * iters / (ms * 1e-3) / 1e9 : -3.0;
+}
 
 // Pinned host memory backed by transparent huge pages where the kernel grants them
 // (2 MB-aligned anonymous mapping, MADV_HUGEPAGE, faulted in, then hipHostRegister): fewer

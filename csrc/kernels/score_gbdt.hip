@@ -152,8 +152,8 @@ __global__ __launch_bounds__(256) void score_gbdt_kernel(ccfd_score_args a, int 
       else fr = valid && (p >= a.threshold);
       const int row = row0 + lane;
       if (valid) {
-        if (a.proba) a.proba[row] = p;
-        if (a.route) a.route[row] = fr ? 1 : 0;
+        if (a.proba) st_g(a.proba + row, p);
+        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
         atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(xs[kAmountCol][lane])], 1u);
       }
       unsigned long long ps = valid ? (unsigned long long)(p * 1e6f + 0.5f) : 0ull;
@@ -329,8 +329,8 @@ __global__ __launch_bounds__(256) void score_gbdt_v2_kernel(ccfd_score_args a) {
       if constexpr (kR) fr = valid && rule_route(a.rules, p, [&](int j) { return q == 0 ? x0[j] : x1[j]; });
       else fr = valid && (p >= a.threshold);
       if (valid) {
-        if (a.proba) a.proba[row] = p;
-        if (a.route) a.route[row] = fr ? 1 : 0;
+        if (a.proba) st_g(a.proba + row, p);
+        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
         psum += (unsigned)(p * 1e6f + 0.5f);
         atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket_fast(q == 0 ? x0[kAmountCol] : x1[kAmountCol])], 1u);
       }

@@ -19,11 +19,12 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
   const int gstride = gridDim.x * kG32Waves;
   int grp = blockIdx.x * kG32Waves + wave;
   const unsigned char* __restrict__ xb = reinterpret_cast<const unsigned char*>(a.x);
+  const bool dw = (a.flags & CCFD_ARG_G20_DWORD) != 0;          // G20 fetch form (g32_core.h)
 
   // rows first: the host-memory latency overlaps the leaf staging below
   G32Row pre[R];
 #pragma unroll
-  for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, grp * R + q, lane, pre[q]);
+  for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, grp * R + q, lane, pre[q], dw);
 
   epi_init(epi);
   stamp_start(a, blockIdx.x);
@@ -50,17 +51,17 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
     unsigned b0[kF], b1[kF];
     unsigned meta[R];                                           // bucket | stamp << 8
     G32Row cur = pre[0];
-    gx_rows<kG20>(xt[wave], lane, cur);
+    gx_rows<kG20>(xt[wave], lane, cur, dw);
     meta[0] = gx_lift<kG20>(cur, b0);
     if constexpr (R == 2) {
       cur = pre[1];
-      gx_rows<kG20>(xt[wave], lane, cur);
+      gx_rows<kG20>(xt[wave], lane, cur, dw);
       meta[1] = gx_lift<kG20>(cur, b1);
     }
     const int nxt = grp + gstride;
     if (nxt < ngroups) {
 #pragma unroll
-      for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, nxt * R + q, lane, pre[q]);
+      for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, nxt * R + q, lane, pre[q], dw);
     }
     float acc[R];
     g32_trees<D, R>(b0, b1, leaves, feat, kbin, T, acc);
@@ -75,8 +76,8 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
       else fr = valid && fresh && (p >= a.threshold);
       if (valid) {
         if (store_out) {
-          if (a.proba) a.proba[row] = p;
-          if (a.route) a.route[row] = fr ? 1 : 0;
+          if (a.proba) st_g(a.proba + row, p);
+          if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
         }
         if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
         atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta[q] & 0xffu), kNB - 1)], 1u);
@@ -103,8 +104,10 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
 // stride beyond).  A 65536-row micro-batch is 1024 chunks = 256 workgroups at R = 1: every
 // CU has its rows in flight at once.  CCFD_G32_R: 64-row chunks per wave step (1 | 2).
 template <int D, int R, bool kG20>
-static void launch_g32_r(const ccfd_score_args& a, hipStream_t s) {
+static void launch_g32_r(const ccfd_score_args& a0, hipStream_t s) {
   constexpr int L = 1 << D;
+  ccfd_score_args a = a0;
+  if (g32_env("CCFD_G20_FETCH_DWORD", 0, 0, 1)) a.flags |= CCFD_ARG_G20_DWORD;
   const int wgs_per_cu = g32_env("CCFD_G32_WGS_PER_CU", 4, 1, 8);   // read per launch: sweepable in-process
   const int nchunks = (a.n + kG32Rows - 1) / kG32Rows;
   const int ngroups = (nchunks + R - 1) / R;

@@ -86,8 +86,8 @@ __device__ __forceinline__ void lr_body(const ccfd_score_args& a, int blk, int n
       fr = valid && (p >= a.threshold);
     }
     if (valid && g == 0) {
-      if (a.proba) a.proba[row] = p;
-      if (a.route) a.route[row] = fr ? 1 : 0;
+      if (a.proba) st_g(a.proba + row, p);
+      if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
       psum += (unsigned)(p * 1e6f + 0.5f);
     }
     fraud += __popcll(__ballot(fr && g == 0));

@@ -103,8 +103,8 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
 
     if (valid && g == 0) {
       if (!(a.flags & CCFD_ARG_ABLATE_OUTPUTS)) {
-        if (a.proba) a.proba[row] = p;
-        if (a.route) a.route[row] = fr ? 1 : 0;
+        if (a.proba) st_g(a.proba + row, p);
+        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
       }
       psum += (unsigned)(p * 1e6f + 0.5f);              // p in [0,1]: u32 convert, u64 sum
     }

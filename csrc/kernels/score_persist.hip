@@ -85,10 +85,12 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     if (s_cmd) break;
 
     const unsigned long long item = s_item;
+    // the item's descriptor in registers: the epilogue reads its pointers with no LDS wait
+    const ccfd_persist_desc dsc = sdesc;
     const int chunk = (int)(item % (unsigned long long)C);
-    const int slot = (int)(sdesc.seq % (unsigned long long)a.ring);
-    const int n = sdesc.n;
-    const float* x = sdesc.x;
+    const int slot = (int)(dsc.seq % (unsigned long long)a.ring);
+    const int n = dsc.n;
+    const float* x = dsc.x;
     const int kTilesPerWave = a.tiles_per_wave;
     const int tile0 = chunk * (4 * kTilesPerWave) + wave;      // wave w: tiles tile0 + 4k
     if (chunk == 0 && tid == 0)                                // K7: micro-batch start (item 0 claimed first)
@@ -122,15 +124,15 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
         fr = valid && (p >= a.threshold);
       }
       if (valid && g == 0) {
-        if (sdesc.proba) sdesc.proba[row] = p;
-        if (sdesc.route) sdesc.route[row] = fr ? 1 : 0;
+        if (dsc.proba) st_g(dsc.proba + row, p);
+        if (dsc.route) st_g(dsc.route + row, (uint8_t)(fr ? 1 : 0));
         ps_w += (unsigned long long)(p * 1e6f + 0.5f);
       }
       const unsigned long long m = __ballot(fr && g == 0);
       nf_w += __popcll(m);
       nv_w += __popcll(__ballot(valid && g == 0));
       if (valid && g == 3) atomicAdd(&epi.hist[(fr ? kNB : 0) + amount_bucket(amount)], 1u);
-      persist_emit_flagged(a, sdesc, slot, m, fr && g == 0, row, lane);
+      persist_emit_flagged(a, dsc, slot, m, fr && g == 0, row, lane);
     };
     // W64 items of 2, 4 or 8 tiles per wave (128 / 256 / 512 rows): every tile
     // of the item in flight at once -- the item costs one PCIe round trip instead of one per
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
       atomicAdd(&epi.rows, nv_w);
       atomicAdd(&epi.psum_e6, ps_w);
     }
-    persist_item_done(a, epi, sdesc, slot, C, tid);
+    persist_item_done(a, epi, dsc, slot, C, tid);
   }
 }
 
@@ -329,8 +331,8 @@ __global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) 
       }
       if (valid && g == 0) {
         if (!(a.flags & CCFD_ARG_ABLATE_OUTPUTS)) {              // diagnostics only
-          if (d.proba) d.proba[row] = p;
-          if (d.route) d.route[row] = fr ? 1 : 0;
+          if (d.proba) st_g(d.proba + row, p);
+          if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
         }
         ps_w += (unsigned long long)(p * 1e6f + 0.5f);
       }

@@ -74,8 +74,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     const bool fr = valid && (kR ? rf : (p >= thr));
     if (valid && g == 0) {
       if (store_out) {
-        if (a.proba) a.proba[row] = p;
-        if (a.route) a.route[row] = fr ? 1 : 0;
+        if (a.proba) st_g(a.proba + row, p);
+        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
       }
       psum += (unsigned)(p * 1e6f + 0.5f);
     }
@@ -125,8 +125,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
       const bool fr = valid && p >= thr;
       if (valid) {
         if (store_out) {
-          if (a.proba) a.proba[row] = p;
-          if (a.route) a.route[row] = fr ? 1 : 0;
+          if (a.proba) st_g(a.proba + row, p);
+          if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
         }
         psum += (unsigned)(p * 1e6f + 0.5f);
       }
