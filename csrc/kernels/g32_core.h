@@ -115,12 +115,13 @@ __device__ __forceinline__ void g20_rows(uint4* __restrict__ t4, int lane, G32Ro
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// G20 chunk in 16-byte lanes (default; CCFD_ARG_G20_DWORD selects the dword form above):
-// lane l loads bytes [16l, 16l+16) and lanes 0..15 also [1024+16l, ...), so the 1280 B chunk
-// is two wave instructions -- one contiguous 1 KB request and one 256 B request -- instead
-// of five 256 B ones (the W64 kernels' 1 KB-per-instruction tiles are the ones that reach
-// the full zero-copy link rate).  A micro-batch may start at any row, so the vectors are
-// only 4-byte aligned.  The batch's last chunk loads dword by dword up to its last byte.
+// G20 chunk in 16-byte lanes (CCFD_ARG_G20_X4, A/B only): lane l loads bytes [16l, 16l+16)
+// and lanes 0..15 also [1024+16l, ...), so the 1280 B chunk is two wave instructions instead
+// of five.  Measured slower: zero-copy reads run at 57.5 GB/s with 4- or 8-byte lanes and
+// 55.5 GB/s with 16-byte lanes (bench/experiments/load_width_probe.py), and the G20 bench
+// gave 2.43e9 vs 2.47e9 tx/s with the dword form (profiles/r3/load_width/).  A micro-batch
+// may start at any row, so the vectors are only 4-byte aligned; the batch's last chunk
+// loads dword by dword up to its last byte.
 
 __device__ __forceinline__ uint4 g20_tail4(const unsigned char* __restrict__ x, long o, long nb) {
   const unsigned* __restrict__ xw = reinterpret_cast<const unsigned*>(x);
@@ -225,23 +226,23 @@ __device__ __forceinline__ unsigned g32_lift(const G32Row& r, unsigned (&b)[kF])
   return r.hi.w >> 16;
 }
 
-// Row-format policy of the binned-row kernels: G32 (u8 bins) or G20 (5-bit bins); `dw`
-// (launch flag CCFD_ARG_G20_DWORD, wave-uniform) selects the dword G20 fetch.
+// Row-format policy of the binned-row kernels: G32 (u8 bins) or G20 (5-bit bins); `x4`
+// (launch flag CCFD_ARG_G20_X4, wave-uniform) selects the 16-byte G20 fetch.
 template <bool kG20>
 __device__ __forceinline__ void gx_fetch(const unsigned char* __restrict__ x, int n, int chunk, int lane, G32Row& r,
-                                         bool dw) {
+                                         bool x4) {
   if constexpr (kG20) {
-    if (dw) g20_fetch(x, n, chunk, lane, r);
-    else g20_fetch_x4(x, n, chunk, lane, r);
+    if (x4) g20_fetch_x4(x, n, chunk, lane, r);
+    else g20_fetch(x, n, chunk, lane, r);
   } else {
     g32_fetch(x, n, chunk, lane, r);
   }
 }
 template <bool kG20>
-__device__ __forceinline__ void gx_rows(uint4* __restrict__ t, int lane, G32Row& r, bool dw) {
+__device__ __forceinline__ void gx_rows(uint4* __restrict__ t, int lane, G32Row& r, bool x4) {
   if constexpr (kG20) {
-    if (dw) g20_rows(t, lane, r);
-    else g20_rows_x4(t, lane, r);
+    if (x4) g20_rows_x4(t, lane, r);
+    else g20_rows(t, lane, r);
   } else {
     g32_rows(t, lane, r);
   }
