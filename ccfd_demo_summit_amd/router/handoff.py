@@ -75,7 +75,9 @@ class KieHandoff:
         self.signals_stale = 0
         self.retries = 0
         self.errors: Deque[str] = collections.deque(maxlen=20)
-        self.failed: List[Tuple[str, Any, str]] = []     # non-retryable answers (kept, reported)
+        # non-retryable answers: the most recent are kept for the operator, all are counted
+        self.failed: Deque[Tuple[str, Any, str]] = collections.deque(maxlen=1000)
+        self.failed_total = 0
         self.outage_s = 0.0
         self._stop = False
         self._inflight = 0
@@ -210,11 +212,14 @@ class KieHandoff:
                     if not _transient(e):
                         # a definite refusal (e.g. 404 unknown container): retrying cannot
                         # help; keep it for the operator instead of wedging the queue
-                        self.failed.append((kind, payload, repr(e)[:300]))
-                        self.errors.append(repr(e)[:300])
+                        with self._cv:
+                            self.failed.append((kind, payload, repr(e)[:300]))
+                            self.failed_total += 1
+                            self.errors.append(repr(e)[:300])
                         break
-                    self.retries += 1
-                    self.errors.append(repr(e)[:300])
+                    with self._cv:
+                        self.retries += 1
+                        self.errors.append(repr(e)[:300])
                     if self.metrics is not None:
                         self.metrics.retries.inc()
                     if t_fail is None:
@@ -225,7 +230,8 @@ class KieHandoff:
                     time.sleep(delay)
                     delay = min(self.max_backoff_s, delay * 2)
             if t_fail is not None:
-                self.outage_s += time.monotonic() - t_fail
+                with self._cv:
+                    self.outage_s += time.monotonic() - t_fail
             self._ack_many(seqs, n_items)
 
     def stats(self) -> Dict[str, Any]:
@@ -233,4 +239,4 @@ class KieHandoff:
             return {"submitted": self.submitted_items, "acked": self.acked_items, "depth": self._queued_items,
                     "acked_seq": self.acked_seq, "last_seq": self._next_seq - 1, "retries": self.retries,
                     "signals_ok": self.signals_ok, "signals_stale": self.signals_stale,
-                    "failed": len(self.failed), "outage_s": round(self.outage_s, 3)}
+                    "failed": self.failed_total, "outage_s": round(self.outage_s, 3)}
