@@ -54,8 +54,6 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_CHUNK_RING 128       // persistent G32: one-chunk prefetch ring (default) instead of the whole item in flight
 #define CCFD_ARG_FLAG_DIRECT 1024      // W64 launch kernels: reserve flag-list slots per ballot (A/B of the LDS staging)
 #define CCFD_ARG_ABLATE_ACQUIRE 512   // persistent kernels: no acquire before reading an item's rows (diagnostics)
-#define CCFD_ARG_G20_X4 2048          // G20 kernels: 16-byte vector loads per chunk instead of five dword loads (A/B; slower)
-#define CCFD_ARG_W64_X2 4096          // persistent W64 kernel: 8-byte lane loads (512 B per instruction) + LDS hand-off (A/B)
 #define CCFD_ARG_PIPE_ITEMS 256       // persistent W64 MLP: statically assigned 64/128-row items, the next
                                       // item's rows fetched while the current one is scored
 

@@ -19,12 +19,11 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
   const int gstride = gridDim.x * kG32Waves;
   int grp = blockIdx.x * kG32Waves + wave;
   const unsigned char* __restrict__ xb = reinterpret_cast<const unsigned char*>(a.x);
-  const bool x4 = (a.flags & CCFD_ARG_G20_X4) != 0;          // G20 fetch form (g32_core.h)
 
   // rows first: the host-memory latency overlaps the leaf staging below
   G32Row pre[R];
 #pragma unroll
-  for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, grp * R + q, lane, pre[q], x4);
+  for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, grp * R + q, lane, pre[q]);
 
   epi_init(epi);
   stamp_start(a, blockIdx.x);
@@ -51,17 +50,17 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
     unsigned b0[kF], b1[kF];
     unsigned meta[R];                                           // bucket | stamp << 8
     G32Row cur = pre[0];
-    gx_rows<kG20>(xt[wave], lane, cur, x4);
+    gx_rows<kG20>(xt[wave], lane, cur);
     meta[0] = gx_lift<kG20>(cur, b0);
     if constexpr (R == 2) {
       cur = pre[1];
-      gx_rows<kG20>(xt[wave], lane, cur, x4);
+      gx_rows<kG20>(xt[wave], lane, cur);
       meta[1] = gx_lift<kG20>(cur, b1);
     }
     const int nxt = grp + gstride;
     if (nxt < ngroups) {
 #pragma unroll
-      for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, nxt * R + q, lane, pre[q], x4);
+      for (int q = 0; q < R; ++q) gx_fetch<kG20>(xb, n, nxt * R + q, lane, pre[q]);
     }
     float acc[R];
     g32_trees<D, R>(b0, b1, leaves, feat, kbin, T, acc);
@@ -104,10 +103,8 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
 // stride beyond).  A 65536-row micro-batch is 1024 chunks = 256 workgroups at R = 1: every
 // CU has its rows in flight at once.  CCFD_G32_R: 64-row chunks per wave step (1 | 2).
 template <int D, int R, bool kG20>
-static void launch_g32_r(const ccfd_score_args& a0, hipStream_t s) {
+static void launch_g32_r(const ccfd_score_args& a, hipStream_t s) {
   constexpr int L = 1 << D;
-  ccfd_score_args a = a0;
-  if (g32_env("CCFD_G20_FETCH_X4", 0, 0, 1)) a.flags |= CCFD_ARG_G20_X4;
   const int wgs_per_cu = g32_env("CCFD_G32_WGS_PER_CU", 4, 1, 8);   // read per launch: sweepable in-process
   const int nchunks = (a.n + kG32Rows - 1) / kG32Rows;
   const int ngroups = (nchunks + R - 1) / R;

@@ -22,7 +22,6 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int C = a.items_per_batch;
   const int cpw = a.tiles_per_wave;                       // 64-row chunks per wave per item
-  const bool x4 = (a.flags & CCFD_ARG_G20_X4) != 0;    // G20 fetch form (g32_core.h)
   if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
     if (wave == 0) persist_doorbell(a, lane);
     return;                                               // no barrier is ever used by WG 0
@@ -46,7 +45,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   unsigned long long psum = 0;
   auto score_chunk = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, G32Row& cur)
       __attribute__((always_inline)) {
-    gx_rows<kG20>(xt[wave], lane, cur, x4);
+    gx_rows<kG20>(xt[wave], lane, cur);
     unsigned b0[kF];
     const unsigned meta = gx_lift<kG20>(cur, b0);
     float acc[1];
@@ -107,7 +106,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
 #pragma unroll
       for (int k = 0; k < CPW; ++k) {
         const int chunk = c0 + kG32Waves * k;
-        if (chunk * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk, lane, r[k], x4);
+        if (chunk * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk, lane, r[k]);
       }
 #pragma unroll
       for (int k = 0; k < CPW; ++k) {
@@ -118,13 +117,13 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     };
     if (a.flags & CCFD_ARG_CHUNK_RING) {                  // default: one chunk ahead
       G32Row pre;
-      if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre, x4);
+      if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre);
 #pragma unroll 1
       for (int k = 0; k < cpw; ++k) {
         const int chunk = c0 + kG32Waves * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
         G32Row cur_row = pre;
-        if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kG32Waves, lane, pre, x4);
+        if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kG32Waves, lane, pre);
         score_chunk(d, slot, n, chunk, cur_row);
       }
     } else if (cpw == 1) {
@@ -146,7 +145,6 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   // trees overlap the next chunk's load better); CCFD_G32_INFLIGHT=1 selects the latter.
   // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
   if (g32_env("CCFD_G32_INFLIGHT", 0, 0, 1) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
-  if (g32_env("CCFD_G20_FETCH_X4", 0, 0, 1)) a.flags |= CCFD_ARG_G20_X4;   // A/B of the G20 fetch form
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
   if (gl) {

@@ -22,7 +22,6 @@
 // while it waits for an unposted batch.  The host never posts batch b into ring slot
 // b % R before observing done for b - R, which is what makes the slot-local state
 // (remaining/nflag reset by the last ticket) safe to reuse.
-#include <cstdlib>
 #include <type_traits>
 
 #include "mlp_core.h"
@@ -142,21 +141,12 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     auto full_item = [&](auto kT) __attribute__((always_inline)) {
       constexpr int T = decltype(kT)::value;
       WireRegs r[T];
-      WireRegs2 r2[T];
-      const bool x2 = (a.flags & CCFD_ARG_W64_X2) != 0;      // 8-byte lane loads (common.h)
 #pragma unroll
-      for (int k = 0; k < T; ++k) {
-        if (x2) wire_issue2(xw, n, tile0 + 4 * k, lane, r2[k]);
-        else wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
-      }
+      for (int k = 0; k < T; ++k) wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
 #pragma unroll
       for (int k = 0; k < T; k += 2) {
         const int ta = tile0 + 4 * k;
         if (ta * kTileRows >= n) break;                    // wave-uniform
-        if (x2) {
-          wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k], r[k]);
-          wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k + 1], r[k + 1]);
-        }
         float pa, pb;
         float xa[8], xb[8];
         if (kModel == CCFD_MODEL_MLP) {
@@ -433,10 +423,8 @@ extern "C" int ccfd_persist_launch(const ccfd_persist_args* a, int grid, void* s
       default: return -2;
     }
   } else if (a->model == CCFD_MODEL_MLP) {
-    ccfd_persist_args am = *a;
-    if (const char* e = getenv("CCFD_W64_FETCH_X2")) if (atoi(e) == 1) am.flags |= CCFD_ARG_W64_X2;   // A/B
-    if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, true>), dim3(grid), dim3(256), 0, s, am);
-    else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, false>), dim3(grid), dim3(256), 0, s, am);
+    if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, true>), dim3(grid), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_MLP, false>), dim3(grid), dim3(256), 0, s, *a);
   } else if (a->model == CCFD_MODEL_LR) {
     if (a->rules) hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_LR, true>), dim3(grid), dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((persist_kernel<CCFD_MODEL_LR, false>), dim3(grid), dim3(256), 0, s, *a);

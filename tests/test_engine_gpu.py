@@ -242,18 +242,6 @@ def test_persistent_wire_item_sizes_exact(gpu, setup, monkeypatch, kind, item_ro
     """Every persistent work-item size on W64 rows -- 256 / 512 take the all-tiles-in-flight
     paired path, the others the one-tile prefetch loop -- scores every row once, full and
     partial micro-batches alike: rows, routes and the proba sum match the wire oracle."""
-    _wire_items_check(gpu, setup, monkeypatch, kind, item_rows)
-
-
-@pytest.mark.parametrize("item_rows", [256, 512])
-def test_persistent_wire_x2_fetch_exact(gpu, setup, monkeypatch, item_rows):
-    """The 8-byte-lane W64 fetch with its LDS hand-off (CCFD_W64_FETCH_X2=1, common.h
-    wire_issue2 / wire_handoff) scores exactly like the 16-byte fetch, partial tiles too."""
-    monkeypatch.setenv("CCFD_W64_FETCH_X2", "1")
-    _wire_items_check(gpu, setup, monkeypatch, "mlp", item_rows)
-
-
-def _wire_items_check(gpu, setup, monkeypatch, kind, item_rows):
     from ccfd_demo_summit_amd.contracts import decode_wire, encode_wire
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel

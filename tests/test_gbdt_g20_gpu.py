@@ -50,13 +50,10 @@ def test_g20_kernel_exact(gpu, data, n, depth):
     assert int(cnt[4]) == 0
 
 
-@pytest.mark.parametrize("fetch_x4", ["0", "1"])
-def test_g20_unaligned_start_and_stale_stamp(gpu, data, monkeypatch, fetch_x4):
-    """A batch starting at row 1 of a buffer is only 4-byte aligned (20 B rows): both fetch
-    forms (dwords by default, 16-byte vectors with CCFD_G20_FETCH_X4=1) still read it
-    exactly, the tail chunk included; rows of another stamp are counted, not scored."""
+def test_g20_unaligned_start_and_stale_stamp(gpu, data):
+    """A batch starting at row 1 of a buffer is only 4-byte aligned (20 B rows): the dword
+    loads still read it exactly; rows of another stamp are counted, not scored."""
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel, new_counters, score
-    monkeypatch.setenv("CCFD_G20_FETCH_X4", fetch_x4)
     X = data[:4098]
     m = _model(6, X)
     dm = DeviceModel(m, gpu, bins="g20")
@@ -112,16 +109,14 @@ def test_g20_engine_pump_exact(gpu, input_mode, exec_mode):
     log.free()
 
 
-@pytest.mark.parametrize("inflight,fetch_x4", [("0", "0"), ("1", "0"), ("0", "1")])
+@pytest.mark.parametrize("inflight", ["0", "1"])
 @pytest.mark.parametrize("item_rows", [256, 1024])
-def test_g20_persistent_partial_batches_exact(gpu, monkeypatch, inflight, fetch_x4, item_rows):
-    """Both persistent item loops and both G20 fetch forms, partial micro-batches starting at
-    rows that are not a multiple of 4 (4-byte-aligned G20 rows): every row scored once,
-    routes exact."""
+def test_g20_persistent_partial_batches_exact(gpu, monkeypatch, inflight, item_rows):
+    """Both persistent item loops, partial micro-batches starting at rows that are not a
+    multiple of 4 (4-byte-aligned G20 rows): every row scored once, routes exact."""
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
     monkeypatch.setenv("CCFD_G32_INFLIGHT", inflight)
-    monkeypatch.setenv("CCFD_G20_FETCH_X4", fetch_x4)
     monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
     B = 8192
     X, _ = generate(B * 3 + 3000, seed=55)
