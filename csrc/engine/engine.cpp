@@ -531,8 +531,10 @@ class Engine {
     const uint64_t sq = seq;                       // caller increments seq after submit
     ccfd_persist_desc& d = pdesc[sq % cfg.depth];
     d.x = x_dev;
-    d.proba = s.h_proba_dev;
-    d.route = s.h_route_dev;
+    // CCFD_ABLATE & 32 (diagnostics only): no per-row outputs, the kernels skip null pointers
+    const bool no_out = (ablate & CCFD_ARG_ABLATE_OUTPUTS) != 0;
+    d.proba = no_out ? nullptr : s.h_proba_dev;
+    d.route = no_out ? nullptr : s.h_route_dev;
     d.flag_idx = s.h_flag_dev;
     d.n = s.rows;
     d.epoch = epoch & 1;
