@@ -18,6 +18,9 @@ _NATIVE = Path(__file__).resolve().parents[1] / "_native"
 # CCFD_SANITIZE=<san>: load the host-sanitizer build (ops/build.py) instead
 _SAN = os.environ.get("CCFD_SANITIZE", "")
 LIB_PATH = _NATIVE / (f"libccfd_hip_{_SAN.replace(',', '_')}.so" if _SAN else "libccfd_hip.so")
+# CCFD_LIB_PATH=<path>: load an A/B build (scripts/build_ab.py) instead
+if os.environ.get("CCFD_LIB_PATH"):
+    LIB_PATH = Path(os.environ["CCFD_LIB_PATH"]).resolve()
 
 MODEL_LR, MODEL_MLP, MODEL_GBDT = 0, 1, 2
 MODEL_IDS = {"lr": MODEL_LR, "mlp": MODEL_MLP, "gbdt": MODEL_GBDT}

@@ -33,6 +33,11 @@ template <class T>
 __device__ __forceinline__ void st_g(T* p, T v) { *(CCFD_GAS T*)p = v; }
 template <class T>
 __device__ __forceinline__ T ld_g(const T* p) { return *(const CCFD_GAS T*)p; }
+typedef unsigned ccfd_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 ld_g8(const void* p) {             // 8-byte aligned
+  const ccfd_u32x2 v = *(const CCFD_GAS ccfd_u32x2*)p;
+  return make_uint2(v.x, v.y);
+}
 __device__ __forceinline__ uint4 ld_g16(const void* p) {            // 16-byte aligned
   const ccfd_u32x4 v = *(const CCFD_GAS ccfd_u32x4*)p;
   return make_uint4(v.x, v.y, v.z, v.w);
@@ -332,6 +337,34 @@ __device__ __forceinline__ void wire_issue(const unsigned char* __restrict__ x, 
                                            WireRegs& r) {
   const int row = tile * kTileRows + c;
   r.v = row < n ? ld_g16(x + (size_t)row * CCFD_WIRE_ROW_BYTES + 16 * g) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// The same tile in 8-byte lanes (compile-time CCFD_W64_FETCH_X2, A/B builds): instruction h covers rows 8h..8h+7 --
+// 512 contiguous bytes, lane l at byte 512h + 8l -- and wire_handoff passes lane (g, c) its
+// 16 bytes of row c through a wave-private 1 KB LDS buffer.  Zero-copy reads of pinned host
+// memory run at 57.5 GB/s with 4- or 8-byte lanes and 55.5 GB/s with 16-byte lanes
+// (bench/experiments/load_width_probe.py).
+struct WireRegs2 { uint2 v[2]; };
+
+__device__ __forceinline__ void wire_issue2(const unsigned char* __restrict__ x, int n, int tile, int lane,
+                                            WireRegs2& r) {
+  const unsigned char* t = x + (size_t)tile * kTileRows * CCFD_WIRE_ROW_BYTES;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = tile * kTileRows + 8 * h + (lane >> 3);
+    r.v[h] = row < n ? ld_g8(t + 512 * h + 8 * lane) : make_uint2(0u, 0u);
+  }
+}
+
+__device__ __forceinline__ void wire_handoff(uint2* __restrict__ lds, int lane, int c, int g, const WireRegs2& r,
+                                             WireRegs& out) {
+  lds[lane] = r.v[0];
+  lds[64 + lane] = r.v[1];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  out.v = reinterpret_cast<const uint4*>(lds)[4 * c + g];     // row c, bytes [16g, 16g+16)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
 __device__ __forceinline__ void wire_features(const WireRegs& r, int g, float xv[8]) {

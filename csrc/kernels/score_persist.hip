@@ -28,6 +28,12 @@
 #include "persist_core.h"
 #include "rules.h"
 
+// A/B build knob (scripts/build_ab.py): W64 rows in 8-byte lanes + LDS hand-off (common.h
+// wire_issue2) instead of 16-byte lanes in the claimed-item kernel.
+#ifndef CCFD_W64_FETCH_X2
+#define CCFD_W64_FETCH_X2 0
+#endif
+
 namespace ccfd {
 
 int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s);   // score_gbdt_g32_persist.hip
@@ -141,12 +147,20 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     auto full_item = [&](auto kT) __attribute__((always_inline)) {
       constexpr int T = decltype(kT)::value;
       WireRegs r[T];
+      [[maybe_unused]] WireRegs2 r2[T];
 #pragma unroll
-      for (int k = 0; k < T; ++k) wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
+      for (int k = 0; k < T; ++k) {
+        if constexpr (CCFD_W64_FETCH_X2) wire_issue2(xw, n, tile0 + 4 * k, lane, r2[k]);
+        else wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
+      }
 #pragma unroll
       for (int k = 0; k < T; k += 2) {
         const int ta = tile0 + 4 * k;
         if (ta * kTileRows >= n) break;                    // wave-uniform
+        if constexpr (CCFD_W64_FETCH_X2) {
+          wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k], r[k]);
+          wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k + 1], r[k + 1]);
+        }
         float pa, pb;
         float xa[8], xb[8];
         if (kModel == CCFD_MODEL_MLP) {
