@@ -172,22 +172,28 @@ def _verify_topology(args, ctx, ident: dict):
 
 def _h2d_probe(lib_, ms: float, mb: int = 256) -> float:
     """Zero-copy kernel read bandwidth from this rank's pinned host memory (GB/s), run for
-    ~``ms`` (the bench/roofline.py method); all ranks run it at once, so host-DRAM and
+    ~``ms``: the better of 16-byte and 4-byte lanes (the link gives ~57.5 GB/s to 4-byte
+    lanes and ~55.5 to 16-byte ones, profiles/r3/load_width/), so the reported ceiling is
+    the link's, not one load width's.  All ranks run it at once, so host-DRAM and
     PCIe-root contention between ranks shows up here."""
     import ctypes as C
     import torch
     from ccfd_demo_summit_amd.engine import PinnedArray
     L = lib_()
-    L.ccfd_bw_probe.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p]
-    L.ccfd_bw_probe.restype = C.c_double
+    L.ccfd_bw_probe_width.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.ccfd_bw_probe_width.restype = C.c_double
     nbytes = mb << 20
     host = PinnedArray(nbytes // 4, "float32")
     host.array[:] = 1.0
     scratch = torch.empty(1 << 16, dtype=torch.uint8, device="cuda")
     try:
-        one = L.ccfd_bw_probe(C.c_void_p(host.ptr), nbytes, 1, 1, C.c_void_p(scratch.data_ptr()))
-        iters = max(1, int(ms / 1e3 * one * 1e9 / nbytes)) if one > 0 else 1
-        return float(L.ccfd_bw_probe(C.c_void_p(host.ptr), nbytes, 1, iters, C.c_void_p(scratch.data_ptr())))
+        best = 0.0
+        for width in (16, 4):
+            one = L.ccfd_bw_probe_width(C.c_void_p(host.ptr), nbytes, width, 2048, 1, C.c_void_p(scratch.data_ptr()))
+            iters = max(1, int(ms / 2e3 * one * 1e9 / nbytes)) if one > 0 else 1
+            best = max(best, float(L.ccfd_bw_probe_width(C.c_void_p(host.ptr), nbytes, width, 2048, iters,
+                                                         C.c_void_p(scratch.data_ptr()))))
+        return best
     finally:
         host.free()
 
