@@ -367,6 +367,44 @@ __device__ __forceinline__ void wire_handoff(uint2* __restrict__ lds, int lane, 
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// The same tile in 4-byte lanes with an in-register transpose (compile-time
+// CCFD_W64_FETCH_Q4, A/B builds): instruction j reads rows 4j..4j+3 -- 256 contiguous bytes,
+// lane 4Q+t takes dword 4(Q>>2)+t of row 4j+(Q&3) -- and a 4x4 transpose inside every quad
+// (two DPP quad_perm butterflies, no LDS) leaves lane (g, c) holding bytes [16g, 16g+16) of
+// row wire_q4_row(c) = 4(c&3) + (c>>2): the MFMA operand layout with the tile's 16 columns
+// permuted, so the epilogue indexes rows through wire_q4_row.
+__device__ __forceinline__ int wire_q4_row(int c) { return 4 * (c & 3) + (c >> 2); }
+
+__device__ __forceinline__ void wire_issue_q4(const unsigned char* __restrict__ x, int n, int tile, int lane,
+                                              WireRegs& r) {
+  const unsigned char* t = x + (size_t)tile * kTileRows * CCFD_WIRE_ROW_BYTES;
+  const int q = lane >> 2, tq = lane & 3;
+  const int off = 4 * (4 * (q >> 2) + tq);
+  unsigned v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 4 * j + (q & 3);
+    v[j] = tile * kTileRows + row < n ? ld_g(reinterpret_cast<const unsigned*>(t + row * CCFD_WIRE_ROW_BYTES + off))
+                                      : 0u;
+  }
+  r.v = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void wire_q4_transpose(int lane, WireRegs& r) {
+  unsigned a0 = r.v.x, a1 = r.v.y, a2 = r.v.z, a3 = r.v.w;
+  const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0;
+  // quad_perm [1,0,3,2] = 0xB1 (partner t^1), [2,3,0,1] = 0x4E (partner t^2)
+  unsigned s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b0 ? a0 : a1), 0xB1, 0xF, 0xF, false);
+  if (b0) a0 = s; else a1 = s;
+  s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b0 ? a2 : a3), 0xB1, 0xF, 0xF, false);
+  if (b0) a2 = s; else a3 = s;
+  s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b1 ? a0 : a2), 0x4E, 0xF, 0xF, false);
+  if (b1) a0 = s; else a2 = s;
+  s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b1 ? a1 : a3), 0x4E, 0xF, 0xF, false);
+  if (b1) a1 = s; else a3 = s;
+  r.v = make_uint4(a0, a1, a2, a3);
+}
+
 __device__ __forceinline__ void wire_features(const WireRegs& r, int g, float xv[8]) {
   const unsigned w0 = r.v.x, w1 = r.v.y, w2 = r.v.z, w3 = r.v.w;
   xv[0] = __uint_as_float(w0 << 16); xv[1] = __uint_as_float(w0 & 0xffff0000u);

@@ -33,6 +33,10 @@
 #ifndef CCFD_W64_FETCH_X2
 #define CCFD_W64_FETCH_X2 0
 #endif
+// ... or in 4-byte lanes with an in-quad DPP transpose (common.h wire_issue_q4).
+#ifndef CCFD_W64_FETCH_Q4
+#define CCFD_W64_FETCH_Q4 0
+#endif
 
 namespace ccfd {
 
@@ -118,8 +122,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     };
     // per-tile epilogue: outputs, route, counters, amount histogram, compacted fraud list;
     // xr = the tile's raw features (routing rules only)
-    auto finish = [&](float p, float amount, int tile, float (&xr)[8]) __attribute__((always_inline)) {
-      const int row = tile * kTileRows + c;
+    auto finish = [&](float p, float amount, int tile, float (&xr)[8], bool q4 = false) __attribute__((always_inline)) {
+      const int row = tile * kTileRows + (q4 ? wire_q4_row(c) : c);   // q4: permuted tile columns
       const bool valid = row < n;
       bool fr;
       if constexpr (kR) {                               // configurable routing rules (rules.h)
@@ -151,6 +155,7 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
 #pragma unroll
       for (int k = 0; k < T; ++k) {
         if constexpr (CCFD_W64_FETCH_X2) wire_issue2(xw, n, tile0 + 4 * k, lane, r2[k]);
+        else if constexpr (CCFD_W64_FETCH_Q4) wire_issue_q4(xw, n, tile0 + 4 * k, lane, r[k]);
         else wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
       }
 #pragma unroll
@@ -160,6 +165,9 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
         if constexpr (CCFD_W64_FETCH_X2) {
           wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k], r[k]);
           wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k + 1], r[k + 1]);
+        } else if constexpr (CCFD_W64_FETCH_Q4) {
+          wire_q4_transpose(lane, r[k]);
+          wire_q4_transpose(lane, r[k + 1]);
         }
         float pa, pb;
         float xa[8], xb[8];
@@ -175,8 +183,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
           pa = lr_p(la);
           pb = lr_p(lb);
         }
-        finish(pa, __uint_as_float(r[k].v.w), ta, xa);
-        finish(pb, __uint_as_float(r[k + 1].v.w), ta + 4, xb);   // rows >= n: no-op epilogue
+        finish(pa, __uint_as_float(r[k].v.w), ta, xa, CCFD_W64_FETCH_Q4 != 0);
+        finish(pb, __uint_as_float(r[k + 1].v.w), ta + 4, xb, CCFD_W64_FETCH_Q4 != 0);   // rows >= n: no-op epilogue
       }
     };
     if (wire && kTilesPerWave == 2) {
