@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r3t
+O=gpurun_out/${R3T_OUT:-r3t}
 mkdir -p $O
 step() { echo "[r3t] $(date +%T) $*"; }
 step smoke
