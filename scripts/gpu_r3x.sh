@@ -7,6 +7,9 @@ export TMPDIR=/tmp
 O=gpurun_out/r3x
 mkdir -p $O
 step() { echo "[r3x] $(date +%T) $*"; }
+step pytest probes
+timeout -k 10 200 python -u -m pytest tests/test_probes_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_probes.log 2>&1 || { tail -40 $O/pytest_probes.log; exit 1; }
+tail -1 $O/pytest_probes.log
 step deploy topology mlp json 1.2e6 60 s
 timeout -k 30 420 python bench/deploy_topology.py --seconds 60 --producers 3 --rate 1200000 --fmt json \
     --log-dir $O/topo_json --out $O/topo_json.json > $O/topo_json.log 2>&1 || { tail -40 $O/topo_json.log; exit 1; }
