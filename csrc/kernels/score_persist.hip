@@ -37,6 +37,10 @@
 #ifndef CCFD_W64_FETCH_Q4
 #define CCFD_W64_FETCH_Q4 0
 #endif
+// The pipelined (latency-mode) kernel's fetch: 4-byte lanes + DPP transpose when 1.
+#ifndef CCFD_PIPE_FETCH_Q4
+#define CCFD_PIPE_FETCH_Q4 0
+#endif
 
 namespace ccfd {
 
@@ -331,17 +335,26 @@ __global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) 
     const int tile0 = (int)(it % (unsigned long long)C) * (4 * T) + wave;   // wave w: tiles tile0 + 4k
     const unsigned char* xw = reinterpret_cast<const unsigned char*>(d.x);
 #pragma unroll
-    for (int k = 0; k < T; ++k) wire_issue(xw, d.n, tile0 + 4 * k, c, g, r[k]);
+    for (int k = 0; k < T; ++k) {
+      if constexpr (CCFD_PIPE_FETCH_Q4) wire_issue_q4(xw, d.n, tile0 + 4 * k, lane, r[k]);
+      else wire_issue(xw, d.n, tile0 + 4 * k, c, g, r[k]);
+    }
   };
   // score item `it` (rows in r), counters into LDS, outputs to the host, then release + ticket
-  auto score = [&](const ccfd_persist_desc& d, unsigned long long it, const WireRegs (&r)[T]) __attribute__((always_inline)) {
+  auto score = [&](const ccfd_persist_desc& d, unsigned long long it, const WireRegs (&r_in)[T]) __attribute__((always_inline)) {
     const int slot = (int)(d.seq % (unsigned long long)a.ring);
     const int n = d.n;
     const int tile0 = (int)(it % (unsigned long long)C) * (4 * T) + wave;
+    WireRegs r[T];
+#pragma unroll
+    for (int k = 0; k < T; ++k) {
+      r[k] = r_in[k];
+      if constexpr (CCFD_PIPE_FETCH_Q4) wire_q4_transpose(lane, r[k]);
+    }
     unsigned nf_w = 0, nv_w = 0;
     unsigned long long ps_w = 0;
     auto finish = [&](float p, const WireRegs& rr, int tile) __attribute__((always_inline)) {
-      const int row = tile * kTileRows + c;
+      const int row = tile * kTileRows + (CCFD_PIPE_FETCH_Q4 ? wire_q4_row(c) : c);
       const bool valid = row < n;
       bool fr;
       if constexpr (kR) {
