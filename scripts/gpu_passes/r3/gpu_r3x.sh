@@ -23,4 +23,4 @@ timeout -k 10 400 python bench.py --min-timed-s 60 --out $O/bench_60s.json > $O/
 python3 -c "import json; d=json.load(open('$O/bench_60s.json')); print(d['value'], d['p50_latency_us'], d['p99_latency_us'], d['timed_region_s'], d['rows_scored']==d['rows_expected'])"
 du -sh gpurun_out
 step done
-bash scripts/gpu_r3y.sh
+bash scripts/gpu_passes/r3/gpu_r3y.sh
