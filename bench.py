@@ -294,39 +294,68 @@ def _encode_cost(args, dm, rows: int):
             "max_thresholds_per_feature": int(ne.max()), "mean_thresholds_per_feature": round(float(ne.mean()), 2)}
 
 
-def _precision(model, dm, args, dev):
-    """Device kernel vs the fp32 oracle on ``--precision-rows`` rows, through the SAME row
-    format and blob as the headline (W64 wire rows when args.wire == 'w64')."""
-    import torch
+def _kernel_name(model: str, exec_mode: str, wire: str) -> str:
+    """The device kernel a (model, exec mode, row format) engine dispatches (csrc/kernels/)."""
+    if exec_mode == "persistent":
+        return {"mlp": "persist_kernel<MLP> (score_persist.hip)", "lr": "persist_kernel<LR> (score_persist.hip)",
+                "gbdt": "persist_gbdt_g32_kernel (score_gbdt_g32_persist.hip)"}[model]
+    if model == "gbdt":
+        return "score_gbdt_g32_kernel" if wire in ("g32", "g20") else "score_gbdt_kernel"
+    return {"mlp": "score_mlp_wire multi-batch kernel" if wire == "w64" else "score_mlp multi-batch kernel",
+            "lr": "score_lr_wire_multi_kernel" if wire == "w64" else "score_lr_multi_kernel"}[model]
+
+
+def _precision(model, dm, args, dev, exec_mode):
+    """Device vs the fp32 oracle on ``--precision-rows`` rows, scored by the SAME engine
+    configuration as the timed region (exec mode, row format, input / output modes, depth,
+    streams, micro-batch, persistent grid): the rows are replayed from a pinned partition log
+    and every row's proba_1 / route comes back through the engine's scored-record ring (the
+    kernel's own per-row outputs), matched to the oracle by transaction id."""
     from ccfd_demo_summit_amd.data import generate
-    from ccfd_demo_summit_amd.engine.stream_engine import WIRE_ROW_F32, encode_g32, encode_w64
-    from ccfd_demo_summit_amd.ops.kernels import ROW_BYTES, score
-    n = int(args.precision_rows)
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    n = max(args.batch, (int(args.precision_rows) // args.batch) * args.batch)
     X, _ = generate(n, seed=args.seed + 4242)
-    if args.wire == "w64":
-        rows = np.empty((n, WIRE_ROW_F32), np.float32)
-        encode_w64(X, rows.ctypes.data)
-        xt = torch.from_numpy(rows).to(dev)
-    elif args.wire in ("g32", "g20"):
-        rows = np.empty((n, ROW_BYTES[args.wire] // 4), np.float32)
-        encode_g32(X, dm.bins, rows.ctypes.data)
-        xt = torch.from_numpy(rows).to(dev)
+    log = PartitionLog(n, wire=args.wire == "w64", bins=dm.bins)
+    if log.row_format != "f32":
+        log.write_rows(0, X)
     else:
-        xt = torch.from_numpy(X).to(dev)
-    pd, rd = score(dm, xt, threshold=args.threshold)
-    torch.cuda.synchronize(dev)
-    pd = pd.cpu().numpy().astype(np.float64)
-    rd = rd.cpu().numpy()
+        log.feats.array[:] = X
+    log.ids.array[:] = np.arange(n, dtype=np.uint64)
+    eng = StreamEngine(dm, batch=args.batch, depth=args.depth, streams=args.streams,
+                       input_mode=args.input_mode, output_mode=args.output_mode, threshold=args.threshold,
+                       device=dev.index, exec_mode=exec_mode, persist_grid=args.persist_grid,
+                       coalesce=args.coalesce)
+    try:
+        eng.enable_scored(n)
+        eng.add_log(0, log)
+        eng.pump(n // args.batch, drain=True)
+        rec = eng.drain_scored()
+        dropped = eng.scored_dropped()
+    finally:
+        eng.close()
+        log.free()
+    ids = rec["tx_id"].astype(np.int64)
+    if len(rec) != n or dropped or not np.array_equal(np.sort(ids), np.arange(n)):
+        raise RuntimeError(f"precision run: {len(rec)} scored records for {n} rows (dropped {dropped})")
+    pd = np.empty(n, np.float64)
+    rd = np.empty(n, bool)
+    pd[ids] = rec["proba"]
+    rd[ids] = rec["route"] != 0
     p32 = model.predict_proba(X).astype(np.float64)
     r32 = (p32 >= args.threshold)
     dp = np.abs(pd - p32)
-    flips = (rd.astype(bool) != r32)
+    flips = (rd != r32)
     outside = np.abs(p32 - args.threshold) > 1e-2
     return {"rows": n, "oracle": "fp32 numpy predict_proba on the unquantised f32 rows",
-            "row_format": args.wire, "max_abs_dp": float(dp.max()), "mean_abs_dp": float(dp.mean()),
+            "kernel": _kernel_name(args.model, exec_mode, args.wire), "exec_mode": exec_mode,
+            "row_format": args.wire, "input_mode": args.input_mode, "output_mode": args.output_mode,
+            "depth": args.depth, "micro_batch": args.batch,
+            "path": "StreamEngine.pump over a pinned partition log -> scored-record ring (same engine "
+                    "configuration as the timed region)",
+            "max_abs_dp": float(dp.max()), "mean_abs_dp": float(dp.mean()),
             "route_flips": int(flips.sum()), "route_flip_rate": float(flips.mean()),
             "route_flips_outside_1e-2_band": int((flips & outside).sum()),
-            "fraud_routed_fp32": int(r32.sum()), "fraud_routed_device": int(rd.astype(bool).sum())}
+            "fraud_routed_fp32": int(r32.sum()), "fraud_routed_device": int(rd.sum())}
 
 
 def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
@@ -630,7 +659,7 @@ def main(argv=None):
     precision = f32_rate = encode = None
     if ctx.rank == 0:
         if args.precision_rows > 0:
-            precision = _precision(model, dm, args, dev)
+            precision = _precision(model, dm, args, dev, exec_mode)
         if args.encode_probe_rows > 0:
             encode = _encode_cost(args, dm, args.encode_probe_rows)
         if args.wire in ("w64", "g32", "g20") and not args.no_f32_probe:
@@ -717,6 +746,7 @@ def main(argv=None):
         "host_encode": encode,
         "f32_wire_tx_s": None if f32_rate is None else round(f32_rate, 1),
         "precision_vs_fp32": precision,
+        "timed_kernel": _kernel_name(args.model, exec_mode, args.wire),
     }
     if total_rows != expected and ctx.rank == 0:
         print(f"[bench] WARNING: counted {total_rows} rows, expected {expected}", file=sys.stderr)

@@ -14,7 +14,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..ops._lib import (BATCH_TRACE_DTYPE, BIN_FORMATS, FLAGGED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig,
+from ..ops._lib import (BATCH_TRACE_DTYPE, BIN_FORMATS, FLAGGED_DTYPE, SCORED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig,
                         EngineStats, Flagged, check, last_error, lib)
 from ..ops.kernels import ROW_BYTES, DeviceModel
 
@@ -376,6 +376,28 @@ class StreamEngine:
             if k < 65536:
                 break
         return np.concatenate(out) if out else np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
+
+    def enable_scored(self, capacity: int = 1 << 20) -> None:
+        """Opt in to a per-row scored-record ring of ``capacity`` rows (0 = off): every
+        completed row -- fraud- and standard-routed -- with the kernel's proba_1 and route
+        (``drain_scored``).  Streaming ``run()`` holds completed batches while it is full."""
+        check(lib().ccfd_engine_scored_enable(C.c_void_p(self.h), int(capacity)), "ccfd_engine_scored_enable")
+        self._scored_cap = int(capacity)
+
+    def drain_scored(self, max_records: int = 1 << 30) -> np.ndarray:
+        """Scored records (SCORED_DTYPE) in completion order, oldest first."""
+        cap = getattr(self, "_scored_cap", 0)
+        if cap <= 0:
+            return np.zeros(0, dtype=np.dtype(SCORED_DTYPE))
+        out = np.empty(min(cap, max_records), dtype=np.dtype(SCORED_DTYPE))
+        k = lib().ccfd_engine_drain_scored(C.c_void_p(self.h), out.ctypes.data, out.size)
+        if k < 0:
+            raise RuntimeError(f"ccfd_engine_drain_scored failed: {last_error()}")
+        return out[:k]
+
+    def scored_dropped(self) -> int:
+        """Rows that completed while the scored ring was full (pump() / drain paths only)."""
+        return int(lib().ccfd_engine_scored_dropped(C.c_void_p(self.h)))
 
     # ------------------------------------------------------------------ ring (streaming) mode
     def set_ring(self, partition: int, capacity: int) -> PartitionLog:

@@ -70,6 +70,10 @@ class EngineStats(C.Structure):
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
                  ("partition", "<u4")]
 
+# ccfd_scored (ccfd_abi.h): one record per scored row (opt-in scored ring)
+SCORED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
+                ("partition", "<u2"), ("route", "u1"), ("pad", "u1")]
+
 # ccfd_batch_trace (ccfd_abi.h): per-micro-batch stage timestamps
 BATCH_TRACE_DTYPE = [("seq", "<i8"), ("partition", "<i4"), ("rows", "<i4"), ("t_arrival", "<i8"),
                      ("t_submit", "<i8"), ("t_landed", "<i8"), ("t_complete", "<i8"), ("dev_start", "<i8"),
@@ -117,6 +121,11 @@ def lib() -> C.CDLL:
         L.ccfd_engine_set_blob.argtypes = [C.c_void_p, C.c_void_p]
         L.ccfd_engine_drain_flagged.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.ccfd_engine_drain_flagged.restype = C.c_int64
+        L.ccfd_engine_scored_enable.argtypes = [C.c_void_p, C.c_int64]
+        L.ccfd_engine_drain_scored.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.ccfd_engine_drain_scored.restype = C.c_int64
+        L.ccfd_engine_scored_dropped.argtypes = [C.c_void_p]
+        L.ccfd_engine_scored_dropped.restype = C.c_int64
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]
         L.ccfd_engine_cursor.restype = C.c_int64
         L.ccfd_engine_reset_stats.argtypes = [C.c_void_p]

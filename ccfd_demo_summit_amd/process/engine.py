@@ -112,6 +112,12 @@ class ProcessEngine:
         self._by_tx: Dict[Any, int] = {}
         self._tx_order = collections.deque()
         self.duplicates = 0
+        # standard starts are idempotent per transaction id too (a re-delivered hand-off batch
+        # must not start a second standard process): tx id -> instance id over a bounded window
+        self.standard_dedupe_window = 1 << 20
+        self._std_by_tx: Dict[Any, int] = {}
+        self._std_order: collections.deque = collections.deque()
+        self.standard_duplicates = 0
 
     @classmethod
     def from_config(cls, kie_cfg, **kw) -> "ProcessEngine":
@@ -134,6 +140,7 @@ class ProcessEngine:
     def recover(cls, journal_path: str, **kw) -> "ProcessEngine":
         """Rebuild from the journal (last record per instance wins), then keep appending."""
         last: Dict[int, dict] = {}
+        std_batches: List[dict] = []
         if os.path.exists(journal_path):
             with open(journal_path) as f:
                 for line in f:
@@ -143,7 +150,10 @@ class ProcessEngine:
                             rec = json.loads(line)
                         except json.JSONDecodeError:
                             continue        # the torn last line of a killed process
-                        last[rec["instance"]["id"]] = rec
+                        if "standard" in rec:
+                            std_batches.append(rec["standard"])
+                        else:
+                            last[rec["instance"]["id"]] = rec
         if os.path.exists(journal_path) and os.path.getsize(journal_path) > 0:
             with open(journal_path, "rb+") as f:            # end a torn last line, so the
                 f.seek(-1, os.SEEK_END)                      # next record starts on its own
@@ -167,6 +177,20 @@ class ProcessEngine:
                 max_task = max(max_task, t.id)
             if inst.state == State.WAITING_CUSTOMER and inst.timer_due is not None:
                 heapq.heappush(eng._timers, (inst.timer_due, iid))
+        for b in std_batches:                   # batched standard starts (start_standard_many)
+            for iid, tx in zip(b["id"], b["transaction_id"]):
+                max_id = max(max_id, iid)
+                eng.standard_count += 1
+                eng.outcome_counts[Outcome.STANDARD.value] += 1
+                if tx is not None:
+                    eng._std_remember(tx, iid)
+        for iid, rec in last.items():
+            if rec["instance"]["process_id"] == cls.STANDARD:
+                eng.standard_count += 1
+                eng.outcome_counts[Outcome.STANDARD.value] += 1
+                tx = rec["instance"]["variables"].get("transaction_id")
+                if tx is not None:
+                    eng._std_remember(tx, iid)
         eng._ids = itertools.count(max_id + 1)
         eng._task_ids = itertools.count(max_task + 1)
         return eng
@@ -177,9 +201,23 @@ class ProcessEngine:
             return self.start_standard(variables)
         return self.start_fraud(variables)
 
+    def _std_remember(self, tx, iid: int) -> None:
+        self._std_by_tx[tx] = iid
+        self._std_order.append(tx)
+        if len(self._std_order) > self.standard_dedupe_window:
+            self._std_by_tx.pop(self._std_order.popleft(), None)
+
     def start_standard(self, variables: Dict[str, Any]) -> int:
+        """Standard process (README.md:552): completes at once as STANDARD.  Idempotent per
+        transaction id, like fraud starts."""
+        txid = variables.get("transaction_id", variables.get("tx_id"))
         with self._lock:
+            if txid is not None and txid in self._std_by_tx:
+                self.standard_duplicates += 1
+                return self._std_by_tx[txid]
             iid = next(self._ids)
+            if txid is not None:
+                self._std_remember(txid, iid)
             now = self.clock()
             inst = ProcessInstance(iid, self.STANDARD, dict(variables), State.COMPLETED,
                                    Outcome.STANDARD.value, now, now, history=["start", "approve"])
@@ -188,6 +226,42 @@ class ProcessEngine:
             self._remember_completed(inst)
             self._log(inst)
             return iid
+
+    def start_standard_many(self, items) -> List[int]:
+        """Standard processes for a whole hand-off batch (the engine's standard-routed rows of a
+        scoring step).  ``items``: a list of variable dicts, or columns ``{"transaction_id":
+        [...], "customer_id": [...], "amount": [...], "proba": [...]}`` (the compact form the
+        router sends at ~1e5 standard rows a second).  Idempotent per transaction id; the batch
+        is journaled as ONE record (ids + columns), which ``recover()`` replays."""
+        cols = columns_of(items)
+        txs = cols.get("transaction_id") or cols.get("tx_id")
+        n = _ncols(cols)
+        out: List[int] = []
+        new_pos: List[int] = []
+        with self._lock:
+            for k in range(n):
+                tx = txs[k] if txs is not None else None
+                if tx is not None:
+                    old = self._std_by_tx.get(tx)
+                    if old is not None:
+                        self.standard_duplicates += 1
+                        out.append(old)
+                        continue
+                iid = next(self._ids)
+                if tx is not None:
+                    self._std_remember(tx, iid)
+                out.append(iid)
+                new_pos.append(k)
+            self.standard_count += len(new_pos)
+            self.outcome_counts[Outcome.STANDARD.value] += len(new_pos)
+            if self._journal is not None and new_pos:
+                rec = {"id": [out[k] for k in new_pos]}
+                for key, vals in cols.items():
+                    rec[key] = [vals[k] for k in new_pos]
+                if "transaction_id" not in rec:
+                    rec["transaction_id"] = [None] * len(new_pos)
+                self._journal.write(json.dumps({"standard": rec}, default=float) + "\n")
+        return out
 
     def start_fraud(self, variables: Dict[str, Any]) -> int:
         """Idempotent per transaction id: at-least-once delivery (a re-scored transaction
@@ -340,6 +414,39 @@ class ProcessEngine:
         if self._journal:
             self._journal.close()
             self._journal = None
+
+
+def columns_of(items) -> Dict[str, list]:
+    """Variables of many process starts as columns: accepts a list of dicts or a dict of
+    equally long lists (``tx_id`` is accepted for ``transaction_id``)."""
+    if isinstance(items, dict):
+        cols = {k: list(v) for k, v in items.items()}
+    else:
+        keys: List[str] = []
+        for it in items:
+            for k in it:
+                if k not in keys:
+                    keys.append(k)
+        cols = {k: [it.get(k) for it in items] for k in keys}
+    if "transaction_id" not in cols and "tx_id" in cols:
+        cols["transaction_id"] = cols.pop("tx_id")
+    lens = {len(v) for v in cols.values()}
+    if len(lens) > 1:
+        raise ValueError("columns of different lengths")
+    return cols
+
+
+def _ncols(cols: Dict[str, list]) -> int:
+    return len(next(iter(cols.values()))) if cols else 0
+
+
+def rows_of(items) -> List[Dict[str, Any]]:
+    """The inverse of columns_of: a list of variable dicts."""
+    if not isinstance(items, dict):
+        return list(items)
+    cols = columns_of(items)
+    keys = list(cols)
+    return [{k: cols[k][i] for k in keys} for i in range(_ncols(cols))]
 
 
 def _truthy(payload: Any) -> bool:

@@ -22,7 +22,7 @@ import requests
 from aiohttp import web
 
 from ..metrics.exporter import CONTENT_TYPE
-from .engine import ProcessEngine
+from .engine import ProcessEngine, rows_of
 
 BASE = "/services/rest/server"
 
@@ -100,13 +100,20 @@ class KieServer:
             return bad
         pid = request.match_info["p"]
         items = json.loads(await request.read() or b"[]")
-        if not isinstance(items, list):
-            return web.json_response({"type": "FAILURE", "msg": "expected a JSON list"}, status=400)
-        if pid == self.standard_pid:
-            ids = [self.engine.start_standard(v) for v in items]
-        elif pid == self.fraud_pid:
-            ids = [self.engine.start_fraud(v) for v in items]
-        else:
+        # a JSON list of variable objects, or columns {"transaction_id": [...], ...} (the
+        # compact form the router uses for standard-routed rows)
+        if not isinstance(items, (list, dict)):
+            return web.json_response({"type": "FAILURE", "msg": "expected a JSON list or columns"}, status=400)
+        try:
+            if pid == self.standard_pid:
+                ids = self.engine.start_standard_many(items)
+            elif pid == self.fraud_pid:
+                ids = [self.engine.start_fraud(v) for v in rows_of(items)]
+            else:
+                ids = None
+        except (ValueError, TypeError, AttributeError) as e:
+            return web.json_response({"type": "FAILURE", "msg": f"bad batch: {e}"}, status=400)
+        if ids is None:
             return web.json_response({"type": "FAILURE", "msg": f"Could not find process definition {pid}"},
                                      status=404)
         return web.json_response(ids, status=201)
@@ -171,7 +178,8 @@ class KieServer:
         with e._lock:
             fraud = sum(1 for i in e.instances.values() if i.process_id == e.FRAUD)
             body = {"fraud_instances_retained": fraud, "fraud_started": len(e._by_tx), "duplicates": e.duplicates,
-                    "standard_started": e.standard_count, "active": sum(1 for i in e.instances.values()
+                    "standard_started": e.standard_count, "standard_duplicates": e.standard_duplicates,
+                    "active": sum(1 for i in e.instances.values()
                                                                         if i.state.value != "completed"),
                     "outcomes": dict(e.outcome_counts), "next_instance_id": None}
         return web.json_response(body)
@@ -235,6 +243,17 @@ class KieClient:
 
     def start_standard(self, variables) -> int:
         return self._start(self.standard_pid, variables)
+
+    def start_standard_many(self, items) -> list:
+        """One request for many standard instances (``/instances/batch`` extension); ``items``
+        may be columns ``{"transaction_id": [...], "customer_id": [...], "amount": [...],
+        "proba": [...]}`` -- ~4x smaller and faster to encode than a list of objects."""
+        if not items or (isinstance(items, dict) and not any(len(v) for v in items.values())):
+            return []
+        r = self.s.post(f"{self.base}/containers/{self.c}/processes/{self.standard_pid}/instances/batch",
+                        data=json.dumps(items), headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        r.raise_for_status()
+        return [int(x) for x in r.json()]
 
     def signal_many(self, items) -> list:
         """Many signals in one request (``signal/batch`` extension): items of

@@ -143,6 +143,11 @@ class Engine {
   uint64_t ring_head = 0, ring_tail = 0;
   std::mutex ring_mu;
   uint64_t dropped = 0;
+  // opt-in scored-record ring (every row; ccfd_engine_scored_enable), same producer/consumer
+  std::vector<ccfd_scored> sring;
+  uint64_t s_head = 0, s_tail = 0, s_dropped = 0;
+  std::mutex s_mu;
+  std::atomic<bool> scored_on{false};
   // per-batch latency: O(1) memory however long the engine runs (a long-lived service
   // scores ~2e5 batches/s): count/sum/max, a 0.25-us linear histogram up to 4 ms for the
   // reported quantiles, and the 4-buckets-per-octave log histogram merged over ranks (X3)
@@ -627,6 +632,44 @@ class Engine {
     ++ring_tail;
   }
 
+  uint64_t scored_room() {
+    std::lock_guard<std::mutex> lk(s_mu);
+    return sring.size() - (s_tail - s_head);
+  }
+
+  // every row of the completed batch `s` -> the scored ring (route from the kernel's route
+  // byte, proba_1 from its output slot; both written by the epilogue before the completion
+  // record); rows that do not fit are counted, never overwrite unread records
+  void push_scored(const Slot& s) {
+    const Partition& P = *parts[s.part];
+    std::lock_guard<std::mutex> lk(s_mu);
+    const uint64_t cap = sring.size();
+    const int n = s.rows;
+    const uint64_t room = cap - (s_tail - s_head);
+    const int take = (int)std::min<uint64_t>(room, (uint64_t)n);
+    s_dropped += (uint64_t)(n - take);
+    for (int i = 0; i < take; ++i) {
+      const int64_t row = s.start + i;
+      ccfd_scored& r = sring[s_tail % cap];
+      r.tx_id = P.ids ? P.ids[row] : (uint64_t)row;
+      r.customer = P.cust ? P.cust[row] : 0u;
+      r.proba = s.h_proba[i];
+      r.amount = amount_f >= 0 ? P.feats[row * rowf + amount_f] : (P.amount ? P.amount[row] : __builtin_nanf(""));
+      r.partition = (uint16_t)s.part;
+      r.route = s.h_route[i] ? 1 : 0;
+      r.pad = 0;
+      ++s_tail;
+    }
+  }
+
+  int64_t drain_scored(ccfd_scored* out, int64_t max) {
+    std::lock_guard<std::mutex> lk(s_mu);
+    const uint64_t cap = sring.size();
+    int64_t k = 0;
+    while (s_head < s_tail && k < max) out[k++] = sring[s_head++ % cap];
+    return k;
+  }
+
   bool is_done(const Slot& s) {
     if (s.use_flag) return s.done_ptr[0] == s.expect;
     return hipEventQuery(s.ev) == hipSuccess;
@@ -711,6 +754,7 @@ class Engine {
       for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
       if (nf) push_flagged(s);
     }
+    if (scored_on.load(std::memory_order_relaxed)) push_scored(s);
     if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
     if (trace_on.load(std::memory_order_relaxed)) record_trace(s, t_landed, nf);
     Partition& P = *parts[s.part];
@@ -1076,6 +1120,9 @@ class Engine {
         Slot& s = slots[(seq + k) % D];
         if (!s.busy) continue;
         if (!is_done(s)) break;
+        // scored ring full: leave the batch (and its ring rows) in place until the consumer
+        // drains -- back-pressure reaches ingest instead of losing standard-route records
+        if (scored_on.load(std::memory_order_relaxed) && scored_room() < (uint64_t)s.rows) break;
         int rc = complete(s, st);
         if (rc) return rc;
         progress = true;
@@ -1197,6 +1244,29 @@ int ccfd_engine_set_blob(void* eng, const void* blob) {
 
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max) {
   return static_cast<Engine*>(eng)->drain_flagged(out, max);
+}
+
+int ccfd_engine_scored_enable(void* eng, int64_t capacity) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!e || capacity < 0 || capacity > (int64_t(1) << 28)) { set_error("bad scored-ring capacity"); return -1; }
+  int rc = e->drain_all();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(e->s_mu);
+  e->sring.assign((size_t)capacity, ccfd_scored{});
+  e->s_head = e->s_tail = e->s_dropped = 0;
+  e->scored_on.store(capacity > 0, std::memory_order_relaxed);
+  return 0;
+}
+
+int64_t ccfd_engine_drain_scored(void* eng, ccfd_scored* out, int64_t max) {
+  if (!eng || (!out && max > 0) || max < 0) return -1;
+  return static_cast<Engine*>(eng)->drain_scored(out, max);
+}
+
+int64_t ccfd_engine_scored_dropped(void* eng) {
+  auto* e = static_cast<Engine*>(eng);
+  std::lock_guard<std::mutex> lk(e->s_mu);
+  return (int64_t)e->s_dropped;
 }
 
 int64_t ccfd_engine_cursor(void* eng, int partition) {

@@ -237,6 +237,19 @@ typedef struct ccfd_flagged {
   uint32_t partition;
 } ccfd_flagged;   // 24 bytes
 
+// Opt-in per-row scored record (ccfd_engine_scored_enable): every completed row, fraud- and
+// standard-routed, with its proba_1 and route -- what the reference router needs to start a
+// standard OR a fraud process per transaction (README.md:549-552).
+typedef struct ccfd_scored {
+  uint64_t tx_id;
+  uint32_t customer;
+  float proba;
+  float amount;
+  uint16_t partition;
+  uint8_t route;               // 1 = fraud (the kernel's route byte), 0 = standard
+  uint8_t pad;
+} ccfd_scored;    // 24 bytes
+
 typedef struct ccfd_engine_stats {
   uint64_t batches, rows, fraud_rows, flagged_dropped;
   double wall_s;
@@ -300,6 +313,15 @@ int ccfd_engine_set_blob(void* eng, const void* blob);
 // Drain up to `max` flagged records (fraud route) into `out`; returns count.
 int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max);
 int64_t ccfd_engine_cursor(void* eng, int partition);
+// Scored-record ring of `capacity` rows (0 = off, the default).  Records are assembled when a
+// micro-batch completes, from the per-row proba_1 / route the kernel's epilogue wrote into the
+// batch's pinned output slots (the same epilogue that compacts the flag list) and the log's
+// id / customer / Amount columns.  ccfd_engine_run() does not retire a batch while the ring
+// lacks room for it (back-pressure to ingest, nothing is lost); pump() / drain paths count
+// rows that do not fit in ccfd_engine_scored_dropped().
+int ccfd_engine_scored_enable(void* eng, int64_t capacity);
+int64_t ccfd_engine_drain_scored(void* eng, ccfd_scored* out, int64_t max);
+int64_t ccfd_engine_scored_dropped(void* eng);
 // Watchdog diagnostics: submitted, completed, persistent posted (-1), kernel resident, in flight.
 int ccfd_engine_progress(void* eng, int64_t* out5);
 // Watchdog exit path: stop a resident persistent kernel, wait <= timeout_ms for it to drain.

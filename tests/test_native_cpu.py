@@ -17,11 +17,11 @@ def L():
 
 
 def test_abi_struct_sizes(L, tmp_path):
-    from ccfd_demo_summit_amd.ops._lib import EngineConfig, EngineStats, Flagged, ScoreArgs
+    from ccfd_demo_summit_amd.ops._lib import SCORED_DTYPE, EngineConfig, EngineStats, Flagged, ScoreArgs
     src = tmp_path / "sz.c"
-    src.write_text('#include <stdio.h>\n#include "ccfd_abi.h"\nint main(){printf("%zu %zu %zu %zu",'
+    src.write_text('#include <stdio.h>\n#include "ccfd_abi.h"\nint main(){printf("%zu %zu %zu %zu %zu",'
                    'sizeof(ccfd_score_args),sizeof(ccfd_engine_config),sizeof(ccfd_flagged),'
-                   'sizeof(ccfd_engine_stats));}\n')
+                   'sizeof(ccfd_engine_stats),sizeof(ccfd_scored));}\n')
     from ccfd_demo_summit_amd.ops.build import CSRC
     exe = tmp_path / "sz"
     r = subprocess.run(["gcc", str(src), "-I", str(CSRC / "include"), "-o", str(exe)], capture_output=True)
@@ -29,7 +29,7 @@ def test_abi_struct_sizes(L, tmp_path):
         pytest.skip("no C compiler")
     out = subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()
     assert [int(v) for v in out] == [C.sizeof(ScoreArgs), C.sizeof(EngineConfig), C.sizeof(Flagged),
-                                     C.sizeof(EngineStats)]
+                                     C.sizeof(EngineStats), np.dtype(SCORED_DTYPE).itemsize]
 
 
 def _parse(L, msgs):
