@@ -63,6 +63,9 @@ class RouterConfig:
     port: int = 8091                                          # README.md:503-506
     rules: str = ""                  # ROUTER_RULES: routing rule file or inline rules ("when ... then
                                      # fraud; otherwise standard"); "" = the reference threshold rule
+    standard_mode: str = "count"     # standard-routed transactions: "count" (counters only -- the
+                                     # default at 1e9 tx/s) | "process": start a standard process per
+                                     # transaction, like the reference router (README.md:552)
 
 
 @dataclass
@@ -92,6 +95,9 @@ class EngineConfig:
     persist_items: str = "auto"      # persistent MLP on W64 rows: claimed (throughput, = auto) | pipelined
     handoff_capacity: int = 1 << 21  # fraud starts queued for KIE before scoring pauses (back-pressure)
     handoff_workers: int = 2         # pooled HTTP workers of the KIE hand-off (router/handoff.py)
+    handoff_dlq: str = ""            # dead-letter journal of requests KIE refused (4xx); "" = no DLQ:
+                                     # a refused request is held and retried, never acked unsent
+    scored_capacity: int = 1 << 20   # standard_mode=process: per-row scored-record ring (rows)
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches
     reduce_period_ms: float = 10.0   # X2 counter all-reduce period
     gbdt_trees: int = 100
@@ -127,6 +133,7 @@ ENV_MAP = {
     "CONFIDENCE_THRESHOLD": ("kie", "confidence_threshold", float),
     "FRAUD_THRESHOLD": ("router", "fraud_threshold", float),
     "ROUTER_RULES": ("router", "rules", str),
+    "ROUTER_STANDARD_MODE": ("router", "standard_mode", str),
     # framework-specific keys
     "CCFD_MODEL": ("engine", "model", str),
     "CCFD_BATCH": ("engine", "batch", int),
@@ -139,6 +146,7 @@ ENV_MAP = {
     "CCFD_EXEC_MODE": ("engine", "exec_mode", str),
     "CCFD_PERSIST_ITEMS": ("engine", "persist_items", str),
     "CCFD_HANDOFF_CAPACITY": ("engine", "handoff_capacity", int),
+    "CCFD_HANDOFF_DLQ": ("engine", "handoff_dlq", str),
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),
     "CCFD_KAFKA_PARTITIONS": ("kafka", "partitions", int),
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),

@@ -18,6 +18,7 @@ services:
                committed counts) + membership generations whose process group carries the
                global X2 counters; a supervised restart rejoins   (--store, --rank, --world)
   supervise    restart-on-crash supervisor:  supervise [--max-restarts N] -- <cmd...>
+  dlq-replay   re-deliver the KIE hand-off dead-letter journal (--dlq PATH) to KIE_SERVER_URL
   operator     FraudDetection CR -> Kubernetes manifests (--render) or a local reconcile
                loop of supervised services (--local); accepts the reference's OpenDataHub CR
 
@@ -77,17 +78,31 @@ def _metrics_app(expose):
 
 
 def _serve_in_thread(app, host, port):
+    """Serve ``app`` on a daemon thread's event loop.  Binds before returning: a port that
+    is taken raises OSError here instead of failing silently inside the thread."""
     from aiohttp import web
+    ready = threading.Event()
+    err = []
 
     def run():
         loop = asyncio.new_event_loop()
         asyncio.set_event_loop(loop)
         runner = web.AppRunner(app)
-        loop.run_until_complete(runner.setup())
-        loop.run_until_complete(web.TCPSite(runner, host, port).start())
+        try:
+            loop.run_until_complete(runner.setup())
+            loop.run_until_complete(web.TCPSite(runner, host, port).start())
+        except BaseException as e:          # noqa: BLE001 -- handed to the caller
+            err.append(e)
+            ready.set()
+            return
+        ready.set()
         loop.run_forever()
     t = threading.Thread(target=run, daemon=True)
     t.start()
+    if not ready.wait(60):
+        raise TimeoutError(f"server on {host}:{port} did not start")
+    if err:
+        raise OSError(f"cannot serve on {host}:{port}: {err[0]!r}") from err[0]
     return t
 
 
@@ -232,6 +247,12 @@ def cmd_router(a, cfg):
         notif.commit()
 
 
+def _rank_path(path: str, rank: int) -> str:
+    """A per-rank file next to ``path`` (ranks never share a journal): x.jsonl -> x.rank3.jsonl."""
+    root, ext = os.path.splitext(path)
+    return f"{root}.rank{rank}{ext or '.jsonl'}"
+
+
 def cmd_engine(a, cfg):
     import numpy as np
     import torch
@@ -261,8 +282,12 @@ def cmd_engine(a, cfg):
                     cfg.kie.signal_name, timeout_s=cfg.seldon.timeout_ms / 1e3, pool_size=cfg.seldon.pool_size)
     # fraud starts and response signals go through a bounded async queue with pooled,
     # retried HTTP: a slow or absent KIE never stalls scoring, commits or X2 (router/handoff.py)
-    handoff = KieHandoff(kie, capacity=cfg.engine.handoff_capacity, workers=cfg.engine.handoff_workers)
-    router = Router(rules, kie, hub.router, handoff=handoff)
+    dlq = None
+    if cfg.engine.handoff_dlq:
+        from ..router.handoff import DeadLetterQueue
+        dlq = DeadLetterQueue(_rank_path(cfg.engine.handoff_dlq, ctx.rank))
+    handoff = KieHandoff(kie, capacity=cfg.engine.handoff_capacity, workers=cfg.engine.handoff_workers, dlq=dlq)
+    router = Router(rules, kie, hub.router, standard_mode=cfg.router.standard_mode, handoff=handoff)
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
         depth=cfg.engine.depth, streams=cfg.engine.streams, input_mode=cfg.engine.input_mode,
@@ -270,6 +295,7 @@ def cmd_engine(a, cfg):
         flush_us=cfg.engine.max_delay_us, reduce_period_ms=cfg.engine.reduce_period_ms,
         threshold=cfg.router.fraud_threshold, coalesce=cfg.engine.coalesce,
         ingest_threads=cfg.engine.ingest_threads, persist_items=cfg.engine.persist_items,
+        standard_mode=cfg.router.standard_mode, scored_capacity=cfg.engine.scored_capacity,
         model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     # the process's node-local rank (torchrun LOCAL_RANK) -- not the device index, which a
@@ -301,13 +327,23 @@ def cmd_engine(a, cfg):
     def _term(*_a):
         raise SystemExit(0)
     signal.signal(signal.SIGTERM, _term)
+    resp_wait = None                  # hand-off seq carrying the last polled responses' signals
     try:
         while True:
             svc.step()           # never raises on a KIE outage: the hand-off retries, commits wait
             if resp is not None:
-                for r in resp.poll(max_records=10_000):
-                    router.on_response(r.value)
-                resp.commit()
+                # customer responses: their offsets are committed only once the signals they
+                # became are acknowledged by KIE (like the fraud starts' offsets), so a crash
+                # with a KIE outage in flight re-delivers them instead of losing them
+                if resp_wait is None or handoff.acked(resp_wait):
+                    if resp_wait is not None:
+                        resp.commit()
+                        resp_wait = None
+                    recs = resp.poll(max_records=10_000)
+                    for r in recs:
+                        router.on_response(r.value)
+                    if recs:
+                        resp_wait = router.last_handoff_seq
                 for r in notif.poll(max_records=10_000):
                     router.on_notification_sent(r.value)
                 notif.commit()
@@ -456,6 +492,24 @@ def cmd_operator(a, cfg):
         op.run(a.cr, until=(lambda: time.time() >= t_end) if a.seconds > 0 else None)
 
 
+def cmd_dlq_replay(a, cfg):
+    """Re-deliver the hand-off dead-letter journal (router/handoff.py DeadLetterQueue) to
+    KIE_SERVER_URL: every pending entry exactly once; prints a JSON summary."""
+    from ..process.kie_server import KieClient
+    from ..router.handoff import DeadLetterQueue
+    path = a.dlq or cfg.engine.handoff_dlq
+    if not path:
+        raise SystemExit("dlq-replay: --dlq PATH (or CCFD_HANDOFF_DLQ) is required")
+    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
+                    cfg.kie.signal_name, timeout_s=cfg.seldon.timeout_ms / 1e3)
+    q = DeadLetterQueue(path)
+    res = q.replay(kie)
+    q.close()
+    print(json.dumps(dict(res, dlq=path)), flush=True)
+    if res["failed"]:
+        sys.exit(1)
+
+
 def cmd_supervise(a, cfg):
     from .supervisor import supervise
     sys.exit(supervise(a.cmd, max_restarts=a.max_restarts, backoff_s=a.backoff))
@@ -473,7 +527,7 @@ def parse_args(argv=None) -> argparse.Namespace:
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
                                         "engine", "producer", "demo", "store", "elastic", "supervise",
-                                        "operator"])
+                                        "operator", "dlq-replay"])
     ap.add_argument("--config", default=None)
     ap.add_argument("--nodes", type=int, default=1, help="kafka-lite: broker listeners (port, port+1, ...)")
     ap.add_argument("--advertise", default=None, help="kafka-lite: broker host name clients are given")
@@ -494,6 +548,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--journal", default=None, help="KIE: append-only process journal for recovery")
+    ap.add_argument("--dlq", default=None, help="dlq-replay: the hand-off dead-letter journal to re-deliver")
     ap.add_argument("--remote-prediction", action="store_true", help="KIE: call the user-task model over HTTP")
     ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
     ap.add_argument("--batch", type=int, default=4096)

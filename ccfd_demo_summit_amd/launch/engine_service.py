@@ -69,6 +69,9 @@ class EngineServiceConfig:
                                      # router / process loop
     model_watch: Optional[str] = None   # rank 0: hot-swap when this safetensors file changes
     handoff_hold_low: float = 0.5    # a held (full) hand-off queue resumes scoring below this fill
+    standard_mode: str = "count"     # "process": every standard-routed row is handed to the router
+                                     # (scored-record ring) to start a standard process
+    scored_capacity: int = 1 << 20   # scored-record ring rows (standard_mode="process")
 
 
 def rule_safe_row_format(model_kind: str, fmt: str, rules) -> Tuple[str, str]:
@@ -127,6 +130,13 @@ class EngineService:
                                    input_mode=cfg.input_mode, output_mode=cfg.output_mode, threshold=threshold,
                                    device=ctx.device.index, exec_mode=self.exec_mode, coalesce=cfg.coalesce,
                                    rules=self.device_rules, persist_items=cfg.persist_items)
+        if cfg.standard_mode not in ("count", "process"):
+            raise ValueError("standard_mode must be 'count' or 'process'")
+        self.standard_mode = cfg.standard_mode
+        if cfg.standard_mode == "process":
+            # every completed row comes back with the kernel's proba / route; run() holds a
+            # batch while the ring is full (back-pressure, never loss)
+            self.engine.enable_scored(max(cfg.scored_capacity, 4 * cfg.batch))
         n_parts = broker.partitions(cfg.topic)
         self.partitions = partitions if partitions is not None else assign_partitions(n_parts, ctx.rank, ctx.world)
         for p in self.partitions:
@@ -173,6 +183,7 @@ class EngineService:
         self._stat_lock = threading.Lock()
         self._rows_new = 0
         self._flagged_new: List[np.ndarray] = []
+        self._standard_new: List[np.ndarray] = []
         self._lat_cum = np.zeros(256, np.int64)
         self._tasks: "queue.SimpleQueue" = queue.SimpleQueue()
         self._score_err: Optional[BaseException] = None
@@ -297,11 +308,17 @@ class EngineService:
         # snapshot follows the drain, so it never covers a row whose fraud record is not yet
         # in _flagged_new (only this thread completes batches)
         flagged = self.engine.drain_flagged() if st.rows else None
+        standard = None
+        if self.standard_mode == "process" and st.rows:
+            rec = self.engine.drain_scored()
+            standard = rec[rec["route"] == 0]
         snap = self._snapshot_commits() if st.rows else None
         with self._stat_lock:
             self._rows_new += int(st.rows)
             if flagged is not None and len(flagged):
                 self._flagged_new.append(flagged)
+            if standard is not None and len(standard):
+                self._standard_new.append(standard)
             if snap:
                 for p, v in snap.items():
                     self._commit_snap[p] = max(self._commit_snap.get(p, v), v)
@@ -365,12 +382,17 @@ class EngineService:
         with self._stat_lock:
             rows, self._rows_new = self._rows_new, 0
             fl, self._flagged_new = self._flagged_new, []
+            sd, self._standard_new = self._standard_new, []
             snap, self._commit_snap = self._commit_snap, {}
             lat_cum = self._lat_cum
         flagged = np.concatenate(fl) if len(fl) > 1 else (fl[0] if fl else np.zeros(0, FLAGGED_NP))
+        standard = (np.concatenate(sd) if len(sd) > 1 else sd[0]) if sd else None
         seq = -1
         if rows or len(flagged):
-            self.router.on_flagged(flagged, rows)      # enqueues; never blocks on KIE
+            if standard is not None:                   # standard_mode="process"
+                self.router.on_flagged(flagged, rows, standard=standard)
+            else:
+                self.router.on_flagged(flagged, rows)  # enqueues; never blocks on KIE
             seq = getattr(self.router, "last_handoff_seq", -1)
         if snap:
             if self.handoff is not None and seq < 0:
@@ -497,7 +519,11 @@ class EngineService:
         if self.handoff is not None:
             hs = self.handoff.stats()
             extra.update(handoff_queue_depth=hs["depth"], handoff_retries=hs["retries"],
-                         handoff_acked=hs["acked"], handoff_failed=hs["failed"])
+                         handoff_acked=hs["acked"], handoff_failed=hs["failed"],
+                         handoff_refused=hs.get("refused", 0),
+                         handoff_dead_letter_total=hs.get("dead_lettered", 0))
+        if self.standard_mode == "process":
+            extra.update(standard_started=getattr(self.router, "standard_started", 0))
         return c, lat, extra
 
     def model_source(self) -> dict:

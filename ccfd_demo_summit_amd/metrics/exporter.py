@@ -283,6 +283,11 @@ class GpuEngineCollector:
                 q.add_metric([str(qq)], hist_quantile(lat, qq) * 1e-9)
             yield q
         for k, v in (extra or {}).items():
+            if k.endswith("_total"):                    # counters keep their own name, e.g.
+                c = CounterMetricFamily(k[:-len("_total")], k)    # handoff_dead_letter_total
+                c.add_metric([], float(v))
+                yield c
+                continue
             g = GaugeMetricFamily(M.GPU_PREFIX + k, k)
             g.add_metric([], float(v))
             yield g

@@ -87,6 +87,9 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
            "CCFD_OUTPUT_MODE": spec.engine.output_mode, "CCFD_PERSIST_ITEMS": spec.engine.persist_items, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
     if spec.engine.rules:
         env["ROUTER_RULES"] = spec.engine.rules
+    env["ROUTER_STANDARD_MODE"] = spec.engine.standard_mode
+    if spec.engine.handoff_dlq:
+        env["CCFD_HANDOFF_DLQ"] = spec.engine.handoff_dlq
     env.update(spec.env)
     w = ["--weights", spec.engine.weights] if spec.engine.weights else []
     svc: Dict[str, tuple] = {}
@@ -115,7 +118,10 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
                       "--rdzv-endpoint", f"127.0.0.1:{29500 + o}"])
         svc["engine"] = (nodes, lambda r: [sys.executable, "-m", "torch.distributed.run"] + dist_args
                          + ["--nproc-per-node", str(g), "-m", "ccfd_demo_summit_amd.launch", "engine", "--host", host,
-                            "--port", str(8091 + o + 16 * r)] + w)
+                            "--port", str(8091 + o + 16 * r),
+                            # the model's /prometheus (+ local rank): its own range, never Seldon's
+                            # 8000 + o + r nor another replica's
+                            "--model-metrics-port", str(8300 + o + 16 * r)] + w)
     if spec.router.deploy:
         svc["router"] = (spec.router.replicas, lambda r: PY + ["router", "--group-membership", "--host", host,
                                                                "--port", str(8191 + o + r)])

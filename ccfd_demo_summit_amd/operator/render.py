@@ -86,6 +86,9 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
            "CCFD_EXEC_MODE": spec.engine.exec_mode, "CCFD_OUTPUT_MODE": spec.engine.output_mode, "CCFD_PERSIST_ITEMS": spec.engine.persist_items}
     if spec.engine.rules:
         env["ROUTER_RULES"] = spec.engine.rules
+    env["ROUTER_STANDARD_MODE"] = spec.engine.standard_mode
+    if spec.engine.handoff_dlq:
+        env["CCFD_HANDOFF_DLQ"] = spec.engine.handoff_dlq
     env.update(spec.env)
     data = dict(env)
     data["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"          # dmabuf IPC for RCCL / cross-process tensors
@@ -128,9 +131,14 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
             out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "ccfd-engine"},
                         "spec": {"clusterIP": "None", "selector": {"app": "ccfd-engine"},
                                  "ports": [{"name": "rendezvous", "port": RDZV_PORT, "targetPort": RDZV_PORT}]}})
-        out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", nodes, [_container(
-            spec, "engine", cmd, ports=ports, gpus=g, probe=("/health/ping", 8091, 120))],
-            annotations=_scrape("/prometheus", 8091)))
+        eng_c = _container(spec, "engine", cmd, ports=ports, gpus=g, probe=("/health/ping", 8091, 120))
+        vols = None
+        if spec.engine.handoff_dlq:            # the hand-off dead-letter journal's directory
+            import posixpath
+            eng_c["volumeMounts"] = [{"name": "handoff-dlq", "mountPath": posixpath.dirname(spec.engine.handoff_dlq)}]
+            vols = [{"name": "handoff-dlq", "emptyDir": {}}]
+        out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", nodes, [eng_c],
+                             annotations=_scrape("/prometheus", 8091), volumes=vols))
 
     if spec.seldon.deploy:
         cmd = LAUNCH + ["seldon", "--device", "auto"] + weights

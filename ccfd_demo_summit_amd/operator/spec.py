@@ -50,6 +50,9 @@ class EngineSpec:
     output_mode: str = "zerocopy"    # zerocopy | dma
     persist_items: str = "auto"      # persistent MLP on W64 rows: claimed (throughput, = auto) | pipelined
     rules: str = ""                  # routing rule text or file (ROUTER_RULES)
+    standard_mode: str = "count"     # count | process: a standard process per standard-routed
+                                     # transaction, as the reference router does (README.md:552)
+    handoff_dlq: str = ""            # dead-letter journal of KIE-refused hand-offs ("" = hold + retry)
 
 
 @dataclass
@@ -124,6 +127,8 @@ class FraudDetectionSpec:
             raise SpecError(f"engine.exec_mode {self.engine.exec_mode!r}: auto | persistent | launch")
         if self.engine.persist_items not in ("pipelined", "claimed", "auto"):
             raise SpecError(f"engine.persist_items {self.engine.persist_items!r}: pipelined | claimed | auto")
+        if self.engine.standard_mode not in ("count", "process"):
+            raise SpecError(f"engine.standard_mode {self.engine.standard_mode!r}: count | process")
         if self.engine.output_mode not in ("zerocopy", "dma"):
             raise SpecError(f"engine.output_mode {self.engine.output_mode!r}: zerocopy | dma")
         if self.engine.exec_mode == "persistent" and self.engine.output_mode != "zerocopy":

@@ -23,39 +23,215 @@ offset commits or the X2 collective schedule on a slow or absent KIE server.  He
   its Kafka consumers stop fetching) until the queue drains -- back-pressure, never an
   exception out of the scoring step.
 
+* standard-routed rows (``Router(standard_mode="process")``, the reference's "standard
+  transaction process", README.md:552) go through the same queue as column batches
+  (``submit_standard``) and gate the same offset commits;
+* a NON-retryable answer (a 4xx other than 408/429, or a client-side error such as a
+  malformed response) is never acknowledged silently: the request is first appended to the
+  durable dead-letter journal (``DeadLetterQueue``: JSONL, fsync'd) and only then acked, so
+  the Kafka offset that covers it is committed only after the DLQ holds it; with no DLQ
+  configured the request is retried (held) like a transient failure and the operator sees
+  ``refused`` grow -- scoring back-pressures instead of losing fraud cases.
+  ``python -m ccfd_demo_summit_amd.launch dlq-replay`` re-delivers the journal, each entry
+  exactly once;
+* customer-response signals are coalesced into one ``signal/batch`` request; if the KIE
+  server does not have that extension (404 / 405) the hand-off falls back, for good, to the
+  standard per-instance ``/instances/{id}/signal/{name}`` route.
+
 ``sink`` is anything with the ProcessEngine hand-off interface (``start_fraud_many`` /
-``start_fraud`` / ``signal``): a ``KieClient`` (HTTP) or an in-process ``ProcessEngine``.
+``start_fraud`` / ``start_standard_many`` / ``signal``): a ``KieClient`` (HTTP) or an
+in-process ``ProcessEngine``.
 """
 from __future__ import annotations
 
 import collections
+import json
+import os
 import threading
 import time
 from typing import Any, Deque, Dict, List, Optional, Tuple
 
 TRANSIENT_HTTP = (500, 502, 503, 504, 429, 408)
+MISSING_ROUTE_HTTP = (404, 405, 501)
 
 
 class HandoffError(RuntimeError):
     """A non-retryable KIE answer (4xx other than 408/429)."""
 
 
+def _status(e: BaseException) -> Optional[int]:
+    resp = getattr(e, "response", None)
+    return getattr(resp, "status_code", None)
+
+
 def _transient(e: BaseException) -> bool:
+    """Worth retrying: the server could not be reached or answered 5xx / 408 / 429.  Every
+    other error -- a 4xx, a non-JSON 200 body, an invalid URL, a ValueError -- is a definite
+    refusal that no retry can fix (requests' exceptions all derive from IOError, so an
+    ``OSError`` catch-all would retry those forever)."""
     try:
         import requests
+        if isinstance(e, requests.HTTPError):
+            st = _status(e)
+            return st is None or st in TRANSIENT_HTTP
         if isinstance(e, (requests.ConnectionError, requests.Timeout)):
-            return True
-        if isinstance(e, requests.HTTPError) and e.response is not None:
-            return e.response.status_code in TRANSIENT_HTTP
+            return not isinstance(e, (requests.exceptions.InvalidURL, requests.exceptions.InvalidSchema,
+                                      requests.exceptions.MissingSchema))
+        if isinstance(e, requests.RequestException):
+            return False
     except ImportError:                    # pragma: no cover
         pass
-    return isinstance(e, (ConnectionError, TimeoutError, OSError))
+    if isinstance(e, ValueError):          # json.JSONDecodeError and friends
+        return False
+    return isinstance(e, (ConnectionError, TimeoutError))
+
+
+def _jsonable(kind: str, payload: Any) -> Any:
+    if kind == "standard":
+        return {k: list(v) for k, v in payload.items()}
+    if kind == "signal":
+        iid, name, body = payload
+        return [iid, name, body]
+    if kind == "signals":
+        return [list(x) for x in payload]
+    return payload
+
+
+def _from_json(kind: str, payload: Any) -> Any:
+    if kind == "signal":
+        return tuple(payload)
+    if kind == "signals":
+        return [tuple(x) for x in payload]
+    return payload
+
+
+class DeadLetterQueue:
+    """Durable journal of hand-off requests KIE refused (README.md:552,558 hops that cannot
+    complete).  One JSON line per refused request: ``{"dlq": id, "kind", "payload", "error",
+    "ts"}``, fsync'd before ``put`` returns (the caller acks -- and the engine commits the Kafka
+    offsets covering it -- only after that).  ``replay(sink)`` re-delivers the entries not yet
+    replayed and appends ``{"replayed": id}`` after each success, so running it twice starts
+    nothing twice (and fraud / standard starts are idempotent per transaction id at KIE)."""
+
+    def __init__(self, path: str, fsync: bool = True):
+        self.path = str(path)
+        self.fsync = bool(fsync)
+        d = os.path.dirname(os.path.abspath(self.path))
+        os.makedirs(d, exist_ok=True)
+        self._lock = threading.Lock()
+        self._next = 0
+        self.total = 0
+        for rec in self._records():
+            if "dlq" in rec:
+                self._next = max(self._next, int(rec["dlq"]) + 1)
+                self.total += 1
+        self._f = open(self.path, "a", buffering=1)
+
+    def _records(self):
+        if not os.path.exists(self.path):
+            return
+        with open(self.path) as f:
+            for line in f:
+                line = line.strip()
+                if not line:
+                    continue
+                try:
+                    yield json.loads(line)
+                except json.JSONDecodeError:
+                    continue                   # a torn last line (killed mid-write)
+
+    def _append(self, rec: Dict[str, Any]) -> None:
+        self._f.write(json.dumps(rec, default=float) + "\n")
+        self._f.flush()
+        if self.fsync:
+            os.fsync(self._f.fileno())
+
+    def put(self, kind: str, payload: Any, error: str) -> int:
+        with self._lock:
+            i = self._next
+            self._next += 1
+            self._append({"dlq": i, "kind": kind, "payload": _jsonable(kind, payload), "error": error[:500],
+                          "ts": time.time()})
+            self.total += 1
+            return i
+
+    def pending(self) -> List[Dict[str, Any]]:
+        """Entries not yet replayed, oldest first."""
+        done = set()
+        ents = []
+        for rec in self._records():
+            if "replayed" in rec:
+                done.add(int(rec["replayed"]))
+            elif "dlq" in rec:
+                ents.append(rec)
+        return [e for e in ents if int(e["dlq"]) not in done]
+
+    def replay(self, sink, stop_on_error: bool = True) -> Dict[str, int]:
+        """Re-deliver every pending entry to ``sink`` (KieClient / ProcessEngine)."""
+        ok = failed = 0
+        for e in self.pending():
+            try:
+                deliver(sink, e["kind"], _from_json(e["kind"], e["payload"]))
+            except BaseException:              # noqa: BLE001 -- reported, entry stays pending
+                failed += 1
+                if stop_on_error:
+                    break
+                continue
+            with self._lock:
+                self._append({"replayed": int(e["dlq"]), "ts": time.time()})
+            ok += 1
+        return {"replayed": ok, "failed": failed, "pending": len(self.pending())}
+
+    def close(self) -> None:
+        with self._lock:
+            if not self._f.closed:
+                self._f.close()
+
+
+def deliver(sink, kind: str, payload: Any, batch_signals: bool = True) -> Tuple[int, int]:
+    """One hand-off request to ``sink``; returns (signals ok, signals stale)."""
+    if kind == "signals":
+        if batch_signals and hasattr(sink, "signal_many"):
+            res = sink.signal_many(payload)
+        else:
+            res = [sink.signal(iid, name, body) for iid, name, body in payload]
+        ok = sum(1 for x in res if x)
+        return ok, len(res) - ok
+    if kind == "start":
+        many = getattr(sink, "start_fraud_many", None)
+        if many is not None and len(payload) > 1:
+            many(payload)
+        else:
+            for v in payload:
+                sink.start_fraud(v)
+        return 0, 0
+    if kind == "standard":
+        many = getattr(sink, "start_standard_many", None)
+        if many is not None:
+            many(payload)
+        else:
+            from ..process.engine import rows_of
+            for v in rows_of(payload):
+                sink.start_standard(v)
+        return 0, 0
+    iid, name, body = payload
+    ok = sink.signal(iid, name, body)
+    return (1, 0) if ok else (0, 1)
 
 
 class KieHandoff:
     def __init__(self, sink, capacity: int = 1 << 21, max_batch: int = 4096, workers: int = 2,
-                 backoff_s: float = 0.05, max_backoff_s: float = 2.0, metrics=None):
+                 backoff_s: float = 0.05, max_backoff_s: float = 2.0, metrics=None,
+                 dlq: Optional[DeadLetterQueue] = None, batch_signals: bool = True):
+        """``dlq``: where refused requests go before they are acked (None: a refused request
+        is held and retried at ``max_backoff_s`` -- never acked unsent).  ``batch_signals``:
+        coalesce response signals into the ``signal/batch`` extension (falls back to the
+        per-instance route by itself when the server lacks it)."""
         self.sink = sink
+        self.dlq = dlq
+        self.batch_signals = bool(batch_signals) and hasattr(sink, "signal_many")
+        self.refused = 0                   # refusals seen (held or dead-lettered)
+        self.dead_lettered = 0
         self.capacity = int(capacity)
         self.max_batch = int(max_batch)
         self.backoff_s = float(backoff_s)
@@ -106,6 +282,18 @@ class KieHandoff:
         for i in range(0, len(items), self.max_batch):
             chunk = items[i:i + self.max_batch]
             seq = self._push("start", chunk, len(chunk))
+        return seq
+
+    def submit_standard(self, cols: Dict[str, list]) -> int:
+        """Enqueue standard-process starts (columns of equal length: transaction_id,
+        customer_id, amount, proba); returns the hand-off sequence number."""
+        n = len(next(iter(cols.values()))) if cols else 0
+        if n == 0:
+            return self.last_seq()
+        seq = -1
+        for i in range(0, n, self.max_batch):
+            chunk = {k: v[i:i + self.max_batch] for k, v in cols.items()}
+            seq = self._push("standard", chunk, min(self.max_batch, n - i))
         return seq
 
     def submit_signal(self, instance_id: int, name: str, payload: Any) -> int:
@@ -160,28 +348,24 @@ class KieHandoff:
             self._cv.notify_all()
 
     def _deliver(self, kind: str, payload: Any) -> None:
-        if kind == "signals":                       # consecutive signals, one request
-            res = self.sink.signal_many(payload)
-            ok = sum(1 for x in res if x)
+        if kind == "signals" and self.batch_signals:
+            try:
+                ok, stale = deliver(self.sink, kind, payload, batch_signals=True)
+            except BaseException as e:             # noqa: BLE001
+                if _status(e) not in MISSING_ROUTE_HTTP:
+                    raise
+                # the KIE server has no signal/batch extension: use the standard
+                # per-instance signal route from now on
+                self.batch_signals = False
+                with self._cv:
+                    self.errors.append(f"signal/batch unsupported ({_status(e)}): per-instance signals")
+                ok, stale = deliver(self.sink, kind, payload, batch_signals=False)
+        else:
+            ok, stale = deliver(self.sink, kind, payload, batch_signals=False)
+        if ok or stale:
             with self._cv:
                 self.signals_ok += ok
-                self.signals_stale += len(res) - ok
-            return
-        if kind == "start":
-            many = getattr(self.sink, "start_fraud_many", None)
-            if many is not None and len(payload) > 1:
-                many(payload)
-            else:
-                for v in payload:
-                    self.sink.start_fraud(v)
-            return
-        iid, name, body = payload
-        ok = self.sink.signal(iid, name, body)
-        with self._cv:
-            if ok:
-                self.signals_ok += 1
-            else:
-                self.signals_stale += 1
+                self.signals_stale += stale
 
     def _run(self) -> None:
         while True:
@@ -192,7 +376,7 @@ class KieHandoff:
                     return
                 seq, kind, payload = self._q.popleft()
                 seqs = [seq]
-                if kind == "signal" and hasattr(self.sink, "signal_many"):
+                if kind == "signal":
                     # coalesce the run of signals queued behind this one (customer responses
                     # arrive one per message; one HTTP request per signal would cap them)
                     batch = [payload]
@@ -201,27 +385,47 @@ class KieHandoff:
                         seqs.append(s2)
                         batch.append(p2)
                     kind, payload = "signals", batch
-            n_items = len(payload) if kind in ("start", "signals") else 1
+            n_items = len(payload) if kind in ("start", "signals") else \
+                (len(next(iter(payload.values()))) if kind == "standard" and payload else 1)
             delay = self.backoff_s
             t_fail = None
+            refused_once = False
             while True:
                 try:
                     self._deliver(kind, payload)
                     break
                 except BaseException as e:          # noqa: BLE001 -- classified below
+                    err = repr(e)[:300]
                     if not _transient(e):
                         # a definite refusal (e.g. 404 unknown container): retrying cannot
-                        # help; keep it for the operator instead of wedging the queue
+                        # help.  Durable first, ack after: the offsets covering it are then
+                        # committed with the request safe in the dead-letter journal
+                        if not refused_once:
+                            refused_once = True
+                            with self._cv:
+                                self.refused += 1
+                                self.failed.append((kind, payload, err))
+                                self.errors.append(err)
+                        if self.dlq is not None:
+                            try:
+                                self.dlq.put(kind, payload, err)
+                            except OSError as de:   # DLQ unwritable: hold, like an outage
+                                with self._cv:
+                                    self.errors.append(f"DLQ write failed: {de!r}"[:300])
+                            else:
+                                with self._cv:
+                                    self.dead_lettered += n_items
+                                    self.failed_total += 1
+                                if self.metrics is not None and hasattr(self.metrics, "dead_letter"):
+                                    self.metrics.dead_letter.inc(n_items)
+                                break
+                        delay = self.max_backoff_s  # no DLQ: hold (never ack an unsent request)
+                    else:
                         with self._cv:
-                            self.failed.append((kind, payload, repr(e)[:300]))
-                            self.failed_total += 1
-                            self.errors.append(repr(e)[:300])
-                        break
-                    with self._cv:
-                        self.retries += 1
-                        self.errors.append(repr(e)[:300])
-                    if self.metrics is not None:
-                        self.metrics.retries.inc()
+                            self.retries += 1
+                            self.errors.append(err)
+                        if self.metrics is not None:
+                            self.metrics.retries.inc()
                     if t_fail is None:
                         t_fail = time.monotonic()
                     with self._cv:
@@ -239,4 +443,6 @@ class KieHandoff:
             return {"submitted": self.submitted_items, "acked": self.acked_items, "depth": self._queued_items,
                     "acked_seq": self.acked_seq, "last_seq": self._next_seq - 1, "retries": self.retries,
                     "signals_ok": self.signals_ok, "signals_stale": self.signals_stale,
-                    "failed": self.failed_total, "outage_s": round(self.outage_s, 3)}
+                    "failed": self.failed_total, "refused": self.refused,
+                    "dead_lettered": self.dead_lettered, "batch_signals": self.batch_signals,
+                    "outage_s": round(self.outage_s, 3)}

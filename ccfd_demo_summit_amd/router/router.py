@@ -27,6 +27,15 @@ from ..metrics.exporter import RouterMetrics
 from .rules import RuleSet
 
 
+def standard_columns(rec: np.ndarray) -> Dict[str, list]:
+    """Scored records -> the column batch a standard-process hand-off carries (probabilities
+    and amounts rounded to 1e-6: the JSON body stays ~4x smaller than full float64 repr)."""
+    return {"transaction_id": rec["tx_id"].astype(np.int64).tolist(),
+            "customer_id": rec["customer"].astype(np.int64).tolist(),
+            "amount": np.round(rec["amount"].astype(np.float64), 6).tolist(),
+            "proba": np.round(rec["proba"].astype(np.float64), 6).tolist()}
+
+
 class Router:
     def __init__(self, rules: RuleSet, processes, metrics: Optional[RouterMetrics] = None,
                  standard_mode: str = "count", handoff=None):
@@ -45,6 +54,7 @@ class Router:
         self.signals_stale = 0
         self.handoff = handoff
         self.last_handoff_seq = -1
+        self.standard_started = 0
 
     # ------------------------------------------------------------------ scoring results
     def on_scored(self, ids, customers, proba, X: Optional[np.ndarray] = None,
@@ -66,27 +76,51 @@ class Router:
             self._start_fraud(int(ids[i]), int(customers[i]) if customers is not None else 0,
                               float(amounts[i]) if amounts is not None else 0.0, float(proba[i]))
         if self.standard_mode == "process":
-            for i in np.nonzero(routes != Route.FRAUD)[0]:
-                self.processes.start_standard({"transaction_id": int(ids[i]), "proba": float(proba[i]),
-                                               "amount": float(amounts[i]) if amounts is not None else 0.0})
+            si = np.nonzero(routes != Route.FRAUD)[0]
+            if len(si):
+                cols = {"transaction_id": [int(ids[i]) for i in si],
+                        "customer_id": [int(customers[i]) if customers is not None else 0 for i in si],
+                        "amount": [float(amounts[i]) if amounts is not None else 0.0 for i in si],
+                        "proba": [float(proba[i]) for i in si]}
+                if self.handoff is not None:
+                    self.last_handoff_seq = self.handoff.submit_standard(cols)
+                elif hasattr(self.processes, "start_standard_many"):
+                    self.processes.start_standard_many(cols)
+                else:
+                    for i in si:
+                        self.processes.start_standard({"transaction_id": int(ids[i]), "proba": float(proba[i]),
+                                                       "amount": float(amounts[i]) if amounts is not None else 0.0})
+                with self._lock:
+                    self.standard_started += len(si)
         return {"incoming": n, "fraud": int(len(fraud_idx)), "standard": int(n - len(fraud_idx))}
 
-    def on_flagged(self, flagged: np.ndarray, total_rows: int) -> Dict[str, int]:
-        """Engine hot path: only fraud-routed rows are materialised on the host (the GPU
-        epilogue counted the rest).  ``flagged`` is the engine's flagged-record array."""
+    def on_flagged(self, flagged: np.ndarray, total_rows: int,
+                   standard: Optional[np.ndarray] = None) -> Dict[str, int]:
+        """Engine hot path: ``flagged`` = the fraud-routed rows (the engine's flagged-record
+        array; the GPU epilogue counted the rest).  ``standard``: with ``standard_mode="process"``
+        the engine's standard-routed scored records (SCORED_DTYPE: tx_id, customer, proba,
+        amount) -- each starts a standard process, like the reference router does for every
+        low-probability transaction (README.md:552)."""
         nf = int(len(flagged))
         self.metrics.tx_incoming.inc(total_rows)
         self.metrics.tx_outgoing.labels(type="fraud").inc(nf)
         self.metrics.tx_outgoing.labels(type="standard").inc(total_rows - nf)
+        std_cols = None
+        if self.standard_mode == "process" and standard is not None and len(standard):
+            std_cols = standard_columns(standard)
         if self.handoff is not None:                        # async, retried, acked later
+            seq = -1
             if nf:
-                self.last_handoff_seq = self.handoff.submit_starts(
+                seq = self.handoff.submit_starts(
                     [{"transaction_id": int(r["tx_id"]), "customer_id": int(r["customer"]),
                       "amount": float(r["amount"]), "proba": float(r["proba"])} for r in flagged])
                 with self._lock:
                     self.fraud_started += nf
-            else:
-                self.last_handoff_seq = -1
+            if std_cols is not None:
+                seq = self.handoff.submit_standard(std_cols)
+                with self._lock:
+                    self.standard_started += len(standard)
+            self.last_handoff_seq = seq
             return {"incoming": total_rows, "fraud": nf, "standard": total_rows - nf}
         many = getattr(self.processes, "start_fraud_many", None)
         if many is not None and nf > 1:                     # one hand-off for the whole step
@@ -97,6 +131,16 @@ class Router:
         else:
             for r in flagged:
                 self._start_fraud(int(r["tx_id"]), int(r["customer"]), float(r["amount"]), float(r["proba"]))
+        if std_cols is not None:
+            smany = getattr(self.processes, "start_standard_many", None)
+            if smany is not None:
+                smany(std_cols)
+            else:
+                from ..process.engine import rows_of
+                for v in rows_of(std_cols):
+                    self.processes.start_standard(v)
+            with self._lock:
+                self.standard_started += len(standard)
         return {"incoming": total_rows, "fraud": nf, "standard": total_rows - nf}
 
     def _start_fraud(self, tx_id: int, customer: int, amount: float, proba: float) -> None:

@@ -218,3 +218,81 @@ def test_persistent_engine_service_kafka_kie_outage_exactly_once(gpu):
         kie.close()
         kb.close()
         lite.stop()
+
+
+def test_engine_service_standard_mode_process_starts_every_row_once(gpu):
+    """standard_mode="process" (README.md:549-552 "instantiate a standard or
+    fraudulent transaction business process, depending on the value returned by Seldon"): the
+    persistent W64 engine surfaces every scored row through the scored-record ring, the router
+    hands standard rows to KIE as column batches next to the fraud starts, and afterwards
+    standard + fraud starts == rows, 0 duplicates, each row's proba_1 (as KIE received it) is
+    the fp32 oracle's within 1e-2, and the committed lag is 0."""
+    from ccfd_demo_summit_amd.contracts import TxBatch
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
+    from ccfd_demo_summit_amd.metrics import MetricsHub
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import DistContext
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    from ccfd_demo_summit_amd.process.kie_server import KieClient
+    from ccfd_demo_summit_amd.router import Router, RuleSet
+    from ccfd_demo_summit_amd.router.handoff import KieHandoff
+    from tests.helpers.kie_thread import KieThread
+
+    seen = {}
+
+    class Recording(ProcessEngine):
+        def start_standard_many(self, items):
+            for tx, p in zip(items["transaction_id"], items["proba"]):
+                seen.setdefault(int(tx), []).append(("standard", float(p)))
+            return super().start_standard_many(items)
+
+        def start_fraud(self, v):
+            seen.setdefault(int(v["transaction_id"]), []).append(("fraud", float(v["proba"])))
+            return super().start_fraud(v)
+
+    n = 40_000
+    X, _ = generate(n, seed=12)
+    ids = np.arange(1, n + 1, dtype=np.uint64) + np.uint64(9 << 32)
+    m = build_model("mlp", seed=5, X_ref=X, calibrate_rate=0.02)
+    lite = KafkaLiteServer("127.0.0.1", 0, default_partitions=2).start_in_thread()
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 2)
+    procs = Recording(notification_timeout_s=1e9)
+    kie = KieThread(procs)
+    client = KieClient(f"http://127.0.0.1:{kie.port}", timeout_s=5.0, pool_size=4)
+    ho = KieHandoff(client, workers=2, max_batch=4096)
+    hub = MetricsHub()
+    router = Router(RuleSet.threshold(0.5), client, hub.router, standard_mode="process", handoff=ho)
+    svc = EngineService(DistContext(0, 1, 0, gpu, "none"), DeviceModel(m, gpu, wire=True), kb, router,
+                        EngineServiceConfig(batch=4096, depth=8, streams=2, ring_rows=1 << 16, flush_us=200,
+                                            reduce_period_ms=2.0, standard_mode="process",
+                                            scored_capacity=1 << 15)).start()
+    try:
+        assert svc.exec_mode == "persistent" and svc.native is not None
+        for k in range(0, n, 2000):
+            kb.produce("odh-demo", TxBatch(ids=ids[k:k + 2000], customer=(ids[k:k + 2000] % 999).astype(np.uint32),
+                                           features=X[k:k + 2000]).encode(), partition=(k // 2000) % 2)
+        t0 = time.time()
+        while (svc.rows_scored < n or ho.depth() or svc.commits_pending()
+               or kb.lag("ccfd-engine", "odh-demo")) and time.time() - t0 < 90:
+            svc.step()
+        assert svc.rows_scored == n and kb.lag("ccfd-engine", "odh-demo") == 0 and ho.depth() == 0
+        nf = int(hub.router.tx_outgoing.labels(type="fraud")._value.get())
+        assert procs.standard_count + len(procs._by_tx) == n
+        assert procs.standard_count == n - nf and router.standard_started == n - nf
+        assert procs.duplicates == 0 and procs.standard_duplicates == 0
+        assert sorted(seen) == ids.astype(np.int64).tolist() and all(len(v) == 1 for v in seen.values())
+        p32 = m.predict_proba(X)
+        got = np.array([seen[int(t)][0][1] for t in ids])
+        assert np.abs(got - p32).max() < 1e-2
+        kinds = np.array([seen[int(t)][0][0] == "fraud" for t in ids])
+        far = np.abs(p32 - 0.5) > 1e-2
+        np.testing.assert_array_equal(kinds[far], (p32 >= 0.5)[far])
+    finally:
+        svc.stop()
+        ho.close()
+        kie.close()
+        kb.close()
+        lite.stop()

@@ -116,14 +116,119 @@ def test_full_queue_reports_backpressure():
     ho.close()
 
 
-def test_non_retryable_answer_is_reported_not_wedged():
+def test_refused_without_dlq_is_held_not_acked():
+    """a non-retryable answer must never be acked unsent (the engine would commit
+    the offsets covering those fraud rows).  Without a DLQ the request is held and retried."""
+    calls = []
+
     class Sink:
         def start_fraud_many(self, items):
+            calls.append(len(items))
             raise ValueError("404 container not instantiated")
+    ho = KieHandoff(Sink(), workers=1, backoff_s=0.01, max_backoff_s=0.05)
+    seq = ho.submit_starts([{"transaction_id": 1}, {"transaction_id": 2}])
+    assert not ho.drain(0.5)
+    st = ho.stats()
+    assert not ho.acked(seq) and st["refused"] == 1 and st["acked"] == 0 and st["depth"] == 2
+    assert len(calls) >= 2                       # still being retried
+    ho._stop = True
+
+
+def test_refused_starts_go_to_the_dlq_then_replay_exactly_once(kie, tmp_path):
+    """KIE answers 404 (unknown container): the refused starts are written
+    to the durable DLQ BEFORE they are acked (so the offsets can be committed), counted in
+    dead_lettered; replay against a healthy KIE starts each exactly once, a second replay
+    starts nothing."""
+    import requests
+    from ccfd_demo_summit_amd.router.handoff import DeadLetterQueue
+    procs, k, px = kie
+    bad = KieClient(px.url, container_id="no-such-container", timeout_s=1.0)
+    with pytest.raises(requests.HTTPError):
+        bad.start_fraud_many([{"transaction_id": 1}, {"transaction_id": 2}])
+    dlq = DeadLetterQueue(str(tmp_path / "handoff-dlq.jsonl"))
+    ho = KieHandoff(bad, workers=2, max_batch=16, backoff_s=0.01, dlq=dlq)
+    router = Router(RuleSet.threshold(0.5), bad, handoff=ho)
+    ids = np.arange(100, 150, dtype=np.uint64)
+    router.on_flagged(_flagged(ids), 4096)
+    seq = router.last_handoff_seq
+    assert ho.drain(10) and ho.acked(seq)
+    st = ho.stats()
+    assert st["dead_lettered"] == 50 and st["refused"] == 4 and st["failed"] == 4
+    assert len(procs.instances) == 0
+    pend = DeadLetterQueue(dlq.path).pending()           # durable: a fresh reader sees them
+    assert sorted(v["transaction_id"] for e in pend for v in e["payload"]) == ids.tolist()
+    good = KieClient(px.url, timeout_s=1.0)
+    res = DeadLetterQueue(dlq.path).replay(good)
+    assert res == {"replayed": 4, "failed": 0, "pending": 0}
+    assert sorted(i.variables["transaction_id"] for i in procs.instances.values()) == ids.tolist()
+    assert DeadLetterQueue(dlq.path).replay(good)["replayed"] == 0
+    assert len(procs.instances) == 50 and procs.duplicates == 0
+    ho.close()
+
+
+def test_transient_classification():
+    import requests
+    from ccfd_demo_summit_amd.router.handoff import _transient
+
+    def http(code):
+        r = requests.Response()
+        r.status_code = code
+        return requests.HTTPError(response=r)
+    assert _transient(requests.ConnectionError("refused")) and _transient(requests.Timeout("slow"))
+    assert _transient(http(503)) and _transient(http(429)) and _transient(http(408))
+    assert not _transient(http(404)) and not _transient(http(400))
+    assert not _transient(requests.exceptions.JSONDecodeError("x", "doc", 0))   # non-JSON 200 body
+    assert not _transient(requests.exceptions.InvalidURL("x"))
+    assert not _transient(requests.exceptions.MissingSchema("x"))
+    assert not _transient(ValueError("bad"))
+    assert _transient(ConnectionRefusedError())
+
+
+def test_signal_batch_falls_back_to_per_instance_route():
+    """a KIE server without the signal/batch extension (404 / 405) must not drop
+    every customer response: the hand-off switches to the per-instance signal route."""
+    import requests
+    got = []
+
+    class Sink:
+        def signal_many(self, items):
+            r = requests.Response()
+            r.status_code = 405
+            raise requests.HTTPError(response=r)
+
+        def signal(self, iid, name, payload):
+            got.append((iid, name, payload))
+            return True
     ho = KieHandoff(Sink(), workers=1)
-    ho.submit_starts([{"transaction_id": 1}, {"transaction_id": 2}])
+    for i in range(5):
+        ho.submit_signal(i, "customerResponse", True)
     assert ho.drain(5)
-    assert ho.stats()["failed"] == 1 and ho.failed[0][0] == "start"
+    st = ho.stats()
+    assert st["signals_ok"] == 5 and st["refused"] == 0 and st["batch_signals"] is False
+    assert sorted(g[0] for g in got) == list(range(5))
+    ho.close()
+
+
+def test_standard_starts_through_the_handoff_exactly_once(kie):
+    """Router(standard_mode="process"): the engine's standard-routed rows start one standard
+    process each (README.md:552) through the same acked hand-off, as column batches; a
+    re-delivered batch (at-least-once) is deduplicated per transaction id at KIE."""
+    procs, _, px = kie
+    client = KieClient(px.url, timeout_s=2.0)
+    ho = KieHandoff(client, workers=2, max_batch=1000, backoff_s=0.02)
+    router = Router(RuleSet.threshold(0.5), client, standard_mode="process", handoff=ho)
+    from ccfd_demo_summit_amd.ops._lib import SCORED_DTYPE
+    std = np.zeros(3000, np.dtype(SCORED_DTYPE))
+    std["tx_id"] = np.arange(10_000, 13_000)
+    std["proba"] = 0.01
+    std["amount"] = 7.5
+    fl = _flagged(np.arange(1, 11, dtype=np.uint64))
+    router.on_flagged(fl, 3010, standard=std)
+    seq = router.last_handoff_seq
+    router.on_flagged(fl[:0], 1000, standard=std[:1000])           # re-delivery of 1000 rows
+    assert ho.drain(20) and ho.acked(seq)
+    assert procs.standard_count == 3000 and procs.standard_duplicates == 1000
+    assert len(procs._by_tx) == 10 and router.standard_started == 4000
     ho.close()
 
 
