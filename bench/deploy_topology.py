@@ -187,6 +187,19 @@ def main(argv=None):
                     help="SIGKILL the KIE process this many seconds into the window (0 = never) ...")
     ap.add_argument("--kie-outage-s", type=float, default=5.0,
                     help="... and restart it from its journal this long after")
+    ap.add_argument("--kafka-kill-at", type=float, default=0.0,
+                    help="SIGKILL kafka-lite this many seconds into the window (0 = never) ...")
+    ap.add_argument("--kafka-down-s", type=float, default=2.0,
+                    help="... and restart it from its data directory this long after")
+    ap.add_argument("--fsync", default="interval", choices=["always", "interval", "never"],
+                    help="kafka-lite durability flush policy (its logs are always on disk here)")
+    ap.add_argument("--standard-mode", default="count", choices=["count", "process"],
+                    help="process: a standard process per standard-routed transaction (README.md:552)")
+    ap.add_argument("--serving", default="native", choices=["native", "python"],
+                    help="engine scoring loop: the C++ serving thread, or the round-3 Python thread")
+    ap.add_argument("--trace", action="store_true",
+                    help="engine ranks record their stage trace + scoring-loop timeline "
+                         "(CCFD_SERVICE_TRACE) and the tail is attributed (bench/tail_attribution.py)")
     ap.add_argument("--sample-s", type=float, default=5.0)
     ap.add_argument("--drain-timeout-s", type=float, default=120.0)
     ap.add_argument("--log-dir", default="gpurun_out/deploy_topology")
@@ -210,12 +223,16 @@ def main(argv=None):
                  "n_gpus": 1 if a.rehearsal else a.ranks, "ranks": a.ranks, "rehearsal": a.rehearsal,
                  "fmt": a.fmt, "producers": a.producers, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
                  "model": a.model}
+    import tempfile
+    kdir = tempfile.mkdtemp(prefix="ccfd-kafka-lite-")          # durable logs + committed offsets
+    out["kafka_durable"] = {"fsync": a.fsync}
     try:
         L = "ccfd_demo_summit_amd.launch"
-        procs.append(Proc("kafka-lite", [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
-                                         "--port", str(kafka_port), "--nodes", str(a.kafka_nodes),
-                                         "--partitions", str(a.partitions), "--metrics-port", str(metrics_port),
-                                         "--retention-batches", str(a.retention_batches)], env, log_dir))
+        kafka_cmd = [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
+                     "--port", str(kafka_port), "--nodes", str(a.kafka_nodes),
+                     "--partitions", str(a.partitions), "--metrics-port", str(metrics_port),
+                     "--retention-batches", str(a.retention_batches), "--data-dir", kdir, "--fsync", a.fsync]
+        procs.append(Proc("kafka-lite", kafka_cmd, env, log_dir))
         wait_port(kafka_port, 60)
         from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
         kb = KafkaBroker(brokers, connect_wait_s=30)
@@ -234,6 +251,12 @@ def main(argv=None):
         wait_port(kie_port, 60)
         eng_env = dict(env)
         eng_env["CCFD_INGEST_THREADS"] = str(a.ingest_threads or max(1, a.partitions // a.ranks))
+        eng_env["ROUTER_STANDARD_MODE"] = a.standard_mode
+        eng_env["CCFD_NATIVE_SERVE"] = "1" if a.serving == "native" else "0"
+        out["serving"] = a.serving
+        if a.trace:
+            eng_env["CCFD_SERVICE_TRACE"] = str(log_dir / "service_trace")
+        eng_env["CCFD_HANDOFF_DLQ"] = str(Path(jdir) / "handoff-dlq.jsonl")
         if a.rehearsal:
             eng_env.update(CCFD_DIST_BACKEND="gloo", CCFD_DEVICE_MODULO="1")
         eng_cmd = [PY, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(a.ranks),
@@ -293,7 +316,18 @@ def main(argv=None):
         r_w0, f_w0, _ = scrape_all()
         last_t, last_r = t_w0, r_w0
         outage = {}
+        koutage = {}
         while any(p.alive() for p in prods):
+            if a.kafka_kill_at > 0 and not koutage and time.time() - t_w0 >= a.kafka_kill_at:
+                kl = [p for p in procs if p.name.startswith("kafka-lite")][-1]
+                kl.stop(sig=signal.SIGKILL, wait=5)            # a crashed broker pod
+                koutage = {"killed_at_s": round(time.time() - t_w0, 1)}
+            if koutage and "restarted_at_s" not in koutage and \
+                    time.time() - t_w0 >= a.kafka_kill_at + a.kafka_down_s:
+                procs.append(Proc("kafka-lite-restarted", kafka_cmd, env, log_dir))   # recovers from disk
+                koutage["restarted_at_s"] = round(time.time() - t_w0, 1)
+                wait_port(kafka_port, 60)
+                koutage["serving_at_s"] = round(time.time() - t_w0, 1)
             if a.kie_outage_at > 0 and not outage and time.time() - t_w0 >= a.kie_outage_at:
                 kie = [p for p in procs if p.name == "kie"][0]
                 kie.stop(sig=signal.SIGKILL, wait=5)           # a crashed KIE pod
@@ -302,13 +336,17 @@ def main(argv=None):
                     time.time() - t_w0 >= a.kie_outage_at + a.kie_outage_s:
                 procs.append(Proc("kie-restarted", kie_cmd, kie_env, log_dir))   # recovers the journal
                 outage["restarted_at_s"] = round(time.time() - t_w0, 1)
-            time.sleep(min(a.sample_s, 1.0) if a.kie_outage_at > 0 else a.sample_s)
+            time.sleep(min(a.sample_s, 0.5) if (a.kie_outage_at > 0 or a.kafka_kill_at > 0) else a.sample_s)
             if time.time() - last_t < a.sample_s:
                 continue
             now = time.time()
             r_now, _, _ = scrape_all()
+            try:
+                lag = kb.lag("ccfd-engine", "odh-demo")
+            except Exception:                               # the broker is down right now
+                lag = None
             samples.append({"t_s": round(now - t_w0, 1), "tx_s": round((r_now - last_r) / (now - last_t), 1),
-                            "lag_msgs": kb.lag("ccfd-engine", "odh-demo")})
+                            "lag_msgs": lag})
             last_t, last_r = now, r_now
         t_w1 = time.time()
         r_w1, _, _ = scrape_all()
@@ -388,6 +426,24 @@ def main(argv=None):
             wait_port(kie_port, 1)
         out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
         out["kie_duplicates"] = stats["duplicates"]
+        out["standard_mode"] = a.standard_mode
+        if a.standard_mode == "process":
+            # every transaction started exactly one process: standard + fraud == incoming
+            t_k = time.time()
+            while int(stats["standard_started"]) + int(stats["fraud_started"]) < int(rows_all) \
+                    and time.time() - t_k < 60:
+                time.sleep(0.5)
+                stats = json.loads(http_text(f"http://127.0.0.1:{kie_port}/rest/stats"))
+            out["kie"] = stats
+            out["kie_standard_plus_fraud_equals_incoming"] = \
+                int(stats["standard_started"]) + int(stats["fraud_started"]) == int(rows_all)
+            out["kie_standard_duplicates"] = stats.get("standard_duplicates")
+        if koutage:
+            rec = re.findall(r"\[kafka-lite\] recovered from .*", "".join(
+                p.text() for p in procs if p.name == "kafka-lite-restarted"))
+            out["kafka_outage"] = dict(koutage, recovered=rec)
+        dlq = Path(jdir) / "handoff-dlq.rank0.jsonl"
+        out["handoff_dead_lettered"] = sum(1 for _ in open(dlq)) if dlq.exists() else 0
         try:
             out["notifier"] = json.loads(http_text(f"http://127.0.0.1:{notif_port}/health/ping"))
         except Exception as e:
@@ -409,7 +465,9 @@ def main(argv=None):
                                        "note": "SparkMetrics.json: the trainer is not part of this topology "
                                                "(tests/test_dashboard_conformance.py scrapes it)"}
         ok = (out["incoming_equals_produced"] and out["every_partition_exactly_one_rank"]
-              and out["kie_fraud_started_equals_routed"] and not rep["unmatched"])
+              and out["kie_fraud_started_equals_routed"] and not rep["unmatched"]
+              and out["kie_duplicates"] == 0
+              and out.get("kie_standard_plus_fraud_equals_incoming", True))
         out["checks_passed"] = bool(ok)
     finally:
         for p in reversed(procs):
@@ -419,6 +477,17 @@ def main(argv=None):
             if journal.exists():
                 out["kie_journal_bytes"] = journal.stat().st_size
             shutil.rmtree(jdir, ignore_errors=True)
+        import shutil
+        try:
+            out["kafka_data_bytes"] = sum(f.stat().st_size for f in Path(kdir).rglob("*") if f.is_file())
+        except OSError:
+            pass
+        shutil.rmtree(kdir, ignore_errors=True)
+    if a.trace:
+        sys.path.insert(0, str(ROOT / "bench"))
+        import tail_attribution
+        out["tail_attribution"] = [tail_attribution.attribute(str(t))
+                                   for t in sorted((log_dir / "service_trace").glob("rank*.npz"))]
     line = json.dumps(out)
     print(line, flush=True)
     if a.out:

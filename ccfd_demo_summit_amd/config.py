@@ -98,6 +98,8 @@ class EngineConfig:
     handoff_dlq: str = ""            # dead-letter journal of requests KIE refused (4xx); "" = no DLQ:
                                      # a refused request is held and retried, never acked unsent
     scored_capacity: int = 1 << 20   # standard_mode=process: per-row scored-record ring (rows)
+    native_serve: bool = True        # score the rings from the engine's C++ serving thread (no Python
+                                     # on the scoring path); False = the Python scoring thread
     max_delay_us: int = 500          # deadline flush for partially filled micro-batches
     reduce_period_ms: float = 10.0   # X2 counter all-reduce period
     gbdt_trees: int = 100
@@ -147,6 +149,7 @@ ENV_MAP = {
     "CCFD_PERSIST_ITEMS": ("engine", "persist_items", str),
     "CCFD_HANDOFF_CAPACITY": ("engine", "handoff_capacity", int),
     "CCFD_HANDOFF_DLQ": ("engine", "handoff_dlq", str),
+    "CCFD_NATIVE_SERVE": ("engine", "native_serve", str),
     "CCFD_KAFKA_BACKEND": ("kafka", "backend", str),
     "CCFD_KAFKA_PARTITIONS": ("kafka", "partitions", int),
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),

@@ -280,9 +280,11 @@ class StreamEngine:
             raise RuntimeError(f"ccfd_engine_create failed: {last_error()}")
         self.logs: Dict[int, PartitionLog] = {}
         self._flag_buf = (Flagged * 65536)()
+        self._flag_cap = max(1024, int(flag_capacity))
 
     def close(self):
         if getattr(self, "h", None):
+            self._serving = False                # destroy stops the serving thread first
             lib().ccfd_engine_destroy(C.c_void_p(self.h))
             self.h = None
 
@@ -398,6 +400,48 @@ class StreamEngine:
     def scored_dropped(self) -> int:
         """Rows that completed while the scored ring was full (pump() / drain paths only)."""
         return int(lib().ccfd_engine_scored_dropped(C.c_void_p(self.h)))
+
+    # ------------------------------------------------------------------ native serving thread
+    def serve_start(self, budget_us: int = 200, flush_us: int = 500) -> None:
+        """Score the rings from a C++ thread (``run(budget_us, flush_us)`` back to back) until
+        ``serve_stop``; collect progress with ``serve_collect`` (engine.cpp serving thread)."""
+        check(lib().ccfd_engine_serve_start(C.c_void_p(self.h), int(budget_us), int(flush_us)),
+              "ccfd_engine_serve_start")
+        self._serving = True
+
+    def serve_stop(self) -> None:
+        if getattr(self, "_serving", False) and getattr(self, "h", None):
+            rc = lib().ccfd_engine_serve_stop(C.c_void_p(self.h))
+            self._serving = False
+            if rc < 0:
+                raise RuntimeError(f"engine serving thread failed: {last_error()}")
+
+    def serve_hold(self, hold: bool) -> None:
+        lib().ccfd_engine_serve_hold(C.c_void_p(self.h), 1 if hold else 0)
+
+    def serve_collect(self, want_scored: bool = False):
+        """(stats, flagged records, scored records or None) -- one consistent cut: the flagged
+        (and scored) records are exactly those of every batch the cumulative stats count that
+        an earlier collect did not return.  Raises if the serving thread failed."""
+        st = EngineStats()
+        if getattr(self, "_collect_flag", None) is None:
+            self._collect_flag = np.empty(max(1024, self._flag_cap), dtype=np.dtype(FLAGGED_DTYPE))
+        sc = None
+        if want_scored:
+            cap = getattr(self, "_scored_cap", 0)
+            if getattr(self, "_collect_scored", None) is None or len(self._collect_scored) != cap:
+                self._collect_scored = np.empty(cap, dtype=np.dtype(SCORED_DTYPE))
+            sc = self._collect_scored
+        nf, ns = C.c_int64(0), C.c_int64(0)
+        rc = lib().ccfd_engine_serve_collect(C.c_void_p(self.h), C.byref(st), self._collect_flag.ctypes.data,
+                                             len(self._collect_flag), C.byref(nf),
+                                             sc.ctypes.data if sc is not None else None,
+                                             len(sc) if sc is not None else 0, C.byref(ns))
+        if rc < 0:
+            raise RuntimeError(f"engine serving thread failed: {last_error()}")
+        fl = self._collect_flag[:nf.value].copy()
+        rec = sc[:ns.value].copy() if sc is not None else None
+        return _stats(st), fl, rec
 
     # ------------------------------------------------------------------ ring (streaming) mode
     def set_ring(self, partition: int, capacity: int) -> PartitionLog:

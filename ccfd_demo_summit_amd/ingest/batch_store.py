@@ -31,6 +31,14 @@ class InvalidBatch(BrokerError):
     pass
 
 
+class OutOfOrderSequence(BrokerError):
+    """An idempotent producer's batch skipped a sequence number (Kafka error 45)."""
+
+
+_PID = struct.Struct(">qhi")          # producerId, producerEpoch, baseSequence (bytes 43..57)
+_PRODUCER_CACHE = 5                   # batches remembered per producer and partition (Kafka: 5)
+
+
 def split_batches(data: bytes, verify_crc: bool = True) -> List[Tuple[int, int, int, memoryview]]:
     """Validate a produced record set: [(lastOffsetDelta, count, attrs, batch bytes)].
     Raises InvalidBatch on a truncated batch, a magic other than 2 or a CRC mismatch."""
@@ -79,6 +87,62 @@ class BatchStore:
         self._topics: Dict[str, List[_Log]] = {}
         self._committed: Dict[Tuple[str, str, int], int] = {}
         self._lock = threading.Lock()
+        # idempotent producers: (topic, partition) -> producer id -> [epoch, [(first seq, last
+        # seq, base offset), ...]] of its last batches; InitProducerId hands out _next_pid
+        self._producers: Dict[Tuple[str, int], Dict[int, list]] = {}
+        self._next_pid = 0
+        self.duplicates_dropped = 0
+
+    # ------------------------------------------------------------------ durability hooks
+    # (no-ops here; ingest/durable_store.py writes segments / offsets / producer ids)
+    def _persist_appended(self, topic: str, partition: int, L: "_Log", first: int) -> None:
+        pass
+
+    def _apply_retention(self, topic: str, partition: int, L: "_Log") -> None:
+        pass
+
+    def _persist_commit(self, group: str, topic: str, partition: int, offset: int) -> None:
+        pass
+
+    def _persist_producer_ids(self) -> None:
+        pass
+
+    # ------------------------------------------------------------------ idempotent producers
+    def init_producer_id(self) -> Tuple[int, int]:
+        """InitProducerId (non-transactional): a fresh producer id, epoch 0."""
+        with self._lock:
+            pid = self._next_pid
+            self._next_pid += 1
+            self._persist_producer_ids()
+            return pid, 0
+
+    def _track_producer(self, topic: str, partition: int, b, base: int) -> None:
+        pid, epoch, seq = _PID.unpack_from(b, 43)
+        if pid < 0:
+            return
+        last = struct.unpack_from(">i", b, 23)[0]
+        st = self._producers.setdefault((topic, partition), {}).setdefault(pid, [epoch, []])
+        if epoch != st[0]:
+            st[0], st[1] = epoch, []
+        st[1].append((seq, seq + last, base))
+        del st[1][:-_PRODUCER_CACHE]
+        self._next_pid = max(self._next_pid, pid + 1)
+
+    def _check_sequence(self, topic: str, partition: int, b) -> Optional[int]:
+        """None: append; an int: the base offset of the already appended copy (duplicate)."""
+        pid, epoch, seq = _PID.unpack_from(b, 43)
+        if pid < 0:
+            return None
+        st = self._producers.get((topic, partition), {}).get(pid)
+        if st is None or epoch != st[0] or not st[1]:
+            return None                     # a new producer (or epoch): accept
+        for first, _last, base in st[1]:
+            if first == seq:
+                return base
+        if seq != st[1][-1][1] + 1:
+            raise OutOfOrderSequence(f"{topic}[{partition}] producer {pid}: sequence {seq}, "
+                                     f"expected {st[1][-1][1] + 1}")
+        return None
 
     # ------------------------------------------------------------------ topics
     def create_topic(self, name: str, partitions: Optional[int] = None) -> None:
@@ -112,24 +176,35 @@ class BatchStore:
         with self._lock:
             L = self._log(topic, partition)
             base0 = L.end
+            first_new = len(L.batches)
             nrec = 0
             now = time.time()
-            for last, count, _attrs, mv in batches:
+            for k, (last, count, _attrs, mv) in enumerate(batches):
+                dup = self._check_sequence(topic, partition, mv)
+                if dup is not None:         # a retried batch that is already in the log
+                    self.duplicates_dropped += 1
+                    if k == 0:
+                        base0 = dup
+                    continue
                 # a writable view is memory the broker owns (kafka-lite receives each produce
                 # request into its own buffer): kept as is, no copy; anything else is copied once
                 b = mv if not mv.readonly else bytearray(mv)
                 struct.pack_into(">q", b, 0, L.end)          # broker-assigned base offset
+                self._track_producer(topic, partition, b, L.end)
                 L.bases.append(L.end)
                 L.batches.append(b)
                 L.ts.append(now)
                 L.end += last + 1
                 L.nbytes += len(b)
                 nrec += count
+            if len(L.batches) > first_new:
+                self._persist_appended(topic, partition, L, first_new)
             if self.retention_batches is not None and len(L.batches) > self.retention_batches:
                 drop = len(L.batches) - self.retention_batches
                 L.nbytes -= sum(len(x) for x in L.batches[:drop])
                 del L.bases[:drop], L.batches[:drop], L.ts[:drop]
                 L.begin = L.bases[0]
+                self._apply_retention(topic, partition, L)
             return base0, nrec
 
     def produce(self, topic: str, value: bytes, key: Optional[bytes] = None,
@@ -188,7 +263,10 @@ class BatchStore:
     def commit(self, group: str, topic: str, partition: int, offset: int) -> None:
         with self._lock:
             k = (group, topic, partition)
-            self._committed[k] = max(offset, self._committed.get(k, 0))
+            v = max(offset, self._committed.get(k, 0))
+            if v != self._committed.get(k):
+                self._committed[k] = v
+                self._persist_commit(group, topic, partition, v)
 
     def committed(self, group: str, topic: str, partition: int) -> Optional[int]:
         with self._lock:

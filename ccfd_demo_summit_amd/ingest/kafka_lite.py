@@ -7,7 +7,11 @@ Stands in for the reference's 3-broker Strimzi cluster (deploy/frauddetection_cr
 protocol to it, and switching to a production cluster is only a ``BROKER_URL`` change.
 
 Storage keeps producer RecordBatches verbatim (``batch_store.py``): Produce validates the
-CRC and stamps the base offset, Fetch slices stored batches -- no per-record work.
+CRC and stamps the base offset, Fetch slices stored batches -- no per-record work.  With
+``--data-dir`` the logs, committed group offsets and idempotent-producer state are also on
+disk (``durable_store.py``: segments + offset index, fsync policy) and a restarted broker
+recovers them; InitProducerId + per-partition sequence numbers make a producer's retry after
+a broker crash store its batch once.
 
 ``KafkaLiteCluster(n)`` runs n broker listeners (node ids 1..n) over one shared log store,
 with partition leadership spread over the nodes (p -> node p % n).  Produce / Fetch /
@@ -26,14 +30,15 @@ from __future__ import annotations
 import argparse
 import asyncio
 import itertools
+import json
 import struct
 import threading
 import time
 from typing import Dict, List, Optional, Set, Tuple
 
-from .batch_store import BatchStore, InvalidBatch
-from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE, ERR_TOPIC_EXISTS,
-                         ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
+from .batch_store import BatchStore, InvalidBatch, OutOfOrderSequence
+from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE, ERR_OUT_OF_ORDER_SEQUENCE,
+                         ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
 
 NODE_ID = 1
 ERR_ILLEGAL_GENERATION, ERR_UNKNOWN_MEMBER, ERR_REBALANCE_IN_PROGRESS = 22, 25, 27
@@ -548,12 +553,20 @@ class KafkaLiteServer:
                     pr.append((p, ERR_NONE, base))
                     self.metrics.messages_in.labels(topic, "Kafka").inc(nrec)
                     self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
+                except OutOfOrderSequence:
+                    pr.append((p, ERR_OUT_OF_ORDER_SEQUENCE, -1))
+                    self.metrics.failed_produce.labels(topic, "Kafka").inc()
                 except InvalidBatch:
                     pr.append((p, ERR_CORRUPT, -1))
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
             resp.append((topic, pr))
         w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
         return w.i32(0).build()
+
+    def _api_22(self, r: Reader) -> bytes:                  # InitProducerId v0 (idempotence only)
+        r.string(); r.i32()
+        pid, epoch = self.store.init_producer_id()
+        return Writer().i32(0).i16(ERR_NONE).i64(pid).i16(epoch).build()
 
     def _api_1(self, r: Reader) -> bytes:                   # Fetch v4: stored batches, sliced
         r.i32(); r.i32(); r.i32(); max_bytes = r.i32(); r.i8()
@@ -783,8 +796,15 @@ class KafkaLiteCluster:
 
     def __init__(self, n: int = 3, host: str = "127.0.0.1", base_port: int = 0, default_partitions: int = 1,
                  auto_create: bool = True, retention_batches: Optional[int] = None,
-                 advertise: Optional[str] = None):
-        self.store = BatchStore(default_partitions=default_partitions, retention_batches=retention_batches)
+                 advertise: Optional[str] = None, data_dir: Optional[str] = None, fsync: str = "interval",
+                 store: Optional[BatchStore] = None):
+        """``data_dir``: keep the logs, committed offsets and producer state on disk
+        (ingest/durable_store.py) and recover them on start; None = in memory only."""
+        if store is None and data_dir:
+            from .durable_store import DurableBatchStore
+            store = DurableBatchStore(data_dir, default_partitions=default_partitions,
+                                      retention_batches=retention_batches, fsync=fsync)
+        self.store = store or BatchStore(default_partitions=default_partitions, retention_batches=retention_batches)
         self.state = ClusterState(self.store)
         self.metrics = BrokerMetrics(self.state)
         self.nodes = [KafkaLiteServer(host, base_port + i if base_port else 0, store=self.store,
@@ -847,6 +867,8 @@ class KafkaLiteCluster:
                 self._loop.stop()
             asyncio.run_coroutine_threadsafe(_shutdown(), self._loop)
             self._thread.join(5)
+        if hasattr(self.store, "close"):
+            self.store.close()
 
 
 def main(argv=None):
@@ -859,9 +881,17 @@ def main(argv=None):
     ap.add_argument("--advertise", default=None, help="host name put in Metadata (default: --host)")
     ap.add_argument("--retention-batches", type=int, default=0,
                     help="record batches kept per partition (0 = unbounded)")
+    ap.add_argument("--data-dir", default=None,
+                    help="durable logs: segments + offset index + committed offsets + producer state, "
+                         "recovered on start (ingest/durable_store.py); default: memory only")
+    ap.add_argument("--fsync", default="interval", choices=["always", "interval", "never"],
+                    help="--data-dir flush policy: before every answer, every second in the background, "
+                         "or left to the OS (a killed broker process loses nothing in any mode)")
     a = ap.parse_args(argv)
     cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions, advertise=a.advertise,
-                          retention_batches=a.retention_batches or None)
+                          retention_batches=a.retention_batches or None, data_dir=a.data_dir, fsync=a.fsync)
+    if a.data_dir:
+        print(f"[kafka-lite] recovered from {a.data_dir}: {json.dumps(cl.store.recovered)}", flush=True)
 
     async def run():
         await cl.start()

@@ -33,16 +33,17 @@ from .broker import BrokerError, Record
 
 # --------------------------------------------------------------------------- api keys
 PRODUCE, FETCH, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH, FIND_COORDINATOR = 0, 1, 2, 3, 8, 9, 10
-API_VERSIONS, CREATE_TOPICS = 18, 19
+API_VERSIONS, CREATE_TOPICS, INIT_PRODUCER_ID = 18, 19, 22
 JOIN_GROUP, HEARTBEAT, LEAVE_GROUP, SYNC_GROUP = 11, 12, 13, 14       # ingest/kafka_group.py
 SUPPORTED = {PRODUCE: 3, FETCH: 4, LIST_OFFSETS: 1, METADATA: 1, OFFSET_COMMIT: 2, OFFSET_FETCH: 1,
              FIND_COORDINATOR: 0, API_VERSIONS: 0, CREATE_TOPICS: 0,
-             JOIN_GROUP: 1, HEARTBEAT: 0, LEAVE_GROUP: 0, SYNC_GROUP: 0}
+             JOIN_GROUP: 1, HEARTBEAT: 0, LEAVE_GROUP: 0, SYNC_GROUP: 0, INIT_PRODUCER_ID: 0}
 
 ERR_NONE, ERR_OFFSET_OUT_OF_RANGE, ERR_UNKNOWN_TOPIC, ERR_CORRUPT = 0, 1, 3, 2
 ERR_LEADER_NOT_AVAILABLE, ERR_NOT_LEADER, ERR_NOT_COORDINATOR = 5, 6, 16
 RETRIABLE = (ERR_UNKNOWN_TOPIC, ERR_LEADER_NOT_AVAILABLE, ERR_NOT_LEADER, ERR_NOT_COORDINATOR)
 ERR_UNSUPPORTED_VERSION, ERR_TOPIC_EXISTS, ERR_INVALID_REQUEST = 35, 36, 42
+ERR_OUT_OF_ORDER_SEQUENCE = 45
 
 # --------------------------------------------------------------------------- crc32c
 _CRC_TABLE = None
@@ -419,7 +420,16 @@ class KafkaBroker:
     RETRIES = 8
 
     def __init__(self, bootstrap: str, client_id: str = "ccfd-mi355x", timeout: float = 10.0,
-                 connect_wait_s: float = 0.0, compression: int = CODEC_NONE):
+                 connect_wait_s: float = 0.0, compression: int = CODEC_NONE, idempotent: bool = False):
+        """``idempotent``: Kafka's idempotent producer -- InitProducerId once, then every
+        produced batch carries (producer id, epoch, base sequence per partition), so a batch
+        re-sent after a lost ack or a broker restart is stored once (the broker answers a
+        duplicate with its original offset)."""
+        self.idempotent = bool(idempotent)
+        self._pid: Optional[Tuple[int, int]] = None
+        self._seq: Dict[Tuple[str, int], int] = {}
+        self._seq_locks: Dict[Tuple[str, int], threading.Lock] = {}
+        self._seq_guard = threading.Lock()
         self.timeout = timeout
         self.client_id = client_id
         self.compression = compression
@@ -554,8 +564,51 @@ class KafkaBroker:
         rb = encode_record_batch(values, keys, compression=self.compression)
         return self.produce_raw(topic, partition, rb, acks)
 
+    def init_producer_id(self) -> Tuple[int, int]:
+        """InitProducerId v0 (no transactional id): (producer id, epoch)."""
+        body = Writer().string(None).i32(60000).build()
+        r = self._boot_request(INIT_PRODUCER_ID, 0, body)
+        r.i32()                                             # throttle
+        err, pid, epoch = r.i16(), r.i64(), r.i16()
+        if err:
+            raise BrokerError(f"InitProducerId error {err}")
+        return pid, epoch
+
+    def _stamp_sequence(self, topic: str, partition: int, record_set) -> Tuple[bytearray, int]:
+        """Write (producer id, epoch, base sequence) into every batch of ``record_set`` and
+        re-seal its CRC; returns (the stamped copy, records in it)."""
+        if self._pid is None:
+            self._pid = self.init_producer_id()
+        pid, epoch = self._pid
+        b = bytearray(record_set)
+        mv = memoryview(b)
+        seq = self._seq.get((topic, partition), 0)
+        o = n_total = 0
+        while o + 61 <= len(b):
+            blen = struct.unpack_from(">i", b, o + 8)[0]
+            count = struct.unpack_from(">i", b, o + 57)[0]
+            struct.pack_into(">qhi", b, o + 43, pid, epoch, seq)
+            struct.pack_into(">I", b, o + 17, crc32c(mv[o + 21:o + 12 + blen]))
+            seq += count
+            n_total += count
+            o += 12 + blen
+        del mv
+        return b, n_total
+
     def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
+        if self.idempotent:
+            key = (topic, partition)
+            with self._seq_guard:
+                lk = self._seq_locks.setdefault(key, threading.Lock())
+            with lk:                     # sequence order == send order on a partition
+                stamped, n = self._stamp_sequence(topic, partition, record_set)
+                base = self._produce_raw(topic, partition, stamped, acks)   # retries resend the same seq
+                self._seq[key] = self._seq.get(key, 0) + n
+                return base
+        return self._produce_raw(topic, partition, record_set, acks)
+
+    def _produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         # [acks, timeout, 1 topic, 1 partition, record set size] + the record set itself, sent
         # without copying it into the request (Connection.request scatter-gather)
         head = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000)).i32(1).string(topic)

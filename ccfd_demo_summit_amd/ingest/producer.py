@@ -221,13 +221,17 @@ class BatchingPublisher:
                 self._cv.notify()
 
     def _run(self):
+        retry = None                          # a batch whose send failed: re-sent AS IS first
         while True:
-            with self._cv:
-                if not self._q and not self._stop:
-                    self._cv.wait(self.linger_s)
-                if self._stop and not self._q:
-                    return
-                batch = [self._q.popleft() for _ in range(min(len(self._q), self.max_batch))]
+            if retry is not None:
+                batch, retry = retry, None
+            else:
+                with self._cv:
+                    if not self._q and not self._stop:
+                        self._cv.wait(self.linger_s)
+                    if self._stop and not self._q:
+                        return
+                    batch = [self._q.popleft() for _ in range(min(len(self._q), self.max_batch))]
             if not batch:
                 continue
             try:
@@ -240,10 +244,16 @@ class BatchingPublisher:
                     for v in batch:
                         self.broker.produce(self.topic, v)
                 self.sent += len(batch)
-            except Exception:                 # broker unavailable: retry the batch later
+            except Exception:                 # broker unavailable: retry the SAME batch later
+                # (an idempotent producer re-sends it under the same sequence number, so a batch
+                # the broker stored before the failure is not stored twice -- and no message
+                # joins it, which would be dropped with the duplicate)
                 self.errors += 1
-                with self._cv:
-                    self._q.extendleft(reversed(batch))
+                retry = batch
+                if self._stop:
+                    with self._cv:
+                        self._q.extendleft(reversed(batch))
+                    return
                 time.sleep(0.05)
 
     def close(self, timeout_s: float = 5.0) -> None:

@@ -38,11 +38,32 @@ import time
 from ..config import load_config
 
 
-def _broker(cfg, inproc=None):
+def _broker(cfg, inproc=None, idempotent: bool = False):
+    """Kafka client.  ``idempotent``: producers (transactions, notifications, responses) use
+    Kafka's idempotent produce, so a batch retried across a broker restart is stored once."""
     if inproc is not None:
         return inproc
     from ..ingest.kafka_wire import KafkaBroker
-    return KafkaBroker(cfg.kafka.broker_url, connect_wait_s=120.0)   # wait for the broker to come up
+    return KafkaBroker(cfg.kafka.broker_url, connect_wait_s=120.0,    # wait for the broker to come up
+                       idempotent=idempotent)
+
+
+def _safe(fn, default=None):
+    """A consumer poll / commit that survives a broker outage (restart, leader election): the
+    error is reported and the caller's loop simply tries again on its next turn."""
+    from ..ingest.broker import BrokerError
+    try:
+        return fn()
+    except (BrokerError, OSError, ConnectionError) as e:
+        now = time.monotonic()
+        if now - _safe.last > 1.0:
+            print(f"[launch] broker unavailable: {e!r}"[:300], file=sys.stderr, flush=True)
+            _safe.last = now
+        time.sleep(0.05)
+        return default
+
+
+_safe.last = 0.0
 
 
 def _consumer(broker, a, group, topics):
@@ -161,7 +182,7 @@ def cmd_kie(a, cfg):
     from ..process.notifier import encode_notification
     from ..process.prediction_service import PredictionService
     from ..serving.client import SeldonClient
-    broker = _broker(cfg)
+    broker = _broker(cfg, idempotent=True)
     topic = cfg.kafka.notification_topic
     # the KIE pod's own SELDON_URL / SELDON_ENDPOINT name ITS prediction-service target (the
     # user-task model, ccd-service.yaml:61-62), not the router's fraud model
@@ -192,7 +213,7 @@ def cmd_notifier(a, cfg):
 
     from ..ingest.producer import BatchingPublisher
     from ..process.notifier import NotificationService
-    broker = _broker(cfg)
+    broker = _broker(cfg, idempotent=True)
     # replies leave in batches (one produce request per linger period, not per reply)
     pub = BatchingPublisher(broker, cfg.kafka.response_topic)
     ns = NotificationService(lambda raw, key: pub.publish(raw),
@@ -204,9 +225,9 @@ def cmd_notifier(a, cfg):
         {"status": "ok", "sent": ns.sent, "replied": ns.replied, "no_reply": ns.no_reply}))
     _serve_in_thread(app, a.host, a.port or cfg.notifier.port)
     while True:
-        for r in cons.poll(timeout=0.05, max_records=10_000):
+        for r in _safe(lambda: cons.poll(timeout=0.05, max_records=10_000), []):
             ns.handle(r.value)
-        cons.commit()
+        _safe(cons.commit)
         ns.tick()
 
 
@@ -296,6 +317,7 @@ def cmd_engine(a, cfg):
         threshold=cfg.router.fraud_threshold, coalesce=cfg.engine.coalesce,
         ingest_threads=cfg.engine.ingest_threads, persist_items=cfg.engine.persist_items,
         standard_mode=cfg.router.standard_mode, scored_capacity=cfg.engine.scored_capacity,
+        native_serve=cfg.engine.native_serve,
         model_watch=(a.watch_model or cfg.engine.model_watch or None))).start()
     hub.gpu_registry.register(GpuEngineCollector(svc.metrics_source, rank_label=str(ctx.rank)))
     # the process's node-local rank (torchrun LOCAL_RANK) -- not the device index, which a
@@ -337,16 +359,17 @@ def cmd_engine(a, cfg):
                 # with a KIE outage in flight re-delivers them instead of losing them
                 if resp_wait is None or handoff.acked(resp_wait):
                     if resp_wait is not None:
-                        resp.commit()
+                        if _safe(lambda: resp.commit() or True) is None:
+                            continue              # broker outage: commit again next turn
                         resp_wait = None
-                    recs = resp.poll(max_records=10_000)
+                    recs = _safe(lambda: resp.poll(max_records=10_000), [])
                     for r in recs:
                         router.on_response(r.value)
                     if recs:
                         resp_wait = router.last_handoff_seq
-                for r in notif.poll(max_records=10_000):
+                for r in _safe(lambda: notif.poll(max_records=10_000), []):
                     router.on_notification_sent(r.value)
-                notif.commit()
+                _safe(notif.commit)
     finally:
         svc.stop()                    # drains; a resident persistent kernel halts here
         handoff.close(drain_s=5.0)
@@ -360,7 +383,7 @@ def cmd_producer(a, cfg):
     pc.fmt, pc.batch, pc.rate_tx_s, pc.id_base, pc.seed = a.fmt, a.batch, a.rate, a.id_base, a.seed_offset
     if a.csv:
         pc.source, pc.csv_path = "csv", a.csv
-    broker = _broker(cfg)
+    broker = _broker(cfg, idempotent=True)
     prod = TransactionProducer(broker, pc)
     if a.fmt == "json" and pc.source == "synthetic":
         prod._ensure_pool()                 # render the message pool before the clock starts

@@ -20,6 +20,7 @@ the processes (README.md:569,605).
 from __future__ import annotations
 
 import collections
+import os
 import queue
 import threading
 import time
@@ -67,6 +68,11 @@ class EngineServiceConfig:
     score_thread: bool = True        # drive engine.run() from a dedicated thread (GIL released in
                                      # native code) so scoring latency does not wait on the Python
                                      # router / process loop
+    native_serve: bool = True        # ...or from the engine's own C++ serving thread (engine.cpp
+                                     # ccfd_engine_serve_start): no Python on the scoring path at
+                                     # all -- the round-3 deployed tail was the Python thread waiting
+                                     # for the GIL between run() calls (profiles/r4/tail/)
+    serve_budget_us: int = 200       # native serving thread: run() budget per iteration
     model_watch: Optional[str] = None   # rank 0: hot-swap when this safetensors file changes
     handoff_hold_low: float = 0.5    # a held (full) hand-off queue resumes scoring below this fill
     standard_mode: str = "count"     # "process": every standard-routed row is handed to the router
@@ -199,6 +205,8 @@ class EngineService:
         self.handoff = getattr(router, "handoff", None)
         self._commit_snap: Dict[int, int] = {}
         self._commit_wait: Deque[Tuple[int, Dict[int, int]]] = collections.deque()
+        self._commit_retry: Dict[int, int] = {}     # acked snapshot a broker outage refused
+        self.commit_failures = 0
         self.held = False                  # hand-off queue full: scoring paused (back-pressure)
         self.hold_events = 0
         # "last request" of the reference model's gauges (proba_1 / Amount / V17 / V10) and the
@@ -206,6 +214,25 @@ class EngineService:
         self.last_scored = None
         self._lat_rows_cum = np.zeros(256, np.int64)
         self._dev_rows_cum = np.zeros(256, np.int64)
+        # CCFD_SERVICE_TRACE=<dir>: tail attribution (bench/tail_attribution.py) -- the engine's
+        # per-batch stage trace plus this process's scoring-loop timeline (every run() call, every
+        # task, every GC pause, hand-off holds), dumped to <dir>/rank<r>.npz at stop()
+        self._native = bool(cfg.native_serve)
+        self._rows_seen = 0
+        self._trace_dir = os.environ.get("CCFD_SERVICE_TRACE") or None
+        if self._trace_dir:
+            import gc
+            self.engine.enable_trace(1 << 18)
+            self._tr_runs = np.zeros((1 << 21, 3), np.int64)    # t_call, t_return, rows
+            self._tr_n = 0
+            self._tr_tasks: List[Tuple[int, int, str]] = []
+            self._tr_gc: List[Tuple[int, int, int]] = []        # t, phase (0 start / 1 stop), generation
+            self._tr_held: List[Tuple[int, int]] = []           # t, held
+
+            def _gc_cb(phase, info, _l=self._tr_gc):
+                _l.append((time.monotonic_ns(), 0 if phase == "start" else 1, int(info.get("generation", -1))))
+            self._gc_cb = _gc_cb
+            gc.callbacks.append(_gc_cb)
 
     # ------------------------------------------------------------------ ingest (producer side)
     def _ingest_once(self) -> int:
@@ -287,8 +314,9 @@ class EngineService:
 
     def _commit_done(self) -> None:
         """Commit every snapshot whose fraud rows the hand-off has acknowledged (all of them
-        when the hand-off is synchronous)."""
-        merged: Dict[int, int] = {}
+        when the hand-off is synchronous).  A commit that fails because the broker is down
+        (restart, leader election) is kept and retried on a later step -- scoring goes on."""
+        merged: Dict[int, int] = dict(self._commit_retry)
         while self._commit_wait:
             seq, snap = self._commit_wait[0]
             if self.handoff is not None and not self.handoff.acked(seq):
@@ -296,13 +324,25 @@ class EngineService:
             self._commit_wait.popleft()
             for p, v in snap.items():
                 merged[p] = max(merged.get(p, v), v)
-        self._commit(merged)
+        if not merged:
+            return
+        from ..ingest.broker import BrokerError
+        try:
+            self._commit(merged)
+            self._commit_retry = {}
+        except (BrokerError, OSError, ConnectionError):
+            self._commit_retry = merged
+            self.commit_failures += 1
 
     def commits_pending(self) -> int:
-        return len(self._commit_wait)
+        return len(self._commit_wait) + (1 if self._commit_retry else 0)
 
     def _run_once(self, budget_us: Optional[int] = None) -> int:
+        t_call = time.monotonic_ns() if self._trace_dir else 0
         st = self.engine.run(self.cfg.run_budget_us if budget_us is None else budget_us, self.cfg.flush_us)
+        if self._trace_dir and self._tr_n < len(self._tr_runs):
+            self._tr_runs[self._tr_n] = (t_call, time.monotonic_ns(), int(st.rows))
+            self._tr_n += 1
         # drain on the same thread, right after the rows were counted: the router must see
         # every completed micro-batch's rows together with its flagged records; the commit
         # snapshot follows the drain, so it never covers a row whose fraud record is not yet
@@ -331,6 +371,40 @@ class EngineService:
                 self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
         return int(st.rows)
 
+    def _collect_native(self) -> int:
+        """Native serving thread: progress since the last call.  The commit snapshot is taken
+        BEFORE the collect, and the collect returns the stats together with every flagged /
+        scored record of the batches they count (one cut under the engine's lock), so a
+        committed offset never covers a row whose records the router has not received."""
+        snap = self._snapshot_commits()
+        st, flagged, rec = self.engine.serve_collect(want_scored=self.standard_mode == "process")
+        rows = int(st.rows) - self._rows_seen
+        self._rows_seen = int(st.rows)
+        standard = rec[rec["route"] == 0] if rec is not None and len(rec) else None
+        with self._stat_lock:
+            self._rows_new += rows
+            if len(flagged):
+                self._flagged_new.append(flagged)
+            if standard is not None and len(standard):
+                self._standard_new.append(standard)
+            for p, v in (snap or {}).items():
+                self._commit_snap[p] = max(self._commit_snap.get(p, v), v)
+            self._lat_cum = st.lat_hist.astype(np.int64)
+            self._lat_rows_cum = st.lat_hist_rows.astype(np.int64)
+            self._dev_rows_cum = st.dev_hist_rows.astype(np.int64)
+            if st.last_seq:
+                self.last_scored = st.last
+            if st.dev_batches:
+                self.kernel_exec_mean_us = st.dev_exec_mean_us
+        return rows
+
+    def _progress(self) -> None:
+        """Wait helper for X2 ticks: the serving thread retires batches by itself."""
+        if self._native:
+            time.sleep(20e-6)
+        else:
+            self._run_once(0)
+
     def _reduce(self, lat_cum: np.ndarray, block: bool = False) -> bool:
         delta = lat_cum - self._lat_prev                # cumulative since reset -> send the delta
         if (delta < 0).any():                           # stats were reset in between
@@ -338,7 +412,7 @@ class EngineService:
         # at most one collective per tick, never waiting for a slower rank (block=False: the
         # tick is skipped while the previous reduction is still in flight); waiting for the
         # closed epoch keeps retiring micro-batches on this (the scoring) thread
-        ok = self.epochs.tick(delta, progress=lambda: self._run_once(0), block=block)
+        ok = self.epochs.tick(delta, progress=self._progress, block=block)
         if ok:
             self._lat_prev = lat_cum
         self.hotswap.poll()                             # runtime X1: swap once the blob landed
@@ -355,7 +429,12 @@ class EngineService:
                         task = self._tasks.get_nowait()
                     except queue.Empty:
                         break
-                    task()
+                    if self._trace_dir:
+                        t0 = time.monotonic_ns()
+                        task()
+                        self._tr_tasks.append((t0, time.monotonic_ns(), getattr(task, "__name__", "task")))
+                    else:
+                        task()
                 if self.held:                           # hand-off back-pressure: rings fill,
                     time.sleep(200e-6)                  # the Kafka consumers stop fetching
                     continue
@@ -375,9 +454,19 @@ class EngineService:
             if not self.held and self.handoff.full():
                 self.held = True
                 self.hold_events += 1
+                if self._native:
+                    self.engine.serve_hold(True)
+                if self._trace_dir:
+                    self._tr_held.append((time.monotonic_ns(), 1))
             elif self.held and self.handoff.has_room(self.cfg.handoff_hold_low):
                 self.held = False
-        if not threaded and not self.held:
+                if self._native:
+                    self.engine.serve_hold(False)
+                if self._trace_dir:
+                    self._tr_held.append((time.monotonic_ns(), 0))
+        if self._native:
+            self._collect_native()
+        elif not threaded and not self.held:
             self._run_once()
         with self._stat_lock:
             rows, self._rows_new = self._rows_new, 0
@@ -408,7 +497,7 @@ class EngineService:
                 self._tasks.put(lambda lat=lat_cum: self._reduce(lat))
             else:
                 self._reduce(lat_cum)
-        if threaded and rows == 0:
+        if (threaded or self._native) and rows == 0:
             time.sleep(50e-6)                            # nothing new: do not spin the GIL
         return rows
 
@@ -458,7 +547,7 @@ class EngineService:
                     with self._stat_lock:
                         lat = self._lat_cum
                     self._reduce(lat, block=True)
-            self.epochs.finish(progress=lambda: self._run_once(0))
+            self.epochs.finish(progress=self._progress)
             self.hotswap.poll(block=True)
         self._on_engine_thread(_do)
 
@@ -480,13 +569,33 @@ class EngineService:
             self._thread = threading.Thread(target=self._ingest_loop, daemon=True, name="ccfd-ingest")
             self._thread.start()
         self._score_thread = None
-        if self.cfg.score_thread:
+        if self._native:
+            self.engine.serve_start(self.cfg.serve_budget_us, self.cfg.flush_us)
+        elif self.cfg.score_thread:
             self._score_thread = threading.Thread(target=self._score_loop, daemon=True, name="ccfd-score")
             self._score_thread.start()
         return self
 
+    def dump_trace(self) -> Optional[str]:
+        """CCFD_SERVICE_TRACE: write <dir>/rank<r>.npz (see __init__)."""
+        if not self._trace_dir:
+            return None
+        import gc
+        if self._gc_cb in gc.callbacks:
+            gc.callbacks.remove(self._gc_cb)
+        os.makedirs(self._trace_dir, exist_ok=True)
+        path = os.path.join(self._trace_dir, f"rank{self.ctx.rank}.npz")
+        tasks = np.array([(a, b) for a, b, _ in self._tr_tasks], np.int64).reshape(-1, 2)
+        np.savez(path, batches=self.engine.read_trace(), runs=self._tr_runs[:self._tr_n], tasks=tasks,
+                 task_names=np.array([n for _, _, n in self._tr_tasks], dtype="U32"),
+                 gc=np.array(self._tr_gc, np.int64).reshape(-1, 3), held=np.array(self._tr_held, np.int64).reshape(-1, 2),
+                 t_dump=np.int64(time.monotonic_ns()), native=np.int64(1 if self._native else 0))
+        return path
+
     def stop(self) -> None:
         self._stop.set()
+        if self._native:
+            self.engine.serve_stop()
         for kc in self.natives:
             kc.stop()
         for th in (getattr(self, "_score_thread", None), getattr(self, "_thread", None)):
@@ -494,6 +603,11 @@ class EngineService:
                 th.join(5)
         for kc in self.natives:
             kc.close()
+        if self._trace_dir:
+            try:
+                print(f"[engine] service trace: {self.dump_trace()}", flush=True)
+            except Exception as e:                       # diagnostics must not block shutdown
+                print(f"[engine] service trace failed: {e!r}", flush=True)
         self.engine.close()
 
     def metrics_source(self):
@@ -501,7 +615,8 @@ class EngineService:
         extra = {"rows_scored_local": self.rows_scored,
                  "kernel_exec_mean_us": self.kernel_exec_mean_us,
                  "model_version": self.hotswap.version,
-                 "commits_pending": len(self._commit_wait), "handoff_held": int(self.held)}
+                 "commits_pending": len(self._commit_wait), "handoff_held": int(self.held),
+                 "commit_failures": self.commit_failures}
         if self.natives:
             # where the native consumer threads spend their time (cumulative seconds):
             # broker I/O, response parsing, row writing / encoding, waiting on full rings

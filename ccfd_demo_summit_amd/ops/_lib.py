@@ -126,6 +126,12 @@ def lib() -> C.CDLL:
         L.ccfd_engine_drain_scored.restype = C.c_int64
         L.ccfd_engine_scored_dropped.argtypes = [C.c_void_p]
         L.ccfd_engine_scored_dropped.restype = C.c_int64
+        L.ccfd_engine_serve_start.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+        L.ccfd_engine_serve_stop.argtypes = [C.c_void_p]
+        L.ccfd_engine_serve_hold.argtypes = [C.c_void_p, C.c_int]
+        L.ccfd_engine_serve_stats.argtypes = [C.c_void_p, C.POINTER(EngineStats), C.POINTER(C.c_int64)]
+        L.ccfd_engine_serve_collect.argtypes = [C.c_void_p, C.POINTER(EngineStats), C.c_void_p, C.c_int64,
+                                                C.POINTER(C.c_int64), C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         L.ccfd_engine_cursor.argtypes = [C.c_void_p, C.c_int]
         L.ccfd_engine_cursor.restype = C.c_int64
         L.ccfd_engine_reset_stats.argtypes = [C.c_void_p]

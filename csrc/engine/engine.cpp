@@ -1194,6 +1194,61 @@ class Engine {
     return submitted;
   }
 
+  // ------------------------------------------------------------------ native serving thread
+  // ccfd_engine_serve_start: a C++ thread calls run() back to back, so scoring latency never
+  // waits on the host language's scheduler (the round-3 deployed-topology tail: the Python
+  // scoring thread had to win the GIL between run() calls, profiles/r4/tail/).  Every other
+  // entry point that touches engine state takes api_mu, which the serving thread holds for one
+  // run() call at a time and yields as soon as a caller is waiting (api_waiters), so flips,
+  // hot swaps and stats reads interleave between run() calls on the caller's thread.  The
+  // flagged / scored rings and the ingest rings have their own locks and never take api_mu.
+  std::mutex api_mu;
+  std::atomic<int> api_waiters{0};
+  std::thread serve_th;
+  std::atomic<bool> serve_stop{false};
+  std::atomic<bool> serving{false};
+  std::atomic<int> serve_hold{0};
+  std::atomic<int> serve_rc{0};
+  int64_t serve_budget_us = 200, serve_flush_us = 500;
+  ccfd_engine_stats serve_st{};            // cumulative (under api_mu)
+  uint64_t serve_iters = 0;
+
+  void serve_loop() {
+    prctl(PR_SET_NAME, "ccfd-serve", 0, 0, 0);
+    (void)hipSetDevice(cfg.device);
+    while (!serve_stop.load(std::memory_order_relaxed)) {
+      if (api_waiters.load(std::memory_order_acquire) > 0) { std::this_thread::yield(); continue; }
+      if (serve_hold.load(std::memory_order_relaxed)) {       // hand-off back-pressure
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        continue;
+      }
+      std::lock_guard<std::mutex> lk(api_mu);
+      const int rc = run(serve_budget_us, serve_flush_us, &serve_st);
+      ++serve_iters;
+      if (rc < 0) { serve_rc.store(rc); break; }             // error text: ccfd_last_error
+    }
+  }
+
+  int serve_start(int64_t budget_us, int64_t flush_us) {
+    if (serving.load()) { set_error("engine already serving"); return -1; }
+    if (budget_us <= 0 || flush_us < 0) { set_error("bad serve budget / flush"); return -1; }
+    serve_budget_us = budget_us;
+    serve_flush_us = flush_us;
+    serve_stop.store(false);
+    serve_rc.store(0);
+    serving.store(true);
+    serve_th = std::thread([this] { serve_loop(); });
+    return 0;
+  }
+
+  int serve_stop_join() {
+    if (!serving.load()) return 0;
+    serve_stop.store(true);
+    if (serve_th.joinable()) serve_th.join();
+    serving.store(false);
+    return serve_rc.load();
+  }
+
   int64_t drain_flagged(ccfd_flagged* out, int64_t max) {
     std::lock_guard<std::mutex> lk(ring_mu);
     const uint64_t cap = ring.size();
@@ -1201,6 +1256,20 @@ class Engine {
     while (ring_head < ring_tail && k < max) out[k++] = ring[ring_head++ % cap];
     return k;
   }
+};
+
+// engine state guard for every API entry point except the ingest rings, the flagged / scored
+// drains and the watchdog paths (see the serving-thread note in Engine)
+struct ApiLock {
+  Engine* e;
+  explicit ApiLock(Engine* e_) : e(e_) {
+    e->api_waiters.fetch_add(1, std::memory_order_acq_rel);
+    e->api_mu.lock();
+    e->api_waiters.fetch_sub(1, std::memory_order_acq_rel);
+  }
+  ~ApiLock() { e->api_mu.unlock(); }
+  ApiLock(const ApiLock&) = delete;
+  ApiLock& operator=(const ApiLock&) = delete;
 };
 
 }  // namespace
@@ -1214,31 +1283,81 @@ void* ccfd_engine_create(const ccfd_engine_config* cfg) {
   return e;
 }
 
-void ccfd_engine_destroy(void* eng) { delete static_cast<Engine*>(eng); }
+void ccfd_engine_destroy(void* eng) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!e) return;
+  e->serve_stop_join();
+  delete e;
+}
+
+int ccfd_engine_serve_start(void* eng, int64_t budget_us, int64_t flush_us) {
+  auto* e = static_cast<Engine*>(eng);
+  ApiLock lk(e);
+  return e->serve_start(budget_us, flush_us);
+}
+
+int ccfd_engine_serve_stop(void* eng) {
+  return static_cast<Engine*>(eng)->serve_stop_join();
+}
+
+int ccfd_engine_serve_hold(void* eng, int hold) {
+  static_cast<Engine*>(eng)->serve_hold.store(hold ? 1 : 0, std::memory_order_relaxed);
+  return 0;
+}
+
+int ccfd_engine_serve_collect(void* eng, ccfd_engine_stats* out, ccfd_flagged* flagged, int64_t max_flagged,
+                              int64_t* n_flagged, ccfd_scored* scored, int64_t max_scored, int64_t* n_scored) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!out || !n_flagged || (max_flagged > 0 && !flagged)) return -1;
+  ApiLock lk(e);                       // no batch completes while the three are read
+  *out = e->serve_st;
+  e->fill_latency(out);
+  out->flagged_dropped = e->dropped;
+  *n_flagged = e->drain_flagged(flagged, max_flagged);
+  if (n_scored) *n_scored = (scored && max_scored > 0) ? e->drain_scored(scored, max_scored) : 0;
+  return e->serve_rc.load();
+}
+
+int ccfd_engine_serve_stats(void* eng, ccfd_engine_stats* out, int64_t* iters) {
+  auto* e = static_cast<Engine*>(eng);
+  if (!out) return -1;
+  ApiLock lk(e);
+  *out = e->serve_st;
+  e->fill_latency(out);
+  out->flagged_dropped = e->dropped;
+  if (iters) *iters = (int64_t)e->serve_iters;
+  return e->serve_rc.load();
+}
 
 int ccfd_engine_set_log(void* eng, int partition, const float* feats, const uint64_t* ids,
                         const uint32_t* customer, int64_t n_rows, int64_t cursor) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->set_log(partition, feats, ids, customer, n_rows, cursor);
 }
 
 int ccfd_engine_pump(void* eng, int64_t n_batches, int32_t batch_rows, int32_t drain,
                      ccfd_engine_stats* st) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->pump(n_batches, batch_rows, drain != 0, st);
 }
 
 int ccfd_engine_score_sync(void* eng, const float* x, int32_t n, float* proba_out, uint8_t* route_out) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->score_sync(x, n, proba_out, route_out);
 }
 
 int ccfd_engine_flip_epoch(void* eng, void* side_stream) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->flip_epoch(side_stream);
 }
 
 int ccfd_engine_epoch_complete(void* eng, int64_t flip_count) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->epoch_complete(flip_count);
 }
 
 int ccfd_engine_set_blob(void* eng, const void* blob) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->set_blob(blob);
 }
 
@@ -1249,9 +1368,10 @@ int64_t ccfd_engine_drain_flagged(void* eng, ccfd_flagged* out, int64_t max) {
 int ccfd_engine_scored_enable(void* eng, int64_t capacity) {
   auto* e = static_cast<Engine*>(eng);
   if (!e || capacity < 0 || capacity > (int64_t(1) << 28)) { set_error("bad scored-ring capacity"); return -1; }
+  ApiLock lk(e);
   int rc = e->drain_all();
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(e->s_mu);
+  std::lock_guard<std::mutex> slk(e->s_mu);
   e->sring.assign((size_t)capacity, ccfd_scored{});
   e->s_head = e->s_tail = e->s_dropped = 0;
   e->scored_on.store(capacity > 0, std::memory_order_relaxed);
@@ -1310,6 +1430,7 @@ int ccfd_engine_emergency_stop(void* eng, int timeout_ms) {
 
 int ccfd_engine_set_amount(void* eng, int partition, const float* amount) {
   auto* e = static_cast<Engine*>(eng);
+  ApiLock lk(e);
   if (partition < 0 || partition >= (int)e->parts.size()) { set_error("bad partition index"); return -1; }
   int rc = e->drain_all();
   if (rc) return rc;
@@ -1319,6 +1440,7 @@ int ccfd_engine_set_amount(void* eng, int partition, const float* amount) {
 
 int ccfd_engine_set_ring(void* eng, int partition, float* feats, uint64_t* ids, uint32_t* customer,
                          int64_t capacity) {
+  ApiLock lk(static_cast<Engine*>(eng));
   return static_cast<Engine*>(eng)->set_ring(partition, feats, ids, customer, capacity);
 }
 
@@ -1331,6 +1453,9 @@ int ccfd_engine_ring_commit(void* eng, int partition, int64_t n) {
 }
 
 int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {
+  auto* e = static_cast<Engine*>(eng);
+  if (e->serving.load()) { ccfd::set_error("engine is serving (ccfd_engine_serve_start): run() is its thread's"); return -1; }
+  ApiLock lk(e);
   return static_cast<Engine*>(eng)->run(budget_us, flush_us, st);
 }
 
@@ -1359,6 +1484,7 @@ int ccfd_engine_trace_read(void* eng, ccfd_batch_trace* out, int32_t max) {
 
 void ccfd_engine_reset_stats(void* eng) {
   auto* e = static_cast<Engine*>(eng);
+  ApiLock lk(e);
   e->reset_latency();
   e->t_submit_ns = e->t_wait_ns = e->t_complete_ns = 0;
   e->dev_batches = e->dev_exec_ns = 0;

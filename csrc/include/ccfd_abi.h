@@ -340,6 +340,21 @@ int64_t ccfd_engine_ring_acquire(void* eng, int partition, int64_t want, int64_t
 int ccfd_engine_ring_commit(void* eng, int partition, int64_t n);
 int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st);
 void ccfd_engine_reset_stats(void* eng);
+// Native serving thread: a C++ thread calls ccfd_engine_run(budget_us, flush_us) back to back
+// (the deployed engine's consumer loop, free of the host language's scheduler).  While it
+// serves, ccfd_engine_run() from another thread is refused; every other call is serialised with
+// it between two run() calls.  hold != 0 pauses scoring (hand-off back-pressure).  serve_stats
+// copies the cumulative counters / latency histograms since serve start (reset_stats zeroes the
+// latencies), returns the serving thread's error code (0 = running or stopped cleanly).
+int ccfd_engine_serve_start(void* eng, int64_t budget_us, int64_t flush_us);
+int ccfd_engine_serve_stop(void* eng);
+int ccfd_engine_serve_hold(void* eng, int hold);
+int ccfd_engine_serve_stats(void* eng, ccfd_engine_stats* out, int64_t* iters);
+// One consistent cut while serving: the cumulative stats AND every flagged (and, if `scored`,
+// scored) record of the batches those stats count, drained together between two run() calls
+// (a commit snapshot taken BEFORE this call never covers a row whose records it misses).
+int ccfd_engine_serve_collect(void* eng, ccfd_engine_stats* out, ccfd_flagged* flagged, int64_t max_flagged,
+                              int64_t* n_flagged, ccfd_scored* scored, int64_t max_scored, int64_t* n_scored);
 
 // Per-micro-batch stage trace (SURVEY.md §5 "per-stage timestamps in a ring buffer"): the
 // last `capacity` completed batches, host times in ns of the engine's monotonic clock, device

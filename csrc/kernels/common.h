@@ -27,23 +27,13 @@ constexpr int kHeader = 64;
 // into the GPU's address space, never LDS.
 #define CCFD_GAS __attribute__((address_space(1)))
 typedef unsigned ccfd_u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned ccfd_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 template <class T>
 __device__ __forceinline__ void st_g(T* p, T v) { *(CCFD_GAS T*)p = v; }
 template <class T>
 __device__ __forceinline__ T ld_g(const T* p) { return *(const CCFD_GAS T*)p; }
-typedef unsigned ccfd_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint2 ld_g8(const void* p) {             // 8-byte aligned
-  const ccfd_u32x2 v = *(const CCFD_GAS ccfd_u32x2*)p;
-  return make_uint2(v.x, v.y);
-}
 __device__ __forceinline__ uint4 ld_g16(const void* p) {            // 16-byte aligned
   const ccfd_u32x4 v = *(const CCFD_GAS ccfd_u32x4*)p;
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint4 ld_g16_a4(const void* p) {         // 4-byte aligned
-  const ccfd_u32x4_a4 v = *(const CCFD_GAS ccfd_u32x4_a4*)p;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ float4 ld_g16f(const void* p) {
@@ -337,72 +327,6 @@ __device__ __forceinline__ void wire_issue(const unsigned char* __restrict__ x, 
                                            WireRegs& r) {
   const int row = tile * kTileRows + c;
   r.v = row < n ? ld_g16(x + (size_t)row * CCFD_WIRE_ROW_BYTES + 16 * g) : make_uint4(0u, 0u, 0u, 0u);
-}
-
-// The same tile in 8-byte lanes (compile-time CCFD_W64_FETCH_X2, A/B builds): instruction h covers rows 8h..8h+7 --
-// 512 contiguous bytes, lane l at byte 512h + 8l -- and wire_handoff passes lane (g, c) its
-// 16 bytes of row c through a wave-private 1 KB LDS buffer.  Zero-copy reads of pinned host
-// memory run at 57.5 GB/s with 4- or 8-byte lanes and 55.5 GB/s with 16-byte lanes
-// (bench/experiments/load_width_probe.py).
-struct WireRegs2 { uint2 v[2]; };
-
-__device__ __forceinline__ void wire_issue2(const unsigned char* __restrict__ x, int n, int tile, int lane,
-                                            WireRegs2& r) {
-  const unsigned char* t = x + (size_t)tile * kTileRows * CCFD_WIRE_ROW_BYTES;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = tile * kTileRows + 8 * h + (lane >> 3);
-    r.v[h] = row < n ? ld_g8(t + 512 * h + 8 * lane) : make_uint2(0u, 0u);
-  }
-}
-
-__device__ __forceinline__ void wire_handoff(uint2* __restrict__ lds, int lane, int c, int g, const WireRegs2& r,
-                                             WireRegs& out) {
-  lds[lane] = r.v[0];
-  lds[64 + lane] = r.v[1];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  out.v = reinterpret_cast<const uint4*>(lds)[4 * c + g];     // row c, bytes [16g, 16g+16)
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
-// The same tile in 4-byte lanes with an in-register transpose (compile-time
-// CCFD_W64_FETCH_Q4, A/B builds): instruction j reads rows 4j..4j+3 -- 256 contiguous bytes,
-// lane 4Q+t takes dword 4(Q>>2)+t of row 4j+(Q&3) -- and a 4x4 transpose inside every quad
-// (two DPP quad_perm butterflies, no LDS) leaves lane (g, c) holding bytes [16g, 16g+16) of
-// row wire_q4_row(c) = 4(c&3) + (c>>2): the MFMA operand layout with the tile's 16 columns
-// permuted, so the epilogue indexes rows through wire_q4_row.
-__device__ __forceinline__ int wire_q4_row(int c) { return 4 * (c & 3) + (c >> 2); }
-
-__device__ __forceinline__ void wire_issue_q4(const unsigned char* __restrict__ x, int n, int tile, int lane,
-                                              WireRegs& r) {
-  const unsigned char* t = x + (size_t)tile * kTileRows * CCFD_WIRE_ROW_BYTES;
-  const int q = lane >> 2, tq = lane & 3;
-  const int off = 4 * (4 * (q >> 2) + tq);
-  unsigned v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = 4 * j + (q & 3);
-    v[j] = tile * kTileRows + row < n ? ld_g(reinterpret_cast<const unsigned*>(t + row * CCFD_WIRE_ROW_BYTES + off))
-                                      : 0u;
-  }
-  r.v = make_uint4(v[0], v[1], v[2], v[3]);
-}
-
-__device__ __forceinline__ void wire_q4_transpose(int lane, WireRegs& r) {
-  unsigned a0 = r.v.x, a1 = r.v.y, a2 = r.v.z, a3 = r.v.w;
-  const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0;
-  // quad_perm [1,0,3,2] = 0xB1 (partner t^1), [2,3,0,1] = 0x4E (partner t^2)
-  unsigned s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b0 ? a0 : a1), 0xB1, 0xF, 0xF, false);
-  if (b0) a0 = s; else a1 = s;
-  s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b0 ? a2 : a3), 0xB1, 0xF, 0xF, false);
-  if (b0) a2 = s; else a3 = s;
-  s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b1 ? a0 : a2), 0x4E, 0xF, 0xF, false);
-  if (b1) a0 = s; else a2 = s;
-  s = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b1 ? a1 : a3), 0x4E, 0xF, 0xF, false);
-  if (b1) a1 = s; else a3 = s;
-  r.v = make_uint4(a0, a1, a2, a3);
 }
 
 __device__ __forceinline__ void wire_features(const WireRegs& r, int g, float xv[8]) {

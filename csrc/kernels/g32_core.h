@@ -30,10 +30,6 @@
 #include "common.h"
 #include "rules.h"
 
-#ifndef CCFD_G20_FETCH_X4
-#define CCFD_G20_FETCH_X4 0
-#endif
-
 #ifndef CCFD_G32_TREE_BLOCK
 #define CCFD_G32_TREE_BLOCK 4
 #endif
@@ -122,52 +118,6 @@ __device__ __forceinline__ void g20_rows(uint4* __restrict__ t4, int lane, G32Ro
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// G20 chunk in 16-byte lanes (compile-time CCFD_G20_FETCH_X4, A/B builds): lane l loads
-// bytes [16l, 16l+16) and lanes 0..15 also [1024+16l, ...), so the 1280 B chunk is two wave
-// instructions -- one contiguous 1 KB request and one 256 B request -- instead of five
-// 256 B ones.  A micro-batch may start at any row, so the vectors are only 4-byte aligned;
-// the batch's last chunk loads dword by dword up to its last byte.
-
-__device__ __forceinline__ uint4 g20_tail4(const unsigned char* __restrict__ x, long o, long nb) {
-  const unsigned* __restrict__ xw = reinterpret_cast<const unsigned*>(x);
-  uint4 v;
-  v.x = o + 4 <= nb ? ld_g(xw + (o >> 2) + 0) : 0u;
-  v.y = o + 8 <= nb ? ld_g(xw + (o >> 2) + 1) : 0u;
-  v.z = o + 12 <= nb ? ld_g(xw + (o >> 2) + 2) : 0u;
-  v.w = o + 16 <= nb ? ld_g(xw + (o >> 2) + 3) : 0u;
-  return v;
-}
-
-__device__ __forceinline__ void g20_fetch_x4(const unsigned char* __restrict__ x, int n, int chunk, int lane,
-                                             G32Row& r) {
-  constexpr long kChunk = (long)kG32Rows * CCFD_G20_ROW_BYTES;
-  const long nb = (long)n * CCFD_G20_ROW_BYTES;
-  const long c0 = (long)chunk * kChunk;
-  const long o0 = c0 + 16 * lane, o1 = c0 + 1024 + 16 * lane;
-  if (c0 + kChunk <= nb) {                                   // wave-uniform: a whole chunk
-    r.lo = ld_g16_a4(x + o0);
-    if (lane < 16) r.hi = ld_g16_a4(x + o1);
-  } else {
-    r.lo = g20_tail4(x, o0, nb);
-    if (lane < 16) r.hi = g20_tail4(x, o1, nb);
-  }
-}
-
-__device__ __forceinline__ void g20_rows_x4(uint4* __restrict__ t4, int lane, G32Row& r) {
-  t4[lane] = r.lo;
-  if (lane < 16) t4[64 + lane] = r.hi;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const unsigned* q = reinterpret_cast<const unsigned*>(t4) + kG20Words * lane;
-  r.lo.x = q[0];
-  r.lo.y = q[1];
-  r.lo.z = q[2];
-  r.lo.w = q[3];
-  r.hi.x = q[4];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
 // Lift a transposed G20 row's 30 five-bit bins (compile-time offsets: one v_bfe, or a
 // v_alignbit + v_and where a field straddles two dwords); returns bucket | stamp << 8.
 __device__ __forceinline__ unsigned g20_lift(const G32Row& r, unsigned (&b)[kF]) {
@@ -234,14 +184,12 @@ __device__ __forceinline__ unsigned g32_lift(const G32Row& r, unsigned (&b)[kF])
 // Row-format policy of the binned-row kernels: G32 (u8 bins) or G20 (5-bit bins).
 template <bool kG20>
 __device__ __forceinline__ void gx_fetch(const unsigned char* __restrict__ x, int n, int chunk, int lane, G32Row& r) {
-  if constexpr (kG20 && CCFD_G20_FETCH_X4) g20_fetch_x4(x, n, chunk, lane, r);
-  else if constexpr (kG20) g20_fetch(x, n, chunk, lane, r);
+  if constexpr (kG20) g20_fetch(x, n, chunk, lane, r);
   else g32_fetch(x, n, chunk, lane, r);
 }
 template <bool kG20>
 __device__ __forceinline__ void gx_rows(uint4* __restrict__ t, int lane, G32Row& r) {
-  if constexpr (kG20 && CCFD_G20_FETCH_X4) g20_rows_x4(t, lane, r);
-  else if constexpr (kG20) g20_rows(t, lane, r);
+  if constexpr (kG20) g20_rows(t, lane, r);
   else g32_rows(t, lane, r);
 }
 template <bool kG20>

@@ -28,20 +28,6 @@
 #include "persist_core.h"
 #include "rules.h"
 
-// A/B build knob (scripts/build_ab.py): W64 rows in 8-byte lanes + LDS hand-off (common.h
-// wire_issue2) instead of 16-byte lanes in the claimed-item kernel.
-#ifndef CCFD_W64_FETCH_X2
-#define CCFD_W64_FETCH_X2 0
-#endif
-// ... or in 4-byte lanes with an in-quad DPP transpose (common.h wire_issue_q4).
-#ifndef CCFD_W64_FETCH_Q4
-#define CCFD_W64_FETCH_Q4 0
-#endif
-// The pipelined (latency-mode) kernel's fetch: 4-byte lanes + DPP transpose when 1.
-#ifndef CCFD_PIPE_FETCH_Q4
-#define CCFD_PIPE_FETCH_Q4 0
-#endif
-
 namespace ccfd {
 
 int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s);   // score_gbdt_g32_persist.hip
@@ -126,8 +112,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     };
     // per-tile epilogue: outputs, route, counters, amount histogram, compacted fraud list;
     // xr = the tile's raw features (routing rules only)
-    auto finish = [&](float p, float amount, int tile, float (&xr)[8], bool q4 = false) __attribute__((always_inline)) {
-      const int row = tile * kTileRows + (q4 ? wire_q4_row(c) : c);   // q4: permuted tile columns
+    auto finish = [&](float p, float amount, int tile, float (&xr)[8]) __attribute__((always_inline)) {
+      const int row = tile * kTileRows + c;
       const bool valid = row < n;
       bool fr;
       if constexpr (kR) {                               // configurable routing rules (rules.h)
@@ -155,24 +141,12 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
     auto full_item = [&](auto kT) __attribute__((always_inline)) {
       constexpr int T = decltype(kT)::value;
       WireRegs r[T];
-      [[maybe_unused]] WireRegs2 r2[T];
 #pragma unroll
-      for (int k = 0; k < T; ++k) {
-        if constexpr (CCFD_W64_FETCH_X2) wire_issue2(xw, n, tile0 + 4 * k, lane, r2[k]);
-        else if constexpr (CCFD_W64_FETCH_Q4) wire_issue_q4(xw, n, tile0 + 4 * k, lane, r[k]);
-        else wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
-      }
+      for (int k = 0; k < T; ++k) wire_issue(xw, n, tile0 + 4 * k, c, g, r[k]);
 #pragma unroll
       for (int k = 0; k < T; k += 2) {
         const int ta = tile0 + 4 * k;
         if (ta * kTileRows >= n) break;                    // wave-uniform
-        if constexpr (CCFD_W64_FETCH_X2) {
-          wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k], r[k]);
-          wire_handoff(reinterpret_cast<uint2*>(tile_lds), lane, c, g, r2[k + 1], r[k + 1]);
-        } else if constexpr (CCFD_W64_FETCH_Q4) {
-          wire_q4_transpose(lane, r[k]);
-          wire_q4_transpose(lane, r[k + 1]);
-        }
         float pa, pb;
         float xa[8], xb[8];
         if (kModel == CCFD_MODEL_MLP) {
@@ -187,8 +161,8 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
           pa = lr_p(la);
           pb = lr_p(lb);
         }
-        finish(pa, __uint_as_float(r[k].v.w), ta, xa, CCFD_W64_FETCH_Q4 != 0);
-        finish(pb, __uint_as_float(r[k + 1].v.w), ta + 4, xb, CCFD_W64_FETCH_Q4 != 0);   // rows >= n: no-op epilogue
+        finish(pa, __uint_as_float(r[k].v.w), ta, xa);
+        finish(pb, __uint_as_float(r[k + 1].v.w), ta + 4, xb);   // rows >= n: no-op epilogue
       }
     };
     if (wire && kTilesPerWave == 2) {
@@ -335,10 +309,7 @@ __global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) 
     const int tile0 = (int)(it % (unsigned long long)C) * (4 * T) + wave;   // wave w: tiles tile0 + 4k
     const unsigned char* xw = reinterpret_cast<const unsigned char*>(d.x);
 #pragma unroll
-    for (int k = 0; k < T; ++k) {
-      if constexpr (CCFD_PIPE_FETCH_Q4) wire_issue_q4(xw, d.n, tile0 + 4 * k, lane, r[k]);
-      else wire_issue(xw, d.n, tile0 + 4 * k, c, g, r[k]);
-    }
+    for (int k = 0; k < T; ++k) wire_issue(xw, d.n, tile0 + 4 * k, c, g, r[k]);
   };
   // score item `it` (rows in r), counters into LDS, outputs to the host, then release + ticket
   auto score = [&](const ccfd_persist_desc& d, unsigned long long it, const WireRegs (&r_in)[T]) __attribute__((always_inline)) {
@@ -347,14 +318,11 @@ __global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) 
     const int tile0 = (int)(it % (unsigned long long)C) * (4 * T) + wave;
     WireRegs r[T];
 #pragma unroll
-    for (int k = 0; k < T; ++k) {
-      r[k] = r_in[k];
-      if constexpr (CCFD_PIPE_FETCH_Q4) wire_q4_transpose(lane, r[k]);
-    }
+    for (int k = 0; k < T; ++k) r[k] = r_in[k];
     unsigned nf_w = 0, nv_w = 0;
     unsigned long long ps_w = 0;
     auto finish = [&](float p, const WireRegs& rr, int tile) __attribute__((always_inline)) {
-      const int row = tile * kTileRows + (CCFD_PIPE_FETCH_Q4 ? wire_q4_row(c) : c);
+      const int row = tile * kTileRows + c;
       const bool valid = row < n;
       bool fr;
       if constexpr (kR) {

@@ -4,7 +4,11 @@ Load it with CCFD_LIB_PATH=<that path> (ops/_lib.py).  Compile-time variants kee
 default kernels free of runtime A/B branches (a runtime branch measurably slowed the
 default path, profiles/r3/load_width/README.md).
 
-    python scripts/build_ab.py --name x2 --src kernels/score_persist.hip -D CCFD_W64_FETCH_X2=1
+    python scripts/build_ab.py --name tb8 --src kernels/score_gbdt_g32_persist.hip -D CCFD_G32_TREE_BLOCK=8
+
+(The round-3 fetch-width variants measured with it -- W64 8- / 4-byte lanes, G20 16-byte
+lanes -- were removed from the sources after they lost; evidence: profiles/r3/load_width/,
+docs/ROUND3.md.)
 """
 import argparse
 import subprocess

@@ -1,0 +1,179 @@
+"""Durable kafka-lite: segments + offset index + committed offsets +
+idempotent-producer state survive a broker crash; torn tails are truncated, a lost index is
+rebuilt, retention deletes whole segments; a SIGKILLed kafka-lite process restarted from its
+data directory serves every acknowledged record exactly once (producers retry; their
+sequence numbers make the retried batches land once)."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from ccfd_demo_summit_amd.ingest.batch_store import OutOfOrderSequence
+from ccfd_demo_summit_amd.ingest.durable_store import DurableBatchStore
+from ccfd_demo_summit_amd.ingest.kafka_wire import decode_record_batches, encode_record_batch
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _batch(vals, pid=-1, seq=0):
+    import struct
+    from ccfd_demo_summit_amd.ingest.kafka_wire import crc32c
+    b = bytearray(encode_record_batch([v if isinstance(v, bytes) else v.encode() for v in vals]))
+    if pid >= 0:
+        struct.pack_into(">qhi", b, 43, pid, 0, seq)
+        struct.pack_into(">I", b, 17, crc32c(memoryview(b)[21:]))
+    return bytes(b)
+
+
+def _values(store, topic, p):
+    recs = decode_record_batches(store.fetch_raw(topic, p, 0, 1 << 30), topic, p, verify_crc=True)
+    return [(r.offset, r.value) for r in recs]
+
+
+def test_logs_offsets_and_producers_survive_a_crash(tmp_path):
+    d = str(tmp_path / "kl")
+    s = DurableBatchStore(d, default_partitions=2, fsync="never")
+    s.create_topic("odh-demo", 2)
+    for k in range(20):
+        s.append_raw("odh-demo", k % 2, _batch([f"tx{k}-{i}" for i in range(5)], pid=7, seq=(k // 2) * 5))
+    s.commit("g", "odh-demo", 0, 30)
+    s.commit("g", "odh-demo", 1, 25)
+    before = {p: _values(s, "odh-demo", p) for p in range(2)}
+    # crash: nothing closed or fsync'd -- the writes are in the page cache
+    s2 = DurableBatchStore(d, fsync="never")
+    assert s2.topics() == {"odh-demo": 2}
+    for p in range(2):
+        assert _values(s2, "odh-demo", p) == before[p]
+        assert s2.end_offset("odh-demo", p) == 50
+    assert s2.committed("g", "odh-demo", 0) == 30 and s2.committed("g", "odh-demo", 1) == 25
+    assert s2.recovered["batches"] == 20 and s2.recovered["records"] == 100
+    # the producer's last sequence was recovered: a retry of its last batch is a duplicate,
+    # a gap is refused, the next batch appends
+    base, n = s2.append_raw("odh-demo", 0, _batch([f"tx18-{i}" for i in range(5)], pid=7, seq=45))
+    assert (base, n) == (45, 0) and s2.end_offset("odh-demo", 0) == 50
+    with pytest.raises(OutOfOrderSequence):
+        s2.append_raw("odh-demo", 0, _batch(["x"], pid=7, seq=77))
+    assert s2.append_raw("odh-demo", 0, _batch(["next"], pid=7, seq=50)) == (50, 1)
+    s2.close()
+    s3 = DurableBatchStore(d, fsync="never")
+    assert s3.end_offset("odh-demo", 0) == 51 and _values(s3, "odh-demo", 0)[-1] == (50, b"next")
+    s3.close()
+
+
+def test_torn_tail_is_truncated_and_index_rebuilt(tmp_path):
+    d = str(tmp_path / "kl")
+    s = DurableBatchStore(d, default_partitions=1, fsync="always")
+    s.create_topic("t", 1)
+    for k in range(4):
+        s.append_raw("t", 0, _batch([f"v{k}"] * 3))
+    s.close()
+    seg = sorted((Path(d) / "t-0").glob("*.log"))[-1]
+    good = seg.stat().st_size
+    with open(seg, "ab") as f:                     # a crash in the middle of the 5th batch
+        f.write(_batch(["torn"] * 3)[:40])
+    (seg.with_suffix(".idx")).write_bytes(b"")     # and a lost index
+    s2 = DurableBatchStore(d, fsync="never")
+    assert s2.recovered["torn_tails_truncated"] == 1
+    assert seg.stat().st_size == good and s2.end_offset("t", 0) == 12
+    assert len(seg.with_suffix(".idx").read_bytes()) == 4 * 16
+    assert [v for _o, v in _values(s2, "t", 0)] == [f"v{k}".encode() for k in range(4) for _ in range(3)]
+    assert s2.append_raw("t", 0, _batch(["after"])) == (12, 1)
+    s2.close()
+
+
+def test_retention_deletes_whole_segments(tmp_path):
+    d = str(tmp_path / "kl")
+    s = DurableBatchStore(d, default_partitions=1, retention_batches=10, fsync="never", segment_bytes=2000)
+    s.create_topic("t", 1)
+    for k in range(60):
+        s.append_raw("t", 0, _batch([f"value-{k:04d}" * 4] * 4))
+    segs = sorted((Path(d) / "t-0").glob("*.log"))
+    first_base = int(segs[0].stem)
+    assert s.begin_offset("t", 0) == 50 * 4 and first_base <= 200
+    assert len(segs) < 20                           # old segments were deleted
+    s2 = DurableBatchStore(d, retention_batches=10, fsync="never", segment_bytes=2000)
+    assert s2.begin_offset("t", 0) == 200 and s2.end_offset("t", 0) == 240
+    s.close()
+    s2.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _start(port, d):
+    return subprocess.Popen([sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
+                             "--port", str(port), "--partitions", "2", "--metrics-port", "0", "--data-dir", d],
+                            cwd=str(ROOT), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                            env=dict(os.environ, PYTHONPATH=str(ROOT)))
+
+
+def _wait(port, t=60):
+    t0 = time.time()
+    while time.time() - t0 < t:
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+            return
+        except OSError:
+            time.sleep(0.1)
+    raise TimeoutError
+
+
+def test_sigkilled_broker_restarts_from_disk_exactly_once(tmp_path):
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    port = _free_port()
+    d = str(tmp_path / "data")
+    proc = _start(port, d)
+    try:
+        _wait(port)
+        prod = KafkaBroker(f"127.0.0.1:{port}", idempotent=True, connect_wait_s=30)
+        prod.create_topic("odh-demo", 2)
+        sent = 0
+        killed = restarted = False
+        t0 = time.time()
+        import threading
+
+        def chaos():
+            nonlocal proc, killed, restarted
+            time.sleep(0.4)
+            proc.send_signal(signal.SIGKILL)        # a crashed broker pod
+            proc.wait(10)
+            killed = True
+            time.sleep(1.0)
+            proc = _start(port, d)                  # restartPolicy: Always
+            restarted = True
+        th = threading.Thread(target=chaos)
+        th.start()
+        while sent < 400 * 50:
+            k = sent // 50
+            prod.produce_batch("odh-demo", k % 2, [f"{sent + i}".encode() for i in range(50)])
+            sent += 50
+            if killed and not restarted:
+                time.sleep(0.01)
+        th.join()
+        assert killed and restarted and time.time() - t0 < 120
+        prod.commit("g", "odh-demo", 0, 100) if hasattr(prod, "commit") else None
+        cons = KafkaBroker(f"127.0.0.1:{port}", connect_wait_s=30)
+        got = []
+        for p in range(2):
+            off = 0
+            end = cons.end_offset("odh-demo", p)
+            while off < end:
+                recs = cons.fetch("odh-demo", p, off, 10_000)
+                got += [int(r.value) for r in recs]
+                off = recs[-1].offset + 1
+        assert len(got) == len(set(got)) == sent           # every acked record once
+        assert sorted(got) == list(range(sent))
+    finally:
+        proc.send_signal(signal.SIGKILL)
+        proc.wait(10)

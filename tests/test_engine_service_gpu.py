@@ -12,8 +12,8 @@ from ccfd_demo_summit_amd.models import build_model
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("score_thread", [True, False])
-def test_engine_service_end_to_end(gpu, score_thread):
+@pytest.mark.parametrize("loop", ["native", "python-thread", "python-inline"])
+def test_engine_service_end_to_end(gpu, loop):
     from ccfd_demo_summit_amd.ingest import InProcBroker, ProducerConfig, TransactionProducer
     from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
     from ccfd_demo_summit_amd.metrics import MetricsHub
@@ -34,7 +34,8 @@ def test_engine_service_end_to_end(gpu, score_thread):
     ctx = DistContext(0, 1, 0, gpu, "none")
     svc = EngineService(ctx, DeviceModel(m, gpu), broker, router,
                         EngineServiceConfig(batch=4096, depth=4, streams=2, ring_rows=16384, flush_us=200,
-                                            reduce_period_ms=1.0, score_thread=score_thread)).start()
+                                            reduce_period_ms=1.0, score_thread=loop == "python-thread",
+                                            native_serve=loop == "native")).start()
     total = 32_000
     t0 = time.time()
     while svc.rows_scored < total and time.time() - t0 < 60:
