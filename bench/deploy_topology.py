@@ -405,6 +405,12 @@ def main(argv=None):
                     q[s.labels["quantile"]] = s.value
         out["arrival_to_scored_p50_us"] = round(q.get("0.5", float("nan")) * 1e6, 1)
         out["arrival_to_scored_p99_us"] = round(q.get("0.99", float("nan")) * 1e6, 1)
+        # producer send (ccfd-ts record header) -> scored, per transaction, per rank
+        out["produce_to_scored_us"] = [
+            {"rank": r, "p50": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_p50_seconds") * 1e6, 1),
+             "p99": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_p99_seconds") * 1e6, 1),
+             "rows": int(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_rows"))}
+            for r in range(a.ranks)]
         model_texts = [http_text(f"http://127.0.0.1:{model_base + r}/prometheus") for r in range(a.ranks)]
         mt = "\n".join(model_texts)
         for qq in (0.5, 0.99):
@@ -426,6 +432,7 @@ def main(argv=None):
             wait_port(kie_port, 1)
         out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
         out["kie_duplicates"] = stats["duplicates"]
+        out["scored_to_process_started_us"] = stats.get("scored_to_started_us")
         out["standard_mode"] = a.standard_mode
         if a.standard_mode == "process":
             # every transaction started exactly one process: standard + fraud == incoming

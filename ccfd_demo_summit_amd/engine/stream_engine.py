@@ -199,6 +199,10 @@ class StepStats:
     dev_hist_rows: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
     last_seq: int = 0                    # batches that produced a "last scored" record
     last: Optional[LastScored] = None
+    # producer send -> scored (ring batches whose rows carried a send time, ccfd-ts header)
+    origin_batches: int = 0
+    origin_hist: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+    origin_hist_rows: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
 
 
 _FMT_BY_ROW_BYTES = {120: "f32", 64: "w64", 32: "g32", 20: "g20"}
@@ -217,7 +221,9 @@ def _stats(st: EngineStats) -> StepStats:
                      (st.dev_exec_ns / st.dev_batches * 1e-3) if st.dev_batches else 0.0,
                      np.ctypeslib.as_array(st.dev_hist).copy(),
                      np.ctypeslib.as_array(st.lat_hist_rows).copy(),
-                     np.ctypeslib.as_array(st.dev_hist_rows).copy(), int(st.last_seq), last)
+                     np.ctypeslib.as_array(st.dev_hist_rows).copy(), int(st.last_seq), last,
+                     int(st.origin_batches), np.ctypeslib.as_array(st.origin_hist).copy(),
+                     np.ctypeslib.as_array(st.origin_hist_rows).copy())
 
 
 class StreamEngine:

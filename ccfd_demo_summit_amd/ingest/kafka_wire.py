@@ -291,6 +291,59 @@ def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optiona
     return struct.pack(">qi", base_offset, batch_len) + head + after_crc
 
 
+PRODUCE_TS_HEADER = b"ccfd-ts"          # record header: producer send time, u64 BE ns (CLOCK_REALTIME)
+
+
+def with_produce_time(record_set, ts_ns: int) -> bytearray:
+    """``record_set`` with a ``ccfd-ts`` header (the send time, ns since the epoch) added to the
+    FIRST record of every uncompressed batch -- the origin stamp behind the engine's
+    produce -> scored latency (csrc/engine/kafka_consumer.cpp reads it).  Batch lengths are
+    fixed up; CRCs are NOT (the caller re-seals them, see ``seal_batches``)."""
+    src = memoryview(record_set)
+    out = bytearray()
+    o = 0
+    hdr = _varint(len(PRODUCE_TS_HEADER)) + PRODUCE_TS_HEADER + _varint(8) + struct.pack(">Q", ts_ns)
+    while o + 61 <= len(src):
+        blen = struct.unpack_from(">i", src, o + 8)[0]
+        end = o + 12 + blen
+        attrs, count = struct.unpack_from(">h", src, o + 21)[0], struct.unpack_from(">i", src, o + 57)[0]
+        if attrs & 0x7 or count <= 0:                       # compressed / empty: left as it is
+            out += src[o:end]
+            o = end
+            continue
+        q = o + 61
+        rlen, q1 = _read_varint(src, q)
+        rend = q1 + rlen
+        p = q1 + 1                                          # attributes
+        for _ in range(3):                                  # timestamp delta, offset delta, key length
+            v, p = _read_varint(src, p)
+        if v > 0:
+            p += v
+        vl, p = _read_varint(src, p)
+        p += max(vl, 0)
+        hc, ph = _read_varint(src, p)                       # header count
+        body = bytes(src[q1:p]) + _varint(hc + 1) + bytes(src[ph:rend]) + hdr
+        first = _varint(len(body)) + body
+        start = len(out)
+        out += src[o:o + 61]
+        out += first
+        out += src[rend:end]
+        struct.pack_into(">i", out, start + 8, len(out) - start - 12)
+        o = end
+    return out
+
+
+def seal_batches(b: bytearray) -> None:
+    """Recompute the CRC-32C of every batch of ``b`` in place."""
+    mv = memoryview(b)
+    o = 0
+    while o + 61 <= len(b):
+        blen = struct.unpack_from(">i", b, o + 8)[0]
+        struct.pack_into(">I", b, o + 17, crc32c(mv[o + 21:o + 12 + blen]))
+        o += 12 + blen
+    del mv
+
+
 def decode_record_batches(data: bytes, topic: str = "", partition: int = 0,
                           verify_crc: bool = True) -> List[Record]:
     out: List[Record] = []
@@ -328,8 +381,21 @@ def decode_record_batches(data: bytes, topic: str = "", partition: int = 0,
             q += max(kl, 0)
             vl, q = _read_varint(mv, q)
             val = None if vl < 0 else bytes(mv[q:q + vl])
+            q += max(vl, 0)
+            hdrs = ()
+            hc, q = _read_varint(mv, q)
+            if hc > 0:
+                hl = []
+                for _h in range(hc):
+                    hk, q = _read_varint(mv, q)
+                    k_ = bytes(mv[q:q + hk]).decode("utf-8", "replace")
+                    q += hk
+                    hv, q = _read_varint(mv, q)
+                    hl.append((k_, None if hv < 0 else bytes(mv[q:q + hv])))
+                    q += max(hv, 0)
+                hdrs = tuple(hl)
             q = rend
-            out.append(Record(topic, partition, base_offset + od, key, val, (base_ts + tsd) / 1000.0))
+            out.append(Record(topic, partition, base_offset + od, key, val, (base_ts + tsd) / 1000.0, hdrs))
         mv = mv_outer
         o = end
     return out
@@ -426,6 +492,9 @@ class KafkaBroker:
         re-sent after a lost ack or a broker restart is stored once (the broker answers a
         duplicate with its original offset)."""
         self.idempotent = bool(idempotent)
+        # stamp_time: the ccfd-ts send-time header on the first record of every batch (the
+        # engine's produce -> scored latency); set by the transaction producer
+        self.stamp_time = False
         self._pid: Optional[Tuple[int, int]] = None
         self._seq: Dict[Tuple[str, int], int] = {}
         self._seq_locks: Dict[Tuple[str, int], threading.Lock] = {}
@@ -574,39 +643,41 @@ class KafkaBroker:
             raise BrokerError(f"InitProducerId error {err}")
         return pid, epoch
 
-    def _stamp_sequence(self, topic: str, partition: int, record_set) -> Tuple[bytearray, int]:
-        """Write (producer id, epoch, base sequence) into every batch of ``record_set`` and
-        re-seal its CRC; returns (the stamped copy, records in it)."""
+    def _stamp_sequence(self, topic: str, partition: int, b: bytearray) -> int:
+        """Write (producer id, epoch, base sequence) into every batch of ``b`` (in place, CRC
+        not re-sealed); returns the records in it."""
         if self._pid is None:
             self._pid = self.init_producer_id()
         pid, epoch = self._pid
-        b = bytearray(record_set)
-        mv = memoryview(b)
         seq = self._seq.get((topic, partition), 0)
         o = n_total = 0
         while o + 61 <= len(b):
             blen = struct.unpack_from(">i", b, o + 8)[0]
             count = struct.unpack_from(">i", b, o + 57)[0]
             struct.pack_into(">qhi", b, o + 43, pid, epoch, seq)
-            struct.pack_into(">I", b, o + 17, crc32c(mv[o + 21:o + 12 + blen]))
             seq += count
             n_total += count
             o += 12 + blen
-        del mv
-        return b, n_total
+        return n_total
 
     def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
-        if self.idempotent:
-            key = (topic, partition)
-            with self._seq_guard:
-                lk = self._seq_locks.setdefault(key, threading.Lock())
-            with lk:                     # sequence order == send order on a partition
-                stamped, n = self._stamp_sequence(topic, partition, record_set)
-                base = self._produce_raw(topic, partition, stamped, acks)   # retries resend the same seq
-                self._seq[key] = self._seq.get(key, 0) + n
-                return base
-        return self._produce_raw(topic, partition, record_set, acks)
+        if not (self.idempotent or self.stamp_time):
+            return self._produce_raw(topic, partition, record_set, acks)
+        # one copy: the produce-time header splice (or a plain copy), sequence stamps, one seal
+        b = with_produce_time(record_set, time.time_ns()) if self.stamp_time else bytearray(record_set)
+        if not self.idempotent:
+            seal_batches(b)
+            return self._produce_raw(topic, partition, b, acks)
+        key = (topic, partition)
+        with self._seq_guard:
+            lk = self._seq_locks.setdefault(key, threading.Lock())
+        with lk:                         # sequence order == send order on a partition
+            n = self._stamp_sequence(topic, partition, b)
+            seal_batches(b)
+            base = self._produce_raw(topic, partition, b, acks)   # retries resend the same seq
+            self._seq[key] = self._seq.get(key, 0) + n
+            return base
 
     def _produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         # [acks, timeout, 1 topic, 1 partition, record set size] + the record set itself, sent

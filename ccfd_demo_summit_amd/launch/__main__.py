@@ -384,6 +384,7 @@ def cmd_producer(a, cfg):
     if a.csv:
         pc.source, pc.csv_path = "csv", a.csv
     broker = _broker(cfg, idempotent=True)
+    broker.stamp_time = True          # ccfd-ts send-time header: the engine's produce -> scored latency
     prod = TransactionProducer(broker, pc)
     if a.fmt == "json" and pc.source == "synthetic":
         prod._ensure_pool()                 # render the message pool before the clock starts

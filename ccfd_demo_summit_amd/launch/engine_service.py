@@ -214,6 +214,7 @@ class EngineService:
         self.last_scored = None
         self._lat_rows_cum = np.zeros(256, np.int64)
         self._dev_rows_cum = np.zeros(256, np.int64)
+        self._origin_rows_cum = np.zeros(256, np.int64)   # producer send -> scored, per transaction
         # CCFD_SERVICE_TRACE=<dir>: tail attribution (bench/tail_attribution.py) -- the engine's
         # per-batch stage trace plus this process's scoring-loop timeline (every run() call, every
         # task, every GC pause, hand-off holds), dumped to <dir>/rank<r>.npz at stop()
@@ -368,7 +369,9 @@ class EngineService:
             if st.last_seq:
                 self.last_scored = st.last
             if st.dev_batches:
-                self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
+                self.kernel_exec_mean_us = st.dev_exec_mean_us
+            self._origin_rows_cum = st.origin_hist_rows.astype(np.int64)     # K7, cumulative mean
+            self._origin_rows_cum = st.origin_hist_rows.astype(np.int64)
         return int(st.rows)
 
     def _collect_native(self) -> int:
@@ -474,6 +477,7 @@ class EngineService:
             sd, self._standard_new = self._standard_new, []
             snap, self._commit_snap = self._commit_snap, {}
             lat_cum = self._lat_cum
+        self.router.scored_ns = time.time_ns()          # hand-off items carry it: scored -> started at KIE
         flagged = np.concatenate(fl) if len(fl) > 1 else (fl[0] if fl else np.zeros(0, FLAGGED_NP))
         standard = (np.concatenate(sd) if len(sd) > 1 else sd[0]) if sd else None
         seq = -1
@@ -639,6 +643,13 @@ class EngineService:
                          handoff_dead_letter_total=hs.get("dead_lettered", 0))
         if self.standard_mode == "process":
             extra.update(standard_started=getattr(self.router, "standard_started", 0))
+        with self._stat_lock:
+            oh = self._origin_rows_cum.copy()
+        if oh.sum() > 0:                        # rows that carried their producer's send time
+            from ..parallel.dp import hist_quantile
+            extra.update(produce_to_scored_p50_seconds=hist_quantile(oh, 0.5) * 1e-9,
+                         produce_to_scored_p99_seconds=hist_quantile(oh, 0.99) * 1e-9,
+                         produce_to_scored_rows=int(oh.sum()))
         return c, lat, extra
 
     def model_source(self) -> dict:

@@ -64,7 +64,9 @@ class EngineStats(C.Structure):
                 ("dev_hist", C.c_uint64 * 256), ("lat_hist_rows", C.c_uint64 * 256),
                 ("dev_hist_rows", C.c_uint64 * 256), ("last_seq", C.c_uint64), ("last_tx_id", C.c_uint64),
                 ("last_proba", C.c_float), ("last_amount", C.c_float), ("last_partition", C.c_int32),
-                ("last_row_bytes", C.c_int32), ("last_row", C.c_uint8 * 128)]
+                ("last_row_bytes", C.c_int32), ("last_row", C.c_uint8 * 128),
+                ("origin_batches", C.c_uint64), ("origin_hist", C.c_uint64 * 256),
+                ("origin_hist_rows", C.c_uint64 * 256)]
 
 
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),
@@ -143,6 +145,7 @@ def lib() -> C.CDLL:
         L.ccfd_engine_ring_acquire.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.POINTER(C.c_int64)]
         L.ccfd_engine_ring_acquire.restype = C.c_int64
         L.ccfd_engine_ring_commit.argtypes = [C.c_void_p, C.c_int, C.c_int64]
+        L.ccfd_engine_ring_commit_at.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64]
         L.ccfd_engine_run.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(EngineStats)]
         L.ccfd_crc32c.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
         L.ccfd_crc32c.restype = C.c_uint32

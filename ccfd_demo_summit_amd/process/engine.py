@@ -118,6 +118,9 @@ class ProcessEngine:
         self._std_by_tx: Dict[Any, int] = {}
         self._std_order: collections.deque = collections.deque()
         self.standard_duplicates = 0
+        # scored -> process started (the engine's hand-off items carry ``scored_ns``, the wall
+        # clock their results were collected): 4 buckets per octave of ns, like the engine's
+        self.handoff_hist = [0] * 256
 
     @classmethod
     def from_config(cls, kie_cfg, **kw) -> "ProcessEngine":
@@ -236,6 +239,9 @@ class ProcessEngine:
         cols = columns_of(items)
         txs = cols.get("transaction_id") or cols.get("tx_id")
         n = _ncols(cols)
+        sc = cols.pop("scored_ns", None)
+        if sc:
+            self._note_handoff(sc[0], n)
         out: List[int] = []
         new_pos: List[int] = []
         with self._lock:
@@ -263,9 +269,34 @@ class ProcessEngine:
                 self._journal.write(json.dumps({"standard": rec}, default=float) + "\n")
         return out
 
+    def _note_handoff(self, scored_ns, n: int = 1) -> None:
+        if not scored_ns or n <= 0:
+            return
+        dt = time.time_ns() - int(scored_ns)
+        if dt > 0:
+            import math
+            self.handoff_hist[min(255, int(4.0 * math.log2(dt)))] += n
+
+    def handoff_latency_us(self) -> Dict[str, Any]:
+        """p50 / p99 of scored -> started over every start that carried ``scored_ns``."""
+        h = self.handoff_hist
+        tot = sum(h)
+        if not tot:
+            return {"n": 0}
+        out = {"n": tot}
+        for q, name in ((0.5, "p50"), (0.99, "p99")):
+            k, c = q * (tot - 1), 0
+            for i, v in enumerate(h):
+                c += v
+                if c > k:
+                    out[name] = round(2.0 ** ((i + 0.5) / 4.0) / 1e3, 1)   # bucket mid, us
+                    break
+        return out
+
     def start_fraud(self, variables: Dict[str, Any]) -> int:
         """Idempotent per transaction id: at-least-once delivery (a re-scored transaction
         after a rank fail-over) returns the existing instance instead of starting another."""
+        self._note_handoff(variables.get("scored_ns"))
         txid = variables.get("transaction_id", variables.get("tx_id"))
         with self._lock:
             if txid is not None and txid in self._by_tx:

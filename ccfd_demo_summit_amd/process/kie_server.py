@@ -179,6 +179,7 @@ class KieServer:
             fraud = sum(1 for i in e.instances.values() if i.process_id == e.FRAUD)
             body = {"fraud_instances_retained": fraud, "fraud_started": len(e._by_tx), "duplicates": e.duplicates,
                     "standard_started": e.standard_count, "standard_duplicates": e.standard_duplicates,
+                    "scored_to_started_us": e.handoff_latency_us(),
                     "active": sum(1 for i in e.instances.values()
                                                                         if i.state.value != "completed"),
                     "outcomes": dict(e.outcome_counts), "next_instance_id": None}

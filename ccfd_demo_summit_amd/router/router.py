@@ -55,6 +55,9 @@ class Router:
         self.handoff = handoff
         self.last_handoff_seq = -1
         self.standard_started = 0
+        # wall-clock ns the current batch of results was collected from the engine (set by the
+        # engine service): hand-off items carry it, KIE measures scored -> process started
+        self.scored_ns: Optional[int] = None
 
     # ------------------------------------------------------------------ scoring results
     def on_scored(self, ids, customers, proba, X: Optional[np.ndarray] = None,
@@ -108,10 +111,16 @@ class Router:
         std_cols = None
         if self.standard_mode == "process" and standard is not None and len(standard):
             std_cols = standard_columns(standard)
+            if self.scored_ns:
+                std_cols["scored_ns"] = [self.scored_ns] * len(standard)
         if self.handoff is not None:                        # async, retried, acked later
             seq = -1
             if nf:
+                ts = self.scored_ns
                 seq = self.handoff.submit_starts(
+                    [{"transaction_id": int(r["tx_id"]), "customer_id": int(r["customer"]),
+                      "amount": float(r["amount"]), "proba": float(r["proba"]), "scored_ns": ts}
+                     for r in flagged] if ts else
                     [{"transaction_id": int(r["tx_id"]), "customer_id": int(r["customer"]),
                       "amount": float(r["amount"]), "proba": float(r["proba"])} for r in flagged])
                 with self._lock:

@@ -81,16 +81,17 @@ struct Partition {
   bool ring = false;
   ccfd::RowRing rr;                  // SPSC row ring (csrc/engine/spsc_ring.h)
   std::mutex arr_mu;
-  std::deque<std::pair<int64_t, int64_t>> arrivals;   // (head after commit, t_ns)
+  struct Arrival { int64_t head, t, origin; };       // head after commit, commit time, producer send time
+  std::deque<Arrival> arrivals;
 
-  int64_t arrival_of(int64_t row) {   // commit time of `row`
+  Arrival arrival_of(int64_t row) {   // commit (and origin) time of `row`
     std::lock_guard<std::mutex> lk(arr_mu);
-    for (auto& a : arrivals) if (a.first > row) return a.second;
-    return arrivals.empty() ? 0 : arrivals.back().second;
+    for (auto& a : arrivals) if (a.head > row) return a;
+    return arrivals.empty() ? Arrival{0, 0, 0} : arrivals.back();
   }
   void forget_before(int64_t row) {
     std::lock_guard<std::mutex> lk(arr_mu);
-    while (!arrivals.empty() && arrivals.front().first <= row) arrivals.pop_front();
+    while (!arrivals.empty() && arrivals.front().head <= row) arrivals.pop_front();
   }
 };
 
@@ -101,6 +102,7 @@ struct Slot {
   int32_t rows = 0;
   int64_t t_submit = 0;
   int64_t t_arrival = 0;           // ring mode: commit time of the batch's first row
+  int64_t t_origin = 0;            // ring mode: producer send time of that row (0 = unknown)
   float* d_x = nullptr;
   float* d_proba = nullptr;
   uint8_t* d_route = nullptr;
@@ -160,6 +162,7 @@ class Engine {
   uint64_t t_submit_ns = 0, t_wait_ns = 0, t_complete_ns = 0;
   uint64_t dev_batches = 0, dev_exec_ns = 0, dev_hist[256] = {};
   uint64_t lat_hist_rows[256] = {}, dev_hist_rows[256] = {};   // row-weighted (Seldon histograms)
+  uint64_t origin_batches = 0, origin_hist[256] = {}, origin_hist_rows[256] = {};   // produce -> scored
   // last completed transaction (model "last request" gauges)
   uint64_t last_seq = 0, last_tx_id = 0;
   float last_proba = 0.f, last_amount = 0.f;
@@ -735,6 +738,12 @@ class Engine {
       lat_hist[b]++;
       lat_hist_rows[b] += (uint64_t)s.rows;
     }
+    if (s.t_origin > 0 && t_landed > s.t_origin) {        // producer send -> results in host memory
+      const int b = std::min(255, (int)std::floor(4.0 * std::log2((double)(t_landed - s.t_origin))));
+      ++origin_batches;
+      origin_hist[b]++;
+      origin_hist_rows[b] += (uint64_t)s.rows;
+    }
     uint64_t nf = 0;
     if (s.use_flag) {
       nf = s.done_ptr[1];
@@ -774,6 +783,7 @@ class Engine {
     }
     s.busy = false;
     s.t_arrival = 0;
+    s.t_origin = 0;
     completed_upto = std::max<int64_t>(completed_upto, s.seq_no + 1);
     t_complete_ns += now_ns() - t;
     return 0;
@@ -958,6 +968,9 @@ class Engine {
     std::fill(lat_fine.begin(), lat_fine.end(), 0ull);
     std::memset(lat_hist, 0, sizeof(lat_hist));
     std::memset(lat_hist_rows, 0, sizeof(lat_hist_rows));
+    origin_batches = 0;
+    std::memset(origin_hist, 0, sizeof(origin_hist));
+    std::memset(origin_hist_rows, 0, sizeof(origin_hist_rows));
   }
 
   void fill_latency(ccfd_engine_stats* st) {
@@ -977,6 +990,9 @@ class Engine {
     st->last_partition = last_partition;
     st->last_row_bytes = rowf * (int32_t)sizeof(float);
     std::memcpy(st->last_row, last_row, sizeof(last_row));
+    st->origin_batches = origin_batches;
+    std::memcpy(st->origin_hist, origin_hist, sizeof(origin_hist));
+    std::memcpy(st->origin_hist_rows, origin_hist_rows, sizeof(origin_hist_rows));
     if (lat_n == 0) return;
     st->lat_p50_us = fine_quantile(0.50);
     st->lat_p99_us = fine_quantile(0.99);
@@ -1082,12 +1098,13 @@ class Engine {
     return parts[p]->rr.acquire(want, row);
   }
 
-  int ring_commit(int p, int64_t n) {
+  int ring_commit(int p, int64_t n, int64_t origin_ns = 0) {
     if (p < 0 || p >= (int)parts.size() || !parts[p]->ring) return -1;
     Partition& P = *parts[p];
     {
       std::lock_guard<std::mutex> lk(P.arr_mu);
-      P.arrivals.emplace_back(P.rr.head_count() + n, now_ns());
+      const int64_t t = now_ns();
+      P.arrivals.push_back(Partition::Arrival{P.rr.head_count() + n, t, origin_ns > 0 && origin_ns <= t ? origin_ns : 0});
     }
     P.rr.commit(n);                    // publish after the arrival stamp exists
     return 0;
@@ -1145,8 +1162,11 @@ class Engine {
           if (K >= 2) {
             int rc = submit_multi((int)q, phys, cfg.max_batch, K);
             if (rc) return rc;
-            for (int k = 0; k < K; ++k)
-              slots[(seq + k) % D].t_arrival = P.arrival_of(P.rr.taken() + (int64_t)k * cfg.max_batch);
+            for (int k = 0; k < K; ++k) {
+              const Partition::Arrival a = P.arrival_of(P.rr.taken() + (int64_t)k * cfg.max_batch);
+              slots[(seq + k) % D].t_arrival = a.t;
+              slots[(seq + k) % D].t_origin = a.origin;
+            }
             seq += K;
             submitted += K;
             P.rr.take((int64_t)K * cfg.max_batch);
@@ -1156,7 +1176,8 @@ class Engine {
           }
           int64_t rows = std::min<int64_t>({avail, (int64_t)cfg.max_batch, P.n - phys});
           const bool full = rows == cfg.max_batch || rows == P.n - phys;
-          const int64_t arr = P.arrival_of(P.rr.taken());
+          const Partition::Arrival arr_rec = P.arrival_of(P.rr.taken());
+          const int64_t arr = arr_rec.t;
           // a partial batch waits for more rows until its deadline -- unless the GPU has
           // nothing in flight (work-conserving: at low / moderate arrival rates a row is
           // scored right away instead of after flush_us; under load the in-flight batches
@@ -1170,6 +1191,7 @@ class Engine {
           int rc = submit(s, P.feats_dev + off, P.feats + off, (int)rows, stream);
           if (rc) return rc;
           s.t_arrival = arr;
+          s.t_origin = arr_rec.origin;
           ++seq;
           ++submitted;
           P.rr.take(rows);
@@ -1450,6 +1472,10 @@ int64_t ccfd_engine_ring_acquire(void* eng, int partition, int64_t want, int64_t
 
 int ccfd_engine_ring_commit(void* eng, int partition, int64_t n) {
   return static_cast<Engine*>(eng)->ring_commit(partition, n);
+}
+
+int ccfd_engine_ring_commit_at(void* eng, int partition, int64_t n, int64_t origin_ns) {
+  return static_cast<Engine*>(eng)->ring_commit(partition, n, origin_ns);
 }
 
 int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st) {

@@ -103,7 +103,8 @@ struct In {
 struct Sink {
   // ring-like contiguous acquire/commit of rows of a partition
   virtual int64_t acquire(int p, int64_t want, int64_t* row) = 0;
-  virtual void commit(int p, int64_t n) = 0;
+  // origin_ns: producer send time of these rows on the engine's steady clock (0 = unknown)
+  virtual void commit(int p, int64_t n, int64_t origin_ns) = 0;
   virtual uint8_t* feats(int p) = 0;
   virtual uint64_t* ids(int p) = 0;
   virtual uint32_t* cust(int p) = 0;
@@ -118,7 +119,9 @@ struct EngineSink : Sink {
   int64_t acquire(int p, int64_t want, int64_t* row) override {
     return ccfd_engine_ring_acquire(eng, parts[p].engine_partition, want, row);
   }
-  void commit(int p, int64_t n) override { ccfd_engine_ring_commit(eng, parts[p].engine_partition, n); }
+  void commit(int p, int64_t n, int64_t origin_ns) override {
+    ccfd_engine_ring_commit_at(eng, parts[p].engine_partition, n, origin_ns);
+  }
   uint8_t* feats(int p) override { return (uint8_t*)parts[p].feats; }
   uint64_t* ids(int p) override { return parts[p].ids; }
   uint32_t* cust(int p) override { return parts[p].customer; }
@@ -134,7 +137,11 @@ struct ArraySink : Sink {                  // tests: flat arrays, no wrap, "rele
     *row = used[p];
     return k;
   }
-  void commit(int p, int64_t n) override { used[p] += n; }
+  void commit(int p, int64_t n, int64_t origin_ns) override {
+    used[p] += n;
+    last_origin = origin_ns;
+  }
+  int64_t last_origin = 0;
   uint8_t* feats(int p) override { return (uint8_t*)parts[p].feats; }
   uint64_t* ids(int p) override { return parts[p].ids; }
   uint32_t* cust(int p) override { return parts[p].customer; }
@@ -180,6 +187,13 @@ class Consumer {
   std::atomic<uint64_t> n_records{0}, n_rows{0}, n_bytes{0}, n_errors{0}, n_fetches{0};
   std::atomic<uint64_t> n_meta{0}, n_resets{0}, n_leaders{0};
   std::atomic<uint64_t> t_io{0}, t_handle{0}, t_encode{0}, t_ring_wait{0};   // ns, see ccfd_kc_stats
+  // producer send time of the batch being ingested, on the steady clock: from the ccfd-ts
+  // header of its first record (ingest/kafka_wire.py with_produce_time), 0 when absent
+  int64_t cur_origin = 0;
+  static int64_t real_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+        .count();
+  }
   static int64_t mono_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
@@ -442,7 +456,7 @@ class Consumer {
       const int64_t te = mono_ns();
       fn(row, done, k);
       t_encode.fetch_add((uint64_t)(mono_ns() - te), std::memory_order_relaxed);
-      sink->commit(pi, k);
+      sink->commit(pi, k, cur_origin);
       done += k;
     }
     return true;
@@ -580,6 +594,7 @@ class Consumer {
         error(std::string("unsupported compression codec ") + (codec <= 4 ? names[codec] : "?"));
         return;                                      // never skip data silently: the partition stalls
       }
+      cur_origin = 0;
       for (int32_t i = 0; i < count && r.ok; ++i) {
         const int64_t rlen = r.varlong();
         if (!r.ok || rlen < 0 || rlen > r.e - r.p) { r.ok = false; break; }
@@ -596,7 +611,25 @@ class Consumer {
         // a value (or key) that runs past its record is a malformed batch (CRC only detects
         // corruption, any producer can build one): stop processing this batch
         if (!rec.ok || vlen > INT32_MAX || (vlen > 0 && val + vlen > rend)) { r.ok = false; break; }
-        r.p = rend;                                  // headers skipped
+        if (i == 0) {                                // the first record may carry the send time
+          const int64_t hc = rec.varlong();
+          for (int64_t h = 0; rec.ok && h < hc && h < 64; ++h) {
+            const int64_t hk = rec.varlong();
+            if (!rec.ok || hk < 0 || hk > rend - rec.p) break;
+            const uint8_t* key = rec.p;
+            rec.skip((size_t)hk);
+            const int64_t hv = rec.varlong();
+            if (!rec.ok || hv > rend - rec.p) break;
+            if (hk == 7 && hv == 8 && std::memcmp(key, "ccfd-ts", 7) == 0) {
+              uint64_t ts = 0;
+              for (int b = 0; b < 8; ++b) ts = (ts << 8) | rec.p[b];
+              const int64_t age = real_ns() - (int64_t)ts;       // send -> now (same host clock)
+              if (age >= 0 && age < 3600ll * 1000000000ll) cur_origin = mono_ns() - age;
+            }
+            if (hv > 0) rec.skip((size_t)hv);
+          }
+        }
+        r.p = rend;                                  // (other) headers skipped
         const int64_t off = base + od;
         PState& s = ps[pi];
         if (off < s.next_offset) continue;           // already consumed (batch starts below the fetch offset)

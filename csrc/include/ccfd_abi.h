@@ -280,6 +280,11 @@ typedef struct ccfd_engine_stats {
   int32_t last_partition;
   int32_t last_row_bytes;
   uint8_t last_row[128];
+  // producer send -> scored (results in host memory) per ring micro-batch whose rows carried a
+  // send time (ccfd_engine_ring_commit_at: the ccfd-ts record header); same bucketing as lat_hist
+  uint64_t origin_batches;
+  uint64_t origin_hist[256];
+  uint64_t origin_hist_rows[256];
 } ccfd_engine_stats;
 
 void* ccfd_engine_create(const ccfd_engine_config* cfg);
@@ -338,6 +343,9 @@ int ccfd_engine_set_ring(void* eng, int partition, float* feats, uint64_t* ids, 
                          int64_t capacity);
 int64_t ccfd_engine_ring_acquire(void* eng, int partition, int64_t want, int64_t* row);
 int ccfd_engine_ring_commit(void* eng, int partition, int64_t n);
+// ... with the producer send time of these rows on the engine's steady clock (ns, 0 = unknown):
+// feeds the produce -> scored histogram (ccfd_engine_stats.origin_hist)
+int ccfd_engine_ring_commit_at(void* eng, int partition, int64_t n, int64_t origin_ns);
 int ccfd_engine_run(void* eng, int64_t budget_us, int64_t flush_us, ccfd_engine_stats* st);
 void ccfd_engine_reset_stats(void* eng);
 // Native serving thread: a C++ thread calls ccfd_engine_run(budget_us, flush_us) back to back
