@@ -71,12 +71,15 @@ def probe_ok(target: tuple, timeout_s: float = 0.5) -> bool:
         return False
 
 
-def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offset: int = 0) -> Dict[str, tuple]:
+def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offset: int = 0,
+                   state_dir: str = ".ccfd-state") -> Dict[str, tuple]:
     """service -> (desired replicas, argv factory(replica index), env (a dict, or a factory of
     the replica index), probe) for a one-node run; every port is the service's reference
     port + ``port_offset`` (+ replica index).
     ``probe`` is (target factory(replica index), start seconds) -- the same health routes the
-    rendered readiness / liveness probes use (render.py) -- or None."""
+    rendered readiness / liveness probes use (render.py) -- or None.  ``state_dir`` holds what
+    must survive a restart: kafka-lite's logs, the KIE journal, the hand-off DLQ."""
+    state = os.path.abspath(state_dir)
     o = port_offset
     kafka_port = 9092 + o
     broker = (spec.kafka.bootstrap if not spec.kafka.deploy
@@ -89,14 +92,16 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
         env["ROUTER_RULES"] = spec.engine.rules
     env["ROUTER_STANDARD_MODE"] = spec.engine.standard_mode
     if spec.engine.handoff_dlq:
-        env["CCFD_HANDOFF_DLQ"] = spec.engine.handoff_dlq
+        # the CR names the pod path; locally the DLQ lives in the state directory
+        env["CCFD_HANDOFF_DLQ"] = os.path.join(state, os.path.basename(spec.engine.handoff_dlq))
     env.update(spec.env)
     w = ["--weights", spec.engine.weights] if spec.engine.weights else []
     svc: Dict[str, tuple] = {}
     if spec.kafka.deploy:
         svc["kafka"] = (1, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite",
                                       "--nodes", str(spec.kafka.brokers), "--port", str(kafka_port), "--host", host,
-                                      "--partitions", str(spec.kafka.partitions), "--metrics-port", str(9404 + o)])
+                                      "--partitions", str(spec.kafka.partitions), "--metrics-port", str(9404 + o),
+                                      "--data-dir", os.path.join(state, "kafka-lite"), "--fsync", spec.kafka.fsync])
     if spec.usertask.deploy:
         svc["usertask"] = (spec.usertask.replicas, lambda r: PY + ["usertask", "--host", host, "--port", str(5000 + o + r)])
     if spec.seldon.deploy:
@@ -104,7 +109,8 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
                          + (["--native", "--workers", str(spec.seldon.workers)] if spec.seldon.native else []))
     if spec.kie.deploy:
         svc["kie"] = (spec.kie.replicas, lambda r: PY + ["kie", "--host", host, "--port", str(8090 + o + r),
-                                                         "--remote-prediction"])
+                                                         "--remote-prediction",
+                                                         "--journal", os.path.join(state, f"kie-journal-{r}.jsonl")])
     if spec.notifier.deploy:
         svc["notifier"] = (spec.notifier.replicas, lambda r: PY + ["notifier", "--host", host,
                                                                    "--port", str(8080 + o + r)])
@@ -148,9 +154,10 @@ class LocalOperator:
     def __init__(self, spec: FraudDetectionSpec, workdir: str = ".", status_path: Optional[str] = None,
                  commands: Optional[Dict[str, tuple]] = None, grace_s: float = 30.0, backoff_s: float = 1.0,
                  max_backoff_s: float = 30.0, log: Callable[[str], None] = print, port_offset: int = 0,
-                 liveness_failures: int = 6):
+                 liveness_failures: int = 6, state_dir: Optional[str] = None):
         self.spec = spec
         self.workdir = workdir
+        self.state_dir = state_dir or os.path.join(workdir, ".ccfd-state")
         self.status_path = status_path
         self.grace_s = grace_s
         self.backoff_s = backoff_s
@@ -161,7 +168,8 @@ class LocalOperator:
         self.port_offset = port_offset
         self.liveness_failures = liveness_failures
         self.services: Dict[str, ServiceState] = {}
-        self._commands = commands if commands is not None else local_commands(spec, port_offset=port_offset)
+        self._commands = commands if commands is not None else local_commands(spec, port_offset=port_offset,
+                                                                              state_dir=self.state_dir)
 
     # ------------------------------------------------------------------ spec changes
     def update(self, spec: FraudDetectionSpec) -> None:
@@ -169,7 +177,7 @@ class LocalOperator:
         self.spec = spec
         self.generation += 1
         if self._commands_override is None:
-            self._commands = local_commands(spec, port_offset=self.port_offset)
+            self._commands = local_commands(spec, port_offset=self.port_offset, state_dir=self.state_dir)
 
     def _env(self, name: str, r: int) -> Dict[str, str]:
         env = self._commands[name][2]

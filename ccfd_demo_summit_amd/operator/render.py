@@ -101,12 +101,23 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
         name = f"{spec.kafka.cluster_name}-kafka"
         ports = [{"containerPort": 9092 + i, "name": f"broker-{i}"} for i in range(spec.kafka.brokers)]
         ports.append({"containerPort": 9404, "name": "metrics"})
-        out.append(_workload("StatefulSet", name, name, 1, [_container(
+        # durable logs (ingest/durable_store.py): a restarted broker pod recovers every
+        # acknowledged record and committed offset from its volume
+        kc = _container(
             spec, "kafka", LAUNCH + ["kafka-lite", "--nodes", str(spec.kafka.brokers), "--port", "9092",
-                                     "--advertise", f"{name}-brokers"],
+                                     "--advertise", f"{name}-brokers", "--data-dir", "/var/lib/kafka-lite",
+                                     "--fsync", spec.kafka.fsync],
             ports=ports, env={"CCFD_KAFKA_PARTITIONS": spec.kafka.partitions}, envfrom=False,
-            probe=(None, 9092, 20))],
-            annotations=_scrape("/metrics", 9404)))
+            probe=(None, 9092, 20))
+        kc["volumeMounts"] = [{"name": "kafka-data", "mountPath": "/var/lib/kafka-lite"}]
+        if spec.kafka.storage:
+            extra = {"volumeClaimTemplates": [{"metadata": {"name": "kafka-data"}, "spec": {
+                "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": spec.kafka.storage}}}}]}
+            out.append(_workload("StatefulSet", name, name, 1, [kc], annotations=_scrape("/metrics", 9404),
+                                 extra_spec=extra))
+        else:
+            out.append(_workload("StatefulSet", name, name, 1, [kc], annotations=_scrape("/metrics", 9404),
+                                 volumes=[{"name": "kafka-data", "emptyDir": {}}]))
         for svc in (f"{name}-brokers", f"{name}-bootstrap"):
             out.append(_service(svc, name, [{"name": f"broker-{i}", "port": 9092 + i, "targetPort": 9092 + i}
                                             for i in range(spec.kafka.brokers)]))

@@ -36,6 +36,9 @@ class KafkaSpec:
     brokers: int = 3                 # kafka-lite listeners (reference: kafka_broker_replicas 3)
     partitions: int = 16
     bootstrap: str = ""              # external bootstrap list when deploy is False
+    storage: str = "50Gi"            # kafka-lite's durable logs (--data-dir): a PersistentVolumeClaim of
+                                     # this size per broker pod; "" = emptyDir (survives container, not pod, restarts)
+    fsync: str = "interval"          # kafka-lite flush policy: always | interval | never
 
 
 @dataclass
@@ -127,6 +130,8 @@ class FraudDetectionSpec:
             raise SpecError(f"engine.exec_mode {self.engine.exec_mode!r}: auto | persistent | launch")
         if self.engine.persist_items not in ("pipelined", "claimed", "auto"):
             raise SpecError(f"engine.persist_items {self.engine.persist_items!r}: pipelined | claimed | auto")
+        if self.kafka.fsync not in ("always", "interval", "never"):
+            raise SpecError(f"kafka.fsync {self.kafka.fsync!r}: always | interval | never")
         if self.engine.standard_mode not in ("count", "process"):
             raise SpecError(f"engine.standard_mode {self.engine.standard_mode!r}: count | process")
         if self.engine.output_mode not in ("zerocopy", "dma"):
