@@ -276,7 +276,7 @@ def test_local_commands_probe_the_rendered_health_routes():
     assert cmds["kafka"][3][0](0)[0] == "tcp" and cmds["producer"][3] is None
 
 
-def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
+def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path, tmp_path):
     """Only the CR's kafka section deployed: the operator starts kafka-lite with 3 listeners
     and a Kafka client produces to / fetches from it through the bootstrap list."""
     from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
@@ -286,7 +286,8 @@ def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
     d["spec"]["kafka"].update(brokers=3, partitions=6)
     spec = parse(d)
     off = random.randint(20000, 40000)
-    op = LocalOperator(spec, workdir=str(ROOT), commands=None, grace_s=5, log=lambda m: None, port_offset=off)
+    op = LocalOperator(spec, workdir=str(ROOT), commands=None, grace_s=5, log=lambda m: None, port_offset=off,
+                       state_dir=str(tmp_path / "state"))
     try:
         assert op.reconcile()["kafka"]["ready"] == 1
         bootstrap = ",".join(f"127.0.0.1:{9092 + off + i}" for i in range(3))
