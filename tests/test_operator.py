@@ -276,7 +276,7 @@ def test_local_commands_probe_the_rendered_health_routes():
     assert cmds["kafka"][3][0](0)[0] == "tcp" and cmds["producer"][3] is None
 
 
-def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path, tmp_path):
+def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
     """Only the CR's kafka section deployed: the operator starts kafka-lite with 3 listeners
     and a Kafka client produces to / fetches from it through the bootstrap list."""
     from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
