@@ -22,4 +22,8 @@ step json process-mode traced
 timeout -k 30 300 python bench/deploy_topology.py --seconds 20 --producers 2 --rate 200000 --fmt json --trace \
   --standard-mode process --log-dir $O/json_proc --out $O/topo_json_process.json > $O/topo_json_process.log 2>&1 || { tail -40 $O/topo_json_process.log; exit 1; }
 python3 -c "import json; d=json.load(open('$O/topo_json_process.json')); print(d['value'], d['checks_passed'], d.get('kie_standard_plus_fraud_equals_incoming'), d['kie']); print(json.dumps(d.get('tail_attribution'))[:1200])"
+
+step counters list
+timeout -k 10 120 rocprofv3 -L > $O/rocprofv3_counters.txt 2>&1 || true
+head -3 $O/rocprofv3_counters.txt
 step done
