@@ -62,6 +62,8 @@ def _bind(L):
     L.ccfd_kc_last_error.restype = C.c_char_p
     L.ccfd_kc_feed_record_set.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
     L.ccfd_kc_feed_record_set.restype = C.c_int64
+    L.ccfd_kc_last_origin.argtypes = [C.c_void_p]
+    L.ccfd_kc_last_origin.restype = C.c_int64
     L.ccfd_kc_set_offset_reset.argtypes = [C.c_void_p, C.c_int]
     L.ccfd_kc_set_offset_reset.restype = C.c_int
     L.ccfd_kc_position.argtypes = [C.c_void_p, C.c_int]
@@ -172,6 +174,11 @@ class NativeKafkaConsumer:
 
     def last_error(self) -> str:
         return (lib().ccfd_kc_last_error(C.c_void_p(self.h)) or b"").decode(errors="replace")
+
+    def last_origin_ns(self) -> int:
+        """Producer send time of the last ingested batch (``ccfd-ts`` header) on the steady
+        clock (time.monotonic_ns), 0 = the batch carried none."""
+        return int(lib().ccfd_kc_last_origin(C.c_void_p(self.h)))
 
     def feed(self, record_set: bytes) -> int:
         """Parse ``record_set`` as partition 0's fetched bytes (array sink, no socket)."""

@@ -889,6 +889,12 @@ int64_t ccfd_kc_position(void* kc, int part_index) {
   return c->ps[part_index].next_offset;
 }
 
+// The producer send time (engine steady clock, ns) of the last ingested batch: 0 when it had
+// no ccfd-ts header (tests; the engine reads it through ccfd_engine_ring_commit_at).
+int64_t ccfd_kc_last_origin(void* kc) {
+  return kc ? static_cast<Consumer*>(kc)->cur_origin : -1;
+}
+
 // Fuzz / unit entry: feed raw bytes as partition 0's record set of an array-sink consumer
 // (no socket).  Returns records accepted.  Used by tests/test_native_cpu.py under ASan.
 int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n) {

@@ -449,6 +449,7 @@ int64_t ccfd_kc_committable(void* kc, int part_index);
 void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out);
 const char* ccfd_kc_last_error(void* kc);
 int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n);   // tests / fuzzing
+int64_t ccfd_kc_last_origin(void* kc);         // send time (steady ns) of the last batch's ccfd-ts header, 0 = none
 int ccfd_kc_set_offset_reset(void* kc, int policy);                           // before start
 int64_t ccfd_kc_position(void* kc, int part_index);                           // next offset to fetch
 // G32 / G20 sinks (wire = 2 / 3): the bin table rows are encoded against (ccfd_encode_g32 layout);

@@ -125,3 +125,30 @@ def test_unsupported_codec_is_reported_not_skipped():
         assert "snappy" in kc.last_error() and kc.stats()["errors"] == 1
     finally:
         kc.close()
+
+
+def test_send_time_header_sets_the_batch_origin():
+    """The ccfd-ts header (ingest/kafka_wire.py with_produce_time) on a batch's first record is
+    the origin of the engine's produce -> scored latency: the consumer converts it to its
+    steady clock; a batch without it has no origin."""
+    import time
+    import numpy as np
+    from ccfd_demo_summit_amd.contracts import TxBatch
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.ingest.kafka_wire import seal_batches, with_produce_time
+    X, _ = generate(100, seed=4)
+    rs = encode_record_batch([TxBatch(ids=np.arange(100, dtype=np.uint64), customer=np.zeros(100, np.uint32),
+                                      features=X).encode()])
+    kc = NativeKafkaConsumer.for_arrays("127.0.0.1:1", "t", {0: 0}, capacity=1000)
+    try:
+        assert kc.feed(rs) == 1 and kc.last_origin_ns() == 0
+        b = with_produce_time(encode_record_batch([b'{"id": 7, "Amount": 1.0}'] * 10, base_offset=1),
+                              time.time_ns() - 5_000_000)
+        seal_batches(b)
+        t_mono = time.monotonic_ns()
+        assert kc.feed(bytes(b)) == 10
+        origin = kc.last_origin_ns()
+        assert abs((t_mono - origin) - 5_000_000) < 3_000_000, (t_mono - origin)
+        assert kc.stats()["errors"] == 0
+    finally:
+        kc.close()
