@@ -903,7 +903,9 @@ def main(argv=None):
             runner = web.AppRunner(app)
             await runner.setup()
             await web.TCPSite(runner, a.host, a.metrics_port).start()
-        print(f"[kafka-lite] {a.nodes} node(s) listening on {cl.bootstrap_all}", flush=True)
+        from ..utils.gcpolicy import tune_for_service
+        print(f"[kafka-lite] {a.nodes} node(s) listening on {cl.bootstrap_all}; gc: {tune_for_service()}",
+              flush=True)
         await asyncio.Event().wait()
     asyncio.run(run())
 

@@ -205,6 +205,8 @@ def cmd_kie(a, cfg):
     else:
         eng = ProcessEngine.from_config(cfg.kie, journal_path=a.journal, **kw)
     srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
+    from ..utils.gcpolicy import tune_for_service
+    print(f"[kie] gc: {tune_for_service()}", flush=True)
     web.run_app(srv.app, host=a.host, port=a.port or cfg.kie.port, print=None, access_log=None)
 
 
@@ -224,6 +226,8 @@ def cmd_notifier(a, cfg):
     app.router.add_get("/health/ping", lambda _r: web.json_response(
         {"status": "ok", "sent": ns.sent, "replied": ns.replied, "no_reply": ns.no_reply}))
     _serve_in_thread(app, a.host, a.port or cfg.notifier.port)
+    from ..utils.gcpolicy import tune_for_service
+    tune_for_service()
     while True:
         for r in _safe(lambda: cons.poll(timeout=0.05, max_records=10_000), []):
             ns.handle(r.value)
@@ -342,6 +346,8 @@ def cmd_engine(a, cfg):
     notif = (broker.consumer(cfg.kafka.group_id + "-notifications", [cfg.kafka.notification_topic])
              if ctx.rank == 0 else None)
     print(f"[engine] rank {ctx.rank}/{ctx.world} partitions {svc.partitions}", flush=True)
+    from ..utils.gcpolicy import tune_for_service
+    print(f"[engine] gc: {tune_for_service()}", flush=True)
     # SIGTERM (pod deletion, torchrun shutdown, a supervisor) ends the loop through the
     # `finally` below: the engine drains and its persistent kernel leaves before exit
     import signal

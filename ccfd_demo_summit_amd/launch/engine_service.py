@@ -369,8 +369,7 @@ class EngineService:
             if st.last_seq:
                 self.last_scored = st.last
             if st.dev_batches:
-                self.kernel_exec_mean_us = st.dev_exec_mean_us
-            self._origin_rows_cum = st.origin_hist_rows.astype(np.int64)     # K7, cumulative mean
+                self.kernel_exec_mean_us = st.dev_exec_mean_us     # K7, cumulative mean
             self._origin_rows_cum = st.origin_hist_rows.astype(np.int64)
         return int(st.rows)
 
@@ -399,6 +398,7 @@ class EngineService:
                 self.last_scored = st.last
             if st.dev_batches:
                 self.kernel_exec_mean_us = st.dev_exec_mean_us
+            self._origin_rows_cum = st.origin_hist_rows.astype(np.int64)
         return rows
 
     def _progress(self) -> None:

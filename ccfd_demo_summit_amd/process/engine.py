@@ -181,7 +181,13 @@ class ProcessEngine:
             if inst.state == State.WAITING_CUSTOMER and inst.timer_due is not None:
                 heapq.heappush(eng._timers, (inst.timer_due, iid))
         for b in std_batches:                   # batched standard starts (start_standard_many)
-            for iid, tx in zip(b["id"], b["transaction_id"]):
+            if "tx_i64" in b:                   # base64 of the new transaction ids (int64 LE)
+                import base64
+
+                import numpy as np
+                b = {"id0": b["id0"], "transaction_id": np.frombuffer(base64.b64decode(b["tx_i64"]), "<i8").tolist()}
+            ids = b["id"] if "id" in b else range(int(b["id0"]), int(b["id0"]) + len(b["transaction_id"]))
+            for iid, tx in zip(ids, b["transaction_id"]):
                 max_id = max(max_id, iid)
                 eng.standard_count += 1
                 eng.outcome_counts[Outcome.STANDARD.value] += 1
@@ -233,40 +239,44 @@ class ProcessEngine:
     def start_standard_many(self, items) -> List[int]:
         """Standard processes for a whole hand-off batch (the engine's standard-routed rows of a
         scoring step).  ``items``: a list of variable dicts, or columns ``{"transaction_id":
-        [...], "customer_id": [...], "amount": [...], "proba": [...]}`` (the compact form the
-        router sends at ~1e5 standard rows a second).  Idempotent per transaction id; the batch
-        is journaled as ONE record (ids + columns), which ``recover()`` replays."""
+        [...], "customer_id": [...], "amount": [...], "proba": [...]}`` (lists or numpy arrays --
+        the compact form the router sends at ~1e5 standard rows a second).  Idempotent per
+        transaction id (a re-delivered batch, or a transaction twice in one batch, starts once).
+        New instances get consecutive ids; the batch is journaled as ONE record (first id + the
+        new transaction ids), which ``recover()`` replays."""
+        numeric = isinstance(items, dict) and hasattr(items.get("transaction_id", items.get("tx_id")), "dtype")
         cols = columns_of(items)
-        txs = cols.get("transaction_id") or cols.get("tx_id")
+        txs = cols.get("transaction_id")
+        if txs is None:
+            txs = cols.get("tx_id")
         n = _ncols(cols)
         sc = cols.pop("scored_ns", None)
         if sc:
             self._note_handoff(sc[0], n)
-        out: List[int] = []
-        new_pos: List[int] = []
+        if txs is None or (not numeric and any(t is None for t in txs)):
+            return [self.start_standard({k: v[i] for k, v in cols.items()}) for i in range(n)]
         with self._lock:
-            for k in range(n):
-                tx = txs[k] if txs is not None else None
-                if tx is not None:
-                    old = self._std_by_tx.get(tx)
-                    if old is not None:
-                        self.standard_duplicates += 1
-                        out.append(old)
-                        continue
-                iid = next(self._ids)
-                if tx is not None:
-                    self._std_remember(tx, iid)
-                out.append(iid)
-                new_pos.append(k)
-            self.standard_count += len(new_pos)
-            self.outcome_counts[Outcome.STANDARD.value] += len(new_pos)
-            if self._journal is not None and new_pos:
-                rec = {"id": [out[k] for k in new_pos]}
-                for key, vals in cols.items():
-                    rec[key] = [vals[k] for k in new_pos]
-                if "transaction_id" not in rec:
-                    rec["transaction_id"] = [None] * len(new_pos)
-                self._journal.write(json.dumps({"standard": rec}, default=float) + "\n")
+            seen = self._std_by_tx
+            new = sorted(set(txs).difference(seen))     # C: iterates the batch, not the dedupe window
+            n_new = len(new)
+            first = 0
+            if n_new:
+                first = next(self._ids)
+                self._ids = itertools.count(first + n_new)
+                seen.update(zip(new, range(first, first + n_new)))
+                self._std_order.extend(new)
+                for _ in range(len(self._std_order) - self.standard_dedupe_window):
+                    seen.pop(self._std_order.popleft(), None)
+            out = [-1 if i is None else i for i in map(seen.get, txs)]
+            self.standard_duplicates += n - n_new
+            self.standard_count += n_new
+            self.outcome_counts[Outcome.STANDARD.value] += n_new
+            if self._journal is not None and n_new:
+                import base64
+
+                import numpy as np
+                tx64 = base64.b64encode(np.asarray(new, np.int64).tobytes()).decode()
+                self._journal.write('{"standard": {"id0": %d, "tx_i64": "%s"}}\n' % (first, tx64))
         return out
 
     def _note_handoff(self, scored_ns, n: int = 1) -> None:
@@ -451,7 +461,7 @@ def columns_of(items) -> Dict[str, list]:
     """Variables of many process starts as columns: accepts a list of dicts or a dict of
     equally long lists (``tx_id`` is accepted for ``transaction_id``)."""
     if isinstance(items, dict):
-        cols = {k: list(v) for k, v in items.items()}
+        cols = {k: (v.tolist() if hasattr(v, "tolist") else list(v)) for k, v in items.items()}
     else:
         keys: List[str] = []
         for it in items:

@@ -27,6 +27,49 @@ from .engine import ProcessEngine, rows_of
 BASE = "/services/rest/server"
 
 
+COLUMNS_CT = "application/x-ccfd-columns"
+_COL_DT = {"q": "<i8", "d": "<f8", "f": "<f4", "I": "<u4"}
+
+
+def encode_columns(cols) -> bytes:
+    """Column batch -> binary body: b"CCOL", u32 rows, u32 columns, then per column u8 name
+    length, name, u8 dtype code (q i64 / d f64 / f f32 / I u32) and the raw little-endian
+    array.  ~20x cheaper to build and parse than the JSON list form at 4096 rows."""
+    import struct
+
+    import numpy as np
+    arrs = {k: np.asarray(v) for k, v in cols.items()}
+    n = len(next(iter(arrs.values()))) if arrs else 0
+    parts = [b"CCOL", struct.pack("<II", n, len(arrs))]
+    for k, a in arrs.items():
+        code = {"i": "q", "u": "q", "f": "f" if a.dtype.itemsize <= 4 else "d"}.get(a.dtype.kind)
+        if code is None or len(a) != n:
+            raise ValueError(f"column {k!r}: numeric columns of one length only")
+        kb = k.encode()
+        parts += [struct.pack("<B", len(kb)), kb, code.encode(), np.ascontiguousarray(a, _COL_DT[code]).tobytes()]
+    return b"".join(parts)
+
+
+def decode_columns(body: bytes):
+    import struct
+
+    import numpy as np
+    if body[:4] != b"CCOL":
+        raise ValueError("not a CCOL column batch")
+    n, k = struct.unpack_from("<II", body, 4)
+    o, cols = 12, {}
+    for _ in range(k):
+        ln = body[o]
+        name = body[o + 1:o + 1 + ln].decode()
+        dt = np.dtype(_COL_DT[chr(body[o + 1 + ln])])
+        o += 2 + ln
+        cols[name] = np.frombuffer(body, dt, n, o)
+        o += n * dt.itemsize
+    if o != len(body):
+        raise ValueError("CCOL body length mismatch")
+    return cols
+
+
 class KieServer:
     def __init__(self, engine: ProcessEngine, container_id: str = "ccd-fraud-kjar",
                  fraud_process_id: str = "ccd-fraud-kjar.CCDProcess",
@@ -99,9 +142,13 @@ class KieServer:
         if bad:
             return bad
         pid = request.match_info["p"]
-        items = json.loads(await request.read() or b"[]")
-        # a JSON list of variable objects, or columns {"transaction_id": [...], ...} (the
-        # compact form the router uses for standard-routed rows)
+        raw = await request.read()
+        try:
+            # a JSON list of variable objects, JSON columns {"transaction_id": [...], ...}, or a
+            # binary column batch (COLUMNS_CT: the router's standard-route hand-off)
+            items = decode_columns(raw) if request.content_type == COLUMNS_CT else json.loads(raw or b"[]")
+        except (ValueError, KeyError, IndexError) as e:
+            return web.json_response({"type": "FAILURE", "msg": f"bad batch body: {e}"}, status=400)
         if not isinstance(items, (list, dict)):
             return web.json_response({"type": "FAILURE", "msg": "expected a JSON list or columns"}, status=400)
         try:
@@ -249,10 +296,16 @@ class KieClient:
         """One request for many standard instances (``/instances/batch`` extension); ``items``
         may be columns ``{"transaction_id": [...], "customer_id": [...], "amount": [...],
         "proba": [...]}`` -- ~4x smaller and faster to encode than a list of objects."""
-        if not items or (isinstance(items, dict) and not any(len(v) for v in items.values())):
-            return []
+        if isinstance(items, dict):
+            if not any(len(v) for v in items.values()):
+                return []
+            body, ct = encode_columns(items), COLUMNS_CT
+        else:
+            if not items:
+                return []
+            body, ct = json.dumps(items), "application/json"
         r = self.s.post(f"{self.base}/containers/{self.c}/processes/{self.standard_pid}/instances/batch",
-                        data=json.dumps(items), headers={"Content-Type": "application/json"}, timeout=self.timeout)
+                        data=body, headers={"Content-Type": ct}, timeout=self.timeout)
         r.raise_for_status()
         return [int(x) for x in r.json()]
 

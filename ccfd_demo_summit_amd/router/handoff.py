@@ -88,7 +88,7 @@ def _transient(e: BaseException) -> bool:
 
 def _jsonable(kind: str, payload: Any) -> Any:
     if kind == "standard":
-        return {k: list(v) for k, v in payload.items()}
+        return {k: (v.tolist() if hasattr(v, "tolist") else list(v)) for k, v in payload.items()}
     if kind == "signal":
         iid, name, body = payload
         return [iid, name, body]

@@ -27,13 +27,11 @@ from ..metrics.exporter import RouterMetrics
 from .rules import RuleSet
 
 
-def standard_columns(rec: np.ndarray) -> Dict[str, list]:
-    """Scored records -> the column batch a standard-process hand-off carries (probabilities
-    and amounts rounded to 1e-6: the JSON body stays ~4x smaller than full float64 repr)."""
-    return {"transaction_id": rec["tx_id"].astype(np.int64).tolist(),
-            "customer_id": rec["customer"].astype(np.int64).tolist(),
-            "amount": np.round(rec["amount"].astype(np.float64), 6).tolist(),
-            "proba": np.round(rec["proba"].astype(np.float64), 6).tolist()}
+def standard_columns(rec: np.ndarray) -> Dict[str, np.ndarray]:
+    """Scored records -> the column batch a standard-process hand-off carries (numpy columns:
+    KieClient sends them as a binary CCOL body, process/kie_server.py encode_columns)."""
+    return {"transaction_id": rec["tx_id"].astype(np.int64), "customer_id": rec["customer"].astype(np.int64),
+            "amount": rec["amount"].astype(np.float32), "proba": rec["proba"].astype(np.float32)}
 
 
 class Router:
@@ -112,7 +110,7 @@ class Router:
         if self.standard_mode == "process" and standard is not None and len(standard):
             std_cols = standard_columns(standard)
             if self.scored_ns:
-                std_cols["scored_ns"] = [self.scored_ns] * len(standard)
+                std_cols["scored_ns"] = np.full(len(standard), self.scored_ns, np.int64)
         if self.handoff is not None:                        # async, retried, acked later
             seq = -1
             if nf:

@@ -1,0 +1,33 @@
+"""Garbage-collector policy of the long-running Python services.
+
+CPython's cyclic GC runs a full (generation 2) collection every ~700 x 10 x 10 allocations,
+and a full collection walks every tracked object while holding the GIL.  A KIE server
+holding ~10^5 process instances, or an engine rank whose router builds a dict per fraud-routed
+row, then stalls for tens of milliseconds: the round-4 deployed-topology trace showed 886 GC
+pauses of up to 98 ms on an engine rank, which were the entire arrival -> scored tail of the
+Python scoring loop (profiles/r4/tail/).  These services create almost no reference cycles
+(their state is dicts / deques of plain values), so:
+
+* ``gc.freeze()`` after start-up moves everything allocated so far (imports, models, config)
+  into the permanent generation -- never scanned again;
+* generation 0 collects every ``gen0`` allocations (default 50 000, not 700) and a full
+  collection needs ``gen2`` generation-1 collections -- about one per 10^9 allocations,
+  i.e. practically only when asked for.
+
+``CCFD_GC=default`` keeps CPython's defaults (A/B switch).
+"""
+from __future__ import annotations
+
+import gc
+import os
+
+
+def tune_for_service(gen0: int = 50_000, gen1: int = 20, gen2: int = 1000) -> str:
+    """Apply the service GC policy (call once start-up is done); returns what was applied."""
+    mode = os.environ.get("CCFD_GC", "service")
+    if mode == "default":
+        return "default"
+    gc.collect()
+    gc.freeze()
+    gc.set_threshold(gen0, gen1, gen2)
+    return f"frozen {gc.get_freeze_count()} objects, thresholds {gc.get_threshold()}"

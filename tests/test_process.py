@@ -164,3 +164,27 @@ def test_journal_recovery_survives_a_torn_last_line(tmp_path):
     r.close()
     r2 = ProcessEngine.recover(j, notification_timeout_s=60)        # the record after the torn line survives
     assert len(r2.instances) == 11 and 50 in r2._by_tx
+
+
+def test_standard_batches_idempotent_and_recovered(tmp_path):
+    """start_standard_many (the engine's standard-route hand-off): one process per transaction
+    id -- within a batch, across re-delivered batches, and across a KIE restart from its
+    journal; numpy columns are accepted."""
+    import numpy as np
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    j = str(tmp_path / "kie.jsonl")
+    e = ProcessEngine(notification_timeout_s=60, journal_path=j)
+    ids1 = e.start_standard_many({"transaction_id": np.array([10, 11, 12, 11], np.int64),
+                                  "proba": np.array([0.1, 0.2, 0.3, 0.2], np.float32)})
+    assert ids1[1] == ids1[3] and len(set(ids1)) == 3
+    ids2 = e.start_standard_many([{"transaction_id": 12}, {"transaction_id": 13}])
+    assert ids2[0] == ids1[2] and ids2[1] not in ids1
+    f = e.start_fraud({"transaction_id": 99, "amount": 5.0, "proba": 0.9})
+    assert e.standard_count == 4 and e.standard_duplicates == 2
+    e.close()
+    r = ProcessEngine.recover(j, notification_timeout_s=60)
+    assert r.standard_count == 4 and r.outcome_counts["standard"] == 4
+    again = r.start_standard_many({"transaction_id": [10, 13, 14]})
+    assert again[:2] == [ids1[0], ids2[1]] and r.standard_count == 5
+    assert again[2] > max(ids1 + ids2 + [f])          # fresh ids never collide after recovery
+    r.close()
