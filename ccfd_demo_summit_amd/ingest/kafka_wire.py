@@ -269,7 +269,8 @@ def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optiona
             k = L.ccfd_kafka_encode_batch(buf, off.ctypes.data, n, ts, C.addressof(ob), len(out))
             if k > 0:
                 del ob
-                return bytes(out[:k])
+                del out[k:]                       # a bytearray: producers stamp it in place
+                return out
     recs = []
     for i, v in enumerate(values):
         k = keys[i] if keys is not None else None
@@ -288,7 +289,10 @@ def encode_record_batch(values: Sequence[bytes], keys: Optional[Sequence[Optiona
     crc = crc32c(after_crc)
     head = struct.pack(">ibI", 0, 2, crc)                 # partitionLeaderEpoch, magic, crc
     batch_len = len(head) + len(after_crc)
-    return struct.pack(">qi", base_offset, batch_len) + head + after_crc
+    out = bytearray(struct.pack(">qi", base_offset, batch_len))   # mutable: stamped in place by
+    out += head                                                    # idempotent producers
+    out += after_crc
+    return out
 
 
 PRODUCE_TS_HEADER = b"ccfd-ts"          # record header: producer send time, u64 BE ns (CLOCK_REALTIME)
@@ -495,6 +499,8 @@ class KafkaBroker:
         # stamp_time: the ccfd-ts send-time header on the first record of every batch (the
         # engine's produce -> scored latency); set by the transaction producer
         self.stamp_time = False
+        self.stamp_every = 8                # every 8th batch: a sampled latency, a fraction of the copies
+        self._stamp_n = 0
         self._pid: Optional[Tuple[int, int]] = None
         self._seq: Dict[Tuple[str, int], int] = {}
         self._seq_locks: Dict[Tuple[str, int], threading.Lock] = {}
@@ -662,10 +668,20 @@ class KafkaBroker:
 
     def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
-        if not (self.idempotent or self.stamp_time):
+        stamp = False
+        if self.stamp_time:                 # a sample of the batches carries its send time
+            stamp = self._stamp_n % max(1, self.stamp_every) == 0
+            self._stamp_n += 1
+        if not (self.idempotent or stamp):
             return self._produce_raw(topic, partition, record_set, acks)
-        # one copy: the produce-time header splice (or a plain copy), sequence stamps, one seal
-        b = with_produce_time(record_set, time.time_ns()) if self.stamp_time else bytearray(record_set)
+        # at most one copy: the send-time header splice, else a bytearray from the encoders is
+        # stamped in place (anything immutable is copied once); sequence stamps; one seal
+        if stamp:
+            b = with_produce_time(record_set, time.time_ns())
+        elif isinstance(record_set, bytearray):
+            b = record_set
+        else:
+            b = bytearray(record_set)
         if not self.idempotent:
             seal_batches(b)
             return self._produce_raw(topic, partition, b, acks)

@@ -182,6 +182,8 @@ class NativeKafkaConsumer:
 
     def feed(self, record_set: bytes) -> int:
         """Parse ``record_set`` as partition 0's fetched bytes (array sink, no socket)."""
+        if not isinstance(record_set, bytes):
+            record_set = bytes(record_set)
         return int(lib().ccfd_kc_feed_record_set(C.c_void_p(self.h), record_set, len(record_set)))
 
     def committable(self) -> Dict[int, int]:

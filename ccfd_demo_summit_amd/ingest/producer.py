@@ -108,7 +108,7 @@ class TransactionProducer:
             X, _ = generate(n, seed=self.cfg.seed + 31)
             self._tails = [json_tail(i % 100_000, X[i]) for i in range(n)]
 
-    def _native_json_record_set(self) -> Optional[bytes]:
+    def _native_json_record_set(self) -> Optional[bytearray]:
         """One RecordBatch of ``batch`` JSON messages built natively (ids formatted in C++,
         csrc/engine/kafka_codec.cpp ccfd_kafka_encode_json_batch); None without the library."""
         if getattr(self, "_nat", None) is None:
@@ -139,7 +139,7 @@ class TransactionProducer:
                                            c.id_base + self.sent, int(time.time() * 1000), out.ctypes.data, out.size)
         if k <= 0:
             raise RuntimeError("ccfd_kafka_encode_json_batch failed")
-        return out[:k].tobytes()
+        return bytearray(out[:k])           # mutable: an idempotent producer stamps it in place
 
     def _json_batch(self) -> list:
         c = self.cfg
