@@ -210,3 +210,41 @@ def test_g20_rules_hot_swap_and_global_leaves(gpu, exec_mode):
     np.testing.assert_array_equal(got, big.predict_proba(X[:n]) >= 0.5)
     eng.close()
     log.free()
+
+
+@pytest.mark.parametrize("fmt", ["g20", "g32"])
+@pytest.mark.parametrize("item_rows", [256, 512])
+def test_item_prefetch_pipeline_exact(gpu, monkeypatch, fmt, item_rows):
+    """CCFD_G32_ITEM_PREFETCH=1: the two-item pipeline (next item claimed and its rows in
+    flight before the current one is scored) -- full, partial and back-to-back micro-batches
+    over several pump calls (the kernel halts and relaunches between them), every row once,
+    proba per row exact (scored ring), counters and histograms exact."""
+    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    monkeypatch.setenv("CCFD_G32_ITEM_PREFETCH", "1")
+    monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
+    B = 65536
+    X, _ = generate(B * 4 + 5000, seed=59)
+    m = _model(14, X[:20000], rate=0.05)
+    dm = DeviceModel(m, gpu, bins=fmt)
+    eng = StreamEngine(dm, batch=B, depth=4, streams=1, exec_mode="persistent")
+    eng.enable_scored(X.shape[0])
+    log = PartitionLog.from_arrays(X, ids=np.arange(X.shape[0], dtype=np.uint64), bins=dm.bins)
+    eng.add_log(0, log)
+    n = 1301 + 3 * B + 2 * 1303
+    got_rows = eng.pump(1, batch_rows=1301).rows + eng.pump(3).rows + eng.pump(2, batch_rows=1303).rows
+    assert got_rows == n
+    rec = eng.drain_scored()
+    ids = rec["tx_id"].astype(np.int64)
+    np.testing.assert_array_equal(np.sort(ids), np.arange(n))
+    pr = m.predict_proba(X[ids])
+    assert np.abs(rec["proba"] - pr).max() < 2e-5
+    np.testing.assert_array_equal(rec["route"] == 1, pr >= 0.5)
+    side = torch.cuda.Stream(gpu)
+    c = eng.flip_epoch(side)
+    side.synchronize()
+    c = c.cpu().numpy()
+    assert c[0] == n and c[1] == (pr >= 0.5).sum() and c[4] == 0
+    assert int(c[8:22].sum() + c[24:38].sum()) == n
+    eng.close()
+    log.free()
