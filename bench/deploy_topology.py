@@ -411,6 +411,11 @@ def main(argv=None):
              "p99": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_p99_seconds") * 1e6, 1),
              "rows": int(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_rows"))}
             for r in range(a.ranks)]
+        # scored -> started, the engine's share: hand-off queue wait and request time per rank
+        out["handoff_engine_us"] = [
+            {"rank": r, **{f"{k}_{q}": round(metric_sum(texts[f"router{r}"], f"ccfd_gpu_handoff_{k}_{q}_seconds") * 1e6, 1)
+                           for k in ("queue_wait", "request") for q in ("p50", "p99")}}
+            for r in range(a.ranks)]
         model_texts = [http_text(f"http://127.0.0.1:{model_base + r}/prometheus") for r in range(a.ranks)]
         mt = "\n".join(model_texts)
         for qq in (0.5, 0.99):
@@ -433,6 +438,7 @@ def main(argv=None):
         out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
         out["kie_duplicates"] = stats["duplicates"]
         out["scored_to_process_started_us"] = stats.get("scored_to_started_us")
+        out["kie_handoff_attribution"] = stats.get("handoff_attribution")
         out["standard_mode"] = a.standard_mode
         if a.standard_mode == "process":
             # every transaction started exactly one process: standard + fraud == incoming

@@ -641,6 +641,10 @@ class EngineService:
                          handoff_acked=hs["acked"], handoff_failed=hs["failed"],
                          handoff_refused=hs.get("refused", 0),
                          handoff_dead_letter_total=hs.get("dead_lettered", 0))
+            for key, h in (("queue_wait", self.handoff.queue_wait), ("request", self.handoff.request_time)):
+                if h.count():                           # scored -> started, the engine's share
+                    extra[f"handoff_{key}_p50_seconds"] = h.quantile_ns(0.5) * 1e-9
+                    extra[f"handoff_{key}_p99_seconds"] = h.quantile_ns(0.99) * 1e-9
         if self.standard_mode == "process":
             extra.update(standard_started=getattr(self.router, "standard_started", 0))
         with self._stat_lock:

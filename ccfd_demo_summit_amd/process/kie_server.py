@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import time
 from dataclasses import asdict
 from typing import Optional
 
@@ -22,6 +23,7 @@ import requests
 from aiohttp import web
 
 from ..metrics.exporter import CONTENT_TYPE
+from ..utils.lathist import LatHist
 from .engine import ProcessEngine, rows_of
 
 BASE = "/services/rest/server"
@@ -95,12 +97,29 @@ class KieServer:
         self.app.on_startup.append(self._startup)
         self.app.on_cleanup.append(self._cleanup)
         self._ticker: Optional[asyncio.Task] = None
+        # scored -> started, the server's share: a start request's arrival after its rows were
+        # scored (engine hand-off queue + network), the handler's own time, the timer tick's
+        # time, and how late the event loop wakes the ticker (everything else on the loop)
+        self.recv_after_scored = LatHist()
+        self.handler_time = LatHist()
+        self.tick_time = LatHist()
+        self.loop_lag = LatHist()
+
+    def attribution(self) -> dict:
+        return {"received_after_scored_us": self.recv_after_scored.summary_us(),
+                "start_handler_us": self.handler_time.summary_us(),
+                "timer_tick_us": self.tick_time.summary_us(),
+                "event_loop_lag_us": self.loop_lag.summary_us()}
 
     async def _startup(self, _app):
         async def loop():
             while True:
+                t0 = time.monotonic_ns()
                 self.engine.tick()
+                t1 = time.monotonic_ns()
+                self.tick_time.add(t1 - t0)
                 await asyncio.sleep(self.tick_s)
+                self.loop_lag.add(time.monotonic_ns() - t1 - int(self.tick_s * 1e9))
         self._ticker = asyncio.get_running_loop().create_task(loop())
 
     async def _cleanup(self, _app):
@@ -142,6 +161,7 @@ class KieServer:
         if bad:
             return bad
         pid = request.match_info["p"]
+        t_in, t0 = time.time_ns(), time.monotonic_ns()
         raw = await request.read()
         try:
             # a JSON list of variable objects, JSON columns {"transaction_id": [...], ...}, or a
@@ -163,7 +183,19 @@ class KieServer:
         if ids is None:
             return web.json_response({"type": "FAILURE", "msg": f"Could not find process definition {pid}"},
                                      status=404)
+        self._note_request(items, t_in, len(ids))
+        self.handler_time.add(time.monotonic_ns() - t0)
         return web.json_response(ids, status=201)
+
+    def _note_request(self, items, t_in: int, n: int) -> None:
+        sc = None
+        if isinstance(items, dict):
+            col = items.get("scored_ns")
+            sc = int(col[0]) if col is not None and len(col) else None
+        elif items and isinstance(items[0], dict):
+            sc = items[0].get("scored_ns")
+        if sc:
+            self.recv_after_scored.add(t_in - int(sc), n)
 
     async def signal(self, request: web.Request):
         bad = self._check_container(request)
@@ -227,6 +259,7 @@ class KieServer:
             body = {"fraud_instances_retained": fraud, "fraud_started": len(e._by_tx), "duplicates": e.duplicates,
                     "standard_started": e.standard_count, "standard_duplicates": e.standard_duplicates,
                     "scored_to_started_us": e.handoff_latency_us(),
+                    "handoff_attribution": self.attribution(),
                     "active": sum(1 for i in e.instances.values()
                                                                         if i.state.value != "completed"),
                     "outcomes": dict(e.outcome_counts), "next_instance_id": None}

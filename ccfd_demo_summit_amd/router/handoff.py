@@ -51,6 +51,8 @@ import threading
 import time
 from typing import Any, Deque, Dict, List, Optional, Tuple
 
+from ..utils.lathist import LatHist
+
 TRANSIENT_HTTP = (500, 502, 503, 504, 429, 408)
 MISSING_ROUTE_HTTP = (404, 405, 501)
 
@@ -238,9 +240,13 @@ class KieHandoff:
         self.max_backoff_s = float(max_backoff_s)
         self.metrics = metrics
         self._cv = threading.Condition()
-        # queue entries: (seq, kind, payload) -- kind "start" (list of variable dicts) or
-        # "signal" ((instance_id, name, payload))
-        self._q: Deque[Tuple[int, str, Any]] = collections.deque()
+        # queue entries: (seq, kind, payload, pushed monotonic ns) -- kind "start" (list of
+        # variable dicts), "standard" (columns) or "signal" ((instance_id, name, payload))
+        self._q: Deque[Tuple[int, str, Any, int]] = collections.deque()
+        # where a hand-off's time goes on this side: queued behind other requests, then the
+        # request itself (HTTP round trip + the server's handler, retries included)
+        self.queue_wait = LatHist()
+        self.request_time = LatHist()
         self._queued_items = 0
         self._next_seq = 0
         self._done: set = set()            # acked seqs above the contiguous prefix
@@ -267,7 +273,7 @@ class KieHandoff:
         with self._cv:
             seq = self._next_seq
             self._next_seq += 1
-            self._q.append((seq, kind, payload))
+            self._q.append((seq, kind, payload, time.monotonic_ns()))
             self._queued_items += n_items
             self.submitted_items += n_items
             self._cv.notify()
@@ -374,19 +380,21 @@ class KieHandoff:
                     self._cv.wait(0.1)
                 if self._stop and not self._q:
                     return
-                seq, kind, payload = self._q.popleft()
+                seq, kind, payload, t_push = self._q.popleft()
                 seqs = [seq]
                 if kind == "signal":
                     # coalesce the run of signals queued behind this one (customer responses
                     # arrive one per message; one HTTP request per signal would cap them)
                     batch = [payload]
                     while self._q and self._q[0][1] == "signal" and len(batch) < self.max_batch:
-                        s2, _k, p2 = self._q.popleft()
+                        s2, _k, p2, _t = self._q.popleft()
                         seqs.append(s2)
                         batch.append(p2)
                     kind, payload = "signals", batch
             n_items = len(payload) if kind in ("start", "signals") else \
                 (len(next(iter(payload.values()))) if kind == "standard" and payload else 1)
+            t_pop = time.monotonic_ns()
+            self.queue_wait.add(t_pop - t_push)
             delay = self.backoff_s
             t_fail = None
             refused_once = False
@@ -436,6 +444,7 @@ class KieHandoff:
             if t_fail is not None:
                 with self._cv:
                     self.outage_s += time.monotonic() - t_fail
+            self.request_time.add(time.monotonic_ns() - t_pop)
             self._ack_many(seqs, n_items)
 
     def stats(self) -> Dict[str, Any]:
@@ -445,4 +454,6 @@ class KieHandoff:
                     "signals_ok": self.signals_ok, "signals_stale": self.signals_stale,
                     "failed": self.failed_total, "refused": self.refused,
                     "dead_lettered": self.dead_lettered, "batch_signals": self.batch_signals,
-                    "outage_s": round(self.outage_s, 3)}
+                    "outage_s": round(self.outage_s, 3),
+                    "queue_wait_us": self.queue_wait.summary_us(),
+                    "request_us": self.request_time.summary_us()}

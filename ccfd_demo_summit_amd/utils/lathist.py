@@ -1,0 +1,55 @@
+"""Thread-safe log-bucket latency histogram for the host services' own timings.
+
+Same bucketing as the engine's device histograms (``parallel.dp.hist_quantile``): bucket i
+holds ns values in [2^(i/4), 2^((i+1)/4)), 256 buckets, so 1 ns .. ~1.8e19 ns.  Used for the
+hand-off attribution (queue wait, request time on the engine side; request arrival, handler
+time and event-loop lag on the KIE side), where a p99 has to be split into where it was spent.
+"""
+from __future__ import annotations
+
+import math
+import threading
+from typing import Dict, Optional
+
+
+class LatHist:
+    N = 256
+
+    def __init__(self):
+        self.h = [0] * self.N
+        self.max_ns = 0
+        self._lock = threading.Lock()
+
+    def add(self, ns: int, n: int = 1) -> None:
+        if ns <= 0 or n <= 0:
+            return
+        i = min(self.N - 1, int(4.0 * math.log2(ns)))
+        with self._lock:
+            self.h[i] += n
+            if ns > self.max_ns:
+                self.max_ns = ns
+
+    def count(self) -> int:
+        return sum(self.h)
+
+    def quantile_ns(self, q: float) -> Optional[float]:
+        with self._lock:
+            h = list(self.h)
+        tot = sum(h)
+        if not tot:
+            return None
+        target, c = q * tot, 0
+        for i, v in enumerate(h):
+            if c + v >= target and v:
+                frac = (target - c) / v
+                return 2.0 ** ((i + frac) / 4.0)
+            c += v
+        return 2.0 ** (self.N / 4.0)
+
+    def summary_us(self) -> Dict[str, float]:
+        """{"n", "p50", "p99", "max"} in microseconds (p50/p99 interpolated in the bucket)."""
+        n = self.count()
+        if not n:
+            return {"n": 0}
+        return {"n": n, "p50": round(self.quantile_ns(0.5) / 1e3, 1),
+                "p99": round(self.quantile_ns(0.99) / 1e3, 1), "max": round(self.max_ns / 1e3, 1)}

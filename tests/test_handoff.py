@@ -275,3 +275,40 @@ def test_signals_are_coalesced_into_batch_requests(kie):
     assert calls and all(c == 201 for c in calls), calls     # every attempt (retries too) is one batch
     assert sum(1 for i in iids if procs.get(i).outcome == "approved_by_customer") == 100
     ho.close()
+
+
+def test_scored_to_started_attribution_on_both_sides(kie):
+    """The scored -> process-started latency is split into where it is spent: the engine's
+    hand-off queue wait and request time (KieHandoff.stats), and at the KIE server the
+    request's arrival after scoring, the handler's own time and the event loop's lag
+    (/rest/stats handoff_attribution)."""
+    import json as _json
+    import urllib.request
+
+    from ccfd_demo_summit_amd.utils.lathist import LatHist
+    procs, k, px = kie
+    client = KieClient(px.url, timeout_s=2.0)
+    ho = KieHandoff(client, workers=1, max_batch=64, backoff_s=0.02)
+    router = Router(RuleSet.threshold(0.5), client, standard_mode="process", handoff=ho)
+    from ccfd_demo_summit_amd.ops._lib import SCORED_DTYPE
+    std = np.zeros(200, np.dtype(SCORED_DTYPE))
+    std["tx_id"] = np.arange(50_000, 50_200)
+    router.scored_ns = time.time_ns()
+    router.on_flagged(_flagged(np.arange(1, 101, dtype=np.uint64)), 300, standard=std)
+    assert ho.drain(20)
+    st = ho.stats()
+    assert st["queue_wait_us"]["n"] == st["request_us"]["n"] >= 2
+    assert st["request_us"]["p50"] > 0
+    time.sleep(0.2)                                 # a few timer ticks
+    body = _json.loads(urllib.request.urlopen(f"http://127.0.0.1:{k.port}/rest/stats", timeout=5).read())
+    att = body["handoff_attribution"]
+    assert att["received_after_scored_us"]["n"] == 300          # every started row counted once
+    assert att["start_handler_us"]["n"] >= 2 and att["timer_tick_us"]["n"] >= 1
+    assert body["scored_to_started_us"]["n"] == 300
+    # the histogram's interpolated quantiles stay inside the bucket of the values added
+    h = LatHist()
+    for v in (1000, 2000, 4000, 1_000_000):
+        h.add(v)
+    s = h.summary_us()
+    assert s["n"] == 4 and 0.8 <= s["p50"] <= 2.5 and s["max"] == 1000.0
+    ho.close()
