@@ -132,11 +132,14 @@ class ProcessEngine:
     def _log(self, inst: ProcessInstance) -> None:
         if self._journal is None:
             return
-        d = asdict(inst)
+        # a shallow copy of the fields: dataclasses.asdict deep-copies recursively and was 87 %
+        # of a fraud start / signal (76 / 58 us -> the KIE event loop ran ~80 % busy at 7 K
+        # fraud starts/s and queued starts for up to 0.6 s, profiles/r4/kie_handoff/)
+        d = dict(vars(inst))
         d["state"] = inst.state.value
         rec = {"instance": d}
         if inst.task_id is not None and inst.task_id in self.tasks:
-            rec["task"] = asdict(self.tasks[inst.task_id])
+            rec["task"] = vars(self.tasks[inst.task_id])
         self._journal.write(json.dumps(rec, default=float) + "\n")
 
     @classmethod

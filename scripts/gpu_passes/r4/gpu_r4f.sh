@@ -32,9 +32,9 @@ summ $O/gbdt_prefetch_item256.json prefetch_item256
 step txb1 open loop, 4 producers, native serving
 timeout -k 30 300 python bench/deploy_topology.py --seconds 30 --producers 4 --rate 0 --fmt txb1 \
   --log-dir $O/txb1 --out $O/topo_txb1_4p.json > $O/topo_txb1_4p.log 2>&1 || { tail -40 $O/topo_txb1_4p.log; exit 1; }
-python3 -c "import json; d=json.load(open('$O/topo_txb1_4p.json')); print(d['value'], d['min_sample_tx_s'], d['producers_tx_s'], d['arrival_to_scored_p50_us'], d['arrival_to_scored_p99_us'], d['produce_to_scored_us'], d['scored_to_process_started_us'], d['checks_passed'])"
+python3 -c "import json; d=json.load(open('$O/topo_txb1_4p.json')); print(d['value'], d['min_sample_tx_s'], d['producers_tx_s'], d['arrival_to_scored_p50_us'], d['arrival_to_scored_p99_us'], d['produce_to_scored_us'], d['scored_to_process_started_us'], d['checks_passed']); print(d.get('handoff_engine_us'), d.get('kie_handoff_attribution'))"
 step json process mode 2e5
 timeout -k 30 300 python bench/deploy_topology.py --seconds 30 --producers 2 --rate 200000 --fmt json \
   --standard-mode process --log-dir $O/json_proc --out $O/topo_json_process.json > $O/topo_json_process.log 2>&1 || { tail -40 $O/topo_json_process.log; exit 1; }
-python3 -c "import json; d=json.load(open('$O/topo_json_process.json')); print(d['value'], d['checks_passed'], d.get('kie_standard_plus_fraud_equals_incoming'), d['scored_to_process_started_us'], d['produce_to_scored_us'], d['arrival_to_scored_p99_us'])"
+python3 -c "import json; d=json.load(open('$O/topo_json_process.json')); print(d['value'], d['checks_passed'], d.get('kie_standard_plus_fraud_equals_incoming'), d['scored_to_process_started_us'], d['produce_to_scored_us'], d['arrival_to_scored_p99_us']); print(d.get('handoff_engine_us'), d.get('kie_handoff_attribution'))"
 step done
