@@ -409,7 +409,10 @@ def main(argv=None):
         out["produce_to_scored_us"] = [
             {"rank": r, "p50": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_p50_seconds") * 1e6, 1),
              "p99": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_p99_seconds") * 1e6, 1),
-             "rows": int(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_rows"))}
+             "rows": int(metric_sum(texts[f"router{r}"], "ccfd_gpu_produce_to_scored_rows")),
+             # the broker's share: send -> the consumer thread has the record batch
+             "fetched_p50": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_ingest_fetch_age_p50_seconds") * 1e6, 1),
+             "fetched_p99": round(metric_sum(texts[f"router{r}"], "ccfd_gpu_ingest_fetch_age_p99_seconds") * 1e6, 1)}
             for r in range(a.ranks)]
         # scored -> started, the engine's share: hand-off queue wait and request time per rank
         out["handoff_engine_us"] = [

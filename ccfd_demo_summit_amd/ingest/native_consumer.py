@@ -64,6 +64,8 @@ def _bind(L):
     L.ccfd_kc_feed_record_set.restype = C.c_int64
     L.ccfd_kc_last_origin.argtypes = [C.c_void_p]
     L.ccfd_kc_last_origin.restype = C.c_int64
+    L.ccfd_kc_fetch_age_hist.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.ccfd_kc_fetch_age_hist.restype = None
     L.ccfd_kc_set_offset_reset.argtypes = [C.c_void_p, C.c_int]
     L.ccfd_kc_set_offset_reset.restype = C.c_int
     L.ccfd_kc_position.argtypes = [C.c_void_p, C.c_int]
@@ -179,6 +181,14 @@ class NativeKafkaConsumer:
         """Producer send time of the last ingested batch (``ccfd-ts`` header) on the steady
         clock (time.monotonic_ns), 0 = the batch carried none."""
         return int(lib().ccfd_kc_last_origin(C.c_void_p(self.h)))
+
+    def fetch_age_hist(self):
+        """Record batches that carried a ``ccfd-ts`` send time, by their age when this
+        consumer had fetched them (ns, 256 buckets, 4 per octave: parallel.dp.hist_quantile)."""
+        import numpy as np
+        out = np.zeros(256, np.uint64)
+        lib().ccfd_kc_fetch_age_hist(C.c_void_p(self.h), out.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return out
 
     def feed(self, record_set: bytes) -> int:
         """Parse ``record_set`` as partition 0's fetched bytes (array sink, no socket)."""

@@ -635,6 +635,11 @@ class EngineService:
                                                - tot.get("ring_wait_ns", 0)) * 1e-9,
                          ingest_encode_seconds=tot.get("encode_ns", 0) * 1e-9,
                          ingest_ring_wait_seconds=tot.get("ring_wait_ns", 0) * 1e-9)
+            fa = sum(kc.fetch_age_hist().astype(np.int64) for kc in self.natives)
+            if int(fa.sum()) > 0:                       # produce -> scored, the broker's share
+                from ..parallel.dp import hist_quantile
+                extra.update(ingest_fetch_age_p50_seconds=hist_quantile(fa, 0.5) * 1e-9,
+                             ingest_fetch_age_p99_seconds=hist_quantile(fa, 0.99) * 1e-9)
         if self.handoff is not None:
             hs = self.handoff.stats()
             extra.update(handoff_queue_depth=hs["depth"], handoff_retries=hs["retries"],

@@ -35,6 +35,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -190,6 +191,9 @@ class Consumer {
   // producer send time of the batch being ingested, on the steady clock: from the ccfd-ts
   // header of its first record (ingest/kafka_wire.py with_produce_time), 0 when absent
   int64_t cur_origin = 0;
+  // send -> this thread has the batch (broker + network + fetch), ns, 4 buckets per octave:
+  // splits the engine's produce -> scored into the broker side and parse + ring + scoring
+  std::atomic<uint64_t> fetch_age_hist[256] = {};
   static int64_t real_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
         .count();
@@ -624,7 +628,11 @@ class Consumer {
               uint64_t ts = 0;
               for (int b = 0; b < 8; ++b) ts = (ts << 8) | rec.p[b];
               const int64_t age = real_ns() - (int64_t)ts;       // send -> now (same host clock)
-              if (age >= 0 && age < 3600ll * 1000000000ll) cur_origin = mono_ns() - age;
+              if (age >= 0 && age < 3600ll * 1000000000ll) {
+                cur_origin = mono_ns() - age;
+                const int bk = age > 0 ? std::min(255, (int)(4.0 * std::log2((double)age))) : 0;
+                fetch_age_hist[bk].fetch_add(1, std::memory_order_relaxed);
+              }
             }
             if (hv > 0) rec.skip((size_t)hv);
           }
@@ -893,6 +901,11 @@ int64_t ccfd_kc_position(void* kc, int part_index) {
 // no ccfd-ts header (tests; the engine reads it through ccfd_engine_ring_commit_at).
 int64_t ccfd_kc_last_origin(void* kc) {
   return kc ? static_cast<Consumer*>(kc)->cur_origin : -1;
+}
+
+void ccfd_kc_fetch_age_hist(void* kc, uint64_t* out256) {
+  auto* c = static_cast<Consumer*>(kc);
+  for (int i = 0; i < 256; ++i) out256[i] = c ? c->fetch_age_hist[i].load(std::memory_order_relaxed) : 0;
 }
 
 // Fuzz / unit entry: feed raw bytes as partition 0's record set of an array-sink consumer

@@ -451,6 +451,7 @@ int64_t ccfd_kc_committable(void* kc, int part_index);
 void ccfd_kc_get_stats(void* kc, ccfd_kc_stats* out);
 const char* ccfd_kc_last_error(void* kc);
 int64_t ccfd_kc_feed_record_set(void* kc, const uint8_t* data, int64_t n);   // tests / fuzzing
+void ccfd_kc_fetch_age_hist(void* kc, uint64_t* out256);   // batches by send -> fetched age (ns, 4 buckets/octave)
 int64_t ccfd_kc_last_origin(void* kc);         // send time (steady ns) of the last batch's ccfd-ts header, 0 = none
 int ccfd_kc_set_offset_reset(void* kc, int policy);                           // before start
 int64_t ccfd_kc_position(void* kc, int part_index);                           // next offset to fetch

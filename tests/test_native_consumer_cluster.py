@@ -150,5 +150,10 @@ def test_send_time_header_sets_the_batch_origin():
         origin = kc.last_origin_ns()
         assert abs((t_mono - origin) - 5_000_000) < 3_000_000, (t_mono - origin)
         assert kc.stats()["errors"] == 0
+        # the batch's send -> fetched age is binned (4 buckets per octave of ns): ~5 ms
+        from ccfd_demo_summit_amd.parallel.dp import hist_quantile
+        h = kc.fetch_age_hist()
+        assert int(h.sum()) == 1
+        assert 4e6 < hist_quantile(h, 0.5) < 9e6, hist_quantile(h, 0.5)
     finally:
         kc.close()
