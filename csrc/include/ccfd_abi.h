@@ -53,8 +53,6 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_ABLATE_FENCE 64      // no per-workgroup system release
 #define CCFD_ARG_CHUNK_RING 128       // persistent G32: one-chunk prefetch ring (default) instead of the whole item in flight
 #define CCFD_ARG_FLAG_DIRECT 1024      // W64 launch kernels: reserve flag-list slots per ballot (A/B of the LDS staging)
-#define CCFD_ARG_ITEM_PREFETCH 2048   // persistent G32 / G20: claim the next item and put its rows in flight
-                                      // before scoring the current one (hides the per-item completion)
 #define CCFD_ARG_ABLATE_ACQUIRE 512   // persistent kernels: no acquire before reading an item's rows (diagnostics)
 #define CCFD_ARG_PIPE_ITEMS 256       // persistent W64 MLP: statically assigned 64/128-row items, the next
                                       // item's rows fetched while the current one is scored

@@ -97,18 +97,6 @@ __device__ __forceinline__ int persist_wait_item(const ccfd_persist_args& a, int
   return 0;
 }
 
-// Thread 0: non-blocking -- if claimed item `item`'s micro-batch is already posted, read its
-// descriptor into `sdesc` and return 1; else 0 (wait later with persist_wait_item).
-__device__ __forceinline__ int persist_try_desc(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
-                                                unsigned long long item, ccfd_persist_desc& sdesc) {
-  const unsigned long long b = item / (unsigned long long)C;
-  if (posted_cache <= b)
-    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (posted_cache <= b) return 0;
-  persist_read_desc(a, b, sdesc);
-  return 1;
-}
-
 // Thread 0: claim the next work item, wait for its micro-batch, read its descriptor into
 // `sdesc`.  Sets cmd = 1 when the host stopped the kernel instead.
 __device__ __forceinline__ void persist_claim(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,

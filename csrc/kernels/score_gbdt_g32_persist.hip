@@ -14,10 +14,8 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   __shared__ uint4 xt[kG32Waves][128];
   __shared__ EpilogueLds epi;
   __shared__ ccfd_persist_desc sdesc;
-  __shared__ ccfd_persist_desc sdesc2[2];                 // CCFD_ARG_ITEM_PREFETCH: current / next item
   __shared__ unsigned long long s_item;
-  __shared__ unsigned long long s_items[2];
-  __shared__ int s_cmd, s_pre;
+  __shared__ int s_cmd;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -89,70 +87,6 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
-  // CCFD_ARG_ITEM_PREFETCH: a two-item software pipeline.  The next item is claimed and, when
-  // its micro-batch is already posted, its rows are put in flight BEFORE the current item is
-  // scored; the current item's completion (vmcnt drain + system release + ticket) then waits
-  // for loads that have been in flight for a whole item's compute instead of starting them
-  // afterwards.  Every item of a wave is in flight at once (cpw <= 2: 256 / 512-row items).
-  if ((a.flags & CCFD_ARG_ITEM_PREFETCH) && cpw <= 2) {
-    G32Row ra[2], rb[2];
-    auto issue = [&](const ccfd_persist_desc& d, unsigned long long it, G32Row (&r)[2]) __attribute__((always_inline)) {
-      const int c0 = (int)(it % (unsigned long long)C) * (kG32Waves * cpw) + wave;
-      const unsigned char* xb = reinterpret_cast<const unsigned char*>(d.x);
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int chunk = c0 + kG32Waves * k;
-        if (k < cpw && chunk * kG32Rows < d.n) gx_fetch<kG20>(xb, d.n, chunk, lane, r[k]);
-      }
-    };
-    auto score_item = [&](const ccfd_persist_desc& d, unsigned long long it, G32Row (&r)[2]) __attribute__((always_inline)) {
-      const int slot = (int)(d.seq % (unsigned long long)a.ring);
-      const int c0 = (int)(it % (unsigned long long)C) * (kG32Waves * cpw) + wave;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int chunk = c0 + kG32Waves * k;
-        if (k >= cpw || chunk * kG32Rows >= d.n) break;   // wave-uniform
-        score_chunk(d, slot, d.n, chunk, r[k]);
-      }
-      item_flush(d, slot);                                 // ends with barriers (persist_item_done)
-    };
-    if (tid == 0) persist_claim(a, C, posted_cache, sdesc2[0], s_items[0], s_cmd);
-    __syncthreads();
-    if (s_cmd) return;
-    int cur = 0;
-    {
-      const ccfd_persist_desc d = sdesc2[0];
-      k7_start(s_items[0], (int)(d.seq % (unsigned long long)a.ring));
-      issue(d, s_items[0], ra);
-    }
-    for (;;) {
-      const int nxt = cur ^ 1;
-      if (tid == 0) {
-        s_items[nxt] = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_pre = persist_try_desc(a, C, posted_cache, s_items[nxt], sdesc2[nxt]);
-      }
-      __syncthreads();
-      const bool pre = s_pre != 0;
-      const ccfd_persist_desc dc = sdesc2[cur];
-      const unsigned long long ic = s_items[cur];
-      if (pre) {
-        const ccfd_persist_desc dn = sdesc2[nxt];
-        k7_start(s_items[nxt], (int)(dn.seq % (unsigned long long)a.ring));
-        if (cur == 0) issue(dn, s_items[nxt], rb); else issue(dn, s_items[nxt], ra);
-      }
-      if (cur == 0) score_item(dc, ic, ra); else score_item(dc, ic, rb);
-      if (!pre) {
-        if (tid == 0) s_cmd = persist_wait_item(a, C, posted_cache, s_items[nxt], sdesc2[nxt]);
-        __syncthreads();
-        if (s_cmd) return;
-        const ccfd_persist_desc dn = sdesc2[nxt];
-        k7_start(s_items[nxt], (int)(dn.seq % (unsigned long long)a.ring));
-        if (cur == 0) issue(dn, s_items[nxt], rb); else issue(dn, s_items[nxt], ra);
-      }
-      cur = nxt;
-    }
-  }
-
   for (;;) {
     if (tid == 0) persist_claim(a, C, posted_cache, sdesc, s_item, s_cmd);
     __syncthreads();
@@ -211,9 +145,6 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   // trees overlap the next chunk's load better); CCFD_G32_INFLIGHT=1 selects the latter.
   // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
   if (g32_env("CCFD_G32_INFLIGHT", 0, 0, 1) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
-  // two-item pipeline (next item's rows in flight while the current one is scored); env
-  // CCFD_G32_ITEM_PREFETCH=0 / 1 (default 0 until measured, profiles/r4/g20/)
-  if (g32_env("CCFD_G32_ITEM_PREFETCH", 0, 0, 1) == 1) a.flags |= CCFD_ARG_ITEM_PREFETCH;
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
   if (gl) {

@@ -214,14 +214,14 @@ def test_g20_rules_hot_swap_and_global_leaves(gpu, exec_mode):
 
 @pytest.mark.parametrize("fmt", ["g20", "g32"])
 @pytest.mark.parametrize("item_rows", [256, 512])
-def test_item_prefetch_pipeline_exact(gpu, monkeypatch, fmt, item_rows):
-    """CCFD_G32_ITEM_PREFETCH=1: the two-item pipeline (next item claimed and its rows in
-    flight before the current one is scored) -- full, partial and back-to-back micro-batches
-    over several pump calls (the kernel halts and relaunches between them), every row once,
-    proba per row exact (scored ring), counters and histograms exact."""
+def test_persistent_item_sizes_exact(gpu, monkeypatch, fmt, item_rows):
+    """The persistent G20 / G32 kernel at 256- and 512-row items: full, partial and
+    back-to-back micro-batches over several pump calls (the kernel halts and relaunches
+    between them), every row once, proba per row exact (scored ring), counters and
+    histograms exact.  (Round 4 also measured a two-item prefetch pipeline here: 2.30 vs
+    2.51 x 10^9 tx/s, removed -- profiles/r4/g20/item_prefetch/.)"""
     from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.ops.kernels import DeviceModel
-    monkeypatch.setenv("CCFD_G32_ITEM_PREFETCH", "1")
     monkeypatch.setenv("CCFD_PERSIST_ITEM_ROWS", str(item_rows))
     B = 65536
     X, _ = generate(B * 4 + 5000, seed=59)
