@@ -200,6 +200,9 @@ def main(argv=None):
     ap.add_argument("--trace", action="store_true",
                     help="engine ranks record their stage trace + scoring-loop timeline "
                          "(CCFD_SERVICE_TRACE) and the tail is attributed (bench/tail_attribution.py)")
+    ap.add_argument("--journal-dir", default=None,
+                    help="parent directory of the KIE journal / hand-off DLQ (default: $TMPDIR, the same "
+                         "disk as kafka-lite's data; /dev/shm separates it from the broker's writeback)")
     ap.add_argument("--sample-s", type=float, default=5.0)
     ap.add_argument("--drain-timeout-s", type=float, default=120.0)
     ap.add_argument("--log-dir", default="gpurun_out/deploy_topology")
@@ -242,7 +245,7 @@ def main(argv=None):
         kie_env["CCFD_KIE_NOTIFICATION_TIMEOUT_S"] = str(a.notification_timeout_s)
         # the journal grows ~1 KB per fraud process: keep it out of the log directory
         import tempfile
-        jdir = tempfile.mkdtemp(prefix="ccfd-kie-journal-")
+        jdir = tempfile.mkdtemp(prefix="ccfd-kie-journal-", dir=a.journal_dir)
         journal = Path(jdir) / "kie-journal.jsonl"
         kie_cmd = [PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_port), "--journal", str(journal)]
         procs.append(Proc("kie", kie_cmd, kie_env, log_dir))

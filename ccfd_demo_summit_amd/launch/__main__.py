@@ -205,8 +205,9 @@ def cmd_kie(a, cfg):
     else:
         eng = ProcessEngine.from_config(cfg.kie, journal_path=a.journal, **kw)
     srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
-    from ..utils.gcpolicy import tune_for_service
+    from ..utils.gcpolicy import track_pauses, tune_for_service
     print(f"[kie] gc: {tune_for_service()}", flush=True)
+    track_pauses(srv.gc_pauses)
     web.run_app(srv.app, host=a.host, port=a.port or cfg.kie.port, print=None, access_log=None)
 
 

@@ -121,6 +121,9 @@ class ProcessEngine:
         # scored -> process started (the engine's hand-off items carry ``scored_ns``, the wall
         # clock their results were collected): 4 buckets per octave of ns, like the engine's
         self.handoff_hist = [0] * 256
+        # journal appends (a write() that dirty-page throttling can stall): attribution
+        from ..utils.lathist import LatHist
+        self.journal_time = LatHist()
 
     @classmethod
     def from_config(cls, kie_cfg, **kw) -> "ProcessEngine":
@@ -140,7 +143,10 @@ class ProcessEngine:
         rec = {"instance": d}
         if inst.task_id is not None and inst.task_id in self.tasks:
             rec["task"] = vars(self.tasks[inst.task_id])
-        self._journal.write(json.dumps(rec, default=float) + "\n")
+        line = json.dumps(rec, default=float) + "\n"
+        t0 = time.monotonic_ns()
+        self._journal.write(line)
+        self.journal_time.add(time.monotonic_ns() - t0)
 
     @classmethod
     def recover(cls, journal_path: str, **kw) -> "ProcessEngine":
@@ -279,7 +285,9 @@ class ProcessEngine:
 
                 import numpy as np
                 tx64 = base64.b64encode(np.asarray(new, np.int64).tobytes()).decode()
+                t0 = time.monotonic_ns()
                 self._journal.write('{"standard": {"id0": %d, "tx_i64": "%s"}}\n' % (first, tx64))
+                self.journal_time.add(time.monotonic_ns() - t0)
         return out
 
     def _note_handoff(self, scored_ns, n: int = 1) -> None:

@@ -104,12 +104,15 @@ class KieServer:
         self.handler_time = LatHist()
         self.tick_time = LatHist()
         self.loop_lag = LatHist()
+        self.gc_pauses = LatHist()          # filled when the service tracks GC (cmd_kie)
 
     def attribution(self) -> dict:
         return {"received_after_scored_us": self.recv_after_scored.summary_us(),
                 "start_handler_us": self.handler_time.summary_us(),
                 "timer_tick_us": self.tick_time.summary_us(),
-                "event_loop_lag_us": self.loop_lag.summary_us()}
+                "event_loop_lag_us": self.loop_lag.summary_us(),
+                "journal_write_us": self.engine.journal_time.summary_us(),
+                "gc_pause_us": self.gc_pauses.summary_us()}
 
     async def _startup(self, _app):
         async def loop():

@@ -31,3 +31,18 @@ def tune_for_service(gen0: int = 50_000, gen1: int = 20, gen2: int = 1000) -> st
     gc.freeze()
     gc.set_threshold(gen0, gen1, gen2)
     return f"frozen {gc.get_freeze_count()} objects, thresholds {gc.get_threshold()}"
+
+
+def track_pauses(hist) -> None:
+    """Record every cyclic-GC pass's duration (ns) into ``hist`` (utils.lathist.LatHist):
+    the services' latency attribution names GC pauses instead of guessing them."""
+    import time
+    t0 = [0]
+
+    def cb(phase, _info):
+        if phase == "start":
+            t0[0] = time.monotonic_ns()
+        elif t0[0]:
+            hist.add(time.monotonic_ns() - t0[0])
+            t0[0] = 0
+    gc.callbacks.append(cb)

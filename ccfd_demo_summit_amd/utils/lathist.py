@@ -51,5 +51,6 @@ class LatHist:
         n = self.count()
         if not n:
             return {"n": 0}
-        return {"n": n, "p50": round(self.quantile_ns(0.5) / 1e3, 1),
-                "p99": round(self.quantile_ns(0.99) / 1e3, 1), "max": round(self.max_ns / 1e3, 1)}
+        mx = self.max_ns                     # interpolation never reports beyond the max seen
+        return {"n": n, "p50": round(min(self.quantile_ns(0.5), mx) / 1e3, 1),
+                "p99": round(min(self.quantile_ns(0.99), mx) / 1e3, 1), "max": round(mx / 1e3, 1)}

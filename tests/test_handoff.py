@@ -304,6 +304,7 @@ def test_scored_to_started_attribution_on_both_sides(kie):
     att = body["handoff_attribution"]
     assert att["received_after_scored_us"]["n"] == 300          # every started row counted once
     assert att["start_handler_us"]["n"] >= 2 and att["timer_tick_us"]["n"] >= 1
+    assert "journal_write_us" in att and "gc_pause_us" in att
     assert body["scored_to_started_us"]["n"] == 300
     # the histogram's interpolated quantiles stay inside the bucket of the values added
     h = LatHist()
