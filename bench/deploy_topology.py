@@ -371,6 +371,9 @@ def main(argv=None):
         steady = [s["tx_s"] for s in samples[1:-1]] or [s["tx_s"] for s in samples]
         out.update({
             "value": round((r_w1 - r_w0) / max(t_w1 - t_w0, 1e-9), 1), "unit": "tx/s",
+            # wall clock of the measured window and of the end of the drain (the services'
+            # attribution maxima carry "max_at" on the same clock)
+            "window_wall": [round(t_w0, 3), round(t_w1, 3)],
             "window_s": round(t_w1 - t_w0, 1), "samples": samples,
             "min_sample_tx_s": min(steady) if steady else None,
             "producers_tx_s": [d["tx_s"] for d in produced_lines],
@@ -378,6 +381,7 @@ def main(argv=None):
             "transaction_incoming_total": rows_all,
             "incoming_equals_produced": int(rows_all) == int(produced),
             "drain_s": round(time.time() - t_d, 1),
+            "drained_wall": round(time.time(), 3),
             "final_lag_msgs": kb.lag("ccfd-engine", "odh-demo"),
         })
         # ---- ingest attribution: the engine's native consumer threads (ccfd_gpu_ingest_*)

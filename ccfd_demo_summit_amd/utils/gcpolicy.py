@@ -10,9 +10,17 @@ Python scoring loop (profiles/r4/tail/).  These services create almost no refere
 
 * ``gc.freeze()`` after start-up moves everything allocated so far (imports, models, config)
   into the permanent generation -- never scanned again;
-* generation 0 collects every ``gen0`` allocations (default 50 000, not 700) and a full
-  collection needs ``gen2`` generation-1 collections -- about one per 10^9 allocations,
-  i.e. practically only when asked for.
+* young collections stay SMALL: generation 0 every ``gen0`` (10 000) allocations and
+  generation 1 on every second one, so a pause scans at most a few 10^4 young objects
+  (~7 ms), and survivors move on to generation 2;
+* generation 2 (a full collection) needs ``gen2`` (10^6) generation-1 collections, i.e.
+  practically never happens by itself.
+
+Round 4 first used (50 000, 20, 1000): generation 1 then held up to 10^6 objects and a KIE
+server starting ~10^4 fraud processes a second paused for up to 240 ms per collection
+(``/rest/stats handoff_attribution.gc_pause_us``, profiles/r4/kie_handoff/): the TXB1
+runs' scored -> process-started tail.  Measured on the KIE start + signal path: the old policy's
+max pause 172 ms, (20 000, 1, 10^6) 13.6 ms, (10 000, 1, 10^6) 6.8 ms at the same throughput.
 
 ``CCFD_GC=default`` keeps CPython's defaults (A/B switch).
 """
@@ -22,7 +30,7 @@ import gc
 import os
 
 
-def tune_for_service(gen0: int = 50_000, gen1: int = 20, gen2: int = 1000) -> str:
+def tune_for_service(gen0: int = 10_000, gen1: int = 1, gen2: int = 1_000_000) -> str:
     """Apply the service GC policy (call once start-up is done); returns what was applied."""
     mode = os.environ.get("CCFD_GC", "service")
     if mode == "default":

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import math
 import threading
+import time
 from typing import Dict, Optional
 
 
@@ -18,6 +19,7 @@ class LatHist:
     def __init__(self):
         self.h = [0] * self.N
         self.max_ns = 0
+        self.max_at = 0.0                    # wall clock (time.time()) of the largest value
         self._lock = threading.Lock()
 
     def add(self, ns: int, n: int = 1) -> None:
@@ -28,6 +30,7 @@ class LatHist:
             self.h[i] += n
             if ns > self.max_ns:
                 self.max_ns = ns
+                self.max_at = time.time()
 
     def count(self) -> int:
         return sum(self.h)
@@ -47,10 +50,12 @@ class LatHist:
         return 2.0 ** (self.N / 4.0)
 
     def summary_us(self) -> Dict[str, float]:
-        """{"n", "p50", "p99", "max"} in microseconds (p50/p99 interpolated in the bucket)."""
+        """{"n", "p50", "p99", "max"} in microseconds (p50/p99 interpolated in the bucket), and
+        "max_at": the wall-clock second the max was seen (to place it in a run's timeline)."""
         n = self.count()
         if not n:
             return {"n": 0}
         mx = self.max_ns                     # interpolation never reports beyond the max seen
         return {"n": n, "p50": round(min(self.quantile_ns(0.5), mx) / 1e3, 1),
-                "p99": round(min(self.quantile_ns(0.99), mx) / 1e3, 1), "max": round(mx / 1e3, 1)}
+                "p99": round(min(self.quantile_ns(0.99), mx) / 1e3, 1), "max": round(mx / 1e3, 1),
+                "max_at": round(self.max_at, 3)}

@@ -18,7 +18,7 @@ def _run(env_mode):
 
 def test_service_policy_and_default_switch():
     out = _run(None)
-    assert "(50000, 20, 1000)" in out and out.startswith("frozen")
+    assert "(10000, 1, 1000000)" in out and out.startswith("frozen")
     assert int(out.split()[-1]) > 1000
     out = _run("default")
     assert out.startswith("default") and "(700, 10, 10)" in out
