@@ -79,6 +79,10 @@ class DurableBatchStore(BatchStore):
         os.makedirs(self.data_dir, exist_ok=True)
         self._segs: Dict[Tuple[str, int], List[_Segment]] = {}
         self._dirty: set = set()            # fds written since the last fsync
+        # fds of rolled / retired segments: fsync'd and closed by flush() (the flusher thread
+        # in "interval" mode), never on the produce path -- a 256 MB segment's fsync under the
+        # store lock stalled every produce and fetch of the broker behind it
+        self._closing: List[int] = []
         self._off_fd = -1
         self.recovered: Dict[str, object] = {}
         self.bytes_written = 0
@@ -114,10 +118,19 @@ class DurableBatchStore(BatchStore):
             self.flush()
 
     def flush(self) -> None:
-        """fsync every file written since the last flush."""
+        """fsync every file written since the last flush; close retired segment files."""
         with self._lock:
             fds, self._dirty = self._dirty, set()
-        self._sync(fds)
+            closing, self._closing = self._closing, []
+        self._sync(fds - set(closing))
+        for fd in closing:                  # not reachable from the store any more
+            if self.fsync != "never":
+                try:
+                    os.fsync(fd)
+                    self.fsyncs += 1
+                except OSError:
+                    pass
+            os.close(fd)
 
     def _atomic_json(self, name: str, obj) -> None:
         path = os.path.join(self.data_dir, name)
@@ -138,17 +151,24 @@ class DurableBatchStore(BatchStore):
         self._segs.setdefault((topic, p), []).append(seg)
         return seg
 
-    def _close_segment(self, seg: _Segment) -> None:
+    def _close_segment(self, seg: _Segment, now: bool = False) -> None:
+        """Retire a segment's files (under the store lock).  ``now``: fsync + close here (shutdown,
+        fsync="always"); "interval" hands them to the flusher thread's next flush(), so the produce
+        path never waits on a big fsync; "never" closes them at once."""
         if seg.closed:
             return
         for fd in (seg.fd, seg.idx_fd):
             if fd >= 0:
                 self._dirty.discard(fd)
-                try:
-                    os.fsync(fd)
-                except OSError:
-                    pass
-                os.close(fd)
+                if self.fsync == "interval" and not now:
+                    self._closing.append(fd)
+                    continue
+                if now or self.fsync == "always":
+                    try:
+                        os.fsync(fd)
+                    except OSError:
+                        pass
+                os.close(fd)                # "never": closed at once, no fsync
         seg.fd = seg.idx_fd = -1
         seg.closed = True
 
@@ -344,10 +364,11 @@ class DurableBatchStore(BatchStore):
         self._stop.set()
         if self._flusher is not None:
             self._flusher.join(5)
+        self.flush()                        # retired segments' deferred fsync + close
         with self._lock:
             for segs in self._segs.values():
                 for seg in segs:
-                    self._close_segment(seg)
+                    self._close_segment(seg, now=True)
             if self._off_fd >= 0:
                 os.fsync(self._off_fd)
                 os.close(self._off_fd)
