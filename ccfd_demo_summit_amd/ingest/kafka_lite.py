@@ -888,6 +888,8 @@ def main(argv=None):
                     help="--data-dir flush policy: before every answer, every second in the background, "
                          "or left to the OS (a killed broker process loses nothing in any mode)")
     a = ap.parse_args(argv)
+    from .kafka_wire import warm_native
+    print(f"[kafka-lite] native codecs loaded in {warm_native():.2f} s", flush=True)
     cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions, advertise=a.advertise,
                           retention_batches=a.retention_batches or None, data_dir=a.data_dir, fsync=a.fsync)
     if a.data_dir:

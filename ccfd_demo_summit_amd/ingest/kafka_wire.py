@@ -93,6 +93,19 @@ def crc32c(data: bytes) -> int:
     return _crc32c_py(data)
 
 
+def warm_native() -> float:
+    """Load the native CRC-32C / RecordBatch codecs now (seconds taken).  They live in the
+    engine's library, whose first load also brings up the HIP runtime -- ~0.3 s with the GIL
+    held.  A service that loaded it lazily on its first produce stalled its event loop right
+    when traffic began: the KIE server's 270-450 ms event-loop lag at the start of every
+    deployed run, which was the whole scored -> process-started p99 (profiles/r4/kie_handoff/).
+    Services call this before they start serving."""
+    t0 = time.perf_counter()
+    crc32c(b"ccfd")
+    _native_encoder()
+    return time.perf_counter() - t0
+
+
 # --------------------------------------------------------------------------- primitives
 class Writer:
     __slots__ = ("parts",)

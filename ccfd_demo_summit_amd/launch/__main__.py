@@ -205,6 +205,8 @@ def cmd_kie(a, cfg):
     else:
         eng = ProcessEngine.from_config(cfg.kie, journal_path=a.journal, **kw)
     srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
+    from ..ingest.kafka_wire import warm_native
+    print(f"[kie] native codecs loaded in {warm_native():.2f} s", flush=True)
     from ..utils.gcpolicy import track_pauses, tune_for_service
     print(f"[kie] gc: {tune_for_service()}", flush=True)
     track_pauses(srv.gc_pauses)
@@ -227,6 +229,8 @@ def cmd_notifier(a, cfg):
     app.router.add_get("/health/ping", lambda _r: web.json_response(
         {"status": "ok", "sent": ns.sent, "replied": ns.replied, "no_reply": ns.no_reply}))
     _serve_in_thread(app, a.host, a.port or cfg.notifier.port)
+    from ..ingest.kafka_wire import warm_native
+    warm_native()                       # the reply publisher's codecs, before the first reply
     from ..utils.gcpolicy import tune_for_service
     tune_for_service()
     while True:
@@ -393,6 +397,10 @@ def cmd_producer(a, cfg):
     broker = _broker(cfg, idempotent=True)
     broker.stamp_time = True          # ccfd-ts send-time header: the engine's produce -> scored latency
     prod = TransactionProducer(broker, pc)
+    from ..ingest.kafka_wire import warm_native
+    warm_native()
+    if a.fmt == "txb1" and pc.source == "synthetic":
+        prod._txb1_pooled()                 # generate the batch pool before the clock starts
     if a.fmt == "json" and pc.source == "synthetic":
         prod._ensure_pool()                 # render the message pool before the clock starts
         prod._native_json_record_set()      # (and load the native encoder)

@@ -142,18 +142,22 @@ def test_send_time_header_sets_the_batch_origin():
     kc = NativeKafkaConsumer.for_arrays("127.0.0.1:1", "t", {0: 0}, capacity=1000)
     try:
         assert kc.feed(rs) == 1 and kc.last_origin_ns() == 0
-        b = with_produce_time(encode_record_batch([b'{"id": 7, "Amount": 1.0}'] * 10, base_offset=1),
-                              time.time_ns() - 5_000_000)
+        t_send = time.time_ns() - 5_000_000
+        b = with_produce_time(encode_record_batch([b'{"id": 7, "Amount": 1.0}'] * 10, base_offset=1), t_send)
         seal_batches(b)
-        t_mono = time.monotonic_ns()
+        t_mono, t_wall = time.monotonic_ns(), time.time_ns()
         assert kc.feed(bytes(b)) == 10
         origin = kc.last_origin_ns()
-        assert abs((t_mono - origin) - 5_000_000) < 3_000_000, (t_mono - origin)
+        # origin is the send time on the steady clock: t_mono - origin == t_wall - t_send (~5 ms
+        # plus the encode above, however long a loaded machine took for it)
+        assert abs((t_mono - origin) - (t_wall - t_send)) < 2_000_000, (t_mono - origin, t_wall - t_send)
         assert kc.stats()["errors"] == 0
         # the batch's send -> fetched age is binned (4 buckets per octave of ns): ~5 ms
         from ccfd_demo_summit_amd.parallel.dp import hist_quantile
         h = kc.fetch_age_hist()
         assert int(h.sum()) == 1
-        assert 4e6 < hist_quantile(h, 0.5) < 9e6, hist_quantile(h, 0.5)
+        upper = time.time_ns() - t_send             # the age can only be smaller than this
+        q = hist_quantile(h, 0.5)                   # log buckets: within one 2^(1/4) bucket
+        assert 5e6 / 1.2 < q < upper * 1.2, (q, upper)
     finally:
         kc.close()
