@@ -22,8 +22,8 @@ def parse_json_batch(values: Sequence[bytes], native: bool = True) -> Tuple[np.n
         return feats, ids, cust
     if native:
         try:
-            from ..ops._lib import lib
-            L = lib()
+            from .kafka_wire import _codec_lib      # host-only library: no GPU runtime
+            L = _codec_lib()
         except Exception:
             L = None
         if L is not None:

@@ -65,6 +65,17 @@ def _crc32c_py(data: bytes, crc: int = 0) -> int:
     return crc ^ 0xFFFFFFFF
 
 
+def _codec_lib():
+    """The host-only codec library (ops/_hostlib.py: no HIP runtime, no GPU); the engine
+    library as a fallback where the host one cannot be built."""
+    try:
+        from ..ops._hostlib import hostlib
+        return hostlib()
+    except Exception:
+        from ..ops._lib import lib
+        return lib()
+
+
 _native_crc = None
 
 
@@ -73,8 +84,7 @@ def crc32c(data: bytes) -> int:
     if _native_crc is None:
         try:
             import ctypes as C
-            from ..ops._lib import lib
-            f = lib().ccfd_crc32c
+            f = _codec_lib().ccfd_crc32c
             f.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
             f.restype = C.c_uint32
             _native_crc = f
@@ -94,12 +104,13 @@ def crc32c(data: bytes) -> int:
 
 
 def warm_native() -> float:
-    """Load the native CRC-32C / RecordBatch codecs now (seconds taken).  They live in the
-    engine's library, whose first load also brings up the HIP runtime -- ~0.3 s with the GIL
-    held.  A service that loaded it lazily on its first produce stalled its event loop right
-    when traffic began: the KIE server's 270-450 ms event-loop lag at the start of every
-    deployed run, which was the whole scored -> process-started p99 (profiles/r4/kie_handoff/).
-    Services call this before they start serving."""
+    """Load the native CRC-32C / RecordBatch codecs now (seconds taken).  They used to be
+    loaded from the engine's library, whose first load also brings up the HIP runtime (~0.3 s
+    with the GIL held): a service that loaded it lazily on its first produce stalled its event
+    loop right when traffic began -- the KIE server's 270-450 ms event-loop lag at the start of
+    every deployed run, the whole scored -> process-started p99 (profiles/r4/kie_handoff/).
+    They now come from the host-only library (ops/_hostlib.py); services still load it before
+    they start serving."""
     t0 = time.perf_counter()
     crc32c(b"ccfd")
     _native_encoder()
@@ -251,8 +262,7 @@ def _native_encoder():
     if _native_enc is None:
         try:
             import ctypes as C
-            from ..ops._lib import lib
-            L = lib()
+            L = _codec_lib()
             L.ccfd_kafka_encode_batch.argtypes = [C.c_char_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64]
             L.ccfd_kafka_encode_batch.restype = C.c_int64
             L.ccfd_kafka_batch_bound.argtypes = [C.c_int64, C.c_int64]

@@ -30,6 +30,40 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 SANITIZE = os.environ.get("CCFD_SANITIZE", "")
 
 
+# Host-only codecs (CRC-32C, Kafka RecordBatch framing, JSON transaction parsing, row
+# encoders) ALSO go into a small library with no HIP dependency: the broker, KIE, notifier
+# and producer processes load only this one, so they never bring up the GPU runtime (CPU-only
+# pods in the operator's deployment; ~0.3 s with the GIL held in a service that loaded the
+# engine library lazily, profiles/r4/kie_handoff/).
+HOST_LIB = NATIVE / "libccfd_host.so"
+HOST_SOURCES = ("crc32c.cpp", "kafka_codec.cpp", "ingest.cpp")
+
+
+def host_sources():
+    return [CSRC / "engine" / n for n in HOST_SOURCES]
+
+
+def build_host(force: bool = False, verbose: bool = True) -> Path:
+    """g++ -> libccfd_host.so (plain C++, no offload, no libamdhip64)."""
+    OBJ.mkdir(parents=True, exist_ok=True)
+    NATIVE.mkdir(parents=True, exist_ok=True)
+    cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++")
+    if not cxx:
+        raise RuntimeError("no host C++ compiler for libccfd_host.so")
+    newest = max([s.stat().st_mtime for s in host_sources()] + [_headers_mtime()])
+    if force or not HOST_LIB.exists() or HOST_LIB.stat().st_mtime < newest:
+        tmp = HOST_LIB.with_suffix(".so.tmp")
+        cmd = [cxx, "-O3", "-fPIC", "-shared", "-std=c++17", "-Wall", "-I", str(CSRC / "include"),
+               "-o", str(tmp)] + [str(s) for s in host_sources()] + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"host lib build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, HOST_LIB)
+    if verbose:
+        print(f"[ccfd build] {HOST_LIB} ({len(HOST_SOURCES)} host sources)")
+    return HOST_LIB
+
+
 def lib_path(sanitize: str = SANITIZE) -> Path:
     return LIB if not sanitize else NATIVE / f"libccfd_hip_{sanitize.replace(',', '_')}.so"
 
@@ -93,6 +127,8 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True, sanitize: st
         os.replace(tmp, LIB)
     if verbose:
         print(f"[ccfd build] {LIB} ({len(srcs)} sources, arch {ARCH})")
+    if not sanitize:
+        build_host(force=force, verbose=verbose)
     return LIB
 
 
