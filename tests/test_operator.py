@@ -276,6 +276,26 @@ def test_local_commands_probe_the_rendered_health_routes():
     assert cmds["kafka"][3][0](0)[0] == "tcp" and cmds["producer"][3] is None
 
 
+def _free_offset(bases, tries=200):
+    import socket
+    for _ in range(tries):
+        off = random.randint(20000, 40000)
+        ok = True
+        for b in bases:
+            sk = socket.socket()
+            try:
+                sk.bind(("127.0.0.1", b + off))
+            except OSError:
+                ok = False
+            finally:
+                sk.close()
+            if not ok:
+                break
+        if ok:
+            return off
+    raise RuntimeError("no free port offset")
+
+
 def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
     """Only the CR's kafka section deployed: the operator starts kafka-lite with 3 listeners
     and a Kafka client produces to / fetches from it through the bootstrap list."""
@@ -285,7 +305,7 @@ def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
         d["spec"][k]["deploy"] = False
     d["spec"]["kafka"].update(brokers=3, partitions=6)
     spec = parse(d)
-    off = random.randint(20000, 40000)
+    off = _free_offset([9092, 9093, 9094, 9404])       # parallel test workers: never a taken port
     op = LocalOperator(spec, workdir=str(ROOT), commands=None, grace_s=5, log=lambda m: None, port_offset=off,
                        state_dir=str(tmp_path / "state"))
     try:
