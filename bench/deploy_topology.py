@@ -193,6 +193,8 @@ def main(argv=None):
                     help="... and restart it from its data directory this long after")
     ap.add_argument("--fsync", default="interval", choices=["always", "interval", "never"],
                     help="kafka-lite durability flush policy (its logs are always on disk here)")
+    ap.add_argument("--kafka-memory", action="store_true",
+                    help="kafka-lite without --data-dir (round 3's in-memory broker): the A/B of durability")
     ap.add_argument("--standard-mode", default="count", choices=["count", "process"],
                     help="process: a standard process per standard-routed transaction (README.md:552)")
     ap.add_argument("--serving", default="native", choices=["native", "python"],
@@ -228,13 +230,14 @@ def main(argv=None):
                  "model": a.model}
     import tempfile
     kdir = tempfile.mkdtemp(prefix="ccfd-kafka-lite-")          # durable logs + committed offsets
-    out["kafka_durable"] = {"fsync": a.fsync}
+    out["kafka_durable"] = {"fsync": a.fsync} if not a.kafka_memory else False
     try:
         L = "ccfd_demo_summit_amd.launch"
         kafka_cmd = [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
                      "--port", str(kafka_port), "--nodes", str(a.kafka_nodes),
                      "--partitions", str(a.partitions), "--metrics-port", str(metrics_port),
-                     "--retention-batches", str(a.retention_batches), "--data-dir", kdir, "--fsync", a.fsync]
+                     "--retention-batches", str(a.retention_batches)] + \
+            ([] if a.kafka_memory else ["--data-dir", kdir, "--fsync", a.fsync])
         procs.append(Proc("kafka-lite", kafka_cmd, env, log_dir))
         wait_port(kafka_port, 60)
         from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
