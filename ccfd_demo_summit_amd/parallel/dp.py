@@ -61,8 +61,12 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     gpu_ok = torch.cuda.is_available()
     use_gpu = gpu_ok and (backend != "gloo" or os.environ.get("CCFD_DIST_BACKEND") == "gloo")
     if use_gpu:
+        n_dev = torch.cuda.device_count()
         if os.environ.get("CCFD_DEVICE_MODULO") == "1":
-            local = local % max(1, torch.cuda.device_count())
+            local = local % max(1, n_dev)
+        elif local >= n_dev:
+            raise RuntimeError(f"LOCAL_RANK {local} but this node has {n_dev} visible GPU(s): one rank per "
+                               "GPU (a rehearsal shares them: bench.py --rehearsal / CCFD_DEVICE_MODULO=1)")
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

@@ -40,5 +40,13 @@ def test_bench_json_contract(gpu):
 
 
 def test_bench_refuses_gpu_count_mismatch(gpu):
-    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1"])
-    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+    # an explicit WORLD_SIZE that disagrees with --gpus is refused, never re-launched
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1"],
+             env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr, r.stderr[-2000:]
+    import torch
+    if torch.cuda.device_count() < 2:
+        # --gpus 2 self-spawns two ranks (launch/local_ranks.py); on a one-GPU box the second
+        # rank refuses with a clear message and the parent exits non-zero
+        r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1"])
+        assert r.returncode != 0 and "visible GPU" in r.stderr, r.stderr[-2000:]
