@@ -24,7 +24,7 @@ from aiohttp import web
 
 from ..metrics.exporter import CONTENT_TYPE
 from ..utils.lathist import LatHist
-from .engine import ProcessEngine, rows_of
+from .engine import ProcessEngine
 
 BASE = "/services/rest/server"
 
@@ -178,7 +178,7 @@ class KieServer:
             if pid == self.standard_pid:
                 ids = self.engine.start_standard_many(items)
             elif pid == self.fraud_pid:
-                ids = [self.engine.start_fraud(v) for v in rows_of(items)]
+                ids = self.engine.start_fraud_many(items)
             else:
                 ids = None
         except (ValueError, TypeError, AttributeError) as e:

@@ -188,3 +188,30 @@ def test_standard_batches_idempotent_and_recovered(tmp_path):
     assert again[:2] == [ids1[0], ids2[1]] and r.standard_count == 5
     assert again[2] > max(ids1 + ids2 + [f])          # fresh ids never collide after recovery
     r.close()
+
+
+def test_start_fraud_many_matches_one_by_one_starts(tmp_path):
+    """The batched fraud start (KIE instances/batch, the in-process router sink) has the
+    per-transaction semantics of start_fraud: a duplicate inside the batch or from an earlier
+    one returns the existing instance and publishes nothing; one journal record and one
+    notification per new instance; the journal recovers the batch (timers included)."""
+    from ccfd_demo_summit_amd.process.engine import ProcessEngine
+    j = str(tmp_path / "j.jsonl")
+    sent = []
+    e = ProcessEngine(notification_timeout_s=30, journal_path=j, publish_notification=sent.append,
+                      clock=lambda: 100.0)
+    first = e.start_fraud({"transaction_id": 7, "customer_id": 1, "amount": 5.0, "proba": 0.9})
+    items = [{"transaction_id": t, "customer_id": t % 3, "amount": float(t), "proba": 0.8, "scored_ns": 1}
+             for t in (1, 2, 7, 3, 2)]
+    ids = e.start_fraud_many(items)
+    assert ids[2] == first and ids[4] == ids[1] and len(set(ids)) == 4
+    assert e.duplicates == 2 and len(e._by_tx) == 4
+    assert [m["transaction_id"] for m in sent] == [7, 1, 2, 3]
+    assert [m["process_id"] for m in sent[1:]] == [ids[0], ids[1], ids[3]]
+    cols = e.start_fraud_many({"transaction_id": [4, 1], "customer_id": [0, 0], "amount": [1.0, 1.0],
+                               "proba": [0.7, 0.7]})
+    assert cols[1] == ids[0] and len(e._by_tx) == 5
+    e.close()
+    r = ProcessEngine.recover(j, notification_timeout_s=30, clock=lambda: 100.0)
+    assert sorted(r._by_tx) == [1, 2, 3, 4, 7]
+    assert r.tick(now=131.0) == 5                      # every recovered timer fires once
