@@ -191,9 +191,11 @@ class Consumer {
   // producer send time of the batch being ingested, on the steady clock: from the ccfd-ts
   // header of its first record (ingest/kafka_wire.py with_produce_time), 0 when absent
   int64_t cur_origin = 0;
-  // send -> this thread has the batch (broker + network + fetch), ns, 4 buckets per octave:
-  // splits the engine's produce -> scored into the broker side and parse + ring + scoring
+  // send -> the fetch response carrying the batch was received (broker + network + fetch
+  // wait), ns, 4 buckets per octave: splits the engine's produce -> scored into the broker
+  // side and parse (including earlier batches of the same response) + ring + scoring
   std::atomic<uint64_t> fetch_age_hist[256] = {};
+  int64_t fetch_real = 0;                           // wall clock the current response arrived
   static int64_t real_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
         .count();
@@ -630,7 +632,8 @@ class Consumer {
               const int64_t age = real_ns() - (int64_t)ts;       // send -> now (same host clock)
               if (age >= 0 && age < 3600ll * 1000000000ll) {
                 cur_origin = mono_ns() - age;
-                const int bk = age > 0 ? std::min(255, (int)(4.0 * std::log2((double)age))) : 0;
+                const int64_t fa = fetch_real > 0 ? std::max<int64_t>(0, fetch_real - (int64_t)ts) : age;
+                const int bk = fa > 0 ? std::min(255, (int)(4.0 * std::log2((double)fa))) : 0;
                 fetch_age_hist[bk].fetch_add(1, std::memory_order_relaxed);
               }
             }
@@ -751,6 +754,7 @@ class Consumer {
         }
         n_fetches.fetch_add(1, std::memory_order_relaxed);
         n_bytes.fetch_add(resp.size(), std::memory_order_relaxed);
+        fetch_real = real_ns();                      // the fetch-age histogram's "fetched"
         const int64_t th = mono_ns();
         any = handle_fetch(resp) || any;
         ti = mono_ns();

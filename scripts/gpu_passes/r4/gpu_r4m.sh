@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4: what the durable broker costs and where the broker share of produce -> scored
 # comes from: JSON 1.2e6/s and TXB1 open loop with fsync=interval (default) / never / the
-# in-memory broker (--kafka-memory).
+# in-memory broker (--kafka-memory); JSON with 1024-message produce requests (the batch's
+# serial parse is part of produce -> scored).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -23,6 +24,7 @@ run() {
 run json_interval --producers 3 --rate 1200000 --fmt json
 run json_never --producers 3 --rate 1200000 --fmt json --fsync never
 run json_memory --producers 3 --rate 1200000 --fmt json --kafka-memory
+run json_batch1024 --producers 3 --rate 1200000 --fmt json --batch 1024
 run txb1_interval --producers 4 --rate 0 --fmt txb1
 run txb1_memory --producers 4 --rate 0 --fmt txb1 --kafka-memory
 step done
