@@ -80,6 +80,10 @@ class ClusterState:
         self.mid = itertools.count(1)
         self.lock = threading.Lock()
         self.leader_moves = 0
+        # long-polling fetches (Fetch max_wait / min_bytes): (topic, partition) -> futures woken
+        # by the next append; the listeners share one event loop, so no cross-thread wake-up
+        self.fetch_waiters: Dict[Tuple[str, int], set] = {}
+        self.long_polls = 0
 
     def live(self) -> List[int]:
         return sorted(n for n, v in self.nodes.items() if v[2])
@@ -364,7 +368,11 @@ class _KafkaConn(asyncio.BufferedProtocol):
 
     async def _finish(self, coro):
         try:
-            self.transport.write(await coro)
+            out = await coro
+            if isinstance(out, list):
+                self.transport.writelines(out)
+            else:
+                self.transport.write(out)
         except Exception:
             self.transport.close()
             return
@@ -463,6 +471,8 @@ class KafkaLiteServer:
         if not isinstance(body, (bytes, bytearray)):
             async def later():
                 b = await body
+                if isinstance(b, list):            # a long-polled fetch: parts, no join
+                    return [struct.pack(">ii", sum(len(x) for x in b) + 4, corr)] + b
                 out = struct.pack(">i", corr) + b
                 return struct.pack(">i", len(out)) + out
             return later()
@@ -551,6 +561,11 @@ class KafkaLiteServer:
                 try:
                     base, nrec = self.store.append_raw(topic, p, rb or b"")
                     pr.append((p, ERR_NONE, base))
+                    ws = self.cluster.fetch_waiters.pop((topic, p), None)
+                    if ws:
+                        for f in ws:
+                            if not f.done():
+                                f.set_result(None)
                     self.metrics.messages_in.labels(topic, "Kafka").inc(nrec)
                     self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
                 except OutOfOrderSequence:
@@ -568,10 +583,43 @@ class KafkaLiteServer:
         pid, epoch = self.store.init_producer_id()
         return Writer().i32(0).i16(ERR_NONE).i64(pid).i16(epoch).build()
 
-    def _api_1(self, r: Reader) -> bytes:                   # Fetch v4: stored batches, sliced
-        r.i32(); r.i32(); r.i32(); max_bytes = r.i32(); r.i8()
+    def _api_1(self, r: Reader):                            # Fetch v4: stored batches, sliced
+        r.i32()
+        max_wait_ms, min_bytes, max_bytes = r.i32(), r.i32(), r.i32()
+        r.i8()
         reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.i32()))))
+        parts, n, ok = self._fetch_parts(reqs, max_bytes)
+        if n == 0 and ok and max_wait_ms > 0 and min_bytes > 0:
+            # Kafka's long poll: hold the request until a requested partition gets data or
+            # max_wait passes.  Without it every idle consumer thread re-fetched every few
+            # hundred microseconds, thousands of empty fetches a second through this event loop
+            return self._fetch_later(reqs, max_bytes, max_wait_ms)
+        return parts
+
+    async def _fetch_later(self, reqs, max_bytes: int, max_wait_ms: int):
+        fut = asyncio.get_running_loop().create_future()
+        tps = [(t, p) for t, ps in reqs for p, _o, _m in ps]
+        waiters = self.cluster.fetch_waiters
+        for tp in tps:
+            waiters.setdefault(tp, set()).add(fut)
+        self.cluster.long_polls += 1
+        try:
+            await asyncio.wait_for(fut, max_wait_ms / 1000.0)
+        except asyncio.TimeoutError:
+            pass
+        finally:
+            for tp in tps:
+                ws = waiters.get(tp)
+                if ws is not None:
+                    ws.discard(fut)
+                    if not ws:
+                        waiters.pop(tp, None)
+        return self._fetch_parts(reqs, max_bytes)[0]
+
+    def _fetch_parts(self, reqs, max_bytes: int):
+        """(response parts, record bytes in them, no partition errored)."""
         resp = []
+        ok = True
         budget = max_bytes
         for topic, parts in reqs:
             pr = []
@@ -581,11 +629,13 @@ class KafkaLiteServer:
                 if err:
                     pr.append((p, err, -1, None))
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
+                    ok = False
                     continue
                 hw = self.store.end_offset(topic, p)
                 if off < self.store.begin_offset(topic, p) or off > hw:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
+                    ok = False
                     continue
                 rb = self.store.fetch_parts(topic, p, off, max(1, min(pmax, budget))) if budget > 0 else []
                 n = sum(len(b) for b in rb)
@@ -605,7 +655,7 @@ class KafkaLiteServer:
                 w2.raw(b)
         w = Writer().i32(0)
         w.array(resp, lambda w_, t: w_.string(t[0]).array(t[1], records))
-        return w.parts                             # a list: written with one gather (_KafkaConn)
+        return w.parts, max_bytes - budget, ok    # parts: written with one gather (_KafkaConn)
 
     def _api_2(self, r: Reader) -> bytes:                   # ListOffsets v1
         r.i32()

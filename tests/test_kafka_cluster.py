@@ -84,3 +84,42 @@ def test_client_routes_and_survives_leader_move_and_node_failure(cluster):
     assert kb.committed("g", "odh-demo", 3) == 42
     kb.close()
     gz.close()
+
+
+def test_fetch_long_polls_until_data_or_max_wait(cluster):
+    """Fetch with max_wait / min_bytes (what the native consumer sends): an empty partition
+    holds the request until a produce lands on it (answered at once, with the data) or max_wait
+    passes (answered empty); a fetch with data, or with min_bytes 0, answers at once."""
+    import threading
+    import time
+    kb = KafkaBroker(cluster.bootstrap)
+    kb.create_topic("lp", 6)
+    node = cluster.leader("lp", 0)
+    srv = cluster.nodes[node - 1]
+    c = Connection(srv.host, srv.port)
+
+    def fetch(offset, max_wait_ms, min_bytes=1):
+        body = (Writer().i32(-1).i32(max_wait_ms).i32(min_bytes).i32(1 << 20).i8(0)
+                .array(["lp"], lambda w, t: w.string(t).array([0], lambda w2, q: w2.i32(q).i64(offset).i32(1 << 20)))
+                .build())
+        t0 = time.perf_counter()
+        r = c.request(FETCH, 4, body)
+        dt = time.perf_counter() - t0
+        r.i32(); r.i32(); r.string(); r.i32(); r.i32()
+        err, _hw, _lso = r.i16(), r.i64(), r.i64()
+        r.array(lambda x: (x.i64(), x.i64()))
+        n = r.i32()
+        return err, n, dt
+
+    err, n, dt = fetch(0, 300)                           # nothing there: waits max_wait
+    assert err == 0 and n == 0 and 0.25 < dt < 2.0, dt
+    err, n, dt = fetch(0, 0, 0)                          # no long poll asked: at once
+    assert n == 0 and dt < 0.2
+    threading.Timer(0.15, lambda: kb.produce("lp", b"x", partition=0)).start()
+    err, n, dt = fetch(0, 5000)                          # woken by the produce, with the data
+    assert err == 0 and n > 0 and 0.1 < dt < 1.5, dt
+    err, n, dt = fetch(0, 5000)                          # data already there: at once
+    assert n > 0 and dt < 0.2
+    assert srv.cluster.long_polls >= 2 and not srv.cluster.fetch_waiters
+    c.close()
+    kb.close()
