@@ -894,6 +894,10 @@ class WireConsumer:
     def poll(self, timeout: float = 0.0, max_records: int = 500) -> List[Record]:
         out: List[Record] = []
         end = time.monotonic() + timeout
+        # idle back-off 1 -> 8 ms: an idle consumer (the notifier, the response consumer) sent
+        # one Fetch per partition every 2 ms -- thousands of empty requests a second through
+        # the broker's event loop; data resets it (the next poll() starts at 1 ms again)
+        nap = 0.001
         while True:
             for tp in self._assignment:
                 if len(out) >= max_records:
@@ -902,9 +906,11 @@ class WireConsumer:
                 if recs:
                     self._positions[tp] = recs[-1].offset + 1
                     out.extend(recs)
-            if out or time.monotonic() >= end:
+            now = time.monotonic()
+            if out or now >= end:
                 break
-            time.sleep(0.002)
+            time.sleep(min(nap, max(0.0, end - now)))
+            nap = min(0.008, nap * 2)
         if self.auto_commit and out:
             self.commit()
         return out
