@@ -390,10 +390,13 @@ class Consumer {
   }
 
   // Fetch v4 for this leader's partitions
-  Out fetch_body(const std::vector<int>& pis) {
+  // wait_ms: the broker holds an empty fetch this long for data (long poll).  Only used when
+  // every partition of this thread has one leader: responses are read in send order, so a
+  // long-polling leader would delay another leader's data
+  Out fetch_body(const std::vector<int>& pis, int wait_ms) {
     Out body;
     body.i32(-1);           // replica id
-    body.i32(max_wait_ms);
+    body.i32(wait_ms);
     body.i32(1);            // min bytes
     body.i32(64 << 20);     // max bytes
     body.i8(0);             // isolation: read uncommitted
@@ -737,7 +740,11 @@ class Consumer {
       for (auto& kv : by_leader) {
         Conn* c = leader_conn(kv.first);
         if (!c) { meta_stale = true; continue; }
-        if (!send_request(*c, 1, 4, fetch_body(kv.second))) { close_conn(*c); meta_stale = true; continue; }
+        if (!send_request(*c, 1, 4, fetch_body(kv.second, by_leader.size() == 1 ? max_wait_ms : 0))) {
+          close_conn(*c);
+          meta_stale = true;
+          continue;
+        }
         sent.push_back(kv.first);
       }
       n_leaders.store(sent.size(), std::memory_order_relaxed);
