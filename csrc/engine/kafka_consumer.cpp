@@ -37,9 +37,13 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <deque>
+#include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -545,6 +549,102 @@ class Consumer {
     return ok;
   }
 
+  // ---- parallel JSON parse (CCFD_KC_PARSE_THREADS > 1): one batch's messages are parsed on
+  // a small pool into scratch rows, then written to the ring in order by this thread.  A
+  // 4096-message batch costs ~5 ms of serial parse; the batch's last row waited for all of it.
+  struct Rec { const uint8_t* val; int32_t vlen; int64_t off; };
+  static constexpr int64_t kParMin = 256;
+  std::vector<Rec> recs;
+  int parse_threads = 1;
+  std::vector<float> pfeat;
+  std::vector<uint64_t> pid;
+  std::vector<uint32_t> pcust;
+  std::vector<uint8_t> pok;
+  struct Pool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done;
+    uint64_t gen = 0;
+    int left = 0;
+    bool quit = false;
+    std::function<void(int)> job;
+    explicit Pool(int helpers) {
+      for (int k = 0; k < helpers; ++k)
+        th.emplace_back([this, k] {
+          uint64_t seen = 0;
+          for (;;) {
+            std::function<void(int)> f;
+            {
+              std::unique_lock<std::mutex> lk(m);
+              cv.wait(lk, [&] { return quit || gen != seen; });
+              if (quit) return;
+              seen = gen;
+              f = job;
+            }
+            f(k + 1);
+            std::lock_guard<std::mutex> lk(m);
+            if (--left == 0) done.notify_one();
+          }
+        });
+    }
+    // run f(0) here and f(1..helpers) on the pool; returns when all are done
+    void run(const std::function<void(int)>& f) {
+      {
+        std::lock_guard<std::mutex> lk(m);
+        job = f;
+        left = (int)th.size();
+        ++gen;
+      }
+      cv.notify_all();
+      f(0);
+      std::unique_lock<std::mutex> lk(m);
+      done.wait(lk, [&] { return left == 0; });
+    }
+    ~Pool() {
+      {
+        std::lock_guard<std::mutex> lk(m);
+        quit = true;
+      }
+      cv.notify_all();
+      for (auto& t : th) t.join();
+    }
+  };
+  std::unique_ptr<Pool> pool;
+
+  void parse_parallel() {
+    const int64_t n = (int64_t)recs.size();
+    pfeat.resize((size_t)n * CCFD_N_FEATURES);
+    pid.resize((size_t)n);
+    pcust.resize((size_t)n);
+    pok.assign((size_t)n, 0);
+    if (!pool) pool.reset(new Pool(parse_threads - 1));
+    const int T = parse_threads;
+    pool->run([this, n, T](int k) {
+      const int64_t lo = n * k / T, hi = n * (k + 1) / T;
+      for (int64_t i = lo; i < hi; ++i) {
+        const Rec& rc = recs[(size_t)i];
+        if (rc.vlen <= 0) continue;
+        const char* v = reinterpret_cast<const char*>(rc.val);
+        pok[(size_t)i] = ccfd::parse_json_row(v, v + rc.vlen, &pfeat[(size_t)i * CCFD_N_FEATURES], &pid[(size_t)i],
+                                              &pcust[(size_t)i]) ? 1 : 0;
+      }
+    });
+  }
+
+  // record i of the last parse_parallel() into the ring (the sequential half of ingest_value)
+  bool put_parsed(int pi, size_t i, int64_t* rows_out) {
+    *rows_out = 0;
+    const float* x = &pfeat[i * CCFD_N_FEATURES];
+    const int rb = row_bytes();
+    const bool ok = write_rows(pi, 1, [&](int64_t row, int64_t, int64_t) {
+      sink->ids(pi)[row] = pid[i];
+      sink->cust(pi)[row] = pcust[i];
+      put_row(pi, x, sink->feats(pi) + row * rb, row);
+    });
+    *rows_out = ok ? 1 : 0;
+    return ok;
+  }
+
   // gzip (codec 1) records section -> `inflated`; false on a corrupt stream
   bool gunzip(const uint8_t* p, size_t n) {
     z_stream zs{};
@@ -604,6 +704,8 @@ class Consumer {
         return;                                      // never skip data silently: the partition stalls
       }
       cur_origin = 0;
+      recs.clear();
+      bool all_json = true;
       for (int32_t i = 0; i < count && r.ok; ++i) {
         const int64_t rlen = r.varlong();
         if (!r.ok || rlen < 0 || rlen > r.e - r.p) { r.ok = false; break; }
@@ -644,11 +746,23 @@ class Consumer {
           }
         }
         r.p = rend;                                  // (other) headers skipped
-        const int64_t off = base + od;
+        if (vlen >= 4 && std::memcmp(val, "TXB1", 4) == 0) all_json = false;
+        recs.push_back({val, (int32_t)std::max<int64_t>(vlen, 0), base + od});
+      }
+      // the records, in order: JSON messages of a large batch are parsed on the parse pool
+      // first (CCFD_KC_PARSE_THREADS), then every record is written / booked sequentially
+      const bool par = all_json && parse_threads > 1 && (int64_t)recs.size() >= kParMin;
+      if (par) parse_parallel();
+      for (size_t i = 0; i < recs.size(); ++i) {
+        const Rec& rc = recs[i];
         PState& s = ps[pi];
-        if (off < s.next_offset) continue;           // already consumed (batch starts below the fetch offset)
+        if (rc.off < s.next_offset) continue;        // already consumed (batch starts below the fetch offset)
         int64_t rows = 0;
-        if (vlen > 0 && !ingest_value(pi, val, (int32_t)vlen, &rows)) {
+        bool ok;
+        if (rc.vlen <= 0) ok = true;
+        else if (par) ok = pok[i] && put_parsed(pi, i, &rows);
+        else ok = ingest_value(pi, rc.val, rc.vlen, &rows);
+        if (!ok) {
           if (stop.load()) return;
           n_errors.fetch_add(1);                     // malformed message: skip it
         }
@@ -656,8 +770,8 @@ class Consumer {
         n_rows.fetch_add((uint64_t)rows, std::memory_order_relaxed);
         std::lock_guard<std::mutex> lk(mu);
         s.rows_in += rows;
-        s.next_offset = off + 1;
-        s.pending.emplace_back(s.rows_in, off + 1);
+        s.next_offset = rc.off + 1;
+        s.pending.emplace_back(s.rows_in, rc.off + 1);
       }
       if (!r.ok) { error("malformed record in batch at offset " + std::to_string(base)); return; }
       p = bend;
@@ -801,6 +915,7 @@ Consumer* make(const char* host, int port, const char* topic, const ccfd_kc_part
   }
   c->topic = topic;
   c->wire = wire;
+  if (const char* e = std::getenv("CCFD_KC_PARSE_THREADS")) c->parse_threads = std::max(1, std::min(16, std::atoi(e)));
   c->ps.resize(n);
   for (int i = 0; i < n; ++i) {
     c->ps[i].kafka_partition = parts[i].kafka_partition;

@@ -161,3 +161,35 @@ def test_send_time_header_sets_the_batch_origin():
         assert 5e6 / 1.2 < q < upper * 1.2, (q, upper)
     finally:
         kc.close()
+
+
+@pytest.mark.parametrize("wire", [False, True])
+def test_parallel_json_parse_matches_serial(monkeypatch, wire):
+    """CCFD_KC_PARSE_THREADS=4: a large JSON batch's messages are parsed on a pool, then written
+    and booked in order -- the ring rows, ids, customers, error count and committable offsets
+    are exactly those of the serial consumer, malformed messages included; small batches and
+    TXB1 batches stay on the serial path."""
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.ingest.kafka_wire import encode_record_batch
+    from ccfd_demo_summit_amd.ingest.producer import json_tail
+    X, _ = generate(1200, seed=11)
+    msgs = [b'{"id":%d' % (100 + i) + json_tail(i % 77, X[i]) for i in range(1200)]
+    for bad in (5, 600, 1199):
+        msgs[bad] = b'{"id": 1, "V1": oops}'
+    sets = [encode_record_batch(msgs[:900]), encode_record_batch(msgs[900:1000], base_offset=900),
+            encode_record_batch(msgs[1000:], base_offset=1000)]
+    out = {}
+    for threads in ("1", "4"):
+        monkeypatch.setenv("CCFD_KC_PARSE_THREADS", threads)
+        kc = NativeKafkaConsumer.for_arrays("127.0.0.1:1", "t", {0: 0}, capacity=4000, wire=wire)
+        try:
+            got = sum(kc.feed(bytes(rs)) for rs in sets)
+            f, ids, cu = (a.copy() for a in kc.arrays[0])
+            out[threads] = (got, f, ids, cu, kc.stats()["errors"], kc.stats()["rows"], kc.committable())
+        finally:
+            kc.close()
+    a, b = out["1"], out["4"]
+    assert a[0] == b[0] == 1200 and a[4] == b[4] == 3 and a[5] == b[5] == 1197
+    for k in (1, 2, 3):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert a[6] == b[6]
