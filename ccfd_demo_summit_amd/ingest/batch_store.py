@@ -67,13 +67,15 @@ def split_batches(data: bytes, verify_crc: bool = True) -> List[Tuple[int, int, 
 
 
 class _Log:
-    __slots__ = ("bases", "batches", "begin", "end", "nbytes", "ts")
+    __slots__ = ("bases", "batches", "begin", "end", "nbytes", "ts", "visible")
 
     def __init__(self):
         self.bases: List[int] = []
         self.batches: List[bytes] = []
         self.begin = 0
-        self.end = 0
+        self.end = 0                  # next offset to assign
+        self.visible = 0              # high watermark: fetches see offsets below it (durable
+                                      # stores: what is written; memory: == end)
         self.nbytes = 0
         self.ts: List[float] = []
 
@@ -106,6 +108,12 @@ class BatchStore:
 
     def _persist_producer_ids(self) -> None:
         pass
+
+    def _appended(self, L: "_Log") -> Optional[int]:
+        """After an append (under the lock): a memory store shows the data at once; a durable
+        one (durable_store.py) returns the write ticket to wait for and shows it once written."""
+        L.visible = L.end
+        return None
 
     # ------------------------------------------------------------------ idempotent producers
     def init_producer_id(self) -> Tuple[int, int]:
@@ -171,7 +179,14 @@ class BatchStore:
 
     # ------------------------------------------------------------------ produce
     def append_raw(self, topic: str, partition: int, data: bytes) -> Tuple[int, int]:
-        """Append a produced record set verbatim; returns (base offset, records)."""
+        """Append a produced record set verbatim; returns (base offset, records) once it is
+        stored (and fetchable)."""
+        base, n, _ticket = self.append_raw_nowait(topic, partition, data)
+        return base, n
+
+    def append_raw_nowait(self, topic: str, partition: int, data: bytes) -> Tuple[int, int, Optional[int]]:
+        """``append_raw`` that does not wait for a durable store's write: (base offset, records,
+        write ticket or None).  kafka-lite answers the produce once the ticket is written."""
         batches = split_batches(data, self.verify_crc)
         with self._lock:
             L = self._log(topic, partition)
@@ -205,7 +220,7 @@ class BatchStore:
                 del L.bases[:drop], L.batches[:drop], L.ts[:drop]
                 L.begin = L.bases[0]
                 self._apply_retention(topic, partition, L)
-            return base0, nrec
+            return base0, nrec, self._appended(L)
 
     def produce(self, topic: str, value: bytes, key: Optional[bytes] = None,
                 partition: Optional[int] = None, headers: Tuple = ()) -> Tuple[int, int]:
@@ -227,13 +242,13 @@ class BatchStore:
         is written to the socket from them)."""
         with self._lock:
             L = self._log(topic, partition)
-            if offset >= L.end or not L.batches:
+            if offset >= L.visible or not L.batches:
                 return []
             i = max(0, bisect.bisect_right(L.bases, offset) - 1)
             out, size = [], 0
             while i < len(L.batches):
                 b = L.batches[i]
-                if out and size + len(b) > max_bytes:
+                if L.bases[i] >= L.visible or (out and size + len(b) > max_bytes):
                     break
                 out.append(b)
                 size += len(b)
@@ -248,8 +263,9 @@ class BatchStore:
         return [r for r in recs if r.offset >= offset][:max_records]
 
     def end_offset(self, topic: str, partition: int) -> int:
+        """The high watermark: the end of what fetches can see."""
         with self._lock:
-            return self._log(topic, partition).end
+            return self._log(topic, partition).visible
 
     def begin_offset(self, topic: str, partition: int) -> int:
         with self._lock:

@@ -22,7 +22,13 @@ committed consumer offset.  ``DurableBatchStore`` is ``BatchStore`` (batch_store
 * fsync policy: ``always`` (segment + index + offsets fsync'd before the request is
   answered), ``interval`` (a background thread fsyncs dirty files every ``fsync_interval_s``,
   default 1 s -- Kafka's ``log.flush.interval.ms`` model; a killed broker PROCESS loses
-  nothing, the writes are in the page cache), ``never``.
+  nothing, the writes are in the page cache), ``never``;
+* write-behind: the segment / index writes run on ONE writer thread in append order, off the
+  broker's event loop.  A produce is answered, and its records become fetchable (the
+  partition's high watermark, ``_Log.visible``), only once they are written, so a killed
+  broker never loses an acknowledged or consumed record.  Writing on the event loop capped
+  the deployed TXB1 topology at 1.0 x 10^7 tx/s against 1.5 x 10^7 with the in-memory store,
+  and put the broker's writes in every fetch's p99 (profiles/r4/broker_ab/).
 
 Recovery maps every segment read-only (``mmap``) and the stored batches are memoryviews of
 those maps, so Fetch stays zero-copy for recovered data too.  A torn tail (a crash in the
@@ -31,6 +37,7 @@ shorter than its segment is rebuilt by scanning the unindexed batches.
 """
 from __future__ import annotations
 
+import collections
 import json
 import mmap
 import os
@@ -87,7 +94,27 @@ class DurableBatchStore(BatchStore):
         self.recovered: Dict[str, object] = {}
         self.bytes_written = 0
         self.fsyncs = 0
+        # write-behind: appends land in memory under the store lock and are queued; ONE writer
+        # thread writes segments / index entries in queue order (os.write releases the GIL, so
+        # kafka-lite's event loop keeps serving while it runs) and then advances the partition's
+        # high watermark -- fetches only see written data, a produce is answered only once its
+        # ticket is written (append_raw waits; kafka-lite awaits on_written), so a killed broker
+        # never loses an acknowledged or consumed record
+        self._wq: collections.deque = collections.deque()
+        self._wcv = threading.Condition()
+        self._ticket = 0                    # last ticket queued (under the store lock)
+        self._written = 0                   # last ticket written (under _wcv)
+        self._wstop = False
+        self._werr: Optional[BaseException] = None
+        self.on_written = None              # callback(ticket, [(topic, partition), ...]), writer thread
+        self._writer_on = False
         self._recover()
+        for parts in self._topics.values():
+            for L in parts:
+                L.visible = L.end           # recovered data is on disk
+        self._writer = threading.Thread(target=self._write_loop, daemon=True, name="kafka-lite-writer")
+        self._writer_on = True
+        self._writer.start()
         self._stop = threading.Event()
         self._flusher = None
         if self.fsync == "interval":
@@ -319,32 +346,127 @@ class DurableBatchStore(BatchStore):
             self._atomic_json("topics.json", {t: len(v) for t, v in self._topics.items()})
 
     def _persist_appended(self, topic: str, partition: int, L: _Log, first: int) -> None:
-        """Called under the store lock after batches [first:] of L were appended."""
+        """Called under the store lock after batches [first:] of L were appended: queued for
+        the writer (the batch objects are referenced, so retention cannot drop them unwritten)."""
+        items = []
+        for i in range(first, len(L.batches)):
+            nxt = L.bases[i + 1] if i + 1 < len(L.bases) else L.end
+            items.append((L.bases[i], L.batches[i], nxt))
+        self._enqueue(("A", topic, partition, items, L.end))
+
+    def _appended(self, L: _Log) -> Optional[int]:
+        return self._ticket                 # visible once the writer has written it
+
+    def _enqueue(self, op) -> None:
+        with self._wcv:
+            self._ticket += 1
+            self._wq.append((self._ticket, op))
+            self._wcv.notify()
+
+    def append_raw(self, topic: str, partition: int, data: bytes) -> Tuple[int, int]:
+        base, n, ticket = self.append_raw_nowait(topic, partition, data)
+        self.wait_written(ticket)
+        return base, n
+
+    def wait_written(self, ticket: Optional[int], timeout: Optional[float] = None) -> bool:
+        """Block until ``ticket`` is written (its records on disk in the page cache, fsync'd
+        first with fsync="always") and fetchable."""
+        if not ticket:
+            return True
+        with self._wcv:
+            ok = self._wcv.wait_for(lambda: self._written >= ticket or self._werr is not None, timeout)
+            if self._werr is not None:
+                raise BrokerError(f"kafka-lite log write failed: {self._werr!r}")
+            return ok
+
+    def written(self) -> int:
+        with self._wcv:
+            return self._written
+
+    def _write_loop(self) -> None:
+        while True:
+            with self._wcv:
+                while not self._wq and not self._wstop:
+                    self._wcv.wait()
+                if not self._wq:
+                    return
+                ops = list(self._wq)
+                self._wq.clear()
+            ends: Dict[Tuple[str, int], int] = {}
+            touched: set = set()
+            try:
+                for _t, op in ops:
+                    kind, topic, p = op[0], op[1], op[2]
+                    if kind == "A":
+                        touched |= self._write_batches(topic, p, op[3])
+                        ends[(topic, p)] = op[4]
+                    else:
+                        self._retire_segments(topic, p, op[3])
+                if self.fsync == "always" and touched:
+                    self._sync(touched)
+            except BaseException as e:           # disk full, ...: fail every waiter loudly
+                with self._wcv:
+                    self._werr = e
+                    self._wcv.notify_all()
+                if self.on_written is not None:
+                    self.on_written(-1, [])
+                return
+            with self._lock:
+                for (topic, p), end in ends.items():
+                    L = self._log(topic, p)
+                    if end > L.visible:
+                        L.visible = end
+                if self.fsync != "always":
+                    self._dirty |= touched
+            with self._wcv:
+                self._written = ops[-1][0]
+                self._wcv.notify_all()
+            cb = self.on_written
+            if cb is not None and ends:
+                cb(ops[-1][0], list(ends))
+
+    def _write_batches(self, topic: str, partition: int, items) -> set:
+        """Writer thread: append (base, batch, next base) items to the partition's segments."""
         segs = self._segs.get((topic, partition))
         seg = segs[-1] if segs and not segs[-1].closed else None
-        for i in range(first, len(L.batches)):
-            b = L.batches[i]
+        touched = set()
+        for base, b, nxt in items:
             if seg is None or seg.size >= self.segment_bytes:
                 if seg is not None:
-                    self._close_segment(seg)
-                seg = self._open_segment(topic, partition, L.bases[i])
-            self._write_all(seg.fd, b)
-            self._write_all(seg.idx_fd, _IDX.pack(L.bases[i], seg.size))
+                    with self._lock:
+                        self._close_segment(seg)
+                    touched.discard(seg.fd)
+                    touched.discard(seg.idx_fd)
+                seg = self._open_segment(topic, partition, base)
+            self._write_raw(seg.fd, b)
+            self._write_raw(seg.idx_fd, _IDX.pack(base, seg.size))
+            touched.update((seg.fd, seg.idx_fd))
             seg.size += len(b)
             seg.nbatches += 1
-            seg.last_end = L.bases[i + 1] if i + 1 < len(L.bases) else L.end
+            seg.last_end = nxt
             self.bytes_written += len(b)
-        if self.fsync == "always" and seg is not None:
-            self._sync((seg.fd, seg.idx_fd))
-            self._dirty.discard(seg.fd)
-            self._dirty.discard(seg.idx_fd)
+        return touched
+
+    @staticmethod
+    def _write_raw(fd: int, data) -> None:
+        mv = memoryview(data)
+        while len(mv):
+            k = os.write(fd, mv)
+            mv = mv[k:]
 
     def _apply_retention(self, topic: str, partition: int, L: _Log) -> None:
-        """Delete whole closed segments below the log start."""
+        """Delete whole closed segments below the log start (in write order once serving)."""
+        if self._writer_on:
+            self._enqueue(("R", topic, partition, L.begin))
+        else:
+            self._retire_segments(topic, partition, L.begin)
+
+    def _retire_segments(self, topic: str, partition: int, begin: int) -> None:
         segs = self._segs.get((topic, partition), [])
-        while len(segs) > 1 and segs[0].last_end <= L.begin:
+        while len(segs) > 1 and segs[0].last_end <= begin:
             seg = segs.pop(0)
-            self._close_segment(seg)
+            with self._lock:
+                self._close_segment(seg)
             for ext in (".log", ".idx"):
                 try:
                     os.unlink(seg.path + ext)
@@ -361,6 +483,10 @@ class DurableBatchStore(BatchStore):
         self._atomic_json("producers.json", {"next_producer_id": self._next_pid})
 
     def close(self) -> None:
+        with self._wcv:                     # everything queued is written first
+            self._wstop = True
+            self._wcv.notify_all()
+        self._writer.join(30)
         self._stop.set()
         if self._flusher is not None:
             self._flusher.join(5)

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import collections
 import itertools
 import json
 import struct
@@ -37,6 +38,7 @@ import time
 from typing import Dict, List, Optional, Set, Tuple
 
 from .batch_store import BatchStore, InvalidBatch, OutOfOrderSequence
+from .broker import BrokerError
 from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE, ERR_OUT_OF_ORDER_SEQUENCE,
                          ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
 
@@ -84,6 +86,10 @@ class ClusterState:
         # by the next append; the listeners share one event loop, so no cross-thread wake-up
         self.fetch_waiters: Dict[Tuple[str, int], set] = {}
         self.long_polls = 0
+        # durable store (write-behind): produce answers waiting for their write ticket, in
+        # ticket order; the last ticket the store's writer reported written
+        self.produce_waiters: collections.deque = collections.deque()
+        self.written = 0
 
     def live(self) -> List[int]:
         return sorted(n for n, v in self.nodes.items() if v[2])
@@ -414,6 +420,9 @@ class KafkaLiteServer:
     # ------------------------------------------------------------------ lifecycle
     async def start(self):
         loop = asyncio.get_running_loop()
+        if hasattr(self.store, "on_written") and self.store.on_written is None:
+            # the durable store's writer thread reports written tickets to this loop
+            self.store.on_written = lambda t, tps: loop.call_soon_threadsafe(self._on_written, t, tps)
         self._server = await loop.create_server(lambda: _KafkaConn(self), self.host, self.port)
         self.port = self._server.sockets[0].getsockname()[1]
         self.cluster.nodes[self.node_id] = [self.advertise, self.port, True]
@@ -477,6 +486,38 @@ class KafkaLiteServer:
                 return struct.pack(">i", len(out)) + out
             return later()
         return struct.pack(">ii", len(body) + 4, corr) + body
+
+    def _on_written(self, ticket: int, tps) -> None:
+        """Loop thread: answer the produces whose records are written (ticket -1: the log
+        write failed -- their connections are dropped, the producers retry), and wake the
+        long-polling fetches of the partitions whose high watermark moved."""
+        cl = self.cluster
+        if ticket < 0:
+            while cl.produce_waiters:
+                _t, f = cl.produce_waiters.popleft()
+                if not f.done():
+                    f.set_exception(BrokerError("kafka-lite log write failed"))
+            return
+        cl.written = max(cl.written, ticket)
+        while cl.produce_waiters and cl.produce_waiters[0][0] <= cl.written:
+            _t, f = cl.produce_waiters.popleft()
+            if not f.done():
+                f.set_result(None)
+        for tp in tps:
+            self._wake_fetches(tp)
+
+    def _wake_fetches(self, tp) -> None:
+        ws = self.cluster.fetch_waiters.pop(tp, None)
+        if ws:
+            for f in ws:
+                if not f.done():
+                    f.set_result(None)
+
+    async def _produce_later(self, body: bytes, ticket: int) -> bytes:
+        fut = asyncio.get_running_loop().create_future()
+        self.cluster.produce_waiters.append((ticket, fut))
+        await fut
+        return body
 
     def _topic(self, name: str) -> bool:
         if name in self.store.topics():
@@ -548,6 +589,7 @@ class KafkaLiteServer:
         r.string(); r.i16(); r.i32()
         data = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.view_()))))
         resp = []
+        ticket = 0
         for topic, parts in data:
             pr = []
             self._topic(topic)
@@ -559,13 +601,12 @@ class KafkaLiteServer:
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
                     continue
                 try:
-                    base, nrec = self.store.append_raw(topic, p, rb or b"")
+                    base, nrec, t = self.store.append_raw_nowait(topic, p, rb or b"")
                     pr.append((p, ERR_NONE, base))
-                    ws = self.cluster.fetch_waiters.pop((topic, p), None)
-                    if ws:
-                        for f in ws:
-                            if not f.done():
-                                f.set_result(None)
+                    if t:
+                        ticket = max(ticket, t)     # answered (and fetchable) once written
+                    else:
+                        self._wake_fetches((topic, p))
                     self.metrics.messages_in.labels(topic, "Kafka").inc(nrec)
                     self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
                 except OutOfOrderSequence:
@@ -576,7 +617,10 @@ class KafkaLiteServer:
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
             resp.append((topic, pr))
         w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
-        return w.i32(0).build()
+        body = w.i32(0).build()
+        if ticket and ticket > self.cluster.written:
+            return self._produce_later(body, ticket)
+        return body
 
     def _api_22(self, r: Reader) -> bytes:                  # InitProducerId v0 (idempotence only)
         r.string(); r.i32()

@@ -200,3 +200,34 @@ def test_sigkilled_broker_restarts_from_disk_exactly_once(tmp_path):
     finally:
         proc.send_signal(signal.SIGKILL)
         proc.wait(10)
+
+
+def test_write_behind_answers_and_shows_only_written_records(tmp_path):
+    """kafka-lite over the durable store writes on a writer thread: a produce is answered only
+    once its batch is in the segment file, and fetches / the high watermark only ever show
+    written records (a killed broker never loses a record that was acknowledged or consumed)."""
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteCluster
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    d = tmp_path / "kl"
+    cl = KafkaLiteCluster(1, default_partitions=2, data_dir=str(d), fsync="interval").start_in_thread()
+    try:
+        kb = KafkaBroker(cl.bootstrap)
+        kb.create_topic("t", 2)
+        store = cl.nodes[0].store
+        seg = None
+        for k in range(40):
+            kb.produce_many("t", [f"v{k}-{i}".encode() * 20 for i in range(50)], partition=0)
+            if seg is None:
+                seg = next((d / "t-0").glob("*.log"))
+            # acknowledged => written: the file holds every acknowledged batch
+            assert store.written() >= 1 and seg.stat().st_size >= (k + 1) * 50 * 40
+            assert store.end_offset("t", 0) == (k + 1) * 50
+        err, hw, raw = kb.fetch_raw("t", 0, 0)
+        assert err == 0 and hw == 2000
+        # a ticket is visible only once written: the append is in memory, the fetch waits for it
+        base, n, ticket = store.append_raw_nowait("t", 1, _batch(["x"] * 10))
+        assert ticket > 0 and store.wait_written(ticket, 5.0)
+        assert store.end_offset("t", 1) == 10 and len(_values(store, "t", 1)) == 10
+        kb.close()
+    finally:
+        cl.stop()
