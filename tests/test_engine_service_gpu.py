@@ -253,6 +253,11 @@ def test_engine_service_standard_mode_process_starts_every_row_once(gpu):
             seen.setdefault(int(v["transaction_id"]), []).append(("fraud", float(v["proba"])))
             return super().start_fraud(v)
 
+        def start_fraud_many(self, items):          # KIE instances/batch (round 4)
+            for v in (items if isinstance(items, list) else []):
+                seen.setdefault(int(v["transaction_id"]), []).append(("fraud", float(v["proba"])))
+            return super().start_fraud_many(items)
+
     n = 40_000
     X, _ = generate(n, seed=12)
     ids = np.arange(1, n + 1, dtype=np.uint64) + np.uint64(9 << 32)
