@@ -33,6 +33,7 @@ import collections
 import itertools
 import json
 import struct
+import sys
 import threading
 import time
 from typing import Dict, List, Optional, Set, Tuple
@@ -982,6 +983,11 @@ def main(argv=None):
                     help="--data-dir flush policy: before every answer, every second in the background, "
                          "or left to the OS (a killed broker process loses nothing in any mode)")
     a = ap.parse_args(argv)
+    # the durable store's writer thread hands every written ticket back to this event loop,
+    # and takes the GIL back after each write: at CPython's 5 ms switch interval a busy loop
+    # kept it waiting for the GIL, so acknowledgements and fetch visibility lagged the writes
+    # (profiles/r4/broker_ab/write_behind/)
+    sys.setswitchinterval(0.0005)
     from .kafka_wire import warm_native
     print(f"[kafka-lite] native codecs loaded in {warm_native():.2f} s", flush=True)
     cl = KafkaLiteCluster(a.nodes, a.host, a.port, a.partitions, advertise=a.advertise,
