@@ -409,7 +409,10 @@ class DurableBatchStore(BatchStore):
                     self._werr = e
                     self._wcv.notify_all()
                 if self.on_written is not None:
-                    self.on_written(-1, [])
+                    try:
+                        self.on_written(-1, [])
+                    except RuntimeError:
+                        pass
                 return
             with self._lock:
                 for (topic, p), end in ends.items():
@@ -423,7 +426,10 @@ class DurableBatchStore(BatchStore):
                 self._wcv.notify_all()
             cb = self.on_written
             if cb is not None and ends:
-                cb(ops[-1][0], list(ends))
+                try:
+                    cb(ops[-1][0], list(ends))
+                except RuntimeError:             # the broker's event loop is gone (shutdown):
+                    pass                         # keep writing -- close() drains the queue
 
     def _write_batches(self, topic: str, partition: int, items) -> set:
         """Writer thread: append (base, batch, next base) items to the partition's segments."""
