@@ -523,7 +523,7 @@ class KafkaBroker:
         # engine's produce -> scored latency); set by the transaction producer
         self.stamp_time = False
         self.stamp_every = 8                # every 8th batch: a sampled latency, a fraction of the copies
-        self._stamp_n = 0
+        self._stamp_n: Dict[Tuple[str, int], int] = {}
         self._pid: Optional[Tuple[int, int]] = None
         self._seq: Dict[Tuple[str, int], int] = {}
         self._seq_locks: Dict[Tuple[str, int], threading.Lock] = {}
@@ -692,9 +692,13 @@ class KafkaBroker:
     def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
         """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
         stamp = False
-        if self.stamp_time:                 # a sample of the batches carries its send time
-            stamp = self._stamp_n % max(1, self.stamp_every) == 0
-            self._stamp_n += 1
+        if self.stamp_time:                 # a sample of the batches carries its send time:
+            # every stamp_every-th batch OF EACH PARTITION -- one counter over round-robin
+            # partitions stamped only partition 0 when stamp_every divided their count, so
+            # the ranks owning the other partitions never saw a sample
+            k = self._stamp_n.get((topic, partition), 0)
+            stamp = k % max(1, self.stamp_every) == 0
+            self._stamp_n[(topic, partition)] = k + 1
         if not (self.idempotent or stamp):
             return self._produce_raw(topic, partition, record_set, acks)
         # at most one copy: the send-time header splice, else a bytearray from the encoders is

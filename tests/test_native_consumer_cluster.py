@@ -193,3 +193,24 @@ def test_parallel_json_parse_matches_serial(monkeypatch, wire):
     for k in (1, 2, 3):
         np.testing.assert_array_equal(a[k], b[k])
     assert a[6] == b[6]
+
+
+def test_send_time_samples_reach_every_partition():
+    """stamp_every counts batches per partition: producing round-robin over 8 partitions with
+    stamp_every=8 stamps a batch of EVERY partition (one counter over all batches stamped
+    only partition 0, and the engine ranks owning the others never saw a latency sample)."""
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteCluster
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker, encode_record_batch
+    cl = KafkaLiteCluster(1, default_partitions=8).start_in_thread()
+    try:
+        kb = KafkaBroker(cl.bootstrap, idempotent=True)
+        kb.stamp_time = True
+        kb.create_topic("t", 8)
+        for k in range(16):
+            kb.produce_raw("t", k % 8, encode_record_batch([b'{"id": %d}' % i for i in range(10)]))
+        store = cl.nodes[0].store
+        for p in range(8):
+            assert b"ccfd-ts" in store.fetch_raw("t", p, 0, 1 << 20), p
+        kb.close()
+    finally:
+        cl.stop()
