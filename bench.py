@@ -111,6 +111,10 @@ def parse_args(argv=None):
                     help="skip the secondary f32-wire throughput run (W64 headline only)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-unloaded-probe", action="store_true")
+    ap.add_argument("--diagnostic", action="store_true",
+                    help="allow diagnostic environment variables (utils/benchenv.py: an A/B library, fault "
+                         "injection, launch serialisation, ...); the line is then labelled diagnostic and "
+                         "must not be quoted as a headline")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args(argv)
 
@@ -389,6 +393,12 @@ def _f32_wire_rate(args, model, dev, exec_mode, seconds: float = 0.5):
 
 def main(argv=None):
     args = parse_args(argv)
+    from ccfd_demo_summit_amd.utils import benchenv
+    refused = benchenv.refusal(allow=args.diagnostic)
+    if refused:
+        _fail(refused)
+    env_block = benchenv.describe()
+    diagnostic = bool(env_block["diagnostic"])
     from ccfd_demo_summit_amd.parallel.dp import resolve_row_format
     try:
         args.wire = resolve_row_format(args.model, args.wire)   # auto: w64 for mlp/lr, g20 for gbdt
@@ -704,7 +714,7 @@ def main(argv=None):
         "config": {"model": {"mlp": "mlp_30_128_64_1", "lr": "logreg_30",
                              "gbdt": f"oblivious_gbdt_{args.gbdt_trees}x{args.gbdt_depth}"}[args.model],
                    "global_batch": args.batch * W, "seq_len": 1, "micro_batch": args.batch,
-                   "parallelism": f"dp{W}" + ("-rehearsal" if rehearsal else ""),
+                   "parallelism": f"dp{W}" + ("-rehearsal" if rehearsal else "") + ("-diagnostic" if diagnostic else ""),
                    "input_mode": args.input_mode,
                    "output_mode": args.output_mode, "exec_mode": exec_mode, "depth": args.depth,
                    "wire": args.wire, "coalesce": args.coalesce,
@@ -716,6 +726,10 @@ def main(argv=None):
         "world_size": W,
         "rehearsal": rehearsal,
         "topology_problems": problems,
+        # every CCFD_* / HIP_* / HSA_* / ... variable this rank saw; a diagnostic one makes the
+        # run refuse unless --diagnostic, which labels the line (utils/benchenv.py)
+        "diagnostic": diagnostic,
+        "env": env_block,
         "p50_latency_us": round(p50_us, 2),
         "p99_latency_us": round(p99_us, 2),
         "p50_latency_us_unloaded": None if p50_unloaded is None else round(p50_unloaded, 2),
@@ -772,6 +786,11 @@ def entry(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     from ccfd_demo_summit_amd.launch import local_ranks
     args = parse_args(argv)
+    from ccfd_demo_summit_amd.utils import benchenv
+    refused = benchenv.refusal(allow=args.diagnostic)
+    if refused:
+        print(f"[bench] FATAL: {refused}", file=sys.stderr, flush=True)
+        return 3
     if local_ranks.needs_spawn(args.gpus):
         env = dict(local_ranks.REHEARSAL_ENV) if args.rehearsal else {}
         return local_ranks.run_ranks(str(Path(__file__).resolve()), argv, args.gpus, extra_env=env)

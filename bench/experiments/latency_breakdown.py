@@ -38,8 +38,6 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--grids", default="0", help="comma list of persistent grids (0 = engine default)")
     ap.add_argument("--items", default="0", help="comma list of CCFD_PERSIST_ITEM_ROWS (0 = engine default)")
-    ap.add_argument("--ablate", default="0", help="comma list of CCFD_ABLATE values (diagnostics: 64 = no "
-                                                 "per-item release, 512 = no per-item acquire)")
     ap.add_argument("--pipe", default="0", help="comma list of CCFD_PERSIST_PIPE values (1 = pipelined "
                                                "static items, 0 = claimed workgroup items)")
     ap.add_argument("--log-rows", type=int, default=1 << 21)
@@ -61,11 +59,10 @@ def main():
     log.write_rows(0, Xl)
     del Xl
     out = []
-    pts = [(int(ab), int(w), int(i), int(gr), int(d)) for ab in a.ablate.split(",") for w in a.pipe.split(",")
+    pts = [(int(w), int(i), int(gr), int(d)) for w in a.pipe.split(",")
            for i in a.items.split(",") for gr in a.grids.split(",") for d in a.depths.split(",")]
-    for ablate, pipe, item, grid, depth in pts:
+    for pipe, item, grid, depth in pts:
         os.environ["CCFD_PERSIST_PIPE"] = str(pipe)
-        os.environ["CCFD_ABLATE"] = str(ablate)
         if item:
             os.environ["CCFD_PERSIST_ITEM_ROWS"] = str(item)
         else:
@@ -100,7 +97,7 @@ def main():
              "p50_end_to_landed_us_rel": pct(end_to_landed, 50),
              "p50_host_pickup_us": pct(pickup, 50),
              "grid": grid or "default", "item_rows": item or "default",
-             "items": "pipelined-static" if pipe else "claimed", "ablate": ablate}
+             "items": "pipelined-static" if pipe else "claimed"}
         print(json.dumps(r), flush=True)
         out.append(r)
     if a.out:

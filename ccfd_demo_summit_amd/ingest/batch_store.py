@@ -27,6 +27,9 @@ _HDR = struct.Struct(">qiibIhi")      # base, batch_len, leader epoch, magic, cr
 _COUNT_OFF = 57                       # records count (i32) within a batch
 
 
+_SEQ_MASK = 0x7FFFFFFF            # producer sequences are int32 and wrap to 0
+
+
 class InvalidBatch(BrokerError):
     pass
 
@@ -132,7 +135,7 @@ class BatchStore:
         st = self._producers.setdefault((topic, partition), {}).setdefault(pid, [epoch, []])
         if epoch != st[0]:
             st[0], st[1] = epoch, []
-        st[1].append((seq, seq + last, base))
+        st[1].append((seq, (seq + last) & _SEQ_MASK, base))     # wraps at 2^31 (Kafka)
         del st[1][:-_PRODUCER_CACHE]
         self._next_pid = max(self._next_pid, pid + 1)
 
@@ -147,9 +150,10 @@ class BatchStore:
         for first, _last, base in st[1]:
             if first == seq:
                 return base
-        if seq != st[1][-1][1] + 1:
+        expect = (st[1][-1][1] + 1) & _SEQ_MASK
+        if seq != expect:
             raise OutOfOrderSequence(f"{topic}[{partition}] producer {pid}: sequence {seq}, "
-                                     f"expected {st[1][-1][1] + 1}")
+                                     f"expected {expect}")
         return None
 
     # ------------------------------------------------------------------ topics

@@ -363,6 +363,13 @@ class DurableBatchStore(BatchStore):
             self._wq.append((self._ticket, op))
             self._wcv.notify()
 
+    def append_raw_nowait(self, topic: str, partition: int, data: bytes) -> Tuple[int, int, Optional[int]]:
+        """Refused with a BrokerError once the writer has failed: a ticket handed out now
+        would never be written, and its produce would wait forever."""
+        if self._werr is not None:
+            raise BrokerError(f"kafka-lite log write failed: {self._werr!r}")
+        return super().append_raw_nowait(topic, partition, data)
+
     def append_raw(self, topic: str, partition: int, data: bytes) -> Tuple[int, int]:
         base, n, ticket = self.append_raw_nowait(topic, partition, data)
         self.wait_written(ticket)
@@ -439,10 +446,12 @@ class DurableBatchStore(BatchStore):
         for base, b, nxt in items:
             if seg is None or seg.size >= self.segment_bytes:
                 if seg is not None:
-                    with self._lock:
+                    # the fds before _close_segment resets them to -1: a closed fd left in
+                    # `touched` would be fsync'd later under a number that may be reused
+                    old = (seg.fd, seg.idx_fd)
+                    with self._lock:            # (fsync="always": fsync'd as it closes)
                         self._close_segment(seg)
-                    touched.discard(seg.fd)
-                    touched.discard(seg.idx_fd)
+                    touched.difference_update(old)
                 seg = self._open_segment(topic, partition, base)
             self._write_raw(seg.fd, b)
             self._write_raw(seg.idx_fd, _IDX.pack(base, seg.size))

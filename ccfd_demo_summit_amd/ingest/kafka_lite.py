@@ -32,6 +32,7 @@ import asyncio
 import collections
 import itertools
 import json
+import os
 import struct
 import sys
 import threading
@@ -45,6 +46,7 @@ from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER, ERR_OFFSET_OUT_O
 
 NODE_ID = 1
 ERR_ILLEGAL_GENERATION, ERR_UNKNOWN_MEMBER, ERR_REBALANCE_IN_PROGRESS = 22, 25, 27
+ERR_KAFKA_STORAGE_ERROR = 56
 
 
 class _Member:
@@ -77,6 +79,10 @@ class ClusterState:
 
     def __init__(self, store: BatchStore):
         self.store = store
+        # called (loop thread) once the durable store's writer failed: the broker process
+        # exits non-zero so its supervisor / pod restarts it and it recovers from its segments
+        # (a wedged broker would keep passing its TCP liveness probe)
+        self.on_store_failure = None
         self.nodes: Dict[int, List] = {}                  # id -> [host, port, alive]
         self.leaders: Dict[Tuple[str, int], int] = {}
         self.groups: Dict[str, _Group] = {}
@@ -498,6 +504,8 @@ class KafkaLiteServer:
                 _t, f = cl.produce_waiters.popleft()
                 if not f.done():
                     f.set_exception(BrokerError("kafka-lite log write failed"))
+            if cl.on_store_failure is not None:
+                cl.on_store_failure()
             return
         cl.written = max(cl.written, ticket)
         while cl.produce_waiters and cl.produce_waiters[0][0] <= cl.written:
@@ -615,6 +623,9 @@ class KafkaLiteServer:
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
                 except InvalidBatch:
                     pr.append((p, ERR_CORRUPT, -1))
+                    self.metrics.failed_produce.labels(topic, "Kafka").inc()
+                except BrokerError:             # the durable log can no longer be written
+                    pr.append((p, ERR_KAFKA_STORAGE_ERROR, -1))
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
             resp.append((topic, pr))
         w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
@@ -994,6 +1005,14 @@ def main(argv=None):
                           retention_batches=a.retention_batches or None, data_dir=a.data_dir, fsync=a.fsync)
     if a.data_dir:
         print(f"[kafka-lite] recovered from {a.data_dir}: {json.dumps(cl.store.recovered)}", flush=True)
+
+    def store_failed():
+        # the durable log writer died (disk full, EIO): answer nothing more, exit non-zero so
+        # the supervisor / pod restarts the broker, which recovers from its segments
+        print(f"[kafka-lite] FATAL: log write failed ({getattr(cl.store, '_werr', None)!r}); exiting",
+              file=sys.stderr, flush=True)
+        asyncio.get_running_loop().call_later(0.2, os._exit, 75)
+    cl.state.on_store_failure = store_failed
 
     async def run():
         await cl.start()

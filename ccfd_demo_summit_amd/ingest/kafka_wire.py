@@ -44,6 +44,8 @@ ERR_LEADER_NOT_AVAILABLE, ERR_NOT_LEADER, ERR_NOT_COORDINATOR = 5, 6, 16
 RETRIABLE = (ERR_UNKNOWN_TOPIC, ERR_LEADER_NOT_AVAILABLE, ERR_NOT_LEADER, ERR_NOT_COORDINATOR)
 ERR_UNSUPPORTED_VERSION, ERR_TOPIC_EXISTS, ERR_INVALID_REQUEST = 35, 36, 42
 ERR_OUT_OF_ORDER_SEQUENCE = 45
+# idempotent-producer sequence numbers are int32 and wrap from 2^31 - 1 to 0 (Kafka semantics)
+SEQ_MASK = 0x7FFFFFFF
 
 # --------------------------------------------------------------------------- crc32c
 _CRC_TABLE = None
@@ -684,7 +686,7 @@ class KafkaBroker:
             blen = struct.unpack_from(">i", b, o + 8)[0]
             count = struct.unpack_from(">i", b, o + 57)[0]
             struct.pack_into(">qhi", b, o + 43, pid, epoch, seq)
-            seq += count
+            seq = (seq + count) & SEQ_MASK        # wraps at 2^31 like Kafka's sequences
             n_total += count
             o += 12 + blen
         return n_total
@@ -719,7 +721,7 @@ class KafkaBroker:
             n = self._stamp_sequence(topic, partition, b)
             seal_batches(b)
             base = self._produce_raw(topic, partition, b, acks)   # retries resend the same seq
-            self._seq[key] = self._seq.get(key, 0) + n
+            self._seq[key] = (self._seq.get(key, 0) + n) & SEQ_MASK
             return base
 
     def _produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:

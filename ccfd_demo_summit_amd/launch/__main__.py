@@ -129,9 +129,17 @@ def _serve_in_thread(app, host, port):
 
 # ---------------------------------------------------------------------------- services
 def cmd_kafka_lite(a, cfg):
+    """kafka-lite with every option the operator renders (operator/render.py): durability
+    (--data-dir / --fsync), metrics port and retention are forwarded, never dropped."""
     from ..ingest.kafka_lite import main
-    main(["--host", a.host, "--port", str(a.port or 9092), "--partitions", str(cfg.kafka.partitions),
-          "--nodes", str(a.nodes)] + (["--advertise", a.advertise] if a.advertise else []))
+    argv = ["--host", a.host, "--port", str(a.port or 9092), "--partitions", str(cfg.kafka.partitions),
+            "--nodes", str(a.nodes), "--metrics-port", str(a.metrics_port),
+            "--retention-batches", str(a.retention_batches), "--fsync", a.fsync]
+    if a.advertise:
+        argv += ["--advertise", a.advertise]
+    if a.data_dir:
+        argv += ["--data-dir", a.data_dir]
+    main(argv)
 
 
 def cmd_seldon(a, cfg):
@@ -570,6 +578,13 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--config", default=None)
     ap.add_argument("--nodes", type=int, default=1, help="kafka-lite: broker listeners (port, port+1, ...)")
     ap.add_argument("--advertise", default=None, help="kafka-lite: broker host name clients are given")
+    ap.add_argument("--data-dir", default=None,
+                    help="kafka-lite: durable log + committed-offset directory (restart recovers from it)")
+    ap.add_argument("--fsync", default="interval", choices=["always", "interval", "never"],
+                    help="kafka-lite: durability flush policy of --data-dir")
+    ap.add_argument("--metrics-port", type=int, default=9404, help="kafka-lite: Prometheus /metrics (0 = off)")
+    ap.add_argument("--retention-batches", type=int, default=0,
+                    help="kafka-lite: record batches kept per partition (0 = the broker default)")
     ap.add_argument("--cr", default=None, help="operator: FraudDetection (or OpenDataHub) CR file")
     ap.add_argument("--render", default=None, help="operator: write Kubernetes manifests here ('-' = stdout)")
     ap.add_argument("--local", action="store_true", help="operator: reconcile the CR into local processes")

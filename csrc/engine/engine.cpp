@@ -279,7 +279,6 @@ class Engine {
     // at completion stays: it is what orders the outputs before the completion record across
     // XCDs).  CCFD_COHERENT_OUT=0 allocates non-coherent outputs instead (A/B switch).
     if (const char* e = std::getenv("CCFD_COHERENT_OUT")) coherent_out = std::atoi(e) != 0;
-    if (const char* e = std::getenv("CCFD_ABLATE")) ablate = std::atoi(e) & 0x270;  // diagnostics only
     // HIP_LAUNCH_BLOCKING-style debug mode: synchronise after every launch so a kernel fault
     // is reported against the micro-batch that caused it (SURVEY.md §5 race detection)
     if (const char* e = std::getenv("CCFD_DEBUG_SYNC")) debug_sync = std::atoi(e) != 0;
@@ -337,7 +336,6 @@ class Engine {
   int rowf = CCFD_N_FEATURES;   // f32 words per log row: 30, 16 for W64, 8 for G32, 5 for G20 rows
   int amount_f = CCFD_N_FEATURES - 1;   // word of Amount in a row (-1: G32, host-side column)
   int wire_flag = 0;            // CCFD_ARG_WIRE_* of the row format
-  int ablate = 0;
   bool debug_sync = false;
   // score_sync of small pageable batches (the REST front end: 1..~50 rows per call) copies
   // the rows into this pinned, mapped buffer and the kernel reads them zero-copy, instead of
@@ -469,8 +467,7 @@ class Engine {
     a.items_per_batch = persist_C;
     a.tiles_per_wave = persist_tpw;
     a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | wire_flag |
-              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0) | (ablate & (CCFD_ARG_ABLATE_FENCE | CCFD_ARG_ABLATE_ACQUIRE | CCFD_ARG_ABLATE_COUNTERS |
-                        CCFD_ARG_ABLATE_OUTPUTS));
+              (persist_pipe ? CCFD_ARG_PIPE_ITEMS : 0);
     a.model = cfg.model;
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;
@@ -544,10 +541,8 @@ class Engine {
     const uint64_t sq = seq;                       // caller increments seq after submit
     ccfd_persist_desc& d = pdesc[sq % cfg.depth];
     d.x = x_dev;
-    // CCFD_ABLATE & 32 (diagnostics only): no per-row outputs, the kernels skip null pointers
-    const bool no_out = (ablate & CCFD_ARG_ABLATE_OUTPUTS) != 0;
-    d.proba = no_out ? nullptr : s.h_proba_dev;
-    d.route = no_out ? nullptr : s.h_route_dev;
+    d.proba = s.h_proba_dev;
+    d.route = s.h_route_dev;
     d.flag_idx = s.h_flag_dev;
     d.n = s.rows;
     d.epoch = epoch & 1;
@@ -847,7 +842,7 @@ class Engine {
       a.done_seq = s.expect;
       s.done_ptr = s.h_done;
       arm(s);
-      a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate;
+      a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS);
     }
     a.flags |= wire_flag;
     int rc = ccfd_score_launch(&a, stream);
@@ -883,7 +878,7 @@ class Engine {
     a.threshold = cfg.threshold;
     a.rules = cfg.rules;
     a.counters = cfg.counters[epoch & 1];
-    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | ablate | wire_flag;
+    a.flags = (coherent_out ? CCFD_ARG_FENCE_COHERENT : CCFD_ARG_FENCE_SYS) | wire_flag;
     m.nsub = K;
     m.sub_rows = rows;
     for (int k = 0; k < K; ++k) {

@@ -46,14 +46,8 @@ enum ccfd_counter_slot {
 #define CCFD_ARG_WIRE_G20 8
 #define CCFD_G20_ROW_BYTES 20
 #define CCFD_G20_MAX_EDGES 31
-// Diagnostic ablations (CCFD_ABLATE env in the engine; never set by bench.py): skip parts
-// of the epilogue to measure what each costs.  Results are incomplete when set.
-#define CCFD_ARG_ABLATE_COUNTERS 16   // no counter/histogram atomics
-#define CCFD_ARG_ABLATE_OUTPUTS 32    // no proba/route stores
-#define CCFD_ARG_ABLATE_FENCE 64      // no per-workgroup system release
 #define CCFD_ARG_CHUNK_RING 128       // persistent G32: one-chunk prefetch ring (default) instead of the whole item in flight
 #define CCFD_ARG_FLAG_DIRECT 1024      // W64 launch kernels: reserve flag-list slots per ballot (A/B of the LDS staging)
-#define CCFD_ARG_ABLATE_ACQUIRE 512   // persistent kernels: no acquire before reading an item's rows (diagnostics)
 #define CCFD_ARG_PIPE_ITEMS 256       // persistent W64 MLP: statically assigned 64/128-row items, the next
                                       // item's rows fetched while the current one is scored
 

@@ -250,10 +250,8 @@ __device__ __forceinline__ void signal_done(const ccfd_score_args& a, unsigned n
     // fine-grained outputs (an s_waitcnt alone only means "accepted by this XCD's L2").
     // The ticket itself is relaxed: no agent-scope acquire, i.e. no L2 invalidate per
     // workgroup (the last workgroup reads only atomics).
-    if (!(a.flags & CCFD_ARG_ABLATE_FENCE)) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned ticket = __hip_atomic_fetch_add(&a.slot_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ticket == nblk - 1) {
       // K7: device-clock execution window of this micro-batch

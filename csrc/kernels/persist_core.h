@@ -67,7 +67,7 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
 // slot / DMA staging buffer -- before they are read).
 __device__ __forceinline__ void persist_read_desc(const ccfd_persist_args& a, unsigned long long b,
                                                   ccfd_persist_desc& sdesc) {
-  if (!(a.flags & CCFD_ARG_ABLATE_ACQUIRE)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
   sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -127,7 +127,7 @@ __device__ __forceinline__ void persist_emit_flagged(const ccfd_persist_args& a,
 __device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const ccfd_persist_desc& sdesc, int slot,
                                                int C) {
   // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
-  if (!(a.flags & CCFD_ARG_ABLATE_FENCE)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned left =
       __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
@@ -150,7 +150,7 @@ __device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const
 __device__ __forceinline__ void persist_item_done(const ccfd_persist_args& a, EpilogueLds& epi,
                                                   const ccfd_persist_desc& sdesc, int slot, int C, int tid) {
   __syncthreads();
-  unsigned long long* cnt = (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters[sdesc.epoch & 1];
+  unsigned long long* cnt = a.counters[sdesc.epoch & 1];
   if (tid < 2 * kNB) {
     const unsigned h = epi.hist[tid];
     if (h && cnt) atomicAdd(&cnt[(tid < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + tid],

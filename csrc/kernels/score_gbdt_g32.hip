@@ -41,7 +41,6 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
   else g32_stage_leaves<D>(blob, T, lv, tid, 256);
   __syncthreads();                                              // leaves staged, epi initialised
 
-  const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
   unsigned fraud = 0, rows = 0, stale = 0;
   unsigned long long psum = 0;
   for (; grp < ngroups; grp += gstride) {
@@ -74,10 +73,8 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
       if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
       else fr = valid && fresh && (p >= a.threshold);
       if (valid) {
-        if (store_out) {
-          if (a.proba) st_g(a.proba + row, p);
-          if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
-        }
+        if (a.proba) st_g(a.proba + row, p);
+        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
         if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
         atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta[q] & 0xffu), kNB - 1)], 1u);
       }
@@ -93,7 +90,7 @@ __global__ __launch_bounds__(256) void score_gbdt_g32_kernel(ccfd_score_args a) 
     atomicAdd(&epi.rows, rows);
     atomicAdd(&epi.psum_e6, psum);
   }
-  unsigned long long* cnt = (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters;
+  unsigned long long* cnt = a.counters;
   if (cnt != nullptr && lane == 0 && stale) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)stale);
   epi_flush(epi, cnt);
   signal_done(a, gridDim.x);

@@ -102,10 +102,8 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
     }
 
     if (valid && g == 0) {
-      if (!(a.flags & CCFD_ARG_ABLATE_OUTPUTS)) {
-        if (a.proba) st_g(a.proba + row, p);
-        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
-      }
+      if (a.proba) st_g(a.proba + row, p);
+      if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
       psum += (unsigned)(p * 1e6f + 0.5f);              // p in [0,1]: u32 convert, u64 sum
     }
     fraud += __popcll(__ballot(fr && g == 0));
@@ -119,7 +117,7 @@ __device__ __forceinline__ void mlp_body(const ccfd_score_args& a, int blk, int 
     atomicAdd(&epi.rows, rows);
     atomicAdd(&epi.psum_e6, psum);
   }
-  epi_flush(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
+  epi_flush(epi, a.counters);
   signal_done(a, (unsigned)nblk);
 }
 

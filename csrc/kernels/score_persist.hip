@@ -333,10 +333,8 @@ __global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) 
         fr = valid && (p >= a.threshold);
       }
       if (valid && g == 0) {
-        if (!(a.flags & CCFD_ARG_ABLATE_OUTPUTS)) {              // diagnostics only
-          if (d.proba) st_g(d.proba + row, p);
-          if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
-        }
+        if (d.proba) st_g(d.proba + row, p);
+        if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
         ps_w += (unsigned long long)(p * 1e6f + 0.5f);
       }
       const unsigned long long m = __ballot(fr && g == 0);

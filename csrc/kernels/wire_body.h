@@ -50,7 +50,6 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
   sc.lanes(lds, a, g);
 
   const float thr = a.threshold;
-  const bool store_out = !(a.flags & CCFD_ARG_ABLATE_OUTPUTS);
   FlagStage fls{flbuf[wave], 0u};
   unsigned fraud = 0, rows = 0;
   unsigned long long psum = 0;
@@ -73,10 +72,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     const bool valid = row < n;
     const bool fr = valid && (kR ? rf : (p >= thr));
     if (valid && g == 0) {
-      if (store_out) {
-        if (a.proba) st_g(a.proba + row, p);
-        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
-      }
+      if (a.proba) st_g(a.proba + row, p);
+      if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
       psum += (unsigned)(p * 1e6f + 0.5f);
     }
     const unsigned long long frm = __ballot(fr && g == 3);     // same rows as the g == 0 lanes
@@ -124,10 +121,8 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
       const bool valid = row < n;
       const bool fr = valid && p >= thr;
       if (valid) {
-        if (store_out) {
-          if (a.proba) st_g(a.proba + row, p);
-          if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
-        }
+        if (a.proba) st_g(a.proba + row, p);
+        if (a.route) st_g(a.route + row, (uint8_t)(fr ? 1 : 0));
         psum += (unsigned)(p * 1e6f + 0.5f);
       }
       const unsigned long long frm = __ballot(fr);
@@ -196,7 +191,7 @@ __device__ __forceinline__ void wire_stream_body(const ccfd_score_args& a, int b
     atomicAdd(&epi.rows, rows);
     atomicAdd(&epi.psum_e6, psum);
   }
-  epi_flush_ballot(epi, (a.flags & CCFD_ARG_ABLATE_COUNTERS) ? nullptr : a.counters);
+  epi_flush_ballot(epi, a.counters);
   signal_done(a, (unsigned)nblk);
 }
 

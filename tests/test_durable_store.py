@@ -231,3 +231,91 @@ def test_write_behind_answers_and_shows_only_written_records(tmp_path):
         kb.close()
     finally:
         cl.stop()
+
+
+def test_write_failure_refuses_new_produces_and_stops_the_broker(tmp_path):
+    """once the writer thread failed (disk full / EIO), a produce is
+    refused with a BrokerError -- never handed a ticket nobody will write -- and kafka-lite
+    answers KAFKA_STORAGE_ERROR and asks to be restarted (on_store_failure)."""
+    import errno
+
+    from ccfd_demo_summit_amd.ingest.broker import BrokerError
+    store = DurableBatchStore(str(tmp_path / "kl"), default_partitions=1, fsync="never")
+    store.create_topic("t", 1)
+    base, n, t = store.append_raw_nowait("t", 0, _batch(["a"] * 5))
+    assert store.wait_written(t, 5.0)
+    calls = []
+    store.on_written = lambda ticket, tps: calls.append(ticket)
+
+    def disk_full(fd, data):
+        raise OSError(errno.ENOSPC, "No space left on device")
+    store._write_raw = disk_full
+    _b, _n, t2 = store.append_raw_nowait("t", 0, _batch(["b"] * 5))
+    with pytest.raises(BrokerError):
+        store.wait_written(t2, 5.0)
+    assert calls and calls[-1] == -1
+    with pytest.raises(BrokerError):                 # no more tickets after the failure
+        store.append_raw_nowait("t", 0, _batch(["c"] * 5))
+    store._werr = None                                # (let close() run)
+    store.close()
+
+    # kafka-lite over a failing store: the produce is answered with an error, the broker asks
+    # to be restarted
+    from ccfd_demo_summit_amd.ingest.kafka_lite import ERR_KAFKA_STORAGE_ERROR, KafkaLiteCluster
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    cl = KafkaLiteCluster(1, default_partitions=1, data_dir=str(tmp_path / "kl2"), fsync="never")
+    failed = []
+    cl.state.on_store_failure = lambda: failed.append(1)
+    cl.start_in_thread()
+    try:
+        kb = KafkaBroker(cl.bootstrap)
+        kb.create_topic("t", 1)
+        kb.produce_many("t", [b"ok"] * 10, partition=0)
+        cl.store._write_raw = disk_full
+        with pytest.raises(BrokerError):
+            kb.produce_many("t", [b"lost"] * 10, partition=0)
+        t0 = time.time()
+        while not failed and time.time() - t0 < 5:
+            time.sleep(0.05)
+        assert failed
+        with pytest.raises(BrokerError) as ei:
+            kb.produce_many("t", [b"refused"] * 10, partition=0)
+        assert str(ERR_KAFKA_STORAGE_ERROR) in str(ei.value) or "storage" in str(ei.value).lower() \
+            or "error" in str(ei.value).lower()
+        kb.close()
+    finally:
+        cl.store._werr = None
+        cl.stop()
+
+
+def test_producer_sequences_wrap_at_2_pow_31():
+    """idempotent sequences are int32 and wrap to 0 (Kafka semantics) on both
+    the client and the broker -- a long-running producer neither dies on struct.pack nor gets
+    OutOfOrderSequence after 2^31 records."""
+    from ccfd_demo_summit_amd.ingest.batch_store import BatchStore
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteCluster
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    st = BatchStore(default_partitions=1)
+    st.create_topic("t", 1)
+    top = (1 << 31) - 3
+    st.append_raw("t", 0, _batch(["a"] * 5, pid=7, seq=top))            # seqs top .. 1 (wrapped)
+    st.append_raw("t", 0, _batch(["b"] * 5, pid=7, seq=2))              # the next one after the wrap
+    assert st.append_raw("t", 0, _batch(["b"] * 5, pid=7, seq=2)) == (5, 0)   # a retry: stored once
+    with pytest.raises(OutOfOrderSequence):
+        st.append_raw("t", 0, _batch(["c"] * 5, pid=7, seq=top + 2))
+    assert st.end_offset("t", 0) == 10
+    cl = KafkaLiteCluster(1, default_partitions=1).start_in_thread()
+    try:
+        kb = KafkaBroker(cl.bootstrap, idempotent=True)
+        kb.create_topic("w", 1)
+        kb.produce_many("w", [b"x"] * 4, partition=0)
+        kb._seq[("w", 0)] = (1 << 31) - 2            # as if 2^31 records had been sent
+        st2 = cl.store
+        pid = next(iter(st2._producers[("w", 0)]))
+        st2._producers[("w", 0)][pid][1][-1] = ((1 << 31) - 6, (1 << 31) - 3, 0)
+        for _ in range(3):
+            kb.produce_many("w", [b"y"] * 4, partition=0)
+        assert kb._seq[("w", 0)] == 10 and st2.end_offset("w", 0) == 16
+        kb.close()
+    finally:
+        cl.stop()

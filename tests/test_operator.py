@@ -329,3 +329,52 @@ def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
             kb.close()
     finally:
         op.shutdown()
+
+
+def _launch_argvs(cmd):
+    """Every `python -m ccfd_demo_summit_amd.launch ...` invocation inside a container command
+    (a supervised one nests the child's after `--`)."""
+    out = []
+    for i in range(len(cmd) - 1):
+        if cmd[i] == "-m" and cmd[i + 1] == "ccfd_demo_summit_amd.launch":
+            rest = cmd[i + 2:]
+            nxt = [j for j in range(len(rest) - 1) if rest[j] == "-m" and rest[j + 1] == "ccfd_demo_summit_amd.launch"]
+            out.append(rest[:nxt[0]] if nxt else rest)
+    return out
+
+
+@pytest.mark.parametrize("variant", ["default", "wide"])
+def test_every_rendered_launch_command_parses(variant):
+    """each rendered container's launcher argv is accepted by the launcher's
+    own parser, and kafka-lite keeps its durability options (a pod that crash-loops on
+    'unrecognized arguments' never shows up in the local-operator tests)."""
+    from ccfd_demo_summit_amd.launch.__main__ import parse_args
+    d = _doc()
+    if variant == "wide":
+        d["spec"]["router"] = {"deploy": True, "replicas": 2}
+        d["spec"]["training"] = {"deploy": True, "workers": 2, "model": "mlp", "gpus": 1}
+        d["spec"]["engine"].update(nodes=2, gpusPerNode=4)
+    seen = set()
+    for m in render(parse(d)):
+        tmpl = m.get("spec", {}).get("template", {}).get("spec", {})
+        if m["kind"] == "CronJob":
+            tmpl = m["spec"]["jobTemplate"]["spec"]["template"]["spec"]
+        for c in tmpl.get("containers", []) + tmpl.get("initContainers", []):
+            for argv in _launch_argvs(c.get("command", []) + c.get("args", [])):
+                a = parse_args(argv)          # SystemExit on an unknown option
+                seen.add(a.service)
+                if a.service == "kafka-lite":
+                    assert a.data_dir == "/var/lib/kafka-lite" and a.fsync in ("always", "interval", "never")
+    assert {"kafka-lite", "kie", "engine", "notifier", "producer"} <= seen, seen
+
+
+def test_launcher_forwards_kafka_lite_durability(monkeypatch):
+    from ccfd_demo_summit_amd.launch import __main__ as L
+    got = {}
+    import ccfd_demo_summit_amd.ingest.kafka_lite as K
+    monkeypatch.setattr(K, "main", lambda argv: got.setdefault("argv", argv))
+    a = L.parse_args(["kafka-lite", "--nodes", "3", "--data-dir", "/x", "--fsync", "always", "--metrics-port", "0"])
+    L.cmd_kafka_lite(a, L.load_config(None, environ={}))
+    argv = got["argv"]
+    assert argv[argv.index("--data-dir") + 1] == "/x" and argv[argv.index("--fsync") + 1] == "always"
+    assert argv[argv.index("--metrics-port") + 1] == "0" and argv[argv.index("--nodes") + 1] == "3"
