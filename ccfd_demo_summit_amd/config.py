@@ -55,6 +55,9 @@ class KieConfig:
     fraud_process_id: str = "ccd-fraud-kjar.CCDProcess"
     standard_process_id: str = "ccd-fraud-kjar.StandardProcess"
     signal_name: str = "customerResponse"
+    shards: int = 1                  # KIE shard processes (process/sharding.py): starts routed by
+                                     # transaction-id hash, signals / tasks by shard-encoded id;
+                                     # KIE_SERVER_URL then lists one URL per shard or a {shard} template
 
 
 @dataclass
@@ -154,6 +157,7 @@ ENV_MAP = {
     "CCFD_KAFKA_PARTITIONS": ("kafka", "partitions", int),
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),
     "CCFD_KIE_NOTIFICATION_TIMEOUT_S": ("kie", "notification_timeout_s", float),
+    "CCFD_KIE_SHARDS": ("kie", "shards", int),
 }
 
 

@@ -217,9 +217,14 @@ class BatchingPublisher:
     messages, README.md:560): ``publish`` enqueues; a daemon thread sends what accumulated as
     one ``produce_many`` RecordBatch every ``linger_s`` (Kafka's linger.ms) instead of one
     produce request per message on the caller's thread -- at 1e6 tx/s the fraud process
-    publishes ~2e3 notifications/s."""
+    publishes ~2e3 notifications/s.
 
-    def __init__(self, broker, topic: str, linger_s: float = 0.002, max_batch: int = 4096):
+    ``publish(value, token)``: ``on_sent(tokens)`` is called (publisher thread) with the tokens
+    of every batch once the broker acknowledged it -- the KIE outbox clears a notification
+    only then, the notifier commits a consumed offset only then (at-least-once hand-over,
+    made exactly-once by idempotent produce + consumer-side dedupe)."""
+
+    def __init__(self, broker, topic: str, linger_s: float = 0.002, max_batch: int = 4096, on_sent=None):
         import collections
         import threading
         self.broker = broker
@@ -233,12 +238,13 @@ class BatchingPublisher:
         self.errors = 0
         self._n_parts = None
         self._rr = 0
+        self.on_sent = on_sent
         self._th = threading.Thread(target=self._run, daemon=True, name=f"publish-{topic}")
         self._th.start()
 
-    def publish(self, value: bytes) -> None:
+    def publish(self, value: bytes, token=None) -> None:
         with self._cv:
-            self._q.append(value)
+            self._q.append((value, token))
             if len(self._q) >= self.max_batch:
                 self._cv.notify()
 
@@ -257,15 +263,20 @@ class BatchingPublisher:
             if not batch:
                 continue
             try:
+                values = [v for v, _t in batch]
                 if hasattr(self.broker, "produce_many"):
                     if self._n_parts is None:
                         self._n_parts = max(1, int(self.broker.partitions(self.topic)))
-                    self.broker.produce_many(self.topic, batch, partition=self._rr % self._n_parts)
+                    self.broker.produce_many(self.topic, values, partition=self._rr % self._n_parts)
                     self._rr += 1
                 else:
-                    for v in batch:
+                    for v in values:
                         self.broker.produce(self.topic, v)
                 self.sent += len(batch)
+                if self.on_sent is not None:
+                    toks = [t for _v, t in batch if t is not None]
+                    if toks:
+                        self.on_sent(toks)
             except Exception:                 # broker unavailable: retry the SAME batch later
                 # (an idempotent producer re-sends it under the same sequence number, so a batch
                 # the broker stored before the failure is not stored twice -- and no message
@@ -277,6 +288,10 @@ class BatchingPublisher:
                         self._q.extendleft(reversed(batch))
                     return
                 time.sleep(0.05)
+
+    def pending(self) -> int:
+        with self._cv:
+            return len(self._q)
 
     def close(self, timeout_s: float = 5.0) -> None:
         t0 = time.time()

@@ -75,6 +75,14 @@ def _consumer(broker, a, group, topics):
     return broker.consumer(group, topics)
 
 
+def _kie_client(cfg, timeout_s: float = 5.0, pool_size: int = 5):
+    """The router / engine side of KIE: one KieClient, or a ShardedKieClient over the
+    ``kie.shards`` servers KIE_SERVER_URL names (process/sharding.py)."""
+    from ..process.sharding import ShardedKieClient
+    sk = ShardedKieClient.from_config(cfg.kie, timeout_s=timeout_s, pool_size=pool_size)
+    return sk.clients[0] if sk.shards == 1 else sk
+
+
 def _model(kind: str, weights: str = None, seed: int = 0):
     from ..data import FRAUD_RATE, generate
     from ..models import build_model, load_model
@@ -190,6 +198,10 @@ def cmd_kie(a, cfg):
     from ..process.notifier import encode_notification
     from ..process.prediction_service import PredictionService
     from ..serving.client import SeldonClient
+    from ..process.sharding import shard_from_env
+    shard, shards = shard_from_env(a.shard), max(1, cfg.kie.shards)
+    if not 0 <= shard < shards:
+        raise SystemExit(f"kie: shard {shard} outside kie.shards={shards}")
     broker = _broker(cfg, idempotent=True)
     topic = cfg.kafka.notification_topic
     # the KIE pod's own SELDON_URL / SELDON_ENDPOINT name ITS prediction-service target (the
@@ -199,20 +211,32 @@ def cmd_kie(a, cfg):
     client = SeldonClient(url, endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
                           cfg.seldon.pool_size) if a.remote_prediction else None
     from ..ingest.producer import BatchingPublisher
-    pub = BatchingPublisher(broker, topic)          # notifications leave in batches, off the request path
-    kw = dict(publish_notification=lambda m: pub.publish(encode_notification(m)), kie_metrics=KieMetrics(),
-              prediction=PredictionService(cfg.kie.confidence_threshold, client=client))
+    # notifications leave in batches, off the request path; the outbox entry of each (its
+    # fraud instance's journal record, written before the start is acknowledged) is cleared
+    # once the broker acknowledged it, and re-published after a crash (process/engine.py)
+    holder = {}
+    pub = BatchingPublisher(broker, topic, on_sent=lambda toks: holder["eng"].mark_notified(toks))
+    kw = dict(publish_notification=lambda m: pub.publish(encode_notification(m), token=m["process_id"]),
+              kie_metrics=KieMetrics(),
+              prediction=PredictionService(cfg.kie.confidence_threshold, client=client), shard=shard, shards=shards)
     if a.journal and os.path.exists(a.journal):
         # restart after a crash: in-flight instances, timers and the per-transaction dedupe
         # index come back from the journal, so re-sent fraud starts are recognised
         eng = ProcessEngine.recover(a.journal, notification_timeout_s=cfg.kie.notification_timeout_s,
                                     dmn_probability_threshold=cfg.kie.dmn_probability_threshold,
                                     dmn_amount_threshold=cfg.kie.dmn_amount_threshold, **kw)
-        print(f"[kie] recovered {len(eng.instances)} instances ({len(eng._by_tx)} fraud transactions) "
-              f"from {a.journal}", flush=True)
+        print(f"[kie] recovered {len(eng.instances)} instances ({eng.fraud_count} fraud, {eng.standard_count} "
+              f"standard) from {a.journal}", flush=True)
     else:
         eng = ProcessEngine.from_config(cfg.kie, journal_path=a.journal, **kw)
+    holder["eng"] = eng
+    outbox = eng.pending_notifications()
+    for m in outbox:                    # notifications whose produce was never acknowledged
+        pub.publish(encode_notification(m), token=m["process_id"])
+    if outbox:
+        print(f"[kie] outbox: re-publishing {len(outbox)} notifications", flush=True)
     srv = KieServer(eng, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id)
+    print(f"[kie] shard {shard} of {shards} on :{a.port or cfg.kie.port}", flush=True)
     from ..ingest.kafka_wire import warm_native
     print(f"[kie] native codecs loaded in {warm_native():.2f} s", flush=True)
     from ..utils.gcpolicy import track_pauses, tune_for_service
@@ -227,25 +251,36 @@ def cmd_notifier(a, cfg):
     from ..ingest.producer import BatchingPublisher
     from ..process.notifier import NotificationService
     broker = _broker(cfg, idempotent=True)
-    # replies leave in batches (one produce request per linger period, not per reply)
-    pub = BatchingPublisher(broker, cfg.kafka.response_topic)
-    ns = NotificationService(lambda raw, key: pub.publish(raw),
+    # replies leave in batches (one produce request per linger period, not per reply); a
+    # consumed notification's offset is committed only once its reply is acknowledged
+    holder = {}
+    pub = BatchingPublisher(broker, cfg.kafka.response_topic, on_sent=lambda toks: holder["ns"].on_published(toks))
+    ns = NotificationService(lambda raw, key, tok: pub.publish(raw, token=tok),
                              cfg.notifier.p_reply, cfg.notifier.p_approve, cfg.notifier.mean_delay_s,
-                             cfg.notifier.seed)
+                             cfg.notifier.seed, ack_async=True)
+    holder["ns"] = ns
     cons = _consumer(broker, a, "notification-service", [cfg.kafka.notification_topic])
     app = web.Application()
-    app.router.add_get("/health/ping", lambda _r: web.json_response(
-        {"status": "ok", "sent": ns.sent, "replied": ns.replied, "no_reply": ns.no_reply}))
+    app.router.add_get("/health/ping", lambda _r: web.json_response(dict(status="ok", **ns.stats())))
     _serve_in_thread(app, a.host, a.port or cfg.notifier.port)
     from ..ingest.kafka_wire import warm_native
     warm_native()                       # the reply publisher's codecs, before the first reply
     from ..utils.gcpolicy import tune_for_service
     tune_for_service()
+    last_commit = 0.0
     while True:
         for r in _safe(lambda: cons.poll(timeout=0.05, max_records=10_000), []):
-            ns.handle(r.value)
-        _safe(cons.commit)
+            ns.handle(r.value, offset=(r.topic, r.partition, r.offset))
         ns.tick()
+        now = time.monotonic()
+        if now - last_commit >= 0.05:
+            offs = ns.committable()
+            own = getattr(cons, "assignment", None)
+            if own is not None:
+                offs = {tp: o for tp, o in offs.items() if tp in set(own)}
+            if offs:
+                _safe(lambda: cons.commit(offs))
+            last_commit = now
 
 
 def cmd_router(a, cfg):
@@ -255,14 +290,12 @@ def cmd_router(a, cfg):
     from ..contracts import seldon
     from ..ingest.codec import decode_records
     from ..metrics.exporter import RouterMetrics
-    from ..process.kie_server import KieClient
     from ..router.router import Router
     from ..router.rules import RuleSet
     from ..serving.client import SeldonClient
     broker = _broker(cfg)
     rm = RouterMetrics()
-    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
-                    cfg.kie.signal_name)
+    kie = _kie_client(cfg)
     router = Router(RuleSet.from_config(cfg.router), kie, rm)
     sc = SeldonClient(cfg.seldon.url, cfg.seldon.endpoint, cfg.seldon.token, cfg.seldon.timeout_ms,
                       cfg.seldon.pool_size)
@@ -285,6 +318,12 @@ def cmd_router(a, cfg):
         notif.commit()
 
 
+def _shard_path(path: str, shard: int) -> str:
+    """A per-KIE-shard file next to ``path``: x.rank0.jsonl -> x.rank0.shard2.jsonl."""
+    root, ext = os.path.splitext(path)
+    return f"{root}.shard{shard}{ext or '.jsonl'}"
+
+
 def _rank_path(path: str, rank: int) -> str:
     """A per-rank file next to ``path`` (ranks never share a journal): x.jsonl -> x.rank3.jsonl."""
     root, ext = os.path.splitext(path)
@@ -300,7 +339,6 @@ def cmd_engine(a, cfg):
     from ..metrics.exporter import EngineModelCollector, GpuEngineCollector, MetricsHub
     from ..ops.kernels import DeviceModel
     from ..parallel.dp import broadcast_model, init_distributed, resolve_row_format
-    from ..process.kie_server import KieClient
     from ..router.handoff import KieHandoff
     from ..router.router import Router
     from ..router.rules import RuleSet
@@ -316,15 +354,20 @@ def cmd_engine(a, cfg):
     dm = broadcast_model(ctx, model, cfg.engine.model, fmt)      # X1 (+ G20 / G32 bin table)
     broker = _broker(cfg)
     hub = MetricsHub()
-    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
-                    cfg.kie.signal_name, timeout_s=cfg.seldon.timeout_ms / 1e3, pool_size=cfg.seldon.pool_size)
+    kie = _kie_client(cfg, timeout_s=cfg.seldon.timeout_ms / 1e3, pool_size=cfg.seldon.pool_size)
     # fraud starts and response signals go through a bounded async queue with pooled,
-    # retried HTTP: a slow or absent KIE never stalls scoring, commits or X2 (router/handoff.py)
-    dlq = None
-    if cfg.engine.handoff_dlq:
-        from ..router.handoff import DeadLetterQueue
-        dlq = DeadLetterQueue(_rank_path(cfg.engine.handoff_dlq, ctx.rank))
-    handoff = KieHandoff(kie, capacity=cfg.engine.handoff_capacity, workers=cfg.engine.handoff_workers, dlq=dlq)
+    # retried HTTP: a slow or absent KIE never stalls scoring, commits or X2 (router/handoff.py);
+    # with a sharded KIE tier one queue (and dead-letter journal) per shard
+    from ..router.handoff import DeadLetterQueue, ShardedHandoff
+    shards = getattr(kie, "shards", 1)
+    dlq_path = _rank_path(cfg.engine.handoff_dlq, ctx.rank) if cfg.engine.handoff_dlq else None
+    if shards == 1:
+        handoff = KieHandoff(kie, capacity=cfg.engine.handoff_capacity, workers=cfg.engine.handoff_workers,
+                             dlq=DeadLetterQueue(dlq_path) if dlq_path else None)
+    else:
+        dlqs = [DeadLetterQueue(_shard_path(dlq_path, k)) if dlq_path else None for k in range(shards)]
+        handoff = ShardedHandoff(kie.clients, dlqs, capacity=cfg.engine.handoff_capacity,
+                                 workers=cfg.engine.handoff_workers)
     router = Router(rules, kie, hub.router, standard_mode=cfg.router.standard_mode, handoff=handoff)
     svc = EngineService(ctx, dm, broker, router, EngineServiceConfig(
         topic=cfg.kafka.transactions_topic, group_id=cfg.kafka.group_id, batch=cfg.engine.batch,
@@ -468,7 +511,6 @@ def cmd_elastic(a, cfg):
     from ..metrics.exporter import RouterMetrics
     from ..parallel.elastic import PartitionLeases
     from ..parallel.membership import ElasticCounterReducer, ElasticGroup
-    from ..process.kie_server import KieClient
     from ..router.router import Router
     from ..router.rules import RuleSet
     from ..serving.scorers import CpuScorer, GpuScorer
@@ -485,8 +527,7 @@ def cmd_elastic(a, cfg):
         from ..process import ProcessEngine
         sink = ProcessEngine(notification_timeout_s=1e9)
     else:
-        sink = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
-                         cfg.kie.signal_name)
+        sink = _kie_client(cfg)
     router = Router(RuleSet.from_config(cfg.router), sink, rm)
     broker = _broker(cfg)
     leases = PartitionLeases(store, a.rank, a.world, a.partitions, ttl_s=a.ttl)
@@ -542,13 +583,11 @@ def cmd_operator(a, cfg):
 def cmd_dlq_replay(a, cfg):
     """Re-deliver the hand-off dead-letter journal (router/handoff.py DeadLetterQueue) to
     KIE_SERVER_URL: every pending entry exactly once; prints a JSON summary."""
-    from ..process.kie_server import KieClient
     from ..router.handoff import DeadLetterQueue
     path = a.dlq or cfg.engine.handoff_dlq
     if not path:
         raise SystemExit("dlq-replay: --dlq PATH (or CCFD_HANDOFF_DLQ) is required")
-    kie = KieClient(cfg.kie.url, cfg.kie.container_id, cfg.kie.fraud_process_id, cfg.kie.standard_process_id,
-                    cfg.kie.signal_name, timeout_s=cfg.seldon.timeout_ms / 1e3)
+    kie = _kie_client(cfg, timeout_s=cfg.seldon.timeout_ms / 1e3)     # routes a sharded tier's entries
     q = DeadLetterQueue(path)
     res = q.replay(kie)
     q.close()
@@ -602,6 +641,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--weights", default=None, help="safetensors model file (models.save_model)")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--journal", default=None, help="KIE: append-only process journal for recovery")
+    ap.add_argument("--shard", type=int, default=-1,
+                    help="KIE: this server's shard of kie.shards (-1 = CCFD_KIE_SHARD or the pod ordinal)")
     ap.add_argument("--dlq", default=None, help="dlq-replay: the hand-off dead-letter journal to re-deliver")
     ap.add_argument("--remote-prediction", action="store_true", help="KIE: call the user-task model over HTTP")
     ap.add_argument("--fmt", default="json", choices=["json", "txb1"])

@@ -31,12 +31,12 @@ SANITIZE = os.environ.get("CCFD_SANITIZE", "")
 
 
 # Host-only codecs (CRC-32C, Kafka RecordBatch framing, JSON transaction parsing, row
-# encoders) ALSO go into a small library with no HIP dependency: the broker, KIE, notifier
+# encoders) and the KIE tier's start-dedupe index ALSO go into a small library with no HIP dependency: the broker, KIE, notifier
 # and producer processes load only this one, so they never bring up the GPU runtime (CPU-only
 # pods in the operator's deployment; ~0.3 s with the GIL held in a service that loaded the
 # engine library lazily, profiles/r4/kie_handoff/).
 HOST_LIB = NATIVE / "libccfd_host.so"
-HOST_SOURCES = ("crc32c.cpp", "kafka_codec.cpp", "ingest.cpp")
+HOST_SOURCES = ("crc32c.cpp", "kafka_codec.cpp", "ingest.cpp", "dedupe.cpp")
 
 
 def host_sources():

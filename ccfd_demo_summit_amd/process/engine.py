@@ -70,6 +70,7 @@ class ProcessInstance:
     timer_due: Optional[float] = None
     task_id: Optional[int] = None
     history: List[str] = field(default_factory=list)
+    notified: bool = False          # its CustomerNotification was acknowledged by the broker
 
     @property
     def amount(self) -> float:
@@ -89,7 +90,11 @@ class ProcessEngine:
                  publish_notification: Optional[Callable[[Dict[str, Any]], None]] = None,
                  kie_metrics=None, prediction: Optional[PredictionService] = None,
                  clock: Callable[[], float] = time.monotonic, journal_path: Optional[str] = None,
-                 keep_completed: int = 100_000):
+                 keep_completed: int = 100_000, shard: int = 0, shards: int = 1,
+                 standard_dedupe_window: int = 1 << 20):
+        """``shard`` / ``shards``: this engine is shard ``shard`` of a K-way KIE tier
+        (process/sharding.py) -- its instance and task ids are ``shard + K * n``, so a signal
+        or task completion that carries only the id reaches the owner."""
         self.timeout = float(notification_timeout_s)
         self.p_thr = float(dmn_probability_threshold)
         self.a_thr = float(dmn_amount_threshold)
@@ -97,10 +102,13 @@ class ProcessEngine:
         self.metrics = kie_metrics
         self.prediction = prediction or PredictionService()
         self.clock = clock
+        self.shard, self.shards = int(shard), max(1, int(shards))
+        if not 0 <= self.shard < self.shards:
+            raise ValueError(f"shard {shard} of {shards}")
         self.instances: Dict[int, ProcessInstance] = {}
         self.tasks: Dict[int, UserTask] = {}
         self._timers: List = []
-        self._ids = itertools.count(1)
+        self._next_n = 1                    # next instance sequence number: iid = shard + K * n
         self._task_ids = itertools.count(1)
         self._lock = threading.RLock()
         self.outcome_counts: Dict[str, int] = {o.value: 0 for o in Outcome}
@@ -112,9 +120,18 @@ class ProcessEngine:
         self._by_tx: Dict[Any, int] = {}
         self._tx_order = collections.deque()
         self.duplicates = 0
+        self.fraud_count = 0                # fraud processes started (all time, recovered)
+        # CustomerNotification outbox: a fraud start's journal record (written before the start
+        # is acknowledged) holds its notification as pending; ``mark_notified`` clears it once
+        # the broker acknowledged the produce; ``recover()`` re-publishes what is still pending
+        self.notified_count = 0
+        self._pending_notes: List[Dict[str, Any]] = []
         # standard starts are idempotent per transaction id too (a re-delivered hand-off batch
-        # must not start a second standard process): tx id -> instance id over a bounded window
-        self.standard_dedupe_window = 1 << 20
+        # must not start a second standard process): tx id -> instance id over a bounded window,
+        # native for integer ids (process/dedupe.py); other ids (e.g. strings) use a dict
+        self.standard_dedupe_window = int(standard_dedupe_window)
+        from .dedupe import DedupeIndex
+        self._std_index = DedupeIndex(self.standard_dedupe_window)
         self._std_by_tx: Dict[Any, int] = {}
         self._std_order: collections.deque = collections.deque()
         self.standard_duplicates = 0
@@ -130,6 +147,25 @@ class ProcessEngine:
         pred = kw.pop("prediction", None) or PredictionService(kie_cfg.confidence_threshold)
         return cls(kie_cfg.notification_timeout_s, kie_cfg.dmn_probability_threshold,
                    kie_cfg.dmn_amount_threshold, prediction=pred, **kw)
+
+    # ------------------------------------------------------------------ ids
+    def _iid(self, n: int) -> int:
+        return self.shard + self.shards * int(n)
+
+    def _n_of(self, iid: int) -> int:
+        return (int(iid) - self.shard) // self.shards
+
+    def _next_iid(self) -> int:
+        iid = self._iid(self._next_n)
+        self._next_n += 1
+        return iid
+
+    def _next_tid(self) -> int:
+        return self.shard + self.shards * next(self._task_ids)
+
+    def owns(self, iid: int) -> bool:
+        """Whether instance / task id ``iid`` belongs to this shard."""
+        return int(iid) % self.shards == self.shard
 
     # ------------------------------------------------------------------ journal
     def _record(self, inst: ProcessInstance) -> str:
@@ -158,6 +194,7 @@ class ProcessEngine:
         """Rebuild from the journal (last record per instance wins), then keep appending."""
         last: Dict[int, dict] = {}
         std_batches: List[dict] = []
+        notified = set()                        # outbox entries the broker acknowledged
         if os.path.exists(journal_path):
             with open(journal_path) as f:
                 for line in f:
@@ -169,7 +206,9 @@ class ProcessEngine:
                             continue        # the torn last line of a killed process
                         if "standard" in rec:
                             std_batches.append(rec["standard"])
-                        else:
+                        elif "notified" in rec:
+                            notified.update(rec["notified"])
+                        elif "instance" in rec:
                             last[rec["instance"]["id"]] = rec
         if os.path.exists(journal_path) and os.path.getsize(journal_path) > 0:
             with open(journal_path, "rb+") as f:            # end a torn last line, so the
@@ -177,52 +216,111 @@ class ProcessEngine:
                 if f.read(1) != b"\n":
                     f.write(b"\n")
         eng = cls(journal_path=journal_path, **kw)
-        max_id, max_task = 0, 0
+        max_n, max_task = 0, 0
         for iid, rec in last.items():
             d = dict(rec["instance"])
             d["state"] = State(d["state"])
             inst = ProcessInstance(**d)
             eng.instances[iid] = inst
-            max_id = max(max_id, iid)
+            max_n = max(max_n, eng._n_of(iid))
             txid = inst.variables.get("transaction_id")
-            if txid is not None and inst.process_id == cls.FRAUD:
-                eng._by_tx[txid] = iid
-                eng._tx_order.append(txid)
+            if inst.process_id == cls.FRAUD:
+                eng.fraud_count += 1
+                if txid is not None:
+                    eng._by_tx[txid] = iid
+                    eng._tx_order.append(txid)
+                # the reference's outcome counters (README.md:593-599) come back too
+                if inst.task_id is not None:
+                    eng.outcome_counts[Outcome.INVESTIGATION.value] += 1
+                if inst.outcome is not None:
+                    eng.outcome_counts[inst.outcome] = eng.outcome_counts.get(inst.outcome, 0) + 1
+                if inst.notified or iid in notified:
+                    inst.notified = True
+                    eng.notified_count += 1
+                else:                           # in the outbox: published again on restart
+                    eng._pending_notes.append(eng._notification(inst))
             if "task" in rec:
                 t = UserTask(**rec["task"])
                 eng.tasks[t.id] = t
-                max_task = max(max_task, t.id)
+                max_task = max(max_task, (t.id - eng.shard) // eng.shards)
             if inst.state == State.WAITING_CUSTOMER and inst.timer_due is not None:
                 heapq.heappush(eng._timers, (inst.timer_due, iid))
+        import numpy as np
         for b in std_batches:                   # batched standard starts (start_standard_many)
             if "tx_i64" in b:                   # base64 of the new transaction ids (int64 LE)
                 import base64
-
-                import numpy as np
-                b = {"id0": b["id0"], "transaction_id": np.frombuffer(base64.b64decode(b["tx_i64"]), "<i8").tolist()}
-            ids = b["id"] if "id" in b else range(int(b["id0"]), int(b["id0"]) + len(b["transaction_id"]))
-            for iid, tx in zip(ids, b["transaction_id"]):
-                max_id = max(max_id, iid)
-                eng.standard_count += 1
-                eng.outcome_counts[Outcome.STANDARD.value] += 1
-                if tx is not None:
-                    eng._std_remember(tx, iid)
+                tx = np.frombuffer(base64.b64decode(b["tx_i64"]), "<i8")
+                ids = int(b["id0"]) + int(b.get("st", 1)) * np.arange(len(tx), dtype=np.int64)
+            else:                               # round-3 form: JSON lists
+                tx = b["transaction_id"]
+                ids = b["id"] if "id" in b else list(range(int(b["id0"]), int(b["id0"]) + len(tx)))
+            if len(ids):
+                max_n = max(max_n, eng._n_of(int(np.max(ids))))
+            eng.standard_count += len(tx)
+            eng.outcome_counts[Outcome.STANDARD.value] += len(tx)
+            eng._std_restore(tx, ids)
         for iid, rec in last.items():
             if rec["instance"]["process_id"] == cls.STANDARD:
                 eng.standard_count += 1
                 eng.outcome_counts[Outcome.STANDARD.value] += 1
                 tx = rec["instance"]["variables"].get("transaction_id")
                 if tx is not None:
-                    eng._std_remember(tx, iid)
-        eng._ids = itertools.count(max_id + 1)
+                    eng._std_restore([tx], [iid])
+        eng._next_n = max_n + 1
         eng._task_ids = itertools.count(max_task + 1)
         return eng
+
+    # ------------------------------------------------------------------ notification outbox
+    @staticmethod
+    def _notification(inst: "ProcessInstance") -> Dict[str, Any]:
+        v = inst.variables
+        return {"customer_id": v.get("customer_id"), "transaction_id": v.get("transaction_id", v.get("tx_id")),
+                "process_id": inst.id, "amount": v.get("amount"), "proba": v.get("proba")}
+
+    def pending_notifications(self) -> List[Dict[str, Any]]:
+        """The recovered outbox: notifications of fraud instances whose produce was never
+        acknowledged (the caller publishes them again; the notifier dedupes by process id)."""
+        with self._lock:
+            out, self._pending_notes = self._pending_notes, []
+        return out
+
+    def mark_notified(self, iids) -> None:
+        """The broker acknowledged these instances' CustomerNotifications: clear them from the
+        outbox (one journal line per acknowledged batch)."""
+        iids = [int(i) for i in iids]
+        if not iids:
+            return
+        with self._lock:
+            for i in iids:
+                inst = self.instances.get(i)
+                if inst is not None:
+                    inst.notified = True
+            self.notified_count += len(iids)
+            if self._journal is not None:
+                self._write_journal('{"notified": %s}\n' % json.dumps(iids))
 
     # ------------------------------------------------------------------ start
     def start(self, process_id: str, variables: Dict[str, Any]) -> int:
         if process_id.endswith(self.STANDARD) or process_id == self.STANDARD:
             return self.start_standard(variables)
         return self.start_fraud(variables)
+
+    @staticmethod
+    def _native_key(tx) -> bool:
+        return isinstance(tx, (int,)) and not isinstance(tx, bool) and tx >= 0
+
+    def _std_restore(self, txs, ids) -> None:
+        """Recovery: put admitted (transaction, instance) pairs back in the dedupe window."""
+        import numpy as np
+        txs = list(txs) if not hasattr(txs, "dtype") else txs
+        if hasattr(txs, "dtype") or all(self._native_key(t) for t in txs):
+            self._std_index.insert(np.asarray(txs, np.int64), np.asarray(ids, np.int64))
+            return
+        for t, i in zip(txs, ids):
+            if self._native_key(t):
+                self._std_index.insert([t], [i])
+            else:
+                self._std_remember(t, int(i))
 
     def _std_remember(self, tx, iid: int) -> None:
         self._std_by_tx[tx] = iid
@@ -234,13 +332,23 @@ class ProcessEngine:
         """Standard process (README.md:552): completes at once as STANDARD.  Idempotent per
         transaction id, like fraud starts."""
         txid = variables.get("transaction_id", variables.get("tx_id"))
+        if isinstance(txid, float) and txid.is_integer():
+            txid = int(txid)
         with self._lock:
-            if txid is not None and txid in self._std_by_tx:
-                self.standard_duplicates += 1
-                return self._std_by_tx[txid]
-            iid = next(self._ids)
-            if txid is not None:
-                self._std_remember(txid, iid)
+            if self._native_key(txid):
+                ids, new = self._std_index.assign([txid], self._iid(self._next_n), self.shards)
+                iid = int(ids[0])
+                if not len(new):
+                    self.standard_duplicates += 1
+                    return iid
+                self._next_n += 1
+            else:
+                if txid is not None and txid in self._std_by_tx:
+                    self.standard_duplicates += 1
+                    return self._std_by_tx[txid]
+                iid = self._next_iid()
+                if txid is not None:
+                    self._std_remember(txid, iid)
             now = self.clock()
             inst = ProcessInstance(iid, self.STANDARD, dict(variables), State.COMPLETED,
                                    Outcome.STANDARD.value, now, now, history=["start", "approve"])
@@ -251,49 +359,59 @@ class ProcessEngine:
             return iid
 
     def start_standard_many(self, items) -> List[int]:
+        """``start_standard_array`` with the ids as a list."""
+        ids = self.start_standard_array(items)
+        return ids.tolist() if hasattr(ids, "tolist") else ids
+
+    def start_standard_array(self, items):
         """Standard processes for a whole hand-off batch (the engine's standard-routed rows of a
         scoring step).  ``items``: a list of variable dicts, or columns ``{"transaction_id":
         [...], "customer_id": [...], "amount": [...], "proba": [...]}`` (lists or numpy arrays --
-        the compact form the router sends at ~1e5 standard rows a second).  Idempotent per
-        transaction id (a re-delivered batch, or a transaction twice in one batch, starts once).
-        New instances get consecutive ids; the batch is journaled as ONE record (first id + the
-        new transaction ids), which ``recover()`` replays."""
-        numeric = isinstance(items, dict) and hasattr(items.get("transaction_id", items.get("tx_id")), "dtype")
-        cols = columns_of(items)
-        txs = cols.get("transaction_id")
-        if txs is None:
-            txs = cols.get("tx_id")
-        n = _ncols(cols)
-        sc = cols.pop("scored_ns", None)
-        if sc:
-            self._note_handoff(sc[0], n)
-        if txs is None or (not numeric and any(t is None for t in txs)):
-            return [self.start_standard({k: v[i] for k, v in cols.items()}) for i in range(n)]
+        the compact form the router sends at ~1e5..1e6 standard rows a second).  Idempotent per
+        transaction id (a re-delivered batch, or a transaction twice in one batch, starts once),
+        through the native dedupe window (process/dedupe.py).  New instances get the shard's
+        next ids in admission order; the batch is journaled as ONE compact record (first id,
+        id stride, the new transaction ids), which ``recover()`` replays.  Returns the instance
+        ids in order (an int64 array for numeric columns)."""
+        import numpy as np
+        if isinstance(items, dict):
+            tx = items.get("transaction_id", items.get("tx_id"))
+            sc = items.get("scored_ns")
+        else:
+            tx = [it.get("transaction_id", it.get("tx_id")) for it in items]
+            sc = [it.get("scored_ns") for it in items] if items and "scored_ns" in items[0] else None
+        n = 0 if tx is None else len(tx)
+        if sc is not None and len(sc) and sc[0]:
+            self._note_handoff(int(sc[0]), n)
+        if tx is None:
+            return [self.start_standard(v) for v in rows_of(items)]
+        if hasattr(tx, "dtype") and tx.dtype.kind in "iu":
+            tx = np.ascontiguousarray(tx, np.int64)
+        else:
+            tl = list(tx)
+            if not tl or not all(self._native_key(t) for t in tl):
+                rows = rows_of(items) if isinstance(items, dict) else list(items)
+                return [self.start_standard(v) for v in rows]
+            tx = np.asarray(tl, np.int64)
+        if n and int(tx.min()) < 0:
+            rows = rows_of(items) if isinstance(items, dict) else list(items)
+            return [self.start_standard(v) for v in rows]
         with self._lock:
-            seen = self._std_by_tx
-            new = sorted(set(txs).difference(seen))     # C: iterates the batch, not the dedupe window
+            first = self._iid(self._next_n)
+            ids, new = self._std_index.assign(tx, first, self.shards)
             n_new = len(new)
-            first = 0
-            if n_new:
-                first = next(self._ids)
-                self._ids = itertools.count(first + n_new)
-                seen.update(zip(new, range(first, first + n_new)))
-                self._std_order.extend(new)
-                for _ in range(len(self._std_order) - self.standard_dedupe_window):
-                    seen.pop(self._std_order.popleft(), None)
-            out = [-1 if i is None else i for i in map(seen.get, txs)]
+            self._next_n += n_new
             self.standard_duplicates += n - n_new
             self.standard_count += n_new
             self.outcome_counts[Outcome.STANDARD.value] += n_new
             if self._journal is not None and n_new:
                 import base64
-
-                import numpy as np
-                tx64 = base64.b64encode(np.asarray(new, np.int64).tobytes()).decode()
+                tx64 = base64.b64encode(new.astype("<i8").tobytes()).decode()
                 t0 = time.monotonic_ns()
-                self._journal.write('{"standard": {"id0": %d, "tx_i64": "%s"}}\n' % (first, tx64))
+                self._journal.write('{"standard": {"id0": %d, "st": %d, "tx_i64": "%s"}}\n'
+                                    % (first, self.shards, tx64))
                 self.journal_time.add(time.monotonic_ns() - t0)
-        return out
+        return ids
 
     def _note_handoff(self, scored_ns, n: int = 1) -> None:
         if not scored_ns or n <= 0:
@@ -328,7 +446,8 @@ class ProcessEngine:
             if txid is not None and txid in self._by_tx:
                 self.duplicates += 1
                 return self._by_tx[txid]
-            iid = next(self._ids)
+            iid = self._next_iid()
+            self.fraud_count += 1
             if txid is not None:
                 self._by_tx[txid] = iid
                 self._tx_order.append(txid)
@@ -372,7 +491,8 @@ class ProcessEngine:
                     self.duplicates += 1
                     out.append(by_tx[txid])
                     continue
-                iid = next(self._ids)
+                iid = self._next_iid()
+                self.fraud_count += 1
                 if txid is not None:
                     by_tx[txid] = iid
                     order.append(txid)
@@ -438,7 +558,7 @@ class ProcessEngine:
                 if self.metrics:
                     self.metrics.investigation.observe(inst.amount)
                 self.outcome_counts[Outcome.INVESTIGATION.value] += 1
-                tid = next(self._task_ids)
+                tid = self._next_tid()
                 task = UserTask(tid, iid, inputs={"amount": inst.amount, "proba": inst.proba,
                                                   "transaction_id": inst.variables.get("transaction_id"),
                                                   "customer_id": inst.variables.get("customer_id")})

@@ -10,6 +10,11 @@ KIE Server REST paths ([EXT], container/process/signal ids configurable, SURVEY.
   PUT  /services/rest/server/containers/{c}/tasks/{t}/states/completed         -> complete
   GET  /rest/metrics                                                           -> Prometheus
 A background task fires process timers (``ProcessEngine.tick``).
+
+Sharded tier (process/sharding.py): a server is shard ``engine.shard`` of ``engine.shards``.
+A start whose transaction hashes to another shard, or a signal / task / instance request for
+an id another shard owns, is answered ``421 Misdirected Request`` -- a misconfigured router
+surfaces (the hand-off dead-letters it) instead of silently breaking per-shard idempotency.
 """
 from __future__ import annotations
 
@@ -30,6 +35,8 @@ BASE = "/services/rest/server"
 
 
 COLUMNS_CT = "application/x-ccfd-columns"
+IDS_CT = "application/x-ccfd-ids"          # response: the instance ids as raw int64 LE
+MISDIRECTED = 421
 _COL_DT = {"q": "<i8", "d": "<f8", "f": "<f4", "I": "<u4"}
 
 
@@ -135,6 +142,42 @@ class KieServer:
             return web.json_response({"type": "FAILURE", "msg": f"Container {c} is not instantiated."}, status=404)
         return None
 
+    @property
+    def shard(self) -> int:
+        return getattr(self.engine, "shard", 0)
+
+    @property
+    def shards(self) -> int:
+        return getattr(self.engine, "shards", 1)
+
+    def _misdirected(self, what: str) -> web.Response:
+        return web.json_response({"type": "FAILURE", "msg": f"{what} belongs to another KIE shard "
+                                  f"(this is shard {self.shard} of {self.shards})"}, status=MISDIRECTED)
+
+    def _foreign_txs(self, items) -> int:
+        """How many of a start request's transactions hash to another shard."""
+        if self.shards <= 1:
+            return 0
+        from .sharding import shard_of_tx
+        if isinstance(items, dict):
+            tx = items.get("transaction_id", items.get("tx_id"))
+            if tx is None:
+                return 0
+            import numpy as np
+            t = np.asarray(tx)
+            if t.dtype.kind not in "iu":
+                t = np.asarray([int(x) for x in tx], np.int64)
+            return int((shard_of_tx(t, self.shards) != self.shard).sum())
+        n = 0
+        for v in items:
+            tx = v.get("transaction_id", v.get("tx_id")) if isinstance(v, dict) else None
+            if isinstance(tx, (int, float)) and shard_of_tx(int(tx), self.shards) != self.shard:
+                n += 1
+        return n
+
+    def _foreign_id(self, iid) -> bool:
+        return self.shards > 1 and int(iid) % self.shards != self.shard
+
     async def info(self, _request):
         return web.json_response({"type": "SUCCESS", "msg": "Kie Server info",
                                   "result": {"kie-server-info": {"id": "ccd-service", "version": "ccfd-mi355x",
@@ -147,6 +190,8 @@ class KieServer:
         pid = request.match_info["p"]
         raw = await request.read()
         variables = json.loads(raw) if raw else {}
+        if self._foreign_txs([variables]):
+            return self._misdirected("transaction")
         if pid == self.standard_pid:
             iid = self.engine.start_standard(variables)
         elif pid == self.fraud_pid:
@@ -175,8 +220,15 @@ class KieServer:
         if not isinstance(items, (list, dict)):
             return web.json_response({"type": "FAILURE", "msg": "expected a JSON list or columns"}, status=400)
         try:
+            foreign = self._foreign_txs(items)
+        except (ValueError, TypeError) as e:
+            return web.json_response({"type": "FAILURE", "msg": f"bad batch: {e}"}, status=400)
+        if foreign:
+            return self._misdirected(f"{foreign} transaction(s) of the batch")
+        try:
             if pid == self.standard_pid:
-                ids = self.engine.start_standard_many(items)
+                ids = self.engine.start_standard_array(items) if hasattr(self.engine, "start_standard_array") \
+                    else self.engine.start_standard_many(items)
             elif pid == self.fraud_pid:
                 ids = self.engine.start_fraud_many(items)
             else:
@@ -187,6 +239,13 @@ class KieServer:
             return web.json_response({"type": "FAILURE", "msg": f"Could not find process definition {pid}"},
                                      status=404)
         self._note_request(items, t_in, len(ids))
+        if IDS_CT in request.headers.get("Accept", ""):
+            import numpy as np                  # binary ids: no JSON list of 4096 ints to build
+            body = np.asarray(ids, np.int64).astype("<i8", copy=False).tobytes()
+            self.handler_time.add(time.monotonic_ns() - t0)
+            return web.Response(body=body, status=201, content_type=IDS_CT)
+        if hasattr(ids, "tolist"):
+            ids = ids.tolist()
         self.handler_time.add(time.monotonic_ns() - t0)
         return web.json_response(ids, status=201)
 
@@ -206,6 +265,8 @@ class KieServer:
             return bad
         raw = await request.read()
         payload = json.loads(raw) if raw else None
+        if self._foreign_id(request.match_info["i"]):
+            return self._misdirected("process instance")
         ok = self.engine.signal(int(request.match_info["i"]), request.match_info["s"], payload)
         return web.Response(status=200 if ok else 404)
 
@@ -219,10 +280,14 @@ class KieServer:
         items = json.loads(await request.read() or b"[]")
         if not isinstance(items, list):
             return web.json_response({"type": "FAILURE", "msg": "expected a JSON list"}, status=400)
+        if any(self._foreign_id(it["instance_id"]) for it in items):
+            return self._misdirected("a process instance of the batch")
         return web.json_response([bool(self.engine.signal(int(it["instance_id"]), it.get("signal", "customerResponse"),
                                                           it.get("payload"))) for it in items])
 
     async def get_instance(self, request: web.Request):
+        if self._foreign_id(request.match_info["i"]):
+            return self._misdirected("process instance")
         inst = self.engine.get(int(request.match_info["i"]))
         if inst is None:
             return web.json_response({"type": "FAILURE"}, status=404)
@@ -242,12 +307,16 @@ class KieServer:
              "confidence": t.confidence} for t in ts]})
 
     async def get_task(self, request: web.Request):
+        if self._foreign_id(request.match_info["t"]):
+            return self._misdirected("task")
         t = self.engine.tasks.get(int(request.match_info["t"]))
         if t is None:
             return web.json_response({"type": "FAILURE"}, status=404)
         return web.json_response(asdict(t), dumps=lambda o: json.dumps(o, default=str))
 
     async def complete_task(self, request: web.Request):
+        if self._foreign_id(request.match_info["t"]):
+            return self._misdirected("task")
         raw = await request.read()
         out = json.loads(raw) if raw else {}
         outcome = out.get("outcome", out.get("approved"))
@@ -259,7 +328,9 @@ class KieServer:
         e = self.engine
         with e._lock:
             fraud = sum(1 for i in e.instances.values() if i.process_id == e.FRAUD)
-            body = {"fraud_instances_retained": fraud, "fraud_started": len(e._by_tx), "duplicates": e.duplicates,
+            body = {"shard": self.shard, "shards": self.shards,
+                    "fraud_instances_retained": fraud, "fraud_started": getattr(e, "fraud_count", len(e._by_tx)),
+                    "duplicates": e.duplicates, "notified": getattr(e, "notified_count", 0),
                     "standard_started": e.standard_count, "standard_duplicates": e.standard_duplicates,
                     "scored_to_started_us": e.handoff_latency_us(),
                     "handoff_attribution": self.attribution(),
@@ -341,8 +412,12 @@ class KieClient:
                 return []
             body, ct = json.dumps(items), "application/json"
         r = self.s.post(f"{self.base}/containers/{self.c}/processes/{self.standard_pid}/instances/batch",
-                        data=body, headers={"Content-Type": ct}, timeout=self.timeout)
+                        data=body, headers={"Content-Type": ct, "Accept": f"{IDS_CT}, application/json"},
+                        timeout=self.timeout)
         r.raise_for_status()
+        if r.headers.get("Content-Type", "").startswith(IDS_CT):
+            import numpy as np
+            return np.frombuffer(r.content, "<i8").tolist()
         return [int(x) for x in r.json()]
 
     def signal_many(self, items) -> list:
@@ -359,6 +434,6 @@ class KieClient:
     def signal(self, instance_id: int, name: str, payload) -> bool:
         r = self.s.post(f"{self.base}/containers/{self.c}/processes/instances/{instance_id}/signal/{name or self.signal_name}",
                         data=json.dumps(payload), headers={"Content-Type": "application/json"}, timeout=self.timeout)
-        if r.status_code >= 500:
-            r.raise_for_status()              # transient: the hand-off retries it
+        if r.status_code >= 500 or r.status_code == MISDIRECTED:
+            r.raise_for_status()              # 5xx transient: retried; 421 misrouted: dead-lettered
         return r.status_code == 200

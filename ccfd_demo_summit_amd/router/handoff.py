@@ -457,3 +457,135 @@ class KieHandoff:
                     "outage_s": round(self.outage_s, 3),
                     "queue_wait_us": self.queue_wait.summary_us(),
                     "request_us": self.request_time.summary_us()}
+
+
+class ShardedHandoff:
+    """The hand-off to a K-shard KIE tier (process/sharding.py): one ``KieHandoff`` per shard
+    -- its own queue, workers, retries and dead-letter journal -- so a slow or restarting shard
+    holds back only its own requests.  Starts are split by transaction-id shard, signals go to
+    the shard that owns the instance id.
+
+    Sequence numbers are global: ``submit_*`` returns ``g`` and records the vector of the
+    shards' last sequence numbers at that moment; ``acked(g)`` holds once every shard has
+    acknowledged up to its entry of that vector, i.e. everything submitted up to ``g`` -- the
+    engine commits a Kafka offset only then, exactly as with one KIE server."""
+
+    def __init__(self, sinks, dlqs: Optional[List[Optional[DeadLetterQueue]]] = None, **kw):
+        if not sinks:
+            raise ValueError("no KIE shards")
+        dlqs = dlqs or [None] * len(sinks)
+        self.shards = len(sinks)
+        self.parts = [KieHandoff(s, dlq=d, **kw) for s, d in zip(sinks, dlqs)]
+        self.capacity = self.parts[0].capacity
+        self._lock = threading.Lock()
+        self._g = -1
+        self._marks: Deque[Tuple[int, Tuple[int, ...]]] = collections.deque()
+        self._acked_g = -1
+
+    # ------------------------------------------------------------------ producer side
+    def _mark(self) -> int:
+        self._g += 1
+        self._marks.append((self._g, tuple(p.last_seq() for p in self.parts)))
+        return self._g
+
+    def submit_starts(self, items: List[Dict[str, Any]]) -> int:
+        from ..process.sharding import shard_of_tx
+        with self._lock:
+            if not items:
+                return self._g
+            groups: Dict[int, List[Dict[str, Any]]] = {}
+            for v in items:
+                tx = v.get("transaction_id", v.get("tx_id"))
+                groups.setdefault(0 if tx is None else shard_of_tx(int(tx), self.shards), []).append(v)
+            for k, sub in groups.items():
+                self.parts[k].submit_starts(sub)
+            return self._mark()
+
+    def submit_standard(self, cols: Dict[str, Any]) -> int:
+        import numpy as np
+
+        from ..process.sharding import shard_of_tx, split_columns, tx_column
+        with self._lock:
+            tx = tx_column(cols)
+            if tx is None or not len(tx):
+                return self._g
+            sh = shard_of_tx(np.asarray(tx), self.shards)
+            for k, sub in enumerate(split_columns(cols, sh, self.shards)):
+                if sub is not None:
+                    self.parts[k].submit_standard(sub)
+            return self._mark()
+
+    def submit_signal(self, instance_id: int, name: str, payload: Any) -> int:
+        with self._lock:
+            self.parts[int(instance_id) % self.shards].submit_signal(instance_id, name, payload)
+            return self._mark()
+
+    def last_seq(self) -> int:
+        with self._lock:
+            return self._g
+
+    def depth(self) -> int:
+        return sum(p.depth() for p in self.parts)
+
+    def full(self) -> bool:
+        return any(p.full() for p in self.parts)
+
+    def has_room(self, low_water: float = 0.5) -> bool:
+        return all(p.has_room(low_water) for p in self.parts)
+
+    def acked(self, seq: int) -> bool:
+        with self._lock:
+            if seq <= self._acked_g:
+                return True
+            acked = [p.acked_seq for p in self.parts]
+            while self._marks and all(a >= v for a, v in zip(acked, self._marks[0][1])):
+                self._acked_g = self._marks.popleft()[0]
+            return seq <= self._acked_g
+
+    @property
+    def acked_seq(self) -> int:
+        self.acked(self._acked_g + 1)
+        return self._acked_g
+
+    def drain(self, timeout_s: float = 30.0) -> bool:
+        t_end = time.monotonic() + timeout_s
+        return all(p.drain(max(0.0, t_end - time.monotonic())) for p in self.parts)
+
+    def close(self, drain_s: float = 5.0) -> None:
+        self.drain(drain_s)
+        for p in self.parts:
+            p.close(0.0)
+
+    @property
+    def queue_wait(self):
+        from ..utils.lathist import merged
+        return merged(p.queue_wait for p in self.parts)
+
+    @property
+    def request_time(self):
+        from ..utils.lathist import merged
+        return merged(p.request_time for p in self.parts)
+
+    @property
+    def refused(self) -> int:
+        return sum(p.refused for p in self.parts)
+
+    @property
+    def dead_lettered(self) -> int:
+        return sum(p.dead_lettered for p in self.parts)
+
+    def stats(self) -> Dict[str, Any]:
+        per = [p.stats() for p in self.parts]
+        out: Dict[str, Any] = {"shards": self.shards}
+        for k in ("submitted", "acked", "depth", "retries", "signals_ok", "signals_stale", "failed", "refused",
+                  "dead_lettered"):
+            out[k] = sum(int(s.get(k, 0)) for s in per)
+        out["outage_s"] = round(sum(float(s.get("outage_s", 0.0)) for s in per), 3)
+        out["acked_seq"] = self.acked_seq
+        out["last_seq"] = self.last_seq()
+        out["batch_signals"] = all(s.get("batch_signals") for s in per)
+        out["queue_wait_us"] = self.queue_wait.summary_us()
+        out["request_us"] = self.request_time.summary_us()
+        out["per_shard"] = [{k: s[k] for k in ("submitted", "acked", "depth", "retries", "dead_lettered")}
+                            for s in per]
+        return out

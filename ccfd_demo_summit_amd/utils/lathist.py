@@ -59,3 +59,14 @@ class LatHist:
         return {"n": n, "p50": round(min(self.quantile_ns(0.5), mx) / 1e3, 1),
                 "p99": round(min(self.quantile_ns(0.99), mx) / 1e3, 1), "max": round(mx / 1e3, 1),
                 "max_at": round(self.max_at, 3)}
+
+
+def merged(hists) -> LatHist:
+    """One histogram holding the samples of several (a sharded hand-off's per-shard queues)."""
+    m = LatHist()
+    for h in hists:
+        with h._lock:
+            m.h = [a + b for a, b in zip(m.h, h.h)]
+            if h.max_ns > m.max_ns:
+                m.max_ns, m.max_at = h.max_ns, h.max_at
+    return m

@@ -115,6 +115,9 @@ def test_rolled_segments_are_closed_without_leaking_fds(tmp_path, policy):
     for k in range(200):
         s.append_raw("t", 0, _batch([f"v{k:04d}" * 8] * 4))
     if policy == "interval":
+        t0 = time.time()                       # (the flusher may hold the swapped-out list)
+        while not (s._closing or s.fsyncs) and time.time() - t0 < 2:
+            time.sleep(0.01)
         assert s._closing or s.fsyncs          # handed to the flusher, not fsync'd inline
         time.sleep(0.3)
         assert not s._closing                  # ... which fsync'd and closed them

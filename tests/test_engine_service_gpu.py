@@ -244,10 +244,10 @@ def test_engine_service_standard_mode_process_starts_every_row_once(gpu):
     seen = {}
 
     class Recording(ProcessEngine):
-        def start_standard_many(self, items):
+        def start_standard_array(self, items):     # KIE instances/batch, column bodies (round 5)
             for tx, p in zip(items["transaction_id"], items["proba"]):
                 seen.setdefault(int(tx), []).append(("standard", float(p)))
-            return super().start_standard_many(items)
+            return super().start_standard_array(items)
 
         def start_fraud(self, v):
             seen.setdefault(int(v["transaction_id"]), []).append(("fraud", float(v["proba"])))
