@@ -27,6 +27,15 @@ The JSON line states ``topology: "shared"`` (vs bench/e2e.py's per-rank stacks).
 
     python bench/deploy_topology.py --seconds 60 --producers 3 --fmt json         # 1 GPU
     python bench/deploy_topology.py --ranks 4 --rehearsal --seconds 20             # 4 ranks, 1 GPU, gloo
+    python bench/deploy_topology.py --standard-mode process --kie-shards 4 --rate 1.2e6 \
+        --kie-outage-at 25 --kie-kill-shard 1                                      # reference semantics
+
+KIE runs as ``--kie-shards`` processes (process/sharding.py): the hand-off routes starts by
+transaction-id hash and signals by shard-encoded instance id; every shard keeps its own
+journal and the engine one hand-off queue + DLQ per shard.  The KIE checks sum the shards'
+``/rest/stats``.  ``--count`` runs a fixed input (each producer a fixed number of
+transactions) so two runs with the same seed can be compared outcome for outcome
+(``--settle``: wait until no fraud process waits for its customer before reading them).
 """
 from __future__ import annotations
 
@@ -183,10 +192,20 @@ def main(argv=None):
     ap.add_argument("--model", default="mlp", choices=["mlp", "lr", "gbdt"])
     ap.add_argument("--ingest-threads", type=int, default=0, help="native consumers per rank (0 = partitions / ranks)")
     ap.add_argument("--notification-timeout-s", type=float, default=30.0)
+    ap.add_argument("--kie-shards", type=int, default=1, help="KIE shard processes (kie.shards)")
     ap.add_argument("--kie-outage-at", type=float, default=0.0,
-                    help="SIGKILL the KIE process this many seconds into the window (0 = never) ...")
+                    help="SIGKILL a KIE shard process this many seconds into the window (0 = never) ...")
     ap.add_argument("--kie-outage-s", type=float, default=5.0,
                     help="... and restart it from its journal this long after")
+    ap.add_argument("--kie-kill-shard", type=int, default=0, help="which KIE shard --kie-outage-at kills")
+    ap.add_argument("--notifier-kill-at", type=float, default=0.0,
+                    help="SIGKILL the notifier this many seconds into the window (0 = never) ...")
+    ap.add_argument("--notifier-down-s", type=float, default=3.0, help="... and restart it this long after")
+    ap.add_argument("--count", type=int, default=0,
+                    help="transactions per producer (fixed input; 0 = open loop for --seconds)")
+    ap.add_argument("--settle", action="store_true",
+                    help="after the drain, wait until no fraud process waits for its customer (outcomes final)")
+    ap.add_argument("--notifier-seed", type=int, default=0, help="the simulated customers' seed")
     ap.add_argument("--kafka-kill-at", type=float, default=0.0,
                     help="SIGKILL kafka-lite this many seconds into the window (0 = never) ...")
     ap.add_argument("--kafka-down-s", type=float, default=2.0,
@@ -214,11 +233,15 @@ def main(argv=None):
     log_dir.mkdir(parents=True, exist_ok=True)
 
     kafka_port, = free_ports(1, a.kafka_nodes)
-    metrics_port, kie_port, notif_port, master_port = free_ports(4)
+    metrics_port, notif_port, master_port = free_ports(3)
+    kie_port, = free_ports(1, max(1, a.kie_shards))
+    K = max(1, a.kie_shards)
+    kie_ports = [kie_port + k for k in range(K)]
     router_base, = free_ports(1, a.ranks)
     model_base, = free_ports(1, a.ranks)
     brokers = ",".join(f"127.0.0.1:{kafka_port + i}" for i in range(a.kafka_nodes))
-    env = dict(os.environ, PYTHONPATH=str(ROOT), BROKER_URL=brokers, KIE_SERVER_URL=f"http://127.0.0.1:{kie_port}",
+    env = dict(os.environ, PYTHONPATH=str(ROOT), BROKER_URL=brokers,
+               KIE_SERVER_URL=",".join(f"http://127.0.0.1:{p}" for p in kie_ports), CCFD_KIE_SHARDS=str(K),
                CCFD_KAFKA_BACKEND="kafka", CCFD_KAFKA_PARTITIONS=str(a.partitions), CCFD_MODEL=a.model,
                HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
     if a.model == "gbdt":
@@ -227,7 +250,7 @@ def main(argv=None):
     out: Dict = {"metric": "end-to-end tx/s, deployed topology (separate processes)", "topology": "shared",
                  "n_gpus": 1 if a.rehearsal else a.ranks, "ranks": a.ranks, "rehearsal": a.rehearsal,
                  "fmt": a.fmt, "producers": a.producers, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
-                 "model": a.model}
+                 "model": a.model, "kie_shards": K}
     import tempfile
     kdir = tempfile.mkdtemp(prefix="ccfd-kafka-lite-")          # durable logs + committed offsets
     out["kafka_durable"] = {"fsync": a.fsync} if not a.kafka_memory else False
@@ -249,12 +272,16 @@ def main(argv=None):
         # the journal grows ~1 KB per fraud process: keep it out of the log directory
         import tempfile
         jdir = tempfile.mkdtemp(prefix="ccfd-kie-journal-", dir=a.journal_dir)
-        journal = Path(jdir) / "kie-journal.jsonl"
-        kie_cmd = [PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_port), "--journal", str(journal)]
-        procs.append(Proc("kie", kie_cmd, kie_env, log_dir))
-        procs.append(Proc("notifier", [PY, "-m", L, "notifier", "--host", "127.0.0.1", "--port", str(notif_port)],
-                          env, log_dir))
-        wait_port(kie_port, 60)
+        journals = [Path(jdir) / f"kie-journal.shard{k}.jsonl" for k in range(K)]
+        kie_cmds = [[PY, "-m", L, "kie", "--host", "127.0.0.1", "--port", str(kie_ports[k]), "--shard", str(k),
+                     "--journal", str(journals[k])] for k in range(K)]
+        for k in range(K):
+            procs.append(Proc(f"kie{k}", kie_cmds[k], kie_env, log_dir))
+        notif_env = dict(env, CCFD_NOTIFIER_SEED=str(a.notifier_seed))
+        notif_cmd = [PY, "-m", L, "notifier", "--host", "127.0.0.1", "--port", str(notif_port)]
+        procs.append(Proc("notifier", notif_cmd, notif_env, log_dir))
+        for p_ in kie_ports:
+            wait_port(p_, 60)
         eng_env = dict(env)
         eng_env["CCFD_INGEST_THREADS"] = str(a.ingest_threads or max(1, a.partitions // a.ranks))
         eng_env["ROUTER_STANDARD_MODE"] = a.standard_mode
@@ -305,7 +332,8 @@ def main(argv=None):
         per_rate = a.rate / a.producers if a.rate > 0 else 0.0
         for i in range(a.producers):
             prods.append(Proc(f"producer{i}", [PY, "-m", L, "producer", "--fmt", a.fmt, "--batch", str(a.batch),
-                                               "--count", "0", "--seconds", str(a.seconds), "--rate", str(per_rate),
+                                               "--count", str(a.count), "--seconds", str(a.seconds),
+                                               "--rate", str(per_rate),
                                                "--id-base", str((i + 1) << 40), "--seed-offset", str(i * 101)],
                               env, log_dir))
         procs.extend(prods)
@@ -323,7 +351,16 @@ def main(argv=None):
         last_t, last_r = t_w0, r_w0
         outage = {}
         koutage = {}
+        noutage = {}
+        kill_name = f"kie{a.kie_kill_shard}"
         while any(p.alive() for p in prods):
+            if a.notifier_kill_at > 0 and not noutage and time.time() - t_w0 >= a.notifier_kill_at:
+                [p for p in procs if p.name.startswith("notifier")][-1].stop(sig=signal.SIGKILL, wait=5)
+                noutage = {"killed_at_s": round(time.time() - t_w0, 1)}
+            if noutage and "restarted_at_s" not in noutage and \
+                    time.time() - t_w0 >= a.notifier_kill_at + a.notifier_down_s:
+                procs.append(Proc("notifier-restarted", notif_cmd, notif_env, log_dir))
+                noutage["restarted_at_s"] = round(time.time() - t_w0, 1)
             if a.kafka_kill_at > 0 and not koutage and time.time() - t_w0 >= a.kafka_kill_at:
                 kl = [p for p in procs if p.name.startswith("kafka-lite")][-1]
                 kl.stop(sig=signal.SIGKILL, wait=5)            # a crashed broker pod
@@ -335,14 +372,16 @@ def main(argv=None):
                 wait_port(kafka_port, 60)
                 koutage["serving_at_s"] = round(time.time() - t_w0, 1)
             if a.kie_outage_at > 0 and not outage and time.time() - t_w0 >= a.kie_outage_at:
-                kie = [p for p in procs if p.name == "kie"][0]
-                kie.stop(sig=signal.SIGKILL, wait=5)           # a crashed KIE pod
-                outage = {"killed_at_s": round(time.time() - t_w0, 1)}
+                kie = [p for p in procs if p.name == kill_name][0]
+                kie.stop(sig=signal.SIGKILL, wait=5)           # a crashed KIE shard pod
+                outage = {"shard": a.kie_kill_shard, "killed_at_s": round(time.time() - t_w0, 1)}
             if outage and "restarted_at_s" not in outage and \
                     time.time() - t_w0 >= a.kie_outage_at + a.kie_outage_s:
-                procs.append(Proc("kie-restarted", kie_cmd, kie_env, log_dir))   # recovers the journal
+                procs.append(Proc(f"{kill_name}-restarted", kie_cmds[a.kie_kill_shard], kie_env,
+                                  log_dir))                    # recovers its journal (+ outbox)
                 outage["restarted_at_s"] = round(time.time() - t_w0, 1)
-            time.sleep(min(a.sample_s, 0.5) if (a.kie_outage_at > 0 or a.kafka_kill_at > 0) else a.sample_s)
+            crashes = a.kie_outage_at > 0 or a.kafka_kill_at > 0 or a.notifier_kill_at > 0
+            time.sleep(min(a.sample_s, 0.5) if crashes else a.sample_s)
             if time.time() - last_t < a.sample_s:
                 continue
             now = time.time()
@@ -434,24 +473,35 @@ def main(argv=None):
         for qq in (0.5, 0.99):
             v = hist_quantile_le(mt, "seldon_api_engine_server_requests_seconds", qq, {"status": "200"})
             out[f"seldon_server_p{int(qq * 100)}_us_bucketed"] = None if v is None else round(v * 1e6, 1)
-        # ---- KIE: exactly one fraud process per fraud-routed transaction (the async hand-off
-        # may still be delivering the last batches)
+        # ---- KIE: exactly one fraud process per fraud-routed transaction, summed over the
+        # shards (the async hand-off may still be delivering the last batches)
+        def kie_stats():
+            per = [json.loads(http_text(f"http://127.0.0.1:{p_}/rest/stats")) for p_ in kie_ports]
+            tot = {k: sum(int(d.get(k) or 0) for d in per)
+                   for k in ("fraud_started", "duplicates", "standard_started", "standard_duplicates", "active",
+                             "notified", "waiting_customer", "fraud_instances_retained")}
+            tot["outcomes"] = {k: sum(int(d["outcomes"].get(k, 0)) for d in per) for k in per[0]["outcomes"]}
+            tot["per_shard"] = [{k: d.get(k) for k in ("shard", "fraud_started", "standard_started", "duplicates",
+                                                      "standard_duplicates", "notified", "scored_to_started_us")}
+                                for d in per]
+            tot["scored_to_started_us"] = {
+                "n": sum(int((d.get("scored_to_started_us") or {}).get("n", 0)) for d in per),
+                "p50_max_over_shards": max(((d.get("scored_to_started_us") or {}).get("p50") or 0) for d in per),
+                "p99_max_over_shards": max(((d.get("scored_to_started_us") or {}).get("p99") or 0) for d in per)}
+            tot["handoff_attribution"] = [d.get("handoff_attribution") for d in per]
+            return tot
         t_k = time.time()
         while True:
-            stats = json.loads(http_text(f"http://127.0.0.1:{kie_port}/rest/stats"))
+            stats = kie_stats()
             if int(stats["fraud_started"]) >= int(fraud_all) or time.time() - t_k > 30:
                 break
             time.sleep(0.5)
         out["fraud_routed_total"] = fraud_all
-        out["kie"] = stats
         if outage:
-            out["kie_outage"] = dict(outage, recovered=re.findall(r"\[kie\] recovered.*", "".join(
-                p.text() for p in procs if p.name == "kie-restarted")))
-            wait_port(kie_port, 1)
+            out["kie_outage"] = dict(outage, recovered=re.findall(r"\[kie\] (?:recovered|outbox).*", "".join(
+                p.text() for p in procs if p.name == f"{kill_name}-restarted")))
         out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
         out["kie_duplicates"] = stats["duplicates"]
-        out["scored_to_process_started_us"] = stats.get("scored_to_started_us")
-        out["kie_handoff_attribution"] = stats.get("handoff_attribution")
         out["standard_mode"] = a.standard_mode
         if a.standard_mode == "process":
             # every transaction started exactly one process: standard + fraud == incoming
@@ -459,21 +509,37 @@ def main(argv=None):
             while int(stats["standard_started"]) + int(stats["fraud_started"]) < int(rows_all) \
                     and time.time() - t_k < 60:
                 time.sleep(0.5)
-                stats = json.loads(http_text(f"http://127.0.0.1:{kie_port}/rest/stats"))
-            out["kie"] = stats
+                stats = kie_stats()
             out["kie_standard_plus_fraud_equals_incoming"] = \
                 int(stats["standard_started"]) + int(stats["fraud_started"]) == int(rows_all)
             out["kie_standard_duplicates"] = stats.get("standard_duplicates")
+        if a.settle:
+            # outcomes are final once no fraud process waits for its customer (timer or reply)
+            t_k = time.time()
+            while int(stats["waiting_customer"]) > 0 and time.time() - t_k < a.notification_timeout_s + 60:
+                time.sleep(1.0)
+                stats = kie_stats()
+            out["settled"] = int(stats["waiting_customer"]) == 0
+            out["settle_s"] = round(time.time() - t_k, 1)
+        out["kie"] = stats
+        out["scored_to_process_started_us"] = stats["scored_to_started_us"]
+        out["kie_handoff_attribution"] = stats["handoff_attribution"]
         if koutage:
             rec = re.findall(r"\[kafka-lite\] recovered from .*", "".join(
                 p.text() for p in procs if p.name == "kafka-lite-restarted"))
             out["kafka_outage"] = dict(koutage, recovered=rec)
-        dlq = Path(jdir) / "handoff-dlq.rank0.jsonl"
-        out["handoff_dead_lettered"] = sum(1 for _ in open(dlq)) if dlq.exists() else 0
+        if noutage:
+            out["notifier_outage"] = noutage
+        out["handoff_dead_lettered"] = sum(sum(1 for _ in open(f)) for f in Path(jdir).glob("handoff-dlq*.jsonl"))
         try:
             out["notifier"] = json.loads(http_text(f"http://127.0.0.1:{notif_port}/health/ping"))
         except Exception as e:
             out["notifier"] = {"error": repr(e)}
+        # the notification loop: every fraud process notified (the KIE outbox drained) and, once
+        # settled, every reply the customers sent applied exactly once (the rest were stale)
+        out["kie_notified_equals_fraud_started"] = int(stats["notified"]) >= int(stats["fraud_started"])
+        oc = stats["outcomes"]
+        out["customer_replies_applied"] = int(oc.get("approved_by_customer", 0)) + int(oc.get("cancelled", 0))
         # ---- the reference dashboards against everything this deployment serves
         from ccfd_demo_summit_amd.metrics import promql
         series = []
@@ -481,7 +547,8 @@ def main(argv=None):
             series += promql.scrape(f"http://127.0.0.1:{router_base + r}/prometheus", "ccfd-pods")
             series += promql.scrape(f"http://127.0.0.1:{model_base + r}/prometheus", "ccfd-model",
                                     instance=f"engine-{r}:8000")   # k8s: <pod ip>:8000 (operator/render.py)
-        series += promql.scrape(f"http://127.0.0.1:{kie_port}/rest/metrics", "ccfd-pods")
+        for p_ in kie_ports:
+            series += promql.scrape(f"http://127.0.0.1:{p_}/rest/metrics", "ccfd-pods")
         series += promql.scrape(f"http://127.0.0.1:{metrics_port}/metrics", "ccfd-pods")
         fx = json.loads((ROOT / "tests/fixtures/reference_dashboard_exprs.json").read_text())
         exprs = {k: [e["expr"] for e in v] for k, v in fx["dashboards"].items() if k != "SparkMetrics.json"}
@@ -493,15 +560,15 @@ def main(argv=None):
         ok = (out["incoming_equals_produced"] and out["every_partition_exactly_one_rank"]
               and out["kie_fraud_started_equals_routed"] and not rep["unmatched"]
               and out["kie_duplicates"] == 0
-              and out.get("kie_standard_plus_fraud_equals_incoming", True))
+              and out.get("kie_standard_plus_fraud_equals_incoming", True)
+              and out["kie_notified_equals_fraud_started"] and out.get("settled", True))
         out["checks_passed"] = bool(ok)
     finally:
         for p in reversed(procs):
             p.stop(wait=40.0 if p.name == "engine" else 10.0)   # the engine drains on SIGTERM
         if "jdir" in locals():
             import shutil
-            if journal.exists():
-                out["kie_journal_bytes"] = journal.stat().st_size
+            out["kie_journal_bytes"] = sum(j.stat().st_size for j in journals if j.exists())
             shutil.rmtree(jdir, ignore_errors=True)
         import shutil
         try:
@@ -509,6 +576,15 @@ def main(argv=None):
         except OSError:
             pass
         shutil.rmtree(kdir, ignore_errors=True)
+    # the engine ranks' hand-off totals (printed as they stop): signals applied vs stale
+    eng_logs = "".join(p.text() for p in procs if p.name == "engine")
+    hs = [json.loads(m) for m in re.findall(r"hand-off (\{.*\})", eng_logs)]
+    if hs:
+        out["handoff_signals"] = {"ok": sum(h.get("signals_ok", 0) for h in hs),
+                                  "stale": sum(h.get("signals_stale", 0) for h in hs),
+                                  "dead_lettered": sum(h.get("dead_lettered", 0) for h in hs)}
+        if "customer_replies_applied" in out:
+            out["every_reply_signalled_once"] = out["handoff_signals"]["ok"] == out["customer_replies_applied"]
     if a.trace:
         sys.path.insert(0, str(ROOT / "bench"))
         import tail_attribution

@@ -158,6 +158,7 @@ ENV_MAP = {
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),
     "CCFD_KIE_NOTIFICATION_TIMEOUT_S": ("kie", "notification_timeout_s", float),
     "CCFD_KIE_SHARDS": ("kie", "shards", int),
+    "CCFD_NOTIFIER_SEED": ("notifier", "seed", int),
 }
 
 

@@ -84,7 +84,10 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     kafka_port = 9092 + o
     broker = (spec.kafka.bootstrap if not spec.kafka.deploy
               else ",".join(f"{host}:{kafka_port + i}" for i in range(spec.kafka.brokers)))
-    env = {"BROKER_URL": broker, "KIE_SERVER_URL": f"http://{host}:{8090 + o}", "SELDON_URL": f"http://{host}:{8000 + o}",
+    K = max(1, spec.kie.shards)
+    kie_url = ",".join(f"http://{host}:{8090 + o + k}" for k in range(K))     # one per shard
+    env = {"BROKER_URL": broker, "KIE_SERVER_URL": kie_url, "CCFD_KIE_SHARDS": str(K),
+           "SELDON_URL": f"http://{host}:{8000 + o}",
            "CCFD_KAFKA_BACKEND": "kafka", "CCFD_KAFKA_PARTITIONS": str(spec.kafka.partitions),
            "CCFD_MODEL": spec.engine.model, "CCFD_EXEC_MODE": spec.engine.exec_mode,
            "CCFD_OUTPUT_MODE": spec.engine.output_mode, "CCFD_PERSIST_ITEMS": spec.engine.persist_items, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
@@ -108,9 +111,10 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
         svc["seldon"] = (spec.seldon.replicas, lambda r: PY + ["seldon", "--host", host, "--port", str(8000 + o + r)] + w
                          + (["--native", "--workers", str(spec.seldon.workers)] if spec.seldon.native else []))
     if spec.kie.deploy:
-        svc["kie"] = (spec.kie.replicas, lambda r: PY + ["kie", "--host", host, "--port", str(8090 + o + r),
-                                                         "--remote-prediction",
-                                                         "--journal", os.path.join(state, f"kie-journal-{r}.jsonl")])
+        # replica r is KIE shard r (its own port and journal)
+        svc["kie"] = (K, lambda r: PY + ["kie", "--host", host, "--port", str(8090 + o + r), "--shard", str(r),
+                                         "--remote-prediction",
+                                         "--journal", os.path.join(state, f"kie-journal-{r}.jsonl")])
     if spec.notifier.deploy:
         svc["notifier"] = (spec.notifier.replicas, lambda r: PY + ["notifier", "--host", host,
                                                                    "--port", str(8080 + o + r)])

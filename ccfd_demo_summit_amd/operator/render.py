@@ -89,6 +89,9 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
     env["ROUTER_STANDARD_MODE"] = spec.engine.standard_mode
     if spec.engine.handoff_dlq:
         env["CCFD_HANDOFF_DLQ"] = spec.engine.handoff_dlq
+    if spec.kie.shards > 1:            # one URL per shard pod (process/sharding.py kie_urls)
+        env["KIE_SERVER_URL"] = "http://ccd-service-{shard}.ccd-service-shards:8090"
+        env["CCFD_KIE_SHARDS"] = str(spec.kie.shards)
     env.update(spec.env)
     data = dict(env)
     data["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"          # dmabuf IPC for RCCL / cross-process tensors
@@ -144,12 +147,17 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
                                  "ports": [{"name": "rendezvous", "port": RDZV_PORT, "targetPort": RDZV_PORT}]}})
         eng_c = _container(spec, "engine", cmd, ports=ports, gpus=g, probe=("/health/ping", 8091, 120))
         vols = None
+        eng_extra = None
         if spec.engine.handoff_dlq:            # the hand-off dead-letter journal's directory
             import posixpath
             eng_c["volumeMounts"] = [{"name": "handoff-dlq", "mountPath": posixpath.dirname(spec.engine.handoff_dlq)}]
-            vols = [{"name": "handoff-dlq", "emptyDir": {}}]
+            if spec.engine.dlq_storage:        # its offsets are committed: it must outlive the pod
+                eng_extra = {"volumeClaimTemplates": [{"metadata": {"name": "handoff-dlq"}, "spec": {
+                    "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": spec.engine.dlq_storage}}}}]}
+            else:                              # emptyDir: survives container restarts, not pod deletion
+                vols = [{"name": "handoff-dlq", "emptyDir": {}}]
         out.append(_workload("StatefulSet", "ccfd-engine", "ccfd-engine", nodes, [eng_c],
-                             annotations=_scrape("/prometheus", 8091), volumes=vols))
+                             annotations=_scrape("/prometheus", 8091), volumes=vols, extra_spec=eng_extra))
 
     if spec.seldon.deploy:
         cmd = LAUNCH + ["seldon", "--device", "auto"] + weights
@@ -169,17 +177,29 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
         out.append(_service("ccfd-seldon-model", "ccfd-seldon-model", [{"name": "http", "port": 5000, "targetPort": 5000}]))
 
     if spec.kie.deploy:
+        # the KIE tier: kie.shards pods of one StatefulSet; pod ccd-service-k is shard k (the
+        # launcher reads the ordinal from its host name) with its own journal volume, reached
+        # through the headless service as ccd-service-k.ccd-service-shards (process/sharding.py)
+        kie_extra: Dict[str, Any] = {"serviceName": "ccd-service-shards", "podManagementPolicy": "Parallel",
+                                     "updateStrategy": {"type": "RollingUpdate"}}
+        kie_vols = None
+        if spec.kie.storage:
+            kie_extra["volumeClaimTemplates"] = [{"metadata": {"name": "journal"}, "spec": {
+                "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": spec.kie.storage}}}}]
+        else:
+            kie_vols = [{"name": "journal", "emptyDir": {}}]
         out.append(_workload(
-            "Deployment", "ccd-service", "ccd-service", spec.kie.replicas,
+            "StatefulSet", "ccd-service", "ccd-service", spec.kie.shards,
             [dict(_container(spec, "kie", LAUNCH + ["kie", "--journal", "/data/bp-journal.jsonl", "--remote-prediction"],
                              ports=[{"containerPort": 8090, "name": "http"}],
                              env={"SELDON_URL": "ccfd-seldon-model:5000", "SELDON_ENDPOINT": "predict"},
                              probe=("/services/rest/server", 8090, 30)),
                   volumeMounts=[{"name": "journal", "mountPath": "/data"}])],
-            annotations=_scrape("/rest/metrics", 8090),
-            extra_spec={"strategy": {"type": "RollingUpdate", "rollingUpdate": {"maxSurge": "25%", "maxUnavailable": "25%"}}},
-            volumes=[{"name": "journal", "emptyDir": {}}]))
+            annotations=_scrape("/rest/metrics", 8090), extra_spec=kie_extra, volumes=kie_vols))
         out.append(_service("ccd-service", "ccd-service", [{"name": "http", "port": 8090, "targetPort": 8090}]))
+        out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": "ccd-service-shards"},
+                    "spec": {"clusterIP": "None", "selector": {"app": "ccd-service"},
+                             "ports": [{"name": "http", "port": 8090, "targetPort": 8090}]}})
 
     if spec.notifier.deploy:
         out.append(_workload("Deployment", "ccfd-notification-service", "ccfd-notification-service",

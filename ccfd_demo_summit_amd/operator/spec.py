@@ -56,12 +56,22 @@ class EngineSpec:
     standard_mode: str = "count"     # count | process: a standard process per standard-routed
                                      # transaction, as the reference router does (README.md:552)
     handoff_dlq: str = ""            # dead-letter journal of KIE-refused hand-offs ("" = hold + retry)
+    dlq_storage: str = "1Gi"         # the DLQ's volume: a PersistentVolumeClaim of this size per engine pod
+                                     # (its entries' offsets are already committed); "" = emptyDir
 
 
 @dataclass
 class ServiceSpec:
     deploy: bool = True
     replicas: int = 1
+
+
+@dataclass
+class KieSpec(ServiceSpec):
+    shards: int = 1                  # KIE shard pods (process/sharding.py): starts routed by transaction
+                                     # hash, signals / tasks by shard-encoded id; replicas stays 1 (a KIE
+                                     # replica with its own state IS a shard)
+    storage: str = "10Gi"            # each shard's journal volume (PVC); "" = emptyDir
 
 
 @dataclass
@@ -95,7 +105,7 @@ class FraudDetectionSpec:
     engine: EngineSpec = field(default_factory=EngineSpec)
     seldon: SeldonSpec = field(default_factory=SeldonSpec)
     usertask: ServiceSpec = field(default_factory=ServiceSpec)
-    kie: ServiceSpec = field(default_factory=ServiceSpec)
+    kie: KieSpec = field(default_factory=KieSpec)
     notifier: ServiceSpec = field(default_factory=ServiceSpec)
     router: ServiceSpec = field(default_factory=lambda: ServiceSpec(deploy=False))   # compat REST router
     producer: ProducerSpec = field(default_factory=ProducerSpec)
@@ -149,6 +159,11 @@ class FraudDetectionSpec:
                      ("notifier", self.notifier), ("router", self.router)):
             if s.replicas < 0:
                 raise SpecError(f"{n}.replicas must be >= 0")
+        if self.kie.shards < 1:
+            raise SpecError("kie.shards must be >= 1")
+        if self.kie.deploy and self.kie.replicas != 1:
+            raise SpecError("kie.replicas must be 1: KIE instances keep their own state, so scale the tier "
+                            "with kie.shards (each shard owns a hash range of transactions)")
         if self.producer.format not in ("txb1", "json"):
             raise SpecError("producer.format: txb1 | json")
         if self.training.workers < 1:

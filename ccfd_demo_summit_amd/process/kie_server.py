@@ -334,8 +334,8 @@ class KieServer:
                     "standard_started": e.standard_count, "standard_duplicates": e.standard_duplicates,
                     "scored_to_started_us": e.handoff_latency_us(),
                     "handoff_attribution": self.attribution(),
-                    "active": sum(1 for i in e.instances.values()
-                                                                        if i.state.value != "completed"),
+                    "active": sum(1 for i in e.instances.values() if i.state.value != "completed"),
+                    "waiting_customer": sum(1 for i in e.instances.values() if i.state.value == "waiting_customer"),
                     "outcomes": dict(e.outcome_counts), "next_instance_id": None}
         return web.json_response(body)
 

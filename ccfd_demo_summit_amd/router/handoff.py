@@ -57,6 +57,15 @@ TRANSIENT_HTTP = (500, 502, 503, 504, 429, 408)
 MISSING_ROUTE_HTTP = (404, 405, 501)
 
 
+def _ncols(cols: Dict[str, Any]) -> int:
+    return len(next(iter(cols.values()))) if cols else 0
+
+
+def _concat_columns(parts: List[Dict[str, Any]]) -> Dict[str, Any]:
+    import numpy as np
+    return {k: np.concatenate([np.asarray(p[k]) for p in parts]) for k in parts[0]}
+
+
 class HandoffError(RuntimeError):
     """A non-retryable KIE answer (4xx other than 408/429)."""
 
@@ -224,7 +233,8 @@ def deliver(sink, kind: str, payload: Any, batch_signals: bool = True) -> Tuple[
 class KieHandoff:
     def __init__(self, sink, capacity: int = 1 << 21, max_batch: int = 4096, workers: int = 2,
                  backoff_s: float = 0.05, max_backoff_s: float = 2.0, metrics=None,
-                 dlq: Optional[DeadLetterQueue] = None, batch_signals: bool = True):
+                 dlq: Optional[DeadLetterQueue] = None, batch_signals: bool = True,
+                 max_standard_batch: int = 16384):
         """``dlq``: where refused requests go before they are acked (None: a refused request
         is held and retried at ``max_backoff_s`` -- never acked unsent).  ``batch_signals``:
         coalesce response signals into the ``signal/batch`` extension (falls back to the
@@ -236,6 +246,10 @@ class KieHandoff:
         self.dead_lettered = 0
         self.capacity = int(capacity)
         self.max_batch = int(max_batch)
+        # standard starts (one a transaction in process mode, ~1e6/s): queued column batches are
+        # coalesced into requests of up to this many rows -- per-request cost, not per-row
+        # cost, is what the engine's side of the hand-off pays (HTTP + GIL)
+        self.max_standard_batch = max(1, int(max_standard_batch))
         self.backoff_s = float(backoff_s)
         self.max_backoff_s = float(max_backoff_s)
         self.metrics = metrics
@@ -297,9 +311,10 @@ class KieHandoff:
         if n == 0:
             return self.last_seq()
         seq = -1
-        for i in range(0, n, self.max_batch):
-            chunk = {k: v[i:i + self.max_batch] for k, v in cols.items()}
-            seq = self._push("standard", chunk, min(self.max_batch, n - i))
+        step = self.max_standard_batch
+        for i in range(0, n, step):
+            chunk = {k: v[i:i + step] for k, v in cols.items()}
+            seq = self._push("standard", chunk, min(step, n - i))
         return seq
 
     def submit_signal(self, instance_id: int, name: str, payload: Any) -> int:
@@ -391,6 +406,17 @@ class KieHandoff:
                         seqs.append(s2)
                         batch.append(p2)
                     kind, payload = "signals", batch
+                elif kind == "standard":
+                    # coalesce the standard batches queued behind this one (same columns)
+                    parts, rows = [payload], _ncols(payload)
+                    while (self._q and self._q[0][1] == "standard" and set(self._q[0][2]) == set(payload)
+                           and rows + _ncols(self._q[0][2]) <= self.max_standard_batch):
+                        s2, _k, p2, _t = self._q.popleft()
+                        seqs.append(s2)
+                        parts.append(p2)
+                        rows += _ncols(p2)
+                    if len(parts) > 1:
+                        payload = _concat_columns(parts)
             n_items = len(payload) if kind in ("start", "signals") else \
                 (len(next(iter(payload.values()))) if kind == "standard" and payload else 1)
             t_pop = time.monotonic_ns()

@@ -313,3 +313,25 @@ def test_scored_to_started_attribution_on_both_sides(kie):
     s = h.summary_us()
     assert s["n"] == 4 and 0.8 <= s["p50"] <= 2.5 and s["max"] == 1000.0
     ho.close()
+
+
+def test_queued_standard_batches_are_coalesced():
+    """Process mode hands off ~1e6 standard starts a second: batches queued behind a request in
+    flight leave as ONE request (up to max_standard_batch rows), every seq still acked."""
+    gate = threading.Event()
+    calls = []
+
+    class Sink:
+        def start_standard_many(self, cols):
+            gate.wait(5)
+            calls.append(len(cols["transaction_id"]))
+            return list(range(len(cols["transaction_id"])))
+    ho = KieHandoff(Sink(), workers=1, max_standard_batch=5000)
+    seqs = [ho.submit_standard({"transaction_id": np.arange(k * 1000, k * 1000 + 1000),
+                                "proba": np.zeros(1000, np.float32)}) for k in range(12)]
+    time.sleep(0.05)
+    gate.set()
+    assert ho.drain(10) and all(ho.acked(s) for s in seqs)
+    assert sum(calls) == 12_000 and len(calls) <= 4 and max(calls) <= 5000
+    assert ho.stats()["depth"] == 0
+    ho.close()

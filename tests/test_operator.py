@@ -148,7 +148,7 @@ def test_validate_reports_broken_manifests():
     ms = render(load(str(CR)))
     bad = copy.deepcopy(ms)
     by = {(m["kind"], m["metadata"]["name"]): m for m in bad}
-    by[("Deployment", "ccd-service")]["spec"]["selector"]["matchLabels"]["app"] = "nope"
+    by[("StatefulSet", "ccd-service")]["spec"]["selector"]["matchLabels"]["app"] = "nope"
     by[("Service", "modelfull-modelfull")]["spec"]["ports"][0]["targetPort"] = 1234
     eng = by[("StatefulSet", "ccfd-engine")]["spec"]["template"]["spec"]["containers"][0]
     eng["resources"]["limits"]["amd.com/gpu"] = 4
@@ -378,3 +378,29 @@ def test_launcher_forwards_kafka_lite_durability(monkeypatch):
     argv = got["argv"]
     assert argv[argv.index("--data-dir") + 1] == "/x" and argv[argv.index("--fsync") + 1] == "always"
     assert argv[argv.index("--metrics-port") + 1] == "0" and argv[argv.index("--nodes") + 1] == "3"
+
+
+def test_kie_shards_render_a_statefulset_and_shard_urls():
+    """kie.shards: a StatefulSet of shard pods (journal PVC each), a headless service for the
+    per-pod names, KIE_SERVER_URL as a {shard} template; replicas > 1 is refused (an unsharded
+    KIE replica would keep state of its own)."""
+    from ccfd_demo_summit_amd.process.sharding import kie_urls
+    d = _doc()
+    d["spec"]["kie"] = {"deploy": True, "shards": 4}
+    ms = render(parse(d))
+    assert validate(ms) == []
+    by = {(m["kind"], m["metadata"]["name"]): m for m in ms}
+    sts = by[("StatefulSet", "ccd-service")]
+    assert sts["spec"]["replicas"] == 4 and sts["spec"]["serviceName"] == "ccd-service-shards"
+    assert sts["spec"]["volumeClaimTemplates"][0]["metadata"]["name"] == "journal"
+    assert by[("Service", "ccd-service-shards")]["spec"]["clusterIP"] == "None"
+    env = by[("ConfigMap", "ccfd-env")]["data"]
+    assert env["CCFD_KIE_SHARDS"] == "4"
+    assert kie_urls(env["KIE_SERVER_URL"], 4)[3] == "http://ccd-service-3.ccd-service-shards:8090"
+    d["spec"]["kie"] = {"deploy": True, "replicas": 2}
+    with pytest.raises(SpecError, match="kie.shards"):
+        parse(d)
+    # the engine's hand-off DLQ lives on a claim of its own, not an emptyDir
+    eng = by[("StatefulSet", "ccfd-engine")]
+    assert eng["spec"]["volumeClaimTemplates"][0]["metadata"]["name"] == "handoff-dlq"
+    assert "volumes" not in eng["spec"]["template"]["spec"]
