@@ -414,12 +414,18 @@ class Engine {
     // (profiles/r3/latency/).  cfg.persist_items: 2 = pipelined, 1 = claimed, 0 = env
     // CCFD_PERSIST_PIPE (default claimed).  CCFD_PERSIST_ITEM_ROWS = 64 / 128 (default 128).
     persist_pipe = false;
-    if (w64 && cfg.model == CCFD_MODEL_MLP) {
+    // GBDT on G32 / G20 rows: the same pipelined static items, 512-row items, leaves in LDS
+    // (score_gbdt_g32_persist.hip persist_gbdt_pipe_kernel)
+    const bool g32_pipe_ok = g32 && !big_trees && ((long)cfg.gbdt_trees << cfg.gbdt_depth) <= 16384;   // kG32LeafLds
+    if ((w64 && cfg.model == CCFD_MODEL_MLP) || g32_pipe_ok) {
       if (cfg.persist_items == 2) persist_pipe = true;
       else if (cfg.persist_items == 0)
         if (const char* e = std::getenv("CCFD_PERSIST_PIPE")) persist_pipe = std::atoi(e) != 0;
     }
-    if (persist_pipe) {
+    if (persist_pipe && g32) {
+      item_rows = 512;
+      persist_tpw = 2;
+    } else if (persist_pipe) {
       item_rows = 128;
       if (const char* e = std::getenv("CCFD_PERSIST_ITEM_ROWS")) if (std::atoi(e) == 64) item_rows = 64;
       persist_tpw = item_rows / 64;

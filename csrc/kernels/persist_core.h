@@ -107,6 +107,39 @@ __device__ __forceinline__ void persist_claim(const ccfd_persist_args& a, int C,
   s_item = item;
 }
 
+// Static-item pipelines (persist_pipe_kernel, persist_gbdt_pipe_kernel): thread 0 reads item
+// `item`'s descriptor if its micro-batch is already posted (1) or reports that it is not yet (0)
+// without waiting; persist_wait_far waits for it (napping longer when it is >= 2 batches
+// ahead) and returns 1 when the host stopped the kernel instead.
+__device__ __forceinline__ int persist_try_item(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
+                                                unsigned long long item, ccfd_persist_desc& sdesc) {
+  const unsigned long long b = item / (unsigned long long)C;
+  if (posted_cache <= b)
+    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (posted_cache <= b) return 0;
+  persist_read_desc(a, b, sdesc);
+  return 1;
+}
+
+__device__ __forceinline__ int persist_wait_far(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
+                                                unsigned long long item, ccfd_persist_desc& sdesc) {
+  const unsigned long long b = item / (unsigned long long)C;
+  unsigned sleep_n = 1;
+  while (posted_cache <= b) {
+    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (posted_cache > b) break;
+    if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 1;
+    if (b - posted_cache >= 2) {                 // >= 2 batches ahead: ~1 us naps
+      for (int k = 0; k < 4; ++k) __builtin_amdgcn_s_sleep(8);
+    } else {
+      for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
+      sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
+    }
+  }
+  persist_read_desc(a, b, sdesc);
+  return 0;
+}
+
 // Append this wave's fraud-routed rows (fr_lane; m = __ballot(fr_lane)) to the slot's
 // compacted flag list (reservation on the slot's device counter).
 __device__ __forceinline__ void persist_emit_flagged(const ccfd_persist_args& a, const ccfd_persist_desc& sdesc,

@@ -137,6 +137,153 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   }
 }
 
+// Pipelined static items (engine persist_items = pipelined / CCFD_PERSIST_PIPE=1; VERDICT r4
+// item 6).  The claimed kernel above ends every item with its outputs' release, a ticket and
+// then -- only then -- the next claim, descriptor read and first loads: a 512-row G20 item is
+// 10 KB, so at ~18 us of loaded PCIe read latency a workgroup has nothing in flight for a
+// large share of each item (profiles/r4/g20/README.md).  Here, as in persist_pipe_kernel
+// (score_persist.hip) for W64 rows:
+//   * worker w (workgroup 1 + w of W) takes items base + w, base + w + W, ... -- no claim
+//     atomic, the next item is known;
+//   * the next item's rows are issued BEFORE the current item is scored, so its PCIe round
+//     trip overlaps the current item's evaluation, output stores, release and ticket (the
+//     release's vmcnt drain then waits on loads that are needed next anyway);
+//   * leaves in LDS only (kGL = false: BASELINE's 100 x 6 is 25.6 KB); 512-row items (CPW 2).
+// Unlike round 4's rejected two-item CLAIM pipeline, nothing is claimed early: the static
+// assignment already fixes which workgroup scores which item.
+template <int D, bool kR, bool kG20, int CPW>
+__global__ __launch_bounds__(256) void persist_gbdt_pipe_kernel(ccfd_persist_args a) {
+  extern __shared__ __attribute__((aligned(16))) float lv[];
+  __shared__ uint4 xt[kG32Waves][128];
+  __shared__ EpilogueLds epi;
+  __shared__ ccfd_persist_desc sdesc[2];
+  __shared__ int s_pre, s_cmd;                            // rewritten by thread 0 after a barrier only
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int C = a.items_per_batch;
+  if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
+    if (wave == 0) persist_doorbell(a, lane);
+    return;
+  }
+  const char* blob = reinterpret_cast<const char*>(a.blob);
+  const int T = a.gbdt_trees;
+  const float base = *reinterpret_cast<const float*>(blob + 16);
+  const unsigned stamp = (unsigned)*reinterpret_cast<const int*>(blob + 20);
+  const int tdw = ((4 * T * D + 15) & ~15) / 4;
+  const g32_cint_p feat = (g32_cint_p)(blob + kHeader);
+  const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
+  g32_stage_leaves<D>(blob, T, lv, tid, 256);
+  const float* leaves = lv;
+  epi_init(epi);
+  __syncthreads();
+  const unsigned long long W = gridDim.x - 1;
+  unsigned long long item = __hip_atomic_load(&a.dev->work_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                            (unsigned long long)(blockIdx.x - 1);
+  unsigned long long posted_cache = 0;                    // thread 0 only
+
+  unsigned fraud = 0, rows = 0, stale = 0;
+  unsigned long long psum = 0;
+  auto k7 = [&](const ccfd_persist_desc& d, unsigned long long it) __attribute__((always_inline)) {
+    if (it % (unsigned long long)C == 0)                  // K7: micro-batch start
+      __hip_atomic_store(&a.dev->tstart[d.seq % (unsigned long long)a.ring], wall_clock64(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto issue = [&](const ccfd_persist_desc& d, unsigned long long it, G32Row (&r)[CPW]) __attribute__((always_inline)) {
+    const int c0 = (int)(it % (unsigned long long)C) * (kG32Waves * CPW) + wave;
+    const unsigned char* xb = reinterpret_cast<const unsigned char*>(d.x);
+#pragma unroll
+    for (int k = 0; k < CPW; ++k) {
+      const int chunk = c0 + kG32Waves * k;
+      if (chunk * kG32Rows < d.n) gx_fetch<kG20>(xb, d.n, chunk, lane, r[k]);
+    }
+  };
+  auto score = [&](const ccfd_persist_desc& d, unsigned long long it, G32Row (&r)[CPW]) __attribute__((always_inline)) {
+    const int slot = (int)(d.seq % (unsigned long long)a.ring);
+    const int n = d.n;
+    const int c0 = (int)(it % (unsigned long long)C) * (kG32Waves * CPW) + wave;
+#pragma unroll
+    for (int k = 0; k < CPW; ++k) {
+      const int chunk = c0 + kG32Waves * k;
+      if (chunk * kG32Rows >= n) break;                   // wave-uniform
+      gx_rows<kG20>(xt[wave], lane, r[k]);
+      unsigned b0[kF];
+      const unsigned meta = gx_lift<kG20>(r[k], b0);
+      float acc[1];
+      g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
+      const int row = chunk * kG32Rows + lane;
+      const bool valid = row < n;
+      const bool fresh = ((meta >> 8) & 0xffu) == stamp;
+      const float p = fresh ? sigmoid(base + acc[0]) : __builtin_nanf("");
+      bool fr;
+      if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
+      else fr = valid && fresh && (p >= a.threshold);
+      if (valid) {
+        if (d.proba) st_g(d.proba + row, p);
+        if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
+        if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
+        atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
+      }
+      const unsigned long long m = __ballot(fr);
+      fraud += __popcll(m);
+      rows += __popcll(__ballot(valid));
+      stale += __popcll(__ballot(valid && !fresh));
+      persist_emit_flagged(a, d, slot, m, fr, row, lane);
+    }
+    psum = wave_sum_u64(psum);
+    if (lane == 0 && rows) {
+      atomicAdd(&epi.fraud, fraud);
+      atomicAdd(&epi.rows, rows);
+      atomicAdd(&epi.psum_e6, psum);
+      unsigned long long* cnt = a.counters[d.epoch & 1];
+      if (stale && cnt) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)stale);
+    }
+    fraud = rows = stale = 0;
+    psum = 0;
+    persist_item_done(a, epi, d, slot, C, tid);           // barriers, release, ticket
+  };
+  // score `it` from (dc, rc) while item it + W is fetched into (dn, rn); true = host stopped
+  auto stage = [&](ccfd_persist_desc& dc, G32Row (&rc)[CPW], ccfd_persist_desc& dn, G32Row (&rn)[CPW],
+                   unsigned long long it) __attribute__((always_inline)) {
+    const unsigned long long nx = it + W;
+    if (tid == 0) {
+      s_pre = persist_try_item(a, C, posted_cache, nx, dn);
+      if (s_pre) k7(dn, nx);
+    }
+    __syncthreads();
+    const bool pre = s_pre != 0;
+    const ccfd_persist_desc d = dc;                       // registers: no LDS reads in the epilogue
+    if (pre) issue(dn, nx, rn);                           // next item's rows in flight now
+    score(d, it, rc);                                     // ends with barriers (persist_item_done)
+    if (!pre) {
+      if (tid == 0) {
+        s_cmd = persist_wait_far(a, C, posted_cache, nx, dn);
+        if (!s_cmd) k7(dn, nx);
+      }
+      __syncthreads();
+      if (s_cmd) return true;
+      issue(dn, nx, rn);
+    }
+    return false;
+  };
+
+  if (tid == 0) {
+    s_cmd = persist_wait_far(a, C, posted_cache, item, sdesc[0]);
+    if (!s_cmd) k7(sdesc[0], item);
+  }
+  __syncthreads();
+  if (s_cmd) return;
+  G32Row ra[CPW], rb[CPW];
+  issue(sdesc[0], item, ra);
+  for (;;) {
+    if (stage(sdesc[0], ra, sdesc[1], rb, item)) break;
+    item += W;
+    if (stage(sdesc[1], rb, sdesc[0], ra, item)) break;
+    item += W;
+  }
+}
+
 template <int D, bool kG20>
 static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream_t s) {
   ccfd_persist_args a = a0;
@@ -147,6 +294,12 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   if (g32_env("CCFD_G32_INFLIGHT", 0, 0, 1) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
+  if (a.flags & CCFD_ARG_PIPE_ITEMS) {                    // pipelined static 512-row items
+    if (gl || a.tiles_per_wave != 2 || grid < 2) return -2;
+    if (a.rules) hipLaunchKernelGGL((persist_gbdt_pipe_kernel<D, true, kG20, 2>), dim3(grid), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((persist_gbdt_pipe_kernel<D, false, kG20, 2>), dim3(grid), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   if (gl) {
     if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, true, kG20>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, true, kG20>), dim3(grid), dim3(256), 0, s, a);

@@ -244,35 +244,6 @@ __global__ __launch_bounds__(256) void persist_kernel(ccfd_persist_args a) {
 //   * a worker waiting for a batch several batches ahead of the posted count sleeps longer,
 //     so idle workers do not hammer the device `posted` word.
 // T = tiles per wave per item (1: 64-row items, 2: 128-row items).
-__device__ __forceinline__ int persist_try_item(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
-                                                unsigned long long item, ccfd_persist_desc& sdesc) {
-  const unsigned long long b = item / (unsigned long long)C;
-  if (posted_cache <= b)
-    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (posted_cache <= b) return 0;
-  persist_read_desc(a, b, sdesc);
-  return 1;
-}
-
-__device__ __forceinline__ int persist_wait_far(const ccfd_persist_args& a, int C, unsigned long long& posted_cache,
-                                                unsigned long long item, ccfd_persist_desc& sdesc) {
-  const unsigned long long b = item / (unsigned long long)C;
-  unsigned sleep_n = 1;
-  while (posted_cache <= b) {
-    posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (posted_cache > b) break;
-    if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 1;
-    if (b - posted_cache >= 2) {                 // >= 2 batches ahead: ~1 us naps
-      for (int k = 0; k < 4; ++k) __builtin_amdgcn_s_sleep(8);
-    } else {
-      for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
-      sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
-    }
-  }
-  persist_read_desc(a, b, sdesc);
-  return 0;
-}
-
 template <bool kR, int T>
 __global__ __launch_bounds__(256) void persist_pipe_kernel(ccfd_persist_args a) {
   static_assert(T == 1 || T == 2, "64- or 128-row items");
