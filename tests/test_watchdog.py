@@ -83,7 +83,8 @@ def test_bench_watchdog_fires_on_stalled_rank(gpu):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "2",
                         "--watchdog-s", "8", "--batches-per-step", "16", "--log-rows", str(1 << 18),
                         "--probe-ms", "0", "--host-probe-s", "0", "--precision-rows", "0",
-                        "--encode-probe-rows", "0", "--no-unloaded-probe", "--no-f32-probe"],
+                        "--encode-probe-rows", "0", "--no-unloaded-probe", "--no-f32-probe",
+                        "--diagnostic"],                 # fault injection: a labelled diagnostic run
                        capture_output=True, text=True, env=env, timeout=110)
     assert r.returncode == EXIT_STALLED, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     line = [ln for ln in r.stderr.splitlines() if ln.startswith("[watchdog]")][0]
