@@ -243,7 +243,8 @@ def main(argv=None):
     env = dict(os.environ, PYTHONPATH=str(ROOT), BROKER_URL=brokers,
                KIE_SERVER_URL=",".join(f"http://127.0.0.1:{p}" for p in kie_ports), CCFD_KIE_SHARDS=str(K),
                CCFD_KAFKA_BACKEND="kafka", CCFD_KAFKA_PARTITIONS=str(a.partitions), CCFD_MODEL=a.model,
-               HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+               HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1",
+               PYTHONFAULTHANDLER="1")          # a native crash prints every thread's Python stack
     if a.model == "gbdt":
         env.setdefault("CCFD_WIRE", "auto")
     procs: List[Proc] = []
@@ -392,6 +393,8 @@ def main(argv=None):
                 lag = None
             samples.append({"t_s": round(now - t_w0, 1), "tx_s": round((r_now - last_r) / (now - last_t), 1),
                             "lag_msgs": lag})
+            print(f"[deploy] {time.strftime('%H:%M:%S')} sample {samples[-1]} kie_outage {outage} "
+                  f"kafka_outage {koutage} notifier_outage {noutage}", file=sys.stderr, flush=True)
             last_t, last_r = now, r_now
         t_w1 = time.time()
         r_w1, _, _ = scrape_all()
