@@ -302,3 +302,75 @@ def test_engine_service_standard_mode_process_starts_every_row_once(gpu):
         kie.close()
         kb.close()
         lite.stop()
+
+
+def test_process_mode_sharded_kie_back_pressure_holds_and_resumes(gpu):
+    """Round 5: process mode over a 2-shard KIE tier whose shard 1 refuses
+    connections for 3 s, with a hand-off capacity small enough that the engine HOLDS (the
+    native serving thread pauses, the scored ring and the ingest rings back up) and resumes
+    several times.  Afterwards every row started exactly one process on the shard its id hashes
+    to, the committed lag is 0, and nothing was lost or repeated."""
+    from ccfd_demo_summit_amd.contracts import TxBatch
+    from ccfd_demo_summit_amd.ingest.kafka_lite import KafkaLiteServer
+    from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+    from ccfd_demo_summit_amd.launch.engine_service import EngineService, EngineServiceConfig
+    from ccfd_demo_summit_amd.metrics import MetricsHub
+    from ccfd_demo_summit_amd.ops.kernels import DeviceModel
+    from ccfd_demo_summit_amd.parallel import DistContext
+    from ccfd_demo_summit_amd.process import ProcessEngine
+    from ccfd_demo_summit_amd.process.kie_server import KieClient
+    from ccfd_demo_summit_amd.process.sharding import ShardedKieClient, shard_of_tx
+    from ccfd_demo_summit_amd.router import Router, RuleSet
+    from ccfd_demo_summit_amd.router.handoff import ShardedHandoff
+    from tests.helpers.faulty_proxy import FaultyProxy
+    from tests.helpers.kie_thread import KieThread
+
+    n = 80_000
+    X, _ = generate(n, seed=21)
+    ids = np.arange(1, n + 1, dtype=np.uint64) + np.uint64(11 << 36)
+    m = build_model("mlp", seed=4, X_ref=X, calibrate_rate=0.01)
+    lite = KafkaLiteServer("127.0.0.1", 0, default_partitions=2).start_in_thread()
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("odh-demo", 2)
+    engines = [ProcessEngine(notification_timeout_s=1e9, shard=k, shards=2) for k in range(2)]
+    kies = [KieThread(e) for e in engines]
+    px = FaultyProxy(kies[1].port)
+    clients = [KieClient(f"http://127.0.0.1:{kies[0].port}", timeout_s=2.0), KieClient(px.url, timeout_s=1.0)]
+    ho = ShardedHandoff(clients, capacity=6000, workers=2, backoff_s=0.02, max_backoff_s=0.2)
+    hub = MetricsHub()
+    router = Router(RuleSet.threshold(0.5), ShardedKieClient(clients), hub.router, standard_mode="process",
+                    handoff=ho)
+    svc = EngineService(DistContext(0, 1, 0, gpu, "none"), DeviceModel(m, gpu, wire=True), kb, router,
+                        EngineServiceConfig(batch=4096, depth=8, streams=2, ring_rows=1 << 15, flush_us=200,
+                                            reduce_period_ms=2.0, standard_mode="process",
+                                            scored_capacity=1 << 14)).start()
+    try:
+        assert svc.exec_mode == "persistent" and svc.native is not None
+        px.set_mode("refuse")
+        for k in range(0, n, 2000):
+            kb.produce("odh-demo", TxBatch(ids=ids[k:k + 2000], customer=(ids[k:k + 2000] % 999).astype(np.uint32),
+                                           features=X[k:k + 2000]).encode(), partition=(k // 2000) % 2)
+        t0 = time.time()
+        while time.time() - t0 < 3.0:
+            svc.step()                                        # never raises while shard 1 is away
+        assert svc.held and svc.hold_events >= 1 and svc.rows_scored < n
+        px.set_mode("pass")
+        t0 = time.time()
+        while (svc.rows_scored < n or ho.depth() or svc.commits_pending()
+               or kb.lag("ccfd-engine", "odh-demo")) and time.time() - t0 < 90:
+            svc.step()
+        assert svc.rows_scored == n and kb.lag("ccfd-engine", "odh-demo") == 0 and ho.depth() == 0
+        tx = ids.astype(np.int64)
+        for k, e in enumerate(engines):
+            assert e.standard_count + e.fraud_count == int((shard_of_tx(tx, 2) == k).sum())
+            assert e.duplicates == 0 and e.standard_duplicates == 0
+        nf = int(hub.router.tx_outgoing.labels(type="fraud")._value.get())
+        assert sum(e.fraud_count for e in engines) == nf
+    finally:
+        svc.stop()
+        ho.close(drain_s=1.0)
+        px.close()
+        for k_ in kies:
+            k_.close()
+        kb.close()
+        lite.stop()
