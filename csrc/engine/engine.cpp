@@ -1304,8 +1304,11 @@ struct ApiLock {
 
 extern "C" {
 
+int ccfd_crash_report_install();          // crash_report.cpp
+
 void* ccfd_engine_create(const ccfd_engine_config* cfg) {
   if (!cfg) { set_error("null config"); return nullptr; }
+  ccfd_crash_report_install();              // a native fault prints its stack (then faulthandler's)
   auto* e = new Engine();
   if (e->init(*cfg) != 0) { delete e; return nullptr; }
   return e;

@@ -345,3 +345,20 @@ def test_corrupt_gzip_batch_stalls_partition(L):
         assert kc.committable() == {}
     finally:
         kc.close()
+
+
+def test_native_crash_report_prints_the_native_stack():
+    """A fault in any thread prints the native stack (module + offset per frame) and then
+    chains to Python's faulthandler (engine.cpp installs it at ccfd_engine_create)."""
+    import pathlib
+    import subprocess
+    import sys
+    code = ("import ctypes, faulthandler, os, signal; faulthandler.enable(); "
+            "from ccfd_demo_summit_amd.ops.build import lib_path; L = ctypes.CDLL(str(lib_path(''))); "
+            "assert L.ccfd_crash_report_install() == 1; assert L.ccfd_crash_report_install() == 0; "
+            "ctypes.string_at(8)")                     # a real SIGSEGV (read of address 8)
+    root = pathlib.Path(__file__).resolve().parents[1]
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=str(root))
+    assert r.returncode != 0
+    assert "[ccfd] native crash: signal 11 at address 0x0000000000000008" in r.stderr, r.stderr[-2000:]
+    assert "native stack (module+offset)" in r.stderr and "Fatal Python error" in r.stderr
