@@ -432,6 +432,13 @@ def cmd_engine(a, cfg):
                 for r in _safe(lambda: notif.poll(max_records=10_000), []):
                     router.on_notification_sent(r.value)
                 _safe(notif.commit)
+    except BaseException as e:
+        if not isinstance(e, SystemExit):     # the cause, before the shutdown path runs
+            import traceback
+            print(f"[engine] rank {ctx.rank} loop failed:", file=sys.stderr, flush=True)
+            traceback.print_exc()
+            sys.stderr.flush()
+        raise
     finally:
         svc.stop()                    # drains; a resident persistent kernel halts here
         handoff.close(drain_s=5.0)

@@ -83,17 +83,26 @@ void handler(int sig, siginfo_t* si, void* uc) {
 
 }  // namespace
 
+// Returns how many signals it (re)installed: a runtime loaded later (HSA / HIP, torch) may
+// have put its own handler in front; calling again puts this one back in front of it.
 extern "C" int ccfd_crash_report_install() {
+  static std::atomic<int> busy{0};
   int expect = 0;
-  if (!g_installed.compare_exchange_strong(expect, 1)) return 0;
-  backtrace(g_frames, 2);                  // load the unwinder now, not inside the handler
+  if (!busy.compare_exchange_strong(expect, 1)) return 0;
+  if (!g_installed.exchange(1)) backtrace(g_frames, 2);   // load the unwinder now, not in the handler
+  int n = 0;
   for (int i = 0; i < kNSigs; ++i) {
+    struct sigaction cur;
+    if (sigaction(kSigs[i], nullptr, &cur) == 0 && (cur.sa_flags & SA_SIGINFO) && cur.sa_sigaction == handler)
+      continue;                            // already in front
     struct sigaction sa;
     std::memset(&sa, 0, sizeof(sa));
     sa.sa_sigaction = handler;
     sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
     sigemptyset(&sa.sa_mask);
     sigaction(kSigs[i], &sa, &g_prev[i]);
+    ++n;
   }
-  return 1;
+  busy.store(0);
+  return n;
 }

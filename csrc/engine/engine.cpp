@@ -530,7 +530,14 @@ class Engine {
       persist_counted = false;
       return;
     }
-    for (auto& s : slots) if (s.busy) wait_done(s);
+    // a completed batch the host never retired (scored-ring back-pressure, a held hand-off,
+    // an exception before the drain) stays busy: wait for it here and mark it retired -- its
+    // completion record lives in pctl, which is freed below (the slot loop in ~Engine must
+    // not read it afterwards)
+    for (auto& s : slots) {
+      if (s.busy) wait_done(s);
+      if (s.use_flag) { s.busy = false; s.use_flag = false; s.done_ptr = nullptr; }
+    }
     persist_halt();
     // teardown: nothing useful can be done about a failed release, so results are dropped
     (void)hipStreamDestroy(pstream);
@@ -1317,6 +1324,7 @@ void* ccfd_engine_create(const ccfd_engine_config* cfg) {
 void ccfd_engine_destroy(void* eng) {
   auto* e = static_cast<Engine*>(eng);
   if (!e) return;
+  ccfd_crash_report_install();              // in front of any handler a runtime added since
   e->serve_stop_join();
   delete e;
 }

@@ -355,7 +355,7 @@ def test_native_crash_report_prints_the_native_stack():
     import sys
     code = ("import ctypes, faulthandler, os, signal; faulthandler.enable(); "
             "from ccfd_demo_summit_amd.ops.build import lib_path; L = ctypes.CDLL(str(lib_path(''))); "
-            "assert L.ccfd_crash_report_install() == 1; assert L.ccfd_crash_report_install() == 0; "
+            "assert L.ccfd_crash_report_install() == 5; assert L.ccfd_crash_report_install() == 0; "
             "ctypes.string_at(8)")                     # a real SIGSEGV (read of address 8)
     root = pathlib.Path(__file__).resolve().parents[1]
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=str(root))
