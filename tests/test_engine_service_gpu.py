@@ -347,13 +347,17 @@ def test_process_mode_sharded_kie_back_pressure_holds_and_resumes(gpu):
     try:
         assert svc.exec_mode == "persistent" and svc.native is not None
         px.set_mode("refuse")
-        for k in range(0, n, 2000):
+        held_rows = []
+        for k in range(0, n, 2000):                           # arriving in waves while shard 1 is away
             kb.produce("odh-demo", TxBatch(ids=ids[k:k + 2000], customer=(ids[k:k + 2000] % 999).astype(np.uint32),
                                            features=X[k:k + 2000]).encode(), partition=(k // 2000) % 2)
-        t0 = time.time()
-        while time.time() - t0 < 3.0:
-            svc.step()                                        # never raises while shard 1 is away
-        assert svc.held and svc.hold_events >= 1 and svc.rows_scored < n
+            t0 = time.time()
+            while time.time() - t0 < 0.075:
+                svc.step()                                    # never raises
+                if svc.held:
+                    held_rows.append(svc.rows_scored)
+        assert svc.hold_events >= 1 and held_rows
+        assert held_rows[-1] < n                              # scoring paused while held
         px.set_mode("pass")
         t0 = time.time()
         while (svc.rows_scored < n or ho.depth() or svc.commits_pending()
