@@ -119,11 +119,14 @@ class BatchStore:
         return None
 
     # ------------------------------------------------------------------ idempotent producers
-    def init_producer_id(self) -> Tuple[int, int]:
-        """InitProducerId (non-transactional): a fresh producer id, epoch 0."""
+    def init_producer_id(self, node: int = 0, stride: int = 1) -> Tuple[int, int]:
+        """InitProducerId (non-transactional): a fresh producer id, epoch 0.  A replicated
+        cluster's brokers hand out disjoint ids: ``node + stride * k``."""
         with self._lock:
             pid = self._next_pid
-            self._next_pid += 1
+            if stride > 1:
+                pid += (node - pid) % stride
+            self._next_pid = pid + 1
             self._persist_producer_ids()
             return pid, 0
 
@@ -226,6 +229,46 @@ class BatchStore:
                 self._apply_retention(topic, partition, L)
             return base0, nrec, self._appended(L)
 
+    def append_replica(self, topic: str, partition: int, data) -> Tuple[int, Optional[int]]:
+        """A follower's append (replicated kafka-lite, ingest/kafka_replica.py): batches fetched
+        from the partition leader, base offsets already stamped by it, appended at exactly
+        those offsets (a batch this log already holds is skipped; a gap is an error).  The
+        idempotent-producer state is tracked as on the leader, so a follower that becomes leader
+        deduplicates retried batches.  Returns (batches appended, write ticket or None)."""
+        batches = split_batches(data, False)            # the leader verified them
+        with self._lock:
+            L = self._log(topic, partition)
+            first_new = len(L.batches)
+            now = time.time()
+            for last, _count, _attrs, mv in batches:
+                base = struct.unpack_from(">q", mv, 0)[0]
+                if base + last + 1 <= L.end:
+                    continue                            # already replicated (a re-fetch)
+                if base != L.end:
+                    raise BrokerError(f"{topic}[{partition}]: replica gap (log end {L.end}, batch {base})")
+                b = mv if not mv.readonly else bytearray(mv)
+                self._track_producer(topic, partition, b, base)
+                L.bases.append(base)
+                L.batches.append(b)
+                L.ts.append(now)
+                L.end = base + last + 1
+                L.nbytes += len(b)
+            n_new = len(L.batches) - first_new
+            if n_new:
+                self._persist_appended(topic, partition, L, first_new)
+            if self.retention_batches is not None and len(L.batches) > self.retention_batches:
+                drop = len(L.batches) - self.retention_batches
+                L.nbytes -= sum(len(x) for x in L.batches[:drop])
+                del L.bases[:drop], L.batches[:drop], L.ts[:drop]
+                L.begin = L.bases[0]
+                self._apply_retention(topic, partition, L)
+            return n_new, self._appended(L) if n_new else None
+
+    def log_end(self, topic: str, partition: int) -> int:
+        """The next offset this log assigns (LEO), written or not."""
+        with self._lock:
+            return self._log(topic, partition).end
+
     def produce(self, topic: str, value: bytes, key: Optional[bytes] = None,
                 partition: Optional[int] = None, headers: Tuple = ()) -> Tuple[int, int]:
         from .kafka_wire import encode_record_batch
@@ -241,18 +284,21 @@ class BatchStore:
         least one batch, like Kafka, so an oversized batch is never stuck)."""
         return b"".join(self.fetch_parts(topic, partition, offset, max_bytes))
 
-    def fetch_parts(self, topic: str, partition: int, offset: int, max_bytes: int) -> list:
+    def fetch_parts(self, topic: str, partition: int, offset: int, max_bytes: int,
+                    upto: Optional[int] = None) -> list:
         """``fetch_raw`` as the list of stored batches themselves (no copy; a fetch response
-        is written to the socket from them)."""
+        is written to the socket from them).  ``upto``: serve only batches below this offset
+        (a replicated leader's consumers see up to the high watermark)."""
         with self._lock:
             L = self._log(topic, partition)
-            if offset >= L.visible or not L.batches:
+            lim = L.visible if upto is None else min(L.visible, upto)
+            if offset >= lim or not L.batches:
                 return []
             i = max(0, bisect.bisect_right(L.bases, offset) - 1)
             out, size = [], 0
             while i < len(L.batches):
                 b = L.batches[i]
-                if L.bases[i] >= L.visible or (out and size + len(b) > max_bytes):
+                if L.bases[i] >= lim or (out and size + len(b) > max_bytes):
                     break
                 out.append(b)
                 size += len(b)

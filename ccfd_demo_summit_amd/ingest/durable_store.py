@@ -74,7 +74,10 @@ class _Segment:
 class DurableBatchStore(BatchStore):
     def __init__(self, data_dir: str, default_partitions: int = 1, retention_batches: Optional[int] = None,
                  verify_crc: bool = True, fsync: str = "interval", fsync_interval_s: float = 1.0,
-                 segment_bytes: int = 256 << 20):
+                 segment_bytes: int = 256 << 20, truncate_to: Optional[Dict[Tuple[str, int], int]] = None):
+        """``truncate_to``: (topic, partition) -> offset: recovery drops every batch at or above
+        it (a replicated broker restarting truncates to its checkpointed high watermark, so its
+        log is a prefix of the current leader's -- ingest/kafka_replica.py)."""
         if fsync not in FSYNC_POLICIES:
             raise ValueError(f"fsync policy {fsync!r}: one of {FSYNC_POLICIES}")
         super().__init__(default_partitions=default_partitions, retention_batches=retention_batches,
@@ -92,6 +95,8 @@ class DurableBatchStore(BatchStore):
         self._closing: List[int] = []
         self._off_fd = -1
         self.recovered: Dict[str, object] = {}
+        self._limits = dict(truncate_to or {})
+        self.truncated_batches = 0
         self.bytes_written = 0
         self.fsyncs = 0
         # write-behind: appends land in memory under the store lock and are queued; ONE writer
@@ -250,6 +255,19 @@ class DurableBatchStore(BatchStore):
         bases = sorted(int(f[:-4]) for f in os.listdir(d) if f.endswith(".log"))
         L = self._log(topic, p)
         nb = nr = torn = 0
+        lim = self._limits.get((topic, p))
+        if lim is not None:
+            # segments that start at or past the limit go entirely (the first one is kept, cut
+            # to empty, so the partition's offsets continue from the limit)
+            keep = [b for b in bases if b < lim] or bases[:1]
+            for b in bases:
+                if b not in keep:
+                    for ext in (".log", ".idx"):
+                        try:
+                            os.unlink(os.path.join(d, _seg_name(b)) + ext)
+                        except OSError:
+                            pass
+            bases = keep
         for k, base in enumerate(bases):
             path = os.path.join(d, _seg_name(base))
             size = os.path.getsize(path + ".log")
@@ -288,9 +306,19 @@ class DurableBatchStore(BatchStore):
                     batches.append((struct.unpack_from(">q", mv, pos)[0], pos, 12 + blen))
                     pos += 12 + blen
                 good_end = pos
+                was_cut = False
+                if lim is not None:             # replicated: cut at the checkpointed HW
+                    cut = [i for i, (bo, _ps, _ln) in enumerate(batches) if bo >= lim]
+                    if cut:
+                        self.truncated_batches += len(batches) - cut[0]
+                        good_end = batches[cut[0]][1]
+                        del batches[cut[0]:]
+                        was_cut = True
                 del mv
-            if good_end < size:                 # torn tail: a crash mid-write
-                torn += 1
+            else:
+                was_cut = False
+            if good_end < size:                 # torn tail (a crash mid-write), or the HW cut
+                torn += 0 if was_cut else 1
                 if mm is not None:
                     mm.close()
                     mm = None
@@ -328,6 +356,8 @@ class DurableBatchStore(BatchStore):
                 self._segs[(topic, p)].pop()
                 act = self._open_segment(topic, p, base)
                 act.nbatches, act.last_end = seg.nbatches, seg.last_end
+        if lim is not None and not L.batches and lim > 0:
+            L.begin = L.end = lim               # everything was past the cut: continue at it
         if self.retention_batches is not None and len(L.batches) > self.retention_batches:
             drop = len(L.batches) - self.retention_batches
             L.nbytes -= sum(len(x) for x in L.batches[:drop])

@@ -41,8 +41,8 @@ from typing import Dict, List, Optional, Set, Tuple
 
 from .batch_store import BatchStore, InvalidBatch, OutOfOrderSequence
 from .broker import BrokerError
-from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE, ERR_OUT_OF_ORDER_SEQUENCE,
-                         ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
+from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_COORDINATOR, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE,
+                         ERR_OUT_OF_ORDER_SEQUENCE, ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
 
 NODE_ID = 1
 ERR_ILLEGAL_GENERATION, ERR_UNKNOWN_MEMBER, ERR_REBALANCE_IN_PROGRESS = 22, 25, 27
@@ -97,11 +97,24 @@ class ClusterState:
         # ticket order; the last ticket the store's writer reported written
         self.produce_waiters: collections.deque = collections.deque()
         self.written = 0
+        # replicated multi-process mode (ingest/kafka_replica.py): the controller's view
+        # replaces the in-process node table and leadership
+        self.replica = None
 
     def live(self) -> List[int]:
+        if self.replica is not None:
+            return self.replica.live_nodes()
         return sorted(n for n, v in self.nodes.items() if v[2])
 
+    def address(self, node: int) -> Tuple[str, int]:
+        if self.replica is not None:
+            return self.replica.nodes[node]
+        host, port, _ = self.nodes[node]
+        return host, port
+
     def leader(self, topic: str, partition: int) -> int:
+        if self.replica is not None:
+            return self.replica.leader(topic, partition)
         with self.lock:
             key = (topic, partition)
             if key not in self.leaders:
@@ -132,14 +145,25 @@ class ClusterState:
                     self.leader_moves += 1
 
     def under_replicated(self) -> int:
+        if self.replica is not None:
+            return self.replica.under_replicated()
         dead = len(self.nodes) - len(self.live())
         return self.partition_count() if dead else 0
 
     def offline(self) -> int:
+        if self.replica is not None:
+            return 0                            # reported by the controller alone (as in Kafka)
         return sum(1 for t, n in self.store.topics().items() for p in range(n) if self.leader(t, p) < 0)
 
     def partition_count(self) -> int:
+        if self.replica is not None:
+            return len(self.replica.hosted())
         return sum(self.store.topics().values())
+
+    def leader_count(self) -> int:
+        if self.replica is not None:
+            return self.replica.led()
+        return self.partition_count() - self.offline()
 
 
 class _GcTimer:
@@ -251,8 +275,7 @@ class BrokerMetrics:
         class _Gauges:
             def collect(self_):
                 for name, v in (("kafka_server_replicamanager_partitioncount", cl.partition_count()),
-                                ("kafka_server_replicamanager_leadercount",
-                                 cl.partition_count() - cl.offline()),
+                                ("kafka_server_replicamanager_leadercount", cl.leader_count()),
                                 ("kafka_server_replicamanager_underreplicatedpartitions", cl.under_replicated()),
                                 ("kafka_controller_kafkacontroller_offlinepartitionscount", cl.offline()),
                                 ("kafka_controller_kafkacontroller_activebrokercount", len(cl.live()))):
@@ -434,6 +457,10 @@ class KafkaLiteServer:
         self.port = self._server.sockets[0].getsockname()[1]
         self.cluster.nodes[self.node_id] = [self.advertise, self.port, True]
         self._reaper = asyncio.get_running_loop().create_task(self._reap_sessions())
+        rep = self.cluster.replica
+        if rep is not None:                     # replicated: join the controller's cluster
+            rep.port, rep.server = self.port, self
+            await rep.start()
 
     def start_in_thread(self) -> "KafkaLiteServer":
         ready = threading.Event()
@@ -514,6 +541,8 @@ class KafkaLiteServer:
                 f.set_result(None)
         for tp in tps:
             self._wake_fetches(tp)
+        if cl.replica is not None:
+            cl.replica.on_written(tps)          # the leader's LEO moved: maybe the HW too
 
     def _wake_fetches(self, tp) -> None:
         ws = self.cluster.fetch_waiters.pop(tp, None)
@@ -523,12 +552,20 @@ class KafkaLiteServer:
                     f.set_result(None)
 
     async def _produce_later(self, body: bytes, ticket: int) -> bytes:
+        await self._written_ticket(ticket)
+        return body
+
+    async def _written_ticket(self, ticket: int) -> None:
+        """Until the durable store's writer has written ``ticket``."""
+        if not ticket or ticket <= self.cluster.written:
+            return
         fut = asyncio.get_running_loop().create_future()
         self.cluster.produce_waiters.append((ticket, fut))
         await fut
-        return body
 
     def _topic(self, name: str) -> bool:
+        if self.cluster.replica is not None:    # topics exist once the controller created them
+            return name in self.cluster.replica.topics
         if name in self.store.topics():
             return True
         if self.auto_create:
@@ -555,10 +592,11 @@ class KafkaLiteServer:
 
     def _api_3(self, r: Reader) -> bytes:                   # Metadata v1
         topics = r.array(lambda x: x.string())
-        names = sorted(self.store.topics()) if topics is None else topics
         cl = self.cluster
+        rep = cl.replica
+        names = sorted(rep.topics if rep is not None else self.store.topics()) if topics is None else topics
         live = cl.live()
-        w = Writer().array([(n, cl.nodes[n][0], cl.nodes[n][1]) for n in live],
+        w = Writer().array([(n,) + tuple(cl.address(n)) for n in live],
                            lambda w_, b: w_.i32(b[0]).string(b[1]).i32(b[2]).string(None))
         w.i32(live[0] if live else -1)                      # controller id
         replicas = sorted(cl.nodes)
@@ -567,12 +605,14 @@ class KafkaLiteServer:
             if not self._topic(name):
                 w_.i16(ERR_UNKNOWN_TOPIC).string(name).i8(0).array([], None)
                 return
-            n = self.store.partitions(name)
+            n = rep.topics[name] if rep is not None else self.store.partitions(name)
 
             def part(w2, p):
                 lead = cl.leader(name, p)
+                reps = rep.replicas(name, p) if rep is not None else replicas
+                isr = rep.isr(name, p) if rep is not None else live
                 w2.i16(ERR_NONE if lead >= 0 else 5).i32(p).i32(lead)
-                w2.array(replicas, lambda w3, x: w3.i32(x)).array(live, lambda w3, x: w3.i32(x))
+                w2.array(reps, lambda w3, x: w3.i32(x)).array(isr, lambda w3, x: w3.i32(x))
             w_.i16(ERR_NONE).string(name).i8(0).array(range(n), part)
         w.array(names, topic)
         return w.build()
@@ -585,6 +625,22 @@ class KafkaLiteServer:
             return name, n
         reqs = r.array(req)
         r.i32()
+        build = lambda res: Writer().array(res, lambda w, t: w.string(t[0]).i16(t[1])).build()
+        rep = self.cluster.replica
+        if rep is not None:                                 # created by the controller
+            async def later():
+                res = []
+                for name, n in reqs:
+                    if name in rep.topics:
+                        res.append((name, ERR_TOPIC_EXISTS))
+                        continue
+                    try:
+                        await rep.create_topic(name, max(1, n))
+                        res.append((name, ERR_NONE))
+                    except Exception:                       # noqa: BLE001 -- controller away
+                        res.append((name, 5))
+                return build(res)
+            return later()
         res = []
         for name, n in reqs:
             if name in self.store.topics():
@@ -592,13 +648,16 @@ class KafkaLiteServer:
             else:
                 self.store.create_topic(name, max(1, n))
                 res.append((name, ERR_NONE))
-        return Writer().array(res, lambda w, t: w.string(t[0]).i16(t[1])).build()
+        return build(res)
 
     def _api_0(self, r: Reader) -> bytes:                   # Produce v3: batches stored verbatim
-        r.string(); r.i16(); r.i32()
+        r.string()
+        acks, timeout_ms = r.i16(), r.i32()
         data = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.view_()))))
         resp = []
         ticket = 0
+        rep = self.cluster.replica
+        waits = []                                          # acks=all: (topic, p, log end, response entry)
         for topic, parts in data:
             pr = []
             self._topic(topic)
@@ -611,7 +670,9 @@ class KafkaLiteServer:
                     continue
                 try:
                     base, nrec, t = self.store.append_raw_nowait(topic, p, rb or b"")
-                    pr.append((p, ERR_NONE, base))
+                    pr.append([p, ERR_NONE, base])
+                    if rep is not None and acks == -1:
+                        waits.append((topic, p, self.store.log_end(topic, p), pr[-1]))
                     if t:
                         ticket = max(ticket, t)     # answered (and fetchable) once written
                     else:
@@ -628,31 +689,57 @@ class KafkaLiteServer:
                     pr.append((p, ERR_KAFKA_STORAGE_ERROR, -1))
                     self.metrics.failed_produce.labels(topic, "Kafka").inc()
             resp.append((topic, pr))
-        w = Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1)))
-        body = w.i32(0).build()
+        build = lambda: Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
+            t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(q[2]).i64(-1))).i32(0).build()
+        if waits:
+            return self._produce_replicated(build, ticket, waits, timeout_ms)
+        body = build()
         if ticket and ticket > self.cluster.written:
             return self._produce_later(body, ticket)
         return body
 
+    async def _produce_replicated(self, build, ticket: int, waits, timeout_ms: int) -> bytes:
+        """acks=all on a replicated leader: answered once written here AND the partition's high
+        watermark covers the batch (every in-sync replica has it).  Leadership lost meanwhile,
+        or the timeout: NOT_LEADER, so the producer refreshes metadata and retries (its
+        idempotent sequence makes a retry of a replicated batch a no-op)."""
+        await self._written_ticket(ticket)
+        rep = self.cluster.replica
+        deadline = time.monotonic() + max(0.1, timeout_ms / 1000.0)
+        for topic, p, end, entry in waits:
+            ok = False
+            try:
+                ok = await asyncio.wait_for(rep.wait_hw(topic, p, end), max(0.0, deadline - time.monotonic()))
+            except asyncio.TimeoutError:
+                ok = False
+            if not ok:
+                entry[1] = ERR_NOT_LEADER
+                self.metrics.failed_produce.labels(topic, "Kafka").inc()
+        return build()
+
     def _api_22(self, r: Reader) -> bytes:                  # InitProducerId v0 (idempotence only)
         r.string(); r.i32()
-        pid, epoch = self.store.init_producer_id()
+        if self.cluster.replica is not None:                # disjoint ids per broker
+            from .kafka_replica import PID_STRIDE
+            pid, epoch = self.store.init_producer_id(self.node_id, PID_STRIDE)
+        else:
+            pid, epoch = self.store.init_producer_id()
         return Writer().i32(0).i16(ERR_NONE).i64(pid).i16(epoch).build()
 
     def _api_1(self, r: Reader):                            # Fetch v4: stored batches, sliced
-        r.i32()
+        replica_id = r.i32()
         max_wait_ms, min_bytes, max_bytes = r.i32(), r.i32(), r.i32()
         r.i8()
         reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.i32()))))
-        parts, n, ok = self._fetch_parts(reqs, max_bytes)
+        parts, n, ok = self._fetch_parts(reqs, max_bytes, replica_id)
         if n == 0 and ok and max_wait_ms > 0 and min_bytes > 0:
             # Kafka's long poll: hold the request until a requested partition gets data or
             # max_wait passes.  Without it every idle consumer thread re-fetched every few
             # hundred microseconds, thousands of empty fetches a second through this event loop
-            return self._fetch_later(reqs, max_bytes, max_wait_ms)
+            return self._fetch_later(reqs, max_bytes, max_wait_ms, replica_id)
         return parts
 
-    async def _fetch_later(self, reqs, max_bytes: int, max_wait_ms: int):
+    async def _fetch_later(self, reqs, max_bytes: int, max_wait_ms: int, replica_id: int = -1):
         fut = asyncio.get_running_loop().create_future()
         tps = [(t, p) for t, ps in reqs for p, _o, _m in ps]
         waiters = self.cluster.fetch_waiters
@@ -670,13 +757,16 @@ class KafkaLiteServer:
                     ws.discard(fut)
                     if not ws:
                         waiters.pop(tp, None)
-        return self._fetch_parts(reqs, max_bytes)[0]
+        return self._fetch_parts(reqs, max_bytes, replica_id)[0]
 
-    def _fetch_parts(self, reqs, max_bytes: int):
-        """(response parts, record bytes in them, no partition errored)."""
+    def _fetch_parts(self, reqs, max_bytes: int, replica_id: int = -1):
+        """(response parts, record bytes in them, no partition errored).  Replicated mode: a
+        follower's fetch (``replica_id`` >= 0) reports its log end to the leader and reads up to
+        the leader's written end; a consumer reads up to the high watermark."""
         resp = []
         ok = True
         budget = max_bytes
+        rep = self.cluster.replica
         for topic, parts in reqs:
             pr = []
             self.metrics.topic(topic)
@@ -688,12 +778,20 @@ class KafkaLiteServer:
                     ok = False
                     continue
                 hw = self.store.end_offset(topic, p)
-                if off < self.store.begin_offset(topic, p) or off > hw:
+                upto = None
+                limit = hw
+                if rep is not None:
+                    if replica_id >= 0:
+                        rep.on_replica_fetch(replica_id, topic, p, off)
+                    else:
+                        upto = limit = rep.high_watermark(topic, p)
+                    hw = rep.high_watermark(topic, p)
+                if off < self.store.begin_offset(topic, p) or off > limit:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     ok = False
                     continue
-                rb = self.store.fetch_parts(topic, p, off, max(1, min(pmax, budget))) if budget > 0 else []
+                rb = self.store.fetch_parts(topic, p, off, max(1, min(pmax, budget)), upto) if budget > 0 else []
                 n = sum(len(b) for b in rb)
                 budget -= n
                 pr.append((p, ERR_NONE, hw, rb))
@@ -725,7 +823,12 @@ class KafkaLiteServer:
                 if err:
                     pr.append((p, err, -1))
                     continue
-                off = self.store.begin_offset(topic, p) if ts == -2 else self.store.end_offset(topic, p)
+                if ts == -2:
+                    off = self.store.begin_offset(topic, p)
+                elif self.cluster.replica is not None:     # consumers see up to the HW
+                    off = self.cluster.replica.high_watermark(topic, p)
+                else:
+                    off = self.store.end_offset(topic, p)
                 pr.append((p, ERR_NONE, off))
             resp.append((topic, pr))
         return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
@@ -734,23 +837,56 @@ class KafkaLiteServer:
     def _api_10(self, r: Reader) -> bytes:                  # FindCoordinator v0
         r.string()
         live = self.cluster.live()
-        node = live[0] if live else self.node_id             # group state is shared: any node works
-        host, port, _ = self.cluster.nodes[node]
+        # one process: group state is shared, any node works; replicated: the lowest live broker
+        # coordinates (offsets are kept by the controller, so a new coordinator has them)
+        node = live[0] if live else self.node_id
+        if self.cluster.replica is not None and node not in self.cluster.replica.nodes:
+            return Writer().i16(ERR_NOT_COORDINATOR).i32(-1).string("").i32(-1).build()
+        host, port = self.cluster.address(node)
         return Writer().i16(ERR_NONE).i32(node).string(host).i32(port).build()
 
     def _api_8(self, r: Reader) -> bytes:                   # OffsetCommit v2
         group = r.string(); r.i32(); r.string(); r.i64()
         reqs = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i64(), y.string()))))
+        build = lambda resp: Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
+            t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]))).build()
+        rep = self.cluster.replica
+        if rep is not None:                                 # durable at the controller first
+            async def later():
+                err = ERR_NONE
+                try:
+                    await rep.commit_offsets(group, [(t, p, off) for t, parts in reqs for p, off, _m in parts])
+                except Exception:                           # noqa: BLE001 -- controller away
+                    err = ERR_NOT_COORDINATOR
+                for t, parts in reqs:
+                    for p, off, _m in parts:
+                        if err == ERR_NONE:
+                            self.store.commit(group, t, p, off)      # this coordinator's cache
+                return build([(t, [(p, err) for p, _o, _m in parts]) for t, parts in reqs])
+            return later()
         resp = []
         for topic, parts in reqs:
             for p, off, _m in parts:
                 self.store.commit(group, topic, p, off)
             resp.append((topic, [(p, ERR_NONE) for p, _o, _m in parts]))
-        return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]))).build()
+        return build(resp)
 
     def _api_9(self, r: Reader) -> bytes:                   # OffsetFetch v1
         group = r.string()
         reqs = r.array(lambda x: (x.string(), x.array(lambda y: y.i32())))
+        build = lambda resp, err=ERR_NONE: Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
+            t[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).string(None).i16(err))).build()
+        rep = self.cluster.replica
+        if rep is not None:
+            async def later():
+                tps = [(t, p) for t, parts in reqs for p in parts]
+                try:
+                    offs = await rep.fetch_offsets(group, tps)
+                except Exception:                           # noqa: BLE001 -- controller away
+                    return build([(t, [(p, -1) for p in parts]) for t, parts in reqs], ERR_NOT_COORDINATOR)
+                got = dict(zip(tps, offs))
+                return build([(t, [(p, int(got[(t, p)])) for p in parts]) for t, parts in reqs])
+            return later()
         resp = []
         for topic, parts in reqs:
             pr = []
@@ -758,8 +894,7 @@ class KafkaLiteServer:
                 c = self.store.committed(group, topic, p)
                 pr.append((p, -1 if c is None else c))
             resp.append((topic, pr))
-        return Writer().array(resp, lambda w_, t: w_.string(t[0]).array(
-            t[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).string(None).i16(ERR_NONE))).build()
+        return build(resp)
 
     # ------------------------------------------------------------------ group coordinator
     # JoinGroup v1 / SyncGroup v0 / Heartbeat v0 / LeaveGroup v0 (client: ingest/kafka_group.py)
@@ -977,6 +1112,53 @@ class KafkaLiteCluster:
             self.store.close()
 
 
+class ReplicatedBroker:
+    """One broker PROCESS of a replicated kafka-lite cluster (ingest/kafka_replica.py): its own
+    durable log (cut to its checkpointed high watermark on start), one listener, a replica
+    manager that heartbeats the controller, follows the partitions other brokers lead and
+    serves the ones it leads."""
+
+    def __init__(self, node_id: int, controller: str, host: str = "127.0.0.1", port: int = 0,
+                 data_dir: Optional[str] = None, fsync: str = "interval", advertise: Optional[str] = None,
+                 retention_batches: Optional[int] = None, hb_s: float = 0.1, replica_lag_s: float = 5.0):
+        from .kafka_replica import ReplicaManager, load_checkpoint
+        if data_dir:
+            from .durable_store import DurableBatchStore
+            self.store = DurableBatchStore(data_dir, retention_batches=retention_batches, fsync=fsync,
+                                           truncate_to=load_checkpoint(data_dir))
+        else:
+            self.store = BatchStore(retention_batches=retention_batches)
+        self.state = ClusterState(self.store)
+        self.server = KafkaLiteServer(host, port, store=self.store, auto_create=False, node_id=node_id,
+                                      cluster=self.state, advertise=advertise)
+        self.state.replica = ReplicaManager(node_id, advertise or host, port, controller, self.store,
+                                            server=self.server, hb_s=hb_s, replica_lag_s=replica_lag_s,
+                                            data_dir=data_dir)
+        self.metrics = self.server.metrics
+
+    @property
+    def replica(self):
+        return self.state.replica
+
+    @property
+    def bootstrap(self) -> str:
+        return self.server.bootstrap
+
+    async def start(self):
+        await self.server.start()
+
+    def start_in_thread(self) -> "ReplicatedBroker":
+        self.server.start_in_thread()
+        return self
+
+    def stop(self):
+        if self.server._loop is not None:
+            asyncio.run_coroutine_threadsafe(self.state.replica.close(), self.server._loop).result(5)
+        self.server.stop()
+        if hasattr(self.store, "close"):
+            self.store.close()
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default="0.0.0.0")
@@ -993,7 +1175,13 @@ def main(argv=None):
     ap.add_argument("--fsync", default="interval", choices=["always", "interval", "never"],
                     help="--data-dir flush policy: before every answer, every second in the background, "
                          "or left to the OS (a killed broker process loses nothing in any mode)")
+    ap.add_argument("--node-id", type=int, default=0,
+                    help="replicated mode: this broker's node id (one broker per process; needs --controller)")
+    ap.add_argument("--controller", default=None,
+                    help="replicated mode: the kafka-lite controller's URL (ingest/kafka_controller.py)")
     a = ap.parse_args(argv)
+    if a.controller:
+        return _main_replicated(a)
     # the durable store's writer thread hands every written ticket back to this event loop,
     # and takes the GIL back after each write: at CPython's 5 ms switch interval a busy loop
     # kept it waiting for the GIL, so acknowledgements and fetch visibility lagged the writes
@@ -1027,6 +1215,42 @@ def main(argv=None):
         from ..utils.gcpolicy import tune_for_service
         print(f"[kafka-lite] {a.nodes} node(s) listening on {cl.bootstrap_all}; gc: {tune_for_service()}",
               flush=True)
+        await asyncio.Event().wait()
+    asyncio.run(run())
+
+
+def _main_replicated(a):
+    """One broker process of a replicated cluster (--node-id N --controller URL)."""
+    if a.node_id <= 0:
+        raise SystemExit("kafka-lite: replicated mode needs --node-id >= 1")
+    sys.setswitchinterval(0.0005)
+    from .kafka_wire import warm_native
+    print(f"[kafka-lite] native codecs loaded in {warm_native():.2f} s", flush=True)
+    br = ReplicatedBroker(a.node_id, a.controller, a.host, a.port, data_dir=a.data_dir, fsync=a.fsync,
+                          advertise=a.advertise, retention_batches=a.retention_batches or None)
+    if a.data_dir:
+        print(f"[kafka-lite] node {a.node_id} recovered from {a.data_dir}: {json.dumps(br.store.recovered)} "
+              f"(cut to the checkpointed HW: {getattr(br.store, 'truncated_batches', 0)} batches)", flush=True)
+
+    def store_failed():
+        print(f"[kafka-lite] FATAL: log write failed ({getattr(br.store, '_werr', None)!r}); exiting",
+              file=sys.stderr, flush=True)
+        asyncio.get_running_loop().call_later(0.2, os._exit, 75)
+    br.state.on_store_failure = store_failed
+
+    async def run():
+        await br.start()
+        if a.metrics_port:
+            from aiohttp import web
+            app = web.Application()
+            app.router.add_get("/metrics", lambda _r: web.Response(
+                body=br.metrics.expose(), headers={"Content-Type": "text/plain; version=0.0.4"}))
+            runner = web.AppRunner(app)
+            await runner.setup()
+            await web.TCPSite(runner, a.host, a.metrics_port).start()
+        from ..utils.gcpolicy import tune_for_service
+        print(f"[kafka-lite] node {a.node_id} listening on {br.bootstrap} (controller {a.controller}); "
+              f"gc: {tune_for_service()}", flush=True)
         await asyncio.Event().wait()
     asyncio.run(run())
 

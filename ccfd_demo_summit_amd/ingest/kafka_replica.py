@@ -1,0 +1,401 @@
+"""Broker side of replicated, multi-process kafka-lite.
+
+Each broker process owns ONE durable log (ingest/durable_store.py) and leads the partitions
+the controller (ingest/kafka_controller.py) gives it; the other replicas of a partition are
+followers that replicate by FETCHING from the leader, as Kafka's replica fetchers do:
+
+* **followers** run one fetcher per leader broker: a Kafka Fetch v4 with ``replica_id`` =
+  their node id, from their log end offset (LEO), appended verbatim at the leader's offsets
+  (``BatchStore.append_replica``) and written before the next fetch -- the fetch offset IS the
+  follower's durable LEO, which is what the leader counts;
+* **the leader** tracks each follower's LEO from its fetches; the partition's high watermark
+  (HW) is the minimum LEO over the in-sync replicas (ISR).  Consumers only see offsets below
+  the HW; a produce with ``acks=all`` (-1) is answered once the HW covers it, so an
+  acknowledged record is on every ISR member;
+* **ISR**: the leader proposes (in its next heartbeat) to drop a follower that has not caught
+  up for ``replica_lag_s`` and to re-admit one that has caught up; the controller applies
+  proposals of the current leader epoch only;
+* **fail-over**: the controller elects the live ISR member with the highest LEO, so every
+  other replica's log is a prefix of the new leader's.  A broker that restarts cuts its logs
+  to its checkpointed HW (``replication.json``, every 200 ms) before rejoining -- except where it
+  was the sole ISR member (its log is then the authority) -- so its log is again a prefix;
+* producer ids are per-broker disjoint (``node + 1024 k``) and the idempotent-producer state
+  is replicated with the batches, so a batch retried against a new leader is stored once.
+
+The under-replicated gauge (``kafka_server_replicamanager_underreplicatedpartitions``, the
+reference Kafka dashboard's panel, deploy/grafana/Kafka.json:271) counts the partitions this
+broker leads whose ISR is smaller than their replica set.
+"""
+from __future__ import annotations
+
+import asyncio
+import heapq
+import json
+import os
+import struct
+import time
+import uuid
+from typing import Any, Dict, List, Optional, Set, Tuple
+
+from .broker import BrokerError
+from .kafka_controller import tp_key, tp_split
+
+TP = Tuple[str, int]
+PID_STRIDE = 1024                      # producer ids: node + PID_STRIDE * k (disjoint per broker)
+FETCH, FETCH_V = 1, 4
+
+
+def load_checkpoint(data_dir: Optional[str]) -> Dict[TP, int]:
+    """The recovery cut of a restarting broker: (topic, partition) -> checkpointed HW, for the
+    partitions where it was NOT the sole in-sync replica."""
+    if not data_dir:
+        return {}
+    p = os.path.join(data_dir, "replication.json")
+    if not os.path.exists(p):
+        return {}
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, json.JSONDecodeError):
+        return {}
+    sole = set(d.get("sole", []))
+    return {tp_split(k): int(v) for k, v in d.get("hw", {}).items() if k not in sole}
+
+
+class ReplicaManager:
+    def __init__(self, node_id: int, advertise_host: str, port: int, controller_url: str, store, server=None,
+                 hb_s: float = 0.1, replica_lag_s: float = 5.0, data_dir: Optional[str] = None):
+        self.node_id = int(node_id)
+        self.host = advertise_host
+        self.port = int(port)
+        self.controller = controller_url.rstrip("/")
+        self.store = store
+        self.server = server                      # KafkaLiteServer: fetch wake-ups
+        self.hb_s = float(hb_s)
+        self.replica_lag_s = float(replica_lag_s)
+        self.data_dir = data_dir
+        self.incarnation = uuid.uuid4().hex
+        self.meta_epoch = -1
+        self.parts: Dict[TP, Dict[str, Any]] = {}
+        self.nodes: Dict[int, Tuple[str, int]] = {}
+        self.topics: Dict[str, int] = {}
+        self.hw: Dict[TP, int] = {}
+        self.fol: Dict[TP, Dict[int, List[float]]] = {}     # leader: follower -> [leo, fetched at, caught up at]
+        self._acks: Dict[TP, list] = {}                      # leader: heap of (end offset, seq, future)
+        self._ack_seq = 0
+        self._isr_prop: Dict[TP, Dict[str, Any]] = {}
+        self._fetchers: Dict[int, asyncio.Task] = {}
+        self._tasks: List[asyncio.Task] = []
+        self._session = None
+        self.ready = None                                    # asyncio.Event: first metadata applied
+        self.controller_ok = False
+        self.replica_fetches = 0
+        self.replicated_bytes = 0
+        self.hb_failures = 0
+        self._lead_since: Dict[TP, float] = {}
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self) -> None:
+        import aiohttp
+        self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=5))
+        self.ready = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        self._tasks = [loop.create_task(self._hb_loop()), loop.create_task(self._isr_loop()),
+                       loop.create_task(self._ckpt_loop())]
+
+    async def close(self) -> None:
+        for t in self._tasks + list(self._fetchers.values()):
+            t.cancel()
+        if self._session is not None:
+            await self._session.close()
+
+    # ------------------------------------------------------------------ metadata view
+    def leader(self, topic: str, p: int) -> int:
+        st = self.parts.get((topic, p))
+        return -1 if st is None else int(st["leader"])
+
+    def is_leader(self, topic: str, p: int) -> bool:
+        return self.leader(topic, p) == self.node_id
+
+    def isr(self, topic: str, p: int) -> List[int]:
+        st = self.parts.get((topic, p))
+        return [] if st is None else list(st["isr"])
+
+    def replicas(self, topic: str, p: int) -> List[int]:
+        st = self.parts.get((topic, p))
+        return [] if st is None else list(st["replicas"])
+
+    def live_nodes(self) -> List[int]:
+        return sorted(self.nodes)
+
+    def under_replicated(self) -> int:
+        return sum(1 for tp, st in self.parts.items()
+                   if st["leader"] == self.node_id and len(st["isr"]) < len(st["replicas"]))
+
+    def led(self) -> int:
+        return sum(1 for st in self.parts.values() if st["leader"] == self.node_id)
+
+    def hosted(self) -> List[TP]:
+        return [tp for tp, st in self.parts.items() if self.node_id in st["replicas"]]
+
+    def high_watermark(self, topic: str, p: int) -> int:
+        return self.hw.get((topic, p), 0)
+
+    def _leo(self, tp: TP) -> int:
+        try:
+            return self.store.end_offset(*tp)          # written (visible) end
+        except BrokerError:
+            return 0
+
+    async def create_topic(self, name: str, partitions: int) -> None:
+        async with self._session.post(f"{self.controller}/topics", json={"name": name, "partitions": int(partitions)}) as r:
+            d = await r.json()
+        self._apply(d)
+
+    async def commit_offsets(self, group: str, entries) -> None:
+        async with self._session.post(f"{self.controller}/offsets/commit",
+                                      json={"group": group, "offsets": [list(e) for e in entries]}) as r:
+            if r.status != 200:
+                raise BrokerError(f"controller commit: HTTP {r.status}")
+
+    async def fetch_offsets(self, group: str, tps) -> List[int]:
+        async with self._session.post(f"{self.controller}/offsets/fetch",
+                                      json={"group": group, "tps": [list(t) for t in tps]}) as r:
+            return (await r.json())["offsets"]
+
+    # ------------------------------------------------------------------ heartbeat
+    async def _hb_loop(self) -> None:
+        while True:
+            body = {"node": self.node_id, "host": self.host, "port": self.port, "incarnation": self.incarnation,
+                    "seen_epoch": self.meta_epoch,
+                    "leos": {tp_key(*tp): self._leo(tp) for tp in self.hosted()},
+                    "isr_changes": list(self._isr_prop.values())}
+            try:
+                async with self._session.post(f"{self.controller}/heartbeat", json=body) as r:
+                    d = await r.json()
+                self._isr_prop.clear()
+                self.controller_ok = True
+                if "parts" in d:
+                    self._apply(d)
+                elif self.ready is not None and not self.ready.is_set() and self.meta_epoch >= 0:
+                    self.ready.set()
+            except Exception:                               # noqa: BLE001 -- controller away
+                self.controller_ok = False
+                self.hb_failures += 1
+            await asyncio.sleep(self.hb_s)
+
+    def _apply(self, d: Dict[str, Any]) -> None:
+        """New metadata from the controller: leadership / ISR / topics / brokers."""
+        if "parts" not in d:
+            return
+        self.meta_epoch = int(d["meta_epoch"])
+        self.nodes = {int(k): (v[0], int(v[1])) for k, v in d["nodes"].items()}
+        for name, n in d["topics"].items():
+            if name not in self.topics:
+                self.store.create_topic(name, int(n))
+            self.topics[name] = int(n)
+        old = self.parts
+        self.parts = {tp_split(k): v for k, v in d["parts"].items()}
+        for tp, st in self.parts.items():
+            was = old.get(tp)
+            if st["leader"] == self.node_id and (was is None or was["leader"] != self.node_id
+                                                 or was["epoch"] != st["epoch"]):
+                # leader from now: followers' LEOs are unknown until they fetch
+                self.fol[tp] = {}
+                self.hw.setdefault(tp, 0)
+                self._lead_since[tp] = time.monotonic()
+            elif st["leader"] != self.node_id:
+                self.fol.pop(tp, None)
+                self._fail_acks(tp)
+            if st["leader"] == self.node_id:
+                self._advance_hw(tp)
+        self._reconcile_fetchers()
+        if self.ready is not None:
+            self.ready.set()
+
+    # ------------------------------------------------------------------ leader side
+    def on_replica_fetch(self, node: int, topic: str, p: int, offset: int) -> None:
+        tp = (topic, p)
+        if not self.is_leader(topic, p):
+            return
+        now = time.monotonic()
+        rec = self.fol.setdefault(tp, {}).setdefault(node, [0, now, 0.0])
+        rec[0], rec[1] = offset, now
+        if offset >= self._leo(tp):
+            rec[2] = now                                 # caught up with the leader
+        self._advance_hw(tp)
+
+    def on_written(self, tps) -> None:
+        """The leader's own write advanced its LEO."""
+        for tp in tps:
+            if self.is_leader(*tp):
+                self._advance_hw(tp)
+
+    def _advance_hw(self, tp: TP) -> None:
+        st = self.parts.get(tp)
+        if st is None or st["leader"] != self.node_id:
+            return
+        leos = [self._leo(tp)]
+        fol = self.fol.get(tp, {})
+        for n in st["isr"]:
+            if n != self.node_id:
+                leos.append(int(fol[n][0]) if n in fol else 0)
+        new = min(leos)
+        if new > self.hw.get(tp, 0):
+            self.hw[tp] = new
+            h = self._acks.get(tp)
+            while h and h[0][0] <= new:
+                _e, _s, fut = heapq.heappop(h)
+                if not fut.done():
+                    fut.set_result(True)
+            if self.server is not None:
+                self.server._wake_fetches(tp)
+
+    def wait_hw(self, topic: str, p: int, end: int) -> "asyncio.Future":
+        """Resolves once the HW reaches ``end`` (acks=all); fails if leadership is lost."""
+        fut = asyncio.get_running_loop().create_future()
+        tp = (topic, p)
+        if self.hw.get(tp, 0) >= end:
+            fut.set_result(True)
+            return fut
+        self._ack_seq += 1
+        heapq.heappush(self._acks.setdefault(tp, []), (end, self._ack_seq, fut))
+        return fut
+
+    def _fail_acks(self, tp: TP) -> None:
+        for _e, _s, fut in self._acks.pop(tp, []):
+            if not fut.done():
+                fut.set_result(False)                    # answered NOT_LEADER: the producer retries
+
+    async def _isr_loop(self) -> None:
+        while True:
+            await asyncio.sleep(0.2)
+            now = time.monotonic()
+            for tp, st in list(self.parts.items()):
+                if st["leader"] != self.node_id:
+                    continue
+                isr = list(st["isr"])
+                fol = self.fol.get(tp, {})
+                leo = self._leo(tp)
+                new = list(isr)
+                for n in st["replicas"]:
+                    if n == self.node_id:
+                        continue
+                    rec = fol.get(n)
+                    if n in isr:
+                        lagging = rec is None or (rec[0] < leo and now - max(rec[2], 0.0) > self.replica_lag_s) \
+                            or now - rec[1] > self.replica_lag_s
+                        if lagging and (rec is not None or now - self._since(tp) > self.replica_lag_s):
+                            new.remove(n)
+                    elif rec is not None and rec[0] >= self.hw.get(tp, 0) and now - rec[1] < 1.0 \
+                            and now - rec[2] < 1.0 and n in self.nodes:
+                        new.append(n)
+                if sorted(new) != sorted(isr):
+                    self._isr_prop[tp] = {"tp": tp_key(*tp), "epoch": st["epoch"], "isr": new}
+
+    def _since(self, tp: TP) -> float:
+        """When this broker became leader of tp (a follower gets replica_lag_s to show up)."""
+        return self._lead_since.setdefault(tp, time.monotonic())
+
+    async def _ckpt_loop(self) -> None:
+        if not self.data_dir:
+            return
+        path = os.path.join(self.data_dir, "replication.json")
+        while True:
+            await asyncio.sleep(0.2)
+            hw = {}
+            sole = []
+            for tp, st in self.parts.items():
+                if self.node_id not in st["replicas"]:
+                    continue
+                h = self.hw.get(tp, 0)
+                if st["leader"] == self.node_id and st["isr"] == [self.node_id]:
+                    sole.append(tp_key(*tp))
+                hw[tp_key(*tp)] = min(h, self._leo(tp))
+            tmp = path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump({"hw": hw, "sole": sole}, f)
+            os.replace(tmp, path)
+
+    # ------------------------------------------------------------------ follower side
+    def _followed(self) -> Dict[int, List[TP]]:
+        by: Dict[int, List[TP]] = {}
+        for tp, st in self.parts.items():
+            if self.node_id in st["replicas"] and st["leader"] not in (self.node_id, -1):
+                by.setdefault(int(st["leader"]), []).append(tp)
+        return by
+
+    def _reconcile_fetchers(self) -> None:
+        want = self._followed()
+        for node, task in list(self._fetchers.items()):
+            if node not in want or task.done():
+                task.cancel()
+                del self._fetchers[node]
+        loop = asyncio.get_running_loop()
+        for node in want:
+            if node not in self._fetchers and node in self.nodes:
+                self._fetchers[node] = loop.create_task(self._fetch_loop(node))
+
+    async def _fetch_loop(self, leader: int) -> None:
+        from .kafka_wire import Reader, Writer
+        corr = 0
+        while True:
+            tps = self._followed().get(leader, [])
+            if not tps or leader not in self.nodes:
+                return
+            host, port = self.nodes[leader]
+            try:
+                reader, writer = await asyncio.open_connection(host, port)
+            except OSError:
+                await asyncio.sleep(0.1)
+                continue
+            try:
+                while True:
+                    tps = self._followed().get(leader, [])
+                    if not tps:
+                        return
+                    by_topic: Dict[str, List[Tuple[int, int]]] = {}
+                    for t, p in tps:
+                        by_topic.setdefault(t, []).append((p, self._leo((t, p))))
+                    body = (Writer().i32(self.node_id).i32(200).i32(1).i32(64 << 20).i8(0)
+                            .array(sorted(by_topic.items()), lambda w, kv: w.string(kv[0]).array(
+                                kv[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).i32(16 << 20))).build())
+                    corr += 1
+                    hdr = Writer().i16(FETCH).i16(FETCH_V).i32(corr).string(f"replica-{self.node_id}").build()
+                    writer.write(struct.pack(">i", len(hdr) + len(body)) + hdr + body)
+                    size = struct.unpack(">i", await reader.readexactly(4))[0]
+                    r = Reader(await reader.readexactly(size))
+                    if r.i32() != corr:
+                        raise BrokerError("replica fetch: correlation mismatch")
+                    r.i32()                                          # throttle
+
+                    def part(x):
+                        idx, err, hw, _lso = x.i32(), x.i16(), x.i64(), x.i64()
+                        x.array(lambda y: (y.i64(), y.i64()))
+                        return idx, err, hw, x.view_()
+                    resp = r.array(lambda x: (x.string(), x.array(part)))
+                    tickets = []
+                    moved = False
+                    for t, parts in resp:
+                        for p, err, hw, recs in parts:
+                            if err:
+                                moved = True                          # not the leader any more
+                                continue
+                            if recs is not None and len(recs):
+                                n, ticket = self.store.append_replica(t, p, recs)
+                                self.replicated_bytes += len(recs)
+                                if ticket:
+                                    tickets.append(ticket)
+                            self.hw[(t, p)] = max(self.hw.get((t, p), 0), min(int(hw), self.store.log_end(t, p)))
+                    self.replica_fetches += 1
+                    if tickets and self.server is not None:
+                        await self.server._written_ticket(max(tickets))   # durable before the next fetch
+                    if moved:
+                        await asyncio.sleep(0.05)
+            except (OSError, asyncio.IncompleteReadError, BrokerError, ConnectionError):
+                await asyncio.sleep(0.05)                            # leader away: metadata will move it
+            finally:
+                try:
+                    writer.close()
+                except Exception:                                    # noqa: BLE001
+                    pass
