@@ -264,6 +264,33 @@ class BatchStore:
                 self._apply_retention(topic, partition, L)
             return n_new, self._appended(L) if n_new else None
 
+    def truncate(self, topic: str, partition: int, offset: int) -> int:
+        """Drop every batch at or above ``offset`` (a replica whose leader changed cuts its
+        un-acknowledged tail to the high watermark before it follows the new leader, so its
+        log is a prefix of the leader's -- ingest/kafka_replica.py).  The idempotent-producer
+        state of the partition is rebuilt from the batches that remain.  Returns the batches
+        dropped."""
+        with self._lock:
+            L = self._log(topic, partition)
+            if offset >= L.end:
+                return 0
+            i = bisect.bisect_left(L.bases, offset)
+            if i < len(L.bases) and L.bases[i] != offset and i > 0:
+                raise BrokerError(f"{topic}[{partition}]: truncation point {offset} inside a batch")
+            dropped = len(L.batches) - i
+            L.nbytes -= sum(len(x) for x in L.batches[i:])
+            del L.bases[i:], L.batches[i:], L.ts[i:]
+            L.end = max(offset, L.begin)
+            L.visible = min(L.visible, L.end)
+            self._producers.pop((topic, partition), None)
+            for base, b in zip(L.bases, L.batches):
+                self._track_producer(topic, partition, b, base)
+            self._persist_truncate(topic, partition, L.end)
+            return dropped
+
+    def _persist_truncate(self, topic: str, partition: int, offset: int) -> None:
+        pass
+
     def log_end(self, topic: str, partition: int) -> int:
         """The next offset this log assigns (LEO), written or not."""
         with self._lock:

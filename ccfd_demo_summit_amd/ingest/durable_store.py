@@ -437,6 +437,9 @@ class DurableBatchStore(BatchStore):
                     if kind == "A":
                         touched |= self._write_batches(topic, p, op[3])
                         ends[(topic, p)] = op[4]
+                    elif kind == "T":
+                        self._truncate_segments(topic, p, op[3])
+                        ends.pop((topic, p), None)
                     else:
                         self._retire_segments(topic, p, op[3])
                 if self.fsync == "always" and touched:
@@ -454,8 +457,8 @@ class DurableBatchStore(BatchStore):
             with self._lock:
                 for (topic, p), end in ends.items():
                     L = self._log(topic, p)
-                    if end > L.visible:
-                        L.visible = end
+                    if end > L.visible:         # (never past a truncation since queued)
+                        L.visible = min(end, L.end)
                 if self.fsync != "always":
                     self._dirty |= touched
             with self._wcv:
@@ -498,6 +501,40 @@ class DurableBatchStore(BatchStore):
         while len(mv):
             k = os.write(fd, mv)
             mv = mv[k:]
+
+    def _persist_truncate(self, topic: str, partition: int, offset: int) -> None:
+        """Under the store lock: the segments follow the in-memory cut, in write order."""
+        self._enqueue(("T", topic, partition, offset))
+
+    def _truncate_segments(self, topic: str, partition: int, offset: int) -> None:
+        """Writer thread: cut the partition's files at ``offset`` (a batch boundary)."""
+        segs = self._segs.get((topic, partition), [])
+        while len(segs) > 1 and segs[-1].base >= offset:
+            seg = segs.pop()
+            with self._lock:
+                self._close_segment(seg, now=True)
+            for ext in (".log", ".idx"):
+                try:
+                    os.unlink(seg.path + ext)
+                except OSError:
+                    pass
+        if not segs:
+            return
+        seg = segs[-1]
+        with open(seg.path + ".idx", "rb") as f:
+            raw = f.read()
+        entries = [_IDX.unpack_from(raw, i) for i in range(0, len(raw) - len(raw) % 16, 16)]
+        k = next((j for j, (bo, _ps) in enumerate(entries) if bo >= offset), None)
+        if k is None:
+            return                              # nothing of this segment is past the cut
+        pos = entries[k][1]
+        if seg.closed or seg.fd < 0:            # a rolled / recovered segment: append to it again
+            seg.fd = os.open(seg.path + ".log", os.O_WRONLY | os.O_APPEND)
+            seg.idx_fd = os.open(seg.path + ".idx", os.O_WRONLY | os.O_APPEND)
+            seg.closed = False
+        os.ftruncate(seg.fd, pos)
+        os.ftruncate(seg.idx_fd, k * _IDX.size)
+        seg.size, seg.nbatches, seg.last_end = pos, k, offset
 
     def _apply_retention(self, topic: str, partition: int, L: _Log) -> None:
         """Delete whole closed segments below the log start (in write order once serving)."""

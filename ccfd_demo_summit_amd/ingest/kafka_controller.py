@@ -13,8 +13,9 @@ process; here each broker is its own process with its own durable log
   stays, the partition goes offline) and the partitions it led are re-elected;
 * **election**: the new leader is the live ISR member with the HIGHEST reported LEO, chosen
   only after every live ISR member has reported since the failure (a follower cannot append
-  once its leader is gone, so the reports are final).  Every replica's log is then a prefix of
-  the new leader's -- no runtime truncation is ever needed.  Unclean election is off: a
+  once its leader is gone, so the reports are final), so no acknowledged record is lost; the
+  other replicas cut their un-acknowledged tails to their high watermark before following it
+  (ingest/kafka_replica.py).  Unclean election is off: a
   partition whose ISR is all dead stays offline until an ISR member returns;
 * **ISR**: leaders propose shrink / expand (a follower that stopped fetching or caught up)
   with their leader epoch; stale proposals are refused;
@@ -55,7 +56,7 @@ class ControllerState:
     """The controller's state machine (no I/O except its own persistence; unit-testable with
     an injected clock)."""
 
-    def __init__(self, data_dir: Optional[str] = None, session_s: float = 0.6, rf: int = 3,
+    def __init__(self, data_dir: Optional[str] = None, session_s: float = 1.5, rf: int = 3,
                  rebalance_s: float = 5.0, clock=time.monotonic):
         self.data_dir = data_dir
         self.session_s = float(session_s)
@@ -349,7 +350,7 @@ def main(argv=None):
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=9093)
     ap.add_argument("--data-dir", default=None)
-    ap.add_argument("--session-s", type=float, default=0.6, help="broker heartbeat timeout")
+    ap.add_argument("--session-s", type=float, default=1.5, help="broker heartbeat timeout")
     ap.add_argument("--rf", type=int, default=3, help="replication factor of new topics")
     a = ap.parse_args(argv)
     from aiohttp import web

@@ -15,10 +15,14 @@ followers that replicate by FETCHING from the leader, as Kafka's replica fetcher
 * **ISR**: the leader proposes (in its next heartbeat) to drop a follower that has not caught
   up for ``replica_lag_s`` and to re-admit one that has caught up; the controller applies
   proposals of the current leader epoch only;
-* **fail-over**: the controller elects the live ISR member with the highest LEO, so every
-  other replica's log is a prefix of the new leader's.  A broker that restarts cuts its logs
-  to its checkpointed HW (``replication.json``, every 200 ms) before rejoining -- except where it
-  was the sole ISR member (its log is then the authority) -- so its log is again a prefix;
+* **fail-over**: the controller elects the live ISR member with the highest LEO (it holds
+  every acknowledged record).  Every other replica -- a deposed leader included -- cuts its log
+  to the HW it knows when it starts following a new leader, and re-fetches from there, so its
+  log is a prefix of the leader's.  A broker that restarts cuts its logs to its checkpointed
+  HW (``replication.json``, every 200 ms) -- except where it was the sole ISR member (its log is
+  then the authority);
+* **pipelined producers** (``max.in.flight`` > 1, kafka_wire.py) keep one request in flight
+  per partition, so a refused batch is never overtaken by a later one;
 * producer ids are per-broker disjoint (``node + 1024 k``) and the idempotent-producer state
   is replicated with the batches, so a batch retried against a new leader is stored once.
 
@@ -93,6 +97,8 @@ class ReplicaManager:
         self.replicated_bytes = 0
         self.hb_failures = 0
         self._lead_since: Dict[TP, float] = {}
+        self.truncations = 0
+        self.truncated_batches = 0
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self) -> None:
@@ -207,6 +213,14 @@ class ReplicaManager:
             elif st["leader"] != self.node_id:
                 self.fol.pop(tp, None)
                 self._fail_acks(tp)
+                # (no leader yet = an election in progress: this replica may be the one elected,
+                # with acknowledged records above the HW it has heard of -- keep them)
+                if self.node_id in st["replicas"] and st["leader"] >= 0 and (
+                        was is None or was["leader"] != st["leader"] or was["epoch"] != st["epoch"]):
+                    # a new leader: cut the tail this replica holds past the high watermark it
+                    # knows (never acknowledged; a deposed leader's may not be on the new one),
+                    # so the log is a prefix of the leader's before following it
+                    self._truncate_to_hw(tp)
             if st["leader"] == self.node_id:
                 self._advance_hw(tp)
         self._reconcile_fetchers()
@@ -317,6 +331,16 @@ class ReplicaManager:
                 json.dump({"hw": hw, "sole": sole}, f)
             os.replace(tmp, path)
 
+    def _truncate_to_hw(self, tp: TP, hw: Optional[int] = None) -> None:
+        h = self.hw.get(tp, 0) if hw is None else hw
+        try:
+            if self.store.log_end(*tp) > h:
+                n = self.store.truncate(tp[0], tp[1], h)
+                self.truncations += 1
+                self.truncated_batches += n
+        except BrokerError:
+            pass
+
     # ------------------------------------------------------------------ follower side
     def _followed(self) -> Dict[int, List[TP]]:
         by: Dict[int, List[TP]] = {}
@@ -378,6 +402,11 @@ class ReplicaManager:
                     moved = False
                     for t, parts in resp:
                         for p, err, hw, recs in parts:
+                            if err == 1 and self.store.log_end(t, p) > int(hw):
+                                # OFFSET_OUT_OF_RANGE past the leader's log: this replica holds
+                                # a tail the leader never had -- cut it to the leader's HW
+                                self._truncate_to_hw((t, p), int(hw))
+                                continue
                             if err:
                                 moved = True                          # not the leader any more
                                 continue

@@ -21,6 +21,7 @@ Heartbeat) lives in ``kafka_group.py``.
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import socket
 import struct
@@ -484,20 +485,35 @@ class Connection:
     def request(self, api_key: int, version: int, body) -> Reader:
         """``body``: bytes, or a list of buffers sent as they are (no concatenation)."""
         with self._lock:
-            corr = next(self._corr)
-            if isinstance(body, list):
-                hdr = Writer().i16(api_key).i16(version).i32(corr).string(self.client_id).build()
-                n = len(hdr) + sum(len(b) for b in body)
-                _sendall_parts(self.sock, [struct.pack(">i", n) + hdr] + body)
-            else:
-                self.sock.sendall(encode_request(api_key, version, corr, self.client_id, body))
-            size = struct.unpack(">i", _recv_exact(self.sock, 4))[0]
-            resp = _recv_exact(self.sock, size)
-        r = Reader(resp)
+            corr = self._send(api_key, version, body)
+            return self._recv(corr)
+
+    def _send(self, api_key: int, version: int, body) -> int:
+        corr = next(self._corr)
+        if isinstance(body, list):
+            hdr = Writer().i16(api_key).i16(version).i32(corr).string(self.client_id).build()
+            n = len(hdr) + sum(len(b) for b in body)
+            _sendall_parts(self.sock, [struct.pack(">i", n) + hdr] + body)
+        else:
+            self.sock.sendall(encode_request(api_key, version, corr, self.client_id, body))
+        return corr
+
+    def _recv(self, corr: int) -> Reader:
+        size = struct.unpack(">i", _recv_exact(self.sock, 4))[0]
+        r = Reader(_recv_exact(self.sock, size))
         got = r.i32()
         if got != corr:
             raise BrokerError(f"correlation id mismatch {got} != {corr}")
         return r
+
+    # pipelining (one owner thread): requests sent back to back, answered in order
+    def send(self, api_key: int, version: int, body) -> int:
+        with self._lock:
+            return self._send(api_key, version, body)
+
+    def recv(self, corr: int) -> Reader:
+        with self._lock:
+            return self._recv(corr)
 
     def close(self):
         try:
@@ -540,6 +556,12 @@ class KafkaBroker:
         self._leaders: Dict[Tuple[str, int], int] = {}
         self._partitions: Dict[str, int] = {}
         self._coord: Dict[str, int] = {}
+        # produce defaults: acks (1 = leader, -1 = all in-sync replicas) and the requests kept in
+        # flight per producer (max.in.flight; > 1 pipelines produce_raw, flush() drains)
+        self.default_acks = 1
+        self.max_in_flight = 1
+        self._pconns: Dict[int, Connection] = {}
+        self._inflight: "collections.deque" = collections.deque()
         self._boot = self._connect_any(connect_wait_s)
         self._rr = itertools.count()
         self.retries_done = 0                               # refresh-and-retry count (tests, metrics)
@@ -660,7 +682,7 @@ class KafkaBroker:
 
     # ---------------------------------------------------------------- produce
     def produce_batch(self, topic: str, partition: int, values: Sequence[bytes],
-                      keys: Optional[Sequence[Optional[bytes]]] = None, acks: int = 1) -> int:
+                      keys: Optional[Sequence[Optional[bytes]]] = None, acks: Optional[int] = None) -> int:
         rb = encode_record_batch(values, keys, compression=self.compression)
         return self.produce_raw(topic, partition, rb, acks)
 
@@ -691,8 +713,11 @@ class KafkaBroker:
             o += 12 + blen
         return n_total
 
-    def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
-        """Produce an already encoded RecordBatch (e.g. from the native encoder)."""
+    def produce_raw(self, topic: str, partition: int, record_set: bytes, acks: Optional[int] = None) -> int:
+        """Produce an already encoded RecordBatch (e.g. from the native encoder).  With
+        ``max_in_flight`` > 1 the request is pipelined: it returns -1 (the base offset arrives
+        later) and ``flush()`` waits for every answer."""
+        acks = self.default_acks if acks is None else acks
         stamp = False
         if self.stamp_time:                 # a sample of the batches carries its send time:
             # every stamp_every-th batch OF EACH PARTITION -- one counter over round-robin
@@ -702,7 +727,7 @@ class KafkaBroker:
             stamp = k % max(1, self.stamp_every) == 0
             self._stamp_n[(topic, partition)] = k + 1
         if not (self.idempotent or stamp):
-            return self._produce_raw(topic, partition, record_set, acks)
+            return self._produce_send(topic, partition, record_set, acks)
         # at most one copy: the send-time header splice, else a bytearray from the encoders is
         # stamped in place (anything immutable is copied once); sequence stamps; one seal
         if stamp:
@@ -713,18 +738,79 @@ class KafkaBroker:
             b = bytearray(record_set)
         if not self.idempotent:
             seal_batches(b)
-            return self._produce_raw(topic, partition, b, acks)
+            return self._produce_send(topic, partition, b, acks)
         key = (topic, partition)
         with self._seq_guard:
             lk = self._seq_locks.setdefault(key, threading.Lock())
         with lk:                         # sequence order == send order on a partition
             n = self._stamp_sequence(topic, partition, b)
             seal_batches(b)
+            if self.max_in_flight > 1:   # the sequence advances at send: answers come in order
+                self._seq[key] = (self._seq.get(key, 0) + n) & SEQ_MASK
+                return self._produce_send(topic, partition, b, acks)
             base = self._produce_raw(topic, partition, b, acks)   # retries resend the same seq
             self._seq[key] = (self._seq.get(key, 0) + n) & SEQ_MASK
             return base
 
-    def _produce_raw(self, topic: str, partition: int, record_set: bytes, acks: int = 1) -> int:
+    # ---------------------------------------------------------------- pipelined produce
+    def _produce_send(self, topic: str, partition: int, record_set, acks: int) -> int:
+        if self.max_in_flight <= 1:
+            return self._produce_raw(topic, partition, record_set, acks)
+        # at most one request in flight PER PARTITION (answers of the previous one first): a
+        # refused batch can then never be overtaken by a later one of the same partition that a
+        # broker without the producer's state would accept out of order
+        while any(e[3] == topic and e[4] == partition for e in self._inflight):
+            self._complete_one()
+        head = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000)).i32(1).string(topic)
+                .i32(1).i32(partition).i32(len(record_set)).build())
+        node = self.leader_of(topic, partition)
+        try:
+            if node < 0:
+                raise BrokerError(f"{topic}[{partition}] has no leader")
+            c = self._pconns.get(node)
+            if c is None:
+                c = self._pconns[node] = Connection(*self._nodes[node], self.client_id, self.timeout)
+            corr = c.send(PRODUCE, 3, [head, record_set])
+        except (OSError, ConnectionError, BrokerError, KeyError):
+            self._drop_pipe(node)
+            c, corr = None, -1
+        self._inflight.append((node, c, corr, topic, partition, record_set, acks))
+        while len(self._inflight) >= self.max_in_flight:
+            self._complete_one()
+        return -1
+
+    def _drop_pipe(self, node: int) -> None:
+        c = self._pconns.pop(node, None)
+        if c is not None:
+            c.close()
+
+    def _complete_one(self) -> None:
+        node, c, corr, topic, partition, rs, acks = self._inflight.popleft()
+        err = ERR_LEADER_NOT_AVAILABLE
+        if c is not None and self._pconns.get(node) is c:
+            try:
+                r = c.recv(corr)
+                resp = r.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+                err = resp[0][1][0][1]
+            except (OSError, ConnectionError, BrokerError):
+                self._drop_pipe(node)
+        if err == ERR_NONE:
+            return
+        if err not in RETRIABLE + (ERR_OUT_OF_ORDER_SEQUENCE,):
+            raise BrokerError(f"{topic}[{partition}] produce error {err}")
+        # the leader moved or died: this batch and every later one in flight to it failed (or
+        # were refused as out of order); they are re-sent, in order, on the synchronous path --
+        # the same sequence numbers, so whatever the old leader did store is not stored twice
+        self._leaders.pop((topic, partition), None)
+        self._produce_raw(topic, partition, rs, acks)
+
+    def flush(self) -> None:
+        """Wait for every pipelined produce's answer (re-sending what failed)."""
+        while self._inflight:
+            self._complete_one()
+
+    def _produce_raw(self, topic: str, partition: int, record_set: bytes, acks: Optional[int] = None) -> int:
+        acks = self.default_acks if acks is None else acks
         # [acks, timeout, 1 topic, 1 partition, record set size] + the record set itself, sent
         # without copying it into the request (Connection.request scatter-gather)
         head = (Writer().string(None).i16(acks).i32(int(self.timeout * 1000)).i32(1).string(topic)
@@ -870,8 +956,12 @@ class KafkaBroker:
         return predicate()
 
     def close(self):
+        try:
+            self.flush()                         # pipelined produces still waiting for answers
+        except BrokerError:
+            pass
         self._boot.close()
-        for c in self._conns.values():
+        for c in list(self._conns.values()) + list(self._pconns.values()):
             c.close()
 
 

@@ -454,6 +454,10 @@ def cmd_producer(a, cfg):
         pc.source, pc.csv_path = "csv", a.csv
     broker = _broker(cfg, idempotent=True)
     broker.stamp_time = True          # ccfd-ts send-time header: the engine's produce -> scored latency
+    broker.default_acks = a.acks      # -1: every in-sync replica (replicated kafka-lite)
+    broker.max_in_flight = max(1, a.max_in_flight)
+    if a.acks == -1:
+        broker.RETRIES = 14           # rides out a leader fail-over (~1 s) instead of failing
     prod = TransactionProducer(broker, pc)
     from ..ingest.kafka_wire import warm_native
     warm_native()
@@ -467,6 +471,7 @@ def cmd_producer(a, cfg):
     # --seconds with --count 0: a time-bounded open-loop run (deployment benchmarks)
     until = t0 + a.seconds if a.count <= 0 else None
     n = prod.produce(a.count if a.count > 0 else 1 << 62, until=until)
+    broker.flush()                    # every pipelined produce answered
     dt = time.perf_counter() - t0
     print(json.dumps({"produced": n, "seconds": round(dt, 3), "tx_s": round(n / max(dt, 1e-9), 1),
                       "topic": pc.topic, "fmt": pc.fmt, "id_base": pc.id_base}), flush=True)
@@ -653,6 +658,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--dlq", default=None, help="dlq-replay: the hand-off dead-letter journal to re-deliver")
     ap.add_argument("--remote-prediction", action="store_true", help="KIE: call the user-task model over HTTP")
     ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
+    ap.add_argument("--acks", type=int, default=1, choices=[0, 1, -1],
+                    help="producer: 1 = the leader, -1 = every in-sync replica (acks=all)")
+    ap.add_argument("--max-in-flight", type=int, default=1,
+                    help="producer: produce requests in flight per producer (pipelined; idempotent order kept)")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--rate", type=float, default=0.0)
     ap.add_argument("--count", type=int, default=100_000, help="producer: transactions (0 = run --seconds)")

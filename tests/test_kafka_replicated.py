@@ -110,7 +110,7 @@ def cluster(tmp_path):
                 "--port", str(bports[k - 1]), "--node-id", str(k), "--controller", f"http://127.0.0.1:{cport}",
                 "--metrics-port", str(mports[k - 1]), "--data-dir", str(tmp_path / f"b{k}"), "--fsync", "interval"]
     start("ctl", [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller", "--host", "127.0.0.1",
-                  "--port", str(cport), "--data-dir", str(tmp_path / "ctl"), "--session-s", "0.6"])
+                  "--port", str(cport), "--data-dir", str(tmp_path / "ctl"), "--session-s", "1.0"])
     _wait(cport)
     for k in (1, 2, 3):
         start(f"b{k}", broker_cmd(k))
@@ -203,4 +203,40 @@ def test_broker_sigkill_loses_no_acknowledged_record(cluster):
     dups = [v for v, n in got.items() if n > 1]
     assert not missing, (len(missing), missing[:5])
     assert not dups, dups[:5]
+    kb.close()
+
+
+def test_pipelined_idempotent_producer_through_a_leader_failover(cluster):
+    """max.in.flight 5 (requests pipelined per leader connection) under acks=all, with the
+    leader of half the partitions SIGKILLed mid-stream: after flush() every record is stored
+    exactly once, in order per partition (re-sent batches keep their sequence numbers)."""
+    boot = ",".join(f"127.0.0.1:{p}" for p in cluster["bports"])
+    deadline = time.time() + 30
+    while len(json.loads(_text(f"http://127.0.0.1:{cluster['cport']}/metadata"))["nodes"]) < 3:
+        assert time.time() < deadline
+        time.sleep(0.1)
+    kb = KafkaBroker(boot, idempotent=True, connect_wait_s=10)
+    kb.RETRIES = 14
+    kb.max_in_flight = 5
+    kb.default_acks = -1
+    kb.create_topic("pipe", 4)
+    n_batches = 400
+    for k in range(n_batches):
+        if k == n_batches // 3:
+            victim = kb.leader_of("pipe", 0)
+            os.killpg(cluster["procs"][f"b{victim}"].pid, signal.SIGKILL)
+        kb.produce_raw("pipe", k % 4, encode_record_batch([b"%d:%d" % (k, i) for i in range(20)]))
+    kb.flush()
+    assert not kb._inflight
+    for p in range(4):
+        end = kb.end_offset("pipe", p)
+        vals = []
+        off = 0
+        while off < end:
+            _e, _hw, raw = kb.fetch_raw("pipe", p, off)
+            recs = [r for r in decode_record_batches(raw, "pipe", p) if r.offset >= off]
+            vals += [r.value for r in recs]
+            off = recs[-1].offset + 1 if recs else end
+        want = [b"%d:%d" % (k, i) for k in range(p, n_batches, 4) for i in range(20)]
+        assert vals == want, (p, len(vals), len(want))
     kb.close()
