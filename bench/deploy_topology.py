@@ -212,6 +212,15 @@ def main(argv=None):
                     help="... and restart it from its data directory this long after")
     ap.add_argument("--fsync", default="interval", choices=["always", "interval", "never"],
                     help="kafka-lite durability flush policy (its logs are always on disk here)")
+    ap.add_argument("--kafka-replicated", action="store_true",
+                    help="replicated kafka-lite: --kafka-nodes broker PROCESSES (each its own durable log, "
+                         "replication factor 3) + the controller (ingest/kafka_controller.py); producers "
+                         "use acks=all; --kafka-kill-at then SIGKILLs broker --kafka-kill-node")
+    ap.add_argument("--kafka-kill-node", type=int, default=2, help="replicated: the broker node id to kill")
+    ap.add_argument("--producer-acks", type=int, default=None, choices=[1, -1],
+                    help="producers' acks (default: -1 with --kafka-replicated, else 1)")
+    ap.add_argument("--producer-max-in-flight", type=int, default=None,
+                    help="producers' pipelined requests (default: 5 with --kafka-replicated, else 1)")
     ap.add_argument("--kafka-memory", action="store_true",
                     help="kafka-lite without --data-dir (round 3's in-memory broker): the A/B of durability")
     ap.add_argument("--standard-mode", default="count", choices=["count", "process"],
@@ -233,7 +242,10 @@ def main(argv=None):
     log_dir.mkdir(parents=True, exist_ok=True)
 
     kafka_port, = free_ports(1, a.kafka_nodes)
-    metrics_port, notif_port, master_port = free_ports(3)
+    metrics_port, notif_port, master_port, ctl_port = free_ports(4)
+    kmetrics = [metrics_port] + (free_ports(a.kafka_nodes - 1) if a.kafka_replicated else [])
+    acks = a.producer_acks if a.producer_acks is not None else (-1 if a.kafka_replicated else 1)
+    inflight = a.producer_max_in_flight if a.producer_max_in_flight is not None else (5 if a.kafka_replicated else 1)
     kie_port, = free_ports(1, max(1, a.kie_shards))
     K = max(1, a.kie_shards)
     kie_ports = [kie_port + k for k in range(K)]
@@ -251,7 +263,8 @@ def main(argv=None):
     out: Dict = {"metric": "end-to-end tx/s, deployed topology (separate processes)", "topology": "shared",
                  "n_gpus": 1 if a.rehearsal else a.ranks, "ranks": a.ranks, "rehearsal": a.rehearsal,
                  "fmt": a.fmt, "producers": a.producers, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
-                 "model": a.model, "kie_shards": K}
+                 "model": a.model, "kie_shards": K, "kafka_replicated": a.kafka_replicated,
+                 "producer_acks": acks, "producer_max_in_flight": inflight}
     import tempfile
     kdir = tempfile.mkdtemp(prefix="ccfd-kafka-lite-")          # durable logs + committed offsets
     out["kafka_durable"] = {"fsync": a.fsync} if not a.kafka_memory else False
@@ -262,8 +275,32 @@ def main(argv=None):
                      "--partitions", str(a.partitions), "--metrics-port", str(metrics_port),
                      "--retention-batches", str(a.retention_batches)] + \
             ([] if a.kafka_memory else ["--data-dir", kdir, "--fsync", a.fsync])
-        procs.append(Proc("kafka-lite", kafka_cmd, env, log_dir))
-        wait_port(kafka_port, 60)
+        broker_cmds = {}
+        if a.kafka_replicated:
+            # the controller + one broker process per node, each with its own durable log
+            ctl_cmd = [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller", "--host", "127.0.0.1",
+                       "--port", str(ctl_port), "--data-dir", str(Path(kdir) / "controller")]
+            procs.append(Proc("kafka-controller", ctl_cmd, env, log_dir))
+            wait_port(ctl_port, 60)
+            for i in range(a.kafka_nodes):
+                broker_cmds[i + 1] = [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
+                                      "--port", str(kafka_port + i), "--node-id", str(i + 1),
+                                      "--controller", f"http://127.0.0.1:{ctl_port}",
+                                      "--metrics-port", str(kmetrics[i]),
+                                      "--retention-batches", str(a.retention_batches),
+                                      "--data-dir", str(Path(kdir) / f"broker{i + 1}"), "--fsync", a.fsync]
+                procs.append(Proc(f"kafka-broker{i + 1}", broker_cmds[i + 1], env, log_dir))
+            for i in range(a.kafka_nodes):
+                wait_port(kafka_port + i, 60)
+            t_md = time.time()
+            while time.time() - t_md < 30:
+                md = json.loads(http_text(f"http://127.0.0.1:{ctl_port}/metadata"))
+                if len(md["nodes"]) == a.kafka_nodes:
+                    break
+                time.sleep(0.2)
+        else:
+            procs.append(Proc("kafka-lite", kafka_cmd, env, log_dir))
+            wait_port(kafka_port, 60)
         from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
         kb = KafkaBroker(brokers, connect_wait_s=30)
         for t, n in (("odh-demo", a.partitions), ("ccd-customer-outgoing", 4), ("ccd-customer-response", 4)):
@@ -334,7 +371,8 @@ def main(argv=None):
         for i in range(a.producers):
             prods.append(Proc(f"producer{i}", [PY, "-m", L, "producer", "--fmt", a.fmt, "--batch", str(a.batch),
                                                "--count", str(a.count), "--seconds", str(a.seconds),
-                                               "--rate", str(per_rate),
+                                               "--rate", str(per_rate), "--acks", str(acks),
+                                               "--max-in-flight", str(inflight),
                                                "--id-base", str((i + 1) << 40), "--seed-offset", str(i * 101)],
                               env, log_dir))
         procs.extend(prods)
@@ -362,15 +400,19 @@ def main(argv=None):
                     time.time() - t_w0 >= a.notifier_kill_at + a.notifier_down_s:
                 procs.append(Proc("notifier-restarted", notif_cmd, notif_env, log_dir))
                 noutage["restarted_at_s"] = round(time.time() - t_w0, 1)
+            kname = f"kafka-broker{a.kafka_kill_node}" if a.kafka_replicated else "kafka-lite"
             if a.kafka_kill_at > 0 and not koutage and time.time() - t_w0 >= a.kafka_kill_at:
-                kl = [p for p in procs if p.name.startswith("kafka-lite")][-1]
+                kl = [p for p in procs if p.name.startswith(kname)][-1]
                 kl.stop(sig=signal.SIGKILL, wait=5)            # a crashed broker pod
                 koutage = {"killed_at_s": round(time.time() - t_w0, 1)}
+                if a.kafka_replicated:
+                    koutage["node"] = a.kafka_kill_node
             if koutage and "restarted_at_s" not in koutage and \
                     time.time() - t_w0 >= a.kafka_kill_at + a.kafka_down_s:
-                procs.append(Proc("kafka-lite-restarted", kafka_cmd, env, log_dir))   # recovers from disk
+                cmd = broker_cmds[a.kafka_kill_node] if a.kafka_replicated else kafka_cmd
+                procs.append(Proc(f"{kname}-restarted", cmd, env, log_dir))   # recovers from disk
                 koutage["restarted_at_s"] = round(time.time() - t_w0, 1)
-                wait_port(kafka_port, 60)
+                wait_port(kafka_port + (a.kafka_kill_node - 1 if a.kafka_replicated else 0), 60)
                 koutage["serving_at_s"] = round(time.time() - t_w0, 1)
             if a.kie_outage_at > 0 and not outage and time.time() - t_w0 >= a.kie_outage_at:
                 kie = [p for p in procs if p.name == kill_name][0]
@@ -393,6 +435,15 @@ def main(argv=None):
                 lag = None
             samples.append({"t_s": round(now - t_w0, 1), "tx_s": round((r_now - last_r) / (now - last_t), 1),
                             "lag_msgs": lag})
+            if a.kafka_replicated:                          # the reference dashboard's panel
+                under = 0
+                for mp in kmetrics:
+                    try:
+                        under += int(metric_sum(http_text(f"http://127.0.0.1:{mp}/metrics", timeout=2.0),
+                                                "kafka_server_replicamanager_underreplicatedpartitions"))
+                    except Exception:                       # that broker is down right now
+                        pass
+                samples[-1]["under_replicated"] = under
             print(f"[deploy] {time.strftime('%H:%M:%S')} sample {samples[-1]} kie_outage {outage} "
                   f"kafka_outage {koutage} notifier_outage {noutage}", file=sys.stderr, flush=True)
             last_t, last_r = now, r_now
@@ -528,9 +579,24 @@ def main(argv=None):
         out["scored_to_process_started_us"] = stats["scored_to_started_us"]
         out["kie_handoff_attribution"] = stats["handoff_attribution"]
         if koutage:
-            rec = re.findall(r"\[kafka-lite\] recovered from .*", "".join(
-                p.text() for p in procs if p.name == "kafka-lite-restarted"))
+            rec = re.findall(r"\[kafka-lite\] (?:node \d+ )?recovered from .*", "".join(
+                p.text() for p in procs if p.name.endswith("-restarted") and p.name.startswith("kafka")))
             out["kafka_outage"] = dict(koutage, recovered=rec)
+            if a.kafka_replicated:
+                # the under-replicated series rose while the broker was away and is back to 0
+                under = [sm.get("under_replicated", 0) for sm in samples]
+                out["under_replicated_max"] = max(under) if under else None
+                fin = 0
+                for mp in kmetrics:
+                    try:
+                        fin += int(metric_sum(http_text(f"http://127.0.0.1:{mp}/metrics", timeout=2.0),
+                                              "kafka_server_replicamanager_underreplicatedpartitions"))
+                    except Exception:
+                        fin = -1
+                out["under_replicated_final"] = fin
+                out["min_sample_ratio"] = (round(min(sm["tx_s"] for sm in samples[1:-1]) /
+                                                 max(sm["tx_s"] for sm in samples[1:-1]), 3)
+                                           if len(samples) > 2 else None)
         if noutage:
             out["notifier_outage"] = noutage
         out["handoff_dead_lettered"] = sum(sum(1 for _ in open(f)) for f in Path(jdir).glob("handoff-dlq*.jsonl"))
@@ -552,7 +618,10 @@ def main(argv=None):
                                     instance=f"engine-{r}:8000")   # k8s: <pod ip>:8000 (operator/render.py)
         for p_ in kie_ports:
             series += promql.scrape(f"http://127.0.0.1:{p_}/rest/metrics", "ccfd-pods")
-        series += promql.scrape(f"http://127.0.0.1:{metrics_port}/metrics", "ccfd-pods")
+        for mp in kmetrics:
+            series += promql.scrape(f"http://127.0.0.1:{mp}/metrics", "ccfd-pods")
+        if a.kafka_replicated:
+            series += promql.scrape(f"http://127.0.0.1:{ctl_port}/metrics", "ccfd-pods")
         fx = json.loads((ROOT / "tests/fixtures/reference_dashboard_exprs.json").read_text())
         exprs = {k: [e["expr"] for e in v] for k, v in fx["dashboards"].items() if k != "SparkMetrics.json"}
         rep = promql.check(exprs, series)
