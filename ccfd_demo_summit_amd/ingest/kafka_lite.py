@@ -784,7 +784,10 @@ class KafkaLiteServer:
                     if replica_id >= 0:
                         rep.on_replica_fetch(replica_id, topic, p, off)
                     else:
-                        upto = limit = rep.high_watermark(topic, p)
+                        # consumers see data below the HW; an offset between the HW and the log
+                        # end is valid (a new leader's HW catches up) -- an empty answer, not
+                        # OFFSET_OUT_OF_RANGE
+                        upto = rep.high_watermark(topic, p)
                     hw = rep.high_watermark(topic, p)
                 if off < self.store.begin_offset(topic, p) or off > limit:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))

@@ -240,3 +240,50 @@ def test_pipelined_idempotent_producer_through_a_leader_failover(cluster):
         want = [b"%d:%d" % (k, i) for k in range(p, n_batches, 4) for i in range(20)]
         assert vals == want, (p, len(vals), len(want))
     kb.close()
+
+
+def test_native_consumer_reads_every_row_once_across_a_broker_kill(cluster):
+    """The engine's C++ consumer (csrc/engine/kafka_consumer.cpp) on the replicated cluster:
+    TXB1 batches produced with acks=all while the leader of two partitions is SIGKILLed; the
+    consumer follows the new leaders (metadata refresh) and every row lands exactly once --
+    it only ever sees records below the high watermark, so nothing it read can vanish."""
+    import numpy as np
+
+    from ccfd_demo_summit_amd.contracts import TxBatch
+    from ccfd_demo_summit_amd.data import generate
+    from ccfd_demo_summit_amd.ingest.native_consumer import NativeKafkaConsumer
+    boot = ",".join(f"127.0.0.1:{p}" for p in cluster["bports"])
+    deadline = time.time() + 30
+    while len(json.loads(_text(f"http://127.0.0.1:{cluster['cport']}/metadata"))["nodes"]) < 3:
+        assert time.time() < deadline
+        time.sleep(0.1)
+    P, per, step = 6, 3000, 250
+    kb = KafkaBroker(boot, idempotent=True, connect_wait_s=10)
+    kb.RETRIES = 14
+    kb.default_acks = -1
+    kb.create_topic("odh-demo", P)
+    X, _ = generate(P * per, seed=3)
+    kc = NativeKafkaConsumer.for_arrays(boot, "odh-demo", {p: 0 for p in range(P)}, capacity=per + 100).start()
+    try:
+        for k in range(per // step):
+            if k == (per // step) // 2:
+                victim = kb.leader_of("odh-demo", 0)
+                os.killpg(cluster["procs"][f"b{victim}"].pid, signal.SIGKILL)
+            for p in range(P):
+                s = p * per + k * step
+                ids = np.arange(s, s + step, dtype=np.uint64)
+                kb.produce("odh-demo", TxBatch(ids=ids, customer=(ids % 1000).astype(np.uint32),
+                                               features=X[s:s + step]).encode(), partition=p)
+        t0 = time.time()
+        while kc.stats()["rows"] < P * per and time.time() - t0 < 60:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        st = kc.stats()
+        assert st["rows"] == P * per, (st, kc.last_error())
+        for p in range(P):
+            _f, ids, _c = kc.arrays[p]
+            np.testing.assert_array_equal(ids[:per], np.arange(p * per, (p + 1) * per, dtype=np.uint64))
+    finally:
+        kc.stop()
+        kc.close()
+        kb.close()
