@@ -279,7 +279,8 @@ def main(argv=None):
         if a.kafka_replicated:
             # the controller + one broker process per node, each with its own durable log
             ctl_cmd = [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller", "--host", "127.0.0.1",
-                       "--port", str(ctl_port), "--data-dir", str(Path(kdir) / "controller")]
+                       "--port", str(ctl_port), "--brokers", str(a.kafka_nodes),
+                       "--data-dir", str(Path(kdir) / "controller")]
             procs.append(Proc("kafka-controller", ctl_cmd, env, log_dir))
             wait_port(ctl_port, 60)
             for i in range(a.kafka_nodes):

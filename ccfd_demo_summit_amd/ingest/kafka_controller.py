@@ -57,7 +57,10 @@ class ControllerState:
     an injected clock)."""
 
     def __init__(self, data_dir: Optional[str] = None, session_s: float = 1.5, rf: int = 3,
-                 rebalance_s: float = 5.0, clock=time.monotonic):
+                 rebalance_s: float = 5.0, clock=time.monotonic, expected_brokers: int = 0):
+        """``expected_brokers``: topics are created only once that many brokers registered
+        (a topic created while one of three brokers is up would get replication factor 1)."""
+        self.expected_brokers = int(expected_brokers)
         self.data_dir = data_dir
         self.session_s = float(session_s)
         self.rf = int(rf)
@@ -137,10 +140,16 @@ class ControllerState:
                     "topics": dict(self.topics),
                     "parts": {k: dict(v) for k, v in self.parts.items()}}
 
+    def can_create(self) -> bool:
+        with self.lock:
+            return len(self.nodes) >= self.expected_brokers
+
     def create_topic(self, name: str, partitions: int) -> bool:
         with self.lock:
             if name in self.topics:
                 return False
+            if not self.can_create():
+                raise RuntimeError(f"{len(self.nodes)} of {self.expected_brokers} brokers registered")
             ids = sorted(self.nodes) or [1]
             rf = max(1, min(self.rf, len(ids)))
             for p in range(max(1, int(partitions))):
@@ -304,7 +313,10 @@ def make_app(state: ControllerState):
 
     async def topics(request):
         d = await request.json()
-        created = state.create_topic(d["name"], int(d["partitions"]))
+        try:
+            created = state.create_topic(d["name"], int(d["partitions"]))
+        except RuntimeError as e:                    # not every broker is up yet: ask again
+            return web.json_response({"error": str(e)}, status=503)
         return web.json_response({"created": created, **state.metadata()})
 
     async def metadata(_request):
@@ -352,9 +364,11 @@ def main(argv=None):
     ap.add_argument("--data-dir", default=None)
     ap.add_argument("--session-s", type=float, default=1.5, help="broker heartbeat timeout")
     ap.add_argument("--rf", type=int, default=3, help="replication factor of new topics")
+    ap.add_argument("--brokers", type=int, default=0,
+                    help="create topics only once this many brokers registered (0 = whatever is up)")
     a = ap.parse_args(argv)
     from aiohttp import web
-    state = ControllerState(a.data_dir, session_s=a.session_s, rf=a.rf)
+    state = ControllerState(a.data_dir, session_s=a.session_s, rf=a.rf, expected_brokers=a.brokers)
     print(f"[kafka-controller] :{a.port} topics {len(state.topics)} meta epoch {state.meta_epoch}", flush=True)
     web.run_app(make_app(state), host=a.host, port=a.port, print=None, access_log=None)
 

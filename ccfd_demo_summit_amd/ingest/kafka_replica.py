@@ -153,9 +153,19 @@ class ReplicaManager:
         except BrokerError:
             return 0
 
-    async def create_topic(self, name: str, partitions: int) -> None:
-        async with self._session.post(f"{self.controller}/topics", json={"name": name, "partitions": int(partitions)}) as r:
-            d = await r.json()
+    async def create_topic(self, name: str, partitions: int, wait_s: float = 30.0) -> None:
+        """Through the controller; while it waits for the cluster's brokers to register (503),
+        asked again every 200 ms."""
+        t_end = time.monotonic() + wait_s
+        while True:
+            async with self._session.post(f"{self.controller}/topics",
+                                          json={"name": name, "partitions": int(partitions)}) as r:
+                d = await r.json()
+                if r.status == 200:
+                    break
+            if time.monotonic() > t_end:
+                raise BrokerError(f"controller: {d.get('error')}")
+            await asyncio.sleep(0.2)
         self._apply(d)
 
     async def commit_offsets(self, group: str, entries) -> None:

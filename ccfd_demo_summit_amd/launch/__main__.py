@@ -4,7 +4,9 @@
     python -m ccfd_demo_summit_amd.launch <service> [options]
 
 services:
-  kafka-lite   Kafka-protocol broker, --nodes N listeners (dev/CI stand-in for Strimzi)
+  kafka-lite   Kafka-protocol broker, --nodes N listeners (dev/CI stand-in for Strimzi); with
+               --controller URL --node-id N|auto: one broker process of a replicated cluster
+  kafka-controller  membership / leader election / ISR / offsets of a replicated kafka-lite cluster
   seldon       fraud model predict() server            (port 8000, modelfull)
   usertask     user-task model predict() server         (port 5000, ccfd-seldon-model)
   kie          business-process server (KIE REST)       (port 8090)
@@ -145,6 +147,22 @@ def cmd_kafka_lite(a, cfg):
             "--retention-batches", str(a.retention_batches), "--fsync", a.fsync]
     if a.advertise:
         argv += ["--advertise", a.advertise]
+    if a.data_dir:
+        argv += ["--data-dir", a.data_dir]
+    if a.controller:                  # one broker process of a replicated cluster
+        node = a.node_id
+        if node in ("auto", "", None):
+            # StatefulSet pod <name>-k is node k + 1
+            from ..process.sharding import shard_from_env
+            node = str(shard_from_env(None) + 1)
+        argv += ["--node-id", str(node), "--controller", a.controller]
+    main(argv)
+
+
+def cmd_kafka_controller(a, cfg):
+    """The replicated kafka-lite cluster's controller (ingest/kafka_controller.py)."""
+    from ..ingest.kafka_controller import main
+    argv = ["--host", a.host, "--port", str(a.port or 9093), "--brokers", str(a.nodes if a.nodes > 1 else 0)]
     if a.data_dir:
         argv += ["--data-dir", a.data_dir]
     main(argv)
@@ -623,7 +641,7 @@ def parse_args(argv=None) -> argparse.Namespace:
         argv, cmd = argv[:i], argv[i + 1:]
     ap = argparse.ArgumentParser(prog="python -m ccfd_demo_summit_amd.launch", description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("service", choices=["kafka-lite", "seldon", "usertask", "kie", "notifier", "router",
+    ap.add_argument("service", choices=["kafka-lite", "kafka-controller", "seldon", "usertask", "kie", "notifier", "router",
                                         "engine", "producer", "demo", "store", "elastic", "supervise",
                                         "operator", "dlq-replay"])
     ap.add_argument("--config", default=None)
@@ -636,6 +654,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--metrics-port", type=int, default=9404, help="kafka-lite: Prometheus /metrics (0 = off)")
     ap.add_argument("--retention-batches", type=int, default=0,
                     help="kafka-lite: record batches kept per partition (0 = the broker default)")
+    ap.add_argument("--node-id", default=None,
+                    help="kafka-lite replicated: this broker's node id, or 'auto' (pod ordinal + 1)")
+    ap.add_argument("--controller", default=None,
+                    help="kafka-lite replicated: the controller's URL (launch kafka-controller)")
     ap.add_argument("--cr", default=None, help="operator: FraudDetection (or OpenDataHub) CR file")
     ap.add_argument("--render", default=None, help="operator: write Kubernetes manifests here ('-' = stdout)")
     ap.add_argument("--local", action="store_true", help="operator: reconcile the CR into local processes")

@@ -82,6 +82,7 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     state = os.path.abspath(state_dir)
     o = port_offset
     kafka_port = 9092 + o
+    ctl_port = 9290 + o                     # replicated kafka-lite's controller
     broker = (spec.kafka.bootstrap if not spec.kafka.deploy
               else ",".join(f"{host}:{kafka_port + i}" for i in range(spec.kafka.brokers)))
     K = max(1, spec.kie.shards)
@@ -100,7 +101,18 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     env.update(spec.env)
     w = ["--weights", spec.engine.weights] if spec.engine.weights else []
     svc: Dict[str, tuple] = {}
-    if spec.kafka.deploy:
+    if spec.kafka.deploy and spec.kafka.replicated:
+        # replica r is broker node r + 1 (its own port, log and metrics port) + one controller
+        svc["kafka-controller"] = (1, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller",
+                                                 "--host", host, "--port", str(ctl_port),
+                                                 "--brokers", str(spec.kafka.brokers),
+                                                 "--data-dir", os.path.join(state, "kafka-controller")])
+        svc["kafka"] = (spec.kafka.brokers, lambda r: [
+            sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", host,
+            "--port", str(kafka_port + r), "--node-id", str(r + 1), "--controller", f"http://{host}:{ctl_port}",
+            "--metrics-port", str(9404 + o + r), "--data-dir", os.path.join(state, f"kafka-lite-{r + 1}"),
+            "--fsync", spec.kafka.fsync])
+    elif spec.kafka.deploy:
         svc["kafka"] = (1, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite",
                                       "--nodes", str(spec.kafka.brokers), "--port", str(kafka_port), "--host", host,
                                       "--partitions", str(spec.kafka.partitions), "--metrics-port", str(9404 + o),
@@ -147,7 +159,8 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
 
     def http(port, path, stride=1):
         return lambda r: ("http", f"http://{host}:{port + o + stride * r}{path}")
-    probes = {"kafka": (lambda r: ("tcp", host, kafka_port), 20),
+    probes = {"kafka": (lambda r: ("tcp", host, kafka_port + (r if spec.kafka.replicated else 0)), 20),
+              "kafka-controller": (lambda r: ("http", f"http://{host}:{ctl_port}/health/ping"), 20),
               "usertask": (http(5000, "/health/ping"), 30), "seldon": (http(8000, "/health/ping"), 60),
               "kie": (http(8090, "/services/rest/server"), 30), "notifier": (http(8080, "/health/ping"), 30),
               "engine": (http(8091, "/health/ping", 16), 120), "router": (http(8191, "/health/ping"), 30)}

@@ -98,7 +98,45 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
     out.append({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "ccfd-env"}, "data": data})
     weights = ["--weights", spec.engine.weights] if spec.engine.weights else []
 
-    if spec.kafka.deploy:
+    if spec.kafka.deploy and spec.kafka.replicated:
+        # replicated kafka-lite (ingest/kafka_replica.py): `brokers` broker pods, each its own
+        # durable log on its own claim, replication factor min(3, brokers); pod k is node k + 1
+        # (--node-id auto), advertised under the headless service; the controller pod keeps
+        # membership, leaders / ISR and the committed offsets (ingest/kafka_controller.py)
+        name = f"{spec.kafka.cluster_name}-kafka"
+        ctl = f"{name}-controller"
+        cc = _container(spec, "controller", LAUNCH + ["kafka-controller", "--port", "9093", "--nodes",
+                                                      str(spec.kafka.brokers), "--data-dir", "/var/lib/kafka-controller"],
+                        ports=[{"containerPort": 9093, "name": "http"}], envfrom=False,
+                        probe=("/health/ping", 9093, 20))
+        cc["volumeMounts"] = [{"name": "controller-data", "mountPath": "/var/lib/kafka-controller"}]
+        ctl_extra = {"volumeClaimTemplates": [{"metadata": {"name": "controller-data"}, "spec": {
+            "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}}]}
+        out.append(_workload("StatefulSet", ctl, ctl, 1, [cc], annotations=_scrape("/metrics", 9093),
+                             extra_spec=ctl_extra))
+        out.append(_service(ctl, ctl, [{"name": "http", "port": 9093, "targetPort": 9093}]))
+        kc = _container(
+            spec, "kafka", LAUNCH + ["kafka-lite", "--node-id", "auto", "--controller", f"http://{ctl}:9093",
+                                     "--port", "9092", "--advertise", f"$(POD_NAME).{name}-brokers",
+                                     "--data-dir", "/var/lib/kafka-lite", "--fsync", spec.kafka.fsync],
+            ports=[{"containerPort": 9092, "name": "broker"}, {"containerPort": 9404, "name": "metrics"}],
+            env={"CCFD_KAFKA_PARTITIONS": spec.kafka.partitions}, envfrom=False, probe=(None, 9092, 20))
+        kc["env"].append({"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}})
+        kc["volumeMounts"] = [{"name": "kafka-data", "mountPath": "/var/lib/kafka-lite"}]
+        extra = {"serviceName": f"{name}-brokers", "podManagementPolicy": "Parallel"}
+        vols = None
+        if spec.kafka.storage:
+            extra["volumeClaimTemplates"] = [{"metadata": {"name": "kafka-data"}, "spec": {
+                "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": spec.kafka.storage}}}}]
+        else:
+            vols = [{"name": "kafka-data", "emptyDir": {}}]
+        out.append(_workload("StatefulSet", name, name, spec.kafka.brokers, [kc], annotations=_scrape("/metrics", 9404),
+                             extra_spec=extra, volumes=vols))
+        out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": f"{name}-brokers"},
+                    "spec": {"clusterIP": "None", "selector": {"app": name},
+                             "ports": [{"name": "broker", "port": 9092, "targetPort": 9092}]}})
+        out.append(_service(f"{name}-bootstrap", name, [{"name": "broker", "port": 9092, "targetPort": 9092}]))
+    elif spec.kafka.deploy:
         # kafka-lite: one process, `brokers` listeners over a shared controller/store (the
         # Strimzi cluster of frauddetection_cr.yaml:71-77 in miniature)
         name = f"{spec.kafka.cluster_name}-kafka"
@@ -284,7 +322,8 @@ def validate(manifests: List[Dict[str, Any]]) -> List[str]:
     seen = set()
     workloads = []
     configmaps = {m["metadata"]["name"] for m in manifests if m.get("kind") == "ConfigMap"}
-    allowed_env = set(REFERENCE_ENV) | set(ENV_MAP) | {"HSA_ENABLE_IPC_MODE_LEGACY", "CCFD_KAFKA_PARTITIONS"}
+    allowed_env = set(REFERENCE_ENV) | set(ENV_MAP) | {"HSA_ENABLE_IPC_MODE_LEGACY", "CCFD_KAFKA_PARTITIONS",
+                                                     "POD_NAME"}   # (downward API: a broker pod's own name)
     for m in manifests:
         for k in ("apiVersion", "kind", "metadata"):
             if k not in m:

@@ -39,6 +39,9 @@ class KafkaSpec:
     storage: str = "50Gi"            # kafka-lite's durable logs (--data-dir): a PersistentVolumeClaim of
                                      # this size per broker pod; "" = emptyDir (survives container, not pod, restarts)
     fsync: str = "interval"          # kafka-lite flush policy: always | interval | never
+    replicated: bool = True          # brokers = separate pods, each its own log, replication factor 3, a
+                                     # controller for fail-over (ingest/kafka_controller.py) -- the
+                                     # reference's replicated Strimzi cluster; False = one pod, N listeners
 
 
 @dataclass
@@ -122,6 +125,9 @@ class FraudDetectionSpec:
                 raise SpecError("kafka.deploy is false but kafka.bootstrap is empty")
             return self.kafka.bootstrap
         host = f"{self.kafka.cluster_name}-kafka-brokers"
+        if self.kafka.replicated:           # one broker pod each: <sts>-<k>.<headless svc>:9092
+            sts = f"{self.kafka.cluster_name}-kafka"
+            return ",".join(f"{sts}-{i}.{host}:9092" for i in range(self.kafka.brokers))
         return ",".join(f"{host}:{9092 + i}" for i in range(self.kafka.brokers))
 
     def validate(self) -> "FraudDetectionSpec":

@@ -110,7 +110,8 @@ def cluster(tmp_path):
                 "--port", str(bports[k - 1]), "--node-id", str(k), "--controller", f"http://127.0.0.1:{cport}",
                 "--metrics-port", str(mports[k - 1]), "--data-dir", str(tmp_path / f"b{k}"), "--fsync", "interval"]
     start("ctl", [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller", "--host", "127.0.0.1",
-                  "--port", str(cport), "--data-dir", str(tmp_path / "ctl"), "--session-s", "1.0"])
+                  "--port", str(cport), "--data-dir", str(tmp_path / "ctl"), "--session-s", "1.0",
+                  "--brokers", "3"])
     _wait(cport)
     for k in (1, 2, 3):
         start(f"b{k}", broker_cmd(k))

@@ -58,8 +58,16 @@ def test_cr_fields_drive_the_rendering():
     assert c["command"][c["command"].index("--nproc-per-node") + 1] == "4"
     assert by[("Deployment", "modelfull-modelfull")]["spec"]["replicas"] == 3
     assert by[("Deployment", "ccd-fuse")]["spec"]["replicas"] == 2
-    kafka = by[("StatefulSet", "odh-message-bus-kafka")]["spec"]["template"]["spec"]["containers"][0]
-    assert len([p for p in kafka["ports"] if p["name"].startswith("broker")]) == 5
+    # replicated kafka-lite: 5 broker pods (one listener each) + the controller
+    sts = by[("StatefulSet", "odh-message-bus-kafka")]
+    kafka = sts["spec"]["template"]["spec"]["containers"][0]
+    assert sts["spec"]["replicas"] == 5 and [p["containerPort"] for p in kafka["ports"]] == [9092, 9404]
+    assert "--controller" in kafka["command"] and ("StatefulSet", "odh-message-bus-kafka-controller") in by
+    assert by[("Service", "odh-message-bus-kafka-brokers")]["spec"]["clusterIP"] == "None"
+    d["spec"]["kafka"]["replicated"] = False                 # one pod with 5 listeners
+    one = {(m["kind"], m["metadata"]["name"]): m for m in render(parse(d))}
+    kafka1 = one[("StatefulSet", "odh-message-bus-kafka")]["spec"]["template"]["spec"]["containers"][0]
+    assert len([p for p in kafka1["ports"] if p["name"].startswith("broker")]) == 5
     train = by[("Job", "ccfd-training")]["spec"]["template"]["spec"]["containers"][0]["command"]
     assert train[train.index("--nproc-per-node") + 1] == "4" and "gbdt" in train
 
@@ -91,7 +99,7 @@ def test_reference_opendatahub_cr_maps_onto_the_stack():
     assert spec.kafka.brokers == 3 and spec.kafka.cluster_name == "odh-message-bus"
     assert spec.training.deploy and spec.training.workers == 2 and spec.seldon.deploy and spec.monitoring.deploy
     assert any("zookeeper" in n for n in spec.notes) and any("notebook" in n for n in spec.notes)
-    assert spec.broker_url.startswith("odh-message-bus-kafka-brokers:9092")
+    assert spec.broker_url.startswith("odh-message-bus-kafka-0.odh-message-bus-kafka-brokers:9092")
     assert validate(render(spec)) == []
 
 
@@ -297,19 +305,26 @@ def _free_offset(bases, tries=200):
 
 
 def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
-    """Only the CR's kafka section deployed: the operator starts kafka-lite with 3 listeners
-    and a Kafka client produces to / fetches from it through the bootstrap list."""
+    """Only the CR's kafka section deployed: the operator starts the replicated kafka-lite
+    cluster (a controller + 3 broker processes) and a Kafka client produces to / fetches from
+    it through the bootstrap list."""
     from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
     d = _doc()
     for k in ("engine", "seldon", "usertask", "kie", "notifier", "producer", "monitoring"):
         d["spec"][k]["deploy"] = False
     d["spec"]["kafka"].update(brokers=3, partitions=6)
     spec = parse(d)
-    off = _free_offset([9092, 9093, 9094, 9404])       # parallel test workers: never a taken port
+    off = _free_offset([9092, 9093, 9094, 9404, 9405, 9406, 9290])   # parallel test workers: never a taken port
     op = LocalOperator(spec, workdir=str(ROOT), commands=None, grace_s=5, log=lambda m: None, port_offset=off,
                        state_dir=str(tmp_path / "state"))
     try:
-        assert op.reconcile()["kafka"]["ready"] == 1
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            st = op.reconcile()
+            if st["kafka"]["ready"] == 3 and st["kafka-controller"]["ready"] == 1:
+                break
+            time.sleep(0.5)
+        assert st["kafka"]["ready"] == 3 and st["kafka-controller"]["ready"] == 1
         bootstrap = ",".join(f"127.0.0.1:{9092 + off + i}" for i in range(3))
         kb = KafkaBroker(bootstrap, connect_wait_s=60.0)
         try:
