@@ -206,6 +206,8 @@ def main(argv=None):
     ap.add_argument("--settle", action="store_true",
                     help="after the drain, wait until no fraud process waits for its customer (outcomes final)")
     ap.add_argument("--notifier-seed", type=int, default=0, help="the simulated customers' seed")
+    ap.add_argument("--compare-to", default=None,
+                    help="a previous run's --out JSON over the same transactions: outcomes must be equal")
     ap.add_argument("--kafka-kill-at", type=float, default=0.0,
                     help="SIGKILL kafka-lite this many seconds into the window (0 = never) ...")
     ap.add_argument("--kafka-down-s", type=float, default=2.0,
@@ -536,6 +538,7 @@ def main(argv=None):
                    for k in ("fraud_started", "duplicates", "standard_started", "standard_duplicates", "active",
                              "notified", "waiting_customer", "fraud_instances_retained")}
             tot["outcomes"] = {k: sum(int(d["outcomes"].get(k, 0)) for d in per) for k in per[0]["outcomes"]}
+            tot["outcome_digest"] = f"{sum(int(d.get('outcome_digest') or '0', 16) for d in per) & (2**64 - 1):016x}"
             tot["per_shard"] = [{k: d.get(k) for k in ("shard", "fraud_started", "standard_started", "duplicates",
                                                       "standard_duplicates", "notified", "scored_to_started_us")}
                                 for d in per]
@@ -610,6 +613,14 @@ def main(argv=None):
         out["kie_notified_equals_fraud_started"] = int(stats["notified"]) >= int(stats["fraud_started"])
         oc = stats["outcomes"]
         out["customer_replies_applied"] = int(oc.get("approved_by_customer", 0)) + int(oc.get("cancelled", 0))
+        if a.compare_to:
+            # the same transactions (--count, same seeds) through a run with crashes: every fraud
+            # process must end with the outcome it had in the reference run
+            ref = json.loads(Path(a.compare_to).read_text())
+            out["same_outcomes_as"] = {
+                "run": a.compare_to, "outcomes_equal": ref["kie"]["outcomes"] == oc,
+                "digest_equal": ref["kie"].get("outcome_digest") == stats["outcome_digest"],
+                "reference_outcomes": ref["kie"]["outcomes"]}
         # ---- the reference dashboards against everything this deployment serves
         from ccfd_demo_summit_amd.metrics import promql
         series = []
@@ -634,7 +645,8 @@ def main(argv=None):
               and out["kie_fraud_started_equals_routed"] and not rep["unmatched"]
               and out["kie_duplicates"] == 0
               and out.get("kie_standard_plus_fraud_equals_incoming", True)
-              and out["kie_notified_equals_fraud_started"] and out.get("settled", True))
+              and out["kie_notified_equals_fraud_started"] and out.get("settled", True)
+              and all(out.get("same_outcomes_as", {"x": True}).get(k, True) for k in ("outcomes_equal", "digest_equal")))
         out["checks_passed"] = bool(ok)
     finally:
         for p in reversed(procs):

@@ -24,6 +24,7 @@ append-only journal").
 from __future__ import annotations
 
 import collections
+import hashlib
 import enum
 import heapq
 import itertools
@@ -112,6 +113,9 @@ class ProcessEngine:
         self._task_ids = itertools.count(1)
         self._lock = threading.RLock()
         self.outcome_counts: Dict[str, int] = {o.value: 0 for o in Outcome}
+        # order-independent digest of every fraud process's (transaction id, outcome): two runs
+        # over the same transactions -- one of them with crashes -- compare outcome for outcome
+        self.outcome_digest = 0
         self.standard_count = 0
         self.keep_completed = keep_completed
         self._completed_order: collections.deque = collections.deque()   # O(1) eviction
@@ -234,6 +238,7 @@ class ProcessEngine:
                     eng.outcome_counts[Outcome.INVESTIGATION.value] += 1
                 if inst.outcome is not None:
                     eng.outcome_counts[inst.outcome] = eng.outcome_counts.get(inst.outcome, 0) + 1
+                    eng._digest(inst)
                 if inst.notified or iid in notified:
                     inst.notified = True
                     eng.notified_count += 1
@@ -610,8 +615,14 @@ class ProcessEngine:
         inst.completed = self.clock()
         inst.timer_due = None
         self.outcome_counts[outcome.value] += 1
+        if inst.process_id == self.FRAUD:
+            self._digest(inst)
         self._log(inst)
         self._remember_completed(inst)
+
+    def _digest(self, inst: ProcessInstance) -> None:
+        h = hashlib.blake2b(f"{inst.variables.get('transaction_id')}:{inst.outcome}".encode(), digest_size=8)
+        self.outcome_digest = (self.outcome_digest + int.from_bytes(h.digest(), "little")) & 0xFFFFFFFFFFFFFFFF
 
     def _remember_completed(self, inst: ProcessInstance) -> None:
         if inst.process_id == self.STANDARD:

@@ -336,7 +336,8 @@ class KieServer:
                     "handoff_attribution": self.attribution(),
                     "active": sum(1 for i in e.instances.values() if i.state.value != "completed"),
                     "waiting_customer": sum(1 for i in e.instances.values() if i.state.value == "waiting_customer"),
-                    "outcomes": dict(e.outcome_counts), "next_instance_id": None}
+                    "outcomes": dict(e.outcome_counts), "outcome_digest": f"{e.outcome_digest:016x}",
+                    "next_instance_id": None}
         return web.json_response(body)
 
     async def metrics(self, _request):

@@ -152,7 +152,9 @@ def test_kill_and_restart_both_sides_keeps_every_reply_once(tmp_path):
         waiting = lambda: any(i.state.value == "waiting_customer" for i in state["eng"].instances.values())
         while waiting() and time.monotonic() - t0 < 30:
             pump(0.1)
-        out = dict(eng.outcome_counts), signals, state["ns"].stats(), eng.notified_count
+        out = dict(eng.outcome_counts), signals, state["ns"].stats(), eng.notified_count, eng.outcome_digest
+        # the digest is rebuilt from the journal: a recovered engine reports the same one
+        assert ProcessEngine.recover(j, notification_timeout_s=5.0).outcome_digest == eng.outcome_digest
         state["pub"].close(1.0)
         state["rpub"].close(1.0)
         kb.close()
@@ -160,8 +162,9 @@ def test_kill_and_restart_both_sides_keeps_every_reply_once(tmp_path):
         return out
     (d1 := tmp_path / "a").mkdir()
     (d2 := tmp_path / "b").mkdir()
-    oc_ref, sig_ref, _ns_ref, _ = run(False, d1)
-    oc, sig, _ns, notified = run(True, d2)
+    oc_ref, sig_ref, _ns_ref, _, dg_ref = run(False, d1)
+    oc, sig, _ns, notified, dg = run(True, d2)
     assert sum(oc_ref.values()) == n and oc == oc_ref, (oc, oc_ref)
+    assert dg == dg_ref != 0                 # outcome for outcome, not only the totals
     assert sig["ok"] == sig_ref["ok"] == oc_ref["approved_by_customer"] + oc_ref["cancelled"]
     assert notified >= n
