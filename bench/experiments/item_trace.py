@@ -1,0 +1,103 @@
+"""Per-item phase table of the persistent G20 GBDT kernel.
+
+Reads the device ring the experiment build dumps (`scripts/build_ab.py --name itrace --src
+kernels/score_gbdt_g32_persist.hip --src engine/engine.cpp -D CCFD_EXP_ITEM_TRACE`, run with
+`CCFD_LIB_PATH=.../ab/itrace.so CCFD_ITEM_TRACE_OUT=<prefix>`; one file per persistent engine
+torn down, `<prefix>.<k>`).  Each record is one claimed item, stamped by its workgroup's thread 0
+with the 100 MHz wall clock:
+
+    claim      the work_next atomic
+    posted     waiting until the item's micro-batch is posted + reading its descriptor
+    load       the first 64-row chunk's zero-copy load (issue -> data in registers)
+    score      every chunk of the item (the next chunk's load overlaps the current one's trees)
+    complete   counters, vmcnt drain of the outputs, system-scope release, ticket
+    gap        from this item's ticket to the same workgroup's next claim
+
+    python bench/experiments/item_trace.py gpurun_out/r5f/itrace.0 [--json out.json]
+"""
+import argparse
+import json
+import sys
+
+import numpy as np
+
+FIELDS = ("item", "wg", "t_claim", "t_claimed", "t_desc", "t_load", "t_scored", "t_done")
+TICK_US = 0.01                                    # s_memrealtime: 100 MHz
+
+
+def load(path: str) -> np.ndarray:
+    raw = np.fromfile(path, dtype=np.uint64)
+    n = int(raw[0])
+    rec = raw[1:].reshape(-1, len(FIELDS))
+    cap = rec.shape[0]
+    if n < cap:
+        rec = rec[:n]
+    else:                                         # ring: oldest first
+        k = n % cap
+        rec = np.concatenate([rec[k:], rec[:k]])
+    return rec.astype(np.int64)
+
+
+def analyse(rec: np.ndarray, skip_frac: float = 0.02) -> dict:
+    rec = rec[rec[:, 7] > 0]
+    rec = rec[np.argsort(rec[:, 2], kind="stable")]
+    lo = int(len(rec) * skip_frac)
+    rec = rec[lo: len(rec) - lo]
+    f = {k: rec[:, i] for i, k in enumerate(FIELDS)}
+    ph = {
+        "claim": f["t_claimed"] - f["t_claim"],
+        "posted": f["t_desc"] - f["t_claimed"],
+        "load": f["t_load"] - f["t_desc"],
+        "score": f["t_scored"] - f["t_load"],
+        "complete": f["t_done"] - f["t_scored"],
+    }
+    # gap to the same workgroup's next claim
+    gap = []
+    for wg in np.unique(f["wg"]):
+        s = rec[f["wg"] == wg]
+        if len(s) > 1:
+            gap.append(s[1:, 2] - s[:-1, 7])
+    ph["gap"] = np.concatenate(gap) if gap else np.zeros(1, np.int64)
+    total = f["t_done"] - f["t_claim"]
+    span_us = (f["t_done"].max() - f["t_claim"].min()) * TICK_US
+    wgs = len(np.unique(f["wg"]))
+    out = {"items": int(len(rec)), "workgroups": wgs, "span_us": round(span_us, 1),
+           "items_per_s": round(len(rec) / (span_us * 1e-6), 1) if span_us > 0 else None,
+           "item_us": {"p50": round(float(np.median(total)) * TICK_US, 2),
+                       "mean": round(float(total.mean()) * TICK_US, 2)},
+           "phases_us": {}}
+    mean_total = float(total.mean() + ph["gap"].mean())
+    for k, v in ph.items():
+        v = v[v >= 0]
+        if len(v) == 0:
+            continue
+        out["phases_us"][k] = {"p10": round(float(np.percentile(v, 10)) * TICK_US, 2),
+                               "p50": round(float(np.median(v)) * TICK_US, 2),
+                               "p90": round(float(np.percentile(v, 90)) * TICK_US, 2),
+                               "mean": round(float(v.mean()) * TICK_US, 2),
+                               "share_of_cycle": round(float(v.mean()) / mean_total, 3)}
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("paths", nargs="+")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args(argv)
+    res = {}
+    for p in a.paths:
+        res[p] = analyse(load(p))
+        r = res[p]
+        print(f"{p}: {r['items']} items over {r['workgroups']} workgroups, {r['items_per_s']:.3g} items/s, "
+              f"item p50 {r['item_us']['p50']} us")
+        print(f"  {'phase':<10} {'p10':>8} {'p50':>8} {'p90':>8} {'mean':>8} {'share':>7}")
+        for k, v in r["phases_us"].items():
+            print(f"  {k:<10} {v['p10']:8.2f} {v['p50']:8.2f} {v['p90']:8.2f} {v['mean']:8.2f} {v['share_of_cycle']:7.1%}")
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(res, fh, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -44,6 +44,9 @@
 
 namespace ccfd {
 void set_error(const std::string& e);
+#ifdef CCFD_EXP_ITEM_TRACE
+int item_trace_dump(const char* path);     // score_gbdt_g32_persist.hip, experiment build only
+#endif
 }
 
 namespace {
@@ -539,6 +542,13 @@ class Engine {
       if (s.use_flag) { s.busy = false; s.use_flag = false; s.done_ptr = nullptr; }
     }
     persist_halt();
+#ifdef CCFD_EXP_ITEM_TRACE
+    if (const char* out = std::getenv("CCFD_ITEM_TRACE_OUT")) {   // experiment build only
+      static int k = 0;
+      const std::string path = std::string(out) + "." + std::to_string(k++);
+      ccfd::item_trace_dump(path.c_str());
+    }
+#endif
     // teardown: nothing useful can be done about a failed release, so results are dropped
     (void)hipStreamDestroy(pstream);
     (void)hipFree(pdev);

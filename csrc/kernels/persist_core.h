@@ -160,7 +160,11 @@ __device__ __forceinline__ void persist_emit_flagged(const ccfd_persist_args& a,
 __device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const ccfd_persist_desc& sdesc, int slot,
                                                int C) {
   // system-scope release of this item's outputs, relaxed ticket (see common.h signal_done)
+#ifdef CCFD_EXP_AGENT_RELEASE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // experiment build only: cost of the system scope
+#else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned left =
       __hip_atomic_fetch_sub(&a.dev->remaining[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;

@@ -3,10 +3,29 @@
 // are staged into LDS ONCE per resident workgroup (a launch per micro-batch re-stages them
 // in every workgroup), and a claimed item is 4 waves x `cpw` 64-row chunks, the next chunk
 // of a wave in flight while the current one is evaluated.
+#include <cstdio>
+#include <vector>
+
 #include "g32_core.h"
 #include "persist_core.h"
 
 namespace ccfd {
+
+#ifdef CCFD_EXP_ITEM_TRACE
+// Experiment build only (scripts/build_ab.py -D CCFD_EXP_ITEM_TRACE; never in the default
+// library): thread 0 stamps each claimed item's phases -- claim atomic, wait for the posting +
+// descriptor, first chunk's load, scoring, release + ticket -- into a device ring that the
+// engine dumps at teardown (engine.cpp persist_free; bench/experiments/item_trace.py reads it).
+struct ItemTrace {
+  unsigned long long item, wg, t_claim, t_claimed, t_desc, t_load, t_scored, t_done;
+};
+constexpr unsigned kItemTraceCap = 1u << 17;
+__device__ ItemTrace g_item_trace[kItemTraceCap];
+__device__ unsigned long long g_item_trace_n;
+#define CCFD_ITRACE(stmt) stmt
+#else
+#define CCFD_ITRACE(stmt)
+#endif
 
 template <int D, bool kR, bool kGL, bool kG20>
 __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args a) {
@@ -58,8 +77,10 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
     else fr = valid && fresh && (p >= a.threshold);
     if (valid) {
+#ifndef CCFD_EXP_NO_OUTPUTS                                // experiment build only: cost of the output stream
       if (d.proba) st_g(d.proba + row, p);
       if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
+#endif
       if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
       atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
     }
@@ -88,7 +109,20 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   };
 
   for (;;) {
+#ifdef CCFD_EXP_ITEM_TRACE
+    unsigned long long t_claim = 0, t_claimed = 0, t_desc = 0, t_load = 0, t_scored = 0;
+    if (tid == 0) {
+      t_claim = wall_clock64();
+      const unsigned long long it =
+          __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t_claimed = wall_clock64();
+      s_cmd = persist_wait_item(a, C, posted_cache, it, sdesc);
+      s_item = it;
+      t_desc = wall_clock64();
+    }
+#else
     if (tid == 0) persist_claim(a, C, posted_cache, sdesc, s_item, s_cmd);
+#endif
     __syncthreads();
     if (s_cmd) break;
     const ccfd_persist_desc d = sdesc;                     // registers: no LDS wait in the epilogue
@@ -123,6 +157,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
         const int chunk = c0 + kG32Waves * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
         G32Row cur_row = pre;
+        CCFD_ITRACE(if (k == 0) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); if (tid == 0) t_load = wall_clock64(); })
         if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kG32Waves, lane, pre);
         score_chunk(d, slot, n, chunk, cur_row);
       }
@@ -133,7 +168,16 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     } else {
       full_item(std::integral_constant<int, 4>{});        // 1024-row items (engine accepts 256/512/1024)
     }
+    CCFD_ITRACE(if (tid == 0) t_scored = wall_clock64();)
     item_flush(d, slot);
+#ifdef CCFD_EXP_ITEM_TRACE
+    if (tid == 0) {
+      const unsigned long long k =
+          __hip_atomic_fetch_add(&g_item_trace_n, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g_item_trace[k % kItemTraceCap] = ItemTrace{s_item, blockIdx.x, t_claim, t_claimed, t_desc, t_load, t_scored,
+                                                  (unsigned long long)wall_clock64()};
+    }
+#endif
   }
 }
 
@@ -315,6 +359,22 @@ static int launch_persist_g32_d(const ccfd_persist_args& a, int grid, hipStream_
   return (a.flags & CCFD_ARG_WIRE_G20) ? launch_persist_g32_f<D, true>(a, grid, s)
                                        : launch_persist_g32_f<D, false>(a, grid, s);
 }
+
+#ifdef CCFD_EXP_ITEM_TRACE
+// host: the item ring -> <path> as {u64 n, ItemTrace[kItemTraceCap]} (record k at k % cap)
+int item_trace_dump(const char* path) {
+  unsigned long long n = 0;
+  std::vector<ItemTrace> v(kItemTraceCap);
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_item_trace_n), sizeof(n)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_item_trace), sizeof(ItemTrace) * v.size()) != hipSuccess) return -1;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return -1;
+  std::fwrite(&n, sizeof(n), 1, f);
+  std::fwrite(v.data(), sizeof(ItemTrace), v.size(), f);
+  std::fclose(f);
+  return 0;
+}
+#endif
 
 int launch_persist_gbdt_g32(const ccfd_persist_args& a, int grid, hipStream_t s) {
   if (a.gbdt_trees <= 0 || a.gbdt_depth < 1 || a.gbdt_depth > 8) return -2;
