@@ -437,7 +437,7 @@ def main(argv=None):
             except Exception:                               # the broker is down right now
                 lag = None
             samples.append({"t_s": round(now - t_w0, 1), "tx_s": round((r_now - last_r) / (now - last_t), 1),
-                            "lag_msgs": lag})
+                            "lag_msgs": lag, "loadavg_1m": round(os.getloadavg()[0], 1)})
             if a.kafka_replicated:                          # the reference dashboard's panel
                 under = 0
                 for mp in kmetrics:
@@ -561,6 +561,9 @@ def main(argv=None):
         out["kie_fraud_started_equals_routed"] = int(stats["fraud_started"]) == int(fraud_all)
         out["kie_duplicates"] = stats["duplicates"]
         out["standard_mode"] = a.standard_mode
+        # the host this topology shares: every service and engine rank runs on these CPUs
+        out["host_cpus"] = {"affinity": len(os.sched_getaffinity(0)), "machine": os.cpu_count(),
+                            "loadavg_1m_max": max((sm.get("loadavg_1m", 0) for sm in samples), default=None)}
         if a.standard_mode == "process":
             # every transaction started exactly one process: standard + fraud == incoming
             t_k = time.time()

@@ -7,7 +7,12 @@ arrival (oldest row committed to the pinned ring) -> submit (descriptor posted /
 landed (completion record in host memory) -> complete (retired).  Its latency splits into
 
 * ``queued``  = submit - arrival: the row waited for the scoring thread to post it, and
-* ``flight``  = landed - submit:  PCIe + kernel + completion record.
+* ``flight``  = landed - submit:  PCIe + kernel + completion record; where the persistent
+  kernel stamped the batch (dev_start / dev_end, device clock) it splits further into
+  ``device_exec`` = dev_end - dev_start (first item claimed -> last item done: the GPU's own
+  time on the batch, which grows when several resident kernels share the device) and
+  ``flight_other`` = the rest (doorbell + claim before the first item, completion record ->
+  host after the last).
 
 The queued part is cut against the scoring thread's own timeline: time INSIDE a native
 ``run()`` call (the thread was polling; a batch can still wait there for a free in-flight slot
@@ -89,7 +94,10 @@ def attribute(path: str, tail_q: float = 0.99) -> dict:
     flight = (b["t_landed"] - b["t_submit"]).astype(np.int64)
     thr = np.quantile(total, tail_q)
     sel = np.nonzero(total >= thr)[0]
-    parts = {k: [] for k in ("in_run", "outside_run", "task", "gc", "held", "interpreter", "flight")}
+    dev = (b["dev_end"] - b["dev_start"]).astype(np.int64) if "dev_end" in b.dtype.names else np.zeros(len(b), np.int64)
+    has_dev = dev > 0
+    parts = {k: [] for k in ("in_run", "outside_run", "task", "gc", "held", "interpreter", "flight",
+                             "device_exec", "flight_other")}
     for i in sel:
         lo, hi = int(b["t_arrival"][i]), int(b["t_submit"][i])
         inside = _overlap(lo, hi, runs)
@@ -119,6 +127,9 @@ def attribute(path: str, tail_q: float = 0.99) -> dict:
         parts["held"].append(t_held)
         parts["interpreter"].append(max(0, outside - t_task - t_gc - t_held))
         parts["flight"].append(int(flight[i]))
+        de = int(dev[i]) if has_dev[i] else 0
+        parts["device_exec"].append(de)
+        parts["flight_other"].append(max(0, int(flight[i]) - de))
     us = lambda v: round(float(v) / 1e3, 1)
     gaps_all = runs[1:, 0] - runs[:-1, 1] if len(runs) > 1 else np.zeros(0, np.int64)
     return {
@@ -128,6 +139,8 @@ def attribute(path: str, tail_q: float = 0.99) -> dict:
                                  "max": us(total.max())},
         "queued_us": {"p50": us(np.quantile(queued, 0.5)), "p99": us(np.quantile(queued, 0.99))},
         "flight_us": {"p50": us(np.quantile(flight, 0.5)), "p99": us(np.quantile(flight, 0.99))},
+        "device_exec_us": ({"p50": us(np.quantile(dev[has_dev], 0.5)), "p99": us(np.quantile(dev[has_dev], 0.99)),
+                            "batches": int(has_dev.sum())} if has_dev.any() else None),
         f"tail_batches_ge_p{int(tail_q * 100)}": int(len(sel)),
         "tail_mean_breakdown_us": {k: us(np.mean(v)) for k, v in parts.items()},
         "scoring_thread": {

@@ -21,6 +21,8 @@ def test_attribution_splits_queue_time(tmp_path):
     a50 = int(b["t_arrival"][50])
     b["t_submit"][50] = a50 + 3000 * us
     b["t_landed"][50] = b["t_submit"][50] + 20 * us
+    b["dev_start"] = b["t_submit"] + 2 * us           # device clock: its own epoch, only differences count
+    b["dev_end"] = b["dev_start"] + 15 * us
     runs = [(0, a50 - 10 * us, 0), (a50 + 2990 * us, 10 ** 12, 0)]
     gc = [(a50 + 100 * us, 0, 2), (a50 + 2900 * us, 1, 2)]
     np.savez(tmp_path / "rank0.npz", batches=b, runs=np.array(runs, np.int64), tasks=np.zeros((0, 2), np.int64),
@@ -31,3 +33,5 @@ def test_attribution_splits_queue_time(tmp_path):
     assert r["batches"] == 100 and r["tail_batches_ge_p99"] == 1
     assert 2790 <= bd["gc"] <= 2810 and bd["outside_run"] >= 2990 and bd["in_run"] <= 10
     assert bd["flight"] == 20.0
+    assert bd["device_exec"] == 15.0 and bd["flight_other"] == 5.0
+    assert r["device_exec_us"]["p99"] == 15.0 and r["device_exec_us"]["batches"] == 100
