@@ -351,6 +351,11 @@ class EpochPipeline:
                 return False
             self._progress_until(lambda: not self.reducer.busy(), progress, timeout_s,
                                  "X2 all-reduce did not complete: a peer rank stopped ticking")
+        if not block and self.pending is not None and not self.engine.epoch_complete(self.pending[1]):
+            # the closed epoch still has batches in flight -- or the engine is HELD (hand-off
+            # back-pressure: the serving thread retires nothing until the caller's next step
+            # releases it), so waiting here would wait for the caller itself: skip the tick
+            return False
         self._complete()
         self.ticks += 1
         if self.pending is not None:

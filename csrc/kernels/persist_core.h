@@ -182,10 +182,10 @@ __device__ __forceinline__ void persist_ticket(const ccfd_persist_args& a, const
 }
 
 // All threads, after the item's rows are scored: flush the item's counters (LDS state is
-// reset for the next item), publish its outputs and take the slot's ticket; the last
-// ticket completes the micro-batch for the host.
-__device__ __forceinline__ void persist_item_done(const ccfd_persist_args& a, EpilogueLds& epi,
-                                                  const ccfd_persist_desc& sdesc, int slot, int C, int tid) {
+// reset for the next item) and drain every wave's output stores; the item is then ready for
+// its ticket (persist_ticket, one thread).
+__device__ __forceinline__ void persist_item_close(const ccfd_persist_args& a, EpilogueLds& epi,
+                                                   const ccfd_persist_desc& sdesc, int tid) {
   __syncthreads();
   unsigned long long* cnt = a.counters[sdesc.epoch & 1];
   if (tid < 2 * kNB) {
@@ -202,9 +202,15 @@ __device__ __forceinline__ void persist_item_done(const ccfd_persist_args& a, Ep
     }
     epi.rows = 0; epi.fraud = 0; epi.psum_e6 = 0;
   }
-  // completion: publish this item's outputs, take a ticket, last ticket signals the host
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+}
+
+// persist_item_close, then the ticket: publish this item's outputs, the last ticket of the
+// micro-batch signals the host.
+__device__ __forceinline__ void persist_item_done(const ccfd_persist_args& a, EpilogueLds& epi,
+                                                  const ccfd_persist_desc& sdesc, int slot, int C, int tid) {
+  persist_item_close(a, epi, sdesc, tid);
   if (tid == 0) persist_ticket(a, sdesc, slot, C);
 }
 

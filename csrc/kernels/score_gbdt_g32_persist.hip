@@ -101,14 +101,28 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     }
     fraud = rows = stale = 0;
     psum = 0;
+#ifdef CCFD_EXP_TICKET_OVERLAP
+    persist_item_close(a, epi, d, tid);                   // ticket: next iteration, beside the claim
+#else
     persist_item_done(a, epi, d, slot, C, tid);
+#endif
   };
   auto k7_start = [&](unsigned long long it, int slot) __attribute__((always_inline)) {
     if (it % (unsigned long long)C == 0 && tid == 0)      // K7: micro-batch start (item 0 claimed first)
       __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
+#ifdef CCFD_EXP_TICKET_OVERLAP
+  // the previous item's ticket (release + ticket) is taken by wave 1 while wave 0 claims the
+  // next item: both before the barrier, so a claim that waits for the next posting never
+  // holds back the ticket that completes the batch the host is waiting on
+  ccfd_persist_desc prev_d{};
+  int prev_slot = -1;
+#endif
   for (;;) {
+#ifdef CCFD_EXP_TICKET_OVERLAP
+    if (tid == 64 && prev_slot >= 0) persist_ticket(a, prev_d, prev_slot, C);
+#endif
 #ifdef CCFD_EXP_ITEM_TRACE
     unsigned long long t_claim = 0, t_claimed = 0, t_desc = 0, t_load = 0, t_scored = 0;
     if (tid == 0) {
@@ -170,6 +184,10 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     }
     CCFD_ITRACE(if (tid == 0) t_scored = wall_clock64();)
     item_flush(d, slot);
+#ifdef CCFD_EXP_TICKET_OVERLAP
+    prev_d = d;
+    prev_slot = slot;
+#endif
 #ifdef CCFD_EXP_ITEM_TRACE
     if (tid == 0) {
       const unsigned long long k =

@@ -2,6 +2,7 @@
 cluster"): broadcast weights bit-identical, all-reduced counters == global truth."""
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -166,6 +167,29 @@ class _FakeEpochEngine(_FakeEngine):
 
     def score(self, rows):
         self.counters[self.cur][0] += rows
+
+
+def test_nonblocking_tick_skips_an_incomplete_epoch():
+    """A held engine (hand-off back-pressure) retires nothing until the caller's next step
+    releases it: a non-blocking tick must return instead of waiting for the closed epoch
+    (the GPU back-pressure test stalled 60 s there), and tick once the epoch completed."""
+    from ccfd_demo_summit_amd.parallel import CounterReducer, DistContext, EpochPipeline
+
+    class Held(_FakeEpochEngine):
+        done = False
+
+        def epoch_complete(self, flip_count):
+            return self.done
+    eng = Held()
+    ep = EpochPipeline(eng, CounterReducer(DistContext(0, 1, 0, torch.device("cpu"), "none"), torch.device("cpu")))
+    assert ep.tick(block=False) and ep.ticks == 1          # opens the first epoch
+    eng.score(10)
+    t0 = time.monotonic()
+    assert ep.tick(block=False) is False and ep.ticks == 1   # closed epoch incomplete: skipped
+    assert time.monotonic() - t0 < 1.0
+    eng.done = True
+    assert ep.tick(block=False) and ep.ticks == 2
+    ep.finish()
 
 
 def _skewed_worker(rank, world, port, q):
