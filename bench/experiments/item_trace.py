@@ -7,7 +7,8 @@ torn down, `<prefix>.<k>`).  Each record is one claimed item, stamped by its wor
 with the 100 MHz wall clock:
 
     claim      the work_next atomic
-    posted     waiting until the item's micro-batch is posted + reading its descriptor
+    wait_post  waiting until the item's micro-batch is posted (device mirror of the doorbell)
+    desc       the per-item agent-scope acquire + the descriptor's atomic loads
     load       the first 64-row chunk's zero-copy load (issue -> data in registers)
     score      every chunk of the item (the next chunk's load overlaps the current one's trees)
     complete   counters, vmcnt drain of the outputs, system-scope release, ticket
@@ -21,14 +22,18 @@ import sys
 
 import numpy as np
 
-FIELDS = ("item", "wg", "t_claim", "t_claimed", "t_desc", "t_load", "t_scored", "t_done")
+FIELDS = ("item", "wg", "t_claim", "t_claimed", "t_seen", "t_desc", "t_load", "t_scored", "t_done")
 TICK_US = 0.01                                    # s_memrealtime: 100 MHz
 
 
 def load(path: str) -> np.ndarray:
     raw = np.fromfile(path, dtype=np.uint64)
     n = int(raw[0])
-    rec = raw[1:].reshape(-1, len(FIELDS))
+    if (raw.size - 1) % len(FIELDS) == 0 and (raw.size - 1) // len(FIELDS) == 1 << 17:
+        rec = raw[1:].reshape(-1, len(FIELDS))
+    else:                                         # the first layout (pass r5f): no t_seen
+        old = raw[1:].reshape(-1, len(FIELDS) - 1)
+        rec = np.insert(old, FIELDS.index("t_seen"), old[:, FIELDS.index("t_claimed")], axis=1)
     cap = rec.shape[0]
     if n < cap:
         rec = rec[:n]
@@ -39,14 +44,15 @@ def load(path: str) -> np.ndarray:
 
 
 def analyse(rec: np.ndarray, skip_frac: float = 0.02) -> dict:
-    rec = rec[rec[:, 7] > 0]
+    rec = rec[rec[:, FIELDS.index("t_done")] > 0]
     rec = rec[np.argsort(rec[:, 2], kind="stable")]
     lo = int(len(rec) * skip_frac)
     rec = rec[lo: len(rec) - lo]
     f = {k: rec[:, i] for i, k in enumerate(FIELDS)}
     ph = {
         "claim": f["t_claimed"] - f["t_claim"],
-        "posted": f["t_desc"] - f["t_claimed"],
+        "wait_post": f["t_seen"] - f["t_claimed"],
+        "desc": f["t_desc"] - f["t_seen"],
         "load": f["t_load"] - f["t_desc"],
         "score": f["t_scored"] - f["t_load"],
         "complete": f["t_done"] - f["t_scored"],
@@ -56,12 +62,15 @@ def analyse(rec: np.ndarray, skip_frac: float = 0.02) -> dict:
     for wg in np.unique(f["wg"]):
         s = rec[f["wg"] == wg]
         if len(s) > 1:
-            gap.append(s[1:, 2] - s[:-1, 7])
-    ph["gap"] = np.concatenate(gap) if gap else np.zeros(1, np.int64)
+            gap.append(s[1:, 2] - s[:-1, FIELDS.index("t_done")])
+    gap = np.concatenate(gap) if gap else np.zeros(1, np.int64)
+    idle = gap >= int(100 / TICK_US)              # >= 100 us: the device had no posted work (phase ends)
+    ph["gap"] = gap[~idle]
     total = f["t_done"] - f["t_claim"]
     span_us = (f["t_done"].max() - f["t_claim"].min()) * TICK_US
     wgs = len(np.unique(f["wg"]))
     out = {"items": int(len(rec)), "workgroups": wgs, "span_us": round(span_us, 1),
+           "idle_gaps_ge_100us": int(idle.sum()), "idle_us_total": round(float(gap[idle].sum()) * TICK_US, 1),
            "items_per_s": round(len(rec) / (span_us * 1e-6), 1) if span_us > 0 else None,
            "item_us": {"p50": round(float(np.median(total)) * TICK_US, 2),
                        "mean": round(float(total.mean()) * TICK_US, 2)},

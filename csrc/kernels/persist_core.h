@@ -67,7 +67,9 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
 // slot / DMA staging buffer -- before they are read).
 __device__ __forceinline__ void persist_read_desc(const ccfd_persist_args& a, unsigned long long b,
                                                   ccfd_persist_desc& sdesc) {
+#ifndef CCFD_EXP_NO_ACQUIRE                  // experiment build only: cost of the per-item acquire
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
   const unsigned long long* d = reinterpret_cast<const unsigned long long*>(a.dev->desc + (b % (unsigned long long)a.ring));
   sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

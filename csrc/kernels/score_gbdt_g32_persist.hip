@@ -17,7 +17,7 @@ namespace ccfd {
 // descriptor, first chunk's load, scoring, release + ticket -- into a device ring that the
 // engine dumps at teardown (engine.cpp persist_free; bench/experiments/item_trace.py reads it).
 struct ItemTrace {
-  unsigned long long item, wg, t_claim, t_claimed, t_desc, t_load, t_scored, t_done;
+  unsigned long long item, wg, t_claim, t_claimed, t_seen, t_desc, t_load, t_scored, t_done;
 };
 constexpr unsigned kItemTraceCap = 1u << 17;
 __device__ ItemTrace g_item_trace[kItemTraceCap];
@@ -124,13 +124,25 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     if (tid == 64 && prev_slot >= 0) persist_ticket(a, prev_d, prev_slot, C);
 #endif
 #ifdef CCFD_EXP_ITEM_TRACE
-    unsigned long long t_claim = 0, t_claimed = 0, t_desc = 0, t_load = 0, t_scored = 0;
+    unsigned long long t_claim = 0, t_claimed = 0, t_seen = 0, t_desc = 0, t_load = 0, t_scored = 0;
     if (tid == 0) {
       t_claim = wall_clock64();
       const unsigned long long it =
           __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       t_claimed = wall_clock64();
-      s_cmd = persist_wait_item(a, C, posted_cache, it, sdesc);
+      // persist_wait_item, split: the wait for the posting, then the descriptor read
+      const unsigned long long b = it / (unsigned long long)C;
+      s_cmd = 0;
+      unsigned sleep_n = 1;
+      while (posted_cache <= b) {
+        posted_cache = __hip_atomic_load(&a.dev->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (posted_cache > b) break;
+        if (__hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { s_cmd = 1; break; }
+        for (unsigned k = 0; k < sleep_n; ++k) __builtin_amdgcn_s_sleep(1);
+        sleep_n = sleep_n < 8 ? sleep_n * 2 : 8;
+      }
+      t_seen = wall_clock64();
+      if (!s_cmd) persist_read_desc(a, b, sdesc);
       s_item = it;
       t_desc = wall_clock64();
     }
@@ -192,7 +204,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     if (tid == 0) {
       const unsigned long long k =
           __hip_atomic_fetch_add(&g_item_trace_n, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      g_item_trace[k % kItemTraceCap] = ItemTrace{s_item, blockIdx.x, t_claim, t_claimed, t_desc, t_load, t_scored,
+      g_item_trace[k % kItemTraceCap] = ItemTrace{s_item, blockIdx.x, t_claim, t_claimed, t_seen, t_desc, t_load, t_scored,
                                                   (unsigned long long)wall_clock64()};
     }
 #endif
