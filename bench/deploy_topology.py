@@ -57,7 +57,20 @@ sys.path.insert(0, str(ROOT))
 PY = sys.executable
 
 
-_PORT_CURSOR = [20000 + (os.getpid() * 37) % 20000]
+def _port_base() -> int:
+    """Service ports come from below the kernel's ephemeral range: a port handed out here and
+    bound later (a restarted broker re-binds its own) must not meanwhile become the local port
+    of some outgoing connection (a restarted broker's metrics port was, once: EADDRINUSE)."""
+    try:
+        lo, _hi = (int(x) for x in Path("/proc/sys/net/ipv4/ip_local_port_range").read_text().split())
+    except (OSError, ValueError):
+        lo = 32768
+    top = max(2048, min(lo, 65535) - 1024)             # leave room below the ephemeral range
+    bottom = max(1024, top - 12000)
+    return bottom + (os.getpid() * 37) % max(1, top - bottom - 2000)
+
+
+_PORT_CURSOR = [_port_base()]
 
 
 def free_ports(n: int, contiguous: int = 1) -> List[int]:
@@ -219,6 +232,8 @@ def main(argv=None):
                          "replication factor 3) + the controller (ingest/kafka_controller.py); producers "
                          "use acks=all; --kafka-kill-at then SIGKILLs broker --kafka-kill-node")
     ap.add_argument("--kafka-kill-node", type=int, default=2, help="replicated: the broker node id to kill")
+    ap.add_argument("--kafka-rf", type=int, default=3,
+                    help="replicated: replication factor (1 = scale-out over the brokers, no copies)")
     ap.add_argument("--producer-acks", type=int, default=None, choices=[1, -1],
                     help="producers' acks (default: -1 with --kafka-replicated, else 1)")
     ap.add_argument("--producer-max-in-flight", type=int, default=None,
@@ -266,7 +281,8 @@ def main(argv=None):
                  "n_gpus": 1 if a.rehearsal else a.ranks, "ranks": a.ranks, "rehearsal": a.rehearsal,
                  "fmt": a.fmt, "producers": a.producers, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
                  "model": a.model, "kie_shards": K, "kafka_replicated": a.kafka_replicated,
-                 "producer_acks": acks, "producer_max_in_flight": inflight}
+                 "producer_acks": acks, "producer_max_in_flight": inflight,
+                 "kafka_rf": a.kafka_rf if a.kafka_replicated else None}
     import tempfile
     kdir = tempfile.mkdtemp(prefix="ccfd-kafka-lite-")          # durable logs + committed offsets
     out["kafka_durable"] = {"fsync": a.fsync} if not a.kafka_memory else False
@@ -281,7 +297,7 @@ def main(argv=None):
         if a.kafka_replicated:
             # the controller + one broker process per node, each with its own durable log
             ctl_cmd = [PY, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller", "--host", "127.0.0.1",
-                       "--port", str(ctl_port), "--brokers", str(a.kafka_nodes),
+                       "--port", str(ctl_port), "--brokers", str(a.kafka_nodes), "--rf", str(a.kafka_rf),
                        "--data-dir", str(Path(kdir) / "controller")]
             procs.append(Proc("kafka-controller", ctl_cmd, env, log_dir))
             wait_port(ctl_port, 60)
@@ -627,16 +643,25 @@ def main(argv=None):
         # ---- the reference dashboards against everything this deployment serves
         from ccfd_demo_summit_amd.metrics import promql
         series = []
+        scrape_errors = []
+
+        def scrape(url, job, **kw):
+            try:
+                return promql.scrape(url, job, **kw)
+            except OSError as e:                    # a service that is down: recorded, not fatal
+                scrape_errors.append(f"{url}: {e}")
+                return []
         for r in range(a.ranks):
-            series += promql.scrape(f"http://127.0.0.1:{router_base + r}/prometheus", "ccfd-pods")
-            series += promql.scrape(f"http://127.0.0.1:{model_base + r}/prometheus", "ccfd-model",
-                                    instance=f"engine-{r}:8000")   # k8s: <pod ip>:8000 (operator/render.py)
+            series += scrape(f"http://127.0.0.1:{router_base + r}/prometheus", "ccfd-pods")
+            series += scrape(f"http://127.0.0.1:{model_base + r}/prometheus", "ccfd-model",
+                             instance=f"engine-{r}:8000")   # k8s: <pod ip>:8000 (operator/render.py)
         for p_ in kie_ports:
-            series += promql.scrape(f"http://127.0.0.1:{p_}/rest/metrics", "ccfd-pods")
+            series += scrape(f"http://127.0.0.1:{p_}/rest/metrics", "ccfd-pods")
         for mp in kmetrics:
-            series += promql.scrape(f"http://127.0.0.1:{mp}/metrics", "ccfd-pods")
+            series += scrape(f"http://127.0.0.1:{mp}/metrics", "ccfd-pods")
         if a.kafka_replicated:
-            series += promql.scrape(f"http://127.0.0.1:{ctl_port}/metrics", "ccfd-pods")
+            series += scrape(f"http://127.0.0.1:{ctl_port}/metrics", "ccfd-pods")
+        out["scrape_errors"] = scrape_errors
         fx = json.loads((ROOT / "tests/fixtures/reference_dashboard_exprs.json").read_text())
         exprs = {k: [e["expr"] for e in v] for k, v in fx["dashboards"].items() if k != "SparkMetrics.json"}
         rep = promql.check(exprs, series)
@@ -649,6 +674,7 @@ def main(argv=None):
               and out["kie_duplicates"] == 0
               and out.get("kie_standard_plus_fraud_equals_incoming", True)
               and out["kie_notified_equals_fraud_started"] and out.get("settled", True)
+              and not scrape_errors and out.get("under_replicated_final", 0) == 0
               and all(out.get("same_outcomes_as", {"x": True}).get(k, True) for k in ("outcomes_equal", "digest_equal")))
         out["checks_passed"] = bool(ok)
     finally:

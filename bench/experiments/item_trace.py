@@ -26,21 +26,51 @@ FIELDS = ("item", "wg", "t_claim", "t_claimed", "t_seen", "t_desc", "t_load", "t
 TICK_US = 0.01                                    # s_memrealtime: 100 MHz
 
 
-def load(path: str) -> np.ndarray:
-    raw = np.fromfile(path, dtype=np.uint64)
-    n = int(raw[0])
-    if (raw.size - 1) % len(FIELDS) == 0 and (raw.size - 1) // len(FIELDS) == 1 << 17:
-        rec = raw[1:].reshape(-1, len(FIELDS))
-    else:                                         # the first layout (pass r5f): no t_seen
-        old = raw[1:].reshape(-1, len(FIELDS) - 1)
-        rec = np.insert(old, FIELDS.index("t_seen"), old[:, FIELDS.index("t_claimed")], axis=1)
+ITEM_CAP, DB_CAP, DB_FIELDS = 1 << 17, 1 << 16, 8
+
+
+def _ring(rec: np.ndarray, n: int) -> np.ndarray:
     cap = rec.shape[0]
     if n < cap:
-        rec = rec[:n]
-    else:                                         # ring: oldest first
-        k = n % cap
-        rec = np.concatenate([rec[k:], rec[:k]])
-    return rec.astype(np.int64)
+        return rec[:n]
+    k = n % cap                                   # ring: oldest first
+    return np.concatenate([rec[k:], rec[:k]])
+
+
+def load(path: str, doorbell: bool = False) -> np.ndarray:
+    raw = np.fromfile(path, dtype=np.uint64)
+    n = int(raw[0])
+    item_words = ITEM_CAP * len(FIELDS)
+    if raw.size in (1 + item_words, 2 + item_words + DB_CAP * DB_FIELDS):
+        rec = raw[1:1 + item_words].reshape(-1, len(FIELDS))
+    else:                                         # the first layout (pass r5f): no t_seen, no doorbell
+        old = raw[1:].reshape(-1, len(FIELDS) - 1)
+        rec = np.insert(old, FIELDS.index("t_seen"), old[:, FIELDS.index("t_claimed")], axis=1)
+    if doorbell:
+        if raw.size != 2 + item_words + DB_CAP * DB_FIELDS:
+            return np.zeros((0, DB_FIELDS), np.int64)
+        ndb = int(raw[1 + item_words])
+        db = raw[2 + item_words:].reshape(-1, DB_FIELDS)
+        return _ring(db, ndb).astype(np.int64)
+    return _ring(rec, n).astype(np.int64)
+
+
+def doorbell(db: np.ndarray, t_lo: int, t_hi: int) -> dict:
+    """Doorbell cycles that found new postings, inside the items' time window: the poll's PCIe
+    round trip, the descriptor copy + publish, batches delivered per cycle, and the interval
+    between deliveries."""
+    db = db[(db[:, 0] >= t_lo) & (db[:, 0] <= t_hi)]
+    if len(db) < 2:
+        return {"cycles": int(len(db))}
+    rt = (db[:, 1] - db[:, 0]) * TICK_US
+    cp = (db[:, 4] - db[:, 1]) * TICK_US
+    nb = db[:, 2] - db[:, 3]
+    iv = np.diff(db[:, 4]) * TICK_US
+    q = lambda v: {"p50": round(float(np.median(v)), 2), "p90": round(float(np.percentile(v, 90)), 2),
+                   "mean": round(float(v.mean()), 2)}
+    return {"cycles": int(len(db)), "poll_round_trip_us": q(rt), "desc_copy_publish_us": q(cp),
+            "batches_per_cycle": q(nb.astype(float)), "interval_between_deliveries_us": q(iv),
+            "backlog_seen_ge2_share": round(float((nb >= 2).mean()), 3)}
 
 
 def analyse(rec: np.ndarray, skip_frac: float = 0.02) -> dict:
@@ -95,13 +125,20 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     res = {}
     for p in a.paths:
-        res[p] = analyse(load(p))
+        items = load(p)
+        res[p] = analyse(items)
+        db = load(p, doorbell=True)
+        if len(db):
+            res[p]["doorbell"] = doorbell(db, int(items[:, FIELDS.index("t_claim")].min()),
+                                          int(items[:, FIELDS.index("t_done")].max()))
         r = res[p]
         print(f"{p}: {r['items']} items over {r['workgroups']} workgroups, {r['items_per_s']:.3g} items/s, "
               f"item p50 {r['item_us']['p50']} us")
         print(f"  {'phase':<10} {'p10':>8} {'p50':>8} {'p90':>8} {'mean':>8} {'share':>7}")
         for k, v in r["phases_us"].items():
             print(f"  {k:<10} {v['p10']:8.2f} {v['p50']:8.2f} {v['p90']:8.2f} {v['mean']:8.2f} {v['share_of_cycle']:7.1%}")
+        if "doorbell" in r:
+            print("  doorbell", json.dumps(r["doorbell"]))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(res, fh, indent=1)

@@ -1,0 +1,123 @@
+"""Produce-only throughput of the replicated kafka-lite: a controller, N broker
+processes (durable), P producer processes (TXB1 by default) for T seconds, no engine.  Runs on
+a CPU box; prints one JSON line with the producers' total tx/s and each producer's own line.
+
+    python bench/experiments/replicated_produce.py --producers 4 --seconds 10 --acks -1
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT / "bench"))
+sys.path.insert(0, str(ROOT))
+from deploy_topology import free_ports, wait_port  # noqa: E402
+
+PY = sys.executable
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--brokers", type=int, default=3)
+    ap.add_argument("--producers", type=int, default=4)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--acks", type=int, default=-1)
+    ap.add_argument("--max-in-flight", type=int, default=5)
+    ap.add_argument("--fmt", default="txb1")
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--single", action="store_true", help="the single-process durable broker instead")
+    ap.add_argument("--rf", type=int, default=3, help="replication factor of the topic (controller --rf)")
+    a = ap.parse_args(argv)
+    kdir = tempfile.mkdtemp(prefix="ccfd-repl-produce-")
+    ctl, = free_ports(1)
+    base, = free_ports(1, a.brokers)
+    mbase, = free_ports(1, a.brokers)
+    env = dict(os.environ, PYTHONPATH=str(ROOT), CCFD_KAFKA_BACKEND="kafka",
+               CCFD_KAFKA_PARTITIONS=str(a.partitions),
+               BROKER_URL=",".join(f"127.0.0.1:{base + i}" for i in range(a.brokers)))
+    procs = []
+    names = []
+    logs = []
+
+    def start(name, cmd):
+        names.append(name)
+        f = open(Path(kdir) / f"{name}.log", "w")
+        logs.append(f)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=f, stderr=subprocess.STDOUT))
+    try:
+        K = "ccfd_demo_summit_amd.ingest."
+        if a.single:
+            start("kafka-lite", [PY, "-m", K + "kafka_lite", "--host", "127.0.0.1", "--port", str(base),
+                                 "--nodes", str(a.brokers), "--partitions", str(a.partitions),
+                                 "--metrics-port", str(mbase), "--data-dir", kdir + "/single"])
+        else:
+            start("controller", [PY, "-m", K + "kafka_controller", "--host", "127.0.0.1", "--port", str(ctl),
+                                 "--brokers", str(a.brokers), "--rf", str(a.rf), "--data-dir", kdir + "/ctl"])
+            wait_port(ctl, 60)
+            for i in range(a.brokers):
+                start(f"broker{i + 1}", [PY, "-m", K + "kafka_lite", "--host", "127.0.0.1", "--port", str(base + i),
+                                         "--node-id", str(i + 1), "--controller", f"http://127.0.0.1:{ctl}",
+                                         "--metrics-port", str(mbase + i), "--data-dir", f"{kdir}/b{i + 1}"])
+        for i in range(a.brokers):
+            wait_port(base + i, 60)
+        from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+        kb = KafkaBroker(env["BROKER_URL"], connect_wait_s=60.0)
+        kb.create_topic("odh-demo", a.partitions)
+        kb.close()
+        prods = []
+        for i in range(a.producers):
+            f = open(Path(kdir) / f"producer{i}.log", "w+")
+            logs.append(f)
+            prods.append((subprocess.Popen(
+                [PY, "-m", "ccfd_demo_summit_amd.launch", "producer", "--fmt", a.fmt, "--batch", str(a.batch), "--count", "0",
+                 "--seconds", str(a.seconds), "--acks", str(a.acks), "--max-in-flight", str(a.max_in_flight),
+                 "--id-base", str((i + 1) << 40), "--seed-offset", str(i * 101)],
+                env=env, stdout=f, stderr=subprocess.STDOUT), f))
+        res = []
+        for p, f in prods:
+            p.wait(timeout=a.seconds + 180)
+            f.seek(0)
+            lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
+            res.append(json.loads(lines[-1]) if lines else {"error": "no result"})
+        import psutil
+        cpu = {}
+        for name, p in zip(names, procs):
+            try:
+                t = psutil.Process(p.pid).cpu_times()
+                cpu[name] = round(t.user + t.system, 1)
+            except psutil.Error:
+                cpu[name] = None
+        tot = sum(r.get("produced", 0) for r in res)
+        secs = max(r.get("seconds", a.seconds) for r in res)
+        print(json.dumps({"tx_s": round(tot / secs, 1), "produced": tot, "producers": a.producers,
+                          "acks": a.acks, "max_in_flight": a.max_in_flight, "replicated": not a.single, "rf": a.rf,
+                          "cpu_s": cpu, "per_producer": res}))
+    except BaseException:
+        for f in logs:
+            f.flush()
+        for lp in sorted(Path(kdir).glob("*.log")):
+            print(f"== {lp.name}\n" + lp.read_text()[-2000:], file=sys.stderr)
+        raise
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for f in logs:
+            f.close()
+        import shutil
+        shutil.rmtree(kdir, ignore_errors=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

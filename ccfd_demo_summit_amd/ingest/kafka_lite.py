@@ -92,6 +92,7 @@ class ClusterState:
         # long-polling fetches (Fetch max_wait / min_bytes): (topic, partition) -> futures woken
         # by the next append; the listeners share one event loop, so no cross-thread wake-up
         self.fetch_waiters: Dict[Tuple[str, int], set] = {}
+        self.replica_waiters: Dict[Tuple[str, int], set] = {}   # followers' long polls: woken on append
         self.long_polls = 0
         # durable store (write-behind): produce answers waiting for their write ticket, in
         # ticket order; the last ticket the store's writer reported written
@@ -319,14 +320,14 @@ class _KafkaConn(asyncio.BufferedProtocol):
         self.frame = None                          # dedicated buffer of the big frame in progress
         self.fw = 0
         self.transport = None
-        self.busy = False                          # awaiting a long-polling response
-        self.pending = None
+        self.outq = None                           # responses not yet written, in request order
+        self.draining = False
 
     # asyncio.BufferedProtocol
     def connection_made(self, transport):
         import collections
         self.transport = transport
-        self.pending = collections.deque()
+        self.outq = collections.deque()
         self.server._writers.add(self)
 
     def connection_lost(self, exc):
@@ -385,36 +386,48 @@ class _KafkaConn(asyncio.BufferedProtocol):
             self.w = tail
 
     def _handle(self, msg, owned: bool):
-        if self.busy:
-            self.pending.append(bytes(msg))
-            return
+        # every request is handled as it arrives -- a produce is appended at once, in request
+        # order -- and only its RESPONSE may wait (written to disk, acks=all behind the high
+        # watermark, a long poll): a pipelining producer's next batches are in the log while
+        # the first one's replicas catch up.  Responses leave in request order (outq).
         try:
             out = self.server._frame(msg)
         except Exception:                          # malformed request: drop the connection
             self.transport.close()
             return
-        if isinstance(out, (bytes, bytearray)):
-            self.transport.write(out)
+        if isinstance(out, (bytes, bytearray, list)):
+            if not self.outq:
+                self._write(out)
+            else:
+                self.outq.append(out)              # behind a response still waited for
             return
+        self.outq.append(asyncio.ensure_future(out))
+        if not self.draining:
+            self.draining = True
+            asyncio.ensure_future(self._drain())
+
+    def _write(self, out) -> None:
         if isinstance(out, list):
             self.transport.writelines(out)
-            return
-        self.busy = True
-        asyncio.ensure_future(self._finish(out))
+        else:
+            self.transport.write(out)
 
-    async def _finish(self, coro):
+    async def _drain(self):
         try:
-            out = await coro
-            if isinstance(out, list):
-                self.transport.writelines(out)
-            else:
-                self.transport.write(out)
-        except Exception:
-            self.transport.close()
-            return
-        self.busy = False
-        while self.pending and not self.busy and not self.transport.is_closing():
-            self._handle(memoryview(bytearray(self.pending.popleft())), owned=True)
+            while self.outq:
+                item = self.outq[0]
+                if isinstance(item, asyncio.Future):
+                    try:
+                        item = await item
+                    except Exception:
+                        self.transport.close()
+                        return
+                self.outq.popleft()
+                if self.transport.is_closing():
+                    return
+                self._write(item)
+        finally:
+            self.draining = False
 
     def close(self):
         if self.transport is not None:
@@ -544,8 +557,8 @@ class KafkaLiteServer:
         if cl.replica is not None:
             cl.replica.on_written(tps)          # the leader's LEO moved: maybe the HW too
 
-    def _wake_fetches(self, tp) -> None:
-        ws = self.cluster.fetch_waiters.pop(tp, None)
+    def _wake_fetches(self, tp, waiters=None) -> None:
+        ws = (self.cluster.fetch_waiters if waiters is None else waiters).pop(tp, None)
         if ws:
             for f in ws:
                 if not f.done():
@@ -677,6 +690,8 @@ class KafkaLiteServer:
                         ticket = max(ticket, t)     # answered (and fetchable) once written
                     else:
                         self._wake_fetches((topic, p))
+                    if rep is not None:
+                        self._wake_fetches((topic, p), self.cluster.replica_waiters)
                     self.metrics.messages_in.labels(topic, "Kafka").inc(nrec)
                     self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
                 except OutOfOrderSequence:
@@ -742,7 +757,7 @@ class KafkaLiteServer:
     async def _fetch_later(self, reqs, max_bytes: int, max_wait_ms: int, replica_id: int = -1):
         fut = asyncio.get_running_loop().create_future()
         tps = [(t, p) for t, ps in reqs for p, _o, _m in ps]
-        waiters = self.cluster.fetch_waiters
+        waiters = self.cluster.fetch_waiters if replica_id < 0 else self.cluster.replica_waiters
         for tp in tps:
             waiters.setdefault(tp, set()).add(fut)
         self.cluster.long_polls += 1
@@ -780,9 +795,14 @@ class KafkaLiteServer:
                 hw = self.store.end_offset(topic, p)
                 upto = None
                 limit = hw
+                unwritten = False
                 if rep is not None:
                     if replica_id >= 0:
                         rep.on_replica_fetch(replica_id, topic, p, off)
+                        # followers copy the log as appended, written or not: replication runs
+                        # beside the leader's own write instead of after it
+                        unwritten = True
+                        limit = self.store.log_end(topic, p)
                     else:
                         # consumers see data below the HW; an offset between the HW and the log
                         # end is valid (a new leader's HW catches up) -- an empty answer, not
@@ -794,7 +814,8 @@ class KafkaLiteServer:
                     self.metrics.failed_fetch.labels(topic, "Kafka").inc()
                     ok = False
                     continue
-                rb = self.store.fetch_parts(topic, p, off, max(1, min(pmax, budget)), upto) if budget > 0 else []
+                rb = (self.store.fetch_parts(topic, p, off, max(1, min(pmax, budget)), upto, unwritten)
+                      if budget > 0 else [])
                 n = sum(len(b) for b in rb)
                 budget -= n
                 pr.append((p, ERR_NONE, hw, rb))

@@ -36,6 +36,7 @@ import asyncio
 import heapq
 import json
 import os
+import socket
 import struct
 import time
 import uuid
@@ -378,27 +379,45 @@ class ReplicaManager:
             if not tps or leader not in self.nodes:
                 return
             host, port = self.nodes[leader]
+            loop = asyncio.get_running_loop()
+            sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            sock.setblocking(False)
             try:
-                reader, writer = await asyncio.open_connection(host, port)
+                await loop.sock_connect(sock, (host, port))
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             except OSError:
+                sock.close()
                 await asyncio.sleep(0.1)
                 continue
+
+            async def recv_exact(n: int) -> bytearray:
+                # straight into one buffer of the response's size: the fetched batches are
+                # stored as views of it (no stream-buffer copies of replicated bytes)
+                buf = bytearray(n)
+                mv = memoryview(buf)
+                got = 0
+                while got < n:
+                    k = await loop.sock_recv_into(sock, mv[got:])
+                    if k == 0:
+                        raise ConnectionError("replica fetch: leader closed the connection")
+                    got += k
+                return buf
             try:
                 while True:
                     tps = self._followed().get(leader, [])
                     if not tps:
                         return
                     by_topic: Dict[str, List[Tuple[int, int]]] = {}
-                    for t, p in tps:
-                        by_topic.setdefault(t, []).append((p, self._leo((t, p))))
+                    for t, p in tps:                # fetch from this replica's log end, written or not
+                        by_topic.setdefault(t, []).append((p, self.store.log_end(t, p)))
                     body = (Writer().i32(self.node_id).i32(200).i32(1).i32(64 << 20).i8(0)
                             .array(sorted(by_topic.items()), lambda w, kv: w.string(kv[0]).array(
                                 kv[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).i32(16 << 20))).build())
                     corr += 1
                     hdr = Writer().i16(FETCH).i16(FETCH_V).i32(corr).string(f"replica-{self.node_id}").build()
-                    writer.write(struct.pack(">i", len(hdr) + len(body)) + hdr + body)
-                    size = struct.unpack(">i", await reader.readexactly(4))[0]
-                    r = Reader(await reader.readexactly(size))
+                    await loop.sock_sendall(sock, struct.pack(">i", len(hdr) + len(body)) + hdr + body)
+                    size = struct.unpack(">i", await recv_exact(4))[0]
+                    r = Reader(memoryview(await recv_exact(size)))
                     if r.i32() != corr:
                         raise BrokerError("replica fetch: correlation mismatch")
                     r.i32()                                          # throttle
@@ -408,7 +427,6 @@ class ReplicaManager:
                         x.array(lambda y: (y.i64(), y.i64()))
                         return idx, err, hw, x.view_()
                     resp = r.array(lambda x: (x.string(), x.array(part)))
-                    tickets = []
                     moved = False
                     for t, parts in resp:
                         for p, err, hw, recs in parts:
@@ -421,20 +439,18 @@ class ReplicaManager:
                                 moved = True                          # not the leader any more
                                 continue
                             if recs is not None and len(recs):
-                                n, ticket = self.store.append_replica(t, p, recs)
+                                self.store.append_replica(t, p, recs)
                                 self.replicated_bytes += len(recs)
-                                if ticket:
-                                    tickets.append(ticket)
                             self.hw[(t, p)] = max(self.hw.get((t, p), 0), min(int(hw), self.store.log_end(t, p)))
                     self.replica_fetches += 1
-                    if tickets and self.server is not None:
-                        await self.server._written_ticket(max(tickets))   # durable before the next fetch
+                    # the next fetch reports this log end to the leader at once, without waiting
+                    # for the local write: an acknowledged batch is then on every in-sync
+                    # replica (in memory, written by each broker's writer right behind) -- a
+                    # single broker's death loses nothing acknowledged, as in Kafka, where a
+                    # follower's append is its page cache
                     if moved:
                         await asyncio.sleep(0.05)
-            except (OSError, asyncio.IncompleteReadError, BrokerError, ConnectionError):
+            except (OSError, BrokerError, ConnectionError):
                 await asyncio.sleep(0.05)                            # leader away: metadata will move it
             finally:
-                try:
-                    writer.close()
-                except Exception:                                    # noqa: BLE001
-                    pass
+                sock.close()

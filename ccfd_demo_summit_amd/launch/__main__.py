@@ -162,7 +162,8 @@ def cmd_kafka_lite(a, cfg):
 def cmd_kafka_controller(a, cfg):
     """The replicated kafka-lite cluster's controller (ingest/kafka_controller.py)."""
     from ..ingest.kafka_controller import main
-    argv = ["--host", a.host, "--port", str(a.port or 9093), "--brokers", str(a.nodes if a.nodes > 1 else 0)]
+    argv = ["--host", a.host, "--port", str(a.port or 9093), "--brokers", str(a.nodes if a.nodes > 1 else 0),
+            "--rf", str(a.replication_factor)]
     if a.data_dir:
         argv += ["--data-dir", a.data_dir]
     main(argv)
@@ -646,6 +647,8 @@ def parse_args(argv=None) -> argparse.Namespace:
                                         "operator", "dlq-replay"])
     ap.add_argument("--config", default=None)
     ap.add_argument("--nodes", type=int, default=1, help="kafka-lite: broker listeners (port, port+1, ...)")
+    ap.add_argument("--replication-factor", type=int, default=3,
+                    help="kafka-controller: copies of every partition of a new topic")
     ap.add_argument("--advertise", default=None, help="kafka-lite: broker host name clients are given")
     ap.add_argument("--data-dir", default=None,
                     help="kafka-lite: durable log + committed-offset directory (restart recovers from it)")

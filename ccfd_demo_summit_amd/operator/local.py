@@ -106,6 +106,7 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
         svc["kafka-controller"] = (1, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller",
                                                  "--host", host, "--port", str(ctl_port),
                                                  "--brokers", str(spec.kafka.brokers),
+                                                 "--rf", str(spec.kafka.replication_factor),
                                                  "--data-dir", os.path.join(state, "kafka-controller")])
         svc["kafka"] = (spec.kafka.brokers, lambda r: [
             sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", host,

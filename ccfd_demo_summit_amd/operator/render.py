@@ -106,7 +106,9 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
         name = f"{spec.kafka.cluster_name}-kafka"
         ctl = f"{name}-controller"
         cc = _container(spec, "controller", LAUNCH + ["kafka-controller", "--port", "9093", "--nodes",
-                                                      str(spec.kafka.brokers), "--data-dir", "/var/lib/kafka-controller"],
+                                                      str(spec.kafka.brokers), "--replication-factor",
+                                                      str(spec.kafka.replication_factor),
+                                                      "--data-dir", "/var/lib/kafka-controller"],
                         ports=[{"containerPort": 9093, "name": "http"}], envfrom=False,
                         probe=("/health/ping", 9093, 20))
         cc["volumeMounts"] = [{"name": "controller-data", "mountPath": "/var/lib/kafka-controller"}]

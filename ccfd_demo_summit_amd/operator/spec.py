@@ -39,9 +39,11 @@ class KafkaSpec:
     storage: str = "50Gi"            # kafka-lite's durable logs (--data-dir): a PersistentVolumeClaim of
                                      # this size per broker pod; "" = emptyDir (survives container, not pod, restarts)
     fsync: str = "interval"          # kafka-lite flush policy: always | interval | never
-    replicated: bool = True          # brokers = separate pods, each its own log, replication factor 3, a
-                                     # controller for fail-over (ingest/kafka_controller.py) -- the
-                                     # reference's replicated Strimzi cluster; False = one pod, N listeners
+    replicated: bool = True          # brokers = separate pods, each its own log, a controller for
+                                     # fail-over (ingest/kafka_controller.py) -- the reference's Strimzi
+                                     # cluster of 3 brokers; False = one pod, N listeners
+    replication_factor: int = 3      # copies of every partition (1 = scale-out only, Kafka's default for
+                                     # auto-created topics; 3 = a broker loss loses nothing acknowledged)
 
 
 @dataclass

@@ -15,6 +15,17 @@
 
 namespace ccfd {
 
+#ifdef CCFD_EXP_ITEM_TRACE
+// Experiment build only: one record per doorbell cycle that found new postings -- poll issued,
+// poll returned, posted count seen, count mirrored before, mirror published (wall clock).
+struct DoorbellTrace {
+  unsigned long long t_poll, t_polled, posted, mirrored, t_mirrored, pad0, pad1, pad2;
+};
+constexpr unsigned kDoorbellTraceCap = 1u << 16;
+static __device__ DoorbellTrace g_db_trace[kDoorbellTraceCap];
+static __device__ unsigned long long g_db_trace_n;
+#endif
+
 // Workgroup 0, wave 0: mirror host descriptors into device memory until `stop`.  The whole
 // wave copies: lane l copies word l % W of descriptor (mirrored + l / W), so up to 10 newly
 // posted descriptors cost ONE PCIe round trip instead of one per word (a thread-0 copy loop
@@ -28,9 +39,15 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
   unsigned sleep_n = 1;
   for (;;) {
     unsigned long long p = 0;
+#ifdef CCFD_EXP_ITEM_TRACE
+    const unsigned long long t_poll = wall_clock64();
+#endif
     if (lane == 0) p = __hip_atomic_load(&a.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     p = __shfl(p, 0);
     if (p > mirrored) {
+#ifdef CCFD_EXP_ITEM_TRACE
+      const unsigned long long t_polled = wall_clock64(), m0 = mirrored;
+#endif
       const unsigned long long nb = min(p - mirrored, (unsigned long long)kPer);
       const int bi = lane / kW, wi = lane % kW;
       if (bi < (int)nb) {
@@ -45,6 +62,14 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       mirrored += nb;
       if (lane == 0) __hip_atomic_store(&a.dev->posted, mirrored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef CCFD_EXP_ITEM_TRACE
+      if (lane == 0) {
+        const unsigned long long k =
+            __hip_atomic_fetch_add(&g_db_trace_n, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g_db_trace[k % kDoorbellTraceCap] =
+            DoorbellTrace{t_poll, t_polled, p, m0, (unsigned long long)wall_clock64(), 0, 0, 0};
+      }
+#endif
       sleep_n = 1;
       continue;
     }

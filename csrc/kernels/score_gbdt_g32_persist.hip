@@ -391,7 +391,8 @@ static int launch_persist_g32_d(const ccfd_persist_args& a, int grid, hipStream_
 }
 
 #ifdef CCFD_EXP_ITEM_TRACE
-// host: the item ring -> <path> as {u64 n, ItemTrace[kItemTraceCap]} (record k at k % cap)
+// host: the item ring -> <path> as {u64 n, ItemTrace[kItemTraceCap]} (record k at k % cap), then the
+// doorbell ring (persist_core.h)
 int item_trace_dump(const char* path) {
   unsigned long long n = 0;
   std::vector<ItemTrace> v(kItemTraceCap);
@@ -401,6 +402,14 @@ int item_trace_dump(const char* path) {
   if (!f) return -1;
   std::fwrite(&n, sizeof(n), 1, f);
   std::fwrite(v.data(), sizeof(ItemTrace), v.size(), f);
+  // then the doorbell ring: {u64 n, DoorbellTrace[kDoorbellTraceCap]}
+  std::vector<DoorbellTrace> db(kDoorbellTraceCap);
+  unsigned long long ndb = 0;
+  if (hipMemcpyFromSymbol(&ndb, HIP_SYMBOL(g_db_trace_n), sizeof(ndb)) == hipSuccess &&
+      hipMemcpyFromSymbol(db.data(), HIP_SYMBOL(g_db_trace), sizeof(DoorbellTrace) * db.size()) == hipSuccess) {
+    std::fwrite(&ndb, sizeof(ndb), 1, f);
+    std::fwrite(db.data(), sizeof(DoorbellTrace), db.size(), f);
+  }
   std::fclose(f);
   return 0;
 }
