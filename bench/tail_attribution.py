@@ -12,7 +12,10 @@ landed (completion record in host memory) -> complete (retired).  Its latency sp
   ``device_exec`` = dev_end - dev_start (first item claimed -> last item done: the GPU's own
   time on the batch, which grows when several resident kernels share the device) and
   ``flight_other`` = the rest (doorbell + claim before the first item, completion record ->
-  host after the last).
+  host after the last).  ``flight_other`` splits again, with the device clock aligned to the
+  host's (``_device_split``), into ``device_start_wait`` (post -> first item claimed) and
+  ``host_notice`` (last item done -> seen by the host); ``device_stall_windows`` lists the
+  host-time windows in which the device started a batch >= 1 ms late or stopped it mid-run.
 
 The queued part is cut against the scoring thread's own timeline: time INSIDE a native
 ``run()`` call (the thread was polling; a batch can still wait there for a free in-flight slot
@@ -77,6 +80,48 @@ def _held(held: np.ndarray, t_end: int) -> np.ndarray:
     return _intervals(np.array(out, np.int64))
 
 
+def _device_split(b: np.ndarray, window_ns: int = 500_000_000):
+    """Per batch (post -> first item claimed, last item done -> seen in host memory), with the
+    device clock aligned to the host's per ``window_ns`` window (drift): in each window the
+    batch noticed fastest defines the offset (its notice = 0), so ``start`` and ``notice`` are
+    exact up to that best-case notice latency (a few us)."""
+    ts = b["t_submit"].astype(np.int64)
+    tl = b["t_landed"].astype(np.int64)
+    ds = b["dev_start"].astype(np.int64)
+    de = b["dev_end"].astype(np.int64)
+    w = (ts - ts.min()) // window_ns
+    c = np.zeros(len(b), np.int64)
+    for k in np.unique(w):
+        m = w == k
+        c[m] = (de[m] - tl[m]).max()
+    return ds - c - ts, tl - (de - c)
+
+
+def stall_windows(b: np.ndarray, start: np.ndarray, exe: np.ndarray, thr_ns: int = 1_000_000) -> dict:
+    """Host-time windows in which a batch waited >= thr for the device to start it or was
+    stopped mid-execution for >= thr: their lengths and spacing (a device time slice between
+    several resident persistent kernels shows as fixed-length windows at a fixed period)."""
+    big = (start >= thr_ns) | (exe >= thr_ns)
+    iv = np.stack([b["t_submit"][big].astype(np.int64), b["t_landed"][big].astype(np.int64)], 1)
+    iv = iv[np.argsort(iv[:, 0])] if len(iv) else iv
+    merged = []
+    for s_, e_ in iv:
+        if merged and s_ <= merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], e_)
+        else:
+            merged.append([s_, e_])
+    m = np.array(merged, np.int64).reshape(-1, 2)
+    if len(m) < 2:
+        return {"windows": int(len(m))}
+    ln = (m[:, 1] - m[:, 0]) / 1e6
+    gap = np.diff(m[:, 0]) / 1e6
+    return {"windows": int(len(m)), "length_ms": {"p50": round(float(np.median(ln)), 2), "max": round(float(ln.max()), 2)},
+            "period_ms": {"p50": round(float(np.median(gap)), 1)},
+            "share_of_time": round(float(ln.sum() / ((m[-1, 1] - m[0, 0]) / 1e6)), 3),
+            "batches_started_late_ge_1ms": int((start >= thr_ns).sum()),
+            "batches_stopped_mid_exec_ge_1ms": int((exe >= thr_ns).sum())}
+
+
 def attribute(path: str, tail_q: float = 0.99) -> dict:
     d = np.load(path)
     b = d["batches"]
@@ -96,8 +141,12 @@ def attribute(path: str, tail_q: float = 0.99) -> dict:
     sel = np.nonzero(total >= thr)[0]
     dev = (b["dev_end"] - b["dev_start"]).astype(np.int64) if "dev_end" in b.dtype.names else np.zeros(len(b), np.int64)
     has_dev = dev > 0
+    dstart = np.zeros(len(b), np.int64)
+    notice = np.zeros(len(b), np.int64)
+    if has_dev.all() and len(b) > 1:
+        dstart, notice = _device_split(b)
     parts = {k: [] for k in ("in_run", "outside_run", "task", "gc", "held", "interpreter", "flight",
-                             "device_exec", "flight_other")}
+                             "device_exec", "flight_other", "device_start_wait", "host_notice")}
     for i in sel:
         lo, hi = int(b["t_arrival"][i]), int(b["t_submit"][i])
         inside = _overlap(lo, hi, runs)
@@ -130,6 +179,8 @@ def attribute(path: str, tail_q: float = 0.99) -> dict:
         de = int(dev[i]) if has_dev[i] else 0
         parts["device_exec"].append(de)
         parts["flight_other"].append(max(0, int(flight[i]) - de))
+        parts["device_start_wait"].append(int(dstart[i]))
+        parts["host_notice"].append(int(notice[i]))
     us = lambda v: round(float(v) / 1e3, 1)
     gaps_all = runs[1:, 0] - runs[:-1, 1] if len(runs) > 1 else np.zeros(0, np.int64)
     return {
@@ -141,6 +192,12 @@ def attribute(path: str, tail_q: float = 0.99) -> dict:
         "flight_us": {"p50": us(np.quantile(flight, 0.5)), "p99": us(np.quantile(flight, 0.99))},
         "device_exec_us": ({"p50": us(np.quantile(dev[has_dev], 0.5)), "p99": us(np.quantile(dev[has_dev], 0.99)),
                             "batches": int(has_dev.sum())} if has_dev.any() else None),
+        # flight = device_start_wait (post -> first item claimed) + device_exec + host_notice
+        "device_start_wait_us": ({"p50": us(np.quantile(dstart, 0.5)), "p99": us(np.quantile(dstart, 0.99))}
+                                 if has_dev.all() and len(b) > 1 else None),
+        "host_notice_us": ({"p50": us(np.quantile(notice, 0.5)), "p99": us(np.quantile(notice, 0.99))}
+                           if has_dev.all() and len(b) > 1 else None),
+        "device_stall_windows": stall_windows(b, dstart, dev) if has_dev.all() and len(b) > 1 else None,
         f"tail_batches_ge_p{int(tail_q * 100)}": int(len(sel)),
         "tail_mean_breakdown_us": {k: us(np.mean(v)) for k, v in parts.items()},
         "scoring_thread": {

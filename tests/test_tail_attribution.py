@@ -34,4 +34,6 @@ def test_attribution_splits_queue_time(tmp_path):
     assert 2790 <= bd["gc"] <= 2810 and bd["outside_run"] >= 2990 and bd["in_run"] <= 10
     assert bd["flight"] == 20.0
     assert bd["device_exec"] == 15.0 and bd["flight_other"] == 5.0
+    # aligned device clock: post -> first claim + last item -> host = 5 us
+    assert bd["device_start_wait"] == 5.0 and bd["host_notice"] == 0.0   # the fastest notice defines 0
     assert r["device_exec_us"]["p99"] == 15.0 and r["device_exec_us"]["batches"] == 100
