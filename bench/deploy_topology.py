@@ -99,6 +99,38 @@ def free_ports(n: int, contiguous: int = 1) -> List[int]:
     return out
 
 
+def cgroup_cpu() -> Dict:
+    """This cgroup's CPU quota and throttling counters (cgroup v2): a deployment sharing a CPU
+    quota stalls in whole scheduler periods once the quota is spent."""
+    out: Dict = {}
+    v1 = Path("/sys/fs/cgroup/cpu")
+    for f in ("cpu.max", "cpu.stat"):
+        try:
+            txt = Path("/sys/fs/cgroup", f).read_text()
+        except OSError:
+            continue
+        if f == "cpu.max":
+            out["cpu.max"] = txt.strip()
+        else:
+            for ln in txt.splitlines():
+                k, _, v = ln.partition(" ")
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    out[k] = int(v)
+    if not out and v1.is_dir():                    # cgroup v1: the same counters, other names
+        try:
+            out["cpu.max"] = (f"{(v1 / 'cpu.cfs_quota_us').read_text().strip()} "
+                              f"{(v1 / 'cpu.cfs_period_us').read_text().strip()}")
+            for ln in (v1 / "cpu.stat").read_text().splitlines():
+                k, _, v = ln.partition(" ")
+                if k in ("nr_periods", "nr_throttled"):
+                    out[k] = int(v)
+                elif k == "throttled_time":
+                    out["throttled_usec"] = int(v) // 1000
+        except OSError:
+            pass
+    return out
+
+
 def wait_port(port: int, timeout: float = 120.0) -> None:
     t0 = time.time()
     while time.time() - t0 < timeout:
@@ -179,6 +211,22 @@ class Proc:
                 self.p.wait(5)
         self.log.close()
         return self.p.returncode
+
+    def cpu_s(self) -> Optional[float]:
+        """CPU seconds of the process and its children so far (torchrun's ranks are children)."""
+        try:
+            import psutil
+            root = psutil.Process(self.p.pid)
+            tot = 0.0
+            for q in [root] + root.children(recursive=True):
+                try:
+                    t = q.cpu_times()
+                    tot += t.user + t.system
+                except psutil.Error:
+                    pass
+            return round(tot, 1)
+        except Exception:                              # noqa: BLE001 -- diagnostics only
+            return None
 
     def text(self) -> str:
         try:
@@ -404,6 +452,8 @@ def main(argv=None):
                 break
             time.sleep(0.2)
         samples = []
+        cg0 = cgroup_cpu()
+        cpu0 = {q.name: q.cpu_s() for q in procs}
         t_w0 = time.time()
         r_w0, f_w0, _ = scrape_all()
         last_t, last_r = t_w0, r_w0
@@ -580,6 +630,15 @@ def main(argv=None):
         # the host this topology shares: every service and engine rank runs on these CPUs
         out["host_cpus"] = {"affinity": len(os.sched_getaffinity(0)), "machine": os.cpu_count(),
                             "loadavg_1m_max": max((sm.get("loadavg_1m", 0) for sm in samples), default=None)}
+        # where the CPU went during the measured window (and whether the cgroup's quota throttled it)
+        cg1 = cgroup_cpu()
+        out["cgroup_cpu"] = {"cpu.max": cg1.get("cpu.max"),
+                             **{k: cg1[k] - cg0.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled",
+                                                                   "throttled_usec") if k in cg1}}
+        out["cpu_s_by_service"] = {q.name: (round(q.cpu_s() - cpu0[q.name], 1)
+                                            if q.cpu_s() is not None and cpu0.get(q.name) is not None else None)
+                                   for q in procs if q.name in cpu0}
+        out["window_s"] = round(time.time() - t_w0, 1)
         if a.standard_mode == "process":
             # every transaction started exactly one process: standard + fraud == incoming
             t_k = time.time()
