@@ -42,7 +42,13 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   const int C = a.items_per_batch;
   const int cpw = a.tiles_per_wave;                       // 64-row chunks per wave per item
   if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
+#ifdef CCFD_EXP_DOORBELL_WAVES
+    // experiment build: all 4 waves poll, a quarter of a poll round trip apart
+    for (int k = 0; k < 40 * wave; ++k) __builtin_amdgcn_s_sleep(127);
+    persist_doorbell(a, lane);
+#else
     if (wave == 0) persist_doorbell(a, lane);
+#endif
     return;                                               // no barrier is ever used by WG 0
   }
   const char* blob = reinterpret_cast<const char*>(a.blob);

@@ -40,4 +40,15 @@ st itrace
 timeout -k 10 240 env CCFD_LIB_PATH=$AB/itrace.so CCFD_ITEM_TRACE_OUT=$O/itrace python bench.py --model gbdt --steps 20 \
     --warmup 5 --diagnostic > $O/gbdt_itrace.json 2> $O/gbdt_itrace.log || { tail -20 $O/gbdt_itrace.log; exit 1; }
 python bench/experiments/item_trace.py $O/itrace.0 --json $O/itrace_phases.json && rm -f $O/itrace.*
+st dbw_itrace
+timeout -k 10 240 env CCFD_LIB_PATH=$AB/dbw_itrace.so CCFD_ITEM_TRACE_OUT=$O/dbw_itrace python bench.py --model gbdt --steps 20 \
+    --warmup 5 --diagnostic > $O/gbdt_dbw_itrace.json 2> $O/gbdt_dbw_itrace.log || { tail -20 $O/gbdt_dbw_itrace.log; exit 1; }
+python bench/experiments/item_trace.py $O/dbw_itrace.0 --json $O/dbw_itrace_phases.json && rm -f $O/dbw_itrace.*
+for v in default dbw default_again; do
+  st gbdt_$v
+  L=""; D=""; [ $v = dbw ] && { L="CCFD_LIB_PATH=$AB/dbw.so"; D=--diagnostic; }
+  timeout -k 10 240 env $L python bench.py --model gbdt --steps 20 --warmup 5 $D > $O/gbdt_$v.json 2> $O/gbdt_$v.log \
+    || { tail -20 $O/gbdt_$v.log; exit 1; }
+  python -c "import json; d=json.load(open('$O/gbdt_$v.json')); print('$v', d['value'], d['p50_latency_us'], d['p99_latency_us'], d.get('precision_vs_fp32', {}).get('route_flips_outside_1e-2_band'), d.get('wire_stale_rows'))"
+done
 st done
