@@ -73,7 +73,7 @@ def doorbell(db: np.ndarray, t_lo: int, t_hi: int) -> dict:
             "backlog_seen_ge2_share": round(float((nb >= 2).mean()), 3)}
 
 
-def analyse(rec: np.ndarray, skip_frac: float = 0.02) -> dict:
+def analyse(rec: np.ndarray, skip_frac: float = 0.02, items_per_batch: int = 0) -> dict:
     rec = rec[rec[:, FIELDS.index("t_done")] > 0]
     rec = rec[np.argsort(rec[:, 2], kind="stable")]
     lo = int(len(rec) * skip_frac)
@@ -113,8 +113,31 @@ def analyse(rec: np.ndarray, skip_frac: float = 0.02) -> dict:
         out["phases_us"][k] = {"p10": round(float(np.percentile(v, 10)) * TICK_US, 2),
                                "p50": round(float(np.median(v)) * TICK_US, 2),
                                "p90": round(float(np.percentile(v, 90)) * TICK_US, 2),
+                               "p99": round(float(np.percentile(v, 99)) * TICK_US, 2),
+                               "max": round(float(v.max()) * TICK_US, 2),
                                "mean": round(float(v.mean()) * TICK_US, 2),
                                "share_of_cycle": round(float(v.mean()) / mean_total, 3)}
+    # per micro-batch (items_per_batch C): first claim -> last item done, and what its last item
+    # spent: a batch completes -- and its ring slot is re-posted -- only behind its slowest item
+    if items_per_batch:
+        bidx = f["item"] // items_per_batch
+        order = np.argsort(bidx, kind="stable")
+        bs, starts = np.unique(bidx[order], return_index=True)
+        spans, last_tot, last_wait = [], [], []
+        for j in range(len(bs)):
+            sl = order[starts[j]: starts[j + 1] if j + 1 < len(bs) else len(order)]
+            if len(sl) != items_per_batch:
+                continue                          # a batch only partly inside the ring
+            k_last = sl[np.argmax(f["t_done"][sl])]
+            spans.append(f["t_done"][sl].max() - f["t_claim"][sl].min())
+            last_tot.append(f["t_done"][k_last] - f["t_claim"][k_last])
+            last_wait.append(f["t_seen"][k_last] - f["t_claimed"][k_last])
+        if spans:
+            q = lambda v: {"p50": round(float(np.median(v)) * TICK_US, 1), "p99": round(float(np.percentile(v, 99)) * TICK_US, 1),
+                           "max": round(float(np.max(v)) * TICK_US, 1)}
+            out["batches"] = {"n": len(spans), "span_first_claim_to_last_done_us": q(np.array(spans)),
+                              "last_item_total_us": q(np.array(last_tot)),
+                              "last_item_wait_post_us": q(np.array(last_wait))}
     return out
 
 
@@ -122,11 +145,12 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("paths", nargs="+")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--items-per-batch", type=int, default=128, help="micro-batch rows / item rows")
     a = ap.parse_args(argv)
     res = {}
     for p in a.paths:
         items = load(p)
-        res[p] = analyse(items)
+        res[p] = analyse(items, items_per_batch=a.items_per_batch)
         db = load(p, doorbell=True)
         if len(db):
             res[p]["doorbell"] = doorbell(db, int(items[:, FIELDS.index("t_claim")].min()),
@@ -137,6 +161,8 @@ def main(argv=None) -> int:
         print(f"  {'phase':<10} {'p10':>8} {'p50':>8} {'p90':>8} {'mean':>8} {'share':>7}")
         for k, v in r["phases_us"].items():
             print(f"  {k:<10} {v['p10']:8.2f} {v['p50']:8.2f} {v['p90']:8.2f} {v['mean']:8.2f} {v['share_of_cycle']:7.1%}")
+        if "batches" in r:
+            print("  batches", json.dumps(r["batches"]))
         if "doorbell" in r:
             print("  doorbell", json.dumps(r["doorbell"]))
     if a.json:

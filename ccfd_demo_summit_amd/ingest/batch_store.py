@@ -291,6 +291,23 @@ class BatchStore:
     def _persist_truncate(self, topic: str, partition: int, offset: int) -> None:
         pass
 
+    def reset_to(self, topic: str, partition: int, offset: int) -> int:
+        """Drop the whole partition log and continue at ``offset`` (a replica that was away
+        longer than its leader's retention: its log end is below the leader's log start, so it
+        restarts from there, as Kafka's follower does).  Returns the batches dropped."""
+        with self._lock:
+            L = self._log(topic, partition)
+            dropped = len(L.batches)
+            L.nbytes = 0
+            del L.bases[:], L.batches[:], L.ts[:]
+            L.begin = L.end = L.visible = int(offset)
+            self._producers.pop((topic, partition), None)
+            self._persist_reset(topic, partition, int(offset))
+            return dropped
+
+    def _persist_reset(self, topic: str, partition: int, offset: int) -> None:
+        pass
+
     def log_end(self, topic: str, partition: int) -> int:
         """The next offset this log assigns (LEO), written or not."""
         with self._lock:

@@ -440,6 +440,9 @@ class DurableBatchStore(BatchStore):
                     elif kind == "T":
                         self._truncate_segments(topic, p, op[3])
                         ends.pop((topic, p), None)
+                    elif kind == "X":
+                        self._reset_segments(topic, p)
+                        ends.pop((topic, p), None)
                     else:
                         self._retire_segments(topic, p, op[3])
                 if self.fsync == "always" and touched:
@@ -505,6 +508,24 @@ class DurableBatchStore(BatchStore):
     def _persist_truncate(self, topic: str, partition: int, offset: int) -> None:
         """Under the store lock: the segments follow the in-memory cut, in write order."""
         self._enqueue(("T", topic, partition, offset))
+
+    def _persist_reset(self, topic: str, partition: int, offset: int) -> None:
+        """Under the store lock: every segment of the partition goes, in write order; the next
+        write opens a segment based at the new start."""
+        self._enqueue(("X", topic, partition, offset))
+
+    def _reset_segments(self, topic: str, partition: int) -> None:
+        """Writer thread: delete every segment file of the partition."""
+        segs = self._segs.get((topic, partition), [])
+        while segs:
+            seg = segs.pop()
+            with self._lock:
+                self._close_segment(seg, now=True)
+            for ext in (".log", ".idx"):
+                try:
+                    os.unlink(seg.path + ext)
+                except OSError:
+                    pass
 
     def _truncate_segments(self, topic: str, partition: int, offset: int) -> None:
         """Writer thread: cut the partition's files at ``offset`` (a batch boundary)."""

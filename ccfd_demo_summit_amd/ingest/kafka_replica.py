@@ -49,7 +49,7 @@ from .kafka_controller import tp_key, tp_split
 
 TP = Tuple[str, int]
 PID_STRIDE = 1024                      # producer ids: node + PID_STRIDE * k (disjoint per broker)
-FETCH, FETCH_V = 1, 4
+FETCH, FETCH_V, LIST_OFFSETS = 1, 4, 2
 
 
 def load_checkpoint(data_dir: Optional[str]) -> Dict[TP, int]:
@@ -107,6 +107,7 @@ class ReplicaManager:
         self.replicated_bytes = 0
         self.fetch_errors: Dict[str, int] = {}       # "leader/topic/p:code" -> count (status line)
         self.isr_changes = 0
+        self.resets = 0                               # partitions restarted at the leader's log start
         self.report_s = float(os.environ.get("CCFD_KAFKA_REPL_REPORT_S", "5"))
         self.hb_failures = 0
         self._lead_since: Dict[TP, float] = {}
@@ -462,12 +463,16 @@ class ReplicaManager:
                         return idx, err, hw, x.view_()
                     resp = r.array(lambda x: (x.string(), x.array(part)))
                     moved = False
+                    below = []
                     for t, parts in resp:
                         for p, err, hw, recs in parts:
                             if err == 1 and self.store.log_end(t, p) > int(hw):
                                 # OFFSET_OUT_OF_RANGE past the leader's log: this replica holds
                                 # a tail the leader never had -- cut it to the leader's HW
                                 self._truncate_to_hw((t, p), int(hw))
+                                continue
+                            if err == 1:
+                                below.append((t, p))                  # before the leader's log start?
                                 continue
                             if err:
                                 k = f"{leader}/{t}/{p}:{err}"
@@ -483,6 +488,31 @@ class ReplicaManager:
                                     raise
                                 self.replicated_bytes += len(recs)
                             self.hw[(t, p)] = max(self.hw.get((t, p), 0), min(int(hw), self.store.log_end(t, p)))
+                    if below:
+                        # away longer than the leader's retention: restart these partitions at
+                        # the leader's log start (ListOffsets earliest), as a Kafka follower does
+                        corr += 1
+                        lo_body = Writer().i32(self.node_id).array(
+                            sorted({t for t, _ in below}), lambda w, t: w.string(t).array(
+                                [q for tt, q in below if tt == t], lambda w2, q: w2.i32(q).i64(-2))).build()
+                        lo_hdr = Writer().i16(LIST_OFFSETS).i16(1).i32(corr).string(f"replica-{self.node_id}").build()
+                        await loop.sock_sendall(sock, struct.pack(">i", len(lo_hdr) + len(lo_body)) + lo_hdr + lo_body)
+                        size = struct.unpack(">i", await recv_exact(4))[0]
+                        r2 = Reader(memoryview(await recv_exact(size)).cast("B"))
+                        if r2.i32() != corr:
+                            raise BrokerError("replica list-offsets: correlation mismatch")
+                        lo = r2.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+                        for t, parts in lo:
+                            for p, err, _ts, start in parts:
+                                if err == 0 and self.store.log_end(t, p) < int(start):
+                                    n = self.store.reset_to(t, p, int(start))
+                                    self.resets += 1
+                                    print(f"[kafka-lite] node {self.node_id}: {t}[{p}] was below leader {leader}'s "
+                                          f"log start {start}: dropped {n} batches, following from there", flush=True)
+                                else:
+                                    k = f"{leader}/{t}/{p}:1"
+                                    self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
+                                    moved = True
                     self.replica_fetches += 1
                     # the next fetch reports this log end to the leader at once, without waiting
                     # for the local write: an acknowledged batch is then on every in-sync

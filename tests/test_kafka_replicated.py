@@ -96,6 +96,15 @@ def test_controller_elects_the_highest_leo_isr_member_and_fences_restarts():
 
 @pytest.fixture()
 def cluster(tmp_path):
+    yield from _cluster(tmp_path, [])
+
+
+@pytest.fixture()
+def small_retention_cluster(tmp_path):
+    yield from _cluster(tmp_path, ["--retention-batches", "20"])
+
+
+def _cluster(tmp_path, extra):
     ports = _free_ports(7)
     cport, bports, mports = ports[0], ports[1:4], ports[4:7]
     env = dict(os.environ, PYTHONPATH=str(ROOT))
@@ -108,7 +117,7 @@ def cluster(tmp_path):
     def broker_cmd(k):
         return [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", "127.0.0.1",
                 "--port", str(bports[k - 1]), "--node-id", str(k), "--controller", f"http://127.0.0.1:{cport}",
-                "--metrics-port", str(mports[k - 1]), "--data-dir", str(tmp_path / f"b{k}"), "--fsync", "interval"]
+                "--metrics-port", str(mports[k - 1]), "--data-dir", str(tmp_path / f"b{k}"), "--fsync", "interval"] + extra
     start("ctl", [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller", "--host", "127.0.0.1",
                   "--port", str(cport), "--data-dir", str(tmp_path / "ctl"), "--session-s", "1.0",
                   "--brokers", "3"])
@@ -288,3 +297,44 @@ def test_native_consumer_reads_every_row_once_across_a_broker_kill(cluster):
         kc.stop()
         kc.close()
         kb.close()
+
+
+def test_broker_away_past_the_leaders_retention_restarts_at_its_log_start(small_retention_cluster):
+    """A follower that was down while its leaders' retention (20 batches here) moved past its
+    log end gets OFFSET_OUT_OF_RANGE below the log start: it restarts those partitions at the
+    leader's log start (ListOffsets earliest), catches up and rejoins every ISR (round 5: the
+    deployed broker-kill run stayed under-replicated until this)."""
+    c = small_retention_cluster
+    boot = ",".join(f"127.0.0.1:{p}" for p in c["bports"])
+    deadline = time.time() + 30
+    while len(json.loads(_text(f"http://127.0.0.1:{c['cport']}/metadata"))["nodes"]) < 3 and time.time() < deadline:
+        time.sleep(0.1)
+    kb = KafkaBroker(boot, idempotent=True, connect_wait_s=10)
+    kb.RETRIES = 14
+    kb.create_topic("t", 3)
+    for k in range(30):
+        kb.produce_raw("t", k % 3, encode_record_batch([b"a%d" % k]), acks=-1)
+    os.killpg(c["procs"]["b2"].pid, signal.SIGKILL)
+    c["procs"]["b2"].wait(10)
+    for k in range(300):                                 # 100 batches per partition: > retention
+        kb.produce_raw("t", k % 3, encode_record_batch([b"b%d" % k]), acks=-1)
+    starts = [kb.begin_offset("t", p) for p in range(3)]
+    assert min(starts) > 30, starts                      # the leaders' logs start past the old end
+    c["start"]("b2", c["broker_cmd"](2))
+    _wait(c["bports"][1])
+    deadline = time.time() + 30
+    md = {}
+    under = [None]
+    while time.time() < deadline:
+        time.sleep(0.3)
+        try:                                             # the restarted broker's metrics come up last
+            md = json.loads(_text(f"http://127.0.0.1:{c['cport']}/metadata"))
+            under = [_gauge(_text(f"http://127.0.0.1:{mp}/metrics"),
+                            "kafka_server_replicamanager_underreplicatedpartitions") for mp in c["mports"]]
+        except OSError:
+            continue
+        if all(len(v["isr"]) == 3 for k_, v in md["parts"].items() if k_.startswith("t/")) and not any(under):
+            break
+    assert all(len(v["isr"]) == 3 for k_, v in md["parts"].items() if k_.startswith("t/")), md["parts"]
+    assert not any(under), under
+    kb.close()
