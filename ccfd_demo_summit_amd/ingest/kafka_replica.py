@@ -445,9 +445,13 @@ class ReplicaManager:
                     by_topic: Dict[str, List[Tuple[int, int]]] = {}
                     for t, p in tps:                # fetch from this replica's log end, written or not
                         by_topic.setdefault(t, []).append((p, self.store.log_end(t, p)))
-                    body = (Writer().i32(self.node_id).i32(200).i32(1).i32(64 << 20).i8(0)
+                    # bounded responses (8 MB, 2 MB a partition): a follower catching up from
+                    # its leader's log start pulls GBs, and the leader's single event loop must
+                    # keep answering produces and consumer fetches between those responses (64 MB
+                    # ones stalled the consumers for seconds after a broker restart)
+                    body = (Writer().i32(self.node_id).i32(200).i32(1).i32(8 << 20).i8(0)
                             .array(sorted(by_topic.items()), lambda w, kv: w.string(kv[0]).array(
-                                kv[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).i32(16 << 20))).build())
+                                kv[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).i32(2 << 20))).build())
                     corr += 1
                     hdr = Writer().i16(FETCH).i16(FETCH_V).i32(corr).string(f"replica-{self.node_id}").build()
                     await loop.sock_sendall(sock, struct.pack(">i", len(hdr) + len(body)) + hdr + body)

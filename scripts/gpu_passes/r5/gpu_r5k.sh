@@ -1,13 +1,13 @@
 #!/usr/bin/env bash
-# Round-5 pass K: (item 4) the RF-3 broker SIGKILL run, 90 s, after the follower restart fix (a
+# Round-5 pass K (rerun as K2: depth 16 and 32; follower fetches bounded to 8 MB): (item 4) the RF-3 broker SIGKILL run, 90 s, after the follower restart fix (a
 # follower below its leader's log start restarts there); (item 6) the G20 item trace at depth 4
 # and 8 with the per-batch straggler view (batch span, its last item).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}" || exit 1
-O=gpurun_out/r5k; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
+O=gpurun_out/${R5K_OUT:-r5k}; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
 AB=ccfd_demo_summit_amd/_native/ab
 st() { echo "[r5k] $(date +%T) $*"; }
-for d in 4 8; do
+for d in 16 32; do
   st itrace_d$d
   timeout -k 10 240 env CCFD_LIB_PATH=$AB/itrace.so CCFD_ITEM_TRACE_OUT=$O/itrace_d$d python bench.py --model gbdt --steps 20 \
       --warmup 5 --depth $d --diagnostic > $O/gbdt_itrace_d$d.json 2> $O/gbdt_itrace_d$d.log || { tail -20 $O/gbdt_itrace_d$d.log; exit 1; }
