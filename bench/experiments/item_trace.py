@@ -6,7 +6,7 @@ kernels/score_gbdt_g32_persist.hip --src engine/engine.cpp -D CCFD_EXP_ITEM_TRAC
 torn down, `<prefix>.<k>`).  Each record is one claimed item, stamped by its workgroup's thread 0
 with the 100 MHz wall clock:
 
-    claim      the work_next atomic
+    claim      the work_next atomic, issue to value back (traces before round-5 pass L: issue only)
     wait_post  waiting until the item's micro-batch is posted (device mirror of the doorbell)
     desc       the per-item agent-scope acquire + the descriptor's atomic loads
     load       the first 64-row chunk's zero-copy load (issue -> data in registers)

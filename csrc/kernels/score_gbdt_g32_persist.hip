@@ -64,6 +64,9 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   epi_init(epi);
   __syncthreads();
   unsigned long long posted_cache = 0;                    // thread 0 only
+#ifdef CCFD_EXP_XCD_QUEUES
+  const unsigned long long work_base = __hip_atomic_load(&a.dev->work_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 
   // per-item accumulators of this wave (flushed by item_flush)
   unsigned fraud = 0, rows = 0, stale = 0;
@@ -135,6 +138,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       t_claim = wall_clock64();
       const unsigned long long it =
           __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the claim's value is back (not just issued)
       t_claimed = wall_clock64();
       // persist_wait_item, split: the wait for the posting, then the descriptor read
       const unsigned long long b = it / (unsigned long long)C;
@@ -151,6 +155,17 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       if (!s_cmd) persist_read_desc(a, b, sdesc);
       s_item = it;
       t_desc = wall_clock64();
+    }
+#elif defined(CCFD_EXP_XCD_QUEUES)
+    // experiment build: 8 claim counters, one per XCD (workgroup i runs on XCD i % 8): item
+    // base + 8k + q -- a claim contends with the ~24 workgroups of its XCD, not all 191
+    if (tid == 0) {
+      const unsigned q = blockIdx.x & 7u;
+      const unsigned long long k =
+          __hip_atomic_fetch_add(&a.dev->work_q[q][0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long it = work_base + 8ull * k + q;
+      s_cmd = persist_wait_item(a, C, posted_cache, it, sdesc);
+      s_item = it;
     }
 #else
     if (tid == 0) persist_claim(a, C, posted_cache, sdesc, s_item, s_cmd);
