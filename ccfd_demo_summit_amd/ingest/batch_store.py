@@ -333,11 +333,14 @@ class BatchStore:
         """``fetch_raw`` as the list of stored batches themselves (no copy; a fetch response
         is written to the socket from them).  ``upto``: serve only batches below this offset
         (a replicated leader's consumers see up to the high watermark).  ``unwritten``: up to
-        the log end, written or not (a follower's replica fetch: the copy on another broker
-        is what protects a batch the leader has not written yet)."""
+        the log end, written or not (a follower's replica fetch, and a replicated leader's
+        consumers below the high watermark: the copies on the other in-sync brokers are what
+        protect a batch the leader has not written yet)."""
         with self._lock:
             L = self._log(topic, partition)
-            lim = (L.end if unwritten else L.visible) if upto is None else min(L.visible, upto)
+            lim = L.end if unwritten else L.visible
+            if upto is not None:
+                lim = min(lim, upto)
             if offset >= lim or not L.batches:
                 return []
             i = max(0, bisect.bisect_right(L.bases, offset) - 1)

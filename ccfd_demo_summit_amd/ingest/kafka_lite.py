@@ -718,7 +718,9 @@ class KafkaLiteServer:
         watermark covers the batch (every in-sync replica has it).  Leadership lost meanwhile,
         or the timeout: NOT_LEADER, so the producer refreshes metadata and retries (its
         idempotent sequence makes a retry of a replicated batch a no-op)."""
-        await self._written_ticket(ticket)
+        # acks=all: answered once the high watermark covers the batch (in the memory of every
+        # in-sync replica, each writing it to disk right behind) -- not after this broker's own
+        # write, which would put the leader's disk latency in front of every acknowledgement
         rep = self.cluster.replica
         deadline = time.monotonic() + max(0.1, timeout_ms / 1000.0)
         for topic, p, end, entry in waits:
@@ -808,6 +810,10 @@ class KafkaLiteServer:
                         # end is valid (a new leader's HW catches up) -- an empty answer, not
                         # OFFSET_OUT_OF_RANGE
                         upto = rep.high_watermark(topic, p)
+                        unwritten = True                  # below the HW = on every in-sync replica
+                        # a consumer may have read (from the old leader) up to a HW that this new
+                        # leader holds in memory but has not written yet: in range, not an error
+                        limit = self.store.log_end(topic, p)
                     hw = rep.high_watermark(topic, p)
                 if off < self.store.begin_offset(topic, p) or off > limit:
                     pr.append((p, ERR_OFFSET_OUT_OF_RANGE, hw, None))

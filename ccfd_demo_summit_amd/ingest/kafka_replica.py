@@ -162,8 +162,13 @@ class ReplicaManager:
         return self.hw.get((topic, p), 0)
 
     def _leo(self, tp: TP) -> int:
+        """This replica's log end offset as appended, written or not: the high watermark is
+        the minimum of these over the ISR, so a record below it is in the memory of every
+        in-sync broker (and on its way to each one's disk) -- one broker's death loses nothing
+        acknowledged, and consumer latency does not wait on the leader's own disk writes
+        (Kafka counts the page cache the same way)."""
         try:
-            return self.store.end_offset(*tp)          # written (visible) end
+            return self.store.log_end(*tp)
         except BrokerError:
             return 0
 
@@ -257,10 +262,14 @@ class ReplicaManager:
         if not self.is_leader(topic, p):
             return
         now = time.monotonic()
-        rec = self.fol.setdefault(tp, {}).setdefault(node, [0, now, 0.0])
+        rec = self.fol.setdefault(tp, {}).setdefault(node, [0, now, 0.0, 0])
+        # caught up = it now holds everything the leader held when it answered the previous
+        # fetch (Kafka's lastCaughtUpTime): under a steady produce stream the leader's log end
+        # has always moved on a little by the time the next fetch arrives
+        if offset >= rec[3]:
+            rec[2] = now
         rec[0], rec[1] = offset, now
-        if offset >= self._leo(tp):
-            rec[2] = now                                 # caught up with the leader
+        rec[3] = self._leo(tp)
         self._advance_hw(tp)
 
     def on_written(self, tps) -> None:
