@@ -27,10 +27,13 @@ __device__ unsigned long long g_item_trace_n;
 #define CCFD_ITRACE(stmt)
 #endif
 
-template <int D, bool kR, bool kGL, bool kG20>
-__global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args a) {
+// kW waves per workgroup: 4 (default), or 8 in an experiment build (CCFD_EXP_G20_WAVES8: two
+// waves per SIMD, each scoring half as many chunks of an item, so one wave's tree-walk
+// latency hides behind the other's)
+template <int D, bool kR, bool kGL, bool kG20, int kW = kG32Waves>
+__global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_args a) {
   extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L floats
-  __shared__ uint4 xt[kG32Waves][128];
+  __shared__ uint4 xt[kW][128];
   __shared__ EpilogueLds epi;
   __shared__ ccfd_persist_desc sdesc;
   __shared__ unsigned long long s_item;
@@ -40,7 +43,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int C = a.items_per_batch;
-  const int cpw = a.tiles_per_wave;                       // 64-row chunks per wave per item
+  const int cpw = a.tiles_per_wave * kG32Waves / kW;      // 64-row chunks per wave per item
   if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
 #ifdef CCFD_EXP_DOORBELL_WAVES
     // experiment build: all 4 waves poll, a quarter of a poll round trip apart
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
   const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
   const float* leaves = lv;
   if constexpr (kGL) leaves = g32_leaves_global(blob, T, D);
-  else g32_stage_leaves<D>(blob, T, lv, tid, 256);
+  else g32_stage_leaves<D>(blob, T, lv, tid, 64 * kW);
   epi_init(epi);
   __syncthreads();
   unsigned long long posted_cache = 0;                    // thread 0 only
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
     const int n = d.n;
     const unsigned char* xb = reinterpret_cast<const unsigned char*>(d.x);
     k7_start(s_item, slot);
-    const int c0 = item * (kG32Waves * cpw) + wave;       // this wave's chunks: c0 + 4k
+    const int c0 = item * (kW * cpw) + wave;              // this wave's chunks: c0 + kW*k
     // CCFD_G32_INFLIGHT=1: every chunk of the wave's share of the item in flight at once
     // (static registers: no copy of a pending load, so no vmcnt(0) between chunks)
     auto full_item = [&](auto kC) __attribute__((always_inline)) {
@@ -186,12 +189,12 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       G32Row r[CPW];
 #pragma unroll
       for (int k = 0; k < CPW; ++k) {
-        const int chunk = c0 + kG32Waves * k;
+        const int chunk = c0 + kW * k;
         if (chunk * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk, lane, r[k]);
       }
 #pragma unroll
       for (int k = 0; k < CPW; ++k) {
-        const int chunk = c0 + kG32Waves * k;
+        const int chunk = c0 + kW * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
         score_chunk(d, slot, n, chunk, r[k]);
       }
@@ -201,11 +204,11 @@ __global__ __launch_bounds__(256) void persist_gbdt_g32_kernel(ccfd_persist_args
       if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre);
 #pragma unroll 1
       for (int k = 0; k < cpw; ++k) {
-        const int chunk = c0 + kG32Waves * k;
+        const int chunk = c0 + kW * k;
         if (chunk * kG32Rows >= n) break;                 // wave-uniform
         G32Row cur_row = pre;
         CCFD_ITRACE(if (k == 0) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); if (tid == 0) t_load = wall_clock64(); })
-        if (k + 1 < cpw && (chunk + kG32Waves) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kG32Waves, lane, pre);
+        if (k + 1 < cpw && (chunk + kW) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kW, lane, pre);
         score_chunk(d, slot, n, chunk, cur_row);
       }
     } else if (cpw == 1) {
@@ -395,6 +398,13 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
     else hipLaunchKernelGGL((persist_gbdt_pipe_kernel<D, false, kG20, 2>), dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }
+#ifdef CCFD_EXP_G20_WAVES8
+  if (!gl && a.tiles_per_wave % 2 == 0) {
+    if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, false, kG20, 8>), dim3(grid), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, false, kG20, 8>), dim3(grid), dim3(512), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
+#endif
   if (gl) {
     if (a.rules) hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, true, true, kG20>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((persist_gbdt_g32_kernel<D, false, true, kG20>), dim3(grid), dim3(256), 0, s, a);
