@@ -34,6 +34,7 @@ import itertools
 import json
 import os
 import struct
+import zlib
 import sys
 import threading
 import time
@@ -865,11 +866,16 @@ class KafkaLiteServer:
             t[1], lambda w2, q: w2.i32(q[0]).i16(q[1]).i64(-1).i64(q[2]))).build()
 
     def _api_10(self, r: Reader) -> bytes:                  # FindCoordinator v0
-        r.string()
+        group = r.string() or ""
         live = self.cluster.live()
-        # one process: group state is shared, any node works; replicated: the lowest live broker
-        # coordinates (offsets are kept by the controller, so a new coordinator has them)
-        node = live[0] if live else self.node_id
+        # one process: group state is shared, any node works; replicated: the group's hash picks
+        # a live broker (offsets are kept by the controller, so any broker can coordinate, and a
+        # new coordinator has them) -- every group's commits on the lowest broker made it the
+        # busiest, and its event loop the produce -> scored tail
+        if self.cluster.replica is not None and live:
+            node = live[zlib.crc32(group.encode()) % len(live)]
+        else:
+            node = live[0] if live else self.node_id
         if self.cluster.replica is not None and node not in self.cluster.replica.nodes:
             return Writer().i16(ERR_NOT_COORDINATOR).i32(-1).string("").i32(-1).build()
         host, port = self.cluster.address(node)

@@ -4,9 +4,9 @@
 # RF 3.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}" || exit 1
-O=gpurun_out/r5p; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
+O=gpurun_out/${R5P_OUT:-r5p}; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
 st() { echo "[r5p] $(date +%T) $*"; }
-for rf in 1 2; do
+for rf in ${R5P_RFS:-1 2}; do
   st rf$rf
   timeout -k 10 300 python bench/deploy_topology.py --kafka-replicated --kafka-rf $rf --producer-acks -1 \
       --producer-max-in-flight 5 --seconds 60 --producers 3 --rate 1.2e6 --fmt json --log-dir $O/rf$rf \
