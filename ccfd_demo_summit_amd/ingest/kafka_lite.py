@@ -693,6 +693,9 @@ class KafkaLiteServer:
                         self._wake_fetches((topic, p))
                     if rep is not None:
                         self._wake_fetches((topic, p), self.cluster.replica_waiters)
+                        # the HW counts in-memory log ends: with no other in-sync replica
+                        # (RF 1, or a shrunk ISR) it moves right here, not after the disk write
+                        rep.on_written([(topic, p)])
                     self.metrics.messages_in.labels(topic, "Kafka").inc(nrec)
                     self.metrics.bytes_in.labels(topic, "Kafka").inc(len(rb or b""))
                 except OutOfOrderSequence:
