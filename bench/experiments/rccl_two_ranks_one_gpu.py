@@ -3,6 +3,11 @@ get)?  Each rank all-reduces a tensor on cuda:0 through the `nccl` (RCCL) backen
 engine's X2 counter reduction (parallel.dp.CounterReducer) runs once.  Prints one JSON line per
 rank; any error is printed and the rank exits non-zero.
 
+Answer on the pool's 1-GPU MI355X box (round 5, `profiles/r5/rccl_two_ranks/out.log`): no --
+RCCL 2.26.6 refuses at communicator init ("Duplicate GPU detected: rank 0 and rank 1 both on
+CUDA device").  Multi-rank RCCL therefore first runs in the driver's 8-GPU scaling bench; the
+rank logic is covered on gloo (tests/test_dist_cpu.py) and by the one-GPU gloo rehearsals.
+
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \\
         bench/experiments/rccl_two_ranks_one_gpu.py
 """
