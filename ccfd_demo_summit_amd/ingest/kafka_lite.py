@@ -42,7 +42,8 @@ from typing import Dict, List, Optional, Set, Tuple
 
 from .batch_store import BatchStore, InvalidBatch, OutOfOrderSequence
 from .broker import BrokerError
-from .kafka_wire import (ERR_CORRUPT, ERR_NONE, ERR_NOT_COORDINATOR, ERR_NOT_LEADER, ERR_OFFSET_OUT_OF_RANGE,
+from .kafka_wire import (ERR_CORRUPT, ERR_LEADER_NOT_AVAILABLE, ERR_NONE, ERR_NOT_COORDINATOR, ERR_NOT_LEADER,
+                         ERR_OFFSET_OUT_OF_RANGE,
                          ERR_OUT_OF_ORDER_SEQUENCE, ERR_TOPIC_EXISTS, ERR_UNKNOWN_TOPIC, ERR_UNSUPPORTED_VERSION, SUPPORTED, Reader, Writer)
 
 NODE_ID = 1
@@ -638,21 +639,24 @@ class KafkaLiteServer:
             x.array(lambda y: (y.string(), y.string()))
             return name, n
         reqs = r.array(req)
-        r.i32()
+        timeout_ms = r.i32()
         build = lambda res: Writer().array(res, lambda w, t: w.string(t[0]).i16(t[1])).build()
         rep = self.cluster.replica
         if rep is not None:                                 # created by the controller
             async def later():
                 res = []
+                # answered within the request's own timeout (the controller waits for every
+                # broker to register): LEADER_NOT_AVAILABLE then, which the client retries
+                wait_s = max(0.5, min(30.0, timeout_ms / 1000.0 - 1.0))
                 for name, n in reqs:
                     if name in rep.topics:
                         res.append((name, ERR_TOPIC_EXISTS))
                         continue
                     try:
-                        await rep.create_topic(name, max(1, n))
+                        await rep.create_topic(name, max(1, n), wait_s=wait_s)
                         res.append((name, ERR_NONE))
-                    except Exception:                       # noqa: BLE001 -- controller away
-                        res.append((name, 5))
+                    except Exception:                       # noqa: BLE001 -- controller away / brokers not all up
+                        res.append((name, ERR_LEADER_NOT_AVAILABLE))
                 return build(res)
             return later()
         res = []

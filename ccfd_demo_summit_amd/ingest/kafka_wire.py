@@ -562,6 +562,7 @@ class KafkaBroker:
         self.max_in_flight = 1
         self._pconns: Dict[int, Connection] = {}
         self._inflight: "collections.deque" = collections.deque()
+        self.connect_wait_s = float(connect_wait_s)
         self._boot = self._connect_any(connect_wait_s)
         self._rr = itertools.count()
         self.retries_done = 0                               # refresh-and-retry count (tests, metrics)
@@ -635,8 +636,16 @@ class KafkaBroker:
             return
         body = (Writer().array([name], lambda w, t: w.string(t).i32(partitions or 1).i16(1)
                                .array([], None).array([], None)).i32(int(self.timeout * 1000)).build())
-        r = self._boot_request(CREATE_TOPICS, 0, body)
-        for tname, err in r.array(lambda x: (x.string(), x.i16())):
+        # a replicated cluster creates topics once every broker has registered: LEADER_NOT_AVAILABLE
+        # until then, retried for up to connect_wait_s (at least 30 s)
+        t_end = time.monotonic() + max(30.0, self.connect_wait_s)
+        while True:
+            r = self._boot_request(CREATE_TOPICS, 0, body)
+            errs = r.array(lambda x: (x.string(), x.i16()))
+            if not any(err == ERR_LEADER_NOT_AVAILABLE for _t, err in errs) or time.monotonic() > t_end:
+                break
+            time.sleep(0.2)
+        for tname, err in errs:
             if err not in (ERR_NONE, ERR_TOPIC_EXISTS):
                 raise BrokerError(f"CreateTopics {tname}: error {err}")
         self.metadata([name])
