@@ -56,4 +56,12 @@ run repl_json_90s_kill 400 $R --seconds 90 --producers 3 --rate 1.2e6 --fmt json
 run repl_txb1_p8_rf1 240 $R --kafka-rf 1 --seconds 30 --producers 8 --rate 0 --fmt txb1 --log-dir $O/rt1 --out $O/repl_txb1_p8_rf1.json
 run topo4_count 300 $D --ranks 4 --rehearsal --seconds 20 --producers 3 --rate 600000 --fmt json --trace \
     --log-dir $O/t4c --out $O/topo4_count.json
+# the same rehearsal with 2 hardware queues per rank (8 in all): is the ~10 ms device time
+# slicing among the 4 resident persistent kernels a hardware-queue oversubscription?
+GPU_MAX_HW_QUEUES=2 run topo4_count_hwq2 300 $D --ranks 4 --rehearsal --seconds 20 --producers 3 --rate 600000 --fmt json \
+    --trace --log-dir $O/t4c_q2 --out $O/topo4_count_hwq2.json
+for t in t4c t4c_q2; do
+  [ -d $O/$t/service_trace ] && python bench/tail_attribution.py $O/$t/service_trace/rank*.npz --out $O/${t}_tail.json > /dev/null \
+    && python -c "import json; [print('$t', r['trace'][-9:], r['arrival_to_landed_us']['p99'], r['device_start_wait_us'], r['device_stall_windows']) for r in json.load(open('$O/${t}_tail.json'))]"
+done
 st done
