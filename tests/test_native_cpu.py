@@ -74,6 +74,23 @@ def test_spsc_ring_stress_under_sanitizers(tmp_path, sanitizer):
     assert "ring stress ok" in out.stdout
 
 
+def test_dedupe_index_stress_under_asan(tmp_path):
+    """The KIE tier's windowed dedupe index (csrc/engine/dedupe.cpp) against a reference model
+    under ASan/UBSan: repeats within and across batches, keys re-admitted after leaving the
+    window, recovery inserts, lookups, a tiny window that wraps the table many times."""
+    from ccfd_demo_summit_amd.ops.build import CSRC
+    exe = tmp_path / "dedupe_stress"
+    r = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                        str(CSRC / "tests" / "dedupe_stress.cpp"), str(CSRC / "engine" / "dedupe.cpp"), "-o", str(exe)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip(f"sanitizer build unavailable: {r.stderr[-300:]}")
+    for rounds, window in ((3000, 1000), (600, 7)):
+        out = subprocess.run([str(exe), str(rounds), str(window)], capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "dedupe stress ok" in out.stdout
+
+
 def test_json_parser_features_array_and_errors(L):
     rc, f, ids, _ = _parse(L, [json.dumps({"features": list(range(30)), "tx_id": "12"})])
     assert rc == 1 and ids[0] == 12
