@@ -391,6 +391,12 @@ def main(argv=None):
         eng_env["CCFD_INGEST_THREADS"] = str(a.ingest_threads or max(1, a.partitions // a.ranks))
         eng_env["ROUTER_STANDARD_MODE"] = a.standard_mode
         eng_env["CCFD_NATIVE_SERVE"] = "1" if a.serving == "native" else "0"
+        if a.rehearsal and a.ranks > 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
+            # several ranks on ONE GPU: 2 hardware queues each (the persistent kernel's and one
+            # for everything else).  With HIP's default 4, 4 ranks' 16 queues oversubscribe the
+            # GPU's queue slots and the scheduler time-slices them -- ~10 ms stalls every ~85 ms,
+            # arrival -> scored p99 8 ms; with 2, p99 45-49 us (profiles/r5/final/)
+            eng_env["GPU_MAX_HW_QUEUES"] = "2"
         out["serving"] = a.serving
         if a.trace:
             eng_env["CCFD_SERVICE_TRACE"] = str(log_dir / "service_trace")
@@ -751,7 +757,13 @@ def main(argv=None):
         shutil.rmtree(kdir, ignore_errors=True)
     # the engine ranks' hand-off totals (printed as they stop): signals applied vs stale
     eng_logs = "".join(p.text() for p in procs if p.name == "engine")
-    hs = [json.loads(m) for m in re.findall(r"hand-off (\{.*\})", eng_logs)]
+    hs = []
+    dec = json.JSONDecoder()
+    for m in re.finditer(r"hand-off \{", eng_logs):      # ranks stopping together may share a line
+        try:
+            hs.append(dec.raw_decode(eng_logs, m.end() - 1)[0])
+        except ValueError:
+            pass
     if hs:
         out["handoff_signals"] = {"ok": sum(h.get("signals_ok", 0) for h in hs),
                                   "stale": sum(h.get("signals_stale", 0) for h in hs),
