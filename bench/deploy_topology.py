@@ -241,6 +241,8 @@ def main(argv=None):
     ap.add_argument("--ranks", type=int, default=1, help="engine ranks (torchrun --nproc-per-node)")
     ap.add_argument("--rehearsal", action="store_true",
                     help="several ranks on one GPU: gloo collectives + CCFD_DEVICE_MODULO (functional check)")
+    ap.add_argument("--rehearsal-hw-queues", type=int, default=2,
+                    help="--rehearsal with several ranks on one GPU: GPU_MAX_HW_QUEUES per rank (0 = inherit)")
     ap.add_argument("--producers", type=int, default=3)
     ap.add_argument("--rate", type=float, default=0.0, help="total produce rate tx/s (0 = open loop, max)")
     ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
@@ -391,12 +393,12 @@ def main(argv=None):
         eng_env["CCFD_INGEST_THREADS"] = str(a.ingest_threads or max(1, a.partitions // a.ranks))
         eng_env["ROUTER_STANDARD_MODE"] = a.standard_mode
         eng_env["CCFD_NATIVE_SERVE"] = "1" if a.serving == "native" else "0"
-        if a.rehearsal and a.ranks > 1 and "GPU_MAX_HW_QUEUES" not in os.environ:
+        if a.rehearsal and a.ranks > 1 and a.rehearsal_hw_queues > 0:
             # several ranks on ONE GPU: 2 hardware queues each (the persistent kernel's and one
             # for everything else).  With HIP's default 4, 4 ranks' 16 queues oversubscribe the
             # GPU's queue slots and the scheduler time-slices them -- ~10 ms stalls every ~85 ms,
             # arrival -> scored p99 8 ms; with 2, p99 45-49 us (profiles/r5/final/)
-            eng_env["GPU_MAX_HW_QUEUES"] = "2"
+            eng_env["GPU_MAX_HW_QUEUES"] = str(a.rehearsal_hw_queues)
         out["serving"] = a.serving
         if a.trace:
             eng_env["CCFD_SERVICE_TRACE"] = str(log_dir / "service_trace")

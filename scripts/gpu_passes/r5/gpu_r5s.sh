@@ -3,7 +3,7 @@
 # default of 2 hardware queues per rank when ranks share one GPU.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}" || exit 1
-O=gpurun_out/r5s; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
+O=gpurun_out/${R5S_OUT:-r5s}; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
 st() { echo "[r5s] $(date +%T) $*"; }
 T="python bench/deploy_topology.py --ranks 4 --rehearsal --seconds 20 --producers 3 --rate 600000 --fmt json --trace"
 for m in count process; do
