@@ -173,7 +173,6 @@ typedef struct ccfd_persist_dev {    // device memory
   unsigned int nflag[CCFD_PERSIST_MAX_RING];      // flagged rows per ring slot
   ccfd_persist_desc desc[CCFD_PERSIST_MAX_RING];  // device mirror of the descriptor ring
   unsigned long long tstart[CCFD_PERSIST_MAX_RING];  // K7: device clock when item 0 was claimed
-  unsigned long long work_q[8][16];               // per-XCD claim counters, one 128-B line each (experiment builds)
 } ccfd_persist_dev;
 
 typedef struct ccfd_persist_args {

@@ -61,11 +61,7 @@ __device__ __forceinline__ void persist_doorbell(const ccfd_persist_args& a, int
       // every lane's descriptor store is ordered before the new posted count
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       mirrored += nb;
-#ifdef CCFD_EXP_DOORBELL_WAVES            // experiment build: several pollers, the count never goes back
-      if (lane == 0) __hip_atomic_fetch_max(&a.dev->posted, mirrored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
       if (lane == 0) __hip_atomic_store(&a.dev->posted, mirrored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 #ifdef CCFD_EXP_ITEM_TRACE
       if (lane == 0) {
         const unsigned long long k =
@@ -108,21 +104,6 @@ __device__ __forceinline__ void persist_read_desc(const ccfd_persist_args& a, un
   sdesc.n = (int32_t)(ne & 0xffffffffull);
   sdesc.epoch = (int32_t)(ne >> 32);
   sdesc.seq = b;
-#ifdef CCFD_EXP_DOORBELL_WAVES
-  // several pollers mirror the ring: a late poller's copy of an older lap must not be taken
-  // for this batch -- the mirrored seq word says which batch a slot holds
-  while (__hip_atomic_load(d + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != b) {
-    __builtin_amdgcn_s_sleep(2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    sdesc.x = reinterpret_cast<const float*>(__hip_atomic_load(d + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sdesc.proba = reinterpret_cast<float*>(__hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sdesc.route = reinterpret_cast<uint8_t*>(__hip_atomic_load(d + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sdesc.flag_idx = reinterpret_cast<unsigned int*>(__hip_atomic_load(d + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned long long ne2 = __hip_atomic_load(d + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sdesc.n = (int32_t)(ne2 & 0xffffffffull);
-    sdesc.epoch = (int32_t)(ne2 >> 32);
-  }
-#endif
 }
 
 // Thread 0: wait until claimed item `item`'s micro-batch is posted, then read its descriptor;

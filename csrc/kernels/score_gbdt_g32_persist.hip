@@ -45,13 +45,7 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
   const int C = a.items_per_batch;
   const int cpw = a.tiles_per_wave * kG32Waves / kW;      // 64-row chunks per wave per item
   if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
-#ifdef CCFD_EXP_DOORBELL_WAVES
-    // experiment build: all 4 waves poll, a quarter of a poll round trip apart
-    for (int k = 0; k < 40 * wave; ++k) __builtin_amdgcn_s_sleep(127);
-    persist_doorbell(a, lane);
-#else
     if (wave == 0) persist_doorbell(a, lane);
-#endif
     return;                                               // no barrier is ever used by WG 0
   }
   const char* blob = reinterpret_cast<const char*>(a.blob);
@@ -67,9 +61,6 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
   epi_init(epi);
   __syncthreads();
   unsigned long long posted_cache = 0;                    // thread 0 only
-#ifdef CCFD_EXP_XCD_QUEUES
-  const unsigned long long work_base = __hip_atomic_load(&a.dev->work_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 
   // per-item accumulators of this wave (flushed by item_flush)
   unsigned fraud = 0, rows = 0, stale = 0;
@@ -113,28 +104,14 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
     }
     fraud = rows = stale = 0;
     psum = 0;
-#ifdef CCFD_EXP_TICKET_OVERLAP
-    persist_item_close(a, epi, d, tid);                   // ticket: next iteration, beside the claim
-#else
     persist_item_done(a, epi, d, slot, C, tid);
-#endif
   };
   auto k7_start = [&](unsigned long long it, int slot) __attribute__((always_inline)) {
     if (it % (unsigned long long)C == 0 && tid == 0)      // K7: micro-batch start (item 0 claimed first)
       __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
-#ifdef CCFD_EXP_TICKET_OVERLAP
-  // the previous item's ticket (release + ticket) is taken by wave 1 while wave 0 claims the
-  // next item: both before the barrier, so a claim that waits for the next posting never
-  // holds back the ticket that completes the batch the host is waiting on
-  ccfd_persist_desc prev_d{};
-  int prev_slot = -1;
-#endif
   for (;;) {
-#ifdef CCFD_EXP_TICKET_OVERLAP
-    if (tid == 64 && prev_slot >= 0) persist_ticket(a, prev_d, prev_slot, C);
-#endif
 #ifdef CCFD_EXP_ITEM_TRACE
     unsigned long long t_claim = 0, t_claimed = 0, t_seen = 0, t_desc = 0, t_load = 0, t_scored = 0;
     if (tid == 0) {
@@ -158,17 +135,6 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
       if (!s_cmd) persist_read_desc(a, b, sdesc);
       s_item = it;
       t_desc = wall_clock64();
-    }
-#elif defined(CCFD_EXP_XCD_QUEUES)
-    // experiment build: 8 claim counters, one per XCD (workgroup i runs on XCD i % 8): item
-    // base + 8k + q -- a claim contends with the ~24 workgroups of its XCD, not all 191
-    if (tid == 0) {
-      const unsigned q = blockIdx.x & 7u;
-      const unsigned long long k =
-          __hip_atomic_fetch_add(&a.dev->work_q[q][0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long it = work_base + 8ull * k + q;
-      s_cmd = persist_wait_item(a, C, posted_cache, it, sdesc);
-      s_item = it;
     }
 #else
     if (tid == 0) persist_claim(a, C, posted_cache, sdesc, s_item, s_cmd);
@@ -220,10 +186,6 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
     }
     CCFD_ITRACE(if (tid == 0) t_scored = wall_clock64();)
     item_flush(d, slot);
-#ifdef CCFD_EXP_TICKET_OVERLAP
-    prev_d = d;
-    prev_slot = slot;
-#endif
 #ifdef CCFD_EXP_ITEM_TRACE
     if (tid == 0) {
       const unsigned long long k =
