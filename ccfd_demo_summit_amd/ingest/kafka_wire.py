@@ -582,12 +582,18 @@ class KafkaBroker:
             time.sleep(0.25)
 
     def _boot_request(self, api: int, ver: int, body: bytes) -> Reader:
-        try:
-            return self._boot.request(api, ver, body)
-        except (OSError, ConnectionError):
-            self._boot.close()
-            self._boot = self._connect_any(self.timeout)
-            return self._boot.request(api, ver, body)
+        # a broker that dies (or is being killed) right as we reconnect to it resets the new
+        # connection too: try a few bootstrap connections before giving up
+        for attempt in range(4):
+            try:
+                return self._boot.request(api, ver, body)
+            except (OSError, ConnectionError):
+                self._boot.close()
+                if attempt == 3:
+                    raise
+                time.sleep(0.05 * attempt)
+                self._boot = self._connect_any(self.timeout)
+        raise AssertionError("unreachable")
 
     def _api_versions(self) -> Dict[int, Tuple[int, int]]:
         r = self._boot_request(API_VERSIONS, 0, b"")
