@@ -356,7 +356,6 @@ def cmd_engine(a, cfg):
     from prometheus_client import CollectorRegistry, generate_latest
 
     from ..metrics.exporter import EngineModelCollector, GpuEngineCollector, MetricsHub
-    from ..ops.kernels import DeviceModel
     from ..parallel.dp import broadcast_model, init_distributed, resolve_row_format
     from ..router.handoff import KieHandoff
     from ..router.router import Router
