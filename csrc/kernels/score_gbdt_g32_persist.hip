@@ -71,7 +71,13 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
     unsigned b0[kF];
     const unsigned meta = gx_lift<kG20>(cur, b0);
     float acc[1];
+#ifdef CCFD_EXP_READ_ONLY
+    // experiment build only: the same items, loads, outputs and protocol with the trees replaced
+    // by a use of the bins -- what the persistent read + completion path alone sustains
+    acc[0] = (float)(b0[0] + b0[kF - 1]) * 1e-3f;
+#else
     g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
+#endif
     const int row = chunk * kG32Rows + lane;
     const bool valid = row < n;
     const bool fresh = ((meta >> 8) & 0xffu) == stamp;
