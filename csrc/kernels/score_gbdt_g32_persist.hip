@@ -203,141 +203,6 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
   }
 }
 
-// Claim-ahead items (CCFD_EXP_CLAIM_AHEAD experiment build).  profiles/r5/G20.md: the claimed
-// kernel's item is [descriptor 2.6 us][first load 3.6 us][trees 20 us][completion 6 us], and the
-// same path with the trees removed sustains 2.78e9 tx/s (96.6 % of the link) -- the link idles
-// while a workgroup's 4 waves evaluate trees.  Here, right before the LAST chunk of an item is
-// scored, thread 0 claims the next item (one atomic) and, if its micro-batch is already posted,
-// every wave issues that item's first chunk: its PCIe round trip overlaps the last chunk's trees
-// and the completion protocol, and the item after starts with its data already in registers.
-// A workgroup holds the next claim only for that last chunk + completion (round 4's rejected
-// two-item pipeline held it for a whole item).
-template <int D, bool kR, bool kG20>
-__global__ __launch_bounds__(256) void persist_gbdt_ahead_kernel(ccfd_persist_args a) {
-  extern __shared__ __attribute__((aligned(16))) float lv[];
-  __shared__ uint4 xt[kG32Waves][128];
-  __shared__ EpilogueLds epi;
-  __shared__ ccfd_persist_desc sdesc[2];
-  __shared__ unsigned long long s_item[2];
-  __shared__ int s_cmd, s_ready;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int C = a.items_per_batch;
-  const int cpw = a.tiles_per_wave;
-  if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
-    if (wave == 0) persist_doorbell(a, lane);
-    return;
-  }
-  const char* blob = reinterpret_cast<const char*>(a.blob);
-  const int T = a.gbdt_trees;
-  const float base = *reinterpret_cast<const float*>(blob + 16);
-  const unsigned stamp = (unsigned)*reinterpret_cast<const int*>(blob + 20);
-  const int tdw = ((4 * T * D + 15) & ~15) / 4;
-  const g32_cint_p feat = (g32_cint_p)(blob + kHeader);
-  const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
-  g32_stage_leaves<D>(blob, T, lv, tid, 256);
-  const float* leaves = lv;
-  epi_init(epi);
-  __syncthreads();
-  unsigned long long posted_cache = 0;                    // thread 0 only
-
-  unsigned fraud = 0, rows = 0, stale = 0;
-  unsigned long long psum = 0;
-  auto score_chunk = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, G32Row& cur)
-      __attribute__((always_inline)) {
-    gx_rows<kG20>(xt[wave], lane, cur);
-    unsigned b0[kF];
-    const unsigned meta = gx_lift<kG20>(cur, b0);
-    float acc[1];
-    g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
-    const int row = chunk * kG32Rows + lane;
-    const bool valid = row < n;
-    const bool fresh = ((meta >> 8) & 0xffu) == stamp;
-    const float p = fresh ? sigmoid(base + acc[0]) : __builtin_nanf("");
-    bool fr;
-    if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
-    else fr = valid && fresh && (p >= a.threshold);
-    if (valid) {
-      if (d.proba) st_g(d.proba + row, p);
-      if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
-      if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
-      atomicAdd(&epi.hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
-    }
-    const unsigned long long m = __ballot(fr);
-    fraud += __popcll(m);
-    rows += __popcll(__ballot(valid));
-    stale += __popcll(__ballot(valid && !fresh));
-    persist_emit_flagged(a, d, slot, m, fr, row, lane);
-  };
-
-  if (tid == 0) persist_claim(a, C, posted_cache, sdesc[0], s_item[0], s_cmd);
-  __syncthreads();
-  if (s_cmd) return;
-  int cur = 0;
-  bool loaded = false;                                    // pre holds this item's first chunk (in flight)
-  G32Row pre;
-  for (;;) {
-    const ccfd_persist_desc d = sdesc[cur];
-    const unsigned long long it = s_item[cur];
-    const int item = (int)(it % (unsigned long long)C);
-    const int slot = (int)(d.seq % (unsigned long long)a.ring);
-    const int n = d.n;
-    const unsigned char* xb = reinterpret_cast<const unsigned char*>(d.x);
-    if (it % (unsigned long long)C == 0 && tid == 0)      // K7: micro-batch start
-      __hip_atomic_store(&a.dev->tstart[slot], wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int c0 = item * (kG32Waves * cpw) + wave;
-    if (!loaded && c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre);
-    // every chunk but the last: the next one in flight while this one is scored
-#pragma unroll 1
-    for (int k = 0; k + 1 < cpw; ++k) {
-      const int chunk = c0 + kG32Waves * k;
-      if (chunk * kG32Rows >= n) break;                   // wave-uniform
-      G32Row cur_row = pre;
-      if ((chunk + kG32Waves) * kG32Rows < n) gx_fetch<kG20>(xb, n, chunk + kG32Waves, lane, pre);
-      score_chunk(d, slot, n, chunk, cur_row);
-    }
-    const int last = c0 + kG32Waves * (cpw - 1);
-    const bool has_last = last * kG32Rows < n;            // then pre holds (is loading) it
-    G32Row last_row = pre;
-    // claim the next item; if its micro-batch is posted, put its first chunk in flight now
-    const int nx = cur ^ 1;
-    if (tid == 0) {
-      const unsigned long long nit =
-          __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_item[nx] = nit;
-      s_ready = persist_try_item(a, C, posted_cache, nit, sdesc[nx]);
-    }
-    __syncthreads();
-    const bool ready = s_ready != 0;
-    if (ready) {
-      const ccfd_persist_desc dn = sdesc[nx];
-      const int c0n = (int)(s_item[nx] % (unsigned long long)C) * (kG32Waves * cpw) + wave;
-      if (c0n * kG32Rows < dn.n) gx_fetch<kG20>(reinterpret_cast<const unsigned char*>(dn.x), dn.n, c0n, lane, pre);
-    }
-    if (has_last) score_chunk(d, slot, n, last, last_row);
-    psum = wave_sum_u64(psum);
-    if (lane == 0 && rows) {
-      atomicAdd(&epi.fraud, fraud);
-      atomicAdd(&epi.rows, rows);
-      atomicAdd(&epi.psum_e6, psum);
-      unsigned long long* cnt = a.counters[d.epoch & 1];
-      if (stale && cnt) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)stale);
-    }
-    fraud = rows = stale = 0;
-    psum = 0;
-    persist_item_done(a, epi, d, slot, C, tid);           // (its vmcnt drain also lands the next item's loads)
-    if (!ready) {                                         // claimed, but its micro-batch was not posted yet
-      if (tid == 0) s_cmd = persist_wait_item(a, C, posted_cache, s_item[nx], sdesc[nx]);
-      __syncthreads();
-      if (s_cmd) return;
-    }
-    cur = nx;
-    loaded = ready;
-  }
-}
-
 // Pipelined static items (engine persist_items = pipelined / CCFD_PERSIST_PIPE=1; VERDICT r4
 // item 6).  The claimed kernel above ends every item with its outputs' release, a ticket and
 // then -- only then -- the next claim, descriptor read and first loads: a 512-row G20 item is
@@ -495,13 +360,6 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   if (g32_env("CCFD_G32_INFLIGHT", 0, 0, 1) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
-#ifdef CCFD_EXP_CLAIM_AHEAD
-  if (!gl && (a.flags & CCFD_ARG_CHUNK_RING) && !(a.flags & CCFD_ARG_PIPE_ITEMS)) {
-    if (a.rules) hipLaunchKernelGGL((persist_gbdt_ahead_kernel<D, true, kG20>), dim3(grid), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((persist_gbdt_ahead_kernel<D, false, kG20>), dim3(grid), dim3(256), lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
-  }
-#endif
   if (a.flags & CCFD_ARG_PIPE_ITEMS) {                    // pipelined static 512-row items
     if (gl || a.tiles_per_wave != 2 || grid < 2) return -2;
     if (a.rules) hipLaunchKernelGGL((persist_gbdt_pipe_kernel<D, true, kG20, 2>), dim3(grid), dim3(256), lds, s, a);
