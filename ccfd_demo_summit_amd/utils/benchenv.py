@@ -36,7 +36,7 @@ DIAGNOSTIC = {
 TUNING = {"CCFD_PERSIST_PIPE", "CCFD_PERSIST_ITEM_ROWS", "CCFD_MLP_WAVES", "CCFD_MLP_TPW", "CCFD_MLP_PF",
           "CCFD_MLP_REGW", "CCFD_MLP_WEIGHTS", "CCFD_GBDT_CPW", "CCFD_GBDT_R", "CCFD_GBDT_KERNEL",
           "CCFD_COHERENT_OUT", "CCFD_IDLE_FLUSH_US", "CCFD_COMPLETION_THREAD", "CCFD_KC_PARSE_THREADS",
-          "GPU_MAX_HW_QUEUES"}
+          "CCFD_G32_INFLIGHT", "CCFD_G32_GLOBAL_LEAVES", "GPU_MAX_HW_QUEUES"}
 
 
 def collect(environ: Optional[Mapping[str, str]] = None) -> Dict[str, str]:
