@@ -62,7 +62,7 @@ def parse_args(argv=None):
     ap.add_argument("--trace", default=None,
                     help="rank 0: write a Chrome / Perfetto timeline of the last 65536 timed micro-batches "
                          "(per-batch stage trace: queued, in flight, device, hand-off)")
-    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 192 for G20, 128 otherwise)")
+    ap.add_argument("--persist-grid", type=int, default=0, help="persistent workgroups (0 = engine default: 64 for W64 rows, 216 for G20, 128 otherwise)")
     ap.add_argument("--coalesce", type=int, default=8,
                     help="launch mode: ready micro-batches per kernel launch (each keeps its own completion)")
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "w64", "g32", "g20"],

@@ -492,8 +492,8 @@ class Engine {
     // workgroups per CU (see persist_init; 700 x 6: 3.8e8 tx/s at 128, 7.3e8 at 256 and
     // 1.01e9 at 512 with 256-row items, profiles/r2/g32_large_ensembles/)
     // G20 rows carry 1.6x the rows of G32 per PCIe byte, so more resident workgroups keep
-    // up: 192 (2.51e9 tx/s at p50 94 us, depth 4, 512-row items) vs 2.18e9 at 128 and
-    // 2.35e9 at 256 (profiles/r2/g20/sweep.txt)
+    // up: 216 (2.56-2.57e9 tx/s at p50 91 us, depth 4, 512-row items) vs 2.52e9 at 192,
+    // 2.53e9 at 240 and 2.45e9 at 249 (profiles/r5/pass_w/; r2: 2.18e9 at 128, g20/sweep.txt)
     const bool big_trees = (wire_flag & CCFD_ARG_WIRE_G32) && cfg.gbdt_trees * cfg.gbdt_depth > 1200;
     const int grid = cfg.persist_grid > 0 ? cfg.persist_grid
                      : persist_pipe ? CCFD_PERSIST_GRID

@@ -145,7 +145,7 @@ int ccfd_score_launch(const ccfd_score_args* a, void* stream);
 #define CCFD_PERSIST_ITEM_ROWS 256   // default item of f32 rows: 4 waves x 4 tiles x 16 rows (W64: 512, G32: 512)
 #define CCFD_PERSIST_GRID 128        // default resident workgroups (+ the doorbell workgroup 0)
 #define CCFD_PERSIST_GRID_W64 64     // ... for W64 rows (512-row items, every tile in flight)
-#define CCFD_PERSIST_GRID_G20 192    // ... for G20 rows (GBDT, BASELINE-size ensembles)
+#define CCFD_PERSIST_GRID_G20 216    // ... for G20 rows (GBDT, BASELINE-size ensembles)
 
 typedef struct ccfd_persist_desc {   // host-coherent pinned, written before `posted`
   const float* x;          // device-visible rows [n][30]
