@@ -3,6 +3,10 @@ processes (durable), P producer processes (TXB1 by default) for T seconds, no en
 a CPU box; prints one JSON line with the producers' total tx/s and each producer's own line.
 
     python bench/experiments/replicated_produce.py --producers 4 --seconds 10 --acks -1
+
+``--probe-ms M`` adds a visibility probe on its own topic: one small acks=all record every M ms,
+and a long-polling consumer that reports produce -> visible-to-consumers (the HW covers it)
+and produce -> acked latencies, p50 / p99 / max, under whatever load the producers add.
 """
 import argparse
 import json
@@ -21,6 +25,63 @@ from deploy_topology import free_ports, wait_port  # noqa: E402
 PY = sys.executable
 
 
+class _Probe:
+    """acks=all records on topic ``probe`` every ``period_ms``; a second connection long-polls
+    the partition and stamps when each offset becomes visible to consumers."""
+
+    def __init__(self, url: str, period_ms: float, seconds: float):
+        import threading
+        from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
+        self.sent, self.acked, self.seen = {}, {}, {}
+        self.prod = KafkaBroker(url, connect_wait_s=30.0)
+        self.cons = KafkaBroker(url, connect_wait_s=30.0)
+        self.period, self.seconds = period_ms / 1e3, seconds
+        self.stop = threading.Event()
+        self.tp = threading.Thread(target=self._produce, daemon=True)
+        self.tc = threading.Thread(target=self._consume, daemon=True)
+        self.tc.start()
+        self.tp.start()
+
+    def _produce(self):
+        t_end = time.monotonic() + self.seconds
+        k = 0
+        while time.monotonic() < t_end:
+            t0 = time.perf_counter()
+            self.sent[k] = t0
+            self.prod.produce_batch("probe", 0, [b"%d" % k], acks=-1)
+            self.acked[k] = time.perf_counter()
+            k += 1
+            time.sleep(max(0.0, self.period - (time.perf_counter() - t0)))
+        time.sleep(0.5)
+        self.stop.set()
+
+    def _consume(self):
+        off = 0
+        while not self.stop.is_set():
+            for r in self.cons.fetch("probe", 0, off, max_wait_ms=200):
+                self.seen.setdefault(int(r.value), time.perf_counter())
+                off = max(off, r.offset + 1)
+
+    def join(self):
+        import numpy as np
+        self.tp.join()
+        self.tc.join(5)
+        self.prod.close()
+        self.cons.close()
+
+        def q(d):
+            v = np.array([(d[k] - self.sent[k]) * 1e3 for k in d if k in self.sent])
+            if not len(v):
+                return None
+            return {"n": int(len(v)), "p50_ms": round(float(np.percentile(v, 50)), 3),
+                    "p99_ms": round(float(np.percentile(v, 99)), 3), "max_ms": round(float(v.max()), 3)}
+        t0 = min(self.sent.values()) if self.sent else 0.0
+        slow = sorted((round((self.sent[k] - t0) * 1e3, 1), round((self.acked[k] - self.sent[k]) * 1e3, 2))
+                      for k in self.acked if self.acked[k] - self.sent[k] > 0.005)
+        return {"visible": q(self.seen), "acked": q(self.acked), "sent": len(self.sent),
+                "slow_acks_at_ms": slow[:40]}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--brokers", type=int, default=3)
@@ -33,6 +94,7 @@ def main(argv=None) -> int:
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--single", action="store_true", help="the single-process durable broker instead")
     ap.add_argument("--rf", type=int, default=3, help="replication factor of the topic (controller --rf)")
+    ap.add_argument("--probe-ms", type=float, default=0.0, help="visibility probe period (0: off)")
     a = ap.parse_args(argv)
     kdir = tempfile.mkdtemp(prefix="ccfd-repl-produce-")
     ctl, = free_ports(1)
@@ -69,7 +131,10 @@ def main(argv=None) -> int:
         from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
         kb = KafkaBroker(env["BROKER_URL"], connect_wait_s=60.0)
         kb.create_topic("odh-demo", a.partitions)
+        if a.probe_ms > 0:
+            kb.create_topic("probe", 1)
         kb.close()
+        probe = _Probe(env["BROKER_URL"], a.probe_ms, a.seconds) if a.probe_ms > 0 else None
         prods = []
         for i in range(a.producers):
             f = open(Path(kdir) / f"producer{i}.log", "w+")
@@ -79,6 +144,7 @@ def main(argv=None) -> int:
                  "--seconds", str(a.seconds), "--acks", str(a.acks), "--max-in-flight", str(a.max_in_flight),
                  "--id-base", str((i + 1) << 40), "--seed-offset", str(i * 101)],
                 env=env, stdout=f, stderr=subprocess.STDOUT), f))
+        probe_res = probe.join() if probe is not None else None
         res = []
         for p, f in prods:
             p.wait(timeout=a.seconds + 180)
@@ -94,10 +160,10 @@ def main(argv=None) -> int:
             except psutil.Error:
                 cpu[name] = None
         tot = sum(r.get("produced", 0) for r in res)
-        secs = max(r.get("seconds", a.seconds) for r in res)
+        secs = max([r.get("seconds", a.seconds) for r in res] or [a.seconds])
         print(json.dumps({"tx_s": round(tot / secs, 1), "produced": tot, "producers": a.producers,
                           "acks": a.acks, "max_in_flight": a.max_in_flight, "replicated": not a.single, "rf": a.rf,
-                          "cpu_s": cpu, "per_producer": res}))
+                          "cpu_s": cpu, "probe": probe_res, "per_producer": res}))
     except BaseException:
         for f in logs:
             f.flush()
@@ -115,6 +181,11 @@ def main(argv=None) -> int:
         for f in logs:
             f.close()
         import shutil
+        if os.environ.get("CCFD_KEEP_LOGS"):            # broker / producer logs kept for reading
+            keep = Path(os.environ["CCFD_KEEP_LOGS"])
+            keep.mkdir(parents=True, exist_ok=True)
+            for lp in Path(kdir).glob("*.log"):
+                shutil.copy(lp, keep / lp.name)
         shutil.rmtree(kdir, ignore_errors=True)
     return 0
 

@@ -526,6 +526,26 @@ class KafkaLiteServer:
         body = self._dispatch(api, ver, r)
         if isinstance(body, list):                 # response parts, written without joining
             return [struct.pack(">ii", sum(len(b) for b in body) + 4, corr)] + body
+        if isinstance(body, asyncio.Future):
+            # a long-polled fetch or an acks=all produce: framed in a done callback, so the
+            # response is written one loop iteration after the event that completes it (a
+            # coroutine wrapper costs a task step per layer -- each a loop iteration, several
+            # on the replication path of every acknowledged batch)
+            out = asyncio.get_running_loop().create_future()
+
+            def framed(f):
+                if f.cancelled():
+                    out.cancel()
+                elif f.exception() is not None:
+                    out.set_exception(f.exception())
+                else:
+                    b = f.result()
+                    if isinstance(b, list):
+                        out.set_result([struct.pack(">ii", sum(len(x) for x in b) + 4, corr)] + b)
+                    else:
+                        out.set_result(struct.pack(">ii", len(b) + 4, corr) + b)
+            body.add_done_callback(framed)
+            return out
         if not isinstance(body, (bytes, bytearray)):
             async def later():
                 b = await body
@@ -721,26 +741,37 @@ class KafkaLiteServer:
             return self._produce_later(body, ticket)
         return body
 
-    async def _produce_replicated(self, build, ticket: int, waits, timeout_ms: int) -> bytes:
-        """acks=all on a replicated leader: answered once written here AND the partition's high
-        watermark covers the batch (every in-sync replica has it).  Leadership lost meanwhile,
-        or the timeout: NOT_LEADER, so the producer refreshes metadata and retries (its
-        idempotent sequence makes a retry of a replicated batch a no-op)."""
+    def _produce_replicated(self, build, ticket: int, waits, timeout_ms: int) -> "asyncio.Future":
+        """acks=all on a replicated leader: answered once the partition's high watermark covers
+        the batch (every in-sync replica has it).  Leadership lost meanwhile, or the timeout:
+        NOT_LEADER, so the producer refreshes metadata and retries (its idempotent sequence
+        makes a retry of a replicated batch a no-op)."""
         # acks=all: answered once the high watermark covers the batch (in the memory of every
         # in-sync replica, each writing it to disk right behind) -- not after this broker's own
-        # write, which would put the leader's disk latency in front of every acknowledgement
+        # write, which would put the leader's disk latency in front of every acknowledgement.
+        # Callbacks, not a coroutine: the response is built in the iteration that moves the HW.
         rep = self.cluster.replica
-        deadline = time.monotonic() + max(0.1, timeout_ms / 1000.0)
-        for topic, p, end, entry in waits:
-            ok = False
-            try:
-                ok = await asyncio.wait_for(rep.wait_hw(topic, p, end), max(0.0, deadline - time.monotonic()))
-            except asyncio.TimeoutError:
-                ok = False
-            if not ok:
-                entry[1] = ERR_NOT_LEADER
-                self.metrics.failed_produce.labels(topic, "Kafka").inc()
-        return build()
+        loop = asyncio.get_running_loop()
+        out = loop.create_future()
+        hw = [(rep.wait_hw(topic, p, end), topic, entry) for topic, p, end, entry in waits]
+
+        def answer(timed_out: bool) -> None:
+            if out.done():
+                return
+            if not timed_out and not all(f.done() for f, _t, _e in hw):
+                return
+            th.cancel()
+            for f, topic, entry in hw:
+                if not (f.done() and f.result()):
+                    entry[1] = ERR_NOT_LEADER
+                    self.metrics.failed_produce.labels(topic, "Kafka").inc()
+            out.set_result(build())
+        th = loop.call_later(max(0.1, timeout_ms / 1000.0), answer, True)
+        for f, _t, _e in hw:
+            if not f.done():
+                f.add_done_callback(lambda _f: answer(False))
+        answer(False)
+        return out
 
     def _api_22(self, r: Reader) -> bytes:                  # InitProducerId v0 (idempotence only)
         r.string(); r.i32()
@@ -764,25 +795,35 @@ class KafkaLiteServer:
             return self._fetch_later(reqs, max_bytes, max_wait_ms, replica_id)
         return parts
 
-    async def _fetch_later(self, reqs, max_bytes: int, max_wait_ms: int, replica_id: int = -1):
-        fut = asyncio.get_running_loop().create_future()
+    def _fetch_later(self, reqs, max_bytes: int, max_wait_ms: int, replica_id: int = -1) -> "asyncio.Future":
+        """The long poll: a future of the response parts, filled in the callback of the wake-up
+        (data / a high watermark move on a requested partition) or of max_wait."""
+        loop = asyncio.get_running_loop()
+        wake = loop.create_future()
+        out = loop.create_future()
         tps = [(t, p) for t, ps in reqs for p, _o, _m in ps]
         waiters = self.cluster.fetch_waiters if replica_id < 0 else self.cluster.replica_waiters
         for tp in tps:
-            waiters.setdefault(tp, set()).add(fut)
+            waiters.setdefault(tp, set()).add(wake)
         self.cluster.long_polls += 1
-        try:
-            await asyncio.wait_for(fut, max_wait_ms / 1000.0)
-        except asyncio.TimeoutError:
-            pass
-        finally:
+        th = loop.call_later(max_wait_ms / 1000.0, lambda: wake.done() or wake.set_result(None))
+
+        def finish(_f) -> None:
+            th.cancel()
             for tp in tps:
                 ws = waiters.get(tp)
                 if ws is not None:
-                    ws.discard(fut)
+                    ws.discard(wake)
                     if not ws:
                         waiters.pop(tp, None)
-        return self._fetch_parts(reqs, max_bytes, replica_id)[0]
+            if out.done():
+                return
+            try:
+                out.set_result(self._fetch_parts(reqs, max_bytes, replica_id)[0])
+            except Exception as e:                      # noqa: BLE001 -- the connection is closed
+                out.set_exception(e)
+        wake.add_done_callback(finish)
+        return out
 
     def _fetch_parts(self, reqs, max_bytes: int, replica_id: int = -1):
         """(response parts, record bytes in them, no partition errored).  Replicated mode: a
