@@ -586,17 +586,26 @@ class KafkaLiteServer:
                 if not f.done():
                     f.set_result(None)
 
-    async def _produce_later(self, body: bytes, ticket: int) -> bytes:
-        await self._written_ticket(ticket)
-        return body
-
-    async def _written_ticket(self, ticket: int) -> None:
-        """Until the durable store's writer has written ``ticket``."""
+    def _produce_later(self, body: bytes, ticket: int) -> "asyncio.Future":
+        """The produce response, once the durable store's writer has written ``ticket`` (a
+        future filled in the done callback of the write, like the long-polled fetches)."""
+        loop = asyncio.get_running_loop()
+        out = loop.create_future()
         if not ticket or ticket <= self.cluster.written:
-            return
-        fut = asyncio.get_running_loop().create_future()
+            out.set_result(body)
+            return out
+        fut = loop.create_future()
         self.cluster.produce_waiters.append((ticket, fut))
-        await fut
+
+        def written(f) -> None:
+            if f.cancelled():
+                out.cancel()
+            elif f.exception() is not None:
+                out.set_exception(f.exception())
+            else:
+                out.set_result(body)
+        fut.add_done_callback(written)
+        return out
 
     def _topic(self, name: str) -> bool:
         if self.cluster.replica is not None:    # topics exist once the controller created them
