@@ -94,6 +94,7 @@ def main(argv=None) -> int:
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--single", action="store_true", help="the single-process durable broker instead")
     ap.add_argument("--rf", type=int, default=3, help="replication factor of the topic (controller --rf)")
+    ap.add_argument("--retention-batches", type=int, default=500, help="per partition (the deploy harness's default)")
     ap.add_argument("--probe-ms", type=float, default=0.0, help="visibility probe period (0: off)")
     a = ap.parse_args(argv)
     kdir = tempfile.mkdtemp(prefix="ccfd-repl-produce-")
@@ -117,7 +118,8 @@ def main(argv=None) -> int:
         if a.single:
             start("kafka-lite", [PY, "-m", K + "kafka_lite", "--host", "127.0.0.1", "--port", str(base),
                                  "--nodes", str(a.brokers), "--partitions", str(a.partitions),
-                                 "--metrics-port", str(mbase), "--data-dir", kdir + "/single"])
+                                 "--metrics-port", str(mbase), "--data-dir", kdir + "/single",
+                                 "--retention-batches", str(a.retention_batches)])
         else:
             start("controller", [PY, "-m", K + "kafka_controller", "--host", "127.0.0.1", "--port", str(ctl),
                                  "--brokers", str(a.brokers), "--rf", str(a.rf), "--data-dir", kdir + "/ctl"])
@@ -125,7 +127,8 @@ def main(argv=None) -> int:
             for i in range(a.brokers):
                 start(f"broker{i + 1}", [PY, "-m", K + "kafka_lite", "--host", "127.0.0.1", "--port", str(base + i),
                                          "--node-id", str(i + 1), "--controller", f"http://127.0.0.1:{ctl}",
-                                         "--metrics-port", str(mbase + i), "--data-dir", f"{kdir}/b{i + 1}"])
+                                         "--metrics-port", str(mbase + i), "--data-dir", f"{kdir}/b{i + 1}",
+                                         "--retention-batches", str(a.retention_batches)])
         for i in range(a.brokers):
             wait_port(base + i, 60)
         from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
