@@ -554,6 +554,7 @@ class Consumer {
   // 4096-message batch costs ~5 ms of serial parse; the batch's last row waited for all of it.
   struct Rec { const uint8_t* val; int32_t vlen; int64_t off; };
   static constexpr int64_t kParMin = 256;
+  static constexpr int64_t kParChunk = 1024;
   std::vector<Rec> recs;
   // 4 by default: in the deployed topology (JSON 1.2e6/s, 4096-message produce requests) the
   // engine's share of produce -> scored p50 fell from 3.2 to 1.4 ms on the same box
@@ -614,16 +615,20 @@ class Consumer {
   };
   std::unique_ptr<Pool> pool;
 
-  void parse_parallel() {
+  // records [c0, c1) of recs, split over the parse pool (results at their record index)
+  void parse_parallel(int64_t c0, int64_t c1) {
     const int64_t n = (int64_t)recs.size();
-    pfeat.resize((size_t)n * CCFD_N_FEATURES);
-    pid.resize((size_t)n);
-    pcust.resize((size_t)n);
-    pok.assign((size_t)n, 0);
+    if (c0 == 0) {
+      pfeat.resize((size_t)n * CCFD_N_FEATURES);
+      pid.resize((size_t)n);
+      pcust.resize((size_t)n);
+      pok.assign((size_t)n, 0);
+    }
     if (!pool) pool.reset(new Pool(parse_threads - 1));
     const int T = parse_threads;
-    pool->run([this, n, T](int k) {
-      const int64_t lo = n * k / T, hi = n * (k + 1) / T;
+    const int64_t m = c1 - c0;
+    pool->run([this, c0, m, T](int k) {
+      const int64_t lo = c0 + m * k / T, hi = c0 + m * (k + 1) / T;
       for (int64_t i = lo; i < hi; ++i) {
         const Rec& rc = recs[(size_t)i];
         if (rc.vlen <= 0) continue;
@@ -753,10 +758,14 @@ class Consumer {
         recs.push_back({val, (int32_t)std::max<int64_t>(vlen, 0), base + od});
       }
       // the records, in order: JSON messages of a large batch are parsed on the parse pool
-      // first (CCFD_KC_PARSE_THREADS), then every record is written / booked sequentially
+      // (CCFD_KC_PARSE_THREADS) kParChunk at a time, each chunk written / booked sequentially
+      // before the next is parsed -- the batch's first rows reach the scoring ring after one
+      // chunk's parse instead of the whole batch's (a 4096-message produce request: ~0.7 ms)
       const bool par = all_json && parse_threads > 1 && (int64_t)recs.size() >= kParMin;
-      if (par) parse_parallel();
-      for (size_t i = 0; i < recs.size(); ++i) {
+      const size_t nrec = recs.size();
+      const size_t step = par ? (size_t)kParChunk : nrec;
+      for (size_t i = 0; i < nrec; ++i) {
+        if (par && i % step == 0) parse_parallel((int64_t)i, (int64_t)std::min(nrec, i + step));
         const Rec& rc = recs[i];
         PState& s = ps[pi];
         if (rc.off < s.next_offset) continue;        // already consumed (batch starts below the fetch offset)

@@ -73,6 +73,35 @@ def test_txb1_and_json_into_rows(lite, fmt):
         kb.close()
 
 
+def test_large_json_batch_parsed_in_chunks_keeps_order(lite):
+    """One produce request of 2500 JSON messages: the parse pool takes it 1024 records at a
+    time (kafka_consumer.cpp kParChunk), each chunk written before the next is parsed -- every
+    row lands once, in offset order, with its own values."""
+    kb = KafkaBroker(lite.bootstrap)
+    kb.create_topic("big", 1)
+    n = 2500
+    X, _ = generate(n, seed=9)
+    ids = np.arange(n, dtype=np.uint64) + 1000
+    cu = (np.arange(n) % 331).astype(np.uint32)
+    msgs = [json.dumps({"id": int(ids[i]), "customer_id": int(cu[i]),
+                        **{nm: float(v) for nm, v in zip(FEATURE_NAMES, X[i])}}).encode() for i in range(n)]
+    kb.produce_many("big", msgs, partition=0)
+    kc = NativeKafkaConsumer.for_arrays(lite.bootstrap, "big", {0: 0}, capacity=4096).start()
+    try:
+        assert _wait(kc, n), (kc.stats(), kc.last_error())
+        st = kc.stats()
+        assert st["records"] == n and st["errors"] == 0
+        f0, i0, c0 = kc.arrays[0]
+        np.testing.assert_array_equal(i0[:n], ids)
+        np.testing.assert_array_equal(c0[:n], cu)
+        np.testing.assert_array_equal(f0[:n], X)
+        assert kc.committable() == {0: n}
+    finally:
+        kc.stop()
+        kc.close()
+        kb.close()
+
+
 def test_resume_from_offset_and_late_data(lite):
     kb = KafkaBroker(lite.bootstrap)
     kb.create_topic("t", 1)
