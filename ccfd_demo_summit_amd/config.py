@@ -58,6 +58,12 @@ class KieConfig:
     shards: int = 1                  # KIE shard processes (process/sharding.py): starts routed by
                                      # transaction-id hash, signals / tasks by shard-encoded id;
                                      # KIE_SERVER_URL then lists one URL per shard or a {shard} template
+    standard_dedupe_window: int = 1 << 20    # standard-start dedupe keys kept at least (per shard)
+    standard_dedupe_capacity: int = 0        # hard bound of uncommitted + kept keys (0 = 4 x window):
+                                             # beyond it a start batch is refused (503, retried) --
+                                             # keys leave only once the engine committed past them
+    standard_audit_rows: int = 1 << 22       # standard instances answerable by transaction id from
+                                             # memory (per shard); older ones from the journal
 
 
 @dataclass
@@ -158,6 +164,9 @@ ENV_MAP = {
     "CCFD_INGEST_THREADS": ("engine", "ingest_threads", int),
     "CCFD_KIE_NOTIFICATION_TIMEOUT_S": ("kie", "notification_timeout_s", float),
     "CCFD_KIE_SHARDS": ("kie", "shards", int),
+    "CCFD_KIE_DEDUPE_WINDOW": ("kie", "standard_dedupe_window", int),
+    "CCFD_KIE_DEDUPE_CAPACITY": ("kie", "standard_dedupe_capacity", int),
+    "CCFD_KIE_AUDIT_ROWS": ("kie", "standard_audit_rows", int),
     "CCFD_NOTIFIER_SEED": ("notifier", "seed", int),
 }
 

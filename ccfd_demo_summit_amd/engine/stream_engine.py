@@ -14,8 +14,8 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..ops._lib import (BATCH_TRACE_DTYPE, BIN_FORMATS, FLAGGED_DTYPE, SCORED_DTYPE, MODEL_IDS, N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig,
-                        EngineStats, Flagged, check, last_error, lib)
+from ..ops._lib import (BATCH_TRACE_DTYPE, BIN_FORMATS, ENGINE_FLAG_FULL, FLAGGED_DTYPE, SCORED_DTYPE, MODEL_IDS,
+                        N_COUNTER_SLOTS, ROW_FORMATS, EngineConfig, EngineStats, Flagged, check, last_error, lib)
 from ..ops.kernels import ROW_BYTES, DeviceModel
 
 N_FEATURES = 30
@@ -203,6 +203,19 @@ class StepStats:
     origin_batches: int = 0
     origin_hist: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
     origin_hist_rows: np.ndarray = field(default_factory=lambda: np.zeros(256, np.uint64))
+    submitted: int = 0                   # micro-batches submitted by the call
+    flag_full_events: int = 0            # completions deferred on a full flagged ring (cumulative)
+
+
+class HandoffLost(RuntimeError):
+    """The engine reports fraud-routed records it could not hand off.  The ring reserves room
+    for a whole batch before retiring it, so this is a broken invariant, never back-pressure:
+    a caller that commits offsets must stop instead of committing past lost fraud cases."""
+
+
+def check_lossless(st: "StepStats") -> None:
+    if st.dropped:
+        raise HandoffLost(f"{st.dropped} fraud-routed records were dropped by the engine's flagged ring")
 
 
 _FMT_BY_ROW_BYTES = {120: "f32", 64: "w64", 32: "g32", 20: "g20"}
@@ -223,7 +236,8 @@ def _stats(st: EngineStats) -> StepStats:
                      np.ctypeslib.as_array(st.lat_hist_rows).copy(),
                      np.ctypeslib.as_array(st.dev_hist_rows).copy(), int(st.last_seq), last,
                      int(st.origin_batches), np.ctypeslib.as_array(st.origin_hist).copy(),
-                     np.ctypeslib.as_array(st.origin_hist_rows).copy())
+                     np.ctypeslib.as_array(st.origin_hist_rows).copy(), int(st.submitted),
+                     int(st.flag_full_events))
 
 
 class StreamEngine:
@@ -286,7 +300,10 @@ class StreamEngine:
             raise RuntimeError(f"ccfd_engine_create failed: {last_error()}")
         self.logs: Dict[int, PartitionLog] = {}
         self._flag_buf = (Flagged * 65536)()
-        self._flag_cap = max(1024, int(flag_capacity))
+        self._flag_cap = max(1024, int(flag_capacity), self.batch)
+        # records taken out of a full flagged ring by a blocking call (drain paths) so it could
+        # finish; drain_flagged / serve_collect return them first, in completion order
+        self._stash: List[np.ndarray] = []
 
     def close(self):
         if getattr(self, "h", None):
@@ -308,21 +325,56 @@ class StreamEngine:
 
     def add_log(self, partition: int, log: PartitionLog, cursor: int = 0) -> None:
         self._check_log(log)
-        check(lib().ccfd_engine_set_log(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
-                                        C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr),
-                                        log.n, int(cursor)), "ccfd_engine_set_log")
+        self._call(lambda: lib().ccfd_engine_set_log(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
+                                                     C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr),
+                                                     log.n, int(cursor)), "ccfd_engine_set_log")
         if log.amount is not None:
-            check(lib().ccfd_engine_set_amount(C.c_void_p(self.h), int(partition), C.c_void_p(log.amount.ptr)),
-                  "ccfd_engine_set_amount")
+            self._call(lambda: lib().ccfd_engine_set_amount(C.c_void_p(self.h), int(partition),
+                                                            C.c_void_p(log.amount.ptr)), "ccfd_engine_set_amount")
         self.logs[partition] = log
 
-    def pump(self, n_batches: int, batch_rows: Optional[int] = None, drain: bool = True) -> StepStats:
+    def _call(self, fn, what: str) -> None:
+        """Run a blocking native call that may need to retire in-flight batches; on a full
+        flagged ring it drains the ring into the stash and calls again (nothing is dropped)."""
+        while True:
+            rc = fn()
+            if rc != ENGINE_FLAG_FULL:
+                check(rc, what)
+                return
+            self._stash_ring()
+
+    def _stash_ring(self) -> int:
+        got = self._drain_ring(1 << 62)
+        if len(got):
+            self._stash.append(got)
+        return len(got)
+
+    def pump(self, n_batches: int, batch_rows: Optional[int] = None, drain: bool = True,
+             on_flagged=None) -> StepStats:
         """Score ``n_batches`` micro-batches.  ``drain=False`` keeps up to ``depth`` batches in
-        flight across calls (steady-state streaming); the last call of a run must drain."""
+        flight across calls (steady-state streaming); the last call of a run must drain.
+
+        Lossless hand-off: when the flagged ring cannot take a finished batch's fraud records,
+        the native pump stops (nothing retired, nothing lost); the ring is drained -- into
+        ``on_flagged(records)`` when given (the caller's hand-off), else into the stash the
+        next ``drain_flagged`` returns -- and pumping resumes with the remaining batches."""
         st = EngineStats()
-        check(lib().ccfd_engine_pump(C.c_void_p(self.h), int(n_batches), int(batch_rows or self.batch),
-                                     1 if drain else 0, C.byref(st)), "ccfd_engine_pump")
-        return _stats(st)
+        left = int(n_batches)
+        rows_b = int(batch_rows or self.batch)
+        while True:
+            before = int(st.submitted)
+            rc = lib().ccfd_engine_pump(C.c_void_p(self.h), left, rows_b, 1 if drain else 0, C.byref(st))
+            left -= int(st.submitted) - before
+            if rc != ENGINE_FLAG_FULL:
+                check(rc, "ccfd_engine_pump")
+                break
+            if on_flagged is not None:
+                on_flagged(self.drain_flagged())
+            else:
+                self._stash_ring()
+        out = _stats(st)
+        check_lossless(out)
+        return out
 
     def score(self, X: np.ndarray):
         """Synchronous score of a host matrix [n,30] -> (proba [n] f32, route [n] u8)."""
@@ -338,8 +390,8 @@ class StreamEngine:
             X = rows
         proba = np.empty(n, np.float32)
         route = np.empty(n, np.uint8)
-        check(lib().ccfd_engine_score_sync(C.c_void_p(self.h), X.ctypes.data, n, proba.ctypes.data,
-                                           route.ctypes.data), "ccfd_engine_score_sync")
+        self._call(lambda: lib().ccfd_engine_score_sync(C.c_void_p(self.h), X.ctypes.data, n, proba.ctypes.data,
+                                                        route.ctypes.data), "ccfd_engine_score_sync")
         return proba, route
 
     def flip_epoch(self, side_stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
@@ -361,8 +413,8 @@ class StreamEngine:
         if self.row_format in BIN_FORMATS and not same_bins(dm.bins, self.bins):
             raise ValueError("G32 hot swap: pack the new ensemble against the live bin table "
                              "(DeviceModel(model, bins=engine.bins)); its thresholds must be bin edges")
-        check(lib().ccfd_engine_set_blob(C.c_void_p(self.h), C.c_void_p(dm.blob.data_ptr())),
-              "ccfd_engine_set_blob")
+        self._call(lambda: lib().ccfd_engine_set_blob(C.c_void_p(self.h), C.c_void_p(dm.blob.data_ptr())),
+                   "ccfd_engine_set_blob")
         self.dm = dm                     # keeps the new blob alive; the old one may be freed now
         self.model_version = getattr(self, "model_version", 0) + 1
 
@@ -371,6 +423,25 @@ class StreamEngine:
         return lib().ccfd_engine_epoch_complete(C.c_void_p(self.h), int(flip_count)) == 1
 
     def drain_flagged(self, max_records: int = 1 << 30) -> np.ndarray:
+        """Fraud-routed records of completed batches, oldest first (stash, then the ring)."""
+        out: List[np.ndarray] = []
+        total = 0
+        while self._stash and total < max_records:
+            a = self._stash[0]
+            take = min(len(a), max_records - total)
+            out.append(a[:take])
+            total += take
+            if take == len(a):
+                self._stash.pop(0)
+            else:
+                self._stash[0] = a[take:]
+        if total < max_records:
+            out.append(self._drain_ring(max_records - total))
+        out = [a for a in out if len(a)]
+        return np.concatenate(out) if len(out) > 1 else out[0] if out else \
+            np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
+
+    def _drain_ring(self, max_records: int) -> np.ndarray:
         out: List[np.ndarray] = []
         total = 0
         while total < max_records:
@@ -389,7 +460,8 @@ class StreamEngine:
         """Opt in to a per-row scored-record ring of ``capacity`` rows (0 = off): every
         completed row -- fraud- and standard-routed -- with the kernel's proba_1 and route
         (``drain_scored``).  Streaming ``run()`` holds completed batches while it is full."""
-        check(lib().ccfd_engine_scored_enable(C.c_void_p(self.h), int(capacity)), "ccfd_engine_scored_enable")
+        self._call(lambda: lib().ccfd_engine_scored_enable(C.c_void_p(self.h), int(capacity)),
+                   "ccfd_engine_scored_enable")
         self._scored_cap = int(capacity)
 
     def drain_scored(self, max_records: int = 1 << 30) -> np.ndarray:
@@ -446,19 +518,24 @@ class StreamEngine:
         if rc < 0:
             raise RuntimeError(f"engine serving thread failed: {last_error()}")
         fl = self._collect_flag[:nf.value].copy()
+        if self._stash:                      # stashed by a blocking call: older than the ring's
+            fl = np.concatenate(self._stash + [fl])
+            self._stash = []
         rec = sc[:ns.value].copy() if sc is not None else None
-        return _stats(st), fl, rec
+        out = _stats(st)
+        check_lossless(out)
+        return out, fl, rec
 
     # ------------------------------------------------------------------ ring (streaming) mode
     def set_ring(self, partition: int, capacity: int) -> PartitionLog:
         """Register partition ``partition`` as a live SPSC ring of ``capacity`` rows."""
         log = PartitionLog(capacity, wire=self.wire, bins=self.bins)
-        check(lib().ccfd_engine_set_ring(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
-                                         C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr), log.n),
-              "ccfd_engine_set_ring")
+        self._call(lambda: lib().ccfd_engine_set_ring(C.c_void_p(self.h), int(partition), C.c_void_p(log.feats.ptr),
+                                                      C.c_void_p(log.ids.ptr), C.c_void_p(log.customer.ptr), log.n),
+                   "ccfd_engine_set_ring")
         if log.amount is not None:
-            check(lib().ccfd_engine_set_amount(C.c_void_p(self.h), int(partition), C.c_void_p(log.amount.ptr)),
-                  "ccfd_engine_set_amount")
+            self._call(lambda: lib().ccfd_engine_set_amount(C.c_void_p(self.h), int(partition),
+                                                            C.c_void_p(log.amount.ptr)), "ccfd_engine_set_amount")
         self.logs[partition] = log
         return log
 
@@ -530,7 +607,9 @@ class StreamEngine:
         rc = lib().ccfd_engine_run(C.c_void_p(self.h), int(budget_us), int(flush_us), C.byref(st))
         if rc < 0:
             raise RuntimeError(f"ccfd_engine_run failed: {last_error()}")
-        return _stats(st)
+        out = _stats(st)
+        check_lossless(out)
+        return out
 
     def reset_stats(self) -> None:
         lib().ccfd_engine_reset_stats(C.c_void_p(self.h))

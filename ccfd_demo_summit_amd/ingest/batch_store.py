@@ -275,7 +275,9 @@ class BatchStore:
             if offset >= L.end:
                 return 0
             i = bisect.bisect_left(L.bases, offset)
-            if i < len(L.bases) and L.bases[i] != offset and i > 0:
+            inside = (0 < i < len(L.bases) and L.bases[i] != offset) or \
+                (i == len(L.bases) and L.bases and L.bases[-1] < offset)      # inside the last batch
+            if inside:
                 raise BrokerError(f"{topic}[{partition}]: truncation point {offset} inside a batch")
             dropped = len(L.batches) - i
             L.nbytes -= sum(len(x) for x in L.batches[i:])

@@ -28,8 +28,10 @@ process; here each broker is its own process with its own durable log
 * everything durable in ``data_dir/controller.json`` (+ an offsets log), so a restarted
   controller resumes with the same metadata.
 
-The controller is off the data path: produces, fetches and replication flow broker to broker;
-while it is down leaders keep serving, only fail-over and offset commits wait for it.
+The controller is off the data path: produces, fetches and replication flow broker to broker.
+It runs as one process, or -- ``--member-id/--peers`` -- as a 3-member replicated quorum
+(ingest/controller_quorum.py, the ZooKeeper ensemble's role): one active member, hot standbys
+with a majority-replicated copy of the state, fail-over in well under a second.
 Metrics (``/metrics``): active controller, offline partitions, leader elections, brokers.
 """
 from __future__ import annotations
@@ -76,6 +78,7 @@ class ControllerState:
         self.meta_epoch = 0
         self.elections = 0
         self.offsets: Dict[str, int] = {}                    # "g|t|p" -> committed offset
+        self.mutations = 0                  # every change (replicated by controller_quorum.py)
         self._last_rebalance = clock()
         self._off_f = None
         self._load()
@@ -130,7 +133,43 @@ class ControllerState:
 
     def _changed(self) -> None:
         self.meta_epoch += 1
+        self.mutations += 1
         self._save()
+
+    # ------------------------------------------------------------------ replication (quorum)
+    def snapshot(self) -> Dict[str, Any]:
+        """The replicated part of the state (controller_quorum.py ships it to the standbys):
+        everything but broker liveness, heartbeat times and LEO reports, which a new active
+        controller collects afresh."""
+        with self.lock:
+            return {"topics": dict(self.topics), "parts": json.loads(json.dumps(self.parts)),
+                    "meta_epoch": self.meta_epoch, "elections": self.elections, "offsets": dict(self.offsets),
+                    "nodes": {str(k): {"host": v["host"], "port": v["port"], "incarnation": v.get("incarnation")}
+                              for k, v in self.nodes.items()}}
+
+    def restore(self, snap: Optional[Dict[str, Any]], takeover: bool = False) -> None:
+        """Adopt a replicated snapshot.  ``takeover``: this process becomes the active
+        controller -- every known broker gets a fresh session (alive, heartbeat now: one that
+        stays silent is failed after ``session_s`` as usual), partitions without a leader wait
+        for new LEO reports before their election."""
+        with self.lock:
+            now = self.clock()
+            if snap is not None:
+                self.topics = {k: int(v) for k, v in snap.get("topics", {}).items()}
+                self.parts = json.loads(json.dumps(snap.get("parts", {})))
+                self.meta_epoch = int(snap.get("meta_epoch", 0))
+                self.elections = int(snap.get("elections", 0))
+                self.offsets = {k: int(v) for k, v in snap.get("offsets", {}).items()}
+                self.nodes = {int(k): {"host": v["host"], "port": int(v["port"]), "incarnation": v.get("incarnation"),
+                                       "alive": False, "hb": now} for k, v in snap.get("nodes", {}).items()}
+            if takeover:
+                for n in self.nodes.values():
+                    n["alive"], n["hb"] = True, now
+                self.leo, self.reported_at = {}, {}
+                self.electing = {k: now for k, st in self.parts.items() if st["leader"] < 0}
+                self._last_rebalance = now
+            self.meta_epoch += 1                 # brokers re-read the metadata from the new active
+            self.mutations += 1
 
     # ------------------------------------------------------------------ metadata
     def metadata(self) -> Dict[str, Any]:
@@ -265,6 +304,7 @@ class ControllerState:
                 v = max(int(o), self.offsets.get(k, 0))
                 if v != self.offsets.get(k):
                     self.offsets[k] = v
+                    self.mutations += 1
                     if self._off_f is not None:
                         self._off_f.write(json.dumps({"k": k, "o": v}) + "\n")
             if self._off_f is not None:
@@ -284,12 +324,12 @@ class ControllerState:
         with self.lock:
             return sum(1 for st in self.parts.values() if len(st["isr"]) < len(st["replicas"]))
 
-    def expose(self) -> bytes:
+    def expose(self, active: bool = True, quorum: Optional[Dict[str, Any]] = None) -> bytes:
         with self.lock:
             alive = sum(1 for n in self.nodes.values() if n["alive"])
             lines = [
                 "# TYPE kafka_controller_kafkacontroller_activecontrollercount gauge",
-                "kafka_controller_kafkacontroller_activecontrollercount 1",
+                f"kafka_controller_kafkacontroller_activecontrollercount {1 if active else 0}",
                 "# TYPE kafka_controller_kafkacontroller_offlinepartitionscount gauge",
                 f"kafka_controller_kafkacontroller_offlinepartitionscount {self.offline()}",
                 "# TYPE kafka_controller_controllerstats_leaderelectionrateandtimems_count counter",
@@ -299,52 +339,115 @@ class ControllerState:
                 "# TYPE ccfd_kafka_controller_underreplicated_partitions gauge",
                 f"ccfd_kafka_controller_underreplicated_partitions {self.under_replicated()}",
             ]
+            if quorum is not None:
+                lines += ["# TYPE ccfd_kafka_controller_quorum_term gauge",
+                          f"ccfd_kafka_controller_quorum_term {quorum['term']}",
+                          "# TYPE ccfd_kafka_controller_quorum_elections_won_total counter",
+                          f"ccfd_kafka_controller_quorum_elections_won_total {quorum['elections_won']}",
+                          "# TYPE ccfd_kafka_controller_quorum_round_failures_total counter",
+                          f"ccfd_kafka_controller_quorum_round_failures_total {quorum['round_failures']}"]
         return ("\n".join(lines) + "\n").encode()
 
 
-def make_app(state: ControllerState):
+def make_app(state: ControllerState, quorum=None):
+    """HTTP front of the controller.  With ``quorum`` (controller_quorum.QuorumMember) this
+    process is one member of a replicated controller: only the active member answers the
+    broker API (a standby answers 421 with the active's URL), and every answer that depends on
+    a change -- new metadata, a created topic, a committed offset -- waits until a majority of
+    the members holds that change (503 if the member lost the active role meanwhile)."""
     from aiohttp import web
 
+    def not_active():
+        return web.json_response({"error": "not the active controller",
+                                  "leader": quorum.leader_url() if quorum is not None else None}, status=421)
+
+    async def durable() -> bool:
+        return quorum is None or await quorum.commit_mutation()
+
+    def standby() -> bool:
+        return quorum is not None and not quorum.is_active()
+
     async def hb(request):
+        if standby():
+            return not_active()
         d = await request.json()
-        return web.json_response(state.heartbeat(int(d["node"]), d["host"], int(d["port"]), str(d["incarnation"]),
-                                                 d.get("leos", {}), d.get("isr_changes", []),
-                                                 int(d.get("seen_epoch", -1))))
+        out = state.heartbeat(int(d["node"]), d["host"], int(d["port"]), str(d["incarnation"]),
+                              d.get("leos", {}), d.get("isr_changes", []), int(d.get("seen_epoch", -1)))
+        if not await durable():                      # never publish metadata a failover could undo
+            return web.json_response({"error": "lost the controller majority"}, status=503)
+        return web.json_response(out)
 
     async def topics(request):
+        if standby():
+            return not_active()
         d = await request.json()
         try:
             created = state.create_topic(d["name"], int(d["partitions"]))
         except RuntimeError as e:                    # not every broker is up yet: ask again
             return web.json_response({"error": str(e)}, status=503)
+        if not await durable():
+            return web.json_response({"error": "lost the controller majority"}, status=503)
         return web.json_response({"created": created, **state.metadata()})
 
     async def metadata(_request):
+        if standby():
+            return not_active()
+        if not await durable():
+            return web.json_response({"error": "lost the controller majority"}, status=503)
         return web.json_response(state.metadata())
 
     async def commit(request):
+        if standby():
+            return not_active()
         d = await request.json()
         state.commit(d["group"], [(e[0], int(e[1]), int(e[2])) for e in d["offsets"]])
+        if not await durable():                      # acknowledged = on a majority of members
+            return web.json_response({"error": "lost the controller majority"}, status=503)
         return web.json_response({"ok": True})
 
     async def fetch(request):
+        if standby():
+            return not_active()
         d = await request.json()
+        if not await durable():                      # never answer an offset a failover could undo
+            return web.json_response({"error": "lost the controller majority"}, status=503)
         return web.json_response({"offsets": state.fetch_offsets(d["group"], [(e[0], int(e[1])) for e in d["tps"]])})
 
     async def metrics(_request):
-        return web.Response(body=state.expose(), headers={"Content-Type": "text/plain; version=0.0.4"})
+        body = state.expose(active=quorum is None or quorum.is_active(),
+                            quorum=quorum.status() if quorum is not None else None)
+        return web.Response(body=body, headers={"Content-Type": "text/plain; version=0.0.4"})
+
+    async def quorum_status(_request):
+        return web.json_response(quorum.status() if quorum is not None else {"role": "single", "active": True})
+
+    async def vote(request):
+        return web.json_response(quorum.on_vote(await request.json()))
+
+    async def append(request):
+        return web.json_response(quorum.on_append(await request.json()))
 
     async def ticker(app):
+        if quorum is not None:
+            await quorum.start()
+
         async def loop():
             while True:
-                state.tick()
+                if quorum is None or quorum.is_active():
+                    state.tick()                     # failure detection / elections: the active only
                 await asyncio.sleep(min(0.05, state.session_s / 4))
         app["ticker"] = asyncio.get_running_loop().create_task(loop())
 
     async def stop(app):
         app["ticker"].cancel()
+        if quorum is not None:
+            await quorum.close()
 
     app = web.Application()
+    app.router.add_get("/quorum", quorum_status)
+    if quorum is not None:
+        app.router.add_post("/quorum/vote", vote)
+        app.router.add_post("/quorum/append", append)
     app.router.add_post("/heartbeat", hb)
     app.router.add_post("/topics", topics)
     app.router.add_get("/metadata", metadata)
@@ -366,8 +469,23 @@ def main(argv=None):
     ap.add_argument("--rf", type=int, default=3, help="replication factor of new topics")
     ap.add_argument("--brokers", type=int, default=0,
                     help="create topics only once this many brokers registered (0 = whatever is up)")
+    ap.add_argument("--member-id", type=int, default=0,
+                    help="replicated controller: this member's id in --peers (0 = a single controller)")
+    ap.add_argument("--peers", default="",
+                    help="replicated controller: every member as id=url, comma-separated "
+                         "(e.g. 1=http://c0:9093,2=http://c1:9093,3=http://c2:9093)")
     a = ap.parse_args(argv)
     from aiohttp import web
+    if a.member_id:
+        from .controller_quorum import QuorumMember, parse_peers
+        peers = parse_peers(a.peers)
+        # the quorum member persists the replicated state itself (quorum.json)
+        state = ControllerState(None, session_s=a.session_s, rf=a.rf, expected_brokers=a.brokers)
+        quorum = QuorumMember(a.member_id, peers, state, data_dir=a.data_dir)
+        print(f"[kafka-controller] member {a.member_id} of {len(peers)} on :{a.port} term {quorum.term} "
+              f"state version {list(quorum.version)}", flush=True)
+        web.run_app(make_app(state, quorum), host=a.host, port=a.port, print=None, access_log=None)
+        return
     state = ControllerState(a.data_dir, session_s=a.session_s, rf=a.rf, expected_brokers=a.brokers)
     print(f"[kafka-controller] :{a.port} topics {len(state.topics)} meta epoch {state.meta_epoch}", flush=True)
     web.run_app(make_app(state), host=a.host, port=a.port, print=None, access_log=None)

@@ -82,7 +82,11 @@ class ReplicaManager:
         self.node_id = int(node_id)
         self.host = advertise_host
         self.port = int(port)
-        self.controller = controller_url.rstrip("/")
+        # one controller URL, or the members of a replicated controller (comma-separated):
+        # requests go to the active member, found by following 421 {"leader": url} answers
+        self.controllers = [u.strip().rstrip("/") for u in controller_url.split(",") if u.strip()]
+        self.controller = self.controllers[0]
+        self.controller_failovers = 0
         self.store = store
         self.server = server                      # KafkaLiteServer: fetch wake-ups
         self.hb_s = float(hb_s)
@@ -172,31 +176,67 @@ class ReplicaManager:
         except BrokerError:
             return 0
 
+    async def _ctl(self, path: str, body: Dict[str, Any], wait_s: float = 5.0) -> Tuple[int, Dict[str, Any]]:
+        """POST to the active controller: a standby's 421 names the active member, an
+        unreachable one or a 503 (the active lost its majority mid-request) moves on to the
+        next member; gives up after ``wait_s`` (an election takes well under a second)."""
+        t_end = time.monotonic() + wait_s
+        last = "unreachable"
+        while True:
+            url = self.controller
+            try:
+                async with self._session.post(url + path, json=body) as r:
+                    d = await r.json(content_type=None)
+                    if r.status == 421 or (r.status == 503 and len(self.controllers) > 1
+                                           and "majority" in str(d.get("error", ""))):
+                        lead = d.get("leader")
+                        self._next_controller(lead if lead in self.controllers else None)
+                        last = f"HTTP {r.status} from {url}"
+                    else:
+                        return r.status, d
+            except (OSError, asyncio.TimeoutError, ValueError) as e:
+                self._next_controller(None)
+                last = f"{url}: {e!r}"
+            except Exception as e:                           # noqa: BLE001 -- aiohttp client errors
+                self._next_controller(None)
+                last = f"{url}: {e!r}"
+            if time.monotonic() > t_end:
+                raise BrokerError(f"no active controller ({last})")
+            await asyncio.sleep(0.05)
+
+    def _next_controller(self, url: Optional[str]) -> None:
+        if len(self.controllers) <= 1:
+            return
+        if url is None:
+            i = self.controllers.index(self.controller) if self.controller in self.controllers else -1
+            url = self.controllers[(i + 1) % len(self.controllers)]
+        if url != self.controller:
+            self.controller = url
+            self.controller_failovers += 1
+
     async def create_topic(self, name: str, partitions: int, wait_s: float = 30.0) -> None:
         """Through the controller; while it waits for the cluster's brokers to register (503),
         asked again every 200 ms."""
         t_end = time.monotonic() + wait_s
         while True:
-            async with self._session.post(f"{self.controller}/topics",
-                                          json={"name": name, "partitions": int(partitions)}) as r:
-                d = await r.json()
-                if r.status == 200:
-                    break
+            status, d = await self._ctl("/topics", {"name": name, "partitions": int(partitions)})
+            if status == 200:
+                break
             if time.monotonic() > t_end:
                 raise BrokerError(f"controller: {d.get('error')}")
             await asyncio.sleep(0.2)
         self._apply(d)
 
     async def commit_offsets(self, group: str, entries) -> None:
-        async with self._session.post(f"{self.controller}/offsets/commit",
-                                      json={"group": group, "offsets": [list(e) for e in entries]}) as r:
-            if r.status != 200:
-                raise BrokerError(f"controller commit: HTTP {r.status}")
+        status, _d = await self._ctl("/offsets/commit", {"group": group, "offsets": [list(e) for e in entries]})
+        if status != 200:
+            raise BrokerError(f"controller commit: HTTP {status}")
 
     async def fetch_offsets(self, group: str, tps) -> List[int]:
-        async with self._session.post(f"{self.controller}/offsets/fetch",
-                                      json={"group": group, "tps": [list(t) for t in tps]}) as r:
-            return (await r.json())["offsets"]
+        status, d = await self._ctl("/offsets/fetch", {"group": group, "tps": [list(t) for t in tps]})
+        if status != 200:
+            raise BrokerError(f"controller offset fetch: HTTP {status}")
+        return d["offsets"]
 
     # ------------------------------------------------------------------ heartbeat
     async def _hb_loop(self) -> None:
@@ -206,8 +246,9 @@ class ReplicaManager:
                     "leos": {tp_key(*tp): self._leo(tp) for tp in self.hosted()},
                     "isr_changes": list(self._isr_prop.values())}
             try:
-                async with self._session.post(f"{self.controller}/heartbeat", json=body) as r:
-                    d = await r.json()
+                status, d = await self._ctl("/heartbeat", body, wait_s=self.hb_s)
+                if status != 200:
+                    raise BrokerError(f"heartbeat: HTTP {status}")
                 self._isr_prop.clear()
                 self.controller_ok = True
                 if "parts" in d:

@@ -237,7 +237,10 @@ def cmd_kie(a, cfg):
     pub = BatchingPublisher(broker, topic, on_sent=lambda toks: holder["eng"].mark_notified(toks))
     kw = dict(publish_notification=lambda m: pub.publish(encode_notification(m), token=m["process_id"]),
               kie_metrics=KieMetrics(),
-              prediction=PredictionService(cfg.kie.confidence_threshold, client=client), shard=shard, shards=shards)
+              prediction=PredictionService(cfg.kie.confidence_threshold, client=client), shard=shard, shards=shards,
+              standard_dedupe_window=cfg.kie.standard_dedupe_window,
+              standard_dedupe_capacity=cfg.kie.standard_dedupe_capacity or None,
+              standard_audit_rows=cfg.kie.standard_audit_rows)
     if a.journal and os.path.exists(a.journal):
         # restart after a crash: in-flight instances, timers and the per-transaction dedupe
         # index come back from the journal, so re-sent fraud starts are recognised

@@ -177,6 +177,12 @@ class EngineService:
         # per partition: (ring row end, next kafka offset) of ingested messages, oldest first
         self._pending: Dict[int, Deque[Tuple[int, int]]] = {p: collections.deque() for p in self.partitions}
         self._rows_in: Dict[int, int] = {p: 0 for p in self.partitions}
+        # per partition: one past the highest offset ever ingested (set before the rows reach
+        # the ring) -- an upper bound on the offset of every row scored so far (_commit_marks)
+        self._ingest_hi: Dict[int, int] = {}
+        self._notice: Dict[int, int] = {}              # committed offsets not yet told to KIE
+        self._notice_t = 0.0
+        self.commit_notice_period_s = 0.2
         self._stop = threading.Event()
         self._ingest_err: Optional[BaseException] = None
         self.rows_scored = 0
@@ -244,6 +250,8 @@ class EngineService:
         by_part: Dict[int, List] = collections.defaultdict(list)
         for r in recs:
             by_part[r.partition].append(r)
+        for p, rs in by_part.items():         # before any row is written: see _commit_marks
+            self._ingest_hi[p] = max(self._ingest_hi.get(p, 0), rs[-1].offset + 1)
         saw_json = False
         for p, rs in by_part.items():
             json_run: List[bytes] = []
@@ -295,12 +303,19 @@ class EngineService:
             return out
         return {p: self.engine.cursor(p) for p in self.partitions}
 
+    def _last_committed_offsets(self, snap: Dict[int, int]) -> Dict[int, int]:
+        out = dict(getattr(self, "_committed_now", {}))
+        self._committed_now = {}
+        return out
+
     def _commit(self, snap: Dict[int, int]) -> None:
+        self._committed_now = {}
         if not snap:
             return
         if self.native is not None:                     # offsets whose rows are all scored
             for p, off in snap.items():
                 self.broker.commit(self.cfg.group_id, self.cfg.topic, p, off)
+            self._committed_now = dict(snap)
             return
         offs = {}
         for p, released in snap.items():
@@ -312,6 +327,7 @@ class EngineService:
                 offs[(self.cfg.topic, p)] = last
         if offs:
             self.consumer.commit(offs)
+            self._committed_now = {p: o for (_t, p), o in offs.items()}
 
     def _commit_done(self) -> None:
         """Commit every snapshot whose fraud rows the hand-off has acknowledged (all of them
@@ -334,6 +350,39 @@ class EngineService:
         except (BrokerError, OSError, ConnectionError):
             self._commit_retry = merged
             self.commit_failures += 1
+            return
+        self._notify_committed(self._last_committed_offsets(merged))
+
+    def _commit_marks(self) -> Dict[int, int]:
+        """partition -> an offset above every row of it scored so far: the native consumers'
+        fetch positions, else the highest ingested offset + 1 (both recorded before the rows
+        reach a ring).  A standard hand-off batch carries it per row (commit_mark): KIE keeps
+        the batch's dedupe keys until the engine's commits pass it (process/engine.py)."""
+        if self.natives:
+            out: Dict[int, int] = {}
+            for kc in self.natives:
+                for p, pos in kc.position().items():
+                    out[p] = max(pos, self._ingest_hi.get(p, 0))
+                    self._ingest_hi[p] = out[p]           # a reset position never lowers a mark
+            return out
+        return dict(self._ingest_hi)
+
+    def _notify_committed(self, offs: Dict[int, int], force: bool = False) -> None:
+        """Tell the KIE shards what this rank committed (throttled): their commit-gated dedupe
+        keys below it can never be re-delivered.  Only standard starts are gated."""
+        if self.standard_mode != "process":
+            return
+        for p, o in offs.items():
+            self._notice[p] = max(self._notice.get(p, o), o)
+        now = time.monotonic()
+        if not self._notice or (not force and now - self._notice_t < self.commit_notice_period_s):
+            return
+        self._notice_t = now
+        note, self._notice = self._notice, {}
+        if self.handoff is not None and hasattr(self.handoff, "submit_committed"):
+            self.handoff.submit_committed(note)
+        elif hasattr(getattr(self.router, "processes", None), "note_committed"):
+            self.router.processes.note_committed(note)
 
     def commits_pending(self) -> int:
         return len(self._commit_wait) + (1 if self._commit_retry else 0)
@@ -347,8 +396,11 @@ class EngineService:
         # drain on the same thread, right after the rows were counted: the router must see
         # every completed micro-batch's rows together with its flagged records; the commit
         # snapshot follows the drain, so it never covers a row whose fraud record is not yet
-        # in _flagged_new (only this thread completes batches)
-        flagged = self.engine.drain_flagged() if st.rows else None
+        # in _flagged_new (only this thread completes batches).  Drained on every call, rows or
+        # not: a full flagged ring holds completed batches back (lossless hand-off), and only
+        # this drain can make room for them.  run() / serve_collect raise HandoffLost rather
+        # than return stats that count a dropped fraud record, so no commit ever covers one.
+        flagged = self.engine.drain_flagged()
         standard = None
         if self.standard_mode == "process" and st.rows:
             rec = self.engine.drain_scored()
@@ -483,7 +535,7 @@ class EngineService:
         seq = -1
         if rows or len(flagged):
             if standard is not None:                   # standard_mode="process"
-                self.router.on_flagged(flagged, rows, standard=standard)
+                self.router.on_flagged(flagged, rows, standard=standard, marks=self._commit_marks())
             else:
                 self.router.on_flagged(flagged, rows)  # enqueues; never blocks on KIE
             seq = getattr(self.router, "last_handoff_seq", -1)

@@ -25,6 +25,7 @@ if os.environ.get("CCFD_LIB_PATH"):
 MODEL_LR, MODEL_MLP, MODEL_GBDT = 0, 1, 2
 MODEL_IDS = {"lr": MODEL_LR, "mlp": MODEL_MLP, "gbdt": MODEL_GBDT}
 N_COUNTER_SLOTS = 64
+ENGINE_FLAG_FULL = 1      # ccfd_abi.h CCFD_ENGINE_FLAG_FULL: drain the flagged ring, call again
 CNT_WIRE_STALE = 4        # ccfd_abi.h CCFD_CNT_WIRE_STALE
 ARG_WIRE_W64, ARG_WIRE_G32, ARG_WIRE_G20 = 2, 4, 8
 ROW_FORMATS = {"f32": 0, "w64": 1, "g32": 2, "g20": 3}      # ccfd_engine_config.wire
@@ -66,7 +67,8 @@ class EngineStats(C.Structure):
                 ("last_proba", C.c_float), ("last_amount", C.c_float), ("last_partition", C.c_int32),
                 ("last_row_bytes", C.c_int32), ("last_row", C.c_uint8 * 128),
                 ("origin_batches", C.c_uint64), ("origin_hist", C.c_uint64 * 256),
-                ("origin_hist_rows", C.c_uint64 * 256)]
+                ("origin_hist_rows", C.c_uint64 * 256), ("submitted", C.c_uint64),
+                ("flag_full_events", C.c_uint64)]
 
 
 FLAGGED_DTYPE = [("tx_id", "<u8"), ("customer", "<u4"), ("proba", "<f4"), ("amount", "<f4"),

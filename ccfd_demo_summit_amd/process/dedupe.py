@@ -24,6 +24,12 @@ def _lib():
     if not _bound:
         L.ccfd_dedupe_new.argtypes = [C.c_int64]
         L.ccfd_dedupe_new.restype = C.c_void_p
+        L.ccfd_dedupe_new_gated.argtypes = [C.c_int64]
+        L.ccfd_dedupe_new_gated.restype = C.c_void_p
+        L.ccfd_dedupe_evict.argtypes = [C.c_void_p, C.c_int64]
+        L.ccfd_dedupe_evict.restype = C.c_int64
+        L.ccfd_dedupe_erase.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.ccfd_dedupe_erase.restype = C.c_int64
         L.ccfd_dedupe_free.argtypes = [C.c_void_p]
         L.ccfd_dedupe_free.restype = None
         L.ccfd_dedupe_size.argtypes = [C.c_void_p]
@@ -43,11 +49,21 @@ def _i64(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a).astype(np.int64, copy=False))
 
 
+class DedupeFull(RuntimeError):
+    """A gated index has no room for the batch: nothing was admitted.  Transient -- the KIE
+    server answers 503 and the router's hand-off retries once committed offsets free room."""
+    transient = True
+
+
 class DedupeIndex:
-    def __init__(self, window: int = 1 << 20):
+    def __init__(self, window: int = 1 << 20, gated: bool = False):
+        """``gated=False``: a count window (the oldest key leaves when ``window`` are held).
+        ``gated=True``: ``window`` is a hard capacity; keys leave only through ``erase`` and an
+        admission that could overflow raises DedupeFull."""
         self.window = int(window)
+        self.gated = bool(gated)
         self._L = _lib()
-        self._h = self._L.ccfd_dedupe_new(self.window)
+        self._h = (self._L.ccfd_dedupe_new_gated if gated else self._L.ccfd_dedupe_new)(self.window)
         if not self._h:
             raise MemoryError(f"dedupe index of {window} entries")
 
@@ -62,15 +78,28 @@ class DedupeIndex:
         new = np.empty(n, np.int64)
         k = self._L.ccfd_dedupe_assign(self._h, t.ctypes.data, n, int(first_id), int(stride),
                                        out.ctypes.data, new.ctypes.data)
+        if k == -2:
+            raise DedupeFull(f"dedupe index full ({len(self)} of {self.window} keys uncommitted)")
         if k < 0:
             raise ValueError("transaction ids must be non-negative integers")
         return out, new[:k]
+
+    def evict(self, k: int) -> int:
+        """Count-window mode: drop the ``k`` oldest admitted keys; returns how many left."""
+        return int(self._L.ccfd_dedupe_evict(self._h, int(k)))
+
+    def erase(self, keys) -> int:
+        """Gated mode: drop these keys; returns how many were present."""
+        t = _i64(keys)
+        return int(self._L.ccfd_dedupe_erase(self._h, t.ctypes.data, len(t)))
 
     def insert(self, tx, ids) -> int:
         t, i = _i64(tx), _i64(ids)
         if len(t) != len(i):
             raise ValueError("keys and ids of different lengths")
         k = self._L.ccfd_dedupe_insert(self._h, t.ctypes.data, i.ctypes.data, len(t))
+        if k == -2:
+            raise DedupeFull(f"dedupe index full ({len(self)} of {self.window} keys)")
         if k < 0:
             raise ValueError("transaction ids must be non-negative integers")
         return int(k)

@@ -92,10 +92,22 @@ class ProcessEngine:
                  kie_metrics=None, prediction: Optional[PredictionService] = None,
                  clock: Callable[[], float] = time.monotonic, journal_path: Optional[str] = None,
                  keep_completed: int = 100_000, shard: int = 0, shards: int = 1,
-                 standard_dedupe_window: int = 1 << 20):
+                 standard_dedupe_window: int = 1 << 20, standard_dedupe_capacity: Optional[int] = None,
+                 standard_audit_rows: int = 1 << 22):
         """``shard`` / ``shards``: this engine is shard ``shard`` of a K-way KIE tier
         (process/sharding.py) -- its instance and task ids are ``shard + K * n``, so a signal
-        or task completion that carries only the id reaches the owner."""
+        or task completion that carries only the id reaches the owner.
+
+        Standard-start idempotency is gated by the engine's committed Kafka offsets: a hand-off
+        batch's columns ``kafka_partition`` / ``commit_mark`` say below which offset of each
+        partition its rows were consumed, and its transaction ids stay in the dedupe index until
+        the engine reports (``note_committed``) that every one of those partitions is committed
+        past the mark -- only then can no replay re-deliver them.  ``standard_dedupe_window`` is
+        the number of keys kept at least (and the plain count window of ungated starts);
+        ``standard_dedupe_capacity`` (default 4x) is a hard bound: a batch that would exceed it is
+        refused (DedupeFull -> 503 -> the router's hand-off retries: back-pressure, never an
+        unsafe eviction).  ``standard_audit_rows``: standard instances answerable from memory by
+        transaction id (``find_transaction``); older ones from the journal."""
         self.timeout = float(notification_timeout_s)
         self.p_thr = float(dmn_probability_threshold)
         self.a_thr = float(dmn_amount_threshold)
@@ -120,6 +132,9 @@ class ProcessEngine:
         self.keep_completed = keep_completed
         self._completed_order: collections.deque = collections.deque()   # O(1) eviction
         self._journal = open(journal_path, "a", buffering=1) if journal_path else None
+        if self._journal is not None and self._journal.tell() == 0:
+            # ids encode (shard, K): recovery must decode them with the K they were written with
+            self._journal.write(json.dumps({"header": {"shard": self.shard, "shards": self.shards, "v": 1}}) + "\n")
         self.dedupe_window = 1_000_000
         self._by_tx: Dict[Any, int] = {}
         self._tx_order = collections.deque()
@@ -134,11 +149,26 @@ class ProcessEngine:
         # must not start a second standard process): tx id -> instance id over a bounded window,
         # native for integer ids (process/dedupe.py); other ids (e.g. strings) use a dict
         self.standard_dedupe_window = int(standard_dedupe_window)
+        self.standard_dedupe_capacity = int(standard_dedupe_capacity or 4 * self.standard_dedupe_window)
+        if self.standard_dedupe_capacity < self.standard_dedupe_window:
+            raise ValueError("standard_dedupe_capacity must be >= standard_dedupe_window")
         from .dedupe import DedupeIndex
-        self._std_index = DedupeIndex(self.standard_dedupe_window)
+        self._std_index = DedupeIndex(self.standard_dedupe_capacity, gated=True)
+        # admission batches of the index, oldest first: [new keys, gate] -- gate {partition: mark}
+        # (erasable once committed past every mark, in any order) or None (ungated: count window)
+        self._std_fifo: List[list] = []
+        self.standard_forced_evictions = 0            # recovery only: journal beyond capacity
+        self._committed: Dict[int, int] = {}          # partition -> engine's committed offset
+        self.standard_evicted = 0
+        self.standard_dedupe_full = 0                 # batches refused for lack of room
         self._std_by_tx: Dict[Any, int] = {}
         self._std_order: collections.deque = collections.deque()
         self.standard_duplicates = 0
+        # audit of standard instances (never retained as objects): per admitted batch the first
+        # id, the id stride, the new transaction ids and their proba / amount, newest last
+        self.standard_audit_rows = int(standard_audit_rows)
+        self._audit: collections.deque = collections.deque()
+        self._audit_rows = 0
         # scored -> process started (the engine's hand-off items carry ``scored_ns``, the wall
         # clock their results were collected): 4 buckets per octave of ns, like the engine's
         self.handoff_hist = [0] * 256
@@ -197,7 +227,7 @@ class ProcessEngine:
     def recover(cls, journal_path: str, **kw) -> "ProcessEngine":
         """Rebuild from the journal (last record per instance wins), then keep appending."""
         last: Dict[int, dict] = {}
-        std_batches: List[dict] = []
+        std_events: List[tuple] = []            # ("std", batch) / ("committed", offsets), in order
         notified = set()                        # outbox entries the broker acknowledged
         if os.path.exists(journal_path):
             with open(journal_path) as f:
@@ -208,8 +238,18 @@ class ProcessEngine:
                             rec = json.loads(line)
                         except json.JSONDecodeError:
                             continue        # the torn last line of a killed process
-                        if "standard" in rec:
-                            std_batches.append(rec["standard"])
+                        if "header" in rec:
+                            h = rec["header"]
+                            want = (int(kw.get("shard", 0)), max(1, int(kw.get("shards", 1))))
+                            if (int(h["shard"]), int(h["shards"])) != want:
+                                raise ValueError(
+                                    f"journal {journal_path} was written by shard {h['shard']} of {h['shards']}, "
+                                    f"this process is shard {want[0]} of {want[1]}: its instance ids would be "
+                                    "decoded wrongly (start this shard with its own journal and kie.shards)")
+                        elif "standard" in rec:
+                            std_events.append(("std", rec["standard"]))
+                        elif "committed" in rec:
+                            std_events.append(("committed", rec["committed"]))
                         elif "notified" in rec:
                             notified.update(rec["notified"])
                         elif "instance" in rec:
@@ -251,11 +291,17 @@ class ProcessEngine:
             if inst.state == State.WAITING_CUSTOMER and inst.timer_due is not None:
                 heapq.heappush(eng._timers, (inst.timer_due, iid))
         import numpy as np
-        for b in std_batches:                   # batched standard starts (start_standard_many)
+        for kind, b in std_events:              # batched standard starts + commit watermarks
+            if kind == "committed":
+                eng._apply_committed(b)
+                continue
             if "tx_i64" in b:                   # base64 of the new transaction ids (int64 LE)
                 import base64
                 tx = np.frombuffer(base64.b64decode(b["tx_i64"]), "<i8")
                 ids = int(b["id0"]) + int(b.get("st", 1)) * np.arange(len(tx), dtype=np.int64)
+                pr = np.frombuffer(base64.b64decode(b["p_f32"]), "<f4") if "p_f32" in b else None
+                am = np.frombuffer(base64.b64decode(b["a_f32"]), "<f4") if "a_f32" in b else None
+                eng._audit_add(int(b["id0"]), int(b.get("st", 1)), tx, pr, am)
             else:                               # round-3 form: JSON lists
                 tx = b["transaction_id"]
                 ids = b["id"] if "id" in b else list(range(int(b["id0"]), int(b["id0"]) + len(tx)))
@@ -263,7 +309,8 @@ class ProcessEngine:
                 max_n = max(max_n, eng._n_of(int(np.max(ids))))
             eng.standard_count += len(tx)
             eng.outcome_counts[Outcome.STANDARD.value] += len(tx)
-            eng._std_restore(tx, ids)
+            gate = {int(k): int(v) for k, v in b["g"].items()} if b.get("g") else None
+            eng._std_restore(tx, ids, gate=gate)
         for iid, rec in last.items():
             if rec["instance"]["process_id"] == cls.STANDARD:
                 eng.standard_count += 1
@@ -271,6 +318,7 @@ class ProcessEngine:
                 tx = rec["instance"]["variables"].get("transaction_id")
                 if tx is not None:
                     eng._std_restore([tx], [iid])
+        eng._std_evict()
         eng._next_n = max_n + 1
         eng._task_ids = itertools.count(max_task + 1)
         return eng
@@ -314,18 +362,200 @@ class ProcessEngine:
     def _native_key(tx) -> bool:
         return isinstance(tx, (int,)) and not isinstance(tx, bool) and tx >= 0
 
-    def _std_restore(self, txs, ids) -> None:
-        """Recovery: put admitted (transaction, instance) pairs back in the dedupe window."""
+    def _std_restore(self, txs, ids, gate=None) -> None:
+        """Recovery: put admitted (transaction, instance) pairs back in the dedupe index."""
         import numpy as np
         txs = list(txs) if not hasattr(txs, "dtype") else txs
         if hasattr(txs, "dtype") or all(self._native_key(t) for t in txs):
-            self._std_index.insert(np.asarray(txs, np.int64), np.asarray(ids, np.int64))
+            t64, i64 = np.asarray(txs, np.int64), np.asarray(ids, np.int64)
+            self._restore_insert(t64, i64)
+            self._fifo_add(t64, gate)
+            self._std_evict()
             return
         for t, i in zip(txs, ids):
             if self._native_key(t):
-                self._std_index.insert([t], [i])
+                self._restore_insert(np.asarray([t], np.int64), np.asarray([i], np.int64))
+                self._fifo_add([t], None)
             else:
                 self._std_remember(t, int(i))
+
+    def _restore_insert(self, t64, i64) -> None:
+        from .dedupe import DedupeFull
+        try:
+            self._std_index.insert(t64, i64)
+            return
+        except DedupeFull:
+            self._std_evict()
+        while len(self._std_index) + len(t64) > self.standard_dedupe_capacity and self._std_fifo:
+            keys, _gate = self._std_fifo.pop(0)       # journal older than the capacity: forced
+            self.standard_forced_evictions += self._std_index.erase(keys)
+        self._std_index.insert(t64, i64)
+
+    # ------------------------------------------------------------------ commit-gated dedupe
+    def _fifo_add(self, keys, gate) -> None:
+        if not len(keys):
+            return
+        f = self._std_fifo
+        if gate is None and f and f[-1][1] is None and isinstance(f[-1][0], list):
+            f[-1][0].extend(int(k) for k in keys)   # runs of ungated starts share one entry
+        else:
+            f.append([list(keys) if gate is None else keys, gate])
+
+    def _gate_open(self, gate) -> bool:
+        c = self._committed
+        return gate is None or all(c.get(p, -1) >= m for p, m in gate.items())
+
+    def _std_evict(self) -> None:
+        """While the index holds more than the window, erase the oldest batches that can no
+        longer be re-delivered (every partition committed past their marks; ungated batches
+        always).  A batch still exposed to a replay is skipped, never erased: the index grows
+        instead, up to its capacity, then refuses admissions."""
+        ix, f = self._std_index, self._std_fifo
+        excess = len(ix) - self.standard_dedupe_window
+        i = 0
+        while excess > 0 and i < len(f):
+            keys, gate = f[i]
+            if not self._gate_open(gate):
+                i += 1
+                continue
+            k = min(len(keys), excess)
+            self.standard_evicted += ix.erase(keys[:k])
+            excess -= k
+            if k == len(keys):
+                del f[i]
+            else:
+                f[i][0] = keys[k:]
+                i += 1
+
+    def _apply_committed(self, offsets) -> bool:
+        changed = False
+        for p, o in offsets.items():
+            p, o = int(p), int(o)
+            if o > self._committed.get(p, -1):
+                self._committed[p] = o
+                changed = True
+        return changed
+
+    def note_committed(self, offsets: Dict[int, int]) -> None:
+        """The engine committed these Kafka offsets (partition -> next offset to consume): no
+        replay will re-deliver a row below them, so dedupe keys gated under them may leave.
+        Journaled (when it moves), so recovery rebuilds the same watermark."""
+        with self._lock:
+            if not self._apply_committed(offsets):
+                return
+            if self._journal is not None:
+                self._write_journal('{"committed": %s}\n' % json.dumps(
+                    {str(p): int(o) for p, o in offsets.items()}))
+            self._std_evict()
+
+    def dedupe_stats(self) -> Dict[str, int]:
+        with self._lock:
+            return {"keys": len(self._std_index), "window": self.standard_dedupe_window,
+                    "capacity": self.standard_dedupe_capacity, "evicted": self.standard_evicted,
+                    "refused_batches": self.standard_dedupe_full, "batches": len(self._std_fifo),
+                    "recovery_forced_evictions": self.standard_forced_evictions,
+                    "committed_partitions": len(self._committed)}
+
+    # ------------------------------------------------------------------ standard audit
+    def _audit_add(self, id0: int, st: int, tx, proba=None, amount=None) -> None:
+        import numpy as np
+        if self.standard_audit_rows <= 0 or not len(tx):
+            return
+        self._audit.append((int(id0), int(st), np.asarray(tx, np.int64),
+                            None if proba is None else np.asarray(proba, np.float32),
+                            None if amount is None else np.asarray(amount, np.float32)))
+        self._audit_rows += len(tx)
+        while self._audit and self._audit_rows - len(self._audit[0][2]) >= self.standard_audit_rows:
+            self._audit_rows -= len(self._audit.popleft()[2])
+
+    def _audit_find(self, iid: int):
+        """(tx, proba, amount) of standard instance ``iid`` from the in-memory audit."""
+        import bisect
+        a = self._audit
+        if not a:
+            return None
+        keys = [b[0] for b in a] if len(a) < 64 else None
+        if keys is not None:
+            i = bisect.bisect_right(keys, iid) - 1
+        else:                                   # ids grow with admission: binary search
+            lo, hi = 0, len(a) - 1
+            i = -1
+            while lo <= hi:
+                mid = (lo + hi) // 2
+                if a[mid][0] <= iid:
+                    i, lo = mid, mid + 1
+                else:
+                    hi = mid - 1
+        if i < 0:
+            return None
+        id0, st, tx, pr, am = a[i]
+        k, r = divmod(iid - id0, st)
+        if r or k >= len(tx):
+            return None
+        return (int(tx[k]), None if pr is None else float(pr[k]), None if am is None else float(am[k]))
+
+    def find_transaction(self, tx_id, deep: bool = False) -> Optional[Dict[str, Any]]:
+        """The process a transaction started on this shard (README.md:552: every transaction
+        starts a standard or a fraud process): instance id, process, route, state / outcome and
+        proba.  Fraud instances come from the live instance table; standard instances (counted,
+        never retained as objects) from the in-memory audit of the last ``standard_audit_rows``
+        admissions -- or, with ``deep``, from a scan of the journal (older history, slow).
+        None: this shard never started a process for it (within the retention)."""
+        if isinstance(tx_id, float) and tx_id.is_integer():
+            tx_id = int(tx_id)
+        with self._lock:
+            iid = self._by_tx.get(tx_id)
+            if iid is not None:
+                inst = self.instances.get(iid)
+                out = {"transaction_id": tx_id, "process-instance-id": iid, "process-id": self.FRAUD,
+                       "route": "fraud", "source": "memory"}
+                if inst is not None:
+                    out.update(state=inst.state.value, outcome=inst.outcome, proba=inst.proba,
+                               amount=inst.amount)
+                return out
+            iid = self._std_index.get(tx_id) if self._native_key(tx_id) else self._std_by_tx.get(tx_id)
+            if iid is not None:
+                out = {"transaction_id": tx_id, "process-instance-id": int(iid), "process-id": self.STANDARD,
+                       "route": "standard", "state": State.COMPLETED.value, "outcome": Outcome.STANDARD.value,
+                       "source": "memory"}
+                hit = self._audit_find(int(iid))
+                if hit is not None and hit[0] == tx_id:
+                    out.update(proba=hit[1], amount=hit[2])
+                return out
+            journal = self._journal.name if self._journal is not None else None
+        if deep and journal:
+            return self._journal_find(journal, tx_id)
+        return None
+
+    def _journal_find(self, path: str, tx_id) -> Optional[Dict[str, Any]]:
+        import base64
+
+        import numpy as np
+        found = None
+        with open(path) as f:
+            for line in f:
+                if '"standard"' not in line[:16]:
+                    continue
+                try:
+                    b = json.loads(line)["standard"]
+                except (json.JSONDecodeError, KeyError):
+                    continue
+                if "tx_i64" not in b:
+                    continue
+                tx = np.frombuffer(base64.b64decode(b["tx_i64"]), "<i8")
+                hit = np.nonzero(tx == int(tx_id))[0]
+                if not len(hit):
+                    continue
+                k = int(hit[0])
+                found = {"transaction_id": int(tx_id), "process-instance-id": int(b["id0"]) + int(b.get("st", 1)) * k,
+                         "process-id": self.STANDARD, "route": "standard", "state": State.COMPLETED.value,
+                         "outcome": Outcome.STANDARD.value, "source": "journal"}
+                if "p_f32" in b:
+                    found["proba"] = float(np.frombuffer(base64.b64decode(b["p_f32"]), "<f4")[k])
+                if "a_f32" in b:
+                    found["amount"] = float(np.frombuffer(base64.b64decode(b["a_f32"]), "<f4")[k])
+                break                            # a transaction is admitted once
+        return found
 
     def _std_remember(self, tx, iid: int) -> None:
         self._std_by_tx[tx] = iid
@@ -341,12 +571,14 @@ class ProcessEngine:
             txid = int(txid)
         with self._lock:
             if self._native_key(txid):
-                ids, new = self._std_index.assign([txid], self._iid(self._next_n), self.shards)
+                ids, new = self._assign_std([txid], self._iid(self._next_n))
                 iid = int(ids[0])
                 if not len(new):
                     self.standard_duplicates += 1
                     return iid
                 self._next_n += 1
+                self._fifo_add([txid], None)
+                self._std_evict()
             else:
                 if txid is not None and txid in self._std_by_tx:
                     self.standard_duplicates += 1
@@ -379,7 +611,12 @@ class ProcessEngine:
         id stride, the new transaction ids), which ``recover()`` replays.  Returns the instance
         ids in order (an int64 array for numeric columns)."""
         import numpy as np
+        gate = None
         if isinstance(items, dict):
+            if "kafka_partition" in items or "commit_mark" in items:
+                items = dict(items)
+                kp, cm = items.pop("kafka_partition", None), items.pop("commit_mark", None)
+                gate = _gate_of(kp, cm)
             tx = items.get("transaction_id", items.get("tx_id"))
             sc = items.get("scored_ns")
         else:
@@ -403,20 +640,49 @@ class ProcessEngine:
             return [self.start_standard(v) for v in rows]
         with self._lock:
             first = self._iid(self._next_n)
-            ids, new = self._std_index.assign(tx, first, self.shards)
+            ids, new = self._assign_std(tx, first)
             n_new = len(new)
             self._next_n += n_new
             self.standard_duplicates += n - n_new
             self.standard_count += n_new
             self.outcome_counts[Outcome.STANDARD.value] += n_new
+            self._fifo_add(new, gate)
+            if n_new:
+                pr, am = _new_rows_column(items, "proba", ids, first, self.shards, n_new), \
+                    _new_rows_column(items, "amount", ids, first, self.shards, n_new)
+                self._audit_add(first, self.shards, new, pr, am)
             if self._journal is not None and n_new:
                 import base64
                 tx64 = base64.b64encode(new.astype("<i8").tobytes()).decode()
+                extra = ""
+                if pr is not None:
+                    extra += ', "p_f32": "%s"' % base64.b64encode(pr.astype("<f4").tobytes()).decode()
+                if am is not None:
+                    extra += ', "a_f32": "%s"' % base64.b64encode(am.astype("<f4").tobytes()).decode()
+                if gate:
+                    extra += ', "g": %s' % json.dumps({str(p): m for p, m in gate.items()})
                 t0 = time.monotonic_ns()
-                self._journal.write('{"standard": {"id0": %d, "st": %d, "tx_i64": "%s"}}\n'
-                                    % (first, self.shards, tx64))
+                self._journal.write('{"standard": {"id0": %d, "st": %d, "tx_i64": "%s"%s}}\n'
+                                    % (first, self.shards, tx64, extra))
                 self.journal_time.add(time.monotonic_ns() - t0)
+            self._std_evict()
         return ids
+
+    def _assign_std(self, tx, first: int):
+        """Admit into the gated index; a full index first evicts what commits allow."""
+        from .dedupe import DedupeFull
+        if len(tx) > self.standard_dedupe_capacity:
+            raise ValueError(f"a standard batch of {len(tx)} rows exceeds the dedupe capacity "
+                             f"({self.standard_dedupe_capacity}): it could never be admitted")
+        try:
+            return self._std_index.assign(tx, first, self.shards)
+        except DedupeFull:
+            self._std_evict()
+            try:
+                return self._std_index.assign(tx, first, self.shards)
+            except DedupeFull:
+                self.standard_dedupe_full += 1
+                raise
 
     def _note_handoff(self, scored_ns, n: int = 1) -> None:
         if not scored_ns or n <= 0:
@@ -666,6 +932,39 @@ def columns_of(items) -> Dict[str, list]:
     if len(lens) > 1:
         raise ValueError("columns of different lengths")
     return cols
+
+
+def _gate_of(kp, cm) -> Optional[Dict[int, int]]:
+    """{partition: max commit mark} of a hand-off batch's gate columns (None if absent)."""
+    import numpy as np
+    if kp is None or cm is None or not len(kp):
+        return None
+    kp = np.asarray(kp, np.int64)
+    cm = np.asarray(cm, np.int64)
+    if kp.shape != cm.shape:
+        raise ValueError("kafka_partition / commit_mark columns of different lengths")
+    out: Dict[int, int] = {}
+    for p in np.unique(kp):
+        out[int(p)] = int(cm[kp == p].max())
+    return out
+
+
+def _new_rows_column(items, name: str, ids, first: int, stride: int, n_new: int):
+    """Column ``name`` of the newly admitted rows of a standard batch (their ids are
+    first + stride * k, k < n_new, each row's position its first occurrence), or None."""
+    import numpy as np
+    col = items.get(name) if isinstance(items, dict) else None
+    if col is None:
+        return None
+    col = np.asarray(col, np.float32)
+    ids = np.asarray(ids, np.int64)
+    k = (ids - first) // stride
+    fresh = (k >= 0) & ((ids - first) % stride == 0)
+    out = np.zeros(n_new, np.float32)
+    pos = np.nonzero(fresh)[0]
+    # duplicates of a new key inside one batch share its id: keep the first occurrence's value
+    out[k[pos][::-1]] = col[pos][::-1]
+    return out
 
 
 def _ncols(cols: Dict[str, list]) -> int:

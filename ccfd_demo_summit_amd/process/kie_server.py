@@ -9,6 +9,14 @@ KIE Server REST paths ([EXT], container/process/signal ids configurable, SURVEY.
   GET  /services/rest/server/containers/{c}/tasks/{t}                          -> task
   PUT  /services/rest/server/containers/{c}/tasks/{t}/states/completed         -> complete
   GET  /rest/metrics                                                           -> Prometheus
+Extensions for the GPU engine's router:
+  POST .../containers/{c}/processes/{p}/instances/batch       many starts in one request
+  POST .../containers/{c}/processes/{p}/instances/committed   the engine's committed offsets
+       (frees commit-gated dedupe keys, process/engine.py note_committed)
+  POST .../containers/{c}/processes/instances/signal/batch    many signals in one request
+  GET  .../containers/{c}/processes/instances/by-transaction/{tx}[?deep=1]
+       the process a transaction started -- standard ones too, which are counted, not
+       retained as instances (process/engine.py find_transaction)
 A background task fires process timers (``ProcessEngine.tick``).
 
 Sharded tier (process/sharding.py): a server is shard ``engine.shard`` of ``engine.shards``.
@@ -29,6 +37,7 @@ from aiohttp import web
 
 from ..metrics.exporter import CONTENT_TYPE
 from ..utils.lathist import LatHist
+from .dedupe import DedupeFull
 from .engine import ProcessEngine
 
 BASE = "/services/rest/server"
@@ -92,6 +101,8 @@ class KieServer:
         r = self.app.router
         r.add_post(BASE + "/containers/{c}/processes/{p}/instances", self.start)
         r.add_post(BASE + "/containers/{c}/processes/{p}/instances/batch", self.start_batch)
+        r.add_post(BASE + "/containers/{c}/processes/{p}/instances/committed", self.committed)
+        r.add_get(BASE + "/containers/{c}/processes/instances/by-transaction/{tx}", self.by_transaction)
         r.add_post(BASE + "/containers/{c}/processes/instances/signal/batch", self.signal_batch)
         r.add_post(BASE + "/containers/{c}/processes/instances/{i}/signal/{s}", self.signal)
         r.add_get(BASE + "/containers/{c}/processes/instances/{i}", self.get_instance)
@@ -233,6 +244,10 @@ class KieServer:
                 ids = self.engine.start_fraud_many(items)
             else:
                 ids = None
+        except DedupeFull as e:
+            # every dedupe key may still be re-delivered: refuse (retried by the hand-off) rather
+            # than evict one -- back-pressure until the engine's commits free room
+            return web.json_response({"type": "FAILURE", "msg": str(e)}, status=503)
         except (ValueError, TypeError, AttributeError) as e:
             return web.json_response({"type": "FAILURE", "msg": f"bad batch: {e}"}, status=400)
         if ids is None:
@@ -248,6 +263,43 @@ class KieServer:
             ids = ids.tolist()
         self.handler_time.add(time.monotonic_ns() - t0)
         return web.json_response(ids, status=201)
+
+    async def committed(self, request: web.Request):
+        """The engine's committed Kafka offsets ({"offsets": {partition: offset}})."""
+        bad = self._check_container(request)
+        if bad:
+            return bad
+        try:
+            body = json.loads(await request.read() or b"{}")
+            offs = {int(p): int(o) for p, o in body.get("offsets", {}).items()}
+        except (ValueError, TypeError, AttributeError) as e:
+            return web.json_response({"type": "FAILURE", "msg": f"bad offsets: {e}"}, status=400)
+        note = getattr(self.engine, "note_committed", None)
+        if note is not None:
+            note(offs)
+        return web.json_response({"type": "SUCCESS"}, status=200)
+
+    async def by_transaction(self, request: web.Request):
+        bad = self._check_container(request)
+        if bad:
+            return bad
+        try:
+            tx = int(request.match_info["tx"])
+        except ValueError:
+            return web.json_response({"type": "FAILURE", "msg": "transaction id must be an integer"}, status=400)
+        if self.shards > 1:
+            from .sharding import shard_of_tx
+            if shard_of_tx(tx, self.shards) != self.shard:
+                return self._misdirected("transaction")
+        deep = request.query.get("deep", "0") not in ("0", "", "false")
+        if deep:                                # journal scan: off the event loop
+            rec = await asyncio.get_running_loop().run_in_executor(None, self.engine.find_transaction, tx, True)
+        else:
+            rec = self.engine.find_transaction(tx)
+        if rec is None:
+            return web.json_response({"type": "FAILURE", "msg": f"no process for transaction {tx} on this shard "
+                                      "within the retention" + ("" if deep else " (try ?deep=1)")}, status=404)
+        return web.json_response(rec)
 
     def _note_request(self, items, t_in: int, n: int) -> None:
         sc = None
@@ -338,6 +390,8 @@ class KieServer:
                     "waiting_customer": sum(1 for i in e.instances.values() if i.state.value == "waiting_customer"),
                     "outcomes": dict(e.outcome_counts), "outcome_digest": f"{e.outcome_digest:016x}",
                     "next_instance_id": None}
+        if hasattr(e, "dedupe_stats"):
+            body["standard_dedupe"] = e.dedupe_stats()
         return web.json_response(body)
 
     async def metrics(self, _request):
@@ -420,6 +474,22 @@ class KieClient:
             import numpy as np
             return np.frombuffer(r.content, "<i8").tolist()
         return [int(x) for x in r.json()]
+
+    def note_committed(self, offsets) -> None:
+        """Tell the shard the engine committed these offsets (``/instances/committed``)."""
+        r = self.s.post(f"{self.base}/containers/{self.c}/processes/{self.standard_pid}/instances/committed",
+                        data=json.dumps({"offsets": {str(int(p)): int(o) for p, o in offsets.items()}}),
+                        headers={"Content-Type": "application/json"}, timeout=self.timeout)
+        r.raise_for_status()
+
+    def find_transaction(self, tx_id: int, deep: bool = False):
+        """The process transaction ``tx_id`` started on this shard (None: none in retention)."""
+        r = self.s.get(f"{self.base}/containers/{self.c}/processes/instances/by-transaction/{int(tx_id)}",
+                       params={"deep": "1"} if deep else None, timeout=max(self.timeout, 60.0 if deep else 0))
+        if r.status_code == 404:
+            return None
+        r.raise_for_status()
+        return r.json()
 
     def signal_many(self, items) -> list:
         """Many signals in one request (``signal/batch`` extension): items of

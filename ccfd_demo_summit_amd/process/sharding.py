@@ -167,6 +167,14 @@ class ShardedKieClient:
                 out[sh == k] = np.asarray(self.clients[k].start_standard_many(sub), np.int64)
         return out.tolist()
 
+    # -- commit watermark / audit
+    def note_committed(self, offsets) -> None:
+        for c in self.clients:
+            c.note_committed(offsets)
+
+    def find_transaction(self, tx_id: int, deep: bool = False):
+        return self.client_for_tx(tx_id).find_transaction(tx_id, deep=deep)
+
     # -- signals
     def signal(self, instance_id: int, name: str, payload) -> bool:
         return self.client_for_id(instance_id).signal(instance_id, name, payload)

@@ -79,7 +79,10 @@ def _transient(e: BaseException) -> bool:
     """Worth retrying: the server could not be reached or answered 5xx / 408 / 429.  Every
     other error -- a 4xx, a non-JSON 200 body, an invalid URL, a ValueError -- is a definite
     refusal that no retry can fix (requests' exceptions all derive from IOError, so an
-    ``OSError`` catch-all would retry those forever)."""
+    ``OSError`` catch-all would retry those forever).  An in-process sink's back-pressure
+    (e.g. process.dedupe.DedupeFull) says so with a ``transient`` attribute."""
+    if getattr(e, "transient", False):
+        return True
     try:
         import requests
         if isinstance(e, requests.HTTPError):
@@ -216,6 +219,11 @@ def deliver(sink, kind: str, payload: Any, batch_signals: bool = True) -> Tuple[
             for v in payload:
                 sink.start_fraud(v)
         return 0, 0
+    if kind == "committed":
+        note = getattr(sink, "note_committed", None)
+        if note is not None:
+            note(payload)
+        return 0, 0
     if kind == "standard":
         many = getattr(sink, "start_standard_many", None)
         if many is not None:
@@ -242,6 +250,7 @@ class KieHandoff:
         self.sink = sink
         self.dlq = dlq
         self.batch_signals = bool(batch_signals) and hasattr(sink, "signal_many")
+        self.commit_notices = True         # False once the server lacks instances/committed
         self.refused = 0                   # refusals seen (held or dead-lettered)
         self.dead_lettered = 0
         self.capacity = int(capacity)
@@ -320,6 +329,11 @@ class KieHandoff:
     def submit_signal(self, instance_id: int, name: str, payload: Any) -> int:
         return self._push("signal", (int(instance_id), name, payload), 1)
 
+    def submit_committed(self, offsets: Dict[int, int]) -> int:
+        """Queue a committed-offsets notice behind every start queued so far (it carries no
+        items: it frees the shard's commit-gated dedupe keys, process/engine.py)."""
+        return self._push("committed", {int(p): int(o) for p, o in offsets.items()}, 0)
+
     def last_seq(self) -> int:
         with self._cv:
             return self._next_seq - 1
@@ -369,6 +383,19 @@ class KieHandoff:
             self._cv.notify_all()
 
     def _deliver(self, kind: str, payload: Any) -> None:
+        if kind == "committed":
+            if not self.commit_notices:
+                return
+            try:
+                deliver(self.sink, kind, payload)
+            except BaseException as e:             # noqa: BLE001
+                if _status(e) not in MISSING_ROUTE_HTTP:
+                    raise
+                # a KIE server without the extension keeps a count-window dedupe: stop telling it
+                self.commit_notices = False
+                with self._cv:
+                    self.errors.append(f"instances/committed unsupported ({_status(e)})")
+            return
         if kind == "signals" and self.batch_signals:
             try:
                 ok, stale = deliver(self.sink, kind, payload, batch_signals=True)
@@ -417,8 +444,17 @@ class KieHandoff:
                         rows += _ncols(p2)
                     if len(parts) > 1:
                         payload = _concat_columns(parts)
+                elif kind == "committed":
+                    # a run of notices is one notice: offsets only grow, keep the max
+                    payload = dict(payload)
+                    while self._q and self._q[0][1] == "committed":
+                        s2, _k, p2, _t = self._q.popleft()
+                        seqs.append(s2)
+                        for p, o in p2.items():
+                            payload[p] = max(payload.get(p, o), o)
             n_items = len(payload) if kind in ("start", "signals") else \
-                (len(next(iter(payload.values()))) if kind == "standard" and payload else 1)
+                (len(next(iter(payload.values()))) if kind == "standard" and payload else
+                 0 if kind == "committed" else 1)
             t_pop = time.monotonic_ns()
             self.queue_wait.add(t_pop - t_push)
             delay = self.backoff_s
@@ -545,6 +581,12 @@ class ShardedHandoff:
         with self._lock:
             self.parts[int(instance_id) % self.shards].submit_signal(instance_id, name, payload)
             return self._mark()
+
+    def submit_committed(self, offsets: Dict[int, int]) -> None:
+        """Every shard admits standard starts of every partition: broadcast the notice."""
+        with self._lock:
+            for p in self.parts:
+                p.submit_committed(offsets)
 
     def last_seq(self) -> int:
         with self._lock:

@@ -27,11 +27,27 @@ from ..metrics.exporter import RouterMetrics
 from .rules import RuleSet
 
 
-def standard_columns(rec: np.ndarray) -> Dict[str, np.ndarray]:
+def standard_columns(rec: np.ndarray, marks: Optional[Dict[int, int]] = None) -> Dict[str, np.ndarray]:
     """Scored records -> the column batch a standard-process hand-off carries (numpy columns:
-    KieClient sends them as a binary CCOL body, process/kie_server.py encode_columns)."""
-    return {"transaction_id": rec["tx_id"].astype(np.int64), "customer_id": rec["customer"].astype(np.int64),
+    KieClient sends them as a binary CCOL body, process/kie_server.py encode_columns).
+
+    ``marks`` (partition -> an offset above every scored row of it, the engine service's
+    commit marks) adds the commit-gate columns ``kafka_partition`` / ``commit_mark``: the KIE
+    shard keeps these transactions in its dedupe index until the engine's committed offsets
+    pass the mark (process/engine.py note_committed)."""
+    cols = {"transaction_id": rec["tx_id"].astype(np.int64), "customer_id": rec["customer"].astype(np.int64),
             "amount": rec["amount"].astype(np.float32), "proba": rec["proba"].astype(np.float32)}
+    if marks:
+        part = rec["partition"].astype(np.int64)
+        lut = np.zeros(int(max(int(part.max()) if len(part) else 0, max(marks))) + 1, np.int64)
+        for p, m in marks.items():
+            lut[int(p)] = int(m)
+        mark = lut[part]
+        if len(mark) and int(mark.min()) <= 0:
+            raise ValueError("standard rows of a partition without a commit mark")
+        cols["kafka_partition"] = part
+        cols["commit_mark"] = mark
+    return cols
 
 
 class Router:
@@ -96,7 +112,7 @@ class Router:
         return {"incoming": n, "fraud": int(len(fraud_idx)), "standard": int(n - len(fraud_idx))}
 
     def on_flagged(self, flagged: np.ndarray, total_rows: int,
-                   standard: Optional[np.ndarray] = None) -> Dict[str, int]:
+                   standard: Optional[np.ndarray] = None, marks: Optional[Dict[int, int]] = None) -> Dict[str, int]:
         """Engine hot path: ``flagged`` = the fraud-routed rows (the engine's flagged-record
         array; the GPU epilogue counted the rest).  ``standard``: with ``standard_mode="process"``
         the engine's standard-routed scored records (SCORED_DTYPE: tx_id, customer, proba,
@@ -108,7 +124,7 @@ class Router:
         self.metrics.tx_outgoing.labels(type="standard").inc(total_rows - nf)
         std_cols = None
         if self.standard_mode == "process" and standard is not None and len(standard):
-            std_cols = standard_columns(standard)
+            std_cols = standard_columns(standard, marks)
             if self.scored_ns:
                 std_cols["scored_ns"] = np.full(len(standard), self.scored_ns, np.int64)
         if self.handoff is not None:                        # async, retried, acked later

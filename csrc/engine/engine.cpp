@@ -152,7 +152,8 @@ class Engine {
   std::vector<ccfd_flagged> ring;
   uint64_t ring_head = 0, ring_tail = 0;
   std::mutex ring_mu;
-  uint64_t dropped = 0;
+  uint64_t dropped = 0;              // must stay 0: complete() reserves room first (lossless)
+  uint64_t flag_full_events = 0;     // completions deferred because the ring was full
   // opt-in scored-record ring (every row; ccfd_engine_scored_enable), same producer/consumer
   std::vector<ccfd_scored> sring;
   uint64_t s_head = 0, s_tail = 0, s_dropped = 0;
@@ -315,7 +316,8 @@ class Engine {
     }
     // never hipDeviceSynchronize here: another engine's persistent kernel may be resident
     HIPCHK(hipStreamSynchronize(streams[0]));
-    ring.resize(std::max(1024, cfg.flag_capacity));
+    // one micro-batch must always fit (a batch is handed off whole or not at all)
+    ring.resize(std::max({1024, cfg.flag_capacity, cfg.max_batch}));
     stamper_on = true;
     if (const char* e = std::getenv("CCFD_COMPLETION_THREAD")) stamper_on = std::atoi(e) != 0;
     if (stamper_on) {
@@ -608,7 +610,7 @@ class Engine {
     if (p < 0 || p > 4096) { set_error("bad partition index"); return -1; }
     if (n < cfg.max_batch) { set_error("partition log shorter than one micro-batch"); return -1; }
     if (reinterpret_cast<uintptr_t>(feats) & 15) { set_error("log must be 16-byte aligned"); return -1; }
-    drain_all();
+    { int rc = drain_all(); if (rc) return rc; }
     while ((int)parts.size() <= p) parts.emplace_back(new Partition());
     Partition& P = *parts[p];
     P.ring = false;
@@ -646,7 +648,25 @@ class Engine {
     for (; i < n; ++i) if (r[i]) emit(P, s, i, cap);
   }
 
+  // free records in the flagged ring (drainers only ever grow it)
+  uint64_t flag_room() {
+    std::lock_guard<std::mutex> lk(ring_mu);
+    return ring.size() - (ring_tail - ring_head);
+  }
+
+  // fraud-routed rows of a finished batch: the kernel-published count, or the route bytes
+  uint64_t nflag_of(const Slot& s) const {
+    if (s.use_flag) return s.done_ptr[1];
+    uint64_t nf = 0;
+    for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
+    return nf;
+  }
+
+  // complete() found the batch's flagged records do not fit: nothing was retired
+  static constexpr int kFlagFull = CCFD_ENGINE_FLAG_FULL;
+
   inline void emit(const Partition& P, const Slot& s, int i, uint64_t cap) {
+    // complete() reserved room for the whole batch before calling in; reaching this is a bug
     if (ring_tail - ring_head >= cap) { ++dropped; return; }
     const int64_t row = s.start + i;
     ccfd_flagged& f = ring[ring_tail % cap];
@@ -739,11 +759,16 @@ class Engine {
     e.pad = 0;
   }
 
+  // Retire finished batch `s`.  Lossless hand-off: when the flagged ring lacks room for the
+  // batch's fraud-routed rows, nothing is retired (the batch stays busy, its ring rows stay
+  // unreleased, so back-pressure reaches ingest) and kFlagFull asks the caller to drain.
   int complete(Slot& s, ccfd_engine_stats* st) {
     const int64_t tw = now_ns();
     { int rc = wait_done(s); if (rc) return rc; }
     const int64_t t = now_ns();
     t_wait_ns += t - tw;
+    const uint64_t nf_need = nflag_of(s);
+    if (nf_need && flag_room() < nf_need) { ++flag_full_events; return kFlagFull; }
     const int64_t t0 = s.t_arrival ? s.t_arrival : s.t_submit;   // ring: end-to-end from commit
     const int64_t t_landed = landed_ns(s, t);                   // results in host memory
     const double us = (t_landed - t0) * 1e-3;
@@ -767,9 +792,8 @@ class Engine {
       origin_hist[b]++;
       origin_hist_rows[b] += (uint64_t)s.rows;
     }
-    uint64_t nf = 0;
+    const uint64_t nf = nf_need;
     if (s.use_flag) {
-      nf = s.done_ptr[1];
       if (nf) push_flagged_idx(s, nf);
       {                                                // K7: device-clock execution window
         const uint64_t t0d = s.done_ptr[2], t1d = s.done_ptr[3];
@@ -782,9 +806,8 @@ class Engine {
           dev_hist_rows[b] += (uint64_t)s.rows;
         }
       }
-    } else {
-      for (int i = 0; i < s.rows; ++i) nf += s.h_route[i];
-      if (nf) push_flagged(s);
+    } else if (nf) {
+      push_flagged(s);
     }
     if (scored_on.load(std::memory_order_relaxed)) push_scored(s);
     if (st) { st->batches++; st->rows += s.rows; st->fraud_rows += nf; }
@@ -817,7 +840,7 @@ class Engine {
     const int D = (int)slots.size();
     for (int k = 0; k < D; ++k) {
       Slot& s = slots[(seq + k) % D];
-      if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
+      if (s.busy) { int rc = complete(s, st); if (rc) return rc; }   // kFlagFull: drain, call again
     }
     // fully drained: let the persistent kernel exit so the device is idle (and a
     // device-wide synchronize by the caller can never wait on a resident kernel)
@@ -929,7 +952,20 @@ class Engine {
     const int64_t t0 = now_ns();
     const int D = (int)slots.size();
     const int kmax = coalesce_max();
-    for (int64_t b = 0; b < n_batches;) {
+    int64_t b = 0;
+    // every exit reports the batches submitted by this call: a kFlagFull return is resumed by
+    // the caller (after draining the flagged ring) with n_batches - submitted
+    auto finish = [&](int rc) {
+      if (st) {
+        st->submitted += (uint64_t)b;
+        st->wall_s += (now_ns() - t0) * 1e-9;
+        st->flagged_dropped = dropped;
+        st->flag_full_events = flag_full_events;
+        fill_latency(st);
+      }
+      return rc;
+    };
+    while (b < n_batches) {
       int p = next_part;
       for (int k = 0; k < (int)parts.size() && (parts[p]->feats == nullptr || parts[p]->ring); ++k)
         p = (p + 1) % parts.size();
@@ -941,11 +977,11 @@ class Engine {
       const int K = (int)std::min<int64_t>({(int64_t)kmax, n_batches - b, (P.n - P.cursor) / batch_rows});
       for (int k = 0; k < K; ++k) {
         Slot& s = slots[(seq + k) % D];
-        if (s.busy) { int rc = complete(s, st); if (rc) return rc; }
+        if (s.busy) { int rc = complete(s, st); if (rc) return finish(rc); }
       }
       if (K > 1) {
         int rc = submit_multi(p, P.cursor, batch_rows, K);
-        if (rc) return rc;
+        if (rc) return finish(rc);
         P.cursor += (int64_t)K * batch_rows;
         seq += K;
         b += K;
@@ -957,20 +993,11 @@ class Engine {
       const size_t off = (size_t)s.start * rowf;
       hipStream_t stream = streams[seq % streams.size()];
       int rc = submit(s, P.feats_dev + off, P.feats + off, batch_rows, stream);
-      if (rc) return rc;
+      if (rc) return finish(rc);
       ++seq;
       ++b;
     }
-    if (drain) {
-      int rc = drain_all(st);
-      if (rc) return rc;
-    }
-    if (st) {
-      st->wall_s += (now_ns() - t0) * 1e-9;
-      st->flagged_dropped = dropped;
-      fill_latency(st);
-    }
-    return 0;
+    return finish(drain ? drain_all(st) : 0);
   }
 
   // nearest-rank quantile from the fine histogram (bucket midpoint); samples beyond its
@@ -1163,7 +1190,9 @@ class Engine {
         // scored ring full: leave the batch (and its ring rows) in place until the consumer
         // drains -- back-pressure reaches ingest instead of losing standard-route records
         if (scored_on.load(std::memory_order_relaxed) && scored_room() < (uint64_t)s.rows) break;
+        // flagged ring full: the same -- the batch waits for the hand-off consumer (never dropped)
         int rc = complete(s, st);
+        if (rc == kFlagFull) break;
         if (rc) return rc;
         progress = true;
       }
@@ -1234,6 +1263,8 @@ class Engine {
     if (st) {
       st->wall_s += (now_ns() - t0) * 1e-9;
       st->flagged_dropped = dropped;
+      st->flag_full_events = flag_full_events;
+      st->submitted += (uint64_t)submitted;
       fill_latency(st);
     }
     return submitted;
@@ -1362,6 +1393,7 @@ int ccfd_engine_serve_collect(void* eng, ccfd_engine_stats* out, ccfd_flagged* f
   *out = e->serve_st;
   e->fill_latency(out);
   out->flagged_dropped = e->dropped;
+  out->flag_full_events = e->flag_full_events;
   *n_flagged = e->drain_flagged(flagged, max_flagged);
   if (n_scored) *n_scored = (scored && max_scored > 0) ? e->drain_scored(scored, max_scored) : 0;
   return e->serve_rc.load();
@@ -1374,6 +1406,7 @@ int ccfd_engine_serve_stats(void* eng, ccfd_engine_stats* out, int64_t* iters) {
   *out = e->serve_st;
   e->fill_latency(out);
   out->flagged_dropped = e->dropped;
+  out->flag_full_events = e->flag_full_events;
   if (iters) *iters = (int64_t)e->serve_iters;
   return e->serve_rc.load();
 }

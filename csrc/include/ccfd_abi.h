@@ -279,7 +279,17 @@ typedef struct ccfd_engine_stats {
   uint64_t origin_batches;
   uint64_t origin_hist[256];
   uint64_t origin_hist_rows[256];
+  // lossless hand-off (round 6): micro-batches submitted by the call(s) that filled this record,
+  // and completions deferred so far because the flagged ring had no room for a batch's records
+  uint64_t submitted;
+  uint64_t flag_full_events;
 } ccfd_engine_stats;
+
+// ccfd_engine_pump / drain paths: a finished micro-batch's fraud-routed records do not fit in
+// the flagged ring.  Nothing was retired or lost; drain the ring (ccfd_engine_drain_flagged) and
+// call again (pump: with n_batches - stats.submitted).  ccfd_engine_run() never returns it: it
+// leaves such batches in flight until a later call finds room.
+#define CCFD_ENGINE_FLAG_FULL 1
 
 void* ccfd_engine_create(const ccfd_engine_config* cfg);
 void ccfd_engine_destroy(void* eng);
@@ -293,7 +303,9 @@ int ccfd_engine_set_log(void* eng, int partition, const float* feats, const uint
 // partitions.  With drain != 0 it blocks until every submitted batch is complete;
 // otherwise up to `depth` batches stay in flight across calls (no pipeline bubble between
 // steps).  Counts of completed batches accumulate into *st; latency percentiles cover all
-// batches completed since the last ccfd_engine_reset_stats().
+// batches completed since the last ccfd_engine_reset_stats().  Returns CCFD_ENGINE_FLAG_FULL
+// (after submitting stats.submitted batches) when the flagged ring cannot take a finished
+// batch's records: the hand-off is lossless, so the caller drains and resumes.
 int ccfd_engine_pump(void* eng, int64_t n_batches, int32_t batch_rows, int32_t drain,
                      ccfd_engine_stats* st);
 // Score one caller-provided batch (pinned host or device pointer) synchronously; proba/route

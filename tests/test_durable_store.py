@@ -322,3 +322,20 @@ def test_producer_sequences_wrap_at_2_pow_31():
         kb.close()
     finally:
         cl.stop()
+
+
+def test_truncate_refuses_a_cut_inside_the_last_batch():
+    """an offset inside the LAST batch (bisect lands past the end) was accepted and
+    left the log end pointing into a stored batch."""
+    from ccfd_demo_summit_amd.ingest.batch_store import BatchStore
+    from ccfd_demo_summit_amd.ingest.broker import BrokerError
+    s = BatchStore(default_partitions=1)
+    s.create_topic("t", 1)
+    s.append_raw("t", 0, _batch(["a", "b", "c"]))
+    s.append_raw("t", 0, _batch(["d", "e", "f"]))
+    with pytest.raises(BrokerError):
+        s.truncate("t", 0, 4)                 # inside the last batch [3, 6)
+    with pytest.raises(BrokerError):
+        s.truncate("t", 0, 1)                 # inside the first batch [0, 3)
+    assert s.end_offset("t", 0) == 6
+    assert s.truncate("t", 0, 3) == 1 and s.end_offset("t", 0) == 3
