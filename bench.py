@@ -538,6 +538,8 @@ def main(argv=None):
 
     wd_state.update(engine=eng, epochs=epochs, phase="warmup")
     watchdog.on_fire = lambda: eng.emergency_stop(5000)     # never exit with a resident kernel
+    if faults is not None:
+        faults.before_exit = lambda: eng.emergency_stop(5000)
     import signal
 
     def _term(signum, _frame):                 # an outer SIGTERM: the kernel leaves first

@@ -6,12 +6,16 @@ followers that replicate by FETCHING from the leader, as Kafka's replica fetcher
 
 * **followers** run one fetcher per leader broker: a Kafka Fetch v4 with ``replica_id`` =
   their node id, from their log end offset (LEO), appended verbatim at the leader's offsets
-  (``BatchStore.append_replica``) and written before the next fetch -- the fetch offset IS the
-  follower's durable LEO, which is what the leader counts;
+  (``BatchStore.append_replica``) and written by the store's writer right behind -- the next
+  fetch reports the in-memory LEO, which is what the leader counts;
 * **the leader** tracks each follower's LEO from its fetches; the partition's high watermark
   (HW) is the minimum LEO over the in-sync replicas (ISR).  Consumers only see offsets below
   the HW; a produce with ``acks=all`` (-1) is answered once the HW covers it, so an
-  acknowledged record is on every ISR member;
+  acknowledged record is on every ISR member.  The LEOs are IN-MEMORY log ends (a follower
+  reports its log end at its next fetch, before its background writer has written it), so the
+  guarantee assumes no correlated crash of every ISR member within the write-behind window --
+  Kafka's page-cache assumption.  With the leader alone in the ISR there is no second copy to
+  cover that window: the HW then counts the leader's WRITTEN offset only;
 * **ISR**: the leader proposes (in its next heartbeat) to drop a follower that has not caught
   up for ``replica_lag_s`` and to re-admit one that has caught up; the controller applies
   proposals of the current leader epoch only;
@@ -20,7 +24,8 @@ followers that replicate by FETCHING from the leader, as Kafka's replica fetcher
   to the HW it knows when it starts following a new leader, and re-fetches from there, so its
   log is a prefix of the leader's.  A broker that restarts cuts its logs to its checkpointed
   HW (``replication.json``, every 200 ms) -- except where it was the sole ISR member (its log is
-  then the authority);
+  then the authority; becoming sole is checkpointed synchronously, before any answer relies
+  on it);
 * **pipelined producers** (``max.in.flight`` > 1, kafka_wire.py) keep one request in flight
   per partition, so a refused batch is never overtaken by a later one;
 * producer ids are per-broker disjoint (``node + 1024 k``) and the idempotent-producer state
@@ -117,6 +122,7 @@ class ReplicaManager:
         self._lead_since: Dict[TP, float] = {}
         self.truncations = 0
         self.truncated_batches = 0
+        self._sole_ckpt: set = set()                  # sole-ISR partitions in replication.json
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self) -> None:
@@ -293,6 +299,11 @@ class ReplicaManager:
                     self._truncate_to_hw(tp)
             if st["leader"] == self.node_id:
                 self._advance_hw(tp)
+        sole = self._sole()
+        if sole - self._sole_ckpt:
+            # newly sole ISR member: checkpoint that NOW -- a restart before the periodic write
+            # would cut this log to an older HW and delete batches acknowledged meanwhile
+            self._write_ckpt_sync()
         self._reconcile_fetchers()
         if self.ready is not None:
             self.ready.set()
@@ -319,11 +330,20 @@ class ReplicaManager:
             if self.is_leader(*tp):
                 self._advance_hw(tp)
 
+    def _written(self, tp: TP) -> int:
+        """This replica's written (durable) log end."""
+        try:
+            return self.store.end_offset(*tp)
+        except BrokerError:
+            return 0
+
     def _advance_hw(self, tp: TP) -> None:
         st = self.parts.get(tp)
         if st is None or st["leader"] != self.node_id:
             return
-        leos = [self._leo(tp)]
+        # alone in the ISR, nothing else holds an unwritten batch: count only what is written
+        # (an in-memory LEO here would acknowledge acks=all records a crash could still lose)
+        leos = [self._leo(tp) if len(st["isr"]) > 1 else self._written(tp)]
         fol = self.fol.get(tp, {})
         for n in st["isr"]:
             if n != self.node_id:
@@ -406,25 +426,36 @@ class ReplicaManager:
         """When this broker became leader of tp (a follower gets replica_lag_s to show up)."""
         return self._lead_since.setdefault(tp, time.monotonic())
 
+    def _sole(self) -> set:
+        return {tp_key(*tp) for tp, st in self.parts.items()
+                if st["leader"] == self.node_id and st["isr"] == [self.node_id]}
+
+    def _ckpt_body(self) -> Dict[str, Any]:
+        hw = {}
+        for tp, st in self.parts.items():
+            if self.node_id in st["replicas"]:
+                hw[tp_key(*tp)] = min(self.hw.get(tp, 0), self._leo(tp))
+        sole = sorted(self._sole())
+        return {"hw": hw, "sole": sole}
+
+    def _write_ckpt_sync(self) -> None:
+        if not self.data_dir:
+            return
+        body = self._ckpt_body()
+        _write_json_atomic(os.path.join(self.data_dir, "replication.json"), body)
+        self._sole_ckpt = set(body["sole"])
+
     async def _ckpt_loop(self) -> None:
         if not self.data_dir:
             return
         path = os.path.join(self.data_dir, "replication.json")
         while True:
             await asyncio.sleep(0.2)
-            hw = {}
-            sole = []
-            for tp, st in self.parts.items():
-                if self.node_id not in st["replicas"]:
-                    continue
-                h = self.hw.get(tp, 0)
-                if st["leader"] == self.node_id and st["isr"] == [self.node_id]:
-                    sole.append(tp_key(*tp))
-                hw[tp_key(*tp)] = min(h, self._leo(tp))
+            body = self._ckpt_body()
             # written off the event loop: the file replace alone took ~4-6 ms on the test boxes'
             # overlay filesystems, every 200 ms, in front of every fetch and produce
-            await asyncio.get_running_loop().run_in_executor(None, _write_json_atomic, path,
-                                                             {"hw": hw, "sole": sole})
+            await asyncio.get_running_loop().run_in_executor(None, _write_json_atomic, path, body)
+            self._sole_ckpt = set(body["sole"])
 
     def _truncate_to_hw(self, tp: TP, hw: Optional[int] = None) -> None:
         h = self.hw.get(tp, 0) if hw is None else hw

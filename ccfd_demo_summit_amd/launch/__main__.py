@@ -166,6 +166,13 @@ def cmd_kafka_controller(a, cfg):
             "--rf", str(a.replication_factor)]
     if a.data_dir:
         argv += ["--data-dir", a.data_dir]
+    if a.peers:                       # one member of a replicated controller
+        member = a.member_id
+        if member in ("auto", "", None):
+            # StatefulSet pod <name>-k is member k + 1
+            from ..process.sharding import shard_from_env
+            member = str(shard_from_env(None) + 1)
+        argv += ["--member-id", str(member), "--peers", a.peers]
     main(argv)
 
 
@@ -432,6 +439,18 @@ def cmd_engine(a, cfg):
     def _term(*_a):
         raise SystemExit(0)
     signal.signal(signal.SIGTERM, _term)
+
+    def _crash(*_a):
+        # SIGUSR1: crash NOW -- no drain, no offset commit, no hand-off flush (what a SIGKILL
+        # leaves behind: the rank restarts from its committed offsets), except that a resident
+        # persistent kernel is stopped first (a process must never end with one resident)
+        try:
+            svc.engine.serve_stop()
+            svc.engine.emergency_stop(5000)
+        finally:
+            print(f"[engine] rank {ctx.rank}: crash (SIGUSR1), no commit", flush=True)
+            os._exit(137)
+    signal.signal(signal.SIGUSR1, _crash)
     resp_wait = None                  # hand-off seq carrying the last polled responses' signals
     try:
         while True:
@@ -662,7 +681,11 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--node-id", default=None,
                     help="kafka-lite replicated: this broker's node id, or 'auto' (pod ordinal + 1)")
     ap.add_argument("--controller", default=None,
-                    help="kafka-lite replicated: the controller's URL (launch kafka-controller)")
+                    help="kafka-lite replicated: the controller's URL, or its members' URLs comma-separated")
+    ap.add_argument("--member-id", default=None,
+                    help="kafka-controller replicated: this member's id in --peers, or 'auto' (pod ordinal + 1)")
+    ap.add_argument("--peers", default=None,
+                    help="kafka-controller replicated: every member as id=url, comma-separated")
     ap.add_argument("--cr", default=None, help="operator: FraudDetection (or OpenDataHub) CR file")
     ap.add_argument("--render", default=None, help="operator: write Kubernetes manifests here ('-' = stdout)")
     ap.add_argument("--local", action="store_true", help="operator: reconcile the CR into local processes")

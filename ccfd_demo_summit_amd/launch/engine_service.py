@@ -204,6 +204,8 @@ class EngineService:
         # applied here: this consumer's position advances on poll, so a drop would be real loss
         from ..utils.faults import FaultPlan
         self.faults = FaultPlan.from_env(ctx.rank)
+        if self.faults is not None:
+            self.faults.before_exit = lambda: (self.engine.serve_stop(), self.engine.emergency_stop(5000))
         self._fetch = self.cfg.max_fetch
         # commit gating on the KIE hand-off: offsets released by scoring (snapshotted on the
         # scoring thread right after the flagged rows of the same batches were drained) wait

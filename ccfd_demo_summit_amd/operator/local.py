@@ -102,15 +102,21 @@ def local_commands(spec: FraudDetectionSpec, host: str = "127.0.0.1", port_offse
     w = ["--weights", spec.engine.weights] if spec.engine.weights else []
     svc: Dict[str, tuple] = {}
     if spec.kafka.deploy and spec.kafka.replicated:
-        # replica r is broker node r + 1 (its own port, log and metrics port) + one controller
-        svc["kafka-controller"] = (1, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller",
-                                                 "--host", host, "--port", str(ctl_port),
-                                                 "--brokers", str(spec.kafka.brokers),
-                                                 "--rf", str(spec.kafka.replication_factor),
-                                                 "--data-dir", os.path.join(state, "kafka-controller")])
+        # replica r is broker node r + 1 (its own port, log and metrics port); controller replica
+        # r is quorum member r + 1 (ingest/controller_quorum.py) on ctl_port + r
+        nctl = max(1, spec.kafka.controllers)
+        peers = ",".join(f"{k + 1}=http://{host}:{ctl_port + k}" for k in range(nctl))
+        ctl_urls = ",".join(f"http://{host}:{ctl_port + k}" for k in range(nctl))
+        svc["kafka-controller"] = (nctl, lambda r: [sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_controller",
+                                                    "--host", host, "--port", str(ctl_port + r),
+                                                    "--brokers", str(spec.kafka.brokers),
+                                                    "--rf", str(spec.kafka.replication_factor),
+                                                    "--data-dir", os.path.join(state, "kafka-controller"
+                                                                               + (f"-{r + 1}" if nctl > 1 else ""))]
+                                   + (["--member-id", str(r + 1), "--peers", peers] if nctl > 1 else []))
         svc["kafka"] = (spec.kafka.brokers, lambda r: [
             sys.executable, "-m", "ccfd_demo_summit_amd.ingest.kafka_lite", "--host", host,
-            "--port", str(kafka_port + r), "--node-id", str(r + 1), "--controller", f"http://{host}:{ctl_port}",
+            "--port", str(kafka_port + r), "--node-id", str(r + 1), "--controller", ctl_urls,
             "--metrics-port", str(9404 + o + r), "--data-dir", os.path.join(state, f"kafka-lite-{r + 1}"),
             "--fsync", spec.kafka.fsync])
     elif spec.kafka.deploy:

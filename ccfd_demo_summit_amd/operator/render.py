@@ -101,24 +101,35 @@ def render(spec: FraudDetectionSpec) -> List[Dict[str, Any]]:
     if spec.kafka.deploy and spec.kafka.replicated:
         # replicated kafka-lite (ingest/kafka_replica.py): `brokers` broker pods, each its own
         # durable log on its own claim, replication factor min(3, brokers); pod k is node k + 1
-        # (--node-id auto), advertised under the headless service; the controller pod keeps
-        # membership, leaders / ISR and the committed offsets (ingest/kafka_controller.py)
+        # (--node-id auto), advertised under the headless service; the controller keeps
+        # membership, leaders / ISR and the committed offsets (ingest/kafka_controller.py) --
+        # `controllers` member pods of a replicated quorum (ingest/controller_quorum.py, the
+        # reference's three ZooKeeper nodes), pod k = member k + 1 (--member-id auto)
         name = f"{spec.kafka.cluster_name}-kafka"
         ctl = f"{name}-controller"
+        nctl = max(1, spec.kafka.controllers)
+        members = [f"http://{ctl}-{k}.{ctl}-members:9093" for k in range(nctl)]
+        quorum = ["--member-id", "auto", "--peers", ",".join(f"{k + 1}={u}" for k, u in enumerate(members))] \
+            if nctl > 1 else []
         cc = _container(spec, "controller", LAUNCH + ["kafka-controller", "--port", "9093", "--nodes",
                                                       str(spec.kafka.brokers), "--replication-factor",
                                                       str(spec.kafka.replication_factor),
-                                                      "--data-dir", "/var/lib/kafka-controller"],
+                                                      "--data-dir", "/var/lib/kafka-controller"] + quorum,
                         ports=[{"containerPort": 9093, "name": "http"}], envfrom=False,
                         probe=("/health/ping", 9093, 20))
         cc["volumeMounts"] = [{"name": "controller-data", "mountPath": "/var/lib/kafka-controller"}]
-        ctl_extra = {"volumeClaimTemplates": [{"metadata": {"name": "controller-data"}, "spec": {
-            "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}}]}
-        out.append(_workload("StatefulSet", ctl, ctl, 1, [cc], annotations=_scrape("/metrics", 9093),
+        ctl_extra = {"serviceName": f"{ctl}-members", "podManagementPolicy": "Parallel",
+                     "volumeClaimTemplates": [{"metadata": {"name": "controller-data"}, "spec": {
+                         "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}}]}
+        out.append(_workload("StatefulSet", ctl, ctl, nctl, [cc], annotations=_scrape("/metrics", 9093),
                              extra_spec=ctl_extra))
         out.append(_service(ctl, ctl, [{"name": "http", "port": 9093, "targetPort": 9093}]))
+        out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": f"{ctl}-members"},
+                    "spec": {"clusterIP": "None", "selector": {"app": ctl}, "publishNotReadyAddresses": True,
+                             "ports": [{"name": "http", "port": 9093, "targetPort": 9093}]}})
+        ctl_urls = ",".join(members) if nctl > 1 else f"http://{ctl}:9093"
         kc = _container(
-            spec, "kafka", LAUNCH + ["kafka-lite", "--node-id", "auto", "--controller", f"http://{ctl}:9093",
+            spec, "kafka", LAUNCH + ["kafka-lite", "--node-id", "auto", "--controller", ctl_urls,
                                      "--port", "9092", "--advertise", f"$(POD_NAME).{name}-brokers",
                                      "--data-dir", "/var/lib/kafka-lite", "--fsync", spec.kafka.fsync],
             ports=[{"containerPort": 9092, "name": "broker"}, {"containerPort": 9404, "name": "metrics"}],

@@ -44,6 +44,8 @@ class KafkaSpec:
                                      # cluster of 3 brokers; False = one pod, N listeners
     replication_factor: int = 3      # copies of every partition (1 = scale-out only, Kafka's default for
                                      # auto-created topics; 3 = a broker loss loses nothing acknowledged)
+    controllers: int = 3             # replicated controller members (ingest/controller_quorum.py) -- the
+                                     # reference's kafka_zookeeper_replicas; 1 = a single controller
 
 
 @dataclass
@@ -240,7 +242,9 @@ def from_odh(doc: Dict[str, Any]) -> FraudDetectionSpec:
     spec.kafka.cluster_name = str(k.get("kafka_cluster_name", spec.kafka.cluster_name))
     spec.kafka.brokers = int(k.get("kafka_broker_replicas", spec.kafka.brokers))
     if "kafka_zookeeper_replicas" in k:
-        spec.notes.append("kafka.kafka_zookeeper_replicas: no ZooKeeper (the kafka-lite controller is in-process)")
+        spec.kafka.controllers = max(1, int(k["kafka_zookeeper_replicas"]))
+        spec.notes.append(f"kafka.kafka_zookeeper_replicas {spec.kafka.controllers} -> a {spec.kafka.controllers}-member "
+                          "replicated kafka-lite controller (ingest/controller_quorum.py) in ZooKeeper's role")
     spec.seldon.deploy = on("seldon")
     spec.monitoring.deploy = on("monitoring")
     jh = s.get("aicoe-jupyterhub") or {}

@@ -58,6 +58,9 @@ class FaultPlan:
 
     def __post_init__(self):
         self._rng = np.random.default_rng(self.seed * 1_000_003 + self.rank)
+        # called right before a crash clause's os._exit: the GPU state a crashed rank must not
+        # leave behind (the engine service stops its persistent kernel here)
+        self.before_exit = None
         self._t0 = time.monotonic()
 
     @classmethod
@@ -113,6 +116,8 @@ class FaultPlan:
                 if due:
                     self.injected["crash"] += 1
                     if c.mode == "exit":
+                        if self.before_exit is not None:
+                            self.before_exit()          # e.g. stop a resident persistent kernel
                         os._exit(17)                    # no cleanup, no commit: like SIGKILL
                     raise InjectedCrash(f"injected crash on rank {self.rank} at step {self.steps}")
 

@@ -338,3 +338,71 @@ def test_broker_away_past_the_leaders_retention_restarts_at_its_log_start(small_
     assert all(len(v["isr"]) == 3 for k_, v in md["parts"].items() if k_.startswith("t/")), md["parts"]
     assert not any(under), under
     kb.close()
+
+
+def test_sole_isr_leader_sigkill_loses_no_acknowledged_record(cluster):
+    """with the ISR shrunk to the leader alone, an acks=all produce must not be
+    answered before the leader WROTE it (no other copy exists), and the leader's sole-ISR
+    status must be on disk before such an answer -- else a SIGKILL + restart cut the log to an
+    older checkpointed HW.  Two brokers die, the third takes acknowledged writes alone, is
+    SIGKILLed right after, restarts: every acknowledged record is there."""
+    c = cluster
+    boot = ",".join(f"127.0.0.1:{p}" for p in c["bports"])
+    deadline = time.time() + 30
+    while len(json.loads(_text(f"http://127.0.0.1:{c['cport']}/metadata"))["nodes"]) < 3:
+        assert time.time() < deadline
+        time.sleep(0.1)
+    kb = KafkaBroker(boot, idempotent=True, connect_wait_s=10)
+    kb.RETRIES = 20
+    kb.create_topic("solo", 3)
+    for k in range(30):
+        kb.produce_raw("solo", k % 3, encode_record_batch([b"pre%d" % k]), acks=-1)
+    for victim in (2, 3):
+        os.killpg(c["procs"][f"b{victim}"].pid, signal.SIGKILL)
+        c["procs"][f"b{victim}"].wait(10)
+    deadline = time.time() + 30                          # every partition: leader 1, ISR [1]
+    while True:
+        md = json.loads(_text(f"http://127.0.0.1:{c['cport']}/metadata"))
+        ps = [v for k, v in md["parts"].items() if k.startswith("solo/")]
+        if all(v["leader"] == 1 and v["isr"] == [1] for v in ps):
+            break
+        assert time.time() < deadline, ps
+        time.sleep(0.1)
+    kb.close()
+    kb = KafkaBroker(f"127.0.0.1:{c['bports'][0]}", idempotent=True, connect_wait_s=10)
+    kb.RETRIES = 20
+    acked = []
+    for k in range(300):
+        vals = [b"solo-%d-%d" % (k, i) for i in range(20)]
+        kb.produce_raw("solo", k % 3, encode_record_batch(vals), acks=-1)
+        acked += vals
+    os.killpg(c["procs"]["b1"].pid, signal.SIGKILL)       # right after the last acknowledgement
+    c["procs"]["b1"].wait(10)
+    kb.close()
+    for k in (1, 2, 3):
+        c["start"](f"b{k}", c["broker_cmd"](k))
+    for p in c["bports"]:
+        _wait(p)
+    kb = KafkaBroker(boot, idempotent=True, connect_wait_s=10)
+    kb.RETRIES = 30
+    got = set()
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        got = set()
+        try:
+            for p in range(3):
+                off, end = 0, kb.end_offset("solo", p)
+                while off < end:
+                    _e, _hw, raw = kb.fetch_raw("solo", p, off)
+                    recs = [r for r in decode_record_batches(raw, "solo", p) if r.offset >= off]
+                    got.update(r.value for r in recs)
+                    off = recs[-1].offset + 1 if recs else end
+        except Exception:                                 # noqa: BLE001 -- leaders still moving
+            time.sleep(0.3)
+            continue
+        if all(v in got for v in acked):
+            break
+        time.sleep(0.3)
+    missing = [v for v in acked if v not in got]
+    assert not missing, (len(missing), missing[:5])
+    kb.close()

@@ -63,6 +63,13 @@ def test_cr_fields_drive_the_rendering():
     kafka = sts["spec"]["template"]["spec"]["containers"][0]
     assert sts["spec"]["replicas"] == 5 and [p["containerPort"] for p in kafka["ports"]] == [9092, 9404]
     assert "--controller" in kafka["command"] and ("StatefulSet", "odh-message-bus-kafka-controller") in by
+    # the controller is a 3-member replicated quorum (ZooKeeper's role); brokers know every member
+    ctl = by[("StatefulSet", "odh-message-bus-kafka-controller")]
+    cc = ctl["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert ctl["spec"]["replicas"] == 3 and ctl["spec"]["serviceName"] == "odh-message-bus-kafka-controller-members"
+    assert cc[cc.index("--member-id") + 1] == "auto" and cc[cc.index("--peers") + 1].count("=http://") == 3
+    assert kafka["command"][kafka["command"].index("--controller") + 1].count("http://") == 3
+    assert by[("Service", "odh-message-bus-kafka-controller-members")]["spec"]["clusterIP"] == "None"
     assert by[("Service", "odh-message-bus-kafka-brokers")]["spec"]["clusterIP"] == "None"
     d["spec"]["kafka"]["replicated"] = False                 # one pod with 5 listeners
     one = {(m["kind"], m["metadata"]["name"]): m for m in render(parse(d))}
@@ -306,25 +313,25 @@ def _free_offset(bases, tries=200):
 
 def test_local_operator_brings_up_a_working_kafka_cluster(tmp_path):
     """Only the CR's kafka section deployed: the operator starts the replicated kafka-lite
-    cluster (a controller + 3 broker processes) and a Kafka client produces to / fetches from
-    it through the bootstrap list."""
+    cluster (a 3-member controller quorum + 3 broker processes) and a Kafka client produces to /
+    fetches from it through the bootstrap list."""
     from ccfd_demo_summit_amd.ingest.kafka_wire import KafkaBroker
     d = _doc()
     for k in ("engine", "seldon", "usertask", "kie", "notifier", "producer", "monitoring"):
         d["spec"][k]["deploy"] = False
     d["spec"]["kafka"].update(brokers=3, partitions=6)
     spec = parse(d)
-    off = _free_offset([9092, 9093, 9094, 9404, 9405, 9406, 9290])   # parallel test workers: never a taken port
+    off = _free_offset([9092, 9093, 9094, 9404, 9405, 9406, 9290, 9291, 9292])   # parallel workers: never a taken port
     op = LocalOperator(spec, workdir=str(ROOT), commands=None, grace_s=5, log=lambda m: None, port_offset=off,
                        state_dir=str(tmp_path / "state"))
     try:
         t0 = time.time()
         while time.time() - t0 < 60:
             st = op.reconcile()
-            if st["kafka"]["ready"] == 3 and st["kafka-controller"]["ready"] == 1:
+            if st["kafka"]["ready"] == 3 and st["kafka-controller"]["ready"] == 3:
                 break
             time.sleep(0.5)
-        assert st["kafka"]["ready"] == 3 and st["kafka-controller"]["ready"] == 1
+        assert st["kafka"]["ready"] == 3 and st["kafka-controller"]["ready"] == 3
         bootstrap = ",".join(f"127.0.0.1:{9092 + off + i}" for i in range(3))
         kb = KafkaBroker(bootstrap, connect_wait_s=60.0)
         try:
