@@ -65,23 +65,13 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
   // per-item accumulators of this wave (flushed by item_flush)
   unsigned fraud = 0, rows = 0, stale = 0;
   unsigned long long psum = 0;
-  auto score_chunk = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, G32Row& cur)
+  // sigmoid, route, outputs, histogram and flag list of one scored 64-row chunk
+  auto chunk_epilogue = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, unsigned meta, float acc)
       __attribute__((always_inline)) {
-    gx_rows<kG20>(xt[wave], lane, cur);
-    unsigned b0[kF];
-    const unsigned meta = gx_lift<kG20>(cur, b0);
-    float acc[1];
-#ifdef CCFD_EXP_READ_ONLY
-    // experiment build only: the same items, loads, outputs and protocol with the trees replaced
-    // by a use of the bins -- what the persistent read + completion path alone sustains
-    acc[0] = (float)(b0[0] + b0[kF - 1]) * 1e-3f;
-#else
-    g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
-#endif
     const int row = chunk * kG32Rows + lane;
     const bool valid = row < n;
     const bool fresh = ((meta >> 8) & 0xffu) == stamp;
-    const float p = fresh ? sigmoid(base + acc[0]) : __builtin_nanf("");
+    const float p = fresh ? sigmoid(base + acc) : __builtin_nanf("");
     bool fr;
     if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
     else fr = valid && fresh && (p >= a.threshold);
@@ -98,6 +88,37 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
     rows += __popcll(__ballot(valid));
     stale += __popcll(__ballot(valid && !fresh));
     persist_emit_flagged(a, d, slot, m, fr, row, lane);
+  };
+  auto score_chunk = [&](const ccfd_persist_desc& d, int slot, int n, int chunk, G32Row& cur)
+      __attribute__((always_inline)) {
+    gx_rows<kG20>(xt[wave], lane, cur);
+    unsigned b0[kF];
+    const unsigned meta = gx_lift<kG20>(cur, b0);
+    float acc[1];
+#ifdef CCFD_EXP_READ_ONLY
+    // experiment build only: the same items, loads, outputs and protocol with the trees replaced
+    // by a use of the bins -- what the persistent read + completion path alone sustains
+    acc[0] = (float)(b0[0] + b0[kF - 1]) * 1e-3f;
+#else
+    g32_trees<D, 1>(b0, b0, leaves, feat, kbin, T, acc);
+#endif
+    chunk_epilogue(d, slot, n, chunk, meta, acc[0]);
+  };
+  // two chunks' rows walked through the trees together (one lane = two row chains): every
+  // split parameter's scalar load, feature select and leaf-table address serves two rows, and
+  // the two independent alignbit chains fill the issue slots one chain's dependencies leave
+  // empty (one wave per SIMD: nothing else hides them)
+  auto score_pair = [&](const ccfd_persist_desc& d, int slot, int n, int ch0, G32Row& r0, G32Row& r1)
+      __attribute__((always_inline)) {
+    gx_rows<kG20>(xt[wave], lane, r0);
+    gx_rows<kG20>(xt[wave], lane, r1);
+    unsigned b0[kF], b1[kF];
+    const unsigned m0 = gx_lift<kG20>(r0, b0);
+    const unsigned m1 = gx_lift<kG20>(r1, b1);
+    float acc[2];
+    g32_trees<D, 2>(b0, b1, leaves, feat, kbin, T, acc);
+    chunk_epilogue(d, slot, n, ch0, m0, acc[0]);
+    if ((ch0 + kW) * kG32Rows < n) chunk_epilogue(d, slot, n, ch0 + kW, m1, acc[1]);   // wave-uniform
   };
   auto item_flush = [&](const ccfd_persist_desc& d, int slot) __attribute__((always_inline)) {
     psum = wave_sum_u64(psum);
@@ -171,7 +192,13 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
         score_chunk(d, slot, n, chunk, r[k]);
       }
     };
-    if (a.flags & CCFD_ARG_CHUNK_RING) {                  // default: one chunk ahead
+    if ((a.flags & CCFD_ARG_PAIR_CHUNKS) && cpw == 2) {   // both chunks in flight, walked as a pair
+      G32Row r0, r1;
+      if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, r0);
+      if ((c0 + kW) * kG32Rows < n) gx_fetch<kG20>(xb, n, c0 + kW, lane, r1);
+      else r1 = r0;                                       // (a lone last chunk: b1 is never used)
+      if (c0 * kG32Rows < n) score_pair(d, slot, n, c0, r0, r1);
+    } else if (a.flags & CCFD_ARG_CHUNK_RING) {           // one chunk ahead
       G32Row pre;
       if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre);
 #pragma unroll 1
@@ -358,6 +385,7 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   // trees overlap the next chunk's load better); CCFD_G32_INFLIGHT=1 selects the latter.
   // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
   if (g32_env("CCFD_G32_INFLIGHT", 0, 0, 1) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
+  if (g32_env("CCFD_G32_PAIR", 0, 0, 1) == 1) a.flags |= CCFD_ARG_PAIR_CHUNKS;
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
   if (a.flags & CCFD_ARG_PIPE_ITEMS) {                    // pipelined static 512-row items
