@@ -1359,6 +1359,8 @@ def _main_replicated(a):
     if a.node_id <= 0:
         raise SystemExit("kafka-lite: replicated mode needs --node-id >= 1")
     sys.setswitchinterval(0.0005)
+    from ..utils.pyprof import install_from_env
+    install_from_env(f"kafka-lite-node{a.node_id}")          # CCFD_PYPROF=<dir>: cProfile of this broker
     from .kafka_wire import warm_native
     print(f"[kafka-lite] native codecs loaded in {warm_native():.2f} s", flush=True)
     br = ReplicatedBroker(a.node_id, a.controller, a.host, a.port, data_dir=a.data_dir, fsync=a.fsync,

@@ -377,6 +377,212 @@ __global__ __launch_bounds__(256) void persist_gbdt_pipe_kernel(ccfd_persist_arg
   }
 }
 
+
+// Wave-specialised G20 kernel (CCFD_ARG_LOADER).  In the claimed kernel
+// above every wave of a workgroup does everything in turn -- claim, descriptor, zero-copy
+// loads, trees, completion -- so an item's PCIe round trip and its tree walk add up.  Here a
+// workgroup is 4 SCORER waves + 1 LOADER wave around a ring of kSpecStages item buffers in LDS:
+//   * the loader claims the next 512-row item, reads its descriptor and loads the item's 10 KB
+//     of G20 rows (40 wave instructions, each one contiguous 256 B request, into 40 VGPRs); the
+//     claim of the following item goes out while those loads are in flight, then the rows are
+//     written into a free LDS stage and the stage is marked full;
+//   * the scorer waves read rows only from LDS (lane l of a chunk reads dwords 5l .. 5l+4 --
+//     stride 5, conflict-free, the transposed read of g20_rows), walk both of their chunks
+//     through the trees as a pair (R = 2), write outputs, and the LAST of the four to finish
+//     an item flushes its counters, releases at system scope, takes the ticket and frees the
+//     stage.  No workgroup barrier after start-up: stage states in LDS order the waves.
+// A stage: EMPTY (0) -> FULL (1, loader) -> EMPTY (last scorer) ..., or STOP (2): the host
+// stopped the kernel; scorers leave when they reach it, the loader has left already.
+constexpr int kSpecStages = 3;
+constexpr int kSpecItemRows = 512;                          // 4 scorer waves x 2 chunks of 64
+constexpr int kSpecStageWords = kSpecItemRows * kG20Words;  // 2560 dwords = 10 KB
+constexpr int kSpecLoads = kSpecStageWords / 64;            // 40 dword wave loads (VGPRs)
+
+struct SpecStage {
+  ccfd_persist_desc d;
+  unsigned long long item;
+  int state;
+  unsigned done;
+  unsigned fraud, rows, stale;
+  unsigned long long psum;
+  unsigned hist[2 * kNB];
+};
+
+template <int D, bool kR>
+__global__ __launch_bounds__(320) void persist_g20_spec_kernel(ccfd_persist_args a) {
+  extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L leaf floats
+  __shared__ __attribute__((aligned(16))) unsigned sdata[kSpecStages][kSpecStageWords];
+  __shared__ SpecStage st[kSpecStages];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int C = a.items_per_batch;
+  if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
+    if (wave == 0) persist_doorbell(a, lane);
+    return;
+  }
+  const char* blob = reinterpret_cast<const char*>(a.blob);
+  const int T = a.gbdt_trees;
+  g32_stage_leaves<D>(blob, T, lv, tid, 320);
+  if (tid < kSpecStages) {
+    SpecStage& z = st[tid];
+    z.state = 0; z.done = 0; z.fraud = 0; z.rows = 0; z.stale = 0; z.psum = 0;
+    for (int i = 0; i < 2 * kNB; ++i) z.hist[i] = 0;
+  }
+  __syncthreads();                                        // the only workgroup barrier
+
+  if (wave == 4) {
+    // ------------------------------------------------------------------ loader wave
+    unsigned long long posted_cache = 0;                  // lane 0 only
+    int pending = -1;                                     // stage whose rows are in v[] (in flight)
+    unsigned v[kSpecLoads];                               // lane l: dwords l + 64 i of that item
+    for (unsigned long long k = 0;; ++k) {
+      const int s = (int)(k % kSpecStages);
+      unsigned long long item = 0;
+      if (lane == 0)
+        item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pending >= 0) {                                 // the claim went out behind those loads
+#pragma unroll
+        for (int i = 0; i < kSpecLoads; ++i) sdata[pending][64 * i + lane] = v[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&st[pending].state, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      pending = -1;
+      int stop = 0;
+      for (unsigned spin = 0; __hip_atomic_load(&st[s].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+           ++spin) {                                      // the scorers still read this stage
+        __builtin_amdgcn_s_sleep(1);
+        if ((spin & 255) == 255 && __hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          stop = 1;
+          break;
+        }
+      }
+      if (stop) break;
+      int cmd = 0;
+      if (lane == 0) {
+        cmd = persist_wait_item(a, C, posted_cache, item, st[s].d);
+        st[s].item = item;
+        if (cmd) __hip_atomic_store(&st[s].state, 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else if (item % (unsigned long long)C == 0)      // K7: micro-batch start
+          __hip_atomic_store(&a.dev->tstart[st[s].d.seq % (unsigned long long)a.ring], wall_clock64(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (__shfl(cmd, 0)) break;
+      item = __shfl(item, 0);                             // the claim was lane 0's
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const unsigned* xw = reinterpret_cast<const unsigned*>(st[s].d.x);
+      const int n = st[s].d.n;
+      const long first = (long)(item % (unsigned long long)C) * kSpecStageWords;
+      const long last = (long)n * kG20Words - 1;          // dwords past the batch: clamped, never scored
+#pragma unroll
+      for (int i = 0; i < kSpecLoads; ++i) v[i] = ld_g(xw + min(first + 64 * i + lane, last));
+      pending = s;
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------------- scorer waves 0..3
+  const float base = *reinterpret_cast<const float*>(blob + 16);
+  const unsigned stamp = (unsigned)*reinterpret_cast<const int*>(blob + 20);
+  const int tdw = ((4 * T * D + 15) & ~15) / 4;
+  const g32_cint_p feat = (g32_cint_p)(blob + kHeader);
+  const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
+  for (unsigned long long k = 0;; ++k) {
+    const int s = (int)(k % kSpecStages);
+    int state;
+    bool stopped = false;
+    for (unsigned spin = 0;
+         (state = __hip_atomic_load(&st[s].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0; ++spin) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((spin & 255) == 255 && __hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        stopped = true;                                   // never left waiting at teardown
+        break;
+      }
+    }
+    if (stopped || state == 2) break;
+    const ccfd_persist_desc d = st[s].d;
+    const unsigned long long item = st[s].item;
+    const int slot = (int)(d.seq % (unsigned long long)a.ring);
+    const int n = d.n;
+    const int rbase = (int)(item % (unsigned long long)C) * kSpecItemRows;
+    // this wave's chunks: wave and wave + 4 of the item's 8
+    G32Row r0, r1;
+    {
+      const unsigned* q0 = &sdata[s][(wave * kG32Rows + lane) * kG20Words];
+      const unsigned* q1 = &sdata[s][((wave + 4) * kG32Rows + lane) * kG20Words];
+      r0.lo = make_uint4(q0[0], q0[1], q0[2], q0[3]); r0.hi.x = q0[4];
+      r1.lo = make_uint4(q1[0], q1[1], q1[2], q1[3]); r1.hi.x = q1[4];
+      r0.hi.y = r0.hi.z = r0.hi.w = 0; r1.hi.y = r1.hi.z = r1.hi.w = 0;
+    }
+    unsigned b0[kF], b1[kF];
+    const unsigned m0 = g20_lift(r0, b0);
+    const unsigned m1 = g20_lift(r1, b1);
+    float acc[2];
+    g32_trees<D, 2>(b0, b1, lv, feat, kbin, T, acc);
+    unsigned fraud = 0, rows = 0, stale = 0;
+    unsigned long long psum = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = rbase + (wave + 4 * h) * kG32Rows + lane;
+      if (rbase + (wave + 4 * h) * kG32Rows >= n) break;  // wave-uniform
+      const unsigned meta = h ? m1 : m0;
+      const bool valid = row < n;
+      const bool fresh = ((meta >> 8) & 0xffu) == stamp;
+      const float p = fresh ? sigmoid(base + acc[h]) : __builtin_nanf("");
+      bool fr;
+      if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
+      else fr = valid && fresh && (p >= a.threshold);
+      if (valid) {
+        if (d.proba) st_g(d.proba + row, p);
+        if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
+        if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
+        atomicAdd(&st[s].hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
+      }
+      const unsigned long long m = __ballot(fr);
+      fraud += __popcll(m);
+      rows += __popcll(__ballot(valid));
+      stale += __popcll(__ballot(valid && !fresh));
+      persist_emit_flagged(a, d, slot, m, fr, row, lane);
+    }
+    psum = wave_sum_u64(psum);
+    if (lane == 0) {
+      atomicAdd(&st[s].fraud, fraud);
+      atomicAdd(&st[s].rows, rows);
+      atomicAdd(&st[s].stale, stale);
+      atomicAdd(&st[s].psum, psum);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this wave's outputs and LDS sums are done
+    unsigned old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&st[s].done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__shfl(old, 0) != 3) continue;                    // not the item's last scorer
+    // last scorer of the item: its counters into the epoch buffer, release, ticket, free the stage
+    unsigned long long* cnt = a.counters[d.epoch & 1];
+    if (lane < 2 * kNB) {
+      const unsigned hv = st[s].hist[lane];
+      if (hv && cnt) atomicAdd(&cnt[(lane < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + lane],
+                               (unsigned long long)hv);
+      st[s].hist[lane] = 0;
+    }
+    if (lane == 32 && cnt) {
+      const unsigned rr = st[s].rows, ff = st[s].fraud, ss = st[s].stale;
+      if (rr) {
+        atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)rr);
+        atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)ff);
+        atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(rr - ff));
+        atomicAdd(&cnt[CCFD_CNT_PROBA_E6], st[s].psum);
+      }
+      if (ss) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)ss);
+    }
+    if (lane == 32) { st[s].rows = 0; st[s].fraud = 0; st[s].stale = 0; st[s].psum = 0; st[s].done = 0; }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      persist_ticket(a, d, slot, C);
+      __hip_atomic_store(&st[s].state, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+
 template <int D, bool kG20>
 static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream_t s) {
   ccfd_persist_args a = a0;
@@ -388,6 +594,14 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   if (g32_env("CCFD_G32_PAIR", 0, 0, 1) == 1) a.flags |= CCFD_ARG_PAIR_CHUNKS;
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
+  if constexpr (kG20) {
+    if (g32_env("CCFD_G32_LOADER", 0, 0, 1) == 1 && !gl && a.tiles_per_wave == 2) {   // wave-specialised
+      a.flags |= CCFD_ARG_LOADER;
+      if (a.rules) hipLaunchKernelGGL((persist_g20_spec_kernel<D, true>), dim3(grid), dim3(320), lds, s, a);
+      else hipLaunchKernelGGL((persist_g20_spec_kernel<D, false>), dim3(grid), dim3(320), lds, s, a);
+      return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+  }
   if (a.flags & CCFD_ARG_PIPE_ITEMS) {                    // pipelined static 512-row items
     if (gl || a.tiles_per_wave != 2 || grid < 2) return -2;
     if (a.rules) hipLaunchKernelGGL((persist_gbdt_pipe_kernel<D, true, kG20, 2>), dim3(grid), dim3(256), lds, s, a);
