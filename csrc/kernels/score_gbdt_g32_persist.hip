@@ -381,7 +381,8 @@ __global__ __launch_bounds__(256) void persist_gbdt_pipe_kernel(ccfd_persist_arg
 // Wave-specialised G20 kernel (CCFD_ARG_LOADER).  In the claimed kernel
 // above every wave of a workgroup does everything in turn -- claim, descriptor, zero-copy
 // loads, trees, completion -- so an item's PCIe round trip and its tree walk add up.  Here a
-// workgroup is 4 SCORER waves + 1 LOADER wave around a ring of kSpecStages item buffers in LDS:
+// workgroup is 4 SCORER waves + kSpecLoaders LOADER waves around a ring of kSpecStages item
+// buffers in LDS:
 //   * the loader claims the next 512-row item, reads its descriptor and loads the item's 10 KB
 //     of G20 rows (40 wave instructions, each one contiguous 256 B request, into 40 VGPRs); the
 //     claim of the following item goes out while those loads are in flight, then the rows are
@@ -390,18 +391,28 @@ __global__ __launch_bounds__(256) void persist_gbdt_pipe_kernel(ccfd_persist_arg
 //     stride 5, conflict-free, the transposed read of g20_rows), walk both of their chunks
 //     through the trees as a pair (R = 2), write outputs, and the LAST of the four to finish
 //     an item flushes its counters, releases at system scope, takes the ticket and frees the
-//     stage.  No workgroup barrier after start-up: stage states in LDS order the waves.
-// A stage: EMPTY (0) -> FULL (1, loader) -> EMPTY (last scorer) ..., or STOP (2): the host
-// stopped the kernel; scorers leave when they reach it, the loader has left already.
-constexpr int kSpecStages = 3;
+//     stage.  No workgroup barrier after start-up: stage generations in LDS order the waves.
+// Stage handshake by GENERATION, never by a bare full / empty flag: item k of the loader's
+// sequence goes to stage k % kSpecStages; the loader publishes full[s] = k + 1 once its rows
+// are in LDS, the last scorer publishes freed[s] = k + 1 when it is done, and the loader reuses
+// the stage for item k + kSpecStages only then.  Each scorer wave waits for full[s] == k + 1
+// exactly: a flag would let a fast scorer wave lap a slow one (three items ahead, it sees the
+// stage still "full" with the slow wave's item and scores it twice -- a lost ticket, a hung
+// batch).  full[s] = kSpecStop: the host stopped the kernel.
+constexpr int kSpecLoaders = 2;                             // loader waves: 2 items in flight a workgroup
+constexpr int kSpecStages = 2 * kSpecLoaders;               // loader j fills stages j, j + kSpecLoaders
+constexpr int kSpecThreads = 64 * (4 + kSpecLoaders);
 constexpr int kSpecItemRows = 512;                          // 4 scorer waves x 2 chunks of 64
 constexpr int kSpecStageWords = kSpecItemRows * kG20Words;  // 2560 dwords = 10 KB
 constexpr int kSpecLoads = kSpecStageWords / 64;            // 40 dword wave loads (VGPRs)
 
+constexpr unsigned kSpecStop = 0xffffffffu;
+
 struct SpecStage {
   ccfd_persist_desc d;
   unsigned long long item;
-  int state;
+  unsigned full;                                            // generation published by the loader
+  unsigned freed;                                           // generation released by the last scorer
   unsigned done;
   unsigned fraud, rows, stale;
   unsigned long long psum;
@@ -409,10 +420,11 @@ struct SpecStage {
 };
 
 template <int D, bool kR>
-__global__ __launch_bounds__(320) void persist_g20_spec_kernel(ccfd_persist_args a) {
+__global__ __launch_bounds__(kSpecThreads) void persist_g20_spec_kernel(ccfd_persist_args a) {
   extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L leaf floats
   __shared__ __attribute__((aligned(16))) unsigned sdata[kSpecStages][kSpecStageWords];
   __shared__ SpecStage st[kSpecStages];
+  __shared__ unsigned s_turn;                               // next sequence number allowed to claim
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -424,33 +436,52 @@ __global__ __launch_bounds__(320) void persist_g20_spec_kernel(ccfd_persist_args
   }
   const char* blob = reinterpret_cast<const char*>(a.blob);
   const int T = a.gbdt_trees;
-  g32_stage_leaves<D>(blob, T, lv, tid, 320);
+  g32_stage_leaves<D>(blob, T, lv, tid, kSpecThreads);
   if (tid < kSpecStages) {
     SpecStage& z = st[tid];
-    z.state = 0; z.done = 0; z.fraud = 0; z.rows = 0; z.stale = 0; z.psum = 0;
+    z.full = 0; z.freed = 0; z.done = 0; z.fraud = 0; z.rows = 0; z.stale = 0; z.psum = 0;
     for (int i = 0; i < 2 * kNB; ++i) z.hist[i] = 0;
   }
+  if (tid == 0) s_turn = 0;
   __syncthreads();                                        // the only workgroup barrier
 
-  if (wave == 4) {
-    // ------------------------------------------------------------------ loader wave
+  if (wave >= 4) {
+    // ------------------------------------------------------------------ loader waves
+    // loader j fills items j, j + L, j + 2L, ... of the workgroup's sequence (L loaders), one
+    // item's rows in flight each: the vmcnt a claim's value waits for drains every earlier load
+    // of the wave, so one wave cannot keep two items in flight past its next claim
+    const int lj = wave - 4;
     unsigned long long posted_cache = 0;                  // lane 0 only
     int pending = -1;                                     // stage whose rows are in v[] (in flight)
     unsigned v[kSpecLoads];                               // lane l: dwords l + 64 i of that item
-    for (unsigned long long k = 0;; ++k) {
+    for (unsigned long long k = lj;; k += kSpecLoaders) {
       const int s = (int)(k % kSpecStages);
+      // claims go out in sequence order (loaders take turns): a workgroup's items then ascend
+      // with k, so its scorers -- who take them in k order -- never wait on an item of a later,
+      // unposted micro-batch ahead of one an earlier batch needs (that ordering is what keeps
+      // the host's batches completing)
+      while (__hip_atomic_load(&s_turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned)k)
+        __builtin_amdgcn_s_sleep(1);
       unsigned long long item = 0;
-      if (lane == 0)
+      if (lane == 0) {
         item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s_turn, (unsigned)k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       if (pending >= 0) {                                 // the claim went out behind those loads
 #pragma unroll
         for (int i = 0; i < kSpecLoads; ++i) sdata[pending][64 * i + lane] = v[i];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&st[pending].state, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0)
+          __hip_atomic_store(&st[pending].full, (unsigned)(k - kSpecLoaders) + 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);                         // item k - L
       }
       pending = -1;
       int stop = 0;
-      for (unsigned spin = 0; __hip_atomic_load(&st[s].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+      // item k - kSpecStages (this stage's previous use) must be released: freed >= k - NS + 1
+      const unsigned need = (unsigned)k - (unsigned)kSpecStages + 1u;
+      for (unsigned spin = 0;
+           k >= (unsigned long long)kSpecStages &&
+           (int)(__hip_atomic_load(&st[s].freed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - need) < 0;
            ++spin) {                                      // the scorers still read this stage
         __builtin_amdgcn_s_sleep(1);
         if ((spin & 255) == 255 && __hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -463,7 +494,7 @@ __global__ __launch_bounds__(320) void persist_g20_spec_kernel(ccfd_persist_args
       if (lane == 0) {
         cmd = persist_wait_item(a, C, posted_cache, item, st[s].d);
         st[s].item = item;
-        if (cmd) __hip_atomic_store(&st[s].state, 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cmd) __hip_atomic_store(&st[s].full, kSpecStop, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         else if (item % (unsigned long long)C == 0)      // K7: micro-batch start
           __hip_atomic_store(&a.dev->tstart[st[s].d.seq % (unsigned long long)a.ring], wall_clock64(),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -490,17 +521,19 @@ __global__ __launch_bounds__(320) void persist_g20_spec_kernel(ccfd_persist_args
   const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
   for (unsigned long long k = 0;; ++k) {
     const int s = (int)(k % kSpecStages);
-    int state;
+    const unsigned gen = (unsigned)k + 1u;
+    unsigned f;
     bool stopped = false;
     for (unsigned spin = 0;
-         (state = __hip_atomic_load(&st[s].state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0; ++spin) {
+         (f = __hip_atomic_load(&st[s].full, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != gen && f != kSpecStop;
+         ++spin) {
       __builtin_amdgcn_s_sleep(1);
       if ((spin & 255) == 255 && __hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         stopped = true;                                   // never left waiting at teardown
         break;
       }
     }
-    if (stopped || state == 2) break;
+    if (stopped || f == kSpecStop) break;
     const ccfd_persist_desc d = st[s].d;
     const unsigned long long item = st[s].item;
     const int slot = (int)(d.seq % (unsigned long long)a.ring);
@@ -578,7 +611,7 @@ __global__ __launch_bounds__(320) void persist_g20_spec_kernel(ccfd_persist_args
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if (lane == 0) {
       persist_ticket(a, d, slot, C);
-      __hip_atomic_store(&st[s].state, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&st[s].freed, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
 }
@@ -597,8 +630,8 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   if constexpr (kG20) {
     if (g32_env("CCFD_G32_LOADER", 0, 0, 1) == 1 && !gl && a.tiles_per_wave == 2) {   // wave-specialised
       a.flags |= CCFD_ARG_LOADER;
-      if (a.rules) hipLaunchKernelGGL((persist_g20_spec_kernel<D, true>), dim3(grid), dim3(320), lds, s, a);
-      else hipLaunchKernelGGL((persist_g20_spec_kernel<D, false>), dim3(grid), dim3(320), lds, s, a);
+      if (a.rules) hipLaunchKernelGGL((persist_g20_spec_kernel<D, true>), dim3(grid), dim3(kSpecThreads), lds, s, a);
+      else hipLaunchKernelGGL((persist_g20_spec_kernel<D, false>), dim3(grid), dim3(kSpecThreads), lds, s, a);
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }
   }
