@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void persist_gbdt_pipe_kernel(ccfd_persist_arg
 // exactly: a flag would let a fast scorer wave lap a slow one (three items ahead, it sees the
 // stage still "full" with the slow wave's item and scores it twice -- a lost ticket, a hung
 // batch).  full[s] = kSpecStop: the host stopped the kernel.
-constexpr int kSpecLoaders = 2;                             // loader waves: 2 items in flight a workgroup
+constexpr int kSpecLoaders = 1;                             // loader waves (each: one item's rows in flight)
 constexpr int kSpecStages = 2 * kSpecLoaders;               // loader j fills stages j, j + kSpecLoaders
 constexpr int kSpecThreads = 64 * (4 + kSpecLoaders);
 constexpr int kSpecItemRows = 512;                          // 4 scorer waves x 2 chunks of 64
@@ -456,28 +456,19 @@ __global__ __launch_bounds__(kSpecThreads) void persist_g20_spec_kernel(ccfd_per
     unsigned v[kSpecLoads];                               // lane l: dwords l + 64 i of that item
     for (unsigned long long k = lj;; k += kSpecLoaders) {
       const int s = (int)(k % kSpecStages);
-      // claims go out in sequence order (loaders take turns): a workgroup's items then ascend
-      // with k, so its scorers -- who take them in k order -- never wait on an item of a later,
-      // unposted micro-batch ahead of one an earlier batch needs (that ordering is what keeps
-      // the host's batches completing)
-      while (__hip_atomic_load(&s_turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned)k)
-        __builtin_amdgcn_s_sleep(1);
-      unsigned long long item = 0;
-      if (lane == 0) {
-        item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&s_turn, (unsigned)k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (pending >= 0) {                                 // the claim went out behind those loads
+      if (pending >= 0) {                                 // item k - L: its rows are back -> LDS
 #pragma unroll
         for (int i = 0; i < kSpecLoads; ++i) sdata[pending][64 * i + lane] = v[i];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0)
           __hip_atomic_store(&st[pending].full, (unsigned)(k - kSpecLoaders) + 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);                         // item k - L
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       pending = -1;
       int stop = 0;
-      // item k - kSpecStages (this stage's previous use) must be released: freed >= k - NS + 1
+      // claim only once this stage's previous item (k - NS) is released: a workgroup never
+      // holds more than NS claimed items, so a micro-batch's last items do not queue behind
+      // others (claim-ahead raised the batch latency, and at a fixed ring depth the rate with it)
       const unsigned need = (unsigned)k - (unsigned)kSpecStages + 1u;
       for (unsigned spin = 0;
            k >= (unsigned long long)kSpecStages &&
@@ -490,6 +481,17 @@ __global__ __launch_bounds__(kSpecThreads) void persist_g20_spec_kernel(ccfd_per
         }
       }
       if (stop) break;
+      // claims go out in sequence order (loaders take turns): a workgroup's items then ascend
+      // with k, so its scorers -- who take them in k order -- never wait on an item of a later,
+      // unposted micro-batch ahead of one an earlier batch needs (that ordering is what keeps
+      // the host's batches completing)
+      while (__hip_atomic_load(&s_turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned)k)
+        __builtin_amdgcn_s_sleep(1);
+      unsigned long long item = 0;
+      if (lane == 0) {
+        item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&s_turn, (unsigned)k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       int cmd = 0;
       if (lane == 0) {
         cmd = persist_wait_item(a, C, posted_cache, item, st[s].d);

@@ -9,7 +9,7 @@ st pytest loader
 CCFD_G32_LOADER=1 timeout -k 10 300 python -u -m pytest tests/test_gbdt_g20_gpu.py tests/test_handoff_lossless_gpu.py \
   -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_loader.log 2>&1 || { tail -40 $O/pytest_loader.log; exit 1; }
 tail -1 $O/pytest_loader.log
-for v in loader loader256 base loader128; do
+for v in loader base loader256; do
   g=0
   case $v in base) e="CCFD_G32_LOADER=0";; loader) e="CCFD_G32_LOADER=1";; loader256) e="CCFD_G32_LOADER=1"; g=256;;
     loader128) e="CCFD_G32_LOADER=1"; g=128;; esac
