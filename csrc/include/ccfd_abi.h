@@ -47,8 +47,6 @@ enum ccfd_counter_slot {
 #define CCFD_G20_ROW_BYTES 20
 #define CCFD_G20_MAX_EDGES 31
 #define CCFD_ARG_CHUNK_RING 128       // persistent G32: one-chunk prefetch ring (default) instead of the whole item in flight
-#define CCFD_ARG_PAIR_CHUNKS 2048     // persistent G32/G20, 2 chunks a wave: both in flight, walked through the trees together
-#define CCFD_ARG_LOADER 4096          // persistent G20: wave-specialised (a loader wave fills LDS stages, 4 scorer waves)
 #define CCFD_ARG_FLAG_DIRECT 1024      // W64 launch kernels: reserve flag-list slots per ballot (A/B of the LDS staging)
 #define CCFD_ARG_PIPE_ITEMS 256       // persistent W64 MLP: statically assigned 64/128-row items, the next
                                       // item's rows fetched while the current one is scored

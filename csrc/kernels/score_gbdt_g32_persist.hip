@@ -3,6 +3,14 @@
 // are staged into LDS ONCE per resident workgroup (a launch per micro-batch re-stages them
 // in every workgroup), and a claimed item is 4 waves x `cpw` 64-row chunks, the next chunk
 // of a wave in flight while the current one is evaluated.
+//
+// Measured against it in round 6 (config 4, depth 4; profiles/r6/pass_c, pass_d; the code is
+// in commit 95a7cf0): both chunks of a wave walked through the trees as a pair (R = 2: two
+// row chains a lane) 2.540 vs 2.545e9 tx/s -- the tree walk's ILP is not the limit; a
+// wave-specialised workgroup (a loader wave filling LDS item stages, 4 scorer waves reading
+// only LDS) 1.78-2.05e9 in every variant (claim-ahead, two loaders, double-buffered without
+// claim-ahead): queued items raise the micro-batch latency, and at a fixed ring depth the
+// rate falls with it (Little's law: 4 x 65536 rows / batch latency).
 #include <cstdio>
 #include <vector>
 
@@ -104,22 +112,6 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
 #endif
     chunk_epilogue(d, slot, n, chunk, meta, acc[0]);
   };
-  // two chunks' rows walked through the trees together (one lane = two row chains): every
-  // split parameter's scalar load, feature select and leaf-table address serves two rows, and
-  // the two independent alignbit chains fill the issue slots one chain's dependencies leave
-  // empty (one wave per SIMD: nothing else hides them)
-  auto score_pair = [&](const ccfd_persist_desc& d, int slot, int n, int ch0, G32Row& r0, G32Row& r1)
-      __attribute__((always_inline)) {
-    gx_rows<kG20>(xt[wave], lane, r0);
-    gx_rows<kG20>(xt[wave], lane, r1);
-    unsigned b0[kF], b1[kF];
-    const unsigned m0 = gx_lift<kG20>(r0, b0);
-    const unsigned m1 = gx_lift<kG20>(r1, b1);
-    float acc[2];
-    g32_trees<D, 2>(b0, b1, leaves, feat, kbin, T, acc);
-    chunk_epilogue(d, slot, n, ch0, m0, acc[0]);
-    if ((ch0 + kW) * kG32Rows < n) chunk_epilogue(d, slot, n, ch0 + kW, m1, acc[1]);   // wave-uniform
-  };
   auto item_flush = [&](const ccfd_persist_desc& d, int slot) __attribute__((always_inline)) {
     psum = wave_sum_u64(psum);
     if (lane == 0 && rows) {
@@ -192,13 +184,7 @@ __global__ __launch_bounds__(64 * kW) void persist_gbdt_g32_kernel(ccfd_persist_
         score_chunk(d, slot, n, chunk, r[k]);
       }
     };
-    if ((a.flags & CCFD_ARG_PAIR_CHUNKS) && cpw == 2) {   // both chunks in flight, walked as a pair
-      G32Row r0, r1;
-      if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, r0);
-      if ((c0 + kW) * kG32Rows < n) gx_fetch<kG20>(xb, n, c0 + kW, lane, r1);
-      else r1 = r0;                                       // (a lone last chunk: b1 is never used)
-      if (c0 * kG32Rows < n) score_pair(d, slot, n, c0, r0, r1);
-    } else if (a.flags & CCFD_ARG_CHUNK_RING) {           // one chunk ahead
+    if (a.flags & CCFD_ARG_CHUNK_RING) {                  // default: one chunk ahead
       G32Row pre;
       if (c0 * kG32Rows < n) gx_fetch<kG20>(xb, n, c0, lane, pre);
 #pragma unroll 1
@@ -378,246 +364,6 @@ __global__ __launch_bounds__(256) void persist_gbdt_pipe_kernel(ccfd_persist_arg
 }
 
 
-// Wave-specialised G20 kernel (CCFD_ARG_LOADER).  In the claimed kernel
-// above every wave of a workgroup does everything in turn -- claim, descriptor, zero-copy
-// loads, trees, completion -- so an item's PCIe round trip and its tree walk add up.  Here a
-// workgroup is 4 SCORER waves + kSpecLoaders LOADER waves around a ring of kSpecStages item
-// buffers in LDS:
-//   * the loader claims the next 512-row item, reads its descriptor and loads the item's 10 KB
-//     of G20 rows (40 wave instructions, each one contiguous 256 B request, into 40 VGPRs); the
-//     claim of the following item goes out while those loads are in flight, then the rows are
-//     written into a free LDS stage and the stage is marked full;
-//   * the scorer waves read rows only from LDS (lane l of a chunk reads dwords 5l .. 5l+4 --
-//     stride 5, conflict-free, the transposed read of g20_rows), walk both of their chunks
-//     through the trees as a pair (R = 2), write outputs, and the LAST of the four to finish
-//     an item flushes its counters, releases at system scope, takes the ticket and frees the
-//     stage.  No workgroup barrier after start-up: stage generations in LDS order the waves.
-// Stage handshake by GENERATION, never by a bare full / empty flag: item k of the loader's
-// sequence goes to stage k % kSpecStages; the loader publishes full[s] = k + 1 once its rows
-// are in LDS, the last scorer publishes freed[s] = k + 1 when it is done, and the loader reuses
-// the stage for item k + kSpecStages only then.  Each scorer wave waits for full[s] == k + 1
-// exactly: a flag would let a fast scorer wave lap a slow one (three items ahead, it sees the
-// stage still "full" with the slow wave's item and scores it twice -- a lost ticket, a hung
-// batch).  full[s] = kSpecStop: the host stopped the kernel.
-constexpr int kSpecLoaders = 1;                             // loader waves (each: one item's rows in flight)
-constexpr int kSpecStages = 2 * kSpecLoaders;               // loader j fills stages j, j + kSpecLoaders
-constexpr int kSpecThreads = 64 * (4 + kSpecLoaders);
-constexpr int kSpecItemRows = 512;                          // 4 scorer waves x 2 chunks of 64
-constexpr int kSpecStageWords = kSpecItemRows * kG20Words;  // 2560 dwords = 10 KB
-constexpr int kSpecLoads = kSpecStageWords / 64;            // 40 dword wave loads (VGPRs)
-
-constexpr unsigned kSpecStop = 0xffffffffu;
-
-struct SpecStage {
-  ccfd_persist_desc d;
-  unsigned long long item;
-  unsigned full;                                            // generation published by the loader
-  unsigned freed;                                           // generation released by the last scorer
-  unsigned done;
-  unsigned fraud, rows, stale;
-  unsigned long long psum;
-  unsigned hist[2 * kNB];
-};
-
-template <int D, bool kR>
-__global__ __launch_bounds__(kSpecThreads) void persist_g20_spec_kernel(ccfd_persist_args a) {
-  extern __shared__ __attribute__((aligned(16))) float lv[];   // T * L leaf floats
-  __shared__ __attribute__((aligned(16))) unsigned sdata[kSpecStages][kSpecStageWords];
-  __shared__ SpecStage st[kSpecStages];
-  __shared__ unsigned s_turn;                               // next sequence number allowed to claim
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int C = a.items_per_batch;
-  if (blockIdx.x == 0) {                                  // doorbell (persist_core.h)
-    if (wave == 0) persist_doorbell(a, lane);
-    return;
-  }
-  const char* blob = reinterpret_cast<const char*>(a.blob);
-  const int T = a.gbdt_trees;
-  g32_stage_leaves<D>(blob, T, lv, tid, kSpecThreads);
-  if (tid < kSpecStages) {
-    SpecStage& z = st[tid];
-    z.full = 0; z.freed = 0; z.done = 0; z.fraud = 0; z.rows = 0; z.stale = 0; z.psum = 0;
-    for (int i = 0; i < 2 * kNB; ++i) z.hist[i] = 0;
-  }
-  if (tid == 0) s_turn = 0;
-  __syncthreads();                                        // the only workgroup barrier
-
-  if (wave >= 4) {
-    // ------------------------------------------------------------------ loader waves
-    // loader j fills items j, j + L, j + 2L, ... of the workgroup's sequence (L loaders), one
-    // item's rows in flight each: the vmcnt a claim's value waits for drains every earlier load
-    // of the wave, so one wave cannot keep two items in flight past its next claim
-    const int lj = wave - 4;
-    unsigned long long posted_cache = 0;                  // lane 0 only
-    int pending = -1;                                     // stage whose rows are in v[] (in flight)
-    unsigned v[kSpecLoads];                               // lane l: dwords l + 64 i of that item
-    for (unsigned long long k = lj;; k += kSpecLoaders) {
-      const int s = (int)(k % kSpecStages);
-      if (pending >= 0) {                                 // item k - L: its rows are back -> LDS
-#pragma unroll
-        for (int i = 0; i < kSpecLoads; ++i) sdata[pending][64 * i + lane] = v[i];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0)
-          __hip_atomic_store(&st[pending].full, (unsigned)(k - kSpecLoaders) + 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      pending = -1;
-      int stop = 0;
-      // claim only once this stage's previous item (k - NS) is released: a workgroup never
-      // holds more than NS claimed items, so a micro-batch's last items do not queue behind
-      // others (claim-ahead raised the batch latency, and at a fixed ring depth the rate with it)
-      const unsigned need = (unsigned)k - (unsigned)kSpecStages + 1u;
-      for (unsigned spin = 0;
-           k >= (unsigned long long)kSpecStages &&
-           (int)(__hip_atomic_load(&st[s].freed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - need) < 0;
-           ++spin) {                                      // the scorers still read this stage
-        __builtin_amdgcn_s_sleep(1);
-        if ((spin & 255) == 255 && __hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          stop = 1;
-          break;
-        }
-      }
-      if (stop) break;
-      // claims go out in sequence order (loaders take turns): a workgroup's items then ascend
-      // with k, so its scorers -- who take them in k order -- never wait on an item of a later,
-      // unposted micro-batch ahead of one an earlier batch needs (that ordering is what keeps
-      // the host's batches completing)
-      while (__hip_atomic_load(&s_turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned)k)
-        __builtin_amdgcn_s_sleep(1);
-      unsigned long long item = 0;
-      if (lane == 0) {
-        item = __hip_atomic_fetch_add(&a.dev->work_next, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&s_turn, (unsigned)k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      int cmd = 0;
-      if (lane == 0) {
-        cmd = persist_wait_item(a, C, posted_cache, item, st[s].d);
-        st[s].item = item;
-        if (cmd) __hip_atomic_store(&st[s].full, kSpecStop, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else if (item % (unsigned long long)C == 0)      // K7: micro-batch start
-          __hip_atomic_store(&a.dev->tstart[st[s].d.seq % (unsigned long long)a.ring], wall_clock64(),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (__shfl(cmd, 0)) break;
-      item = __shfl(item, 0);                             // the claim was lane 0's
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      const unsigned* xw = reinterpret_cast<const unsigned*>(st[s].d.x);
-      const int n = st[s].d.n;
-      const long first = (long)(item % (unsigned long long)C) * kSpecStageWords;
-      const long last = (long)n * kG20Words - 1;          // dwords past the batch: clamped, never scored
-#pragma unroll
-      for (int i = 0; i < kSpecLoads; ++i) v[i] = ld_g(xw + min(first + 64 * i + lane, last));
-      pending = s;
-    }
-    return;
-  }
-
-  // -------------------------------------------------------------------- scorer waves 0..3
-  const float base = *reinterpret_cast<const float*>(blob + 16);
-  const unsigned stamp = (unsigned)*reinterpret_cast<const int*>(blob + 20);
-  const int tdw = ((4 * T * D + 15) & ~15) / 4;
-  const g32_cint_p feat = (g32_cint_p)(blob + kHeader);
-  const g32_cint_p kbin = (g32_cint_p)(blob + kHeader + 4 * tdw);
-  for (unsigned long long k = 0;; ++k) {
-    const int s = (int)(k % kSpecStages);
-    const unsigned gen = (unsigned)k + 1u;
-    unsigned f;
-    bool stopped = false;
-    for (unsigned spin = 0;
-         (f = __hip_atomic_load(&st[s].full, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != gen && f != kSpecStop;
-         ++spin) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((spin & 255) == 255 && __hip_atomic_load(&a.dev->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        stopped = true;                                   // never left waiting at teardown
-        break;
-      }
-    }
-    if (stopped || f == kSpecStop) break;
-    const ccfd_persist_desc d = st[s].d;
-    const unsigned long long item = st[s].item;
-    const int slot = (int)(d.seq % (unsigned long long)a.ring);
-    const int n = d.n;
-    const int rbase = (int)(item % (unsigned long long)C) * kSpecItemRows;
-    // this wave's chunks: wave and wave + 4 of the item's 8
-    G32Row r0, r1;
-    {
-      const unsigned* q0 = &sdata[s][(wave * kG32Rows + lane) * kG20Words];
-      const unsigned* q1 = &sdata[s][((wave + 4) * kG32Rows + lane) * kG20Words];
-      r0.lo = make_uint4(q0[0], q0[1], q0[2], q0[3]); r0.hi.x = q0[4];
-      r1.lo = make_uint4(q1[0], q1[1], q1[2], q1[3]); r1.hi.x = q1[4];
-      r0.hi.y = r0.hi.z = r0.hi.w = 0; r1.hi.y = r1.hi.z = r1.hi.w = 0;
-    }
-    unsigned b0[kF], b1[kF];
-    const unsigned m0 = g20_lift(r0, b0);
-    const unsigned m1 = g20_lift(r1, b1);
-    float acc[2];
-    g32_trees<D, 2>(b0, b1, lv, feat, kbin, T, acc);
-    unsigned fraud = 0, rows = 0, stale = 0;
-    unsigned long long psum = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = rbase + (wave + 4 * h) * kG32Rows + lane;
-      if (rbase + (wave + 4 * h) * kG32Rows >= n) break;  // wave-uniform
-      const unsigned meta = h ? m1 : m0;
-      const bool valid = row < n;
-      const bool fresh = ((meta >> 8) & 0xffu) == stamp;
-      const float p = fresh ? sigmoid(base + acc[h]) : __builtin_nanf("");
-      bool fr;
-      if constexpr (kR) fr = valid && fresh && rule_route(a.rules, p, [](int) { return 0.f; });
-      else fr = valid && fresh && (p >= a.threshold);
-      if (valid) {
-        if (d.proba) st_g(d.proba + row, p);
-        if (d.route) st_g(d.route + row, (uint8_t)(fr ? 1 : 0));
-        if (fresh) psum += (unsigned)(p * 1e6f + 0.5f);
-        atomicAdd(&st[s].hist[(fr ? kNB : 0) + min((int)(meta & 0xffu), kNB - 1)], 1u);
-      }
-      const unsigned long long m = __ballot(fr);
-      fraud += __popcll(m);
-      rows += __popcll(__ballot(valid));
-      stale += __popcll(__ballot(valid && !fresh));
-      persist_emit_flagged(a, d, slot, m, fr, row, lane);
-    }
-    psum = wave_sum_u64(psum);
-    if (lane == 0) {
-      atomicAdd(&st[s].fraud, fraud);
-      atomicAdd(&st[s].rows, rows);
-      atomicAdd(&st[s].stale, stale);
-      atomicAdd(&st[s].psum, psum);
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this wave's outputs and LDS sums are done
-    unsigned old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(&st[s].done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (__shfl(old, 0) != 3) continue;                    // not the item's last scorer
-    // last scorer of the item: its counters into the epoch buffer, release, ticket, free the stage
-    unsigned long long* cnt = a.counters[d.epoch & 1];
-    if (lane < 2 * kNB) {
-      const unsigned hv = st[s].hist[lane];
-      if (hv && cnt) atomicAdd(&cnt[(lane < kNB ? CCFD_CNT_HIST_STD : CCFD_CNT_HIST_FRAUD - kNB) + lane],
-                               (unsigned long long)hv);
-      st[s].hist[lane] = 0;
-    }
-    if (lane == 32 && cnt) {
-      const unsigned rr = st[s].rows, ff = st[s].fraud, ss = st[s].stale;
-      if (rr) {
-        atomicAdd(&cnt[CCFD_CNT_INCOMING], (unsigned long long)rr);
-        atomicAdd(&cnt[CCFD_CNT_FRAUD], (unsigned long long)ff);
-        atomicAdd(&cnt[CCFD_CNT_STANDARD], (unsigned long long)(rr - ff));
-        atomicAdd(&cnt[CCFD_CNT_PROBA_E6], st[s].psum);
-      }
-      if (ss) atomicAdd(&cnt[CCFD_CNT_WIRE_STALE], (unsigned long long)ss);
-    }
-    if (lane == 32) { st[s].rows = 0; st[s].fraud = 0; st[s].stale = 0; st[s].psum = 0; st[s].done = 0; }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      persist_ticket(a, d, slot, C);
-      __hip_atomic_store(&st[s].freed, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-}
-
 template <int D, bool kG20>
 static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream_t s) {
   ccfd_persist_args a = a0;
@@ -626,17 +372,8 @@ static int launch_persist_g32_f(const ccfd_persist_args& a0, int grid, hipStream
   // trees overlap the next chunk's load better); CCFD_G32_INFLIGHT=1 selects the latter.
   // Read per launch: sweepable in-process (profiles/r2/persist_full_item/g32_inflight_ab.jsonl)
   if (g32_env("CCFD_G32_INFLIGHT", 0, 0, 1) == 0) a.flags |= CCFD_ARG_CHUNK_RING;
-  if (g32_env("CCFD_G32_PAIR", 0, 0, 1) == 1) a.flags |= CCFD_ARG_PAIR_CHUNKS;
   const bool gl = ((long)a.gbdt_trees << D) > kG32LeafLds || g32_env("CCFD_G32_GLOBAL_LEAVES", 0, 0, 1);
   const size_t lds = gl ? 0 : (size_t)a.gbdt_trees * (1 << D) * sizeof(float);
-  if constexpr (kG20) {
-    if (g32_env("CCFD_G32_LOADER", 0, 0, 1) == 1 && !gl && a.tiles_per_wave == 2) {   // wave-specialised
-      a.flags |= CCFD_ARG_LOADER;
-      if (a.rules) hipLaunchKernelGGL((persist_g20_spec_kernel<D, true>), dim3(grid), dim3(kSpecThreads), lds, s, a);
-      else hipLaunchKernelGGL((persist_g20_spec_kernel<D, false>), dim3(grid), dim3(kSpecThreads), lds, s, a);
-      return hipGetLastError() == hipSuccess ? 0 : -5;
-    }
-  }
   if (a.flags & CCFD_ARG_PIPE_ITEMS) {                    // pipelined static 512-row items
     if (gl || a.tiles_per_wave != 2 || grid < 2) return -2;
     if (a.rules) hipLaunchKernelGGL((persist_gbdt_pipe_kernel<D, true, kG20, 2>), dim3(grid), dim3(256), lds, s, a);
