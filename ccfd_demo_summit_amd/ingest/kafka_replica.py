@@ -108,8 +108,9 @@ class ReplicaManager:
         self._acks: Dict[TP, list] = {}                      # leader: heap of (end offset, seq, future)
         self._ack_seq = 0
         self._isr_prop: Dict[TP, Dict[str, Any]] = {}
-        self._fetchers: Dict[int, threading.Thread] = {}
+        self._fetchers: Dict[int, Any] = {}
         self._stopping = False
+        self.fetch_mode = os.environ.get("CCFD_REPLICA_FETCH", "loop")
         self._tasks: List[asyncio.Task] = []
         self._session = None
         self.ready = None                                    # asyncio.Event: first metadata applied
@@ -137,7 +138,7 @@ class ReplicaManager:
 
     async def close(self) -> None:
         self._stopping = True                          # the fetcher threads leave at their next turn
-        for t in self._tasks:
+        for t in self._tasks + [f for f in self._fetchers.values() if isinstance(f, asyncio.Task)]:
             t.cancel()
         if self._session is not None:
             await self._session.close()
@@ -479,17 +480,150 @@ class ReplicaManager:
         return by
 
     def _reconcile_fetchers(self) -> None:
-        """One fetcher THREAD per leader this broker follows (event-loop thread)."""
+        """One fetcher per leader this broker follows (event-loop thread): a thread
+        (CCFD_REPLICA_FETCH=thread) or a task on the event loop (=loop, the default)."""
         want = self._followed()
         for node, th in list(self._fetchers.items()):
-            if not th.is_alive():
+            done = th.done() if isinstance(th, asyncio.Task) else not th.is_alive()
+            if node not in want and isinstance(th, asyncio.Task):
+                th.cancel()
+                done = True
+            if done:
                 del self._fetchers[node]
         for node in want:
             if node not in self._fetchers and node in self.nodes:
-                th = threading.Thread(target=self._fetch_thread, args=(node,), daemon=True,
-                                      name=f"replica-fetch-{node}")
-                self._fetchers[node] = th
-                th.start()
+                if self.fetch_mode == "thread":
+                    th = threading.Thread(target=self._fetch_thread, args=(node,), daemon=True,
+                                          name=f"replica-fetch-{node}")
+                    self._fetchers[node] = th
+                    th.start()
+                else:
+                    self._fetchers[node] = asyncio.get_running_loop().create_task(self._fetch_loop(node))
+
+    async def _fetch_loop(self, leader: int) -> None:
+        from .kafka_wire import Reader, Writer
+        corr = 0
+        while True:
+            tps = self._followed().get(leader, [])
+            if not tps or leader not in self.nodes:
+                return
+            host, port = self.nodes[leader]
+            loop = asyncio.get_running_loop()
+            sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            sock.setblocking(False)
+            try:
+                await loop.sock_connect(sock, (host, port))
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            except OSError:
+                sock.close()
+                await asyncio.sleep(0.1)
+                continue
+
+            async def recv_exact(n: int):
+                # straight into one buffer of the response's size (uninitialised: a zero-filled
+                # bytearray cost ~1 ms per large response): the fetched batches are stored as
+                # views of it (no stream-buffer copies of replicated bytes)
+                buf = np.empty(n, np.uint8)
+                mv = memoryview(buf).cast("B")
+                got = 0
+                while got < n:
+                    k = await loop.sock_recv_into(sock, mv[got:])
+                    if k == 0:
+                        raise ConnectionError("replica fetch: leader closed the connection")
+                    got += k
+                return buf
+            try:
+                while True:
+                    tps = self._followed().get(leader, [])
+                    if not tps:
+                        return
+                    by_topic: Dict[str, List[Tuple[int, int]]] = {}
+                    for t, p in tps:                # fetch from this replica's log end, written or not
+                        by_topic.setdefault(t, []).append((p, self.store.log_end(t, p)))
+                    # bounded responses (8 MB, 2 MB a partition): a follower catching up from
+                    # its leader's log start pulls GBs, and the leader's single event loop must
+                    # keep answering produces and consumer fetches between those responses (64 MB
+                    # ones stalled the consumers for seconds after a broker restart)
+                    body = (Writer().i32(self.node_id).i32(200).i32(1).i32(8 << 20).i8(0)
+                            .array(sorted(by_topic.items()), lambda w, kv: w.string(kv[0]).array(
+                                kv[1], lambda w2, q: w2.i32(q[0]).i64(q[1]).i32(2 << 20))).build())
+                    corr += 1
+                    hdr = Writer().i16(FETCH).i16(FETCH_V).i32(corr).string(f"replica-{self.node_id}").build()
+                    await loop.sock_sendall(sock, struct.pack(">i", len(hdr) + len(body)) + hdr + body)
+                    size = struct.unpack(">i", await recv_exact(4))[0]
+                    r = Reader(memoryview(await recv_exact(size)).cast("B"))
+                    if r.i32() != corr:
+                        raise BrokerError("replica fetch: correlation mismatch")
+                    r.i32()                                          # throttle
+
+                    def part(x):
+                        idx, err, hw, _lso = x.i32(), x.i16(), x.i64(), x.i64()
+                        x.array(lambda y: (y.i64(), y.i64()))
+                        return idx, err, hw, x.view_()
+                    resp = r.array(lambda x: (x.string(), x.array(part)))
+                    moved = False
+                    below = []
+                    for t, parts in resp:
+                        for p, err, hw, recs in parts:
+                            if err == 1 and self.store.log_end(t, p) > int(hw):
+                                # OFFSET_OUT_OF_RANGE past the leader's log: this replica holds
+                                # a tail the leader never had -- cut it to the leader's HW
+                                self._truncate_to_hw((t, p), int(hw))
+                                continue
+                            if err == 1:
+                                below.append((t, p))                  # before the leader's log start?
+                                continue
+                            if err:
+                                k = f"{leader}/{t}/{p}:{err}"
+                                self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
+                                moved = True                          # not the leader any more
+                                continue
+                            if recs is not None and len(recs):
+                                try:
+                                    self.store.append_replica(t, p, recs)
+                                except BrokerError:
+                                    k = f"{leader}/{t}/{p}:gap"
+                                    self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
+                                    raise
+                                self.replicated_bytes += len(recs)
+                            self.hw[(t, p)] = max(self.hw.get((t, p), 0), min(int(hw), self.store.log_end(t, p)))
+                    if below:
+                        # away longer than the leader's retention: restart these partitions at
+                        # the leader's log start (ListOffsets earliest), as a Kafka follower does
+                        corr += 1
+                        lo_body = Writer().i32(self.node_id).array(
+                            sorted({t for t, _ in below}), lambda w, t: w.string(t).array(
+                                [q for tt, q in below if tt == t], lambda w2, q: w2.i32(q).i64(-2))).build()
+                        lo_hdr = Writer().i16(LIST_OFFSETS).i16(1).i32(corr).string(f"replica-{self.node_id}").build()
+                        await loop.sock_sendall(sock, struct.pack(">i", len(lo_hdr) + len(lo_body)) + lo_hdr + lo_body)
+                        size = struct.unpack(">i", await recv_exact(4))[0]
+                        r2 = Reader(memoryview(await recv_exact(size)).cast("B"))
+                        if r2.i32() != corr:
+                            raise BrokerError("replica list-offsets: correlation mismatch")
+                        lo = r2.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
+                        for t, parts in lo:
+                            for p, err, _ts, start in parts:
+                                if err == 0 and self.store.log_end(t, p) < int(start):
+                                    n = self.store.reset_to(t, p, int(start))
+                                    self.resets += 1
+                                    print(f"[kafka-lite] node {self.node_id}: {t}[{p}] was below leader {leader}'s "
+                                          f"log start {start}: dropped {n} batches, following from there", flush=True)
+                                else:
+                                    k = f"{leader}/{t}/{p}:1"
+                                    self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
+                                    moved = True
+                    self.replica_fetches += 1
+                    # the next fetch reports this log end to the leader at once, without waiting
+                    # for the local write: an acknowledged batch is then on every in-sync
+                    # replica (in memory, written by each broker's writer right behind) -- a
+                    # single broker's death loses nothing acknowledged, as in Kafka, where a
+                    # follower's append is its page cache
+                    if moved:
+                        await asyncio.sleep(0.05)
+            except (OSError, BrokerError, ConnectionError):
+                await asyncio.sleep(0.05)                            # leader away: metadata will move it
+            finally:
+                sock.close()
 
     def _fetch_thread(self, leader: int) -> None:
         """Replicate the partitions ``leader`` leads: Fetch v4 as replica ``node_id`` from this
