@@ -24,6 +24,9 @@ def main() -> None:
     ap.add_argument("--name", required=True)
     ap.add_argument("--src", action="append", required=True, help="csrc-relative source(s) to recompile")
     ap.add_argument("-D", dest="defs", action="append", default=[])
+    ap.add_argument("--from-rev", default=None,
+                    help="compile the --src files as they were at this git revision (a variant "
+                         "removed from the tree after it lost), against today's headers")
     args = ap.parse_args()
     from ccfd_demo_summit_amd.ops import build as B
     B.build(verbose=False)                       # regular objects up to date
@@ -33,8 +36,15 @@ def main() -> None:
     for rel in args.src:
         src = B.CSRC / rel
         obj = B.OBJ / f"ab_{args.name}_{src.parent.name}_{src.stem}.o"
+        comp = src
+        if args.from_rev:
+            comp = B.OBJ / f"ab_{args.name}_{src.stem}{src.suffix}"
+            text = subprocess.run(["git", "-C", str(ROOT), "show", f"{args.from_rev}:csrc/{rel}"],
+                                  check=True, capture_output=True, text=True).stdout
+            comp.write_text(text)
         cmd = [B.hipcc(), "-O3", "-fPIC", "-std=c++17", f"--offload-arch={B.ARCH}", "-Wall", "-Wno-unused-result",
-               "-I", str(B.CSRC / "include")] + [f"-D{d}" for d in args.defs] + ["-c", str(src), "-o", str(obj)]
+               "-I", str(B.CSRC / "include"), "-I", str(src.parent)] + [f"-D{d}" for d in args.defs] + \
+              ["-c", str(comp), "-o", str(obj)]
         subprocess.run(cmd, check=True)
         objs[src] = obj
     lib = out_dir / f"{args.name}.so"
