@@ -36,6 +36,14 @@ def main() -> None:
     ap.add_argument("--partitions", type=int, default=2)     # bench.py: 2 partitions a rank
     ap.add_argument("--log-rows", type=int, default=1 << 22)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--threshold", type=float, default=0.5)
+    ap.add_argument("--fraud-rate", type=float, default=None,
+                    help="calibrated share of fraud-routed rows (default: the dataset prior, ~0.17 %%)")
+    ap.add_argument("--segments", type=int, default=1,
+                    help="pump --batches in this many equal segments, each one's rate reported "
+                         "(the flagged ring is drained between segments)")
+    ap.add_argument("--flag-capacity", type=int, default=1 << 23)
+    ap.add_argument("--numa-bind", action="store_true", help="pin to the GPU's NUMA node first, as bench.py does")
     a = ap.parse_args()
     import torch
 
@@ -49,11 +57,17 @@ def main() -> None:
         raise SystemExit("pmc_persist.py needs a GPU")
     wire = resolve_row_format(a.model, "auto")
     ctx = init_distributed()
+    numa = None
+    if a.numa_bind:
+        from ccfd_demo_summit_amd.utils.numa import bind_to_gpu
+        numa = bind_to_gpu(ctx.device.index)
     Xcal, _ = generate(200_000, seed=a.seed + 999)
-    model = build_model(a.model, seed=a.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE, threshold=0.5)
+    model = build_model(a.model, seed=a.seed, X_ref=Xcal, calibrate_rate=FRAUD_RATE if a.fraud_rate is None else a.fraud_rate,
+                        threshold=a.threshold)
     dm = broadcast_model(ctx, model, a.model, wire)
     eng = StreamEngine(dm, batch=a.batch, depth=a.depth, streams=a.streams, input_mode="zerocopy", output_mode="zerocopy",
-                       threshold=0.5, device=ctx.device.index, exec_mode="persistent", flag_capacity=1 << 23)
+                       threshold=a.threshold, device=ctx.device.index, exec_mode="persistent",
+                      flag_capacity=a.flag_capacity)
     rows_per_part = max(a.batch * 4, a.log_rows // a.partitions)
     logs = []
     for p in range(a.partitions):
@@ -69,16 +83,26 @@ def main() -> None:
     def handoff(records):
         handed[0] += len(records)
 
+    seg_rates = []
+    per = max(1, a.batches // max(1, a.segments))
+    rows = fraud = 0
     t0 = time.perf_counter()
-    st = eng.pump(a.batches, drain=True, on_flagged=handoff)
+    for k in range(max(1, a.segments)):
+        ts = time.perf_counter()
+        st = eng.pump(per, drain=(k == a.segments - 1), on_flagged=handoff)
+        handoff(eng.drain_flagged())
+        rows += st.rows
+        fraud += st.fraud_rows
+        seg_rates.append(round(st.rows / max(time.perf_counter() - ts, 1e-9) / 1e9, 4))
     dt = time.perf_counter() - t0
     handoff(eng.drain_flagged())
     eng.close()                         # the persistent kernel ends: its counters are collected
     print(json.dumps({"model": a.model, "row_format": dm.row_format, "batches": a.batches, "batch": a.batch,
-                      "depth": a.depth, "rows": st.rows, "wall_s": round(dt, 4),
-                      "tx_s": round(st.rows / max(dt, 1e-9), 1), "p50_us": round(st.lat_p50_us, 1),
-                      "fraud_routed": st.fraud_rows, "handed_off": handed[0],
-                      "lib": os.environ.get("CCFD_LIB_PATH", "default")}), flush=True)
+                      "depth": a.depth, "rows": rows, "wall_s": round(dt, 4),
+                      "tx_s": round(rows / max(dt, 1e-9), 1), "segment_gtx_s": seg_rates,
+                      "flag_full_events": st.flag_full_events, "p50_us": round(st.p50_us, 1),
+                      "fraud_routed": fraud, "handed_off": handed[0],
+                      "numa_node": numa, "lib": os.environ.get("CCFD_LIB_PATH", "default")}), flush=True)
 
 
 if __name__ == "__main__":
