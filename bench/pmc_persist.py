@@ -43,12 +43,15 @@ def main() -> None:
                     help="pump --batches in this many equal segments, each one's rate reported "
                          "(the flagged ring is drained between segments)")
     ap.add_argument("--flag-capacity", type=int, default=1 << 23)
+    ap.add_argument("--drainer", action="store_true",
+                    help="hand off on a collector thread beside the pump (bench.py's way) instead of "
+                         "draining between segments")
     ap.add_argument("--numa-bind", action="store_true", help="pin to the GPU's NUMA node first, as bench.py does")
     a = ap.parse_args()
     import torch
 
     from ccfd_demo_summit_amd.data import FRAUD_RATE, generate
-    from ccfd_demo_summit_amd.engine import PartitionLog, StreamEngine
+    from ccfd_demo_summit_amd.engine import FlaggedDrainer, PartitionLog, StreamEngine
     from ccfd_demo_summit_amd.models import build_model
     from ccfd_demo_summit_amd.parallel import broadcast_model, init_distributed
     from ccfd_demo_summit_amd.parallel.dp import resolve_row_format
@@ -80,8 +83,12 @@ def main() -> None:
     torch.cuda.synchronize()            # every setup dispatch done before the kernel is resident
     handed = [0]
 
+    mu = __import__("threading").Lock()
+
     def handoff(records):
-        handed[0] += len(records)
+        with mu:
+            handed[0] += len(records)
+    drainer = FlaggedDrainer(eng, handoff).start() if a.drainer else None
 
     seg_rates = []
     per = max(1, a.batches // max(1, a.segments))
@@ -90,10 +97,13 @@ def main() -> None:
     for k in range(max(1, a.segments)):
         ts = time.perf_counter()
         st = eng.pump(per, drain=(k == a.segments - 1), on_flagged=handoff)
-        handoff(eng.drain_flagged())
+        if drainer is None:
+            handoff(eng.drain_flagged())
         rows += st.rows
         fraud += st.fraud_rows
         seg_rates.append(round(st.rows / max(time.perf_counter() - ts, 1e-9) / 1e9, 4))
+    if drainer is not None:
+        drainer.stop()
     dt = time.perf_counter() - t0
     handoff(eng.drain_flagged())
     eng.close()                         # the persistent kernel ends: its counters are collected

@@ -1,4 +1,4 @@
 """GPU-resident micro-batching engine (native core in csrc/engine/engine.cpp)."""
-from .stream_engine import PartitionLog, PinnedArray, StepStats, StreamEngine
+from .stream_engine import FlaggedDrainer, PartitionLog, PinnedArray, StepStats, StreamEngine
 
-__all__ = ["PartitionLog", "PinnedArray", "StepStats", "StreamEngine"]
+__all__ = ["FlaggedDrainer", "PartitionLog", "PinnedArray", "StepStats", "StreamEngine"]

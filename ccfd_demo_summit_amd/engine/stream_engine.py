@@ -8,6 +8,8 @@ collectives on a side stream between steps (parallel/dp.py).
 from __future__ import annotations
 
 import ctypes as C
+import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -218,6 +220,70 @@ def check_lossless(st: "StepStats") -> None:
         raise HandoffLost(f"{st.dropped} fraud-routed records were dropped by the engine's flagged ring")
 
 
+class FlaggedDrainer:
+    """The router's collector beside a pumping engine: a thread that moves fraud-routed
+    records from the engine's flagged ring into ``sink(records)`` while the caller's thread
+    keeps submitting micro-batches (the pump is a native call that releases the GIL).
+
+    The streaming service works this way (native serving thread + Python collector); a
+    replay that drained inline instead -- pump a step, then drain -- left the GPU with no new
+    work for the length of every drain: ~1e6 fraud records a 0.25 s config-4 step cost it
+    4-10 % of its rate (profiles/r6/pass_h/).  ``stop()`` joins the thread and drains what is
+    left, so every record reaches ``sink`` exactly once, in completion order; an exception in
+    ``sink`` is raised again there."""
+
+    def __init__(self, engine: "StreamEngine", sink, idle_s: float = 2e-4):
+        self.engine = engine
+        self.sink = sink
+        self.idle_s = float(idle_s)
+        self.records = 0
+        self.drains = 0
+        self._stop = threading.Event()
+        self._err: Optional[BaseException] = None
+        self._th: Optional[threading.Thread] = None
+
+    def start(self) -> "FlaggedDrainer":
+        self._stop.clear()
+        self._th = threading.Thread(target=self._run, name="flagged-drainer", daemon=True)
+        self._th.start()
+        return self
+
+    def _hand(self, recs: np.ndarray) -> None:
+        if len(recs):
+            self.sink(recs)
+            self.records += len(recs)
+            self.drains += 1
+
+    def _run(self) -> None:
+        try:
+            while not self._stop.is_set():
+                recs = self.engine.drain_flagged()
+                if len(recs):
+                    self._hand(recs)
+                else:
+                    time.sleep(self.idle_s)
+        except BaseException as e:       # noqa: BLE001 -- re-raised on the caller's thread
+            self._err = e
+
+    def stop(self) -> int:
+        """Join the thread, hand off what is left in the ring; returns the records handed."""
+        if self._th is not None:
+            self._stop.set()
+            self._th.join()
+            self._th = None
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise e
+        self._hand(self.engine.drain_flagged())
+        return self.records
+
+    def __enter__(self) -> "FlaggedDrainer":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+
 _FMT_BY_ROW_BYTES = {120: "f32", 64: "w64", 32: "g32", 20: "g20"}
 
 
@@ -304,6 +370,9 @@ class StreamEngine:
         # records taken out of a full flagged ring by a blocking call (drain paths) so it could
         # finish; drain_flagged / serve_collect return them first, in completion order
         self._stash: List[np.ndarray] = []
+        # the flagged drains may run on a collector thread beside the pump (FlaggedDrainer):
+        # the ring's native drain is lock-protected, the stash and the copy-out are guarded here
+        self._drain_lock = threading.Lock()
 
     def close(self):
         if getattr(self, "h", None):
@@ -344,10 +413,11 @@ class StreamEngine:
             self._stash_ring()
 
     def _stash_ring(self) -> int:
-        got = self._drain_ring(1 << 62)
-        if len(got):
-            self._stash.append(got)
-        return len(got)
+        with self._drain_lock:
+            got = self._drain_ring(1 << 62)
+            if len(got):
+                self._stash.append(got)
+            return len(got)
 
     def pump(self, n_batches: int, batch_rows: Optional[int] = None, drain: bool = True,
              on_flagged=None) -> StepStats:
@@ -423,7 +493,12 @@ class StreamEngine:
         return lib().ccfd_engine_epoch_complete(C.c_void_p(self.h), int(flip_count)) == 1
 
     def drain_flagged(self, max_records: int = 1 << 30) -> np.ndarray:
-        """Fraud-routed records of completed batches, oldest first (stash, then the ring)."""
+        """Fraud-routed records of completed batches, oldest first (stash, then the ring).
+        Safe beside a pump on another thread (the native drain holds only the ring's lock)."""
+        with self._drain_lock:
+            return self._drain_flagged_locked(max_records)
+
+    def _drain_flagged_locked(self, max_records: int) -> np.ndarray:
         out: List[np.ndarray] = []
         total = 0
         while self._stash and total < max_records:
@@ -441,20 +516,24 @@ class StreamEngine:
         return np.concatenate(out) if len(out) > 1 else out[0] if out else \
             np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
 
-    def _drain_ring(self, max_records: int) -> np.ndarray:
+    def _drain_ring(self, max_records: int, chunk: int = 16384) -> np.ndarray:
+        # straight into the returned arrays (one copy out of the ring); bounded chunks keep the
+        # ring lock -- which the pump's completions also take -- held for tens of microseconds
         out: List[np.ndarray] = []
         total = 0
         while total < max_records:
-            k = lib().ccfd_engine_drain_flagged(C.c_void_p(self.h), self._flag_buf,
-                                                min(65536, max_records - total))
+            want = min(chunk, max_records - total)
+            arr = np.empty(want, dtype=np.dtype(FLAGGED_DTYPE))
+            k = lib().ccfd_engine_drain_flagged(C.c_void_p(self.h), arr.ctypes.data, want)
             if k <= 0:
                 break
-            arr = np.frombuffer(self._flag_buf, dtype=np.dtype(FLAGGED_DTYPE), count=k).copy()
-            out.append(arr)
+            out.append(arr[:k])
             total += k
-            if k < 65536:
+            if k < want:
                 break
-        return np.concatenate(out) if out else np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
+        if not out:
+            return np.zeros(0, dtype=np.dtype(FLAGGED_DTYPE))
+        return out[0] if len(out) == 1 else np.concatenate(out)
 
     def enable_scored(self, capacity: int = 1 << 20) -> None:
         """Opt in to a per-row scored-record ring of ``capacity`` rows (0 = off): every
@@ -518,9 +597,10 @@ class StreamEngine:
         if rc < 0:
             raise RuntimeError(f"engine serving thread failed: {last_error()}")
         fl = self._collect_flag[:nf.value].copy()
-        if self._stash:                      # stashed by a blocking call: older than the ring's
-            fl = np.concatenate(self._stash + [fl])
-            self._stash = []
+        with self._drain_lock:
+            if self._stash:                  # stashed by a blocking call: older than the ring's
+                fl = np.concatenate(self._stash + [fl])
+                self._stash = []
         rec = sc[:ns.value].copy() if sc is not None else None
         out = _stats(st)
         check_lossless(out)

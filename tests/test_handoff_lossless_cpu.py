@@ -3,6 +3,8 @@ native pump that stopped on a full flagged ring, routes the drained records to t
 hand-off (or the stash) in completion order, and any report of a dropped record is refused
 -- by the engine wrapper (HandoffLost) and by bench.py (no JSON line, exit 5)."""
 import ctypes as C
+import threading
+import time
 
 import numpy as np
 import pytest
@@ -22,19 +24,23 @@ class FakeNative:
         self.dropped = 0
         self.full_events = 0
         self.pump_calls = 0
+        self.mu = threading.Lock()                           # engine.cpp ring_mu
 
     def ccfd_engine_pump(self, h, n, rows, drain, st_ref):
         st = st_ref._obj
         self.pump_calls += 1
         done = 0
         while done < n:
-            if len(self.ring) + self.rows > self.cap:        # no room: stop, lose nothing
+            with self.mu:
+                full = len(self.ring) + self.rows > self.cap
+                if not full:
+                    self.ring.extend(range(self.next_id, self.next_id + self.rows))
+                    self.next_id += self.rows
+            if full:                                         # no room: stop, lose nothing
                 self.full_events += 1
                 st.submitted += done
                 st.flag_full_events = self.full_events
                 return ENGINE_FLAG_FULL
-            self.ring.extend(range(self.next_id, self.next_id + self.rows))
-            self.next_id += self.rows
             st.batches += 1
             st.rows += self.rows
             st.fraud_rows += self.rows
@@ -45,8 +51,11 @@ class FakeNative:
         return 0
 
     def ccfd_engine_drain_flagged(self, h, buf, k):
-        take = self.ring[:k]
-        del self.ring[:k]
+        with self.mu:
+            take = self.ring[:k]
+            del self.ring[:k]
+        if isinstance(buf, int):                             # an address (numpy array's data)
+            buf = (se.Flagged * max(1, k)).from_address(buf)
         arr = np.frombuffer(buf, dtype=np.dtype(FLAGGED_DTYPE), count=len(take))
         arr["tx_id"] = take
         return len(take)
@@ -59,6 +68,7 @@ def _engine(fake, monkeypatch):
     eng.batch = fake.rows
     eng._flag_buf = (se.Flagged * 65536)()
     eng._stash = []
+    eng._drain_lock = threading.Lock()
     return eng
 
 
@@ -112,3 +122,39 @@ def test_bench_refuses_a_lossy_line():
     assert bench.handoff_refusal(21_772_280, 21_772_280) is None
     msg = bench.handoff_refusal(20_971_520, 21_772_280)     # the round-5 config-4 line
     assert msg and "refusing" in msg
+
+
+def test_collector_thread_beside_the_pump_hands_off_everything_once(monkeypatch):
+    """bench.py's hand-off: a FlaggedDrainer thread drains while this thread pumps (the
+    pump's own full-ring path drains into the same sink); every record arrives exactly once,
+    in completion order, and stop() leaves the ring empty."""
+    fake = FakeNative(cap=64, rows=4)
+    eng = _engine(fake, monkeypatch)
+    got = []
+    mu = threading.Lock()
+
+    def sink(r):
+        with mu:
+            got.extend(r["tx_id"].tolist())
+    dr = se.FlaggedDrainer(eng, sink, idle_s=1e-5).start()
+    for _ in range(50):
+        eng.pump(40, on_flagged=sink)
+    n = dr.stop()
+    assert got == list(range(50 * 40 * 4))
+    assert n <= len(got) and dr.drains > 0
+    assert fake.ring == []
+    eng.h = None
+
+
+def test_collector_thread_reraises_a_sink_failure(monkeypatch):
+    fake = FakeNative(cap=64, rows=4)
+    eng = _engine(fake, monkeypatch)
+
+    def sink(_r):
+        raise RuntimeError("router down")
+    dr = se.FlaggedDrainer(eng, sink, idle_s=1e-5).start()
+    eng.pump(2, on_flagged=lambda r: None)
+    time.sleep(0.05)
+    with pytest.raises(RuntimeError, match="router down"):
+        dr.stop()
+    eng.h = None
