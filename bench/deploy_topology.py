@@ -274,7 +274,8 @@ def main(argv=None):
     ap.add_argument("--producers", type=int, default=3)
     ap.add_argument("--rate", type=float, default=0.0, help="total produce rate tx/s (0 = open loop, max)")
     ap.add_argument("--fmt", default="json", choices=["json", "txb1"])
-    ap.add_argument("--batch", type=int, default=4096, help="messages (json) / rows (txb1) per produce request")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="messages (json, default 1024) / rows (txb1, default 4096) per produce request")
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--kafka-nodes", type=int, default=3)
     ap.add_argument("--retention-batches", type=int, default=500,
@@ -342,6 +343,8 @@ def main(argv=None):
     ap.add_argument("--log-dir", default="gpurun_out/deploy_topology")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
+    if a.batch is None:
+        a.batch = 1024 if a.fmt == "json" else 4096
     log_dir = ROOT / a.log_dir
     log_dir.mkdir(parents=True, exist_ok=True)
 
@@ -369,7 +372,7 @@ def main(argv=None):
     procs: List[Proc] = []
     out: Dict = {"metric": "end-to-end tx/s, deployed topology (separate processes)", "topology": "shared",
                  "n_gpus": 1 if a.rehearsal else a.ranks, "ranks": a.ranks, "rehearsal": a.rehearsal,
-                 "fmt": a.fmt, "producers": a.producers, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
+                 "fmt": a.fmt, "producers": a.producers, "producer_batch": a.batch, "partitions": a.partitions, "kafka_nodes": a.kafka_nodes,
                  "model": a.model, "kie_shards": K, "kafka_replicated": a.kafka_replicated,
                  "producer_acks": acks, "producer_max_in_flight": inflight,
                  "kafka_rf": a.kafka_rf if a.kafka_replicated else None}

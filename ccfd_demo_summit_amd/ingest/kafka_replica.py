@@ -110,7 +110,14 @@ class ReplicaManager:
         self._isr_prop: Dict[TP, Dict[str, Any]] = {}
         self._fetchers: Dict[int, Any] = {}
         self._stopping = False
-        self.fetch_mode = os.environ.get("CCFD_REPLICA_FETCH", "loop")
+        # follower fetchers: a thread per leader (default; round-6 pass E2: RF-3 JSON produce ->
+        # scored p99 4.3 ms vs 15.5 ms as event-loop tasks at 1024-message produces) or a task
+        # on the broker's event loop (=loop)
+        self.fetch_mode = os.environ.get("CCFD_REPLICA_FETCH", "thread")
+        # a fetcher thread checks a partition's leader epoch and appends under this lock, and
+        # new metadata is applied under it: no append from a deposed leader's response can
+        # land after the truncation that starts following the new one
+        self._follow_lock = threading.RLock()
         self._tasks: List[asyncio.Task] = []
         self._session = None
         self.ready = None                                    # asyncio.Event: first metadata applied
@@ -274,6 +281,10 @@ class ReplicaManager:
         """New metadata from the controller: leadership / ISR / topics / brokers."""
         if "parts" not in d:
             return
+        with self._follow_lock:
+            self._apply_locked(d)
+
+    def _apply_locked(self, d: Dict[str, Any]) -> None:
         self.meta_epoch = int(d["meta_epoch"])
         self.nodes = {int(k): (v[0], int(v[1])) for k, v in d["nodes"].items()}
         for name, n in d["topics"].items():
@@ -697,32 +708,33 @@ class ReplicaManager:
                     below = []
                     for t, parts in resp:
                         for p, err, hw, recs in parts:
-                            cur = self.parts.get((t, p))
-                            if cur is None or (cur["leader"], cur["epoch"]) != epochs.get((t, p)):
-                                moved = True                          # leadership moved meanwhile
-                                continue
-                            if err == 1 and self.store.log_end(t, p) > int(hw):
-                                # OFFSET_OUT_OF_RANGE past the leader's log: this replica holds
-                                # a tail the leader never had -- cut it to the leader's HW
-                                self._truncate_to_hw((t, p), int(hw))
-                                continue
-                            if err == 1:
-                                below.append((t, p))                  # before the leader's log start?
-                                continue
-                            if err:
-                                k = f"{leader}/{t}/{p}:{err}"
-                                self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
-                                moved = True                          # not the leader any more
-                                continue
-                            if recs is not None and len(recs):
-                                try:
-                                    self.store.append_replica(t, p, recs)
-                                except BrokerError:
-                                    k = f"{leader}/{t}/{p}:gap"
+                            with self._follow_lock:                   # epoch check + append, atomic
+                                cur = self.parts.get((t, p))          # against _apply
+                                if cur is None or (cur["leader"], cur["epoch"]) != epochs.get((t, p)):
+                                    moved = True                      # leadership moved meanwhile
+                                    continue
+                                if err == 1 and self.store.log_end(t, p) > int(hw):
+                                    # OFFSET_OUT_OF_RANGE past the leader's log: this replica holds
+                                    # a tail the leader never had -- cut it to the leader's HW
+                                    self._truncate_to_hw((t, p), int(hw))
+                                    continue
+                                if err == 1:
+                                    below.append((t, p))              # before the leader's log start?
+                                    continue
+                                if err:
+                                    k = f"{leader}/{t}/{p}:{err}"
                                     self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
-                                    raise
-                                self.replicated_bytes += len(recs)
-                            self.hw[(t, p)] = max(self.hw.get((t, p), 0), min(int(hw), self.store.log_end(t, p)))
+                                    moved = True                      # not the leader any more
+                                    continue
+                                if recs is not None and len(recs):
+                                    try:
+                                        self.store.append_replica(t, p, recs)
+                                    except BrokerError:
+                                        k = f"{leader}/{t}/{p}:gap"
+                                        self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
+                                        raise
+                                    self.replicated_bytes += len(recs)
+                                self.hw[(t, p)] = max(self.hw.get((t, p), 0), min(int(hw), self.store.log_end(t, p)))
                     if below:
                         # away longer than the leader's retention: restart these partitions at
                         # the leader's log start (ListOffsets earliest), as a Kafka follower does
@@ -739,15 +751,18 @@ class ReplicaManager:
                         lo = r2.array(lambda x: (x.string(), x.array(lambda y: (y.i32(), y.i16(), y.i64(), y.i64()))))
                         for t, parts in lo:
                             for p, err, _ts, start in parts:
-                                if err == 0 and self.store.log_end(t, p) < int(start):
-                                    n = self.store.reset_to(t, p, int(start))
-                                    self.resets += 1
-                                    print(f"[kafka-lite] node {self.node_id}: {t}[{p}] was below leader {leader}'s "
-                                          f"log start {start}: dropped {n} batches, following from there", flush=True)
-                                else:
-                                    k = f"{leader}/{t}/{p}:1"
-                                    self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
-                                    moved = True
+                                with self._follow_lock:
+                                    cur = self.parts.get((t, p))
+                                    same = cur is not None and (cur["leader"], cur["epoch"]) == epochs.get((t, p))
+                                    if same and err == 0 and self.store.log_end(t, p) < int(start):
+                                        n = self.store.reset_to(t, p, int(start))
+                                        self.resets += 1
+                                        print(f"[kafka-lite] node {self.node_id}: {t}[{p}] was below leader {leader}'s "
+                                              f"log start {start}: dropped {n} batches, following from there", flush=True)
+                                    else:
+                                        k = f"{leader}/{t}/{p}:1"
+                                        self.fetch_errors[k] = self.fetch_errors.get(k, 0) + 1
+                                        moved = True
                     self.replica_fetches += 1
                     # the next fetch reports this log end to the leader at once, without waiting
                     # for the local write: an acknowledged batch is then on every in-sync

@@ -712,7 +712,10 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="producer: 1 = the leader, -1 = every in-sync replica (acks=all)")
     ap.add_argument("--max-in-flight", type=int, default=1,
                     help="producer: produce requests in flight per producer (pipelined; idempotent order kept)")
-    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="producer: JSON messages per produce request (default 1024) / TXB1 rows per "
+                         "message (default 4096); 1024-message requests keep the RF-3 produce -> scored "
+                         "p99 at ~4 ms (4096: ~7-13 ms, docs/ROUND6.md section 5)")
     ap.add_argument("--rate", type=float, default=0.0)
     ap.add_argument("--count", type=int, default=100_000, help="producer: transactions (0 = run --seconds)")
     ap.add_argument("--id-base", type=int, default=0, help="producer: first transaction id")
@@ -734,6 +737,8 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="elastic: fraud hand-off to KIE_SERVER_URL or an in-process engine")
     a = ap.parse_args(argv)
     a.cmd = cmd
+    if a.batch is None:
+        a.batch = 1024 if a.fmt == "json" else 4096
     if a.service == "elastic" and a.partitions <= 0:
         a.partitions = 2 * a.world
     if a.service in ("elastic", "operator") and a.seconds == 10.0 and "--seconds" not in argv:

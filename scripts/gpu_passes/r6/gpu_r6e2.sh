@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}" || exit 1
 O=gpurun_out/r6e2; mkdir -p $O; export TMPDIR=/tmp PYTHONFAULTHANDLER=1
 st() { echo "[r6e2] $(date +%T) $*"; }
 # cfg = <fetcher>-q<controllers>-b<producer batch: JSON messages per produce request>
-for cfg in loop-q3-b4096 loop-q3-b1024 loop-q3-b2048 thread-q3-b4096 loop-q1-b4096 loop-q3-b1024x; do
+for cfg in loop-q3-b1024 loop-q3-b4096 thread-q3-b1024 loop-q3-b2048 thread-q3-b4096; do
   mode=${cfg%%-*}; rest=${cfg#*-}; q=${rest%%-*}; q=${q#q}; b=${rest#*-b}; b=${b%x}
   st run $cfg
   CCFD_REPLICA_FETCH=$mode timeout -k 10 300 python -u bench/deploy_topology.py --kafka-replicated --kafka-controllers $q \
